@@ -1,0 +1,598 @@
+// Cross-shaped stripe attention + LePE for gfx950 (MI355X, CDNA4).
+//
+// Replaces LePEAttention.forward (train_cswinunet_segmentation.py cswin:271-298) together with
+// its window layout (img2windows/windows2img cswin:199-217, im2cswin/get_lepe cswin:248-269)
+// and the branch split/concat of CSWinBlock.forward (cswin:358-363).  No layout copies: every
+// window token is gathered straight from the (B, L, 3C) qkv buffer and the result is written
+// straight to its channels of the (B, L, C) output.
+//
+// Work decomposition: one 256-thread workgroup = one (branch, image, window, head, 128-row
+// block); each of its 4 waves owns 32 rows.  The other operand streams through LDS in chunks of
+// KC = 128 rows.  All products are 32x32 MFMA tiles:
+//   bf16 storage: v_mfma_f32_32x32x16_bf16 (fp32 accumulate);
+//   fp32 storage: v_mfma_f32_32x32x2_f32  (exact f32 fma chain -- the fp32 parity path).
+// "Swapped" orientation: S^T = K Q^T puts the query on the lane and 16 keys in registers, so
+// the softmax row statistics need one cross-half shuffle and the probabilities are already the
+// B operand of O^T += V^T P^T (accumulator-as-operand, cdna_hip_programming.md §3).
+//
+// Backward = two kernels (query-owner: dQ and delta; key-owner: dK, dV including the LePE
+// input gradient) plus a deterministic two-pass reduction for the LePE weight/bias gradient.
+#include "common.hpp"
+
+namespace csu {
+namespace {
+
+constexpr int HD = 32;     // head dim (fixed by the model: SURVEY §0.5)
+constexpr int KC = 128;    // rows of the streamed operand per LDS chunk
+constexpr int QR = 128;    // rows owned by one workgroup (4 waves x 32)
+constexpr int NT = 256;
+
+template <typename T> struct Cfg;
+template <> struct Cfg<bf16> {
+    static constexpr int KSTR = HD + 8;   // 80-B rows: conflict-free ds_read_b128 of row chunks
+    static constexpr int VSTR = KC + 4;   // 264-B rows: conflict-free ds_read_b64 of transposed rows
+};
+template <> struct Cfg<float> {
+    static constexpr int KSTR = HD + 4;   // 144-B rows
+    static constexpr int VSTR = KC + 1;   // odd stride: conflict-free ds_read_b32 column reads
+};
+
+// select a branch without dynamic indexing of the kernel-argument struct (no scratch copy)
+__device__ __forceinline__ const csu_stripe_branch& branch(const csu_stripe_args& a, int i) {
+    return i ? a.br[1] : a.br[0];
+}
+
+struct Win {
+    int br, b, h, wy, wx, blk;  // branch, image, head, window row/col, 128-row block
+    int H_sp, W_sp, N;
+    int chq;                    // channel of (branch, head) inside the C-wide Q/K/V slot
+};
+
+__device__ __forceinline__ Win decode_block(const csu_stripe_args& a) {
+    Win w;
+    w.br = blockIdx.y;
+    const csu_stripe_branch& g = branch(a, w.br);
+    w.H_sp = g.H_sp;
+    w.W_sp = g.W_sp;
+    w.N = w.H_sp * w.W_sp;
+    const int nwx = a.reso / w.W_sp, nwin = (a.reso / w.H_sp) * nwx;
+    const int nblk = (w.N + QR - 1) / QR;
+    int id = blockIdx.x;
+    w.blk = id % nblk; id /= nblk;
+    w.h = id % a.heads; id /= a.heads;
+    const int win = id % nwin;
+    w.b = id / nwin;
+    w.wy = win / nwx;
+    w.wx = win % nwx;
+    w.chq = g.ch_off + w.h * HD;
+    return w;
+}
+
+// token index (inside its image) of window-local position n
+__device__ __forceinline__ int tok_of(const Win& w, int reso, int n) {
+    const int iy = n / w.W_sp, ix = n - iy * w.W_sp;
+    return (w.wy * w.H_sp + iy) * reso + w.wx * w.W_sp + ix;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Operand fragments of one 32-row tile: row r = lane & 31, half h = lane >> 5.
+//   bf16: k-step s (16 wide) -> elements [16s + 8h, +8) of the row
+//   f32 : k-step t (2 wide)  -> element 16h + t of the row (t = 0..15)
+// Both A (rows from LDS) and B (rows from registers) use the same inner-index permutation.
+// ---------------------------------------------------------------------------------------------
+template <typename T> struct Frag;
+template <> struct Frag<bf16> { bf16x8 v[2]; };
+template <> struct Frag<float> { float v[16]; };
+
+__device__ __forceinline__ void load_frag(Frag<bf16>& f, const bf16* row, int h, bool valid) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+        if (valid) f.v[s] = *reinterpret_cast<const bf16x8*>(row + 16 * s + 8 * h);
+        else f.v[s] = bf16x8{};
+    }
+}
+__device__ __forceinline__ void load_frag(Frag<float>& f, const float* row, int h, bool valid) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        f32x4 x = valid ? *reinterpret_cast<const f32x4*>(row + 16 * h + 4 * i) : f32x4{};
+        f.v[4 * i] = x[0]; f.v[4 * i + 1] = x[1]; f.v[4 * i + 2] = x[2]; f.v[4 * i + 3] = x[3];
+    }
+}
+
+// acc += A_lds(rows 32) * B_frag^T   (A rows are row-major [row][KSTR] in LDS)
+__device__ __forceinline__ void mma_rows(f32x16& acc, const bf16* A, int r, int h, const Frag<bf16>& B) {
+    constexpr int S = Cfg<bf16>::KSTR;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+        bf16x8 a = *reinterpret_cast<const bf16x8*>(A + r * S + 16 * s + 8 * h);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, B.v[s], acc, 0, 0, 0);
+    }
+}
+__device__ __forceinline__ void mma_rows(f32x16& acc, const float* A, int r, int h, const Frag<float>& B) {
+    constexpr int S = Cfg<float>::KSTR;
+    float a[16];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        f32x4 x = *reinterpret_cast<const f32x4*>(A + r * S + 16 * h + 4 * i);
+        a[4 * i] = x[0]; a[4 * i + 1] = x[1]; a[4 * i + 2] = x[2]; a[4 * i + 3] = x[3];
+    }
+#pragma unroll
+    for (int t = 0; t < 16; ++t) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[t], B.v[t], acc, 0, 0, 0);
+}
+
+// acc(d, col) += sum_k At[d][k0 + k] * X[k][col], X = 32x32 f32 accumulator tile of this wave
+// (column on the lane, row k in registers).  At is a transposed [HD][VSTR] LDS image.
+__device__ __forceinline__ void mma_acc_operand(f32x16& acc, const bf16* At, int k0, int r, int h, const f32x16& X) {
+    constexpr int S = Cfg<bf16>::VSTR;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+        bf16x8 b;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) b[j] = (bf16)X[8 * s + j];
+        const bf16* p = At + r * S + k0 + 16 * s + 4 * h;
+        bf16x4 lo = *reinterpret_cast<const bf16x4*>(p);
+        bf16x4 hi = *reinterpret_cast<const bf16x4*>(p + 8);
+        bf16x8 a = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc, 0, 0, 0);
+    }
+}
+__device__ __forceinline__ void mma_acc_operand(f32x16& acc, const float* At, int k0, int r, int h, const f32x16& X) {
+    constexpr int S = Cfg<float>::VSTR;
+#pragma unroll
+    for (int t = 0; t < 16; ++t)
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(At[r * S + k0 + crow(t, h)], X[t], acc, 0, 0, 0);
+}
+
+// Cooperative gather of `nrows` window rows (rows >= valid_rows are zero) of one head into
+//   nat: natural [KC][KSTR] image (optional) and tr: transposed [HD][VSTR] image (optional).
+template <typename T>
+__device__ __forceinline__ void stage_rows(const Win& w, int reso, const T* img, int rstride, int ch,
+                                           int row0, int N, T* nat, T* tr) {
+    constexpr int VEC = 16 / sizeof(T);
+    constexpr int PER = HD / VEC;
+    for (int it = threadIdx.x; it < KC * PER; it += NT) {
+        const int rr = it / PER, d0 = (it % PER) * VEC;
+        const int n = row0 + rr;
+        float v[VEC];
+        if (n < N) {
+            const T* src = img + (size_t)tok_of(w, reso, n) * rstride + ch + d0;
+            if constexpr (VEC == 8) load8(src, v); else load4(src, v);
+        } else {
+#pragma unroll
+            for (int j = 0; j < VEC; ++j) v[j] = 0.f;
+        }
+        if (nat) {
+            if constexpr (VEC == 8) store8(nat + rr * Cfg<T>::KSTR + d0, v);
+            else store4(nat + rr * Cfg<T>::KSTR + d0, v);
+        }
+        if (tr) {
+#pragma unroll
+            for (int j = 0; j < VEC; ++j) tr[(d0 + j) * Cfg<T>::VSTR + rr] = from_f<T>(v[j]);
+        }
+    }
+}
+
+// LePE (depthwise 3x3, window-local zero padding) of window position n for 4 consecutive head
+// channels c0..c0+3; wts = [HD][9] weights + [HD] bias of this head in LDS.
+// sign = +1: sum_t w[t] * img[n + off(t)] + bias (forward conv, cswin:244/265)
+// sign = -1: sum_t w[t] * img[n - off(t)]        (transposed conv = input gradient)
+template <typename T>
+__device__ __forceinline__ void lepe4(const Win& w, int reso, const T* img, int rstride, int ch, int n,
+                                      int c0, const float* wts, int sign, float* acc) {
+    const int iy = n / w.W_sp, ix = n - iy * w.W_sp;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[j] = sign > 0 ? wts[HD * 9 + c0 + j] : 0.f;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+        const int dy = sign * (t / 3 - 1), dx = sign * (t % 3 - 1);
+        const int y = iy + dy, x = ix + dx;
+        if (y < 0 || y >= w.H_sp || x < 0 || x >= w.W_sp) continue;
+        float v[4];
+        load4(img + (size_t)tok_of(w, reso, y * w.W_sp + x) * rstride + ch + c0, v);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[j] += wts[(c0 + j) * 9 + t] * v[j];
+    }
+}
+
+__device__ __forceinline__ void stage_lepe_weights(const csu_stripe_branch& g, int h, float* wts) {
+    for (int i = threadIdx.x; i < HD * 10; i += NT)
+        wts[i] = i < HD * 9 ? g.lepe_w[h * HD * 9 + i] : g.lepe_b[h * HD + i - HD * 9];
+}
+
+__device__ __forceinline__ size_t stat_index(const csu_stripe_args& a, const Win& w, int tok) {
+    const int L = a.reso * a.reso;
+    return ((size_t)(w.br * a.B + w.b) * a.heads + w.h) * L + tok;
+}
+
+// =============================================================================================
+// Forward
+// =============================================================================================
+template <typename T>
+__global__ __launch_bounds__(NT) void stripe_fwd(csu_stripe_args a, const T* __restrict__ qkv,
+                                                 T* __restrict__ out, float* __restrict__ lse) {
+    __shared__ __attribute__((aligned(16))) T Ks[KC * Cfg<T>::KSTR];
+    __shared__ __attribute__((aligned(16))) T Vt[HD * Cfg<T>::VSTR];
+    __shared__ float wts[HD * 10];
+
+    const Win w = decode_block(a);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int r = lane & 31, h = lane >> 5;
+    const int L = a.reso * a.reso, C = a.C, C3 = 3 * C;
+    const T* img = qkv + (size_t)w.b * L * C3;
+    const int qn = w.blk * QR + wave * 32 + r;
+    const bool qvalid = qn < w.N;
+    const bool wave_active = w.blk * QR + wave * 32 < w.N;
+    const int qtok = qvalid ? tok_of(w, a.reso, qn) : 0;
+
+    stage_lepe_weights(branch(a, w.br), w.h, wts);
+    Frag<T> qf;
+    load_frag(qf, img + (size_t)qtok * C3 + w.chq, h, qvalid);
+
+    const float c = a.scale * kLog2e;
+    float m = -INFINITY, l = 0.f;
+    f32x16 o = {};
+
+    for (int k0 = 0; k0 < w.N; k0 += KC) {
+        __syncthreads();
+        stage_rows<T>(w, a.reso, img, C3, C + w.chq, k0, w.N, Ks, nullptr);
+        stage_rows<T>(w, a.reso, img, C3, 2 * C + w.chq, k0, w.N, nullptr, Vt);
+        __syncthreads();
+        if (!wave_active) continue;
+        const int nk = min(KC, w.N - k0);
+        for (int kb = 0; kb < nk; kb += 32) {
+            f32x16 s = {};
+            mma_rows(s, Ks + kb * Cfg<T>::KSTR, r, h, qf);
+            float bm = -INFINITY;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const bool kv = k0 + kb + crow(i, h) < w.N;
+                s[i] = kv ? s[i] * c : -INFINITY;
+                bm = fmaxf(bm, s[i]);
+            }
+            bm = fmaxf(bm, __shfl_xor(bm, 32, 64));
+            const float mn = fmaxf(m, bm);
+            const float alpha = exp2f(m - mn);
+            m = mn;
+            float ls = 0.f;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                s[i] = exp2f(s[i] - mn);
+                ls += s[i];
+            }
+            l = l * alpha + ls;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) o[i] *= alpha;
+            mma_acc_operand(o, Vt, kb, r, h, s);
+        }
+    }
+    if (!qvalid) return;
+    const float lt = l + __shfl_xor(l, 32, 64);
+    const float inv = 1.f / lt;
+    if (h == 0) lse[stat_index(a, w, qtok)] = (m + log2f(lt)) * kLn2;
+    T* orow = out + ((size_t)w.b * L + qtok) * C + w.chq;
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+        const int d0 = 8 * g4 + 4 * h;   // registers 4*g4..4*g4+3 hold channels d0..d0+3
+        float lp[4];
+        lepe4<T>(w, a.reso, img, C3, 2 * C + w.chq, qn, d0, wts, +1, lp);
+        float v[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = o[4 * g4 + j] * inv + lp[j];
+        store4(orow + d0, v);
+    }
+}
+
+// =============================================================================================
+// Backward, query owner: delta = rowsum(dO * O_attn), dQ
+// =============================================================================================
+template <typename T>
+__global__ __launch_bounds__(NT) void stripe_bwd_dq(csu_stripe_args a, const T* __restrict__ qkv,
+                                                    const T* __restrict__ out, const T* __restrict__ dout,
+                                                    const float* __restrict__ lse, float* __restrict__ delta,
+                                                    T* __restrict__ dqkv) {
+    __shared__ __attribute__((aligned(16))) T Ks[KC * Cfg<T>::KSTR];
+    __shared__ __attribute__((aligned(16))) T Vs[KC * Cfg<T>::KSTR];
+    __shared__ __attribute__((aligned(16))) T Kt[HD * Cfg<T>::VSTR];
+    __shared__ float wts[HD * 10];
+
+    const Win w = decode_block(a);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int r = lane & 31, h = lane >> 5;
+    const int L = a.reso * a.reso, C = a.C, C3 = 3 * C;
+    const T* img = qkv + (size_t)w.b * L * C3;
+    const T* oimg = out + (size_t)w.b * L * C;
+    const T* gimg = dout + (size_t)w.b * L * C;
+    const int qn = w.blk * QR + wave * 32 + r;
+    const bool qvalid = qn < w.N;
+    const bool wave_active = w.blk * QR + wave * 32 < w.N;
+    const int qtok = qvalid ? tok_of(w, a.reso, qn) : 0;
+
+    stage_lepe_weights(branch(a, w.br), w.h, wts);
+    Frag<T> qf, gf;
+    load_frag(qf, img + (size_t)qtok * C3 + w.chq, h, qvalid);
+    load_frag(gf, gimg + (size_t)qtok * C + w.chq, h, qvalid);
+    __syncthreads();
+
+    // delta over this lane's 16 channels (the dO fragment's channels), O_attn = out - lepe
+    float dl = 0.f;
+    if (qvalid) {
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+            const int d0 = sizeof(T) == 2 ? 16 * (g4 >> 1) + 8 * h + 4 * (g4 & 1) : 16 * h + 4 * g4;
+            float lp[4], ov[4];
+            lepe4<T>(w, a.reso, img, C3, 2 * C + w.chq, qn, d0, wts, +1, lp);
+            load4(oimg + (size_t)qtok * C + w.chq + d0, ov);
+            float gv[4];
+            load4(gimg + (size_t)qtok * C + w.chq + d0, gv);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) dl += gv[j] * (ov[j] - lp[j]);
+        }
+    }
+    dl += __shfl_xor(dl, 32, 64);
+    const size_t si = stat_index(a, w, qtok);
+    if (qvalid && h == 0) delta[si] = dl;
+    const float lq = qvalid ? lse[si] * kLog2e : 0.f;
+
+    const float c = a.scale * kLog2e;
+    f32x16 dq = {};
+    for (int k0 = 0; k0 < w.N; k0 += KC) {
+        __syncthreads();
+        stage_rows<T>(w, a.reso, img, C3, C + w.chq, k0, w.N, Ks, Kt);
+        stage_rows<T>(w, a.reso, img, C3, 2 * C + w.chq, k0, w.N, Vs, nullptr);
+        __syncthreads();
+        if (!wave_active) continue;
+        const int nk = min(KC, w.N - k0);
+        for (int kb = 0; kb < nk; kb += 32) {
+            f32x16 s = {}, dp = {};
+            mma_rows(s, Ks + kb * Cfg<T>::KSTR, r, h, qf);
+            mma_rows(dp, Vs + kb * Cfg<T>::KSTR, r, h, gf);
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const bool kv = k0 + kb + crow(i, h) < w.N;
+                const float p = kv ? exp2f(s[i] * c - lq) : 0.f;
+                s[i] = p * (dp[i] - dl);   // dS^T
+            }
+            mma_acc_operand(dq, Kt, kb, r, h, s);
+        }
+    }
+    if (!qvalid) return;
+    T* drow = dqkv + ((size_t)w.b * L + qtok) * C3 + w.chq;
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+        const int d0 = 8 * g4 + 4 * h;
+        float v[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = dq[4 * g4 + j] * a.scale;
+        store4(drow + d0, v);
+    }
+}
+
+// =============================================================================================
+// Backward, key owner: dK, dV (+ LePE input gradient)
+// =============================================================================================
+template <typename T>
+__global__ __launch_bounds__(NT) void stripe_bwd_dkdv(csu_stripe_args a, const T* __restrict__ qkv,
+                                                      const T* __restrict__ dout, const float* __restrict__ lse,
+                                                      const float* __restrict__ delta, T* __restrict__ dqkv) {
+    __shared__ __attribute__((aligned(16))) T Qs[KC * Cfg<T>::KSTR];
+    __shared__ __attribute__((aligned(16))) T Gs[KC * Cfg<T>::KSTR];
+    __shared__ __attribute__((aligned(16))) T Qt[HD * Cfg<T>::VSTR];
+    __shared__ __attribute__((aligned(16))) T Gt[HD * Cfg<T>::VSTR];
+    __shared__ float lse_s[KC], dl_s[KC];
+    __shared__ float wts[HD * 10];
+
+    const Win w = decode_block(a);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int r = lane & 31, h = lane >> 5;
+    const int L = a.reso * a.reso, C = a.C, C3 = 3 * C;
+    const T* img = qkv + (size_t)w.b * L * C3;
+    const T* gimg = dout + (size_t)w.b * L * C;
+    const int kn = w.blk * QR + wave * 32 + r;
+    const bool kvalid = kn < w.N;
+    const bool wave_active = w.blk * QR + wave * 32 < w.N;
+    const int ktok = kvalid ? tok_of(w, a.reso, kn) : 0;
+
+    stage_lepe_weights(branch(a, w.br), w.h, wts);
+    Frag<T> kf, vf;
+    load_frag(kf, img + (size_t)ktok * C3 + C + w.chq, h, kvalid);
+    load_frag(vf, img + (size_t)ktok * C3 + 2 * C + w.chq, h, kvalid);
+
+    const float c = a.scale * kLog2e;
+    f32x16 dk = {}, dv = {};
+    for (int q0 = 0; q0 < w.N; q0 += KC) {
+        __syncthreads();
+        stage_rows<T>(w, a.reso, img, C3, w.chq, q0, w.N, Qs, Qt);
+        stage_rows<T>(w, a.reso, gimg, C, w.chq, q0, w.N, Gs, Gt);
+        for (int i = threadIdx.x; i < KC; i += NT) {
+            const int n = q0 + i;
+            const bool v = n < w.N;
+            const size_t si = stat_index(a, w, v ? tok_of(w, a.reso, n) : 0);
+            lse_s[i] = v ? lse[si] * kLog2e : INFINITY;   // +inf -> p = 0 for padded queries
+            dl_s[i] = v ? delta[si] : 0.f;
+        }
+        __syncthreads();
+        if (!wave_active) continue;
+        const int nq = min(KC, w.N - q0);
+        for (int qb = 0; qb < nq; qb += 32) {
+            f32x16 s = {}, dp = {};
+            mma_rows(s, Qs + qb * Cfg<T>::KSTR, r, h, kf);    // S[q][key]
+            mma_rows(dp, Gs + qb * Cfg<T>::KSTR, r, h, vf);   // dP[q][key]
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int qi = qb + crow(i, h);
+                const float p = exp2f(s[i] * c - lse_s[qi]);
+                s[i] = p;
+                dp[i] = p * (dp[i] - dl_s[qi]);   // dS
+            }
+            mma_acc_operand(dv, Gt, qb, r, h, s);    // dV^T += dO^T P
+            mma_acc_operand(dk, Qt, qb, r, h, dp);   // dK^T += Q^T dS
+        }
+    }
+    if (!kvalid) return;
+    T* drow = dqkv + ((size_t)w.b * L + ktok) * C3 + w.chq;
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+        const int d0 = 8 * g4 + 4 * h;
+        float vk[4], vv[4], lp[4];
+        lepe4<T>(w, a.reso, gimg, C, w.chq, kn, d0, wts, -1, lp);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            vk[j] = dk[4 * g4 + j] * a.scale;
+            vv[j] = dv[4 * g4 + j] + lp[j];
+        }
+        store4(drow + C + d0, vk);
+        store4(drow + 2 * C + d0, vv);
+    }
+}
+
+// =============================================================================================
+// LePE weight/bias gradient: dW[c][t] = sum_q dout[q][c] * V[q + off(t)][c], db[c] = sum_q dout
+// Pass 1: per (branch, token chunk) partial sums (fixed order); pass 2: sum chunks in order.
+// =============================================================================================
+constexpr int WG_CH = 256;   // channel lanes per pass-1 block
+
+template <typename T>
+__global__ __launch_bounds__(NT) void lepe_wgrad_partial(csu_stripe_args a, const T* __restrict__ qkv,
+                                                         const T* __restrict__ dout, int chunk, int nchunks,
+                                                         float* __restrict__ part) {
+    __shared__ float red[NT * 10];
+    const int br = blockIdx.y;
+    const csu_stripe_branch& g = branch(a, br);
+    const int Cb = a.heads * HD;
+    const int L = a.reso * a.reso, C = a.C, C3 = 3 * C;
+    const int cw = min(Cb, WG_CH), tpc = NT / cw;
+    const int tl = threadIdx.x / cw, cl = threadIdx.x % cw;
+    const long t_begin = (long)blockIdx.x * chunk;
+    const long t_end = min((long)a.B * L, t_begin + chunk);
+    for (int cbase = 0; cbase < Cb; cbase += cw) {
+        const int c = cbase + cl;
+        float acc[10];
+#pragma unroll
+        for (int k = 0; k < 10; ++k) acc[k] = 0.f;
+        for (long t = t_begin + tl; t < t_end; t += tpc) {
+            const int b = (int)(t / L), tok = (int)(t % L);
+            const int y = tok / a.reso, x = tok % a.reso;
+            const int iy = y % g.H_sp, ix = x % g.W_sp;
+            const float gv = to_f(dout[((size_t)b * L + tok) * C + g.ch_off + c]);
+            acc[9] += gv;
+            const T* vimg = qkv + (size_t)b * L * C3 + 2 * C + g.ch_off + c;
+#pragma unroll
+            for (int k = 0; k < 9; ++k) {
+                const int dy = k / 3 - 1, dx = k % 3 - 1;
+                if (iy + dy < 0 || iy + dy >= g.H_sp || ix + dx < 0 || ix + dx >= g.W_sp) continue;
+                acc[k] += gv * to_f(vimg[(size_t)((y + dy) * a.reso + x + dx) * C3]);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 10; ++k) red[k * NT + threadIdx.x] = acc[k];
+        __syncthreads();
+        if (tl == 0) {
+            for (int k = 0; k < 10; ++k) {
+                float s = 0.f;
+                for (int j = 0; j < tpc; ++j) s += red[k * NT + j * cw + cl];
+                part[(((size_t)br * nchunks + blockIdx.x) * Cb + c) * 10 + k] = s;
+            }
+        }
+        __syncthreads();
+    }
+}
+
+__global__ void lepe_wgrad_reduce(csu_stripe_args a, int nchunks, const float* __restrict__ part) {
+    const int br = blockIdx.y;
+    const int Cb = a.heads * HD;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;   // (c, k) pair
+    if (i >= Cb * 10) return;
+    const int c = i / 10, k = i % 10;
+    float s = 0.f;
+    for (int j = 0; j < nchunks; ++j) s += part[(((size_t)br * nchunks + j) * Cb + c) * 10 + k];
+    const csu_stripe_branch& g = branch(a, br);
+    if (k < 9) g.lepe_dw[c * 9 + k] = s;
+    else g.lepe_db[c] = s;
+}
+
+int wgrad_chunks(const csu_stripe_args& a, int* chunk) {
+    const long tokens = (long)a.B * a.reso * a.reso;
+    int ch = (int)((tokens + 511) / 512);
+    if (ch < 64) ch = 64;
+    *chunk = ch;
+    return (int)((tokens + ch - 1) / ch);
+}
+
+int validate(const csu_stripe_args* a, int dtype) {
+    if (!a) return fail(CSU_E_ARG, "stripe_attn: null args");
+    if (a->head_dim != HD) return fail(CSU_E_UNSUPPORTED, "stripe_attn: head_dim must be 32");
+    if (dtype != CSU_F32 && dtype != CSU_BF16) return fail(CSU_E_ARG, "stripe_attn: bad dtype");
+    if (a->nbranch < 1 || a->nbranch > 2 || a->B < 1 || a->reso < 1 || a->heads < 1)
+        return fail(CSU_E_ARG, "stripe_attn: bad B/reso/heads/nbranch");
+    if (a->C % 8) return fail(CSU_E_ARG, "stripe_attn: C must be a multiple of 8");
+    for (int i = 0; i < a->nbranch; ++i) {
+        const csu_stripe_branch& g = a->br[i];
+        if (g.H_sp < 1 || g.W_sp < 1 || a->reso % g.H_sp || a->reso % g.W_sp)
+            return fail(CSU_E_ARG, "stripe_attn: resolution not divisible by the stripe window (cswin:204)");
+        if (g.ch_off < 0 || g.ch_off + a->heads * HD > a->C)
+            return fail(CSU_E_ARG, "stripe_attn: branch channels outside C");
+        if (i > 0 && g.H_sp * g.W_sp != a->br[0].H_sp * a->br[0].W_sp)
+            return fail(CSU_E_ARG, "stripe_attn: branches must have equal window size");
+        if (!g.lepe_w || !g.lepe_b) return fail(CSU_E_ARG, "stripe_attn: null LePE weights");
+    }
+    return 0;
+}
+
+dim3 grid_of(const csu_stripe_args& a) {
+    const int N = a.br[0].H_sp * a.br[0].W_sp;
+    const int nwin = (a.reso / a.br[0].H_sp) * (a.reso / a.br[0].W_sp);
+    return dim3(a.B * nwin * a.heads * ((N + QR - 1) / QR), a.nbranch);
+}
+
+}  // namespace
+}  // namespace csu
+
+using namespace csu;
+
+extern "C" int csu_stripe_attn_fwd(const csu_stripe_args* a, int dtype, const void* qkv, void* out,
+                                   float* lse, void* stream) {
+    if (int e = validate(a, dtype)) return e;
+    if (!qkv || !out || !lse) return fail(CSU_E_ARG, "stripe_attn_fwd: null buffer");
+    const dim3 grid = grid_of(*a);
+    if (dtype == CSU_BF16)
+        stripe_fwd<bf16><<<grid, NT, 0, as_stream(stream)>>>(*a, (const bf16*)qkv, (bf16*)out, lse);
+    else
+        stripe_fwd<float><<<grid, NT, 0, as_stream(stream)>>>(*a, (const float*)qkv, (float*)out, lse);
+    return check_launch("stripe_attn_fwd");
+}
+
+extern "C" size_t csu_stripe_attn_bwd_workspace(const csu_stripe_args* a) {
+    if (!a) return 0;
+    int chunk;
+    const int n = wgrad_chunks(*a, &chunk);
+    return (size_t)a->nbranch * n * a->heads * HD * 10 * sizeof(float);
+}
+
+extern "C" int csu_stripe_attn_bwd(const csu_stripe_args* a, int dtype, const void* qkv, const void* out,
+                                   const void* dout, const float* lse, float* delta, void* dqkv,
+                                   void* workspace, size_t workspace_bytes, void* stream) {
+    if (int e = validate(a, dtype)) return e;
+    if (!qkv || !out || !dout || !lse || !delta || !dqkv) return fail(CSU_E_ARG, "stripe_attn_bwd: null buffer");
+    for (int i = 0; i < a->nbranch; ++i)
+        if (!a->br[i].lepe_dw || !a->br[i].lepe_db) return fail(CSU_E_ARG, "stripe_attn_bwd: null LePE grads");
+    if (workspace_bytes < csu_stripe_attn_bwd_workspace(a) || !workspace)
+        return fail(CSU_E_WORKSPACE, "stripe_attn_bwd: workspace too small");
+    hipStream_t st = as_stream(stream);
+    const dim3 grid = grid_of(*a);
+    int chunk;
+    const int nch = wgrad_chunks(*a, &chunk);
+    float* part = (float*)workspace;
+    const int Cb = a->heads * HD;
+    const dim3 rgrid((Cb * 10 + 255) / 256, a->nbranch);
+    if (dtype == CSU_BF16) {
+        stripe_bwd_dq<bf16><<<grid, NT, 0, st>>>(*a, (const bf16*)qkv, (const bf16*)out, (const bf16*)dout, lse, delta, (bf16*)dqkv);
+        stripe_bwd_dkdv<bf16><<<grid, NT, 0, st>>>(*a, (const bf16*)qkv, (const bf16*)dout, lse, delta, (bf16*)dqkv);
+        lepe_wgrad_partial<bf16><<<dim3(nch, a->nbranch), NT, 0, st>>>(*a, (const bf16*)qkv, (const bf16*)dout, chunk, nch, part);
+    } else {
+        stripe_bwd_dq<float><<<grid, NT, 0, st>>>(*a, (const float*)qkv, (const float*)out, (const float*)dout, lse, delta, (float*)dqkv);
+        stripe_bwd_dkdv<float><<<grid, NT, 0, st>>>(*a, (const float*)qkv, (const float*)dout, lse, delta, (float*)dqkv);
+        lepe_wgrad_partial<float><<<dim3(nch, a->nbranch), NT, 0, st>>>(*a, (const float*)qkv, (const float*)dout, chunk, nch, part);
+    }
+    lepe_wgrad_reduce<<<rgrid, 256, 0, st>>>(*a, nch, part);
+    return check_launch("stripe_attn_bwd");
+}

@@ -1,0 +1,103 @@
+"""ctypes binding of libcsu_hip.so (C ABI declared in include/csu.h).
+
+torch is imported first on purpose: it loads its bundled HIP runtime (soname libamdhip64.so.7),
+and the dynamic loader then resolves our library's DT_NEEDED to that same runtime, so torch's
+device pointers and streams are valid for our kernels.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch  # noqa: F401  (must precede the dlopen, see module docstring)
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libcsu_hip.so")
+
+c_int32, c_float, c_void_p, c_size_t = ctypes.c_int32, ctypes.c_float, ctypes.c_void_p, ctypes.c_size_t
+
+CSU_F32, CSU_BF16 = 0, 1
+
+
+class StripeBranch(ctypes.Structure):
+    _fields_ = [("H_sp", c_int32), ("W_sp", c_int32), ("ch_off", c_int32), ("_pad", c_int32),
+                ("lepe_w", c_void_p), ("lepe_b", c_void_p), ("lepe_dw", c_void_p), ("lepe_db", c_void_p)]
+
+
+class StripeArgs(ctypes.Structure):
+    _fields_ = [("B", c_int32), ("reso", c_int32), ("C", c_int32), ("heads", c_int32), ("head_dim", c_int32),
+                ("nbranch", c_int32), ("scale", c_float), ("_pad", c_int32), ("br", StripeBranch * 2)]
+
+
+# name -> (restype, argtypes); mirrors include/csu.h
+_SIGS = {
+    "csu_last_error_string": (ctypes.c_char_p, []),
+    "csu_build_info": (ctypes.c_char_p, []),
+    "csu_stripe_attn_fwd": (ctypes.c_int, [ctypes.POINTER(StripeArgs), ctypes.c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "csu_stripe_attn_bwd_workspace": (c_size_t, [ctypes.POINTER(StripeArgs)]),
+    "csu_stripe_attn_bwd": (ctypes.c_int, [ctypes.POINTER(StripeArgs), ctypes.c_int, c_void_p, c_void_p, c_void_p,
+                                           c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "csu_layernorm_fwd": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, c_float, ctypes.c_int, c_void_p, c_void_p, c_void_p,
+                                         ctypes.c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "csu_layernorm_bwd_workspace": (c_size_t, [ctypes.c_int, ctypes.c_int]),
+    "csu_layernorm_bwd": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                                         ctypes.c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,
+                                         c_void_p]),
+    "csu_simam_workspace": (c_size_t, [ctypes.c_int, ctypes.c_int, ctypes.c_int]),
+    "csu_simam_fwd": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, c_float, ctypes.c_int, c_void_p, c_void_p,
+                                     c_void_p, c_void_p, c_size_t, c_void_p]),
+    "csu_simam_bwd": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_void_p, c_void_p, c_void_p,
+                                     c_void_p, c_void_p, c_size_t, c_void_p]),
+}
+
+_lib = None
+_lock = threading.Lock()
+
+
+class CsuError(RuntimeError):
+    pass
+
+
+def lib():
+    """The loaded library; raises loudly when it has not been built (no fallback exists)."""
+    global _lib
+    if _lib is None:
+        with _lock:
+            if _lib is None:
+                if not os.path.exists(LIB_PATH):
+                    raise CsuError(f"libcsu_hip.so not built ({LIB_PATH}); run `python __graft_entry__.py build` "
+                                   "or `make -C cswin-simam-unet_amd/csrc`")
+                L = ctypes.CDLL(LIB_PATH)
+                for name, (res, args) in _SIGS.items():
+                    fn = getattr(L, name)
+                    fn.restype, fn.argtypes = res, args
+                _lib = L
+    return _lib
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        msg = lib().csu_last_error_string().decode(errors="replace")
+        raise CsuError(f"{what} failed (code {rc}): {msg}")
+
+
+def dtype_code(t: torch.Tensor) -> int:
+    if t.dtype == torch.float32:
+        return CSU_F32
+    if t.dtype == torch.bfloat16:
+        return CSU_BF16
+    raise CsuError(f"unsupported dtype {t.dtype} (float32 or bfloat16)")
+
+
+def ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def stream_ptr(device=None):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def require_device(*ts: torch.Tensor):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise CsuError("csu kernels run on the MI355X only: got a CPU tensor (there is no CPU fallback)")

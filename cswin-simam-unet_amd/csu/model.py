@@ -1,0 +1,373 @@
+"""Drop-in nn.Modules of the CSWin-(SimAM-)UNet (train_cswinunet_segmentation.py cswin:180-688).
+
+Class names, constructor signatures, parameter registration order and therefore state_dict keys
+are those of the reference, so reference ``.pth`` files load unchanged (cswin:992) and
+``model.apply(model._init_weights)`` reproduces the reference initialisation (cswin:605-614).
+Forward passes run the hand-written gfx950 kernels of libcsu_hip.so (``csu.ops``) on
+token-major (B, L, C) = NHWC activations; the dense projections (qkv/proj/fc1/fc2/concat_linear)
+and the remaining convolutions run on the platform GEMM/conv libraries (hipBLASLt/MIOpen).
+
+Precision policy (bf16 under ``torch.autocast('cuda', torch.bfloat16)``, the BASELINE setting):
+residual stream fp32; LayerNorm emits the GEMM's input dtype directly; attention, MLP and
+upsampling activations bf16; softmax/LN statistics and all reductions fp32; loss head fp32.
+"""
+from __future__ import annotations
+
+import math
+from typing import List, Optional
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import ops
+from .simam import SimAM
+
+
+def _compute_dtype(x: torch.Tensor) -> torch.dtype:
+    if x.is_cuda and torch.is_autocast_enabled("cuda"):
+        return torch.get_autocast_dtype("cuda")
+    return x.dtype
+
+
+def trunc_normal_(t, std=1.0, a=-2.0, b=2.0):
+    """timm.models.layers.trunc_normal_ semantics (cswin:14, 609): absolute cut-offs a, b."""
+    return nn.init.trunc_normal_(t, mean=0.0, std=std, a=a, b=b)
+
+
+class DropPath(nn.Module):
+    """Stochastic depth (timm DropPath, cswin:344): per-sample Bernoulli(keep)/keep in training."""
+
+    def __init__(self, drop_prob: float = 0.0):
+        super().__init__()
+        self.drop_prob = drop_prob
+
+    def forward(self, x):
+        if self.drop_prob == 0.0 or not self.training:
+            return x
+        keep = 1.0 - self.drop_prob
+        mask = x.new_empty((x.shape[0],) + (1,) * (x.ndim - 1)).bernoulli_(keep)
+        return x * mask / keep
+
+
+def _ln(x: torch.Tensor, norm: nn.LayerNorm, out_dtype=None) -> torch.Tensor:
+    return ops.layer_norm(x, norm.weight, norm.bias, norm.eps, out_dtype)
+
+
+def _tokens_as_nchw(x: torch.Tensor) -> torch.Tensor:
+    """(B, L, C) token tensor viewed (no copy) as a channels_last NCHW tensor."""
+    B, L, C = x.shape
+    H = W = int(math.isqrt(L))
+    return x.transpose(1, 2).reshape(B, C, H, W)
+
+
+def _nchw_as_tokens(x: torch.Tensor) -> torch.Tensor:
+    B, C = x.shape[:2]
+    return x.reshape(B, C, -1).transpose(1, 2)
+
+
+class Mlp(nn.Module):
+    """fc1 -> GELU(erf) -> Dropout -> fc2 -> Dropout (cswin:180-196)."""
+
+    def __init__(self, in_features, hidden_features=None, out_features=None, act_layer=nn.GELU, drop=0.0):
+        super().__init__()
+        out_features = out_features or in_features
+        hidden_features = hidden_features or in_features
+        self.fc1 = nn.Linear(in_features, hidden_features)
+        self.act = act_layer()
+        self.fc2 = nn.Linear(hidden_features, out_features)
+        self.drop = nn.Dropout(drop)
+
+    def forward(self, x):
+        return self.drop(self.fc2(self.drop(self.act(self.fc1(x)))))
+
+
+def img2windows(img: torch.Tensor, H_sp: int, W_sp: int) -> torch.Tensor:
+    """(B, C, H, W) -> (B*nWin, H_sp*W_sp, C) (cswin:199-206).  Layout utility kept for API
+    compatibility; the hot path never materialises windows (the kernels gather by index)."""
+    B, C, H, W = img.shape
+    t = img.reshape(B, C, H // H_sp, H_sp, W // W_sp, W_sp)
+    return t.permute(0, 2, 4, 3, 5, 1).reshape(-1, H_sp * W_sp, C)
+
+
+def windows2img(img_splits_hw: torch.Tensor, H_sp: int, W_sp: int, H: int, W: int) -> torch.Tensor:
+    """(B*nWin, H_sp*W_sp, C) -> (B, H, W, C) (cswin:209-217)."""
+    B = int(img_splits_hw.shape[0] / (H * W / H_sp / W_sp))
+    t = img_splits_hw.reshape(B, H // H_sp, W // W_sp, H_sp, W_sp, -1)
+    return t.permute(0, 1, 3, 2, 4, 5).reshape(B, H, W, -1)
+
+
+class LePEAttention(nn.Module):
+    """Stripe-window MHSA + LePE (cswin:220-298).  forward(qkv (3, B, L, C)) -> (B, L, C)."""
+
+    def __init__(self, dim, resolution, idx, split_size, dim_out=None, num_heads=9, attn_drop=0.0,
+                 proj_drop=0.0, qk_scale=None):
+        super().__init__()
+        self.dim = dim
+        self.dim_out = dim_out or dim
+        self.resolution = resolution
+        self.split_size = split_size
+        self.num_heads = num_heads
+        self.idx = idx
+        head_dim = dim // num_heads
+        self.scale = qk_scale or head_dim ** -0.5
+        if idx == -1:
+            H_sp, W_sp = resolution, resolution
+        elif idx == 0:
+            H_sp, W_sp = resolution, split_size
+        elif idx == 1:
+            W_sp, H_sp = resolution, split_size
+        else:
+            raise ValueError(f"ERROR MODE {idx}")   # the reference prints and exit(0)s (cswin:239-240)
+        self.H_sp, self.W_sp = H_sp, W_sp
+        self.get_v = nn.Conv2d(dim, dim, kernel_size=3, stride=1, padding=1, groups=dim)
+        self.attn_drop_p = attn_drop
+        self.attn_drop = nn.Dropout(attn_drop)
+
+    def forward(self, qkv):
+        if self.training and self.attn_drop_p > 0:
+            raise NotImplementedError("attention dropout inside the fused stripe kernel is not implemented yet")
+        _, B, L, C = qkv.shape
+        packed = torch.cat([qkv[0], qkv[1], qkv[2]], dim=-1)
+        geom = ops.StripeGeometry(self.resolution, C, self.num_heads, [(self.H_sp, self.W_sp, 0)], self.scale)
+        return ops.stripe_attention(packed, geom, [self.get_v.weight], [self.get_v.bias])
+
+
+class CSWinBlock(nn.Module):
+    """Pre-LN CSWin block (cswin:301-370); both stripe branches run in one fused launch."""
+
+    def __init__(self, dim, reso, num_heads, split_size, mlp_ratio=4.0, qkv_bias=False, qk_scale=None, drop=0.0,
+                 attn_drop=0.0, drop_path=0.0, act_layer=nn.GELU, norm_layer=nn.LayerNorm, last_stage=False):
+        super().__init__()
+        self.dim = dim
+        self.num_heads = num_heads
+        self.patches_resolution = reso
+        self.split_size = split_size
+        self.mlp_ratio = mlp_ratio
+        self.qkv = nn.Linear(dim, dim * 3, bias=qkv_bias)
+        self.norm1 = norm_layer(dim)
+        if self.patches_resolution == split_size:
+            last_stage = True
+        self.branch_num = 1 if last_stage else 2
+        self.proj = nn.Linear(dim, dim)
+        self.proj_drop = nn.Dropout(drop)          # built but never applied, as in cswin:324/366
+        if last_stage:
+            self.attns = nn.ModuleList([LePEAttention(dim, resolution=reso, idx=-1, split_size=split_size,
+                                                      num_heads=num_heads, dim_out=dim, qk_scale=qk_scale,
+                                                      attn_drop=attn_drop, proj_drop=drop)])
+        else:
+            self.attns = nn.ModuleList([LePEAttention(dim // 2, resolution=reso, idx=i, split_size=split_size,
+                                                      num_heads=num_heads // 2, dim_out=dim // 2, qk_scale=qk_scale,
+                                                      attn_drop=attn_drop, proj_drop=drop)
+                                        for i in range(self.branch_num)])
+        mlp_hidden_dim = int(dim * mlp_ratio)
+        self.drop_path = DropPath(drop_path) if drop_path > 0.0 else nn.Identity()
+        self.mlp = Mlp(in_features=dim, hidden_features=mlp_hidden_dim, out_features=dim, act_layer=act_layer, drop=drop)
+        self.norm2 = norm_layer(dim)
+        a0 = self.attns[0]
+        offs = [0] if last_stage else [0, dim // 2]
+        self._geom = ops.StripeGeometry(reso, dim, a0.num_heads,
+                                        [(a.H_sp, a.W_sp, o) for a, o in zip(self.attns, offs)], a0.scale,
+                                        head_dim=a0.dim // a0.num_heads)
+
+    def forward(self, x):
+        H = W = self.patches_resolution
+        B, L, C = x.shape
+        assert L == H * W, "flatten img_tokens has wrong size"
+        if self.training and self.attns[0].attn_drop_p > 0:
+            raise NotImplementedError("attention dropout inside the fused stripe kernel is not implemented yet")
+        cd = _compute_dtype(x)
+        qkv = self.qkv(_ln(x, self.norm1, cd))
+        att = ops.stripe_attention(qkv, self._geom, [a.get_v.weight for a in self.attns],
+                                   [a.get_v.bias for a in self.attns])
+        x = x + self.drop_path(self.proj(att))
+        x = x + self.drop_path(self.mlp(_ln(x, self.norm2, cd)))
+        return x
+
+
+class Merge_Block(nn.Module):
+    """Conv3x3 s2 p1 (C -> C') + LayerNorm (cswin:373-388)."""
+
+    def __init__(self, dim, dim_out, norm_layer=nn.LayerNorm):
+        super().__init__()
+        self.conv = nn.Conv2d(dim, dim_out, 3, 2, 1)
+        self.norm = norm_layer(dim_out)
+
+    def forward(self, x):
+        B, new_HW, C = x.shape
+        y = self.conv(_tokens_as_nchw(x))
+        return _ln(_nchw_as_tokens(y), self.norm, torch.float32 if y.dtype == torch.bfloat16 else y.dtype)
+
+
+class CARAFE(nn.Module):
+    """Content-aware reassembly upsampling (cswin:391-437).  forward((B, L, C)) -> (B, s^2 L, C_out)."""
+
+    def __init__(self, dim, dim_out, kernel_size=3, up_factor=2):
+        super().__init__()
+        self.kernel_size = kernel_size
+        self.up_factor = up_factor
+        self.down = nn.Conv2d(dim, dim // 4, 1)
+        self.encoder = nn.Conv2d(dim // 4, self.up_factor ** 2 * self.kernel_size ** 2, self.kernel_size, 1,
+                                 self.kernel_size // 2)
+        self.out = nn.Conv2d(dim, dim_out, 1)
+
+    def forward(self, x):
+        B, L, C = x.shape
+        H = W = int(math.isqrt(L))
+        s, k = self.up_factor, self.kernel_size
+        xi = _tokens_as_nchw(x)
+        kern = self.encoder(self.down(xi))                                   # (B, 9 s^2, H, W)
+        kern = kern.reshape(B, k * k, s, s, H, W).softmax(dim=1)            # (b, tap, i, j, y, x)
+        nb = F.unfold(xi, k, padding=k // 2).reshape(B, C, k * k, H, W)
+        o = torch.einsum("btijhw,bcthw->bhiwjc", kern.to(nb.dtype), nb).reshape(B, H * s * W * s, C)
+        return F.linear(o, self.out.weight.reshape(self.out.weight.shape[0], C), self.out.bias)
+
+
+class CARAFE4(CARAFE):
+    """CARAFE with up_factor 4 (cswin:440-486)."""
+
+    def __init__(self, dim, dim_out, kernel_size=3, up_factor=4):
+        super().__init__(dim, dim_out, kernel_size, up_factor)
+
+
+class CSWinTransformer(nn.Module):
+    """CSWin-Transformer U-Net with CARAFE upsampling (cswin:489-688).
+
+    Extra (not in the reference): ``simam=True`` applies the parameter-free SimAM gate to the
+    skip features x1/x2/x3 before the concat_linear fusions; the default False
+    is exact reference behaviour.  State_dict keys are unchanged either way."""
+
+    def __init__(self, img_size=224, patch_size=16, in_chans=3, num_classes=1, embed_dim=64, depth=[1, 2, 9, 1],
+                 split_size=[1, 2, 7, 7], num_heads=[2, 4, 8, 16], mlp_ratio=4.0, qkv_bias=True, qk_scale=None,
+                 drop_rate=0.0, attn_drop_rate=0.0, drop_path_rate=0.0, hybrid_backbone=None,
+                 norm_layer=nn.LayerNorm, use_chk=False, simam=False):
+        super().__init__()
+        self.use_chk = use_chk
+        self.num_classes = num_classes
+        self.num_features = self.embed_dim = embed_dim
+        self.img_size = img_size
+        heads = num_heads
+        self.stage1_conv_embed = nn.Sequential(nn.Conv2d(in_chans, embed_dim, 7, 4, 2), _TokensRearrange(img_size // 4),
+                                               nn.LayerNorm(embed_dim))
+        curr_dim = embed_dim
+        self.pos_drop = nn.Dropout(p=drop_rate)
+        dpr = [x.item() for x in torch.linspace(0, drop_path_rate, int(np.sum(depth)))]
+
+        def blocks(dim, reso, nh, sp, dps, last=False):
+            return nn.ModuleList([CSWinBlock(dim=dim, num_heads=nh, reso=reso, mlp_ratio=mlp_ratio, qkv_bias=qkv_bias,
+                                             qk_scale=qk_scale, split_size=sp, drop=drop_rate, attn_drop=attn_drop_rate,
+                                             drop_path=dp, norm_layer=norm_layer, last_stage=last) for dp in dps])
+
+        d0, d1, d2 = int(np.sum(depth[:1])), int(np.sum(depth[:2])), int(np.sum(depth[:-1]))
+        self.stage1 = blocks(curr_dim, img_size // 4, heads[0], split_size[0], dpr[:depth[0]])
+        self.merge1 = Merge_Block(curr_dim, curr_dim * 2)
+        curr_dim *= 2
+        self.stage2 = blocks(curr_dim, img_size // 8, heads[1], split_size[1], dpr[d0:d0 + depth[1]])
+        self.merge2 = Merge_Block(curr_dim, curr_dim * 2)
+        curr_dim *= 2
+        self.stage3 = blocks(curr_dim, img_size // 16, heads[2], split_size[2], dpr[d1:d1 + depth[2]])
+        self.merge3 = Merge_Block(curr_dim, curr_dim * 2)
+        curr_dim *= 2
+        self.stage4 = blocks(curr_dim, img_size // 32, heads[3], split_size[-1], dpr[d2:d2 + depth[-1]], last=True)
+        self.norm = norm_layer(curr_dim)
+        # decoder (reuses the encoder drop-path indices, cswin:562/574/587/598)
+        self.stage_up4 = blocks(curr_dim, img_size // 32, heads[3], split_size[-1], dpr[d2:d2 + depth[-1]], last=True)
+        self.upsample4 = CARAFE(curr_dim, curr_dim // 2)
+        curr_dim //= 2
+        self.concat_linear4 = nn.Linear(512, 256)
+        self.stage_up3 = blocks(curr_dim, img_size // 16, heads[2], split_size[2], dpr[d1:d1 + depth[2]])
+        self.upsample3 = CARAFE(curr_dim, curr_dim // 2)
+        curr_dim //= 2
+        self.concat_linear3 = nn.Linear(256, 128)
+        self.stage_up2 = blocks(curr_dim, img_size // 8, heads[1], split_size[1], dpr[d0:d0 + depth[1]])
+        self.upsample2 = CARAFE(curr_dim, curr_dim // 2)
+        curr_dim //= 2
+        self.concat_linear2 = nn.Linear(128, 64)
+        self.stage_up1 = blocks(curr_dim, img_size // 4, heads[0], split_size[0], dpr[:depth[0]])
+        self.upsample1 = CARAFE4(curr_dim, 64)
+        self.norm_up = norm_layer(embed_dim)
+        self.output = nn.Conv2d(in_channels=embed_dim, out_channels=self.num_classes, kernel_size=1, bias=False)
+        self.simam = SimAM() if simam else None
+        self.apply(self._init_weights)
+
+    def _init_weights(self, m):
+        if isinstance(m, nn.Linear):
+            trunc_normal_(m.weight, std=0.02)
+            if m.bias is not None:
+                nn.init.constant_(m.bias, 0)
+        elif isinstance(m, (nn.LayerNorm, nn.BatchNorm2d)):
+            nn.init.constant_(m.bias, 0)
+            nn.init.constant_(m.weight, 1.0)
+
+    @torch.jit.ignore
+    def no_weight_decay(self):
+        return {"pos_embed", "cls_token"}
+
+    @torch.jit.ignore
+    def no_weight_decay_keywords(self):
+        return {"relative_position_bias_table"}
+
+    def _skip(self, t):
+        return self.simam(t) if self.simam is not None else t
+
+    def forward_features(self, x):
+        conv, _, ln = self.stage1_conv_embed
+        y = conv(x.contiguous(memory_format=torch.channels_last))
+        x = _ln(_nchw_as_tokens(y), ln, torch.float32 if y.dtype == torch.bfloat16 else y.dtype)
+        x = self.pos_drop(x)
+        for blk in self.stage1:
+            x = blk(x)
+        self.x1 = x
+        x = self.merge1(x)
+        for blk in self.stage2:
+            x = blk(x)
+        self.x2 = x
+        x = self.merge2(x)
+        for blk in self.stage3:
+            x = blk(x)
+        self.x3 = x
+        x = self.merge3(x)
+        for blk in self.stage4:
+            x = blk(x)
+        return _ln(x, self.norm)
+
+    def forward_up_features(self, x):
+        for blk in self.stage_up4:
+            x = blk(x)
+        x = self.concat_linear4(torch.cat([self._skip(self.x3), self.upsample4(x)], -1))
+        for blk in self.stage_up3:
+            x = blk(x)
+        x = self.concat_linear3(torch.cat([self._skip(self.x2), self.upsample3(x)], -1))
+        for blk in self.stage_up2:
+            x = blk(x)
+        x = self.concat_linear2(torch.cat([self._skip(self.x1), self.upsample2(x)], -1))
+        for blk in self.stage_up1:
+            x = blk(x)
+        return _ln(x, self.norm_up, _compute_dtype(x))
+
+    def up_x4(self, x):
+        B, new_HW, C = x.shape
+        H = W = int(math.isqrt(new_HW))
+        x = self.upsample1(x)                                             # (B, 16 L, 64) tokens
+        w = self.output.weight.reshape(self.num_classes, -1)
+        logits = F.linear(x, w)                                           # 1x1 conv, no bias
+        return logits.transpose(1, 2).reshape(B, self.num_classes, 4 * H, 4 * W)
+
+    def forward(self, x):
+        x = self.forward_features(x)
+        x = self.forward_up_features(x)
+        x = self.up_x4(x)
+        return torch.sigmoid(x.float())
+
+
+class _TokensRearrange(nn.Module):
+    """einops Rearrange('b c h w -> b (h w) c', h=w=reso) (cswin:506); no parameters."""
+
+    def __init__(self, reso):
+        super().__init__()
+        self.reso = reso
+
+    def forward(self, x):
+        assert x.shape[2] == self.reso and x.shape[3] == self.reso
+        return _nchw_as_tokens(x)

@@ -1,0 +1,137 @@
+"""Training-step API of the reference (train_cswinunet_segmentation.py cswin:692-841).
+
+Same names, arguments and return values as the reference's ``dice_coefficient``, ``iou_score``,
+``evaluate_model`` and ``train_model``.  Differences are performance-only: per-batch metrics are
+accumulated on the device and synchronised once per epoch instead of four ``.item()`` host syncs
+per step (cswin:698, 708, 797, 803), and under ``torch.distributed`` the metric sums are
+all-reduced so every rank (and the LR scheduler) sees the global values.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional
+
+import torch
+import torch.distributed as dist
+import torch.nn.functional as F
+
+try:
+    from tqdm import tqdm
+except ImportError:  # pragma: no cover
+    tqdm = None
+
+
+def bce_loss(prob: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
+    """nn.BCELoss() (mean; log clamped at -100) computed in fp32 (cswin:936)."""
+    return F.binary_cross_entropy(prob.float(), target.float())
+
+
+def _dice_t(pred, target, smooth=1e-6):
+    pred, target = pred.reshape(-1), target.reshape(-1)
+    inter = (pred * target).sum()
+    return (2.0 * inter + smooth) / (pred.sum() + target.sum() + smooth)
+
+
+def _iou_t(pred, target, smooth=1e-6):
+    pred, target = pred.reshape(-1), target.reshape(-1)
+    inter = (pred * target).sum()
+    return (inter + smooth) / (pred.sum() + target.sum() - inter + smooth)
+
+
+def dice_coefficient(pred, target, smooth=1e-6) -> float:
+    """Batch-flattened Dice (cswin:692-698)."""
+    return _dice_t(pred, target, smooth).item()
+
+
+def iou_score(pred, target, smooth=1e-6) -> float:
+    """Batch-flattened IoU (cswin:701-708)."""
+    return _iou_t(pred, target, smooth).item()
+
+
+def _world():
+    return dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+
+
+def _global_mean(t: torch.Tensor) -> torch.Tensor:
+    if _world() > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        t = t / _world()
+    return t
+
+
+def evaluate_model(model, data_loader, criterion, device):
+    """eval mode, no grad; mean over batches of (loss, Dice, IoU) (cswin:712-747)."""
+    model.eval()
+    acc = torch.zeros(3, dtype=torch.float64, device=device)
+    n = 0
+    with torch.no_grad():
+        for images, masks in data_loader:
+            images = images.to(device, non_blocking=True)
+            masks = masks.to(device, non_blocking=True)
+            outputs = model(images)
+            loss = criterion(outputs, masks)
+            preds = (outputs > 0.5).float()
+            acc += torch.stack([loss.detach().double(), _dice_t(preds, masks).double(), _iou_t(preds, masks).double()])
+            n += 1
+    acc = _global_mean(acc / max(n, 1))
+    loss, dice, iou = acc.tolist()
+    return loss, dice, iou
+
+
+def train_step(model, images, masks, criterion, optimizer):
+    """One reference step (cswin:779-794): zero_grad, forward, loss, backward, optimizer step,
+    thresholded metrics.  Returns device tensors (loss, dice, iou) -- no host sync."""
+    optimizer.zero_grad(set_to_none=True)
+    outputs = model(images)
+    loss = criterion(outputs, masks)
+    loss.backward()
+    optimizer.step()
+    with torch.no_grad():
+        preds = (outputs > 0.5).float()
+        return loss.detach(), _dice_t(preds, masks), _iou_t(preds, masks)
+
+
+def train_model(model, train_loader, test_loader, criterion, optimizer, scheduler, device, num_epochs=100,
+                verbose: bool = True) -> Dict[str, List[float]]:
+    """Epoch loop with per-epoch history and ReduceLROnPlateau on the test loss (cswin:751-841)."""
+    history = {"train_loss": [], "train_dice": [], "train_iou": [], "test_loss": [], "test_dice": [], "test_iou": [],
+               "learning_rates": []}
+    rank0 = not (dist.is_available() and dist.is_initialized()) or dist.get_rank() == 0
+    for epoch in range(num_epochs):
+        model.train()
+        acc = torch.zeros(3, dtype=torch.float64, device=device)
+        it = train_loader
+        if verbose and rank0 and tqdm is not None:
+            it = tqdm(train_loader, desc=f"Epoch {epoch + 1}/{num_epochs} [TRAIN]")
+        nb = 0
+        for images, masks in it:
+            images = images.to(device, non_blocking=True)
+            masks = masks.to(device, non_blocking=True)
+            l, d, i = train_step(model, images, masks, criterion, optimizer)
+            acc += torch.stack([l.double(), d.double(), i.double()])
+            nb += 1
+        acc = _global_mean(acc / max(nb, 1))
+        train_loss, train_dice, train_iou = acc.tolist()
+        test_loss, test_dice, test_iou = evaluate_model(model, test_loader, criterion, device)
+        if scheduler is not None:
+            scheduler.step(test_loss)
+        current_lr = optimizer.param_groups[0]["lr"]
+        for k, v in zip(history, (train_loss, train_dice, train_iou, test_loss, test_dice, test_iou, current_lr)):
+            history[k].append(v)
+        if verbose and rank0:
+            print(f'\n{"=" * 70}\nEpoch {epoch + 1}/{num_epochs}:')
+            print(f"  [TRAIN] Loss: {train_loss:.4f} | Dice: {train_dice:.4f} | IoU: {train_iou:.4f}")
+            print(f"  [TEST]  Loss: {test_loss:.4f} | Dice: {test_dice:.4f} | IoU: {test_iou:.4f}")
+            print(f'  [LR]    Learning Rate: {current_lr:.6f}\n{"=" * 70}\n')
+    return history
+
+
+def make_optimizer(model, lr=1e-4, weight_decay=1e-4):
+    """AdamW as in cswin:937-941 (fused multi-tensor implementation on the device)."""
+    kw = {"fused": True} if next(model.parameters()).is_cuda else {}
+    return torch.optim.AdamW(model.parameters(), lr=lr, weight_decay=weight_decay, **kw)
+
+
+def make_scheduler(optimizer, factor=0.5, patience=5, min_lr=1e-7):
+    """ReduceLROnPlateau of cswin:944-951 without the ``verbose`` kwarg torch 2.10 rejects."""
+    return torch.optim.lr_scheduler.ReduceLROnPlateau(optimizer, mode="min", factor=factor, patience=patience,
+                                                      min_lr=min_lr)

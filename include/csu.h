@@ -1,0 +1,109 @@
+/*
+ * csu.h -- C ABI of libcsu_hip.so, the MI355X (gfx950) kernels of the CSWin-(SimAM-)UNet
+ * training path.  Plain pointers, int sizes and a hipStream_t passed as void*; no framework
+ * types.  Every buffer is owned by the caller (the library never allocates); every call is
+ * asynchronous on `stream` and reentrant.  Return 0 on success, a positive hipError_t, or a
+ * negative CSU_E* code; csu_last_error_string() describes the last failure of the calling thread.
+ *
+ * Layout convention: activations are token-major "(B, L, C)" = NHWC with L = H*W, exactly the
+ * reference's token layout (train_cswinunet_segmentation.py, the `B, L, C` tensors of
+ * cswin:349-370), so no NCHW transposes are needed between ops.
+ *
+ * The reference has no FFI (it is pure PyTorch); each entry point below names the reference
+ * operator it replaces (cswin:N = train_cswinunet_segmentation.py line N,
+ * unet:N = train_unet_segmentation.py line N).  The Python binding is csu/_lib.py (ctypes).
+ */
+#ifndef CSU_H_
+#define CSU_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum csu_dtype { CSU_F32 = 0, CSU_BF16 = 1 };
+
+enum csu_status {
+    CSU_OK = 0,
+    CSU_E_ARG = -1,       /* invalid argument (shape, dtype, null pointer) */
+    CSU_E_UNSUPPORTED = -2,
+    CSU_E_WORKSPACE = -3  /* workspace too small */
+};
+
+const char* csu_last_error_string(void);
+/* Library version and the offload arch it was built for ("gfx950"). */
+const char* csu_build_info(void);
+
+/* ---------------------------------------------------------------------------------------
+ * Cross-shaped stripe attention with LePE (LePEAttention.forward, cswin:271-298, geometry
+ * cswin:232-240, get_v depthwise 3x3 cswin:244/256-269; branch split + concat of
+ * CSWinBlock.forward cswin:358-363).  One call runs every branch of a CSWinBlock: branch i
+ * reads its Q/K/V channels [ch_off, ch_off + heads*head_dim) of the (B, L, 3C) qkv Linear
+ * output and writes the same channels of the (B, L, C) output (the torch.cat is free).
+ * ------------------------------------------------------------------------------------- */
+typedef struct {
+    int32_t H_sp, W_sp;      /* stripe window: idx0 (reso, sw), idx1 (sw, reso), idx-1 (reso, reso) */
+    int32_t ch_off;          /* first channel of this branch inside C (0 or C/2) */
+    int32_t _pad;
+    const float* lepe_w;     /* get_v.weight (C_b, 1, 3, 3), fp32 master weight */
+    const float* lepe_b;     /* get_v.bias (C_b), fp32 */
+    float* lepe_dw;          /* backward: written (not accumulated) gradient of lepe_w */
+    float* lepe_db;          /* backward: gradient of lepe_b */
+} csu_stripe_branch;
+
+typedef struct {
+    int32_t B, reso, C;      /* L = reso*reso tokens; qkv rows are 3C wide, output rows C wide */
+    int32_t heads;           /* heads per branch (num_heads/2, or num_heads for the last stage) */
+    int32_t head_dim;        /* must be 32 (embed_dim is hard-wired to 64: SURVEY §0.5) */
+    int32_t nbranch;         /* 1 (last stage, idx -1) or 2 (idx 0 and idx 1) */
+    float scale;             /* qk_scale or head_dim**-0.5 (cswin:231) */
+    int32_t _pad;
+    csu_stripe_branch br[2];
+} csu_stripe_args;
+
+/* out (B, L, C) dtype; lse fp32 [nbranch][B][heads][L] (softmax log-sum-exp, saved for bwd). */
+int csu_stripe_attn_fwd(const csu_stripe_args* a, int dtype, const void* qkv, void* out,
+                        float* lse, void* stream);
+
+/* Workspace bytes csu_stripe_attn_bwd needs (fp32 partial sums of the LePE weight gradient). */
+size_t csu_stripe_attn_bwd_workspace(const csu_stripe_args* a);
+
+/* Gradient of the forward above.  out = forward output, dout = its gradient (B, L, C);
+ * delta fp32 scratch shaped like lse; dqkv (B, L, 3C) is fully written (Q|K|V slots of every
+ * branch's channels); lepe_dw / lepe_db of each branch are written. */
+int csu_stripe_attn_bwd(const csu_stripe_args* a, int dtype, const void* qkv, const void* out,
+                        const void* dout, const float* lse, float* delta, void* dqkv,
+                        void* workspace, size_t workspace_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * LayerNorm over the last dim C of (rows, C) (nn.LayerNorm: norm1/norm2 cswin:315/347,
+ * Merge_Block.norm cswin:377, patch-embed LN cswin:507, norm/norm_up cswin:554/602).
+ * x dtype = xdtype, y dtype = ydtype (bf16 output feeds the next GEMM directly), gamma/beta
+ * fp32; mean/rstd fp32 [rows] are saved for backward.
+ * ------------------------------------------------------------------------------------- */
+int csu_layernorm_fwd(int rows, int C, float eps, int xdtype, const void* x, const float* gamma,
+                      const float* beta, int ydtype, void* y, float* mean, float* rstd, void* stream);
+size_t csu_layernorm_bwd_workspace(int rows, int C);
+/* dx (xdtype) written; dgamma/dbeta fp32 written (deterministic two-pass reduction). */
+int csu_layernorm_bwd(int rows, int C, int xdtype, const void* x, const float* gamma,
+                      const float* mean, const float* rstd, int dydtype, const void* dy,
+                      void* dx, float* dgamma, float* dbeta, void* workspace, size_t ws_bytes,
+                      void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * SimAM (parameter-free energy gate) on token rows (B, L, C), statistics per (b, c) over L.
+ * NOT in the reference: public SimAM formula; parity unpinned vs the
+ * reference.  stats fp32 [B][C][2] = (mean, 4*(var_unbiased + lambda)) saved for backward.
+ * ------------------------------------------------------------------------------------- */
+size_t csu_simam_workspace(int B, int L, int C);
+int csu_simam_fwd(int B, int L, int C, float lambda, int dtype, const void* x, void* y, float* stats,
+                  void* workspace, size_t ws_bytes, void* stream);
+int csu_simam_bwd(int B, int L, int C, int dtype, const void* x, const float* stats, const void* dy,
+                  void* dx, void* workspace, size_t ws_bytes, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CSU_H_ */

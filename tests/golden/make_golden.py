@@ -1,0 +1,254 @@
+"""Generate the golden fixtures by running the REFERENCE itself.
+
+Run in the build container (the reference lives at /root/reference and never travels):
+    python tests/golden/make_golden.py [--skip-traj]
+The reference scripts are imported with two stub modules: ``cv2`` (only used by the data/augment
+code, cswin:49-161) and ``timm.models.layers`` (``DropPath``, ``trunc_normal_``: cswin:14).  With
+drop_path_rate = 0 (the parity setting) DropPath is never constructed (cswin:344); weights are
+loaded from the deterministic recipe (oracle/recipe.py) so ``trunc_normal_`` never matters.
+Outputs: small ``.npz``/``.json`` fixtures next to this script -- data only, no reference source.
+"""
+from __future__ import annotations
+
+import argparse
+import importlib.util
+import json
+import os
+import sys
+import time
+import types
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "cswin-simam-unet_amd"))
+REF = "/root/reference"
+
+from oracle.recipe import recipe_from_contract  # noqa: E402
+from oracle import cswin_ref as O  # noqa: E402
+from oracle import unet_ref as U  # noqa: E402
+
+
+def load_reference():
+    sys.modules.setdefault("cv2", types.ModuleType("cv2"))
+    timm = types.ModuleType("timm")
+    tm = types.ModuleType("timm.models")
+    tl = types.ModuleType("timm.models.layers")
+
+    class DropPath(nn.Module):  # timm semantics: per-sample Bernoulli(keep)/keep in training
+        def __init__(self, p=0.0):
+            super().__init__()
+            self.p = p
+
+        def forward(self, x):
+            if self.p == 0.0 or not self.training:
+                return x
+            keep = 1 - self.p
+            m = x.new_empty((x.shape[0],) + (1,) * (x.ndim - 1)).bernoulli_(keep)
+            return x * m / keep
+
+    tl.DropPath = DropPath
+    tl.trunc_normal_ = nn.init.trunc_normal_
+    timm.models, tm.layers = tm, tl
+    sys.modules.update({"timm": timm, "timm.models": tm, "timm.models.layers": tl})
+    mods = {}
+    for name, fn in (("cswin", "train_cswinunet_segmentation.py"), ("unet", "train_unet_segmentation.py")):
+        spec = importlib.util.spec_from_file_location("ref_" + name, os.path.join(REF, fn))
+        m = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(m)
+        mods[name] = m
+    return mods["cswin"], mods["unet"]
+
+
+def npz(name, **arrs):
+    path = os.path.join(HERE, name)
+    def conv(v):
+        a = v.detach().cpu().numpy() if torch.is_tensor(v) else np.asarray(v)
+        return a.astype(np.float32) if a.dtype == np.float64 else a   # fp64 results stored as fp32
+    np.savez_compressed(path, **{k: conv(v) for k, v in arrs.items()})
+    print(f"wrote {name} ({os.path.getsize(path) / 1024:.1f} KB)")
+
+
+def f1_lepe(R):
+    """LePEAttention idx 0/1/-1: forward + grads (qkv, get_v.weight, get_v.bias)."""
+    cases = [(16, 0, 1, 32, 1), (16, 1, 1, 32, 1), (16, 0, 2, 64, 2), (16, 1, 2, 64, 2),
+             (16, 0, 4, 32, 1), (8, -1, 8, 64, 2), (14, 0, 7, 32, 1), (7, -1, 7, 64, 2)]
+    out = {}
+    for ci, (reso, idx, sw, cb, heads) in enumerate(cases):
+        torch.manual_seed(100 + ci)
+        m = R.LePEAttention(cb, resolution=reso, idx=idx, split_size=sw, num_heads=heads).double()
+        B, L = 1, reso * reso
+        qkv = torch.randn(3, B, L, cb).double().requires_grad_(True)
+        y = m(qkv)
+        g = torch.randn(y.shape).double()
+        y.backward(g)
+        pre = f"c{ci}_"
+        out.update({pre + "meta": np.array([reso, idx, sw, cb, heads]), pre + "qkv": qkv, pre + "w": m.get_v.weight,
+                    pre + "b": m.get_v.bias, pre + "out": y, pre + "gout": g, pre + "dqkv": qkv.grad,
+                    pre + "dw": m.get_v.weight.grad, pre + "db": m.get_v.bias.grad})
+    npz("f1_lepe.npz", **out)
+
+
+def _module_case(mod, x, out, pre):
+    y = mod(x)
+    g = torch.randn(y.shape).double()
+    y.backward(g)
+    out[pre + "x"], out[pre + "y"], out[pre + "gy"], out[pre + "dx"] = x, y, g, x.grad
+    for k, v in mod.state_dict().items():
+        out[pre + "p:" + k] = v
+    for k, v in mod.named_parameters():
+        out[pre + "g:" + k] = v.grad
+
+
+def f2_block(R):
+    out = {}
+    for pre, (dim, reso, heads, sw, last) in {"two_": (64, 8, 2, 2, False), "last_": (64, 4, 2, 4, True),
+                                              "s1_": (32, 8, 2, 1, False)}.items():
+        torch.manual_seed(7)
+        m = R.CSWinBlock(dim=dim, reso=reso, num_heads=heads, split_size=sw, qkv_bias=True, last_stage=last).double()
+        x = torch.randn(2, reso * reso, dim).double().requires_grad_(True)
+        out[pre + "meta"] = np.array([dim, reso, heads, sw, int(last)])
+        _module_case(m, x, out, pre)
+    npz("f2_block.npz", **out)
+
+
+def f3_modules(R):
+    out = {}
+    torch.manual_seed(11)
+    def inp(*shape, fn=torch.randn):
+        return fn(*shape).double().requires_grad_(True)
+    _module_case(R.Merge_Block(32, 64).double(), inp(2, 64, 32), out, "merge_")
+    embed = nn.Sequential(nn.Conv2d(3, 64, 7, 4, 2), R.Rearrange("b c h w -> b (h w) c", h=8, w=8), nn.LayerNorm(64)).double()
+    _module_case(embed, inp(2, 3, 32, 32, fn=torch.rand), out, "embed_")
+    _module_case(R.CARAFE(64, 32).double(), inp(2, 16, 64), out, "carafe_")
+    _module_case(R.CARAFE4(32, 64).double(), inp(2, 16, 32), out, "carafe4_")
+    _module_case(R.Mlp(32, 128).double(), inp(2, 16, 32), out, "mlp_")
+    npz("f3_modules.npz", **out)
+
+
+def ref_model(R, cfg):
+    return R.CSWinTransformer(img_size=cfg.img_size, in_chans=cfg.in_chans, num_classes=cfg.num_classes,
+                              embed_dim=cfg.embed_dim, depth=cfg.depth, split_size=cfg.split_size,
+                              num_heads=cfg.num_heads, mlp_ratio=cfg.mlp_ratio)
+
+
+def f4_model(R):
+    cfg = O.CSWinConfig(img_size=128, split_size=(1, 2, 4, 4))
+    m = ref_model(R, cfg)
+    m.load_state_dict(O.recipe_params(cfg, seed=0))
+    from csu.data import ellipse_batch
+    x, t = ellipse_batch(np.random.default_rng(5), 2, 128)
+    y = m(x)
+    loss = nn.BCELoss()(y, t)
+    loss.backward()
+    names = [k for k, _ in m.named_parameters()]
+    gn = np.array([p.grad.double().norm().item() for _, p in m.named_parameters()])
+    keep = ["output.weight", "stage4.0.attns.0.get_v.weight", "stage1.0.attns.0.get_v.weight",
+            "stage_up1.0.norm2.weight", "upsample1.encoder.bias", "stage1_conv_embed.0.weight"]
+    grads = {"g:" + k: dict(m.named_parameters())[k].grad for k in keep}
+    npz("f4_model.npz", x=x, t=t, y=y, loss=loss, grad_norms=gn, grad_names=np.array(names), **grads,
+        x1=m.x1, x3=m.x3)
+
+
+def f5_metrics(R):
+    g = torch.Generator().manual_seed(3)
+    p = torch.rand(4, 1, 16, 16, generator=g)
+    t = (torch.rand(4, 1, 16, 16, generator=g) > 0.6).float()
+    p[0, 0, 0, :4] = torch.tensor([0.0, 1.0, 1e-50, 0.5])  # clamp / threshold edge cases
+    pred = (p > 0.5).float()
+    npz("f5_metrics.npz", p=p, t=t, bce=nn.BCELoss()(p, t), dice=R.dice_coefficient(pred, t), iou=R.iou_score(pred, t),
+        dice_empty=R.dice_coefficient(torch.zeros(8), torch.zeros(8)), iou_empty=R.iou_score(torch.zeros(8), torch.zeros(8)))
+
+
+def f6_unet(RU):
+    torch.manual_seed(0)
+    m = RU.UNet(3, 1)
+    m.load_state_dict(recipe_from_contract(U.unet_contract(), seed=1))
+    x = torch.rand(2, 3, 32, 32, generator=torch.Generator().manual_seed(9))
+    t = (torch.rand(2, 1, 32, 32, generator=torch.Generator().manual_seed(10)) > 0.5).float()
+    m.train()
+    y = m(x)
+    loss = nn.BCELoss()(y, t)
+    loss.backward()
+    gn = np.array([p.grad.norm().item() for _, p in m.named_parameters()])
+    rm = {"rm:" + k: v for k, v in m.state_dict().items() if "running" in k and k.startswith("inc.")}
+    m.eval()
+    with torch.no_grad():
+        ye = m(x)
+    npz("f6_unet.npz", x=x, t=t, y_train=y, loss=loss, grad_norms=gn, y_eval=ye,
+        grad_names=np.array([k for k, _ in m.named_parameters()]), **rm)
+
+
+def f7_contract(R, RU):
+    res = {}
+    for name, kw in {"default_224": dict(img_size=224), "cfg512": dict(img_size=512, split_size=[1, 2, 8, 8]),
+                     "deep512": dict(img_size=512, depth=[2, 4, 32, 2], split_size=[1, 2, 8, 8])}.items():
+        m = R.CSWinTransformer(**kw)
+        res[name] = [[k, list(v.shape)] for k, v in m.state_dict().items()]
+    res["unet"] = [[k, list(v.shape)] for k, v in RU.UNet(3, 1).state_dict().items()]
+    with open(os.path.join(HERE, "f7_contract.json"), "w") as f:
+        json.dump(res, f)
+    print("wrote f7_contract.json", {k: len(v) for k, v in res.items()})
+
+
+def f8_trajectory(R, steps=120, batch=8, size=128):
+    """fp32 AdamW(1e-4, wd 1e-4) trajectory on the synthetic generator (cswin:775-806, 937-941)."""
+    torch.set_num_threads(8)
+    cfg = O.CSWinConfig(img_size=size, split_size=(1, 2, 4, 4))
+    m = ref_model(R, cfg)
+    m.load_state_dict(O.recipe_params(cfg, seed=0))
+    opt = torch.optim.AdamW(m.parameters(), lr=1e-4, weight_decay=1e-4)
+    crit = nn.BCELoss()
+    from csu.data import ellipse_batch
+    rng = np.random.default_rng(1234)
+    xe, te = ellipse_batch(np.random.default_rng(99), 16, size)
+    rec = {"loss": [], "dice": [], "iou": [], "eval_step": [], "eval_loss": [], "eval_dice": [], "eval_iou": []}
+    t0 = time.time()
+    for step in range(1, steps + 1):
+        x, t = ellipse_batch(rng, batch, size)
+        m.train()
+        opt.zero_grad()
+        y = m(x)
+        loss = crit(y, t)
+        loss.backward()
+        opt.step()
+        with torch.no_grad():
+            pred = (y > 0.5).float()
+            rec["loss"].append(loss.item())
+            rec["dice"].append(R.dice_coefficient(pred, t))
+            rec["iou"].append(R.iou_score(pred, t))
+        if step % 20 == 0:
+            m.eval()
+            with torch.no_grad():
+                ye = m(xe)
+                rec["eval_step"].append(step)
+                rec["eval_loss"].append(crit(ye, te).item())
+                pe = (ye > 0.5).float()
+                rec["eval_dice"].append(R.dice_coefficient(pe, te))
+                rec["eval_iou"].append(R.iou_score(pe, te))
+            print(f"step {step} loss {loss.item():.4f} eval dice {rec['eval_dice'][-1]:.5f} ({time.time() - t0:.0f}s)")
+    with open(os.path.join(HERE, "f8_trajectory.json"), "w") as f:
+        json.dump({"config": {"img_size": size, "split_size": [1, 2, 4, 4], "batch": batch, "steps": steps,
+                              "lr": 1e-4, "weight_decay": 1e-4, "seed_weights": 0, "train_rng": 1234, "eval_rng": 99},
+                   **rec}, f)
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--skip-traj", action="store_true")
+    ap.add_argument("--only", default="")
+    a = ap.parse_args()
+    R, RU = load_reference()
+    jobs = {"f1": lambda: f1_lepe(R), "f2": lambda: f2_block(R), "f3": lambda: f3_modules(R), "f4": lambda: f4_model(R),
+            "f5": lambda: f5_metrics(R), "f6": lambda: f6_unet(RU), "f7": lambda: f7_contract(R, RU),
+            "f8": lambda: f8_trajectory(R)}
+    for k, fn in jobs.items():
+        if a.only and k not in a.only.split(","):
+            continue
+        if k == "f8" and a.skip_traj:
+            continue
+        fn()

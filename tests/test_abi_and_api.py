@@ -1,0 +1,98 @@
+"""CPU-side checks: the C-ABI library loads and exports every symbol include/csu.h declares, the
+ctypes struct layouts match the header, the nn.Module surface matches the reference's
+state_dict contract (fixture F7), and the product path refuses CPU tensors (no fallback)."""
+import ctypes
+import json
+import os
+import re
+
+import pytest
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_functions():
+    src = open(os.path.join(REPO, "include", "csu.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(csu_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_exports_every_header_symbol():
+    from csu import _lib
+    L = _lib.lib()
+    names = header_functions()
+    assert len(names) >= 10
+    for n in names:
+        assert hasattr(L, n), n
+        assert n in _lib._SIGS, f"{n} missing from the ctypes signature table"
+    assert b"gfx950" in L.csu_build_info()
+
+
+def test_struct_layout_matches_header():
+    from csu import _lib
+    # csu_stripe_branch: 4 x int32 + 4 pointers; csu_stripe_args: 8 x int32/float + 2 branches
+    assert ctypes.sizeof(_lib.StripeBranch) == 16 + 4 * 8
+    assert ctypes.sizeof(_lib.StripeArgs) == 32 + 2 * ctypes.sizeof(_lib.StripeBranch)
+    assert _lib.StripeArgs.br.offset == 32
+
+
+def test_error_path_reports_text():
+    from csu import _lib
+    L = _lib.lib()
+    a = _lib.StripeArgs()
+    a.head_dim = 16   # unsupported -> CSU_E_UNSUPPORTED before any device work
+    rc = L.csu_stripe_attn_fwd(ctypes.byref(a), 0, None, None, None, None)
+    assert rc == -2
+    assert b"head_dim" in L.csu_last_error_string()
+    rc = L.csu_layernorm_fwd(4, 96, 1e-5, 0, None, None, None, 0, None, None, None, None)
+    assert rc == -2
+
+
+@pytest.mark.parametrize("name,kw", [("default_224", dict(img_size=224)),
+                                     ("cfg512", dict(img_size=512, split_size=[1, 2, 8, 8])),
+                                     ("deep512", dict(img_size=512, depth=[2, 4, 32, 2], split_size=[1, 2, 8, 8]))])
+def test_state_dict_contract_matches_reference(golden_dir, name, kw):
+    from csu.model import CSWinTransformer
+    ref = json.load(open(os.path.join(golden_dir, "f7_contract.json")))[name]
+    m = CSWinTransformer(**kw)
+    assert [[k, list(v.shape)] for k, v in m.state_dict().items()] == ref
+    m2 = CSWinTransformer(simam=True, **kw)
+    assert list(m2.state_dict().keys()) == [k for k, _ in ref]
+
+
+def test_reference_init_statistics():
+    """_init_weights (cswin:607-614): Linear ~ trunc N(0, .02), zero bias; LN (1, 0)."""
+    from csu.model import CSWinTransformer
+    torch.manual_seed(0)
+    m = CSWinTransformer(img_size=128, split_size=[1, 2, 4, 4])
+    w = m.stage3[0].mlp.fc1.weight
+    assert abs(float(w.std()) - 0.02) < 2e-3 and float(m.stage3[0].mlp.fc1.bias.abs().max()) == 0
+    assert float((m.norm.weight - 1).abs().max()) == 0
+
+
+def test_product_refuses_cpu_tensors():
+    from csu import ops
+    from csu._lib import CsuError
+    geom = ops.StripeGeometry(8, 32, 1, [(8, 1, 0)], 32 ** -0.5)
+    with pytest.raises(CsuError):
+        ops.stripe_attention(torch.zeros(1, 64, 96), geom, [torch.zeros(32, 1, 3, 3)], [torch.zeros(32)])
+    with pytest.raises(CsuError):
+        ops.layer_norm(torch.zeros(4, 64), torch.ones(64), torch.zeros(64))
+
+
+def test_geometry_validation_mirrors_reference():
+    from csu import ops
+    with pytest.raises(ValueError):   # img2windows view fails when reso % split != 0 (cswin:204)
+        ops.StripeGeometry(16, 64, 2, [(16, 7, 0)], 0.1)
+
+
+def test_dice_iou_metrics_match_reference_fixture(golden_dir):
+    import numpy as np
+    from csu.train import bce_loss, dice_coefficient, iou_score
+    z = np.load(os.path.join(golden_dir, "f5_metrics.npz"))
+    p, t = torch.from_numpy(z["p"]), torch.from_numpy(z["t"])
+    pred = (p > 0.5).float()
+    assert abs(dice_coefficient(pred, t) - float(z["dice"])) < 1e-7
+    assert abs(iou_score(pred, t) - float(z["iou"])) < 1e-7
+    assert abs(bce_loss(p, t).item() - float(z["bce"])) < 1e-6

@@ -1,0 +1,152 @@
+"""Kernel-level parity on the MI355X: HIP path (through the C ABI) vs the CPU oracle.
+
+Tolerances: fp32 kernels rtol 1e-4 / atol 1e-5 (relative to the tensor's max magnitude);
+bf16 kernels are compared with the fp64 oracle on the same bf16-rounded inputs by relative L2
+error <= 2e-2 and max-abs <= 3e-2 * max|ref| (SURVEY §8c calibration)."""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from oracle import cswin_ref as O
+
+
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch.device("cuda:0")
+
+
+def rel_l2(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return float((a - b).norm() / b.norm().clamp_min(1e-30))
+
+
+def assert_close(a, b, dtype):
+    a, b = a.double().cpu(), b.double().cpu()
+    scale = float(b.abs().max().clamp_min(1e-30))
+    if dtype == torch.float32:
+        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-5 * max(1.0, scale))
+    else:
+        assert rel_l2(a, b) < 2e-2, rel_l2(a, b)
+        assert float((a - b).abs().max()) < 3e-2 * scale
+
+
+# (reso, idx, sw, cb, heads, B): covers width-1 stripes, N % 32 != 0 (masking), N up to 1024
+ATTN_CASES = [
+    (16, 0, 1, 32, 1, 2), (16, 1, 1, 32, 1, 2), (16, 0, 2, 64, 2, 2), (16, 1, 4, 64, 2, 1),
+    (8, -1, 8, 128, 4, 2), (14, 0, 7, 64, 2, 1), (7, -1, 7, 64, 2, 2), (32, 0, 8, 128, 4, 1),
+    (16, -1, 16, 64, 2, 1), (32, -1, 32, 32, 1, 1), (64, 1, 2, 64, 2, 1), (56, 0, 1, 32, 1, 1),
+]
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("case", ATTN_CASES)
+def test_stripe_attention_vs_oracle(case, dtype):
+    from csu import ops
+    d = dev()
+    reso, idx, sw, cb, heads, B = case
+    g = torch.Generator().manual_seed(hash(case) % 1000)
+    L = reso * reso
+    qkv = torch.randn(B, L, 3 * cb, generator=g).to(dtype)
+    w = torch.randn(cb, 1, 3, 3, generator=g) * 0.3
+    b = torch.randn(cb, generator=g) * 0.1
+    gout = torch.randn(B, L, cb, generator=g).to(dtype)
+    hs, ws = O.stripe_geometry(reso, idx, sw)
+    scale = (cb // heads) ** -0.5
+    # oracle (fp64, on the same rounded inputs)
+    q64 = qkv.double().requires_grad_(True)
+    w64, b64 = w.double().requires_grad_(True), b.double().requires_grad_(True)
+    ref = O.lepe_attention(q64[..., :cb], q64[..., cb:2 * cb], q64[..., 2 * cb:], reso, hs, ws, heads, w64, b64, scale)
+    ref.backward(gout.double())
+    # HIP
+    qd = qkv.to(d).requires_grad_(True)
+    wd, bd = w.to(d).requires_grad_(True), b.to(d).requires_grad_(True)
+    geom = ops.StripeGeometry(reso, cb, heads, [(hs, ws, 0)], scale)
+    out = ops.stripe_attention(qd, geom, [wd], [bd])
+    out.backward(gout.to(d))
+    torch.cuda.synchronize()
+    assert out.dtype == dtype
+    assert_close(out, ref, dtype)
+    assert_close(qd.grad, q64.grad, dtype)
+    assert_close(wd.grad, w64.grad, dtype)
+    assert_close(bd.grad, b64.grad, dtype)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_two_branch_fused_launch(dtype):
+    """Both LePE branches of a CSWinBlock in one launch == two separate oracle branches + cat."""
+    from csu import ops
+    d = dev()
+    reso, C, heads, sw, B = 32, 128, 4, 2, 2
+    g = torch.Generator().manual_seed(3)
+    qkv = torch.randn(B, reso * reso, 3 * C, generator=g).to(dtype)
+    ws_ = [torch.randn(C // 2, 1, 3, 3, generator=g) * 0.3 for _ in range(2)]
+    bs_ = [torch.randn(C // 2, generator=g) * 0.1 for _ in range(2)]
+    scale = (C // heads) ** -0.5
+    q = qkv.double()
+    outs = []
+    for i, sl in enumerate((slice(0, C // 2), slice(C // 2, C))):
+        hs, wsp = O.stripe_geometry(reso, i, sw)
+        outs.append(O.lepe_attention(q[..., :C][..., sl], q[..., C:2 * C][..., sl], q[..., 2 * C:][..., sl], reso, hs,
+                                     wsp, heads // 2, ws_[i].double(), bs_[i].double(), scale))
+    ref = torch.cat(outs, -1)
+    geom = ops.StripeGeometry(reso, C, heads // 2, [(reso, sw, 0), (sw, reso, C // 2)], scale)
+    out = ops.stripe_attention(qkv.to(d), geom, [w.to(d) for w in ws_], [b.to(d) for b in bs_])
+    assert_close(out, ref, dtype)
+
+
+@pytest.mark.parametrize("C", [64, 128, 256, 512])
+@pytest.mark.parametrize("xdt,ydt", [(torch.float32, torch.float32), (torch.float32, torch.bfloat16),
+                                     (torch.bfloat16, torch.bfloat16)])
+def test_layernorm_vs_torch_fp64(C, xdt, ydt):
+    from csu import ops
+    d = dev()
+    g = torch.Generator().manual_seed(C)
+    x = (torch.randn(3, 517, C, generator=g) * 2 + 0.5).to(xdt)
+    w = torch.randn(C, generator=g)
+    b = torch.randn(C, generator=g)
+    dy = torch.randn(3, 517, C, generator=g).to(ydt)
+    x64 = x.double().requires_grad_(True)
+    w64, b64 = w.double().requires_grad_(True), b.double().requires_grad_(True)
+    ref = torch.nn.functional.layer_norm(x64, (C,), w64, b64, 1e-5)
+    ref.backward(dy.double())
+    xd = x.to(d).requires_grad_(True)
+    wd, bd = w.to(d).requires_grad_(True), b.to(d).requires_grad_(True)
+    y = ops.layer_norm(xd, wd, bd, 1e-5, ydt)
+    y.backward(dy.to(d))
+    assert y.dtype == ydt
+    tol_dt = torch.float32 if (xdt, ydt) == (torch.float32, torch.float32) else torch.bfloat16
+    assert_close(y, ref, tol_dt)
+    assert_close(xd.grad, x64.grad, tol_dt)
+    assert_close(wd.grad, w64.grad, tol_dt)
+    assert_close(bd.grad, b64.grad, tol_dt)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("shape", [(2, 64, 32), (2, 1024, 64), (1, 4096, 128), (3, 17, 200)])
+def test_simam_vs_formula(shape, dtype):
+    """SimAM vs the float64 formula (parity unpinned vs the reference, which has no SimAM)."""
+    from csu.simam import simam
+    d = dev()
+    g = torch.Generator().manual_seed(sum(shape))
+    x = (torch.randn(*shape, generator=g) * 1.5 + 0.3).to(dtype)
+    dy = torch.randn(*shape, generator=g).to(dtype)
+    x64 = x.double().requires_grad_(True)
+    ref = O.simam(x64)
+    ref.backward(dy.double())
+    xd = x.to(d).requires_grad_(True)
+    y = simam(xd)
+    y.backward(dy.to(d))
+    assert_close(y, ref, dtype)
+    assert_close(xd.grad, x64.grad, dtype)
+
+
+def test_cpu_tensor_fails_loudly():
+    from csu import ops
+    from csu._lib import CsuError
+    geom = ops.StripeGeometry(8, 32, 1, [(8, 1, 0)], 32 ** -0.5)
+    with pytest.raises(CsuError):
+        ops.stripe_attention(torch.zeros(1, 64, 96), geom, [torch.zeros(32, 1, 3, 3)], [torch.zeros(32)])
