@@ -1,0 +1,198 @@
+"""Benchmark: CSWin-UNet training throughput (images/sec) at 512x512 bf16, batch 16 per GPU.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+N > 1 is launched by the driver with torch.distributed.run (one process per GPU, RCCL).
+One step = forward + BCE + backward (+ DDP gradient all-reduce) + fused AdamW on a batch of
+synthetic 512x512 images already resident in HBM.  Prints ONE JSON line (rank 0).
+
+roofline: the stripe-attention forward kernel (csu_stripe_attn_fwd), timed live with HIP events
+around every launch of the timed region on the launch stream; achieved = algorithmic bytes
+(qkv read once + output written once + log-sum-exp) / measured time.  cpu_baseline: the CPU
+oracle (a restatement of the reference) timed on this host for a bounded sample.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+for _p in (REPO, os.path.join(REPO, "cswin-simam-unet_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
+BF16_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=16, help="images per GPU")
+    ap.add_argument("--img", type=int, default=512)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--depth", default="1,2,9,1")
+    ap.add_argument("--split", default="1,2,8,8")
+    ap.add_argument("--simam", action="store_true")
+    ap.add_argument("--cpu-baseline", default="auto", choices=["auto", "on", "off"])
+    ap.add_argument("--no-roofline", action="store_true")
+    return ap.parse_args()
+
+
+def synthetic_batches(n, batch, img, device, seed):
+    from csu.data import ellipse_batch
+    rng = np.random.default_rng(seed)
+    out = []
+    for _ in range(n):
+        x, t = ellipse_batch(rng, batch, img)
+        out.append((x.to(device), t.to(device)))
+    return out
+
+
+def cpu_baseline(args, dtype):
+    """Oracle (CPU restatement of the reference) fwd+BCE+bwd+AdamW, bounded sample."""
+    from oracle import cswin_ref as O
+    threads = min(16, len(os.sched_getaffinity(0)))
+    torch.set_num_threads(threads)
+    cfg = O.CSWinConfig(img_size=args.img, depth=[int(v) for v in args.depth.split(",")],
+                        split_size=[int(v) for v in args.split.split(",")], simam=args.simam)
+    m = O.OracleCSWin(cfg, O.recipe_params(cfg, seed=0))
+    opt = torch.optim.AdamW(m.parameters(), lr=1e-4, weight_decay=1e-4)
+    from csu.data import ellipse_batch
+    b = 2
+    x, t = ellipse_batch(np.random.default_rng(7), b, args.img)
+
+    def step():
+        opt.zero_grad()
+        with torch.autocast("cpu", dtype=torch.bfloat16, enabled=dtype == torch.bfloat16):
+            y = m(x)
+        loss = O.bce_loss(y.float(), t)
+        loss.backward()
+        opt.step()
+
+    step()  # warm-up
+    n, t0 = 0, time.perf_counter()
+    while n < 2 or (time.perf_counter() - t0 < 10.0 and n < 8):
+        step()
+        n += 1
+    el = time.perf_counter() - t0
+    return {"value": round(n * b / el, 4), "unit": "images/sec", "cores": threads, "kind": "port",
+            "sample": f"{n} train steps x batch {b} at {args.img}x{args.img} "
+                      f"({'bf16 autocast' if dtype == torch.bfloat16 else 'fp32'}), oracle/cswin_ref.py, "
+                      f"{el:.1f}s, {threads} threads"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    device = torch.device("cuda", local)
+    torch.backends.cudnn.benchmark = True
+    dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+
+    from csu import ops
+    from csu.model import CSWinTransformer
+    from csu.train import bce_loss, make_optimizer
+
+    depth = [int(v) for v in args.depth.split(",")]
+    split = [int(v) for v in args.split.split(",")]
+    torch.manual_seed(0)
+    model = CSWinTransformer(img_size=args.img, depth=depth, split_size=split, simam=args.simam).to(device)
+    nparams = sum(p.numel() for p in model.parameters())
+    if world > 1:
+        model = torch.nn.parallel.DistributedDataParallel(model, device_ids=[local], gradient_as_bucket_view=True,
+                                                          static_graph=True, bucket_cap_mb=64)
+    opt = make_optimizer(model)
+    batches = synthetic_batches(2, args.batch, args.img, device, seed=1234 + rank)
+
+    def step(i):
+        x, t = batches[i % len(batches)]
+        opt.zero_grad(set_to_none=True)
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=dtype == torch.bfloat16):
+            y = model(x)
+        loss = bce_loss(y, t)
+        loss.backward()
+        opt.step()
+        return loss
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    prof = [] if not args.no_roofline else None
+    ops.set_kernel_timer(prof)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        loss = step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    ops.set_kernel_timer(None)
+    t = torch.tensor([el], dtype=torch.float64, device=device)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    el = float(t.item())
+    images = args.batch * world * args.steps
+    roof = None
+    if prof:
+        torch.cuda.synchronize()
+        ms = sum(s.elapsed_time(e) for s, e, _, _ in prof)
+        nbytes = sum(b for _, _, b, _ in prof)
+        flops = sum(f for _, _, _, f in prof)
+        n = len(prof)
+        achieved = nbytes / n / (ms / n * 1e-3) / 1e9
+        roof = {"kernel": "csu_stripe_attn_fwd (stripe_fwd<bf16>)", "bound": "hbm", "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": _pmc_traffic(), "launches": n, "avg_us": round(ms / n * 1e3, 2),
+                "bytes_per_launch": int(nbytes / n), "flops_per_launch": int(flops / n),
+                "achieved_tflops": round(flops / (ms * 1e-3) / 1e12, 2)}
+    cpu = None
+    if rank == 0 and world == 1 and (args.cpu_baseline == "on" or (args.cpu_baseline == "auto")):
+        try:
+            cpu = cpu_baseline(args, dtype)
+        except Exception as e:  # baseline is informational; never hide the GPU number
+            cpu = {"value": None, "error": repr(e)[:200]}
+    if rank == 0:
+        rec = {"metric": "images/sec at 512x512 bf16 (CSWin-UNet train step)", "value": round(images / el, 3),
+               "unit": "images/sec", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+               "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+               "vs_baseline": None, "dtype": args.dtype, "data": "synthetic (ellipse masks, SURVEY §8d), random-init weights",
+               "config": {"workload": f"CSWin-UNet train step {args.img}x{args.img} depth {depth} split {split}"
+                                      f"{' +SimAM' if args.simam else ''}, AdamW",
+                          "model": "CSWinTransformer", "params": nparams, "global_batch": args.batch * world,
+                          "per_gpu_batch": args.batch, "img": args.img, "parallelism": f"dp{world}"},
+               "roofline": roof, "cpu_baseline": cpu, "final_loss": round(float(loss.item()), 5)}
+        print(json.dumps(rec), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def _pmc_traffic():
+    """HBM bytes per launch of stripe_fwd from the committed rocprofv3 PMC summary, if present."""
+    p = os.path.join(REPO, "profiles", "pmc_stripe_fwd.json")
+    if not os.path.exists(p):
+        return None
+    try:
+        with open(p) as f:
+            return json.load(f).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+if __name__ == "__main__":
+    main()

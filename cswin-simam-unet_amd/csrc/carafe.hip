@@ -1,0 +1,303 @@
+// Fused CARAFE content-aware reassembly (+ the 1-class output head) for gfx950.
+//
+// Replaces, of CARAFE/CARAFE4.forward (cswin:401-437 / 450-486), everything between the encoder
+// conv and the `out` 1x1 conv: pixel_shuffle of the kernel logits (cswin:410), softmax over the
+// k^2 = 9 taps (cswin:412), both unfolds/reshape/permute (cswin:413-427), the per-pixel
+// (C x 9) @ (9 x s^2) matmul (cswin:429) and the final pixel_shuffle (cswin:432).  Token-major
+// (NHWC) in and out; the 9x-expanded unfold tensor and every layout copy disappear.
+//   out[b, Y, X, c] = sum_t w[b, y, x, t, i, j] * x[b, y + ky - 1, x + kx - 1, c]   (zero padded)
+//   with Y = y*s + i, X = x*s + j, t = 3*ky + kx, w = softmax_t(enc[b, y, x, t*s*s + i*s + j]).
+// HBM-bound: one thread = one output pixel x 8 channels (16-B vectors); neighbour rows of x are
+// re-read from L1/L2.  The softmax weights are saved (fp32) for the backward pass.
+//
+// Head (up_x4 + sigmoid, cswin:674-688): prob[b, p] = sigmoid(sum_c x[b, p, c] * w[c]) for the
+// 1-class 1x1 conv without bias; backward gives dx = dlogit * w and deterministic dW partials.
+#include "common.hpp"
+
+namespace csu {
+namespace {
+
+constexpr int NT = 256;
+constexpr int KT = 9;   // 3x3 taps
+
+template <typename T>
+__global__ __launch_bounds__(NT) void carafe_fwd(int B, int H, int W, int C, int s, const T* __restrict__ x,
+                                                 const T* __restrict__ enc, T* __restrict__ out,
+                                                 float* __restrict__ wsave) {
+    const int G = C / 8;
+    const long gid = (long)blockIdx.x * NT + threadIdx.x;
+    const int sW = s * W, sH = s * H;
+    const long total = (long)B * sH * sW * G;
+    if (gid >= total) return;
+    const int g = gid % G;
+    long p = gid / G;
+    const int X = p % sW; p /= sW;
+    const int Y = p % sH;
+    const int b = p / sH;
+    const int y = Y / s, i = Y - y * s, xx = X / s, j = X - xx * s;
+    const int s2 = s * s, sub = i * s + j;
+    const size_t lpix = ((size_t)b * H + y) * W + xx;
+    const T* e = enc + lpix * KT * s2 + sub;
+    float lg[KT], mx = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < KT; ++t) {
+        lg[t] = to_f(e[t * s2]);
+        mx = fmaxf(mx, lg[t]);
+    }
+    float den = 0.f;
+#pragma unroll
+    for (int t = 0; t < KT; ++t) {
+        lg[t] = __expf(lg[t] - mx);
+        den += lg[t];
+    }
+    const float inv = 1.f / den;
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < KT; ++t) {
+        lg[t] *= inv;
+        const int yy = y + t / 3 - 1, xq = xx + t % 3 - 1;
+        if (yy < 0 || yy >= H || xq < 0 || xq >= W) continue;
+        float v[8];
+        load8(x + (((size_t)b * H + yy) * W + xq) * C + 8 * g, v);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[k] += lg[t] * v[k];
+    }
+    store8(out + (((size_t)b * sH + Y) * sW + X) * C + 8 * g, acc);
+    if (g == 0) {
+        float* ws = wsave + lpix * KT * s2 + sub;
+#pragma unroll
+        for (int t = 0; t < KT; ++t) ws[t * s2] = lg[t];
+    }
+}
+
+// d enc: per output pixel, dw_t = sum_c dout[c] x[nbr_t][c]; dlogit_t = w_t (dw_t - sum_u w_u dw_u).
+// G = C/8 lanes cooperate on one output pixel (G in {8, 16, 32, 64} divides the wave).
+template <typename T>
+__global__ __launch_bounds__(NT) void carafe_bwd_enc(int B, int H, int W, int C, int s, const T* __restrict__ x,
+                                                     const float* __restrict__ wsave, const T* __restrict__ dout,
+                                                     T* __restrict__ denc) {
+    const int G = C / 8;
+    const long gid = (long)blockIdx.x * NT + threadIdx.x;
+    const int sW = s * W, sH = s * H;
+    const long total = (long)B * sH * sW * G;
+    const bool live = gid < total;
+    const long gg = live ? gid : 0;
+    const int g = gg % G;
+    long p = gg / G;
+    const int X = p % sW; p /= sW;
+    const int Y = p % sH;
+    const int b = p / sH;
+    const int y = Y / s, i = Y - y * s, xx = X / s, j = X - xx * s;
+    const int s2 = s * s, sub = i * s + j;
+    const size_t lpix = ((size_t)b * H + y) * W + xx;
+    float go[8];
+    load8(dout + (((size_t)b * sH + Y) * sW + X) * C + 8 * g, go);
+    float dw[KT];
+#pragma unroll
+    for (int t = 0; t < KT; ++t) {
+        const int yy = y + t / 3 - 1, xq = xx + t % 3 - 1;
+        float d = 0.f;
+        if (yy >= 0 && yy < H && xq >= 0 && xq < W) {
+            float v[8];
+            load8(x + (((size_t)b * H + yy) * W + xq) * C + 8 * g, v);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) d += go[k] * v[k];
+        }
+        dw[t] = d;
+    }
+    // reduce over the G lanes of this pixel (aligned groups of G consecutive lanes)
+#pragma unroll
+    for (int t = 0; t < KT; ++t)
+        for (int o = G >> 1; o > 0; o >>= 1) dw[t] += __shfl_xor(dw[t], o, 64);
+    if (!live || g != 0) return;
+    const float* ws = wsave + lpix * KT * s2 + sub;
+    float wt[KT], sum = 0.f;
+#pragma unroll
+    for (int t = 0; t < KT; ++t) {
+        wt[t] = ws[t * s2];
+        sum += wt[t] * dw[t];
+    }
+    T* de = denc + lpix * KT * s2 + sub;
+#pragma unroll
+    for (int t = 0; t < KT; ++t) de[t * s2] = from_f<T>(wt[t] * (dw[t] - sum));
+}
+
+// dx[y', x', c] = sum_t sum_{i,j} w[(y,x), t, (i,j)] dout[(y s + i, x s + j), c],  (y, x) = (y'-ky+1, x'-kx+1)
+template <typename T>
+__global__ __launch_bounds__(NT) void carafe_bwd_x(int B, int H, int W, int C, int s, const float* __restrict__ wsave,
+                                                   const T* __restrict__ dout, T* __restrict__ dx) {
+    const int G = C / 8;
+    const long gid = (long)blockIdx.x * NT + threadIdx.x;
+    const long total = (long)B * H * W * G;
+    if (gid >= total) return;
+    const int g = gid % G;
+    long p = gid / G;
+    const int xp = p % W; p /= W;
+    const int yp = p % H;
+    const int b = p / H;
+    const int s2 = s * s, sW = s * W, sH = s * H;
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int t = 0; t < KT; ++t) {
+        const int y = yp - (t / 3 - 1), xx = xp - (t % 3 - 1);
+        if (y < 0 || y >= H || xx < 0 || xx >= W) continue;
+        const float* ws = wsave + (((size_t)b * H + y) * W + xx) * KT * s2 + t * s2;
+        for (int i = 0; i < s; ++i)
+            for (int j = 0; j < s; ++j) {
+                const float w = ws[i * s + j];
+                float v[8];
+                load8(dout + (((size_t)b * sH + y * s + i) * sW + xx * s + j) * C + 8 * g, v);
+#pragma unroll
+                for (int k = 0; k < 8; ++k) acc[k] += w * v[k];
+            }
+    }
+    store8(dx + (((size_t)b * H + yp) * W + xp) * C + 8 * g, acc);
+}
+
+// ---- 1-class head: prob = sigmoid(x . w) ----------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(NT) void head_fwd(long P, int C, const T* __restrict__ x, const float* __restrict__ w,
+                                               float* __restrict__ prob) {
+    const int G = C / 8;   // lanes per pixel
+    const long gid = (long)blockIdx.x * NT + threadIdx.x;
+    const bool live = gid < P * G;
+    const long p = live ? gid / G : 0;
+    const int g = live ? gid % G : 0;
+    float v[8];
+    load8(x + p * C + 8 * g, v);
+    float d = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) d += v[k] * w[8 * g + k];
+    for (int o = G >> 1; o > 0; o >>= 1) d += __shfl_xor(d, o, 64);
+    if (live && g == 0) prob[p] = 1.f / (1.f + __expf(-d));
+}
+
+// dlogit = dprob * p (1 - p); dx = dlogit * w; per-block partial of dW = sum_p dlogit x
+template <typename T>
+__global__ __launch_bounds__(NT) void head_bwd(long P, int C, long pix_per_block, const T* __restrict__ x,
+                                               const float* __restrict__ w, const float* __restrict__ prob,
+                                               const float* __restrict__ dprob, T* __restrict__ dx,
+                                               float* __restrict__ part) {
+    __shared__ float red[NT][8];
+    const int G = C / 8;              // lanes per pixel (C <= 64)
+    const int PPI = NT / G;           // pixels per iteration
+    const int g = threadIdx.x % G, pl = threadIdx.x / G;
+    const long p0 = (long)blockIdx.x * pix_per_block, p1 = min(P, p0 + pix_per_block);
+    float wv[8], acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < 8; ++k) wv[k] = w[8 * g + k];
+    for (long p = p0 + pl; p < p1; p += PPI) {
+        const float pr = prob[p];
+        const float dl = dprob[p] * pr * (1.f - pr);
+        float v[8], o[8];
+        load8(x + p * C + 8 * g, v);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            acc[k] += dl * v[k];
+            o[k] = dl * wv[k];
+        }
+        store8(dx + p * C + 8 * g, o);
+    }
+    // combine the PPI pixel lanes in a fixed order
+#pragma unroll
+    for (int k = 0; k < 8; ++k) red[threadIdx.x][k] = acc[k];
+    __syncthreads();
+    if (threadIdx.x < C) {
+        const int gc = threadIdx.x / 8, kc = threadIdx.x % 8;
+        float s = 0.f;
+        for (int q = 0; q < PPI; ++q) s += red[q * G + gc][kc];
+        part[(size_t)blockIdx.x * C + threadIdx.x] = s;
+    }
+}
+
+__global__ void head_wreduce(int C, int nb, const float* __restrict__ part, float* __restrict__ dw) {
+    __shared__ float red[4][64];
+    const int c = threadIdx.x & 63, l = threadIdx.x >> 6;
+    float s = 0.f;
+    if (c < C)
+        for (int b = l; b < nb; b += 4) s += part[(size_t)b * C + c];
+    red[l][c] = s;
+    __syncthreads();
+    if (l == 0 && c < C) dw[c] = red[0][c] + red[1][c] + red[2][c] + red[3][c];
+}
+
+unsigned blocks(long threads) { return (unsigned)((threads + NT - 1) / NT); }
+
+int check_args(int B, int H, int W, int C, int s) {
+    if (B < 1 || H < 1 || W < 1 || s < 1 || C < 8 || C % 8 || C / 8 > 64 || ((C / 8) & (C / 8 - 1)))
+        return fail(CSU_E_ARG, "carafe: need C = 8 * 2^k <= 512");
+    return 0;
+}
+
+}  // namespace
+}  // namespace csu
+
+using namespace csu;
+
+extern "C" int csu_carafe_fwd(int B, int H, int W, int C, int s, int dtype, const void* x, const void* enc,
+                              void* out, float* wsave, void* stream) {
+    if (int e = check_args(B, H, W, C, s)) return e;
+    if (!x || !enc || !out || !wsave) return fail(CSU_E_ARG, "carafe_fwd: null buffer");
+    const long n = (long)B * H * s * W * s * (C / 8);
+    hipStream_t st = as_stream(stream);
+    if (dtype == CSU_BF16)
+        carafe_fwd<bf16><<<blocks(n), NT, 0, st>>>(B, H, W, C, s, (const bf16*)x, (const bf16*)enc, (bf16*)out, wsave);
+    else if (dtype == CSU_F32)
+        carafe_fwd<float><<<blocks(n), NT, 0, st>>>(B, H, W, C, s, (const float*)x, (const float*)enc, (float*)out, wsave);
+    else
+        return fail(CSU_E_ARG, "carafe_fwd: bad dtype");
+    return check_launch("carafe_fwd");
+}
+
+extern "C" int csu_carafe_bwd(int B, int H, int W, int C, int s, int dtype, const void* x, const float* wsave,
+                              const void* dout, void* dx, void* denc, void* stream) {
+    if (int e = check_args(B, H, W, C, s)) return e;
+    if (!x || !wsave || !dout || !dx || !denc) return fail(CSU_E_ARG, "carafe_bwd: null buffer");
+    const long n_out = (long)B * H * s * W * s * (C / 8), n_in = (long)B * H * W * (C / 8);
+    hipStream_t st = as_stream(stream);
+    if (dtype == CSU_BF16) {
+        carafe_bwd_enc<bf16><<<blocks(n_out), NT, 0, st>>>(B, H, W, C, s, (const bf16*)x, wsave, (const bf16*)dout, (bf16*)denc);
+        carafe_bwd_x<bf16><<<blocks(n_in), NT, 0, st>>>(B, H, W, C, s, wsave, (const bf16*)dout, (bf16*)dx);
+    } else if (dtype == CSU_F32) {
+        carafe_bwd_enc<float><<<blocks(n_out), NT, 0, st>>>(B, H, W, C, s, (const float*)x, wsave, (const float*)dout, (float*)denc);
+        carafe_bwd_x<float><<<blocks(n_in), NT, 0, st>>>(B, H, W, C, s, wsave, (const float*)dout, (float*)dx);
+    } else {
+        return fail(CSU_E_ARG, "carafe_bwd: bad dtype");
+    }
+    return check_launch("carafe_bwd");
+}
+
+static long head_ppb(long P) { long r = (P + 1023) / 1024; return r < 64 ? 64 : r; }
+
+extern "C" size_t csu_head_bwd_workspace(long P, int C) {
+    const long ppb = head_ppb(P);
+    return (size_t)((P + ppb - 1) / ppb) * C * sizeof(float);
+}
+
+extern "C" int csu_head_fwd(long P, int C, int dtype, const void* x, const float* w, float* prob, void* stream) {
+    if (P < 1 || C < 8 || C > 64 || C % 8 || ((C / 8) & (C / 8 - 1)) || !x || !w || !prob)
+        return fail(CSU_E_ARG, "head_fwd: need C in {8,16,32,64}");
+    hipStream_t st = as_stream(stream);
+    if (dtype == CSU_BF16) head_fwd<bf16><<<blocks(P * (C / 8)), NT, 0, st>>>(P, C, (const bf16*)x, w, prob);
+    else if (dtype == CSU_F32) head_fwd<float><<<blocks(P * (C / 8)), NT, 0, st>>>(P, C, (const float*)x, w, prob);
+    else return fail(CSU_E_ARG, "head_fwd: bad dtype");
+    return check_launch("head_fwd");
+}
+
+extern "C" int csu_head_bwd(long P, int C, int dtype, const void* x, const float* w, const float* prob,
+                            const float* dprob, void* dx, float* dw, void* workspace, size_t ws_bytes, void* stream) {
+    if (P < 1 || C < 8 || C > 64 || C % 8 || ((C / 8) & (C / 8 - 1)) || !x || !w || !prob || !dprob || !dx || !dw)
+        return fail(CSU_E_ARG, "head_bwd: bad args");
+    if (!workspace || ws_bytes < csu_head_bwd_workspace(P, C)) return fail(CSU_E_WORKSPACE, "head_bwd: workspace");
+    hipStream_t st = as_stream(stream);
+    const long ppb = head_ppb(P);
+    const int nb = (int)((P + ppb - 1) / ppb);
+    float* part = (float*)workspace;
+    if (dtype == CSU_BF16)
+        head_bwd<bf16><<<nb, NT, 0, st>>>(P, C, ppb, (const bf16*)x, w, prob, dprob, (bf16*)dx, part);
+    else if (dtype == CSU_F32)
+        head_bwd<float><<<nb, NT, 0, st>>>(P, C, ppb, (const float*)x, w, prob, dprob, (float*)dx, part);
+    else
+        return fail(CSU_E_ARG, "head_bwd: bad dtype");
+    head_wreduce<<<1, 256, 0, st>>>(C, nb, part, dw);
+    return check_launch("head_bwd");
+}

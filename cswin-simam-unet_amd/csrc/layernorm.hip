@@ -116,18 +116,26 @@ __global__ __launch_bounds__(NT) void ln_bwd(int rows, int C, int rows_per_block
     }
 }
 
-__global__ void ln_bwd_reduce(int C, int nblocks, const float* __restrict__ part, float* __restrict__ dgamma,
-                              float* __restrict__ dbeta) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= 2 * C) return;
+// sum the per-block partials in a fixed order: 64 columns x 4 block-lanes per workgroup, the
+// 4 lanes' partial sums combined in LDS in lane order (deterministic, fully parallel over columns)
+__global__ __launch_bounds__(256) void ln_bwd_reduce(int C, int nblocks, const float* __restrict__ part,
+                                                     float* __restrict__ dgamma, float* __restrict__ dbeta) {
+    __shared__ float red[4][64];
+    const int col = blockIdx.x * 64 + (threadIdx.x & 63), lane4 = threadIdx.x >> 6;
     float s = 0.f;
-    for (int b = 0; b < nblocks; ++b) s += part[(size_t)b * 2 * C + i];
-    if (i < C) dgamma[i] = s;
-    else dbeta[i - C] = s;
+    if (col < 2 * C)
+        for (int b = lane4; b < nblocks; b += 4) s += part[(size_t)b * 2 * C + col];
+    red[lane4][threadIdx.x & 63] = s;
+    __syncthreads();
+    if (lane4 == 0 && col < 2 * C) {
+        s = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+        if (col < C) dgamma[col] = s;
+        else dbeta[col - C] = s;
+    }
 }
 
 int ln_blocks(int rows, int* rpb) {
-    int r = (rows + 1023) / 1024;
+    int r = (rows + 511) / 512;
     r = ((r + WAVES - 1) / WAVES) * WAVES;
     if (r < WAVES) r = WAVES;
     *rpb = r;
@@ -165,7 +173,7 @@ int launch_bwd(int rows, int C, const void* x, const float* g, const float* m, c
         case 8: ln_bwd<TX, TG, 8><<<nb, NT, 0, st>>>(rows, C, rpb, (const TX*)x, g, m, r, (const TG*)dy, (TX*)dx, part); break;
         default: return fail(CSU_E_UNSUPPORTED, "layernorm: C/64 must be 1, 2, 4 or 8");
     }
-    ln_bwd_reduce<<<(2 * C + 255) / 256, 256, 0, st>>>(C, nb, part, dgamma, dbeta);
+    ln_bwd_reduce<<<(2 * C + 63) / 64, 256, 0, st>>>(C, nb, part, dgamma, dbeta);
     return check_launch("layernorm_bwd");
 }
 

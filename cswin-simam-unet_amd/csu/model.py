@@ -215,13 +215,16 @@ class CARAFE(nn.Module):
     def forward(self, x):
         B, L, C = x.shape
         H = W = int(math.isqrt(L))
-        s, k = self.up_factor, self.kernel_size
-        xi = _tokens_as_nchw(x)
-        kern = self.encoder(self.down(xi))                                   # (B, 9 s^2, H, W)
-        kern = kern.reshape(B, k * k, s, s, H, W).softmax(dim=1)            # (b, tap, i, j, y, x)
-        nb = F.unfold(xi, k, padding=k // 2).reshape(B, C, k * k, H, W)
-        o = torch.einsum("btijhw,bcthw->bhiwjc", kern.to(nb.dtype), nb).reshape(B, H * s * W * s, C)
-        return F.linear(o, self.out.weight.reshape(self.out.weight.shape[0], C), self.out.bias)
+        s = self.up_factor
+        if self.kernel_size != 3:
+            raise NotImplementedError("the fused CARAFE kernel is specialised for kernel_size=3 (the reference's)")
+        xc = x.to(_compute_dtype(x))
+        # kernel prediction (cswin:408-409): 1x1 down as a token GEMM, 3x3 encoder on the NHWC view
+        d = F.linear(xc, self.down.weight.reshape(C // 4, C), self.down.bias)
+        enc = self.encoder(_tokens_as_nchw(d))                             # (B, 9 s^2, H, W), channels_last
+        # fused pixel_shuffle + softmax + unfold + matmul + pixel_shuffle (cswin:410-432)
+        r = ops.carafe_reassemble(xc, enc.permute(0, 2, 3, 1), H, W, s)   # (B, s^2 L, C)
+        return F.linear(r, self.out.weight.reshape(self.out.weight.shape[0], C), self.out.bias)
 
 
 class CARAFE4(CARAFE):
@@ -347,18 +350,25 @@ class CSWinTransformer(nn.Module):
         return _ln(x, self.norm_up, _compute_dtype(x))
 
     def up_x4(self, x):
+        """CARAFE4 x4 upsampling + 1x1 output conv (cswin:674-682); returns LOGITS only when the
+        fused sigmoid head cannot be used (num_classes != 1)."""
         B, new_HW, C = x.shape
         H = W = int(math.isqrt(new_HW))
         x = self.upsample1(x)                                             # (B, 16 L, 64) tokens
         w = self.output.weight.reshape(self.num_classes, -1)
-        logits = F.linear(x, w)                                           # 1x1 conv, no bias
+        logits = F.linear(x, w)
         return logits.transpose(1, 2).reshape(B, self.num_classes, 4 * H, 4 * W)
 
     def forward(self, x):
         x = self.forward_features(x)
         x = self.forward_up_features(x)
-        x = self.up_x4(x)
-        return torch.sigmoid(x.float())
+        if self.num_classes == 1:
+            B, L, C = x.shape
+            H = W = int(math.isqrt(L))
+            y = self.upsample1(x)                                         # (B, 16 L, 64)
+            prob = ops.sigmoid_head(y, self.output.weight)                # fused 1x1 conv + sigmoid
+            return prob.reshape(B, 1, 4 * H, 4 * W)
+        return torch.sigmoid(self.up_x4(x).float())
 
 
 class _TokensRearrange(nn.Module):

@@ -11,6 +11,27 @@ from . import _lib
 from ._lib import check, dtype_code, lib, ptr, require_device, stream_ptr
 
 
+_KERNEL_TIMER = None
+
+
+def set_kernel_timer(sink):
+    """Record (start_event, end_event, algorithmic_bytes, flops) of every csu_stripe_attn_fwd
+    launch into the list ``sink`` (None disables).  Events are recorded on the launch stream."""
+    global _KERNEL_TIMER
+    _KERNEL_TIMER = sink
+
+
+def _stripe_fwd_work(geom, B, esize):
+    """Algorithmic bytes (qkv read once, output + lse written once) and FLOPs of one launch."""
+    L = geom.reso * geom.reso
+    nb = len(geom.branches)
+    hs, ws, _ = geom.branches[0]
+    N = hs * ws
+    nbytes = B * L * (3 * geom.C + geom.C) * esize + nb * B * geom.heads * L * 4
+    flops = B * L * nb * geom.heads * 4 * N * geom.head_dim + 18 * B * L * geom.C
+    return nbytes, flops
+
+
 # ---------------------------------------------------------------------------------------------
 # Stripe attention + LePE (LePEAttention cswin:220-298, branches of CSWinBlock cswin:358-363)
 # ---------------------------------------------------------------------------------------------
@@ -57,8 +78,15 @@ class _StripeAttnFn(torch.autograd.Function):
         out = torch.empty(B, L, geom.C, dtype=qkv.dtype, device=qkv.device)
         lse = torch.empty(nb, B, geom.heads, L, dtype=torch.float32, device=qkv.device)
         a = geom.args(B, ws, bs)
+        timer = _KERNEL_TIMER
+        if timer is not None:
+            ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            ev0.record()
         check(lib().csu_stripe_attn_fwd(ctypes.byref(a), dtype_code(qkv), ptr(qkv), ptr(out), ptr(lse),
                                         stream_ptr(qkv.device)), "csu_stripe_attn_fwd")
+        if timer is not None:
+            ev1.record()
+            timer.append((ev0, ev1) + _stripe_fwd_work(geom, B, qkv.element_size()))
         ctx.geom = geom
         ctx.lepe_dtypes = [t.dtype for t in lepe]
         ctx.save_for_backward(qkv, out, lse, *ws, *bs)
@@ -137,3 +165,74 @@ class _LayerNormFn(torch.autograd.Function):
 def layer_norm(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, eps: float = 1e-5,
                out_dtype: Optional[torch.dtype] = None) -> torch.Tensor:
     return _LayerNormFn.apply(x, weight, bias, eps, out_dtype or x.dtype)
+
+
+# ---------------------------------------------------------------------------------------------
+# CARAFE reassembly (cswin:410-432 / 459-481) and the 1-class sigmoid head (cswin:680, 688)
+# ---------------------------------------------------------------------------------------------
+class _CarafeFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, enc, H: int, W: int, s: int):
+        require_device(x, enc)
+        x = x.contiguous()
+        enc = enc.to(x.dtype).contiguous()
+        B, L, C = x.shape
+        if L != H * W or tuple(enc.shape) != (B, H, W, 9 * s * s):
+            raise ValueError("carafe: shape mismatch")
+        out = torch.empty(B, L * s * s, C, dtype=x.dtype, device=x.device)
+        wsave = torch.empty(B, H, W, 9 * s * s, dtype=torch.float32, device=x.device)
+        check(lib().csu_carafe_fwd(B, H, W, C, s, dtype_code(x), ptr(x), ptr(enc), ptr(out), ptr(wsave),
+                                   stream_ptr(x.device)), "csu_carafe_fwd")
+        ctx.save_for_backward(x, wsave)
+        ctx.geo = (B, H, W, C, s)
+        ctx.enc_dtype = enc.dtype
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        x, wsave = ctx.saved_tensors
+        B, H, W, C, s = ctx.geo
+        dout = dout.to(x.dtype).contiguous()
+        dx = torch.empty_like(x)
+        denc = torch.empty(B, H, W, 9 * s * s, dtype=x.dtype, device=x.device)
+        check(lib().csu_carafe_bwd(B, H, W, C, s, dtype_code(x), ptr(x), ptr(wsave), ptr(dout), ptr(dx), ptr(denc),
+                                   stream_ptr(x.device)), "csu_carafe_bwd")
+        return dx, denc, None, None, None
+
+
+def carafe_reassemble(x: torch.Tensor, enc_nhwc: torch.Tensor, H: int, W: int, s: int) -> torch.Tensor:
+    """x (B, H*W, C) tokens, enc_nhwc (B, H, W, 9*s*s) kernel logits -> (B, s*s*H*W, C)."""
+    return _CarafeFn.apply(x, enc_nhwc, H, W, s)
+
+
+class _HeadFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w):
+        require_device(x, w)
+        x = x.contiguous()
+        wf = w.detach().float().contiguous().view(-1)
+        P, C = x.numel() // x.shape[-1], x.shape[-1]
+        prob = torch.empty(x.shape[:-1], dtype=torch.float32, device=x.device)
+        check(lib().csu_head_fwd(P, C, dtype_code(x), ptr(x), ptr(wf), ptr(prob), stream_ptr(x.device)), "csu_head_fwd")
+        ctx.save_for_backward(x, wf, prob)
+        ctx.wshape, ctx.wdtype = w.shape, w.dtype
+        return prob
+
+    @staticmethod
+    def backward(ctx, dprob):
+        x, wf, prob = ctx.saved_tensors
+        dprob = dprob.float().contiguous()
+        P, C = x.numel() // x.shape[-1], x.shape[-1]
+        dx = torch.empty_like(x)
+        dw = torch.empty(C, dtype=torch.float32, device=x.device)
+        L = lib()
+        n = L.csu_head_bwd_workspace(P, C)
+        work = torch.empty(max(n, 16), dtype=torch.uint8, device=x.device)
+        check(L.csu_head_bwd(P, C, dtype_code(x), ptr(x), ptr(wf), ptr(prob), ptr(dprob), ptr(dx), ptr(dw), ptr(work), n,
+                             stream_ptr(x.device)), "csu_head_bwd")
+        return dx, dw.view(ctx.wshape).to(ctx.wdtype)
+
+
+def sigmoid_head(x: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
+    """sigmoid(x @ w) for a 1-class 1x1 conv without bias: x (..., C) -> (...) fp32."""
+    return _HeadFn.apply(x, weight)

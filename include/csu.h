@@ -103,6 +103,30 @@ int csu_simam_fwd(int B, int L, int C, float lambda, int dtype, const void* x, v
 int csu_simam_bwd(int B, int L, int C, int dtype, const void* x, const float* stats, const void* dy,
                   void* dx, void* workspace, size_t ws_bytes, void* stream);
 
+/* ---------------------------------------------------------------------------------------
+ * CARAFE content-aware reassembly (CARAFE/CARAFE4.forward cswin:401-437 / 450-486, from the
+ * encoder logits to the input of the `out` 1x1 conv: pixel_shuffle + softmax over 9 taps +
+ * unfold + (C x 9)@(9 x s^2) + pixel_shuffle, fused).  x (B, H*W, C) tokens, enc (B, H, W, 9*s*s)
+ * NHWC logits with channel t*s*s + i*s + j, out (B, sH*sW, C); wsave fp32 (B, H, W, 9*s*s)
+ * softmax weights written by fwd for bwd.  C = 8 * 2^k <= 512.
+ * ------------------------------------------------------------------------------------- */
+int csu_carafe_fwd(int B, int H, int W, int C, int s, int dtype, const void* x, const void* enc,
+                   void* out, float* wsave, void* stream);
+/* dx (B, H*W, C) and denc (B, H, W, 9*s*s) written. */
+int csu_carafe_bwd(int B, int H, int W, int C, int s, int dtype, const void* x, const float* wsave,
+                   const void* dout, void* dx, void* denc, void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * 1-class output head: 1x1 conv without bias + sigmoid (CSWinTransformer.up_x4 `output`
+ * cswin:603/680 and forward's torch.sigmoid cswin:688).  x (P, C) tokens, w (C) fp32,
+ * prob (P) fp32.  C in {8, 16, 32, 64}.
+ * ------------------------------------------------------------------------------------- */
+int csu_head_fwd(long P, int C, int dtype, const void* x, const float* w, float* prob, void* stream);
+size_t csu_head_bwd_workspace(long P, int C);
+/* dprob -> dx (P, C) and dw (C) (deterministic two-pass reduction). */
+int csu_head_bwd(long P, int C, int dtype, const void* x, const float* w, const float* prob,
+                 const float* dprob, void* dx, float* dw, void* workspace, size_t ws_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -150,3 +150,48 @@ def test_cpu_tensor_fails_loudly():
     geom = ops.StripeGeometry(8, 32, 1, [(8, 1, 0)], 32 ** -0.5)
     with pytest.raises(CsuError):
         ops.stripe_attention(torch.zeros(1, 64, 96), geom, [torch.zeros(32, 1, 3, 3)], [torch.zeros(32)])
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("B,H,C,s", [(2, 8, 64, 2), (1, 16, 32, 4), (2, 4, 512, 2), (1, 7, 128, 2), (1, 5, 64, 4)])
+def test_carafe_module_vs_oracle(B, H, C, s, dtype):
+    """CARAFE / CARAFE4 module (HIP reassembly + conv/GEMM kernel prediction) vs the oracle."""
+    from csu.model import CARAFE
+    d = dev()
+    torch.manual_seed(B * 100 + H * 10 + s)
+    m = CARAFE(C, C // 2 if C > 32 else C, up_factor=s)
+    x = torch.randn(B, H * H, C)
+    gy = torch.randn(B, H * H * s * s, m.out.weight.shape[0])
+    p64 = {"." + k: v.double().requires_grad_(True) for k, v in m.state_dict().items()}
+    x64 = x.double().requires_grad_(True)
+    ref = O.carafe(x64, p64, "", s)
+    ref.backward(gy.double())
+    md = m.to(d)
+    xd = x.to(d).requires_grad_(True)
+    with torch.autocast("cuda", dtype=torch.bfloat16, enabled=dtype == torch.bfloat16):
+        y = md(xd)
+    y.float().backward(gy.to(d))
+    assert_close(y.float(), ref, dtype)
+    assert_close(xd.grad, x64.grad, dtype)
+    for k, p in md.named_parameters():
+        assert_close(p.grad, p64["." + k].grad, dtype)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_sigmoid_head_vs_torch(dtype):
+    from csu import ops
+    d = dev()
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(3, 4099, 64, generator=g).to(dtype)
+    w = torch.randn(1, 64, 1, 1, generator=g) * 0.2
+    dp = torch.randn(3, 4099, generator=g)
+    x64, w64 = x.double().requires_grad_(True), w.double().requires_grad_(True)
+    ref = torch.sigmoid(x64 @ w64.view(64))
+    ref.backward(dp.double())
+    xd, wd = x.to(d).requires_grad_(True), w.to(d).requires_grad_(True)
+    p = ops.sigmoid_head(xd, wd)
+    p.backward(dp.to(d))
+    assert p.dtype == torch.float32
+    assert_close(p, ref, dtype)
+    assert_close(xd.grad, x64.grad, dtype)
+    assert_close(wd.grad, w64.grad, dtype)
