@@ -13,6 +13,7 @@ oracle (a restatement of the reference) timed on this host for a bounded sample.
 from __future__ import annotations
 
 import argparse
+import faulthandler
 import json
 import os
 import sys
@@ -44,6 +45,8 @@ def parse():
     ap.add_argument("--simam", action="store_true")
     ap.add_argument("--cpu-baseline", default="auto", choices=["auto", "on", "off"])
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--graph", default="auto", choices=["auto", "on", "off"],
+                    help="capture the whole step in a HIP graph (single process)")
     return ap.parse_args()
 
 
@@ -91,6 +94,7 @@ def cpu_baseline(args, dtype):
 
 
 def main():
+    faulthandler.enable()
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -114,26 +118,48 @@ def main():
     if world > 1:
         model = torch.nn.parallel.DistributedDataParallel(model, device_ids=[local], gradient_as_bucket_view=True,
                                                           static_graph=True, bucket_cap_mb=64)
-    opt = make_optimizer(model)
+    use_graph = args.graph == "on" or (args.graph == "auto" and world == 1)
+    opt = make_optimizer(model, capturable=use_graph)
     batches = synthetic_batches(2, args.batch, args.img, device, seed=1234 + rank)
+    amp = torch.bfloat16 if dtype == torch.bfloat16 else None
 
-    def step(i):
+    def eager_step(i):
         x, t = batches[i % len(batches)]
         opt.zero_grad(set_to_none=True)
-        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=dtype == torch.bfloat16):
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp is not None):
             y = model(x)
         loss = bce_loss(y, t)
         loss.backward()
         opt.step()
         return loss
 
-    for i in range(args.warmup):
+    step = eager_step
+    if use_graph:
+        # capture first (its eager warm-up runs on a side stream); eager steps on the default
+        # stream before the capture crash hipGraphInstantiate at this size (ROCm 7.2 / torch 2.10)
+        from csu.train import GraphedTrainStep
+        gstep = GraphedTrainStep(model, opt, bce_loss, batches[0][0], batches[0][1], amp, warmup=args.warmup)
+
+        def step(i):
+            x, t = batches[i % len(batches)]
+            return gstep(x, t)[0]
+    else:
+        for i in range(args.warmup):
+            eager_step(i)
+    # roofline leg: time every stripe-attention forward launch of a few eager steps of the same
+    # workload with HIP events on the launch stream (graph replays cannot host-record events)
+    prof = None
+    if not args.no_roofline:
+        prof = []
+        ops.set_kernel_timer(prof)
+        for i in range(min(args.steps, 3)):
+            eager_step(i)
+        ops.set_kernel_timer(None)
+    for i in range(2):
         step(i)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    prof = [] if not args.no_roofline else None
-    ops.set_kernel_timer(prof)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
@@ -142,7 +168,6 @@ def main():
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
-    ops.set_kernel_timer(None)
     t = torch.tensor([el], dtype=torch.float64, device=device)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -176,7 +201,8 @@ def main():
                                       f"{' +SimAM' if args.simam else ''}, AdamW",
                           "model": "CSWinTransformer", "params": nparams, "global_batch": args.batch * world,
                           "per_gpu_batch": args.batch, "img": args.img, "parallelism": f"dp{world}"},
-               "roofline": roof, "cpu_baseline": cpu, "final_loss": round(float(loss.item()), 5)}
+               "roofline": roof, "cpu_baseline": cpu, "final_loss": round(float(loss.item()), 5),
+               "hip_graph": use_graph}
         print(json.dumps(rec), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -78,6 +78,10 @@ __device__ __forceinline__ float wave_max(float v) {
 // row = (reg & 3) + 8 * (reg >> 2) + 4 * h, column = lane & 31.
 __device__ __forceinline__ constexpr int crow(int reg, int h) { return (reg & 3) + 8 * (reg >> 2) + 4 * h; }
 
+// deterministic column sum out[c] = sum_r in[r][c] (reduce.hip); ws of colsum_workspace() bytes
+size_t colsum_workspace(long rows, long cols, int dtype);
+int colsum_launch(long rows, long cols, int dtype, const void* in, float* out, float* ws, hipStream_t st);
+
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 }  // namespace csu

@@ -107,30 +107,13 @@ __global__ __launch_bounds__(NT) void ln_bwd(int rows, int C, int rows_per_block
         red[wave][1][c0 + j] = db[j];
     }
     __syncthreads();
+    // partials laid out [2][nblocks][C] (dgamma slab, then dbeta slab) for the column-sum pass
     for (int i = threadIdx.x; i < 2 * C; i += NT) {
         const int k = i / C, c = i % C;
         float s = 0.f;
 #pragma unroll
         for (int wv = 0; wv < WAVES; ++wv) s += red[wv][k][c];
-        part[(size_t)blockIdx.x * 2 * C + i] = s;
-    }
-}
-
-// sum the per-block partials in a fixed order: 64 columns x 4 block-lanes per workgroup, the
-// 4 lanes' partial sums combined in LDS in lane order (deterministic, fully parallel over columns)
-__global__ __launch_bounds__(256) void ln_bwd_reduce(int C, int nblocks, const float* __restrict__ part,
-                                                     float* __restrict__ dgamma, float* __restrict__ dbeta) {
-    __shared__ float red[4][64];
-    const int col = blockIdx.x * 64 + (threadIdx.x & 63), lane4 = threadIdx.x >> 6;
-    float s = 0.f;
-    if (col < 2 * C)
-        for (int b = lane4; b < nblocks; b += 4) s += part[(size_t)b * 2 * C + col];
-    red[lane4][threadIdx.x & 63] = s;
-    __syncthreads();
-    if (lane4 == 0 && col < 2 * C) {
-        s = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
-        if (col < C) dgamma[col] = s;
-        else dbeta[col - C] = s;
+        part[((size_t)k * gridDim.x + blockIdx.x) * C + c] = s;
     }
 }
 
@@ -173,8 +156,10 @@ int launch_bwd(int rows, int C, const void* x, const float* g, const float* m, c
         case 8: ln_bwd<TX, TG, 8><<<nb, NT, 0, st>>>(rows, C, rpb, (const TX*)x, g, m, r, (const TG*)dy, (TX*)dx, part); break;
         default: return fail(CSU_E_UNSUPPORTED, "layernorm: C/64 must be 1, 2, 4 or 8");
     }
-    ln_bwd_reduce<<<(2 * C + 63) / 64, 256, 0, st>>>(C, nb, part, dgamma, dbeta);
-    return check_launch("layernorm_bwd");
+    if (int e = check_launch("layernorm_bwd")) return e;
+    float* cws = part + (size_t)2 * nb * C;
+    if (int e = colsum_launch(nb, C, CSU_F32, part, dgamma, cws, st)) return e;
+    return colsum_launch(nb, C, CSU_F32, part + (size_t)nb * C, dbeta, cws, st);
 }
 
 }  // namespace
@@ -196,7 +181,8 @@ extern "C" int csu_layernorm_fwd(int rows, int C, float eps, int xdtype, const v
 
 extern "C" size_t csu_layernorm_bwd_workspace(int rows, int C) {
     int rpb;
-    return (size_t)ln_blocks(rows, &rpb) * 2 * C * sizeof(float);
+    const int nb = ln_blocks(rows, &rpb);
+    return (size_t)nb * 2 * C * sizeof(float) + colsum_workspace(nb, C, CSU_F32);
 }
 
 extern "C" int csu_layernorm_bwd(int rows, int C, int xdtype, const void* x, const float* gamma, const float* mean,

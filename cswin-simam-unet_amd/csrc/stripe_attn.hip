@@ -447,75 +447,121 @@ __global__ __launch_bounds__(NT) void stripe_bwd_dkdv(csu_stripe_args a, const T
 
 // =============================================================================================
 // LePE weight/bias gradient: dW[c][t] = sum_q dout[q][c] * V[q + off(t)][c], db[c] = sum_q dout
-// Pass 1: per (branch, token chunk) partial sums (fixed order); pass 2: sum chunks in order.
+// (window-local zero padding).  Pass 1: one thread = (image row, XS-token run, 4 channels); it
+// walks the run along x keeping a 3x3 register window of V (3 new loads per token instead of 9)
+// and writes per-block partial sums; pass 2 sums the block partials in a fixed order.
 // =============================================================================================
-constexpr int WG_CH = 256;   // channel lanes per pass-1 block
+constexpr int XS = 16;   // tokens per thread run
 
 template <typename T>
 __global__ __launch_bounds__(NT) void lepe_wgrad_partial(csu_stripe_args a, const T* __restrict__ qkv,
-                                                         const T* __restrict__ dout, int chunk, int nchunks,
-                                                         float* __restrict__ part) {
-    __shared__ float red[NT * 10];
+                                                         const T* __restrict__ dout, float* __restrict__ part) {
+    __shared__ float red[NT][41];
     const int br = blockIdx.y;
     const csu_stripe_branch& g = branch(a, br);
-    const int Cb = a.heads * HD;
-    const int L = a.reso * a.reso, C = a.C, C3 = 3 * C;
-    const int cw = min(Cb, WG_CH), tpc = NT / cw;
-    const int tl = threadIdx.x / cw, cl = threadIdx.x % cw;
-    const long t_begin = (long)blockIdx.x * chunk;
-    const long t_end = min((long)a.B * L, t_begin + chunk);
-    for (int cbase = 0; cbase < Cb; cbase += cw) {
-        const int c = cbase + cl;
-        float acc[10];
+    const int Cb = a.heads * HD, nq = Cb / 4;
+    const int reso = a.reso, L = reso * reso, C = a.C, C3 = 3 * C;
+    const int nseg = (reso + XS - 1) / XS;
+    const long items = (long)a.B * reso * nseg * nq;
+    const long it = (long)blockIdx.x * NT + threadIdx.x;
+    float acc[10][4];
 #pragma unroll
-        for (int k = 0; k < 10; ++k) acc[k] = 0.f;
-        for (long t = t_begin + tl; t < t_end; t += tpc) {
-            const int b = (int)(t / L), tok = (int)(t % L);
-            const int y = tok / a.reso, x = tok % a.reso;
-            const int iy = y % g.H_sp, ix = x % g.W_sp;
-            const float gv = to_f(dout[((size_t)b * L + tok) * C + g.ch_off + c]);
-            acc[9] += gv;
-            const T* vimg = qkv + (size_t)b * L * C3 + 2 * C + g.ch_off + c;
+    for (int k = 0; k < 10; ++k)
 #pragma unroll
-            for (int k = 0; k < 9; ++k) {
-                const int dy = k / 3 - 1, dx = k % 3 - 1;
-                if (iy + dy < 0 || iy + dy >= g.H_sp || ix + dx < 0 || ix + dx >= g.W_sp) continue;
-                acc[k] += gv * to_f(vimg[(size_t)((y + dy) * a.reso + x + dx) * C3]);
+        for (int j = 0; j < 4; ++j) acc[k][j] = 0.f;
+    const int cq = (int)(it % nq);
+    if (it < items) {
+        long r = it / nq;
+        const int seg = r % nseg; r /= nseg;
+        const int y = r % reso;
+        const int b = (int)(r / reso);
+        const int c0 = g.ch_off + 4 * cq;
+        const int iy = y % g.H_sp;
+        const T* vimg = qkv + (size_t)b * L * C3 + 2 * C + c0;
+        const T* gimg = dout + (size_t)b * L * C + c0;
+        bool yv[3];
+#pragma unroll
+        for (int dy = 0; dy < 3; ++dy) yv[dy] = iy + dy - 1 >= 0 && iy + dy - 1 < g.H_sp;
+        const int x0 = seg * XS, x1 = min(reso, x0 + XS);
+        float win[3][3][4];   // [dy][dx][ch]: V at (y+dy-1, x+dx-1)
+#pragma unroll
+        for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+            for (int dx = 0; dx < 2; ++dx) {
+                const int yy = y + dy - 1, xx = x0 + dx - 1;
+                if (yv[dy] && xx >= 0) load4(vimg + (size_t)(yy * reso + xx) * C3, win[dy][dx + 1]);
+                else win[dy][dx + 1][0] = win[dy][dx + 1][1] = win[dy][dx + 1][2] = win[dy][dx + 1][3] = 0.f;
+            }
+        for (int x = x0; x < x1; ++x) {
+#pragma unroll
+            for (int dy = 0; dy < 3; ++dy) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    win[dy][0][j] = win[dy][1][j];
+                    win[dy][1][j] = win[dy][2][j];
+                }
+                const int yy = y + dy - 1;
+                if (yv[dy] && x + 1 < reso) load4(vimg + (size_t)(yy * reso + x + 1) * C3, win[dy][2]);
+                else win[dy][2][0] = win[dy][2][1] = win[dy][2][2] = win[dy][2][3] = 0.f;
+            }
+            float gv[4];
+            load4(gimg + (size_t)(y * reso + x) * C, gv);
+            const int ix = x % g.W_sp;
+            const float mx[3] = {ix > 0 ? 1.f : 0.f, 1.f, ix + 1 < g.W_sp ? 1.f : 0.f};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                acc[9][j] += gv[j];
+#pragma unroll
+                for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+                    for (int dx = 0; dx < 3; ++dx) acc[dy * 3 + dx][j] += gv[j] * mx[dx] * win[dy][dx][j];
             }
         }
+    }
+    // block partial: threads sharing a channel quad are combined in thread order
 #pragma unroll
-        for (int k = 0; k < 10; ++k) red[k * NT + threadIdx.x] = acc[k];
-        __syncthreads();
-        if (tl == 0) {
-            for (int k = 0; k < 10; ++k) {
-                float s = 0.f;
-                for (int j = 0; j < tpc; ++j) s += red[k * NT + j * cw + cl];
-                part[(((size_t)br * nchunks + blockIdx.x) * Cb + c) * 10 + k] = s;
-            }
+    for (int k = 0; k < 10; ++k)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) red[threadIdx.x][k * 4 + j] = acc[k][j];
+    __syncthreads();
+    const int per = NT < nq ? 1 : NT / nq;          // threads per channel quad in this block
+    const int base_q = (int)(((long)blockIdx.x * NT) % nq);
+    for (int o = threadIdx.x; o < min(nq, NT) * 40; o += NT) {
+        const int ql = o / 40, kj = o % 40;          // local quad slot, (k, j)
+        float s = 0.f;
+        for (int m = 0; m < per; ++m) {
+            const int t = ql + m * min(nq, NT);
+            if (t < NT) s += red[t][kj];
         }
-        __syncthreads();
+        const int q = (base_q + ql) % nq;
+        const int c = 4 * q + (kj & 3), k = kj >> 2;
+        part[(((size_t)br * gridDim.x + blockIdx.x) * Cb + c) * 10 + k] = s;
     }
 }
 
-__global__ void lepe_wgrad_reduce(csu_stripe_args a, int nchunks, const float* __restrict__ part) {
+__global__ __launch_bounds__(256) void lepe_wgrad_reduce(csu_stripe_args a, int nblk, const float* __restrict__ part) {
+    __shared__ float red[8][32];
     const int br = blockIdx.y;
     const int Cb = a.heads * HD;
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;   // (c, k) pair
-    if (i >= Cb * 10) return;
-    const int c = i / 10, k = i % 10;
+    const int i = blockIdx.x * 32 + (threadIdx.x & 31);   // (c, k) pair
+    const int lane8 = threadIdx.x >> 5;
     float s = 0.f;
-    for (int j = 0; j < nchunks; ++j) s += part[(((size_t)br * nchunks + j) * Cb + c) * 10 + k];
-    const csu_stripe_branch& g = branch(a, br);
-    if (k < 9) g.lepe_dw[c * 9 + k] = s;
-    else g.lepe_db[c] = s;
+    if (i < Cb * 10)
+        for (int j = lane8; j < nblk; j += 8) s += part[((size_t)br * nblk + j) * Cb * 10 + i];
+    red[lane8][threadIdx.x & 31] = s;
+    __syncthreads();
+    if (lane8 == 0 && i < Cb * 10) {
+        for (int l = 1; l < 8; ++l) s += red[l][threadIdx.x];
+        const csu_stripe_branch& g = branch(a, br);
+        const int c = i / 10, k = i % 10;
+        if (k < 9) g.lepe_dw[c * 9 + k] = s;
+        else g.lepe_db[c] = s;
+    }
 }
 
-int wgrad_chunks(const csu_stripe_args& a, int* chunk) {
-    const long tokens = (long)a.B * a.reso * a.reso;
-    int ch = (int)((tokens + 511) / 512);
-    if (ch < 64) ch = 64;
-    *chunk = ch;
-    return (int)((tokens + ch - 1) / ch);
+int wgrad_blocks(const csu_stripe_args& a) {
+    const long items = (long)a.B * a.reso * ((a.reso + XS - 1) / XS) * (a.heads * HD / 4);
+    return (int)((items + NT - 1) / NT);
 }
 
 int validate(const csu_stripe_args* a, int dtype) {
@@ -563,9 +609,7 @@ extern "C" int csu_stripe_attn_fwd(const csu_stripe_args* a, int dtype, const vo
 
 extern "C" size_t csu_stripe_attn_bwd_workspace(const csu_stripe_args* a) {
     if (!a) return 0;
-    int chunk;
-    const int n = wgrad_chunks(*a, &chunk);
-    return (size_t)a->nbranch * n * a->heads * HD * 10 * sizeof(float);
+    return (size_t)a->nbranch * wgrad_blocks(*a) * a->heads * HD * 10 * sizeof(float);
 }
 
 extern "C" int csu_stripe_attn_bwd(const csu_stripe_args* a, int dtype, const void* qkv, const void* out,
@@ -579,20 +623,19 @@ extern "C" int csu_stripe_attn_bwd(const csu_stripe_args* a, int dtype, const vo
         return fail(CSU_E_WORKSPACE, "stripe_attn_bwd: workspace too small");
     hipStream_t st = as_stream(stream);
     const dim3 grid = grid_of(*a);
-    int chunk;
-    const int nch = wgrad_chunks(*a, &chunk);
+    const int nblk = wgrad_blocks(*a);
     float* part = (float*)workspace;
     const int Cb = a->heads * HD;
-    const dim3 rgrid((Cb * 10 + 255) / 256, a->nbranch);
+    const dim3 rgrid((Cb * 10 + 31) / 32, a->nbranch);
     if (dtype == CSU_BF16) {
         stripe_bwd_dq<bf16><<<grid, NT, 0, st>>>(*a, (const bf16*)qkv, (const bf16*)out, (const bf16*)dout, lse, delta, (bf16*)dqkv);
         stripe_bwd_dkdv<bf16><<<grid, NT, 0, st>>>(*a, (const bf16*)qkv, (const bf16*)dout, lse, delta, (bf16*)dqkv);
-        lepe_wgrad_partial<bf16><<<dim3(nch, a->nbranch), NT, 0, st>>>(*a, (const bf16*)qkv, (const bf16*)dout, chunk, nch, part);
+        lepe_wgrad_partial<bf16><<<dim3(nblk, a->nbranch), NT, 0, st>>>(*a, (const bf16*)qkv, (const bf16*)dout, part);
     } else {
         stripe_bwd_dq<float><<<grid, NT, 0, st>>>(*a, (const float*)qkv, (const float*)out, (const float*)dout, lse, delta, (float*)dqkv);
         stripe_bwd_dkdv<float><<<grid, NT, 0, st>>>(*a, (const float*)qkv, (const float*)dout, lse, delta, (float*)dqkv);
-        lepe_wgrad_partial<float><<<dim3(nch, a->nbranch), NT, 0, st>>>(*a, (const float*)qkv, (const float*)dout, chunk, nch, part);
+        lepe_wgrad_partial<float><<<dim3(nblk, a->nbranch), NT, 0, st>>>(*a, (const float*)qkv, (const float*)dout, part);
     }
-    lepe_wgrad_reduce<<<rgrid, 256, 0, st>>>(*a, nch, part);
+    lepe_wgrad_reduce<<<rgrid, 256, 0, st>>>(*a, nblk, part);
     return check_launch("stripe_attn_bwd");
 }

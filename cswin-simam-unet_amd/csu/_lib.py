@@ -53,6 +53,9 @@ _SIGS = {
     "csu_head_fwd": (ctypes.c_int, [ctypes.c_long, ctypes.c_int, ctypes.c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
     "csu_head_bwd_workspace": (c_size_t, [ctypes.c_long, ctypes.c_int]),
     "csu_head_bwd": (ctypes.c_int, [ctypes.c_long, ctypes.c_int, ctypes.c_int] + [c_void_p] * 7 + [c_size_t, c_void_p]),
+    "csu_colsum_workspace": (c_size_t, [ctypes.c_long, ctypes.c_long, ctypes.c_int]),
+    "csu_colsum": (ctypes.c_int, [ctypes.c_long, ctypes.c_long, ctypes.c_int, c_void_p, c_void_p, c_void_p, c_size_t,
+                                  c_void_p]),
 }
 
 _lib = None

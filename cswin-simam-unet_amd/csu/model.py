@@ -80,7 +80,8 @@ class Mlp(nn.Module):
         self.drop = nn.Dropout(drop)
 
     def forward(self, x):
-        return self.drop(self.fc2(self.drop(self.act(self.fc1(x)))))
+        h = self.act(ops.linear(x, self.fc1.weight, self.fc1.bias))
+        return self.drop(ops.linear(self.drop(h), self.fc2.weight, self.fc2.bias))
 
 
 def img2windows(img: torch.Tensor, H_sp: int, W_sp: int) -> torch.Tensor:
@@ -178,10 +179,10 @@ class CSWinBlock(nn.Module):
         if self.training and self.attns[0].attn_drop_p > 0:
             raise NotImplementedError("attention dropout inside the fused stripe kernel is not implemented yet")
         cd = _compute_dtype(x)
-        qkv = self.qkv(_ln(x, self.norm1, cd))
+        qkv = ops.linear(_ln(x, self.norm1, cd), self.qkv.weight, self.qkv.bias)
         att = ops.stripe_attention(qkv, self._geom, [a.get_v.weight for a in self.attns],
                                    [a.get_v.bias for a in self.attns])
-        x = x + self.drop_path(self.proj(att))
+        x = x + self.drop_path(ops.linear(att, self.proj.weight, self.proj.bias))
         x = x + self.drop_path(self.mlp(_ln(x, self.norm2, cd)))
         return x
 
@@ -220,11 +221,11 @@ class CARAFE(nn.Module):
             raise NotImplementedError("the fused CARAFE kernel is specialised for kernel_size=3 (the reference's)")
         xc = x.to(_compute_dtype(x))
         # kernel prediction (cswin:408-409): 1x1 down as a token GEMM, 3x3 encoder on the NHWC view
-        d = F.linear(xc, self.down.weight.reshape(C // 4, C), self.down.bias)
+        d = ops.linear(xc, self.down.weight.reshape(C // 4, C), self.down.bias)
         enc = self.encoder(_tokens_as_nchw(d))                             # (B, 9 s^2, H, W), channels_last
         # fused pixel_shuffle + softmax + unfold + matmul + pixel_shuffle (cswin:410-432)
         r = ops.carafe_reassemble(xc, enc.permute(0, 2, 3, 1), H, W, s)   # (B, s^2 L, C)
-        return F.linear(r, self.out.weight.reshape(self.out.weight.shape[0], C), self.out.bias)
+        return ops.linear(r, self.out.weight.reshape(self.out.weight.shape[0], C), self.out.bias)
 
 
 class CARAFE4(CARAFE):
@@ -311,6 +312,10 @@ class CSWinTransformer(nn.Module):
     def no_weight_decay_keywords(self):
         return {"relative_position_bias_table"}
 
+    @staticmethod
+    def _fuse(lin: nn.Linear, x: torch.Tensor) -> torch.Tensor:
+        return ops.linear(x, lin.weight, lin.bias)
+
     def _skip(self, t):
         return self.simam(t) if self.simam is not None else t
 
@@ -338,13 +343,13 @@ class CSWinTransformer(nn.Module):
     def forward_up_features(self, x):
         for blk in self.stage_up4:
             x = blk(x)
-        x = self.concat_linear4(torch.cat([self._skip(self.x3), self.upsample4(x)], -1))
+        x = self._fuse(self.concat_linear4, torch.cat([self._skip(self.x3), self.upsample4(x)], -1))
         for blk in self.stage_up3:
             x = blk(x)
-        x = self.concat_linear3(torch.cat([self._skip(self.x2), self.upsample3(x)], -1))
+        x = self._fuse(self.concat_linear3, torch.cat([self._skip(self.x2), self.upsample3(x)], -1))
         for blk in self.stage_up2:
             x = blk(x)
-        x = self.concat_linear2(torch.cat([self._skip(self.x1), self.upsample2(x)], -1))
+        x = self._fuse(self.concat_linear2, torch.cat([self._skip(self.x1), self.upsample2(x)], -1))
         for blk in self.stage_up1:
             x = blk(x)
         return _ln(x, self.norm_up, _compute_dtype(x))
@@ -359,7 +364,24 @@ class CSWinTransformer(nn.Module):
         logits = F.linear(x, w)
         return logits.transpose(1, 2).reshape(B, self.num_classes, 4 * H, 4 * W)
 
+    def _linear_weights(self):
+        for m in self.modules():
+            if isinstance(m, nn.Linear):
+                yield m.weight
+
     def forward(self, x):
+        cd = _compute_dtype(x)
+        if cd != torch.float32 and x.is_cuda:
+            if not hasattr(self, "_cast_cache"):
+                self._cast_cache = ops.CastCache()
+            self._cast_cache.refresh(self._linear_weights(), cd)   # one multi-tensor cast per step
+            ops.set_cast_cache(self._cast_cache)
+        try:
+            return self._forward(x)
+        finally:
+            ops.set_cast_cache(None)
+
+    def _forward(self, x):
         x = self.forward_features(x)
         x = self.forward_up_features(x)
         if self.num_classes == 1:

@@ -236,3 +236,108 @@ class _HeadFn(torch.autograd.Function):
 def sigmoid_head(x: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
     """sigmoid(x @ w) for a 1-class 1x1 conv without bias: x (..., C) -> (...) fp32."""
     return _HeadFn.apply(x, weight)
+
+
+# ---------------------------------------------------------------------------------------------
+# Token Linear (nn.Linear on (B, L, C) tokens) with a split-K weight gradient.
+# The weight gradient dW = dY^T X reduces over all B*L tokens (K up to 4M); a plain GEMM keeps
+# only (N/64)*(K/64) workgroups busy for the whole token range, so it is split into S token
+# chunks computed as one batched GEMM and summed in fp32 (deterministic).
+# ---------------------------------------------------------------------------------------------
+def colsum(x2: torch.Tensor) -> torch.Tensor:
+    """Deterministic fp32 column sum of a 2-D (rows, cols) tensor on the device (csu_colsum)."""
+    require_device(x2)
+    x2 = x2.contiguous()
+    rows, cols = x2.shape
+    out = torch.empty(cols, dtype=torch.float32, device=x2.device)
+    L = lib()
+    n = L.csu_colsum_workspace(rows, cols, dtype_code(x2))
+    work = torch.empty(max(n, 16), dtype=torch.uint8, device=x2.device)
+    check(L.csu_colsum(rows, cols, dtype_code(x2), ptr(x2), ptr(out), ptr(work), n, stream_ptr(x2.device)), "csu_colsum")
+    return out
+
+
+def _splitk_wgrad(dy2: torch.Tensor, x2: torch.Tensor) -> torch.Tensor:
+    M = dy2.shape[0]
+    S = max(1, min(128, M // 2048))
+    while S > 1 and M % S:
+        S -= 1
+    if S == 1:
+        return (dy2.t() @ x2).float()
+    N, K = dy2.shape[1], x2.shape[1]
+    part = torch.bmm(dy2.view(S, M // S, N).transpose(1, 2), x2.view(S, M // S, K))
+    return colsum(part.view(S, N * K)).view(N, K)
+
+
+class _LinearFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, cd, wc):
+        xc = x if x.dtype == cd else x.to(cd)
+        if wc is None:
+            wc = weight.to(cd)
+        y = torch.nn.functional.linear(xc, wc, None if bias is None else bias.to(cd))
+        ctx.save_for_backward(xc, wc)
+        ctx.meta = (x.dtype, weight.dtype, None if bias is None else bias.dtype)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        xc, wc = ctx.saved_tensors
+        xdt, wdt, bdt = ctx.meta
+        K, N = xc.shape[-1], dy.shape[-1]
+        dy2 = dy.reshape(-1, N)
+        if dy2.dtype != wc.dtype:
+            dy2 = dy2.to(wc.dtype)
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = (dy2 @ wc).view(xc.shape)
+            if dx.dtype != xdt:
+                dx = dx.to(xdt)
+        if ctx.needs_input_grad[1]:
+            dw = _splitk_wgrad(dy2, xc.reshape(-1, K)).to(wdt)
+        if bdt is not None and ctx.needs_input_grad[2]:
+            db = colsum(dy2).to(bdt)
+        return dx, dw, db, None, None
+
+
+class CastCache:
+    """bf16 shadow copies of fp32 master weights, refreshed with ONE multi-tensor copy per
+    forward (instead of one cast kernel per Linear).  Gradients still flow to the fp32 params."""
+
+    def __init__(self):
+        self.params, self.shadow, self.dtype = [], [], None
+        self.index = {}
+
+    def refresh(self, params, dtype):
+        params = list(params)
+        if self.dtype != dtype or len(params) != len(self.params) or any(a is not b for a, b in zip(params, self.params)):
+            self.params, self.dtype = params, dtype
+            self.shadow = [torch.empty(p.shape, dtype=dtype, device=p.device) for p in params]
+            self.index = {id(p): i for i, p in enumerate(params)}
+        with torch.no_grad():
+            torch._foreach_copy_(self.shadow, [p.detach() for p in self.params])
+
+    def get(self, p, dtype):
+        i = self.index.get(id(p))
+        if i is None or self.dtype != dtype:
+            return None
+        return self.shadow[i]
+
+
+_ACTIVE_CACHE: Optional[CastCache] = None
+
+
+def set_cast_cache(cache: Optional[CastCache]):
+    global _ACTIVE_CACHE
+    _ACTIVE_CACHE = cache
+
+
+def linear(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """nn.Linear on tokens in the autocast compute dtype (bf16 under autocast) with split-K dW."""
+    if x.is_cuda and torch.is_autocast_enabled("cuda"):
+        cd = torch.get_autocast_dtype("cuda")
+    else:
+        cd = torch.promote_types(x.dtype, weight.dtype)
+    wc = _ACTIVE_CACHE.get(weight, cd) if _ACTIVE_CACHE is not None else None
+    with torch.autocast("cuda", enabled=False):
+        return _LinearFn.apply(x, weight, bias, cd, wc)

@@ -127,6 +127,15 @@ size_t csu_head_bwd_workspace(long P, int C);
 int csu_head_bwd(long P, int C, int dtype, const void* x, const float* w, const float* prob,
                  const float* dprob, void* dx, float* dw, void* workspace, size_t ws_bytes, void* stream);
 
+/* ---------------------------------------------------------------------------------------
+ * Deterministic column sum out[c] = sum_r in[r][c], fp32 accumulation (rows x cols row-major,
+ * dtype in; out fp32).  The bias gradient of every nn.Linear (cswin:185/187/314/323/568/581/592)
+ * is the column sum of dY over the B*L tokens; also reduces split-K weight-gradient slabs.
+ * ------------------------------------------------------------------------------------- */
+size_t csu_colsum_workspace(long rows, long cols, int dtype);
+int csu_colsum(long rows, long cols, int dtype, const void* in, float* out, void* workspace,
+               size_t ws_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -195,3 +195,30 @@ def test_sigmoid_head_vs_torch(dtype):
     assert_close(p, ref, dtype)
     assert_close(xd.grad, x64.grad, dtype)
     assert_close(wd.grad, w64.grad, dtype)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("rows,cols", [(1, 8), (262144, 64), (4096, 2048), (128, 12288), (7, 40), (100000, 200)])
+def test_colsum_deterministic(rows, cols, dtype):
+    from csu import ops
+    d = dev()
+    x = torch.randn(rows, cols, device=d).to(dtype)
+    a, b = ops.colsum(x), ops.colsum(x)
+    assert torch.equal(a, b)                      # bitwise reproducible
+    ref = x.double().sum(0)
+    torch.testing.assert_close(a.double(), ref, rtol=1e-5, atol=1e-3 * max(1.0, rows ** 0.5) * 1e-2)
+
+
+def test_linear_splitk_matches_torch():
+    from csu import ops
+    d = dev()
+    x = torch.randn(8, 4096, 64, device=d, requires_grad=True)
+    w = torch.randn(256, 64, device=d, requires_grad=True)
+    b = torch.randn(256, device=d, requires_grad=True)
+    gy = torch.randn(8, 4096, 256, device=d)
+    y = ops.linear(x, w, b)
+    y.backward(gy)
+    x2, w2, b2 = (t.detach().double().requires_grad_(True) for t in (x, w, b))
+    torch.nn.functional.linear(x2, w2, b2).backward(gy.double())
+    for a_, r_ in ((y, torch.nn.functional.linear(x2, w2, b2)), (x.grad, x2.grad), (w.grad, w2.grad), (b.grad, b2.grad)):
+        assert_close(a_, r_, torch.float32)

@@ -110,3 +110,36 @@ def test_simam_model_runs_and_differs():
     yo = O.cswin_forward({k: v.double() for k, v in p.items()}, xs, O.CSWinConfig(img_size=128, split_size=(1, 2, 4, 4), simam=True))
     yg = b(xs.float().to(d))
     torch.testing.assert_close(yg.double().cpu(), yo, rtol=1e-4, atol=1e-4)
+
+
+def test_graphed_train_step_matches_eager():
+    """The HIP-graph captured step (GraphedTrainStep) reproduces eager training steps."""
+    import copy
+    from csu.model import CSWinTransformer
+    from csu.train import GraphedTrainStep, bce_loss, make_optimizer
+    d = dev()
+    cfg = O.CSWinConfig(img_size=128, split_size=(1, 2, 4, 4))
+    p = O.recipe_params(cfg, seed=0)
+    ma = CSWinTransformer(img_size=128, split_size=[1, 2, 4, 4]).to(d)
+    ma.load_state_dict(p)
+    mb = copy.deepcopy(ma)
+    oa, ob = make_optimizer(ma), make_optimizer(mb, capturable=True)
+    g = torch.Generator().manual_seed(1)
+    xs = [torch.rand(2, 3, 128, 128, generator=g).to(d) for _ in range(3)]
+    ts = [(torch.rand(2, 1, 128, 128, generator=g) > 0.5).float().to(d) for _ in range(3)]
+    gs = GraphedTrainStep(mb, ob, bce_loss, xs[0], ts[0], None, warmup=1)
+    # the constructor runs one eager warm-up step on (xs[0], ts[0]); mirror it, then compare 3 steps
+    oa.zero_grad(set_to_none=True)
+    bce_loss(ma(xs[0]), ts[0]).backward()
+    oa.step()
+    la = []
+    for x, t in zip(xs, ts):
+        oa.zero_grad(set_to_none=True)
+        loss = bce_loss(ma(x), t)
+        loss.backward()
+        oa.step()
+        la.append(loss.item())
+    lb = [gs(x, t)[0].item() for x, t in zip(xs, ts)]
+    np.testing.assert_allclose(lb, la, rtol=1e-4, atol=1e-6)
+    for (ka, pa), (kb, pb) in zip(ma.named_parameters(), mb.named_parameters()):
+        torch.testing.assert_close(pb, pa, rtol=1e-4, atol=1e-5)
