@@ -107,13 +107,13 @@ __global__ __launch_bounds__(NT) void ln_bwd(int rows, int C, int rows_per_block
         red[wave][1][c0 + j] = db[j];
     }
     __syncthreads();
-    // partials laid out [2][nblocks][C] (dgamma slab, then dbeta slab) for the column-sum pass
+    // partials laid out [nblocks][2C] (dgamma | dbeta) for the column-sum pass
     for (int i = threadIdx.x; i < 2 * C; i += NT) {
         const int k = i / C, c = i % C;
         float s = 0.f;
 #pragma unroll
         for (int wv = 0; wv < WAVES; ++wv) s += red[wv][k][c];
-        part[((size_t)k * gridDim.x + blockIdx.x) * C + c] = s;
+        part[(size_t)blockIdx.x * 2 * C + i] = s;
     }
 }
 
@@ -158,8 +158,13 @@ int launch_bwd(int rows, int C, const void* x, const float* g, const float* m, c
     }
     if (int e = check_launch("layernorm_bwd")) return e;
     float* cws = part + (size_t)2 * nb * C;
-    if (int e = colsum_launch(nb, C, CSU_F32, part, dgamma, cws, st)) return e;
-    return colsum_launch(nb, C, CSU_F32, part + (size_t)nb * C, dbeta, cws, st);
+    if (dbeta == dgamma + C) return colsum_launch(nb, 2 * C, CSU_F32, part, dgamma, cws, st);
+    float* tmp = cws + colsum_workspace(nb, 2 * C, CSU_F32) / sizeof(float);
+    if (int e = colsum_launch(nb, 2 * C, CSU_F32, part, tmp, cws, st)) return e;
+    if (hipMemcpyAsync(dgamma, tmp, C * sizeof(float), hipMemcpyDeviceToDevice, st) != hipSuccess ||
+        hipMemcpyAsync(dbeta, tmp + C, C * sizeof(float), hipMemcpyDeviceToDevice, st) != hipSuccess)
+        return check_launch("layernorm_bwd copy");
+    return 0;
 }
 
 }  // namespace
@@ -182,7 +187,7 @@ extern "C" int csu_layernorm_fwd(int rows, int C, float eps, int xdtype, const v
 extern "C" size_t csu_layernorm_bwd_workspace(int rows, int C) {
     int rpb;
     const int nb = ln_blocks(rows, &rpb);
-    return (size_t)nb * 2 * C * sizeof(float) + colsum_workspace(nb, C, CSU_F32);
+    return (size_t)nb * 2 * C * sizeof(float) + colsum_workspace(nb, 2 * C, CSU_F32) + 2 * C * sizeof(float);
 }
 
 extern "C" int csu_layernorm_bwd(int rows, int C, int xdtype, const void* x, const float* gamma, const float* mean,

@@ -102,7 +102,7 @@ Plan plan(long rows, long cols, int V) {
     p.tpr = t;
     p.colblocks = (int)((vecs + p.tpr - 1) / p.tpr);
     const int rpi = NT / p.tpr;
-    long want = (512 + p.colblocks - 1) / p.colblocks;
+    long want = rows <= 256 ? 1 : (512 + p.colblocks - 1) / p.colblocks;
     const long maxc = (rows + 8 * rpi - 1) / (8 * rpi);   // >= 8 rows per thread
     if (want > maxc) want = maxc;
     if (want < 1) want = 1;

@@ -1,0 +1,248 @@
+// Linear weight + bias gradient over token rows for gfx950 (bf16/fp32 in, fp32 out).
+//
+//   dW[n][k] = sum_m dY[m][n] * X[m][k],   db[n] = sum_m dY[m][n]       (m = the B*L tokens)
+// This is the backward of every nn.Linear of the model (qkv/proj/fc1/fc2 cswin:185/187/314/323,
+// concat_linear cswin:568/581/592, the CARAFE 1x1 convs cswin:396/399).  M is huge (up to 4M
+// tokens) while N, K <= 2048, so the reduction dim is split: workgroup (n-tile, k-tile, chunk)
+// accumulates a 64x64 tile over its token chunk with v_mfma_f32_32x32x16_bf16 (f32: 32x32x2),
+// both operands staged transposed in LDS ([n][m] / [k][m]) so MFMA fragments are 16-B reads.
+// Partial tiles (and the db partials of the k-tile-0 workgroups) go to a [chunk][N*K + N] slab
+// that one deterministic column-sum pass reduces in chunk order.
+#include "common.hpp"
+
+namespace csu {
+namespace {
+
+constexpr int NT = 256;
+constexpr int TM = 64;    // tokens per LDS step
+constexpr int TN = 64;    // output tile (n) per workgroup
+constexpr int TK = 64;    // output tile (k) per workgroup
+
+template <typename T> struct WCfg;
+template <> struct WCfg<bf16> { static constexpr int S = TM + 8; };  // [n][m] row stride (bf16 uses the tr-read path)
+template <> struct WCfg<float> { static constexpr int S = TM + 4; };
+
+// stage a TM x 64 row-major tile (rows m0.., columns c0..) of a (M, ld) matrix transposed into
+// img[64][S]; rows >= M and columns >= ncols are zero.  Pairs of rows are packed per LDS write.
+template <typename T>
+__device__ __forceinline__ void stage_t(const T* __restrict__ g, long M, int ld, int ncols, long m0, int c0, T* img) {
+    constexpr int V = 16 / sizeof(T);           // elements per 16-B load
+    constexpr int CPR = 64 / V;                 // chunks per row
+    constexpr int S = WCfg<T>::S;
+    for (int it = threadIdx.x; it < (TM / 2) * CPR; it += NT) {
+        const int pr = it / CPR, q = it % CPR;  // row pair, column chunk
+        const long m = m0 + 2 * pr;
+        const int c = c0 + q * V;
+        float a[V], b[V];
+        const bool cv = c < ncols;
+        if (cv && m < M) { if constexpr (V == 8) load8(g + m * ld + c, a); else load4(g + m * ld + c, a); }
+        else for (int j = 0; j < V; ++j) a[j] = 0.f;
+        if (cv && m + 1 < M) { if constexpr (V == 8) load8(g + (m + 1) * ld + c, b); else load4(g + (m + 1) * ld + c, b); }
+        else for (int j = 0; j < V; ++j) b[j] = 0.f;
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+            T* p = img + (q * V + j) * S + 2 * pr;
+            p[0] = from_f<T>(a[j]);
+            p[1] = from_f<T>(b[j]);
+        }
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(NT) void wgrad_kernel(long M, int N, int K, long rows_per_chunk, const T* __restrict__ dy,
+                                                   const T* __restrict__ x, float* __restrict__ part) {
+    constexpr int S = WCfg<T>::S;
+    __shared__ __attribute__((aligned(16))) T At[TN * S];   // dY^T tile [n][m]
+    __shared__ __attribute__((aligned(16))) T Bt[TK * S];   // X^T  tile [k][m]
+    __shared__ float bred[NT];
+    const int n0 = blockIdx.x * TN, k0 = blockIdx.y * TK;
+    const long m_begin = (long)blockIdx.z * rows_per_chunk;
+    const long m_end = min(M, m_begin + rows_per_chunk);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int r = lane & 31, h = lane >> 5;
+    const int wn = (wave >> 1) * 32, wk = (wave & 1) * 32;
+    const bool do_bias = blockIdx.y == 0;
+    f32x16 acc = {};
+    float bsum = 0.f;   // db partial of column n0 + (threadIdx.x & 63), rows threadIdx.x>>6 (mod 4)
+    for (long m0 = m_begin; m0 < m_end; m0 += TM) {
+        __syncthreads();
+        stage_t<T>(dy, m_end, N, N, m0, n0, At);
+        stage_t<T>(x, m_end, K, K, m0, k0, Bt);
+        __syncthreads();
+        if (do_bias) {   // column sums of the staged dY^T image: thread -> (n, quarter of m)
+            const int n = threadIdx.x & 63, qq = threadIdx.x >> 6;
+#pragma unroll
+            for (int j = 0; j < TM / 4; ++j) bsum += to_f(At[n * S + qq * (TM / 4) + j]);
+        }
+        if constexpr (sizeof(T) == 2) {
+#pragma unroll
+            for (int s = 0; s < TM / 16; ++s) {
+                const bf16x8 a = *reinterpret_cast<const bf16x8*>(At + (wn + r) * S + 16 * s + 8 * h);
+                const bf16x8 b = *reinterpret_cast<const bf16x8*>(Bt + (wk + r) * S + 16 * s + 8 * h);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc, 0, 0, 0);
+            }
+        } else {
+#pragma unroll
+            for (int t = 0; t < TM / 2; ++t)
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(At[(wn + r) * S + 2 * t + h], Bt[(wk + r) * S + 2 * t + h], acc, 0, 0, 0);
+        }
+    }
+    // acc[reg] = dW[n0 + wn + crow(reg, h)][k0 + wk + r]
+    const long slab = (long)N * K + N;
+    float* out = part + (long)blockIdx.z * slab;
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+        const int n = n0 + wn + crow(reg, h), k = k0 + wk + r;
+        if (n < N && k < K) out[(long)n * K + k] = acc[reg];
+    }
+    if (do_bias) {
+        bred[threadIdx.x] = bsum;
+        __syncthreads();
+        if (threadIdx.x < 64 && n0 + threadIdx.x < N)
+            out[(long)N * K + n0 + threadIdx.x] =
+                ((bred[threadIdx.x] + bred[threadIdx.x + 64]) + bred[threadIdx.x + 128]) + bred[threadIdx.x + 192];
+    }
+}
+
+// bf16 fast path: row-major LDS tiles filled by coalesced 16-B loads (prefetched one step ahead
+// in registers), MFMA fragments gathered with the gfx950 transposing read ds_read_b64_tr_b16
+// (lane 4q+p of a 16-lane group addresses row q, columns 4p..4p+3; lane i receives column i of
+// the 4 rows).  192-B rows make the transposed reads bank-conflict free.
+typedef short v4s __attribute__((ext_vector_type(4)));
+constexpr int RS = 96;   // bf16 elements per LDS row (64 data + 32 pad)
+
+__device__ __forceinline__ v4s tr_read(const bf16* p) {
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(p));
+}
+
+// 32x32x16 operand fragment of columns [c0, c0+32) at k-step rows [16s + 8h, +8) of a [TM][RS] tile
+__device__ __forceinline__ bf16x8 tr_frag(const bf16* img, int c0, int s, int lane) {
+    const int grp = lane >> 4, l = lane & 15, q = l >> 2, p = l & 3;
+    const int col = c0 + 16 * (grp & 1) + 4 * p;
+    const int row = 16 * s + 8 * (grp >> 1) + q;
+    const v4s lo = tr_read(img + row * RS + col);
+    const v4s hi = tr_read(img + (row + 4) * RS + col);
+    const v4s v[2] = {lo, hi};
+    bf16x8 out;
+    __builtin_memcpy(&out, v, 16);
+    return out;
+}
+
+__global__ __launch_bounds__(NT) void wgrad_bf16_tr(long M, int N, int K, long rows_per_chunk, const bf16* __restrict__ dy,
+                                                   const bf16* __restrict__ x, float* __restrict__ part) {
+    __shared__ __attribute__((aligned(16))) bf16 At[TM * RS];   // dY tile [m][n]
+    __shared__ __attribute__((aligned(16))) bf16 Bt[TM * RS];   // X  tile [m][k]
+    __shared__ float bred[NT][9];
+    const int n0 = blockIdx.x * TN, k0 = blockIdx.y * TK;
+    const long m_begin = (long)blockIdx.z * rows_per_chunk;
+    const long m_end = min(M, m_begin + rows_per_chunk);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int r = lane & 31, h = lane >> 5;
+    const int wn = (wave >> 1) * 32, wk = (wave & 1) * 32;
+    const bool do_bias = blockIdx.y == 0;
+    // this thread's two 16-B chunks per operand: chunk c = tid + 256 i -> row c / 8, column group c % 8
+    const int cg = threadIdx.x & 7, rr = threadIdx.x >> 3;   // rows rr and rr + 32
+    const bool nv = n0 + 8 * cg < N, kv = k0 + 8 * cg < K;
+    bf16x8 ra[2], rb[2];
+    float bsum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    auto load = [&](long m0) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const long m = m0 + rr + 32 * i;
+            const bool mv = m < m_end;
+            ra[i] = (mv && nv) ? *reinterpret_cast<const bf16x8*>(dy + m * N + n0 + 8 * cg) : bf16x8{};
+            rb[i] = (mv && kv) ? *reinterpret_cast<const bf16x8*>(x + m * K + k0 + 8 * cg) : bf16x8{};
+        }
+    };
+    f32x16 acc = {};
+    load(m_begin);
+    for (long m0 = m_begin; m0 < m_end; m0 += TM) {
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            *reinterpret_cast<bf16x8*>(At + (rr + 32 * i) * RS + 8 * cg) = ra[i];
+            *reinterpret_cast<bf16x8*>(Bt + (rr + 32 * i) * RS + 8 * cg) = rb[i];
+            if (do_bias)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) bsum[j] += (float)ra[i][j];
+        }
+        __syncthreads();
+        if (m0 + TM < m_end) load(m0 + TM);      // next step's loads fly during the MFMAs
+#pragma unroll
+        for (int s = 0; s < TM / 16; ++s) {
+            const bf16x8 a = tr_frag(At, wn, s, lane);
+            const bf16x8 b = tr_frag(Bt, wk, s, lane);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc, 0, 0, 0);
+        }
+    }
+    const long slab = (long)N * K + N;
+    float* out = part + (long)blockIdx.z * slab;
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+        const int n = n0 + wn + crow(reg, h), k = k0 + wk + r;
+        if (n < N && k < K) out[(long)n * K + k] = acc[reg];
+    }
+    if (do_bias) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) bred[threadIdx.x][j] = bsum[j];
+        __syncthreads();
+        if (threadIdx.x < 64) {
+            const int g = threadIdx.x >> 3, j = threadIdx.x & 7;   // column n0 + 8g + j
+            float s = 0.f;
+            for (int t = g; t < NT; t += 8) s += bred[t][j];
+            if (n0 + 8 * g + j < N) out[(long)N * K + n0 + 8 * g + j] = s;
+        }
+    }
+}
+
+struct WPlan {
+    int nt, kt, chunks;
+    long rpc;
+};
+
+WPlan wplan(long M, int N, int K) {
+    WPlan p;
+    p.nt = (N + TN - 1) / TN;
+    p.kt = (K + TK - 1) / TK;
+    long want = (1024 + p.nt * p.kt - 1) / (p.nt * p.kt);
+    const long maxc = (M + 511) / 512;          // >= 512 tokens per chunk
+    if (want > maxc) want = maxc;
+    if (want > 256) want = 256;
+    if (want < 1) want = 1;
+    p.chunks = (int)want;
+    p.rpc = ((M + p.chunks - 1) / p.chunks + TM - 1) / TM * TM;
+    p.chunks = (int)((M + p.rpc - 1) / p.rpc);
+    return p;
+}
+
+}  // namespace
+}  // namespace csu
+
+using namespace csu;
+
+extern "C" size_t csu_linear_wgrad_workspace(long M, int N, int K) {
+    const WPlan p = wplan(M, N, K);
+    const long slab = (long)N * K + N;
+    return (size_t)p.chunks * slab * sizeof(float) + colsum_workspace(p.chunks, slab, CSU_F32);
+}
+
+extern "C" int csu_linear_wgrad(long M, int N, int K, int dtype, const void* dy, const void* x, float* dw_db,
+                                void* workspace, size_t ws_bytes, void* stream) {
+    if (M < 1 || N < 1 || K < 1 || !dy || !x || !dw_db) return fail(CSU_E_ARG, "linear_wgrad: bad args");
+    const int V = dtype == CSU_BF16 ? 8 : 4;
+    if (N % V || K % V) return fail(CSU_E_ARG, "linear_wgrad: N and K must be multiples of 16 bytes");
+    if (!workspace || ws_bytes < csu_linear_wgrad_workspace(M, N, K)) return fail(CSU_E_WORKSPACE, "linear_wgrad: workspace");
+    hipStream_t st = as_stream(stream);
+    const WPlan p = wplan(M, N, K);
+    float* part = (float*)workspace;
+    const long slab = (long)N * K + N;
+    const dim3 grid(p.nt, p.kt, p.chunks);
+    if (dtype == CSU_BF16)
+        wgrad_bf16_tr<<<grid, NT, 0, st>>>(M, N, K, p.rpc, (const bf16*)dy, (const bf16*)x, part);
+    else if (dtype == CSU_F32)
+        wgrad_kernel<float><<<grid, NT, 0, st>>>(M, N, K, p.rpc, (const float*)dy, (const float*)x, part);
+    else
+        return fail(CSU_E_ARG, "linear_wgrad: bad dtype");
+    if (int e = check_launch("linear_wgrad")) return e;
+    return colsum_launch(p.chunks, slab, CSU_F32, part, dw_db, part + (size_t)p.chunks * slab, st);
+}

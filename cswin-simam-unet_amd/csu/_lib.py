@@ -56,6 +56,9 @@ _SIGS = {
     "csu_colsum_workspace": (c_size_t, [ctypes.c_long, ctypes.c_long, ctypes.c_int]),
     "csu_colsum": (ctypes.c_int, [ctypes.c_long, ctypes.c_long, ctypes.c_int, c_void_p, c_void_p, c_void_p, c_size_t,
                                   c_void_p]),
+    "csu_linear_wgrad_workspace": (c_size_t, [ctypes.c_long, ctypes.c_int, ctypes.c_int]),
+    "csu_linear_wgrad": (ctypes.c_int, [ctypes.c_long, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_void_p, c_void_p,
+                                        c_void_p, c_void_p, c_size_t, c_void_p]),
 }
 
 _lib = None

@@ -368,6 +368,8 @@ class CSWinTransformer(nn.Module):
         for m in self.modules():
             if isinstance(m, nn.Linear):
                 yield m.weight
+                if m.bias is not None:
+                    yield m.bias
 
     def forward(self, x):
         cd = _compute_dtype(x)

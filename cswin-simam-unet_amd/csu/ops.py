@@ -151,8 +151,8 @@ class _LayerNormFn(torch.autograd.Function):
         C = x.shape[-1]
         rows = x.numel() // C
         dx = torch.empty_like(x)
-        dg = torch.empty(C, dtype=torch.float32, device=x.device)
-        db = torch.empty(C, dtype=torch.float32, device=x.device)
+        dgb = torch.empty(2 * C, dtype=torch.float32, device=x.device)   # contiguous: one reduction pass
+        dg, db = dgb[:C], dgb[C:]
         L = lib()
         nbytes = L.csu_layernorm_bwd_workspace(rows, C)
         work = torch.empty(max(nbytes, 16), dtype=torch.uint8, device=x.device)
@@ -269,13 +269,32 @@ def _splitk_wgrad(dy2: torch.Tensor, x2: torch.Tensor) -> torch.Tensor:
     return colsum(part.view(S, N * K)).view(N, K)
 
 
+def linear_wgrad(dy2: torch.Tensor, x2: torch.Tensor):
+    """(dW (N, K), db (N)) fp32 of a token Linear: one MFMA split-K kernel + one reduction."""
+    require_device(dy2, x2)
+    M, N = dy2.shape
+    K = x2.shape[1]
+    out = torch.empty(N * K + N, dtype=torch.float32, device=dy2.device)
+    L = lib()
+    n = L.csu_linear_wgrad_workspace(M, N, K)
+    work = torch.empty(max(n, 16), dtype=torch.uint8, device=dy2.device)
+    check(L.csu_linear_wgrad(M, N, K, dtype_code(dy2), ptr(dy2), ptr(x2), ptr(out), ptr(work), n,
+                             stream_ptr(dy2.device)), "csu_linear_wgrad")
+    return out[:N * K].view(N, K), out[N * K:]
+
+
 class _LinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, cd, wc):
         xc = x if x.dtype == cd else x.to(cd)
         if wc is None:
             wc = weight.to(cd)
-        y = torch.nn.functional.linear(xc, wc, None if bias is None else bias.to(cd))
+        bc = None
+        if bias is not None:
+            bc = _ACTIVE_CACHE.get(bias, cd) if _ACTIVE_CACHE is not None else None
+            if bc is None:
+                bc = bias.to(cd)
+        y = torch.nn.functional.linear(xc, wc, bc)
         ctx.save_for_backward(xc, wc)
         ctx.meta = (x.dtype, weight.dtype, None if bias is None else bias.dtype)
         return y
@@ -293,6 +312,14 @@ class _LinearFn(torch.autograd.Function):
             dx = (dy2 @ wc).view(xc.shape)
             if dx.dtype != xdt:
                 dx = dx.to(xdt)
+        vec = 16 // dy2.element_size()
+        if N % vec == 0 and K % vec == 0 and dy2.dtype in (torch.float32, torch.bfloat16):
+            dwf, dbf = linear_wgrad(dy2.contiguous(), xc.reshape(-1, K))
+            if ctx.needs_input_grad[1]:
+                dw = dwf.to(wdt)
+            if bdt is not None and ctx.needs_input_grad[2]:
+                db = dbf.to(bdt)
+            return dx, dw, db, None, None
         if ctx.needs_input_grad[1]:
             dw = _splitk_wgrad(dy2, xc.reshape(-1, K)).to(wdt)
         if bdt is not None and ctx.needs_input_grad[2]:

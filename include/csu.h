@@ -136,6 +136,16 @@ size_t csu_colsum_workspace(long rows, long cols, int dtype);
 int csu_colsum(long rows, long cols, int dtype, const void* in, float* out, void* workspace,
                size_t ws_bytes, void* stream);
 
+/* ---------------------------------------------------------------------------------------
+ * Linear weight + bias gradient over M token rows (backward of every nn.Linear on tokens:
+ * cswin:185/187/314/323/568/581/592 and the CARAFE 1x1 convs cswin:396/399).
+ * dy (M, N), x (M, K) row-major, dtype in; dw_db fp32 [N*K + N] = dW (N, K) then db (N).
+ * Split-K over M with MFMA tiles + a deterministic reduction.  N, K multiples of 16 bytes.
+ * ------------------------------------------------------------------------------------- */
+size_t csu_linear_wgrad_workspace(long M, int N, int K);
+int csu_linear_wgrad(long M, int N, int K, int dtype, const void* dy, const void* x, float* dw_db,
+                     void* workspace, size_t ws_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

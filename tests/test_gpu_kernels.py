@@ -222,3 +222,22 @@ def test_linear_splitk_matches_torch():
     torch.nn.functional.linear(x2, w2, b2).backward(gy.double())
     for a_, r_ in ((y, torch.nn.functional.linear(x2, w2, b2)), (x.grad, x2.grad), (w.grad, w2.grad), (b.grad, b2.grad)):
         assert_close(a_, r_, torch.float32)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("M,N,K", [(262144, 256, 64), (4096, 512, 2048), (1000, 16, 64), (16384, 768, 256), (77, 64, 8)])
+def test_linear_wgrad_kernel(M, N, K, dtype):
+    from csu import ops
+    d = dev()
+    g = torch.Generator(device=d).manual_seed(M + N + K)
+    dy = torch.randn(M, N, device=d, generator=g).to(dtype)
+    x = torch.randn(M, K, device=d, generator=g).to(dtype)
+    dw, db = ops.linear_wgrad(dy, x)
+    dw2, db2 = ops.linear_wgrad(dy, x)
+    assert torch.equal(dw, dw2) and torch.equal(db, db2)       # deterministic
+    ref_w = dy.double().t() @ x.double()
+    ref_b = dy.double().sum(0)
+    scale_w = float(ref_w.abs().max())
+    tol = 1e-5 if dtype == torch.float32 else 1e-2
+    assert float((dw.double() - ref_w).abs().max()) <= tol * max(scale_w, M ** 0.5)
+    assert float((db.double() - ref_b).abs().max()) <= tol * max(float(ref_b.abs().max()), M ** 0.5)
