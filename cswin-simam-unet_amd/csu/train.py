@@ -51,43 +51,53 @@ def _world():
     return dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
 
 
-def _global_mean(t: torch.Tensor) -> torch.Tensor:
-    if _world() > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.SUM)
-        t = t / _world()
-    return t
+def _step_stats(loss, outputs, masks):
+    """Per-step sums (loss, sum(p*t), sum(p), sum(t)) of thresholded predictions, on device."""
+    preds = (outputs > 0.5).to(torch.float64).reshape(-1)
+    t = masks.to(torch.float64).reshape(-1)
+    return torch.stack([loss.detach().double(), (preds * t).sum(), preds.sum(), t.sum()])
+
+
+def _epoch_means(stats: List[torch.Tensor], smooth: float = 1e-6):
+    """Mean over steps of (loss, Dice, IoU) of the GLOBAL batch: the per-step sums of every rank
+    are all-reduced once per epoch, so each step's Dice/IoU is the reference's batch-flattened
+    value over the concatenation of all ranks' batches (cswin:692-708, 797-811)."""
+    if not stats:
+        return 0.0, 0.0, 0.0
+    s = torch.stack(stats)
+    w = _world()
+    if w > 1:
+        dist.all_reduce(s, op=dist.ReduceOp.SUM)
+        s[:, 0] /= w
+    inter, ps, ts = s[:, 1], s[:, 2], s[:, 3]
+    dice = (2.0 * inter + smooth) / (ps + ts + smooth)
+    iou = (inter + smooth) / (ps + ts - inter + smooth)
+    return float(s[:, 0].mean()), float(dice.mean()), float(iou.mean())
 
 
 def evaluate_model(model, data_loader, criterion, device):
     """eval mode, no grad; mean over batches of (loss, Dice, IoU) (cswin:712-747)."""
     model.eval()
-    acc = torch.zeros(3, dtype=torch.float64, device=device)
-    n = 0
+    stats = []
     with torch.no_grad():
         for images, masks in data_loader:
             images = images.to(device, non_blocking=True)
             masks = masks.to(device, non_blocking=True)
             outputs = model(images)
-            loss = criterion(outputs, masks)
-            preds = (outputs > 0.5).float()
-            acc += torch.stack([loss.detach().double(), _dice_t(preds, masks).double(), _iou_t(preds, masks).double()])
-            n += 1
-    acc = _global_mean(acc / max(n, 1))
-    loss, dice, iou = acc.tolist()
-    return loss, dice, iou
+            stats.append(_step_stats(criterion(outputs, masks), outputs, masks))
+    return _epoch_means(stats)
 
 
 def train_step(model, images, masks, criterion, optimizer):
-    """One reference step (cswin:779-794): zero_grad, forward, loss, backward, optimizer step,
-    thresholded metrics.  Returns device tensors (loss, dice, iou) -- no host sync."""
+    """One reference step (cswin:779-794): zero_grad, forward, loss, backward, optimizer step.
+    Returns the device tensor of per-step sums (loss, sum(p*t), sum(p), sum(t)) -- no host sync."""
     optimizer.zero_grad(set_to_none=True)
     outputs = model(images)
     loss = criterion(outputs, masks)
     loss.backward()
     optimizer.step()
     with torch.no_grad():
-        preds = (outputs > 0.5).float()
-        return loss.detach(), _dice_t(preds, masks), _iou_t(preds, masks)
+        return _step_stats(loss, outputs, masks)
 
 
 def train_model(model, train_loader, test_loader, criterion, optimizer, scheduler, device, num_epochs=100,
@@ -98,19 +108,18 @@ def train_model(model, train_loader, test_loader, criterion, optimizer, schedule
     rank0 = not (dist.is_available() and dist.is_initialized()) or dist.get_rank() == 0
     for epoch in range(num_epochs):
         model.train()
-        acc = torch.zeros(3, dtype=torch.float64, device=device)
+        sampler = getattr(train_loader, "sampler", None)
+        if hasattr(sampler, "set_epoch"):
+            sampler.set_epoch(epoch)
         it = train_loader
         if verbose and rank0 and tqdm is not None:
             it = tqdm(train_loader, desc=f"Epoch {epoch + 1}/{num_epochs} [TRAIN]")
-        nb = 0
+        stats = []
         for images, masks in it:
             images = images.to(device, non_blocking=True)
             masks = masks.to(device, non_blocking=True)
-            l, d, i = train_step(model, images, masks, criterion, optimizer)
-            acc += torch.stack([l.double(), d.double(), i.double()])
-            nb += 1
-        acc = _global_mean(acc / max(nb, 1))
-        train_loss, train_dice, train_iou = acc.tolist()
+            stats.append(train_step(model, images, masks, criterion, optimizer))
+        train_loss, train_dice, train_iou = _epoch_means(stats)
         test_loss, test_dice, test_iou = evaluate_model(model, test_loader, criterion, device)
         if scheduler is not None:
             scheduler.step(test_loss)

@@ -1,0 +1,91 @@
+"""Multi-process data-parallel logic on CPU (gloo, world size 2): DDP gradient averaging of the
+sharded batch == the single-process global batch, and the all-reduced per-step metric sums give
+the reference's batch-flattened Dice/IoU of the global batch."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _setup(seed=0):
+    from oracle import cswin_ref as O
+    from csu.data import ellipse_batch
+    cfg = O.CSWinConfig(img_size=64, split_size=(1, 2, 2, 2))
+    torch.manual_seed(seed)
+    model = O.OracleCSWin(cfg, O.recipe_params(cfg, seed=0))
+    xs, ts = ellipse_batch(np.random.default_rng(3), 4, 64)
+    return model, xs, ts
+
+
+def _train(model, batches, steps=2):
+    from csu.train import bce_loss, train_step
+    opt = torch.optim.AdamW(model.parameters(), lr=1e-3, weight_decay=1e-4)
+    stats = []
+    for i in range(steps):
+        x, t = batches[i % len(batches)]
+        stats.append(train_step(model, x, t, bce_loss, opt))
+    return stats
+
+
+def _worker(rank, world, port, out_path):
+    sys.path[:0] = [REPO, os.path.join(REPO, "cswin-simam-unet_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(2)
+    from csu.dist import init_distributed, wrap_ddp
+    from csu.train import _epoch_means
+    r, w, device = init_distributed("gloo")
+    model, xs, ts = _setup()
+    ddp = wrap_ddp(model, device)
+    shard = slice(2 * r, 2 * r + 2)
+    stats = _train(ddp, [(xs[shard], ts[shard])])
+    means = _epoch_means(stats)
+    if r == 0:
+        torch.save({"params": [p.detach().clone() for p in model.parameters()], "means": means}, out_path)
+    torch.distributed.destroy_process_group()
+
+
+def test_ddp_two_ranks_equals_global_batch(tmp_path):
+    out = str(tmp_path / "ddp.pt")
+    mp.spawn(_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    got = torch.load(out, weights_only=True)
+    from csu.train import _epoch_means
+    torch.set_num_threads(4)
+    model, xs, ts = _setup()
+    stats = _train(model, [(xs, ts)])
+    ref_means = _epoch_means(stats)
+    for a, b in zip(got["params"], model.parameters()):
+        torch.testing.assert_close(a, b.detach(), rtol=1e-3, atol=1e-5)   # Adam step of fp32 grads summed in another order
+    # loss: mean of per-rank means == global mean (equal shards); Dice/IoU from global sums
+    np.testing.assert_allclose(got["means"], ref_means, rtol=1e-6, atol=1e-7)
+
+
+def test_epoch_means_match_reference_formula():
+    """Single process: per-step batch-flattened Dice/IoU averaged over steps (cswin:692-708, 809-811)."""
+    from csu.train import _epoch_means, _step_stats
+    from oracle import cswin_ref as O
+    g = torch.Generator().manual_seed(0)
+    stats, ref = [], []
+    for _ in range(3):
+        p = torch.rand(2, 1, 16, 16, generator=g)
+        t = (torch.rand(2, 1, 16, 16, generator=g) > 0.5).float()
+        loss = O.bce_loss(p, t)
+        stats.append(_step_stats(loss, p, t))
+        d, i = O.dice_iou(p, t)
+        ref.append((loss.item(), d, i))
+    got = _epoch_means(stats)
+    np.testing.assert_allclose(got, np.mean(np.array(ref), axis=0), rtol=1e-6)
