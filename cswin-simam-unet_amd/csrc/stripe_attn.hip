@@ -564,6 +564,328 @@ int wgrad_blocks(const csu_stripe_args& a) {
     return (int)((items + NT - 1) / NT);
 }
 
+// =============================================================================================
+// v2 (bf16, window <= 256 tokens -- every stage of the 512x512 model): the whole window of the
+// head is resident in LDS.  Images are "natural" [token][32] rows of 64 B whose 16-B chunks are
+// XOR-swizzled by (row >> 2) & 3, which makes the 32-row ds_read_b128 fragment reads AND the
+// gfx950 transposing reads (ds_read_b64_tr_b16) used for the V^T / K^T / Q^T / dO^T operands
+// bank-conflict free; LePE neighbours are read from the same images.  One image serves both
+// orientations, so nothing is ever written transposed.
+// =============================================================================================
+constexpr int WMAX = 256;   // window tokens held in LDS
+
+__device__ __forceinline__ int swz(int row, int col) {   // element offset in a swizzled image
+    return row * HD + ((((col >> 3) ^ (row >> 2)) & 3) << 3) + (col & 7);
+}
+
+typedef short v4s __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ v4s tr_read(const bf16* p) {
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(p));
+}
+
+// A operand of X^T-orientation products: lane (r = channel d, h) gets image[k][d] for
+// k = kbase + 16s + 8(j>>2) + 4h + (j&3), the k order of an accumulator tile used as B operand.
+__device__ __forceinline__ bf16x8 tr_frag_acc(const bf16* img, int kbase, int s, int lane) {
+    const int grp = lane >> 4, l = lane & 15, q = l >> 2, p = l & 3;
+    const int col = 16 * (grp & 1) + 4 * p;
+    const int row = kbase + 16 * s + 4 * (grp >> 1) + q;
+    const v4s lo = tr_read(img + swz(row, col));
+    const v4s hi = tr_read(img + swz(row + 8, col));
+    const v4s v[2] = {lo, hi};
+    bf16x8 out;
+    __builtin_memcpy(&out, v, 16);
+    return out;
+}
+
+// acc += A(32 rows of the image starting at row0) * B^T, A rows read as 16-B fragments
+__device__ __forceinline__ void mma_rows_sw(f32x16& acc, const bf16* img, int row0, int r, int h, const Frag<bf16>& B) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(img + swz(row0 + r, 16 * s + 8 * h));
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, B.v[s], acc, 0, 0, 0);
+    }
+}
+
+__device__ __forceinline__ void mma_acc_sw(f32x16& acc, const bf16* img, int kbase, int lane, const f32x16& X) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+        bf16x8 b;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) b[j] = (bf16)X[8 * s + j];
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr_frag_acc(img, kbase, s, lane), b, acc, 0, 0, 0);
+    }
+}
+
+// gather the window rows [0, npad) of one head's channels into a swizzled image (rows >= N zero)
+__device__ __forceinline__ void stage_win(const Win& w, int reso, const bf16* img, int rstride, int ch, int npad,
+                                          bf16* dst) {
+    for (int it = threadIdx.x; it < npad * 4; it += NT) {
+        const int n = it >> 2, c = (it & 3) * 8;
+        bf16x8 v = {};
+        if (n < w.N) v = *reinterpret_cast<const bf16x8*>(img + (size_t)tok_of(w, reso, n) * rstride + ch + c);
+        *reinterpret_cast<bf16x8*>(dst + swz(n, c)) = v;
+    }
+}
+
+// LePE of window position n, channels c0..c0+3, from a swizzled LDS image
+__device__ __forceinline__ void lepe4_lds(const Win& w, const bf16* img, int n, int c0, const float* wts, int sign,
+                                          float* acc) {
+    const int iy = n / w.W_sp, ix = n - iy * w.W_sp;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[j] = sign > 0 ? wts[HD * 9 + c0 + j] : 0.f;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+        const int dy = sign * (t / 3 - 1), dx = sign * (t % 3 - 1);
+        const int y = iy + dy, x = ix + dx;
+        if (y < 0 || y >= w.H_sp || x < 0 || x >= w.W_sp) continue;
+        const bf16x4 v = *reinterpret_cast<const bf16x4*>(img + swz(y * w.W_sp + x, c0));
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[j] += wts[(c0 + j) * 9 + t] * (float)v[j];
+    }
+}
+
+__device__ __forceinline__ Win decode_w(const csu_stripe_args& a, int split) {
+    Win w;
+    w.br = blockIdx.y;
+    const csu_stripe_branch& g = branch(a, w.br);
+    w.H_sp = g.H_sp;
+    w.W_sp = g.W_sp;
+    w.N = w.H_sp * w.W_sp;
+    const int nwx = a.reso / w.W_sp, nwin = (a.reso / w.H_sp) * nwx;
+    int id = blockIdx.x;
+    w.blk = id % split; id /= split;
+    w.h = id % a.heads; id /= a.heads;
+    const int win = id % nwin;
+    w.b = id / nwin;
+    w.wy = win / nwx;
+    w.wx = win % nwx;
+    w.chq = g.ch_off + w.h * HD;
+    return w;
+}
+
+__global__ __launch_bounds__(NT) void stripe_fwd_w(csu_stripe_args a, int split, const bf16* __restrict__ qkv,
+                                                   bf16* __restrict__ out, float* __restrict__ lse) {
+    __shared__ __attribute__((aligned(16))) bf16 Ks[WMAX * HD];
+    __shared__ __attribute__((aligned(16))) bf16 Vs[WMAX * HD];
+    __shared__ float wts[HD * 10];
+    const Win w = decode_w(a, split);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int r = lane & 31, h = lane >> 5;
+    const int L = a.reso * a.reso, C = a.C, C3 = 3 * C;
+    const bf16* img = qkv + (size_t)w.b * L * C3;
+    const int npad = (w.N + 31) & ~31;
+    const int rows = (npad + split - 1) / split;            // query rows of this workgroup
+    const int qbeg = w.blk * rows, qend = min(npad, qbeg + rows);
+    stage_lepe_weights(branch(a, w.br), w.h, wts);
+    stage_win(w, a.reso, img, C3, C + w.chq, (npad + 63) & ~63, Ks);   // zero rows up to a 64-key step
+    stage_win(w, a.reso, img, C3, 2 * C + w.chq, (npad + 63) & ~63, Vs);
+    __syncthreads();
+    const float c = a.scale * kLog2e;
+    for (int q0 = qbeg + 32 * wave; q0 < qend; q0 += 128) {
+        const int qn = q0 + r;
+        const bool qvalid = qn < w.N;
+        const int qtok = qvalid ? tok_of(w, a.reso, qn) : 0;
+        Frag<bf16> qf;
+        load_frag(qf, img + (size_t)qtok * C3 + w.chq, h, qvalid);
+        float m = -INFINITY, l = 0.f;
+        f32x16 o = {};
+        // 64 keys per online-softmax step: two independent S^T tiles, one rescale of O
+        for (int kb = 0; kb < npad; kb += 64) {
+            f32x16 s0 = {}, s1 = {};
+            mma_rows_sw(s0, Ks, kb, r, h, qf);
+            mma_rows_sw(s1, Ks, kb + 32, r, h, qf);
+            float bm = -INFINITY;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                s0[i] = kb + crow(i, h) < w.N ? s0[i] * c : -INFINITY;
+                s1[i] = kb + 32 + crow(i, h) < w.N ? s1[i] * c : -INFINITY;
+                bm = fmaxf(bm, fmaxf(s0[i], s1[i]));
+            }
+            bm = fmaxf(bm, __shfl_xor(bm, 32, 64));
+            const float mn = fmaxf(m, bm);
+            const float alpha = __builtin_amdgcn_exp2f(m - mn);
+            m = mn;
+            float ls = 0.f;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                s0[i] = __builtin_amdgcn_exp2f(s0[i] - mn);
+                s1[i] = __builtin_amdgcn_exp2f(s1[i] - mn);
+                ls += s0[i] + s1[i];
+            }
+            l = l * alpha + ls;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) o[i] *= alpha;
+            mma_acc_sw(o, Vs, kb, lane, s0);
+            mma_acc_sw(o, Vs, kb + 32, lane, s1);
+        }
+        const float lt = l + __shfl_xor(l, 32, 64);
+        if (!qvalid) continue;
+        const float inv = 1.f / lt;
+        if (h == 0) lse[stat_index(a, w, qtok)] = (m + log2f(lt)) * kLn2;
+        bf16* orow = out + ((size_t)w.b * L + qtok) * C + w.chq;
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+            const int d0 = 8 * g4 + 4 * h;
+            float lp[4], v[4];
+            lepe4_lds(w, Vs, qn, d0, wts, +1, lp);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[j] = o[4 * g4 + j] * inv + lp[j];
+            store4(orow + d0, v);
+        }
+    }
+}
+
+__global__ __launch_bounds__(NT) void stripe_bwd_dq_w(csu_stripe_args a, int split, const bf16* __restrict__ qkv,
+                                                      const bf16* __restrict__ out, const bf16* __restrict__ dout,
+                                                      const float* __restrict__ lse, float* __restrict__ delta,
+                                                      bf16* __restrict__ dqkv) {
+    __shared__ __attribute__((aligned(16))) bf16 Ks[WMAX * HD];
+    __shared__ __attribute__((aligned(16))) bf16 Vs[WMAX * HD];
+    __shared__ float wts[HD * 10];
+    const Win w = decode_w(a, split);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int r = lane & 31, h = lane >> 5;
+    const int L = a.reso * a.reso, C = a.C, C3 = 3 * C;
+    const bf16* img = qkv + (size_t)w.b * L * C3;
+    const bf16* oimg = out + (size_t)w.b * L * C;
+    const bf16* gimg = dout + (size_t)w.b * L * C;
+    const int npad = (w.N + 31) & ~31;
+    const int rows = (npad + split - 1) / split;
+    const int qbeg = w.blk * rows, qend = min(npad, qbeg + rows);
+    stage_lepe_weights(branch(a, w.br), w.h, wts);
+    stage_win(w, a.reso, img, C3, C + w.chq, npad, Ks);
+    stage_win(w, a.reso, img, C3, 2 * C + w.chq, npad, Vs);
+    __syncthreads();
+    const float c = a.scale * kLog2e;
+    for (int q0 = qbeg + 32 * wave; q0 < qend; q0 += 128) {
+        const int qn = q0 + r;
+        const bool qvalid = qn < w.N;
+        const int qtok = qvalid ? tok_of(w, a.reso, qn) : 0;
+        Frag<bf16> qf, gf;
+        load_frag(qf, img + (size_t)qtok * C3 + w.chq, h, qvalid);
+        load_frag(gf, gimg + (size_t)qtok * C + w.chq, h, qvalid);
+        float dl = 0.f;
+        if (qvalid) {
+#pragma unroll
+            for (int g4 = 0; g4 < 4; ++g4) {
+                const int d0 = 8 * g4 + 4 * h;
+                float lp[4], ov[4], gv[4];
+                lepe4_lds(w, Vs, qn, d0, wts, +1, lp);
+                load4(oimg + (size_t)qtok * C + w.chq + d0, ov);
+                load4(gimg + (size_t)qtok * C + w.chq + d0, gv);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) dl += gv[j] * (ov[j] - lp[j]);
+            }
+        }
+        dl += __shfl_xor(dl, 32, 64);
+        const size_t si = stat_index(a, w, qtok);
+        if (qvalid && h == 0) delta[si] = dl;
+        const float lq = qvalid ? lse[si] * kLog2e : 0.f;
+        f32x16 dq = {};
+        for (int kb = 0; kb < npad; kb += 32) {
+            f32x16 s = {}, dp = {};
+            mma_rows_sw(s, Ks, kb, r, h, qf);
+            mma_rows_sw(dp, Vs, kb, r, h, gf);
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const float p = kb + crow(i, h) < w.N ? __builtin_amdgcn_exp2f(s[i] * c - lq) : 0.f;
+                s[i] = p * (dp[i] - dl);
+            }
+            mma_acc_sw(dq, Ks, kb, lane, s);
+        }
+        if (!qvalid) continue;
+        bf16* drow = dqkv + ((size_t)w.b * L + qtok) * C3 + w.chq;
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+            const int d0 = 8 * g4 + 4 * h;
+            float v[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[j] = dq[4 * g4 + j] * a.scale;
+            store4(drow + d0, v);
+        }
+    }
+}
+
+__global__ __launch_bounds__(NT) void stripe_bwd_dkdv_w(csu_stripe_args a, int split, const bf16* __restrict__ qkv,
+                                                        const bf16* __restrict__ dout, const float* __restrict__ lse,
+                                                        const float* __restrict__ delta, bf16* __restrict__ dqkv) {
+    __shared__ __attribute__((aligned(16))) bf16 Qs[WMAX * HD];
+    __shared__ __attribute__((aligned(16))) bf16 Gs[WMAX * HD];
+    __shared__ float lse_s[WMAX], dl_s[WMAX];
+    __shared__ float wts[HD * 10];
+    const Win w = decode_w(a, split);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int r = lane & 31, h = lane >> 5;
+    const int L = a.reso * a.reso, C = a.C, C3 = 3 * C;
+    const bf16* img = qkv + (size_t)w.b * L * C3;
+    const bf16* gimg = dout + (size_t)w.b * L * C;
+    const int npad = (w.N + 31) & ~31;
+    const int rows = (npad + split - 1) / split;
+    const int kbeg = w.blk * rows, kend = min(npad, kbeg + rows);
+    stage_lepe_weights(branch(a, w.br), w.h, wts);
+    stage_win(w, a.reso, img, C3, w.chq, npad, Qs);
+    stage_win(w, a.reso, gimg, C, w.chq, npad, Gs);
+    for (int i = threadIdx.x; i < npad; i += NT) {
+        const bool v = i < w.N;
+        const size_t si = stat_index(a, w, v ? tok_of(w, a.reso, i) : 0);
+        lse_s[i] = v ? lse[si] * kLog2e : INFINITY;
+        dl_s[i] = v ? delta[si] : 0.f;
+    }
+    __syncthreads();
+    const float c = a.scale * kLog2e;
+    for (int k0 = kbeg + 32 * wave; k0 < kend; k0 += 128) {
+        const int kn = k0 + r;
+        const bool kvalid = kn < w.N;
+        const int ktok = kvalid ? tok_of(w, a.reso, kn) : 0;
+        Frag<bf16> kf, vf;
+        load_frag(kf, img + (size_t)ktok * C3 + C + w.chq, h, kvalid);
+        load_frag(vf, img + (size_t)ktok * C3 + 2 * C + w.chq, h, kvalid);
+        f32x16 dk = {}, dv = {};
+        for (int qb = 0; qb < npad; qb += 32) {
+            f32x16 s = {}, dp = {};
+            mma_rows_sw(s, Qs, qb, r, h, kf);
+            mma_rows_sw(dp, Gs, qb, r, h, vf);
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int qi = qb + crow(i, h);
+                const float p = __builtin_amdgcn_exp2f(s[i] * c - lse_s[qi]);
+                s[i] = p;
+                dp[i] = p * (dp[i] - dl_s[qi]);
+            }
+            mma_acc_sw(dv, Gs, qb, lane, s);
+            mma_acc_sw(dk, Qs, qb, lane, dp);
+        }
+        if (!kvalid) continue;
+        bf16* drow = dqkv + ((size_t)w.b * L + ktok) * C3 + w.chq;
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+            const int d0 = 8 * g4 + 4 * h;
+            float vk[4], vv[4], lp[4];
+            lepe4_lds(w, Gs, kn, d0, wts, -1, lp);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                vk[j] = dk[4 * g4 + j] * a.scale;
+                vv[j] = dv[4 * g4 + j] + lp[j];
+            }
+            store4(drow + C + d0, vk);
+            store4(drow + 2 * C + d0, vv);
+        }
+    }
+}
+
+// split factor of the whole-window kernels: 2 workgroups per window-head when one per window-head
+// would leave fewer than 1024 workgroups (stage 3/4 at 512x512), else 1
+int wsplit(const csu_stripe_args& a) {
+    const int N = a.br[0].H_sp * a.br[0].W_sp;
+    const int nwin = (a.reso / a.br[0].H_sp) * (a.reso / a.br[0].W_sp);
+    const long wgs = (long)a.B * nwin * a.heads * a.nbranch;
+    return (N > 128 && wgs < 1024) ? 2 : 1;
+}
+
+bool use_window_path(const csu_stripe_args& a, int dtype) {
+    return dtype == CSU_BF16 && a.br[0].H_sp * a.br[0].W_sp <= WMAX;
+}
+
 int validate(const csu_stripe_args* a, int dtype) {
     if (!a) return fail(CSU_E_ARG, "stripe_attn: null args");
     if (a->head_dim != HD) return fail(CSU_E_UNSUPPORTED, "stripe_attn: head_dim must be 32");
@@ -599,6 +921,13 @@ extern "C" int csu_stripe_attn_fwd(const csu_stripe_args* a, int dtype, const vo
                                    float* lse, void* stream) {
     if (int e = validate(a, dtype)) return e;
     if (!qkv || !out || !lse) return fail(CSU_E_ARG, "stripe_attn_fwd: null buffer");
+    if (use_window_path(*a, dtype)) {
+        const int sp = wsplit(*a);
+        const int nwin = (a->reso / a->br[0].H_sp) * (a->reso / a->br[0].W_sp);
+        const dim3 g(a->B * nwin * a->heads * sp, a->nbranch);
+        stripe_fwd_w<<<g, NT, 0, as_stream(stream)>>>(*a, sp, (const bf16*)qkv, (bf16*)out, lse);
+        return check_launch("stripe_attn_fwd");
+    }
     const dim3 grid = grid_of(*a);
     if (dtype == CSU_BF16)
         stripe_fwd<bf16><<<grid, NT, 0, as_stream(stream)>>>(*a, (const bf16*)qkv, (bf16*)out, lse);
@@ -627,7 +956,14 @@ extern "C" int csu_stripe_attn_bwd(const csu_stripe_args* a, int dtype, const vo
     float* part = (float*)workspace;
     const int Cb = a->heads * HD;
     const dim3 rgrid((Cb * 10 + 31) / 32, a->nbranch);
-    if (dtype == CSU_BF16) {
+    if (use_window_path(*a, dtype)) {
+        const int sp = wsplit(*a);
+        const int nwin = (a->reso / a->br[0].H_sp) * (a->reso / a->br[0].W_sp);
+        const dim3 g(a->B * nwin * a->heads * sp, a->nbranch);
+        stripe_bwd_dq_w<<<g, NT, 0, st>>>(*a, sp, (const bf16*)qkv, (const bf16*)out, (const bf16*)dout, lse, delta, (bf16*)dqkv);
+        stripe_bwd_dkdv_w<<<g, NT, 0, st>>>(*a, sp, (const bf16*)qkv, (const bf16*)dout, lse, delta, (bf16*)dqkv);
+        lepe_wgrad_partial<bf16><<<dim3(nblk, a->nbranch), NT, 0, st>>>(*a, (const bf16*)qkv, (const bf16*)dout, part);
+    } else if (dtype == CSU_BF16) {
         stripe_bwd_dq<bf16><<<grid, NT, 0, st>>>(*a, (const bf16*)qkv, (const bf16*)out, (const bf16*)dout, lse, delta, (bf16*)dqkv);
         stripe_bwd_dkdv<bf16><<<grid, NT, 0, st>>>(*a, (const bf16*)qkv, (const bf16*)dout, lse, delta, (bf16*)dqkv);
         lepe_wgrad_partial<bf16><<<dim3(nblk, a->nbranch), NT, 0, st>>>(*a, (const bf16*)qkv, (const bf16*)dout, part);
