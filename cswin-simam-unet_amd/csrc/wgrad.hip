@@ -19,7 +19,6 @@ constexpr int TN = 64;    // output tile (n) per workgroup
 constexpr int TK = 64;    // output tile (k) per workgroup
 
 template <typename T> struct WCfg;
-template <> struct WCfg<bf16> { static constexpr int S = TM + 8; };  // [n][m] row stride (bf16 uses the tr-read path)
 template <> struct WCfg<float> { static constexpr int S = TM + 4; };
 
 // stage a TM x 64 row-major tile (rows m0.., columns c0..) of a (M, ld) matrix transposed into
@@ -128,6 +127,9 @@ __device__ __forceinline__ bf16x8 tr_frag(const bf16* img, int c0, int s, int la
     return out;
 }
 
+__device__ __forceinline__ float gelu_w(float v) { return 0.5f * v * (1.f + erff(v * 0.70710678118654752f)); }
+
+template <bool GELU_X>
 __global__ __launch_bounds__(NT) void wgrad_bf16_tr(long M, int N, int K, long rows_per_chunk, const bf16* __restrict__ dy,
                                                    const bf16* __restrict__ x, float* __restrict__ part) {
     __shared__ __attribute__((aligned(16))) bf16 At[TM * RS];   // dY tile [m][n]
@@ -161,7 +163,12 @@ __global__ __launch_bounds__(NT) void wgrad_bf16_tr(long M, int N, int K, long r
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
             *reinterpret_cast<bf16x8*>(At + (rr + 32 * i) * RS + 8 * cg) = ra[i];
-            *reinterpret_cast<bf16x8*>(Bt + (rr + 32 * i) * RS + 8 * cg) = rb[i];
+            bf16x8 xv = rb[i];
+            if constexpr (GELU_X) {   // X = gelu(h) on the fly (fc2's input, never materialised)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) xv[j] = (bf16)gelu_w((float)xv[j]);
+            }
+            *reinterpret_cast<bf16x8*>(Bt + (rr + 32 * i) * RS + 8 * cg) = xv;
             if (do_bias)
 #pragma unroll
                 for (int j = 0; j < 8; ++j) bsum[j] += (float)ra[i][j];
@@ -226,8 +233,16 @@ extern "C" size_t csu_linear_wgrad_workspace(long M, int N, int K) {
     return (size_t)p.chunks * slab * sizeof(float) + colsum_workspace(p.chunks, slab, CSU_F32);
 }
 
+extern "C" int csu_linear_wgrad_ex(long M, int N, int K, int dtype, const void* dy, const void* x, int x_gelu,
+                                   float* dw_db, void* workspace, size_t ws_bytes, void* stream);
+
 extern "C" int csu_linear_wgrad(long M, int N, int K, int dtype, const void* dy, const void* x, float* dw_db,
                                 void* workspace, size_t ws_bytes, void* stream) {
+    return csu_linear_wgrad_ex(M, N, K, dtype, dy, x, 0, dw_db, workspace, ws_bytes, stream);
+}
+
+extern "C" int csu_linear_wgrad_ex(long M, int N, int K, int dtype, const void* dy, const void* x, int x_gelu,
+                                   float* dw_db, void* workspace, size_t ws_bytes, void* stream) {
     if (M < 1 || N < 1 || K < 1 || !dy || !x || !dw_db) return fail(CSU_E_ARG, "linear_wgrad: bad args");
     const int V = dtype == CSU_BF16 ? 8 : 4;
     if (N % V || K % V) return fail(CSU_E_ARG, "linear_wgrad: N and K must be multiples of 16 bytes");
@@ -237,8 +252,11 @@ extern "C" int csu_linear_wgrad(long M, int N, int K, int dtype, const void* dy,
     float* part = (float*)workspace;
     const long slab = (long)N * K + N;
     const dim3 grid(p.nt, p.kt, p.chunks);
-    if (dtype == CSU_BF16)
-        wgrad_bf16_tr<<<grid, NT, 0, st>>>(M, N, K, p.rpc, (const bf16*)dy, (const bf16*)x, part);
+    if (x_gelu && dtype != CSU_BF16) return fail(CSU_E_UNSUPPORTED, "linear_wgrad: GELU prologue is bf16-only");
+    if (dtype == CSU_BF16 && x_gelu)
+        wgrad_bf16_tr<true><<<grid, NT, 0, st>>>(M, N, K, p.rpc, (const bf16*)dy, (const bf16*)x, part);
+    else if (dtype == CSU_BF16)
+        wgrad_bf16_tr<false><<<grid, NT, 0, st>>>(M, N, K, p.rpc, (const bf16*)dy, (const bf16*)x, part);
     else if (dtype == CSU_F32)
         wgrad_kernel<float><<<grid, NT, 0, st>>>(M, N, K, p.rpc, (const float*)dy, (const float*)x, part);
     else

@@ -59,6 +59,11 @@ _SIGS = {
     "csu_linear_wgrad_workspace": (c_size_t, [ctypes.c_long, ctypes.c_int, ctypes.c_int]),
     "csu_linear_wgrad": (ctypes.c_int, [ctypes.c_long, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_void_p, c_void_p,
                                         c_void_p, c_void_p, c_size_t, c_void_p]),
+    "csu_linear_wgrad_ex": (ctypes.c_int, [ctypes.c_long, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_void_p, c_void_p,
+                                           ctypes.c_int, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "csu_gemm": (ctypes.c_int, [ctypes.c_long, ctypes.c_int, ctypes.c_int, c_void_p, ctypes.c_int, c_void_p, ctypes.c_int,
+                                ctypes.c_int, ctypes.c_int, c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_int,
+                                ctypes.c_int, c_void_p]),
 }
 
 _lib = None

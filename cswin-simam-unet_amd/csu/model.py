@@ -182,6 +182,11 @@ class CSWinBlock(nn.Module):
         qkv = ops.linear(_ln(x, self.norm1, cd), self.qkv.weight, self.qkv.bias)
         att = ops.stripe_attention(qkv, self._geom, [a.get_v.weight for a in self.attns],
                                    [a.get_v.bias for a in self.attns])
+        plain = isinstance(self.drop_path, nn.Identity) and not (self.training and self.mlp.drop.p > 0)
+        if plain and ops.fused_ok(x, C, self.mlp.fc1.out_features):
+            # bf16 fused path: proj + residual in one GEMM; fc1 -> GELU -> fc2 + residual in two
+            x = ops.linear_residual(x, att, self.proj.weight, self.proj.bias)
+            return ops.mlp_residual(x, _ln(x, self.norm2, cd), self.mlp.fc1, self.mlp.fc2)
         x = x + self.drop_path(ops.linear(att, self.proj.weight, self.proj.bias))
         x = x + self.drop_path(self.mlp(_ln(x, self.norm2, cd)))
         return x

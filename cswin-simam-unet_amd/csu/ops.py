@@ -283,18 +283,53 @@ def linear_wgrad(dy2: torch.Tensor, x2: torch.Tensor):
     return out[:N * K].view(N, K), out[N * K:]
 
 
+def gemm(a2: torch.Tensor, b: torch.Tensor, b_trans: bool, out_dtype, bias=None, a_gelu=False, gelu_aux=None,
+         resid=None) -> torch.Tensor:
+    """csu_gemm: out = epi(pro(a2) @ B) with B = b^T (b_trans False, b is (N, K)) or b (b_trans True, (K, N))."""
+    M, K = a2.shape
+    N = b.shape[1] if b_trans else b.shape[0]
+    out = torch.empty(M, N, dtype=out_dtype, device=a2.device)
+    check(lib().csu_gemm(M, N, K, ptr(a2), a2.stride(0), ptr(b), b.stride(0), int(b_trans), int(a_gelu), ptr(bias),
+                         ptr(gelu_aux), ptr(resid), ptr(out), N, dtype_code(out), stream_ptr(a2.device)), "csu_gemm")
+    return out
+
+
+def linear_wgrad_gelu(dy2: torch.Tensor, h2: torch.Tensor):
+    """(dW, db) of a Linear whose input is gelu(h2), with gelu applied on the fly (bf16)."""
+    M, N = dy2.shape
+    K = h2.shape[1]
+    out = torch.empty(N * K + N, dtype=torch.float32, device=dy2.device)
+    L = lib()
+    n = L.csu_linear_wgrad_workspace(M, N, K)
+    work = torch.empty(max(n, 16), dtype=torch.uint8, device=dy2.device)
+    check(L.csu_linear_wgrad_ex(M, N, K, dtype_code(dy2), ptr(dy2), ptr(h2), 1, ptr(out), ptr(work), n,
+                                stream_ptr(dy2.device)), "csu_linear_wgrad_ex")
+    return out[:N * K].view(N, K), out[N * K:]
+
+
+def _gemm_ok(*dims):
+    return all(d % 8 == 0 for d in dims)
+
+
 class _LinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, cd, wc):
         xc = x if x.dtype == cd else x.to(cd)
         if wc is None:
             wc = weight.to(cd)
-        bc = None
-        if bias is not None:
-            bc = _ACTIVE_CACHE.get(bias, cd) if _ACTIVE_CACHE is not None else None
-            if bc is None:
-                bc = bias.to(cd)
-        y = torch.nn.functional.linear(xc, wc, bc)
+        K, N = xc.shape[-1], wc.shape[0]
+        ctx.fast = cd == torch.bfloat16 and xc.is_cuda and _gemm_ok(K, N)
+        if ctx.fast:
+            x2 = xc.reshape(-1, K).contiguous()
+            y = gemm(x2, wc, False, cd, bias=None if bias is None else bias.detach().float().contiguous())
+            y = y.view(*xc.shape[:-1], N)
+        else:
+            bc = None
+            if bias is not None:
+                bc = _ACTIVE_CACHE.get(bias, cd) if _ACTIVE_CACHE is not None else None
+                if bc is None:
+                    bc = bias.to(cd)
+            y = torch.nn.functional.linear(xc, wc, bc)
         ctx.save_for_backward(xc, wc)
         ctx.meta = (x.dtype, weight.dtype, None if bias is None else bias.dtype)
         return y
@@ -307,14 +342,19 @@ class _LinearFn(torch.autograd.Function):
         dy2 = dy.reshape(-1, N)
         if dy2.dtype != wc.dtype:
             dy2 = dy2.to(wc.dtype)
+        dy2 = dy2.contiguous()
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            dx = (dy2 @ wc).view(xc.shape)
+            if ctx.fast:
+                odt = xdt if xdt in (torch.float32, torch.bfloat16) else wc.dtype
+                dx = gemm(dy2, wc, True, odt).view(xc.shape)
+            else:
+                dx = (dy2 @ wc).view(xc.shape)
             if dx.dtype != xdt:
                 dx = dx.to(xdt)
         vec = 16 // dy2.element_size()
         if N % vec == 0 and K % vec == 0 and dy2.dtype in (torch.float32, torch.bfloat16):
-            dwf, dbf = linear_wgrad(dy2.contiguous(), xc.reshape(-1, K))
+            dwf, dbf = linear_wgrad(dy2, xc.reshape(-1, K))
             if ctx.needs_input_grad[1]:
                 dw = dwf.to(wdt)
             if bdt is not None and ctx.needs_input_grad[2]:
@@ -325,6 +365,77 @@ class _LinearFn(torch.autograd.Function):
         if bdt is not None and ctx.needs_input_grad[2]:
             db = colsum(dy2).to(bdt)
         return dx, dw, db, None, None
+
+
+class _LinearResidualFn(torch.autograd.Function):
+    """res + x @ W^T + b in one csu_gemm (fp32 out): proj + residual of CSWinBlock (cswin:366-367)."""
+
+    @staticmethod
+    def forward(ctx, res, x, weight, bias, wc):
+        res2 = res.float().contiguous().view(-1, res.shape[-1])
+        x2 = x.reshape(-1, x.shape[-1]).contiguous()
+        y = gemm(x2, wc, False, torch.float32, bias=bias.detach().float().contiguous(), resid=res2)
+        ctx.save_for_backward(x2, wc)
+        ctx.meta = (res.dtype, x.shape, weight.dtype, bias.dtype)
+        return y.view(res.shape)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, wc = ctx.saved_tensors
+        rdt, xshape, wdt, bdt = ctx.meta
+        dyb = dy.reshape(-1, dy.shape[-1]).to(torch.bfloat16).contiguous()
+        dx = gemm(dyb, wc, True, torch.bfloat16).view(xshape)
+        dw, db = linear_wgrad(dyb, x2)
+        return dy.to(rdt), dx, dw.to(wdt), db.to(bdt), None
+
+
+class _MlpResidualFn(torch.autograd.Function):
+    """res + fc2(gelu(fc1(x))) (Mlp cswin:180-196 + residual cswin:368) as two csu_gemm calls:
+    fc1 writes the pre-activation h (bf16); fc2 applies GELU to h on load and adds the residual in
+    its epilogue; backward fuses GELU' into the fc2 input-gradient epilogue."""
+
+    @staticmethod
+    def forward(ctx, res, x, w1, b1, w2, b2, w1c, w2c):
+        res2 = res.float().contiguous().view(-1, res.shape[-1])
+        x2 = x.reshape(-1, x.shape[-1]).contiguous()
+        h = gemm(x2, w1c, False, torch.bfloat16, bias=b1.detach().float().contiguous())
+        y = gemm(h, w2c, False, torch.float32, bias=b2.detach().float().contiguous(), a_gelu=True, resid=res2)
+        ctx.save_for_backward(x2, h, w1c, w2c)
+        ctx.meta = (res.dtype, x.shape, w1.dtype, b1.dtype, w2.dtype, b2.dtype)
+        return y.view(res.shape)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, h, w1c, w2c = ctx.saved_tensors
+        rdt, xshape, w1dt, b1dt, w2dt, b2dt = ctx.meta
+        dyb = dy.reshape(-1, dy.shape[-1]).to(torch.bfloat16).contiguous()
+        dh = gemm(dyb, w2c, True, torch.bfloat16, gelu_aux=h)          # (dY W2) * gelu'(h)
+        dw2, db2 = linear_wgrad_gelu(dyb, h)                            # X = gelu(h) on the fly
+        dx = gemm(dh, w1c, True, torch.bfloat16).view(xshape)
+        dw1, db1 = linear_wgrad(dh, x2)
+        return dy.to(rdt), dx, dw1.to(w1dt), db1.to(b1dt), dw2.to(w2dt), db2.to(b2dt), None, None
+
+
+def _weight_bf16(w):
+    wc = _ACTIVE_CACHE.get(w, torch.bfloat16) if _ACTIVE_CACHE is not None else None
+    return wc if wc is not None else w.detach().to(torch.bfloat16).contiguous()
+
+
+def fused_ok(x: torch.Tensor, *dims) -> bool:
+    """True when the bf16 fused-GEMM path applies (CUDA, autocast bf16, 16-B aligned dims)."""
+    return (x.is_cuda and torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16
+            and _gemm_ok(*dims))
+
+
+def linear_residual(res, x, weight, bias):
+    with torch.autocast("cuda", enabled=False):
+        return _LinearResidualFn.apply(res, x, weight, bias, _weight_bf16(weight))
+
+
+def mlp_residual(res, x, fc1: torch.nn.Linear, fc2: torch.nn.Linear):
+    with torch.autocast("cuda", enabled=False):
+        return _MlpResidualFn.apply(res, x, fc1.weight, fc1.bias, fc2.weight, fc2.bias, _weight_bf16(fc1.weight),
+                                    _weight_bf16(fc2.weight))
 
 
 class CastCache:

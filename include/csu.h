@@ -145,6 +145,22 @@ int csu_colsum(long rows, long cols, int dtype, const void* in, float* out, void
 size_t csu_linear_wgrad_workspace(long M, int N, int K);
 int csu_linear_wgrad(long M, int N, int K, int dtype, const void* dy, const void* x, float* dw_db,
                      void* workspace, size_t ws_bytes, void* stream);
+/* Same with x replaced by gelu(x) on the fly (x_gelu = 1; bf16 only): dW of fc2 from fc1's
+ * pre-activation h (Mlp cswin:191-194) without materialising gelu(h). */
+int csu_linear_wgrad_ex(long M, int N, int K, int dtype, const void* dy, const void* x, int x_gelu,
+                        float* dw_db, void* workspace, size_t ws_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Token GEMM, bf16 operands, fp32 accumulation, fused prologue/epilogue (nn.Linear of
+ * CSWinBlock/Mlp cswin:185-195, 314-368 plus the GELU, GELU-backward and residual-add passes):
+ *   out[m][n] = ((sum_k pro(a[m][k]) * B(n,k)) + bias[n]) * gelu'(gelu_aux[m][n]) + resid[m][n]
+ *   B(n,k) = b[n*ldb + k] (b_trans = 0) or b[k*ldb + n] (b_trans = 1); pro = gelu if a_gelu.
+ * bias / gelu_aux (bf16, ld = ldc) / resid (fp32, ld = ldc) may be NULL; resid needs out fp32.
+ * K, lda, ldb multiples of 8 (and N when b_trans).
+ * ------------------------------------------------------------------------------------- */
+int csu_gemm(long M, int N, int K, const void* a, int lda, const void* b, int ldb, int b_trans, int a_gelu,
+             const float* bias, const void* gelu_aux, const float* resid, void* out, int ldc, int out_dtype,
+             void* stream);
 
 #ifdef __cplusplus
 }

@@ -241,3 +241,63 @@ def test_linear_wgrad_kernel(M, N, K, dtype):
     tol = 1e-5 if dtype == torch.float32 else 1e-2
     assert float((dw.double() - ref_w).abs().max()) <= tol * max(scale_w, M ** 0.5)
     assert float((db.double() - ref_b).abs().max()) <= tol * max(float(ref_b.abs().max()), M ** 0.5)
+
+
+def _gelu(t):
+    return torch.nn.functional.gelu(t)
+
+
+@pytest.mark.parametrize("M,N,K", [(1000, 64, 64), (4099, 192, 64), (2048, 768, 256), (300, 128, 1024), (513, 256, 32)])
+@pytest.mark.parametrize("b_trans", [False, True])
+@pytest.mark.parametrize("mode", ["plain", "bias_gelu_a", "gelu_aux", "resid"])
+def test_gemm_vs_torch(M, N, K, b_trans, mode):
+    from csu import ops
+    d = dev()
+    g = torch.Generator(device=d).manual_seed(M + N + K)
+    a = torch.randn(M, K, device=d, generator=g).bfloat16()
+    w = (torch.randn(N, K, device=d, generator=g) * 0.1).bfloat16()       # nn.Linear weight (N, K)
+    b = torch.randn(K, N, device=d, generator=g).bfloat16() * 0.1 if b_trans else w
+    bias = torch.randn(N, device=d, generator=g) if mode == "bias_gelu_a" else None
+    aux = torch.randn(M, N, device=d, generator=g).bfloat16() if mode == "gelu_aux" else None
+    res = torch.randn(M, N, device=d, generator=g) if mode == "resid" else None
+    odt = torch.float32 if mode == "resid" else torch.bfloat16
+    out = ops.gemm(a, b, b_trans, odt, bias=bias, a_gelu=mode == "bias_gelu_a", gelu_aux=aux, resid=res)
+    A = a.double()
+    if mode == "bias_gelu_a":
+        A = _gelu(a.float()).bfloat16().double()
+    ref = A @ (b.double() if b_trans else b.double().t())
+    if bias is not None:
+        ref = ref + bias.double()
+    if aux is not None:
+        x = aux.double()
+        ref = ref * (0.5 * (1 + torch.erf(x / 2 ** 0.5)) + x * torch.exp(-0.5 * x * x) / (2 * torch.pi) ** 0.5)
+    if res is not None:
+        ref = ref + res.double()
+    assert out.dtype == odt
+    assert_close(out, ref, torch.bfloat16)
+
+
+def test_fused_mlp_residual_matches_unfused():
+    """mlp_residual / linear_residual (bf16 fused GEMMs) == the unfused autocast composition."""
+    from csu import ops
+    d = dev()
+    torch.manual_seed(0)
+    fc1, fc2, proj = torch.nn.Linear(128, 512).to(d), torch.nn.Linear(512, 128).to(d), torch.nn.Linear(128, 128).to(d)
+    res = torch.randn(2, 1000, 128, device=d, requires_grad=True)
+    xin = torch.randn(2, 1000, 128, device=d).bfloat16().requires_grad_(True)
+    gy = torch.randn(2, 1000, 128, device=d)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = ops.mlp_residual(ops.linear_residual(res, xin, proj.weight, proj.bias), xin, fc1, fc2)
+    y.backward(gy)
+    grads = [t.grad.clone() for t in (res, xin, fc1.weight, fc1.bias, fc2.weight, fc2.bias, proj.weight, proj.bias)]
+    for t in (res, xin, fc1.weight, fc1.bias, fc2.weight, fc2.bias, proj.weight, proj.bias):
+        t.grad = None
+    r64, x64 = res.detach().double().requires_grad_(True), xin.detach().double().requires_grad_(True)
+    ps = [p.detach().double().requires_grad_(True) for p in (fc1.weight, fc1.bias, fc2.weight, fc2.bias, proj.weight, proj.bias)]
+    F = torch.nn.functional
+    z = r64 + F.linear(x64, ps[4], ps[5])
+    ref = z + F.linear(F.gelu(F.linear(x64, ps[0], ps[1])), ps[2], ps[3])
+    ref.backward(gy.double())
+    assert_close(y, ref, torch.bfloat16)
+    for got, r in zip(grads, [r64.grad, x64.grad] + [p.grad for p in ps]):
+        assert_close(got, r, torch.bfloat16)
