@@ -1,0 +1,317 @@
+// Implicit-GEMM NHWC convolution for gfx950 (bf16 or fp32 operands, fp32 accumulation).
+//
+// Replaces the convolutions of the path: patch embed Conv2d(3,64,7,4,2) (cswin:505), Merge_Block
+// Conv2d(C,2C,3,2,1) (cswin:376), the CARAFE encoder Conv2d(C/4, 9 s^2, 3, 1, 1) (cswin:397/446)
+// and the plain-UNet DoubleConv 3x3 / ConvTranspose2d(k2, s2) stages (unet:182-211; a transposed
+// conv is this file's input-gradient operator).  Activations stay NHWC (= the (B, L, C) tokens), so
+// no im2col buffer and no layout transposes:
+//   forward : out[m = (b,oy,ox)][n]      = bias[n] + sum_{k=(ky,kx,c)} x[b, oy*s-p+ky, ox*s-p+kx, c] * Wf[n][k]
+//   dgrad   : dx [m = (b,iy,ix)][c]      = sum_{k=(ky,kx,n)} dy[b, (iy+p-ky)/s, (ix+p-kx)/s, n] * Wd[c][k]
+//             (terms whose division is inexact or out of range are zero)
+//   wgrad   : dW [n][k = (ky,kx,c)]      = sum_m dy[m][n] * x[pixel(m, ky, kx)][c],  db[n] = sum_m dy[m][n]
+// Wf = weight permuted to [n][ky][kx][c] (OHWI), Wd = [c][ky][kx][n] (IHWO); both prepared by the caller.
+// Tiles: 64 x 64 outputs per 256-thread workgroup, 4 waves of one 32x32 MFMA tile, 32-deep K slices
+// gathered per 8-channel chunk (16-B loads when the gathered channel count is a multiple of 8).
+#include "common.hpp"
+
+namespace csu {
+namespace {
+
+constexpr int NT = 256;
+constexpr int TBM = 64, TBN = 64, TBK = 32;
+
+template <typename T> struct CT;
+template <> struct CT<bf16> { static constexpr int AS = TBK; };        // swizzled 64-B rows
+template <> struct CT<float> { static constexpr int AS = TBK + 4; };   // padded 144-B rows
+
+__device__ __forceinline__ int cswz(int row, int col) {
+    return row * TBK + ((((col >> 3) ^ (row >> 2)) & 3) << 3) + (col & 7);
+}
+
+struct Geo {
+    int B, H, W, C, OH, OW, N, KH, KW, s, p;
+};
+
+// element index of the gathered operand for GEMM row m, reduction index k (or -1 when zero)
+template <int MODE>   // 0 forward (rows = output pixels, k = (ky,kx,c) over x); 1 dgrad (rows = input pixels, k = (ky,kx,n) over dy)
+__device__ __forceinline__ long gather_index(const Geo& g, long m, int k, long Mrows) {
+    if (m >= Mrows) return -1;
+    if (MODE == 0) {
+        const int KC = g.C;
+        if (k >= g.KH * g.KW * KC) return -1;
+        const int tap = k / KC, c = k - tap * KC;
+        const int ky = tap / g.KW, kx = tap - ky * g.KW;
+        const int ox = (int)(m % g.OW);
+        const long t = m / g.OW;
+        const int oy = (int)(t % g.OH), b = (int)(t / g.OH);
+        const int iy = oy * g.s - g.p + ky, ix = ox * g.s - g.p + kx;
+        if (iy < 0 || iy >= g.H || ix < 0 || ix >= g.W) return -1;
+        return (((long)b * g.H + iy) * g.W + ix) * g.C + c;
+    } else {
+        const int KN = g.N;
+        if (k >= g.KH * g.KW * KN) return -1;
+        const int tap = k / KN, n = k - tap * KN;
+        const int ky = tap / g.KW, kx = tap - ky * g.KW;
+        const int ix = (int)(m % g.W);
+        const long t = m / g.W;
+        const int iy = (int)(t % g.H), b = (int)(t / g.H);
+        const int ny = iy + g.p - ky, nx = ix + g.p - kx;
+        if (ny < 0 || nx < 0 || ny % g.s || nx % g.s) return -1;
+        const int oy = ny / g.s, ox = nx / g.s;
+        if (oy >= g.OH || ox >= g.OW) return -1;
+        return (((long)b * g.OH + oy) * g.OW + ox) * g.N + n;
+    }
+}
+
+// 8 consecutive reduction indices k..k+7 of row m -> v (zeros where out of range)
+template <int MODE, typename T, bool VEC>
+__device__ __forceinline__ void gather8(const Geo& g, const T* src, long m, int k, long Mrows, float* v) {
+    if constexpr (VEC) {
+        const long idx = gather_index<MODE>(g, m, k, Mrows);
+        if (idx >= 0) load8(src + idx, v);
+        else
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = 0.f;
+    } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const long idx = gather_index<MODE>(g, m, k + j, Mrows);
+            v[j] = idx >= 0 ? to_f(src[idx]) : 0.f;
+        }
+    }
+}
+
+// out[m][n] = bias[n] + sum_k A(m, k) * Bw[n][k];  Bw row-major (Ncols x Kdim)
+template <typename T, int MODE, bool VEC>
+__global__ __launch_bounds__(NT) void conv_gemm(Geo g, long Mrows, int Ncols, int Kdim, const T* __restrict__ src,
+                                                const T* __restrict__ Bw, const float* __restrict__ bias,
+                                                T* __restrict__ out) {
+    constexpr int AS = CT<T>::AS;
+    __shared__ __attribute__((aligned(16))) T As[TBM * AS];
+    __shared__ __attribute__((aligned(16))) T Bs[TBN * AS];
+    const long m0 = (long)blockIdx.x * TBM;
+    const int n0 = blockIdx.y * TBN;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int r = lane & 31, h = lane >> 5;
+    const int wm = (wave >> 1) * 32, wn = (wave & 1) * 32;
+    f32x16 acc = {};
+    const bool bvec = Kdim % 8 == 0;   // 16-B aligned weight rows
+    // staging: 64 rows x 4 chunks of 8 per operand = 256 chunks -> one per thread
+    const int srow = threadIdx.x >> 2, sch = threadIdx.x & 3;
+    auto put = [&](T* img, int row, int ch, const float* v) {
+        if constexpr (sizeof(T) == 2) store8(img + cswz(row, ch * 8), v);
+        else store8(img + row * AS + ch * 8, v);
+    };
+    for (int k0 = 0; k0 < Kdim; k0 += TBK) {
+        float va[8], vb[8];
+        gather8<MODE, T, VEC>(g, src, m0 + srow, k0 + sch * 8, Mrows, va);
+        {
+            const int n = n0 + srow, k = k0 + sch * 8;
+            if (bvec && n < Ncols && k + 8 <= Kdim) load8(Bw + (long)n * Kdim + k, vb);
+            else
+#pragma unroll
+                for (int j = 0; j < 8; ++j) vb[j] = (n < Ncols && k + j < Kdim) ? to_f(Bw[(long)n * Kdim + k + j]) : 0.f;
+        }
+        __syncthreads();
+        put(As, srow, sch, va);
+        put(Bs, srow, sch, vb);
+        __syncthreads();
+        if constexpr (sizeof(T) == 2) {
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                const bf16x8 a = *reinterpret_cast<const bf16x8*>(As + cswz(wm + r, 16 * s + 8 * h));
+                const bf16x8 b = *reinterpret_cast<const bf16x8*>(Bs + cswz(wn + r, 16 * s + 8 * h));
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc, 0, 0, 0);
+            }
+        } else {
+#pragma unroll
+            for (int t = 0; t < 16; ++t)
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(As[(wm + r) * AS + 16 * h + t], Bs[(wn + r) * AS + 16 * h + t],
+                                                           acc, 0, 0, 0);
+        }
+    }
+    const int n = n0 + wn + r;
+    if (n >= Ncols) return;
+    const float bv = bias ? bias[n] : 0.f;
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+        const long m = m0 + wm + crow(reg, h);
+        if (m < Mrows) out[m * Ncols + n] = from_f<T>(acc[reg] + bv);
+    }
+}
+
+// dW partial slabs: workgroup (n tile, k tile, m chunk) accumulates dY^T X_gather over its rows.
+// Operands staged transposed ([n][m], [k][m]) in LDS; db from the k-tile-0 workgroups.
+template <typename T, bool VEC>
+__global__ __launch_bounds__(NT) void conv_wgrad_kernel(Geo g, long Mrows, int Ncols, int Kdim, long rows_per_chunk,
+                                                        const T* __restrict__ x, const T* __restrict__ dy,
+                                                        float* __restrict__ part) {
+    constexpr int TM = 32;               // rows per step
+    constexpr int S = TM + (sizeof(T) == 2 ? 8 : 4);
+    __shared__ __attribute__((aligned(16))) T At[TBN * S];   // dy^T [n][m]
+    __shared__ __attribute__((aligned(16))) T Bt[TBN * S];   // X^T  [k][m]
+    const int n0 = blockIdx.x * TBN, k0 = blockIdx.y * TBN;
+    const long mb = (long)blockIdx.z * rows_per_chunk, me = min(Mrows, mb + rows_per_chunk);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int r = lane & 31, h = lane >> 5;
+    const int wn = (wave >> 1) * 32, wk = (wave & 1) * 32;
+    const bool do_bias = blockIdx.y == 0;
+    f32x16 acc = {};
+    float bsum = 0.f;
+    // staging: 32 rows x 8 chunks = 256 chunks per operand -> one per thread
+    const int srow = threadIdx.x >> 3, sch = threadIdx.x & 7;
+    for (long m0 = mb; m0 < me; m0 += TM) {
+        const long m = m0 + srow;
+        float va[8], vb[8];
+        {
+            const int n = n0 + sch * 8;
+            if (Ncols % 8 == 0 && m < me && n + 8 <= Ncols) load8(dy + m * Ncols + n, va);
+            else
+#pragma unroll
+                for (int j = 0; j < 8; ++j) va[j] = (m < me && n + j < Ncols) ? to_f(dy[m * Ncols + n + j]) : 0.f;
+        }
+        gather8<0, T, VEC>(g, x, m, k0 + sch * 8, me, vb);
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            At[(sch * 8 + j) * S + srow] = from_f<T>(va[j]);
+            Bt[(sch * 8 + j) * S + srow] = from_f<T>(vb[j]);
+        }
+        __syncthreads();
+        if (do_bias && threadIdx.x < TBN) {
+#pragma unroll
+            for (int j = 0; j < TM; ++j) bsum += to_f(At[threadIdx.x * S + j]);
+        }
+        if constexpr (sizeof(T) == 2) {
+#pragma unroll
+            for (int s = 0; s < TM / 16; ++s) {
+                const bf16x8 a = *reinterpret_cast<const bf16x8*>(At + (wn + r) * S + 16 * s + 8 * h);
+                const bf16x8 b = *reinterpret_cast<const bf16x8*>(Bt + (wk + r) * S + 16 * s + 8 * h);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc, 0, 0, 0);
+            }
+        } else {
+#pragma unroll
+            for (int t = 0; t < TM / 2; ++t)
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(At[(wn + r) * S + 2 * t + h], Bt[(wk + r) * S + 2 * t + h],
+                                                           acc, 0, 0, 0);
+        }
+    }
+    const long slab = (long)Ncols * Kdim + Ncols;
+    float* out = part + (long)blockIdx.z * slab;
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+        const int n = n0 + wn + crow(reg, h), k = k0 + wk + r;
+        if (n < Ncols && k < Kdim) out[(long)n * Kdim + k] = acc[reg];
+    }
+    if (do_bias && threadIdx.x < TBN && n0 + threadIdx.x < Ncols) out[(long)Ncols * Kdim + n0 + threadIdx.x] = bsum;
+}
+
+int check_geo(const csu_conv_geom* g) {
+    if (!g || g->B < 1 || g->H < 1 || g->W < 1 || g->C < 1 || g->OH < 1 || g->OW < 1 || g->N < 1 || g->KH < 1 ||
+        g->KW < 1 || g->stride < 1 || g->pad < 0)
+        return fail(CSU_E_ARG, "conv2d: bad geometry");
+    if (g->OH != (g->H + 2 * g->pad - g->KH) / g->stride + 1 || g->OW != (g->W + 2 * g->pad - g->KW) / g->stride + 1)
+        return fail(CSU_E_ARG, "conv2d: output size inconsistent with H, W, kernel, stride, pad");
+    return 0;
+}
+
+Geo to_geo(const csu_conv_geom* g) {
+    return Geo{g->B, g->H, g->W, g->C, g->OH, g->OW, g->N, g->KH, g->KW, g->stride, g->pad};
+}
+
+struct WPl {
+    int chunks;
+    long rpc;
+};
+WPl wplan(long M, int N, int K) {
+    const long tiles = (long)((N + TBN - 1) / TBN) * ((K + TBN - 1) / TBN);
+    long want = (1024 + tiles - 1) / tiles;
+    const long maxc = (M + 255) / 256;
+    if (want > maxc) want = maxc;
+    if (want > 256) want = 256;
+    if (want < 1) want = 1;
+    WPl p;
+    p.rpc = ((M + want - 1) / want + 31) / 32 * 32;
+    p.chunks = (int)((M + p.rpc - 1) / p.rpc);
+    return p;
+}
+
+template <typename T, int MODE>
+int launch_gemm(const Geo& g, long M, int Ncols, int Kdim, const void* src, const void* w, const float* bias, void* out,
+                bool vec, hipStream_t st) {
+    const dim3 grid((unsigned)((M + TBM - 1) / TBM), (Ncols + TBN - 1) / TBN);
+    if (vec)
+        conv_gemm<T, MODE, true><<<grid, NT, 0, st>>>(g, M, Ncols, Kdim, (const T*)src, (const T*)w, bias, (T*)out);
+    else
+        conv_gemm<T, MODE, false><<<grid, NT, 0, st>>>(g, M, Ncols, Kdim, (const T*)src, (const T*)w, bias, (T*)out);
+    return check_launch("conv2d");
+}
+
+}  // namespace
+}  // namespace csu
+
+using namespace csu;
+
+extern "C" int csu_conv2d_fwd(const csu_conv_geom* gm, int dtype, const void* x, const void* w_ohwi, const float* bias,
+                              void* out, void* stream) {
+    if (int e = check_geo(gm)) return e;
+    if (!x || !w_ohwi || !out) return fail(CSU_E_ARG, "conv2d_fwd: null buffer");
+    const Geo g = to_geo(gm);
+    const long M = (long)g.B * g.OH * g.OW;
+    const int K = g.KH * g.KW * g.C;
+    const bool vec = g.C % 8 == 0;
+    hipStream_t st = as_stream(stream);
+    if (dtype == CSU_BF16) return launch_gemm<bf16, 0>(g, M, g.N, K, x, w_ohwi, bias, out, vec, st);
+    if (dtype == CSU_F32) return launch_gemm<float, 0>(g, M, g.N, K, x, w_ohwi, bias, out, vec, st);
+    return fail(CSU_E_ARG, "conv2d_fwd: bad dtype");
+}
+
+extern "C" int csu_conv2d_dgrad(const csu_conv_geom* gm, int dtype, const void* dy, const void* w_ihwo,
+                                const float* bias, void* dx, void* stream) {
+    if (int e = check_geo(gm)) return e;
+    if (!dy || !w_ihwo || !dx) return fail(CSU_E_ARG, "conv2d_dgrad: null buffer");
+    const Geo g = to_geo(gm);
+    const long M = (long)g.B * g.H * g.W;
+    const int K = g.KH * g.KW * g.N;
+    const bool vec = g.N % 8 == 0;
+    hipStream_t st = as_stream(stream);
+    if (dtype == CSU_BF16) return launch_gemm<bf16, 1>(g, M, g.C, K, dy, w_ihwo, bias, dx, vec, st);
+    if (dtype == CSU_F32) return launch_gemm<float, 1>(g, M, g.C, K, dy, w_ihwo, bias, dx, vec, st);
+    return fail(CSU_E_ARG, "conv2d_dgrad: bad dtype");
+}
+
+extern "C" size_t csu_conv2d_wgrad_workspace(const csu_conv_geom* gm) {
+    if (check_geo(gm)) return 0;
+    const long M = (long)gm->B * gm->OH * gm->OW;
+    const int K = gm->KH * gm->KW * gm->C;
+    const WPl p = wplan(M, gm->N, K);
+    const long slab = (long)gm->N * K + gm->N;
+    return (size_t)p.chunks * slab * sizeof(float) + colsum_workspace(p.chunks, slab, CSU_F32);
+}
+
+extern "C" int csu_conv2d_wgrad(const csu_conv_geom* gm, int dtype, const void* x, const void* dy, float* dw_db,
+                                void* workspace, size_t ws_bytes, void* stream) {
+    if (int e = check_geo(gm)) return e;
+    if (!x || !dy || !dw_db) return fail(CSU_E_ARG, "conv2d_wgrad: null buffer");
+    if (!workspace || ws_bytes < csu_conv2d_wgrad_workspace(gm)) return fail(CSU_E_WORKSPACE, "conv2d_wgrad: workspace");
+    const Geo g = to_geo(gm);
+    const long M = (long)g.B * g.OH * g.OW;
+    const int K = g.KH * g.KW * g.C;
+    const WPl p = wplan(M, g.N, K);
+    const long slab = (long)g.N * K + g.N;
+    float* part = (float*)workspace;
+    const dim3 grid((g.N + TBN - 1) / TBN, (K + TBN - 1) / TBN, p.chunks);
+    const bool vec = g.C % 8 == 0;
+    hipStream_t st = as_stream(stream);
+    if (dtype == CSU_BF16) {
+        if (vec) conv_wgrad_kernel<bf16, true><<<grid, NT, 0, st>>>(g, M, g.N, K, p.rpc, (const bf16*)x, (const bf16*)dy, part);
+        else conv_wgrad_kernel<bf16, false><<<grid, NT, 0, st>>>(g, M, g.N, K, p.rpc, (const bf16*)x, (const bf16*)dy, part);
+    } else if (dtype == CSU_F32) {
+        if (vec) conv_wgrad_kernel<float, true><<<grid, NT, 0, st>>>(g, M, g.N, K, p.rpc, (const float*)x, (const float*)dy, part);
+        else conv_wgrad_kernel<float, false><<<grid, NT, 0, st>>>(g, M, g.N, K, p.rpc, (const float*)x, (const float*)dy, part);
+    } else {
+        return fail(CSU_E_ARG, "conv2d_wgrad: bad dtype");
+    }
+    if (int e = check_launch("conv2d_wgrad")) return e;
+    return colsum_launch(p.chunks, slab, CSU_F32, part, dw_db, part + (size_t)p.chunks * slab, st);
+}

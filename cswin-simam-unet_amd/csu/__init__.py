@@ -8,9 +8,10 @@ constructor arguments and state_dict keys; compute runs in hand-written gfx950 k
 from .model import (CARAFE, CARAFE4, CSWinBlock, CSWinTransformer, DropPath, LePEAttention, Merge_Block, Mlp,
                     img2windows, windows2img)
 from .simam import SimAM, simam
+from .unet import DoubleConv, Down, UNet, Up
 from .train import (bce_loss, dice_coefficient, evaluate_model, iou_score, make_optimizer, make_scheduler,
                     train_model, train_step)
 
-__all__ = ["CARAFE", "CARAFE4", "CSWinBlock", "CSWinTransformer", "DropPath", "LePEAttention", "Merge_Block", "Mlp",
+__all__ = ["UNet", "DoubleConv", "Down", "Up", "CARAFE", "CARAFE4", "CSWinBlock", "CSWinTransformer", "DropPath", "LePEAttention", "Merge_Block", "Mlp",
            "img2windows", "windows2img", "SimAM", "simam", "bce_loss", "dice_coefficient", "evaluate_model",
            "iou_score", "make_optimizer", "make_scheduler", "train_model", "train_step"]

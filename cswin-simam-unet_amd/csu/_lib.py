@@ -29,6 +29,10 @@ class StripeArgs(ctypes.Structure):
                 ("nbranch", c_int32), ("scale", c_float), ("_pad", c_int32), ("br", StripeBranch * 2)]
 
 
+class ConvGeom(ctypes.Structure):
+    _fields_ = [(n, c_int32) for n in ("B", "H", "W", "C", "OH", "OW", "N", "KH", "KW", "stride", "pad")]
+
+
 # name -> (restype, argtypes); mirrors include/csu.h
 _SIGS = {
     "csu_last_error_string": (ctypes.c_char_p, []),
@@ -64,6 +68,13 @@ _SIGS = {
     "csu_gemm": (ctypes.c_int, [ctypes.c_long, ctypes.c_int, ctypes.c_int, c_void_p, ctypes.c_int, c_void_p, ctypes.c_int,
                                 ctypes.c_int, ctypes.c_int, c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_int,
                                 ctypes.c_int, c_void_p]),
+    "csu_conv2d_fwd": (ctypes.c_int, [ctypes.POINTER(ConvGeom), ctypes.c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                                      c_void_p]),
+    "csu_conv2d_dgrad": (ctypes.c_int, [ctypes.POINTER(ConvGeom), ctypes.c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                                        c_void_p]),
+    "csu_conv2d_wgrad_workspace": (c_size_t, [ctypes.POINTER(ConvGeom)]),
+    "csu_conv2d_wgrad": (ctypes.c_int, [ctypes.POINTER(ConvGeom), ctypes.c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                                        c_size_t, c_void_p]),
 }
 
 _lib = None

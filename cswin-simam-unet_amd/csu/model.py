@@ -201,9 +201,12 @@ class Merge_Block(nn.Module):
         self.norm = norm_layer(dim_out)
 
     def forward(self, x):
-        B, new_HW, C = x.shape
-        y = self.conv(_tokens_as_nchw(x))
-        return _ln(_nchw_as_tokens(y), self.norm, torch.float32 if y.dtype == torch.bfloat16 else y.dtype)
+        B, L, C = x.shape
+        H = W = int(math.isqrt(L))
+        # implicit-GEMM 3x3/s2 conv straight on the NHWC token layout (csu_conv2d_fwd)
+        y = ops.conv2d(x.reshape(B, H, W, C), self.conv.weight, self.conv.bias, 2, 1)
+        y = y.reshape(B, -1, y.shape[-1])
+        return _ln(y, self.norm, torch.float32 if y.dtype == torch.bfloat16 else y.dtype)
 
 
 class CARAFE(nn.Module):
@@ -227,9 +230,10 @@ class CARAFE(nn.Module):
         xc = x.to(_compute_dtype(x))
         # kernel prediction (cswin:408-409): 1x1 down as a token GEMM, 3x3 encoder on the NHWC view
         d = ops.linear(xc, self.down.weight.reshape(C // 4, C), self.down.bias)
-        enc = self.encoder(_tokens_as_nchw(d))                             # (B, 9 s^2, H, W), channels_last
+        enc = ops.conv2d(d.reshape(B, H, W, C // 4), self.encoder.weight, self.encoder.bias, 1,
+                         self.kernel_size // 2)                            # (B, H, W, 9 s^2) NHWC
         # fused pixel_shuffle + softmax + unfold + matmul + pixel_shuffle (cswin:410-432)
-        r = ops.carafe_reassemble(xc, enc.permute(0, 2, 3, 1), H, W, s)   # (B, s^2 L, C)
+        r = ops.carafe_reassemble(xc, enc, H, W, s)                        # (B, s^2 L, C)
         return ops.linear(r, self.out.weight.reshape(self.out.weight.shape[0], C), self.out.bias)
 
 
@@ -326,8 +330,11 @@ class CSWinTransformer(nn.Module):
 
     def forward_features(self, x):
         conv, _, ln = self.stage1_conv_embed
-        y = conv(x.contiguous(memory_format=torch.channels_last))
-        x = _ln(_nchw_as_tokens(y), ln, torch.float32 if y.dtype == torch.bfloat16 else y.dtype)
+        B = x.shape[0]
+        # patch embed Conv2d(3, 64, 7, 4, 2) as an implicit-GEMM conv on the NHWC image
+        y = ops.conv2d(x.permute(0, 2, 3, 1), conv.weight, conv.bias, conv.stride[0], conv.padding[0])
+        y = y.reshape(B, -1, y.shape[-1])
+        x = _ln(y, ln, torch.float32 if y.dtype == torch.bfloat16 else y.dtype)
         x = self.pos_drop(x)
         for blk in self.stage1:
             x = blk(x)

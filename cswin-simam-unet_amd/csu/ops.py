@@ -307,6 +307,14 @@ def linear_wgrad_gelu(dy2: torch.Tensor, h2: torch.Tensor):
     return out[:N * K].view(N, K), out[N * K:]
 
 
+import os as _os
+
+# csu_gemm (fused bias/GELU/residual token GEMM) for the nn.Linear forward/input-gradient GEMMs.
+# Off by default: on the 512x512 step it is still slower than hipBLASLt for the input-gradient
+# and GELU-prologue shapes (profiles/README.md); CSU_FUSED_GEMM=1 turns it on.
+FUSED_GEMM = _os.environ.get("CSU_FUSED_GEMM", "0") == "1"
+
+
 def _gemm_ok(*dims):
     return all(d % 8 == 0 for d in dims)
 
@@ -318,7 +326,7 @@ class _LinearFn(torch.autograd.Function):
         if wc is None:
             wc = weight.to(cd)
         K, N = xc.shape[-1], wc.shape[0]
-        ctx.fast = cd == torch.bfloat16 and xc.is_cuda and _gemm_ok(K, N)
+        ctx.fast = FUSED_GEMM and cd == torch.bfloat16 and xc.is_cuda and _gemm_ok(K, N)
         if ctx.fast:
             x2 = xc.reshape(-1, K).contiguous()
             y = gemm(x2, wc, False, cd, bias=None if bias is None else bias.detach().float().contiguous())
@@ -423,8 +431,8 @@ def _weight_bf16(w):
 
 def fused_ok(x: torch.Tensor, *dims) -> bool:
     """True when the bf16 fused-GEMM path applies (CUDA, autocast bf16, 16-B aligned dims)."""
-    return (x.is_cuda and torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16
-            and _gemm_ok(*dims))
+    return (FUSED_GEMM and x.is_cuda and torch.is_autocast_enabled("cuda")
+            and torch.get_autocast_dtype("cuda") == torch.bfloat16 and _gemm_ok(*dims))
 
 
 def linear_residual(res, x, weight, bias):
@@ -479,3 +487,128 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] =
     wc = _ACTIVE_CACHE.get(weight, cd) if _ACTIVE_CACHE is not None else None
     with torch.autocast("cuda", enabled=False):
         return _LinearFn.apply(x, weight, bias, cd, wc)
+
+
+# ---------------------------------------------------------------------------------------------
+# Implicit-GEMM NHWC convolutions (patch embed cswin:505, Merge_Block cswin:376, CARAFE encoder
+# cswin:397/446, UNet DoubleConv / ConvTranspose2d unet:182-211)
+# ---------------------------------------------------------------------------------------------
+def _conv_geom(B, H, W, C, N, KH, KW, stride, pad):
+    g = _lib.ConvGeom()
+    g.B, g.H, g.W, g.C, g.N, g.KH, g.KW, g.stride, g.pad = B, H, W, C, N, KH, KW, stride, pad
+    g.OH, g.OW = (H + 2 * pad - KH) // stride + 1, (W + 2 * pad - KW) // stride + 1
+    return g
+
+
+def _conv_wgrad(g, x, dy, dt):
+    """fp32 (dW in [N][KH][KW][C] order, db) of the forward conv with geometry g."""
+    L = lib()
+    out = torch.empty(g.N * g.KH * g.KW * g.C + g.N, dtype=torch.float32, device=x.device)
+    n = L.csu_conv2d_wgrad_workspace(ctypes.byref(g))
+    work = torch.empty(max(n, 16), dtype=torch.uint8, device=x.device)
+    check(L.csu_conv2d_wgrad(ctypes.byref(g), dt, ptr(x), ptr(dy), ptr(out), ptr(work), n, stream_ptr(x.device)),
+          "csu_conv2d_wgrad")
+    k = g.N * g.KH * g.KW * g.C
+    return out[:k].view(g.N, g.KH, g.KW, g.C), out[k:]
+
+
+class _Conv2dFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, stride: int, pad: int, cd):
+        require_device(x, weight)
+        xc = (x if x.dtype == cd else x.to(cd)).contiguous()
+        B, H, W, C = xc.shape
+        N, Cw, KH, KW = weight.shape
+        if Cw != C:
+            raise ValueError(f"conv2d: input has {C} channels, weight expects {Cw}")
+        g = _conv_geom(B, H, W, C, N, KH, KW, stride, pad)
+        w_ohwi = weight.detach().permute(0, 2, 3, 1).to(cd).contiguous()
+        y = torch.empty(B, g.OH, g.OW, N, dtype=cd, device=x.device)
+        bf = None if bias is None else bias.detach().float().contiguous()
+        check(lib().csu_conv2d_fwd(ctypes.byref(g), dtype_code(xc), ptr(xc), ptr(w_ohwi), ptr(bf), ptr(y),
+                                   stream_ptr(x.device)), "csu_conv2d_fwd")
+        ctx.save_for_backward(xc, weight)
+        ctx.conf = (stride, pad, cd, x.dtype, bias is not None, None if bias is None else bias.dtype)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        xc, weight = ctx.saved_tensors
+        stride, pad, cd, xdt, has_b, bdt = ctx.conf
+        B, H, W, C = xc.shape
+        N, _, KH, KW = weight.shape
+        g = _conv_geom(B, H, W, C, N, KH, KW, stride, pad)
+        dy = dy.to(cd).contiguous()
+        dx = None
+        if ctx.needs_input_grad[0]:
+            w_ihwo = weight.detach().permute(1, 2, 3, 0).to(cd).contiguous()
+            dx = torch.empty(B, H, W, C, dtype=cd, device=dy.device)
+            check(lib().csu_conv2d_dgrad(ctypes.byref(g), dtype_code(dy), ptr(dy), ptr(w_ihwo), None, ptr(dx),
+                                         stream_ptr(dy.device)), "csu_conv2d_dgrad")
+            if dx.dtype != xdt:
+                dx = dx.to(xdt)
+        dw, db = _conv_wgrad(g, xc, dy, dtype_code(dy))
+        return dx, dw.permute(0, 3, 1, 2).to(weight.dtype), (db.to(bdt) if has_b else None), None, None, None
+
+
+def conv2d(x_nhwc: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor], stride: int = 1,
+           pad: int = 0) -> torch.Tensor:
+    """nn.Conv2d on a channels-last (B, H, W, C) tensor -> (B, OH, OW, N); torch weight (N, C, KH, KW)."""
+    if x_nhwc.is_cuda and torch.is_autocast_enabled("cuda"):
+        cd = torch.get_autocast_dtype("cuda")
+    else:
+        cd = torch.promote_types(x_nhwc.dtype, weight.dtype)
+    with torch.autocast("cuda", enabled=False):
+        return _Conv2dFn.apply(x_nhwc, weight, bias, stride, pad, cd)
+
+
+class _ConvTranspose2dFn(torch.autograd.Function):
+    """ConvTranspose2d(k, stride=k, pad 0) = the input-gradient operator of the matching conv."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, stride: int, cd):
+        require_device(x, weight)
+        xc = (x if x.dtype == cd else x.to(cd)).contiguous()
+        B, H, W, N = xc.shape                       # N = in channels of the transposed conv
+        Nw, C, KH, KW = weight.shape                # torch ConvTranspose2d weight (in, out, kh, kw)
+        OH, OW = (H - 1) * stride + KH, (W - 1) * stride + KW
+        g = _conv_geom(B, OH, OW, C, N, KH, KW, stride, 0)
+        w_ihwo = weight.detach().permute(1, 2, 3, 0).to(cd).contiguous()
+        y = torch.empty(B, OH, OW, C, dtype=cd, device=x.device)
+        bf = None if bias is None else bias.detach().float().contiguous()
+        check(lib().csu_conv2d_dgrad(ctypes.byref(g), dtype_code(xc), ptr(xc), ptr(w_ihwo), ptr(bf), ptr(y),
+                                     stream_ptr(x.device)), "csu_conv2d_dgrad (transposed conv)")
+        ctx.save_for_backward(xc, weight)
+        ctx.conf = (stride, cd, x.dtype, bias is not None, None if bias is None else bias.dtype)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        xc, weight = ctx.saved_tensors
+        stride, cd, xdt, has_b, bdt = ctx.conf
+        B, H, W, N = xc.shape
+        _, C, KH, KW = weight.shape
+        dy = dy.to(cd).contiguous()
+        g = _conv_geom(B, dy.shape[1], dy.shape[2], C, N, KH, KW, stride, 0)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            w_ohwi = weight.detach().permute(0, 2, 3, 1).to(cd).contiguous()
+            dx = torch.empty(B, H, W, N, dtype=cd, device=dy.device)
+            check(lib().csu_conv2d_fwd(ctypes.byref(g), dtype_code(dy), ptr(dy), ptr(w_ohwi), None, ptr(dx),
+                                       stream_ptr(dy.device)), "csu_conv2d_fwd (transposed conv backward)")
+            if dx.dtype != xdt:
+                dx = dx.to(xdt)
+        dw, _ = _conv_wgrad(g, dy, xc, dtype_code(dy))   # roles swapped: "input" = dy, "output grad" = x
+        db = colsum(dy.view(-1, C)).to(bdt) if has_b else None
+        return dx, dw.permute(0, 3, 1, 2).to(weight.dtype), db, None, None
+
+
+def conv_transpose2d(x_nhwc: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor],
+                     stride: int) -> torch.Tensor:
+    """nn.ConvTranspose2d(k, stride) with padding 0 on channels-last tensors."""
+    if x_nhwc.is_cuda and torch.is_autocast_enabled("cuda"):
+        cd = torch.get_autocast_dtype("cuda")
+    else:
+        cd = torch.promote_types(x_nhwc.dtype, weight.dtype)
+    with torch.autocast("cuda", enabled=False):
+        return _ConvTranspose2dFn.apply(x_nhwc, weight, bias, stride, cd)

@@ -162,6 +162,29 @@ int csu_gemm(long M, int N, int K, const void* a, int lda, const void* b, int ld
              const float* bias, const void* gelu_aux, const float* resid, void* out, int ldc, int out_dtype,
              void* stream);
 
+/* ---------------------------------------------------------------------------------------
+ * Implicit-GEMM NHWC convolution (patch embed cswin:505, Merge_Block.conv cswin:376, CARAFE
+ * encoder cswin:397/446, plain-UNet DoubleConv 3x3 unet:182/185 and ConvTranspose2d(k2,s2)
+ * unet:211 = the dgrad operator).  x (B,H,W,C), y (B,OH,OW,N) channels-last; weights prepared by
+ * the caller: w_ohwi = [N][KH][KW][C], w_ihwo = [C][KH][KW][N] (same dtype as activations).
+ * ------------------------------------------------------------------------------------- */
+typedef struct {
+    int32_t B, H, W, C;        /* input (of the forward conv) */
+    int32_t OH, OW, N;         /* output */
+    int32_t KH, KW, stride, pad;
+} csu_conv_geom;
+
+/* y = conv(x) + bias (bias fp32 or NULL) */
+int csu_conv2d_fwd(const csu_conv_geom* g, int dtype, const void* x, const void* w_ohwi, const float* bias,
+                   void* y, void* stream);
+/* dx = conv^T(dy) (+ bias, used when this operator is a ConvTranspose2d forward) */
+int csu_conv2d_dgrad(const csu_conv_geom* g, int dtype, const void* dy, const void* w_ihwo, const float* bias,
+                     void* dx, void* stream);
+size_t csu_conv2d_wgrad_workspace(const csu_conv_geom* g);
+/* dw_db fp32 [N*KH*KW*C + N] = dW in [N][KH][KW][C] order, then db (sum of dy) */
+int csu_conv2d_wgrad(const csu_conv_geom* g, int dtype, const void* x, const void* dy, float* dw_db,
+                     void* workspace, size_t ws_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -301,3 +301,62 @@ def test_fused_mlp_residual_matches_unfused():
     assert_close(y, ref, torch.bfloat16)
     for got, r in zip(grads, [r64.grad, x64.grad] + [p.grad for p in ps]):
         assert_close(got, r, torch.bfloat16)
+
+
+CONV_CASES = [  # (B, H, C, N, k, stride, pad)
+    (2, 32, 3, 64, 7, 4, 2),      # patch embed (cswin:505)
+    (2, 16, 64, 128, 3, 2, 1),    # Merge_Block (cswin:376)
+    (1, 8, 16, 144, 3, 1, 1),     # CARAFE4 encoder (cswin:446)
+    (2, 9, 32, 36, 3, 1, 1),      # CARAFE encoder, odd size / N % 8 != 0
+    (1, 12, 8, 24, 3, 1, 1),      # UNet DoubleConv-like
+    (2, 6, 40, 16, 1, 1, 0),      # 1x1
+]
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv2d_nhwc_vs_torch(case, dtype):
+    from csu import ops
+    d = dev()
+    B, H, C, N, k, s, p = case
+    g = torch.Generator().manual_seed(sum(case))
+    x = torch.randn(B, H, H, C, generator=g).to(dtype)
+    w = torch.randn(N, C, k, k, generator=g) * (1.0 / (C * k * k) ** 0.5)
+    b = torch.randn(N, generator=g) * 0.1
+    x64, w64, b64 = x.double().requires_grad_(True), w.double().requires_grad_(True), b.double().requires_grad_(True)
+    ref = torch.nn.functional.conv2d(x64.permute(0, 3, 1, 2), w64, b64, stride=s, padding=p).permute(0, 2, 3, 1)
+    gy = torch.randn(ref.shape, generator=g).to(dtype)
+    ref.backward(gy.double())
+    xd, wd, bd = x.to(d).requires_grad_(True), w.to(d).requires_grad_(True), b.to(d).requires_grad_(True)
+    with torch.autocast("cuda", dtype=torch.bfloat16, enabled=dtype == torch.bfloat16):
+        y = ops.conv2d(xd, wd, bd, s, p)
+    y.backward(gy.to(d).to(y.dtype))
+    assert tuple(y.shape) == tuple(ref.shape)
+    assert_close(y.float(), ref, dtype)
+    assert_close(xd.grad, x64.grad, dtype)
+    assert_close(wd.grad, w64.grad, dtype)
+    assert_close(bd.grad, b64.grad, dtype)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("B,H,Cin,Cout", [(2, 8, 64, 32), (1, 5, 128, 64)])
+def test_conv_transpose2d_nhwc_vs_torch(B, H, Cin, Cout, dtype):
+    """UNet Up.up = ConvTranspose2d(C, C/2, 2, 2) (unet:211)."""
+    from csu import ops
+    d = dev()
+    g = torch.Generator().manual_seed(B + H + Cin)
+    x = torch.randn(B, H, H, Cin, generator=g).to(dtype)
+    w = torch.randn(Cin, Cout, 2, 2, generator=g) * 0.1
+    b = torch.randn(Cout, generator=g) * 0.1
+    x64, w64, b64 = x.double().requires_grad_(True), w.double().requires_grad_(True), b.double().requires_grad_(True)
+    ref = torch.nn.functional.conv_transpose2d(x64.permute(0, 3, 1, 2), w64, b64, stride=2).permute(0, 2, 3, 1)
+    gy = torch.randn(ref.shape, generator=g).to(dtype)
+    ref.backward(gy.double())
+    xd, wd, bd = x.to(d).requires_grad_(True), w.to(d).requires_grad_(True), b.to(d).requires_grad_(True)
+    with torch.autocast("cuda", dtype=torch.bfloat16, enabled=dtype == torch.bfloat16):
+        y = ops.conv_transpose2d(xd, wd, bd, 2)
+    y.backward(gy.to(d).to(y.dtype))
+    assert_close(y.float(), ref, dtype)
+    assert_close(xd.grad, x64.grad, dtype)
+    assert_close(wd.grad, w64.grad, dtype)
+    assert_close(bd.grad, b64.grad, dtype)

@@ -143,3 +143,69 @@ def test_graphed_train_step_matches_eager():
     np.testing.assert_allclose(lb, la, rtol=1e-4, atol=1e-6)
     for (ka, pa), (kb, pb) in zip(ma.named_parameters(), mb.named_parameters()):
         torch.testing.assert_close(pb, pa, rtol=1e-4, atol=1e-5)
+
+
+def _unet(d):
+    from csu.unet import UNet
+    from oracle import unet_ref as U
+    from oracle.recipe import recipe_from_contract
+    p = recipe_from_contract(U.unet_contract(), seed=1)
+    m = UNet(3, 1).to(d)
+    m.load_state_dict(p)
+    return m, p
+
+
+def test_unet_fp32_vs_golden(golden_dir):
+    """Plain UNet (unet:177-250) with the NHWC implicit-GEMM convs vs fixture F6 (reference, fp64)."""
+    from csu.train import bce_loss
+    d = dev()
+    z = np.load(os.path.join(golden_dir, "f6_unet.npz"))
+    m, _ = _unet(d)
+    m.train()
+    x, t = torch.from_numpy(z["x"]).to(d), torch.from_numpy(z["t"]).to(d)
+    y = m(x)
+    torch.testing.assert_close(y.cpu(), torch.from_numpy(z["y_train"]), rtol=1e-4, atol=1e-4)
+    loss = bce_loss(y, t)
+    assert abs(loss.item() - float(z["loss"])) < 1e-5 * abs(float(z["loss"])) + 1e-6
+    loss.backward()
+    params = dict(m.named_parameters())
+    gn = np.array([params[k].grad.double().norm().item() for k in list(z["grad_names"])])
+    np.testing.assert_allclose(gn, z["grad_norms"], rtol=2e-3, atol=1e-6)
+    bufs = dict(m.named_buffers())
+    for k in z.files:
+        if k.startswith("rm:"):
+            torch.testing.assert_close(bufs[k[3:]].cpu(), torch.from_numpy(z[k]), rtol=1e-4, atol=1e-5)
+    m.eval()
+    with torch.no_grad():
+        ye = m(x)
+    torch.testing.assert_close(ye.cpu(), torch.from_numpy(z["y_eval"]), rtol=1e-4, atol=1e-4)
+
+
+def test_unet_bf16_vs_oracle():
+    """bf16 autocast UNet at 64x64 vs the fp32 oracle on identical weights."""
+    from csu.train import bce_loss
+    from oracle import unet_ref as U
+    d = dev()
+    m, p = _unet(d)
+    g = torch.Generator().manual_seed(5)
+    x = torch.rand(2, 3, 64, 64, generator=g)
+    t = (torch.rand(2, 1, 64, 64, generator=g) > 0.5).float()
+    for k, v in p.items():
+        if v.is_floating_point() and "running" not in k:
+            v.requires_grad_(True)
+    yr = U.unet_forward(p, x, training=True)
+    lr = O.bce_loss(yr, t)
+    lr.backward()
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = m(x.to(d))
+        loss = bce_loss(y, t.to(d))
+    loss.backward()
+    assert (y.float().cpu() - yr.detach()).abs().max().item() < 2e-2
+    assert abs(loss.item() - lr.item()) < 1e-2 * abs(lr.item())
+    gmax = max(v.grad.norm().item() for k, v in p.items() if v.grad is not None)
+    for k, q in m.named_parameters():
+        ref = p[k].grad
+        if ref.norm().item() < 1e-3 * gmax:
+            continue
+        rel = (q.grad.float().cpu() - ref).norm().item() / ref.norm().item()
+        assert rel < 5e-2, (k, rel)
