@@ -196,7 +196,7 @@ __global__ __launch_bounds__(NT) void conv_wgrad_kernel(Geo g, long Mrows, int N
                                                            acc, 0, 0, 0);
         }
     }
-    const long slab = (long)Ncols * Kdim + Ncols;
+    const long slab = ((long)Ncols * Kdim + Ncols + 3) & ~3L;   // 16-B aligned slab rows for colsum
     float* out = part + (long)blockIdx.z * slab;
 #pragma unroll
     for (int reg = 0; reg < 16; ++reg) {
@@ -285,8 +285,9 @@ extern "C" size_t csu_conv2d_wgrad_workspace(const csu_conv_geom* gm) {
     const long M = (long)gm->B * gm->OH * gm->OW;
     const int K = gm->KH * gm->KW * gm->C;
     const WPl p = wplan(M, gm->N, K);
-    const long slab = (long)gm->N * K + gm->N;
-    return (size_t)p.chunks * slab * sizeof(float) + colsum_workspace(p.chunks, slab, CSU_F32);
+    const long slab = ((long)gm->N * K + gm->N + 3) & ~3L;
+    const size_t stage = slab != (long)gm->N * K + gm->N ? slab * sizeof(float) : 0;   // padded colsum output
+    return (size_t)p.chunks * slab * sizeof(float) + stage + colsum_workspace(p.chunks, slab, CSU_F32);
 }
 
 extern "C" int csu_conv2d_wgrad(const csu_conv_geom* gm, int dtype, const void* x, const void* dy, float* dw_db,
@@ -298,7 +299,8 @@ extern "C" int csu_conv2d_wgrad(const csu_conv_geom* gm, int dtype, const void* 
     const long M = (long)g.B * g.OH * g.OW;
     const int K = g.KH * g.KW * g.C;
     const WPl p = wplan(M, g.N, K);
-    const long slab = (long)g.N * K + g.N;
+    const long used = (long)g.N * K + g.N;
+    const long slab = (used + 3) & ~3L;
     float* part = (float*)workspace;
     const dim3 grid((g.N + TBN - 1) / TBN, (K + TBN - 1) / TBN, p.chunks);
     const bool vec = g.C % 8 == 0;
@@ -313,5 +315,10 @@ extern "C" int csu_conv2d_wgrad(const csu_conv_geom* gm, int dtype, const void* 
         return fail(CSU_E_ARG, "conv2d_wgrad: bad dtype");
     }
     if (int e = check_launch("conv2d_wgrad")) return e;
-    return colsum_launch(p.chunks, slab, CSU_F32, part, dw_db, part + (size_t)p.chunks * slab, st);
+    if (slab == used) return colsum_launch(p.chunks, slab, CSU_F32, part, dw_db, part + (size_t)p.chunks * slab, st);
+    float* stage = part + (size_t)p.chunks * slab;
+    if (int e = colsum_launch(p.chunks, slab, CSU_F32, part, stage, stage + slab, st)) return e;
+    if (hipMemcpyAsync(dw_db, stage, used * sizeof(float), hipMemcpyDeviceToDevice, st) != hipSuccess)
+        return fail(CSU_E_ARG, "conv2d_wgrad: copy-out failed");
+    return 0;
 }

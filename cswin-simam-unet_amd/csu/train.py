@@ -22,7 +22,8 @@ except ImportError:  # pragma: no cover
 
 def bce_loss(prob: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
     """nn.BCELoss() (mean; log clamped at -100) computed in fp32 (cswin:936)."""
-    return F.binary_cross_entropy(prob.float(), target.float())
+    with torch.autocast(prob.device.type, enabled=False):   # BCE is autocast-unsafe; always fp32
+        return F.binary_cross_entropy(prob.float(), target.float())
 
 
 def _dice_t(pred, target, smooth=1e-6):

@@ -182,7 +182,9 @@ def test_unet_fp32_vs_golden(golden_dir):
 
 
 def test_unet_bf16_vs_oracle():
-    """bf16 autocast UNet at 64x64 vs the fp32 oracle on identical weights."""
+    """bf16 autocast UNet at 64x64 vs the fp32 oracle on identical weights.  Gradients of convs
+    followed by BatchNorm cancel heavily, so each tensor's bf16 error is bounded by
+    max(5e-2, 2x the error of the same oracle graph run by torch under bf16 autocast)."""
     from csu.train import bce_loss
     from oracle import unet_ref as U
     d = dev()
@@ -190,22 +192,32 @@ def test_unet_bf16_vs_oracle():
     g = torch.Generator().manual_seed(5)
     x = torch.rand(2, 3, 64, 64, generator=g)
     t = (torch.rand(2, 1, 64, 64, generator=g) > 0.5).float()
-    for k, v in p.items():
-        if v.is_floating_point() and "running" not in k:
-            v.requires_grad_(True)
-    yr = U.unet_forward(p, x, training=True)
+
+    def leaf(src, dv):
+        out = {}
+        for k, v in src.items():
+            v = v.detach().clone().to(dv)
+            if v.is_floating_point() and "running" not in k:
+                v.requires_grad_(True)
+            out[k] = v
+        return out
+    pr, pt = leaf(p, "cpu"), leaf(p, d)
+    yr = U.unet_forward(pr, x, training=True)
     lr = O.bce_loss(yr, t)
     lr.backward()
     with torch.autocast("cuda", dtype=torch.bfloat16):
+        yt = U.unet_forward(pt, x.to(d), training=True)
         y = m(x.to(d))
-        loss = bce_loss(y, t.to(d))
+    bce_loss(yt, t.to(d)).backward()
+    loss = bce_loss(y, t.to(d))
     loss.backward()
     assert (y.float().cpu() - yr.detach()).abs().max().item() < 2e-2
     assert abs(loss.item() - lr.item()) < 1e-2 * abs(lr.item())
-    gmax = max(v.grad.norm().item() for k, v in p.items() if v.grad is not None)
+    gmax = max(v.grad.norm().item() for v in pr.values() if v.grad is not None)
     for k, q in m.named_parameters():
-        ref = p[k].grad
+        ref = pr[k].grad
         if ref.norm().item() < 1e-3 * gmax:
             continue
         rel = (q.grad.float().cpu() - ref).norm().item() / ref.norm().item()
-        assert rel < 5e-2, (k, rel)
+        rel_torch = (pt[k].grad.float().cpu() - ref).norm().item() / ref.norm().item()
+        assert rel < max(5e-2, 2 * rel_torch), (k, rel, rel_torch)
