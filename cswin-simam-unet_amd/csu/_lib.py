@@ -54,6 +54,9 @@ _SIGS = {
                                      c_void_p, c_void_p, c_size_t, c_void_p]),
     "csu_carafe_fwd": (ctypes.c_int, [ctypes.c_int] * 6 + [c_void_p] * 5),
     "csu_carafe_bwd": (ctypes.c_int, [ctypes.c_int] * 6 + [c_void_p] * 6),
+    "csu_carafe_head_fwd": (ctypes.c_int, [ctypes.c_int] * 6 + [c_void_p] * 7),
+    "csu_carafe_head_bwd_workspace": (c_size_t, [ctypes.c_int] * 5),
+    "csu_carafe_head_bwd": (ctypes.c_int, [ctypes.c_int] * 6 + [c_void_p] * 11 + [c_size_t, c_void_p]),
     "csu_head_fwd": (ctypes.c_int, [ctypes.c_long, ctypes.c_int, ctypes.c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
     "csu_head_bwd_workspace": (c_size_t, [ctypes.c_long, ctypes.c_int]),
     "csu_head_bwd": (ctypes.c_int, [ctypes.c_long, ctypes.c_int, ctypes.c_int] + [c_void_p] * 7 + [c_size_t, c_void_p]),

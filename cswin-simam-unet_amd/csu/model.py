@@ -227,14 +227,38 @@ class CARAFE(nn.Module):
         s = self.up_factor
         if self.kernel_size != 3:
             raise NotImplementedError("the fused CARAFE kernel is specialised for kernel_size=3 (the reference's)")
-        xc = x.to(_compute_dtype(x))
-        # kernel prediction (cswin:408-409): 1x1 down as a token GEMM, 3x3 encoder on the NHWC view
-        d = ops.linear(xc, self.down.weight.reshape(C // 4, C), self.down.bias)
-        enc = ops.conv2d(d.reshape(B, H, W, C // 4), self.encoder.weight, self.encoder.bias, 1,
-                         self.kernel_size // 2)                            # (B, H, W, 9 s^2) NHWC
+        xc, enc = self.kernels(x)
         # fused pixel_shuffle + softmax + unfold + matmul + pixel_shuffle (cswin:410-432)
         r = ops.carafe_reassemble(xc, enc, H, W, s)                        # (B, s^2 L, C)
         return ops.linear(r, self.out.weight.reshape(self.out.weight.shape[0], C), self.out.bias)
+
+    def kernels(self, x):
+        """Kernel prediction (cswin:408-409): 1x1 down as a token GEMM, 3x3 encoder conv on the
+        NHWC view.  Returns (x in the compute dtype, enc (B, H, W, 9 s^2) NHWC logits)."""
+        B, L, C = x.shape
+        H = W = int(math.isqrt(L))
+        if self.kernel_size != 3:
+            raise NotImplementedError("the fused CARAFE kernel is specialised for kernel_size=3 (the reference's)")
+        xc = x.to(_compute_dtype(x))
+        d = ops.linear(xc, self.down.weight.reshape(C // 4, C), self.down.bias)
+        enc = ops.conv2d(d.reshape(B, H, W, C // 4), self.encoder.weight, self.encoder.bias, 1, self.kernel_size // 2)
+        return xc, enc
+
+
+def carafe_sigmoid_head(up: CARAFE, w_output: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
+    """sigmoid(output(up(x))) for the 1-class bias-free `output` conv (cswin:674-688) in one pass.
+
+    CARAFE reassembly -> `out` 1x1 conv -> `output` 1x1 conv is linear up to the sigmoid, so it
+    collapses to u = W_out^T w_output and c = w_output . b_out (tiny fp32 autograd ops here) and the
+    fused kernel ops.carafe_head.  Returns prob (B, 1, sH, sW) fp32."""
+    B, L, C = x.shape
+    H = W = int(math.isqrt(L))
+    xc, enc = up.kernels(x)
+    w_out = up.out.weight.reshape(up.out.weight.shape[0], C).float()
+    w_h = w_output.reshape(-1).float()
+    u = w_out.t() @ w_h
+    cb = (w_h * up.out.bias.float()).sum()
+    return ops.carafe_head(xc, enc, u, cb, H, W, up.up_factor)
 
 
 class CARAFE4(CARAFE):
@@ -401,9 +425,7 @@ class CSWinTransformer(nn.Module):
         if self.num_classes == 1:
             B, L, C = x.shape
             H = W = int(math.isqrt(L))
-            y = self.upsample1(x)                                         # (B, 16 L, 64)
-            prob = ops.sigmoid_head(y, self.output.weight)                # fused 1x1 conv + sigmoid
-            return prob.reshape(B, 1, 4 * H, 4 * W)
+            return carafe_sigmoid_head(self.upsample1, self.output.weight, x)
         return torch.sigmoid(self.up_x4(x).float())
 
 

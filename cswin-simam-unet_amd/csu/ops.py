@@ -238,6 +238,50 @@ def sigmoid_head(x: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
     return _HeadFn.apply(x, weight)
 
 
+class _CarafeHeadFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, enc, u, cb, H, W, s):
+        require_device(x, enc, u, cb)
+        x, enc = x.contiguous(), enc.to(x.dtype).contiguous()
+        uf, cf = u.detach().float().contiguous(), cb.detach().float().reshape(1).contiguous()
+        B, C = x.shape[0], x.shape[-1]
+        if x.numel() != B * H * W * C or enc.numel() != B * H * W * 9 * s * s:
+            raise ValueError("carafe_head: x must be (B, H*W, C) and enc (B, H, W, 9 s^2)")
+        z = torch.empty(B * H * W, dtype=torch.float32, device=x.device)
+        prob = torch.empty(B, 1, s * H, s * W, dtype=torch.float32, device=x.device)
+        check(lib().csu_carafe_head_fwd(B, H, W, C, s, dtype_code(x), ptr(x), ptr(enc), ptr(uf), ptr(cf), ptr(z),
+                                         ptr(prob), stream_ptr(x.device)), "csu_carafe_head_fwd")
+        ctx.save_for_backward(x, enc, z, uf, prob)
+        ctx.geo = (B, H, W, C, s)
+        ctx.dtypes = (u.dtype, cb.dtype, cb.shape)
+        return prob
+
+    @staticmethod
+    def backward(ctx, dprob):
+        x, enc, z, uf, prob = ctx.saved_tensors
+        B, H, W, C, s = ctx.geo
+        dprob = dprob.float().contiguous()
+        dx, denc = torch.empty_like(x), torch.empty_like(enc)
+        du = torch.empty(C, dtype=torch.float32, device=x.device)
+        dcb = torch.empty(1, dtype=torch.float32, device=x.device)
+        L = lib()
+        n = L.csu_carafe_head_bwd_workspace(B, H, W, C, s)
+        work = torch.empty(max(n, 16), dtype=torch.uint8, device=x.device)
+        check(L.csu_carafe_head_bwd(B, H, W, C, s, dtype_code(x), ptr(x), ptr(enc), ptr(z), ptr(uf), ptr(prob),
+                                    ptr(dprob), ptr(dx), ptr(denc), ptr(du), ptr(dcb), ptr(work), n,
+                                    stream_ptr(x.device)), "csu_carafe_head_bwd")
+        udt, cdt, cshape = ctx.dtypes
+        return dx, denc, du.to(udt), dcb.to(cdt).reshape(cshape), None, None, None
+
+
+def carafe_head(x: torch.Tensor, enc: torch.Tensor, u: torch.Tensor, cb: torch.Tensor, H: int, W: int,
+                s: int) -> torch.Tensor:
+    """sigmoid(output(CARAFE(x).out)) for a 1-class bias-free head, fused (csu_carafe_head_*):
+    x (B, H*W, C) tokens, enc (B, H, W, 9 s^2) encoder logits, u = W_out^T w_output (C),
+    cb = w_output . b_out (scalar tensor) -> prob (B, 1, sH, sW) fp32."""
+    return _CarafeHeadFn.apply(x, enc, u, cb, H, W, s)
+
+
 # ---------------------------------------------------------------------------------------------
 # Token Linear (nn.Linear on (B, L, C) tokens) with a split-K weight gradient.
 # The weight gradient dW = dY^T X reduces over all B*L tokens (K up to 4M); a plain GEMM keeps

@@ -128,6 +128,23 @@ int csu_head_bwd(long P, int C, int dtype, const void* x, const float* w, const 
                  const float* dprob, void* dx, float* dw, void* workspace, size_t ws_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------------------
+ * Fused CARAFE4 + 1-class output head (CSWinTransformer.up_x4 + sigmoid, cswin:674-688):
+ * everything after upsample1's encoder conv is linear up to the sigmoid, so with
+ * u = W_out^T w_output (C fp32) and cb = w_output . b_out (1 fp32, device), computed by the caller,
+ *   prob[b, s y + i, s x + j] = sigmoid(sum_t m[t] z[nbr_t(y, x)] + cb),  z[q] = u . x[q]
+ * (m = softmax over the 9 taps of enc[b, y, x, t*s*s + i*s + j]; cswin:456-481).  x (B, H*W, C)
+ * tokens, enc NHWC (B, H, W, 9 s^2), z fp32 (B*H*W) written for bwd, prob fp32 (B, sH, sW).
+ * s in {2, 4}; C = 8 * 2^k <= 512.
+ * ------------------------------------------------------------------------------------- */
+int csu_carafe_head_fwd(int B, int H, int W, int C, int s, int dtype, const void* x, const void* enc,
+                        const float* u, const float* cb, float* z, float* prob, void* stream);
+size_t csu_carafe_head_bwd_workspace(int B, int H, int W, int C, int s);
+/* dprob -> dx (B, H*W, C), denc (B, H, W, 9 s^2), du (C) and dcb (1), fp32 reductions deterministic. */
+int csu_carafe_head_bwd(int B, int H, int W, int C, int s, int dtype, const void* x, const void* enc,
+                        const float* z, const float* u, const float* prob, const float* dprob, void* dx,
+                        void* denc, float* du, float* dcb, void* workspace, size_t ws_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------------------
  * Deterministic column sum out[c] = sum_r in[r][c], fp32 accumulation (rows x cols row-major,
  * dtype in; out fp32).  The bias gradient of every nn.Linear (cswin:185/187/314/323/568/581/592)
  * is the column sum of dY over the B*L tokens; also reduces split-K weight-gradient slabs.

@@ -178,6 +178,38 @@ def test_carafe_module_vs_oracle(B, H, C, s, dtype):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("B,H,C,s", [(2, 8, 64, 4), (1, 5, 32, 4), (2, 6, 64, 2)])
+def test_carafe_sigmoid_head_vs_oracle(B, H, C, s, dtype):
+    """Fused CARAFE(4) + `out` conv + 1-class `output` conv + sigmoid (csu_carafe_head_*) vs the
+    oracle's unfused chain in fp64 (cswin:450-486, 674-688)."""
+    from csu.model import CARAFE, carafe_sigmoid_head
+    d = dev()
+    torch.manual_seed(B * 100 + H * 10 + s + C)
+    m = CARAFE(C, C, up_factor=s)
+    with torch.no_grad():
+        m.out.bias.normal_(0, 0.3)
+    wo = torch.randn(1, C, 1, 1) * 0.3
+    x = torch.randn(B, H * H, C)
+    dp = torch.randn(B, 1, s * H, s * H)
+    p64 = {"." + k: v.double().requires_grad_(True) for k, v in m.state_dict().items()}
+    x64, wo64 = x.double().requires_grad_(True), wo.double().requires_grad_(True)
+    y = O.carafe(x64, p64, "", s)                                           # (B, s^2 L, C)
+    ref = torch.sigmoid(y @ wo64.view(C)).view(B, 1, s * H, s * H)
+    ref.backward(dp.double())
+    md, wod = m.to(d), wo.to(d).requires_grad_(True)
+    xd = x.to(d).requires_grad_(True)
+    with torch.autocast("cuda", dtype=torch.bfloat16, enabled=dtype == torch.bfloat16):
+        p = carafe_sigmoid_head(md, wod, xd)
+    p.backward(dp.to(d))
+    assert p.dtype == torch.float32 and p.shape == ref.shape
+    assert_close(p, ref, dtype)
+    assert_close(xd.grad, x64.grad, dtype)
+    assert_close(wod.grad, wo64.grad, dtype)
+    for k, q in md.named_parameters():
+        assert_close(q.grad, p64["." + k].grad, dtype)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_sigmoid_head_vs_torch(dtype):
     from csu import ops
     d = dev()
