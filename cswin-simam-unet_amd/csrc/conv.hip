@@ -206,6 +206,201 @@ __global__ __launch_bounds__(NT) void conv_wgrad_kernel(Geo g, long Mrows, int N
     if (do_bias && threadIdx.x < TBN && n0 + threadIdx.x < Ncols) out[(long)Ncols * Kdim + n0 + threadIdx.x] = bsum;
 }
 
+// ---- bf16 implicit GEMM, v2: 128/256 x BN tiles, 64-deep K slices, double-buffered LDS ----------
+// One problem description covers the forward conv and each stride phase of the input gradient:
+//   row (b, ry, rx) gathers source pixel (ry*ay + by + ty*sty, rx*ax + bx + tx*stx) for tap (ty, tx),
+//   weight column ((ty*wty + w0y)*KWf + tx*wtx + w0x)*Cs + c, output pixel (ry*oya + oyb, rx*oxa + oxb).
+// Input gradient of a stride-s conv is split into s*s phases (input pixel parity), each a dense conv
+// over only the taps that hit it (3x3/s2: 1, 2 or 4 taps instead of 9 mostly-zero ones).
+struct IG {
+    int Hs, Ws, Cs;
+    int RH, RW;
+    int ay, by, ax, bx;
+    int nty, ntx, sty, stx;
+    int ldw, KWf, wty, w0y, wtx, w0x;
+    int OHo, OWo, oya, oyb, oxa, oxb;
+    int B, Ncols, Kd;
+    long M;
+};
+
+__device__ __forceinline__ int swz128(int row, int chunk) { return row * 64 + ((chunk ^ (row & 7)) << 3); }
+
+template <int BN, int VW>
+__global__ __launch_bounds__(NT) void igemm_bf16(IG g, const bf16* __restrict__ src, const bf16* __restrict__ Bw,
+                                                 const float* __restrict__ bias, bf16* __restrict__ out) {
+    constexpr int WN = BN / 32, WM = 4 / WN, BM = WM * 64, BK = 64;
+    constexpr int ACH = BM * 8 / NT, BCH = BN * 8 / NT, NP = 8 / VW;
+    __shared__ __attribute__((aligned(16))) bf16 As[2][BM * BK];
+    __shared__ __attribute__((aligned(16))) bf16 Bs[2][BN * BK];
+    __shared__ long ooff[BM];
+    const long m0 = (long)blockIdx.x * BM;
+    const int n0 = blockIdx.y * BN;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int r = lane & 31, h = lane >> 5;
+    const int wn = (wave % WN) * 32, wm = (wave / WN) * 64;
+    const int ch = threadIdx.x & 7, rbase = threadIdx.x >> 3;
+
+    // per staging row: image base pixel row and source base coordinates
+    int rb[ACH], ryb[ACH], rxb[ACH];
+#pragma unroll
+    for (int i = 0; i < ACH; ++i) {
+        const long m = m0 + rbase + 32 * i;
+        if (m < g.M) {
+            const int rx = (int)(m % g.RW);
+            const long t = m / g.RW;
+            const int ry = (int)(t % g.RH);
+            rb[i] = (int)(t / g.RH) * g.Hs;
+            ryb[i] = ry * g.ay + g.by;
+            rxb[i] = rx * g.ax + g.bx;
+        } else {
+            rb[i] = 0;
+            ryb[i] = -(1 << 29);   // never in range
+            rxb[i] = 0;
+        }
+    }
+    bf16x8 ra[ACH], rbw[BCH];
+    auto load = [&](int k0) {
+#pragma unroll
+        for (int pc = 0; pc < NP; ++pc) {
+            const int k = k0 + 8 * ch + VW * pc;
+            const bool kin = k < g.Kd;
+            const int t = kin ? k / g.Cs : 0, c = k - t * g.Cs;
+            const int ty = t / g.ntx, tx = t - ty * g.ntx;
+            const int oy = ty * g.sty, ox = tx * g.stx;
+            const int wcol = ((ty * g.wty + g.w0y) * g.KWf + tx * g.wtx + g.w0x) * g.Cs + c;
+#pragma unroll
+            for (int i = 0; i < ACH; ++i) {
+                const int y = ryb[i] + oy, x = rxb[i] + ox;
+                const bool ok = kin && y >= 0 && y < g.Hs && x >= 0 && x < g.Ws;
+                const bf16* p = src + (((long)rb[i] + y) * g.Ws + x) * g.Cs + c;
+                if constexpr (VW == 8) {
+                    ra[i] = ok ? *reinterpret_cast<const bf16x8*>(p) : bf16x8{};
+                } else {
+                    const bf16x4 v = ok ? *reinterpret_cast<const bf16x4*>(p) : bf16x4{};
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) ra[i][4 * pc + j] = v[j];
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < BCH; ++j) {
+                const int n = n0 + rbase + 32 * j;
+                const bool ok = kin && n < g.Ncols;
+                const bf16* p = Bw + (long)n * g.ldw + wcol;
+                if constexpr (VW == 8) {
+                    rbw[j] = ok ? *reinterpret_cast<const bf16x8*>(p) : bf16x8{};
+                } else {
+                    const bf16x4 v = ok ? *reinterpret_cast<const bf16x4*>(p) : bf16x4{};
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) rbw[j][4 * pc + e] = v[e];
+                }
+            }
+        }
+    };
+    auto store = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < ACH; ++i) *reinterpret_cast<bf16x8*>(&As[buf][swz128(rbase + 32 * i, ch)]) = ra[i];
+#pragma unroll
+        for (int j = 0; j < BCH; ++j) *reinterpret_cast<bf16x8*>(&Bs[buf][swz128(rbase + 32 * j, ch)]) = rbw[j];
+    };
+
+    f32x16 acc[2] = {f32x16{}, f32x16{}};
+    if (g.Kd > 0) {
+        load(0);
+        store(0);
+    }
+    __syncthreads();
+    int buf = 0;
+    for (int k0 = 0; k0 < g.Kd; k0 += BK) {
+        const bool more = k0 + BK < g.Kd;
+        if (more) load(k0 + BK);
+#pragma unroll
+        for (int s = 0; s < BK / 16; ++s) {
+            const bf16x8 b = *reinterpret_cast<const bf16x8*>(&Bs[buf][swz128(wn + r, 2 * s + h)]);
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const bf16x8 a = *reinterpret_cast<const bf16x8*>(&As[buf][swz128(wm + 32 * i + r, 2 * s + h)]);
+                acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc[i], 0, 0, 0);
+            }
+        }
+        if (more) store(buf ^ 1);
+        __syncthreads();
+        buf ^= 1;
+    }
+    // output pixel offsets of the BM rows
+    for (int i = threadIdx.x; i < BM; i += NT) {
+        const long m = m0 + i;
+        long o = -1;
+        if (m < g.M) {
+            const int rx = (int)(m % g.RW);
+            const long t = m / g.RW;
+            const int ry = (int)(t % g.RH), b = (int)(t / g.RH);
+            o = (((long)b * g.OHo + ry * g.oya + g.oyb) * g.OWo + rx * g.oxa + g.oxb) * g.Ncols;
+        }
+        ooff[i] = o;
+    }
+    __syncthreads();
+    const int n = n0 + wn + r;
+    if (n >= g.Ncols) return;
+    const float bv = bias ? bias[n] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) {
+            const long o = ooff[wm + 32 * i + crow(reg, h)];
+            if (o >= 0) out[o + n] = (bf16)(acc[i][reg] + bv);
+        }
+}
+
+int launch_ig(const IG& g, const void* src, const void* w, const float* bias, void* out, hipStream_t st) {
+    const int vw = g.Cs % 8 == 0 ? 8 : 4;
+    const bool narrow = g.Ncols <= 32;
+    const int BM = narrow ? 256 : 128, BN = narrow ? 32 : 64;
+    const dim3 grid((unsigned)((g.M + BM - 1) / BM), (g.Ncols + BN - 1) / BN);
+    const bf16* s = (const bf16*)src;
+    const bf16* wb = (const bf16*)w;
+    bf16* o = (bf16*)out;
+    if (narrow) {
+        if (vw == 8) igemm_bf16<32, 8><<<grid, NT, 0, st>>>(g, s, wb, bias, o);
+        else igemm_bf16<32, 4><<<grid, NT, 0, st>>>(g, s, wb, bias, o);
+    } else {
+        if (vw == 8) igemm_bf16<64, 8><<<grid, NT, 0, st>>>(g, s, wb, bias, o);
+        else igemm_bf16<64, 4><<<grid, NT, 0, st>>>(g, s, wb, bias, o);
+    }
+    return check_launch("conv2d (igemm)");
+}
+
+IG ig_forward(const csu_conv_geom& c) {
+    IG g{};
+    g.Hs = c.H; g.Ws = c.W; g.Cs = c.C;
+    g.RH = c.OH; g.RW = c.OW;
+    g.ay = c.stride; g.by = -c.pad; g.ax = c.stride; g.bx = -c.pad;
+    g.nty = c.KH; g.ntx = c.KW; g.sty = 1; g.stx = 1;
+    g.ldw = c.KH * c.KW * c.C; g.KWf = c.KW; g.wty = 1; g.w0y = 0; g.wtx = 1; g.w0x = 0;
+    g.OHo = c.OH; g.OWo = c.OW; g.oya = 1; g.oyb = 0; g.oxa = 1; g.oxb = 0;
+    g.B = c.B; g.Ncols = c.N; g.Kd = c.KH * c.KW * c.C;
+    g.M = (long)c.B * c.OH * c.OW;
+    return g;
+}
+
+// phase (ry_, rx_) of the input gradient: input pixels with (iy + pad) % s == ry_, taps ky = ry_ + s*ty
+IG ig_dgrad_phase(const csu_conv_geom& c, int ry_, int rx_) {
+    const int s = c.stride, p = c.pad;
+    const int iy0 = ((ry_ - p) % s + s) % s, ix0 = ((rx_ - p) % s + s) % s;
+    IG g{};
+    g.Hs = c.OH; g.Ws = c.OW; g.Cs = c.N;
+    g.RH = iy0 < c.H ? (c.H - iy0 + s - 1) / s : 0;
+    g.RW = ix0 < c.W ? (c.W - ix0 + s - 1) / s : 0;
+    g.ay = 1; g.by = (iy0 + p - ry_) / s; g.ax = 1; g.bx = (ix0 + p - rx_) / s;
+    g.nty = ry_ < c.KH ? (c.KH - ry_ + s - 1) / s : 0;
+    g.ntx = rx_ < c.KW ? (c.KW - rx_ + s - 1) / s : 0;
+    g.sty = -1; g.stx = -1;
+    g.ldw = c.KH * c.KW * c.N; g.KWf = c.KW; g.wty = s; g.w0y = ry_; g.wtx = s; g.w0x = rx_;
+    g.OHo = c.H; g.OWo = c.W; g.oya = s; g.oyb = iy0; g.oxa = s; g.oxb = ix0;
+    g.B = c.B; g.Ncols = c.C; g.Kd = g.nty * g.ntx * c.N;
+    g.M = (long)c.B * g.RH * g.RW;
+    return g;
+}
+
 int check_geo(const csu_conv_geom* g) {
     if (!g || g->B < 1 || g->H < 1 || g->W < 1 || g->C < 1 || g->OH < 1 || g->OW < 1 || g->N < 1 || g->KH < 1 ||
         g->KW < 1 || g->stride < 1 || g->pad < 0)
@@ -261,6 +456,7 @@ extern "C" int csu_conv2d_fwd(const csu_conv_geom* gm, int dtype, const void* x,
     const int K = g.KH * g.KW * g.C;
     const bool vec = g.C % 8 == 0;
     hipStream_t st = as_stream(stream);
+    if (dtype == CSU_BF16 && g.C % 4 == 0) return launch_ig(ig_forward(*gm), x, w_ohwi, bias, out, st);
     if (dtype == CSU_BF16) return launch_gemm<bf16, 0>(g, M, g.N, K, x, w_ohwi, bias, out, vec, st);
     if (dtype == CSU_F32) return launch_gemm<float, 0>(g, M, g.N, K, x, w_ohwi, bias, out, vec, st);
     return fail(CSU_E_ARG, "conv2d_fwd: bad dtype");
@@ -275,6 +471,15 @@ extern "C" int csu_conv2d_dgrad(const csu_conv_geom* gm, int dtype, const void* 
     const int K = g.KH * g.KW * g.N;
     const bool vec = g.N % 8 == 0;
     hipStream_t st = as_stream(stream);
+    if (dtype == CSU_BF16 && g.N % 4 == 0) {
+        for (int py = 0; py < g.s; ++py)
+            for (int px = 0; px < g.s; ++px) {
+                const IG ig = ig_dgrad_phase(*gm, py, px);
+                if (ig.M == 0) continue;
+                if (int e = launch_ig(ig, dy, w_ihwo, bias, dx, st)) return e;
+            }
+        return 0;
+    }
     if (dtype == CSU_BF16) return launch_gemm<bf16, 1>(g, M, g.C, K, dy, w_ihwo, bias, dx, vec, st);
     if (dtype == CSU_F32) return launch_gemm<float, 1>(g, M, g.C, K, dy, w_ihwo, bias, dx, vec, st);
     return fail(CSU_E_ARG, "conv2d_dgrad: bad dtype");

@@ -342,6 +342,9 @@ CONV_CASES = [  # (B, H, C, N, k, stride, pad)
     (2, 9, 32, 36, 3, 1, 1),      # CARAFE encoder, odd size / N % 8 != 0
     (1, 12, 8, 24, 3, 1, 1),      # UNet DoubleConv-like
     (2, 6, 40, 16, 1, 1, 0),      # 1x1
+    (2, 11, 64, 128, 3, 2, 1),    # stride 2 on an odd size (phase split of the input gradient)
+    (1, 70, 64, 72, 3, 1, 1),     # several 128/256-row tiles, N tail
+    (1, 13, 12, 20, 5, 3, 2),     # stride 3, 5x5: phases with 1-2 taps per axis
 ]
 
 
