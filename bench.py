@@ -5,9 +5,12 @@ N > 1 is launched by the driver with torch.distributed.run (one process per GPU,
 One step = forward + BCE + backward (+ DDP gradient all-reduce) + fused AdamW on a batch of
 synthetic 512x512 images already resident in HBM.  Prints ONE JSON line (rank 0).
 
-roofline: the stripe-attention forward kernel (csu_stripe_attn_fwd), timed live with HIP events
-around every launch of the timed region on the launch stream; achieved = algorithmic bytes
-(qkv read once + output written once + log-sum-exp) / measured time.  cpu_baseline: the CPU
+roofline: the stripe-attention forward kernel (csu_stripe_attn_fwd -> stripe_fwd_w), timed live
+with HIP events on the launch stream around 8 back-to-back repeats of every launch of 3 eager
+steps of the same workload (HIP events cannot be recorded inside the graph replays of the timed
+region: hipErrorInvalidHandle); achieved = algorithmic bytes (qkv read once + output written once
++ log-sum-exp) / measured time.  traffic = HBM bytes per launch from the committed rocprofv3 PMC
+summary (profiles/pmc_stripe_fwd.json, FETCH_SIZE x2 + WRITE_SIZE, tools/pmc_traffic.py).  cpu_baseline: the CPU
 oracle (a restatement of the reference) timed on this host for a bounded sample.
 """
 from __future__ import annotations
@@ -147,11 +150,11 @@ def main():
         for i in range(args.warmup):
             eager_step(i)
     # roofline leg: time every stripe-attention forward launch of a few eager steps of the same
-    # workload with HIP events on the launch stream (graph replays cannot host-record events)
+    # workload with HIP events on the launch stream (events cannot be recorded in graph replays)
     prof = None
     if not args.no_roofline:
         prof = []
-        ops.set_kernel_timer(prof)
+        ops.set_kernel_timer(prof, repeat=8)
         for i in range(min(args.steps, 3)):
             eager_step(i)
         ops.set_kernel_timer(None)
@@ -176,12 +179,12 @@ def main():
     roof = None
     if prof:
         torch.cuda.synchronize()
-        ms = sum(s.elapsed_time(e) for s, e, _, _ in prof)
-        nbytes = sum(b for _, _, b, _ in prof)
-        flops = sum(f for _, _, _, f in prof)
-        n = len(prof)
+        ms = sum(s.elapsed_time(e) for s, e, _, _, _ in prof)
+        nbytes = sum(p[2] for p in prof)
+        flops = sum(p[3] for p in prof)
+        n = sum(p[4] for p in prof)
         achieved = nbytes / n / (ms / n * 1e-3) / 1e9
-        roof = {"kernel": "csu_stripe_attn_fwd (stripe_fwd<bf16>)", "bound": "hbm", "achieved": round(achieved, 1),
+        roof = {"kernel": "csu_stripe_attn_fwd (stripe_fwd_w, bf16)", "bound": "hbm", "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": _pmc_traffic(), "launches": n, "avg_us": round(ms / n * 1e3, 2),
                 "bytes_per_launch": int(nbytes / n), "flops_per_launch": int(flops / n),

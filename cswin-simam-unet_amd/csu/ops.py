@@ -12,13 +12,18 @@ from ._lib import check, dtype_code, lib, ptr, require_device, stream_ptr
 
 
 _KERNEL_TIMER = None
+_KERNEL_TIMER_REPEAT = 1
 
 
-def set_kernel_timer(sink):
-    """Record (start_event, end_event, algorithmic_bytes, flops) of every csu_stripe_attn_fwd
-    launch into the list ``sink`` (None disables).  Events are recorded on the launch stream."""
-    global _KERNEL_TIMER
+def set_kernel_timer(sink, repeat: int = 1):
+    """Time csu_stripe_attn_fwd: after each real launch, ``repeat`` identical back-to-back launches
+    (same inputs, same outputs) are bracketed by two HIP events on the launch stream, and
+    (start_event, end_event, algorithmic_bytes, flops, launches) is appended to the list ``sink``
+    (None disables).  Back-to-back launches keep the per-event overhead (a few us on a ~30 us
+    kernel) out of the per-launch duration, so it matches the rocprofv3 kernel-trace average."""
+    global _KERNEL_TIMER, _KERNEL_TIMER_REPEAT
     _KERNEL_TIMER = sink
+    _KERNEL_TIMER_REPEAT = max(1, int(repeat))
 
 
 def _stripe_fwd_work(geom, B, esize):
@@ -78,15 +83,19 @@ class _StripeAttnFn(torch.autograd.Function):
         out = torch.empty(B, L, geom.C, dtype=qkv.dtype, device=qkv.device)
         lse = torch.empty(nb, B, geom.heads, L, dtype=torch.float32, device=qkv.device)
         a = geom.args(B, ws, bs)
+        launch = lambda: check(lib().csu_stripe_attn_fwd(ctypes.byref(a), dtype_code(qkv), ptr(qkv), ptr(out),
+                                                         ptr(lse), stream_ptr(qkv.device)), "csu_stripe_attn_fwd")
+        launch()
         timer = _KERNEL_TIMER
         if timer is not None:
+            rep = _KERNEL_TIMER_REPEAT
             ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            ev0.record()
-        check(lib().csu_stripe_attn_fwd(ctypes.byref(a), dtype_code(qkv), ptr(qkv), ptr(out), ptr(lse),
-                                        stream_ptr(qkv.device)), "csu_stripe_attn_fwd")
-        if timer is not None:
+            ev0.record()   # torch's current stream == the launch stream (stream_ptr above)
+            for _ in range(rep):
+                launch()
             ev1.record()
-            timer.append((ev0, ev1) + _stripe_fwd_work(geom, B, qkv.element_size()))
+            nbytes, flops = _stripe_fwd_work(geom, B, qkv.element_size())
+            timer.append((ev0, ev1, nbytes * rep, flops * rep, rep))
         ctx.geom = geom
         ctx.lepe_dtypes = [t.dtype for t in lepe]
         ctx.save_for_backward(qkv, out, lse, *ws, *bs)
