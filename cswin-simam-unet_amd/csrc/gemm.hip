@@ -179,22 +179,224 @@ int launch_t(long M, int N, int K, const bf16* A, int lda, const bf16* B, int ld
     return check_launch("gemm");
 }
 
+// ---- v3: b[n][k] operand only, 64-deep K slices, double-buffered LDS (one barrier per slice),
+// tile BM x BN in {64, 128}^2 chosen per shape for >= 2 workgroups per CU, LDS-staged epilogue
+// writing 16-B row vectors (bias / GELU' / residual applied there with vector loads).
+__device__ __forceinline__ int swz128g(int row, int chunk) { return row * 64 + ((chunk ^ (row & 7)) << 3); }
+
+__device__ __forceinline__ float gelu_fast(float x) {
+    // exact-erf GELU; erf via erfc(z) = t exp(-z^2 + P(t)), t = 1/(1 + z/2) (|rel err| < 1.2e-7)
+    const float z = fabsf(x) * 0.70710678118654752f;
+    const float t = 1.f / (1.f + 0.5f * z);
+    const float p = -1.26551223f + t * (1.00002368f + t * (0.37409196f + t * (0.09678418f + t * (-0.18628806f +
+                    t * (0.27886807f + t * (-1.13520398f + t * (1.48851587f + t * (-0.82215223f + t * 0.17087277f))))))));
+    const float erfc_z = t * __expf(-z * z + p);
+    const float erf_abs = 1.f - erfc_z;
+    const float e = x >= 0.f ? erf_abs : -erf_abs;
+    return 0.5f * x * (1.f + e);
+}
+
+template <int BM, int BN, bool GELU_A, typename TOUT>
+__global__ __launch_bounds__(NT) void gemm3_kernel(long M, int N, int K, const bf16* __restrict__ A, int lda,
+                                                   const bf16* __restrict__ Bm, int ldb, const float* __restrict__ bias,
+                                                   const bf16* __restrict__ gaux, const float* __restrict__ resid,
+                                                   TOUT* __restrict__ out, bf16* __restrict__ gout, int ldc) {
+    constexpr int BK3 = 64;
+    constexpr int TMW = BM / 64, TN = BN / 64;     // 32x32 MFMA tiles per wave (waves 2 x 2)
+    constexpr int CA = BM / 32, CB = BN / 32;      // 16-B staging chunks per thread
+    constexpr int STAGE = 2 * (BM + BN) * BK3;     // bf16 elements, double buffered
+    constexpr int EPI = BM * (BN + 4) * 2;         // fp32 epilogue tile, in bf16 units
+    constexpr int LDS = STAGE > EPI ? STAGE : EPI;
+    __shared__ __attribute__((aligned(16))) bf16 smem[LDS];
+    bf16* As = smem;                     // [2][BM * 64]
+    bf16* Bs = smem + 2 * BM * BK3;      // [2][BN * 64]
+    const long m0 = (long)blockIdx.x * BM;
+    const int n0 = blockIdx.y * BN;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int r = lane & 31, h = lane >> 5;
+    const int wm = (wave >> 1) * (BM / 2), wn = (wave & 1) * (BN / 2);
+    const int ch = threadIdx.x & 7, rb = threadIdx.x >> 3;
+    bf16x8 ra[CA], rbv[CB];
+    auto load = [&](int k0) {
+        const int k = k0 + 8 * ch;
+#pragma unroll
+        for (int i = 0; i < CA; ++i) {
+            const long m = m0 + rb + 32 * i;
+            ra[i] = (m < M && k < K) ? *reinterpret_cast<const bf16x8*>(A + m * lda + k) : bf16x8{};
+        }
+#pragma unroll
+        for (int j = 0; j < CB; ++j) {
+            const int n = n0 + rb + 32 * j;
+            rbv[j] = (n < N && k < K) ? *reinterpret_cast<const bf16x8*>(Bm + (long)n * ldb + k) : bf16x8{};
+        }
+    };
+    auto store = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < CA; ++i) {
+            bf16x8 v = ra[i];
+            if constexpr (GELU_A) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) v[j] = (bf16)gelu_fast((float)v[j]);
+            }
+            *reinterpret_cast<bf16x8*>(As + buf * BM * BK3 + swz128g(rb + 32 * i, ch)) = v;
+        }
+#pragma unroll
+        for (int j = 0; j < CB; ++j)
+            *reinterpret_cast<bf16x8*>(Bs + buf * BN * BK3 + swz128g(rb + 32 * j, ch)) = rbv[j];
+    };
+    f32x16 acc[TMW][TN];
+#pragma unroll
+    for (int i = 0; i < TMW; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = f32x16{};
+    load(0);
+    store(0);
+    __syncthreads();
+    int buf = 0;
+    for (int k0 = 0; k0 < K; k0 += BK3) {
+        const bool more = k0 + BK3 < K;
+        if (more) load(k0 + BK3);
+        const bf16* Ab = As + buf * BM * BK3;
+        const bf16* Bb = Bs + buf * BN * BK3;
+#pragma unroll
+        for (int s = 0; s < BK3 / 16; ++s) {
+            bf16x8 af[TMW], bfg[TN];
+#pragma unroll
+            for (int i = 0; i < TMW; ++i) af[i] = *reinterpret_cast<const bf16x8*>(Ab + swz128g(wm + 32 * i + r, 2 * s + h));
+#pragma unroll
+            for (int j = 0; j < TN; ++j) bfg[j] = *reinterpret_cast<const bf16x8*>(Bb + swz128g(wn + 32 * j + r, 2 * s + h));
+#pragma unroll
+            for (int i = 0; i < TMW; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfg[j], acc[i][j], 0, 0, 0);
+        }
+        if (more) store(buf ^ 1);
+        __syncthreads();
+        buf ^= 1;
+    }
+    // ---- epilogue: accumulators -> fp32 LDS tile [BM][BN + 4] -> 8-column row vectors ----
+    float* Ct = reinterpret_cast<float*>(smem);
+    constexpr int CS = BN + 4;
+#pragma unroll
+    for (int i = 0; i < TMW; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int reg = 0; reg < 16; ++reg)
+                Ct[(wm + 32 * i + crow(reg, h)) * CS + wn + 32 * j + r] = acc[i][j][reg];
+    __syncthreads();
+    constexpr int VPR = BN / 8;                     // 8-column vectors per row
+    for (int v = threadIdx.x; v < BM * VPR; v += NT) {
+        const int row = v / VPR, c8 = (v % VPR) * 8;
+        const long m = m0 + row;
+        const int n = n0 + c8;
+        if (m >= M || n >= N) continue;
+        float o[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = Ct[row * CS + c8 + e];
+        if (bias) {
+            float b8[8];
+            load8(bias + n, b8);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) o[e] += b8[e];
+        }
+        if (gaux) {
+            float g8[8];
+            load8(gaux + m * ldc + n, g8);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) o[e] *= gelu_grad(g8[e]);
+        }
+        if (resid) {
+            float r8[8];
+            load8(resid + m * ldc + n, r8);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) o[e] += r8[e];
+        }
+        store8(out + m * ldc + n, o);
+        if (gout) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) o[e] = gelu_fast(o[e]);
+            store8(gout + m * ldc + n, o);
+        }
+    }
+}
+
+template <int BM, int BN, bool GA>
+int launch3_t(long M, int N, int K, const bf16* A, int lda, const bf16* B, int ldb, const float* bias, const bf16* gaux,
+              const float* resid, void* out, bf16* gout, int ldc, int odt, hipStream_t st) {
+    const dim3 grid((unsigned)((M + BM - 1) / BM), (N + BN - 1) / BN);
+    if (odt == CSU_BF16)
+        gemm3_kernel<BM, BN, GA, bf16><<<grid, NT, 0, st>>>(M, N, K, A, lda, B, ldb, bias, gaux, resid, (bf16*)out, gout, ldc);
+    else
+        gemm3_kernel<BM, BN, GA, float><<<grid, NT, 0, st>>>(M, N, K, A, lda, B, ldb, bias, gaux, resid, (float*)out, gout, ldc);
+    return check_launch("gemm3");
+}
+
+// tile choice: the largest tile that still gives >= 2 workgroups per CU (256 CUs), else 64 x 64
+int pick_cfg(long M, int N) {
+    auto wgs = [&](int bm, int bn) { return ((M + bm - 1) / bm) * (long)((N + bn - 1) / bn); };
+    if (N > 64 && wgs(128, 128) >= 512) return 3;
+    if (wgs(128, 64) >= 512) return 2;
+    if (N > 64 && wgs(64, 128) >= 512) return 1;
+    return 0;
+}
+
+int launch3(int cfg, long M, int N, int K, const bf16* A, int lda, const bf16* B, int ldb, const float* bias,
+            const bf16* g, const float* resid, void* out, bf16* gout, int ldc, int odt, bool ga, hipStream_t st) {
+#define CSU_G3(BM_, BN_)                                                                                       \
+    return ga ? launch3_t<BM_, BN_, true>(M, N, K, A, lda, B, ldb, bias, g, resid, out, gout, ldc, odt, st)   \
+              : launch3_t<BM_, BN_, false>(M, N, K, A, lda, B, ldb, bias, g, resid, out, gout, ldc, odt, st)
+    switch (cfg) {
+        case 3: CSU_G3(128, 128);
+        case 2: CSU_G3(128, 64);
+        case 1: CSU_G3(64, 128);
+        default: CSU_G3(64, 64);
+    }
+#undef CSU_G3
+}
+
 }  // namespace
 }  // namespace csu
 
 using namespace csu;
 
+extern "C" int csu_gemm_ex(const csu_gemm_desc* d, void* stream);
+
 extern "C" int csu_gemm(long M, int N, int K, const void* a, int lda, const void* b, int ldb, int b_trans, int a_gelu,
                         const float* bias, const void* gelu_aux, const float* resid, void* out, int ldc, int out_dtype,
                         void* stream) {
-    if (M < 1 || N < 1 || K < 1 || !a || !b || !out) return fail(CSU_E_ARG, "gemm: bad args");
+    csu_gemm_desc d{};
+    d.M = M; d.N = N; d.K = K; d.a = a; d.b = b; d.lda = lda; d.ldb = ldb; d.b_trans = b_trans; d.a_gelu = a_gelu;
+    d.bias = bias; d.gelu_aux = gelu_aux; d.resid = resid; d.out = out; d.gelu_out = nullptr; d.ldc = ldc;
+    d.out_dtype = out_dtype; d.cfg = -1;
+    return csu_gemm_ex(&d, stream);
+}
+
+extern "C" int csu_gemm_ex(const csu_gemm_desc* d, void* stream) {
+    if (!d) return fail(CSU_E_ARG, "gemm: null descriptor");
+    const long M = d->M;
+    const int N = d->N, K = d->K, lda = d->lda, ldb = d->ldb, ldc = d->ldc, out_dtype = d->out_dtype;
+    const int b_trans = d->b_trans, a_gelu = d->a_gelu;
+    const float* bias = d->bias;
+    const float* resid = d->resid;
+    void* out = d->out;
+    int cfg = d->cfg;
+    if (M < 1 || N < 1 || K < 1 || !d->a || !d->b || !out) return fail(CSU_E_ARG, "gemm: bad args");
     if (K % 8 || lda % 8 || ldb % 8 || (b_trans && N % 8)) return fail(CSU_E_ARG, "gemm: K, lda, ldb (and N when b_trans) must be multiples of 8");
     if (out_dtype != CSU_BF16 && out_dtype != CSU_F32) return fail(CSU_E_ARG, "gemm: bad out dtype");
     if (resid && out_dtype != CSU_F32) return fail(CSU_E_ARG, "gemm: residual epilogue needs an fp32 output");
+    if (d->gelu_out && (out_dtype != CSU_BF16 || d->gelu_aux || resid || b_trans || N % 8 || ldc % 8))
+        return fail(CSU_E_ARG, "gemm: gelu_out needs a bf16 output, b_trans = 0, no gelu_aux/resid, N and ldc % 8 == 0");
     hipStream_t st = as_stream(stream);
-    const bf16* A = (const bf16*)a;
-    const bf16* B = (const bf16*)b;
-    const bf16* g = (const bf16*)gelu_aux;
+    const bf16* A = (const bf16*)d->a;
+    const bf16* B = (const bf16*)d->b;
+    const bf16* g = (const bf16*)d->gelu_aux;
+    if (!b_trans && N % 8 == 0 && ldc % 8 == 0) {
+        if (cfg < 0 || cfg > 3) cfg = pick_cfg(M, N);
+        return launch3(cfg, M, N, K, A, lda, B, ldb, bias, g, resid, out, (bf16*)d->gelu_out, ldc, out_dtype,
+                       a_gelu != 0, st);
+    }
     const bool wide = N > 64;
 #define CSU_GEMM_CASE(BN, BT, GA) return launch_t<BN, BT, GA>(M, N, K, A, lda, B, ldb, bias, g, resid, out, ldc, out_dtype, st)
     if (wide) {

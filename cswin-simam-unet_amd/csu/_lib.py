@@ -29,6 +29,14 @@ class StripeArgs(ctypes.Structure):
                 ("nbranch", c_int32), ("scale", c_float), ("_pad", c_int32), ("br", StripeBranch * 2)]
 
 
+class GemmDesc(ctypes.Structure):
+    """csu_gemm_desc (include/csu.h)."""
+    _fields_ = [("M", ctypes.c_int64), ("N", c_int32), ("K", c_int32), ("a", c_void_p), ("b", c_void_p),
+                ("lda", c_int32), ("ldb", c_int32), ("b_trans", c_int32), ("a_gelu", c_int32), ("bias", c_void_p),
+                ("gelu_aux", c_void_p), ("resid", c_void_p), ("out", c_void_p), ("gelu_out", c_void_p),
+                ("ldc", c_int32), ("out_dtype", c_int32), ("cfg", c_int32), ("_pad", c_int32)]
+
+
 class ConvGeom(ctypes.Structure):
     _fields_ = [(n, c_int32) for n in ("B", "H", "W", "C", "OH", "OW", "N", "KH", "KW", "stride", "pad")]
 
@@ -71,6 +79,8 @@ _SIGS = {
     "csu_gemm": (ctypes.c_int, [ctypes.c_long, ctypes.c_int, ctypes.c_int, c_void_p, ctypes.c_int, c_void_p, ctypes.c_int,
                                 ctypes.c_int, ctypes.c_int, c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_int,
                                 ctypes.c_int, c_void_p]),
+    "csu_cast_bf16_batch": (ctypes.c_int, [c_void_p, ctypes.c_int, ctypes.c_long, c_void_p]),
+    "csu_gemm_ex": (ctypes.c_int, [ctypes.POINTER(GemmDesc), c_void_p]),
     "csu_conv2d_fwd": (ctypes.c_int, [ctypes.POINTER(ConvGeom), ctypes.c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                                       c_void_p]),
     "csu_conv2d_dgrad": (ctypes.c_int, [ctypes.POINTER(ConvGeom), ctypes.c_int, c_void_p, c_void_p, c_void_p, c_void_p,

@@ -401,11 +401,16 @@ class CSWinTransformer(nn.Module):
         return logits.transpose(1, 2).reshape(B, self.num_classes, 4 * H, 4 * W)
 
     def _linear_weights(self):
+        """Weights the bf16 cast cache shadows: every nn.Linear and the CARAFE 1x1 convs that run
+        as token Linears (down / out)."""
         for m in self.modules():
             if isinstance(m, nn.Linear):
                 yield m.weight
                 if m.bias is not None:
                     yield m.bias
+            elif isinstance(m, CARAFE):
+                yield m.down.weight
+                yield m.out.weight
 
     def forward(self, x):
         cd = _compute_dtype(x)

@@ -337,14 +337,20 @@ def linear_wgrad(dy2: torch.Tensor, x2: torch.Tensor):
 
 
 def gemm(a2: torch.Tensor, b: torch.Tensor, b_trans: bool, out_dtype, bias=None, a_gelu=False, gelu_aux=None,
-         resid=None) -> torch.Tensor:
-    """csu_gemm: out = epi(pro(a2) @ B) with B = b^T (b_trans False, b is (N, K)) or b (b_trans True, (K, N))."""
+         resid=None, cfg: int = -1, gelu_out: bool = False):
+    """csu_gemm_ex: out = epi(pro(a2) @ B) with B = b^T (b_trans False, b is (N, K)) or b (b_trans True, (K, N)).
+    ``cfg`` forces a tile configuration of the b_trans=False kernel (-1: per-shape choice);
+    ``gelu_out`` also returns gelu(out) (bf16) written by the same epilogue: (out, gelu(out))."""
     M, K = a2.shape
     N = b.shape[1] if b_trans else b.shape[0]
     out = torch.empty(M, N, dtype=out_dtype, device=a2.device)
-    check(lib().csu_gemm(M, N, K, ptr(a2), a2.stride(0), ptr(b), b.stride(0), int(b_trans), int(a_gelu), ptr(bias),
-                         ptr(gelu_aux), ptr(resid), ptr(out), N, dtype_code(out), stream_ptr(a2.device)), "csu_gemm")
-    return out
+    g = torch.empty(M, N, dtype=torch.bfloat16, device=a2.device) if gelu_out else None
+    d = _lib.GemmDesc()
+    d.M, d.N, d.K, d.a, d.b, d.lda, d.ldb = M, N, K, ptr(a2), ptr(b), a2.stride(0), b.stride(0)
+    d.b_trans, d.a_gelu, d.bias, d.gelu_aux, d.resid = int(b_trans), int(a_gelu), ptr(bias), ptr(gelu_aux), ptr(resid)
+    d.out, d.gelu_out, d.ldc, d.out_dtype, d.cfg = ptr(out), ptr(g), N, dtype_code(out), int(cfg)
+    check(lib().csu_gemm_ex(ctypes.byref(d), stream_ptr(a2.device)), "csu_gemm_ex")
+    return (out, g) if gelu_out else out
 
 
 def linear_wgrad_gelu(dy2: torch.Tensor, h2: torch.Tensor):
@@ -362,14 +368,19 @@ def linear_wgrad_gelu(dy2: torch.Tensor, h2: torch.Tensor):
 
 import os as _os
 
-# csu_gemm (fused bias/GELU/residual token GEMM) for the nn.Linear forward/input-gradient GEMMs.
-# Off by default: on the 512x512 step it is still slower than hipBLASLt for the input-gradient
-# and GELU-prologue shapes (profiles/README.md); CSU_FUSED_GEMM=1 turns it on.
-FUSED_GEMM = _os.environ.get("CSU_FUSED_GEMM", "0") == "1"
+# csu_gemm_ex (fused bias / GELU / GELU' / residual token GEMM) for the bf16 nn.Linear forward and
+# input-gradient GEMMs; CSU_FUSED_GEMM=0 falls back to torch.matmul (hipBLASLt) for A/B checks.
+FUSED_GEMM = _os.environ.get("CSU_FUSED_GEMM", "1") == "1"
 
 
 def _gemm_ok(*dims):
     return all(d % 8 == 0 for d in dims)
+
+
+def _weight_t(w, wc):
+    """(K, N) bf16 transpose of the (N, K) weight w: the cast cache's copy, else made here."""
+    wt = _ACTIVE_CACHE.get_t(w, torch.bfloat16) if _ACTIVE_CACHE is not None else None
+    return wt if wt is not None else wc.t().contiguous()
 
 
 class _LinearFn(torch.autograd.Function):
@@ -380,10 +391,12 @@ class _LinearFn(torch.autograd.Function):
             wc = weight.to(cd)
         K, N = xc.shape[-1], wc.shape[0]
         ctx.fast = FUSED_GEMM and cd == torch.bfloat16 and xc.is_cuda and _gemm_ok(K, N)
+        wt = None
         if ctx.fast:
             x2 = xc.reshape(-1, K).contiguous()
             y = gemm(x2, wc, False, cd, bias=None if bias is None else bias.detach().float().contiguous())
             y = y.view(*xc.shape[:-1], N)
+            wt = _weight_t(weight, wc)
         else:
             bc = None
             if bias is not None:
@@ -391,13 +404,13 @@ class _LinearFn(torch.autograd.Function):
                 if bc is None:
                     bc = bias.to(cd)
             y = torch.nn.functional.linear(xc, wc, bc)
-        ctx.save_for_backward(xc, wc)
+        ctx.save_for_backward(xc, wt if ctx.fast else wc)
         ctx.meta = (x.dtype, weight.dtype, None if bias is None else bias.dtype)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        xc, wc = ctx.saved_tensors
+        xc, wc = ctx.saved_tensors          # wc: (K, N) transpose on the fast path
         xdt, wdt, bdt = ctx.meta
         K, N = xc.shape[-1], dy.shape[-1]
         dy2 = dy.reshape(-1, N)
@@ -408,7 +421,7 @@ class _LinearFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             if ctx.fast:
                 odt = xdt if xdt in (torch.float32, torch.bfloat16) else wc.dtype
-                dx = gemm(dy2, wc, True, odt).view(xc.shape)
+                dx = gemm(dy2, wc, False, odt).view(xc.shape)
             else:
                 dx = (dy2 @ wc).view(xc.shape)
             if dx.dtype != xdt:
@@ -436,43 +449,43 @@ class _LinearResidualFn(torch.autograd.Function):
         res2 = res.float().contiguous().view(-1, res.shape[-1])
         x2 = x.reshape(-1, x.shape[-1]).contiguous()
         y = gemm(x2, wc, False, torch.float32, bias=bias.detach().float().contiguous(), resid=res2)
-        ctx.save_for_backward(x2, wc)
+        ctx.save_for_backward(x2, _weight_t(weight, wc))
         ctx.meta = (res.dtype, x.shape, weight.dtype, bias.dtype)
         return y.view(res.shape)
 
     @staticmethod
     def backward(ctx, dy):
-        x2, wc = ctx.saved_tensors
+        x2, wt = ctx.saved_tensors
         rdt, xshape, wdt, bdt = ctx.meta
         dyb = dy.reshape(-1, dy.shape[-1]).to(torch.bfloat16).contiguous()
-        dx = gemm(dyb, wc, True, torch.bfloat16).view(xshape)
+        dx = gemm(dyb, wt, False, torch.bfloat16).view(xshape)
         dw, db = linear_wgrad(dyb, x2)
         return dy.to(rdt), dx, dw.to(wdt), db.to(bdt), None
 
 
 class _MlpResidualFn(torch.autograd.Function):
-    """res + fc2(gelu(fc1(x))) (Mlp cswin:180-196 + residual cswin:368) as two csu_gemm calls:
-    fc1 writes the pre-activation h (bf16); fc2 applies GELU to h on load and adds the residual in
-    its epilogue; backward fuses GELU' into the fc2 input-gradient epilogue."""
+    """res + fc2(gelu(fc1(x))) (Mlp cswin:180-196 + residual cswin:368) as two csu_gemm_ex calls:
+    fc1's epilogue writes the pre-activation h and gelu(h) (bf16); fc2 adds bias and the residual
+    in its epilogue; backward fuses GELU' into the fc2 input-gradient epilogue."""
 
     @staticmethod
     def forward(ctx, res, x, w1, b1, w2, b2, w1c, w2c):
         res2 = res.float().contiguous().view(-1, res.shape[-1])
         x2 = x.reshape(-1, x.shape[-1]).contiguous()
-        h = gemm(x2, w1c, False, torch.bfloat16, bias=b1.detach().float().contiguous())
-        y = gemm(h, w2c, False, torch.float32, bias=b2.detach().float().contiguous(), a_gelu=True, resid=res2)
-        ctx.save_for_backward(x2, h, w1c, w2c)
+        h, g = gemm(x2, w1c, False, torch.bfloat16, bias=b1.detach().float().contiguous(), gelu_out=True)
+        y = gemm(g, w2c, False, torch.float32, bias=b2.detach().float().contiguous(), resid=res2)
+        ctx.save_for_backward(x2, h, g, _weight_t(w1, w1c), _weight_t(w2, w2c))
         ctx.meta = (res.dtype, x.shape, w1.dtype, b1.dtype, w2.dtype, b2.dtype)
         return y.view(res.shape)
 
     @staticmethod
     def backward(ctx, dy):
-        x2, h, w1c, w2c = ctx.saved_tensors
+        x2, h, g, w1t, w2t = ctx.saved_tensors
         rdt, xshape, w1dt, b1dt, w2dt, b2dt = ctx.meta
         dyb = dy.reshape(-1, dy.shape[-1]).to(torch.bfloat16).contiguous()
-        dh = gemm(dyb, w2c, True, torch.bfloat16, gelu_aux=h)          # (dY W2) * gelu'(h)
-        dw2, db2 = linear_wgrad_gelu(dyb, h)                            # X = gelu(h) on the fly
-        dx = gemm(dh, w1c, True, torch.bfloat16).view(xshape)
+        dh = gemm(dyb, w2t, False, torch.bfloat16, gelu_aux=h)         # (dY W2) * gelu'(h)
+        dw2, db2 = linear_wgrad(dyb, g)
+        dx = gemm(dh, w1t, False, torch.bfloat16).view(xshape)
         dw1, db1 = linear_wgrad(dh, x2)
         return dy.to(rdt), dx, dw1.to(w1dt), db1.to(b1dt), dw2.to(w2dt), db2.to(b2dt), None, None
 
@@ -500,27 +513,68 @@ def mlp_residual(res, x, fc1: torch.nn.Linear, fc2: torch.nn.Linear):
 
 
 class CastCache:
-    """bf16 shadow copies of fp32 master weights, refreshed with ONE multi-tensor copy per
-    forward (instead of one cast kernel per Linear).  Gradients still flow to the fp32 params."""
+    """bf16 shadow copies of fp32 master weights, refreshed once per forward by ONE launch of
+    csu_cast_bf16_batch (instead of one cast kernel per Linear), plus a transposed (K, N) copy of
+    every 2-D weight for the input-gradient GEMM.  Gradients still flow to the fp32 params.
+    Lookup is by storage address, so reshaped views of a cached weight (the CARAFE 1x1 convs used
+    as token Linears) hit the cache too."""
 
     def __init__(self):
-        self.params, self.shadow, self.dtype = [], [], None
-        self.index = {}
+        self.params, self.shadow, self.shadow_t, self.dtype = [], [], [], None
+        self.index, self.ptrs = {}, []
+        self.items, self.tiles = None, 0
+
+    def _build(self, params, dtype):
+        self.params, self.dtype = params, dtype
+        self.ptrs = [p.data_ptr() for p in params]
+        self.shadow = [torch.empty(p.shape, dtype=dtype, device=p.device) for p in params]
+        self.shadow_t = [torch.empty(p.shape[1:].numel() if p.dim() > 1 else 0, p.shape[0], dtype=dtype, device=p.device)
+                         if p.dim() > 1 else None for p in params]
+        self.index = {p.data_ptr(): i for i, p in enumerate(params)}
+        self.items = None
+        if (dtype == torch.bfloat16 and params and all(p.is_cuda and p.dtype == torch.float32 and p.is_contiguous()
+                                                       for p in params)):
+            import numpy as np
+            rec = np.zeros(len(params), dtype=np.dtype([("src", "<u8"), ("dst", "<u8"), ("dst_t", "<u8"),
+                                                          ("rows", "<i4"), ("cols", "<i4"), ("tile0", "<i8")]))
+            t0 = 0
+            for i, p in enumerate(params):
+                rows = p.shape[0] if p.dim() > 1 else 1
+                cols = p.numel() // rows
+                st = self.shadow_t[i]
+                rec[i] = (p.data_ptr(), self.shadow[i].data_ptr(), 0 if st is None else st.data_ptr(), rows, cols, t0)
+                t0 += -(-rows // 64) * -(-cols // 64)
+            self.tiles = t0
+            self.items = torch.frombuffer(bytearray(rec.tobytes()), dtype=torch.uint8).to(params[0].device)
 
     def refresh(self, params, dtype):
         params = list(params)
-        if self.dtype != dtype or len(params) != len(self.params) or any(a is not b for a, b in zip(params, self.params)):
-            self.params, self.dtype = params, dtype
-            self.shadow = [torch.empty(p.shape, dtype=dtype, device=p.device) for p in params]
-            self.index = {id(p): i for i, p in enumerate(params)}
+        if (self.dtype != dtype or len(params) != len(self.params) or any(a is not b for a, b in zip(params, self.params))
+                or any(p.data_ptr() != q for p, q in zip(params, self.ptrs))):
+            self._build(params, dtype)
+        if self.items is not None:
+            check(lib().csu_cast_bf16_batch(ptr(self.items), len(self.params), self.tiles,
+                                            stream_ptr(self.params[0].device)), "csu_cast_bf16_batch")
+            return
         with torch.no_grad():
             torch._foreach_copy_(self.shadow, [p.detach() for p in self.params])
+            for st, p in zip(self.shadow_t, self.params):
+                if st is not None:
+                    st.copy_(p.detach().reshape(p.shape[0], -1).t())
 
     def get(self, p, dtype):
-        i = self.index.get(id(p))
-        if i is None or self.dtype != dtype:
+        i = self.index.get(p.data_ptr())
+        if i is None or self.dtype != dtype or self.params[i].numel() != p.numel():
             return None
-        return self.shadow[i]
+        return self.shadow[i].view(p.shape)
+
+    def get_t(self, p, dtype):
+        """(K, N) bf16 transpose of a 2-D (N, K) view of a cached weight, or None."""
+        i = self.index.get(p.data_ptr())
+        if i is None or self.dtype != dtype or p.dim() != 2 or self.shadow_t[i] is None:
+            return None
+        st = self.shadow_t[i]
+        return st if tuple(st.shape) == (p.shape[1], p.shape[0]) else None
 
 
 _ACTIVE_CACHE: Optional[CastCache] = None

@@ -178,6 +178,42 @@ int csu_linear_wgrad_ex(long M, int N, int K, int dtype, const void* dy, const v
 int csu_gemm(long M, int N, int K, const void* a, int lda, const void* b, int ldb, int b_trans, int a_gelu,
              const float* bias, const void* gelu_aux, const float* resid, void* out, int ldc, int out_dtype,
              void* stream);
+/* Extended form: everything csu_gemm takes plus
+ *   gelu_out  bf16 (M, ldc) or NULL: also write gelu(out) (exact erf GELU) -- fc1's activation
+ *             next to its pre-activation (needs out bf16, no gelu_aux/resid);
+ *   cfg       tile configuration of the b_trans = 0 kernel (0: 64x64, 1: 64x128, 2: 128x64,
+ *             3: 128x128; -1 = per-shape choice, what csu_gemm uses). */
+typedef struct {
+    int64_t M;
+    int32_t N, K;
+    const void* a;
+    const void* b;
+    int32_t lda, ldb;
+    int32_t b_trans, a_gelu;
+    const float* bias;
+    const void* gelu_aux;
+    const float* resid;
+    void* out;
+    void* gelu_out;
+    int32_t ldc, out_dtype;
+    int32_t cfg, _pad;
+} csu_gemm_desc;
+int csu_gemm_ex(const csu_gemm_desc* d, void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Batched weight cast: for each item, dst (rows, cols) bf16 = src fp32, and when dst_t is not
+ * NULL also dst_t (cols, rows) bf16 = src^T.  items is a DEVICE array sorted by tile0, the first
+ * 64x64-tile index of the item (tile0[i+1] = tile0[i] + ceil(rows/64) * ceil(cols/64));
+ * total_tiles = the sum.  One launch per step refreshes every bf16 shadow weight.
+ * ------------------------------------------------------------------------------------- */
+typedef struct {
+    const float* src;
+    void* dst;
+    void* dst_t;
+    int32_t rows, cols;
+    int64_t tile0;
+} csu_cast_item;
+int csu_cast_bf16_batch(const csu_cast_item* items, int count, long total_tiles, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * Implicit-GEMM NHWC convolution (patch embed cswin:505, Merge_Block.conv cswin:376, CARAFE

@@ -309,6 +309,45 @@ def test_gemm_vs_torch(M, N, K, b_trans, mode):
     assert_close(out, ref, torch.bfloat16)
 
 
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3])
+@pytest.mark.parametrize("M,N,K", [(1000, 64, 64), (4099, 192, 128), (300, 520, 1024)])
+def test_gemm_tile_configs_and_gelu_out(M, N, K, cfg):
+    """Every tile configuration of the b[n][k] kernel, with the dual (h, gelu(h)) epilogue."""
+    from csu import ops
+    d = dev()
+    g = torch.Generator(device=d).manual_seed(M + N + K + cfg)
+    a = torch.randn(M, K, device=d, generator=g).bfloat16()
+    w = (torch.randn(N, K, device=d, generator=g) * 0.1).bfloat16()
+    bias = torch.randn(N, device=d, generator=g)
+    h, gh = ops.gemm(a, w, False, torch.bfloat16, bias=bias, cfg=cfg, gelu_out=True)
+    ref = a.double() @ w.double().t() + bias.double()
+    assert_close(h, ref, torch.bfloat16)
+    assert_close(gh, _gelu(ref), torch.bfloat16)
+    # the GELU output is computed from the fp32 accumulator (before the bf16 rounding of h)
+    assert float((gh.float() - _gelu(h.float())).abs().max()) < 2e-2 * float(ref.abs().max())
+
+
+def test_cast_cache_batch_kernel():
+    """csu_cast_bf16_batch: bf16 shadows and (K, N) transposes of 2-D, 1-D and 4-D weights."""
+    from csu import ops
+    d = dev()
+    torch.manual_seed(3)
+    ps = [torch.randn(192, 64, device=d), torch.randn(70, device=d), torch.randn(16, 64, 1, 1, device=d),
+          torch.randn(130, 333, device=d), torch.randn(5, device=d)]
+    c = ops.CastCache()
+    c.refresh(ps, torch.bfloat16)
+    assert c.items is not None
+    for p in ps:
+        torch.testing.assert_close(c.get(p, torch.bfloat16), p.bfloat16(), rtol=0, atol=0)
+        if p.dim() > 1:
+            v = p.reshape(p.shape[0], -1)
+            torch.testing.assert_close(c.get_t(v, torch.bfloat16), v.t().bfloat16(), rtol=0, atol=0)
+    with torch.no_grad():
+        ps[0].mul_(2)
+    c.refresh(ps, torch.bfloat16)
+    torch.testing.assert_close(c.get(ps[0], torch.bfloat16), ps[0].bfloat16(), rtol=0, atol=0)
+
+
 def test_fused_mlp_residual_matches_unfused():
     """mlp_residual / linear_residual (bf16 fused GEMMs) == the unfused autocast composition."""
     from csu import ops
