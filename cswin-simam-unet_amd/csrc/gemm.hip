@@ -184,19 +184,25 @@ int launch_t(long M, int N, int K, const bf16* A, int lda, const bf16* B, int ld
 // writing 16-B row vectors (bias / GELU' / residual applied there with vector loads).
 __device__ __forceinline__ int swz128g(int row, int chunk) { return row * 64 + ((chunk ^ (row & 7)) << 3); }
 
+// erf(|x|/sqrt2) by Abramowitz-Stegun 7.1.26 (|abs err| < 1.5e-7): one rcp, one exp, 6 FMAs.
+__device__ __forceinline__ float erf_as(float z) {   // z >= 0
+    const float t = __frcp_rn(1.f + 0.3275911f * z);
+    const float p = t * (0.254829592f + t * (-0.284496736f + t * (1.421413741f + t * (-1.453152027f + t * 1.061405429f))));
+    return 1.f - p * __expf(-z * z);
+}
 __device__ __forceinline__ float gelu_fast(float x) {
-    // exact-erf GELU; erf via erfc(z) = t exp(-z^2 + P(t)), t = 1/(1 + z/2) (|rel err| < 1.2e-7)
-    const float z = fabsf(x) * 0.70710678118654752f;
-    const float t = 1.f / (1.f + 0.5f * z);
-    const float p = -1.26551223f + t * (1.00002368f + t * (0.37409196f + t * (0.09678418f + t * (-0.18628806f +
-                    t * (0.27886807f + t * (-1.13520398f + t * (1.48851587f + t * (-0.82215223f + t * 0.17087277f))))))));
-    const float erfc_z = t * __expf(-z * z + p);
-    const float erf_abs = 1.f - erfc_z;
-    const float e = x >= 0.f ? erf_abs : -erf_abs;
-    return 0.5f * x * (1.f + e);
+    const float e = erf_as(fabsf(x) * 0.70710678118654752f);
+    return 0.5f * x * (1.f + (x >= 0.f ? e : -e));
+}
+__device__ __forceinline__ float gelu_grad_fast(float x) {
+    const float e = erf_as(fabsf(x) * 0.70710678118654752f);
+    return 0.5f * (1.f + (x >= 0.f ? e : -e)) + x * 0.3989422804014327f * __expf(-0.5f * x * x);
 }
 
-template <int BM, int BN, bool GELU_A, typename TOUT>
+// STG = LDS stages (1 when K <= 64: a single slice, no prefetch).  The epilogue runs in two
+// row halves so its fp32 staging tile fits in the (smaller) stage buffers: with one stage a
+// 128 x 128 tile needs 34 KB of LDS and four workgroups share a CU.
+template <int BM, int BN, int STG, bool GELU_A, typename TOUT>
 __global__ __launch_bounds__(NT) void gemm3_kernel(long M, int N, int K, const bf16* __restrict__ A, int lda,
                                                    const bf16* __restrict__ Bm, int ldb, const float* __restrict__ bias,
                                                    const bf16* __restrict__ gaux, const float* __restrict__ resid,
@@ -204,17 +210,19 @@ __global__ __launch_bounds__(NT) void gemm3_kernel(long M, int N, int K, const b
     constexpr int BK3 = 64;
     constexpr int TMW = BM / 64, TN = BN / 64;     // 32x32 MFMA tiles per wave (waves 2 x 2)
     constexpr int CA = BM / 32, CB = BN / 32;      // 16-B staging chunks per thread
-    constexpr int STAGE = 2 * (BM + BN) * BK3;     // bf16 elements, double buffered
-    constexpr int EPI = BM * (BN + 4) * 2;         // fp32 epilogue tile, in bf16 units
+    constexpr int STAGE = STG * (BM + BN) * BK3;   // bf16 elements
+    constexpr int HB = BM / 2;                     // epilogue rows per half
+    constexpr int CS = BN + 4;                     // fp32 row stride of the epilogue tile
+    constexpr int EPI = HB * CS * 2;               // in bf16 units
     constexpr int LDS = STAGE > EPI ? STAGE : EPI;
     __shared__ __attribute__((aligned(16))) bf16 smem[LDS];
-    bf16* As = smem;                     // [2][BM * 64]
-    bf16* Bs = smem + 2 * BM * BK3;      // [2][BN * 64]
+    bf16* As = smem;                       // [STG][BM * 64]
+    bf16* Bs = smem + STG * BM * BK3;      // [STG][BN * 64]
     const long m0 = (long)blockIdx.x * BM;
     const int n0 = blockIdx.y * BN;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int r = lane & 31, h = lane >> 5;
-    const int wm = (wave >> 1) * (BM / 2), wn = (wave & 1) * (BN / 2);
+    const int wm = (wave >> 1) * HB, wn = (wave & 1) * (BN / 2);
     const int ch = threadIdx.x & 7, rb = threadIdx.x >> 3;
     bf16x8 ra[CA], rbv[CB];
     auto load = [&](int k0) {
@@ -254,7 +262,7 @@ __global__ __launch_bounds__(NT) void gemm3_kernel(long M, int N, int K, const b
     __syncthreads();
     int buf = 0;
     for (int k0 = 0; k0 < K; k0 += BK3) {
-        const bool more = k0 + BK3 < K;
+        const bool more = STG > 1 && k0 + BK3 < K;
         if (more) load(k0 + BK3);
         const bf16* Ab = As + buf * BM * BK3;
         const bf16* Bb = Bs + buf * BN * BK3;
@@ -273,73 +281,101 @@ __global__ __launch_bounds__(NT) void gemm3_kernel(long M, int N, int K, const b
         }
         if (more) store(buf ^ 1);
         __syncthreads();
-        buf ^= 1;
+        if constexpr (STG > 1) buf ^= 1;
     }
-    // ---- epilogue: accumulators -> fp32 LDS tile [BM][BN + 4] -> 8-column row vectors ----
+    // ---- epilogue, per row half: prefetch bias/aux/resid vectors -> accumulators to the fp32 LDS
+    // tile [HB][BN + 4] -> 8-column row vectors with the fused ops, 16-B stores ----
     float* Ct = reinterpret_cast<float*>(smem);
-    constexpr int CS = BN + 4;
+    constexpr int VPR = BN / 8;                    // 8-column vectors per row
+    constexpr int EV = HB * VPR / NT;              // vectors per thread per half (>= 1)
+    static_assert(EV >= 1 && HB * VPR % NT == 0, "epilogue split");
+    const int c8 = (threadIdx.x % VPR) * 8;
+    const int n = n0 + c8;
+    float bv[8];
+    if (bias && n < N) load8(bias + n, bv);
+    else
 #pragma unroll
-    for (int i = 0; i < TMW; ++i)
+        for (int e = 0; e < 8; ++e) bv[e] = 0.f;
 #pragma unroll
-        for (int j = 0; j < TN; ++j)
+    for (int half = 0; half < 2; ++half) {
+        float pre[EV][8];
 #pragma unroll
-            for (int reg = 0; reg < 16; ++reg)
-                Ct[(wm + 32 * i + crow(reg, h)) * CS + wn + 32 * j + r] = acc[i][j][reg];
-    __syncthreads();
-    constexpr int VPR = BN / 8;                     // 8-column vectors per row
-    for (int v = threadIdx.x; v < BM * VPR; v += NT) {
-        const int row = v / VPR, c8 = (v % VPR) * 8;
-        const long m = m0 + row;
-        const int n = n0 + c8;
-        if (m >= M || n >= N) continue;
-        float o[8];
+        for (int v = 0; v < EV; ++v) {
+            const int row = (threadIdx.x + v * NT) / VPR;
+            const long m = m0 + half * HB + row;
+            const bool ok = m < M && n < N;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) o[e] = Ct[row * CS + c8 + e];
-        if (bias) {
-            float b8[8];
-            load8(bias + n, b8);
-#pragma unroll
-            for (int e = 0; e < 8; ++e) o[e] += b8[e];
+            for (int e = 0; e < 8; ++e) pre[v][e] = 0.f;
+            if (gaux && ok) load8(gaux + m * ldc + n, pre[v]);
+            else if (resid && ok) load8(resid + m * ldc + n, pre[v]);
         }
-        if (gaux) {
-            float g8[8];
-            load8(gaux + m * ldc + n, g8);
+        if ((wave >> 1) == half) {
 #pragma unroll
-            for (int e = 0; e < 8; ++e) o[e] *= gelu_grad(g8[e]);
-        }
-        if (resid) {
-            float r8[8];
-            load8(resid + m * ldc + n, r8);
+            for (int i = 0; i < TMW; ++i)
 #pragma unroll
-            for (int e = 0; e < 8; ++e) o[e] += r8[e];
-        }
-        store8(out + m * ldc + n, o);
-        if (gout) {
+                for (int j = 0; j < TN; ++j)
 #pragma unroll
-            for (int e = 0; e < 8; ++e) o[e] = gelu_fast(o[e]);
-            store8(gout + m * ldc + n, o);
+                    for (int reg = 0; reg < 16; ++reg)
+                        Ct[(32 * i + crow(reg, h)) * CS + wn + 32 * j + r] = acc[i][j][reg];
         }
+        __syncthreads();
+#pragma unroll
+        for (int v = 0; v < EV; ++v) {
+            const int row = (threadIdx.x + v * NT) / VPR;
+            const long m = m0 + half * HB + row;
+            if (m >= M || n >= N) continue;
+            float o[8];
+            const f32x4 lo = *reinterpret_cast<const f32x4*>(Ct + row * CS + c8);
+            const f32x4 hi = *reinterpret_cast<const f32x4*>(Ct + row * CS + c8 + 4);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                o[e] = lo[e] + bv[e];
+                o[e + 4] = hi[e] + bv[e + 4];
+            }
+            if (gaux) {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) o[e] *= gelu_grad_fast(pre[v][e]);
+            } else if (resid) {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) o[e] += pre[v][e];
+            }
+            store8(out + m * ldc + n, o);
+            if (gout) {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) o[e] = gelu_fast(o[e]);
+                store8(gout + m * ldc + n, o);
+            }
+        }
+        __syncthreads();
     }
+}
+
+template <int BM, int BN, int STG, bool GA>
+int launch3_s(long M, int N, int K, const bf16* A, int lda, const bf16* B, int ldb, const float* bias, const bf16* gaux,
+              const float* resid, void* out, bf16* gout, int ldc, int odt, hipStream_t st) {
+    const dim3 grid((unsigned)((M + BM - 1) / BM), (N + BN - 1) / BN);
+    if (odt == CSU_BF16)
+        gemm3_kernel<BM, BN, STG, GA, bf16><<<grid, NT, 0, st>>>(M, N, K, A, lda, B, ldb, bias, gaux, resid, (bf16*)out, gout, ldc);
+    else
+        gemm3_kernel<BM, BN, STG, GA, float><<<grid, NT, 0, st>>>(M, N, K, A, lda, B, ldb, bias, gaux, resid, (float*)out, gout, ldc);
+    return check_launch("gemm3");
 }
 
 template <int BM, int BN, bool GA>
 int launch3_t(long M, int N, int K, const bf16* A, int lda, const bf16* B, int ldb, const float* bias, const bf16* gaux,
               const float* resid, void* out, bf16* gout, int ldc, int odt, hipStream_t st) {
-    const dim3 grid((unsigned)((M + BM - 1) / BM), (N + BN - 1) / BN);
-    if (odt == CSU_BF16)
-        gemm3_kernel<BM, BN, GA, bf16><<<grid, NT, 0, st>>>(M, N, K, A, lda, B, ldb, bias, gaux, resid, (bf16*)out, gout, ldc);
-    else
-        gemm3_kernel<BM, BN, GA, float><<<grid, NT, 0, st>>>(M, N, K, A, lda, B, ldb, bias, gaux, resid, (float*)out, gout, ldc);
-    return check_launch("gemm3");
+    if (K <= 64) return launch3_s<BM, BN, 1, GA>(M, N, K, A, lda, B, ldb, bias, gaux, resid, out, gout, ldc, odt, st);
+    return launch3_s<BM, BN, 2, GA>(M, N, K, A, lda, B, ldb, bias, gaux, resid, out, gout, ldc, odt, st);
 }
 
-// tile choice: the largest tile that still gives >= 2 workgroups per CU (256 CUs), else 64 x 64
-int pick_cfg(long M, int N) {
-    auto wgs = [&](int bm, int bn) { return ((M + bm - 1) / bm) * (long)((N + bn - 1) / bn); };
-    if (N > 64 && wgs(128, 128) >= 512) return 3;
-    if (wgs(128, 64) >= 512) return 2;
-    if (N > 64 && wgs(64, 128) >= 512) return 1;
-    return 0;
+// tile choice (measured on the CSWin-UNet token shapes, tools/gemm_probe3.py): 128 x 64 for a
+// plain / bias epilogue; 64 x 64 when the epilogue streams a second tensor (GELU' aux, residual,
+// h + gelu(h)) -- more workgroups per CU overlap those epilogue loads/stores with other tiles'
+// main loops; 64 x 64 as well when 128 x 64 would leave fewer than one workgroup per CU.
+int pick_cfg(long M, int N, bool heavy_epilogue) {
+    const long wgs2 = ((M + 127) / 128) * (long)((N + 63) / 64);
+    if (heavy_epilogue || wgs2 < 256) return 0;
+    return 2;
 }
 
 int launch3(int cfg, long M, int N, int K, const bf16* A, int lda, const bf16* B, int ldb, const float* bias,
@@ -393,7 +429,7 @@ extern "C" int csu_gemm_ex(const csu_gemm_desc* d, void* stream) {
     const bf16* B = (const bf16*)d->b;
     const bf16* g = (const bf16*)d->gelu_aux;
     if (!b_trans && N % 8 == 0 && ldc % 8 == 0) {
-        if (cfg < 0 || cfg > 3) cfg = pick_cfg(M, N);
+        if (cfg < 0 || cfg > 3) cfg = pick_cfg(M, N, d->gelu_out || d->gelu_aux || resid);
         return launch3(cfg, M, N, K, A, lda, B, ldb, bias, g, resid, out, (bf16*)d->gelu_out, ldc, out_dtype,
                        a_gelu != 0, st);
     }

@@ -31,20 +31,25 @@ def timeit(fn, n=20):
     return e0.elapsed_time(e1) / n * 1e3
 
 
-for name, M, K, N in shapes:
-    x = torch.randn(M, K, device=d, dtype=torch.bfloat16)
-    w = torch.randn(N, K, device=d, dtype=torch.bfloat16)
-    dy = torch.randn(M, N, device=d, dtype=torch.bfloat16)
-    bias = torch.randn(N, device=d)
-    wt = w.t().contiguous()
-    t_f = timeit(lambda: torch.nn.functional.linear(x, w))
-    t_d = timeit(lambda: dy @ w)
-    cf = [timeit(lambda: ops.gemm(x, w, False, torch.bfloat16, bias=bias, cfg=c)) for c in range(4)]
-    cd = [timeit(lambda: ops.gemm(dy, wt, False, torch.bfloat16, cfg=c)) for c in range(4)]
-    c_a = timeit(lambda: ops.gemm(x, w, False, torch.bfloat16, bias=bias))
-    c_g = timeit(lambda: ops.gemm(x, w, False, torch.bfloat16, bias=bias, a_gelu=True))
-    err = (ops.gemm(x, w, False, torch.float32) - (x.float() @ w.float().t())).abs().max().item()
-    errd = (ops.gemm(dy, wt, False, torch.float32) - (dy.float() @ w.float())).abs().max().item()
-    print(f"{name:8s} M={M:7d} K={K:5d} N={N:5d}  torch fwd {t_f:6.1f} dgrad {t_d:6.1f} | csu auto fwd {c_a:6.1f} "
-          f"gelu-fwd {c_g:6.1f} | cfg fwd " + " ".join(f"{v:6.1f}" for v in cf) + " | cfg dgrad " +
-          " ".join(f"{v:6.1f}" for v in cd) + f"  err {err:.2g} {errd:.2g}", flush=True)
+def main():
+  for name, M, K, N in shapes:
+      x = torch.randn(M, K, device=d, dtype=torch.bfloat16)
+      w = torch.randn(N, K, device=d, dtype=torch.bfloat16)
+      dy = torch.randn(M, N, device=d, dtype=torch.bfloat16)
+      bias = torch.randn(N, device=d)
+      wt = w.t().contiguous()
+      t_f = timeit(lambda: torch.nn.functional.linear(x, w))
+      t_d = timeit(lambda: dy @ w)
+      cf = [timeit(lambda: ops.gemm(x, w, False, torch.bfloat16, bias=bias, cfg=c)) for c in range(4)]
+      cd = [timeit(lambda: ops.gemm(dy, wt, False, torch.bfloat16, cfg=c)) for c in range(4)]
+      c_a = timeit(lambda: ops.gemm(x, w, False, torch.bfloat16, bias=bias))
+      c_g = timeit(lambda: ops.gemm(x, w, False, torch.bfloat16, bias=bias, a_gelu=True))
+      err = (ops.gemm(x, w, False, torch.float32) - (x.float() @ w.float().t())).abs().max().item()
+      errd = (ops.gemm(dy, wt, False, torch.float32) - (dy.float() @ w.float())).abs().max().item()
+      print(f"{name:8s} M={M:7d} K={K:5d} N={N:5d}  torch fwd {t_f:6.1f} dgrad {t_d:6.1f} | csu auto fwd {c_a:6.1f} "
+            f"gelu-fwd {c_g:6.1f} | cfg fwd " + " ".join(f"{v:6.1f}" for v in cf) + " | cfg dgrad " +
+            " ".join(f"{v:6.1f}" for v in cd) + f"  err {err:.2g} {errd:.2g}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
