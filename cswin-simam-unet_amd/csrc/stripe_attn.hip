@@ -195,8 +195,16 @@ __device__ __forceinline__ void lepe4(const Win& w, int reso, const T* img, int 
 }
 
 __device__ __forceinline__ void stage_lepe_weights(const csu_stripe_branch& g, int h, float* wts) {
-    for (int i = threadIdx.x; i < HD * 10; i += NT)
-        wts[i] = i < HD * 9 ? g.lepe_w[h * HD * 9 + i] : g.lepe_b[h * HD + i - HD * 9];
+    constexpr int IT = (HD * 10 + NT - 1) / NT;
+    float v[IT];
+#pragma unroll
+    for (int k = 0; k < IT; ++k) {
+        const int i = threadIdx.x + k * NT;
+        v[k] = i < HD * 9 ? g.lepe_w[h * HD * 9 + i] : (i < HD * 10 ? g.lepe_b[h * HD + i - HD * 9] : 0.f);
+    }
+#pragma unroll
+    for (int k = 0; k < IT; ++k)
+        if (threadIdx.x + k * NT < HD * 10) wts[threadIdx.x + k * NT] = v[k];
 }
 
 __device__ __forceinline__ size_t stat_index(const csu_stripe_args& a, const Win& w, int tok) {
@@ -616,14 +624,30 @@ __device__ __forceinline__ void mma_acc_sw(f32x16& acc, const bf16* img, int kba
     }
 }
 
-// gather the window rows [0, npad) of one head's channels into a swizzled image (rows >= N zero)
-__device__ __forceinline__ void stage_win(const Win& w, int reso, const bf16* img, int rstride, int ch, int npad,
-                                          bf16* dst) {
-    for (int it = threadIdx.x; it < npad * 4; it += NT) {
+// gather the window rows [0, npad) of one head's channels of two tensors into swizzled images
+// (rows >= N zero).  All global loads of the thread are issued before the first LDS store, so the
+// staging costs one memory latency instead of one per row group.
+__device__ __forceinline__ void stage_win2(const Win& w, int reso, const bf16* imgA, int strideA, int chA,
+                                           const bf16* imgB, int strideB, int chB, int npad, bf16* dstA, bf16* dstB) {
+    constexpr int MAXIT = WMAX * 4 / NT;
+    bf16x8 va[MAXIT], vb[MAXIT];
+#pragma unroll
+    for (int i = 0; i < MAXIT; ++i) {
+        const int it = threadIdx.x + i * NT;
         const int n = it >> 2, c = (it & 3) * 8;
-        bf16x8 v = {};
-        if (n < w.N) v = *reinterpret_cast<const bf16x8*>(img + (size_t)tok_of(w, reso, n) * rstride + ch + c);
-        *reinterpret_cast<bf16x8*>(dst + swz(n, c)) = v;
+        const bool ok = it < npad * 4 && n < w.N;
+        const size_t tok = ok ? (size_t)tok_of(w, reso, n) : 0;
+        va[i] = ok ? *reinterpret_cast<const bf16x8*>(imgA + tok * strideA + chA + c) : bf16x8{};
+        vb[i] = ok ? *reinterpret_cast<const bf16x8*>(imgB + tok * strideB + chB + c) : bf16x8{};
+    }
+#pragma unroll
+    for (int i = 0; i < MAXIT; ++i) {
+        const int it = threadIdx.x + i * NT;
+        if (it < npad * 4) {
+            const int n = it >> 2, c = (it & 3) * 8;
+            *reinterpret_cast<bf16x8*>(dstA + swz(n, c)) = va[i];
+            *reinterpret_cast<bf16x8*>(dstB + swz(n, c)) = vb[i];
+        }
     }
 }
 
@@ -676,17 +700,27 @@ __global__ __launch_bounds__(NT) void stripe_fwd_w(csu_stripe_args a, int split,
     const int npad = (w.N + 31) & ~31;
     const int rows = (npad + split - 1) / split;            // query rows of this workgroup
     const int qbeg = w.blk * rows, qend = min(npad, qbeg + rows);
+    // this wave's first query fragment is loaded together with the K/V staging loads
+    Frag<bf16> qnext;
+    {
+        const int qn = qbeg + 32 * wave + r;
+        const bool qv = qbeg + 32 * wave < qend && qn < w.N;
+        load_frag(qnext, img + (size_t)(qv ? tok_of(w, a.reso, qn) : 0) * C3 + w.chq, h, qv);
+    }
     stage_lepe_weights(branch(a, w.br), w.h, wts);
-    stage_win(w, a.reso, img, C3, C + w.chq, (npad + 63) & ~63, Ks);   // zero rows up to a 64-key step
-    stage_win(w, a.reso, img, C3, 2 * C + w.chq, (npad + 63) & ~63, Vs);
+    stage_win2(w, a.reso, img, C3, C + w.chq, img, C3, 2 * C + w.chq, (npad + 63) & ~63, Ks, Vs);  // zero rows up to a 64-key step
     __syncthreads();
     const float c = a.scale * kLog2e;
     for (int q0 = qbeg + 32 * wave; q0 < qend; q0 += 128) {
         const int qn = q0 + r;
         const bool qvalid = qn < w.N;
         const int qtok = qvalid ? tok_of(w, a.reso, qn) : 0;
-        Frag<bf16> qf;
-        load_frag(qf, img + (size_t)qtok * C3 + w.chq, h, qvalid);
+        const Frag<bf16> qf = qnext;
+        if (q0 + 128 < qend) {
+            const int qn2 = q0 + 128 + r;
+            const bool qv2 = qn2 < w.N;
+            load_frag(qnext, img + (size_t)(qv2 ? tok_of(w, a.reso, qn2) : 0) * C3 + w.chq, h, qv2);
+        }
         float m = -INFINITY, l = 0.f;
         f32x16 o = {};
         // 64 keys per online-softmax step: two independent S^T tiles, one rescale of O
@@ -752,18 +786,30 @@ __global__ __launch_bounds__(NT) void stripe_bwd_dq_w(csu_stripe_args a, int spl
     const int npad = (w.N + 31) & ~31;
     const int rows = (npad + split - 1) / split;
     const int qbeg = w.blk * rows, qend = min(npad, qbeg + rows);
+    Frag<bf16> qn_f, gn_f;   // first query block's fragments, loaded with the staging loads
+    {
+        const int qn = qbeg + 32 * wave + r;
+        const bool qv = qbeg + 32 * wave < qend && qn < w.N;
+        const size_t t = qv ? tok_of(w, a.reso, qn) : 0;
+        load_frag(qn_f, img + t * C3 + w.chq, h, qv);
+        load_frag(gn_f, gimg + t * C + w.chq, h, qv);
+    }
     stage_lepe_weights(branch(a, w.br), w.h, wts);
-    stage_win(w, a.reso, img, C3, C + w.chq, npad, Ks);
-    stage_win(w, a.reso, img, C3, 2 * C + w.chq, npad, Vs);
+    stage_win2(w, a.reso, img, C3, C + w.chq, img, C3, 2 * C + w.chq, npad, Ks, Vs);
     __syncthreads();
     const float c = a.scale * kLog2e;
     for (int q0 = qbeg + 32 * wave; q0 < qend; q0 += 128) {
         const int qn = q0 + r;
         const bool qvalid = qn < w.N;
         const int qtok = qvalid ? tok_of(w, a.reso, qn) : 0;
-        Frag<bf16> qf, gf;
-        load_frag(qf, img + (size_t)qtok * C3 + w.chq, h, qvalid);
-        load_frag(gf, gimg + (size_t)qtok * C + w.chq, h, qvalid);
+        const Frag<bf16> qf = qn_f, gf = gn_f;
+        if (q0 + 128 < qend) {
+            const int qn2 = q0 + 128 + r;
+            const bool qv2 = qn2 < w.N;
+            const size_t t2 = qv2 ? tok_of(w, a.reso, qn2) : 0;
+            load_frag(qn_f, img + t2 * C3 + w.chq, h, qv2);
+            load_frag(gn_f, gimg + t2 * C + w.chq, h, qv2);
+        }
         float dl = 0.f;
         if (qvalid) {
 #pragma unroll
@@ -822,9 +868,16 @@ __global__ __launch_bounds__(NT) void stripe_bwd_dkdv_w(csu_stripe_args a, int s
     const int npad = (w.N + 31) & ~31;
     const int rows = (npad + split - 1) / split;
     const int kbeg = w.blk * rows, kend = min(npad, kbeg + rows);
+    Frag<bf16> kn_f, vn_f;   // first key block's fragments, loaded with the staging loads
+    {
+        const int kn = kbeg + 32 * wave + r;
+        const bool kv = kbeg + 32 * wave < kend && kn < w.N;
+        const size_t t = kv ? tok_of(w, a.reso, kn) : 0;
+        load_frag(kn_f, img + t * C3 + C + w.chq, h, kv);
+        load_frag(vn_f, img + t * C3 + 2 * C + w.chq, h, kv);
+    }
     stage_lepe_weights(branch(a, w.br), w.h, wts);
-    stage_win(w, a.reso, img, C3, w.chq, npad, Qs);
-    stage_win(w, a.reso, gimg, C, w.chq, npad, Gs);
+    stage_win2(w, a.reso, img, C3, w.chq, gimg, C, w.chq, npad, Qs, Gs);
     for (int i = threadIdx.x; i < npad; i += NT) {
         const bool v = i < w.N;
         const size_t si = stat_index(a, w, v ? tok_of(w, a.reso, i) : 0);
@@ -837,9 +890,14 @@ __global__ __launch_bounds__(NT) void stripe_bwd_dkdv_w(csu_stripe_args a, int s
         const int kn = k0 + r;
         const bool kvalid = kn < w.N;
         const int ktok = kvalid ? tok_of(w, a.reso, kn) : 0;
-        Frag<bf16> kf, vf;
-        load_frag(kf, img + (size_t)ktok * C3 + C + w.chq, h, kvalid);
-        load_frag(vf, img + (size_t)ktok * C3 + 2 * C + w.chq, h, kvalid);
+        const Frag<bf16> kf = kn_f, vf = vn_f;
+        if (k0 + 128 < kend) {
+            const int kn2 = k0 + 128 + r;
+            const bool kv2 = kn2 < w.N;
+            const size_t t2 = kv2 ? tok_of(w, a.reso, kn2) : 0;
+            load_frag(kn_f, img + t2 * C3 + C + w.chq, h, kv2);
+            load_frag(vn_f, img + t2 * C3 + 2 * C + w.chq, h, kv2);
+        }
         f32x16 dk = {}, dv = {};
         for (int qb = 0; qb < npad; qb += 32) {
             f32x16 s = {}, dp = {};

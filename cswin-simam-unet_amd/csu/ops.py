@@ -3,6 +3,7 @@ kernel; there is no CPU or eager-PyTorch fallback (CPU tensors raise ``CsuError`
 from __future__ import annotations
 
 import ctypes
+import os as _os
 from typing import List, Optional, Sequence, Tuple
 
 import torch
@@ -353,6 +354,64 @@ def gemm(a2: torch.Tensor, b: torch.Tensor, b_trans: bool, out_dtype, bias=None,
     return (out, g) if gelu_out else out
 
 
+# ---------------------------------------------------------------------------------------------
+# Weight gradients on a side stream.  dW = dY^T X of a Linear is off the backward critical path
+# (nothing in the rest of backward reads it), and each wgrad/colsum launch alone leaves most CUs
+# waiting on memory latency, so it runs on a second HIP stream overlapped with the input-gradient
+# chain.  Fork: the side stream waits on the launching stream; inputs are record_stream'ed; the
+# launching stream waits on every side event at the end of backward (autograd final callback),
+# before the optimizer or any user code can read .grad.  Off under multi-rank DDP (its reducer
+# reads gradients from hooks during backward).  Opt-in (CSU_SIDE_WGRAD=1): on the 512x512 step the
+# overlapped kernels slow each other down and the graphed step time does not improve.
+# ---------------------------------------------------------------------------------------------
+SIDE_WGRAD = _os.environ.get("CSU_SIDE_WGRAD", "0") == "1"
+_SIDE_STREAMS = {}
+_SIDE_PENDING = []
+_SIDE_JOIN_QUEUED = [False]
+
+
+def _side_ok(t: torch.Tensor, *dtypes) -> bool:
+    if not (SIDE_WGRAD and t.is_cuda) or any(d not in (None, torch.float32) for d in dtypes):
+        return False
+    dist = torch.distributed
+    return not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1)
+
+
+def join_side_streams():
+    """Make each launching stream wait for the side-stream weight gradients it forked."""
+    for main, ev in _SIDE_PENDING:
+        main.wait_event(ev)
+    _SIDE_PENDING.clear()
+    _SIDE_JOIN_QUEUED[0] = False
+
+
+def _side_run(fn, *inputs):
+    dev = inputs[0].device
+    main = torch.cuda.current_stream(dev)
+    side = _SIDE_STREAMS.get(dev)
+    if side is None:
+        side = _SIDE_STREAMS[dev] = torch.cuda.Stream(dev)
+    side.wait_stream(main)
+    with torch.cuda.stream(side):
+        out = fn()
+    for t in inputs:
+        t.record_stream(side)
+    ev = torch.cuda.Event()
+    ev.record(side)
+    _SIDE_PENDING.append((main, ev))
+    if not _SIDE_JOIN_QUEUED[0]:
+        torch.autograd.Variable._execution_engine.queue_callback(join_side_streams)
+        _SIDE_JOIN_QUEUED[0] = True
+    return out
+
+
+def wgrad_maybe_side(dy2: torch.Tensor, x2: torch.Tensor, wdt, bdt):
+    """linear_wgrad on the side stream when allowed (fp32 master weights), else inline."""
+    if _side_ok(dy2, wdt, bdt):
+        return _side_run(lambda: linear_wgrad(dy2, x2), dy2, x2)
+    return linear_wgrad(dy2, x2)
+
+
 def linear_wgrad_gelu(dy2: torch.Tensor, h2: torch.Tensor):
     """(dW, db) of a Linear whose input is gelu(h2), with gelu applied on the fly (bf16)."""
     M, N = dy2.shape
@@ -366,7 +425,6 @@ def linear_wgrad_gelu(dy2: torch.Tensor, h2: torch.Tensor):
     return out[:N * K].view(N, K), out[N * K:]
 
 
-import os as _os
 
 # csu_gemm_ex (fused bias / GELU / GELU' / residual token GEMM) for the bf16 nn.Linear forward and
 # input-gradient GEMMs; CSU_FUSED_GEMM=0 falls back to torch.matmul (hipBLASLt) for A/B checks.
@@ -428,7 +486,8 @@ class _LinearFn(torch.autograd.Function):
                 dx = dx.to(xdt)
         vec = 16 // dy2.element_size()
         if N % vec == 0 and K % vec == 0 and dy2.dtype in (torch.float32, torch.bfloat16):
-            dwf, dbf = linear_wgrad(dy2, xc.reshape(-1, K))
+            dwf, dbf = wgrad_maybe_side(dy2, xc.reshape(-1, K), wdt if ctx.needs_input_grad[1] else None,
+                                        bdt if ctx.needs_input_grad[2] else None)
             if ctx.needs_input_grad[1]:
                 dw = dwf.to(wdt)
             if bdt is not None and ctx.needs_input_grad[2]:
@@ -459,7 +518,7 @@ class _LinearResidualFn(torch.autograd.Function):
         rdt, xshape, wdt, bdt = ctx.meta
         dyb = dy.reshape(-1, dy.shape[-1]).to(torch.bfloat16).contiguous()
         dx = gemm(dyb, wt, False, torch.bfloat16).view(xshape)
-        dw, db = linear_wgrad(dyb, x2)
+        dw, db = wgrad_maybe_side(dyb, x2, wdt, bdt)
         return dy.to(rdt), dx, dw.to(wdt), db.to(bdt), None
 
 
@@ -484,9 +543,9 @@ class _MlpResidualFn(torch.autograd.Function):
         rdt, xshape, w1dt, b1dt, w2dt, b2dt = ctx.meta
         dyb = dy.reshape(-1, dy.shape[-1]).to(torch.bfloat16).contiguous()
         dh = gemm(dyb, w2t, False, torch.bfloat16, gelu_aux=h)         # (dY W2) * gelu'(h)
-        dw2, db2 = linear_wgrad(dyb, g)
+        dw2, db2 = wgrad_maybe_side(dyb, g, w2dt, b2dt)
         dx = gemm(dh, w1t, False, torch.bfloat16).view(xshape)
-        dw1, db1 = linear_wgrad(dh, x2)
+        dw1, db1 = wgrad_maybe_side(dh, x2, w1dt, b1dt)
         return dy.to(rdt), dx, dw1.to(w1dt), db1.to(b1dt), dw2.to(w2dt), db2.to(b2dt), None, None
 
 
