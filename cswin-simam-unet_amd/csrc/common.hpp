@@ -82,6 +82,63 @@ __device__ __forceinline__ constexpr int crow(int reg, int h) { return (reg & 3)
 size_t colsum_workspace(long rows, long cols, int dtype);
 int colsum_launch(long rows, long cols, int dtype, const void* in, float* out, float* ws, hipStream_t st);
 
+// XCD-aware tile order.  Workgroups are dispatched round-robin over the 8 XCDs (workgroup id i
+// runs on XCD i % 8), each with its own L2.  Remap the hardware id so that XCD x walks a
+// contiguous range of logical tiles: tiles that share an operand panel (consecutive logical ids)
+// then run concurrently on one XCD and the panel is fetched from HBM once into that XCD's L2.
+constexpr int kXcds = 8;
+__device__ __forceinline__ long xcd_tile(long id, long total) {
+    const long q = total / kXcds, rem = total % kXcds;
+    const long x = id % kXcds, k = id / kXcds;
+    return x < rem ? x * (q + 1) + k : rem * (q + 1) + (x - rem) * q + k;
+}
+
+// ---- raw buffer access: out-of-range offsets are dropped (stores) / read as 0 (loads) by the
+// hardware, so bounds checks need no branches (a branch around a store makes hipcc wait
+// vmcnt(0) at the join, serialising an epilogue's stores).
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+constexpr unsigned kOOB = 0x80000000u;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, long bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)(bytes < 0x7fffffffL ? bytes : 0x7fffffffL),
+                                             0x00020000);
+}
+__device__ __forceinline__ void buf_st4(__amdgpu_buffer_rsrc_t rs, unsigned off, const float* v) {   // 4 x f32
+    u32x4 x = {__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])};
+    __builtin_amdgcn_raw_buffer_store_b128(x, rs, off, 0, 0);
+}
+__device__ __forceinline__ void buf_st4bf(__amdgpu_buffer_rsrc_t rs, unsigned off, const float* v) {   // 4 x bf16
+    bf16x4 b = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+    u32x2 x;
+    __builtin_memcpy(&x, &b, 8);
+    __builtin_amdgcn_raw_buffer_store_b64(x, rs, off, 0, 0);
+}
+__device__ __forceinline__ void buf_st8bf(__amdgpu_buffer_rsrc_t rs, unsigned off, const float* v) {   // 8 x bf16
+    bf16x8 b;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) b[e] = (bf16)v[e];
+    u32x4 x;
+    __builtin_memcpy(&x, &b, 16);
+    __builtin_amdgcn_raw_buffer_store_b128(x, rs, off, 0, 0);
+}
+__device__ __forceinline__ void buf_ld8bf(__amdgpu_buffer_rsrc_t rs, unsigned off, float* v) {
+    const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+    bf16x8 b;
+    __builtin_memcpy(&b, &x, 16);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = (float)b[e];
+}
+__device__ __forceinline__ void buf_ld4(__amdgpu_buffer_rsrc_t rs, unsigned off, float* v) {
+    const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+    v[0] = __uint_as_float(x[0]); v[1] = __uint_as_float(x[1]); v[2] = __uint_as_float(x[2]); v[3] = __uint_as_float(x[3]);
+}
+__device__ __forceinline__ void buf_ld4bf(__amdgpu_buffer_rsrc_t rs, unsigned off, float* v) {
+    const u32x2 x = __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, 0);
+    bf16x4 b;
+    __builtin_memcpy(&b, &x, 8);
+    v[0] = (float)b[0]; v[1] = (float)b[1]; v[2] = (float)b[2]; v[3] = (float)b[3];
+}
+
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 }  // namespace csu

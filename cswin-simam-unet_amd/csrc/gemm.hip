@@ -218,8 +218,10 @@ __global__ __launch_bounds__(NT) void gemm3_kernel(long M, int N, int K, const b
     __shared__ __attribute__((aligned(16))) bf16 smem[LDS];
     bf16* As = smem;                       // [STG][BM * 64]
     bf16* Bs = smem + STG * BM * BK3;      // [STG][BN * 64]
-    const long m0 = (long)blockIdx.x * BM;
-    const int n0 = blockIdx.y * BN;
+    const int nbn = (N + BN - 1) / BN;     // n fastest: the N tiles of one A panel share an XCD's L2
+    const long t = xcd_tile(blockIdx.x, gridDim.x);
+    const long m0 = (t / nbn) * BM;
+    const int n0 = (int)(t % nbn) * BN;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int r = lane & 31, h = lane >> 5;
     const int wm = (wave >> 1) * HB, wn = (wave & 1) * (BN / 2);
@@ -353,7 +355,7 @@ __global__ __launch_bounds__(NT) void gemm3_kernel(long M, int N, int K, const b
 template <int BM, int BN, int STG, bool GA>
 int launch3_s(long M, int N, int K, const bf16* A, int lda, const bf16* B, int ldb, const float* bias, const bf16* gaux,
               const float* resid, void* out, bf16* gout, int ldc, int odt, hipStream_t st) {
-    const dim3 grid((unsigned)((M + BM - 1) / BM), (N + BN - 1) / BN);
+    const dim3 grid((unsigned)(((M + BM - 1) / BM) * ((N + BN - 1) / BN)));
     if (odt == CSU_BF16)
         gemm3_kernel<BM, BN, STG, GA, bf16><<<grid, NT, 0, st>>>(M, N, K, A, lda, B, ldb, bias, gaux, resid, (bf16*)out, gout, ldc);
     else
@@ -393,6 +395,9 @@ int launch3(int cfg, long M, int N, int K, const bf16* A, int lda, const bf16* B
 }
 
 }  // namespace
+
+int gemm4_run(int cfg, int epi, int odt, long M, int N, int K, const bf16* A, int lda, const bf16* W, int ldw,
+              const float* bias, const bf16* gaux, const float* resid, void* out, bf16* gout, int ldc, hipStream_t st);
 }  // namespace csu
 
 using namespace csu;
@@ -428,6 +433,17 @@ extern "C" int csu_gemm_ex(const csu_gemm_desc* d, void* stream) {
     const bf16* A = (const bf16*)d->a;
     const bf16* B = (const bf16*)d->b;
     const bf16* g = (const bf16*)d->gelu_aux;
+    // gemm4 (LDS-DMA staging, register epilogue): weight (N, K) operand, K % 64 == 0, no GELU prologue.
+    // cfg -1 = auto, 10..15 force a gemm4 configuration, 0..3 force a gemm3 tile.
+    const bool g4_ok = !b_trans && !a_gelu && K % 64 == 0 && N % 8 == 0 && M * (long)lda < (1L << 30) && (long)N * ldb < (1L << 30) && ldc % 8 == 0 &&
+                       !(d->gelu_out && out_dtype != CSU_BF16) && !(d->gelu_aux && d->gelu_out) &&
+                       !(resid && (d->gelu_aux || d->gelu_out));
+    if (g4_ok && (cfg < 0 || cfg >= 10)) {
+        const int epi = d->gelu_out ? 1 : d->gelu_aux ? 2 : resid ? 3 : 0;
+        return gemm4_run(cfg < 0 ? -1 : cfg - 10, epi, out_dtype, M, N, K, A, lda, B, ldb, bias, g, resid, out,
+                         (bf16*)d->gelu_out, ldc, st);
+    }
+    if (cfg >= 10) cfg = -1;
     if (!b_trans && N % 8 == 0 && ldc % 8 == 0) {
         if (cfg < 0 || cfg > 3) cfg = pick_cfg(M, N, d->gelu_out || d->gelu_aux || resid);
         return launch3(cfg, M, N, K, A, lda, B, ldb, bias, g, resid, out, (bf16*)d->gelu_out, ldc, out_dtype,

@@ -1,0 +1,363 @@
+// gemm4: token GEMM for gfx950 with LDS-DMA operand staging and a register epilogue.
+//
+//   out[m][n] = epi( sum_k A[m][k] * W[n][k] )      A (M, K) tokens, W (N, K) nn.Linear weight
+//
+// The nn.Linear forward / input-gradient GEMMs of CSWinBlock / Mlp (cswin:185-195, 314-368) and
+// concat_linear (cswin:568-592) with bias / GELU / GELU' / residual fused into the epilogue.
+//
+// Design (MI355X):
+//  * 256 threads = 4 waves in 2 x 2, tile BM x BN in {64,128}^2, BK = 64.
+//  * Both operands go global -> LDS by global_load_lds_dwordx4 (no VGPR round trip): one wave
+//    instruction fills 8 rows x 128 B of a [rows][64] bf16 image whose 16-B chunks are XOR-swizzled
+//    by (row & 7) -- the swizzle is applied to the per-lane SOURCE address (the DMA destination is
+//    lane-linear) and to the fragment reads, so ds_read_b128 fragment reads are conflict-free.
+//  * Two LDS stages; the next K slice's DMA stays in flight across the barrier (counted vmcnt,
+//    raw s_barrier), so a workgroup overlaps its own loads with its MFMAs.
+//  * v_mfma_f32_32x32x16_bf16 with the WEIGHT fragment as the A operand: the accumulator of lane
+//    (r, h) holds token r and features crow(reg, h) = 4 consecutive features per register group,
+//    so the epilogue reads bias / GELU-aux / residual and writes outputs as 4-wide vectors
+//    straight from registers (no LDS staging, no barriers).
+//  * XCD-aware tile order (xcd_tile): the N tiles of one token panel run on one XCD's L2.
+#include "common.hpp"
+
+namespace csu {
+namespace {
+
+constexpr int G4_NT = 256;
+constexpr int G4_BK = 64;
+
+
+enum { G4_PLAIN = 0, G4_GELU_OUT = 1, G4_GAUX = 2, G4_RESID = 3 };
+
+// element offset of 16-B chunk `chunk` of row `row` in a swizzled [rows][64] bf16 image
+__device__ __forceinline__ int g4_off(int row, int chunk) { return row * G4_BK + ((chunk ^ (row & 7)) << 3); }
+
+// erf(|x|/sqrt2) by Abramowitz-Stegun 7.1.26 (|abs err| < 1.5e-7)
+__device__ __forceinline__ float g4_erf(float z) {   // z >= 0
+    const float t = __frcp_rn(1.f + 0.3275911f * z);
+    const float p = t * (0.254829592f + t * (-0.284496736f + t * (1.421413741f + t * (-1.453152027f + t * 1.061405429f))));
+    return 1.f - p * __expf(-z * z);
+}
+__device__ __forceinline__ float g4_gelu(float x) {
+    const float e = g4_erf(fabsf(x) * 0.70710678118654752f);
+    return 0.5f * x * (1.f + (x >= 0.f ? e : -e));
+}
+__device__ __forceinline__ float g4_gelu_grad(float x) {
+    const float e = g4_erf(fabsf(x) * 0.70710678118654752f);
+    return 0.5f * (1.f + (x >= 0.f ? e : -e)) + x * 0.3989422804014327f * __expf(-0.5f * x * x);
+}
+
+// Per-lane byte offsets of the DMA of a ROWS x 64 bf16 slice (rows 0.., k 0..63 relative to the
+// slice origin) of a row-major matrix with leading dimension ld into a swizzled [ROWS][64] image:
+// wave instruction i of this wave fills image rows rb..rb+7 (rb = (wave * ROWS/32 + i) * 8), lane l
+// row rb + l/8, 16-B chunk (l & 7) ^ (row & 7).  Constant for the whole kernel.
+template <int ROWS>
+__device__ __forceinline__ void g4_voff(int ld, int wave, int lane, unsigned* voff) {
+#pragma unroll
+    for (int i = 0; i < ROWS / 32; ++i) {
+        const int row = (wave * (ROWS / 32) + i) * 8 + (lane >> 3);
+        voff[i] = (unsigned)row * ld * 2 + (((lane & 7) ^ (row & 7)) << 4);
+    }
+}
+
+// DMA the slice: raw buffer loads to LDS from a resource whose base is the slice's first row and
+// whose size ends at the matrix's last row, so rows past the end read as 0 (hardware range check);
+// soff = the k offset in bytes (scalar).  Only scalar work per call: the lane offsets are fixed.
+template <int ROWS>
+__device__ __forceinline__ void g4_dma(__amdgpu_buffer_rsrc_t rs, const unsigned* voff, unsigned soff, bf16* img,
+                                       int wave) {
+#pragma unroll
+    for (int i = 0; i < ROWS / 32; ++i)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(img + (wave * (ROWS / 32) + i) * 8 * G4_BK),
+                                                 16, voff[i], soff, 0, 0);
+}
+
+template <int N> __device__ __forceinline__ void g4_vmwait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+
+template <typename T> struct V4;
+template <> struct V4<float> {
+    static __device__ __forceinline__ void ld(const float* p, float* v) { load4(p, v); }
+    static __device__ __forceinline__ void st(float* p, const float* v) { store4(p, v); }
+};
+template <> struct V4<bf16> {
+    static __device__ __forceinline__ void ld(const bf16* p, float* v) { load4(p, v); }
+    static __device__ __forceinline__ void st(bf16* p, const float* v) { store4(p, v); }
+};
+
+// s_waitcnt vmcnt(k) for the largest multiple of 8 <= c (waiting for more than needed is safe)
+__device__ __forceinline__ void g4_vmwait_floor(int c) {
+    switch (c >= 63 ? 7 : c >> 3) {
+        case 0: g4_vmwait<0>(); break;
+        case 1: g4_vmwait<8>(); break;
+        case 2: g4_vmwait<16>(); break;
+        case 3: g4_vmwait<24>(); break;
+        case 4: g4_vmwait<32>(); break;
+        case 5: g4_vmwait<40>(); break;
+        case 6: g4_vmwait<48>(); break;
+        default: g4_vmwait<56>(); break;
+    }
+}
+
+// Persistent workgroups, S-stage LDS ring.  A workgroup walks its tiles' K slices as one stream of
+// "units" (tile, k-slice); the DMA of unit u + S - 1 is issued while unit u is multiplied, so the
+// loads of the next tile overlap the last slices and the epilogue of the current one.
+// vmcnt counts every vector-memory op of a wave in issue order (DMA, loads, stores), so the wait for
+// unit u counts exactly the ops issued after its DMA.  Every step issues exactly D DMA ops (past
+// the last unit it re-fetches the last unit into the free stage), and a tile's last step issues
+// its L epilogue loads BEFORE its DMA (so waiting for them does not wait for the prefetch) and its
+// ST stores after the MFMAs.
+template <int BM, int BN, int S, int OCC, int EPI, typename TOUT>
+__global__ __launch_bounds__(G4_NT, OCC) void gemm4_kernel(long M, int N, int K, const bf16* __restrict__ A, int lda,
+                                                           const bf16* __restrict__ W, int ldw, const float* __restrict__ bias,
+                                                           const bf16* __restrict__ gaux, const float* __restrict__ resid,
+                                                           TOUT* __restrict__ out, bf16* __restrict__ gout, int ldc) {
+    constexpr int TMW = BM / 64, TNW = BN / 64;      // 32x32 tiles per wave (tokens, features)
+    constexpr int STAGE = (BM + BN) * G4_BK;         // bf16 elements per stage
+    constexpr int D = (BM + BN) / 32;                // DMA instructions per wave per unit
+    constexpr int P = S - 1;                         // units in flight ahead of the one multiplied
+    constexpr bool PRE = EPI == G4_GAUX || EPI == G4_RESID;
+    // epilogue: each wave transposes its (BM/2) x WC accumulator tile through its own fp32 LDS
+    // region, 32 token rows per pass, and then reads/writes whole 8-feature row chunks (16/32-B
+    // vectors, consecutive lanes along a row): row-contiguous loads and stores.
+    constexpr int WC = BN / 2;                       // features per wave
+    constexpr int CPR = WC / 8;                      // 8-feature chunks per row
+    constexpr int RPS = 64 / CPR;                    // rows per wave instruction
+    constexpr int Q = 32 / RPS;                      // instructions per 32-row pass
+    constexpr int ERS = WC + 4;                      // fp32 row stride of the transposition region
+    constexpr int OS = sizeof(TOUT);
+    constexpr int L = 2 + (EPI == G4_RESID ? 2 : EPI == G4_GAUX ? 1 : 0) * TMW * Q;   // epilogue loads per wave
+    constexpr int ST = TMW * Q * ((OS == 4 ? 2 : 1) + (EPI == G4_GELU_OUT ? 1 : 0));   // epilogue stores per wave
+    constexpr int EPB = 32 * ERS * 4;                // bytes per wave
+    __shared__ __attribute__((aligned(1024))) bf16 smem[S * STAGE + 4 * EPB / 2];
+    const unsigned nbn = (N + BN - 1) / BN;
+    const unsigned T = (unsigned)((M + BM - 1) / BM) * nbn;
+    // tiles of this workgroup: its XCD's contiguous tile range, strided by the XCD's workgroups
+    const unsigned x = blockIdx.x % kXcds, kk = blockIdx.x / kXcds, nloc = gridDim.x / kXcds;
+    const unsigned q = T / kXcds, rem = T % kXcds;
+    const unsigned lo = x < rem ? x * (q + 1) : rem * (q + 1) + (x - rem) * q;
+    const unsigned cnt = q + (x < rem ? 1 : 0);
+    const int mytiles = kk < cnt ? (int)((cnt - kk + nloc - 1) / nloc) : 0;
+    if (mytiles == 0) return;
+    const int nk = K / G4_BK;
+    const int U = mytiles * nk;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int r = lane & 31, h = lane >> 5;
+    const int wm = (wave >> 1) * (BM / 2), wn = (wave & 1) * (BN / 2);
+
+    unsigned voffA[BM / 32], voffW[BN / 32];
+    g4_voff<BM>(lda, wave, lane, voffA);
+    g4_voff<BN>(ldw, wave, lane, voffW);
+    auto issue = [&](int u) {   // DMA of unit min(u, U - 1) into stage u % S
+        const int uu = u < U ? u : U - 1;
+        const unsigned tile = lo + kk + (unsigned)(uu / nk) * nloc;
+        const unsigned soff = (unsigned)(uu % nk) * G4_BK * 2;
+        bf16* st = smem + (u % S) * STAGE;
+        const long ra = (long)(tile / nbn) * BM, rw = (long)(tile % nbn) * BN;
+        g4_dma<BM>(buf_rsrc(A + ra * lda, (M - ra) * lda * 2), voffA, soff, st, wave);
+        g4_dma<BN>(buf_rsrc(W + rw * ldw, (N - rw) * ldw * 2), voffW, soff, st + BM * G4_BK, wave);
+    };
+    auto wait_unit = [&](int u) {   // vector-memory ops issued after unit u's DMA (issued at step u - P)
+        const int w = u - P;
+        int c = (w >= 0 && w % nk == nk - 1) ? ST : 0;
+        for (int v = w + 1; v < u; ++v) c += D + ((v >= 0 && v % nk == nk - 1) ? L + ST : 0);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        g4_vmwait_floor(c);
+        __builtin_amdgcn_s_barrier();   // unit u landed for every wave; stage (u-1)%S is free
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    f32x16 acc[TMW][TNW];
+#pragma unroll
+    for (int i = 0; i < TMW; ++i)
+#pragma unroll
+        for (int j = 0; j < TNW; ++j) acc[i][j] = f32x16{};
+    auto mma = [&](int u) {
+        const bf16* As = smem + (u % S) * STAGE;
+        const bf16* Ws = As + BM * G4_BK;
+        // fragments of k-step s + 1 are read while the MFMAs of step s run
+        bf16x8 af[2][TMW], wf[2][TNW];
+        auto frags = [&](int s, int b) {
+#pragma unroll
+            for (int i = 0; i < TMW; ++i) af[b][i] = *reinterpret_cast<const bf16x8*>(As + g4_off(wm + 32 * i + r, 2 * s + h));
+#pragma unroll
+            for (int j = 0; j < TNW; ++j) wf[b][j] = *reinterpret_cast<const bf16x8*>(Ws + g4_off(wn + 32 * j + r, 2 * s + h));
+        };
+        frags(0, 0);
+#pragma unroll
+        for (int s = 0; s < G4_BK / 16; ++s) {
+            if (s + 1 < G4_BK / 16) frags(s + 1, (s + 1) & 1);
+#pragma unroll
+            for (int i = 0; i < TMW; ++i)
+#pragma unroll
+                for (int j = 0; j < TNW; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[s & 1][j], af[s & 1][i], acc[i][j], 0, 0, 0);
+        }
+    };
+
+#pragma unroll
+    for (int p = 0; p < P; ++p) issue(p);
+    int u = 0;
+    for (int t = 0; t < mytiles; ++t) {
+        for (int ks = 0; ks + 1 < nk; ++ks, ++u) {   // all but the tile's last K slice
+            wait_unit(u);
+            issue(u + P);
+            mma(u);
+        }
+        // ---- last K slice + epilogue.  acc[i][j][4g + e] = C[wm + 32i + r][wn + 32j + 8g + 4h + e] of the
+        // tile; after the transposition lane l holds row (l / CPR) + RPS q of pass i, features
+        // 8 (l % CPR) .. + 7.  Raw buffer ops relative to the tile's first row; out-of-tile
+        // elements get an out-of-range offset (no branches: see buf_rsrc).
+        wait_unit(u);
+        const unsigned tile = lo + kk + (unsigned)t * nloc;
+        const long m0 = (long)(tile / nbn) * BM;
+        const int n0 = (int)(tile % nbn) * BN;
+        const long rows = M - m0 < BM ? M - m0 : BM;
+        const int c8 = lane % CPR, rr = lane / CPR;
+        const int n = n0 + wn + 8 * c8;
+        unsigned off[TMW][Q];   // element offsets, kOOB when outside
+#pragma unroll
+        for (int i = 0; i < TMW; ++i)
+#pragma unroll
+            for (int q = 0; q < Q; ++q) {
+                const int ml = wm + 32 * i + RPS * q + rr;
+                off[i][q] = (ml < rows && n < N) ? (unsigned)(ml * ldc + n) : kOOB;
+            }
+        float bv[8];
+        const auto rs_b = buf_rsrc(bias, bias ? (long)N * 4 : 0);   // null bias: every load reads 0
+        buf_ld4(rs_b, n < N ? (unsigned)n * 4 : kOOB, bv);
+        buf_ld4(rs_b, n < N ? (unsigned)n * 4 + 16 : kOOB, bv + 4);
+        float pre[TMW][Q][8];
+        if constexpr (PRE) {
+            const auto rs_pre = EPI == G4_GAUX ? buf_rsrc(gaux + m0 * ldc, rows * ldc * 2) : buf_rsrc(resid + m0 * ldc, rows * ldc * 4);
+#pragma unroll
+            for (int i = 0; i < TMW; ++i)
+#pragma unroll
+                for (int q = 0; q < Q; ++q) {
+                    const unsigned o = off[i][q];
+                    if constexpr (EPI == G4_GAUX) {
+                        buf_ld8bf(rs_pre, o == kOOB ? kOOB : o * 2, pre[i][q]);
+                    } else {
+                        buf_ld4(rs_pre, o == kOOB ? kOOB : o * 4, pre[i][q]);
+                        buf_ld4(rs_pre, o == kOOB ? kOOB : o * 4 + 16, pre[i][q] + 4);
+                    }
+                }
+        }
+        asm volatile("" ::: "memory");      // keep the epilogue loads ahead of the next DMA (vmcnt order)
+        __builtin_amdgcn_sched_barrier(0);
+        issue(u + P);
+        mma(u);
+        const auto rs_out = buf_rsrc(out + m0 * ldc, rows * ldc * OS);
+        const auto rs_g = buf_rsrc(gout ? gout + m0 * ldc : nullptr, gout ? rows * ldc * 2 : 0);
+        float* ep = reinterpret_cast<float*>(smem + S * STAGE) + wave * (EPB / 4);
+#pragma unroll
+        for (int i = 0; i < TMW; ++i) {
+#pragma unroll
+            for (int j = 0; j < TNW; ++j)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const f32x4 v = {acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]};
+                    *reinterpret_cast<f32x4*>(ep + r * ERS + 32 * j + 8 * g + 4 * h) = v;
+                }
+            asm volatile("" ::: "memory");  // the wave's own LDS writes, then its reads (in order per wave)
+#pragma unroll
+            for (int q = 0; q < Q; ++q) {
+                const float* src = ep + (RPS * q + rr) * ERS + 8 * c8;
+                const f32x4 lo4 = *reinterpret_cast<const f32x4*>(src);
+                const f32x4 hi4 = *reinterpret_cast<const f32x4*>(src + 4);
+                float v[8];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    v[e] = lo4[e] + bv[e];
+                    v[e + 4] = hi4[e] + bv[e + 4];
+                }
+                if constexpr (EPI == G4_GAUX) {
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) v[e] *= g4_gelu_grad(pre[i][q][e]);
+                } else if constexpr (EPI == G4_RESID) {
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) v[e] += pre[i][q][e];
+                }
+                const unsigned o = off[i][q];
+                if constexpr (OS == 4) {
+                    buf_st4(rs_out, o == kOOB ? kOOB : o * 4, v);
+                    buf_st4(rs_out, o == kOOB ? kOOB : o * 4 + 16, v + 4);
+                } else {
+                    buf_st8bf(rs_out, o == kOOB ? kOOB : o * 2, v);
+                }
+                if constexpr (EPI == G4_GELU_OUT) {
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) v[e] = g4_gelu(v[e]);
+                    buf_st8bf(rs_g, o == kOOB ? kOOB : o * 2, v);
+                }
+            }
+            asm volatile("" ::: "memory");
+        }
+#pragma unroll
+        for (int i = 0; i < TMW; ++i)
+#pragma unroll
+            for (int j = 0; j < TNW; ++j) acc[i][j] = f32x16{};
+        ++u;
+    }
+    g4_vmwait<0>();   // drain the re-fetch DMAs before the workgroup's LDS is released
+}
+
+struct G4Cfg { int bm, bn, s, occ; };
+constexpr G4Cfg kG4Cfgs[] = {{64, 64, 3, 2}, {128, 64, 2, 2}, {128, 128, 2, 1}, {128, 128, 3, 1}, {64, 128, 2, 1},
+                             {128, 64, 3, 1}};
+constexpr int kG4NCfg = 6;
+
+int g4_grid(int occ) {
+    static int cus = 0;
+    if (!cus) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            cus = 256;
+        cus = (cus + kXcds - 1) / kXcds * kXcds;
+    }
+    return cus * occ;
+}
+
+template <int BM, int BN, int S, int OCC, int EPI, typename TOUT>
+int g4_launch(long M, int N, int K, const bf16* A, int lda, const bf16* W, int ldw, const float* bias, const bf16* gaux,
+              const float* resid, void* out, bf16* gout, int ldc, hipStream_t st) {
+    gemm4_kernel<BM, BN, S, OCC, EPI, TOUT><<<dim3(g4_grid(OCC)), G4_NT, 0, st>>>(M, N, K, A, lda, W, ldw, bias, gaux, resid,
+                                                                                 (TOUT*)out, gout, ldc);
+    return check_launch("gemm4");
+}
+
+template <int C>
+int g4_epi(int epi, int odt, long M, int N, int K, const bf16* A, int lda, const bf16* W, int ldw, const float* bias,
+           const bf16* gaux, const float* resid, void* out, bf16* gout, int ldc, hipStream_t st) {
+    constexpr int BM = kG4Cfgs[C].bm, BN = kG4Cfgs[C].bn, S = kG4Cfgs[C].s, O = kG4Cfgs[C].occ;
+    switch (epi) {
+        case G4_GELU_OUT: return g4_launch<BM, BN, S, O, G4_GELU_OUT, bf16>(M, N, K, A, lda, W, ldw, bias, gaux, resid, out, gout, ldc, st);
+        case G4_GAUX:
+            if (odt == CSU_F32) return g4_launch<BM, BN, S, O, G4_GAUX, float>(M, N, K, A, lda, W, ldw, bias, gaux, resid, out, gout, ldc, st);
+            return g4_launch<BM, BN, S, O, G4_GAUX, bf16>(M, N, K, A, lda, W, ldw, bias, gaux, resid, out, gout, ldc, st);
+        case G4_RESID: return g4_launch<BM, BN, S, O, G4_RESID, float>(M, N, K, A, lda, W, ldw, bias, gaux, resid, out, gout, ldc, st);
+        default:
+            if (odt == CSU_F32) return g4_launch<BM, BN, S, O, G4_PLAIN, float>(M, N, K, A, lda, W, ldw, bias, gaux, resid, out, gout, ldc, st);
+            return g4_launch<BM, BN, S, O, G4_PLAIN, bf16>(M, N, K, A, lda, W, ldw, bias, gaux, resid, out, gout, ldc, st);
+    }
+}
+
+}  // namespace
+
+// Tile choice (tools/linear_probe.py, every token-GEMM shape of the 512x512 step): 128 x 64 with a
+// 2-stage ring at 2 workgroups per CU was fastest or within 5 % everywhere.  cfg indexes kG4Cfgs.
+int gemm4_pick(long, int, int) { return 1; }
+
+int gemm4_run(int cfg, int epi, int odt, long M, int N, int K, const bf16* A, int lda, const bf16* W, int ldw,
+              const float* bias, const bf16* gaux, const float* resid, void* out, bf16* gout, int ldc, hipStream_t st) {
+    if (cfg < 0 || cfg >= kG4NCfg) cfg = gemm4_pick(M, N, K);
+    switch (cfg) {
+        case 5: return g4_epi<5>(epi, odt, M, N, K, A, lda, W, ldw, bias, gaux, resid, out, gout, ldc, st);
+        case 4: return g4_epi<4>(epi, odt, M, N, K, A, lda, W, ldw, bias, gaux, resid, out, gout, ldc, st);
+        case 3: return g4_epi<3>(epi, odt, M, N, K, A, lda, W, ldw, bias, gaux, resid, out, gout, ldc, st);
+        case 2: return g4_epi<2>(epi, odt, M, N, K, A, lda, W, ldw, bias, gaux, resid, out, gout, ldc, st);
+        case 1: return g4_epi<1>(epi, odt, M, N, K, A, lda, W, ldw, bias, gaux, resid, out, gout, ldc, st);
+        default: return g4_epi<0>(epi, odt, M, N, K, A, lda, W, ldw, bias, gaux, resid, out, gout, ldc, st);
+    }
+}
+
+}  // namespace csu

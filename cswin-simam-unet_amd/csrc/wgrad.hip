@@ -135,13 +135,17 @@ __global__ __launch_bounds__(NT) void wgrad_bf16_tr(long M, int N, int K, long r
     __shared__ __attribute__((aligned(16))) bf16 At[TM * RS];   // dY tile [m][n]
     __shared__ __attribute__((aligned(16))) bf16 Bt[TM * RS];   // X  tile [m][k]
     __shared__ float bred[NT][9];
-    const int n0 = blockIdx.x * TN, k0 = blockIdx.y * TK;
-    const long m_begin = (long)blockIdx.z * rows_per_chunk;
+    // tiles of one token chunk are consecutive logical ids -> one XCD reads the chunk once
+    const int nt = (N + TN - 1) / TN, kt = (K + TK - 1) / TK;
+    const long t = xcd_tile(blockIdx.x, gridDim.x);
+    const int chunk = (int)(t / (nt * kt)), tt = (int)(t % (nt * kt));
+    const int n0 = (tt / kt) * TN, k0 = (tt % kt) * TK;
+    const long m_begin = (long)chunk * rows_per_chunk;
     const long m_end = min(M, m_begin + rows_per_chunk);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int r = lane & 31, h = lane >> 5;
     const int wn = (wave >> 1) * 32, wk = (wave & 1) * 32;
-    const bool do_bias = blockIdx.y == 0;
+    const bool do_bias = k0 == 0;
     // this thread's two 16-B chunks per operand: chunk c = tid + 256 i -> row c / 8, column group c % 8
     const int cg = threadIdx.x & 7, rr = threadIdx.x >> 3;   // rows rr and rr + 32
     const bool nv = n0 + 8 * cg < N, kv = k0 + 8 * cg < K;
@@ -183,7 +187,7 @@ __global__ __launch_bounds__(NT) void wgrad_bf16_tr(long M, int N, int K, long r
         }
     }
     const long slab = (long)N * K + N;
-    float* out = part + (long)blockIdx.z * slab;
+    float* out = part + (long)chunk * slab;
 #pragma unroll
     for (int reg = 0; reg < 16; ++reg) {
         const int n = n0 + wn + crow(reg, h), k = k0 + wk + r;
@@ -253,10 +257,11 @@ extern "C" int csu_linear_wgrad_ex(long M, int N, int K, int dtype, const void* 
     const long slab = (long)N * K + N;
     const dim3 grid(p.nt, p.kt, p.chunks);
     if (x_gelu && dtype != CSU_BF16) return fail(CSU_E_UNSUPPORTED, "linear_wgrad: GELU prologue is bf16-only");
+    const dim3 grid1((unsigned)(p.nt * p.kt * p.chunks));
     if (dtype == CSU_BF16 && x_gelu)
-        wgrad_bf16_tr<true><<<grid, NT, 0, st>>>(M, N, K, p.rpc, (const bf16*)dy, (const bf16*)x, part);
+        wgrad_bf16_tr<true><<<grid1, NT, 0, st>>>(M, N, K, p.rpc, (const bf16*)dy, (const bf16*)x, part);
     else if (dtype == CSU_BF16)
-        wgrad_bf16_tr<false><<<grid, NT, 0, st>>>(M, N, K, p.rpc, (const bf16*)dy, (const bf16*)x, part);
+        wgrad_bf16_tr<false><<<grid1, NT, 0, st>>>(M, N, K, p.rpc, (const bf16*)dy, (const bf16*)x, part);
     else if (dtype == CSU_F32)
         wgrad_kernel<float><<<grid, NT, 0, st>>>(M, N, K, p.rpc, (const float*)dy, (const float*)x, part);
     else
