@@ -455,111 +455,124 @@ __global__ __launch_bounds__(NT) void stripe_bwd_dkdv(csu_stripe_args a, const T
 
 // =============================================================================================
 // LePE weight/bias gradient: dW[c][t] = sum_q dout[q][c] * V[q + off(t)][c], db[c] = sum_q dout
-// (window-local zero padding).  Pass 1: one thread = (image row, XS-token run, 4 channels); it
-// walks the run along x keeping a 3x3 register window of V (3 new loads per token instead of 9)
-// and writes per-block partial sums; pass 2 sums the block partials in a fixed order.
+// (window-local zero padding).  Pass 1: grid-stride over (image row, XR-token run) units with a
+// fixed channel quad per thread: each unit issues all its loads at once (V of the 3 x (XR+2)
+// neighbourhood and dout of the XR tokens; clamped addresses and 0/1 masks instead of branches, so
+// the loads stay in flight together), then 40 FMAs per token.  Per-block partials are combined in
+// thread order; pass 2 sums the block partials in a fixed order (deterministic).
 // =============================================================================================
-constexpr int XS = 16;   // tokens per thread run
+constexpr int XR = 4;            // tokens per run
+constexpr int LW_MAXBLK = 512;   // pass-1 blocks per branch
+
+template <typename T> struct Raw4;   // 4 channels as loaded (8 B bf16 / 16 B fp32)
+template <> struct Raw4<bf16> {
+    typedef bf16x4 type;
+    static __device__ __forceinline__ float at(const type& v, int j) { return (float)v[j]; }
+};
+template <> struct Raw4<float> {
+    typedef f32x4 type;
+    static __device__ __forceinline__ float at(const type& v, int j) { return v[j]; }
+};
 
 template <typename T>
-__global__ __launch_bounds__(NT) void lepe_wgrad_partial(csu_stripe_args a, const T* __restrict__ qkv,
+__global__ __launch_bounds__(NT, 4) void lepe_wgrad_partial(csu_stripe_args a, const T* __restrict__ qkv,
                                                          const T* __restrict__ dout, float* __restrict__ part) {
-    __shared__ float red[NT][41];
+    typedef typename Raw4<T>::type R4;
+    __shared__ float red[4][64][11];
     const int br = blockIdx.y;
     const csu_stripe_branch& g = branch(a, br);
-    const int Cb = a.heads * HD, nq = Cb / 4;
+    const int Cb = a.heads * HD, nq = Cb / 4;       // power of two dividing NT (checked by the caller)
     const int reso = a.reso, L = reso * reso, C = a.C, C3 = 3 * C;
-    const int nseg = (reso + XS - 1) / XS;
-    const long items = (long)a.B * reso * nseg * nq;
-    const long it = (long)blockIdx.x * NT + threadIdx.x;
-    float acc[10][4];
+    const int nseg = (reso + XR - 1) / XR;
+    const long runs = (long)a.B * reso * nseg;
+    const int per_blk = NT / nq;
+    const int cq = threadIdx.x % nq;
+    const int c0 = g.ch_off + 4 * cq;
+    float acc[40];   // [k][j]: tap k (9 = bias) x channel j of the quad
 #pragma unroll
-    for (int k = 0; k < 10; ++k)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[k][j] = 0.f;
-    const int cq = (int)(it % nq);
-    if (it < items) {
-        long r = it / nq;
-        const int seg = r % nseg; r /= nseg;
-        const int y = r % reso;
-        const int b = (int)(r / reso);
-        const int c0 = g.ch_off + 4 * cq;
-        const int iy = y % g.H_sp;
+    for (int i = 0; i < 40; ++i) acc[i] = 0.f;
+    for (long ri = (long)blockIdx.x * per_blk + threadIdx.x / nq; ri < runs; ri += (long)gridDim.x * per_blk) {
+        const int seg = (int)(ri % nseg);
+        const long r2 = ri / nseg;
+        const int y = (int)(r2 % reso), b = (int)(r2 / reso);
+        const int x0 = seg * XR, iy = y % g.H_sp;
         const T* vimg = qkv + (size_t)b * L * C3 + 2 * C + c0;
         const T* gimg = dout + (size_t)b * L * C + c0;
-        bool yv[3];
+        R4 vw[3][XR + 2], gv[XR];
+        unsigned mask = 0;   // bit dy*(XR+2)+cx: V neighbour inside the image; bit 30-XR+tx: token inside
 #pragma unroll
-        for (int dy = 0; dy < 3; ++dy) yv[dy] = iy + dy - 1 >= 0 && iy + dy - 1 < g.H_sp;
-        const int x0 = seg * XS, x1 = min(reso, x0 + XS);
-        float win[3][3][4];   // [dy][dx][ch]: V at (y+dy-1, x+dx-1)
+        for (int dy = 0; dy < 3; ++dy) {
+            const int yy = y + dy - 1;
+            const bool yok = iy + dy - 1 >= 0 && iy + dy - 1 < g.H_sp;
+            const int yc = min(max(yy, 0), reso - 1);
 #pragma unroll
-        for (int dy = 0; dy < 3; ++dy)
-#pragma unroll
-            for (int dx = 0; dx < 2; ++dx) {
-                const int yy = y + dy - 1, xx = x0 + dx - 1;
-                if (yv[dy] && xx >= 0) load4(vimg + (size_t)(yy * reso + xx) * C3, win[dy][dx + 1]);
-                else win[dy][dx + 1][0] = win[dy][dx + 1][1] = win[dy][dx + 1][2] = win[dy][dx + 1][3] = 0.f;
+            for (int cx = 0; cx < XR + 2; ++cx) {
+                const int xx = x0 - 1 + cx;
+                vw[dy][cx] = *reinterpret_cast<const R4*>(vimg + (size_t)(yc * reso + min(max(xx, 0), reso - 1)) * C3);
+                mask |= (yok && xx >= 0 && xx < reso) ? 1u << (dy * (XR + 2) + cx) : 0u;
             }
-        for (int x = x0; x < x1; ++x) {
+        }
 #pragma unroll
-            for (int dy = 0; dy < 3; ++dy) {
+        for (int tx = 0; tx < XR; ++tx)
+            gv[tx] = *reinterpret_cast<const R4*>(gimg + (size_t)(y * reso + min(x0 + tx, reso - 1)) * C);
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    win[dy][0][j] = win[dy][1][j];
-                    win[dy][1][j] = win[dy][2][j];
-                }
-                const int yy = y + dy - 1;
-                if (yv[dy] && x + 1 < reso) load4(vimg + (size_t)(yy * reso + x + 1) * C3, win[dy][2]);
-                else win[dy][2][0] = win[dy][2][1] = win[dy][2][2] = win[dy][2][3] = 0.f;
-            }
-            float gv[4];
-            load4(gimg + (size_t)(y * reso + x) * C, gv);
-            const int ix = x % g.W_sp;
+        for (int tx = 0; tx < XR; ++tx) {
+            const int x = x0 + tx, ix = x % g.W_sp;
+            if (x >= reso) break;
             const float mx[3] = {ix > 0 ? 1.f : 0.f, 1.f, ix + 1 < g.W_sp ? 1.f : 0.f};
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                acc[9][j] += gv[j];
+                const float gj = Raw4<T>::at(gv[tx], j);
+                acc[36 + j] += gj;
 #pragma unroll
                 for (int dy = 0; dy < 3; ++dy)
 #pragma unroll
-                    for (int dx = 0; dx < 3; ++dx) acc[dy * 3 + dx][j] += gv[j] * mx[dx] * win[dy][dx][j];
+                    for (int dx = 0; dx < 3; ++dx) {
+                        const float m = ((mask >> (dy * (XR + 2) + tx + dx)) & 1u) ? mx[dx] : 0.f;
+                        acc[(dy * 3 + dx) * 4 + j] += gj * m * Raw4<T>::at(vw[dy][tx + dx], j);
+                    }
             }
         }
     }
-    // block partial: threads sharing a channel quad are combined in thread order
+    // threads sharing a quad: lanes l ^ (nq, 2nq, ..) inside a wave (fixed xor tree), then the 4
+    // waves through LDS, 10 values per pass
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (int m = nq; m < 64; m <<= 1)
 #pragma unroll
-    for (int k = 0; k < 10; ++k)
+        for (int i = 0; i < 40; ++i) acc[i] += __shfl_xor(acc[i], m, 64);
+    const int slots = nq < 64 ? nq : 64;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) red[threadIdx.x][k * 4 + j] = acc[k][j];
-    __syncthreads();
-    const int per = NT < nq ? 1 : NT / nq;          // threads per channel quad in this block
-    const int base_q = (int)(((long)blockIdx.x * NT) % nq);
-    for (int o = threadIdx.x; o < min(nq, NT) * 40; o += NT) {
-        const int ql = o / 40, kj = o % 40;          // local quad slot, (k, j)
-        float s = 0.f;
-        for (int m = 0; m < per; ++m) {
-            const int t = ql + m * min(nq, NT);
-            if (t < NT) s += red[t][kj];
+    for (int p = 0; p < 4; ++p) {
+        if (lane < slots)
+#pragma unroll
+            for (int e = 0; e < 10; ++e) red[wave][lane][e] = acc[p * 10 + e];
+        __syncthreads();
+        for (int o = threadIdx.x; o < nq * 10; o += NT) {
+            const int q = o / 10, e = o % 10, l = q % 64;
+            float sum = 0.f;
+#pragma unroll
+            for (int w = 0; w < 4; ++w)
+                if ((w * 64 + l) % nq == q) sum += red[w][l][e];
+            const int kj = p * 10 + e, k = kj >> 2, c = 4 * q + (kj & 3);
+            part[((size_t)br * Cb * 10 + c * 10 + k) * gridDim.x + blockIdx.x] = sum;   // [branch][value][block]
         }
-        const int q = (base_q + ql) % nq;
-        const int c = 4 * q + (kj & 3), k = kj >> 2;
-        part[(((size_t)br * gridDim.x + blockIdx.x) * Cb + c) * 10 + k] = s;
+        __syncthreads();
     }
 }
 
+// one wave per (branch, value): lanes stride over the block partials (contiguous), then a fixed
+// xor-shuffle tree -- deterministic
 __global__ __launch_bounds__(256) void lepe_wgrad_reduce(csu_stripe_args a, int nblk, const float* __restrict__ part) {
-    __shared__ float red[8][32];
-    const int br = blockIdx.y;
     const int Cb = a.heads * HD;
-    const int i = blockIdx.x * 32 + (threadIdx.x & 31);   // (c, k) pair
-    const int lane8 = threadIdx.x >> 5;
+    const int v = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (v >= a.nbranch * Cb * 10) return;
+    const float* src = part + (size_t)v * nblk;
     float s = 0.f;
-    if (i < Cb * 10)
-        for (int j = lane8; j < nblk; j += 8) s += part[((size_t)br * nblk + j) * Cb * 10 + i];
-    red[lane8][threadIdx.x & 31] = s;
-    __syncthreads();
-    if (lane8 == 0 && i < Cb * 10) {
-        for (int l = 1; l < 8; ++l) s += red[l][threadIdx.x];
+    for (int j = lane; j < nblk; j += 64) s += src[j];
+    s = wave_sum(s);
+    if (lane == 0) {
+        const int br = v / (Cb * 10), i = v % (Cb * 10);
         const csu_stripe_branch& g = branch(a, br);
         const int c = i / 10, k = i % 10;
         if (k < 9) g.lepe_dw[c * 9 + k] = s;
@@ -568,8 +581,9 @@ __global__ __launch_bounds__(256) void lepe_wgrad_reduce(csu_stripe_args a, int 
 }
 
 int wgrad_blocks(const csu_stripe_args& a) {
-    const long items = (long)a.B * a.reso * ((a.reso + XS - 1) / XS) * (a.heads * HD / 4);
-    return (int)((items + NT - 1) / NT);
+    const long items = (long)a.B * a.reso * ((a.reso + XR - 1) / XR) * (a.heads * HD / 4);
+    const long blk = (items + NT - 1) / NT;
+    return (int)(blk < LW_MAXBLK ? blk : LW_MAXBLK);
 }
 
 // =============================================================================================
@@ -1008,12 +1022,17 @@ extern "C" int csu_stripe_attn_bwd(const csu_stripe_args* a, int dtype, const vo
         if (!a->br[i].lepe_dw || !a->br[i].lepe_db) return fail(CSU_E_ARG, "stripe_attn_bwd: null LePE grads");
     if (workspace_bytes < csu_stripe_attn_bwd_workspace(a) || !workspace)
         return fail(CSU_E_WORKSPACE, "stripe_attn_bwd: workspace too small");
+    {
+        const int nq = a->heads * HD / 4;   // LePE weight-gradient layout: channel quads per branch
+        if (NT % nq || (nq & (nq - 1)))
+            return fail(CSU_E_UNSUPPORTED, "stripe_attn_bwd: heads per branch must be a power of two <= 32");
+    }
     hipStream_t st = as_stream(stream);
     const dim3 grid = grid_of(*a);
     const int nblk = wgrad_blocks(*a);
     float* part = (float*)workspace;
     const int Cb = a->heads * HD;
-    const dim3 rgrid((Cb * 10 + 31) / 32, a->nbranch);
+    const dim3 rgrid((a->nbranch * Cb * 10 + 3) / 4);
     if (use_window_path(*a, dtype)) {
         const int sp = wsplit(*a);
         const int nwin = (a->reso / a->br[0].H_sp) * (a->reso / a->br[0].W_sp);

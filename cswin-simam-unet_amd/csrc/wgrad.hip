@@ -8,6 +8,8 @@
 // both operands staged transposed in LDS ([n][m] / [k][m]) so MFMA fragments are 16-B reads.
 // Partial tiles (and the db partials of the k-tile-0 workgroups) go to a [chunk][N*K + N] slab
 // that one deterministic column-sum pass reduces in chunk order.
+#include <cstdlib>
+
 #include "common.hpp"
 
 namespace csu {
@@ -227,14 +229,32 @@ WPlan wplan(long M, int N, int K) {
 }
 
 }  // namespace
+
+bool wgrad4_ok(long M, int N, int K);
+size_t wgrad4_workspace(long M, int N, int K);
+int wgrad4_run(long M, int N, int K, const bf16* dy, const bf16* x, float* dw_db, void* ws, hipStream_t st);
 }  // namespace csu
 
 using namespace csu;
 
+// CSU_WGRAD4=1 routes the bf16 path to wgrad4 (LDS-DMA + transposing reads).  Off by default: on
+// the 512x512 step shapes it measured 0-40 % slower than the register-staged kernel below (both are
+// bound by re-reading the operand panels once per output tile, tools/linear_probe.py).
+static bool use_wgrad4() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("CSU_WGRAD4");
+        v = e && e[0] == '1';
+    }
+    return v == 1;
+}
+
 extern "C" size_t csu_linear_wgrad_workspace(long M, int N, int K) {
     const WPlan p = wplan(M, N, K);
     const long slab = (long)N * K + N;
-    return (size_t)p.chunks * slab * sizeof(float) + colsum_workspace(p.chunks, slab, CSU_F32);
+    const size_t a = (size_t)p.chunks * slab * sizeof(float) + colsum_workspace(p.chunks, slab, CSU_F32);
+    const size_t b = wgrad4_ok(M, N, K) ? wgrad4_workspace(M, N, K) : 0;
+    return a > b ? a : b;
 }
 
 extern "C" int csu_linear_wgrad_ex(long M, int N, int K, int dtype, const void* dy, const void* x, int x_gelu,
@@ -252,6 +272,8 @@ extern "C" int csu_linear_wgrad_ex(long M, int N, int K, int dtype, const void* 
     if (N % V || K % V) return fail(CSU_E_ARG, "linear_wgrad: N and K must be multiples of 16 bytes");
     if (!workspace || ws_bytes < csu_linear_wgrad_workspace(M, N, K)) return fail(CSU_E_WORKSPACE, "linear_wgrad: workspace");
     hipStream_t st = as_stream(stream);
+    if (dtype == CSU_BF16 && !x_gelu && use_wgrad4() && wgrad4_ok(M, N, K))
+        return wgrad4_run(M, N, K, (const bf16*)dy, (const bf16*)x, dw_db, workspace, st);
     const WPlan p = wplan(M, N, K);
     float* part = (float*)workspace;
     const long slab = (long)N * K + N;

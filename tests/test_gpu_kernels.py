@@ -258,7 +258,7 @@ def test_linear_splitk_matches_torch():
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("M,N,K", [(262144, 256, 64), (4096, 512, 2048), (1000, 16, 64), (16384, 768, 256), (77, 64, 8),
-                                   (3001, 136, 200), (130, 1024, 256)])
+                                   (3001, 136, 200), (130, 1024, 256), (65536, 128, 512), (4096, 2048, 512), (700, 64, 64)])
 def test_linear_wgrad_kernel(M, N, K, dtype):
     from csu import ops
     d = dev()
