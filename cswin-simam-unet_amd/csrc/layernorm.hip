@@ -31,59 +31,84 @@ template <typename T, int V> __device__ __forceinline__ void stv(T* p, const flo
     }
 }
 
-template <typename TX, typename TY, int V>
+// LPR lanes per row (C = LPR * V, 16-B or 8-B vectors), 64 / LPR rows per wave: C = 64 rows take a
+// quarter wave each instead of a whole wave of 2-4-byte accesses.
+template <int LPR> __device__ __forceinline__ float group_sum(float v) {
+#pragma unroll
+    for (int o = LPR / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+template <typename TX, typename TY, int V, int LPR>
 __global__ __launch_bounds__(NT) void ln_fwd(int rows, int C, float eps, const TX* __restrict__ x,
                                              const float* __restrict__ gamma, const float* __restrict__ beta,
                                              TY* __restrict__ y, float* __restrict__ mean, float* __restrict__ rstd) {
+    constexpr int RPW = 64 / LPR;
     const int lane = threadIdx.x & 63;
-    const int row = blockIdx.x * WAVES + (threadIdx.x >> 6);
-    if (row >= rows) return;
-    const int c0 = lane * V;
+    const int row = (blockIdx.x * WAVES + (threadIdx.x >> 6)) * RPW + lane / LPR;
+    const int c0 = (lane % LPR) * V;
+    const bool ok = row < rows;
     float v[V];
-    ldv<TX, V>(x + (size_t)row * C + c0, v);
+    if (ok) ldv<TX, V>(x + (size_t)row * C + c0, v);
+    else
+#pragma unroll
+        for (int j = 0; j < V; ++j) v[j] = 0.f;
     float s = 0.f;
 #pragma unroll
     for (int j = 0; j < V; ++j) s += v[j];
-    const float mu = wave_sum(s) / C;
+    const float mu = group_sum<LPR>(s) / C;
     float q = 0.f;
 #pragma unroll
     for (int j = 0; j < V; ++j) {
         v[j] -= mu;
         q += v[j] * v[j];
     }
-    const float rs = rsqrtf(wave_sum(q) / C + eps);
-    float o[V];
+    const float rs = rsqrtf(group_sum<LPR>(q) / C + eps);
+    if (!ok) return;
+    float gw[V], bw[V], o[V];
+    ldv<float, V>(gamma + c0, gw);
+    ldv<float, V>(beta + c0, bw);
 #pragma unroll
-    for (int j = 0; j < V; ++j) o[j] = v[j] * rs * gamma[c0 + j] + beta[c0 + j];
+    for (int j = 0; j < V; ++j) o[j] = v[j] * rs * gw[j] + bw[j];
     stv<TY, V>(y + (size_t)row * C + c0, o);
-    if (lane == 0) {
+    if (lane % LPR == 0) {
         mean[row] = mu;
         rstd[row] = rs;
     }
 }
 
-// dx = rstd * (g*gamma - mean(g*gamma) - xhat * mean(g*gamma*xhat)); partial dgamma/dbeta per block
-template <typename TX, typename TG, int V>
+// dx = dres + rstd * (g*gamma - mean(g*gamma) - xhat * mean(g*gamma*xhat)); optionally also a bf16
+// copy of dx (the next GEMM's operand).  dres = the gradient reaching x through the residual branch
+// (x + f(LN(x)) of CSWinBlock, cswin:367-368): the autograd add of the two branches is fused here.
+// dgamma/dbeta: per-block partials, written [2C][nblocks] for the wave-per-value reduction.
+template <typename TX, typename TG, int V, int LPR>
 __global__ __launch_bounds__(NT) void ln_bwd(int rows, int C, int rows_per_block, const TX* __restrict__ x,
                                              const float* __restrict__ gamma, const float* __restrict__ mean,
                                              const float* __restrict__ rstd, const TG* __restrict__ dy,
-                                             TX* __restrict__ dx, float* __restrict__ part) {
+                                             const float* __restrict__ dres, TX* __restrict__ dx,
+                                             bf16* __restrict__ dxb, float* __restrict__ part) {
+    constexpr int RPW = 64 / LPR;
     __shared__ float red[WAVES][2][512];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int c0 = lane * V;
+    const int c0 = (lane % LPR) * V;
     float gw[V], dg[V], db[V];
+    ldv<float, V>(gamma + c0, gw);
 #pragma unroll
-    for (int j = 0; j < V; ++j) {
-        gw[j] = gamma[c0 + j];
-        dg[j] = 0.f;
-        db[j] = 0.f;
-    }
+    for (int j = 0; j < V; ++j) dg[j] = db[j] = 0.f;
     const int r0 = blockIdx.x * rows_per_block, r1 = min(rows, r0 + rows_per_block);
-    for (int row = r0 + wave; row < r1; row += WAVES) {
-        float xv[V], g[V];
-        ldv<TX, V>(x + (size_t)row * C + c0, xv);
-        ldv<TG, V>(dy + (size_t)row * C + c0, g);
-        const float mu = mean[row], rs = rstd[row];
+    for (int rb = r0 + wave * RPW; rb < r1; rb += WAVES * RPW) {
+        const int row = rb + lane / LPR;
+        const bool ok = row < r1;
+        float xv[V], g[V], mu = 0.f, rs = 0.f;
+        if (ok) {
+            ldv<TX, V>(x + (size_t)row * C + c0, xv);
+            ldv<TG, V>(dy + (size_t)row * C + c0, g);
+            mu = mean[row];
+            rs = rstd[row];
+        } else {
+#pragma unroll
+            for (int j = 0; j < V; ++j) xv[j] = g[j] = 0.f;
+        }
         float s1 = 0.f, s2 = 0.f;
 #pragma unroll
         for (int j = 0; j < V; ++j) {
@@ -94,33 +119,60 @@ __global__ __launch_bounds__(NT) void ln_bwd(int rows, int C, int rows_per_block
             dg[j] += g[j] * xv[j];
             db[j] += g[j];
         }
-        s1 = wave_sum(s1) / C;
-        s2 = wave_sum(s2) / C;
+        s1 = group_sum<LPR>(s1) / C;
+        s2 = group_sum<LPR>(s2) / C;
+        if (!ok) continue;
         float o[V];
 #pragma unroll
         for (int j = 0; j < V; ++j) o[j] = rs * (g[j] * gw[j] - s1 - xv[j] * s2);
-        stv<TX, V>(dx + (size_t)row * C + c0, o);
-    }
+        if (dres) {
+            float rv[V];
+            ldv<float, V>(dres + (size_t)row * C + c0, rv);
 #pragma unroll
-    for (int j = 0; j < V; ++j) {
-        red[wave][0][c0 + j] = dg[j];
-        red[wave][1][c0 + j] = db[j];
+            for (int j = 0; j < V; ++j) o[j] += rv[j];
+        }
+        stv<TX, V>(dx + (size_t)row * C + c0, o);
+        if (dxb) stv<bf16, V>(dxb + (size_t)row * C + c0, o);
     }
+    // column partials: lanes of one column inside the wave (fixed xor tree), then the waves
+#pragma unroll
+    for (int o = LPR; o < 64; o <<= 1)
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+            dg[j] += __shfl_xor(dg[j], o, 64);
+            db[j] += __shfl_xor(db[j], o, 64);
+        }
+    if (lane < LPR)
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+            red[wave][0][c0 + j] = dg[j];
+            red[wave][1][c0 + j] = db[j];
+        }
     __syncthreads();
-    // partials laid out [nblocks][2C] (dgamma | dbeta) for the column-sum pass
     for (int i = threadIdx.x; i < 2 * C; i += NT) {
         const int k = i / C, c = i % C;
         float s = 0.f;
 #pragma unroll
         for (int wv = 0; wv < WAVES; ++wv) s += red[wv][k][c];
-        part[(size_t)blockIdx.x * 2 * C + i] = s;
+        part[(size_t)i * gridDim.x + blockIdx.x] = s;
     }
 }
 
-int ln_blocks(int rows, int* rpb) {
+// out[v] = sum_b part[v][b] (v < 2C: dgamma | dbeta), one wave per value, fixed order
+__global__ __launch_bounds__(NT) void ln_param_reduce(int C, int nb, const float* __restrict__ part,
+                                                      float* __restrict__ dgamma, float* __restrict__ dbeta) {
+    const int v = blockIdx.x * WAVES + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (v >= 2 * C) return;
+    float s = 0.f;
+    for (int b = lane; b < nb; b += 64) s += part[(size_t)v * nb + b];
+    s = wave_sum(s);
+    if (lane == 0) (v < C ? dgamma[v] : dbeta[v - C]) = s;
+}
+
+int ln_blocks(int rows, int rpw, int* rpb) {   // <= 512 blocks, rows per block a multiple of a block's row step
+    const int step = WAVES * rpw;
     int r = (rows + 511) / 512;
-    r = ((r + WAVES - 1) / WAVES) * WAVES;
-    if (r < WAVES) r = WAVES;
+    r = ((r + step - 1) / step) * step;
     *rpb = r;
     return (rows + r - 1) / r;
 }
@@ -133,38 +185,40 @@ int check_c(int C) {
 template <typename TX, typename TY>
 int launch_fwd(int rows, int C, float eps, const void* x, const float* g, const float* b, void* y, float* m,
                float* r, hipStream_t st) {
-    const dim3 grid((rows + WAVES - 1) / WAVES);
+#define CSU_LNF(V, LPR)                                                                                           \
+    ln_fwd<TX, TY, V, LPR><<<(rows + WAVES * (64 / LPR) - 1) / (WAVES * (64 / LPR)), NT, 0, st>>>(rows, C, eps,      \
+                                                                                                  (const TX*)x, g, b, \
+                                                                                                  (TY*)y, m, r)
     switch (C / 64) {
-        case 1: ln_fwd<TX, TY, 1><<<grid, NT, 0, st>>>(rows, C, eps, (const TX*)x, g, b, (TY*)y, m, r); break;
-        case 2: ln_fwd<TX, TY, 2><<<grid, NT, 0, st>>>(rows, C, eps, (const TX*)x, g, b, (TY*)y, m, r); break;
-        case 4: ln_fwd<TX, TY, 4><<<grid, NT, 0, st>>>(rows, C, eps, (const TX*)x, g, b, (TY*)y, m, r); break;
-        case 8: ln_fwd<TX, TY, 8><<<grid, NT, 0, st>>>(rows, C, eps, (const TX*)x, g, b, (TY*)y, m, r); break;
+        case 1: CSU_LNF(4, 16); break;
+        case 2: CSU_LNF(4, 32); break;
+        case 4: CSU_LNF(4, 64); break;
+        case 8: CSU_LNF(8, 64); break;
         default: return fail(CSU_E_UNSUPPORTED, "layernorm: C/64 must be 1, 2, 4 or 8");
     }
+#undef CSU_LNF
     return check_launch("layernorm_fwd");
 }
 
 template <typename TX, typename TG>
 int launch_bwd(int rows, int C, const void* x, const float* g, const float* m, const float* r, const void* dy,
-               void* dx, float* dgamma, float* dbeta, float* part, hipStream_t st) {
-    int rpb;
-    const int nb = ln_blocks(rows, &rpb);
+               const float* dres, void* dx, bf16* dxb, float* dgamma, float* dbeta, float* part, hipStream_t st) {
+    int rpb, nb;
+#define CSU_LNB(V, LPR)                                                                                              \
+    nb = ln_blocks(rows, 64 / LPR, &rpb);                                                                            \
+    ln_bwd<TX, TG, V, LPR><<<nb, NT, 0, st>>>(rows, C, rpb, (const TX*)x, g, m, r, (const TG*)dy, dres, (TX*)dx, dxb, \
+                                             part)
     switch (C / 64) {
-        case 1: ln_bwd<TX, TG, 1><<<nb, NT, 0, st>>>(rows, C, rpb, (const TX*)x, g, m, r, (const TG*)dy, (TX*)dx, part); break;
-        case 2: ln_bwd<TX, TG, 2><<<nb, NT, 0, st>>>(rows, C, rpb, (const TX*)x, g, m, r, (const TG*)dy, (TX*)dx, part); break;
-        case 4: ln_bwd<TX, TG, 4><<<nb, NT, 0, st>>>(rows, C, rpb, (const TX*)x, g, m, r, (const TG*)dy, (TX*)dx, part); break;
-        case 8: ln_bwd<TX, TG, 8><<<nb, NT, 0, st>>>(rows, C, rpb, (const TX*)x, g, m, r, (const TG*)dy, (TX*)dx, part); break;
+        case 1: CSU_LNB(4, 16); break;
+        case 2: CSU_LNB(4, 32); break;
+        case 4: CSU_LNB(4, 64); break;
+        case 8: CSU_LNB(8, 64); break;
         default: return fail(CSU_E_UNSUPPORTED, "layernorm: C/64 must be 1, 2, 4 or 8");
     }
+#undef CSU_LNB
     if (int e = check_launch("layernorm_bwd")) return e;
-    float* cws = part + (size_t)2 * nb * C;
-    if (dbeta == dgamma + C) return colsum_launch(nb, 2 * C, CSU_F32, part, dgamma, cws, st);
-    float* tmp = cws + colsum_workspace(nb, 2 * C, CSU_F32) / sizeof(float);
-    if (int e = colsum_launch(nb, 2 * C, CSU_F32, part, tmp, cws, st)) return e;
-    if (hipMemcpyAsync(dgamma, tmp, C * sizeof(float), hipMemcpyDeviceToDevice, st) != hipSuccess ||
-        hipMemcpyAsync(dbeta, tmp + C, C * sizeof(float), hipMemcpyDeviceToDevice, st) != hipSuccess)
-        return check_launch("layernorm_bwd copy");
-    return 0;
+    ln_param_reduce<<<(2 * C + WAVES - 1) / WAVES, NT, 0, st>>>(C, nb, part, dgamma, dbeta);
+    return check_launch("layernorm_bwd reduce");
 }
 
 }  // namespace
@@ -186,23 +240,35 @@ extern "C" int csu_layernorm_fwd(int rows, int C, float eps, int xdtype, const v
 
 extern "C" size_t csu_layernorm_bwd_workspace(int rows, int C) {
     int rpb;
-    const int nb = ln_blocks(rows, &rpb);
-    return (size_t)nb * 2 * C * sizeof(float) + colsum_workspace(nb, 2 * C, CSU_F32) + 2 * C * sizeof(float);
+    const int nb = ln_blocks(rows, C >= 256 ? 1 : 256 / C, &rpb);   // rows per wave = 64 / LPR, LPR = min(64, C/4)
+    return (size_t)nb * 2 * C * sizeof(float);
 }
 
-extern "C" int csu_layernorm_bwd(int rows, int C, int xdtype, const void* x, const float* gamma, const float* mean,
-                                 const float* rstd, int dydtype, const void* dy, void* dx, float* dgamma,
-                                 float* dbeta, void* workspace, size_t ws_bytes, void* stream) {
+extern "C" int csu_layernorm_bwd_ex(int rows, int C, int xdtype, const void* x, const float* gamma, const float* mean,
+                                    const float* rstd, int dydtype, const void* dy, const float* dres, void* dx,
+                                    void* dx_bf16, float* dgamma, float* dbeta, void* workspace, size_t ws_bytes,
+                                    void* stream) {
     if (int e = check_c(C)) return e;
     if (rows < 1 || !x || !gamma || !mean || !rstd || !dy || !dx || !dgamma || !dbeta)
         return fail(CSU_E_ARG, "layernorm_bwd: bad args");
     if (!workspace || ws_bytes < csu_layernorm_bwd_workspace(rows, C))
         return fail(CSU_E_WORKSPACE, "layernorm_bwd: workspace too small");
+    if (dres && xdtype != CSU_F32) return fail(CSU_E_ARG, "layernorm_bwd: a residual gradient needs fp32 x/dx");
     hipStream_t st = as_stream(stream);
     float* part = (float*)workspace;
-    if (xdtype == CSU_F32 && dydtype == CSU_F32) return launch_bwd<float, float>(rows, C, x, gamma, mean, rstd, dy, dx, dgamma, dbeta, part, st);
-    if (xdtype == CSU_F32 && dydtype == CSU_BF16) return launch_bwd<float, bf16>(rows, C, x, gamma, mean, rstd, dy, dx, dgamma, dbeta, part, st);
-    if (xdtype == CSU_BF16 && dydtype == CSU_F32) return launch_bwd<bf16, float>(rows, C, x, gamma, mean, rstd, dy, dx, dgamma, dbeta, part, st);
-    if (xdtype == CSU_BF16 && dydtype == CSU_BF16) return launch_bwd<bf16, bf16>(rows, C, x, gamma, mean, rstd, dy, dx, dgamma, dbeta, part, st);
+    bf16* dxb = (bf16*)dx_bf16;
+#define CSU_LNB_CALL(TX, TG) return launch_bwd<TX, TG>(rows, C, x, gamma, mean, rstd, dy, dres, dx, dxb, dgamma, dbeta, part, st)
+    if (xdtype == CSU_F32 && dydtype == CSU_F32) CSU_LNB_CALL(float, float);
+    if (xdtype == CSU_F32 && dydtype == CSU_BF16) CSU_LNB_CALL(float, bf16);
+    if (xdtype == CSU_BF16 && dydtype == CSU_F32) CSU_LNB_CALL(bf16, float);
+    if (xdtype == CSU_BF16 && dydtype == CSU_BF16) CSU_LNB_CALL(bf16, bf16);
+#undef CSU_LNB_CALL
     return fail(CSU_E_ARG, "layernorm_bwd: bad dtype");
+}
+
+extern "C" int csu_layernorm_bwd(int rows, int C, int xdtype, const void* x, const float* gamma, const float* mean,
+                                 const float* rstd, int dydtype, const void* dy, void* dx, float* dgamma,
+                                 float* dbeta, void* workspace, size_t ws_bytes, void* stream) {
+    return csu_layernorm_bwd_ex(rows, C, xdtype, x, gamma, mean, rstd, dydtype, dy, nullptr, dx, nullptr, dgamma, dbeta,
+                                workspace, ws_bytes, stream);
 }

@@ -55,6 +55,9 @@ _SIGS = {
     "csu_layernorm_bwd": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                                          ctypes.c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,
                                          c_void_p]),
+    "csu_layernorm_bwd_ex": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, c_void_p, c_void_p, c_void_p,
+                                            c_void_p, ctypes.c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                            c_void_p, c_void_p, c_size_t, c_void_p]),
     "csu_simam_workspace": (c_size_t, [ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     "csu_simam_fwd": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, c_float, ctypes.c_int, c_void_p, c_void_p,
                                      c_void_p, c_void_p, c_size_t, c_void_p]),

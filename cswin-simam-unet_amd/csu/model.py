@@ -179,17 +179,22 @@ class CSWinBlock(nn.Module):
         if self.training and self.attns[0].attn_drop_p > 0:
             raise NotImplementedError("attention dropout inside the fused stripe kernel is not implemented yet")
         cd = _compute_dtype(x)
-        qkv = ops.linear(_ln(x, self.norm1, cd), self.qkv.weight, self.qkv.bias)
+        # residual junctions x -> (x, LN(x)): their backward adds the two branch gradients in the
+        # LayerNorm-backward kernel and hands the upstream GEMMs a bf16 copy (ops.layer_norm_fork)
+        n1, n2 = self.norm1, self.norm2
+        xa, h1 = ops.layer_norm_fork(x, n1.weight, n1.bias, n1.eps, cd)
+        qkv = ops.linear(h1, self.qkv.weight, self.qkv.bias)
         att = ops.stripe_attention(qkv, self._geom, [a.get_v.weight for a in self.attns],
                                    [a.get_v.bias for a in self.attns])
         plain = isinstance(self.drop_path, nn.Identity) and not (self.training and self.mlp.drop.p > 0)
         if plain and ops.fused_ok(x, C, self.mlp.fc1.out_features):
             # bf16 fused path: proj + residual in one GEMM; fc1 -> GELU -> fc2 + residual in two
-            x = ops.linear_residual(x, att, self.proj.weight, self.proj.bias)
-            return ops.mlp_residual(x, _ln(x, self.norm2, cd), self.mlp.fc1, self.mlp.fc2)
-        x = x + self.drop_path(ops.linear(att, self.proj.weight, self.proj.bias))
-        x = x + self.drop_path(self.mlp(_ln(x, self.norm2, cd)))
-        return x
+            x = ops.linear_residual(xa, att, self.proj.weight, self.proj.bias)
+            xb, h2 = ops.layer_norm_fork(x, n2.weight, n2.bias, n2.eps, cd)
+            return ops.mlp_residual(xb, h2, self.mlp.fc1, self.mlp.fc2)
+        x = xa + self.drop_path(ops.linear(att, self.proj.weight, self.proj.bias))
+        xb, h2 = ops.layer_norm_fork(x, n2.weight, n2.bias, n2.eps, cd)
+        return xb + self.drop_path(self.mlp(h2))
 
 
 class Merge_Block(nn.Module):

@@ -177,6 +177,72 @@ def layer_norm(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, eps: f
     return _LayerNormFn.apply(x, weight, bias, eps, out_dtype or x.dtype)
 
 
+def _bf16_of(g: torch.Tensor) -> torch.Tensor:
+    """bf16 copy of a gradient: the one a residual junction attached to it (csu_layernorm_bwd_ex
+    writes it in the same pass), else a fresh cast."""
+    b = getattr(g, "_csu_bf16", None)
+    if b is not None and b.shape == g.shape:
+        return b
+    return g.reshape(g.shape).to(torch.bfloat16).contiguous()
+
+
+class _LayerNormForkFn(torch.autograd.Function):
+    """Residual junction x -> (x, LN(x)) of CSWinBlock (x + f(LN(x)), cswin:367-368).  Backward
+    gets the residual-branch gradient and the LN-branch gradient together and writes
+    dx = dres + dLN in ONE kernel (no autograd add), plus the bf16 copy of dx that the upstream
+    GEMM backward consumes (attached to dx as ``_csu_bf16``)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, eps: float, out_dtype):
+        require_device(x, weight, bias)
+        x = x.contiguous()
+        C = x.shape[-1]
+        rows = x.numel() // C
+        w = weight.detach().float().contiguous()
+        b = bias.detach().float().contiguous()
+        y = torch.empty(x.shape, dtype=out_dtype, device=x.device)
+        mean = torch.empty(rows, dtype=torch.float32, device=x.device)
+        rstd = torch.empty(rows, dtype=torch.float32, device=x.device)
+        check(lib().csu_layernorm_fwd(rows, C, float(eps), dtype_code(x), ptr(x), ptr(w), ptr(b), dtype_code(y), ptr(y),
+                                      ptr(mean), ptr(rstd), stream_ptr(x.device)), "csu_layernorm_fwd")
+        ctx.save_for_backward(x, w, mean, rstd)
+        ctx.pdtypes = (weight.dtype, bias.dtype)
+        return x.view_as(x), y
+
+    @staticmethod
+    def backward(ctx, dres, dy):
+        x, w, mean, rstd = ctx.saved_tensors
+        C = x.shape[-1]
+        rows = x.numel() // C
+        if dy is None:
+            dy = torch.zeros(x.shape, dtype=torch.float32, device=x.device)
+        dy = dy.contiguous()
+        if dy.dtype not in (torch.float32, torch.bfloat16):
+            dy = dy.float()
+        fp32 = x.dtype == torch.float32
+        dres_k = dres.float().contiguous() if (dres is not None and fp32) else None
+        dx = torch.empty_like(x)
+        dxb = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device) if fp32 else None
+        dgb = torch.empty(2 * C, dtype=torch.float32, device=x.device)
+        L = lib()
+        nbytes = L.csu_layernorm_bwd_workspace(rows, C)
+        work = torch.empty(max(nbytes, 16), dtype=torch.uint8, device=x.device)
+        check(L.csu_layernorm_bwd_ex(rows, C, dtype_code(x), ptr(x), ptr(w), ptr(mean), ptr(rstd), dtype_code(dy), ptr(dy),
+                                     ptr(dres_k), ptr(dx), ptr(dxb), ptr(dgb[:C]), ptr(dgb[C:]), ptr(work), nbytes,
+                                     stream_ptr(x.device)), "csu_layernorm_bwd_ex")
+        if dres is not None and not fp32:    # non-fp32 residual stream: plain add (not on the bf16 path)
+            dx = dx + dres.to(dx.dtype)
+        if dxb is not None:
+            dx._csu_bf16 = dxb
+        return dx, dgb[:C].to(ctx.pdtypes[0]), dgb[C:].to(ctx.pdtypes[1]), None, None
+
+
+def layer_norm_fork(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, eps: float = 1e-5,
+                    out_dtype: Optional[torch.dtype] = None):
+    """(x, LN(x)) for a residual junction; use the first output as the residual input."""
+    return _LayerNormForkFn.apply(x, weight, bias, eps, out_dtype or x.dtype)
+
+
 # ---------------------------------------------------------------------------------------------
 # CARAFE reassembly (cswin:410-432 / 459-481) and the 1-class sigmoid head (cswin:680, 688)
 # ---------------------------------------------------------------------------------------------
@@ -516,7 +582,7 @@ class _LinearResidualFn(torch.autograd.Function):
     def backward(ctx, dy):
         x2, wt = ctx.saved_tensors
         rdt, xshape, wdt, bdt = ctx.meta
-        dyb = dy.reshape(-1, dy.shape[-1]).to(torch.bfloat16).contiguous()
+        dyb = _bf16_of(dy).view(-1, dy.shape[-1])
         dx = gemm(dyb, wt, False, torch.bfloat16).view(xshape)
         dw, db = wgrad_maybe_side(dyb, x2, wdt, bdt)
         return dy.to(rdt), dx, dw.to(wdt), db.to(bdt), None
@@ -541,7 +607,7 @@ class _MlpResidualFn(torch.autograd.Function):
     def backward(ctx, dy):
         x2, h, g, w1t, w2t = ctx.saved_tensors
         rdt, xshape, w1dt, b1dt, w2dt, b2dt = ctx.meta
-        dyb = dy.reshape(-1, dy.shape[-1]).to(torch.bfloat16).contiguous()
+        dyb = _bf16_of(dy).view(-1, dy.shape[-1])
         dh = gemm(dyb, w2t, False, torch.bfloat16, gelu_aux=h)         # (dY W2) * gelu'(h)
         dw2, db2 = wgrad_maybe_side(dyb, g, w2dt, b2dt)
         dx = gemm(dh, w1t, False, torch.bfloat16).view(xshape)

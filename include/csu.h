@@ -91,6 +91,14 @@ int csu_layernorm_bwd(int rows, int C, int xdtype, const void* x, const float* g
                       const float* mean, const float* rstd, int dydtype, const void* dy,
                       void* dx, float* dgamma, float* dbeta, void* workspace, size_t ws_bytes,
                       void* stream);
+/* Residual-junction backward of y = LN(x) inside x_out = x + f(y) (CSWinBlock cswin:367-368):
+ * dx = dres + dLN(dy) in one pass (dres fp32 [rows][C] or NULL; x/dx fp32 when dres is given),
+ * plus an optional bf16 copy dx_bf16 (the next GEMM's operand; NULL to skip).  Replaces the
+ * autograd add of the two branches and the bf16 cast of the summed gradient. */
+int csu_layernorm_bwd_ex(int rows, int C, int xdtype, const void* x, const float* gamma,
+                         const float* mean, const float* rstd, int dydtype, const void* dy,
+                         const float* dres, void* dx, void* dx_bf16, float* dgamma, float* dbeta,
+                         void* workspace, size_t ws_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * SimAM (parameter-free energy gate) on token rows (B, L, C), statistics per (b, c) over L.

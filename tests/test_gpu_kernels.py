@@ -125,6 +125,46 @@ def test_layernorm_vs_torch_fp64(C, xdt, ydt):
     assert_close(bd.grad, b64.grad, tol_dt)
 
 
+@pytest.mark.parametrize("C", [64, 128, 256, 512])
+@pytest.mark.parametrize("gdt", [torch.float32, torch.bfloat16])
+def test_layernorm_fork_residual_junction(C, gdt):
+    """x -> (x, LN(x)) used as x + f(LN(x)): one-kernel dx = dres + dLN == torch fp64, and the bf16
+    copy handed to the upstream GEMM equals the fp32 gradient rounded."""
+    from csu import ops
+    d = dev()
+    g = torch.Generator().manual_seed(C + 7)
+    x = torch.randn(2, 1029, C, generator=g) * 2 + 0.5
+    w, b = torch.randn(C, generator=g), torch.randn(C, generator=g)
+    gres = torch.randn(2, 1029, C, generator=g)          # gradient through the residual branch
+    gln = torch.randn(2, 1029, C, generator=g).to(gdt)    # gradient through the LayerNorm branch
+    x64 = x.double().requires_grad_(True)
+    w64, b64 = w.double().requires_grad_(True), b.double().requires_grad_(True)
+    y64 = torch.nn.functional.layer_norm(x64, (C,), w64, b64, 1e-5)
+    ((x64 * gres.double()).sum() + (y64 * gln.double()).sum()).backward()
+    seen = {}
+
+    class Probe(torch.autograd.Function):   # upstream consumer: records the gradient object it receives
+        @staticmethod
+        def forward(ctx, t):
+            return t.view_as(t)
+
+        @staticmethod
+        def backward(ctx, gt):
+            seen["g"] = gt
+            return gt
+
+    x0 = x.to(d).requires_grad_(True)
+    wd, bd = w.to(d).requires_grad_(True), b.to(d).requires_grad_(True)
+    xa, y = ops.layer_norm_fork(Probe.apply(x0), wd, bd, 1e-5, gdt)   # LN output dtype = its gradient's dtype
+    assert y.dtype == gdt and xa.data_ptr() == x0.data_ptr()
+    ((xa * gres.to(d)).sum() + (y.float() * gln.to(d).float()).sum()).backward()
+    assert_close(x0.grad, x64.grad, torch.float32 if gdt == torch.float32 else torch.bfloat16)
+    assert_close(wd.grad, w64.grad, torch.bfloat16)
+    assert_close(bd.grad, b64.grad, torch.bfloat16)
+    gb = getattr(seen["g"], "_csu_bf16", None)
+    assert gb is not None and torch.equal(gb, seen["g"].to(torch.bfloat16))
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("shape", [(2, 64, 32), (2, 1024, 64), (1, 4096, 128), (3, 17, 200)])
 def test_simam_vs_formula(shape, dtype):
