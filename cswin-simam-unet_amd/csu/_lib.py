@@ -83,6 +83,9 @@ _SIGS = {
                                 ctypes.c_int, ctypes.c_int, c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_int,
                                 ctypes.c_int, c_void_p]),
     "csu_cast_bf16_batch": (ctypes.c_int, [c_void_p, ctypes.c_int, ctypes.c_long, c_void_p]),
+    "csu_adamw_chunk_elems": (ctypes.c_long, []),
+    "csu_adamw_step": (ctypes.c_int, [c_void_p, ctypes.c_int, ctypes.c_long, c_void_p, c_float, c_float, c_float, c_float,
+                                      c_float, c_void_p, c_float, c_void_p]),
     "csu_gemm_ex": (ctypes.c_int, [ctypes.POINTER(GemmDesc), c_void_p]),
     "csu_conv2d_fwd": (ctypes.c_int, [ctypes.POINTER(ConvGeom), ctypes.c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                                       c_void_p]),

@@ -1,0 +1,117 @@
+"""Fused AdamW on the csu_adamw_step kernel (the optimizer of cswin:937-941).
+
+Drop-in for ``torch.optim.AdamW`` (same constructor arguments, param_groups, state keys
+``step`` / ``exp_avg`` / ``exp_avg_sq`` and state_dict format, ReduceLROnPlateau works on it): one
+kernel launch updates every parameter of a group from a device table of pointers.  The table is
+rebuilt only when the set of (param, grad) buffers changes, from a pinned host buffer, so the step
+can also be captured into a HIP graph (lr and the step count then live in device tensors that are
+updated in place: ``capturable=True``)."""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import check, lib, stream_ptr
+
+_ITEM = np.dtype([("param", "<u8"), ("grad", "<u8"), ("exp_avg", "<u8"), ("exp_avg_sq", "<u8"), ("numel", "<i8"),
+                  ("chunk0", "<i8")])
+
+
+class FusedAdamW(torch.optim.Optimizer):
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2, capturable=False):
+        if not 0.0 <= lr or not 0.0 <= eps or not 0.0 <= weight_decay:
+            raise ValueError("invalid AdamW hyper-parameter")
+        if not (0.0 <= betas[0] < 1.0 and 0.0 <= betas[1] < 1.0):
+            raise ValueError(f"invalid betas {betas}")
+        super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, capturable=capturable))
+        self._tables = {}
+        self._gstate = {}
+        # one pinned table buffer per group, reserved for a HIP-graph capture of step()
+        self._pinned = {gi: torch.empty(max(1, len(g["params"])) * _ITEM.itemsize, dtype=torch.uint8, pin_memory=True)
+                        for gi, g in enumerate(self.param_groups)} if torch.cuda.is_available() else {}
+
+    def _table(self, gi, items, device):
+        """Device item table for the current (param, grad) buffers, rebuilt when they change.
+        Eager: a pageable (host-synchronous) copy.  Under HIP-graph capture: an async copy from a
+        pinned buffer reserved for that capture (pinned memory cannot be allocated while
+        capturing); the graph's copy node re-reads it on every replay, so it is never rewritten."""
+        key = (gi,) + tuple(v for it in items for v in it[:4])
+        t = self._tables.get(gi)
+        if t is not None and t[0] == key:
+            return t
+        chunk = lib().csu_adamw_chunk_elems()
+        rec = np.zeros(len(items), dtype=_ITEM)
+        c0 = 0
+        for i, (p, g, m, v, n) in enumerate(items):
+            rec[i] = (p, g, m, v, n, c0)
+            c0 += -(-n // chunk)
+        raw = np.frombuffer(rec.tobytes(), dtype=np.uint8)
+        if torch.cuda.is_current_stream_capturing():
+            host = self._pinned.get(gi)
+            if host is None or host.numel() < raw.size:
+                raise RuntimeError("FusedAdamW: no pinned table buffer for this capture (one capture per optimizer)")
+            del self._pinned[gi]                      # frozen: owned by the captured graph from now on
+            host[:raw.size].numpy()[:] = raw
+            dev = torch.empty(raw.size, dtype=torch.uint8, device=device)
+            dev.copy_(host[:raw.size], non_blocking=True)
+        else:
+            host = None
+            dev = torch.from_numpy(raw.copy()).to(device)
+        t = (key, host, dev, len(items), c0)
+        self._tables[gi] = t
+        return t
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        for gi, group in enumerate(self.param_groups):
+            items, dev = [], None
+            for p in group["params"]:
+                if p.grad is None:
+                    continue
+                if p.grad.is_sparse or p.dtype != torch.float32 or not p.is_cuda:
+                    raise RuntimeError("FusedAdamW: dense fp32 CUDA parameters only")
+                st = self.state[p]
+                if not st:
+                    st["step"] = torch.zeros((), dtype=torch.float32, device=p.device)
+                    st["exp_avg"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
+                    st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
+                g = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
+                if not p.is_contiguous():
+                    raise RuntimeError("FusedAdamW: contiguous parameters only")
+                items.append((p.data_ptr(), g.data_ptr(), st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr(),
+                              p.numel()))
+                dev = p.device
+            if not items:
+                continue
+            gs = self._gstate.get(gi)
+            if gs is None:
+                # one device step count per group (every parameter of a group steps together);
+                # resumes from a loaded state_dict's per-parameter step
+                st0 = next((self.state[p]["step"] for p in group["params"] if "step" in self.state[p]
+                            and self.state[p]["step"] is not None), None)
+                step0 = float(st0) if st0 is not None else 0.0
+                gs = self._gstate[gi] = {"step": torch.full((), step0, dtype=torch.float32, device=dev),
+                                         "lr": torch.full((), group["lr"], dtype=torch.float32, device=dev)}
+            gs["step"] += 1
+            for p in group["params"]:
+                if p.grad is not None:
+                    self.state[p]["step"] = gs["step"]
+            _, _, table, n, chunks = self._table(gi, items, dev)
+            lr_ptr = gs["lr"].data_ptr() if group["capturable"] else None
+            b1, b2 = group["betas"]
+            check(lib().csu_adamw_step(table.data_ptr(), n, chunks, lr_ptr, float(group["lr"]), float(b1), float(b2),
+                                       float(group["eps"]), float(group["weight_decay"]), gs["step"].data_ptr(), 0.0,
+                                       stream_ptr(dev)), "csu_adamw_step")
+        return loss
+
+    def sync_lr(self):
+        """Copy the host lr of every group into its device tensor (capturable groups read it at
+        replay time): call after a scheduler step, outside graph replay."""
+        for gi, g in enumerate(self.param_groups):
+            if gi in self._gstate:
+                self._gstate[gi]["lr"].fill_(g["lr"])

@@ -136,12 +136,13 @@ def train_model(model, train_loader, test_loader, criterion, optimizer, schedule
 
 
 def make_optimizer(model, lr=1e-4, weight_decay=1e-4, capturable=False):
-    """AdamW as in cswin:937-941 (fused multi-tensor implementation on the device;
-    ``capturable=True`` keeps lr/step on the device so the step can live in a HIP graph)."""
-    kw = {"fused": True} if next(model.parameters()).is_cuda else {}
-    if capturable:
-        kw["capturable"] = True
-    return torch.optim.AdamW(model.parameters(), lr=lr, weight_decay=weight_decay, **kw)
+    """AdamW as in cswin:937-941.  On the GPU: csu.optim.FusedAdamW (one csu_adamw_step launch for
+    all 463 tensors; ``capturable=True`` reads lr/step from device tensors so the step can live in a
+    HIP graph); on the CPU: torch.optim.AdamW."""
+    if next(model.parameters()).is_cuda:
+        from .optim import FusedAdamW
+        return FusedAdamW(model.parameters(), lr=lr, weight_decay=weight_decay, capturable=capturable)
+    return torch.optim.AdamW(model.parameters(), lr=lr, weight_decay=weight_decay)
 
 
 class GraphedTrainStep:

@@ -224,6 +224,27 @@ typedef struct {
 int csu_cast_bf16_batch(const csu_cast_item* items, int count, long total_tiles, void* stream);
 
 /* ---------------------------------------------------------------------------------------
+ * Fused multi-tensor AdamW step (torch.optim.AdamW semantics, cswin:937-941): for every item,
+ * param *= 1 - lr*wd; m = lerp(m, g, 1-beta1); v = beta2 v + (1-beta2) g^2;
+ * param -= lr/(1-beta1^t) * m / (sqrt(v)/sqrt(1-beta2^t) + eps).  items: DEVICE array sorted
+ * by chunk0 = first chunk index of the item (chunk0[i+1] = chunk0[i] + ceil(numel /
+ * csu_adamw_chunk_elems())); total_chunks = the sum.  lr_dev / step_dev: device scalars (HIP
+ * graph capture) or NULL to use lr / step.  Replaces torch's fused AdamW launches.
+ * ------------------------------------------------------------------------------------- */
+typedef struct {
+    float* param;
+    const float* grad;
+    float* exp_avg;
+    float* exp_avg_sq;
+    int64_t numel;
+    int64_t chunk0;
+} csu_adamw_item;
+long csu_adamw_chunk_elems(void);
+int csu_adamw_step(const csu_adamw_item* items, int count, long total_chunks, const float* lr_dev, float lr,
+                   float beta1, float beta2, float eps, float weight_decay, const float* step_dev, float step,
+                   void* stream);
+
+/* ---------------------------------------------------------------------------------------
  * Implicit-GEMM NHWC convolution (patch embed cswin:505, Merge_Block.conv cswin:376, CARAFE
  * encoder cswin:397/446, plain-UNet DoubleConv 3x3 unet:182/185 and ConvTranspose2d(k2,s2)
  * unet:211 = the dgrad operator).  x (B,H,W,C), y (B,OH,OW,N) channels-last; weights prepared by

@@ -476,3 +476,33 @@ def test_conv_transpose2d_nhwc_vs_torch(B, H, Cin, Cout, dtype):
     assert_close(xd.grad, x64.grad, dtype)
     assert_close(wd.grad, w64.grad, dtype)
     assert_close(bd.grad, b64.grad, dtype)
+
+
+@pytest.mark.parametrize("capturable", [False, True])
+def test_fused_adamw_matches_torch(capturable):
+    """csu_adamw_step (one launch, all tensors) == torch.optim.AdamW over several steps, incl.
+    ragged numels and a ReduceLROnPlateau-style lr change; bias corrections in fp32 -> rtol 1e-5."""
+    from csu.optim import FusedAdamW
+    d = dev()
+    g = torch.Generator(device=d).manual_seed(0)
+    shapes = [(256, 64), (64,), (3, 7, 11), (1,), (4099,), (512, 2048)]
+    ps = [torch.randn(s, device=d, generator=g) for s in shapes]
+    ref = [p.clone().requires_grad_(True) for p in ps]
+    mine = [p.clone().requires_grad_(True) for p in ps]
+    o_ref = torch.optim.AdamW(ref, lr=1e-3, weight_decay=1e-2, foreach=False)
+    o_mine = FusedAdamW(mine, lr=1e-3, weight_decay=1e-2, capturable=capturable)
+    for it in range(6):
+        if it == 3:
+            for o in (o_ref, o_mine):
+                o.param_groups[0]["lr"] = 5e-4
+            o_mine.sync_lr()
+        grads = [torch.randn(s, device=d, generator=g) for s in shapes]
+        for p, q, gr in zip(ref, mine, grads):
+            p.grad, q.grad = gr.clone(), gr.clone()
+        o_ref.step()
+        o_mine.step()
+    for p, q in zip(ref, mine):
+        torch.testing.assert_close(q.detach(), p.detach(), rtol=1e-5, atol=1e-6)
+    for p, q in zip(ref, mine):
+        torch.testing.assert_close(o_mine.state[q]["exp_avg"], o_ref.state[p]["exp_avg"], rtol=1e-5, atol=1e-7)
+        torch.testing.assert_close(o_mine.state[q]["exp_avg_sq"], o_ref.state[p]["exp_avg_sq"], rtol=5e-5, atol=1e-9)

@@ -4,7 +4,7 @@ path = sys.argv[1]
 nsteps = int(sys.argv[2]) if len(sys.argv) > 2 else 2
 rows = list(csv.DictReader(open(path)))
 rows.sort(key=lambda r: int(r['Start_Timestamp']))
-opt = [r for r in rows if 'multi_tensor_apply' in r['Kernel_Name'] or 'FusedAdam' in r['Kernel_Name']]
+opt = [r for r in rows if 'multi_tensor_apply' in r['Kernel_Name'] or 'FusedAdam' in r['Kernel_Name'] or 'adamw_kernel' in r['Kernel_Name']]
 ends = sorted(set(int(r['End_Timestamp']) for r in opt))
 steps, last = [], None
 for e in ends:

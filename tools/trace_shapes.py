@@ -3,7 +3,7 @@ import csv, collections, sys
 path, nsteps = sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 2
 pat = sys.argv[3] if len(sys.argv) > 3 else ""
 rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r['Start_Timestamp']))
-opt = [r for r in rows if 'multi_tensor_apply' in r['Kernel_Name'] or 'FusedAdam' in r['Kernel_Name']]
+opt = [r for r in rows if 'multi_tensor_apply' in r['Kernel_Name'] or 'FusedAdam' in r['Kernel_Name'] or 'adamw_kernel' in r['Kernel_Name']]
 ends, steps, last = sorted(set(int(r['End_Timestamp']) for r in opt)), [], None
 for e in ends:
     if last is None or e - last > 3e6:
