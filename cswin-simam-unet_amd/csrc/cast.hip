@@ -3,6 +3,9 @@
 // cswin:185-195/314-368) and writes W^T (K, N) next to W (N, K), so the input-gradient GEMM
 // dX = dY W is a plain b[n][k] GEMM (csu_gemm_ex, b_trans = 0).
 // One workgroup = one 64 x 64 tile of one item; items are found by binary search on tile0.
+// Conv-weight items (taps > 0) write the two channels-last layouts of the implicit-GEMM conv
+// kernels instead (OHWI for the forward / transposed-conv input gradient, IHWO for the
+// input gradient / transposed-conv forward), 4096 elements per workgroup.
 #include "common.hpp"
 
 namespace csu {
@@ -20,6 +23,20 @@ __global__ __launch_bounds__(NT) void cast_batch(const csu_cast_item* __restrict
         if (items[mid].tile0 <= b) lo = mid; else hi = mid - 1;
     }
     const csu_cast_item it = items[lo];
+    if (it.taps > 0) {   // conv weight (rows = N, cols = C, taps = KH*KW): OHWI and IHWO bf16 layouts
+        const int n_el = it.rows * it.cols * it.taps;       // < 2^31 (conv weights)
+        const unsigned CT = it.cols * it.taps, TP = it.taps;
+        bf16* o = (bf16*)it.dst;
+        bf16* t = (bf16*)it.dst_t;
+        const int e0 = (int)(b - it.tile0) * (T * T), e1 = min(n_el, e0 + T * T);
+        for (int e = e0 + threadIdx.x; e < e1; e += NT) {
+            const unsigned n = (unsigned)e / CT, rem = (unsigned)e - n * CT, c = rem / TP, k = rem - c * TP;
+            const bf16 v = (bf16)it.src[e];                        // src [n][c][k]
+            o[(n * TP + k) * it.cols + c] = v;                     // OHWI [n][k][c]
+            if (t) t[(c * TP + k) * it.rows + n] = v;              // IHWO [c][k][n]
+        }
+        return;
+    }
     const int tk = (it.cols + T - 1) / T;
     const long t = b - it.tile0;
     const int r0 = (int)(t / tk) * T, c0 = (int)(t % tk) * T;

@@ -352,7 +352,9 @@ class CSWinTransformer(nn.Module):
 
     @staticmethod
     def _fuse(lin: nn.Linear, x: torch.Tensor) -> torch.Tensor:
-        return ops.linear(x, lin.weight, lin.bias)
+        """concat_linear (cswin:568/581/592): its output starts a decoder residual stream, kept
+        fp32 like the encoder's (written fp32 by the GEMM epilogue, no conversion pass)."""
+        return ops.linear(x, lin.weight, lin.bias, out_dtype=torch.float32 if x.is_cuda else None)
 
     def _skip(self, t):
         return self.simam(t) if self.simam is not None else t
@@ -417,12 +419,23 @@ class CSWinTransformer(nn.Module):
                 yield m.down.weight
                 yield m.out.weight
 
+    def _conv_weights(self):
+        """KxK conv weights whose channels-last bf16 layouts the cast cache keeps (patch embed,
+        Merge_Block, CARAFE encoders)."""
+        yield self.stage1_conv_embed[0].weight
+        for m in self.modules():
+            if isinstance(m, Merge_Block):
+                yield m.conv.weight
+            elif isinstance(m, CARAFE):
+                yield m.encoder.weight
+
     def forward(self, x):
         cd = _compute_dtype(x)
         if cd != torch.float32 and x.is_cuda:
             if not hasattr(self, "_cast_cache"):
                 self._cast_cache = ops.CastCache()
-            self._cast_cache.refresh(self._linear_weights(), cd)   # one multi-tensor cast per step
+            # one launch per step: bf16 shadows of every Linear weight (+ transposes) and conv layouts
+            self._cast_cache.refresh(self._linear_weights(), cd, self._conv_weights())
             ops.set_cast_cache(self._cast_cache)
         try:
             return self._forward(x)

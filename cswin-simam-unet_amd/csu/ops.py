@@ -509,7 +509,7 @@ def _weight_t(w, wc):
 
 class _LinearFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, cd, wc):
+    def forward(ctx, x, weight, bias, cd, wc, odt=None):
         xc = x if x.dtype == cd else x.to(cd)
         if wc is None:
             wc = weight.to(cd)
@@ -518,7 +518,7 @@ class _LinearFn(torch.autograd.Function):
         wt = None
         if ctx.fast:
             x2 = xc.reshape(-1, K).contiguous()
-            y = gemm(x2, wc, False, cd, bias=None if bias is None else bias.detach().float().contiguous())
+            y = gemm(x2, wc, False, odt or cd, bias=None if bias is None else bias.detach().float().contiguous())
             y = y.view(*xc.shape[:-1], N)
             wt = _weight_t(weight, wc)
         else:
@@ -537,9 +537,12 @@ class _LinearFn(torch.autograd.Function):
         xc, wc = ctx.saved_tensors          # wc: (K, N) transpose on the fast path
         xdt, wdt, bdt = ctx.meta
         K, N = xc.shape[-1], dy.shape[-1]
-        dy2 = dy.reshape(-1, N)
-        if dy2.dtype != wc.dtype:
-            dy2 = dy2.to(wc.dtype)
+        if dy.dtype != wc.dtype and wc.dtype == torch.bfloat16:
+            dy2 = _bf16_of(dy).reshape(-1, N)   # the junction's bf16 copy when the gradient carries one
+        else:
+            dy2 = dy.reshape(-1, N)
+            if dy2.dtype != wc.dtype:
+                dy2 = dy2.to(wc.dtype)
         dy2 = dy2.contiguous()
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
@@ -558,12 +561,12 @@ class _LinearFn(torch.autograd.Function):
                 dw = dwf.to(wdt)
             if bdt is not None and ctx.needs_input_grad[2]:
                 db = dbf.to(bdt)
-            return dx, dw, db, None, None
+            return dx, dw, db, None, None, None
         if ctx.needs_input_grad[1]:
             dw = _splitk_wgrad(dy2, xc.reshape(-1, K)).to(wdt)
         if bdt is not None and ctx.needs_input_grad[2]:
             db = colsum(dy2).to(bdt)
-        return dx, dw, db, None, None
+        return dx, dw, db, None, None, None
 
 
 class _LinearResidualFn(torch.autograd.Function):
@@ -640,52 +643,78 @@ def mlp_residual(res, x, fc1: torch.nn.Linear, fc2: torch.nn.Linear):
 class CastCache:
     """bf16 shadow copies of fp32 master weights, refreshed once per forward by ONE launch of
     csu_cast_bf16_batch (instead of one cast kernel per Linear), plus a transposed (K, N) copy of
-    every 2-D weight for the input-gradient GEMM.  Gradients still flow to the fp32 params.
-    Lookup is by storage address, so reshaped views of a cached weight (the CARAFE 1x1 convs used
-    as token Linears) hit the cache too."""
+    every 2-D weight for the input-gradient GEMM, and the two channels-last layouts (OHWI, IHWO)
+    of every KxK conv weight for the implicit-GEMM conv kernels.  Gradients still flow to the fp32
+    params.  Lookup is by storage address, so reshaped views of a cached weight (the CARAFE 1x1
+    convs used as token Linears) hit the cache too."""
+
+    _REC = None
 
     def __init__(self):
         self.params, self.shadow, self.shadow_t, self.dtype = [], [], [], None
-        self.index, self.ptrs = {}, []
+        self.convs, self.conv_o, self.conv_i = [], [], []
+        self.index, self.cindex, self.ptrs = {}, {}, []
         self.items, self.tiles = None, 0
 
-    def _build(self, params, dtype):
-        self.params, self.dtype = params, dtype
-        self.ptrs = [p.data_ptr() for p in params]
+    @classmethod
+    def _rec(cls):
+        import numpy as np
+        if cls._REC is None:
+            cls._REC = np.dtype([("src", "<u8"), ("dst", "<u8"), ("dst_t", "<u8"), ("rows", "<i4"), ("cols", "<i4"),
+                                 ("tile0", "<i8"), ("taps", "<i4"), ("pad", "<i4")])
+        return cls._REC
+
+    def _build(self, params, convs, dtype):
+        self.params, self.convs, self.dtype = params, convs, dtype
+        self.ptrs = [p.data_ptr() for p in params + convs]
         self.shadow = [torch.empty(p.shape, dtype=dtype, device=p.device) for p in params]
         self.shadow_t = [torch.empty(p.shape[1:].numel() if p.dim() > 1 else 0, p.shape[0], dtype=dtype, device=p.device)
                          if p.dim() > 1 else None for p in params]
+        self.conv_o = [torch.empty(w.shape[0], w.shape[2], w.shape[3], w.shape[1], dtype=dtype, device=w.device) for w in convs]
+        self.conv_i = [torch.empty(w.shape[1], w.shape[2], w.shape[3], w.shape[0], dtype=dtype, device=w.device) for w in convs]
         self.index = {p.data_ptr(): i for i, p in enumerate(params)}
+        self.cindex = {w.data_ptr(): i for i, w in enumerate(convs)}
         self.items = None
-        if (dtype == torch.bfloat16 and params and all(p.is_cuda and p.dtype == torch.float32 and p.is_contiguous()
-                                                       for p in params)):
+        allp = params + convs
+        if (dtype == torch.bfloat16 and allp and all(p.is_cuda and p.dtype == torch.float32 and p.is_contiguous()
+                                                     for p in allp)):
             import numpy as np
-            rec = np.zeros(len(params), dtype=np.dtype([("src", "<u8"), ("dst", "<u8"), ("dst_t", "<u8"),
-                                                          ("rows", "<i4"), ("cols", "<i4"), ("tile0", "<i8")]))
+            rec = np.zeros(len(allp), dtype=self._rec())
             t0 = 0
             for i, p in enumerate(params):
                 rows = p.shape[0] if p.dim() > 1 else 1
                 cols = p.numel() // rows
                 st = self.shadow_t[i]
-                rec[i] = (p.data_ptr(), self.shadow[i].data_ptr(), 0 if st is None else st.data_ptr(), rows, cols, t0)
+                rec[i] = (p.data_ptr(), self.shadow[i].data_ptr(), 0 if st is None else st.data_ptr(), rows, cols, t0, 0, 0)
                 t0 += -(-rows // 64) * -(-cols // 64)
+            for j, w in enumerate(convs):
+                N, C, KH, KW = w.shape
+                rec[len(params) + j] = (w.data_ptr(), self.conv_o[j].data_ptr(), self.conv_i[j].data_ptr(), N, C, t0,
+                                        KH * KW, 0)
+                t0 += -(-(N * C * KH * KW) // 4096)
             self.tiles = t0
-            self.items = torch.frombuffer(bytearray(rec.tobytes()), dtype=torch.uint8).to(params[0].device)
+            self.items = torch.frombuffer(bytearray(rec.tobytes()), dtype=torch.uint8).to(allp[0].device)
 
-    def refresh(self, params, dtype):
-        params = list(params)
-        if (self.dtype != dtype or len(params) != len(self.params) or any(a is not b for a, b in zip(params, self.params))
-                or any(p.data_ptr() != q for p, q in zip(params, self.ptrs))):
-            self._build(params, dtype)
+    def refresh(self, params, dtype, convs=()):
+        params, convs = list(params), list(convs)
+        allp = params + convs
+        if (self.dtype != dtype or len(params) != len(self.params) or len(convs) != len(self.convs)
+                or any(a is not b for a, b in zip(allp, self.params + self.convs))
+                or any(p.data_ptr() != q for p, q in zip(allp, self.ptrs))):
+            self._build(params, convs, dtype)
         if self.items is not None:
-            check(lib().csu_cast_bf16_batch(ptr(self.items), len(self.params), self.tiles,
-                                            stream_ptr(self.params[0].device)), "csu_cast_bf16_batch")
+            check(lib().csu_cast_bf16_batch(ptr(self.items), len(allp), self.tiles, stream_ptr(allp[0].device)),
+                  "csu_cast_bf16_batch")
             return
         with torch.no_grad():
-            torch._foreach_copy_(self.shadow, [p.detach() for p in self.params])
+            if self.params:
+                torch._foreach_copy_(self.shadow, [p.detach() for p in self.params])
             for st, p in zip(self.shadow_t, self.params):
                 if st is not None:
                     st.copy_(p.detach().reshape(p.shape[0], -1).t())
+            for w, o, i in zip(self.convs, self.conv_o, self.conv_i):
+                o.copy_(w.detach().permute(0, 2, 3, 1))
+                i.copy_(w.detach().permute(1, 2, 3, 0))
 
     def get(self, p, dtype):
         i = self.index.get(p.data_ptr())
@@ -701,6 +730,13 @@ class CastCache:
         st = self.shadow_t[i]
         return st if tuple(st.shape) == (p.shape[1], p.shape[0]) else None
 
+    def get_conv(self, w, dtype):
+        """(OHWI, IHWO) bf16 layouts of a cached conv weight, or None."""
+        j = self.cindex.get(w.data_ptr())
+        if j is None or self.dtype != dtype or tuple(self.convs[j].shape) != tuple(w.shape):
+            return None
+        return self.conv_o[j], self.conv_i[j]
+
 
 _ACTIVE_CACHE: Optional[CastCache] = None
 
@@ -710,15 +746,18 @@ def set_cast_cache(cache: Optional[CastCache]):
     _ACTIVE_CACHE = cache
 
 
-def linear(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """nn.Linear on tokens in the autocast compute dtype (bf16 under autocast) with split-K dW."""
+def linear(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None,
+           out_dtype: Optional[torch.dtype] = None) -> torch.Tensor:
+    """nn.Linear on tokens in the autocast compute dtype (bf16 under autocast) with split-K dW.
+    ``out_dtype`` (bf16 path only): write the output in that dtype from the fp32 accumulator, e.g.
+    fp32 for a Linear that starts a residual stream."""
     if x.is_cuda and torch.is_autocast_enabled("cuda"):
         cd = torch.get_autocast_dtype("cuda")
     else:
         cd = torch.promote_types(x.dtype, weight.dtype)
     wc = _ACTIVE_CACHE.get(weight, cd) if _ACTIVE_CACHE is not None else None
     with torch.autocast("cuda", enabled=False):
-        return _LinearFn.apply(x, weight, bias, cd, wc)
+        return _LinearFn.apply(x, weight, bias, cd, wc, out_dtype)
 
 
 # ---------------------------------------------------------------------------------------------
@@ -754,12 +793,14 @@ class _Conv2dFn(torch.autograd.Function):
         if Cw != C:
             raise ValueError(f"conv2d: input has {C} channels, weight expects {Cw}")
         g = _conv_geom(B, H, W, C, N, KH, KW, stride, pad)
-        w_ohwi = weight.detach().permute(0, 2, 3, 1).to(cd).contiguous()
+        cached = _ACTIVE_CACHE.get_conv(weight, cd) if _ACTIVE_CACHE is not None else None
+        w_ohwi = cached[0] if cached else weight.detach().permute(0, 2, 3, 1).to(cd).contiguous()
         y = torch.empty(B, g.OH, g.OW, N, dtype=cd, device=x.device)
         bf = None if bias is None else bias.detach().float().contiguous()
         check(lib().csu_conv2d_fwd(ctypes.byref(g), dtype_code(xc), ptr(xc), ptr(w_ohwi), ptr(bf), ptr(y),
                                    stream_ptr(x.device)), "csu_conv2d_fwd")
         ctx.save_for_backward(xc, weight)
+        ctx.w_ihwo = cached[1] if cached else None   # refreshed only by the next forward's cast
         ctx.conf = (stride, pad, cd, x.dtype, bias is not None, None if bias is None else bias.dtype)
         return y
 
@@ -773,7 +814,7 @@ class _Conv2dFn(torch.autograd.Function):
         dy = dy.to(cd).contiguous()
         dx = None
         if ctx.needs_input_grad[0]:
-            w_ihwo = weight.detach().permute(1, 2, 3, 0).to(cd).contiguous()
+            w_ihwo = ctx.w_ihwo if ctx.w_ihwo is not None else weight.detach().permute(1, 2, 3, 0).to(cd).contiguous()
             dx = torch.empty(B, H, W, C, dtype=cd, device=dy.device)
             check(lib().csu_conv2d_dgrad(ctypes.byref(g), dtype_code(dy), ptr(dy), ptr(w_ihwo), None, ptr(dx),
                                          stream_ptr(dy.device)), "csu_conv2d_dgrad")

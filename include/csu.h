@@ -220,6 +220,9 @@ typedef struct {
     void* dst_t;
     int32_t rows, cols;
     int64_t tile0;
+    int32_t taps;   /* 0: matrix item.  > 0: conv weight src (rows=N, cols=C, taps=KH*KW) -> dst = OHWI
+                       [N][KH][KW][C], dst_t = IHWO [C][KH][KW][N] (or NULL); ceil(N*C*taps/4096) tiles */
+    int32_t pad_;
 } csu_cast_item;
 int csu_cast_bf16_batch(const csu_cast_item* items, int count, long total_tiles, void* stream);
 

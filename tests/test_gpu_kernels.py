@@ -376,18 +376,24 @@ def test_cast_cache_batch_kernel():
     torch.manual_seed(3)
     ps = [torch.randn(192, 64, device=d), torch.randn(70, device=d), torch.randn(16, 64, 1, 1, device=d),
           torch.randn(130, 333, device=d), torch.randn(5, device=d)]
+    convs = [torch.randn(36, 16, 3, 3, device=d), torch.randn(64, 3, 7, 7, device=d), torch.randn(256, 128, 3, 3, device=d)]
     c = ops.CastCache()
-    c.refresh(ps, torch.bfloat16)
+    c.refresh(ps, torch.bfloat16, convs)
     assert c.items is not None
     for p in ps:
         torch.testing.assert_close(c.get(p, torch.bfloat16), p.bfloat16(), rtol=0, atol=0)
         if p.dim() > 1:
             v = p.reshape(p.shape[0], -1)
             torch.testing.assert_close(c.get_t(v, torch.bfloat16), v.t().bfloat16(), rtol=0, atol=0)
+    for w in convs:   # channels-last conv layouts written by the same launch
+        o, i = c.get_conv(w, torch.bfloat16)
+        assert torch.equal(o, w.permute(0, 2, 3, 1).bfloat16()) and torch.equal(i, w.permute(1, 2, 3, 0).bfloat16())
     with torch.no_grad():
         ps[0].mul_(2)
-    c.refresh(ps, torch.bfloat16)
+        convs[1].mul_(3)
+    c.refresh(ps, torch.bfloat16, convs)
     torch.testing.assert_close(c.get(ps[0], torch.bfloat16), ps[0].bfloat16(), rtol=0, atol=0)
+    assert torch.equal(c.get_conv(convs[1], torch.bfloat16)[0], convs[1].permute(0, 2, 3, 1).bfloat16())
 
 
 def test_fused_mlp_residual_matches_unfused():
