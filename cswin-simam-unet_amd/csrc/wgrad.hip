@@ -108,15 +108,17 @@ __global__ __launch_bounds__(NT) void wgrad_kernel(long M, int N, int K, long ro
 // bf16 fast path: row-major LDS tiles filled by coalesced 16-B loads (prefetched one step ahead
 // in registers), MFMA fragments gathered with the gfx950 transposing read ds_read_b64_tr_b16
 // (lane 4q+p of a 16-lane group addresses row q, columns 4p..4p+3; lane i receives column i of
-// the 4 rows).  192-B rows make the transposed reads bank-conflict free.
+// the 4 rows).  Rows padded by 64 B make the transposed reads of 4 rows bank-conflict free.
+// Tile T x T (T = 64 or 128) per workgroup, each wave (T/2) x (T/2): at T = 128 every fragment
+// feeds two MFMAs and the operand panels are re-read half as often (N/T + K/T passes).
 typedef short v4s __attribute__((ext_vector_type(4)));
-constexpr int RS = 96;   // bf16 elements per LDS row (64 data + 32 pad)
 
 __device__ __forceinline__ v4s tr_read(const bf16* p) {
     return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(p));
 }
 
 // 32x32x16 operand fragment of columns [c0, c0+32) at k-step rows [16s + 8h, +8) of a [TM][RS] tile
+template <int RS>
 __device__ __forceinline__ bf16x8 tr_frag(const bf16* img, int c0, int s, int lane) {
     const int grp = lane >> 4, l = lane & 15, q = l >> 2, p = l & 3;
     const int col = c0 + 16 * (grp & 1) + 4 * p;
@@ -131,50 +133,58 @@ __device__ __forceinline__ bf16x8 tr_frag(const bf16* img, int c0, int s, int la
 
 __device__ __forceinline__ float gelu_w(float v) { return 0.5f * v * (1.f + erff(v * 0.70710678118654752f)); }
 
-template <bool GELU_X>
+template <int T, bool GELU_X>
 __global__ __launch_bounds__(NT) void wgrad_bf16_tr(long M, int N, int K, long rows_per_chunk, const bf16* __restrict__ dy,
                                                    const bf16* __restrict__ x, float* __restrict__ part) {
+    constexpr int RS = T + 32;          // bf16 elements per LDS row (T data + 64 B pad)
+    constexpr int CPR = T / 8;          // 16-B chunks per row
+    constexpr int RPP = NT / CPR;       // rows per pass of the workgroup
+    constexpr int NP = TM / RPP;        // passes (chunks per thread per operand)
+    constexpr int AT = T / 64;          // 32x32 tiles per wave per dim
     __shared__ __attribute__((aligned(16))) bf16 At[TM * RS];   // dY tile [m][n]
     __shared__ __attribute__((aligned(16))) bf16 Bt[TM * RS];   // X  tile [m][k]
     __shared__ float bred[NT][9];
     // tiles of one token chunk are consecutive logical ids -> one XCD reads the chunk once
-    const int nt = (N + TN - 1) / TN, kt = (K + TK - 1) / TK;
+    const int nt = (N + T - 1) / T, kt = (K + T - 1) / T;
     const long t = xcd_tile(blockIdx.x, gridDim.x);
     const int chunk = (int)(t / (nt * kt)), tt = (int)(t % (nt * kt));
-    const int n0 = (tt / kt) * TN, k0 = (tt % kt) * TK;
+    const int n0 = (tt / kt) * T, k0 = (tt % kt) * T;
     const long m_begin = (long)chunk * rows_per_chunk;
     const long m_end = min(M, m_begin + rows_per_chunk);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int r = lane & 31, h = lane >> 5;
-    const int wn = (wave >> 1) * 32, wk = (wave & 1) * 32;
+    const int wn = (wave >> 1) * (T / 2), wk = (wave & 1) * (T / 2);
     const bool do_bias = k0 == 0;
-    // this thread's two 16-B chunks per operand: chunk c = tid + 256 i -> row c / 8, column group c % 8
-    const int cg = threadIdx.x & 7, rr = threadIdx.x >> 3;   // rows rr and rr + 32
+    const int cg = threadIdx.x % CPR, rr = threadIdx.x / CPR;   // rows rr + RPP i
     const bool nv = n0 + 8 * cg < N, kv = k0 + 8 * cg < K;
-    bf16x8 ra[2], rb[2];
+    bf16x8 ra[NP], rb[NP];
     float bsum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     auto load = [&](long m0) {
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const long m = m0 + rr + 32 * i;
+        for (int i = 0; i < NP; ++i) {
+            const long m = m0 + rr + RPP * i;
             const bool mv = m < m_end;
             ra[i] = (mv && nv) ? *reinterpret_cast<const bf16x8*>(dy + m * N + n0 + 8 * cg) : bf16x8{};
             rb[i] = (mv && kv) ? *reinterpret_cast<const bf16x8*>(x + m * K + k0 + 8 * cg) : bf16x8{};
         }
     };
-    f32x16 acc = {};
+    f32x16 acc[AT][AT];
+#pragma unroll
+    for (int a = 0; a < AT; ++a)
+#pragma unroll
+        for (int b = 0; b < AT; ++b) acc[a][b] = f32x16{};
     load(m_begin);
     for (long m0 = m_begin; m0 < m_end; m0 += TM) {
         __syncthreads();
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            *reinterpret_cast<bf16x8*>(At + (rr + 32 * i) * RS + 8 * cg) = ra[i];
+        for (int i = 0; i < NP; ++i) {
+            *reinterpret_cast<bf16x8*>(At + (rr + RPP * i) * RS + 8 * cg) = ra[i];
             bf16x8 xv = rb[i];
             if constexpr (GELU_X) {   // X = gelu(h) on the fly (fc2's input, never materialised)
 #pragma unroll
                 for (int j = 0; j < 8; ++j) xv[j] = (bf16)gelu_w((float)xv[j]);
             }
-            *reinterpret_cast<bf16x8*>(Bt + (rr + 32 * i) * RS + 8 * cg) = xv;
+            *reinterpret_cast<bf16x8*>(Bt + (rr + RPP * i) * RS + 8 * cg) = xv;
             if (do_bias)
 #pragma unroll
                 for (int j = 0; j < 8; ++j) bsum[j] += (float)ra[i][j];
@@ -183,41 +193,69 @@ __global__ __launch_bounds__(NT) void wgrad_bf16_tr(long M, int N, int K, long r
         if (m0 + TM < m_end) load(m0 + TM);      // next step's loads fly during the MFMAs
 #pragma unroll
         for (int s = 0; s < TM / 16; ++s) {
-            const bf16x8 a = tr_frag(At, wn, s, lane);
-            const bf16x8 b = tr_frag(Bt, wk, s, lane);
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc, 0, 0, 0);
+            bf16x8 fa[AT], fb[AT];
+#pragma unroll
+            for (int a = 0; a < AT; ++a) fa[a] = tr_frag<RS>(At, wn + 32 * a, s, lane);
+#pragma unroll
+            for (int b = 0; b < AT; ++b) fb[b] = tr_frag<RS>(Bt, wk + 32 * b, s, lane);
+#pragma unroll
+            for (int a = 0; a < AT; ++a)
+#pragma unroll
+                for (int b = 0; b < AT; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[a], fb[b], acc[a][b], 0, 0, 0);
         }
     }
     const long slab = (long)N * K + N;
     float* out = part + (long)chunk * slab;
 #pragma unroll
-    for (int reg = 0; reg < 16; ++reg) {
-        const int n = n0 + wn + crow(reg, h), k = k0 + wk + r;
-        if (n < N && k < K) out[(long)n * K + k] = acc[reg];
-    }
+    for (int a = 0; a < AT; ++a)
+#pragma unroll
+        for (int b = 0; b < AT; ++b)
+#pragma unroll
+            for (int reg = 0; reg < 16; ++reg) {
+                const int n = n0 + wn + 32 * a + crow(reg, h), k = k0 + wk + 32 * b + r;
+                if (n < N && k < K) out[(long)n * K + k] = acc[a][b][reg];
+            }
     if (do_bias) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) bred[threadIdx.x][j] = bsum[j];
         __syncthreads();
-        if (threadIdx.x < 64) {
+        if (threadIdx.x < T) {
             const int g = threadIdx.x >> 3, j = threadIdx.x & 7;   // column n0 + 8g + j
-            float s = 0.f;
-            for (int t = g; t < NT; t += 8) s += bred[t][j];
-            if (n0 + 8 * g + j < N) out[(long)N * K + n0 + 8 * g + j] = s;
+            float sum = 0.f;
+            for (int q = g; q < NT; q += CPR) sum += bred[q][j];
+            if (n0 + 8 * g + j < N) out[(long)N * K + n0 + 8 * g + j] = sum;
         }
     }
 }
 
 struct WPlan {
-    int nt, kt, chunks;
+    int t, nt, kt, chunks;
     long rpc;
 };
 
-WPlan wplan(long M, int N, int K) {
+// bf16 tiles: 128 x 128 when both N and K allow it (half the operand re-reads of 64 x 64), else
+// 64 x 64; fp32 path 64 x 64.  ~1024 workgroups, >= 512 tokens per chunk.
+int env_int(const char* name, int dflt) {
+    const char* e = getenv(name);
+    return e ? atoi(e) : dflt;
+}
+int wgrad_tile_env() {   // CSU_WGRAD_T=64|128 forces the tile (A/B comparisons)
+    static int v = env_int("CSU_WGRAD_T", 0);
+    return v;
+}
+int wgrad_target_env() {   // CSU_WGRAD_WGS: target workgroup count of the split-K plan
+    static int v = env_int("CSU_WGRAD_WGS", 1024);
+    return v;
+}
+
+WPlan wplan(long M, int N, int K, bool bf16_path) {
     WPlan p;
-    p.nt = (N + TN - 1) / TN;
-    p.kt = (K + TK - 1) / TK;
-    long want = (1024 + p.nt * p.kt - 1) / (p.nt * p.kt);
+    const int te = wgrad_tile_env();
+    p.t = (bf16_path && N >= 128 && K >= 128 && te != 64) ? 128 : 64;
+    p.nt = (N + p.t - 1) / p.t;
+    p.kt = (K + p.t - 1) / p.t;
+    const long target = wgrad_target_env();
+    long want = (target + p.nt * p.kt - 1) / (p.nt * p.kt);
     const long maxc = (M + 511) / 512;          // >= 512 tokens per chunk
     if (want > maxc) want = maxc;
     if (want > 256) want = 256;
@@ -250,9 +288,13 @@ static bool use_wgrad4() {
 }
 
 extern "C" size_t csu_linear_wgrad_workspace(long M, int N, int K) {
-    const WPlan p = wplan(M, N, K);
     const long slab = (long)N * K + N;
-    const size_t a = (size_t)p.chunks * slab * sizeof(float) + colsum_workspace(p.chunks, slab, CSU_F32);
+    size_t a = 0;
+    for (int bf = 0; bf < 2; ++bf) {   // the dtype is not an argument: the larger of both plans
+        const WPlan p = wplan(M, N, K, bf == 1);
+        const size_t w = (size_t)p.chunks * slab * sizeof(float) + colsum_workspace(p.chunks, slab, CSU_F32);
+        a = w > a ? w : a;
+    }
     const size_t b = wgrad4_ok(M, N, K) ? wgrad4_workspace(M, N, K) : 0;
     return a > b ? a : b;
 }
@@ -274,16 +316,18 @@ extern "C" int csu_linear_wgrad_ex(long M, int N, int K, int dtype, const void* 
     hipStream_t st = as_stream(stream);
     if (dtype == CSU_BF16 && !x_gelu && use_wgrad4() && wgrad4_ok(M, N, K))
         return wgrad4_run(M, N, K, (const bf16*)dy, (const bf16*)x, dw_db, workspace, st);
-    const WPlan p = wplan(M, N, K);
+    const WPlan p = wplan(M, N, K, dtype == CSU_BF16);
     float* part = (float*)workspace;
     const long slab = (long)N * K + N;
     const dim3 grid(p.nt, p.kt, p.chunks);
     if (x_gelu && dtype != CSU_BF16) return fail(CSU_E_UNSUPPORTED, "linear_wgrad: GELU prologue is bf16-only");
     const dim3 grid1((unsigned)(p.nt * p.kt * p.chunks));
-    if (dtype == CSU_BF16 && x_gelu)
-        wgrad_bf16_tr<true><<<grid1, NT, 0, st>>>(M, N, K, p.rpc, (const bf16*)dy, (const bf16*)x, part);
-    else if (dtype == CSU_BF16)
-        wgrad_bf16_tr<false><<<grid1, NT, 0, st>>>(M, N, K, p.rpc, (const bf16*)dy, (const bf16*)x, part);
+    const bf16* dyb = (const bf16*)dy;
+    const bf16* xb = (const bf16*)x;
+    if (dtype == CSU_BF16 && p.t == 128 && x_gelu) wgrad_bf16_tr<128, true><<<grid1, NT, 0, st>>>(M, N, K, p.rpc, dyb, xb, part);
+    else if (dtype == CSU_BF16 && p.t == 128) wgrad_bf16_tr<128, false><<<grid1, NT, 0, st>>>(M, N, K, p.rpc, dyb, xb, part);
+    else if (dtype == CSU_BF16 && x_gelu) wgrad_bf16_tr<64, true><<<grid1, NT, 0, st>>>(M, N, K, p.rpc, dyb, xb, part);
+    else if (dtype == CSU_BF16) wgrad_bf16_tr<64, false><<<grid1, NT, 0, st>>>(M, N, K, p.rpc, dyb, xb, part);
     else if (dtype == CSU_F32)
         wgrad_kernel<float><<<grid, NT, 0, st>>>(M, N, K, p.rpc, (const float*)dy, (const float*)x, part);
     else
