@@ -139,6 +139,53 @@ __device__ __forceinline__ void buf_ld4bf(__amdgpu_buffer_rsrc_t rs, unsigned of
     v[0] = (float)b[0]; v[1] = (float)b[1]; v[2] = (float)b[2]; v[3] = (float)b[3];
 }
 
+// GELU (exact-erf form of nn.GELU) with erf by Abramowitz-Stegun 7.1.26 (|abs err| < 1.5e-7):
+// one v_exp + one v_rcp (the hardware 1-ulp reciprocal: __frcp_rn expands to the ~10-instruction
+// correctly rounded division sequence).  gelu_pair_as returns gelu and gelu' sharing both.
+__device__ __forceinline__ float erf_poly_as(float t) {
+    return t * (0.254829592f + t * (-0.284496736f + t * (1.421413741f + t * (-1.453152027f + t * 1.061405429f))));
+}
+__device__ __forceinline__ float erf_as(float z) {   // z >= 0
+    const float t = __builtin_amdgcn_rcpf(1.f + 0.3275911f * z);
+    return 1.f - erf_poly_as(t) * __expf(-z * z);
+}
+__device__ __forceinline__ float gelu_as(float x) {
+    const float e = erf_as(fabsf(x) * 0.70710678118654752f);
+    return 0.5f * x * (1.f + (x >= 0.f ? e : -e));
+}
+__device__ __forceinline__ float gelu_grad_as(float x) {
+    const float e = erf_as(fabsf(x) * 0.70710678118654752f);
+    return 0.5f * (1.f + (x >= 0.f ? e : -e)) + x * 0.3989422804014327f * __expf(-0.5f * x * x);
+}
+__device__ __forceinline__ void gelu_pair_as(float x, float& g, float& dg) {
+    const float z = fabsf(x) * 0.70710678118654752f;
+    const float ex = __expf(-z * z);                  // = exp(-x^2 / 2)
+    const float e = 1.f - erf_poly_as(__builtin_amdgcn_rcpf(1.f + 0.3275911f * z)) * ex;
+    const float phi2 = 0.5f * (1.f + (x >= 0.f ? e : -e));   // Phi(x)
+    g = x * phi2;
+    dg = phi2 + x * 0.3989422804014327f * ex;
+}
+
+// Cheaper GELU for the bf16 paths: 0.5 erfc(|x|/sqrt2) by Abramowitz-Stegun 7.1.25 (|err| <
+// 1.25e-5 on Phi, far below bf16 resolution): one v_rcp, one v_exp, ~10 mostly packable ops.
+__device__ __forceinline__ float half_erfc_as(float x, float& ex) {   // 0.5 erfc(|x| / sqrt2); ex = exp(-x^2/2)
+    const float t = __builtin_amdgcn_rcpf(fmaf(0.33267904f, fabsf(x), 1.f));   // p = 0.47047 / sqrt2
+    ex = __builtin_amdgcn_exp2f(-0.72134752f * (x * x));
+    return t * (0.1740121f + t * (-0.0479399f + t * 0.3739278f)) * ex;
+}
+__device__ __forceinline__ float gelu_fast(float x) {
+    float ex;
+    const float q = half_erfc_as(x, ex);
+    return x * (x >= 0.f ? 1.f - q : q);
+}
+__device__ __forceinline__ void gelu_pair_fast(float x, float& g, float& dg) {
+    float ex;
+    const float q = half_erfc_as(x, ex);
+    const float phi = x >= 0.f ? 1.f - q : q;
+    g = x * phi;
+    dg = fmaf(x * 0.3989422804014327f, ex, phi);
+}
+
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 }  // namespace csu

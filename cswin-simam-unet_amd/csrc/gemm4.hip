@@ -32,21 +32,6 @@ enum { G4_PLAIN = 0, G4_GELU_OUT = 1, G4_GAUX = 2, G4_RESID = 3 };
 // element offset of 16-B chunk `chunk` of row `row` in a swizzled [rows][64] bf16 image
 __device__ __forceinline__ int g4_off(int row, int chunk) { return row * G4_BK + ((chunk ^ (row & 7)) << 3); }
 
-// erf(|x|/sqrt2) by Abramowitz-Stegun 7.1.26 (|abs err| < 1.5e-7)
-__device__ __forceinline__ float g4_erf(float z) {   // z >= 0
-    const float t = __frcp_rn(1.f + 0.3275911f * z);
-    const float p = t * (0.254829592f + t * (-0.284496736f + t * (1.421413741f + t * (-1.453152027f + t * 1.061405429f))));
-    return 1.f - p * __expf(-z * z);
-}
-__device__ __forceinline__ float g4_gelu(float x) {
-    const float e = g4_erf(fabsf(x) * 0.70710678118654752f);
-    return 0.5f * x * (1.f + (x >= 0.f ? e : -e));
-}
-__device__ __forceinline__ float g4_gelu_grad(float x) {
-    const float e = g4_erf(fabsf(x) * 0.70710678118654752f);
-    return 0.5f * (1.f + (x >= 0.f ? e : -e)) + x * 0.3989422804014327f * __expf(-0.5f * x * x);
-}
-
 // Per-lane byte offsets of the DMA of a ROWS x 64 bf16 slice (rows 0.., k 0..63 relative to the
 // slice origin) of a row-major matrix with leading dimension ld into a swizzled [ROWS][64] image:
 // wave instruction i of this wave fills image rows rb..rb+7 (rb = (wave * ROWS/32 + i) * 8), lane l
@@ -272,7 +257,7 @@ __global__ __launch_bounds__(G4_NT, OCC) void gemm4_kernel(long M, int N, int K,
                 }
                 if constexpr (EPI == G4_GAUX) {
 #pragma unroll
-                    for (int e = 0; e < 8; ++e) v[e] *= g4_gelu_grad(pre[i][q][e]);
+                    for (int e = 0; e < 8; ++e) v[e] *= gelu_grad_as(pre[i][q][e]);
                 } else if constexpr (EPI == G4_RESID) {
 #pragma unroll
                     for (int e = 0; e < 8; ++e) v[e] += pre[i][q][e];
@@ -286,7 +271,7 @@ __global__ __launch_bounds__(G4_NT, OCC) void gemm4_kernel(long M, int N, int K,
                 }
                 if constexpr (EPI == G4_GELU_OUT) {
 #pragma unroll
-                    for (int e = 0; e < 8; ++e) v[e] = g4_gelu(v[e]);
+                    for (int e = 0; e < 8; ++e) v[e] = gelu_as(v[e]);
                     buf_st8bf(rs_g, o == kOOB ? kOOB : o * 2, v);
                 }
             }

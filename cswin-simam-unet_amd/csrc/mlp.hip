@@ -1,0 +1,537 @@
+// Fused Mlp + residual for gfx950: fc1 -> GELU -> fc2 with the 4C-wide hidden layer kept on chip.
+//
+//   forward   y  = res + fc2(gelu(fc1(x)))                     (Mlp cswin:180-196, residual cswin:368)
+//   backward  h  = fc1(x) (recomputed), g = gelu(h)
+//             dH = (dY W2) * gelu'(h),  dX = dH W1             (the two input-gradient GEMMs + GELU')
+//             writes dH and g for the weight-gradient GEMMs dW1 = dH^T x, dW2 = dY^T g
+//
+// The unfused form moves the hidden layer (M x 4C bf16) through HBM three times in the forward
+// (h and gelu(h) written, gelu(h) read) and three more in the backward; here the forward reads x
+// and res and writes y only, and the backward reads x and dY and writes dH, g and dX.
+//
+// Design (MI355X):
+//  * one workgroup (4 waves) per 64-token panel.  Wave (t, u) owns tokens 32t..32t+31 and, of
+//    every 64-feature hidden chunk j, the 32 features 32u..32u+31: GEMM1 H = W1_sub x^T (K = C),
+//    GELU on the accumulator, GEMM2 y_u += W2_sub g^T (K = 32) into a C x 32 partial output.
+//    The two hidden halves' partials are added through LDS once, at the end.
+//  * the token operands (x, dY) are loaded once into registers as MFMA B fragments; the weights
+//    stream through a two-stage LDS ring (W1 chunk [64][C] + W2 chunk [C][64] per stage,
+//    buffer_load ... lds DMA issued one chunk ahead, one barrier per chunk).
+//  * the hidden activations never leave registers: the accumulator of lane (r, h) holds token r,
+//    features 16s+4h+0..3 and 16s+8+4h+0..3 of k-step s, which is used directly as the B operand
+//    of the next GEMM with the SAME permutation of k applied to the A operand (two 8-B reads, or
+//    two transposed reads, of the weight image instead of one 16-B read): a contraction does not
+//    care about the order of k.
+//  * XOR swizzle of the 16-B chunks of every weight image (applied to the DMA source address),
+//    key = bit-reversal of the row: ds_read_b128 row reads and ds_read_b64_tr_b16 transposed
+//    reads are both bank-conflict free.
+//  * v_mfma_f32_32x32x16_bf16 with weights as the A operand: lane (r, h) of an accumulator holds
+//    token r and 4 consecutive features per register group; bias / GELU / GELU' / residual are
+//    elementwise on registers.
+#include "common.hpp"
+
+// m0 is reserved (not saved around asm); the DMA asm sets it right before use and nothing in
+// these kernels keeps a live value in it
+#pragma clang diagnostic ignored "-Winline-asm"
+
+#include <type_traits>
+
+namespace csu {
+namespace {
+
+constexpr int MT = 256;   // threads (4 waves)
+constexpr int BM = 64;    // tokens per workgroup
+constexpr int HC = 64;    // hidden features per chunk
+
+// swizzle key of an image row.  RB = bytes per row.  128-B rows: two rows share a 256-B bank row,
+// key = bitrev3((row >> 1) & 7); >= 256-B rows: key = bitrev4(row & 15).
+template <int RB>
+__device__ __forceinline__ int mkey(int row) {
+    if constexpr (RB == 128) {
+        const int v = (row >> 1) & 7;
+        return ((v & 1) << 2) | (v & 2) | ((v >> 2) & 1);
+    } else {
+        const int v = row & 15;
+        return ((v & 1) << 3) | ((v & 2) << 1) | ((v >> 1) & 2) | ((v >> 3) & 1);
+    }
+}
+// element offset of column `col` (bf16) of row `row` in a swizzled [rows][RB/2] image
+template <int RB>
+__device__ __forceinline__ int moff(int row, int col) {
+    return row * (RB / 2) + ((((col >> 3) ^ mkey<RB>(row))) << 3) + (col & 7);
+}
+
+// DMA of an R-row image of RB-byte rows from a row-major bf16 matrix (leading dimension ld
+// elements): wave instruction i of wave w fills image bytes [(w * NW + i) * 1024, +1024); lane l
+// the 16 B at + 16 l = row p / RB, slot (p % RB) / 16, whose source chunk is slot ^ key(row).
+template <int R, int RB>
+struct Dma {
+    static constexpr int NW = R * RB / 4096;   // instructions per wave
+    static_assert(NW >= 1 && R * RB % 4096 == 0, "image must be a multiple of 4 KB");
+    unsigned v[NW];
+    __device__ __forceinline__ void init(int ld, int wave, int lane) {
+#pragma unroll
+        for (int i = 0; i < NW; ++i) {
+            const int p = (wave * NW + i) * 1024 + lane * 16;
+            const int row = p / RB, slot = (p % RB) >> 4;
+            v[i] = (unsigned)row * ld * 2 + ((slot ^ mkey<RB>(row)) << 4);
+        }
+    }
+};
+
+// buffer resource words (base, num_records, raw-buffer flags as buf_rsrc) for inline asm
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ i32x4 rsrc4(const void* base, long bytes) {
+    const unsigned long a = reinterpret_cast<unsigned long>(base);
+    return i32x4{(int)(unsigned)a, (int)((a >> 32) & 0xffff), (int)(bytes < 0x7fffffffL ? bytes : 0x7fffffffL), 0x00020000};
+}
+
+// Issue the DMA of image `img`: NW wave instructions at the per-lane offsets voff, k offset soff
+// (bytes).  Inline asm, not __builtin_amdgcn_raw_ptr_buffer_load_lds: the compiler cannot tell the
+// two ring stages apart and would put s_waitcnt vmcnt(0) before every later LDS read, exposing
+// the whole prefetch; completion is tracked by the explicit vmwait<> instead.  (Also a free
+// function: as a member of Dma, hipcc dropped the host stub of the kernel.)
+template <int NW>
+__device__ __forceinline__ void dma(i32x4 rs, const unsigned* voff, unsigned soff, bf16* img, int wave) {
+#pragma unroll
+    for (int i = 0; i < NW; ++i) {
+        const unsigned lds = (unsigned)reinterpret_cast<unsigned long>(
+            (__attribute__((address_space(3))) bf16*)(img + (wave * NW + i) * 512));
+        asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+                     :: "s"(lds), "v"(voff[i]), "s"(rs), "s"(soff) : "memory", "m0");
+    }
+}
+
+template <int N> __device__ __forceinline__ void vmwait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+
+// every wave's LDS traffic and (already waited-for) DMA visible to the workgroup
+__device__ __forceinline__ void lds_sync() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+__device__ __forceinline__ bf16x8 frag(const bf16* img, int off) { return *reinterpret_cast<const bf16x8*>(img + off); }
+
+typedef short v4s __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ v4s tr4(const bf16* p) {
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(p));
+}
+__device__ __forceinline__ bf16x8 cat8(v4s lo, v4s hi) {
+    const v4s v[2] = {lo, hi};
+    bf16x8 out;
+    __builtin_memcpy(&out, v, 16);
+    return out;
+}
+
+// 32x32x16 operand fragment A[i = c0 + (lane & 31)][k = 16 s + 8 h .. + 7] from an image whose
+// ROWS are k and COLUMNS are i (transposing read: lane 4q+p of a 16-lane group addresses row q,
+// columns 4p..4p+3; lane i of the group receives column i of the 4 rows).
+template <int RB>
+__device__ __forceinline__ bf16x8 trfrag(const bf16* img, int c0, int s, int lane) {
+    const int grp = lane >> 4, l = lane & 15, q = l >> 2, p = l & 3;
+    const int col = c0 + 16 * (grp & 1) + 4 * p;
+    const int row = 16 * s + 8 * (grp >> 1) + q;
+    return cat8(tr4(img + moff<RB>(row, col)), tr4(img + moff<RB>(row + 4, col)));
+}
+// the permuted-k form (see header): k = image rows k0 + 4h + 0..3 and k0 + 8 + 4h + 0..3
+template <int RB>
+__device__ __forceinline__ bf16x8 ptrfrag(const bf16* img, int c0, int k0, int lane) {
+    const int grp = lane >> 4, l = lane & 15, q = l >> 2, p = l & 3;
+    const int col = c0 + 16 * (grp & 1) + 4 * p;
+    const int row = k0 + 4 * (grp >> 1) + q;
+    return cat8(tr4(img + moff<RB>(row, col)), tr4(img + moff<RB>(row + 8, col)));
+}
+// permuted-k row fragment: row `row` of the image, k = columns k0 + 4h + 0..3, k0 + 8 + 4h + 0..3
+template <int RB>
+__device__ __forceinline__ bf16x8 pfrag(const bf16* img, int row, int k0, int h) {
+    const bf16x4 lo = *reinterpret_cast<const bf16x4*>(img + moff<RB>(row, k0 + 4 * h));
+    const bf16x4 hi = *reinterpret_cast<const bf16x4*>(img + moff<RB>(row, k0 + 8 + 4 * h));
+    return bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+// B operand of k-step s2 from accumulator-resident activations v (16 per lane, accumulator order)
+__device__ __forceinline__ bf16x8 pack_b(const float* v, int s2) {
+    bf16x8 b;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) b[i] = (bf16)v[8 * s2 + i];
+    return b;
+}
+
+// token-operand B fragments of 32 rows (lane: row r, k = 16 s + 8 h .. + 7); rows past the end
+// read as 0
+template <int C>
+__device__ __forceinline__ void load_bfrags(__amdgpu_buffer_rsrc_t rs, int tok, bool ok, int h, bf16x8* f) {
+#pragma unroll
+    for (int s = 0; s < C / 16; ++s) {
+        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, ok ? (unsigned)(tok * C + 16 * s + 8 * h) * 2 : kOOB, 0, 0);
+        __builtin_memcpy(&f[s], &v, 16);
+    }
+}
+
+// Add the partner wave's partial sums for this wave's half of the C x 32 output: acc[TF] holds the
+// wave's partial over its hidden half for all C features; afterwards acc[U*HT .. U*HT+HT-1] hold
+// the full sums of features [U*C/2, (U+1)*C/2).  xch: 4 x HT x 16 x 64 floats of LDS.
+template <int C, int U>
+__device__ __forceinline__ void exchange_half(f32x16* acc, float* xch, int wave, int lane) {
+    constexpr int HT = C / 64;
+#pragma unroll
+    for (int q = 0; q < HT; ++q)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) xch[((wave * HT + q) * 16 + e) * 64 + lane] = acc[(1 - U) * HT + q][e];
+    lds_sync();
+    const int partner = wave ^ 1;
+#pragma unroll
+    for (int q = 0; q < HT; ++q)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[U * HT + q][e] += xch[((partner * HT + q) * 16 + e) * 64 + lane];
+}
+
+template <int C, int U>
+__device__ __forceinline__ void fwd_epilogue(const f32x16* acc, __amdgpu_buffer_rsrc_t rs_res, __amdgpu_buffer_rsrc_t rs_out,
+                                             const float* b2, int tok, bool ok, int h) {
+    constexpr int HT = C / 64;
+#pragma unroll
+    for (int q = 0; q < HT; ++q)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int f = (U * HT + q) * 32 + 8 * g + 4 * h;
+            const unsigned off = ok ? (unsigned)(tok * C + f) * 4 : kOOB;
+            float rv[4], bv[4], v[4];
+            buf_ld4(rs_res, off, rv);
+            load4(b2 + f, bv);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = acc[U * HT + q][4 * g + e] + bv[e] + rv[e];
+            buf_st4(rs_out, off, v);
+        }
+}
+
+template <int C, int U>
+__device__ __forceinline__ void bwd_epilogue(const f32x16* acc, __amdgpu_buffer_rsrc_t rs_dx, int tok, bool ok, int h) {
+    constexpr int HT = C / 64;
+#pragma unroll
+    for (int q = 0; q < HT; ++q)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int f = (U * HT + q) * 32 + 8 * g + 4 * h;
+            float v[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = acc[U * HT + q][4 * g + e];
+            buf_st4bf(rs_dx, ok ? (unsigned)(tok * C + f) * 2 : kOOB, v);
+        }
+}
+
+// b1 of the accumulator layout: hidden base + crow(e, h), from the LDS copy (4 x ds_read_b128)
+__device__ __forceinline__ void bias16(const float* b1s, int base, int h, float* bv) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+        const f32x4 v = *reinterpret_cast<const f32x4*>(b1s + base + 8 * g + 4 * h);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) bv[4 * g + e] = v[e];
+    }
+}
+
+template <bool V> using bconst = std::integral_constant<bool, V>;
+template <int V> using iconst = std::integral_constant<int, V>;
+
+// Forward.  Rings: W1 chunks in 2 stages, W2 chunks in 2 stages.  Step j (after one barrier):
+// DMA W1(j+2), W2(j+1); GEMM1(j+1) on the MFMA pipe while GELU(j) runs on the VALU; GEMM2(j).
+template <int C>
+__global__ __launch_bounds__(MT) void mlp_fwd_kernel(long M, const bf16* __restrict__ X, const bf16* __restrict__ W1,
+                                                     const float* __restrict__ b1, const bf16* __restrict__ W2,
+                                                     const float* __restrict__ b2, const float* __restrict__ res,
+                                                     float* __restrict__ out) {
+    constexpr int NCH = 4 * C / HC;     // hidden chunks
+    constexpr int KS = C / 16;          // k-steps of GEMM1
+    constexpr int TF = C / 32;          // 32-feature output tiles (all C, partial over the hidden half)
+    constexpr int IMG = HC * C;         // bf16 per weight-chunk image (W1 [HC][C] or W2 [C][HC])
+    using D1 = Dma<HC, 2 * C>;
+    using D2 = Dma<C, 2 * HC>;
+    __shared__ __attribute__((aligned(1024))) bf16 ring[4 * IMG];
+    __shared__ __attribute__((aligned(16))) float b1s[4 * C];
+    bf16* const w1r = ring;
+    bf16* const w2r = ring + 2 * IMG;
+
+    const long m0 = (long)blockIdx.x * BM;
+    const long rows = M - m0;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int r = lane & 31, h = lane >> 5;
+    const int t = wave >> 1, u = wave & 1;
+    const int tok = 32 * t + r;
+    const bool ok = tok < rows;
+    const int hs = 32 * u;              // this wave's hidden features within a chunk
+    for (int i = threadIdx.x; i < 4 * C; i += MT) b1s[i] = b1[i];
+    bf16x8 xf[KS];
+    load_bfrags<C>(buf_rsrc(X + m0 * C, rows * C * 2), tok, ok, h, xf);
+
+    D1 d1;
+    D2 d2;
+    d1.init(C, wave, lane);
+    d2.init(4 * C, wave, lane);
+    const i32x4 rs_w1 = rsrc4(W1, 4L * C * C * 2);
+    const i32x4 rs_w2 = rsrc4(W2, 4L * C * C * 2);
+    asm volatile("" ::: "memory");
+    dma<D1::NW>(rs_w1, d1.v, 0, w1r, wave);
+    dma<D2::NW>(rs_w2, d2.v, 0, w2r, wave);
+    dma<D1::NW>(rs_w1, d1.v, HC * C * 2, w1r + IMG, wave);
+
+    auto gemm1 = [&](const bf16* img) {
+        bf16x8 wf[KS];
+#pragma unroll
+        for (int s = 0; s < KS; ++s) wf[s] = frag(img, moff<2 * C>(hs + r, 16 * s + 8 * h));
+        f32x16 a = f32x16{};
+#pragma unroll
+        for (int s = 0; s < KS; ++s) a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[s], xf[s], a, 0, 0, 0);
+        return a;
+    };
+    f32x16 acc[TF];
+#pragma unroll
+    for (int i = 0; i < TF; ++i) acc[i] = f32x16{};
+    vmwait<0>();
+    lds_sync();
+    f32x16 ha = gemm1(w1r), hb;
+
+    // par = j & 1 as a compile-time constant: every LDS address is a per-lane base + immediate
+    auto step = [&](auto more, auto par, int j, const f32x16& cur, f32x16& nxt) {
+        constexpr int P = decltype(par)::value;
+#ifndef MLP_EXP_NOBAR
+        vmwait<0>();                    // W1(j+1), W2(j): issued one step ago
+        lds_sync();                     // every wave is past GEMM1(j) and GEMM2(j-1)
+#endif
+#ifndef MLP_EXP_NODMA
+        if (j + 2 < NCH) dma<D1::NW>(rs_w1, d1.v, (unsigned)(j + 2) * HC * C * 2, w1r + P * IMG, wave);
+        if (j + 1 < NCH) dma<D2::NW>(rs_w2, d2.v, (unsigned)(j + 1) * HC * 2, w2r + (1 - P) * IMG, wave);
+#endif
+        float bv[16], gv[16];
+        bias16(b1s, j * HC + hs, h, bv);
+        if constexpr (decltype(more)::value) nxt = gemm1(w1r + (1 - P) * IMG);
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+#ifdef MLP_EXP_NOGELU
+            gv[e] = cur[e] + bv[e];
+#else
+            gv[e] = gelu_fast(cur[e] + bv[e]);
+#endif
+        }
+        const bf16* w2c = w2r + P * IMG;
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+            const bf16x8 gb = pack_b(gv, s2);
+#pragma unroll
+            for (int ft = 0; ft < TF; ++ft)
+                acc[ft] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pfrag<2 * HC>(w2c, 32 * ft + r, hs + 16 * s2, h), gb, acc[ft], 0, 0, 0);
+        }
+    };
+    int j = 0;
+    for (; j + 2 < NCH; j += 2) {
+        step(bconst<true>{}, iconst<0>{}, j, ha, hb);
+        step(bconst<true>{}, iconst<1>{}, j + 1, hb, ha);
+    }
+    step(bconst<true>{}, iconst<0>{}, j, ha, hb);
+    step(bconst<false>{}, iconst<1>{}, j + 1, hb, ha);
+
+    lds_sync();                         // ring free: partial-sum exchange
+    float* xch = reinterpret_cast<float*>(ring);
+    const auto rs_res = buf_rsrc(res + m0 * C, rows * C * 4);
+    const auto rs_out = buf_rsrc(out + m0 * C, rows * C * 4);
+    if (u == 0) {
+        exchange_half<C, 0>(acc, xch, wave, lane);
+        fwd_epilogue<C, 0>(acc, rs_res, rs_out, b2, tok, ok, h);
+    } else {
+        exchange_half<C, 1>(acc, xch, wave, lane);
+        fwd_epilogue<C, 1>(acc, rs_res, rs_out, b2, tok, ok, h);
+    }
+}
+
+// Backward.  Rings: W1 chunks in 3 stages (GEMM1 of chunk j+1 and GEMM4 of chunk j overlap, plus
+// the prefetch), W2 chunks in 2.  Step j (after one barrier): DMA W1(j+2), W2(j+2); GEMM1/GEMM3 of
+// chunk j+1 on the MFMA pipe while chunk j's GELU / GELU' / g, dH stores run on the VALU; GEMM4(j).
+template <int C>
+__global__ __launch_bounds__(MT) void mlp_bwd_kernel(long M, const bf16* __restrict__ X, const bf16* __restrict__ dY,
+                                                     const bf16* __restrict__ W1, const float* __restrict__ b1,
+                                                     const bf16* __restrict__ W2, bf16* __restrict__ dH,
+                                                     bf16* __restrict__ G, bf16* __restrict__ dX) {
+    constexpr int NCH = 4 * C / HC;
+    constexpr int KS = C / 16;
+    constexpr int TF = C / 32;
+    constexpr int IMG = HC * C;
+    using D1 = Dma<HC, 2 * C>;
+    using D2 = Dma<C, 2 * HC>;
+    // C = 256: two accumulator sets (overlap) would not fit in 512 registers -> plain order
+    constexpr bool PIPE = C < 256;
+    constexpr int W1S = PIPE ? 3 : 2;   // W1 ring stages
+    __shared__ __attribute__((aligned(1024))) bf16 ring[(W1S + 2) * IMG];
+    __shared__ __attribute__((aligned(16))) float b1s[4 * C];
+    bf16* const w1r = ring;
+    bf16* const w2r = ring + W1S * IMG;
+
+    const long m0 = (long)blockIdx.x * BM;
+    const long rows = M - m0;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int r = lane & 31, h = lane >> 5;
+    const int t = wave >> 1, u = wave & 1;
+    const int tok = 32 * t + r;
+    const bool ok = tok < rows;
+    const int hs = 32 * u;
+    for (int i = threadIdx.x; i < 4 * C; i += MT) b1s[i] = b1[i];
+    bf16x8 xf[KS], dyf[KS];
+    load_bfrags<C>(buf_rsrc(X + m0 * C, rows * C * 2), tok, ok, h, xf);
+    load_bfrags<C>(buf_rsrc(dY + m0 * C, rows * C * 2), tok, ok, h, dyf);
+
+    D1 d1;
+    D2 d2;
+    d1.init(C, wave, lane);
+    d2.init(4 * C, wave, lane);
+    const i32x4 rs_w1 = rsrc4(W1, 4L * C * C * 2);
+    const i32x4 rs_w2 = rsrc4(W2, 4L * C * C * 2);
+    const auto rs_dh = buf_rsrc(dH + m0 * 4 * C, rows * 4 * C * 2);
+    const auto rs_g = buf_rsrc(G + m0 * 4 * C, rows * 4 * C * 2);
+    asm volatile("" ::: "memory");
+    dma<D1::NW>(rs_w1, d1.v, 0, w1r, wave);
+    dma<D2::NW>(rs_w2, d2.v, 0, w2r, wave);
+    if constexpr (PIPE) {
+        dma<D1::NW>(rs_w1, d1.v, HC * C * 2, w1r + IMG, wave);
+        dma<D2::NW>(rs_w2, d2.v, HC * 2, w2r + IMG, wave);
+    }
+
+    // GEMM1 (h = W1_sub x^T) and GEMM3 (dg = W2_sub^T dY^T) of one chunk
+    auto gemm13 = [&](const bf16* w1c, const bf16* w2c, f32x16& ha, f32x16& ga) {
+        ha = f32x16{};
+        ga = f32x16{};
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+            ha = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag(w1c, moff<2 * C>(hs + r, 16 * s + 8 * h)), xf[s], ha, 0, 0, 0);
+            ga = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag<2 * HC>(w2c, hs, s, lane), dyf[s], ga, 0, 0, 0);
+        }
+    };
+    f32x16 acc[TF];
+#pragma unroll
+    for (int i = 0; i < TF; ++i) acc[i] = f32x16{};
+    // chunk j's epilogue (GELU, GELU', g / dH stores: 8 per wave) and GEMM4 (dx += W1_sub^T dH^T)
+    auto finish = [&](int j, const f32x16& hc, const f32x16& gc, const float* bv, const bf16* w1c) {
+        float gv[16], dv[16];
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            float dg;
+            gelu_pair_fast(hc[e] + bv[e], gv[e], dg);
+            dv[e] = gc[e] * dg;
+        }
+        const unsigned base = ok ? (unsigned)(tok * 4 * C + j * HC + hs + 4 * h) * 2 : kOOB;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {   // features 8g + 4h .. + 3 of the wave's 32
+            const unsigned o = base == kOOB ? kOOB : base + 16 * g;
+            buf_st4bf(rs_g, o, gv + 4 * g);
+            buf_st4bf(rs_dh, o, dv + 4 * g);
+        }
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+            const bf16x8 db = pack_b(dv, s2);
+#pragma unroll
+            for (int ft = 0; ft < TF; ++ft)
+                acc[ft] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ptrfrag<2 * C>(w1c, 32 * ft, hs + 16 * s2, lane), db, acc[ft], 0, 0, 0);
+        }
+    };
+    f32x16 ha, ga;
+    if constexpr (PIPE) {
+        vmwait<0>();
+        lds_sync();
+        f32x16 hb, gb;
+        gemm13(w1r, w2r, ha, ga);
+        auto step = [&](auto more, int j, const f32x16& hc, const f32x16& gc, f32x16& hn, f32x16& gn) {
+            vmwait<8>();                // W1(j+1), W2(j+1) landed; only chunk j-1's 8 stores after them
+            lds_sync();                 // every wave is past GEMM4(j-1) and GEMM3(j)
+            if (j + 2 < NCH) {
+                dma<D1::NW>(rs_w1, d1.v, (unsigned)(j + 2) * HC * C * 2, w1r + ((j + 2) % 3) * IMG, wave);
+                dma<D2::NW>(rs_w2, d2.v, (unsigned)(j + 2) * HC * 2, w2r + (j & 1) * IMG, wave);
+            }
+            float bv[16];
+            bias16(b1s, j * HC + hs, h, bv);
+            if constexpr (decltype(more)::value) gemm13(w1r + ((j + 1) % 3) * IMG, w2r + ((j + 1) & 1) * IMG, hn, gn);
+            finish(j, hc, gc, bv, w1r + (j % 3) * IMG);
+        };
+        int j = 0;
+        for (; j + 2 < NCH; j += 2) {
+            step(bconst<true>{}, j, ha, ga, hb, gb);
+            step(bconst<true>{}, j + 1, hb, gb, ha, ga);
+        }
+        step(bconst<true>{}, j, ha, ga, hb, gb);
+        step(bconst<false>{}, j + 1, hb, gb, ha, ga);
+    } else {
+        for (int j = 0; j < NCH; ++j) {
+            // chunk j landed: after its DMA this wave issued only chunk j-1's 8 g / dH stores
+            if (j == 0) vmwait<0>(); else vmwait<8>();
+            lds_sync();                 // every wave is past chunk j-1: its stage is free
+            if (j + 1 < NCH) {
+                dma<D1::NW>(rs_w1, d1.v, (unsigned)(j + 1) * HC * C * 2, w1r + ((j + 1) & 1) * IMG, wave);
+                dma<D2::NW>(rs_w2, d2.v, (unsigned)(j + 1) * HC * 2, w2r + ((j + 1) & 1) * IMG, wave);
+            }
+            float bv[16];
+            bias16(b1s, j * HC + hs, h, bv);
+            gemm13(w1r + (j & 1) * IMG, w2r + (j & 1) * IMG, ha, ga);
+            finish(j, ha, ga, bv, w1r + (j & 1) * IMG);
+        }
+    }
+
+    lds_sync();
+    float* xch = reinterpret_cast<float*>(ring);
+    const auto rs_dx = buf_rsrc(dX + m0 * C, rows * C * 2);
+    if (u == 0) {
+        exchange_half<C, 0>(acc, xch, wave, lane);
+        bwd_epilogue<C, 0>(acc, rs_dx, tok, ok, h);
+    } else {
+        exchange_half<C, 1>(acc, xch, wave, lane);
+        bwd_epilogue<C, 1>(acc, rs_dx, tok, ok, h);
+    }
+}
+
+
+template <int C>
+int fwd_launch(long M, const void* x, const void* w1, const float* b1, const void* w2, const float* b2, const float* res,
+               float* out, hipStream_t st) {
+    mlp_fwd_kernel<C><<<dim3((unsigned)((M + BM - 1) / BM)), MT, 0, st>>>(M, (const bf16*)x, (const bf16*)w1, b1,
+                                                                          (const bf16*)w2, b2, res, out);
+    return check_launch("mlp_fwd");
+}
+
+template <int C>
+int bwd_launch(long M, const void* x, const void* dy, const void* w1, const float* b1, const void* w2, void* dh, void* g,
+               void* dx, hipStream_t st) {
+    mlp_bwd_kernel<C><<<dim3((unsigned)((M + BM - 1) / BM)), MT, 0, st>>>(M, (const bf16*)x, (const bf16*)dy,
+                                                                          (const bf16*)w1, b1, (const bf16*)w2, (bf16*)dh,
+                                                                          (bf16*)g, (bf16*)dx);
+    return check_launch("mlp_bwd");
+}
+
+}  // namespace
+}  // namespace csu
+
+using namespace csu;
+
+extern "C" int csu_mlp_supported(int C) { return C == 64 || C == 128 || C == 256; }
+
+extern "C" int csu_mlp_fwd(long M, int C, const void* x, const void* w1, const float* b1, const void* w2, const float* b2,
+                           const float* res, float* out, void* stream) {
+    if (M < 1 || !x || !w1 || !b1 || !w2 || !b2 || !res || !out) return fail(CSU_E_ARG, "mlp_fwd: bad arguments");
+    if (M * 4L * C * 2 > 0x7fffffffL) return fail(CSU_E_ARG, "mlp_fwd: tensor exceeds 2 GB buffer range");
+    const hipStream_t st = as_stream(stream);
+    switch (C) {
+        case 64: return fwd_launch<64>(M, x, w1, b1, w2, b2, res, out, st);
+        case 128: return fwd_launch<128>(M, x, w1, b1, w2, b2, res, out, st);
+        case 256: return fwd_launch<256>(M, x, w1, b1, w2, b2, res, out, st);
+        default: return fail(CSU_E_ARG, "mlp_fwd: C must be 64, 128 or 256");
+    }
+}
+
+extern "C" int csu_mlp_bwd(long M, int C, const void* x, const void* dy, const void* w1, const float* b1, const void* w2,
+                           void* dh, void* g, void* dx, void* stream) {
+    if (M < 1 || !x || !dy || !w1 || !b1 || !w2 || !dh || !g || !dx) return fail(CSU_E_ARG, "mlp_bwd: bad arguments");
+    if (M * 4L * C * 2 > 0x7fffffffL) return fail(CSU_E_ARG, "mlp_bwd: tensor exceeds 2 GB buffer range");
+    const hipStream_t st = as_stream(stream);
+    switch (C) {
+        case 64: return bwd_launch<64>(M, x, dy, w1, b1, w2, dh, g, dx, st);
+        case 128: return bwd_launch<128>(M, x, dy, w1, b1, w2, dh, g, dx, st);
+        case 256: return bwd_launch<256>(M, x, dy, w1, b1, w2, dh, g, dx, st);
+        default: return fail(CSU_E_ARG, "mlp_bwd: C must be 64, 128 or 256");
+    }
+}

@@ -12,7 +12,8 @@ import threading
 
 import torch  # noqa: F401  (must precede the dlopen, see module docstring)
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libcsu_hip.so")
+# CSU_LIB_PATH: load another build of the library (A/B experiments)
+LIB_PATH = os.environ.get("CSU_LIB_PATH") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libcsu_hip.so")
 
 c_int32, c_float, c_void_p, c_size_t = ctypes.c_int32, ctypes.c_float, ctypes.c_void_p, ctypes.c_size_t
 
@@ -87,6 +88,11 @@ _SIGS = {
     "csu_adamw_step": (ctypes.c_int, [c_void_p, ctypes.c_int, ctypes.c_long, c_void_p, c_float, c_float, c_float, c_float,
                                       c_float, c_void_p, c_float, c_void_p]),
     "csu_gemm_ex": (ctypes.c_int, [ctypes.POINTER(GemmDesc), c_void_p]),
+    "csu_mlp_supported": (ctypes.c_int, [ctypes.c_int]),
+    "csu_mlp_fwd": (ctypes.c_int, [ctypes.c_long, ctypes.c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                   c_void_p, c_void_p]),
+    "csu_mlp_bwd": (ctypes.c_int, [ctypes.c_long, ctypes.c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                   c_void_p, c_void_p, c_void_p]),
     "csu_conv2d_fwd": (ctypes.c_int, [ctypes.POINTER(ConvGeom), ctypes.c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                                       c_void_p]),
     "csu_conv2d_dgrad": (ctypes.c_int, [ctypes.POINTER(ConvGeom), ctypes.c_int, c_void_p, c_void_p, c_void_p, c_void_p,

@@ -634,7 +634,51 @@ def linear_residual(res, x, weight, bias):
         return _LinearResidualFn.apply(res, x, weight, bias, _weight_bf16(weight))
 
 
+class _MlpFusedFn(torch.autograd.Function):
+    """res + fc2(gelu(fc1(x))) (Mlp cswin:180-196 + residual cswin:368) in ONE csu_mlp_fwd launch
+    (the 4C hidden layer never reaches HBM).  Backward: one csu_mlp_bwd launch recomputes
+    h = fc1(x) and writes dh = (dY W2) * gelu'(h), g = gelu(h) and dx = dh W1; then the two
+    weight-gradient GEMMs dW1 = dh^T x, dW2 = dY^T g (+ column sums for the biases)."""
+
+    @staticmethod
+    def forward(ctx, res, x, w1, b1, w2, b2, w1c, w2c):
+        C = x.shape[-1]
+        res2 = res.float().contiguous().view(-1, C)
+        x2 = x.reshape(-1, C).contiguous()
+        b1f = b1.detach().float().contiguous()
+        y = torch.empty_like(res2)
+        check(lib().csu_mlp_fwd(x2.shape[0], C, ptr(x2), ptr(w1c), ptr(b1f), ptr(w2c), ptr(b2.detach().float().contiguous()),
+                                ptr(res2), ptr(y), stream_ptr(x2.device)), "csu_mlp_fwd")
+        ctx.save_for_backward(x2, w1c, b1f, w2c)
+        ctx.meta = (res.dtype, x.shape, w1.dtype, b1.dtype, w2.dtype, b2.dtype)
+        return y.view(res.shape)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w1c, b1f, w2c = ctx.saved_tensors
+        rdt, xshape, w1dt, b1dt, w2dt, b2dt = ctx.meta
+        M, C = x2.shape
+        dyb = _bf16_of(dy).view(-1, C)
+        dh = torch.empty(M, 4 * C, dtype=torch.bfloat16, device=x2.device)
+        g = torch.empty_like(dh)
+        dx = torch.empty(M, C, dtype=torch.bfloat16, device=x2.device)
+        check(lib().csu_mlp_bwd(M, C, ptr(x2), ptr(dyb), ptr(w1c), ptr(b1f), ptr(w2c), ptr(dh), ptr(g), ptr(dx),
+                                stream_ptr(x2.device)), "csu_mlp_bwd")
+        dw2, db2 = wgrad_maybe_side(dyb, g, w2dt, b2dt)
+        dw1, db1 = wgrad_maybe_side(dh, x2, w1dt, b1dt)
+        return dy.to(rdt), dx.view(xshape), dw1.to(w1dt), db1.to(b1dt), dw2.to(w2dt), db2.to(b2dt), None, None
+
+
+# CSU_FUSED_MLP=0 selects the two-GEMM Mlp (A/B comparisons)
+FUSED_MLP = _os.environ.get("CSU_FUSED_MLP", "1") == "1"
+
+
 def mlp_residual(res, x, fc1: torch.nn.Linear, fc2: torch.nn.Linear):
+    C = x.shape[-1]
+    if FUSED_MLP and fc1.out_features == 4 * C and lib().csu_mlp_supported(C):
+        with torch.autocast("cuda", enabled=False):
+            return _MlpFusedFn.apply(res, x, fc1.weight, fc1.bias, fc2.weight, fc2.bias, _weight_bf16(fc1.weight),
+                                     _weight_bf16(fc2.weight))
     with torch.autocast("cuda", enabled=False):
         return _MlpResidualFn.apply(res, x, fc1.weight, fc1.bias, fc2.weight, fc2.bias, _weight_bf16(fc1.weight),
                                     _weight_bf16(fc2.weight))

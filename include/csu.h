@@ -248,6 +248,19 @@ int csu_adamw_step(const csu_adamw_item* items, int count, long total_chunks, co
                    void* stream);
 
 /* ---------------------------------------------------------------------------------------
+ * Fused Mlp + residual (Mlp cswin:180-196 with the residual add of CSWinBlock cswin:368):
+ * fc1 -> GELU -> fc2 with the 4C hidden layer kept on chip.  x (M, C) bf16; w1 (4C, C) and
+ * w2 (C, 4C) bf16 nn.Linear weights; b1 (4C), b2 (C) fp32; res / out (M, C) fp32 (may alias).
+ * Backward recomputes h = fc1(x) and writes dh = (dy w2) * gelu'(h) (M, 4C), g = gelu(h)
+ * (M, 4C) for the weight gradients and dx = dh w1 (M, C), all bf16.  C in {64, 128, 256}.
+ * ------------------------------------------------------------------------------------- */
+int csu_mlp_supported(int C);
+int csu_mlp_fwd(long M, int C, const void* x, const void* w1, const float* b1, const void* w2, const float* b2,
+                const float* res, float* out, void* stream);
+int csu_mlp_bwd(long M, int C, const void* x, const void* dy, const void* w1, const float* b1, const void* w2,
+                void* dh, void* g, void* dx, void* stream);
+
+/* ---------------------------------------------------------------------------------------
  * Implicit-GEMM NHWC convolution (patch embed cswin:505, Merge_Block.conv cswin:376, CARAFE
  * encoder cswin:397/446, plain-UNet DoubleConv 3x3 unet:182/185 and ConvTranspose2d(k2,s2)
  * unet:211 = the dgrad operator).  x (B,H,W,C), y (B,OH,OW,N) channels-last; weights prepared by

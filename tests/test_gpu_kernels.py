@@ -422,6 +422,40 @@ def test_fused_mlp_residual_matches_unfused():
         assert_close(got, r, torch.bfloat16)
 
 
+@pytest.mark.parametrize("C,M", [(64, 4096), (64, 37), (128, 1000), (256, 4160), (256, 100)])
+def test_mlp_fused_kernels_vs_fp64(C, M):
+    """csu_mlp_fwd / csu_mlp_bwd (fc1 -> GELU -> fc2 + residual with the hidden layer on chip) vs
+    the fp64 composition on the same bf16 inputs: y, and the backward's dh = (dy W2) gelu'(h),
+    g = gelu(h), dx = dh W1.  Ragged M exercises the token tail of the last 64-token panel."""
+    from csu._lib import check, lib, ptr, stream_ptr
+    d = dev()
+    torch.manual_seed(C + M)
+    x = torch.randn(M, C, device=d).bfloat16()
+    w1 = (torch.randn(4 * C, C, device=d) * C ** -0.5).bfloat16()
+    w2 = (torch.randn(C, 4 * C, device=d) * (4 * C) ** -0.5).bfloat16()
+    b1, b2 = torch.randn(4 * C, device=d) * 0.1, torch.randn(C, device=d) * 0.1
+    res = torch.randn(M, C, device=d)
+    dy = torch.randn(M, C, device=d).bfloat16()
+    y = torch.empty(M, C, device=d)
+    st = stream_ptr(d)
+    check(lib().csu_mlp_fwd(M, C, ptr(x), ptr(w1), ptr(b1), ptr(w2), ptr(b2), ptr(res), ptr(y), st), "mlp_fwd")
+    dh = torch.empty(M, 4 * C, device=d, dtype=torch.bfloat16)
+    g = torch.empty_like(dh)
+    dx = torch.empty(M, C, device=d, dtype=torch.bfloat16)
+    check(lib().csu_mlp_bwd(M, C, ptr(x), ptr(dy), ptr(w1), ptr(b1), ptr(w2), ptr(dh), ptr(g), ptr(dx), st), "mlp_bwd")
+    torch.cuda.synchronize()
+    X, W1, W2, B1, B2 = (t.double().cpu() for t in (x, w1, w2, b1, b2))
+    F = torch.nn.functional
+    h = X @ W1.T + B1
+    gr = F.gelu(h)
+    assert_close(y, res.double().cpu() + gr @ W2.T + B2, torch.bfloat16)
+    assert_close(g, gr, torch.bfloat16)
+    hg = h.clone().requires_grad_(True)
+    F.gelu(hg).backward(dy.double().cpu() @ W2)
+    assert_close(dh, hg.grad, torch.bfloat16)
+    assert_close(dx, hg.grad @ W1, torch.bfloat16)
+
+
 CONV_CASES = [  # (B, H, C, N, k, stride, pad)
     (2, 32, 3, 64, 7, 4, 2),      # patch embed (cswin:505)
     (2, 16, 64, 128, 3, 2, 1),    # Merge_Block (cswin:376)

@@ -1,7 +1,8 @@
 """Average rocprofv3 PMC counters per dispatch over the counter_collection CSVs under a directory
-(skipping the first 5 dispatches): python tools/pmc_sum.py <dir> [kernel-substring]."""
+(skipping the first `skip` dispatches, default 5): python tools/pmc_sum.py <dir> [kernel-substring] [skip]."""
 import collections, csv, glob, sys
 pat = sys.argv[2] if len(sys.argv) > 2 else ""
+skip = int(sys.argv[3]) if len(sys.argv) > 3 else 5
 vals = collections.defaultdict(list)
 for f in sorted(glob.glob(sys.argv[1] + "/**/*counter_collection.csv", recursive=True)):
     per = collections.defaultdict(dict)
@@ -9,7 +10,7 @@ for f in sorted(glob.glob(sys.argv[1] + "/**/*counter_collection.csv", recursive
         if pat in r["Kernel_Name"]:
             per[int(r["Dispatch_Id"])][r["Counter_Name"]] = float(r["Counter_Value"])
     for i, (d, cs) in enumerate(sorted(per.items())):
-        if i >= 5:
+        if i >= skip:
             for k, v in cs.items():
                 vals[k].append(v)
 for k, v in vals.items():
