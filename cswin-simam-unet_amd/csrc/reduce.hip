@@ -93,20 +93,21 @@ struct Plan {
     long rpc;
 };
 
+// Latency-bound shapes (a few dozen slab rows x 10^5 columns) need many workgroups and few
+// dependent loads per thread: at most 64 column threads per row group (>= 4 row lanes per
+// workgroup) and ~8 rows per thread, i.e. two rounds of the 4-stream loop.
 Plan plan(long rows, long cols, int V) {
     Plan p;
     const long vecs = (cols + V - 1) / V;
-    p.tpr = (int)(vecs >= NT ? NT : vecs);
+    p.tpr = (int)(vecs >= 64 ? 64 : vecs);
     int t = 1;                                  // round tpr up to a power of two dividing NT
     while (t < p.tpr) t <<= 1;
     p.tpr = t;
     p.colblocks = (int)((vecs + p.tpr - 1) / p.tpr);
     const int rpi = NT / p.tpr;
-    long want = rows <= 256 ? 1 : (512 + p.colblocks - 1) / p.colblocks;
-    const long maxc = (rows + 8 * rpi - 1) / (8 * rpi);   // >= 8 rows per thread
-    if (want > maxc) want = maxc;
-    if (want < 1) want = 1;
+    long want = (rows + 8L * rpi - 1) / (8L * rpi);   // ~8 rows per thread
     if (want > 256) want = 256;
+    if (want < 1) want = 1;
     p.chunks = (int)want;
     p.rpc = (rows + p.chunks - 1) / p.chunks;
     return p;
