@@ -13,6 +13,7 @@ namespace {
 
 constexpr int NT = 256;
 constexpr int WAVES = NT / 64;
+constexpr int LU = 4;       // ln_bwd: row groups per wave iteration
 
 template <typename T, int V> __device__ __forceinline__ void ldv(const T* p, float* v) {
     if constexpr (V == 8) load8(p, v);
@@ -96,43 +97,48 @@ __global__ __launch_bounds__(NT) void ln_bwd(int rows, int C, int rows_per_block
 #pragma unroll
     for (int j = 0; j < V; ++j) dg[j] = db[j] = 0.f;
     const int r0 = blockIdx.x * rows_per_block, r1 = min(rows, r0 + rows_per_block);
-    for (int rb = r0 + wave * RPW; rb < r1; rb += WAVES * RPW) {
-        const int row = rb + lane / LPR;
-        const bool ok = row < r1;
-        float xv[V], g[V], mu = 0.f, rs = 0.f;
-        if (ok) {
-            ldv<TX, V>(x + (size_t)row * C + c0, xv);
-            ldv<TG, V>(dy + (size_t)row * C + c0, g);
-            mu = mean[row];
-            rs = rstd[row];
-        } else {
+    // LU row groups per wave iteration, all loads issued before any math: one memory round trip
+    // per LU rows instead of per row (the loop is latency-bound, not bandwidth-bound)
+    for (int rb = r0 + wave * RPW * LU; rb < r1; rb += WAVES * RPW * LU) {
+        float xv[LU][V], g[LU][V], rv[LU][V], mu[LU], rs[LU];
+        bool ok[LU];
 #pragma unroll
-            for (int j = 0; j < V; ++j) xv[j] = g[j] = 0.f;
+        for (int u = 0; u < LU; ++u) {
+            const int row = rb + u * RPW + lane / LPR;
+            ok[u] = row < r1;
+            mu[u] = rs[u] = 0.f;
+#pragma unroll
+            for (int j = 0; j < V; ++j) xv[u][j] = g[u][j] = rv[u][j] = 0.f;
+            if (ok[u]) {
+                ldv<TX, V>(x + (size_t)row * C + c0, xv[u]);
+                ldv<TG, V>(dy + (size_t)row * C + c0, g[u]);
+                if (dres) ldv<float, V>(dres + (size_t)row * C + c0, rv[u]);
+                mu[u] = mean[row];
+                rs[u] = rstd[row];
+            }
         }
-        float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-        for (int j = 0; j < V; ++j) {
-            xv[j] = (xv[j] - mu) * rs;   // xhat
-            const float gg = g[j] * gw[j];
-            s1 += gg;
-            s2 += gg * xv[j];
-            dg[j] += g[j] * xv[j];
-            db[j] += g[j];
+        for (int u = 0; u < LU; ++u) {
+            float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+            for (int j = 0; j < V; ++j) {
+                xv[u][j] = (xv[u][j] - mu[u]) * rs[u];   // xhat
+                const float gg = g[u][j] * gw[j];
+                s1 += gg;
+                s2 += gg * xv[u][j];
+                dg[j] += g[u][j] * xv[u][j];
+                db[j] += g[u][j];
+            }
+            s1 = group_sum<LPR>(s1) / C;
+            s2 = group_sum<LPR>(s2) / C;
+            if (!ok[u]) continue;
+            const int row = rb + u * RPW + lane / LPR;
+            float o[V];
+#pragma unroll
+            for (int j = 0; j < V; ++j) o[j] = rs[u] * (g[u][j] * gw[j] - s1 - xv[u][j] * s2) + rv[u][j];
+            stv<TX, V>(dx + (size_t)row * C + c0, o);
+            if (dxb) stv<bf16, V>(dxb + (size_t)row * C + c0, o);
         }
-        s1 = group_sum<LPR>(s1) / C;
-        s2 = group_sum<LPR>(s2) / C;
-        if (!ok) continue;
-        float o[V];
-#pragma unroll
-        for (int j = 0; j < V; ++j) o[j] = rs * (g[j] * gw[j] - s1 - xv[j] * s2);
-        if (dres) {
-            float rv[V];
-            ldv<float, V>(dres + (size_t)row * C + c0, rv);
-#pragma unroll
-            for (int j = 0; j < V; ++j) o[j] += rv[j];
-        }
-        stv<TX, V>(dx + (size_t)row * C + c0, o);
-        if (dxb) stv<bf16, V>(dxb + (size_t)row * C + c0, o);
     }
     // column partials: lanes of one column inside the wave (fixed xor tree), then the waves
 #pragma unroll
@@ -169,9 +175,9 @@ __global__ __launch_bounds__(NT) void ln_param_reduce(int C, int nb, const float
     if (lane == 0) (v < C ? dgamma[v] : dbeta[v - C]) = s;
 }
 
-int ln_blocks(int rows, int rpw, int* rpb) {   // <= 512 blocks, rows per block a multiple of a block's row step
-    const int step = WAVES * rpw;
-    int r = (rows + 511) / 512;
+int ln_blocks(int rows, int rpw, int* rpb) {   // <= 2048 blocks, rows per block a multiple of a block's row step
+    const int step = WAVES * rpw * LU;
+    int r = (rows + 2047) / 2048;
     r = ((r + step - 1) / step) * step;
     *rpb = r;
     return (rows + r - 1) / r;

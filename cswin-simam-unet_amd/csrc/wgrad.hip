@@ -248,6 +248,11 @@ int wgrad_target_env() {   // CSU_WGRAD_WGS: target workgroup count of the split
     return v;
 }
 
+int wgrad_mintok_env() {   // CSU_WGRAD_MINTOK: minimum tokens per split-K chunk
+    static int v = env_int("CSU_WGRAD_MINTOK", 512);
+    return v;
+}
+
 WPlan wplan(long M, int N, int K, bool bf16_path) {
     WPlan p;
     const int te = wgrad_tile_env();
@@ -256,7 +261,8 @@ WPlan wplan(long M, int N, int K, bool bf16_path) {
     p.kt = (K + p.t - 1) / p.t;
     const long target = wgrad_target_env();
     long want = (target + p.nt * p.kt - 1) / (p.nt * p.kt);
-    const long maxc = (M + 511) / 512;          // >= 512 tokens per chunk
+    const long mt = wgrad_mintok_env();
+    const long maxc = (M + mt - 1) / mt;        // >= mt tokens per chunk
     if (want > maxc) want = maxc;
     if (want > 256) want = 256;
     if (want < 1) want = 1;
@@ -268,6 +274,8 @@ WPlan wplan(long M, int N, int K, bool bf16_path) {
 
 }  // namespace
 
+int wgrad5_launch(int cfg, long M, int N, int K, long rpc, int chunks, const bf16* dy, const bf16* x, float* part,
+                  hipStream_t st);
 bool wgrad4_ok(long M, int N, int K);
 size_t wgrad4_workspace(long M, int N, int K);
 int wgrad4_run(long M, int N, int K, const bf16* dy, const bf16* x, float* dw_db, void* ws, hipStream_t st);
@@ -285,6 +293,17 @@ static bool use_wgrad4() {
         v = e && e[0] == '1';
     }
     return v == 1;
+}
+
+// CSU_WGRAD5=<cfg> selects the deep LDS-DMA pipeline kernel (wgrad5.hip) for the bf16 128-tile
+// plans; -1 = the register-staged kernel.
+static int wgrad5_cfg() {
+    static int v = -2;
+    if (v == -2) {
+        const char* e = getenv("CSU_WGRAD5");
+        v = e ? atoi(e) : -1;
+    }
+    return v;
 }
 
 extern "C" size_t csu_linear_wgrad_workspace(long M, int N, int K) {
@@ -324,7 +343,9 @@ extern "C" int csu_linear_wgrad_ex(long M, int N, int K, int dtype, const void* 
     const dim3 grid1((unsigned)(p.nt * p.kt * p.chunks));
     const bf16* dyb = (const bf16*)dy;
     const bf16* xb = (const bf16*)x;
-    if (dtype == CSU_BF16 && p.t == 128 && x_gelu) wgrad_bf16_tr<128, true><<<grid1, NT, 0, st>>>(M, N, K, p.rpc, dyb, xb, part);
+    if (dtype == CSU_BF16 && p.t == 128 && !x_gelu && wgrad5_cfg() >= 0) {
+        if (int e = wgrad5_launch(wgrad5_cfg(), M, N, K, p.rpc, p.chunks, dyb, xb, part, st)) return e;
+    } else if (dtype == CSU_BF16 && p.t == 128 && x_gelu) wgrad_bf16_tr<128, true><<<grid1, NT, 0, st>>>(M, N, K, p.rpc, dyb, xb, part);
     else if (dtype == CSU_BF16 && p.t == 128) wgrad_bf16_tr<128, false><<<grid1, NT, 0, st>>>(M, N, K, p.rpc, dyb, xb, part);
     else if (dtype == CSU_BF16 && x_gelu) wgrad_bf16_tr<64, true><<<grid1, NT, 0, st>>>(M, N, K, p.rpc, dyb, xb, part);
     else if (dtype == CSU_BF16) wgrad_bf16_tr<64, false><<<grid1, NT, 0, st>>>(M, N, K, p.rpc, dyb, xb, part);
