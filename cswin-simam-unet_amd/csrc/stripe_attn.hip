@@ -19,6 +19,8 @@
 // input gradient) plus a deterministic two-pass reduction for the LePE weight/bias gradient.
 #include "common.hpp"
 
+#include <type_traits>
+
 namespace csu {
 namespace {
 
@@ -595,6 +597,7 @@ int wgrad_blocks(const csu_stripe_args& a) {
 // orientations, so nothing is ever written transposed.
 // =============================================================================================
 constexpr int WMAX = 256;   // window tokens held in LDS
+typedef float f2 __attribute__((ext_vector_type(2)));   // packed-f32 pairs (v_pk_fma/mul/add_f32)
 
 __device__ __forceinline__ int swz(int row, int col) {   // element offset in a swizzled image
     return row * HD + ((((col >> 3) ^ (row >> 2)) & 3) << 3) + (col & 7);
@@ -737,39 +740,55 @@ __global__ __launch_bounds__(NT) void stripe_fwd_w(csu_stripe_args a, int split,
         }
         float m = -INFINITY, l = 0.f;
         f32x16 o = {};
-        // 64 keys per online-softmax step: two independent S^T tiles, one rescale of O
-        for (int kb = 0; kb < npad; kb += 64) {
+        // 64 keys per online-softmax step: two independent S^T tiles, one rescale of O.  VALU per
+        // score: 1/2 v_max3, 1/2 v_pk_fma (scale and max shift folded), v_exp, 1/2 v_pk_add; the
+        // key mask only on the tail step (uniform branch)
+        auto step = [&](int kb, auto masked) {
             f32x16 s0 = {}, s1 = {};
             mma_rows_sw(s0, Ks, kb, r, h, qf);
             mma_rows_sw(s1, Ks, kb + 32, r, h, qf);
-            float bm = -INFINITY;
+            if constexpr (decltype(masked)::value) {
 #pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                s0[i] = kb + crow(i, h) < w.N ? s0[i] * c : -INFINITY;
-                s1[i] = kb + 32 + crow(i, h) < w.N ? s1[i] * c : -INFINITY;
-                bm = fmaxf(bm, fmaxf(s0[i], s1[i]));
+                for (int i = 0; i < 16; ++i) {
+                    if (kb + crow(i, h) >= w.N) s0[i] = -INFINITY;
+                    if (kb + 32 + crow(i, h) >= w.N) s1[i] = -INFINITY;
+                }
             }
-            bm = fmaxf(bm, __shfl_xor(bm, 32, 64));
-            const float mn = fmaxf(m, bm);
-            const float alpha = __builtin_amdgcn_exp2f(m - mn);
+            float mn = m;   // raw-score running max (scale applied in the exponent)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) mn = fmaxf(mn, fmaxf(s0[i], s1[i]));
+            mn = fmaxf(mn, __shfl_xor(mn, 32, 64));
+            const float alpha = __builtin_amdgcn_exp2f((m - mn) * c);
             m = mn;
-            float ls = 0.f;
+            const f2 cc = {c, c}, mc = {mn * c, mn * c};
+            f2 ls = {0.f, 0.f};
 #pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                s0[i] = __builtin_amdgcn_exp2f(s0[i] - mn);
-                s1[i] = __builtin_amdgcn_exp2f(s1[i] - mn);
-                ls += s0[i] + s1[i];
+            for (int i = 0; i < 16; i += 2) {
+                f2 a = f2{s0[i], s0[i + 1]} * cc - mc;
+                f2 b = f2{s1[i], s1[i + 1]} * cc - mc;
+                a = f2{__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)};
+                b = f2{__builtin_amdgcn_exp2f(b.x), __builtin_amdgcn_exp2f(b.y)};
+                s0[i] = a.x; s0[i + 1] = a.y;
+                s1[i] = b.x; s1[i + 1] = b.y;
+                ls += a + b;
             }
-            l = l * alpha + ls;
+            l = l * alpha + (ls.x + ls.y);
+            const f2 al = {alpha, alpha};
 #pragma unroll
-            for (int i = 0; i < 16; ++i) o[i] *= alpha;
+            for (int i = 0; i < 16; i += 2) {
+                const f2 ov = f2{o[i], o[i + 1]} * al;
+                o[i] = ov.x; o[i + 1] = ov.y;
+            }
             mma_acc_sw(o, Vs, kb, lane, s0);
             mma_acc_sw(o, Vs, kb + 32, lane, s1);
-        }
+        };
+        const int nfull = w.N & ~63;   // steps without a key tail: no mask at all
+        for (int kb = 0; kb < nfull; kb += 64) step(kb, std::false_type{});
+        if (nfull < w.N) step(nfull, std::true_type{});
         const float lt = l + __shfl_xor(l, 32, 64);
         if (!qvalid) continue;
         const float inv = 1.f / lt;
-        if (h == 0) lse[stat_index(a, w, qtok)] = (m + log2f(lt)) * kLn2;
+        if (h == 0) lse[stat_index(a, w, qtok)] = (m * c + log2f(lt)) * kLn2;   // m is the raw-score max
         bf16* orow = out + ((size_t)w.b * L + qtok) * C + w.chq;
 #pragma unroll
         for (int g4 = 0; g4 < 4; ++g4) {
@@ -842,15 +861,19 @@ __global__ __launch_bounds__(NT) void stripe_bwd_dq_w(csu_stripe_args a, int spl
         if (qvalid && h == 0) delta[si] = dl;
         const float lq = qvalid ? lse[si] * kLog2e : 0.f;
         f32x16 dq = {};
+        const f2 cc = {c, c}, lq2 = {lq, lq}, dl2 = {dl, dl};
         for (int kb = 0; kb < npad; kb += 32) {
             f32x16 s = {}, dp = {};
             mma_rows_sw(s, Ks, kb, r, h, qf);
             mma_rows_sw(dp, Vs, kb, r, h, gf);
 #pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                const float p = kb + crow(i, h) < w.N ? __builtin_amdgcn_exp2f(s[i] * c - lq) : 0.f;
-                s[i] = p * (dp[i] - dl);
+            for (int i = 0; i < 16; i += 2) {   // dS = P dP - P delta, packed pairs
+                f2 p = f2{s[i], s[i + 1]} * cc - lq2;
+                p = f2{__builtin_amdgcn_exp2f(p.x), __builtin_amdgcn_exp2f(p.y)};
+                const f2 t = p * f2{dp[i], dp[i + 1]} - p * dl2;
+                s[i] = t.x; s[i + 1] = t.y;
             }
+            // no key mask: keys >= N have zero K rows in LDS, so their dS rows add nothing to dQ
             mma_acc_sw(dq, Ks, kb, lane, s);
         }
         if (!qvalid) continue;
@@ -871,7 +894,7 @@ __global__ __launch_bounds__(NT) void stripe_bwd_dkdv_w(csu_stripe_args a, int s
                                                         const float* __restrict__ delta, bf16* __restrict__ dqkv) {
     __shared__ __attribute__((aligned(16))) bf16 Qs[WMAX * HD];
     __shared__ __attribute__((aligned(16))) bf16 Gs[WMAX * HD];
-    __shared__ float lse_s[WMAX], dl_s[WMAX];
+    __shared__ __attribute__((aligned(16))) float lse_s[WMAX], dl_s[WMAX];
     __shared__ float wts[HD * 10];
     const Win w = decode_w(a, split);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -913,16 +936,24 @@ __global__ __launch_bounds__(NT) void stripe_bwd_dkdv_w(csu_stripe_args a, int s
             load_frag(vn_f, img + t2 * C3 + 2 * C + w.chq, h, kv2);
         }
         f32x16 dk = {}, dv = {};
+        const f2 cc = {c, c};
         for (int qb = 0; qb < npad; qb += 32) {
             f32x16 s = {}, dp = {};
             mma_rows_sw(s, Qs, qb, r, h, kf);
             mma_rows_sw(dp, Gs, qb, r, h, vf);
 #pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                const int qi = qb + crow(i, h);
-                const float p = __builtin_amdgcn_exp2f(s[i] * c - lse_s[qi]);
-                s[i] = p;
-                dp[i] = p * (dp[i] - dl_s[qi]);
+            for (int g4 = 0; g4 < 4; ++g4) {   // rows qb + 8 g4 + 4 h + 0..3: one 16-B LDS read each
+                const f32x4 lq = *reinterpret_cast<const f32x4*>(lse_s + qb + 8 * g4 + 4 * h);
+                const f32x4 dq4 = *reinterpret_cast<const f32x4*>(dl_s + qb + 8 * g4 + 4 * h);
+#pragma unroll
+                for (int e = 0; e < 4; e += 2) {
+                    const int i = 4 * g4 + e;
+                    f2 p = f2{s[i], s[i + 1]} * cc - f2{lq[e], lq[e + 1]};
+                    p = f2{__builtin_amdgcn_exp2f(p.x), __builtin_amdgcn_exp2f(p.y)};
+                    const f2 t = p * (f2{dp[i], dp[i + 1]} - f2{dq4[e], dq4[e + 1]});
+                    s[i] = p.x; s[i + 1] = p.y;
+                    dp[i] = t.x; dp[i + 1] = t.y;
+                }
             }
             mma_acc_sw(dv, Gs, qb, lane, s);
             mma_acc_sw(dk, Qs, qb, lane, dp);

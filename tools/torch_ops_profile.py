@@ -1,0 +1,36 @@
+"""Which aten ops launch GPU kernels in one eager bench step (torch.profiler, shapes recorded):
+the PyTorch-side kernels left between the csu kernels."""
+import os, sys
+sys.path[:0] = [os.path.join(os.path.dirname(__file__), ".."), os.path.join(os.path.dirname(__file__), "..", "cswin-simam-unet_amd")]
+import numpy as np
+import torch
+from torch.profiler import profile, ProfilerActivity
+from csu.model import CSWinTransformer
+from csu.train import bce_loss, make_optimizer
+from csu.data import ellipse_batch
+
+d = torch.device("cuda:0")
+torch.manual_seed(0)
+model = CSWinTransformer(img_size=512, depth=[1, 2, 9, 1], split_size=[1, 2, 8, 8]).to(d)
+opt = make_optimizer(model)
+x, t = ellipse_batch(np.random.default_rng(1), 16, 512)
+x, t = x.to(d), t.to(d)
+
+
+def step():
+    opt.zero_grad(set_to_none=True)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = model(x)
+    loss = bce_loss(y, t)
+    loss.backward()
+    opt.step()
+
+
+for _ in range(3):
+    step()
+torch.cuda.synchronize()
+with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True) as prof:
+    step()
+    torch.cuda.synchronize()
+print(prof.key_averages(group_by_input_shape=True).table(sort_by="self_cuda_time_total", row_limit=45, max_name_column_width=40,
+                                                         max_shapes_column_width=70))
