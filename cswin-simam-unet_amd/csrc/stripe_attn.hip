@@ -693,7 +693,9 @@ __device__ __forceinline__ Win decode_w(const csu_stripe_args& a, int split) {
     w.W_sp = g.W_sp;
     w.N = w.H_sp * w.W_sp;
     const int nwx = a.reso / w.W_sp, nwin = (a.reso / w.H_sp) * nwx;
-    int id = blockIdx.x;
+    // XCD-aware order: the split partners of a window-head (consecutive logical ids) run on one
+    // XCD, so the window's K/V gather is fetched into that XCD's L2 once
+    int id = (int)xcd_tile(blockIdx.x, gridDim.x);
     w.blk = id % split; id /= split;
     w.h = id % a.heads; id /= a.heads;
     const int win = id % nwin;

@@ -1,0 +1,32 @@
+"""Stage-3 (and stage-1/2) stripe attention fwd / bwd kernel times with HIP events (eager)."""
+import os, sys
+sys.path[:0] = [os.path.join(os.path.dirname(__file__), ".."), os.path.join(os.path.dirname(__file__), "..", "cswin-simam-unet_amd")]
+import torch
+from csu import ops
+d = torch.device("cuda")
+
+
+def t(fn, n=20):
+    fn()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(n):
+        fn()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / n * 1e3
+
+
+for B, reso, C, heads, sw in [(16, 32, 256, 8, 8), (16, 64, 128, 4, 2), (16, 128, 64, 2, 1)]:
+    geom = ops.StripeGeometry(reso, C, heads // 2, [(reso, sw, 0), (sw, reso, C // 2)], 32 ** -0.5)
+    qkv = torch.randn(B, reso * reso, 3 * C, device=d, dtype=torch.bfloat16, requires_grad=True)
+    ws = [torch.randn(C // 2, 1, 3, 3, device=d, requires_grad=True) for _ in range(2)]
+    bs = [torch.randn(C // 2, device=d, requires_grad=True) for _ in range(2)]
+    g = torch.randn(B, reso * reso, C, device=d, dtype=torch.bfloat16)
+    f = t(lambda: ops.stripe_attention(qkv, geom, ws, bs))
+    def fb():
+        out = ops.stripe_attention(qkv, geom, ws, bs)
+        out.backward(g)
+    tb = t(fb)
+    print(f"reso {reso} C {C} sw {sw}: fwd {f:7.1f} us  fwd+bwd {tb:7.1f} us", flush=True)
