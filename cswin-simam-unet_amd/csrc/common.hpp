@@ -93,6 +93,13 @@ __device__ __forceinline__ long xcd_tile(long id, long total) {
     return x < rem ? x * (q + 1) + k : rem * (q + 1) + (x - rem) * q + k;
 }
 
+// xcd_tile over the whole (x, y, z) grid: the logical id of this workgroup
+__device__ __forceinline__ long xcd_block() {
+    const long total = (long)gridDim.x * gridDim.y * gridDim.z;
+    const long id = blockIdx.x + (long)gridDim.x * (blockIdx.y + (long)gridDim.y * blockIdx.z);
+    return xcd_tile(id, total);
+}
+
 // ---- raw buffer access: out-of-range offsets are dropped (stores) / read as 0 (loads) by the
 // hardware, so bounds checks need no branches (a branch around a store makes hipcc wait
 // vmcnt(0) at the join, serialising an epilogue's stores).
