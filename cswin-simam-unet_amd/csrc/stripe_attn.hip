@@ -493,7 +493,10 @@ __global__ __launch_bounds__(NT, 4) void lepe_wgrad_partial(csu_stripe_args a, c
     float acc[40];   // [k][j]: tap k (9 = bias) x channel j of the quad
 #pragma unroll
     for (int i = 0; i < 40; ++i) acc[i] = 0.f;
-    for (long ri = (long)blockIdx.x * per_blk + threadIdx.x / nq; ri < runs; ri += (long)gridDim.x * per_blk) {
+    // XCD-aware: consecutive logical blocks (adjacent image rows, which share V neighbourhood rows)
+    // run on one XCD
+    const long lb = xcd_tile(blockIdx.x, gridDim.x);
+    for (long ri = lb * per_blk + threadIdx.x / nq; ri < runs; ri += (long)gridDim.x * per_blk) {
         const int seg = (int)(ri % nseg);
         const long r2 = ri / nseg;
         const int y = (int)(r2 % reso), b = (int)(r2 / reso);
