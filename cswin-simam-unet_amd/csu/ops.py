@@ -427,10 +427,11 @@ def gemm(a2: torch.Tensor, b: torch.Tensor, b_trans: bool, out_dtype, bias=None,
 # chain.  Fork: the side stream waits on the launching stream; inputs are record_stream'ed; the
 # launching stream waits on every side event at the end of backward (autograd final callback),
 # before the optimizer or any user code can read .grad.  Off under multi-rank DDP (its reducer
-# reads gradients from hooks during backward).  Opt-in (CSU_SIDE_WGRAD=1): on the 512x512 step the
-# overlapped kernels slow each other down and the graphed step time does not improve.
+# reads gradients from hooks during backward).  On by default since the latency-bound kernels of
+# the fused Mlp / attention backward left room for it: +0.6 % on the graphed 512x512 step
+# (978 -> 984 img/s, two interleaved A/B pairs, tools/ab_env.sh); CSU_SIDE_WGRAD=0 disables.
 # ---------------------------------------------------------------------------------------------
-SIDE_WGRAD = _os.environ.get("CSU_SIDE_WGRAD", "0") == "1"
+SIDE_WGRAD = _os.environ.get("CSU_SIDE_WGRAD", "1") == "1"
 _SIDE_STREAMS = {}
 _SIDE_PENDING = []
 _SIDE_JOIN_QUEUED = [False]
