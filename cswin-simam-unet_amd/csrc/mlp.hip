@@ -140,11 +140,12 @@ template <int V> using iconst = std::integral_constant<int, V>;
 
 // Forward.  Rings: W1 chunks in 2 stages, W2 chunks in 2 stages.  Step j (after one barrier):
 // DMA W1(j+2), W2(j+1); GEMM1(j+1) on the MFMA pipe while GELU(j) runs on the VALU; GEMM2(j).
-template <int C>
+// STORE_H: also write the pre-activation h = fc1(x) (bf16, M x 4C) for a GEMM-form backward
+template <int C, bool STORE_H>
 __global__ __launch_bounds__(MT) void mlp_fwd_kernel(long M, const bf16* __restrict__ X, const bf16* __restrict__ W1,
                                                      const float* __restrict__ b1, const bf16* __restrict__ W2,
                                                      const float* __restrict__ b2, const float* __restrict__ res,
-                                                     float* __restrict__ out) {
+                                                     float* __restrict__ out, bf16* __restrict__ hout) {
     constexpr int NCH = 4 * C / HC;     // hidden chunks
     constexpr int KS = C / 16;          // k-steps of GEMM1
     constexpr int TF = C / 32;          // 32-feature output tiles (all C, partial over the hidden half)
@@ -197,10 +198,12 @@ __global__ __launch_bounds__(MT) void mlp_fwd_kernel(long M, const bf16* __restr
     f32x16 ha = gemm1(w1r), hb;
 
     // par = j & 1 as a compile-time constant: every LDS address is a per-lane base + immediate
+    const auto rs_h = buf_rsrc(STORE_H ? hout + m0 * 4 * C : nullptr, STORE_H ? rows * 4 * C * 2 : 0);
     auto step = [&](auto more, auto par, int j, const f32x16& cur, f32x16& nxt) {
         constexpr int P = decltype(par)::value;
 #ifndef MLP_EXP_NOBAR
-        vmwait<0>();                    // W1(j+1), W2(j): issued one step ago
+        // W1(j+1), W2(j): issued one step ago; after them only the previous step's 4 h stores
+        if constexpr (STORE_H) vmwait<4>(); else vmwait<0>();
         lds_sync();                     // every wave is past GEMM1(j) and GEMM2(j-1)
 #endif
 #ifndef MLP_EXP_NODMA
@@ -217,6 +220,16 @@ __global__ __launch_bounds__(MT) void mlp_fwd_kernel(long M, const bf16* __restr
 #else
             gv[e] = gelu_fast(cur[e] + bv[e]);
 #endif
+        }
+        if constexpr (STORE_H) {   // h of chunk j: features hs + 8g + 4h .. + 3 of token tok
+            const unsigned base = ok ? (unsigned)(tok * 4 * C + j * HC + hs + 4 * h) * 2 : kOOB;
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                float hv[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) hv[e] = cur[4 * g + e] + bv[4 * g + e];
+                buf_st4bf(rs_h, base == kOOB ? kOOB : base + 16 * g, hv);
+            }
         }
         const bf16* w2c = w2r + P * IMG;
 #pragma unroll
@@ -393,9 +406,14 @@ __global__ __launch_bounds__(MT) void mlp_bwd_kernel(long M, const bf16* __restr
 
 template <int C>
 int fwd_launch(long M, const void* x, const void* w1, const float* b1, const void* w2, const float* b2, const float* res,
-               float* out, hipStream_t st) {
-    mlp_fwd_kernel<C><<<dim3((unsigned)((M + BM - 1) / BM)), MT, 0, st>>>(M, (const bf16*)x, (const bf16*)w1, b1,
-                                                                          (const bf16*)w2, b2, res, out);
+               float* out, void* h, hipStream_t st) {
+    const dim3 grid((unsigned)((M + BM - 1) / BM));
+    if (h)
+        mlp_fwd_kernel<C, true><<<grid, MT, 0, st>>>(M, (const bf16*)x, (const bf16*)w1, b1, (const bf16*)w2, b2, res, out,
+                                                     (bf16*)h);
+    else
+        mlp_fwd_kernel<C, false><<<grid, MT, 0, st>>>(M, (const bf16*)x, (const bf16*)w1, b1, (const bf16*)w2, b2, res, out,
+                                                      nullptr);
     return check_launch("mlp_fwd");
 }
 
@@ -415,15 +433,23 @@ using namespace csu;
 
 extern "C" int csu_mlp_supported(int C) { return C == 64 || C == 128 || C == 256; }
 
+extern "C" int csu_mlp_fwd_ex(long M, int C, const void* x, const void* w1, const float* b1, const void* w2,
+                              const float* b2, const float* res, float* out, void* h, void* stream);
+
 extern "C" int csu_mlp_fwd(long M, int C, const void* x, const void* w1, const float* b1, const void* w2, const float* b2,
                            const float* res, float* out, void* stream) {
+    return csu_mlp_fwd_ex(M, C, x, w1, b1, w2, b2, res, out, nullptr, stream);
+}
+
+extern "C" int csu_mlp_fwd_ex(long M, int C, const void* x, const void* w1, const float* b1, const void* w2,
+                              const float* b2, const float* res, float* out, void* h, void* stream) {
     if (M < 1 || !x || !w1 || !b1 || !w2 || !b2 || !res || !out) return fail(CSU_E_ARG, "mlp_fwd: bad arguments");
     if (M * 4L * C * 2 > 0x7fffffffL) return fail(CSU_E_ARG, "mlp_fwd: tensor exceeds 2 GB buffer range");
     const hipStream_t st = as_stream(stream);
     switch (C) {
-        case 64: return fwd_launch<64>(M, x, w1, b1, w2, b2, res, out, st);
-        case 128: return fwd_launch<128>(M, x, w1, b1, w2, b2, res, out, st);
-        case 256: return fwd_launch<256>(M, x, w1, b1, w2, b2, res, out, st);
+        case 64: return fwd_launch<64>(M, x, w1, b1, w2, b2, res, out, h, st);
+        case 128: return fwd_launch<128>(M, x, w1, b1, w2, b2, res, out, h, st);
+        case 256: return fwd_launch<256>(M, x, w1, b1, w2, b2, res, out, h, st);
         default: return fail(CSU_E_ARG, "mlp_fwd: C must be 64, 128 or 256");
     }
 }

@@ -131,7 +131,7 @@ __device__ __forceinline__ bf16x8 tr_frag(const bf16* img, int c0, int s, int la
     return out;
 }
 
-__device__ __forceinline__ float gelu_w(float v) { return 0.5f * v * (1.f + erff(v * 0.70710678118654752f)); }
+__device__ __forceinline__ float gelu_w(float v) { return gelu_fast(v); }   // common.hpp (A-S 7.1.25)
 
 template <int T, bool GELU_X>
 __global__ __launch_bounds__(NT) void wgrad_bf16_tr(long M, int N, int K, long rows_per_chunk, const bf16* __restrict__ dy,

@@ -91,6 +91,8 @@ _SIGS = {
     "csu_mlp_supported": (ctypes.c_int, [ctypes.c_int]),
     "csu_mlp_fwd": (ctypes.c_int, [ctypes.c_long, ctypes.c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                    c_void_p, c_void_p]),
+    "csu_mlp_fwd_ex": (ctypes.c_int, [ctypes.c_long, ctypes.c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                      c_void_p, c_void_p, c_void_p]),
     "csu_mlp_bwd": (ctypes.c_int, [ctypes.c_long, ctypes.c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                    c_void_p, c_void_p, c_void_p]),
     "csu_conv2d_fwd": (ctypes.c_int, [ctypes.POINTER(ConvGeom), ctypes.c_int, c_void_p, c_void_p, c_void_p, c_void_p,

@@ -637,9 +637,15 @@ def linear_residual(res, x, weight, bias):
 
 class _MlpFusedFn(torch.autograd.Function):
     """res + fc2(gelu(fc1(x))) (Mlp cswin:180-196 + residual cswin:368) in ONE csu_mlp_fwd launch
-    (the 4C hidden layer never reaches HBM).  Backward: one csu_mlp_bwd launch recomputes
-    h = fc1(x) and writes dh = (dY W2) * gelu'(h), g = gelu(h) and dx = dh W1; then the two
-    weight-gradient GEMMs dW1 = dh^T x, dW2 = dY^T g (+ column sums for the biases)."""
+    (the 4C hidden layer never reaches HBM as gelu(h)).
+
+    Backward, two forms (CSU_MLP_BWD):
+      "fused" (default): one csu_mlp_bwd launch recomputes h and writes dh, g = gelu(h) and dx;
+      "gemm": the forward also writes h = fc1(x) (csu_mlp_fwd_ex); dh = (dY W2) * gelu'(h) is one
+        gemm4 launch with the GELU' epilogue, dx = dh W1 a second, dW2 = dY^T gelu(h) with gelu
+        applied while staging h (linear_wgrad_gelu), dW1 = dh^T x.  Faster in isolation
+        (tools/mlp_probe.py) but 4 % slower on the graphed step (941 vs 983 img/s, A/B r01aa):
+        the h write and the extra launches cost more than the fused kernel's latency."""
 
     @staticmethod
     def forward(ctx, res, x, w1, b1, w2, b2, w1c, w2c):
@@ -648,16 +654,33 @@ class _MlpFusedFn(torch.autograd.Function):
         x2 = x.reshape(-1, C).contiguous()
         b1f = b1.detach().float().contiguous()
         y = torch.empty_like(res2)
-        check(lib().csu_mlp_fwd(x2.shape[0], C, ptr(x2), ptr(w1c), ptr(b1f), ptr(w2c), ptr(b2.detach().float().contiguous()),
-                                ptr(res2), ptr(y), stream_ptr(x2.device)), "csu_mlp_fwd")
-        ctx.save_for_backward(x2, w1c, b1f, w2c)
-        ctx.meta = (res.dtype, x.shape, w1.dtype, b1.dtype, w2.dtype, b2.dtype)
+        h = torch.empty(x2.shape[0], 4 * C, dtype=torch.bfloat16, device=x2.device) if MLP_BWD == "gemm" else None
+        check(lib().csu_mlp_fwd_ex(x2.shape[0], C, ptr(x2), ptr(w1c), ptr(b1f), ptr(w2c),
+                                   ptr(b2.detach().float().contiguous()), ptr(res2), ptr(y), ptr(h) if h is not None else None,
+                                   stream_ptr(x2.device)), "csu_mlp_fwd_ex")
+        if h is not None:
+            ctx.save_for_backward(x2, h, _weight_t(w1, w1c), _weight_t(w2, w2c))
+        else:
+            ctx.save_for_backward(x2, w1c, b1f, w2c)
+        ctx.meta = (res.dtype, x.shape, w1.dtype, b1.dtype, w2.dtype, b2.dtype, h is not None)
         return y.view(res.shape)
 
     @staticmethod
     def backward(ctx, dy):
+        rdt, xshape, w1dt, b1dt, w2dt, b2dt, gemm_form = ctx.meta
+        if gemm_form:
+            x2, h, w1t, w2t = ctx.saved_tensors
+            M, C = x2.shape
+            dyb = _bf16_of(dy).view(-1, C)
+            dh = gemm(dyb, w2t, False, torch.bfloat16, gelu_aux=h)         # (dY W2) * gelu'(h)
+            if _side_ok(dyb, w2dt, b2dt):
+                dw2, db2 = _side_run(lambda: linear_wgrad_gelu(dyb, h), dyb, h)
+            else:
+                dw2, db2 = linear_wgrad_gelu(dyb, h)
+            dx = gemm(dh, w1t, False, torch.bfloat16)
+            dw1, db1 = wgrad_maybe_side(dh, x2, w1dt, b1dt)
+            return dy.to(rdt), dx.view(xshape), dw1.to(w1dt), db1.to(b1dt), dw2.to(w2dt), db2.to(b2dt), None, None
         x2, w1c, b1f, w2c = ctx.saved_tensors
-        rdt, xshape, w1dt, b1dt, w2dt, b2dt = ctx.meta
         M, C = x2.shape
         dyb = _bf16_of(dy).view(-1, C)
         dh = torch.empty(M, 4 * C, dtype=torch.bfloat16, device=x2.device)
@@ -670,8 +693,9 @@ class _MlpFusedFn(torch.autograd.Function):
         return dy.to(rdt), dx.view(xshape), dw1.to(w1dt), db1.to(b1dt), dw2.to(w2dt), db2.to(b2dt), None, None
 
 
-# CSU_FUSED_MLP=0 selects the two-GEMM Mlp (A/B comparisons)
+# CSU_FUSED_MLP=0 selects the two-GEMM Mlp (A/B comparisons); CSU_MLP_BWD=gemm|fused the backward form
 FUSED_MLP = _os.environ.get("CSU_FUSED_MLP", "1") == "1"
+MLP_BWD = _os.environ.get("CSU_MLP_BWD", "fused")
 
 
 def mlp_residual(res, x, fc1: torch.nn.Linear, fc2: torch.nn.Linear):

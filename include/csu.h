@@ -259,6 +259,11 @@ int csu_mlp_fwd(long M, int C, const void* x, const void* w1, const float* b1, c
                 const float* res, float* out, void* stream);
 int csu_mlp_bwd(long M, int C, const void* x, const void* dy, const void* w1, const float* b1, const void* w2,
                 void* dh, void* g, void* dx, void* stream);
+/* csu_mlp_fwd plus the pre-activation h = fc1(x) (bf16, M x 4C) written to `h` (NULL: not
+ * written) -- the operand of the GEMM-form backward (dh = (dy w2) * gelu'(h) in a GEMM epilogue,
+ * dW2 from gelu(h) on the fly in the weight-gradient GEMM). */
+int csu_mlp_fwd_ex(long M, int C, const void* x, const void* w1, const float* b1, const void* w2, const float* b2,
+                   const float* res, float* out, void* h, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * Implicit-GEMM NHWC convolution (patch embed cswin:505, Merge_Block.conv cswin:376, CARAFE
