@@ -18,12 +18,19 @@
 //    so the epilogue reads bias / GELU-aux / residual and writes outputs as 4-wide vectors
 //    straight from registers (no LDS staging, no barriers).
 //  * XCD-aware tile order (xcd_tile): the N tiles of one token panel run on one XCD's L2.
-#include "common.hpp"
+#include "lds_dma.hpp"
 
 namespace csu {
 namespace {
 
 constexpr int G4_NT = 256;
+
+#ifdef G4_TIMING   // debug build only: per-workgroup phase timestamps (s_memtime), read by csu_debug_g4_ts
+__device__ unsigned long long g4_ts[8][4096];
+#define G4_STAMP(k) do { if (threadIdx.x == 0 && blockIdx.x < 4096) g4_ts[k][blockIdx.x] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define G4_STAMP(k) do {} while (0)
+#endif
 constexpr int G4_BK = 64;
 
 
@@ -49,12 +56,18 @@ __device__ __forceinline__ void g4_voff(int ld, int wave, int lane, unsigned* vo
 // whose size ends at the matrix's last row, so rows past the end read as 0 (hardware range check);
 // soff = the k offset in bytes (scalar).  Only scalar work per call: the lane offsets are fixed.
 template <int ROWS>
-__device__ __forceinline__ void g4_dma(__amdgpu_buffer_rsrc_t rs, const unsigned* voff, unsigned soff, bf16* img,
-                                       int wave) {
+__device__ __forceinline__ void g4_dma(i32x4 rs, const unsigned* voff, unsigned soff, bf16* img, int wave) {
+#ifdef G4_BUILTIN_DMA
+    const __amdgpu_buffer_rsrc_t r = __builtin_bit_cast(__amdgpu_buffer_rsrc_t, rs);
 #pragma unroll
     for (int i = 0; i < ROWS / 32; ++i)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(img + (wave * (ROWS / 32) + i) * 8 * G4_BK),
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)(img + (wave * (ROWS / 32) + i) * 8 * G4_BK),
                                                  16, voff[i], soff, 0, 0);
+#else
+    // inline asm (lds_dma.hpp): the compiler would otherwise wait vmcnt(0) before LDS reads that may
+    // alias an in-flight DMA stage, which makes every ring deeper than 2 stages useless
+    dma<ROWS / 32>(rs, voff, soff, img, wave);   // same lane-linear 1-KB blocks: (wave * ROWS/32 + i) * 512
+#endif
 }
 
 template <int N> __device__ __forceinline__ void g4_vmwait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
@@ -139,8 +152,8 @@ __global__ __launch_bounds__(G4_NT, OCC) void gemm4_kernel(long M, int N, int K,
         const unsigned soff = (unsigned)(uu % nk) * G4_BK * 2;
         bf16* st = smem + (u % S) * STAGE;
         const long ra = (long)(tile / nbn) * BM, rw = (long)(tile % nbn) * BN;
-        g4_dma<BM>(buf_rsrc(A + ra * lda, (M - ra) * lda * 2), voffA, soff, st, wave);
-        g4_dma<BN>(buf_rsrc(W + rw * ldw, (N - rw) * ldw * 2), voffW, soff, st + BM * G4_BK, wave);
+        g4_dma<BM>(rsrc4(A + ra * lda, (M - ra) * lda * 2), voffA, soff, st, wave);
+        g4_dma<BN>(rsrc4(W + rw * ldw, (N - rw) * ldw * 2), voffW, soff, st + BM * G4_BK, wave);
     };
     auto wait_unit = [&](int u) {   // vector-memory ops issued after unit u's DMA (issued at step u - P)
         const int w = u - P;
@@ -179,12 +192,14 @@ __global__ __launch_bounds__(G4_NT, OCC) void gemm4_kernel(long M, int N, int K,
         }
     };
 
+    G4_STAMP(0);
 #pragma unroll
     for (int p = 0; p < P; ++p) issue(p);
     int u = 0;
     for (int t = 0; t < mytiles; ++t) {
         for (int ks = 0; ks + 1 < nk; ++ks, ++u) {   // all but the tile's last K slice
             wait_unit(u);
+            if (t == 0 && ks == 0) G4_STAMP(1);
             issue(u + P);
             mma(u);
         }
@@ -193,6 +208,7 @@ __global__ __launch_bounds__(G4_NT, OCC) void gemm4_kernel(long M, int N, int K,
         // 8 (l % CPR) .. + 7.  Raw buffer ops relative to the tile's first row; out-of-tile
         // elements get an out-of-range offset (no branches: see buf_rsrc).
         wait_unit(u);
+        if (t == 0) G4_STAMP(2);
         const unsigned tile = lo + kk + (unsigned)t * nloc;
         const long m0 = (long)(tile / nbn) * BM;
         const int n0 = (int)(tile % nbn) * BN;
@@ -231,6 +247,7 @@ __global__ __launch_bounds__(G4_NT, OCC) void gemm4_kernel(long M, int N, int K,
         __builtin_amdgcn_sched_barrier(0);
         issue(u + P);
         mma(u);
+        if (t == 0) G4_STAMP(3);
         const auto rs_out = buf_rsrc(out + m0 * ldc, rows * ldc * OS);
         const auto rs_g = buf_rsrc(gout ? gout + m0 * ldc : nullptr, gout ? rows * ldc * 2 : 0);
         float* ep = reinterpret_cast<float*>(smem + S * STAGE) + wave * (EPB / 4);
@@ -282,8 +299,10 @@ __global__ __launch_bounds__(G4_NT, OCC) void gemm4_kernel(long M, int N, int K,
 #pragma unroll
             for (int j = 0; j < TNW; ++j) acc[i][j] = f32x16{};
         ++u;
+        if (t == 0) G4_STAMP(4);
     }
     g4_vmwait<0>();   // drain the re-fetch DMAs before the workgroup's LDS is released
+    G4_STAMP(5);
 }
 
 struct G4Cfg { int bm, bn, s, occ; };
@@ -346,3 +365,9 @@ int gemm4_run(int cfg, int epi, int odt, long M, int N, int K, const bf16* A, in
 }
 
 }  // namespace csu
+
+#ifdef G4_TIMING
+extern "C" int csu_debug_g4_ts(unsigned long long* host, int n) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(csu::g4_ts), (size_t)n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : 1;
+}
+#endif

@@ -32,5 +32,7 @@ torch.cuda.synchronize()
 with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True) as prof:
     step()
     torch.cuda.synchronize()
-print(prof.key_averages(group_by_input_shape=True).table(sort_by="self_cuda_time_total", row_limit=45, max_name_column_width=40,
-                                                         max_shapes_column_width=70))
+rows = [e for e in prof.key_averages(group_by_input_shape=True) if e.key.startswith("aten::") and e.self_device_time_total > 0]
+rows.sort(key=lambda e: -e.self_device_time_total)
+for e in rows[:40]:
+    print(f"{e.self_device_time_total:9.1f} us  n={e.count:4d}  {e.key:32s} {str(e.input_shapes)[:150]}")
