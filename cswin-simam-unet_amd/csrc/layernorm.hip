@@ -223,6 +223,7 @@ int launch_bwd(int rows, int C, const void* x, const float* g, const float* m, c
     }
 #undef CSU_LNB
     if (int e = check_launch("layernorm_bwd")) return e;
+    if (!dgamma) return 0;   // partials stay in the workspace: csu_layernorm_param_reduce
     ln_param_reduce<<<(2 * C + WAVES - 1) / WAVES, NT, 0, st>>>(C, nb, part, dgamma, dbeta);
     return check_launch("layernorm_bwd reduce");
 }
@@ -255,7 +256,7 @@ extern "C" int csu_layernorm_bwd_ex(int rows, int C, int xdtype, const void* x, 
                                     void* dx_bf16, float* dgamma, float* dbeta, void* workspace, size_t ws_bytes,
                                     void* stream) {
     if (int e = check_c(C)) return e;
-    if (rows < 1 || !x || !gamma || !mean || !rstd || !dy || !dx || !dgamma || !dbeta)
+    if (rows < 1 || !x || !gamma || !mean || !rstd || !dy || !dx || (!dgamma) != (!dbeta))
         return fail(CSU_E_ARG, "layernorm_bwd: bad args");
     if (!workspace || ws_bytes < csu_layernorm_bwd_workspace(rows, C))
         return fail(CSU_E_WORKSPACE, "layernorm_bwd: workspace too small");
@@ -277,4 +278,17 @@ extern "C" int csu_layernorm_bwd(int rows, int C, int xdtype, const void* x, con
                                  float* dbeta, void* workspace, size_t ws_bytes, void* stream) {
     return csu_layernorm_bwd_ex(rows, C, xdtype, x, gamma, mean, rstd, dydtype, dy, nullptr, dx, nullptr, dgamma, dbeta,
                                 workspace, ws_bytes, stream);
+}
+
+// dgamma / dbeta from the per-block partials a csu_layernorm_bwd_ex call with NULL dgamma/dbeta
+// left in `workspace` (the same rows / C): lets the reduction run on another stream
+extern "C" int csu_layernorm_param_reduce(int rows, int C, const void* workspace, float* dgamma, float* dbeta,
+                                          void* stream) {
+    if (int e = check_c(C)) return e;
+    if (rows < 1 || !workspace || !dgamma || !dbeta) return fail(CSU_E_ARG, "layernorm_param_reduce: bad args");
+    int rpb;
+    const int nb = ln_blocks(rows, C >= 256 ? 1 : 256 / C, &rpb);
+    ln_param_reduce<<<(2 * C + WAVES - 1) / WAVES, NT, 0, as_stream(stream)>>>(C, nb, (const float*)workspace, dgamma,
+                                                                                dbeta);
+    return check_launch("layernorm_param_reduce");
 }

@@ -1054,9 +1054,12 @@ extern "C" int csu_stripe_attn_bwd(const csu_stripe_args* a, int dtype, const vo
                                    void* workspace, size_t workspace_bytes, void* stream) {
     if (int e = validate(a, dtype)) return e;
     if (!qkv || !out || !dout || !lse || !delta || !dqkv) return fail(CSU_E_ARG, "stripe_attn_bwd: null buffer");
-    for (int i = 0; i < a->nbranch; ++i)
-        if (!a->br[i].lepe_dw || !a->br[i].lepe_db) return fail(CSU_E_ARG, "stripe_attn_bwd: null LePE grads");
-    if (workspace_bytes < csu_stripe_attn_bwd_workspace(a) || !workspace)
+    // all LePE weight-gradient pointers NULL: skip that part (csu_stripe_lepe_wgrad, e.g. on another stream)
+    int nnull = 0;
+    for (int i = 0; i < a->nbranch; ++i) nnull += (!a->br[i].lepe_dw) + (!a->br[i].lepe_db);
+    const bool do_lepe = nnull == 0;
+    if (nnull && nnull != 2 * a->nbranch) return fail(CSU_E_ARG, "stripe_attn_bwd: null LePE grads");
+    if (do_lepe && (workspace_bytes < csu_stripe_attn_bwd_workspace(a) || !workspace))
         return fail(CSU_E_WORKSPACE, "stripe_attn_bwd: workspace too small");
     {
         const int nq = a->heads * HD / 4;   // LePE weight-gradient layout: channel quads per branch
@@ -1075,16 +1078,41 @@ extern "C" int csu_stripe_attn_bwd(const csu_stripe_args* a, int dtype, const vo
         const dim3 g(a->B * nwin * a->heads * sp, a->nbranch);
         stripe_bwd_dq_w<<<g, NT, 0, st>>>(*a, sp, (const bf16*)qkv, (const bf16*)out, (const bf16*)dout, lse, delta, (bf16*)dqkv);
         stripe_bwd_dkdv_w<<<g, NT, 0, st>>>(*a, sp, (const bf16*)qkv, (const bf16*)dout, lse, delta, (bf16*)dqkv);
-        lepe_wgrad_partial<bf16><<<dim3(nblk, a->nbranch), NT, 0, st>>>(*a, (const bf16*)qkv, (const bf16*)dout, part);
     } else if (dtype == CSU_BF16) {
         stripe_bwd_dq<bf16><<<grid, NT, 0, st>>>(*a, (const bf16*)qkv, (const bf16*)out, (const bf16*)dout, lse, delta, (bf16*)dqkv);
         stripe_bwd_dkdv<bf16><<<grid, NT, 0, st>>>(*a, (const bf16*)qkv, (const bf16*)dout, lse, delta, (bf16*)dqkv);
-        lepe_wgrad_partial<bf16><<<dim3(nblk, a->nbranch), NT, 0, st>>>(*a, (const bf16*)qkv, (const bf16*)dout, part);
     } else {
         stripe_bwd_dq<float><<<grid, NT, 0, st>>>(*a, (const float*)qkv, (const float*)out, (const float*)dout, lse, delta, (float*)dqkv);
         stripe_bwd_dkdv<float><<<grid, NT, 0, st>>>(*a, (const float*)qkv, (const float*)dout, lse, delta, (float*)dqkv);
-        lepe_wgrad_partial<float><<<dim3(nblk, a->nbranch), NT, 0, st>>>(*a, (const float*)qkv, (const float*)dout, part);
     }
-    lepe_wgrad_reduce<<<rgrid, 256, 0, st>>>(*a, nblk, part);
+    if (do_lepe) {
+        if (dtype == CSU_BF16)
+            lepe_wgrad_partial<bf16><<<dim3(nblk, a->nbranch), NT, 0, st>>>(*a, (const bf16*)qkv, (const bf16*)dout, part);
+        else
+            lepe_wgrad_partial<float><<<dim3(nblk, a->nbranch), NT, 0, st>>>(*a, (const float*)qkv, (const float*)dout, part);
+        lepe_wgrad_reduce<<<rgrid, 256, 0, st>>>(*a, nblk, part);
+    }
     return check_launch("stripe_attn_bwd");
+}
+
+extern "C" int csu_stripe_lepe_wgrad(const csu_stripe_args* a, int dtype, const void* qkv, const void* dout,
+                                     void* workspace, size_t workspace_bytes, void* stream) {
+    if (int e = validate(a, dtype)) return e;
+    if (!qkv || !dout) return fail(CSU_E_ARG, "stripe_lepe_wgrad: null buffer");
+    for (int i = 0; i < a->nbranch; ++i)
+        if (!a->br[i].lepe_dw || !a->br[i].lepe_db) return fail(CSU_E_ARG, "stripe_lepe_wgrad: null LePE grads");
+    if (workspace_bytes < csu_stripe_attn_bwd_workspace(a) || !workspace)
+        return fail(CSU_E_WORKSPACE, "stripe_lepe_wgrad: workspace too small");
+    const int nq = a->heads * HD / 4;
+    if (NT % nq || (nq & (nq - 1))) return fail(CSU_E_UNSUPPORTED, "stripe_lepe_wgrad: heads per branch must be a power of two <= 32");
+    hipStream_t st = as_stream(stream);
+    const int nblk = wgrad_blocks(*a);
+    float* part = (float*)workspace;
+    const dim3 rgrid((a->nbranch * a->heads * HD * 10 + 3) / 4);
+    if (dtype == CSU_BF16)
+        lepe_wgrad_partial<bf16><<<dim3(nblk, a->nbranch), NT, 0, st>>>(*a, (const bf16*)qkv, (const bf16*)dout, part);
+    else
+        lepe_wgrad_partial<float><<<dim3(nblk, a->nbranch), NT, 0, st>>>(*a, (const float*)qkv, (const float*)dout, part);
+    lepe_wgrad_reduce<<<rgrid, 256, 0, st>>>(*a, nblk, part);
+    return check_launch("stripe_lepe_wgrad");
 }

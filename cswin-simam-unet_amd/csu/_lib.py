@@ -89,6 +89,9 @@ _SIGS = {
                                       c_float, c_void_p, c_float, c_void_p]),
     "csu_gemm_ex": (ctypes.c_int, [ctypes.POINTER(GemmDesc), c_void_p]),
     "csu_mlp_supported": (ctypes.c_int, [ctypes.c_int]),
+    "csu_layernorm_param_reduce": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "csu_stripe_lepe_wgrad": (ctypes.c_int, [ctypes.POINTER(StripeArgs), ctypes.c_int, c_void_p, c_void_p, c_void_p, c_size_t,
+                                             c_void_p]),
     "csu_mlp_fwd": (ctypes.c_int, [ctypes.c_long, ctypes.c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                    c_void_p, c_void_p]),
     "csu_mlp_fwd_ex": (ctypes.c_int, [ctypes.c_long, ctypes.c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,

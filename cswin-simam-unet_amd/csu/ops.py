@@ -112,10 +112,26 @@ class _StripeAttnFn(torch.autograd.Function):
         B = qkv.shape[0]
         dqkv = torch.empty_like(qkv)
         delta = torch.empty_like(lse)
+        L = lib()
+        if SIDE_AUX and _side_ok(qkv, *ctx.lepe_dtypes):
+            # LePE weight gradient on the side stream, concurrent with the dQ / dK / dV kernels
+            def lepe_grads():
+                dws = [torch.empty_like(w) for w in ws]
+                dbs = [torch.empty_like(b) for b in bs]
+                a2 = geom.args(B, ws, bs, dws, dbs)
+                nb2 = L.csu_stripe_attn_bwd_workspace(ctypes.byref(a2))
+                work2 = torch.empty(max(nb2, 16), dtype=torch.uint8, device=qkv.device)
+                check(L.csu_stripe_lepe_wgrad(ctypes.byref(a2), dtype_code(qkv), ptr(qkv), ptr(dout), ptr(work2), nb2,
+                                              stream_ptr(qkv.device)), "csu_stripe_lepe_wgrad")
+                return dws + dbs
+            grads = _side_run(lepe_grads, qkv, dout)
+            a = geom.args(B, ws, bs)        # NULL LePE gradients: the main call skips them
+            check(L.csu_stripe_attn_bwd(ctypes.byref(a), dtype_code(qkv), ptr(qkv), ptr(out), ptr(dout), ptr(lse),
+                                        ptr(delta), ptr(dqkv), None, 0, stream_ptr(qkv.device)), "csu_stripe_attn_bwd")
+            return (dqkv, None, *grads)
         dws = [torch.empty_like(w) for w in ws]
         dbs = [torch.empty_like(b) for b in bs]
         a = geom.args(B, ws, bs, dws, dbs)
-        L = lib()
         nbytes = L.csu_stripe_attn_bwd_workspace(ctypes.byref(a))
         work = torch.empty(max(nbytes, 16), dtype=torch.uint8, device=qkv.device)
         check(L.csu_stripe_attn_bwd(ctypes.byref(a), dtype_code(qkv), ptr(qkv), ptr(out), ptr(dout), ptr(lse),
@@ -223,13 +239,22 @@ class _LayerNormForkFn(torch.autograd.Function):
         dres_k = dres.float().contiguous() if (dres is not None and fp32) else None
         dx = torch.empty_like(x)
         dxb = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device) if fp32 else None
-        dgb = torch.empty(2 * C, dtype=torch.float32, device=x.device)
         L = lib()
         nbytes = L.csu_layernorm_bwd_workspace(rows, C)
         work = torch.empty(max(nbytes, 16), dtype=torch.uint8, device=x.device)
+        side = SIDE_AUX and _side_ok(x, *ctx.pdtypes)
+        dgb = None if side else torch.empty(2 * C, dtype=torch.float32, device=x.device)
         check(L.csu_layernorm_bwd_ex(rows, C, dtype_code(x), ptr(x), ptr(w), ptr(mean), ptr(rstd), dtype_code(dy), ptr(dy),
-                                     ptr(dres_k), ptr(dx), ptr(dxb), ptr(dgb[:C]), ptr(dgb[C:]), ptr(work), nbytes,
-                                     stream_ptr(x.device)), "csu_layernorm_bwd_ex")
+                                     ptr(dres_k), ptr(dx), ptr(dxb), None if side else ptr(dgb[:C]),
+                                     None if side else ptr(dgb[C:]), ptr(work), nbytes, stream_ptr(x.device)),
+              "csu_layernorm_bwd_ex")
+        if side:   # dgamma / dbeta reduction off the input-gradient chain
+            def reduce():
+                out = torch.empty(2 * C, dtype=torch.float32, device=x.device)
+                check(L.csu_layernorm_param_reduce(rows, C, ptr(work), ptr(out[:C]), ptr(out[C:]), stream_ptr(x.device)),
+                      "csu_layernorm_param_reduce")
+                return out
+            dgb = _side_run(reduce, work)
         if dres is not None and not fp32:    # non-fp32 residual stream: plain add (not on the bf16 path)
             dx = dx + dres.to(dx.dtype)
         if dxb is not None:
@@ -432,6 +457,10 @@ def gemm(a2: torch.Tensor, b: torch.Tensor, b_trans: bool, out_dtype, bias=None,
 # (978 -> 984 img/s, two interleaved A/B pairs, tools/ab_env.sh); CSU_SIDE_WGRAD=0 disables.
 # ---------------------------------------------------------------------------------------------
 SIDE_WGRAD = _os.environ.get("CSU_SIDE_WGRAD", "1") == "1"
+# CSU_SIDE_AUX=1: also the LePE weight gradient and the LayerNorm dgamma/dbeta reduction.  Off:
+# measured 1-2 % slower (969-979 vs 988 img/s, two A/B pairs) -- the extra graph branches delay
+# the critical-path kernels more than the overlap saves
+SIDE_AUX = _os.environ.get("CSU_SIDE_AUX", "0") == "1"
 _SIDE_STREAMS = {}
 _SIDE_PENDING = []
 _SIDE_JOIN_QUEUED = [False]

@@ -76,6 +76,11 @@ size_t csu_stripe_attn_bwd_workspace(const csu_stripe_args* a);
 int csu_stripe_attn_bwd(const csu_stripe_args* a, int dtype, const void* qkv, const void* out,
                         const void* dout, const float* lse, float* delta, void* dqkv,
                         void* workspace, size_t workspace_bytes, void* stream);
+/* LePE weight/bias gradient alone (csu_stripe_attn_bwd skips it when every lepe_dw / lepe_db of
+ * the args is NULL): lets it run on a second stream, concurrently with the dQ / dK / dV kernels.
+ * Workspace: csu_stripe_attn_bwd_workspace bytes. */
+int csu_stripe_lepe_wgrad(const csu_stripe_args* a, int dtype, const void* qkv, const void* dout,
+                          void* workspace, size_t workspace_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * LayerNorm over the last dim C of (rows, C) (nn.LayerNorm: norm1/norm2 cswin:315/347,
@@ -105,6 +110,11 @@ int csu_layernorm_bwd_ex(int rows, int C, int xdtype, const void* x, const float
  * NOT in the reference: public SimAM formula; parity unpinned vs the
  * reference.  stats fp32 [B][C][2] = (mean, 4*(var_unbiased + lambda)) saved for backward.
  * ------------------------------------------------------------------------------------- */
+/* dgamma / dbeta from the per-block partials that csu_layernorm_bwd_ex left in `workspace` when
+ * called with dgamma = dbeta = NULL (same rows / C): the parameter reduction can then run on a
+ * second stream, off the input-gradient chain. */
+int csu_layernorm_param_reduce(int rows, int C, const void* workspace, float* dgamma, float* dbeta, void* stream);
+
 size_t csu_simam_workspace(int B, int L, int C);
 int csu_simam_fwd(int B, int L, int C, float lambda, int dtype, const void* x, void* y, float* stats,
                   void* workspace, size_t ws_bytes, void* stream);
