@@ -25,7 +25,7 @@ __global__ __launch_bounds__(NT) void carafe_fwd(int B, int H, int W, int C, int
                                                  const T* __restrict__ enc, T* __restrict__ out,
                                                  float* __restrict__ wsave) {
     const int G = C / 8;
-    const long gid = (long)blockIdx.x * NT + threadIdx.x;
+    const long gid = xcd_tile(blockIdx.x, gridDim.x) * NT + threadIdx.x;   // neighbour blocks share one L2
     const int sW = s * W, sH = s * H;
     const long total = (long)B * sH * sW * G;
     if (gid >= total) return;
@@ -77,7 +77,7 @@ __global__ __launch_bounds__(NT) void carafe_bwd_enc(int B, int H, int W, int C,
                                                      const float* __restrict__ wsave, const T* __restrict__ dout,
                                                      T* __restrict__ denc) {
     const int G = C / 8;
-    const long gid = (long)blockIdx.x * NT + threadIdx.x;
+    const long gid = xcd_tile(blockIdx.x, gridDim.x) * NT + threadIdx.x;   // neighbour blocks share one L2
     const int sW = s * W, sH = s * H;
     const long total = (long)B * sH * sW * G;
     const bool live = gid < total;
@@ -127,7 +127,7 @@ template <typename T>
 __global__ __launch_bounds__(NT) void carafe_bwd_x(int B, int H, int W, int C, int s, const float* __restrict__ wsave,
                                                    const T* __restrict__ dout, T* __restrict__ dx) {
     const int G = C / 8;
-    const long gid = (long)blockIdx.x * NT + threadIdx.x;
+    const long gid = xcd_tile(blockIdx.x, gridDim.x) * NT + threadIdx.x;   // neighbour blocks share one L2
     const long total = (long)B * H * W * G;
     if (gid >= total) return;
     const int g = gid % G;
