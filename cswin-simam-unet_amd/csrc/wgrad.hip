@@ -326,6 +326,43 @@ extern "C" int csu_linear_wgrad(long M, int N, int K, int dtype, const void* dy,
     return csu_linear_wgrad_ex(M, N, K, dtype, dy, x, 0, dw_db, workspace, ws_bytes, stream);
 }
 
+// split-K partial slabs only (the reduction is left to csu_colsum_batch)
+static int wgrad_partials(const WPlan& p, long M, int N, int K, int dtype, const void* dy, const void* x, int x_gelu,
+                          float* part, hipStream_t st) {
+    const dim3 grid(p.nt, p.kt, p.chunks);
+    const dim3 grid1((unsigned)(p.nt * p.kt * p.chunks));
+    const bf16* dyb = (const bf16*)dy;
+    const bf16* xb = (const bf16*)x;
+    if (x_gelu && dtype != CSU_BF16) return fail(CSU_E_UNSUPPORTED, "linear_wgrad: GELU prologue is bf16-only");
+    if (dtype == CSU_BF16 && p.t == 128 && !x_gelu && wgrad5_cfg() >= 0) {
+        if (int e = wgrad5_launch(wgrad5_cfg(), M, N, K, p.rpc, p.chunks, dyb, xb, part, st)) return e;
+    } else if (dtype == CSU_BF16 && p.t == 128 && x_gelu) wgrad_bf16_tr<128, true><<<grid1, NT, 0, st>>>(M, N, K, p.rpc, dyb, xb, part);
+    else if (dtype == CSU_BF16 && p.t == 128) wgrad_bf16_tr<128, false><<<grid1, NT, 0, st>>>(M, N, K, p.rpc, dyb, xb, part);
+    else if (dtype == CSU_BF16 && x_gelu) wgrad_bf16_tr<64, true><<<grid1, NT, 0, st>>>(M, N, K, p.rpc, dyb, xb, part);
+    else if (dtype == CSU_BF16) wgrad_bf16_tr<64, false><<<grid1, NT, 0, st>>>(M, N, K, p.rpc, dyb, xb, part);
+    else if (dtype == CSU_F32)
+        wgrad_kernel<float><<<grid, NT, 0, st>>>(M, N, K, p.rpc, (const float*)dy, (const float*)x, part);
+    else
+        return fail(CSU_E_ARG, "linear_wgrad: bad dtype");
+    return check_launch("linear_wgrad");
+}
+
+extern "C" size_t csu_linear_wgrad_partial_bytes(long M, int N, int K, int dtype) {
+    const WPlan p = wplan(M, N, K, dtype == CSU_BF16);
+    return (size_t)p.chunks * ((size_t)N * K + N) * sizeof(float);
+}
+
+extern "C" int csu_linear_wgrad_partial(long M, int N, int K, int dtype, const void* dy, const void* x, int x_gelu,
+                                        float* slabs, size_t slab_bytes, int* chunks, void* stream) {
+    if (M < 1 || N < 1 || K < 1 || !dy || !x || !slabs || !chunks) return fail(CSU_E_ARG, "linear_wgrad_partial: bad args");
+    const int V = dtype == CSU_BF16 ? 8 : 4;
+    if (N % V || K % V) return fail(CSU_E_ARG, "linear_wgrad_partial: N and K must be multiples of 16 bytes");
+    if (slab_bytes < csu_linear_wgrad_partial_bytes(M, N, K, dtype)) return fail(CSU_E_WORKSPACE, "linear_wgrad_partial: slabs");
+    const WPlan p = wplan(M, N, K, dtype == CSU_BF16);
+    *chunks = p.chunks;
+    return wgrad_partials(p, M, N, K, dtype, dy, x, x_gelu, slabs, as_stream(stream));
+}
+
 extern "C" int csu_linear_wgrad_ex(long M, int N, int K, int dtype, const void* dy, const void* x, int x_gelu,
                                    float* dw_db, void* workspace, size_t ws_bytes, void* stream) {
     if (M < 1 || N < 1 || K < 1 || !dy || !x || !dw_db) return fail(CSU_E_ARG, "linear_wgrad: bad args");
@@ -338,21 +375,6 @@ extern "C" int csu_linear_wgrad_ex(long M, int N, int K, int dtype, const void* 
     const WPlan p = wplan(M, N, K, dtype == CSU_BF16);
     float* part = (float*)workspace;
     const long slab = (long)N * K + N;
-    const dim3 grid(p.nt, p.kt, p.chunks);
-    if (x_gelu && dtype != CSU_BF16) return fail(CSU_E_UNSUPPORTED, "linear_wgrad: GELU prologue is bf16-only");
-    const dim3 grid1((unsigned)(p.nt * p.kt * p.chunks));
-    const bf16* dyb = (const bf16*)dy;
-    const bf16* xb = (const bf16*)x;
-    if (dtype == CSU_BF16 && p.t == 128 && !x_gelu && wgrad5_cfg() >= 0) {
-        if (int e = wgrad5_launch(wgrad5_cfg(), M, N, K, p.rpc, p.chunks, dyb, xb, part, st)) return e;
-    } else if (dtype == CSU_BF16 && p.t == 128 && x_gelu) wgrad_bf16_tr<128, true><<<grid1, NT, 0, st>>>(M, N, K, p.rpc, dyb, xb, part);
-    else if (dtype == CSU_BF16 && p.t == 128) wgrad_bf16_tr<128, false><<<grid1, NT, 0, st>>>(M, N, K, p.rpc, dyb, xb, part);
-    else if (dtype == CSU_BF16 && x_gelu) wgrad_bf16_tr<64, true><<<grid1, NT, 0, st>>>(M, N, K, p.rpc, dyb, xb, part);
-    else if (dtype == CSU_BF16) wgrad_bf16_tr<64, false><<<grid1, NT, 0, st>>>(M, N, K, p.rpc, dyb, xb, part);
-    else if (dtype == CSU_F32)
-        wgrad_kernel<float><<<grid, NT, 0, st>>>(M, N, K, p.rpc, (const float*)dy, (const float*)x, part);
-    else
-        return fail(CSU_E_ARG, "linear_wgrad: bad dtype");
-    if (int e = check_launch("linear_wgrad")) return e;
+    if (int e = wgrad_partials(p, M, N, K, dtype, dy, x, x_gelu, part, st)) return e;
     return colsum_launch(p.chunks, slab, CSU_F32, part, dw_db, part + (size_t)p.chunks * slab, st);
 }

@@ -473,12 +473,59 @@ def _side_ok(t: torch.Tensor, *dtypes) -> bool:
     return not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1)
 
 
+# CSU_DEFER_WGRAD_REDUCE=1 (side-stream mode): every weight gradient leaves its split-K partial slabs
+# and one csu_colsum_batch launch per CSU_DEFER_BATCH weights (the rest at the end of backward)
+# reduces them, instead of a colsum launch (or two) per weight.  Off: measured 1.5-2 % slower on the
+# graphed step (979-986 vs 993-1001 img/s, batches of 4 and 8; all-at-the-end 2 % slower) --
+# the per-weight reductions overlap the backward better than a few large ones
+DEFER_REDUCE = _os.environ.get("CSU_DEFER_WGRAD_REDUCE", "0") == "1"
+_DEFERRED = []   # (slabs, out, rows, cols) pending on the side stream
+DEFER_BATCH = int(_os.environ.get("CSU_DEFER_BATCH", "8"))
+
+
 def join_side_streams():
-    """Make each launching stream wait for the side-stream weight gradients it forked."""
+    """Flush the deferred slab reductions on the side stream, then make each launching stream wait
+    for the side-stream weight gradients it forked."""
+    if _DEFERRED:
+        dev = _DEFERRED[0][0].device
+        side = _SIDE_STREAMS[dev]
+        with torch.cuda.stream(side):
+            _flush_deferred()
+            ev = torch.cuda.Event()
+            ev.record(side)
+        for main in {m for m, _ in _SIDE_PENDING}:
+            main.wait_event(ev)
     for main, ev in _SIDE_PENDING:
         main.wait_event(ev)
     _SIDE_PENDING.clear()
     _SIDE_JOIN_QUEUED[0] = False
+
+
+def _flush_deferred():
+    """One csu_colsum_batch launch (current stream = the side stream) over the pending slabs."""
+    dev = _DEFERRED[0][0].device
+    items = (_lib.ColsumItem * len(_DEFERRED))()
+    for i, (slabs, out, rows, cols) in enumerate(_DEFERRED):
+        items[i].in_, items[i].out, items[i].cols, items[i].rows = slabs.data_ptr(), out.data_ptr(), cols, rows
+    check(lib().csu_colsum_batch(items, len(_DEFERRED), stream_ptr(dev)), "csu_colsum_batch")
+    _DEFERRED.clear()
+
+
+def linear_wgrad_deferred(dy2: torch.Tensor, x2: torch.Tensor):
+    """(dW, db) views of an output the end-of-backward csu_colsum_batch fills (side stream only)."""
+    M, N = dy2.shape
+    K = x2.shape[1]
+    L = lib()
+    nb = L.csu_linear_wgrad_partial_bytes(M, N, K, dtype_code(dy2))
+    slabs = torch.empty(max(nb // 4, 4), dtype=torch.float32, device=dy2.device)
+    out = torch.empty(N * K + N, dtype=torch.float32, device=dy2.device)
+    ch = ctypes.c_int(0)
+    check(L.csu_linear_wgrad_partial(M, N, K, dtype_code(dy2), ptr(dy2), ptr(x2), 0, ptr(slabs), nb, ctypes.byref(ch),
+                                     stream_ptr(dy2.device)), "csu_linear_wgrad_partial")
+    _DEFERRED.append((slabs, out, ch.value, N * K + N))
+    if len(_DEFERRED) >= DEFER_BATCH:   # reduce in batches during backward (overlapped), not all at the end
+        _flush_deferred()
+    return out[:N * K].view(N, K), out[N * K:]
 
 
 def _side_run(fn, *inputs):
@@ -504,7 +551,7 @@ def _side_run(fn, *inputs):
 def wgrad_maybe_side(dy2: torch.Tensor, x2: torch.Tensor, wdt, bdt):
     """linear_wgrad on the side stream when allowed (fp32 master weights), else inline."""
     if _side_ok(dy2, wdt, bdt):
-        return _side_run(lambda: linear_wgrad(dy2, x2), dy2, x2)
+        return _side_run(lambda: (linear_wgrad_deferred if DEFER_REDUCE else linear_wgrad)(dy2, x2), dy2, x2)
     return linear_wgrad(dy2, x2)
 
 

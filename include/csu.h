@@ -177,6 +177,21 @@ int csu_colsum(long rows, long cols, int dtype, const void* in, float* out, void
  * dy (M, N), x (M, K) row-major, dtype in; dw_db fp32 [N*K + N] = dW (N, K) then db (N).
  * Split-K over M with MFMA tiles + a deterministic reduction.  N, K multiples of 16 bytes.
  * ------------------------------------------------------------------------------------- */
+/* Deferred form: the split-K partial slabs ([*chunks][N*K + N] fp32) of csu_linear_wgrad_ex go to
+ * `slabs` (csu_linear_wgrad_partial_bytes) and their reduction is left to one csu_colsum_batch
+ * call for many weights at the end of the backward pass. */
+size_t csu_linear_wgrad_partial_bytes(long M, int N, int K, int dtype);
+int csu_linear_wgrad_partial(long M, int N, int K, int dtype, const void* dy, const void* x, int x_gelu,
+                             float* slabs, size_t slab_bytes, int* chunks, void* stream);
+typedef struct {
+    const float* in;    /* [rows][cols] fp32 */
+    float* out;         /* [cols] fp32: out[c] = sum_r in[r][c], fixed order */
+    int64_t cols;       /* multiple of 4 */
+    int32_t rows;
+    int32_t pad_;
+} csu_colsum_item;
+int csu_colsum_batch(const csu_colsum_item* items, int count, void* stream);
+
 size_t csu_linear_wgrad_workspace(long M, int N, int K);
 int csu_linear_wgrad(long M, int N, int K, int dtype, const void* dy, const void* x, float* dw_db,
                      void* workspace, size_t ws_bytes, void* stream);

@@ -458,6 +458,41 @@ def test_mlp_fused_kernels_vs_fp64(C, M):
     assert_close(dx, hg.grad @ W1, torch.bfloat16)
 
 
+def test_colsum_batch_and_deferred_wgrad():
+    """csu_colsum_batch (the end-of-backward reduction of every deferred split-K weight gradient):
+    fixed-order column sums of many slab stacks in one launch == fp64 sums, bitwise reproducible;
+    linear_wgrad_deferred + the side-stream join == linear_wgrad."""
+    import ctypes
+    from csu import ops, _lib
+    from csu._lib import check, lib, stream_ptr
+    d = dev()
+    torch.manual_seed(0)
+    shapes = [(1, 4), (3, 8), (32, 65792), (7, 1028), (256, 4096)] * 8   # 40 items: two launches of <= 32
+    ins = [torch.randn(r, c, device=d) for r, c in shapes]
+    outs = [torch.empty(c, device=d) for _, c in shapes]
+    outs2 = [torch.empty(c, device=d) for _, c in shapes]
+    for o in (outs, outs2):
+        items = (_lib.ColsumItem * len(ins))()
+        for i, (t, z) in enumerate(zip(ins, o)):
+            items[i].in_, items[i].out, items[i].cols, items[i].rows = t.data_ptr(), z.data_ptr(), t.shape[1], t.shape[0]
+        check(lib().csu_colsum_batch(items, len(ins), stream_ptr(d)), "colsum_batch")
+    torch.cuda.synchronize()
+    for t, a, b in zip(ins, outs, outs2):
+        assert torch.equal(a, b)
+        torch.testing.assert_close(a.double(), t.double().sum(0), rtol=1e-5, atol=1e-5 * t.shape[0] ** 0.5)
+    dy = torch.randn(4096, 256, device=d).bfloat16()
+    x = torch.randn(4096, 768, device=d).bfloat16()
+    side = torch.cuda.Stream(d)
+    with torch.cuda.stream(side):
+        dw, db = ops.linear_wgrad_deferred(dy, x)
+    ops._SIDE_STREAMS[d] = side
+    ops.join_side_streams()
+    torch.cuda.synchronize()
+    rw, rb = ops.linear_wgrad(dy, x)
+    torch.testing.assert_close(dw, rw, rtol=1e-5, atol=1e-4)
+    torch.testing.assert_close(db, rb, rtol=1e-5, atol=1e-4)
+
+
 CONV_CASES = [  # (B, H, C, N, k, stride, pad)
     (2, 32, 3, 64, 7, 4, 2),      # patch embed (cswin:505)
     (2, 16, 64, 128, 3, 2, 1),    # Merge_Block (cswin:376)
