@@ -17,6 +17,8 @@
 //
 // Backward = two kernels (query-owner: dQ and delta; key-owner: dK, dV including the LePE
 // input gradient) plus a deterministic two-pass reduction for the LePE weight/bias gradient.
+#include <cstdlib>
+
 #include "common.hpp"
 
 #include <type_traits>
@@ -987,6 +989,12 @@ int wsplit(const csu_stripe_args& a) {
     const int N = a.br[0].H_sp * a.br[0].W_sp;
     const int nwin = (a.reso / a.br[0].H_sp) * (a.reso / a.br[0].W_sp);
     const long wgs = (long)a.B * nwin * a.heads * a.nbranch;
+    static int env = -1;   // CSU_ATTN_SPLIT=<n>: force the split of windows above 128 tokens (A/B)
+    if (env < 0) {
+        const char* e = getenv("CSU_ATTN_SPLIT");
+        env = e ? atoi(e) : 0;
+    }
+    if (env > 0 && N > 128) return env;
     return (N > 128 && wgs < 1024) ? 2 : 1;
 }
 
