@@ -31,10 +31,10 @@ __device__ __forceinline__ int moff(int row, int col) {
 // DMA of an R-row image of RB-byte rows from a row-major bf16 matrix (leading dimension ld
 // elements): wave instruction i of wave w fills image bytes [(w * NW + i) * 1024, +1024); lane l
 // the 16 B at + 16 l = row p / RB, slot (p % RB) / 16, whose source chunk is slot ^ key(row).
-template <int R, int RB>
+template <int R, int RB, int WAVES = 4>
 struct Dma {
-    static constexpr int NW = R * RB / 4096;   // instructions per wave
-    static_assert(NW >= 1 && R * RB % 4096 == 0, "image must be a multiple of 4 KB");
+    static constexpr int NW = R * RB / (1024 * WAVES);   // instructions per wave
+    static_assert(NW >= 1 && R * RB % (1024 * WAVES) == 0, "image must be a multiple of WAVES KB");
     unsigned v[NW];
     __device__ __forceinline__ void init(int ld, int wave, int lane) {
 #pragma unroll

@@ -30,12 +30,22 @@
 //    elementwise on registers.
 #include "lds_dma.hpp"
 
+#include <cstdlib>
 #include <type_traits>
 
 namespace csu {
 namespace {
 
 constexpr int MT = 256;   // threads (4 waves)
+
+#ifdef MLP_TIMING   // debug build only: per-workgroup timestamps of mlp_fwd (s_memrealtime, 100 MHz)
+__device__ unsigned long long mlp_ts[6][4096];
+#define MLP_STAMP(k, v) do { if (threadIdx.x == 0 && blockIdx.x < 4096) mlp_ts[k][blockIdx.x] = (v); } while (0)
+#define MLP_NOW() __builtin_amdgcn_s_memrealtime()
+#else
+#define MLP_STAMP(k, v) do {} while (0)
+#define MLP_NOW() 0ull
+#endif
 constexpr int BM = 64;    // tokens per workgroup
 constexpr int HC = 64;    // hidden features per chunk
 
@@ -185,6 +195,9 @@ __global__ __launch_bounds__(MT) void mlp_fwd_kernel(long M, const bf16* __restr
         bf16x8 wf[KS];
 #pragma unroll
         for (int s = 0; s < KS; ++s) wf[s] = frag(img, moff<2 * C>(hs + r, 16 * s + 8 * h));
+#ifdef MLP_PREF
+        __builtin_amdgcn_sched_barrier(0);   // every fragment read in flight before the first MFMA
+#endif
         f32x16 a = f32x16{};
 #pragma unroll
         for (int s = 0; s < KS; ++s) a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[s], xf[s], a, 0, 0, 0);
@@ -193,8 +206,14 @@ __global__ __launch_bounds__(MT) void mlp_fwd_kernel(long M, const bf16* __restr
     f32x16 acc[TF];
 #pragma unroll
     for (int i = 0; i < TF; ++i) acc[i] = f32x16{};
+    [[maybe_unused]] const unsigned long long t_entry = MLP_NOW();
+#ifdef MLP_TIMING
+    const unsigned long long t_clk0 = __builtin_amdgcn_s_memtime();
+#endif
+    [[maybe_unused]] unsigned long long t_wait = 0;
     vmwait<0>();
     lds_sync();
+    MLP_STAMP(1, MLP_NOW() - t_entry);
     f32x16 ha = gemm1(w1r), hb;
 
     // par = j & 1 as a compile-time constant: every LDS address is a per-lane base + immediate
@@ -202,9 +221,11 @@ __global__ __launch_bounds__(MT) void mlp_fwd_kernel(long M, const bf16* __restr
     auto step = [&](auto more, auto par, int j, const f32x16& cur, f32x16& nxt) {
         constexpr int P = decltype(par)::value;
 #ifndef MLP_EXP_NOBAR
+        const unsigned long long tw = MLP_NOW();
         // W1(j+1), W2(j): issued one step ago; after them only the previous step's 4 h stores
         if constexpr (STORE_H) vmwait<4>(); else vmwait<0>();
         lds_sync();                     // every wave is past GEMM1(j) and GEMM2(j-1)
+        t_wait += MLP_NOW() - tw;
 #endif
 #ifndef MLP_EXP_NODMA
         if (j + 2 < NCH) dma<D1::NW>(rs_w1, d1.v, (unsigned)(j + 2) * HC * C * 2, w1r + P * IMG, wave);
@@ -234,10 +255,20 @@ __global__ __launch_bounds__(MT) void mlp_fwd_kernel(long M, const bf16* __restr
         const bf16* w2c = w2r + P * IMG;
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) {
+#ifdef MLP_PREF
+            bf16x8 wf2[TF];
+#pragma unroll
+            for (int ft = 0; ft < TF; ++ft) wf2[ft] = pfrag<2 * HC>(w2c, 32 * ft + r, hs + 16 * s2, h);
+            __builtin_amdgcn_sched_barrier(0);
+            const bf16x8 gb = pack_b(gv, s2);
+#pragma unroll
+            for (int ft = 0; ft < TF; ++ft) acc[ft] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf2[ft], gb, acc[ft], 0, 0, 0);
+#else
             const bf16x8 gb = pack_b(gv, s2);
 #pragma unroll
             for (int ft = 0; ft < TF; ++ft)
                 acc[ft] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pfrag<2 * HC>(w2c, 32 * ft + r, hs + 16 * s2, h), gb, acc[ft], 0, 0, 0);
+#endif
         }
     };
     int j = 0;
@@ -247,6 +278,8 @@ __global__ __launch_bounds__(MT) void mlp_fwd_kernel(long M, const bf16* __restr
     }
     step(bconst<true>{}, iconst<0>{}, j, ha, hb);
     step(bconst<false>{}, iconst<1>{}, j + 1, hb, ha);
+    MLP_STAMP(2, MLP_NOW() - t_entry);
+    MLP_STAMP(3, t_wait);
 
     lds_sync();                         // ring free: partial-sum exchange
     float* xch = reinterpret_cast<float*>(ring);
@@ -259,6 +292,136 @@ __global__ __launch_bounds__(MT) void mlp_fwd_kernel(long M, const bf16* __restr
         exchange_half<C, 1>(acc, xch, wave, lane);
         fwd_epilogue<C, 1>(acc, rs_res, rs_out, b2, tok, ok, h);
     }
+    MLP_STAMP(0, t_entry);
+    MLP_STAMP(4, MLP_NOW() - t_entry);
+#ifdef MLP_TIMING
+    MLP_STAMP(5, __builtin_amdgcn_s_memtime() - t_clk0);   // shader-clock cycles over the same span
+#endif
+}
+
+// Forward, 8 waves (2 per SIMD) for C = 256, where the 4-wave kernel gets one wave per SIMD and
+// runs VALU (GELU) and MFMA back to back.  Wave w: token tile t = w & 1, hidden half u = (w >> 1) & 1
+// of each 64-feature chunk, input-channel half v = w >> 2 of GEMM1 (x fragments: C/2 channels,
+// half the registers).  Per chunk: GEMM1 partial (K = C/2) -> the two v waves swap halves of their
+// partial H through LDS and each finalises 8 of the 16 values (bias, GELU) -> g to a [64][64] LDS
+// image -> GEMM2 by wave (t, f = w >> 1): output features 64 f .. + 63, K = 64 hidden.  Every wave
+// ends with full sums of its 64 features (no final exchange).  Three barriers per chunk.
+template <int C, bool STORE_H>
+__global__ __launch_bounds__(2 * MT) void mlp_fwd8_kernel(long M, const bf16* __restrict__ X, const bf16* __restrict__ W1,
+                                                          const float* __restrict__ b1, const bf16* __restrict__ W2,
+                                                          const float* __restrict__ b2, const float* __restrict__ res,
+                                                          float* __restrict__ out, bf16* __restrict__ hout) {
+    constexpr int NCH = 4 * C / HC;
+    constexpr int KH = C / 2;           // GEMM1 input channels per wave
+    constexpr int KS = KH / 16;
+    constexpr int IMG = HC * C;
+    using D1 = Dma<HC, 2 * C, 8>;
+    using D2 = Dma<C, 2 * HC, 8>;
+    __shared__ __attribute__((aligned(1024))) bf16 ring[4 * IMG];   // W1 stages 0, 1 | W2 stages 0, 1
+    __shared__ __attribute__((aligned(1024))) bf16 gs[BM * HC];     // g of the chunk [token][hidden]
+    __shared__ __attribute__((aligned(16))) float xch[8][8][64];   // partial-H halves
+    __shared__ __attribute__((aligned(16))) float b1s[4 * C];
+    bf16* const w1r = ring;
+    bf16* const w2r = ring + 2 * IMG;
+
+    const long m0 = (long)blockIdx.x * BM;
+    const long rows = M - m0;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int r = lane & 31, h = lane >> 5;
+    const int t = wave & 1, u = (wave >> 1) & 1, v = wave >> 2, f = wave >> 1;
+    const int tok = 32 * t + r;
+    const bool ok = tok < rows;
+    const int hs = 32 * u;
+    for (int i = threadIdx.x; i < 4 * C; i += 2 * MT) b1s[i] = b1[i];
+    bf16x8 xf[KS];
+    {
+        const auto rs = buf_rsrc(X + m0 * C, rows * C * 2);
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+            const u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(rs, ok ? (unsigned)(tok * C + v * KH + 16 * s + 8 * h) * 2 : kOOB, 0, 0);
+            __builtin_memcpy(&xf[s], &q, 16);
+        }
+    }
+    D1 d1;
+    D2 d2;
+    d1.init(C, wave, lane);
+    d2.init(4 * C, wave, lane);
+    const i32x4 rs_w1 = rsrc4(W1, 4L * C * C * 2);
+    const i32x4 rs_w2 = rsrc4(W2, 4L * C * C * 2);
+    const auto rs_h = buf_rsrc(STORE_H ? hout + m0 * 4 * C : nullptr, STORE_H ? rows * 4 * C * 2 : 0);
+    asm volatile("" ::: "memory");
+    dma<D1::NW>(rs_w1, d1.v, 0, w1r, wave);
+    dma<D2::NW>(rs_w2, d2.v, 0, w2r, wave);
+
+    f32x16 acc[2] = {f32x16{}, f32x16{}};
+    for (int j = 0; j < NCH; ++j) {
+        const int P = j & 1;
+        vmwait<STORE_H ? 2 : 0>();      // chunk j landed (after it: only chunk j-1's 2 h stores)
+        lds_sync();                     // all waves past chunk j-1: its stages and gs are free
+        if (j + 1 < NCH) {
+            dma<D1::NW>(rs_w1, d1.v, (unsigned)(j + 1) * HC * C * 2, w1r + (1 - P) * IMG, wave);
+            dma<D2::NW>(rs_w2, d2.v, (unsigned)(j + 1) * HC * 2, w2r + (1 - P) * IMG, wave);
+        }
+        const bf16* w1c = w1r + P * IMG;
+        const bf16* w2c = w2r + P * IMG;
+        bf16x8 wf[KS];
+#pragma unroll
+        for (int s = 0; s < KS; ++s) wf[s] = frag(w1c, moff<2 * C>(hs + r, v * KH + 16 * s + 8 * h));
+        __builtin_amdgcn_sched_barrier(0);
+        f32x16 hp = f32x16{};
+#pragma unroll
+        for (int s = 0; s < KS; ++s) hp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[s], xf[s], hp, 0, 0, 0);
+        // swap halves: this wave finalises registers 8v .. 8v+7, the partner (w ^ 4) the others
+#pragma unroll
+        for (int e = 0; e < 8; ++e) xch[wave][e][lane] = hp[8 * (1 - v) + e];
+        lds_sync();
+        float hv[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) hv[e] = hp[8 * v + e] + xch[wave ^ 4][e][lane] + b1s[j * HC + hs + crow(8 * v + e, h)];
+        if constexpr (STORE_H) {
+            const unsigned base = ok ? (unsigned)(tok * 4 * C + j * HC + hs + 16 * v + 4 * h) * 2 : kOOB;
+            buf_st4bf(rs_h, base, hv);
+            buf_st4bf(rs_h, base == kOOB ? kOOB : base + 16, hv + 4);
+        }
+#pragma unroll
+        for (int g2 = 0; g2 < 2; ++g2) {   // register groups 2v + g2: hidden hs + 8 (2v + g2) + 4h .. + 3
+            float gv[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) gv[e] = gelu_fast(hv[4 * g2 + e]);
+            const bf16x4 b = {(bf16)gv[0], (bf16)gv[1], (bf16)gv[2], (bf16)gv[3]};
+            *reinterpret_cast<bf16x4*>(gs + moff<2 * HC>(tok, hs + 8 * (2 * v + g2) + 4 * h)) = b;
+        }
+        lds_sync();
+        bf16x8 gf[HC / 16], af[2][HC / 16];
+#pragma unroll
+        for (int s = 0; s < HC / 16; ++s) {
+            gf[s] = frag(gs, moff<2 * HC>(tok, 16 * s + 8 * h));
+#pragma unroll
+            for (int ft = 0; ft < 2; ++ft) af[ft][s] = frag(w2c, moff<2 * HC>(64 * f + 32 * ft + r, 16 * s + 8 * h));
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int s = 0; s < HC / 16; ++s)
+#pragma unroll
+            for (int ft = 0; ft < 2; ++ft) acc[ft] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[ft][s], gf[s], acc[ft], 0, 0, 0);
+    }
+    // y[token][feature] = acc + b2 + res; lane: token tok, features 64 f + 32 ft + 8 g + 4 h .. + 3
+    const auto rs_res = buf_rsrc(res + m0 * C, rows * C * 4);
+    const auto rs_out = buf_rsrc(out + m0 * C, rows * C * 4);
+#pragma unroll
+    for (int ft = 0; ft < 2; ++ft)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int fe = 64 * f + 32 * ft + 8 * g + 4 * h;
+            const unsigned off = ok ? (unsigned)(tok * C + fe) * 4 : kOOB;
+            float rv[4], bv[4], o[4];
+            buf_ld4(rs_res, off, rv);
+            load4(b2 + fe, bv);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) o[e] = acc[ft][4 * g + e] + bv[e] + rv[e];
+            buf_st4(rs_out, off, o);
+        }
 }
 
 // Backward.  Rings: W1 chunks in 3 stages (GEMM1 of chunk j+1 and GEMM4 of chunk j overlap, plus
@@ -404,10 +567,32 @@ __global__ __launch_bounds__(MT) void mlp_bwd_kernel(long M, const bf16* __restr
 }
 
 
+// CSU_MLP8=1 selects the 8-wave forward at C = 256.  Opt-in: parity-green but not faster
+// (43.3 vs 40-45 us per launch, 991 vs 997-1004 img/s on the graphed step, A/B r01ae)
+static bool use_fwd8() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("CSU_MLP8");
+        v = e ? atoi(e) : 0;
+    }
+    return v != 0;
+}
+
 template <int C>
 int fwd_launch(long M, const void* x, const void* w1, const float* b1, const void* w2, const float* b2, const float* res,
                float* out, void* h, hipStream_t st) {
     const dim3 grid((unsigned)((M + BM - 1) / BM));
+    if constexpr (C == 256) {
+        if (use_fwd8()) {
+            if (h)
+                mlp_fwd8_kernel<C, true><<<grid, 2 * MT, 0, st>>>(M, (const bf16*)x, (const bf16*)w1, b1, (const bf16*)w2, b2,
+                                                                  res, out, (bf16*)h);
+            else
+                mlp_fwd8_kernel<C, false><<<grid, 2 * MT, 0, st>>>(M, (const bf16*)x, (const bf16*)w1, b1, (const bf16*)w2, b2,
+                                                                   res, out, nullptr);
+            return check_launch("mlp_fwd8");
+        }
+    }
     if (h)
         mlp_fwd_kernel<C, true><<<grid, MT, 0, st>>>(M, (const bf16*)x, (const bf16*)w1, b1, (const bf16*)w2, b2, res, out,
                                                      (bf16*)h);
@@ -466,3 +651,9 @@ extern "C" int csu_mlp_bwd(long M, int C, const void* x, const void* dy, const v
         default: return fail(CSU_E_ARG, "mlp_bwd: C must be 64, 128 or 256");
     }
 }
+
+#ifdef MLP_TIMING
+extern "C" int csu_debug_mlp_ts(unsigned long long* host, int n) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(csu::mlp_ts), (size_t)n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : 1;
+}
+#endif
