@@ -195,7 +195,7 @@ __global__ __launch_bounds__(MT) void mlp_fwd_kernel(long M, const bf16* __restr
         bf16x8 wf[KS];
 #pragma unroll
         for (int s = 0; s < KS; ++s) wf[s] = frag(img, moff<2 * C>(hs + r, 16 * s + 8 * h));
-#ifdef MLP_PREF
+#ifndef MLP_NO_PREF
         __builtin_amdgcn_sched_barrier(0);   // every fragment read in flight before the first MFMA
 #endif
         f32x16 a = f32x16{};
@@ -255,7 +255,7 @@ __global__ __launch_bounds__(MT) void mlp_fwd_kernel(long M, const bf16* __restr
         const bf16* w2c = w2r + P * IMG;
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) {
-#ifdef MLP_PREF
+#ifndef MLP_NO_PREF
             bf16x8 wf2[TF];
 #pragma unroll
             for (int ft = 0; ft < TF; ++ft) wf2[ft] = pfrag<2 * HC>(w2c, 32 * ft + r, hs + 16 * s2, h);
