@@ -480,11 +480,31 @@ __global__ __launch_bounds__(MT) void mlp_bwd_kernel(long M, const bf16* __restr
     auto gemm13 = [&](const bf16* w1c, const bf16* w2c, f32x16& ha, f32x16& ga) {
         ha = f32x16{};
         ga = f32x16{};
+#ifndef MLP_NO_PREF
+        // fragments of KS/2 k-steps in flight before their MFMAs (two halves: register budget)
+        constexpr int KP = KS / 2;
+#pragma unroll
+        for (int s0 = 0; s0 < KS; s0 += KP) {
+            bf16x8 fa[KP], fb[KP];
+#pragma unroll
+            for (int s = 0; s < KP; ++s) {
+                fa[s] = frag(w1c, moff<2 * C>(hs + r, 16 * (s0 + s) + 8 * h));
+                fb[s] = trfrag<2 * HC>(w2c, hs, s0 + s, lane);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int s = 0; s < KP; ++s) {
+                ha = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[s], xf[s0 + s], ha, 0, 0, 0);
+                ga = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[s], dyf[s0 + s], ga, 0, 0, 0);
+            }
+        }
+#else
 #pragma unroll
         for (int s = 0; s < KS; ++s) {
             ha = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag(w1c, moff<2 * C>(hs + r, 16 * s + 8 * h)), xf[s], ha, 0, 0, 0);
             ga = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag<2 * HC>(w2c, hs, s, lane), dyf[s], ga, 0, 0, 0);
         }
+#endif
     };
     f32x16 acc[TF];
 #pragma unroll
@@ -508,9 +528,18 @@ __global__ __launch_bounds__(MT) void mlp_bwd_kernel(long M, const bf16* __restr
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) {
             const bf16x8 db = pack_b(dv, s2);
+#ifndef MLP_NO_PREF
+            bf16x8 fw[TF];
+#pragma unroll
+            for (int ft = 0; ft < TF; ++ft) fw[ft] = ptrfrag<2 * C>(w1c, 32 * ft, hs + 16 * s2, lane);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int ft = 0; ft < TF; ++ft) acc[ft] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fw[ft], db, acc[ft], 0, 0, 0);
+#else
 #pragma unroll
             for (int ft = 0; ft < TF; ++ft)
                 acc[ft] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ptrfrag<2 * C>(w1c, 32 * ft, hs + 16 * s2, lane), db, acc[ft], 0, 0, 0);
+#endif
         }
     };
     f32x16 ha, ga;
