@@ -2,7 +2,8 @@
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
 N > 1 is launched by the driver with torch.distributed.run (one process per GPU, RCCL).
-One step = forward + BCE + backward (+ DDP gradient all-reduce) + fused AdamW on a batch of
+One step = forward + BCE + backward (+ bucketed RCCL gradient all-reduce, captured in the same HIP
+graph, csu.dist.GradAllReduce) + fused AdamW on a batch of
 synthetic 512x512 images already resident in HBM.  Prints ONE JSON line (rank 0).
 
 roofline: the stripe-attention forward kernel (csu_stripe_attn_fwd -> stripe_fwd_w), timed live
@@ -49,7 +50,10 @@ def parse():
     ap.add_argument("--cpu-baseline", default="auto", choices=["auto", "on", "off"])
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--graph", default="auto", choices=["auto", "on", "off"],
-                    help="capture the whole step in a HIP graph (single process)")
+                    help="capture the whole step in a HIP graph (N > 1: with the bucketed all-reduce; off: eager DDP)")
+    ap.add_argument("--bucket-mb", type=float, default=32.0, help="gradient all-reduce bucket size (N > 1)")
+    ap.add_argument("--dp-force", action="store_true",
+                    help="run the data-parallel path (RCCL process group + captured all-reduce) even at N = 1")
     return ap.parse_args()
 
 
@@ -102,8 +106,13 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    dp = world > 1 or args.dp_force
+    if dp:
         torch.cuda.set_device(local)
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29517")
+        os.environ.setdefault("RANK", str(rank))
+        os.environ.setdefault("WORLD_SIZE", str(world))
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     device = torch.device("cuda", local)
     torch.backends.cudnn.benchmark = True
@@ -118,10 +127,15 @@ def main():
     torch.manual_seed(0)
     model = CSWinTransformer(img_size=args.img, depth=depth, split_size=split, simam=args.simam).to(device)
     nparams = sum(p.numel() for p in model.parameters())
-    if world > 1:
+    use_graph = args.graph in ("on", "auto")
+    reducer = None
+    if dp and use_graph:
+        # graph-captured bucketed all-reduce (DDP cannot be captured; eager steps cost ~3x)
+        from csu.dist import GradAllReduce
+        reducer = GradAllReduce(model.parameters(), bucket_mb=args.bucket_mb)
+    elif dp:
         model = torch.nn.parallel.DistributedDataParallel(model, device_ids=[local], gradient_as_bucket_view=True,
                                                           static_graph=True, bucket_cap_mb=64)
-    use_graph = args.graph == "on" or (args.graph == "auto" and world == 1)
     opt = make_optimizer(model, capturable=use_graph)
     batches = synthetic_batches(2, args.batch, args.img, device, seed=1234 + rank)
     amp = torch.bfloat16 if dtype == torch.bfloat16 else None
@@ -133,6 +147,8 @@ def main():
             y = model(x)
         loss = bce_loss(y, t)
         loss.backward()
+        if reducer is not None:
+            reducer.finish()
         opt.step()
         return loss
 
@@ -141,7 +157,8 @@ def main():
         # capture first (its eager warm-up runs on a side stream); eager steps on the default
         # stream before the capture crash hipGraphInstantiate at this size (ROCm 7.2 / torch 2.10)
         from csu.train import GraphedTrainStep
-        gstep = GraphedTrainStep(model, opt, bce_loss, batches[0][0], batches[0][1], amp, warmup=args.warmup)
+        gstep = GraphedTrainStep(model, opt, bce_loss, batches[0][0], batches[0][1], amp, warmup=args.warmup,
+                                 reducer=reducer)
 
         def step(i):
             x, t = batches[i % len(batches)]
@@ -161,18 +178,18 @@ def main():
     for i in range(2):
         step(i)
     torch.cuda.synchronize()
-    if world > 1:
+    if dp:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
         loss = step(i)
     torch.cuda.synchronize()
-    if world > 1:
+    if dp:
         dist.barrier()
     el = time.perf_counter() - t0
     t = torch.tensor([el], dtype=torch.float64, device=device)
-    if world > 1:
+    if dp:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     el = float(t.item())
     images = args.batch * world * args.steps
@@ -205,9 +222,10 @@ def main():
                           "model": "CSWinTransformer", "params": nparams, "global_batch": args.batch * world,
                           "per_gpu_batch": args.batch, "img": args.img, "parallelism": f"dp{world}"},
                "roofline": roof, "cpu_baseline": cpu, "final_loss": round(float(loss.item()), 5),
-               "hip_graph": use_graph}
+               "hip_graph": use_graph,
+               "grad_allreduce": None if not dp else ("graph-captured buckets" if reducer is not None else "DDP eager")}
         print(json.dumps(rec), flush=True)
-    if world > 1:
+    if dp:
         dist.destroy_process_group()
 
 

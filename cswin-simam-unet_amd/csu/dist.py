@@ -3,9 +3,13 @@
 The reference is single-device (cswin:865); SURVEY §8e: CSWin-UNet has no BatchNorm, so averaging
 per-rank gradients of equal per-rank batches equals the global-batch gradient.  Buckets are sized
 for xGMI point-to-point rings: 94 MB of fp32 gradients go in 64 MB buckets (2 all-reduces per step,
-the first overlapped with the rest of backward)."""
+the first overlapped with the rest of backward).
+
+``GradAllReduce`` is the graph-capturable replacement bench.py uses at N > 1: the same bucketed
+averaging, recorded into the train step's HIP graph (DDP is the eager fallback)."""
 from __future__ import annotations
 
+import contextlib
 import os
 
 import torch
@@ -49,3 +53,109 @@ def make_loader(dataset, batch_size: int, shuffle: bool, seed: int = 42, num_wor
     return torch.utils.data.DataLoader(dataset, batch_size=batch_size, shuffle=shuffle, sampler=sampler,
                                        num_workers=num_workers, pin_memory=torch.cuda.is_available(),
                                        drop_last=drop_last)
+
+
+class GradAllReduce:
+    """Bucketed gradient averaging that can be captured into the HIP graph of a whole train step.
+
+    ``DistributedDataParallel`` cannot sit inside ``GraphedTrainStep``'s capture, and an eager
+    step costs ~3x a graph replay at 512x512 (51 vs 16 ms), so multi-GPU training would lose most
+    of its per-GPU speed to host launches.  This reducer does DDP's job for a fixed parameter set:
+    post-accumulate-grad hooks count the gradients of each bucket as backward produces them
+    (buckets in reverse registration order = backward order); a complete bucket is packed into its
+    flat fp32 buffer (one ``cat``) and all-reduced on a side stream while backward continues.
+    ``finish()`` (call after ``backward()``, before ``optimizer.step()``) launches any bucket still
+    pending, joins the side stream and re-points every ``p.grad`` at its averaged slice of the flat
+    buffers, which the optimizer then reads in place.  Every call is a stream operation, so the same
+    sequence is recorded into a graph on capture and replayed with one launch per step (RCCL
+    collectives are capturable once the communicator exists: run one eager step first).
+
+    Averaging: ``ReduceOp.AVG`` on nccl (= RCCL), SUM then a scale on gloo.  Bucket size 32 MB:
+    94 MB of CSWin-UNet gradients -> 3 all-reduces, the first two overlapped with backward, each
+    large enough to run the xGMI rings at bandwidth."""
+
+    def __init__(self, params, bucket_mb: float = 32.0, group=None):
+        self.params = [p for p in params if p.requires_grad]
+        if not self.params:
+            raise ValueError("GradAllReduce: no trainable parameters")
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.avg = dist.get_backend(group) == "nccl"
+        dev = self.params[0].device
+        cap = int(bucket_mb * (1 << 20)) // 4
+        self.buckets, cur, size = [], [], 0
+        for p in reversed(self.params):
+            if p.dtype != torch.float32 or not p.is_contiguous():
+                raise ValueError("GradAllReduce: contiguous fp32 parameters only")
+            cur.append(p)
+            size += p.numel()
+            if size >= cap:
+                self.buckets.append(cur)
+                cur, size = [], 0
+        if cur:
+            self.buckets.append(cur)
+        self.flat = [torch.zeros(sum(p.numel() for p in b), dtype=torch.float32, device=dev) for b in self.buckets]
+        self.views = []
+        for b, f in zip(self.buckets, self.flat):
+            off, vs = 0, []
+            for p in b:
+                vs.append(f[off:off + p.numel()].view_as(p))
+                off += p.numel()
+            self.views.append(vs)
+        self.where = {id(p): bi for bi, b in enumerate(self.buckets) for p in b}
+        self.side = torch.cuda.Stream(dev) if dev.type == "cuda" else None
+        self._reset()
+        self.handles = [p.register_post_accumulate_grad_hook(self._hook) for p in self.params]
+
+    def _reset(self):
+        self.pending = [len(b) for b in self.buckets]
+        self.launched = [False] * len(self.buckets)
+        self.held = []     # gradients read on the side stream: alive until finish() joined it
+
+    def _hook(self, p):
+        bi = self.where[id(p)]
+        self.pending[bi] -= 1
+        if self.pending[bi] == 0:
+            self._launch(bi)
+
+    def _launch(self, bi):
+        grads = []
+        for p in self.buckets[bi]:
+            if p.grad is None:      # parameter without a gradient this step: contributes zeros
+                p.grad = torch.zeros_like(p)
+            grads.append(p.grad.reshape(-1))
+        flat = self.flat[bi]
+        alias = [g.data_ptr() == v.data_ptr() for g, v in zip(grads, self.views[bi])]
+        if any(alias) and not all(alias):   # zero_grad(set_to_none=False) after a partial step
+            grads = [g.clone() if a else g for g, a in zip(grads, alias)]
+        self.held.append(grads)
+        if self.side is not None:
+            self.side.wait_stream(torch.cuda.current_stream(flat.device))
+            ctx = torch.cuda.stream(self.side)
+        else:
+            ctx = contextlib.nullcontext()
+        with ctx:
+            if not all(alias):              # already in place: grads accumulated into the views
+                torch.cat(grads, out=flat)
+            if self.avg:
+                dist.all_reduce(flat, op=dist.ReduceOp.AVG, group=self.group)
+            else:
+                dist.all_reduce(flat, group=self.group)
+                flat.mul_(1.0 / self.world)
+        self.launched[bi] = True
+
+    def finish(self):
+        for bi in range(len(self.buckets)):
+            if not self.launched[bi]:
+                self._launch(bi)
+        if self.side is not None:
+            torch.cuda.current_stream(self.flat[0].device).wait_stream(self.side)
+        for b, vs in zip(self.buckets, self.views):
+            for p, v in zip(b, vs):
+                p.grad = v
+        self._reset()
+
+    def remove(self):
+        for h in self.handles:
+            h.remove()
+

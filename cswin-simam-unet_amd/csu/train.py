@@ -89,13 +89,16 @@ def evaluate_model(model, data_loader, criterion, device):
     return _epoch_means(stats)
 
 
-def train_step(model, images, masks, criterion, optimizer):
+def train_step(model, images, masks, criterion, optimizer, reducer=None):
     """One reference step (cswin:779-794): zero_grad, forward, loss, backward, optimizer step.
+    ``reducer``: a ``csu.dist.GradAllReduce`` averaging the gradients across ranks (instead of DDP).
     Returns the device tensor of per-step sums (loss, sum(p*t), sum(p), sum(t)) -- no host sync."""
     optimizer.zero_grad(set_to_none=True)
     outputs = model(images)
     loss = criterion(outputs, masks)
     loss.backward()
+    if reducer is not None:
+        reducer.finish()
     optimizer.step()
     with torch.no_grad():
         return _step_stats(loss, outputs, masks)
@@ -150,10 +153,15 @@ class GraphedTrainStep:
     HIP graph and replayed: removes every host launch (~2k kernels per 512x512 step).
 
     Inputs are copied into static device buffers before each replay; the optimizer must be
-    built with ``capturable=True``.  Single-process only (the DDP all-reduce is not captured)."""
+    built with ``capturable=True``.  Data parallel: pass a ``csu.dist.GradAllReduce`` over the
+    (unwrapped) model's parameters as ``reducer``; its bucketed RCCL all-reduces, overlapped with
+    backward on a side stream, are captured into the same graph (``DistributedDataParallel`` is
+    not capturable)."""
 
-    def __init__(self, model, optimizer, criterion, example_x, example_t, autocast_dtype=None, warmup=3):
+    def __init__(self, model, optimizer, criterion, example_x, example_t, autocast_dtype=None, warmup=3,
+                 reducer=None):
         self.model, self.opt, self.crit = model, optimizer, criterion
+        self.reducer = reducer
         self.x = example_x.clone()
         self.t = example_t.clone()
         self.dtype = autocast_dtype
@@ -175,6 +183,8 @@ class GraphedTrainStep:
             out = self.model(self.x)
         loss = self.crit(out, self.t)
         loss.backward()
+        if self.reducer is not None:
+            self.reducer.finish()
         self.opt.step()
         return loss.detach(), out.detach()
 

@@ -31,17 +31,17 @@ def _setup(seed=0):
     return model, xs, ts
 
 
-def _train(model, batches, steps=2):
+def _train(model, batches, steps=2, reducer=None):
     from csu.train import bce_loss, train_step
     opt = torch.optim.AdamW(model.parameters(), lr=1e-3, weight_decay=1e-4)
     stats = []
     for i in range(steps):
         x, t = batches[i % len(batches)]
-        stats.append(train_step(model, x, t, bce_loss, opt))
+        stats.append(train_step(model, x, t, bce_loss, opt, reducer=reducer))
     return stats
 
 
-def _worker(rank, world, port, out_path):
+def _worker(rank, world, port, out_path, mode="ddp"):
     sys.path[:0] = [REPO, os.path.join(REPO, "cswin-simam-unet_amd")]
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
@@ -50,18 +50,24 @@ def _worker(rank, world, port, out_path):
     from csu.train import _epoch_means
     r, w, device = init_distributed("gloo")
     model, xs, ts = _setup()
-    ddp = wrap_ddp(model, device)
     shard = slice(2 * r, 2 * r + 2)
-    stats = _train(ddp, [(xs[shard], ts[shard])])
+    if mode == "ddp":
+        stats = _train(wrap_ddp(model, device), [(xs[shard], ts[shard])])
+    else:   # the graph-capturable bucketed reducer bench.py uses at N > 1, here eager on gloo
+        from csu.dist import GradAllReduce
+        red = GradAllReduce(model.parameters(), bucket_mb=0.05)   # tiny buckets: several per step
+        assert len(red.buckets) > 2
+        stats = _train(model, [(xs[shard], ts[shard])], reducer=red)
     means = _epoch_means(stats)
     if r == 0:
         torch.save({"params": [p.detach().clone() for p in model.parameters()], "means": means}, out_path)
     torch.distributed.destroy_process_group()
 
 
-def test_ddp_two_ranks_equals_global_batch(tmp_path):
+@pytest.mark.parametrize("mode", ["ddp", "reducer"])
+def test_ddp_two_ranks_equals_global_batch(tmp_path, mode):
     out = str(tmp_path / "ddp.pt")
-    mp.spawn(_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    mp.spawn(_worker, args=(2, _free_port(), out, mode), nprocs=2, join=True)
     got = torch.load(out, weights_only=True)
     from csu.train import _epoch_means
     torch.set_num_threads(4)
