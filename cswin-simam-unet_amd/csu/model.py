@@ -359,6 +359,20 @@ class CSWinTransformer(nn.Module):
     def _skip(self, t):
         return self.simam(t) if self.simam is not None else t
 
+    def _share_skip(self, x):
+        """(merge input, decoder skip) for an encoder stage output.  bf16 autocast on the device
+        without SimAM: one shared bf16 copy feeds both the Merge_Block conv and the split-weight
+        concat_linear (ops.shared_cast / ops.concat_linear); otherwise x twice (reference form)."""
+        if self.simam is None and x.is_cuda and torch.is_autocast_enabled("cuda") \
+                and torch.get_autocast_dtype("cuda") == torch.bfloat16 and x.dtype == torch.float32:
+            return ops.shared_cast(x, torch.bfloat16)
+        return x, None
+
+    def _concat(self, lin, skip_fp, skip_b, up):
+        if skip_b is not None and up.dtype == torch.bfloat16:
+            return ops.concat_linear(skip_b, up, lin.weight, lin.bias)
+        return self._fuse(lin, torch.cat([self._skip(skip_fp), up], -1))
+
     def forward_features(self, x):
         conv, _, ln = self.stage1_conv_embed
         B = x.shape[0]
@@ -370,14 +384,17 @@ class CSWinTransformer(nn.Module):
         for blk in self.stage1:
             x = blk(x)
         self.x1 = x
+        x, self._x1s = self._share_skip(x)
         x = self.merge1(x)
         for blk in self.stage2:
             x = blk(x)
         self.x2 = x
+        x, self._x2s = self._share_skip(x)
         x = self.merge2(x)
         for blk in self.stage3:
             x = blk(x)
         self.x3 = x
+        x, self._x3s = self._share_skip(x)
         x = self.merge3(x)
         for blk in self.stage4:
             x = blk(x)
@@ -386,13 +403,13 @@ class CSWinTransformer(nn.Module):
     def forward_up_features(self, x):
         for blk in self.stage_up4:
             x = blk(x)
-        x = self._fuse(self.concat_linear4, torch.cat([self._skip(self.x3), self.upsample4(x)], -1))
+        x = self._concat(self.concat_linear4, self.x3, self._x3s, self.upsample4(x))
         for blk in self.stage_up3:
             x = blk(x)
-        x = self._fuse(self.concat_linear3, torch.cat([self._skip(self.x2), self.upsample3(x)], -1))
+        x = self._concat(self.concat_linear3, self.x2, self._x2s, self.upsample3(x))
         for blk in self.stage_up2:
             x = blk(x)
-        x = self._fuse(self.concat_linear2, torch.cat([self._skip(self.x1), self.upsample2(x)], -1))
+        x = self._concat(self.concat_linear2, self.x1, self._x1s, self.upsample2(x))
         for blk in self.stage_up1:
             x = blk(x)
         return _ln(x, self.norm_up, _compute_dtype(x))

@@ -646,6 +646,90 @@ class _LinearFn(torch.autograd.Function):
         return dx, dw, db, None, None, None
 
 
+class _SharedCastFn(torch.autograd.Function):
+    """One bf16 copy of an fp32 activation handed to two consumers (the encoder skip x1/x2/x3 feeds
+    both Merge_Block's conv and the decoder's concat_linear, cswin:530-545 / 568-592).  Autocast
+    casts it once per consumer; here it is cast once, and the two bf16 input gradients are summed
+    in fp32 as autocast's two cast nodes would."""
+
+    @staticmethod
+    def forward(ctx, x, dtype):
+        y = x.to(dtype)
+        ctx.xdt = x.dtype
+        return y, y.view_as(y)
+
+    @staticmethod
+    def backward(ctx, g1, g2):
+        if g1 is None and g2 is None:
+            return None, None
+        if g1 is None or g2 is None:
+            return (g1 if g2 is None else g2).to(ctx.xdt), None
+        g = g1.to(ctx.xdt)
+        g.add_(g2)
+        return g, None
+
+
+def shared_cast(x: torch.Tensor, dtype: torch.dtype):
+    """(xc, xc) -- the same `dtype` copy of x for two consumers (see _SharedCastFn)."""
+    return _SharedCastFn.apply(x, dtype)
+
+
+def _concat_wgrad(dy2, a2, b2):
+    dwa, db = linear_wgrad(dy2, a2)
+    dwb, _ = linear_wgrad(dy2, b2)
+    return torch.cat([dwa, dwb], 1), db
+
+
+class _ConcatLinearFn(torch.autograd.Function):
+    """Linear(cat([a, b], -1)) without the cat (the decoder's concat_linear, cswin:568/581/592):
+    y = a @ W[:, :Ca]^T + bias, then y += b @ W[:, Ca:]^T, two bf16 GEMMs (fp32 out, the second
+    with the residual epilogue) reading the weight halves in place (ldb = Ca + Cb).  The
+    reference path writes the fp32 concatenation and casts it to bf16 again (2176 -> 1408 B per
+    token at C = 64); backward: two input-gradient GEMMs into the separate halves (no strided
+    slices of a concatenated gradient) and two weight-gradient GEMMs."""
+
+    @staticmethod
+    def forward(ctx, a, b, weight, bias, wc):
+        Ca, Cb, N = a.shape[-1], b.shape[-1], weight.shape[0]
+        a2 = a.reshape(-1, Ca).contiguous()
+        b2 = b.reshape(-1, Cb).contiguous()
+        bf = bias.detach().float().contiguous()
+        y1 = gemm(a2, wc[:, :Ca], False, torch.float32, bias=bf)
+        y = gemm(b2, wc[:, Ca:], False, torch.float32, resid=y1)
+        ctx.save_for_backward(a2, b2, _weight_t(weight, wc))
+        ctx.meta = (a.shape, b.shape, a.dtype, b.dtype, weight.dtype, bias.dtype)
+        return y.view(*a.shape[:-1], N)
+
+    @staticmethod
+    def backward(ctx, dy):
+        a2, b2, wt = ctx.saved_tensors     # wt: (Ca + Cb, N)
+        ashape, bshape, adt, bdt_in, wdt, bdt = ctx.meta
+        Ca = a2.shape[1]
+        dy2 = _bf16_of(dy).reshape(-1, dy.shape[-1]).contiguous()
+        da = gemm(dy2, wt[:Ca], False, adt).view(ashape) if ctx.needs_input_grad[0] else None
+        db_in = gemm(dy2, wt[Ca:], False, bdt_in).view(bshape) if ctx.needs_input_grad[1] else None
+        if _side_ok(dy2, wdt, bdt):
+            dw, dbias = _side_run(lambda: _concat_wgrad(dy2, a2, b2), dy2, a2, b2)
+        else:
+            dw, dbias = _concat_wgrad(dy2, a2, b2)
+        return da, db_in, dw.to(wdt), dbias.to(bdt), None
+
+
+def concat_linear(a: torch.Tensor, b: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor) -> torch.Tensor:
+    """fp32 Linear(cat([a, b], -1)) for bf16 a, b under bf16 autocast (see _ConcatLinearFn); other
+    inputs take the reference form (cat, then linear with an fp32 output)."""
+    Ca, Cb, N = a.shape[-1], b.shape[-1], weight.shape[0]
+    if (a.is_cuda and FUSED_GEMM and torch.is_autocast_enabled("cuda")
+            and torch.get_autocast_dtype("cuda") == torch.bfloat16 and a.dtype == b.dtype == torch.bfloat16
+            and bias is not None and _gemm_ok(Ca, Cb, N)):
+        wc = _ACTIVE_CACHE.get(weight, torch.bfloat16) if _ACTIVE_CACHE is not None else None
+        if wc is None:
+            wc = weight.to(torch.bfloat16)
+        with torch.autocast("cuda", enabled=False):
+            return _ConcatLinearFn.apply(a, b, weight, bias, wc)
+    return linear(torch.cat([a, b], -1), weight, bias, out_dtype=torch.float32 if a.is_cuda else None)
+
+
 class _LinearResidualFn(torch.autograd.Function):
     """res + x @ W^T + b in one csu_gemm (fp32 out): proj + residual of CSWinBlock (cswin:366-367)."""
 

@@ -171,6 +171,9 @@ class GraphedTrainStep:
             for _ in range(warmup):
                 self._body()
         torch.cuda.current_stream().wait_stream(side)
+        # drain the warm-up (its RCCL work included) before capturing: nothing of it is pending
+        # when the capture starts
+        torch.cuda.synchronize()
         self.graph = torch.cuda.CUDAGraph()
         self.opt.zero_grad(set_to_none=True)
         with torch.cuda.graph(self.graph):

@@ -583,3 +583,36 @@ def test_fused_adamw_matches_torch(capturable):
     for p, q in zip(ref, mine):
         torch.testing.assert_close(o_mine.state[q]["exp_avg"], o_ref.state[p]["exp_avg"], rtol=1e-5, atol=1e-7)
         torch.testing.assert_close(o_mine.state[q]["exp_avg_sq"], o_ref.state[p]["exp_avg_sq"], rtol=5e-5, atol=1e-9)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,L,C,N", [(2, 4096, 64, 64), (2, 1024, 128, 128), (3, 256, 256, 256), (1, 100, 64, 64)])
+def test_concat_linear_and_shared_cast_vs_fp64(B, L, C, N):
+    """Decoder skip fusion without the cat (ops.concat_linear: two GEMMs on the weight halves) and
+    the shared bf16 skip copy (ops.shared_cast) vs Linear(cat([skip, up])) in fp64 (cswin:568-592)."""
+    from csu import ops
+    d = dev()
+    g = torch.Generator(device=d).manual_seed(B * L + C)
+    skip = torch.randn(B, L, C, device=d, generator=g, requires_grad=True)
+    up = torch.randn(B, L, C, device=d, generator=g).bfloat16().requires_grad_(True)
+    w = (torch.randn(N, 2 * C, device=d, generator=g) * 0.05).requires_grad_(True)
+    b = torch.randn(N, device=d, generator=g).requires_grad_(True)
+    gy = torch.randn(B, L, N, device=d, generator=g)
+    gm = torch.randn(B, L, C, device=d, generator=g)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        sm, sk = ops.shared_cast(skip, torch.bfloat16)
+        y = ops.concat_linear(sk, up, w, b)
+    assert y.dtype == torch.float32 and sm.dtype == torch.bfloat16 and sm.data_ptr() == sk.data_ptr()
+    # second consumer of the shared copy (stands in for Merge_Block's conv)
+    (y * gy).sum().backward(retain_graph=True)
+    (sm.float() * gm).sum().backward()
+    s2, u2, w2, b2 = (t.detach().double().requires_grad_(True) for t in (skip, up, w, b))
+    sb = s2.bfloat16().double()            # the bf16 rounding autocast applies to the GEMM input
+    y2 = torch.nn.functional.linear(torch.cat([sb, u2], -1), w2.bfloat16().double(), b2)
+    (y2 * gy.double()).sum().backward()
+    gskip_ref = s2.grad + gm.double()
+    for got, ref, name in ((y, y2, "y"), (skip.grad, gskip_ref, "dskip"), (up.grad, u2.grad, "dup"),
+                           (w.grad, w2.grad, "dw"), (b.grad, b2.grad, "db")):
+        ref = ref.detach()
+        err = float((got.double() - ref).norm() / ref.norm().clamp_min(1e-30))
+        assert err <= 2e-2, (name, err)
