@@ -104,6 +104,9 @@ class GradAllReduce:
             self.views.append(vs)
         self.where = {id(p): bi for bi, b in enumerate(self.buckets) for p in b}
         self.side = torch.cuda.Stream(dev) if dev.type == "cuda" else None
+        from . import ops
+        self._ops = ops
+        ops._DIST_SAFE[0] = True   # side-stream weight gradients: ordered by _launch below
         self._reset()
         self.handles = [p.register_post_accumulate_grad_hook(self._hook) for p in self.params]
 
@@ -131,6 +134,11 @@ class GradAllReduce:
         self.held.append(grads)
         if self.side is not None:
             self.side.wait_stream(torch.cuda.current_stream(flat.device))
+            ws = self._ops.side_stream(flat.device)
+            if ws is not None:      # weight gradients still being written on the csu side stream
+                self.side.wait_stream(ws)
+            for g in grads:
+                g.record_stream(self.side)
             ctx = torch.cuda.stream(self.side)
         else:
             ctx = contextlib.nullcontext()

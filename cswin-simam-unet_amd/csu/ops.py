@@ -470,7 +470,17 @@ def _side_ok(t: torch.Tensor, *dtypes) -> bool:
     if not (SIDE_WGRAD and t.is_cuda) or any(d not in (None, torch.float32) for d in dtypes):
         return False
     dist = torch.distributed
-    return not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1)
+    return _DIST_SAFE[0] or not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1)
+
+
+# set by csu.dist.GradAllReduce: its hooks order their reads after the side stream (side_stream()),
+# so side-stream weight gradients stay on under multi-rank training with it (not with DDP)
+_DIST_SAFE = [False]
+
+
+def side_stream(device) -> Optional["torch.cuda.Stream"]:
+    """The side stream weight gradients of `device` are computed on (None before the first)."""
+    return _SIDE_STREAMS.get(device)
 
 
 # CSU_DEFER_WGRAD_REDUCE=1 (side-stream mode): every weight gradient leaves its split-K partial slabs

@@ -29,10 +29,13 @@ def step():
 for _ in range(3):
     step()
 torch.cuda.synchronize()
-with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True) as prof:
+STACK = os.environ.get("STACK", "0") == "1"   # group by the Python call site instead of the shapes
+with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True, with_stack=STACK) as prof:
     step()
     torch.cuda.synchronize()
-rows = [e for e in prof.key_averages(group_by_input_shape=True) if e.key.startswith("aten::") and e.self_device_time_total > 0]
+ka = prof.key_averages(group_by_stack_n=6) if STACK else prof.key_averages(group_by_input_shape=True)
+rows = [e for e in ka if e.key.startswith("aten::") and e.self_device_time_total > 0]
 rows.sort(key=lambda e: -e.self_device_time_total)
 for e in rows[:40]:
-    print(f"{e.self_device_time_total:9.1f} us  n={e.count:4d}  {e.key:32s} {str(e.input_shapes)[:150]}")
+    where = " <- ".join(f.split("/")[-1] for f in e.stack[:6] if "csu" in f or "model" in f) if STACK else str(e.input_shapes)[:150]
+    print(f"{e.self_device_time_total:9.1f} us  n={e.count:4d}  {e.key:32s} {where}")
