@@ -10,6 +10,8 @@ from __future__ import annotations
 
 from typing import Dict, List, Optional
 
+import time
+
 import torch
 import torch.distributed as dist
 import torch.nn.functional as F
@@ -174,9 +176,17 @@ class GraphedTrainStep:
         # drain the warm-up (its RCCL work included) before capturing: nothing of it is pending
         # when the capture starts
         torch.cuda.synchronize()
+        mode = "global"
+        if reducer is not None:
+            # the RCCL process group's watchdog thread polls the events of finished collectives
+            # (hipEventQuery); under a global-mode capture that call fails in the other thread and
+            # aborts the process.  Let it retire the warm-up's work items, and capture in
+            # thread-local mode so its polling stays legal.
+            time.sleep(0.5)
+            mode = "thread_local"
         self.graph = torch.cuda.CUDAGraph()
         self.opt.zero_grad(set_to_none=True)
-        with torch.cuda.graph(self.graph):
+        with torch.cuda.graph(self.graph, capture_error_mode=mode):
             self.loss, self.out = self._body(zero=False)
 
     def _body(self, zero=True):

@@ -221,3 +221,29 @@ def test_unet_bf16_vs_oracle():
         rel = (q.grad.float().cpu() - ref).norm().item() / ref.norm().item()
         rel_torch = (pt[k].grad.float().cpu() - ref).norm().item() / ref.norm().item()
         assert rel < max(5e-2, 2 * rel_torch), (k, rel, rel_torch)
+
+
+@pytest.mark.gpu
+def test_dp_path_graph_captured_allreduce_matches_single_process():
+    """bench.py --dp-force: RCCL process group + GradAllReduce captured in the step graph, with the
+    side-stream weight gradients on (world size 1: AVG is exact), trains like the plain
+    single-process graph step (equal final loss, 5 decimals, after the same steps)."""
+    import json
+    import socket
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    base = [sys.executable, os.path.join(repo, "bench.py"), "--steps", "3", "--warmup", "2", "--img", "256",
+            "--batch", "4", "--no-roofline", "--cpu-baseline", "off"]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    out = {}
+    for tag, extra in (("single", []), ("dp", ["--dp-force"])):
+        r = subprocess.run(base + extra, env=env, capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr[-2000:]
+        out[tag] = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["dp"]["grad_allreduce"] == "graph-captured buckets" and out["dp"]["hip_graph"]
+    assert out["dp"]["final_loss"] == out["single"]["final_loss"], out
