@@ -461,6 +461,8 @@ SIDE_WGRAD = _os.environ.get("CSU_SIDE_WGRAD", "1") == "1"
 # measured 1-2 % slower (969-979 vs 988 img/s, two A/B pairs) -- the extra graph branches delay
 # the critical-path kernels more than the overlap saves
 SIDE_AUX = _os.environ.get("CSU_SIDE_AUX", "0") == "1"
+# CSU_SIDE_CONV=0: convolution weight gradients inline on the launching stream
+SIDE_CONV = _os.environ.get("CSU_SIDE_CONV", "1") == "1"
 _SIDE_STREAMS = {}
 _SIDE_PENDING = []
 _SIDE_JOIN_QUEUED = [False]
@@ -1059,6 +1061,14 @@ class _Conv2dFn(torch.autograd.Function):
                                          stream_ptr(dy.device)), "csu_conv2d_dgrad")
             if dx.dtype != xdt:
                 dx = dx.to(xdt)
+        if SIDE_CONV and _side_ok(dy, weight.dtype, bdt if has_b else None):
+            # weight gradient (+ its OIHW re-layout, so the returned grad is stolen as-is) on the
+            # side stream, like the token-Linear weight gradients
+            def wg():
+                w_, b_ = _conv_wgrad(g, xc, dy, dtype_code(dy))
+                return w_.permute(0, 3, 1, 2).contiguous(), b_
+            dw, db = _side_run(wg, xc, dy)
+            return dx, dw, (db if has_b else None), None, None, None
         dw, db = _conv_wgrad(g, xc, dy, dtype_code(dy))
         return dx, dw.permute(0, 3, 1, 2).to(weight.dtype), (db.to(bdt) if has_b else None), None, None, None
 
