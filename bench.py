@@ -213,7 +213,7 @@ def main():
         except Exception as e:  # baseline is informational; never hide the GPU number
             cpu = {"value": None, "error": repr(e)[:200]}
     if rank == 0:
-        rec = {"metric": "images/sec at 512x512 bf16 (CSWin-UNet train step)", "value": round(images / el, 3),
+        rec = {"metric": f"images/sec at {args.img}x{args.img} {args.dtype} (CSWin-UNet train step)", "value": round(images / el, 3),
                "unit": "images/sec", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
                "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
                "vs_baseline": None, "dtype": args.dtype, "data": "synthetic (ellipse masks, SURVEY §8d), random-init weights",
