@@ -12,6 +12,8 @@
 // Wf = weight permuted to [n][ky][kx][c] (OHWI), Wd = [c][ky][kx][n] (IHWO); both prepared by the caller.
 // Tiles: 64 x 64 outputs per 256-thread workgroup, 4 waves of one 32x32 MFMA tile, 32-deep K slices
 // gathered per 8-channel chunk (16-B loads when the gathered channel count is a multiple of 8).
+#include <cstdlib>
+
 #include "common.hpp"
 
 namespace csu {
@@ -146,7 +148,8 @@ template <typename T, bool VEC>
 __global__ __launch_bounds__(NT) void conv_wgrad_kernel(Geo g, long Mrows, int Ncols, int Kdim, long rows_per_chunk,
                                                         const T* __restrict__ x, const T* __restrict__ dy,
                                                         float* __restrict__ part) {
-    constexpr int TM = 32;               // rows per step
+    constexpr int TM = 64;               // rows per step: two row groups per thread, both loads in flight
+    constexpr int RG = TM / 32;
     constexpr int S = TM + (sizeof(T) == 2 ? 8 : 4);
     __shared__ __attribute__((aligned(16))) T At[TBN * S];   // dy^T [n][m]
     __shared__ __attribute__((aligned(16))) T Bt[TBN * S];   // X^T  [k][m]
@@ -158,25 +161,48 @@ __global__ __launch_bounds__(NT) void conv_wgrad_kernel(Geo g, long Mrows, int N
     const bool do_bias = blockIdx.y == 0;
     f32x16 acc = {};
     float bsum = 0.f;
-    // staging: 32 rows x 8 chunks = 256 chunks per operand -> one per thread
+    // staging: RG x (32 rows x 8 chunks) = RG chunks per operand per thread, all loads issued
+    // before the LDS stores (one memory round trip per TM rows)
     const int srow = threadIdx.x >> 3, sch = threadIdx.x & 7;
+    // VEC: this thread's 8 reduction indices are one (ky, kx) tap and 8 channels of one pixel,
+    // fixed for the whole loop -- decomposed once; rows are decomposed with 32-bit arithmetic
+    // (the generic gather8 spent ~4 64-bit divisions per load)
+    const int kk = k0 + sch * 8;
+    const bool kval = kk < Kdim;
+    const int ktap = kk / g.C, kc = kk - ktap * g.C;
+    const int kdy = ktap / g.KW - g.p, kdx = ktap % g.KW - g.p;
     for (long m0 = mb; m0 < me; m0 += TM) {
-        const long m = m0 + srow;
-        float va[8], vb[8];
-        {
+        float va[RG][8], vb[RG][8];
+#pragma unroll
+        for (int q = 0; q < RG; ++q) {
+            const long m = m0 + 32 * q + srow;
             const int n = n0 + sch * 8;
-            if (Ncols % 8 == 0 && m < me && n + 8 <= Ncols) load8(dy + m * Ncols + n, va);
+            if (Ncols % 8 == 0 && m < me && n + 8 <= Ncols) load8(dy + m * Ncols + n, va[q]);
             else
 #pragma unroll
-                for (int j = 0; j < 8; ++j) va[j] = (m < me && n + j < Ncols) ? to_f(dy[m * Ncols + n + j]) : 0.f;
+                for (int j = 0; j < 8; ++j) va[q][j] = (m < me && n + j < Ncols) ? to_f(dy[m * Ncols + n + j]) : 0.f;
+            if constexpr (VEC) {
+                const int mi = (int)m;             // M < 2^31 (check_geo)
+                const int ox = mi % g.OW, t = mi / g.OW;
+                const int oy = t % g.OH, b = t / g.OH;
+                const int iy = oy * g.s + kdy, ix = ox * g.s + kdx;
+                if (kval && m < me && iy >= 0 && iy < g.H && ix >= 0 && ix < g.W)
+                    load8(x + (((long)b * g.H + iy) * g.W + ix) * g.C + kc, vb[q]);
+                else
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) vb[q][j] = 0.f;
+            } else {
+                gather8<0, T, VEC>(g, x, m, k0 + sch * 8, me, vb[q]);
+            }
         }
-        gather8<0, T, VEC>(g, x, m, k0 + sch * 8, me, vb);
         __syncthreads();
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            At[(sch * 8 + j) * S + srow] = from_f<T>(va[j]);
-            Bt[(sch * 8 + j) * S + srow] = from_f<T>(vb[j]);
-        }
+        for (int q = 0; q < RG; ++q)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                At[(sch * 8 + j) * S + 32 * q + srow] = from_f<T>(va[q][j]);
+                Bt[(sch * 8 + j) * S + 32 * q + srow] = from_f<T>(vb[q][j]);
+            }
         __syncthreads();
         if (do_bias && threadIdx.x < TBN) {
 #pragma unroll
@@ -204,6 +230,98 @@ __global__ __launch_bounds__(NT) void conv_wgrad_kernel(Geo g, long Mrows, int N
         if (n < Ncols && k < Kdim) out[(long)n * Kdim + k] = acc[reg];
     }
     if (do_bias && threadIdx.x < TBN && n0 + threadIdx.x < Ncols) out[(long)Ncols * Kdim + n0 + threadIdx.x] = bsum;
+}
+
+// bf16 weight gradient, v2 (C % 8 == 0): operand tiles staged ROW-major in LDS ([m][n] of dy,
+// [m][k] of the gathered x) with 16-B stores, MFMA fragments gathered by the gfx950 transposing
+// read ds_read_b64_tr_b16 (as wgrad.hip) -- the v1 kernel above stores both tiles transposed with
+// 2-B LDS writes, 64 per thread per step, most of them bank conflicts.  64 rows per step, both
+// row groups' global loads in flight together; the thread's tap is decomposed once.
+typedef short cv4s __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ cv4s ctr_read(const bf16* p) {
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) cv4s*)(p));
+}
+template <int RS>
+__device__ __forceinline__ bf16x8 ctr_frag(const bf16* img, int c0, int s, int lane) {
+    const int grp = lane >> 4, l = lane & 15, q = l >> 2, p = l & 3;
+    const int col = c0 + 16 * (grp & 1) + 4 * p;
+    const int row = 16 * s + 8 * (grp >> 1) + q;
+    const cv4s v[2] = {ctr_read(img + row * RS + col), ctr_read(img + (row + 4) * RS + col)};
+    bf16x8 out;
+    __builtin_memcpy(&out, v, 16);
+    return out;
+}
+
+__global__ __launch_bounds__(NT) void conv_wgrad_bf16(Geo g, long Mrows, int Ncols, int Kdim, long rows_per_chunk,
+                                                      const bf16* __restrict__ x, const bf16* __restrict__ dy,
+                                                      float* __restrict__ part) {
+    constexpr int TM = 64, RG = TM / 32;
+    constexpr int RS = TBN + 32;          // 64 data + 64 B pad: conflict-free transposing reads
+    __shared__ __attribute__((aligned(16))) bf16 At[TM * RS];   // dy tile [m][n]
+    __shared__ __attribute__((aligned(16))) bf16 Bt[TM * RS];   // x  tile [m][k] (gathered)
+    const int n0 = blockIdx.x * TBN, k0 = blockIdx.y * TBN;
+    const long mb = (long)blockIdx.z * rows_per_chunk, me = min(Mrows, mb + rows_per_chunk);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int h = lane >> 5;
+    const int wn = (wave >> 1) * 32, wk = (wave & 1) * 32;
+    const bool do_bias = blockIdx.y == 0;
+    f32x16 acc = {};
+    float bsum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    const int srow = threadIdx.x >> 3, sch = threadIdx.x & 7;
+    const int kk = k0 + sch * 8;
+    const bool kval = kk < Kdim;
+    const int ktap = kk / g.C, kc = kk - ktap * g.C;
+    const int kdy = ktap / g.KW - g.p, kdx = ktap % g.KW - g.p;
+    const int n = n0 + sch * 8;
+    const bool nval = n + 8 <= Ncols;      // Ncols % 8 == 0 on this path
+    for (long m0 = mb; m0 < me; m0 += TM) {
+        bf16x8 va[RG], vb[RG];
+#pragma unroll
+        for (int q = 0; q < RG; ++q) {
+            const long m = m0 + 32 * q + srow;
+            const bool mv = m < me;
+            va[q] = (mv && nval) ? *reinterpret_cast<const bf16x8*>(dy + m * Ncols + n) : bf16x8{};
+            const int mi = (int)m;             // M < 2^31 (check_geo)
+            const int ox = mi % g.OW, t = mi / g.OW;
+            const int oy = t % g.OH, b = t / g.OH;
+            const int iy = oy * g.s + kdy, ix = ox * g.s + kdx;
+            vb[q] = (kval && mv && iy >= 0 && iy < g.H && ix >= 0 && ix < g.W)
+                        ? *reinterpret_cast<const bf16x8*>(x + (((long)b * g.H + iy) * g.W + ix) * g.C + kc)
+                        : bf16x8{};
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < RG; ++q) {
+            *reinterpret_cast<bf16x8*>(At + (32 * q + srow) * RS + sch * 8) = va[q];
+            *reinterpret_cast<bf16x8*>(Bt + (32 * q + srow) * RS + sch * 8) = vb[q];
+            if (do_bias)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) bsum[j] += (float)va[q][j];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int s = 0; s < TM / 16; ++s)
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ctr_frag<RS>(At, wn, s, lane), ctr_frag<RS>(Bt, wk, s, lane),
+                                                          acc, 0, 0, 0);
+    }
+    const long slab = ((long)Ncols * Kdim + Ncols + 3) & ~3L;   // 16-B aligned slab rows for colsum
+    float* out = part + (long)blockIdx.z * slab;
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+        const int nn = n0 + wn + crow(reg, h), k = k0 + wk + (lane & 31);
+        if (nn < Ncols && k < Kdim) out[(long)nn * Kdim + k] = acc[reg];
+    }
+    if (do_bias) {   // column sums: 8 columns per thread, 32 row-threads per column group
+        __shared__ float bcol[32][TBN + 1];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) bcol[srow][sch * 8 + j] = bsum[j];
+        __syncthreads();
+        if (threadIdx.x < TBN && n0 + threadIdx.x < Ncols) {
+            float sacc = 0.f;
+            for (int r = 0; r < 32; ++r) sacc += bcol[r][threadIdx.x];
+            out[(long)Ncols * Kdim + n0 + threadIdx.x] = sacc;
+        }
+    }
 }
 
 // ---- bf16 implicit GEMM, v2: 128/256 x BN tiles, 64-deep K slices, double-buffered LDS ----------
@@ -407,6 +525,8 @@ int check_geo(const csu_conv_geom* g) {
         return fail(CSU_E_ARG, "conv2d: bad geometry");
     if (g->OH != (g->H + 2 * g->pad - g->KH) / g->stride + 1 || g->OW != (g->W + 2 * g->pad - g->KW) / g->stride + 1)
         return fail(CSU_E_ARG, "conv2d: output size inconsistent with H, W, kernel, stride, pad");
+    if ((long)g->B * g->H * g->W >= (1L << 31) || (long)g->B * g->OH * g->OW >= (1L << 31))
+        return fail(CSU_E_UNSUPPORTED, "conv2d: more than 2^31 pixels");
     return 0;
 }
 
@@ -418,15 +538,31 @@ struct WPl {
     int chunks;
     long rpc;
 };
+bool conv_wgrad_v2() {   // CSU_CONV_WGRAD_V1=1: the transposed-staging v1 kernel (A/B)
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("CSU_CONV_WGRAD_V1");
+        v = !(e && e[0] == '1');
+    }
+    return v == 1;
+}
+int conv_wg_target() {   // CSU_CONV_WGS: target workgroups of the weight-gradient split (A/B)
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("CSU_CONV_WGS");
+        v = e ? atoi(e) : 2048;
+    }
+    return v;
+}
 WPl wplan(long M, int N, int K) {
     const long tiles = (long)((N + TBN - 1) / TBN) * ((K + TBN - 1) / TBN);
-    long want = (1024 + tiles - 1) / tiles;
+    long want = (conv_wg_target() + tiles - 1) / tiles;
     const long maxc = (M + 255) / 256;
     if (want > maxc) want = maxc;
-    if (want > 256) want = 256;
+    if (want > 512) want = 512;
     if (want < 1) want = 1;
     WPl p;
-    p.rpc = ((M + want - 1) / want + 31) / 32 * 32;
+    p.rpc = ((M + want - 1) / want + 63) / 64 * 64;
     p.chunks = (int)((M + p.rpc - 1) / p.rpc);
     return p;
 }
@@ -511,7 +647,9 @@ extern "C" int csu_conv2d_wgrad(const csu_conv_geom* gm, int dtype, const void* 
     const bool vec = g.C % 8 == 0;
     hipStream_t st = as_stream(stream);
     if (dtype == CSU_BF16) {
-        if (vec) conv_wgrad_kernel<bf16, true><<<grid, NT, 0, st>>>(g, M, g.N, K, p.rpc, (const bf16*)x, (const bf16*)dy, part);
+        if (vec && g.N % 8 == 0 && conv_wgrad_v2())
+            conv_wgrad_bf16<<<grid, NT, 0, st>>>(g, M, g.N, K, p.rpc, (const bf16*)x, (const bf16*)dy, part);
+        else if (vec) conv_wgrad_kernel<bf16, true><<<grid, NT, 0, st>>>(g, M, g.N, K, p.rpc, (const bf16*)x, (const bf16*)dy, part);
         else conv_wgrad_kernel<bf16, false><<<grid, NT, 0, st>>>(g, M, g.N, K, p.rpc, (const bf16*)x, (const bf16*)dy, part);
     } else if (dtype == CSU_F32) {
         if (vec) conv_wgrad_kernel<float, true><<<grid, NT, 0, st>>>(g, M, g.N, K, p.rpc, (const float*)x, (const float*)dy, part);

@@ -461,6 +461,9 @@ SIDE_WGRAD = _os.environ.get("CSU_SIDE_WGRAD", "1") == "1"
 # measured 1-2 % slower (969-979 vs 988 img/s, two A/B pairs) -- the extra graph branches delay
 # the critical-path kernels more than the overlap saves
 SIDE_AUX = _os.environ.get("CSU_SIDE_AUX", "0") == "1"
+# CSU_PAD_CHANNELS=0: convolutions of inputs with C % 8 != 0 (the 3-channel image) without the zero
+# channel padding (per-element gathers; A/B)
+PAD_CHANNELS = _os.environ.get("CSU_PAD_CHANNELS", "1") == "1"
 # CSU_SIDE_CONV=0: convolution weight gradients inline on the launching stream
 SIDE_CONV = _os.environ.get("CSU_SIDE_CONV", "1") == "1"
 _SIDE_STREAMS = {}
@@ -1028,14 +1031,24 @@ class _Conv2dFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, stride: int, pad: int, cd):
         require_device(x, weight)
-        xc = (x if x.dtype == cd else x.to(cd)).contiguous()
-        B, H, W, C = xc.shape
+        B, H, W, C = x.shape
         N, Cw, KH, KW = weight.shape
         if Cw != C:
             raise ValueError(f"conv2d: input has {C} channels, weight expects {Cw}")
-        g = _conv_geom(B, H, W, C, N, KH, KW, stride, pad)
-        cached = _ACTIVE_CACHE.get_conv(weight, cd) if _ACTIVE_CACHE is not None else None
-        w_ohwi = cached[0] if cached else weight.detach().permute(0, 2, 3, 1).to(cd).contiguous()
+        cp = (C + 7) // 8 * 8 if (C % 8 and PAD_CHANNELS) else C
+        if cp != C:
+            # few-channel input (the 3-channel image of the patch embed): zero channels up to a
+            # multiple of 8 in the image and the weight -- 16-B vector gathers in the conv kernels
+            # instead of per-element ones; the padded taps add exact zeros
+            xc = torch.zeros(B, H, W, cp, dtype=cd, device=x.device)
+            xc[..., :C] = x
+            w_ohwi = torch.nn.functional.pad(weight.detach().permute(0, 2, 3, 1).to(cd), (0, cp - C)).contiguous()
+            cached = None
+        else:
+            xc = (x if x.dtype == cd else x.to(cd)).contiguous()
+            cached = _ACTIVE_CACHE.get_conv(weight, cd) if _ACTIVE_CACHE is not None else None
+            w_ohwi = cached[0] if cached else weight.detach().permute(0, 2, 3, 1).to(cd).contiguous()
+        g = _conv_geom(B, H, W, cp, N, KH, KW, stride, pad)
         y = torch.empty(B, g.OH, g.OW, N, dtype=cd, device=x.device)
         bf = None if bias is None else bias.detach().float().contiguous()
         check(lib().csu_conv2d_fwd(ctypes.byref(g), dtype_code(xc), ptr(xc), ptr(w_ohwi), ptr(bf), ptr(y),
@@ -1049,28 +1062,35 @@ class _Conv2dFn(torch.autograd.Function):
     def backward(ctx, dy):
         xc, weight = ctx.saved_tensors
         stride, pad, cd, xdt, has_b, bdt = ctx.conf
-        B, H, W, C = xc.shape
-        N, _, KH, KW = weight.shape
-        g = _conv_geom(B, H, W, C, N, KH, KW, stride, pad)
+        B, H, W, cp = xc.shape                 # cp: channels incl. the zero padding
+        N, C, KH, KW = weight.shape
+        g = _conv_geom(B, H, W, cp, N, KH, KW, stride, pad)
         dy = dy.to(cd).contiguous()
         dx = None
         if ctx.needs_input_grad[0]:
-            w_ihwo = ctx.w_ihwo if ctx.w_ihwo is not None else weight.detach().permute(1, 2, 3, 0).to(cd).contiguous()
-            dx = torch.empty(B, H, W, C, dtype=cd, device=dy.device)
+            if cp != C:
+                w_ihwo = torch.nn.functional.pad(weight.detach().permute(1, 2, 3, 0).to(cd), (0, 0, 0, 0, 0, 0, 0, cp - C))
+                w_ihwo = w_ihwo.contiguous()
+            else:
+                w_ihwo = ctx.w_ihwo if ctx.w_ihwo is not None else weight.detach().permute(1, 2, 3, 0).to(cd).contiguous()
+            dx = torch.empty(B, H, W, cp, dtype=cd, device=dy.device)
             check(lib().csu_conv2d_dgrad(ctypes.byref(g), dtype_code(dy), ptr(dy), ptr(w_ihwo), None, ptr(dx),
                                          stream_ptr(dy.device)), "csu_conv2d_dgrad")
+            if cp != C:
+                dx = dx[..., :C]
             if dx.dtype != xdt:
                 dx = dx.to(xdt)
+
+        def wg():   # (dW (N, C, KH, KW) contiguous, db): also the OIHW re-layout and the unpadding
+            w_, b_ = _conv_wgrad(g, xc, dy, dtype_code(dy))
+            return w_[..., :C].permute(0, 3, 1, 2).contiguous(), b_
         if SIDE_CONV and _side_ok(dy, weight.dtype, bdt if has_b else None):
-            # weight gradient (+ its OIHW re-layout, so the returned grad is stolen as-is) on the
-            # side stream, like the token-Linear weight gradients
-            def wg():
-                w_, b_ = _conv_wgrad(g, xc, dy, dtype_code(dy))
-                return w_.permute(0, 3, 1, 2).contiguous(), b_
+            # on the side stream, like the token-Linear weight gradients; the returned grad is
+            # contiguous fp32, so autograd steals it without a kernel on this stream
             dw, db = _side_run(wg, xc, dy)
             return dx, dw, (db if has_b else None), None, None, None
-        dw, db = _conv_wgrad(g, xc, dy, dtype_code(dy))
-        return dx, dw.permute(0, 3, 1, 2).to(weight.dtype), (db.to(bdt) if has_b else None), None, None, None
+        dw, db = wg()
+        return dx, dw.to(weight.dtype), (db.to(bdt) if has_b else None), None, None, None
 
 
 def conv2d(x_nhwc: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor], stride: int = 1,
