@@ -343,15 +343,26 @@ struct IG {
 
 __device__ __forceinline__ int swz128(int row, int chunk) { return row * 64 + ((chunk ^ (row & 7)) << 3); }
 
+// up to 4 independent problems in one launch (blockIdx.z): the stride phases of an input gradient
+// run concurrently instead of as 1-4 small launches each (a 16x16x512 -> 32x32x256 input gradient
+// is 4 launches of 128 workgroups)
+struct IG4 {
+    IG g[4];
+};
+
 template <int BN, int VW>
-__global__ __launch_bounds__(NT) void igemm_bf16(IG g, const bf16* __restrict__ src, const bf16* __restrict__ Bw,
+__global__ __launch_bounds__(NT) void igemm_bf16(IG4 gs, const bf16* __restrict__ src, const bf16* __restrict__ Bw,
                                                  const float* __restrict__ bias, bf16* __restrict__ out) {
     constexpr int WN = BN / 32, WM = 4 / WN, BM = WM * 64, BK = 64;
     constexpr int ACH = BM * 8 / NT, BCH = BN * 8 / NT, NP = 8 / VW;
     __shared__ __attribute__((aligned(16))) bf16 As[2][BM * BK];
     __shared__ __attribute__((aligned(16))) bf16 Bs[2][BN * BK];
     __shared__ long ooff[BM];
+    // problem of this z-slice (selects, not a dynamic index into the kernel-argument struct)
+    const int z = blockIdx.z;
+    const IG g = z == 0 ? gs.g[0] : z == 1 ? gs.g[1] : z == 2 ? gs.g[2] : gs.g[3];
     const long m0 = (long)blockIdx.x * BM;
+    if (m0 >= g.M) return;   // phases differ in size: the grid covers the largest
     const int n0 = blockIdx.y * BN;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int r = lane & 31, h = lane >> 5;
@@ -469,22 +480,41 @@ __global__ __launch_bounds__(NT) void igemm_bf16(IG g, const bf16* __restrict__ 
         }
 }
 
-int launch_ig(const IG& g, const void* src, const void* w, const float* bias, void* out, hipStream_t st) {
+// n problems with equal Ncols and channel count (the phases of one input gradient, or one forward)
+int launch_ig(const IG* gv, int n, const void* src, const void* w, const float* bias, void* out, hipStream_t st) {
+    IG4 gs{};
+    long maxm = 0;
+    for (int i = 0; i < n; ++i) {
+        gs.g[i] = gv[i];
+        maxm = gv[i].M > maxm ? gv[i].M : maxm;
+    }
+    const IG& g = gv[0];
     const int vw = g.Cs % 8 == 0 ? 8 : 4;
     const bool narrow = g.Ncols <= 32;
     const int BM = narrow ? 256 : 128, BN = narrow ? 32 : 64;
-    const dim3 grid((unsigned)((g.M + BM - 1) / BM), (g.Ncols + BN - 1) / BN);
+    const dim3 grid((unsigned)((maxm + BM - 1) / BM), (g.Ncols + BN - 1) / BN, n);
     const bf16* s = (const bf16*)src;
     const bf16* wb = (const bf16*)w;
     bf16* o = (bf16*)out;
     if (narrow) {
-        if (vw == 8) igemm_bf16<32, 8><<<grid, NT, 0, st>>>(g, s, wb, bias, o);
-        else igemm_bf16<32, 4><<<grid, NT, 0, st>>>(g, s, wb, bias, o);
+        if (vw == 8) igemm_bf16<32, 8><<<grid, NT, 0, st>>>(gs, s, wb, bias, o);
+        else igemm_bf16<32, 4><<<grid, NT, 0, st>>>(gs, s, wb, bias, o);
     } else {
-        if (vw == 8) igemm_bf16<64, 8><<<grid, NT, 0, st>>>(g, s, wb, bias, o);
-        else igemm_bf16<64, 4><<<grid, NT, 0, st>>>(g, s, wb, bias, o);
+        if (vw == 8) igemm_bf16<64, 8><<<grid, NT, 0, st>>>(gs, s, wb, bias, o);
+        else igemm_bf16<64, 4><<<grid, NT, 0, st>>>(gs, s, wb, bias, o);
     }
     return check_launch("conv2d (igemm)");
+}
+int launch_ig(const IG& g, const void* src, const void* w, const float* bias, void* out, hipStream_t st) {
+    return launch_ig(&g, 1, src, w, bias, out, st);
+}
+bool ig_phases_fused() {   // CSU_CONV_PHASE_LAUNCHES=1: one launch per stride phase (A/B)
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("CSU_CONV_PHASE_LAUNCHES");
+        v = !(e && e[0] == '1');
+    }
+    return v == 1;
 }
 
 IG ig_forward(const csu_conv_geom& c) {
@@ -608,13 +638,19 @@ extern "C" int csu_conv2d_dgrad(const csu_conv_geom* gm, int dtype, const void* 
     const bool vec = g.N % 8 == 0;
     hipStream_t st = as_stream(stream);
     if (dtype == CSU_BF16 && g.N % 4 == 0) {
+        IG ph[4];
+        int np = 0;
         for (int py = 0; py < g.s; ++py)
             for (int px = 0; px < g.s; ++px) {
                 const IG ig = ig_dgrad_phase(*gm, py, px);
                 if (ig.M == 0) continue;
-                if (int e = launch_ig(ig, dy, w_ihwo, bias, dx, st)) return e;
+                if (np > 0 && (np == 4 || !ig_phases_fused())) {   // stride > 2 (or the A/B switch): flush
+                    if (int e = launch_ig(ph, np, dy, w_ihwo, bias, dx, st)) return e;
+                    np = 0;
+                }
+                ph[np++] = ig;
             }
-        return 0;
+        return np ? launch_ig(ph, np, dy, w_ihwo, bias, dx, st) : 0;
     }
     if (dtype == CSU_BF16) return launch_gemm<bf16, 1>(g, M, g.C, K, dy, w_ihwo, bias, dx, vec, st);
     if (dtype == CSU_F32) return launch_gemm<float, 1>(g, M, g.C, K, dy, w_ihwo, bias, dx, vec, st);
