@@ -414,15 +414,18 @@ def _splitk_wgrad(dy2: torch.Tensor, x2: torch.Tensor) -> torch.Tensor:
     return colsum(part.view(S, N * K)).view(N, K)
 
 
-def linear_wgrad(dy2: torch.Tensor, x2: torch.Tensor):
-    """(dW (N, K), db (N)) fp32 of a token Linear: one MFMA split-K kernel + one reduction."""
+def linear_wgrad(dy2: torch.Tensor, x2: torch.Tensor, out=None, work=None):
+    """(dW (N, K), db (N)) fp32 of a token Linear: one MFMA split-K kernel + one reduction.
+    ``out`` / ``work``: caller-allocated result (N*K + N fp32) and workspace buffers."""
     require_device(dy2, x2)
     M, N = dy2.shape
     K = x2.shape[1]
-    out = torch.empty(N * K + N, dtype=torch.float32, device=dy2.device)
     L = lib()
     n = L.csu_linear_wgrad_workspace(M, N, K)
-    work = torch.empty(max(n, 16), dtype=torch.uint8, device=dy2.device)
+    if out is None:
+        out = torch.empty(N * K + N, dtype=torch.float32, device=dy2.device)
+    if work is None:
+        work = torch.empty(max(n, 16), dtype=torch.uint8, device=dy2.device)
     check(L.csu_linear_wgrad(M, N, K, dtype_code(dy2), ptr(dy2), ptr(x2), ptr(out), ptr(work), n,
                              stream_ptr(dy2.device)), "csu_linear_wgrad")
     return out[:N * K].view(N, K), out[N * K:]
@@ -461,6 +464,12 @@ SIDE_WGRAD = _os.environ.get("CSU_SIDE_WGRAD", "1") == "1"
 # measured 1-2 % slower (969-979 vs 988 img/s, two A/B pairs) -- the extra graph branches delay
 # the critical-path kernels more than the overlap saves
 SIDE_AUX = _os.environ.get("CSU_SIDE_AUX", "0") == "1"
+# CSU_SIDE_IN_GRAPH=1: keep the side stream inside a HIP-graph capture.  Off by default: replays of
+# a captured step with side-stream weight gradients are not bitwise reproducible (tools/det_graph.py:
+# run-to-run loss differences ~1e-6 after a few steps, 0 with this off or with an immediate join;
+# eager steps with the side stream are reproducible, tools/det_eager.py) -- a missing cross-stream
+# dependency in the captured graph that is not yet understood, so the graph runs single-stream.
+SIDE_IN_GRAPH = _os.environ.get("CSU_SIDE_IN_GRAPH", "0") == "1"
 # CSU_PAD_CHANNELS=0: convolutions of inputs with C % 8 != 0 (the 3-channel image) without the zero
 # channel padding (per-element gathers; A/B)
 PAD_CHANNELS = _os.environ.get("CSU_PAD_CHANNELS", "1") == "1"
@@ -473,6 +482,8 @@ _SIDE_JOIN_QUEUED = [False]
 
 def _side_ok(t: torch.Tensor, *dtypes) -> bool:
     if not (SIDE_WGRAD and t.is_cuda) or any(d not in (None, torch.float32) for d in dtypes):
+        return False
+    if not SIDE_IN_GRAPH and torch.cuda.is_current_stream_capturing():
         return False
     dist = torch.distributed
     return _DIST_SAFE[0] or not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1)
@@ -556,6 +567,8 @@ def _side_run(fn, *inputs):
         t.record_stream(side)
     ev = torch.cuda.Event()
     ev.record(side)
+    if _os.environ.get("CSU_SIDE_JOIN_NOW") == "1":   # debug: join right away (no overlap)
+        main.wait_event(ev)
     _SIDE_PENDING.append((main, ev))
     if not _SIDE_JOIN_QUEUED[0]:
         torch.autograd.Variable._execution_engine.queue_callback(join_side_streams)
@@ -563,9 +576,16 @@ def _side_run(fn, *inputs):
     return out
 
 
-def wgrad_maybe_side(dy2: torch.Tensor, x2: torch.Tensor, wdt, bdt):
+_SIDE_SITES = _os.environ.get("CSU_SIDE_SITES", "")   # debug: comma list of call sites allowed on the side stream
+
+
+def _site(name):
+    return not _SIDE_SITES or name in _SIDE_SITES.split(",")
+
+
+def wgrad_maybe_side(dy2: torch.Tensor, x2: torch.Tensor, wdt, bdt, site="lin"):
     """linear_wgrad on the side stream when allowed (fp32 master weights), else inline."""
-    if _side_ok(dy2, wdt, bdt):
+    if _side_ok(dy2, wdt, bdt) and _site(site):
         return _side_run(lambda: (linear_wgrad_deferred if DEFER_REDUCE else linear_wgrad)(dy2, x2), dy2, x2)
     return linear_wgrad(dy2, x2)
 
@@ -723,7 +743,7 @@ class _ConcatLinearFn(torch.autograd.Function):
         dy2 = _bf16_of(dy).reshape(-1, dy.shape[-1]).contiguous()
         da = gemm(dy2, wt[:Ca], False, adt).view(ashape) if ctx.needs_input_grad[0] else None
         db_in = gemm(dy2, wt[Ca:], False, bdt_in).view(bshape) if ctx.needs_input_grad[1] else None
-        if _side_ok(dy2, wdt, bdt):
+        if _side_ok(dy2, wdt, bdt) and _site("cat"):
             dw, dbias = _side_run(lambda: _concat_wgrad(dy2, a2, b2), dy2, a2, b2)
         else:
             dw, dbias = _concat_wgrad(dy2, a2, b2)
@@ -763,7 +783,7 @@ class _LinearResidualFn(torch.autograd.Function):
         rdt, xshape, wdt, bdt = ctx.meta
         dyb = _bf16_of(dy).view(-1, dy.shape[-1])
         dx = gemm(dyb, wt, False, torch.bfloat16).view(xshape)
-        dw, db = wgrad_maybe_side(dyb, x2, wdt, bdt)
+        dw, db = wgrad_maybe_side(dyb, x2, wdt, bdt, site="res")
         return dy.to(rdt), dx, dw.to(wdt), db.to(bdt), None
 
 
@@ -863,8 +883,8 @@ class _MlpFusedFn(torch.autograd.Function):
         dx = torch.empty(M, C, dtype=torch.bfloat16, device=x2.device)
         check(lib().csu_mlp_bwd(M, C, ptr(x2), ptr(dyb), ptr(w1c), ptr(b1f), ptr(w2c), ptr(dh), ptr(g), ptr(dx),
                                 stream_ptr(x2.device)), "csu_mlp_bwd")
-        dw2, db2 = wgrad_maybe_side(dyb, g, w2dt, b2dt)
-        dw1, db1 = wgrad_maybe_side(dh, x2, w1dt, b1dt)
+        dw2, db2 = wgrad_maybe_side(dyb, g, w2dt, b2dt, site="mlp2")
+        dw1, db1 = wgrad_maybe_side(dh, x2, w1dt, b1dt, site="mlp1")
         return dy.to(rdt), dx.view(xshape), dw1.to(w1dt), db1.to(b1dt), dw2.to(w2dt), db2.to(b2dt), None, None
 
 
@@ -1084,7 +1104,7 @@ class _Conv2dFn(torch.autograd.Function):
         def wg():   # (dW (N, C, KH, KW) contiguous, db): also the OIHW re-layout and the unpadding
             w_, b_ = _conv_wgrad(g, xc, dy, dtype_code(dy))
             return w_[..., :C].permute(0, 3, 1, 2).contiguous(), b_
-        if SIDE_CONV and _side_ok(dy, weight.dtype, bdt if has_b else None):
+        if SIDE_CONV and _side_ok(dy, weight.dtype, bdt if has_b else None) and _site("conv"):
             # on the side stream, like the token-Linear weight gradients; the returned grad is
             # contiguous fp32, so autograd steals it without a kernel on this stream
             dw, db = _side_run(wg, xc, dy)
