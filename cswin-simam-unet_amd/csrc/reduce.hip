@@ -113,43 +113,6 @@ Plan plan(long rows, long cols, int V) {
     return p;
 }
 
-// Batched column sums of many [rows][cols] fp32 slab stacks in ONE launch (the deferred split-K
-// weight-gradient reductions of a whole backward pass): the item table travels by value in the
-// kernel arguments (graph-capture safe, no host buffers).  Workgroup = (item, 256 columns): 64
-// column threads x 4 row lanes, 16-B loads, four independent row streams per thread; lanes are
-// combined in lane order in LDS -- a fixed summation order (bitwise reproducible).
-constexpr int CB_MAX = 32;
-struct CBItem { const float* in; float* out; long cols; int rows; int blk0; };
-struct CBBatch { int n; CBItem it[CB_MAX]; };
-
-__global__ __launch_bounds__(NT) void colsum_batch_kernel(CBBatch b) {
-    __shared__ f32x4 red[4][64];
-    const int blk = blockIdx.x;
-    int i = 0;
-    while (i + 1 < b.n && b.it[i + 1].blk0 <= blk) ++i;
-    const CBItem it = b.it[i];
-    const long c = ((long)(blk - it.blk0) * 64 + (threadIdx.x & 63)) * 4;
-    const int rl = threadIdx.x >> 6;
-    f32x4 a0 = {}, a1 = {}, a2 = {}, a3 = {};
-    if (c < it.cols) {
-        int r = rl;
-        for (; r + 12 < it.rows; r += 16) {
-            a0 += *reinterpret_cast<const f32x4*>(it.in + (long)r * it.cols + c);
-            a1 += *reinterpret_cast<const f32x4*>(it.in + (long)(r + 4) * it.cols + c);
-            a2 += *reinterpret_cast<const f32x4*>(it.in + (long)(r + 8) * it.cols + c);
-            a3 += *reinterpret_cast<const f32x4*>(it.in + (long)(r + 12) * it.cols + c);
-        }
-        for (; r < it.rows; r += 4) a0 += *reinterpret_cast<const f32x4*>(it.in + (long)r * it.cols + c);
-    }
-    red[rl][threadIdx.x & 63] = (a0 + a1) + (a2 + a3);
-    __syncthreads();
-    if (rl == 0 && c < it.cols) {
-        const int l = threadIdx.x & 63;
-        const f32x4 v = ((red[0][l] + red[1][l]) + red[2][l]) + red[3][l];
-        *reinterpret_cast<f32x4*>(it.out + c) = v;
-    }
-}
-
 }  // namespace
 
 size_t colsum_workspace(long rows, long cols, int dtype) {
@@ -184,24 +147,4 @@ extern "C" int csu_colsum(long rows, long cols, int dtype, const void* in, float
     if (ws_bytes < colsum_workspace(rows, cols, dtype) || (colsum_workspace(rows, cols, dtype) && !workspace))
         return fail(CSU_E_WORKSPACE, "colsum: workspace too small");
     return colsum_launch(rows, cols, dtype, in, out, (float*)workspace, as_stream(stream));
-}
-
-extern "C" int csu_colsum_batch(const csu_colsum_item* items, int count, void* stream) {
-    if (count < 0 || (count && !items)) return fail(CSU_E_ARG, "colsum_batch: bad args");
-    for (int k = 0; k < count; ++k)
-        if (!items[k].in || !items[k].out || items[k].rows < 1 || items[k].cols < 1 || items[k].cols % 4)
-            return fail(CSU_E_ARG, "colsum_batch: bad item (cols must be a multiple of 4)");
-    for (int k0 = 0; k0 < count; k0 += CB_MAX) {
-        CBBatch b;
-        b.n = count - k0 < CB_MAX ? count - k0 : CB_MAX;
-        int blocks = 0;
-        for (int j = 0; j < b.n; ++j) {
-            const csu_colsum_item& s = items[k0 + j];
-            b.it[j] = CBItem{s.in, s.out, s.cols, s.rows, blocks};
-            blocks += (int)((s.cols + 255) / 256);
-        }
-        colsum_batch_kernel<<<blocks, NT, 0, as_stream(stream)>>>(b);
-        if (int e = check_launch("colsum_batch")) return e;
-    }
-    return 0;
 }

@@ -3,12 +3,22 @@
 //   dW[n][k] = sum_m dY[m][n] * X[m][k],   db[n] = sum_m dY[m][n]       (m = the B*L tokens)
 // This is the backward of every nn.Linear of the model (qkv/proj/fc1/fc2 cswin:185/187/314/323,
 // concat_linear cswin:568/581/592, the CARAFE 1x1 convs cswin:396/399).  M is huge (up to 4M
-// tokens) while N, K <= 2048, so the reduction dim is split: workgroup (n-tile, k-tile, chunk)
-// accumulates a 64x64 tile over its token chunk with v_mfma_f32_32x32x16_bf16 (f32: 32x32x2),
-// both operands staged transposed in LDS ([n][m] / [k][m]) so MFMA fragments are 16-B reads.
-// Partial tiles (and the db partials of the k-tile-0 workgroups) go to a [chunk][N*K + N] slab
-// that one deterministic column-sum pass reduces in chunk order.
+// tokens) while N, K <= 2048: the output has few tiles, so the token (reduction) dimension is split
+// into `chunks` and the chunk partials are summed in a fixed order (bitwise reproducible, no float
+// atomics).
+//
+// bf16 path (wgrad_tile): one workgroup = one TN x TK output tile (TN, TK in {64, 128}) over one
+// token chunk, 4 waves each owning a (TN/2) x (TK/2) block of 32x32x16 MFMA tiles.  Operands are
+// staged row-major ([token][column], XOR-swizzled 16-B chunks) through TWO LDS buffers with a
+// two-step register prefetch (branch-free buffer loads), fragments gathered with the transposing
+// ds_read_b64_tr_b16.  Measured (tools/wgrad_timing.py, tools/wgrad_bench.py): a step is bound by
+// the per-CU load rate (L2 hits ~70 GB/s/CU, the compulsory HBM part slower), not by latency or
+// the MFMAs, so the plan uses about one workgroup per CU with as few chunks as fill the chip; the
+// chunk partials of a tile are combined IN the launch (arrival counter, agent-scope
+// release/acquire, each workgroup sums 1/chunks of the tile in chunk order) -- no reduce launch.
+// fp32 path: 64x64 tiles, v_mfma_f32_32x32x2f32, [chunk][N*K + N] slabs + csu_colsum.
 #include <cstdlib>
+#include <type_traits>
 
 #include "common.hpp"
 
@@ -17,46 +27,49 @@ namespace {
 
 constexpr int NT = 256;
 constexpr int TM = 64;    // tokens per LDS step
-constexpr int TN = 64;    // output tile (n) per workgroup
-constexpr int TK = 64;    // output tile (k) per workgroup
 
-template <typename T> struct WCfg;
-template <> struct WCfg<float> { static constexpr int S = TM + 4; };
+#ifdef WG_TIMING   // debug build only: per-workgroup phase timestamps (100 MHz), read by csu_debug_wgrad_ts
+__device__ unsigned long long wg_ts[4][16384];
+#define WG_STAMP(k) do { if (threadIdx.x < 1 && blockIdx.x < 16384) wg_ts[k][blockIdx.x + threadIdx.x] = __builtin_amdgcn_s_memrealtime(); } while (0)
+__device__ unsigned long long wg_steps[4][64];   // core-clock stamps of the phases of the first 64 steps of block 0
+#define STEP_STAMP(k, i) do { if (blockIdx.x == 0 && threadIdx.x < 1 && (i) < 64) wg_steps[k][(i) + threadIdx.x] = __builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define WG_STAMP(k) do {} while (0)
+#define STEP_STAMP(k, i) do {} while (0)
+#endif
 
-// stage a TM x 64 row-major tile (rows m0.., columns c0..) of a (M, ld) matrix transposed into
-// img[64][S]; rows >= M and columns >= ncols are zero.  Pairs of rows are packed per LDS write.
-template <typename T>
-__device__ __forceinline__ void stage_t(const T* __restrict__ g, long M, int ld, int ncols, long m0, int c0, T* img) {
-    constexpr int V = 16 / sizeof(T);           // elements per 16-B load
-    constexpr int CPR = 64 / V;                 // chunks per row
-    constexpr int S = WCfg<T>::S;
-    for (int it = threadIdx.x; it < (TM / 2) * CPR; it += NT) {
-        const int pr = it / CPR, q = it % CPR;  // row pair, column chunk
+// ------------------------------------------------------------------------------------------
+// fp32 path
+// ------------------------------------------------------------------------------------------
+constexpr int TN32 = 64, TK32 = 64, S32 = TM + 4;
+
+// stage a TM x 64 row-major fp32 tile (rows m0.., columns c0..) transposed into img[64][S32];
+// rows >= M and columns >= ncols are zero.
+__device__ __forceinline__ void stage_t32(const float* __restrict__ g, long M, int ld, int ncols, long m0, int c0,
+                                          float* img) {
+    for (int it = threadIdx.x; it < (TM / 2) * 16; it += NT) {
+        const int pr = it / 16, q = it % 16;  // row pair, 4-column chunk
         const long m = m0 + 2 * pr;
-        const int c = c0 + q * V;
-        float a[V], b[V];
+        const int c = c0 + q * 4;
+        float a[4], b[4];
         const bool cv = c < ncols;
-        if (cv && m < M) { if constexpr (V == 8) load8(g + m * ld + c, a); else load4(g + m * ld + c, a); }
-        else for (int j = 0; j < V; ++j) a[j] = 0.f;
-        if (cv && m + 1 < M) { if constexpr (V == 8) load8(g + (m + 1) * ld + c, b); else load4(g + (m + 1) * ld + c, b); }
-        else for (int j = 0; j < V; ++j) b[j] = 0.f;
+        if (cv && m < M) load4(g + m * ld + c, a); else for (int j = 0; j < 4; ++j) a[j] = 0.f;
+        if (cv && m + 1 < M) load4(g + (m + 1) * ld + c, b); else for (int j = 0; j < 4; ++j) b[j] = 0.f;
 #pragma unroll
-        for (int j = 0; j < V; ++j) {
-            T* p = img + (q * V + j) * S + 2 * pr;
-            p[0] = from_f<T>(a[j]);
-            p[1] = from_f<T>(b[j]);
+        for (int j = 0; j < 4; ++j) {
+            float* p = img + (q * 4 + j) * S32 + 2 * pr;
+            p[0] = a[j];
+            p[1] = b[j];
         }
     }
 }
 
-template <typename T>
-__global__ __launch_bounds__(NT) void wgrad_kernel(long M, int N, int K, long rows_per_chunk, const T* __restrict__ dy,
-                                                   const T* __restrict__ x, float* __restrict__ part) {
-    constexpr int S = WCfg<T>::S;
-    __shared__ __attribute__((aligned(16))) T At[TN * S];   // dY^T tile [n][m]
-    __shared__ __attribute__((aligned(16))) T Bt[TK * S];   // X^T  tile [k][m]
+__global__ __launch_bounds__(NT) void wgrad_f32(long M, int N, int K, long rows_per_chunk, const float* __restrict__ dy,
+                                                const float* __restrict__ x, float* __restrict__ part) {
+    __shared__ __attribute__((aligned(16))) float At[TN32 * S32];   // dY^T tile [n][m]
+    __shared__ __attribute__((aligned(16))) float Bt[TK32 * S32];   // X^T  tile [k][m]
     __shared__ float bred[NT];
-    const int n0 = blockIdx.x * TN, k0 = blockIdx.y * TK;
+    const int n0 = blockIdx.x * TN32, k0 = blockIdx.y * TK32;
     const long m_begin = (long)blockIdx.z * rows_per_chunk;
     const long m_end = min(M, m_begin + rows_per_chunk);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -67,28 +80,19 @@ __global__ __launch_bounds__(NT) void wgrad_kernel(long M, int N, int K, long ro
     float bsum = 0.f;   // db partial of column n0 + (threadIdx.x & 63), rows threadIdx.x>>6 (mod 4)
     for (long m0 = m_begin; m0 < m_end; m0 += TM) {
         __syncthreads();
-        stage_t<T>(dy, m_end, N, N, m0, n0, At);
-        stage_t<T>(x, m_end, K, K, m0, k0, Bt);
+        stage_t32(dy, m_end, N, N, m0, n0, At);
+        stage_t32(x, m_end, K, K, m0, k0, Bt);
         __syncthreads();
-        if (do_bias) {   // column sums of the staged dY^T image: thread -> (n, quarter of m)
+        if (do_bias) {
             const int n = threadIdx.x & 63, qq = threadIdx.x >> 6;
 #pragma unroll
-            for (int j = 0; j < TM / 4; ++j) bsum += to_f(At[n * S + qq * (TM / 4) + j]);
+            for (int j = 0; j < TM / 4; ++j) bsum += At[n * S32 + qq * (TM / 4) + j];
         }
-        if constexpr (sizeof(T) == 2) {
 #pragma unroll
-            for (int s = 0; s < TM / 16; ++s) {
-                const bf16x8 a = *reinterpret_cast<const bf16x8*>(At + (wn + r) * S + 16 * s + 8 * h);
-                const bf16x8 b = *reinterpret_cast<const bf16x8*>(Bt + (wk + r) * S + 16 * s + 8 * h);
-                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc, 0, 0, 0);
-            }
-        } else {
-#pragma unroll
-            for (int t = 0; t < TM / 2; ++t)
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(At[(wn + r) * S + 2 * t + h], Bt[(wk + r) * S + 2 * t + h], acc, 0, 0, 0);
-        }
+        for (int t = 0; t < TM / 2; ++t)
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(At[(wn + r) * S32 + 2 * t + h], Bt[(wk + r) * S32 + 2 * t + h], acc,
+                                                      0, 0, 0);
     }
-    // acc[reg] = dW[n0 + wn + crow(reg, h)][k0 + wk + r]
     const long slab = (long)N * K + N;
     float* out = part + (long)blockIdx.z * slab;
 #pragma unroll
@@ -105,276 +109,410 @@ __global__ __launch_bounds__(NT) void wgrad_kernel(long M, int N, int K, long ro
     }
 }
 
-// bf16 fast path: row-major LDS tiles filled by coalesced 16-B loads (prefetched one step ahead
-// in registers), MFMA fragments gathered with the gfx950 transposing read ds_read_b64_tr_b16
-// (lane 4q+p of a 16-lane group addresses row q, columns 4p..4p+3; lane i receives column i of
-// the 4 rows).  Rows padded by 64 B make the transposed reads of 4 rows bank-conflict free.
-// Tile T x T (T = 64 or 128) per workgroup, each wave (T/2) x (T/2): at T = 128 every fragment
-// feeds two MFMAs and the operand panels are re-read half as often (N/T + K/T passes).
+struct Plan32 {
+    int nt, kt, chunks;
+    long rpc;
+};
+
+Plan32 plan32(long M, int N, int K) {
+    Plan32 p;
+    p.nt = (N + TN32 - 1) / TN32;
+    p.kt = (K + TK32 - 1) / TK32;
+    long want = (1024 + p.nt * p.kt - 1) / (p.nt * p.kt);
+    const long maxc = (M + 511) / 512;
+    if (want > maxc) want = maxc;
+    if (want > 256) want = 256;
+    if (want < 1) want = 1;
+    p.rpc = ((M + want - 1) / want + TM - 1) / TM * TM;
+    p.chunks = (int)((M + p.rpc - 1) / p.rpc);
+    return p;
+}
+
+// ------------------------------------------------------------------------------------------
+// bf16 path
+// ------------------------------------------------------------------------------------------
 typedef short v4s __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ v4s tr_read(const bf16* p) {
     return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(p));
 }
 
-// 32x32x16 operand fragment of columns [c0, c0+32) at k-step rows [16s + 8h, +8) of a [TM][RS] tile
-template <int RS>
+// LDS operand images are [TM tokens][T columns] bf16 with no padding; the 16-B chunks of a row are
+// XOR-swizzled so that a ds_read_b64_tr_b16 (each 32-lane half reads 4 consecutive rows x 64 B)
+// and the ds_write_b128 staging are bank-conflict free: T = 128 (256-B rows, one bank row each):
+// key = 4 (row & 3); T = 64 (two rows per bank row): key = 4 ((row >> 1) & 1).
+template <int T>
+__device__ __forceinline__ int swz(int row, int chunk) {
+    const int key = T == 128 ? 4 * (row & 3) : 4 * ((row >> 1) & 1);
+    return row * T + ((chunk ^ key) << 3);
+}
+
+// 32x32x16 operand fragment of columns [c0, c0+32) at k-step rows [16s + 8h, +8) of a [TM][T]
+// swizzled image: lane 4q+p of a 16-lane group reads row q, columns 4p..4p+3 and receives column
+// (lane & 15) of the 4 rows; two reads (rows q and q+4) give the 8 tokens of the fragment.
+template <int T>
 __device__ __forceinline__ bf16x8 tr_frag(const bf16* img, int c0, int s, int lane) {
     const int grp = lane >> 4, l = lane & 15, q = l >> 2, p = l & 3;
     const int col = c0 + 16 * (grp & 1) + 4 * p;
     const int row = 16 * s + 8 * (grp >> 1) + q;
-    const v4s lo = tr_read(img + row * RS + col);
-    const v4s hi = tr_read(img + (row + 4) * RS + col);
+    const v4s lo = tr_read(img + swz<T>(row, col >> 3) + (col & 7));
+    const v4s hi = tr_read(img + swz<T>(row + 4, col >> 3) + (col & 7));
     const v4s v[2] = {lo, hi};
     bf16x8 out;
     __builtin_memcpy(&out, v, 16);
     return out;
 }
 
-__device__ __forceinline__ float gelu_w(float v) { return gelu_fast(v); }   // common.hpp (A-S 7.1.25)
-
-template <int T, bool GELU_X>
-__global__ __launch_bounds__(NT) void wgrad_bf16_tr(long M, int N, int K, long rows_per_chunk, const bf16* __restrict__ dy,
-                                                   const bf16* __restrict__ x, float* __restrict__ part) {
-    constexpr int RS = T + 32;          // bf16 elements per LDS row (T data + 64 B pad)
-    constexpr int CPR = T / 8;          // 16-B chunks per row
-    constexpr int RPP = NT / CPR;       // rows per pass of the workgroup
-    constexpr int NP = TM / RPP;        // passes (chunks per thread per operand)
-    constexpr int AT = T / 64;          // 32x32 tiles per wave per dim
-    __shared__ __attribute__((aligned(16))) bf16 At[TM * RS];   // dY tile [m][n]
-    __shared__ __attribute__((aligned(16))) bf16 Bt[TM * RS];   // X  tile [m][k]
-    __shared__ float bred[NT][9];
-    // tiles of one token chunk are consecutive logical ids -> one XCD reads the chunk once
-    const int nt = (N + T - 1) / T, kt = (K + T - 1) / T;
-    const long t = xcd_tile(blockIdx.x, gridDim.x);
-    const int chunk = (int)(t / (nt * kt)), tt = (int)(t % (nt * kt));
-    const int n0 = (tt / kt) * T, k0 = (tt % kt) * T;
-    const long m_begin = (long)chunk * rows_per_chunk;
-    const long m_end = min(M, m_begin + rows_per_chunk);
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int r = lane & 31, h = lane >> 5;
-    const int wn = (wave >> 1) * (T / 2), wk = (wave & 1) * (T / 2);
-    const bool do_bias = k0 == 0;
-    const int cg = threadIdx.x % CPR, rr = threadIdx.x / CPR;   // rows rr + RPP i
-    const bool nv = n0 + 8 * cg < N, kv = k0 + 8 * cg < K;
-    bf16x8 ra[NP], rb[NP];
-    float bsum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    auto load = [&](long m0) {
-#pragma unroll
-        for (int i = 0; i < NP; ++i) {
-            const long m = m0 + rr + RPP * i;
-            const bool mv = m < m_end;
-            ra[i] = (mv && nv) ? *reinterpret_cast<const bf16x8*>(dy + m * N + n0 + 8 * cg) : bf16x8{};
-            rb[i] = (mv && kv) ? *reinterpret_cast<const bf16x8*>(x + m * K + k0 + 8 * cg) : bf16x8{};
-        }
-    };
-    f32x16 acc[AT][AT];
-#pragma unroll
-    for (int a = 0; a < AT; ++a)
-#pragma unroll
-        for (int b = 0; b < AT; ++b) acc[a][b] = f32x16{};
-    load(m_begin);
-    for (long m0 = m_begin; m0 < m_end; m0 += TM) {
-        __syncthreads();
-#pragma unroll
-        for (int i = 0; i < NP; ++i) {
-            *reinterpret_cast<bf16x8*>(At + (rr + RPP * i) * RS + 8 * cg) = ra[i];
-            bf16x8 xv = rb[i];
-            if constexpr (GELU_X) {   // X = gelu(h) on the fly (fc2's input, never materialised)
-#pragma unroll
-                for (int j = 0; j < 8; ++j) xv[j] = (bf16)gelu_w((float)xv[j]);
-            }
-            *reinterpret_cast<bf16x8*>(Bt + (rr + RPP * i) * RS + 8 * cg) = xv;
-            if (do_bias)
-#pragma unroll
-                for (int j = 0; j < 8; ++j) bsum[j] += (float)ra[i][j];
-        }
-        __syncthreads();
-        if (m0 + TM < m_end) load(m0 + TM);      // next step's loads fly during the MFMAs
-#pragma unroll
-        for (int s = 0; s < TM / 16; ++s) {
-            bf16x8 fa[AT], fb[AT];
-#pragma unroll
-            for (int a = 0; a < AT; ++a) fa[a] = tr_frag<RS>(At, wn + 32 * a, s, lane);
-#pragma unroll
-            for (int b = 0; b < AT; ++b) fb[b] = tr_frag<RS>(Bt, wk + 32 * b, s, lane);
-#pragma unroll
-            for (int a = 0; a < AT; ++a)
-#pragma unroll
-                for (int b = 0; b < AT; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[a], fb[b], acc[a][b], 0, 0, 0);
-        }
-    }
-    const long slab = (long)N * K + N;
-    float* out = part + (long)chunk * slab;
-#pragma unroll
-    for (int a = 0; a < AT; ++a)
-#pragma unroll
-        for (int b = 0; b < AT; ++b)
-#pragma unroll
-            for (int reg = 0; reg < 16; ++reg) {
-                const int n = n0 + wn + 32 * a + crow(reg, h), k = k0 + wk + 32 * b + r;
-                if (n < N && k < K) out[(long)n * K + k] = acc[a][b][reg];
-            }
-    if (do_bias) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) bred[threadIdx.x][j] = bsum[j];
-        __syncthreads();
-        if (threadIdx.x < T) {
-            const int g = threadIdx.x >> 3, j = threadIdx.x & 7;   // column n0 + 8g + j
-            float sum = 0.f;
-            for (int q = g; q < NT; q += CPR) sum += bred[q][j];
-            if (n0 + 8 * g + j < N) out[(long)N * K + n0 + 8 * g + j] = sum;
-        }
+// f(i + J, set (J + 1) % D, LDS buffer (J + 1) % 2) for J = 0 .. U-1, all indices compile-time
+template <int J, int U, int D, typename F>
+__device__ __forceinline__ void unroll_steps(F& f, int i) {
+    if constexpr (J < U) {
+        f(i + J, std::integral_constant<int, (J + 1) % D>{}, std::integral_constant<int, (J + 1) % 2>{});
+        unroll_steps<J + 1, U, D>(f, i);
     }
 }
 
-struct WPlan {
-    int t, nt, kt, chunks;
+template <int TN, int TK>
+struct TileCfg {
+    static constexpr int CPRA = TN / 8, RPPA = NT / CPRA, NPA = TM / RPPA;   // 16-B chunks per row, rows per pass, passes
+    static constexpr int CPRB = TK / 8, RPPB = NT / CPRB, NPB = TM / RPPB;
+    static constexpr int AN = TN / 64, AK = TK / 64;            // 32x32 MFMA tiles per wave per dim
+    static constexpr int BUF = TM * (TN + TK);                  // bf16 per LDS buffer (A image then B image)
+};
+
+// One TN x TK tile of dW (and db when k0 == 0) over tokens [m_begin, m_end).  chunks == 1: dW / db
+// are written to dst (N*K + N fp32); else the partial tile goes to slab[tile][chunk][TN][TK] and the
+// db partial to bslab[n_tile][chunk][TN], and the workgroups of the tile combine them in-launch.
+// Pipeline per 64-token step i: stage step i+1 from registers into LDS buffer (i+1)&1, issue the
+// global loads of step i+3 into the register set just freed, MFMAs of step i, one barrier -- two
+// steps of MFMA work between a load's issue and its use, 64 KB LDS (T = 128) for 2 workgroups/CU.
+template <int TN, int TK, int D>
+__global__ __launch_bounds__(NT, D > 2 ? 1 : 2) void wgrad_tile(long M, int N, int K, long rpc, int chunks,
+                                                    const bf16* __restrict__ dy, const bf16* __restrict__ x,
+                                                    float* __restrict__ dst, unsigned* __restrict__ cnt,
+                                                    float* __restrict__ slab) {
+    using C = TileCfg<TN, TK>;
+    __shared__ __attribute__((aligned(16))) bf16 lds[2 * C::BUF];
+    WG_STAMP(0);
+    const int nt = (N + TN - 1) / TN, kt = (K + TK - 1) / TK, tiles = nt * kt;
+    // tiles of one token chunk are consecutive logical ids -> one XCD streams the chunk once
+    // (readfirstlane: keep the tile decode in SGPRs -- a buffer resource built from a VGPR base
+    // turns every buffer load into a waterfall loop)
+    const int t = __builtin_amdgcn_readfirstlane((int)xcd_tile(blockIdx.x, gridDim.x));
+    const int chunk = __builtin_amdgcn_readfirstlane(t / tiles), tile = __builtin_amdgcn_readfirstlane(t % tiles);
+    const int ntile = tile / kt;
+    const int n0 = ntile * TN, k0 = (tile % kt) * TK;
+    const long m_begin = (long)chunk * rpc;
+    const long m_end = min(M, m_begin + rpc);
+    const int nsteps = (int)((m_end - m_begin + TM - 1) / TM);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int r = lane & 31, h = lane >> 5;
+    const int wn = (wave >> 1) * (TN / 2), wk = (wave & 1) * (TK / 2);
+    const bool do_bias = k0 == 0;
+    const int cga = threadIdx.x % C::CPRA, rra = threadIdx.x / C::CPRA;   // A: rows rra + RPPA i, chunk cga
+    const int cgb = threadIdx.x % C::CPRB, rrb = threadIdx.x / C::CPRB;
+    const bool nv = n0 + 8 * cga < N, kv = k0 + 8 * cgb < K;
+    bf16x8 ra[D][C::NPA], rb[D][C::NPB];
+    float bsum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    // buffer loads over this chunk's rows: rows past m_end fall outside the resource (read as 0) and
+    // out-of-range columns get an offset past it -- no branches around the loads (a branch per load
+    // makes hipcc wait for each one separately)
+    const __amdgpu_buffer_rsrc_t rsa = buf_rsrc(dy + m_begin * N, (m_end - m_begin) * N * 2);
+    const __amdgpu_buffer_rsrc_t rsb = buf_rsrc(x + m_begin * K, (m_end - m_begin) * K * 2);
+    const unsigned offa = nv ? (unsigned)((rra * N + n0 + 8 * cga) * 2) : kOOB;
+    const unsigned offb = kv ? (unsigned)((rrb * K + k0 + 8 * cgb) * 2) : kOOB;
+    auto load = [&](bf16x8* A, bf16x8* B, int step) {   // rows m_begin + TM*step + ...
+#pragma unroll
+        for (int i = 0; i < C::NPA; ++i) {
+            const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rsa, offa + (unsigned)((TM * step + C::RPPA * i) * N * 2), 0, 0);
+            __builtin_memcpy(&A[i], &v, 16);
+        }
+#pragma unroll
+        for (int i = 0; i < C::NPB; ++i) {
+            const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rsb, offb + (unsigned)((TM * step + C::RPPB * i) * K * 2), 0, 0);
+            __builtin_memcpy(&B[i], &v, 16);
+        }
+    };
+    auto stage = [&](const bf16x8* A, const bf16x8* B, int buf) {
+        bf16* la = lds + buf * C::BUF;
+        bf16* lb = la + TM * TN;
+#pragma unroll
+        for (int i = 0; i < C::NPA; ++i) {
+            *reinterpret_cast<bf16x8*>(la + swz<TN>(rra + C::RPPA * i, cga)) = A[i];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) bsum[j] += (float)A[i][j];   // db partial (used when k0 == 0)
+        }
+#pragma unroll
+        for (int i = 0; i < C::NPB; ++i) *reinterpret_cast<bf16x8*>(lb + swz<TK>(rrb + C::RPPB * i, cgb)) = B[i];
+    };
+    f32x16 acc[C::AN][C::AK];
+#pragma unroll
+    for (int a = 0; a < C::AN; ++a)
+#pragma unroll
+        for (int b = 0; b < C::AK; ++b) acc[a][b] = f32x16{};
+    auto mfmas = [&](int buf) {
+        const bf16* la = lds + buf * C::BUF;
+        const bf16* lb = la + TM * TN;
+#pragma unroll
+        for (int s = 0; s < TM / 16; ++s) {
+            bf16x8 fa[C::AN], fb[C::AK];
+#pragma unroll
+            for (int a = 0; a < C::AN; ++a) fa[a] = tr_frag<TN>(la, wn + 32 * a, s, lane);
+#pragma unroll
+            for (int b = 0; b < C::AK; ++b) fb[b] = tr_frag<TK>(lb, wk + 32 * b, s, lane);
+#pragma unroll
+            for (int a = 0; a < C::AN; ++a)
+#pragma unroll
+                for (int b = 0; b < C::AK; ++b)
+                    acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[a], fb[b], acc[a][b], 0, 0, 0);
+        }
+    };
+    // Register set s % D holds step s, LDS buffer s & 1.  The loop runs a multiple of lcm(D, 2) steps
+    // with no conditions inside (steps past the chunk load zeros from outside the buffer resource):
+    // a conditional load or stage makes hipcc wait for every load in flight.
+#pragma unroll
+    for (int q = 0; q < D; ++q) load(ra[q], rb[q], q);
+    stage(ra[0], rb[0], 0);
+    load(ra[0], rb[0], D);
+    __syncthreads();
+    WG_STAMP(1);
+    auto body = [&](int i, auto Q, auto B) {   // Q: register set of step i + 1, B: its LDS buffer
+        constexpr int q = decltype(Q)::value, nb = decltype(B)::value;
+        STEP_STAMP(0, i);
+        stage(ra[q], rb[q], nb);                             // LDS buffer nb last read in step i - 1
+        STEP_STAMP(1, i);
+        load(ra[q], rb[q], i + 1 + D);
+        mfmas(nb ^ 1);
+        STEP_STAMP(2, i);
+        __syncthreads();
+        STEP_STAMP(3, i);
+    };
+    constexpr int U = D % 2 ? 2 * D : D;                     // unroll: lcm(D, 2)
+    for (int i = 0; i < nsteps; i += U) unroll_steps<0, U, D>(body, i);
+    WG_STAMP(2);
+    // acc[a][b][reg] = dW[n0 + wn + 32a + crow(reg, h)][k0 + wk + 32b + r]
+    if (chunks == 1) {   // buffer stores: out-of-range elements get an offset past the resource (dropped)
+        const __amdgpu_buffer_rsrc_t rd = buf_rsrc(dst, (long)N * K * 4);
+#pragma unroll
+        for (int a = 0; a < C::AN; ++a)
+#pragma unroll
+            for (int b = 0; b < C::AK; ++b)
+#pragma unroll
+                for (int reg = 0; reg < 16; ++reg) {
+                    const int n = n0 + wn + 32 * a + crow(reg, h), k = k0 + wk + 32 * b + r;
+                    const unsigned off = (n < N && k < K) ? (unsigned)(n * K + k) * 4u : kOOB;
+                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[a][b][reg]), rd, off, 0, 0);
+                }
+    } else {
+        float* o = slab + ((long)tile * chunks + chunk) * (TN * TK);
+#pragma unroll
+        for (int a = 0; a < C::AN; ++a)
+#pragma unroll
+            for (int b = 0; b < C::AK; ++b)
+#pragma unroll
+                for (int reg = 0; reg < 16; ++reg)
+                    o[(wn + 32 * a + crow(reg, h)) * TK + wk + 32 * b + r] = acc[a][b][reg];
+    }
+    if (do_bias) {   // column sums of dY: threads with the same cga hold the same 8 columns
+        float* red = reinterpret_cast<float*>(lds);   // [NT][9]: both LDS buffers are free now
+#pragma unroll
+        for (int j = 0; j < 8; ++j) red[threadIdx.x * 9 + j] = bsum[j];
+        __syncthreads();
+        if (threadIdx.x < TN) {
+            const int g = threadIdx.x >> 3, j = threadIdx.x & 7;   // column n0 + 8g + j
+            float sum = 0.f;
+            for (int q = g; q < NT; q += C::CPRA) sum += red[q * 9 + j];
+            if (chunks == 1) {
+                if (n0 + threadIdx.x < N) dst[(long)N * K + n0 + threadIdx.x] = sum;
+            } else {
+                float* bs = slab + (long)tiles * chunks * (TN * TK);
+                bs[((long)ntile * chunks + chunk) * TN + threadIdx.x] = sum;
+            }
+        }
+    }
+    if (chunks > 1) {
+        // In-launch split-K combine (cdna_hip_programming.md section 5 / Guideline 16): publish this
+        // chunk's partial (every wave drains its stores, barrier, ONE agent-scope release, then the
+        // ticket), wait until all `chunks` workgroups of the tile have published (the plan keeps the
+        // grid <= #CUs, so every workgroup is resident; the spin is bounded), ONE agent-scope
+        // acquire, then this workgroup sums its 1/chunks share of the tile over the chunks in chunk
+        // order (fixed order: bitwise reproducible) and writes dW (and, chunk 0 of a k-tile-0 tile,
+        // db).  cnt[tile] was zeroed by the memset in front of the launch.
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        unsigned* red = reinterpret_cast<unsigned*>(lds);   // LDS word: the spin outcome
+        if (threadIdx.x == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_fetch_add(cnt + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            unsigned spins = 0, ok = 1;
+            while (__hip_atomic_load(cnt + tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)chunks) {
+                __builtin_amdgcn_s_sleep(2);
+                if (++spins > (1u << 22)) {   // a partner never arrived: flag it, never hang
+                    __hip_atomic_store(cnt + tiles, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    ok = 0;
+                    break;
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            red[0] = ok;
+        }
+        __syncthreads();
+        constexpr int E4 = TN * TK / 4;                        // float4s per tile
+        const int per = (E4 + chunks - 1) / chunks;
+        const f32x4* src = reinterpret_cast<const f32x4*>(slab + (long)tile * chunks * (TN * TK));
+        const __amdgpu_buffer_rsrc_t rd = buf_rsrc(dst, (long)N * K * 4);
+        for (int e4 = chunk * per + threadIdx.x; e4 < min(E4, (chunk + 1) * per); e4 += NT) {
+            f32x4 v = src[e4];
+            for (int c = 1; c < chunks; ++c) v += src[(long)c * E4 + e4];
+            const int nl = (e4 * 4) / TK, kl = (e4 * 4) % TK;
+            const int n = n0 + nl, k = k0 + kl;
+            const unsigned off = (n < N && k < K) ? (unsigned)(n * K + k) * 4u : kOOB;
+            u32x4 w = {__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])};
+            __builtin_amdgcn_raw_buffer_store_b128(w, rd, off, 0, 0);
+        }
+        if (do_bias && chunk == 0 && threadIdx.x < TN && n0 + threadIdx.x < N) {
+            const float* bs = slab + (long)tiles * chunks * (TN * TK) + (long)ntile * chunks * TN + threadIdx.x;
+            float v = bs[0];
+            for (int c = 1; c < chunks; ++c) v += bs[(long)c * TN];
+            dst[(long)N * K + n0 + threadIdx.x] = v;
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    WG_STAMP(3);
+}
+
+int num_cus() {
+    static int v = 0;
+    if (!v) {
+        int dev = 0, n = 0;
+        if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess
+            && n > 0)
+            v = n;
+        else
+            v = 256;
+    }
+    return v;
+}
+
+struct Plan {
+    int tn, tk, nt, kt, chunks, depth;
     long rpc;
 };
 
-// bf16 tiles: 128 x 128 when both N and K allow it (half the operand re-reads of 64 x 64), else
-// 64 x 64; fp32 path 64 x 64.  ~1024 workgroups, >= 512 tokens per chunk.
-int env_int(const char* name, int dflt) {
-    const char* e = getenv(name);
-    return e ? atoi(e) : dflt;
-}
-int wgrad_tile_env() {   // CSU_WGRAD_T=64|128 forces the tile (A/B comparisons)
-    static int v = env_int("CSU_WGRAD_T", 0);
-    return v;
-}
-int wgrad_target_env() {   // CSU_WGRAD_WGS: target workgroup count of the split-K plan
-    static int v = env_int("CSU_WGRAD_WGS", 1024);
-    return v;
-}
-
-int wgrad_mintok_env() {   // CSU_WGRAD_MINTOK: minimum tokens per split-K chunk
-    static int v = env_int("CSU_WGRAD_MINTOK", 512);
-    return v;
-}
-
-WPlan wplan(long M, int N, int K, bool bf16_path) {
-    WPlan p;
-    const int te = wgrad_tile_env();
-    p.t = (bf16_path && N >= 128 && K >= 128 && te != 64) ? 128 : 64;
-    p.nt = (N + p.t - 1) / p.t;
-    p.kt = (K + p.t - 1) / p.t;
-    const long target = wgrad_target_env();
-    long want = (target + p.nt * p.kt - 1) / (p.nt * p.kt);
-    const long mt = wgrad_mintok_env();
-    const long maxc = (M + mt - 1) / mt;        // >= mt tokens per chunk
-    if (want > maxc) want = maxc;
-    if (want > 256) want = 256;
+// Tiles 128 wide where the dimension is a multiple of 128 (fewer operand re-reads), else 64.
+// Chunks: about one workgroup per CU over all tiles, >= 256 tokens each -- the fewest split-K
+// partials that still fill the chip -- and never more workgroups than CUs when split (the in-launch
+// combine needs every workgroup of a tile resident).  tn / tk / chunks > 0 override
+// (csu_linear_wgrad_tuned; a forced split is still capped at one workgroup per CU).
+Plan make_plan(long M, int N, int K, int tn, int tk, int chunks) {
+    Plan p;
+    p.tn = tn > 0 ? tn : (N % 128 == 0 ? 128 : 64);
+    p.tk = tk > 0 ? tk : (K % 128 == 0 ? 128 : 64);
+    p.nt = (N + p.tn - 1) / p.tn;
+    p.kt = (K + p.tk - 1) / p.tk;
+    const long tiles = (long)p.nt * p.kt;
+    long want = chunks;
+    if (want <= 0) {
+        want = (num_cus() + tiles - 1) / tiles;
+        const long maxc = (M + 255) / 256;
+        if (want > maxc) want = maxc;
+    }
+    const long cap = num_cus() / tiles;                    // resident-grid limit of a split launch
+    if (want > cap) want = cap;
     if (want < 1) want = 1;
-    p.chunks = (int)want;
-    p.rpc = ((M + p.chunks - 1) / p.chunks + TM - 1) / TM * TM;
+    p.rpc = ((M + want - 1) / want + TM - 1) / TM * TM;
     p.chunks = (int)((M + p.rpc - 1) / p.rpc);
+    p.depth = 2;
     return p;
 }
 
-}  // namespace
+// workspace: [tiles + 1 counters (the last: spin-timeout flag), padded to 256 B][partial tiles
+// [tile][chunk][TN][TK]][db partials [n_tile][chunk][TN]]
+size_t cnt_bytes(const Plan& p) { return ((size_t)(p.nt * p.kt + 1) * 4 + 255) / 256 * 256; }
+size_t plan_bytes(const Plan& p) {
+    if (p.chunks == 1) return 0;
+    return cnt_bytes(p) + ((size_t)p.nt * p.kt * p.tn * p.tk + (size_t)p.nt * p.tn) * p.chunks * sizeof(float);
+}
 
-int wgrad5_launch(int cfg, long M, int N, int K, long rpc, int chunks, const bf16* dy, const bf16* x, float* part,
-                  hipStream_t st);
-bool wgrad4_ok(long M, int N, int K);
-size_t wgrad4_workspace(long M, int N, int K);
-int wgrad4_run(long M, int N, int K, const bf16* dy, const bf16* x, float* dw_db, void* ws, hipStream_t st);
+template <int TN, int TK>
+void launch_tile(const Plan& p, unsigned grid, long M, int N, int K, const bf16* dy, const bf16* x, float* dst,
+                 unsigned* cnt, float* slab, hipStream_t st) {
+    if (p.depth >= 4) wgrad_tile<TN, TK, 4><<<grid, NT, 0, st>>>(M, N, K, p.rpc, p.chunks, dy, x, dst, cnt, slab);
+    else if (p.depth == 3) wgrad_tile<TN, TK, 3><<<grid, NT, 0, st>>>(M, N, K, p.rpc, p.chunks, dy, x, dst, cnt, slab);
+    else wgrad_tile<TN, TK, 2><<<grid, NT, 0, st>>>(M, N, K, p.rpc, p.chunks, dy, x, dst, cnt, slab);
+}
+
+int run_bf16(const Plan& p, long M, int N, int K, const bf16* dy, const bf16* x, float* dst, void* ws, hipStream_t st) {
+    const unsigned grid = (unsigned)((long)p.nt * p.kt * p.chunks);
+    unsigned* cnt = (unsigned*)ws;
+    float* slab = (float*)((char*)ws + cnt_bytes(p));
+    if (p.chunks > 1) {   // zero the arrival counters in front of every launch (a memset node when captured)
+        const hipError_t e = hipMemsetAsync(cnt, 0, cnt_bytes(p), st);
+        if (e != hipSuccess) return fail((int)e, "linear_wgrad: counter memset");
+    } else {
+        cnt = nullptr;
+        slab = nullptr;
+    }
+    if (p.tn == 128 && p.tk == 128) launch_tile<128, 128>(p, grid, M, N, K, dy, x, dst, cnt, slab, st);
+    else if (p.tn == 128 && p.tk == 64) launch_tile<128, 64>(p, grid, M, N, K, dy, x, dst, cnt, slab, st);
+    else if (p.tn == 64 && p.tk == 128) launch_tile<64, 128>(p, grid, M, N, K, dy, x, dst, cnt, slab, st);
+    else if (p.tn == 64 && p.tk == 64) launch_tile<64, 64>(p, grid, M, N, K, dy, x, dst, cnt, slab, st);
+    else return fail(CSU_E_ARG, "linear_wgrad: tile must be 64 or 128");
+    return check_launch("linear_wgrad");
+}
+
+}  // namespace
 }  // namespace csu
 
 using namespace csu;
 
-// CSU_WGRAD4=1 routes the bf16 path to wgrad4 (LDS-DMA + transposing reads).  Off by default: on
-// the 512x512 step shapes it measured 0-40 % slower than the register-staged kernel below (both are
-// bound by re-reading the operand panels once per output tile, tools/linear_probe.py).
-static bool use_wgrad4() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("CSU_WGRAD4");
-        v = e && e[0] == '1';
-    }
-    return v == 1;
-}
-
-// CSU_WGRAD5=<cfg> selects the deep LDS-DMA pipeline kernel (wgrad5.hip) for the bf16 128-tile
-// plans; -1 = the register-staged kernel.
-static int wgrad5_cfg() {
-    static int v = -2;
-    if (v == -2) {
-        const char* e = getenv("CSU_WGRAD5");
-        v = e ? atoi(e) : -1;
-    }
-    return v;
-}
-
-extern "C" size_t csu_linear_wgrad_workspace(long M, int N, int K) {
-    const long slab = (long)N * K + N;
-    size_t a = 0;
-    for (int bf = 0; bf < 2; ++bf) {   // the dtype is not an argument: the larger of both plans
-        const WPlan p = wplan(M, N, K, bf == 1);
-        const size_t w = (size_t)p.chunks * slab * sizeof(float) + colsum_workspace(p.chunks, slab, CSU_F32);
-        a = w > a ? w : a;
-    }
-    const size_t b = wgrad4_ok(M, N, K) ? wgrad4_workspace(M, N, K) : 0;
+extern "C" size_t csu_linear_wgrad_tuned_workspace(long M, int N, int K, int tn, int tk, int chunks) {
+    const Plan32 q = plan32(M, N, K);
+    const size_t a = (size_t)q.chunks * ((size_t)N * K + N) * sizeof(float) +
+                     colsum_workspace(q.chunks, (long)N * K + N, CSU_F32);
+    const size_t b = plan_bytes(make_plan(M, N, K, tn, tk, chunks));
     return a > b ? a : b;
 }
 
-extern "C" int csu_linear_wgrad_ex(long M, int N, int K, int dtype, const void* dy, const void* x, int x_gelu,
-                                   float* dw_db, void* workspace, size_t ws_bytes, void* stream);
-
-extern "C" int csu_linear_wgrad(long M, int N, int K, int dtype, const void* dy, const void* x, float* dw_db,
-                                void* workspace, size_t ws_bytes, void* stream) {
-    return csu_linear_wgrad_ex(M, N, K, dtype, dy, x, 0, dw_db, workspace, ws_bytes, stream);
+extern "C" size_t csu_linear_wgrad_workspace(long M, int N, int K) {
+    return csu_linear_wgrad_tuned_workspace(M, N, K, 0, 0, 0);
 }
 
-// split-K partial slabs only (the reduction is left to csu_colsum_batch)
-static int wgrad_partials(const WPlan& p, long M, int N, int K, int dtype, const void* dy, const void* x, int x_gelu,
-                          float* part, hipStream_t st) {
-    const dim3 grid(p.nt, p.kt, p.chunks);
-    const dim3 grid1((unsigned)(p.nt * p.kt * p.chunks));
-    const bf16* dyb = (const bf16*)dy;
-    const bf16* xb = (const bf16*)x;
-    if (x_gelu && dtype != CSU_BF16) return fail(CSU_E_UNSUPPORTED, "linear_wgrad: GELU prologue is bf16-only");
-    if (dtype == CSU_BF16 && p.t == 128 && !x_gelu && wgrad5_cfg() >= 0) {
-        if (int e = wgrad5_launch(wgrad5_cfg(), M, N, K, p.rpc, p.chunks, dyb, xb, part, st)) return e;
-    } else if (dtype == CSU_BF16 && p.t == 128 && x_gelu) wgrad_bf16_tr<128, true><<<grid1, NT, 0, st>>>(M, N, K, p.rpc, dyb, xb, part);
-    else if (dtype == CSU_BF16 && p.t == 128) wgrad_bf16_tr<128, false><<<grid1, NT, 0, st>>>(M, N, K, p.rpc, dyb, xb, part);
-    else if (dtype == CSU_BF16 && x_gelu) wgrad_bf16_tr<64, true><<<grid1, NT, 0, st>>>(M, N, K, p.rpc, dyb, xb, part);
-    else if (dtype == CSU_BF16) wgrad_bf16_tr<64, false><<<grid1, NT, 0, st>>>(M, N, K, p.rpc, dyb, xb, part);
-    else if (dtype == CSU_F32)
-        wgrad_kernel<float><<<grid, NT, 0, st>>>(M, N, K, p.rpc, (const float*)dy, (const float*)x, part);
-    else
-        return fail(CSU_E_ARG, "linear_wgrad: bad dtype");
-    return check_launch("linear_wgrad");
-}
-
-extern "C" size_t csu_linear_wgrad_partial_bytes(long M, int N, int K, int dtype) {
-    const WPlan p = wplan(M, N, K, dtype == CSU_BF16);
-    return (size_t)p.chunks * ((size_t)N * K + N) * sizeof(float);
-}
-
-extern "C" int csu_linear_wgrad_partial(long M, int N, int K, int dtype, const void* dy, const void* x, int x_gelu,
-                                        float* slabs, size_t slab_bytes, int* chunks, void* stream) {
-    if (M < 1 || N < 1 || K < 1 || !dy || !x || !slabs || !chunks) return fail(CSU_E_ARG, "linear_wgrad_partial: bad args");
-    const int V = dtype == CSU_BF16 ? 8 : 4;
-    if (N % V || K % V) return fail(CSU_E_ARG, "linear_wgrad_partial: N and K must be multiples of 16 bytes");
-    if (slab_bytes < csu_linear_wgrad_partial_bytes(M, N, K, dtype)) return fail(CSU_E_WORKSPACE, "linear_wgrad_partial: slabs");
-    const WPlan p = wplan(M, N, K, dtype == CSU_BF16);
-    *chunks = p.chunks;
-    return wgrad_partials(p, M, N, K, dtype, dy, x, x_gelu, slabs, as_stream(stream));
-}
-
-extern "C" int csu_linear_wgrad_ex(long M, int N, int K, int dtype, const void* dy, const void* x, int x_gelu,
-                                   float* dw_db, void* workspace, size_t ws_bytes, void* stream) {
+extern "C" int csu_linear_wgrad_tuned(long M, int N, int K, int dtype, const void* dy, const void* x, float* dw_db,
+                                      void* workspace, size_t ws_bytes, int tn, int tk, int chunks, void* stream) {
     if (M < 1 || N < 1 || K < 1 || !dy || !x || !dw_db) return fail(CSU_E_ARG, "linear_wgrad: bad args");
     const int V = dtype == CSU_BF16 ? 8 : 4;
     if (N % V || K % V) return fail(CSU_E_ARG, "linear_wgrad: N and K must be multiples of 16 bytes");
-    if (!workspace || ws_bytes < csu_linear_wgrad_workspace(M, N, K)) return fail(CSU_E_WORKSPACE, "linear_wgrad: workspace");
+    if (ws_bytes < csu_linear_wgrad_tuned_workspace(M, N, K, tn, tk, chunks) ||
+        (!workspace && csu_linear_wgrad_tuned_workspace(M, N, K, tn, tk, chunks)))
+        return fail(CSU_E_WORKSPACE, "linear_wgrad: workspace");
     hipStream_t st = as_stream(stream);
-    if (dtype == CSU_BF16 && !x_gelu && use_wgrad4() && wgrad4_ok(M, N, K))
-        return wgrad4_run(M, N, K, (const bf16*)dy, (const bf16*)x, dw_db, workspace, st);
-    const WPlan p = wplan(M, N, K, dtype == CSU_BF16);
-    float* part = (float*)workspace;
+    if (dtype == CSU_BF16) {
+        if ((tn && tn != 64 && tn != 128) || (tk && tk != 64 && tk != 128)) return fail(CSU_E_ARG, "linear_wgrad: tile");
+        const Plan p = make_plan(M, N, K, tn, tk, chunks);
+        return run_bf16(p, M, N, K, (const bf16*)dy, (const bf16*)x, dw_db, workspace, st);
+    }
+    if (dtype != CSU_F32) return fail(CSU_E_ARG, "linear_wgrad: bad dtype");
+    const Plan32 q = plan32(M, N, K);
     const long slab = (long)N * K + N;
-    if (int e = wgrad_partials(p, M, N, K, dtype, dy, x, x_gelu, part, st)) return e;
-    return colsum_launch(p.chunks, slab, CSU_F32, part, dw_db, part + (size_t)p.chunks * slab, st);
+    float* part = (float*)workspace;
+    wgrad_f32<<<dim3(q.nt, q.kt, q.chunks), NT, 0, st>>>(M, N, K, q.rpc, (const float*)dy, (const float*)x, part);
+    if (int e = check_launch("linear_wgrad f32")) return e;
+    return colsum_launch(q.chunks, slab, CSU_F32, part, dw_db, part + (size_t)q.chunks * slab, st);
 }
+
+extern "C" int csu_linear_wgrad(long M, int N, int K, int dtype, const void* dy, const void* x, float* dw_db,
+                                void* workspace, size_t ws_bytes, void* stream) {
+    return csu_linear_wgrad_tuned(M, N, K, dtype, dy, x, dw_db, workspace, ws_bytes, 0, 0, 0, stream);
+}
+
+#ifdef WG_TIMING
+extern "C" int csu_debug_wgrad_ts(unsigned long long* host) {
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(csu::wg_ts), sizeof(csu::wg_ts), 0, hipMemcpyDeviceToHost);
+}
+extern "C" int csu_debug_wgrad_steps(unsigned long long* host) {
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(csu::wg_steps), sizeof(csu::wg_steps), 0, hipMemcpyDeviceToHost);
+}
+#endif

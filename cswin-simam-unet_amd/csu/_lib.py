@@ -38,11 +38,6 @@ class GemmDesc(ctypes.Structure):
                 ("ldc", c_int32), ("out_dtype", c_int32), ("cfg", c_int32), ("_pad", c_int32)]
 
 
-class ColsumItem(ctypes.Structure):
-    _fields_ = [("in_", ctypes.c_void_p), ("out", ctypes.c_void_p), ("cols", ctypes.c_int64), ("rows", ctypes.c_int32),
-                ("pad_", ctypes.c_int32)]
-
-
 class ConvGeom(ctypes.Structure):
     _fields_ = [(n, c_int32) for n in ("B", "H", "W", "C", "OH", "OW", "N", "KH", "KW", "stride", "pad")]
 
@@ -83,8 +78,11 @@ _SIGS = {
     "csu_linear_wgrad_workspace": (c_size_t, [ctypes.c_long, ctypes.c_int, ctypes.c_int]),
     "csu_linear_wgrad": (ctypes.c_int, [ctypes.c_long, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_void_p, c_void_p,
                                         c_void_p, c_void_p, c_size_t, c_void_p]),
-    "csu_linear_wgrad_ex": (ctypes.c_int, [ctypes.c_long, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_void_p, c_void_p,
-                                           ctypes.c_int, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "csu_linear_wgrad_tuned_workspace": (c_size_t, [ctypes.c_long, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                    ctypes.c_int]),
+    "csu_linear_wgrad_tuned": (ctypes.c_int, [ctypes.c_long, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_void_p, c_void_p,
+                                              c_void_p, c_void_p, c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                              c_void_p]),
     "csu_gemm": (ctypes.c_int, [ctypes.c_long, ctypes.c_int, ctypes.c_int, c_void_p, ctypes.c_int, c_void_p, ctypes.c_int,
                                 ctypes.c_int, ctypes.c_int, c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_int,
                                 ctypes.c_int, c_void_p]),
@@ -94,10 +92,6 @@ _SIGS = {
                                       c_float, c_void_p, c_float, c_void_p]),
     "csu_gemm_ex": (ctypes.c_int, [ctypes.POINTER(GemmDesc), c_void_p]),
     "csu_mlp_supported": (ctypes.c_int, [ctypes.c_int]),
-    "csu_linear_wgrad_partial_bytes": (c_size_t, [ctypes.c_long, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
-    "csu_linear_wgrad_partial": (ctypes.c_int, [ctypes.c_long, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_void_p, c_void_p,
-                                                ctypes.c_int, c_void_p, c_size_t, ctypes.POINTER(ctypes.c_int), c_void_p]),
-    "csu_colsum_batch": (ctypes.c_int, [ctypes.POINTER(ColsumItem), ctypes.c_int, c_void_p]),
     "csu_layernorm_param_reduce": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
     "csu_stripe_lepe_wgrad": (ctypes.c_int, [ctypes.POINTER(StripeArgs), ctypes.c_int, c_void_p, c_void_p, c_void_p, c_size_t,
                                              c_void_p]),

@@ -113,22 +113,6 @@ class _StripeAttnFn(torch.autograd.Function):
         dqkv = torch.empty_like(qkv)
         delta = torch.empty_like(lse)
         L = lib()
-        if SIDE_AUX and _side_ok(qkv, *ctx.lepe_dtypes):
-            # LePE weight gradient on the side stream, concurrent with the dQ / dK / dV kernels
-            def lepe_grads():
-                dws = [torch.empty_like(w) for w in ws]
-                dbs = [torch.empty_like(b) for b in bs]
-                a2 = geom.args(B, ws, bs, dws, dbs)
-                nb2 = L.csu_stripe_attn_bwd_workspace(ctypes.byref(a2))
-                work2 = torch.empty(max(nb2, 16), dtype=torch.uint8, device=qkv.device)
-                check(L.csu_stripe_lepe_wgrad(ctypes.byref(a2), dtype_code(qkv), ptr(qkv), ptr(dout), ptr(work2), nb2,
-                                              stream_ptr(qkv.device)), "csu_stripe_lepe_wgrad")
-                return dws + dbs
-            grads = _side_run(lepe_grads, qkv, dout)
-            a = geom.args(B, ws, bs)        # NULL LePE gradients: the main call skips them
-            check(L.csu_stripe_attn_bwd(ctypes.byref(a), dtype_code(qkv), ptr(qkv), ptr(out), ptr(dout), ptr(lse),
-                                        ptr(delta), ptr(dqkv), None, 0, stream_ptr(qkv.device)), "csu_stripe_attn_bwd")
-            return (dqkv, None, *grads)
         dws = [torch.empty_like(w) for w in ws]
         dbs = [torch.empty_like(b) for b in bs]
         a = geom.args(B, ws, bs, dws, dbs)
@@ -242,19 +226,10 @@ class _LayerNormForkFn(torch.autograd.Function):
         L = lib()
         nbytes = L.csu_layernorm_bwd_workspace(rows, C)
         work = torch.empty(max(nbytes, 16), dtype=torch.uint8, device=x.device)
-        side = SIDE_AUX and _side_ok(x, *ctx.pdtypes)
-        dgb = None if side else torch.empty(2 * C, dtype=torch.float32, device=x.device)
+        dgb = torch.empty(2 * C, dtype=torch.float32, device=x.device)
         check(L.csu_layernorm_bwd_ex(rows, C, dtype_code(x), ptr(x), ptr(w), ptr(mean), ptr(rstd), dtype_code(dy), ptr(dy),
-                                     ptr(dres_k), ptr(dx), ptr(dxb), None if side else ptr(dgb[:C]),
-                                     None if side else ptr(dgb[C:]), ptr(work), nbytes, stream_ptr(x.device)),
-              "csu_layernorm_bwd_ex")
-        if side:   # dgamma / dbeta reduction off the input-gradient chain
-            def reduce():
-                out = torch.empty(2 * C, dtype=torch.float32, device=x.device)
-                check(L.csu_layernorm_param_reduce(rows, C, ptr(work), ptr(out[:C]), ptr(out[C:]), stream_ptr(x.device)),
-                      "csu_layernorm_param_reduce")
-                return out
-            dgb = _side_run(reduce, work)
+                                     ptr(dres_k), ptr(dx), ptr(dxb), ptr(dgb[:C]), ptr(dgb[C:]), ptr(work), nbytes,
+                                     stream_ptr(x.device)), "csu_layernorm_bwd_ex")
         if dres is not None and not fp32:    # non-fp32 residual stream: plain add (not on the bf16 path)
             dx = dx + dres.to(dx.dtype)
         if dxb is not None:
@@ -450,48 +425,59 @@ def gemm(a2: torch.Tensor, b: torch.Tensor, b_trans: bool, out_dtype, bias=None,
 
 # ---------------------------------------------------------------------------------------------
 # Weight gradients on a side stream.  dW = dY^T X of a Linear is off the backward critical path
-# (nothing in the rest of backward reads it), and each wgrad/colsum launch alone leaves most CUs
-# waiting on memory latency, so it runs on a second HIP stream overlapped with the input-gradient
-# chain.  Fork: the side stream waits on the launching stream; inputs are record_stream'ed; the
-# launching stream waits on every side event at the end of backward (autograd final callback),
-# before the optimizer or any user code can read .grad.  Off under multi-rank DDP (its reducer
-# reads gradients from hooks during backward).  On by default since the latency-bound kernels of
-# the fused Mlp / attention backward left room for it: +0.6 % on the graphed 512x512 step
-# (978 -> 984 img/s, two interleaved A/B pairs, tools/ab_env.sh); CSU_SIDE_WGRAD=0 disables.
+# (nothing in the rest of backward reads it), so in eager steps it runs on a second HIP stream
+# overlapped with the input-gradient chain.  Fork: the side stream waits on the launching stream;
+# inputs are record_stream'ed.  Join: the launching stream waits on every side event at the end of
+# backward (autograd final callback), before the optimizer or any user code can read .grad.
+#
+# The returned gradient is handed to autograd on the launching stream while the side kernel may
+# still be writing it, so the side stream is only used when nothing reads it before the join:
+# AccumulateGrad then just steals the tensor.  That holds when the parameter has no .grad yet
+# (zero_grad(set_to_none=True)), no tensor hooks, and no post-accumulate hooks other than
+# csu.dist.GradAllReduce's (which order their reads after side_stream()).  Gradient accumulation
+# (an existing .grad: AccumulateGrad adds in place on the launching stream), DDP and user hooks run
+# the weight gradient inline.  Graph capture runs inline too (CSU_SIDE_IN_GRAPH=1 keeps the side
+# stream under capture; DESIGN.md §6 has the determinism record).  CSU_SIDE_WGRAD=0 disables.
 # ---------------------------------------------------------------------------------------------
 SIDE_WGRAD = _os.environ.get("CSU_SIDE_WGRAD", "1") == "1"
-# CSU_SIDE_AUX=1: also the LePE weight gradient and the LayerNorm dgamma/dbeta reduction.  Off:
-# measured 1-2 % slower (969-979 vs 988 img/s, two A/B pairs) -- the extra graph branches delay
-# the critical-path kernels more than the overlap saves
-SIDE_AUX = _os.environ.get("CSU_SIDE_AUX", "0") == "1"
-# CSU_SIDE_IN_GRAPH=1: keep the side stream inside a HIP-graph capture.  Off by default: replays of
-# a captured step with side-stream weight gradients are not bitwise reproducible (tools/det_graph.py:
-# run-to-run loss differences ~1e-6 after a few steps, 0 with this off or with an immediate join;
-# eager steps with the side stream are reproducible, tools/det_eager.py) -- a missing cross-stream
-# dependency in the captured graph that is not yet understood, so the graph runs single-stream.
 SIDE_IN_GRAPH = _os.environ.get("CSU_SIDE_IN_GRAPH", "0") == "1"
 # CSU_PAD_CHANNELS=0: convolutions of inputs with C % 8 != 0 (the 3-channel image) without the zero
 # channel padding (per-element gathers; A/B)
 PAD_CHANNELS = _os.environ.get("CSU_PAD_CHANNELS", "1") == "1"
-# CSU_SIDE_CONV=0: convolution weight gradients inline on the launching stream
-SIDE_CONV = _os.environ.get("CSU_SIDE_CONV", "1") == "1"
 _SIDE_STREAMS = {}
 _SIDE_PENDING = []
 _SIDE_JOIN_QUEUED = [False]
+# set by csu.dist.GradAllReduce: its hooks order their reads after the side stream (side_stream()),
+# so side-stream weight gradients stay on under multi-rank training with it (not with DDP)
+_DIST_SAFE = [False]
 
 
-def _side_ok(t: torch.Tensor, *dtypes) -> bool:
+def _leaf(p):
+    while p is not None and getattr(p, "_base", None) is not None:
+        p = p._base
+    return p
+
+
+def _param_safe(p) -> bool:
+    """True when no reader of p.grad can run before the end-of-backward join (see above)."""
+    p = _leaf(p)
+    if p is None:
+        return True
+    if p.grad is not None or p._backward_hooks:
+        return False
+    hooks = getattr(p, "_post_accumulate_grad_hooks", None)
+    return not hooks or _DIST_SAFE[0]
+
+
+def _side_ok(t: torch.Tensor, *dtypes, params=()) -> bool:
     if not (SIDE_WGRAD and t.is_cuda) or any(d not in (None, torch.float32) for d in dtypes):
         return False
     if not SIDE_IN_GRAPH and torch.cuda.is_current_stream_capturing():
         return False
+    if not all(_param_safe(p) for p in params):
+        return False
     dist = torch.distributed
     return _DIST_SAFE[0] or not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1)
-
-
-# set by csu.dist.GradAllReduce: its hooks order their reads after the side stream (side_stream()),
-# so side-stream weight gradients stay on under multi-rank training with it (not with DDP)
-_DIST_SAFE = [False]
 
 
 def side_stream(device) -> Optional["torch.cuda.Stream"]:
@@ -499,59 +485,12 @@ def side_stream(device) -> Optional["torch.cuda.Stream"]:
     return _SIDE_STREAMS.get(device)
 
 
-# CSU_DEFER_WGRAD_REDUCE=1 (side-stream mode): every weight gradient leaves its split-K partial slabs
-# and one csu_colsum_batch launch per CSU_DEFER_BATCH weights (the rest at the end of backward)
-# reduces them, instead of a colsum launch (or two) per weight.  Off: measured 1.5-2 % slower on the
-# graphed step (979-986 vs 993-1001 img/s, batches of 4 and 8; all-at-the-end 2 % slower) --
-# the per-weight reductions overlap the backward better than a few large ones
-DEFER_REDUCE = _os.environ.get("CSU_DEFER_WGRAD_REDUCE", "0") == "1"
-_DEFERRED = []   # (slabs, out, rows, cols) pending on the side stream
-DEFER_BATCH = int(_os.environ.get("CSU_DEFER_BATCH", "8"))
-
-
 def join_side_streams():
-    """Flush the deferred slab reductions on the side stream, then make each launching stream wait
-    for the side-stream weight gradients it forked."""
-    if _DEFERRED:
-        dev = _DEFERRED[0][0].device
-        side = _SIDE_STREAMS[dev]
-        with torch.cuda.stream(side):
-            _flush_deferred()
-            ev = torch.cuda.Event()
-            ev.record(side)
-        for main in {m for m, _ in _SIDE_PENDING}:
-            main.wait_event(ev)
+    """Make each launching stream wait for the side-stream weight gradients it forked."""
     for main, ev in _SIDE_PENDING:
         main.wait_event(ev)
     _SIDE_PENDING.clear()
     _SIDE_JOIN_QUEUED[0] = False
-
-
-def _flush_deferred():
-    """One csu_colsum_batch launch (current stream = the side stream) over the pending slabs."""
-    dev = _DEFERRED[0][0].device
-    items = (_lib.ColsumItem * len(_DEFERRED))()
-    for i, (slabs, out, rows, cols) in enumerate(_DEFERRED):
-        items[i].in_, items[i].out, items[i].cols, items[i].rows = slabs.data_ptr(), out.data_ptr(), cols, rows
-    check(lib().csu_colsum_batch(items, len(_DEFERRED), stream_ptr(dev)), "csu_colsum_batch")
-    _DEFERRED.clear()
-
-
-def linear_wgrad_deferred(dy2: torch.Tensor, x2: torch.Tensor):
-    """(dW, db) views of an output the end-of-backward csu_colsum_batch fills (side stream only)."""
-    M, N = dy2.shape
-    K = x2.shape[1]
-    L = lib()
-    nb = L.csu_linear_wgrad_partial_bytes(M, N, K, dtype_code(dy2))
-    slabs = torch.empty(max(nb // 4, 4), dtype=torch.float32, device=dy2.device)
-    out = torch.empty(N * K + N, dtype=torch.float32, device=dy2.device)
-    ch = ctypes.c_int(0)
-    check(L.csu_linear_wgrad_partial(M, N, K, dtype_code(dy2), ptr(dy2), ptr(x2), 0, ptr(slabs), nb, ctypes.byref(ch),
-                                     stream_ptr(dy2.device)), "csu_linear_wgrad_partial")
-    _DEFERRED.append((slabs, out, ch.value, N * K + N))
-    if len(_DEFERRED) >= DEFER_BATCH:   # reduce in batches during backward (overlapped), not all at the end
-        _flush_deferred()
-    return out[:N * K].view(N, K), out[N * K:]
 
 
 def _side_run(fn, *inputs):
@@ -567,8 +506,6 @@ def _side_run(fn, *inputs):
         t.record_stream(side)
     ev = torch.cuda.Event()
     ev.record(side)
-    if _os.environ.get("CSU_SIDE_JOIN_NOW") == "1":   # debug: join right away (no overlap)
-        main.wait_event(ev)
     _SIDE_PENDING.append((main, ev))
     if not _SIDE_JOIN_QUEUED[0]:
         torch.autograd.Variable._execution_engine.queue_callback(join_side_streams)
@@ -576,32 +513,11 @@ def _side_run(fn, *inputs):
     return out
 
 
-_SIDE_SITES = _os.environ.get("CSU_SIDE_SITES", "")   # debug: comma list of call sites allowed on the side stream
-
-
-def _site(name):
-    return not _SIDE_SITES or name in _SIDE_SITES.split(",")
-
-
-def wgrad_maybe_side(dy2: torch.Tensor, x2: torch.Tensor, wdt, bdt, site="lin"):
-    """linear_wgrad on the side stream when allowed (fp32 master weights), else inline."""
-    if _side_ok(dy2, wdt, bdt) and _site(site):
-        return _side_run(lambda: (linear_wgrad_deferred if DEFER_REDUCE else linear_wgrad)(dy2, x2), dy2, x2)
+def wgrad_maybe_side(dy2: torch.Tensor, x2: torch.Tensor, wdt, bdt, params=()):
+    """linear_wgrad on the side stream when allowed (fp32 master weights, see above), else inline."""
+    if _side_ok(dy2, wdt, bdt, params=params):
+        return _side_run(lambda: linear_wgrad(dy2, x2), dy2, x2)
     return linear_wgrad(dy2, x2)
-
-
-def linear_wgrad_gelu(dy2: torch.Tensor, h2: torch.Tensor):
-    """(dW, db) of a Linear whose input is gelu(h2), with gelu applied on the fly (bf16)."""
-    M, N = dy2.shape
-    K = h2.shape[1]
-    out = torch.empty(N * K + N, dtype=torch.float32, device=dy2.device)
-    L = lib()
-    n = L.csu_linear_wgrad_workspace(M, N, K)
-    work = torch.empty(max(n, 16), dtype=torch.uint8, device=dy2.device)
-    check(L.csu_linear_wgrad_ex(M, N, K, dtype_code(dy2), ptr(dy2), ptr(h2), 1, ptr(out), ptr(work), n,
-                                stream_ptr(dy2.device)), "csu_linear_wgrad_ex")
-    return out[:N * K].view(N, K), out[N * K:]
-
 
 
 # csu_gemm_ex (fused bias / GELU / GELU' / residual token GEMM) for the bf16 nn.Linear forward and
@@ -642,6 +558,7 @@ class _LinearFn(torch.autograd.Function):
             y = torch.nn.functional.linear(xc, wc, bc)
         ctx.save_for_backward(xc, wt if ctx.fast else wc)
         ctx.meta = (x.dtype, weight.dtype, None if bias is None else bias.dtype)
+        ctx.params = (weight, bias)
         return y
 
     @staticmethod
@@ -668,7 +585,7 @@ class _LinearFn(torch.autograd.Function):
         vec = 16 // dy2.element_size()
         if N % vec == 0 and K % vec == 0 and dy2.dtype in (torch.float32, torch.bfloat16):
             dwf, dbf = wgrad_maybe_side(dy2, xc.reshape(-1, K), wdt if ctx.needs_input_grad[1] else None,
-                                        bdt if ctx.needs_input_grad[2] else None)
+                                        bdt if ctx.needs_input_grad[2] else None, params=ctx.params)
             if ctx.needs_input_grad[1]:
                 dw = dwf.to(wdt)
             if bdt is not None and ctx.needs_input_grad[2]:
@@ -733,6 +650,7 @@ class _ConcatLinearFn(torch.autograd.Function):
         y = gemm(b2, wc[:, Ca:], False, torch.float32, resid=y1)
         ctx.save_for_backward(a2, b2, _weight_t(weight, wc))
         ctx.meta = (a.shape, b.shape, a.dtype, b.dtype, weight.dtype, bias.dtype)
+        ctx.params = (weight, bias)
         return y.view(*a.shape[:-1], N)
 
     @staticmethod
@@ -743,7 +661,7 @@ class _ConcatLinearFn(torch.autograd.Function):
         dy2 = _bf16_of(dy).reshape(-1, dy.shape[-1]).contiguous()
         da = gemm(dy2, wt[:Ca], False, adt).view(ashape) if ctx.needs_input_grad[0] else None
         db_in = gemm(dy2, wt[Ca:], False, bdt_in).view(bshape) if ctx.needs_input_grad[1] else None
-        if _side_ok(dy2, wdt, bdt) and _site("cat"):
+        if _side_ok(dy2, wdt, bdt, params=ctx.params):
             dw, dbias = _side_run(lambda: _concat_wgrad(dy2, a2, b2), dy2, a2, b2)
         else:
             dw, dbias = _concat_wgrad(dy2, a2, b2)
@@ -775,6 +693,7 @@ class _LinearResidualFn(torch.autograd.Function):
         y = gemm(x2, wc, False, torch.float32, bias=bias.detach().float().contiguous(), resid=res2)
         ctx.save_for_backward(x2, _weight_t(weight, wc))
         ctx.meta = (res.dtype, x.shape, weight.dtype, bias.dtype)
+        ctx.params = (weight, bias)
         return y.view(res.shape)
 
     @staticmethod
@@ -783,7 +702,7 @@ class _LinearResidualFn(torch.autograd.Function):
         rdt, xshape, wdt, bdt = ctx.meta
         dyb = _bf16_of(dy).view(-1, dy.shape[-1])
         dx = gemm(dyb, wt, False, torch.bfloat16).view(xshape)
-        dw, db = wgrad_maybe_side(dyb, x2, wdt, bdt, site="res")
+        dw, db = wgrad_maybe_side(dyb, x2, wdt, bdt, params=ctx.params)
         return dy.to(rdt), dx, dw.to(wdt), db.to(bdt), None
 
 
@@ -800,6 +719,7 @@ class _MlpResidualFn(torch.autograd.Function):
         y = gemm(g, w2c, False, torch.float32, bias=b2.detach().float().contiguous(), resid=res2)
         ctx.save_for_backward(x2, h, g, _weight_t(w1, w1c), _weight_t(w2, w2c))
         ctx.meta = (res.dtype, x.shape, w1.dtype, b1.dtype, w2.dtype, b2.dtype)
+        ctx.params = (w1, b1, w2, b2)
         return y.view(res.shape)
 
     @staticmethod
@@ -808,9 +728,9 @@ class _MlpResidualFn(torch.autograd.Function):
         rdt, xshape, w1dt, b1dt, w2dt, b2dt = ctx.meta
         dyb = _bf16_of(dy).view(-1, dy.shape[-1])
         dh = gemm(dyb, w2t, False, torch.bfloat16, gelu_aux=h)         # (dY W2) * gelu'(h)
-        dw2, db2 = wgrad_maybe_side(dyb, g, w2dt, b2dt)
+        dw2, db2 = wgrad_maybe_side(dyb, g, w2dt, b2dt, params=ctx.params[2:])
         dx = gemm(dh, w1t, False, torch.bfloat16).view(xshape)
-        dw1, db1 = wgrad_maybe_side(dh, x2, w1dt, b1dt)
+        dw1, db1 = wgrad_maybe_side(dh, x2, w1dt, b1dt, params=ctx.params[:2])
         return dy.to(rdt), dx, dw1.to(w1dt), db1.to(b1dt), dw2.to(w2dt), db2.to(b2dt), None, None
 
 
@@ -832,15 +752,8 @@ def linear_residual(res, x, weight, bias):
 
 class _MlpFusedFn(torch.autograd.Function):
     """res + fc2(gelu(fc1(x))) (Mlp cswin:180-196 + residual cswin:368) in ONE csu_mlp_fwd launch
-    (the 4C hidden layer never reaches HBM as gelu(h)).
-
-    Backward, two forms (CSU_MLP_BWD):
-      "fused" (default): one csu_mlp_bwd launch recomputes h and writes dh, g = gelu(h) and dx;
-      "gemm": the forward also writes h = fc1(x) (csu_mlp_fwd_ex); dh = (dY W2) * gelu'(h) is one
-        gemm4 launch with the GELU' epilogue, dx = dh W1 a second, dW2 = dY^T gelu(h) with gelu
-        applied while staging h (linear_wgrad_gelu), dW1 = dh^T x.  Faster in isolation
-        (tools/mlp_probe.py) but 4 % slower on the graphed step (941 vs 983 img/s, A/B r01aa):
-        the h write and the extra launches cost more than the fused kernel's latency."""
+    (the 4C hidden layer never reaches HBM).  Backward: one csu_mlp_bwd launch recomputes h and
+    writes dh, g = gelu(h) and dx; then the two weight gradients."""
 
     @staticmethod
     def forward(ctx, res, x, w1, b1, w2, b2, w1c, w2c):
@@ -849,32 +762,16 @@ class _MlpFusedFn(torch.autograd.Function):
         x2 = x.reshape(-1, C).contiguous()
         b1f = b1.detach().float().contiguous()
         y = torch.empty_like(res2)
-        h = torch.empty(x2.shape[0], 4 * C, dtype=torch.bfloat16, device=x2.device) if MLP_BWD == "gemm" else None
-        check(lib().csu_mlp_fwd_ex(x2.shape[0], C, ptr(x2), ptr(w1c), ptr(b1f), ptr(w2c),
-                                   ptr(b2.detach().float().contiguous()), ptr(res2), ptr(y), ptr(h) if h is not None else None,
-                                   stream_ptr(x2.device)), "csu_mlp_fwd_ex")
-        if h is not None:
-            ctx.save_for_backward(x2, h, _weight_t(w1, w1c), _weight_t(w2, w2c))
-        else:
-            ctx.save_for_backward(x2, w1c, b1f, w2c)
-        ctx.meta = (res.dtype, x.shape, w1.dtype, b1.dtype, w2.dtype, b2.dtype, h is not None)
+        check(lib().csu_mlp_fwd(x2.shape[0], C, ptr(x2), ptr(w1c), ptr(b1f), ptr(w2c), ptr(b2.detach().float().contiguous()),
+                                ptr(res2), ptr(y), stream_ptr(x2.device)), "csu_mlp_fwd")
+        ctx.save_for_backward(x2, w1c, b1f, w2c)
+        ctx.meta = (res.dtype, x.shape, w1.dtype, b1.dtype, w2.dtype, b2.dtype)
+        ctx.params = (w1, b1, w2, b2)
         return y.view(res.shape)
 
     @staticmethod
     def backward(ctx, dy):
-        rdt, xshape, w1dt, b1dt, w2dt, b2dt, gemm_form = ctx.meta
-        if gemm_form:
-            x2, h, w1t, w2t = ctx.saved_tensors
-            M, C = x2.shape
-            dyb = _bf16_of(dy).view(-1, C)
-            dh = gemm(dyb, w2t, False, torch.bfloat16, gelu_aux=h)         # (dY W2) * gelu'(h)
-            if _side_ok(dyb, w2dt, b2dt):
-                dw2, db2 = _side_run(lambda: linear_wgrad_gelu(dyb, h), dyb, h)
-            else:
-                dw2, db2 = linear_wgrad_gelu(dyb, h)
-            dx = gemm(dh, w1t, False, torch.bfloat16)
-            dw1, db1 = wgrad_maybe_side(dh, x2, w1dt, b1dt)
-            return dy.to(rdt), dx.view(xshape), dw1.to(w1dt), db1.to(b1dt), dw2.to(w2dt), db2.to(b2dt), None, None
+        rdt, xshape, w1dt, b1dt, w2dt, b2dt = ctx.meta
         x2, w1c, b1f, w2c = ctx.saved_tensors
         M, C = x2.shape
         dyb = _bf16_of(dy).view(-1, C)
@@ -883,14 +780,13 @@ class _MlpFusedFn(torch.autograd.Function):
         dx = torch.empty(M, C, dtype=torch.bfloat16, device=x2.device)
         check(lib().csu_mlp_bwd(M, C, ptr(x2), ptr(dyb), ptr(w1c), ptr(b1f), ptr(w2c), ptr(dh), ptr(g), ptr(dx),
                                 stream_ptr(x2.device)), "csu_mlp_bwd")
-        dw2, db2 = wgrad_maybe_side(dyb, g, w2dt, b2dt, site="mlp2")
-        dw1, db1 = wgrad_maybe_side(dh, x2, w1dt, b1dt, site="mlp1")
+        dw2, db2 = wgrad_maybe_side(dyb, g, w2dt, b2dt, params=ctx.params[2:])
+        dw1, db1 = wgrad_maybe_side(dh, x2, w1dt, b1dt, params=ctx.params[:2])
         return dy.to(rdt), dx.view(xshape), dw1.to(w1dt), db1.to(b1dt), dw2.to(w2dt), db2.to(b2dt), None, None
 
 
-# CSU_FUSED_MLP=0 selects the two-GEMM Mlp (A/B comparisons); CSU_MLP_BWD=gemm|fused the backward form
+# CSU_FUSED_MLP=0 selects the two-GEMM Mlp (A/B comparisons)
 FUSED_MLP = _os.environ.get("CSU_FUSED_MLP", "1") == "1"
-MLP_BWD = _os.environ.get("CSU_MLP_BWD", "fused")
 
 
 def mlp_residual(res, x, fc1: torch.nn.Linear, fc2: torch.nn.Linear):
@@ -1075,6 +971,7 @@ class _Conv2dFn(torch.autograd.Function):
                                    stream_ptr(x.device)), "csu_conv2d_fwd")
         ctx.save_for_backward(xc, weight)
         ctx.w_ihwo = cached[1] if cached else None   # refreshed only by the next forward's cast
+        ctx.bias = bias
         ctx.conf = (stride, pad, cd, x.dtype, bias is not None, None if bias is None else bias.dtype)
         return y
 
@@ -1104,7 +1001,7 @@ class _Conv2dFn(torch.autograd.Function):
         def wg():   # (dW (N, C, KH, KW) contiguous, db): also the OIHW re-layout and the unpadding
             w_, b_ = _conv_wgrad(g, xc, dy, dtype_code(dy))
             return w_[..., :C].permute(0, 3, 1, 2).contiguous(), b_
-        if SIDE_CONV and _side_ok(dy, weight.dtype, bdt if has_b else None) and _site("conv"):
+        if _side_ok(dy, weight.dtype, bdt if has_b else None, params=(weight, ctx.bias)):
             # on the side stream, like the token-Linear weight gradients; the returned grad is
             # contiguous fp32, so autograd steals it without a kernel on this stream
             dw, db = _side_run(wg, xc, dy)

@@ -32,10 +32,13 @@ class FusedAdamW(torch.optim.Optimizer):
                         for gi, g in enumerate(self.param_groups)} if torch.cuda.is_available() else {}
 
     def _table(self, gi, items, device):
-        """Device item table for the current (param, grad) buffers, rebuilt when they change.
-        Eager: a pageable (host-synchronous) copy.  Under HIP-graph capture: an async copy from a
-        pinned buffer reserved for that capture (pinned memory cannot be allocated while
-        capturing); the graph's copy node re-reads it on every replay, so it is never rewritten."""
+        """Device item table for the current (param, grad) buffers, rebuilt when they change
+        (e.g. every step under zero_grad(set_to_none=True) when the allocator hands out other grad
+        buffers).  Eager: an asynchronous copy from a fresh pinned buffer (no host sync; the
+        caching host allocator keeps it alive until the copy has run).  Under HIP-graph capture:
+        an async copy from a pinned buffer reserved for that capture (pinned memory cannot be
+        allocated while capturing); the graph's copy node re-reads it on every replay, so it is
+        never rewritten."""
         key = (gi,) + tuple(v for it in items for v in it[:4])
         t = self._tables.get(gi)
         if t is not None and t[0] == key:
@@ -56,8 +59,10 @@ class FusedAdamW(torch.optim.Optimizer):
             dev = torch.empty(raw.size, dtype=torch.uint8, device=device)
             dev.copy_(host[:raw.size], non_blocking=True)
         else:
-            host = None
-            dev = torch.from_numpy(raw.copy()).to(device)
+            host = torch.empty(raw.size, dtype=torch.uint8, pin_memory=True)
+            host.numpy()[:] = raw
+            dev = torch.empty(raw.size, dtype=torch.uint8, device=device)
+            dev.copy_(host, non_blocking=True)
         t = (key, host, dev, len(items), c0)
         self._tables[gi] = t
         return t
@@ -69,7 +74,7 @@ class FusedAdamW(torch.optim.Optimizer):
             with torch.enable_grad():
                 loss = closure()
         for gi, group in enumerate(self.param_groups):
-            items, dev = [], None
+            items, dev, keep = [], None, []
             for p in group["params"]:
                 if p.grad is None:
                     continue
@@ -81,6 +86,7 @@ class FusedAdamW(torch.optim.Optimizer):
                     st["exp_avg"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
                     st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
                 g = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
+                keep.append(g)          # a contiguous temporary must outlive the launch below
                 if not p.is_contiguous():
                     raise RuntimeError("FusedAdamW: contiguous parameters only")
                 items.append((p.data_ptr(), g.data_ptr(), st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr(),
@@ -108,6 +114,23 @@ class FusedAdamW(torch.optim.Optimizer):
                                        float(group["eps"]), float(group["weight_decay"]), gs["step"].data_ptr(), 0.0,
                                        stream_ptr(dev)), "csu_adamw_step")
         return loss
+
+    def state_dict(self):
+        """torch.optim.AdamW format with a separate ``step`` tensor per parameter (the live state
+        shares one device step tensor per group), so the checkpoint also loads into
+        torch.optim.AdamW, whose per-parameter steps would otherwise advance once per parameter."""
+        sd = super().state_dict()
+        for st in sd["state"].values():
+            if isinstance(st.get("step"), torch.Tensor):
+                st["step"] = st["step"].detach().clone()
+        return sd
+
+    def load_state_dict(self, state_dict):
+        """Load an AdamW / FusedAdamW state; the device step / lr of every group and the pointer
+        tables are rebuilt from it on the next step()."""
+        super().load_state_dict(state_dict)
+        self._gstate = {}
+        self._tables = {}
 
     def sync_lr(self):
         """Copy the host lr of every group into its device tensor (capturable groups read it at

@@ -10,8 +10,6 @@ from __future__ import annotations
 
 from typing import Dict, List, Optional
 
-import time
-
 import torch
 import torch.distributed as dist
 import torch.nn.functional as F
@@ -78,25 +76,34 @@ def _epoch_means(stats: List[torch.Tensor], smooth: float = 1e-6):
     return float(s[:, 0].mean()), float(dice.mean()), float(iou.mean())
 
 
-def evaluate_model(model, data_loader, criterion, device):
-    """eval mode, no grad; mean over batches of (loss, Dice, IoU) (cswin:712-747)."""
+def _autocast(device, amp_dtype):
+    dt = torch.device(device).type if not isinstance(device, torch.device) else device.type
+    return torch.autocast(dt, dtype=amp_dtype or torch.float32, enabled=amp_dtype is not None)
+
+
+def evaluate_model(model, data_loader, criterion, device, amp_dtype=None):
+    """eval mode, no grad; mean over batches of (loss, Dice, IoU) (cswin:712-747).  ``amp_dtype``
+    (not in the reference): run the forward under autocast (e.g. torch.bfloat16)."""
     model.eval()
     stats = []
     with torch.no_grad():
         for images, masks in data_loader:
             images = images.to(device, non_blocking=True)
             masks = masks.to(device, non_blocking=True)
-            outputs = model(images)
+            with _autocast(images.device, amp_dtype):
+                outputs = model(images)
             stats.append(_step_stats(criterion(outputs, masks), outputs, masks))
     return _epoch_means(stats)
 
 
-def train_step(model, images, masks, criterion, optimizer, reducer=None):
+def train_step(model, images, masks, criterion, optimizer, reducer=None, amp_dtype=None):
     """One reference step (cswin:779-794): zero_grad, forward, loss, backward, optimizer step.
     ``reducer``: a ``csu.dist.GradAllReduce`` averaging the gradients across ranks (instead of DDP).
+    ``amp_dtype``: forward under autocast (the loss stays fp32).
     Returns the device tensor of per-step sums (loss, sum(p*t), sum(p), sum(t)) -- no host sync."""
     optimizer.zero_grad(set_to_none=True)
-    outputs = model(images)
+    with _autocast(images.device, amp_dtype):
+        outputs = model(images)
     loss = criterion(outputs, masks)
     loss.backward()
     if reducer is not None:
@@ -107,12 +114,24 @@ def train_step(model, images, masks, criterion, optimizer, reducer=None):
 
 
 def train_model(model, train_loader, test_loader, criterion, optimizer, scheduler, device, num_epochs=100,
-                verbose: bool = True) -> Dict[str, List[float]]:
-    """Epoch loop with per-epoch history and ReduceLROnPlateau on the test loss (cswin:751-841)."""
+                verbose: bool = True, checkpoint_path: Optional[str] = None,
+                resume_from: Optional[str] = None, amp_dtype=None) -> Dict[str, List[float]]:
+    """Epoch loop with per-epoch history and ReduceLROnPlateau on the test loss (cswin:751-841).
+
+    Beyond the reference: ``checkpoint_path`` writes a resumable checkpoint (model, optimizer,
+    scheduler, epoch, history; csu.report.save_checkpoint) after every epoch, and ``resume_from``
+    restores one and continues from the epoch after it (the history then covers all epochs);
+    ``amp_dtype`` runs the forward passes under autocast (the reference trains in fp32)."""
     history = {"train_loss": [], "train_dice": [], "train_iou": [], "test_loss": [], "test_dice": [], "test_iou": [],
                "learning_rates": []}
     rank0 = not (dist.is_available() and dist.is_initialized()) or dist.get_rank() == 0
-    for epoch in range(num_epochs):
+    start = 0
+    if resume_from is not None:
+        from .report import load_checkpoint
+        start, past = load_checkpoint(resume_from, model, optimizer, scheduler, map_location=device)
+        for k in history:
+            history[k] = list(past.get(k, []))
+    for epoch in range(start, num_epochs):
         model.train()
         sampler = getattr(train_loader, "sampler", None)
         if hasattr(sampler, "set_epoch"):
@@ -124,14 +143,19 @@ def train_model(model, train_loader, test_loader, criterion, optimizer, schedule
         for images, masks in it:
             images = images.to(device, non_blocking=True)
             masks = masks.to(device, non_blocking=True)
-            stats.append(train_step(model, images, masks, criterion, optimizer))
+            stats.append(train_step(model, images, masks, criterion, optimizer, amp_dtype=amp_dtype))
         train_loss, train_dice, train_iou = _epoch_means(stats)
-        test_loss, test_dice, test_iou = evaluate_model(model, test_loader, criterion, device)
+        test_loss, test_dice, test_iou = evaluate_model(model, test_loader, criterion, device, amp_dtype=amp_dtype)
         if scheduler is not None:
             scheduler.step(test_loss)
+            if hasattr(optimizer, "sync_lr"):   # FusedAdamW: the device lr a captured step reads
+                optimizer.sync_lr()
         current_lr = optimizer.param_groups[0]["lr"]
         for k, v in zip(history, (train_loss, train_dice, train_iou, test_loss, test_dice, test_iou, current_lr)):
             history[k].append(v)
+        if checkpoint_path is not None:
+            from .report import save_checkpoint
+            save_checkpoint(checkpoint_path, model, optimizer, scheduler, epoch + 1, history)
         if verbose and rank0:
             print(f'\n{"=" * 70}\nEpoch {epoch + 1}/{num_epochs}:')
             print(f"  [TRAIN] Loss: {train_loss:.4f} | Dice: {train_dice:.4f} | IoU: {train_iou:.4f}")
@@ -178,11 +202,15 @@ class GraphedTrainStep:
         torch.cuda.synchronize()
         mode = "global"
         if reducer is not None:
-            # the RCCL process group's watchdog thread polls the events of finished collectives
-            # (hipEventQuery); under a global-mode capture that call fails in the other thread and
-            # aborts the process.  Let it retire the warm-up's work items, and capture in
-            # thread-local mode so its polling stays legal.
-            time.sleep(0.5)
+            # The RCCL process group's watchdog thread polls the events of its collectives
+            # (hipEventQuery) concurrently with this thread.  A global-mode capture makes that query
+            # illegal in every thread (hipErrorStreamCaptureUnsupported -> the watchdog aborts the
+            # process); a thread-local capture restricts only this thread, so the polling stays
+            # legal whatever the watchdog's timing.  The barrier lines the ranks up so no rank's
+            # capture overlaps another rank's warm-up collectives.
+            if dist.is_available() and dist.is_initialized():
+                dist.barrier()
+                torch.cuda.synchronize()
             mode = "thread_local"
         self.graph = torch.cuda.CUDAGraph()
         self.opt.zero_grad(set_to_none=True)

@@ -174,31 +174,18 @@ int csu_colsum(long rows, long cols, int dtype, const void* in, float* out, void
 /* ---------------------------------------------------------------------------------------
  * Linear weight + bias gradient over M token rows (backward of every nn.Linear on tokens:
  * cswin:185/187/314/323/568/581/592 and the CARAFE 1x1 convs cswin:396/399).
- * dy (M, N), x (M, K) row-major, dtype in; dw_db fp32 [N*K + N] = dW (N, K) then db (N).
- * Split-K over M with MFMA tiles + a deterministic reduction.  N, K multiples of 16 bytes.
+ * dy (M, N), x (M, K) row-major, dtype in; dw_db fp32 [N*K + N] = dW (N, K) then db (N), written.
+ * Split-K over M with MFMA tiles; the chunk partials are summed in a fixed order (bitwise
+ * reproducible).  N, K multiples of 16 bytes.
  * ------------------------------------------------------------------------------------- */
-/* Deferred form: the split-K partial slabs ([*chunks][N*K + N] fp32) of csu_linear_wgrad_ex go to
- * `slabs` (csu_linear_wgrad_partial_bytes) and their reduction is left to one csu_colsum_batch
- * call for many weights at the end of the backward pass. */
-size_t csu_linear_wgrad_partial_bytes(long M, int N, int K, int dtype);
-int csu_linear_wgrad_partial(long M, int N, int K, int dtype, const void* dy, const void* x, int x_gelu,
-                             float* slabs, size_t slab_bytes, int* chunks, void* stream);
-typedef struct {
-    const float* in;    /* [rows][cols] fp32 */
-    float* out;         /* [cols] fp32: out[c] = sum_r in[r][c], fixed order */
-    int64_t cols;       /* multiple of 4 */
-    int32_t rows;
-    int32_t pad_;
-} csu_colsum_item;
-int csu_colsum_batch(const csu_colsum_item* items, int count, void* stream);
-
 size_t csu_linear_wgrad_workspace(long M, int N, int K);
 int csu_linear_wgrad(long M, int N, int K, int dtype, const void* dy, const void* x, float* dw_db,
                      void* workspace, size_t ws_bytes, void* stream);
-/* Same with x replaced by gelu(x) on the fly (x_gelu = 1; bf16 only): dW of fc2 from fc1's
- * pre-activation h (Mlp cswin:191-194) without materialising gelu(h). */
-int csu_linear_wgrad_ex(long M, int N, int K, int dtype, const void* dy, const void* x, int x_gelu,
-                        float* dw_db, void* workspace, size_t ws_bytes, void* stream);
+/* Same with the plan forced (tuning / tests): bf16 output tile tn x tk (64 or 128; 0 = auto) and
+ * the number of token chunks (0 = auto).  The fp32 path ignores them. */
+size_t csu_linear_wgrad_tuned_workspace(long M, int N, int K, int tn, int tk, int chunks);
+int csu_linear_wgrad_tuned(long M, int N, int K, int dtype, const void* dy, const void* x, float* dw_db,
+                           void* workspace, size_t ws_bytes, int tn, int tk, int chunks, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * Token GEMM, bf16 operands, fp32 accumulation, fused prologue/epilogue (nn.Linear of

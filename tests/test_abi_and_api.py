@@ -87,6 +87,18 @@ def test_geometry_validation_mirrors_reference():
         ops.StripeGeometry(16, 64, 2, [(16, 7, 0)], 0.1)
 
 
+@pytest.mark.parametrize("img,depth", [(512, [1, 2, 9, 1]), (512, [2, 4, 32, 2]), (1024, [1, 2, 9, 1]), (256, [1, 2, 9, 1])])
+def test_default_split_rejected_where_reference_crashes(img, depth):
+    """The reference default split_size [1,2,7,7] (cswin:494) cannot run at 256/512/1024: the
+    stage-3 resolution img/16 is not a multiple of 7 and img2windows' view fails (cswin:204, SURVEY
+    0.4) -- including BASELINE config 4 (deep, 512).  csu rejects the model at construction with the
+    same cause; [1,2,8,8] builds (no device work happens in __init__)."""
+    from csu.model import CSWinTransformer
+    with pytest.raises(ValueError, match="not divisible"):
+        CSWinTransformer(img_size=img, depth=depth, split_size=[1, 2, 7, 7])
+    CSWinTransformer(img_size=img, depth=depth, split_size=[1, 2, 8, 8])
+
+
 def test_dice_iou_metrics_match_reference_fixture(golden_dir):
     import numpy as np
     from csu.train import bce_loss, dice_coefficient, iou_score

@@ -458,39 +458,59 @@ def test_mlp_fused_kernels_vs_fp64(C, M):
     assert_close(dx, hg.grad @ W1, torch.bfloat16)
 
 
-def test_colsum_batch_and_deferred_wgrad():
-    """csu_colsum_batch (the end-of-backward reduction of every deferred split-K weight gradient):
-    fixed-order column sums of many slab stacks in one launch == fp64 sums, bitwise reproducible;
-    linear_wgrad_deferred + the side-stream join == linear_wgrad."""
-    import ctypes
-    from csu import ops, _lib
-    from csu._lib import check, lib, stream_ptr
+@pytest.mark.parametrize("M,N,K", [(16384, 1024, 256), (4099, 192, 64), (262144, 64, 128), (4096, 2048, 512), (700, 32, 128)])
+@pytest.mark.parametrize("tn,tk,chunks", [(64, 64, 1), (128, 128, 0), (128, 64, 5), (64, 128, 37), (0, 0, 0), (128, 128, 300)])
+def test_linear_wgrad_plans(M, N, K, tn, tk, chunks):
+    """csu_linear_wgrad_tuned: every output tile (64/128 x 64/128) and split-K chunking (1 chunk =
+    direct write; >1 = tile-local slabs + the fixed-order reduce) == fp64, bitwise reproducible."""
+    from csu._lib import check, lib, ptr, stream_ptr
+    d = dev()
+    g = torch.Generator(device=d).manual_seed(M + N + K + tn + chunks)
+    dy = torch.randn(M, N, device=d, generator=g).bfloat16()
+    x = torch.randn(M, K, device=d, generator=g).bfloat16()
+    L = lib()
+    outs = []
+    for _ in range(2):
+        n = L.csu_linear_wgrad_tuned_workspace(M, N, K, tn, tk, chunks)
+        ws = torch.full((max(n, 16) // 4,), float("nan"), device=d)      # poisoned workspace
+        out = torch.full((N * K + N,), float("nan"), device=d)
+        check(L.csu_linear_wgrad_tuned(M, N, K, 1, ptr(dy), ptr(x), ptr(out), ptr(ws), n, tn, tk, chunks, stream_ptr(d)),
+              "linear_wgrad_tuned")
+        outs.append(out)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+    ref_w = dy.double().t() @ x.double()
+    ref_b = dy.double().sum(0)
+    dw, db = outs[0][:N * K].view(N, K), outs[0][N * K:]
+    assert float((dw.double() - ref_w).abs().max()) <= 1e-2 * max(float(ref_w.abs().max()), M ** 0.5)
+    assert float((db.double() - ref_b).abs().max()) <= 1e-2 * max(float(ref_b.abs().max()), M ** 0.5)
+
+
+def test_side_stream_wgrad_with_gradient_accumulation():
+    """Two backward passes without zeroing (gradient accumulation: AccumulateGrad adds in place on
+    the launching stream) give bitwise the same .grad with the side stream on and off: a parameter
+    that already holds a .grad takes its weight gradient inline (ops._param_safe)."""
+    from csu import ops
     d = dev()
     torch.manual_seed(0)
-    shapes = [(1, 4), (3, 8), (32, 65792), (7, 1028), (256, 4096)] * 8   # 40 items: two launches of <= 32
-    ins = [torch.randn(r, c, device=d) for r, c in shapes]
-    outs = [torch.empty(c, device=d) for _, c in shapes]
-    outs2 = [torch.empty(c, device=d) for _, c in shapes]
-    for o in (outs, outs2):
-        items = (_lib.ColsumItem * len(ins))()
-        for i, (t, z) in enumerate(zip(ins, o)):
-            items[i].in_, items[i].out, items[i].cols, items[i].rows = t.data_ptr(), z.data_ptr(), t.shape[1], t.shape[0]
-        check(lib().csu_colsum_batch(items, len(ins), stream_ptr(d)), "colsum_batch")
-    torch.cuda.synchronize()
-    for t, a, b in zip(ins, outs, outs2):
+    res = {}
+    for side in (True, False):
+        old = ops.SIDE_WGRAD
+        ops.SIDE_WGRAD = side
+        try:
+            torch.manual_seed(1)
+            fc1, fc2 = torch.nn.Linear(256, 1024).to(d), torch.nn.Linear(1024, 256).to(d)
+            x = torch.randn(4, 4096, 256, device=d)
+            for _ in range(2):
+                with torch.autocast("cuda", dtype=torch.bfloat16):
+                    y = ops.mlp_residual(x, x.bfloat16(), fc1, fc2)
+                y.float().square().mean().backward()
+            torch.cuda.synchronize()
+            res[side] = [p.grad.clone() for p in (fc1.weight, fc1.bias, fc2.weight, fc2.bias)]
+        finally:
+            ops.SIDE_WGRAD = old
+    for a, b in zip(res[True], res[False]):
         assert torch.equal(a, b)
-        torch.testing.assert_close(a.double(), t.double().sum(0), rtol=1e-5, atol=1e-5 * t.shape[0] ** 0.5)
-    dy = torch.randn(4096, 256, device=d).bfloat16()
-    x = torch.randn(4096, 768, device=d).bfloat16()
-    side = torch.cuda.Stream(d)
-    with torch.cuda.stream(side):
-        dw, db = ops.linear_wgrad_deferred(dy, x)
-    ops._SIDE_STREAMS[d] = side
-    ops.join_side_streams()
-    torch.cuda.synchronize()
-    rw, rb = ops.linear_wgrad(dy, x)
-    torch.testing.assert_close(dw, rw, rtol=1e-5, atol=1e-4)
-    torch.testing.assert_close(db, rb, rtol=1e-5, atol=1e-4)
 
 
 CONV_CASES = [  # (B, H, C, N, k, stride, pad)
