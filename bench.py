@@ -6,13 +6,17 @@ One step = forward + BCE + backward (+ bucketed RCCL gradient all-reduce, captur
 graph, csu.dist.GradAllReduce) + fused AdamW on a batch of
 synthetic 512x512 images already resident in HBM.  Prints ONE JSON line (rank 0).
 
-roofline: the stripe-attention forward kernel (csu_stripe_attn_fwd -> stripe_fwd_w), timed live
-with HIP events on the launch stream around 8 back-to-back repeats of every launch of 3 eager
-steps of the same workload (HIP events cannot be recorded inside the graph replays of the timed
-region: hipErrorInvalidHandle); achieved = algorithmic bytes (qkv read once + output written once
-+ log-sum-exp) / measured time.  traffic = HBM bytes per launch from the committed rocprofv3 PMC
-summary (profiles/pmc_stripe_fwd.json, FETCH_SIZE x2 + WRITE_SIZE, tools/pmc_traffic.py).  cpu_baseline: the CPU
-oracle (a restatement of the reference) timed on this host for a bounded sample.
+roofline: every csu kernel launch of 2 eager steps of the same workload is timed live with HIP
+events on its launch stream (csu.ledger: idempotent launches re-run back-to-back between the events;
+HIP events cannot be recorded inside the graph replays of the timed region) and carries its
+algorithmic FLOPs and bytes (each input read once, each output written once).  Per kernel:
+t_roof = max(FLOPs / P_mfma, bytes / 8 TB/s); the reported object is the kernel with the most time
+per step (achieved GB/s or TFLOP/s vs its peak), plus "step_frac" = sum of t_roof over every launch of
+a step / ms_per_step of the timed graph replays, and the per-kernel list.  traffic = HBM bytes per
+launch of that kernel from the committed rocprofv3 PMC summary for this workload
+(profiles/pmc_traffic.json, FETCH_SIZE x2 + WRITE_SIZE per the gfx950 correction), or null.
+cpu_baseline: the CPU oracle (a restatement of the reference, parity-pinned to it) timed on this
+host for a bounded sample of the same workload.
 """
 from __future__ import annotations
 
@@ -32,8 +36,6 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
-BF16_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA
 
 
 def parse():
@@ -67,8 +69,21 @@ def synthetic_batches(n, batch, img, device, seed):
     return out
 
 
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(args, dtype):
-    """Oracle (CPU restatement of the reference) fwd+BCE+bwd+AdamW, bounded sample."""
+    """Oracle (CPU restatement of the reference) fwd+BCE+bwd+AdamW on the same per-GPU batch:
+    1 warm-up + 2 timed steps (~10-30 s).  Threads: the process's CPU affinity, capped at 16 -- the
+    GPU box's CPU share per GPU (more threads than the share only contend)."""
     from oracle import cswin_ref as O
     threads = min(16, len(os.sched_getaffinity(0)))
     torch.set_num_threads(threads)
@@ -77,7 +92,7 @@ def cpu_baseline(args, dtype):
     m = O.OracleCSWin(cfg, O.recipe_params(cfg, seed=0))
     opt = torch.optim.AdamW(m.parameters(), lr=1e-4, weight_decay=1e-4)
     from csu.data import ellipse_batch
-    b = 2
+    b = args.batch
     x, t = ellipse_batch(np.random.default_rng(7), b, args.img)
 
     def step():
@@ -90,14 +105,15 @@ def cpu_baseline(args, dtype):
 
     step()  # warm-up
     n, t0 = 0, time.perf_counter()
-    while n < 2 or (time.perf_counter() - t0 < 10.0 and n < 8):
+    while n < 2:
         step()
         n += 1
     el = time.perf_counter() - t0
     return {"value": round(n * b / el, 4), "unit": "images/sec", "cores": threads, "kind": "port",
+            "cpu": _cpu_model(),
             "sample": f"{n} train steps x batch {b} at {args.img}x{args.img} "
-                      f"({'bf16 autocast' if dtype == torch.bfloat16 else 'fp32'}), oracle/cswin_ref.py, "
-                      f"{el:.1f}s, {threads} threads"}
+                      f"({'bf16 autocast' if dtype == torch.bfloat16 else 'fp32'}) after 1 warm-up step, "
+                      f"oracle/cswin_ref.py, {el:.1f}s, {threads} threads"}
 
 
 def main():
@@ -166,15 +182,19 @@ def main():
     else:
         for i in range(args.warmup):
             eager_step(i)
-    # roofline leg: time every stripe-attention forward launch of a few eager steps of the same
-    # workload with HIP events on the launch stream (events cannot be recorded in graph replays)
-    prof = None
+    # roofline leg: every kernel launch of 2 eager steps of the same workload, timed with HIP
+    # events on its launch stream (events cannot be recorded in graph replays)
+    ledger = None
     if not args.no_roofline:
-        prof = []
-        ops.set_kernel_timer(prof, repeat=8)
-        for i in range(min(args.steps, 3)):
-            eager_step(i)
-        ops.set_kernel_timer(None)
+        from csu.ledger import KernelLedger
+        ledger = KernelLedger(repeat=4)
+        side, ops.SIDE_WGRAD = ops.SIDE_WGRAD, False   # serialized, like the single-stream graph replay
+        try:
+            with ledger:
+                for i in range(2):
+                    eager_step(i)
+        finally:
+            ops.SIDE_WGRAD = side
     for i in range(2):
         step(i)
     torch.cuda.synchronize()
@@ -194,18 +214,8 @@ def main():
     el = float(t.item())
     images = args.batch * world * args.steps
     roof = None
-    if prof:
-        torch.cuda.synchronize()
-        ms = sum(s.elapsed_time(e) for s, e, _, _, _ in prof)
-        nbytes = sum(p[2] for p in prof)
-        flops = sum(p[3] for p in prof)
-        n = sum(p[4] for p in prof)
-        achieved = nbytes / n / (ms / n * 1e-3) / 1e9
-        roof = {"kernel": "csu_stripe_attn_fwd (stripe_fwd_w, bf16)", "bound": "hbm", "achieved": round(achieved, 1),
-                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": _pmc_traffic(), "launches": n, "avg_us": round(ms / n * 1e3, 2),
-                "bytes_per_launch": int(nbytes / n), "flops_per_launch": int(flops / n),
-                "achieved_tflops": round(flops / (ms * 1e-3) / 1e12, 2)}
+    if ledger is not None:
+        roof = _roofline(ledger.summary(steps=2), el / args.steps * 1e3, args)
     cpu = None
     if rank == 0 and world == 1 and (args.cpu_baseline == "on" or (args.cpu_baseline == "auto")):
         try:
@@ -213,7 +223,7 @@ def main():
         except Exception as e:  # baseline is informational; never hide the GPU number
             cpu = {"value": None, "error": repr(e)[:200]}
     if rank == 0:
-        rec = {"metric": f"images/sec at {args.img}x{args.img} {args.dtype} (CSWin-UNet train step)", "value": round(images / el, 3),
+        rec = {"metric": _metric(args), "value": round(images / el, 3),
                "unit": "images/sec", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
                "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
                "vs_baseline": None, "dtype": args.dtype, "data": "synthetic (ellipse masks, SURVEY §8d), random-init weights",
@@ -229,14 +239,45 @@ def main():
         dist.destroy_process_group()
 
 
-def _pmc_traffic():
-    """HBM bytes per launch of stripe_fwd from the committed rocprofv3 PMC summary, if present."""
-    p = os.path.join(REPO, "profiles", "pmc_stripe_fwd.json")
+def _metric(args):
+    """BASELINE.json's metric string for its headline workload (512x512 bf16, default depth); the
+    same form naming the resolution / precision otherwise."""
+    if (args.img, args.dtype, args.depth, args.split) == (512, "bf16", "1,2,9,1", "1,2,8,8"):
+        try:
+            with open(os.path.join(REPO, "BASELINE.json")) as f:
+                return json.load(f)["metric"]
+        except Exception:
+            pass
+    return f"images/sec at {args.img}x{args.img} {args.dtype} (CSWin-UNet train step)"
+
+
+def _roofline(kernels, ms_per_step, args):
+    """Dominant kernel (most time per step) vs its roofline, the step fraction and the table."""
+    top = kernels[0]
+    if top["bound"] == "hbm":
+        achieved, peak, unit = top["achieved_GBs"], 8000.0, "GB/s"
+    else:
+        from csu.ledger import PEAK_TFLOPS
+        achieved, peak, unit = top["achieved_TFLOPs"], PEAK_TFLOPS[top["precision"]], "TFLOP/s"
+    t_roof_step = sum(k["t_roof_us"] * k["launches_per_step"] for k in kernels) / 1e3
+    return {"kernel": top["kernel"], "bound": top["bound"], "achieved": achieved, "peak": peak, "unit": unit,
+            "frac": round(achieved / peak, 4), "traffic": _pmc_traffic(top["kernel"], args),
+            "avg_us": top["avg_us"], "launches_per_step": top["launches_per_step"],
+            "bytes_per_launch": top["bytes_per_launch"], "flops_per_launch": top["flops_per_launch"],
+            "step_frac": round(t_roof_step / ms_per_step, 4), "step_t_roof_ms": round(t_roof_step, 3),
+            "eager_kernel_ms_per_step": round(sum(k["us_per_step"] for k in kernels) / 1e3, 3),
+            "kernels": kernels}
+
+
+def _pmc_traffic(kernel, args):
+    """HBM bytes per launch of `kernel` for THIS workload from the committed rocprofv3 PMC summary
+    (profiles/pmc_traffic.json: {"<kernel>|<img>|<batch>|<dtype>": bytes}), else None."""
+    p = os.path.join(REPO, "profiles", "pmc_traffic.json")
     if not os.path.exists(p):
         return None
     try:
         with open(p) as f:
-            return json.load(f).get("hbm_bytes_per_launch")
+            return json.load(f).get(f"{kernel}|{args.img}|{args.batch}|{args.dtype}")
     except Exception:
         return None
 

@@ -12,10 +12,10 @@
 // staged row-major ([token][column], XOR-swizzled 16-B chunks) through TWO LDS buffers with a
 // two-step register prefetch (branch-free buffer loads), fragments gathered with the transposing
 // ds_read_b64_tr_b16.  Measured (tools/wgrad_timing.py, tools/wgrad_bench.py): a step is bound by
-// the per-CU load rate (L2 hits ~70 GB/s/CU, the compulsory HBM part slower), not by latency or
-// the MFMAs, so the plan uses about one workgroup per CU with as few chunks as fill the chip; the
-// chunk partials of a tile are combined IN the launch (arrival counter, agent-scope
-// release/acquire, each workgroup sums 1/chunks of the tile in chunk order) -- no reduce launch.
+// the per-CU load rate (L2 hits ~70 GB/s/CU, the compulsory HBM part slower), not by latency
+// (deeper prefetch, more workgroups per CU: no change) nor the MFMAs.  The chunk partials go to
+// tile-local slabs reduced by ONE coalesced pass in chunk order (wslab_reduce): an in-launch
+// combine (arrival counters, agent-scope release/acquire) measured 1.3-4x slower per launch.
 // fp32 path: 64x64 tiles, v_mfma_f32_32x32x2f32, [chunk][N*K + N] slabs + csu_colsum.
 #include <cstdlib>
 #include <type_traits>
@@ -182,15 +182,14 @@ struct TileCfg {
 
 // One TN x TK tile of dW (and db when k0 == 0) over tokens [m_begin, m_end).  chunks == 1: dW / db
 // are written to dst (N*K + N fp32); else the partial tile goes to slab[tile][chunk][TN][TK] and the
-// db partial to bslab[n_tile][chunk][TN], and the workgroups of the tile combine them in-launch.
+// db partial to bslab[n_tile][chunk][TN]; wslab_reduce sums them.
 // Pipeline per 64-token step i: stage step i+1 from registers into LDS buffer (i+1)&1, issue the
 // global loads of step i+3 into the register set just freed, MFMAs of step i, one barrier -- two
 // steps of MFMA work between a load's issue and its use, 64 KB LDS (T = 128) for 2 workgroups/CU.
 template <int TN, int TK, int D>
 __global__ __launch_bounds__(NT, D > 2 ? 1 : 2) void wgrad_tile(long M, int N, int K, long rpc, int chunks,
                                                     const bf16* __restrict__ dy, const bf16* __restrict__ x,
-                                                    float* __restrict__ dst, unsigned* __restrict__ cnt,
-                                                    float* __restrict__ slab) {
+                                                    float* __restrict__ dst, float* __restrict__ slab) {
     using C = TileCfg<TN, TK>;
     __shared__ __attribute__((aligned(16))) bf16 lds[2 * C::BUF];
     WG_STAMP(0);
@@ -330,57 +329,43 @@ __global__ __launch_bounds__(NT, D > 2 ? 1 : 2) void wgrad_tile(long M, int N, i
             }
         }
     }
-    if (chunks > 1) {
-        // In-launch split-K combine (cdna_hip_programming.md section 5 / Guideline 16): publish this
-        // chunk's partial (every wave drains its stores, barrier, ONE agent-scope release, then the
-        // ticket), wait until all `chunks` workgroups of the tile have published (the plan keeps the
-        // grid <= #CUs, so every workgroup is resident; the spin is bounded), ONE agent-scope
-        // acquire, then this workgroup sums its 1/chunks share of the tile over the chunks in chunk
-        // order (fixed order: bitwise reproducible) and writes dW (and, chunk 0 of a k-tile-0 tile,
-        // db).  cnt[tile] was zeroed by the memset in front of the launch.
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        unsigned* red = reinterpret_cast<unsigned*>(lds);   // LDS word: the spin outcome
-        if (threadIdx.x == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __hip_atomic_fetch_add(cnt + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            unsigned spins = 0, ok = 1;
-            while (__hip_atomic_load(cnt + tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)chunks) {
-                __builtin_amdgcn_s_sleep(2);
-                if (++spins > (1u << 22)) {   // a partner never arrived: flag it, never hang
-                    __hip_atomic_store(cnt + tiles, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    ok = 0;
-                    break;
-                }
-            }
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            red[0] = ok;
-        }
-        __syncthreads();
-        constexpr int E4 = TN * TK / 4;                        // float4s per tile
-        const int per = (E4 + chunks - 1) / chunks;
-        const f32x4* src = reinterpret_cast<const f32x4*>(slab + (long)tile * chunks * (TN * TK));
-        const __amdgpu_buffer_rsrc_t rd = buf_rsrc(dst, (long)N * K * 4);
-        for (int e4 = chunk * per + threadIdx.x; e4 < min(E4, (chunk + 1) * per); e4 += NT) {
-            f32x4 v = src[e4];
-            for (int c = 1; c < chunks; ++c) v += src[(long)c * E4 + e4];
-            const int nl = (e4 * 4) / TK, kl = (e4 * 4) % TK;
-            const int n = n0 + nl, k = k0 + kl;
-            const unsigned off = (n < N && k < K) ? (unsigned)(n * K + k) * 4u : kOOB;
-            u32x4 w = {__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]), __float_as_uint(v[3])};
-            __builtin_amdgcn_raw_buffer_store_b128(w, rd, off, 0, 0);
-        }
-        if (do_bias && chunk == 0 && threadIdx.x < TN && n0 + threadIdx.x < N) {
-            const float* bs = slab + (long)tiles * chunks * (TN * TK) + (long)ntile * chunks * TN + threadIdx.x;
-            float v = bs[0];
-            for (int c = 1; c < chunks; ++c) v += bs[(long)c * TN];
-            dst[(long)N * K + n0 + threadIdx.x] = v;
-        }
-    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     WG_STAMP(3);
+}
+
+// dst[n][k] = sum_c slab[tile(n, k)][c][n % TN][k % TK] (c = 0 .. chunks-1 in order), then
+// dst[N*K + n] = sum_c bslab[n / TN][c][n % TN].  One thread per 4 outputs.
+__global__ __launch_bounds__(NT) void wslab_reduce(int N, int K, int TN, int TK, int chunks,
+                                                   const float* __restrict__ slab, float* __restrict__ dst) {
+    const long e = ((long)blockIdx.x * NT + threadIdx.x) * 4;
+    const long NK = (long)N * K;
+    const int kt = (K + TK - 1) / TK, nt = (N + TN - 1) / TN;
+    const long step = (long)TN * TK;
+    const float* p;
+    long stride;
+    if (e < NK) {
+        const int n = (int)(e / K), k = (int)(e % K);
+        const long tile = (long)(n / TN) * kt + k / TK;
+        p = slab + tile * chunks * step + (long)(n % TN) * TK + (k % TK);
+        stride = step;
+    } else if (e < NK + N) {
+        const int n = (int)(e - NK);
+        p = slab + (long)nt * kt * chunks * step + ((long)(n / TN) * chunks) * TN + (n % TN);
+        stride = TN;
+    } else {
+        return;
+    }
+    f32x4 s = *reinterpret_cast<const f32x4*>(p);
+    int c = 1;
+    for (; c + 3 < chunks; c += 4) {   // 4 loads in flight, added in chunk order
+        const f32x4 v1 = *reinterpret_cast<const f32x4*>(p + c * stride);
+        const f32x4 v2 = *reinterpret_cast<const f32x4*>(p + (c + 1) * stride);
+        const f32x4 v3 = *reinterpret_cast<const f32x4*>(p + (c + 2) * stride);
+        const f32x4 v4 = *reinterpret_cast<const f32x4*>(p + (c + 3) * stride);
+        s += v1; s += v2; s += v3; s += v4;
+    }
+    for (; c < chunks; ++c) s += *reinterpret_cast<const f32x4*>(p + c * stride);
+    *reinterpret_cast<f32x4*>(dst + e) = s;
 }
 
 int num_cus() {
@@ -401,26 +386,26 @@ struct Plan {
     long rpc;
 };
 
-// Tiles 128 wide where the dimension is a multiple of 128 (fewer operand re-reads), else 64.
-// Chunks: about one workgroup per CU over all tiles, >= 256 tokens each -- the fewest split-K
-// partials that still fill the chip -- and never more workgroups than CUs when split (the in-launch
-// combine needs every workgroup of a tile resident).  tn / tk / chunks > 0 override
-// (csu_linear_wgrad_tuned; a forced split is still capped at one workgroup per CU).
+// Plan (tools/wgrad_bench.py sweeps, 512x512 B16 step shapes): a step is bound by the per-CU load
+// rate, so per-workgroup fixed costs (first loads ~2 us, slab write ~1.5 us) must be amortised over
+// many 64-token steps: 128-wide tiles only when they still give >= 16 tiles, chunks for about one
+// workgroup per CU but >= 1024 tokens each (>= 2048 with <= 2 tiles).  tn / tk / chunks > 0 override
+// (csu_linear_wgrad_tuned).
 Plan make_plan(long M, int N, int K, int tn, int tk, int chunks) {
     Plan p;
-    p.tn = tn > 0 ? tn : (N % 128 == 0 ? 128 : 64);
-    p.tk = tk > 0 ? tk : (K % 128 == 0 ? 128 : 64);
+    const bool big = N % 128 == 0 && K % 128 == 0 && (N / 128) * (K / 128) >= 16;
+    p.tn = tn > 0 ? tn : (big ? 128 : 64);
+    p.tk = tk > 0 ? tk : (big ? 128 : 64);
     p.nt = (N + p.tn - 1) / p.tn;
     p.kt = (K + p.tk - 1) / p.tk;
     const long tiles = (long)p.nt * p.kt;
     long want = chunks;
     if (want <= 0) {
         want = (num_cus() + tiles - 1) / tiles;
-        const long maxc = (M + 255) / 256;
+        const long mintok = tiles <= 2 ? 2048 : 1024;
+        const long maxc = (M + mintok - 1) / mintok;
         if (want > maxc) want = maxc;
     }
-    const long cap = num_cus() / tiles;                    // resident-grid limit of a split launch
-    if (want > cap) want = cap;
     if (want < 1) want = 1;
     p.rpc = ((M + want - 1) / want + TM - 1) / TM * TM;
     p.chunks = (int)((M + p.rpc - 1) / p.rpc);
@@ -428,39 +413,33 @@ Plan make_plan(long M, int N, int K, int tn, int tk, int chunks) {
     return p;
 }
 
-// workspace: [tiles + 1 counters (the last: spin-timeout flag), padded to 256 B][partial tiles
-// [tile][chunk][TN][TK]][db partials [n_tile][chunk][TN]]
-size_t cnt_bytes(const Plan& p) { return ((size_t)(p.nt * p.kt + 1) * 4 + 255) / 256 * 256; }
+// workspace: [partial tiles [tile][chunk][TN][TK]][db partials [n_tile][chunk][TN]]
 size_t plan_bytes(const Plan& p) {
     if (p.chunks == 1) return 0;
-    return cnt_bytes(p) + ((size_t)p.nt * p.kt * p.tn * p.tk + (size_t)p.nt * p.tn) * p.chunks * sizeof(float);
+    return ((size_t)p.nt * p.kt * p.tn * p.tk + (size_t)p.nt * p.tn) * p.chunks * sizeof(float);
 }
 
 template <int TN, int TK>
 void launch_tile(const Plan& p, unsigned grid, long M, int N, int K, const bf16* dy, const bf16* x, float* dst,
-                 unsigned* cnt, float* slab, hipStream_t st) {
-    if (p.depth >= 4) wgrad_tile<TN, TK, 4><<<grid, NT, 0, st>>>(M, N, K, p.rpc, p.chunks, dy, x, dst, cnt, slab);
-    else if (p.depth == 3) wgrad_tile<TN, TK, 3><<<grid, NT, 0, st>>>(M, N, K, p.rpc, p.chunks, dy, x, dst, cnt, slab);
-    else wgrad_tile<TN, TK, 2><<<grid, NT, 0, st>>>(M, N, K, p.rpc, p.chunks, dy, x, dst, cnt, slab);
+                 float* slab, hipStream_t st) {
+    wgrad_tile<TN, TK, 2><<<grid, NT, 0, st>>>(M, N, K, p.rpc, p.chunks, dy, x, dst, slab);
 }
 
 int run_bf16(const Plan& p, long M, int N, int K, const bf16* dy, const bf16* x, float* dst, void* ws, hipStream_t st) {
     const unsigned grid = (unsigned)((long)p.nt * p.kt * p.chunks);
-    unsigned* cnt = (unsigned*)ws;
-    float* slab = (float*)((char*)ws + cnt_bytes(p));
-    if (p.chunks > 1) {   // zero the arrival counters in front of every launch (a memset node when captured)
-        const hipError_t e = hipMemsetAsync(cnt, 0, cnt_bytes(p), st);
-        if (e != hipSuccess) return fail((int)e, "linear_wgrad: counter memset");
-    } else {
-        cnt = nullptr;
-        slab = nullptr;
-    }
-    if (p.tn == 128 && p.tk == 128) launch_tile<128, 128>(p, grid, M, N, K, dy, x, dst, cnt, slab, st);
-    else if (p.tn == 128 && p.tk == 64) launch_tile<128, 64>(p, grid, M, N, K, dy, x, dst, cnt, slab, st);
-    else if (p.tn == 64 && p.tk == 128) launch_tile<64, 128>(p, grid, M, N, K, dy, x, dst, cnt, slab, st);
-    else if (p.tn == 64 && p.tk == 64) launch_tile<64, 64>(p, grid, M, N, K, dy, x, dst, cnt, slab, st);
+    float* slab = p.chunks > 1 ? (float*)ws : nullptr;
+    if (p.tn == 128 && p.tk == 128) launch_tile<128, 128>(p, grid, M, N, K, dy, x, dst, slab, st);
+    else if (p.tn == 128 && p.tk == 64) launch_tile<128, 64>(p, grid, M, N, K, dy, x, dst, slab, st);
+    else if (p.tn == 64 && p.tk == 128) launch_tile<64, 128>(p, grid, M, N, K, dy, x, dst, slab, st);
+    else if (p.tn == 64 && p.tk == 64) launch_tile<64, 64>(p, grid, M, N, K, dy, x, dst, slab, st);
     else return fail(CSU_E_ARG, "linear_wgrad: tile must be 64 or 128");
-    return check_launch("linear_wgrad");
+    if (int e = check_launch("linear_wgrad")) return e;
+    if (p.chunks > 1) {
+        const long outs = ((long)N * K + N) / 4;
+        wslab_reduce<<<(unsigned)((outs + NT - 1) / NT), NT, 0, st>>>(N, K, p.tn, p.tk, p.chunks, slab, dst);
+        return check_launch("linear_wgrad reduce");
+    }
+    return 0;
 }
 
 }  // namespace

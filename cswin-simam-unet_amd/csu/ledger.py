@@ -1,0 +1,101 @@
+"""Per-kernel roofline ledger: every C-ABI launch of csu goes through ``launch()``, which names the
+call and states its ALGORITHMIC work (FLOPs; bytes = each input read once + each output written
+once).  While a ``KernelLedger`` is active (eager steps only -- HIP events cannot be recorded in a
+graph replay), each launch is timed with HIP events on its own stream: idempotent launches are
+re-run ``repeat`` times back-to-back between the two events (the per-event overhead then stays out
+of the per-launch time, which matches the rocprofv3 kernel trace); non-idempotent ones (the
+in-place AdamW) are timed once.  ``summary()`` gives, per call name, launches, measured time,
+achieved GB/s / TFLOP/s, the roofline time t_roof = max(FLOPs / P_mfma, bytes / BW_hbm) and the
+fraction t_roof / t_measured (MI355X_MICROARCH.md peaks: HBM 8 TB/s, dense bf16 MFMA 2.5 PF/s,
+fp32 MFMA 157.3 TF/s)."""
+from __future__ import annotations
+
+import collections
+from typing import Callable, Dict, List, Optional
+
+import torch
+
+from ._lib import check
+
+HBM_GBS = 8000.0
+PEAK_TFLOPS = {"bf16": 2500.0, "f32": 157.3, "fp8": 5000.0}
+
+_ACTIVE: Optional["KernelLedger"] = None
+
+
+class KernelLedger:
+    def __init__(self, repeat: int = 4):
+        self.repeat = max(1, int(repeat))
+        self.rows: List[tuple] = []
+
+    def __enter__(self):
+        global _ACTIVE
+        self._prev, _ACTIVE = _ACTIVE, self
+        return self
+
+    def __exit__(self, *exc):
+        global _ACTIVE
+        _ACTIVE = self._prev
+        return False
+
+    def summary(self, steps: int = 1) -> List[Dict]:
+        """Per call name (sorted by measured time): launches per step, avg us per launch, algorithmic
+        bytes / FLOPs per launch, achieved GB/s and TFLOP/s, bound, t_roof and frac."""
+        torch.cuda.synchronize()
+        agg = collections.OrderedDict()
+        for name, e0, e1, reps, flops, nbytes, prec in self.rows:
+            a = agg.setdefault(name, {"n": 0, "ms": 0.0, "flops": 0.0, "bytes": 0.0, "prec": prec})
+            a["n"] += 1
+            a["ms"] += e0.elapsed_time(e1) / reps
+            a["flops"] += flops
+            a["bytes"] += nbytes
+        out = []
+        for name, a in agg.items():
+            n = a["n"]
+            us = a["ms"] / n * 1e3
+            peak = PEAK_TFLOPS[a["prec"]]
+            t_mem = a["bytes"] / n / (HBM_GBS * 1e9) * 1e6           # us
+            t_mma = a["flops"] / n / (peak * 1e12) * 1e6
+            t_roof = max(t_mem, t_mma)
+            out.append({"kernel": name, "launches_per_step": round(n / steps, 2), "avg_us": round(us, 2),
+                        "us_per_step": round(us * n / steps, 1),
+                        "bytes_per_launch": int(a["bytes"] / n), "flops_per_launch": int(a["flops"] / n),
+                        "achieved_GBs": round(a["bytes"] / n / (us * 1e-6) / 1e9, 1),
+                        "achieved_TFLOPs": round(a["flops"] / n / (us * 1e-6) / 1e12, 2),
+                        "bound": "hbm" if t_mem >= t_mma else "mfma", "precision": a["prec"],
+                        "t_roof_us": round(t_roof, 3), "frac": round(t_roof / us, 4) if us > 0 else None})
+        out.sort(key=lambda r: -r["us_per_step"])
+        return out
+
+
+def launch(name: str, fn: Callable[[], int], flops: float = 0.0, nbytes: float = 0.0, idem: bool = True,
+           prec: str = "bf16"):
+    """Run ``fn`` (a C-ABI call returning its status code) and check it; time it when a ledger is
+    active.  ``idem``: the call can be repeated without changing its result (outputs overwritten
+    from unchanged inputs)."""
+    led = _ACTIVE
+    if led is None or torch.cuda.is_current_stream_capturing():
+        check(fn(), name)
+        return
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if idem:
+        check(fn(), name)
+        e0.record()
+        for _ in range(led.repeat):
+            check(fn(), name)
+        e1.record()
+        reps = led.repeat
+    else:
+        e0.record()
+        check(fn(), name)
+        e1.record()
+        reps = 1
+    led.rows.append((name, e0, e1, reps, float(flops), float(nbytes), prec))
+
+
+def esize(t) -> int:
+    return 0 if t is None else t.element_size()
+
+
+def prec_of(t) -> str:
+    return "f32" if t is not None and t.dtype == torch.float32 else "bf16"

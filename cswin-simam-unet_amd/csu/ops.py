@@ -10,21 +10,7 @@ import torch
 
 from . import _lib
 from ._lib import check, dtype_code, lib, ptr, require_device, stream_ptr
-
-
-_KERNEL_TIMER = None
-_KERNEL_TIMER_REPEAT = 1
-
-
-def set_kernel_timer(sink, repeat: int = 1):
-    """Time csu_stripe_attn_fwd: after each real launch, ``repeat`` identical back-to-back launches
-    (same inputs, same outputs) are bracketed by two HIP events on the launch stream, and
-    (start_event, end_event, algorithmic_bytes, flops, launches) is appended to the list ``sink``
-    (None disables).  Back-to-back launches keep the per-event overhead (a few us on a ~30 us
-    kernel) out of the per-launch duration, so it matches the rocprofv3 kernel-trace average."""
-    global _KERNEL_TIMER, _KERNEL_TIMER_REPEAT
-    _KERNEL_TIMER = sink
-    _KERNEL_TIMER_REPEAT = max(1, int(repeat))
+from .ledger import esize, launch as _launch, prec_of
 
 
 def _stripe_fwd_work(geom, B, esize):
@@ -84,19 +70,10 @@ class _StripeAttnFn(torch.autograd.Function):
         out = torch.empty(B, L, geom.C, dtype=qkv.dtype, device=qkv.device)
         lse = torch.empty(nb, B, geom.heads, L, dtype=torch.float32, device=qkv.device)
         a = geom.args(B, ws, bs)
-        launch = lambda: check(lib().csu_stripe_attn_fwd(ctypes.byref(a), dtype_code(qkv), ptr(qkv), ptr(out),
-                                                         ptr(lse), stream_ptr(qkv.device)), "csu_stripe_attn_fwd")
-        launch()
-        timer = _KERNEL_TIMER
-        if timer is not None:
-            rep = _KERNEL_TIMER_REPEAT
-            ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            ev0.record()   # torch's current stream == the launch stream (stream_ptr above)
-            for _ in range(rep):
-                launch()
-            ev1.record()
-            nbytes, flops = _stripe_fwd_work(geom, B, qkv.element_size())
-            timer.append((ev0, ev1, nbytes * rep, flops * rep, rep))
+        nbytes, flops = _stripe_fwd_work(geom, B, qkv.element_size())
+        _launch("stripe_attn_fwd", lambda: lib().csu_stripe_attn_fwd(ctypes.byref(a), dtype_code(qkv), ptr(qkv), ptr(out),
+                                                                     ptr(lse), stream_ptr(qkv.device)),
+                flops, nbytes, prec=prec_of(qkv))
         ctx.geom = geom
         ctx.lepe_dtypes = [t.dtype for t in lepe]
         ctx.save_for_backward(qkv, out, lse, *ws, *bs)
@@ -118,9 +95,14 @@ class _StripeAttnFn(torch.autograd.Function):
         a = geom.args(B, ws, bs, dws, dbs)
         nbytes = L.csu_stripe_attn_bwd_workspace(ctypes.byref(a))
         work = torch.empty(max(nbytes, 16), dtype=torch.uint8, device=qkv.device)
-        check(L.csu_stripe_attn_bwd(ctypes.byref(a), dtype_code(qkv), ptr(qkv), ptr(out), ptr(dout), ptr(lse),
-                                    ptr(delta), ptr(dqkv), ptr(work), nbytes, stream_ptr(qkv.device)),
-              "csu_stripe_attn_bwd")
+        e = qkv.element_size()
+        fb, ff = _stripe_fwd_work(geom, B, e)
+        # algorithmic: qkv + out + dout read, dqkv written, lse read; FLOPs 2x forward (dP, dV, dQ, dK)
+        bw = B * geom.reso * geom.reso * (3 * geom.C * 2 + 2 * geom.C) * e + lse.numel() * 4
+        _launch("stripe_attn_bwd", lambda: L.csu_stripe_attn_bwd(ctypes.byref(a), dtype_code(qkv), ptr(qkv), ptr(out),
+                                                                 ptr(dout), ptr(lse), ptr(delta), ptr(dqkv), ptr(work),
+                                                                 nbytes, stream_ptr(qkv.device)),
+                2 * ff, bw, prec=prec_of(qkv))
         grads = [g.to(dt) for g, dt in zip(dws + dbs, ctx.lepe_dtypes)]
         return (dqkv, None, *grads)
 
@@ -146,8 +128,10 @@ class _LayerNormFn(torch.autograd.Function):
         y = torch.empty(x.shape, dtype=out_dtype, device=x.device)
         mean = torch.empty(rows, dtype=torch.float32, device=x.device)
         rstd = torch.empty(rows, dtype=torch.float32, device=x.device)
-        check(lib().csu_layernorm_fwd(rows, C, float(eps), dtype_code(x), ptr(x), ptr(w), ptr(b), dtype_code(y), ptr(y),
-                                      ptr(mean), ptr(rstd), stream_ptr(x.device)), "csu_layernorm_fwd")
+        _launch("layernorm_fwd", lambda: lib().csu_layernorm_fwd(rows, C, float(eps), dtype_code(x), ptr(x), ptr(w), ptr(b),
+                                                                 dtype_code(y), ptr(y), ptr(mean), ptr(rstd),
+                                                                 stream_ptr(x.device)),
+                8 * rows * C, rows * C * (esize(x) + esize(y)) + rows * 8, prec=prec_of(x))
         ctx.save_for_backward(x, w, mean, rstd)
         ctx.pdtypes = (weight.dtype, bias.dtype)
         return y
@@ -166,9 +150,10 @@ class _LayerNormFn(torch.autograd.Function):
         L = lib()
         nbytes = L.csu_layernorm_bwd_workspace(rows, C)
         work = torch.empty(max(nbytes, 16), dtype=torch.uint8, device=x.device)
-        check(L.csu_layernorm_bwd(rows, C, dtype_code(x), ptr(x), ptr(w), ptr(mean), ptr(rstd), dtype_code(dy), ptr(dy),
-                                  ptr(dx), ptr(dg), ptr(db), ptr(work), nbytes, stream_ptr(x.device)),
-              "csu_layernorm_bwd")
+        _launch("layernorm_bwd", lambda: L.csu_layernorm_bwd(rows, C, dtype_code(x), ptr(x), ptr(w), ptr(mean), ptr(rstd),
+                                                             dtype_code(dy), ptr(dy), ptr(dx), ptr(dg), ptr(db), ptr(work),
+                                                             nbytes, stream_ptr(x.device)),
+                12 * rows * C, rows * C * (2 * esize(x) + esize(dy)) + rows * 8, prec=prec_of(x))
         return dx, dg.to(ctx.pdtypes[0]), db.to(ctx.pdtypes[1]), None, None
 
 
@@ -203,8 +188,10 @@ class _LayerNormForkFn(torch.autograd.Function):
         y = torch.empty(x.shape, dtype=out_dtype, device=x.device)
         mean = torch.empty(rows, dtype=torch.float32, device=x.device)
         rstd = torch.empty(rows, dtype=torch.float32, device=x.device)
-        check(lib().csu_layernorm_fwd(rows, C, float(eps), dtype_code(x), ptr(x), ptr(w), ptr(b), dtype_code(y), ptr(y),
-                                      ptr(mean), ptr(rstd), stream_ptr(x.device)), "csu_layernorm_fwd")
+        _launch("layernorm_fwd", lambda: lib().csu_layernorm_fwd(rows, C, float(eps), dtype_code(x), ptr(x), ptr(w), ptr(b),
+                                                                 dtype_code(y), ptr(y), ptr(mean), ptr(rstd),
+                                                                 stream_ptr(x.device)),
+                8 * rows * C, rows * C * (esize(x) + esize(y)) + rows * 8, prec=prec_of(x))
         ctx.save_for_backward(x, w, mean, rstd)
         ctx.pdtypes = (weight.dtype, bias.dtype)
         return x.view_as(x), y
@@ -227,9 +214,12 @@ class _LayerNormForkFn(torch.autograd.Function):
         nbytes = L.csu_layernorm_bwd_workspace(rows, C)
         work = torch.empty(max(nbytes, 16), dtype=torch.uint8, device=x.device)
         dgb = torch.empty(2 * C, dtype=torch.float32, device=x.device)
-        check(L.csu_layernorm_bwd_ex(rows, C, dtype_code(x), ptr(x), ptr(w), ptr(mean), ptr(rstd), dtype_code(dy), ptr(dy),
-                                     ptr(dres_k), ptr(dx), ptr(dxb), ptr(dgb[:C]), ptr(dgb[C:]), ptr(work), nbytes,
-                                     stream_ptr(x.device)), "csu_layernorm_bwd_ex")
+        _launch("layernorm_bwd", lambda: L.csu_layernorm_bwd_ex(rows, C, dtype_code(x), ptr(x), ptr(w), ptr(mean),
+                                                                ptr(rstd), dtype_code(dy), ptr(dy), ptr(dres_k), ptr(dx),
+                                                                ptr(dxb), ptr(dgb[:C]), ptr(dgb[C:]), ptr(work), nbytes,
+                                                                stream_ptr(x.device)),
+                12 * rows * C, rows * C * (2 * esize(x) + esize(dy) + esize(dres_k) + esize(dxb)) + rows * 8,
+                prec=prec_of(x))
         if dres is not None and not fp32:    # non-fp32 residual stream: plain add (not on the bf16 path)
             dx = dx + dres.to(dx.dtype)
         if dxb is not None:
@@ -257,8 +247,10 @@ class _CarafeFn(torch.autograd.Function):
             raise ValueError("carafe: shape mismatch")
         out = torch.empty(B, L * s * s, C, dtype=x.dtype, device=x.device)
         wsave = torch.empty(B, H, W, 9 * s * s, dtype=torch.float32, device=x.device)
-        check(lib().csu_carafe_fwd(B, H, W, C, s, dtype_code(x), ptr(x), ptr(enc), ptr(out), ptr(wsave),
-                                   stream_ptr(x.device)), "csu_carafe_fwd")
+        e, T = x.element_size(), 9 * s * s
+        _launch("carafe_fwd", lambda: lib().csu_carafe_fwd(B, H, W, C, s, dtype_code(x), ptr(x), ptr(enc), ptr(out),
+                                                           ptr(wsave), stream_ptr(x.device)),
+                B * H * W * s * s * C * 18, B * H * W * (C * e * (1 + s * s) + T * (e + 4)), prec=prec_of(x))
         ctx.save_for_backward(x, wsave)
         ctx.geo = (B, H, W, C, s)
         ctx.enc_dtype = enc.dtype
@@ -271,8 +263,10 @@ class _CarafeFn(torch.autograd.Function):
         dout = dout.to(x.dtype).contiguous()
         dx = torch.empty_like(x)
         denc = torch.empty(B, H, W, 9 * s * s, dtype=x.dtype, device=x.device)
-        check(lib().csu_carafe_bwd(B, H, W, C, s, dtype_code(x), ptr(x), ptr(wsave), ptr(dout), ptr(dx), ptr(denc),
-                                   stream_ptr(x.device)), "csu_carafe_bwd")
+        e, T = x.element_size(), 9 * s * s
+        _launch("carafe_bwd", lambda: lib().csu_carafe_bwd(B, H, W, C, s, dtype_code(x), ptr(x), ptr(wsave), ptr(dout),
+                                                           ptr(dx), ptr(denc), stream_ptr(x.device)),
+                B * H * W * s * s * C * 36, B * H * W * (C * e * (2 + s * s) + T * (4 + e)), prec=prec_of(x))
         return dx, denc, None, None, None
 
 
@@ -289,7 +283,8 @@ class _HeadFn(torch.autograd.Function):
         wf = w.detach().float().contiguous().view(-1)
         P, C = x.numel() // x.shape[-1], x.shape[-1]
         prob = torch.empty(x.shape[:-1], dtype=torch.float32, device=x.device)
-        check(lib().csu_head_fwd(P, C, dtype_code(x), ptr(x), ptr(wf), ptr(prob), stream_ptr(x.device)), "csu_head_fwd")
+        _launch("head_fwd", lambda: lib().csu_head_fwd(P, C, dtype_code(x), ptr(x), ptr(wf), ptr(prob), stream_ptr(x.device)),
+                2 * P * C, P * (C * x.element_size() + 4), prec=prec_of(x))
         ctx.save_for_backward(x, wf, prob)
         ctx.wshape, ctx.wdtype = w.shape, w.dtype
         return prob
@@ -304,8 +299,9 @@ class _HeadFn(torch.autograd.Function):
         L = lib()
         n = L.csu_head_bwd_workspace(P, C)
         work = torch.empty(max(n, 16), dtype=torch.uint8, device=x.device)
-        check(L.csu_head_bwd(P, C, dtype_code(x), ptr(x), ptr(wf), ptr(prob), ptr(dprob), ptr(dx), ptr(dw), ptr(work), n,
-                             stream_ptr(x.device)), "csu_head_bwd")
+        _launch("head_bwd", lambda: L.csu_head_bwd(P, C, dtype_code(x), ptr(x), ptr(wf), ptr(prob), ptr(dprob), ptr(dx),
+                                                   ptr(dw), ptr(work), n, stream_ptr(x.device)),
+                4 * P * C, P * (2 * C * x.element_size() + 8), prec=prec_of(x))
         return dx, dw.view(ctx.wshape).to(ctx.wdtype)
 
 
@@ -325,8 +321,10 @@ class _CarafeHeadFn(torch.autograd.Function):
             raise ValueError("carafe_head: x must be (B, H*W, C) and enc (B, H, W, 9 s^2)")
         z = torch.empty(B * H * W, dtype=torch.float32, device=x.device)
         prob = torch.empty(B, 1, s * H, s * W, dtype=torch.float32, device=x.device)
-        check(lib().csu_carafe_head_fwd(B, H, W, C, s, dtype_code(x), ptr(x), ptr(enc), ptr(uf), ptr(cf), ptr(z),
-                                         ptr(prob), stream_ptr(x.device)), "csu_carafe_head_fwd")
+        e, T = x.element_size(), 9 * s * s
+        _launch("carafe_head_fwd", lambda: lib().csu_carafe_head_fwd(B, H, W, C, s, dtype_code(x), ptr(x), ptr(enc), ptr(uf),
+                                                                     ptr(cf), ptr(z), ptr(prob), stream_ptr(x.device)),
+                B * H * W * (2 * C + 2 * T), B * H * W * (C * e + T * e + 4 + s * s * 4), prec=prec_of(x))
         ctx.save_for_backward(x, enc, z, uf, prob)
         ctx.geo = (B, H, W, C, s)
         ctx.dtypes = (u.dtype, cb.dtype, cb.shape)
@@ -343,9 +341,11 @@ class _CarafeHeadFn(torch.autograd.Function):
         L = lib()
         n = L.csu_carafe_head_bwd_workspace(B, H, W, C, s)
         work = torch.empty(max(n, 16), dtype=torch.uint8, device=x.device)
-        check(L.csu_carafe_head_bwd(B, H, W, C, s, dtype_code(x), ptr(x), ptr(enc), ptr(z), ptr(uf), ptr(prob),
-                                    ptr(dprob), ptr(dx), ptr(denc), ptr(du), ptr(dcb), ptr(work), n,
-                                    stream_ptr(x.device)), "csu_carafe_head_bwd")
+        e, T = x.element_size(), 9 * s * s
+        _launch("carafe_head_bwd", lambda: L.csu_carafe_head_bwd(B, H, W, C, s, dtype_code(x), ptr(x), ptr(enc), ptr(z),
+                                                                 ptr(uf), ptr(prob), ptr(dprob), ptr(dx), ptr(denc), ptr(du),
+                                                                 ptr(dcb), ptr(work), n, stream_ptr(x.device)),
+                B * H * W * (4 * C + 4 * T), B * H * W * (2 * C * e + 2 * T * e + 4 + s * s * 8), prec=prec_of(x))
         udt, cdt, cshape = ctx.dtypes
         return dx, denc, du.to(udt), dcb.to(cdt).reshape(cshape), None, None, None
 
@@ -373,7 +373,9 @@ def colsum(x2: torch.Tensor) -> torch.Tensor:
     L = lib()
     n = L.csu_colsum_workspace(rows, cols, dtype_code(x2))
     work = torch.empty(max(n, 16), dtype=torch.uint8, device=x2.device)
-    check(L.csu_colsum(rows, cols, dtype_code(x2), ptr(x2), ptr(out), ptr(work), n, stream_ptr(x2.device)), "csu_colsum")
+    _launch("colsum", lambda: L.csu_colsum(rows, cols, dtype_code(x2), ptr(x2), ptr(out), ptr(work), n,
+                                           stream_ptr(x2.device)),
+            rows * cols, rows * cols * x2.element_size() + cols * 4, prec=prec_of(x2))
     return out
 
 
@@ -401,8 +403,9 @@ def linear_wgrad(dy2: torch.Tensor, x2: torch.Tensor, out=None, work=None):
         out = torch.empty(N * K + N, dtype=torch.float32, device=dy2.device)
     if work is None:
         work = torch.empty(max(n, 16), dtype=torch.uint8, device=dy2.device)
-    check(L.csu_linear_wgrad(M, N, K, dtype_code(dy2), ptr(dy2), ptr(x2), ptr(out), ptr(work), n,
-                             stream_ptr(dy2.device)), "csu_linear_wgrad")
+    _launch("linear_wgrad", lambda: L.csu_linear_wgrad(M, N, K, dtype_code(dy2), ptr(dy2), ptr(x2), ptr(out), ptr(work), n,
+                                                       stream_ptr(dy2.device)),
+            2 * M * N * K, M * (N + K) * dy2.element_size() + (N * K + N) * 4, prec=prec_of(dy2))
     return out[:N * K].view(N, K), out[N * K:]
 
 
@@ -419,7 +422,9 @@ def gemm(a2: torch.Tensor, b: torch.Tensor, b_trans: bool, out_dtype, bias=None,
     d.M, d.N, d.K, d.a, d.b, d.lda, d.ldb = M, N, K, ptr(a2), ptr(b), a2.stride(0), b.stride(0)
     d.b_trans, d.a_gelu, d.bias, d.gelu_aux, d.resid = int(b_trans), int(a_gelu), ptr(bias), ptr(gelu_aux), ptr(resid)
     d.out, d.gelu_out, d.ldc, d.out_dtype, d.cfg = ptr(out), ptr(g), N, dtype_code(out), int(cfg)
-    check(lib().csu_gemm_ex(ctypes.byref(d), stream_ptr(a2.device)), "csu_gemm_ex")
+    nb = (M * K * a2.element_size() + N * K * b.element_size() + M * N * out.element_size()
+          + (M * N * 2 if gelu_aux is not None else 0) + (M * N * 4 if resid is not None else 0) + (M * N * 2 if gelu_out else 0))
+    _launch("gemm", lambda: lib().csu_gemm_ex(ctypes.byref(d), stream_ptr(a2.device)), 2 * M * N * K, nb, prec=prec_of(a2))
     return (out, g) if gelu_out else out
 
 
@@ -762,8 +767,11 @@ class _MlpFusedFn(torch.autograd.Function):
         x2 = x.reshape(-1, C).contiguous()
         b1f = b1.detach().float().contiguous()
         y = torch.empty_like(res2)
-        check(lib().csu_mlp_fwd(x2.shape[0], C, ptr(x2), ptr(w1c), ptr(b1f), ptr(w2c), ptr(b2.detach().float().contiguous()),
-                                ptr(res2), ptr(y), stream_ptr(x2.device)), "csu_mlp_fwd")
+        M = x2.shape[0]
+        b2f = b2.detach().float().contiguous()
+        _launch("mlp_fwd", lambda: lib().csu_mlp_fwd(M, C, ptr(x2), ptr(w1c), ptr(b1f), ptr(w2c), ptr(b2f), ptr(res2), ptr(y),
+                                                     stream_ptr(x2.device)),
+                16 * M * C * C, M * C * (2 + 4 + 4) + 16 * C * C)
         ctx.save_for_backward(x2, w1c, b1f, w2c)
         ctx.meta = (res.dtype, x.shape, w1.dtype, b1.dtype, w2.dtype, b2.dtype)
         ctx.params = (w1, b1, w2, b2)
@@ -778,8 +786,9 @@ class _MlpFusedFn(torch.autograd.Function):
         dh = torch.empty(M, 4 * C, dtype=torch.bfloat16, device=x2.device)
         g = torch.empty_like(dh)
         dx = torch.empty(M, C, dtype=torch.bfloat16, device=x2.device)
-        check(lib().csu_mlp_bwd(M, C, ptr(x2), ptr(dyb), ptr(w1c), ptr(b1f), ptr(w2c), ptr(dh), ptr(g), ptr(dx),
-                                stream_ptr(x2.device)), "csu_mlp_bwd")
+        _launch("mlp_bwd", lambda: lib().csu_mlp_bwd(M, C, ptr(x2), ptr(dyb), ptr(w1c), ptr(b1f), ptr(w2c), ptr(dh), ptr(g),
+                                                     ptr(dx), stream_ptr(x2.device)),
+                24 * M * C * C, M * C * (2 + 2 + 2) + M * 4 * C * (2 + 2) + 16 * C * C)
         dw2, db2 = wgrad_maybe_side(dyb, g, w2dt, b2dt, params=ctx.params[2:])
         dw1, db1 = wgrad_maybe_side(dh, x2, w1dt, b1dt, params=ctx.params[:2])
         return dy.to(rdt), dx.view(xshape), dw1.to(w1dt), db1.to(b1dt), dw2.to(w2dt), db2.to(b2dt), None, None
@@ -863,8 +872,11 @@ class CastCache:
                 or any(p.data_ptr() != q for p, q in zip(allp, self.ptrs))):
             self._build(params, convs, dtype)
         if self.items is not None:
-            check(lib().csu_cast_bf16_batch(ptr(self.items), len(allp), self.tiles, stream_ptr(allp[0].device)),
-                  "csu_cast_bf16_batch")
+            n = sum(p.numel() for p in allp)
+            nt = sum(p.numel() for p in self.params if p.dim() > 1) + sum(w.numel() for w in self.convs)
+            _launch("cast_bf16_batch", lambda: lib().csu_cast_bf16_batch(ptr(self.items), len(allp), self.tiles,
+                                                                         stream_ptr(allp[0].device)),
+                    0, n * 6 + nt * 2)
             return
         with torch.no_grad():
             if self.params:
@@ -937,8 +949,10 @@ def _conv_wgrad(g, x, dy, dt):
     out = torch.empty(g.N * g.KH * g.KW * g.C + g.N, dtype=torch.float32, device=x.device)
     n = L.csu_conv2d_wgrad_workspace(ctypes.byref(g))
     work = torch.empty(max(n, 16), dtype=torch.uint8, device=x.device)
-    check(L.csu_conv2d_wgrad(ctypes.byref(g), dt, ptr(x), ptr(dy), ptr(out), ptr(work), n, stream_ptr(x.device)),
-          "csu_conv2d_wgrad")
+    _launch("conv_wgrad", lambda: L.csu_conv2d_wgrad(ctypes.byref(g), dt, ptr(x), ptr(dy), ptr(out), ptr(work), n,
+                                                     stream_ptr(x.device)),
+            2 * g.B * g.OH * g.OW * g.N * g.KH * g.KW * g.C,
+            (g.B * g.H * g.W * g.C + g.B * g.OH * g.OW * g.N) * x.element_size() + out.numel() * 4, prec=prec_of(x))
     k = g.N * g.KH * g.KW * g.C
     return out[:k].view(g.N, g.KH, g.KW, g.C), out[k:]
 
@@ -967,8 +981,9 @@ class _Conv2dFn(torch.autograd.Function):
         g = _conv_geom(B, H, W, cp, N, KH, KW, stride, pad)
         y = torch.empty(B, g.OH, g.OW, N, dtype=cd, device=x.device)
         bf = None if bias is None else bias.detach().float().contiguous()
-        check(lib().csu_conv2d_fwd(ctypes.byref(g), dtype_code(xc), ptr(xc), ptr(w_ohwi), ptr(bf), ptr(y),
-                                   stream_ptr(x.device)), "csu_conv2d_fwd")
+        _launch("conv_fwd", lambda: lib().csu_conv2d_fwd(ctypes.byref(g), dtype_code(xc), ptr(xc), ptr(w_ohwi), ptr(bf),
+                                                         ptr(y), stream_ptr(x.device)),
+                2 * y.numel() * KH * KW * cp, (xc.numel() + w_ohwi.numel() + y.numel()) * xc.element_size(), prec=prec_of(xc))
         ctx.save_for_backward(xc, weight)
         ctx.w_ihwo = cached[1] if cached else None   # refreshed only by the next forward's cast
         ctx.bias = bias
@@ -991,8 +1006,10 @@ class _Conv2dFn(torch.autograd.Function):
             else:
                 w_ihwo = ctx.w_ihwo if ctx.w_ihwo is not None else weight.detach().permute(1, 2, 3, 0).to(cd).contiguous()
             dx = torch.empty(B, H, W, cp, dtype=cd, device=dy.device)
-            check(lib().csu_conv2d_dgrad(ctypes.byref(g), dtype_code(dy), ptr(dy), ptr(w_ihwo), None, ptr(dx),
-                                         stream_ptr(dy.device)), "csu_conv2d_dgrad")
+            _launch("conv_dgrad", lambda: lib().csu_conv2d_dgrad(ctypes.byref(g), dtype_code(dy), ptr(dy), ptr(w_ihwo), None,
+                                                                 ptr(dx), stream_ptr(dy.device)),
+                    2 * dy.numel() * KH * KW * cp, (dy.numel() + w_ihwo.numel() + dx.numel()) * dy.element_size(),
+                    prec=prec_of(dy))
             if cp != C:
                 dx = dx[..., :C]
             if dx.dtype != xdt:
@@ -1035,8 +1052,9 @@ class _ConvTranspose2dFn(torch.autograd.Function):
         w_ihwo = weight.detach().permute(1, 2, 3, 0).to(cd).contiguous()
         y = torch.empty(B, OH, OW, C, dtype=cd, device=x.device)
         bf = None if bias is None else bias.detach().float().contiguous()
-        check(lib().csu_conv2d_dgrad(ctypes.byref(g), dtype_code(xc), ptr(xc), ptr(w_ihwo), ptr(bf), ptr(y),
-                                     stream_ptr(x.device)), "csu_conv2d_dgrad (transposed conv)")
+        _launch("convT_fwd", lambda: lib().csu_conv2d_dgrad(ctypes.byref(g), dtype_code(xc), ptr(xc), ptr(w_ihwo), ptr(bf),
+                                                            ptr(y), stream_ptr(x.device)),
+                2 * xc.numel() * KH * KW * C, (xc.numel() + w_ihwo.numel() + y.numel()) * xc.element_size(), prec=prec_of(xc))
         ctx.save_for_backward(xc, weight)
         ctx.conf = (stride, cd, x.dtype, bias is not None, None if bias is None else bias.dtype)
         return y
@@ -1053,8 +1071,10 @@ class _ConvTranspose2dFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             w_ohwi = weight.detach().permute(0, 2, 3, 1).to(cd).contiguous()
             dx = torch.empty(B, H, W, N, dtype=cd, device=dy.device)
-            check(lib().csu_conv2d_fwd(ctypes.byref(g), dtype_code(dy), ptr(dy), ptr(w_ohwi), None, ptr(dx),
-                                       stream_ptr(dy.device)), "csu_conv2d_fwd (transposed conv backward)")
+            _launch("convT_dgrad", lambda: lib().csu_conv2d_fwd(ctypes.byref(g), dtype_code(dy), ptr(dy), ptr(w_ohwi), None,
+                                                                ptr(dx), stream_ptr(dy.device)),
+                    2 * dx.numel() * KH * KW * C, (dy.numel() + w_ohwi.numel() + dx.numel()) * dy.element_size(),
+                    prec=prec_of(dy))
             if dx.dtype != xdt:
                 dx = dx.to(xdt)
         dw, _ = _conv_wgrad(g, dy, xc, dtype_code(dy))   # roles swapped: "input" = dy, "output grad" = x

@@ -12,7 +12,8 @@ import numpy as np
 import torch
 
 from . import _lib
-from ._lib import check, lib, stream_ptr
+from ._lib import lib, stream_ptr
+from .ledger import launch
 
 _ITEM = np.dtype([("param", "<u8"), ("grad", "<u8"), ("exp_avg", "<u8"), ("exp_avg_sq", "<u8"), ("numel", "<i8"),
                   ("chunk0", "<i8")])
@@ -110,9 +111,11 @@ class FusedAdamW(torch.optim.Optimizer):
             _, _, table, n, chunks = self._table(gi, items, dev)
             lr_ptr = gs["lr"].data_ptr() if group["capturable"] else None
             b1, b2 = group["betas"]
-            check(lib().csu_adamw_step(table.data_ptr(), n, chunks, lr_ptr, float(group["lr"]), float(b1), float(b2),
-                                       float(group["eps"]), float(group["weight_decay"]), gs["step"].data_ptr(), 0.0,
-                                       stream_ptr(dev)), "csu_adamw_step")
+            numel = sum(it[4] for it in items)
+            launch("adamw", lambda: lib().csu_adamw_step(table.data_ptr(), n, chunks, lr_ptr, float(group["lr"]), float(b1),
+                                                         float(b2), float(group["eps"]), float(group["weight_decay"]),
+                                                         gs["step"].data_ptr(), 0.0, stream_ptr(dev)),
+                   12 * numel, 28 * numel, idem=False, prec="f32")
         return loss
 
     def state_dict(self):

@@ -10,7 +10,8 @@ from __future__ import annotations
 import torch
 import torch.nn as nn
 
-from ._lib import check, dtype_code, lib, ptr, require_device, stream_ptr
+from ._lib import dtype_code, lib, ptr, require_device, stream_ptr
+from .ledger import launch, prec_of
 
 
 class _SimAMFn(torch.autograd.Function):
@@ -24,8 +25,9 @@ class _SimAMFn(torch.autograd.Function):
         Lb = lib()
         n = Lb.csu_simam_workspace(B, L, C)
         work = torch.empty(max(n, 16), dtype=torch.uint8, device=x.device)
-        check(Lb.csu_simam_fwd(B, L, C, float(lam), dtype_code(x), ptr(x), ptr(y), ptr(stats), ptr(work), n,
-                               stream_ptr(x.device)), "csu_simam_fwd")
+        launch("simam_fwd", lambda: Lb.csu_simam_fwd(B, L, C, float(lam), dtype_code(x), ptr(x), ptr(y), ptr(stats),
+                                                     ptr(work), n, stream_ptr(x.device)),
+               8 * x.numel(), 2 * x.numel() * x.element_size(), prec=prec_of(x))
         ctx.save_for_backward(x, stats)
         return y
 
@@ -38,8 +40,9 @@ class _SimAMFn(torch.autograd.Function):
         Lb = lib()
         n = Lb.csu_simam_workspace(B, L, C)
         work = torch.empty(max(n, 16), dtype=torch.uint8, device=x.device)
-        check(Lb.csu_simam_bwd(B, L, C, dtype_code(x), ptr(x), ptr(stats), ptr(dy), ptr(dx), ptr(work), n,
-                               stream_ptr(x.device)), "csu_simam_bwd")
+        launch("simam_bwd", lambda: Lb.csu_simam_bwd(B, L, C, dtype_code(x), ptr(x), ptr(stats), ptr(dy), ptr(dx),
+                                                     ptr(work), n, stream_ptr(x.device)),
+               16 * x.numel(), 3 * x.numel() * x.element_size(), prec=prec_of(x))
         return dx, None
 
 
