@@ -29,6 +29,7 @@
 //    token r and 4 consecutive features per register group; bias / GELU / GELU' / residual are
 //    elementwise on registers.
 #include "lds_dma.hpp"
+#include "rng.hpp"
 
 #include <cstdlib>
 #include <type_traits>
@@ -38,14 +39,17 @@ namespace {
 
 constexpr int MT = 256;   // threads (4 waves)
 
-#ifdef MLP_TIMING   // debug build only: per-workgroup timestamps of mlp_fwd (s_memrealtime, 100 MHz)
-__device__ unsigned long long mlp_ts[6][4096];
-#define MLP_STAMP(k, v) do { if (threadIdx.x == 0 && blockIdx.x < 4096) mlp_ts[k][blockIdx.x] = (v); } while (0)
-#define MLP_NOW() __builtin_amdgcn_s_memrealtime()
-#else
-#define MLP_STAMP(k, v) do {} while (0)
-#define MLP_NOW() 0ull
-#endif
+// Mlp dropout (cswin:190/193) and DropPath (cswin:368) of one launch: hidden mask on g = gelu(h)
+// (site_hidden, element m * 4C + f), output mask (site_out, element m * C + c) and the per-sample
+// DropPath scale row_scale[m / rows_per_sample] on the Mlp output before the residual add.
+struct MlpDrop {
+    const uint64_t* rng;
+    unsigned site_h, site_o;
+    float p;
+    const float* row_scale;
+    long rps;
+};
+
 constexpr int BM = 64;    // tokens per workgroup
 constexpr int HC = 64;    // hidden features per chunk
 
@@ -101,12 +105,20 @@ __device__ __forceinline__ void exchange_half(f32x16* acc, float* xch, int wave,
         for (int e = 0; e < 16; ++e) acc[U * HT + q][e] += xch[((partner * HT + q) * 16 + e) * 64 + lane];
 }
 
-template <int C, int U>
+template <int C, int U, bool DROP>
 __device__ __forceinline__ void fwd_epilogue(const f32x16* acc, __amdgpu_buffer_rsrc_t rs_res, __amdgpu_buffer_rsrc_t rs_out,
-                                             const float* b2, int tok, bool ok, int h) {
+                                             const float* b2, int tok, bool ok, int h, long mg, const MlpDrop& dd) {
     constexpr int HT = C / 64;
+    float sdp = 1.f;
+    DropoutRng R;
+    if constexpr (DROP) {
+        R = load_rng(dd.rng, dd.site_o, dd.p);
+        if (dd.row_scale) sdp = dd.row_scale[mg / dd.rps];
+    }
 #pragma unroll
-    for (int q = 0; q < HT; ++q)
+    for (int q = 0; q < HT; ++q) {
+        unsigned km = 0xffffu;
+        if constexpr (DROP) if (dd.p > 0.f) km = keep16_crow(R, ((uint64_t)mg * C + (U * HT + q) * 32) >> 3, h);
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
             const int f = (U * HT + q) * 32 + 8 * g + 4 * h;
@@ -115,9 +127,14 @@ __device__ __forceinline__ void fwd_epilogue(const f32x16* acc, __amdgpu_buffer_
             buf_ld4(rs_res, off, rv);
             load4(b2 + f, bv);
 #pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] = acc[U * HT + q][4 * g + e] + bv[e] + rv[e];
+            for (int e = 0; e < 4; ++e) {
+                float z = acc[U * HT + q][4 * g + e] + bv[e];
+                if constexpr (DROP) z *= ((km >> (4 * g + e)) & 1u) ? sdp * R.scale : 0.f;
+                v[e] = z + rv[e];
+            }
             buf_st4(rs_out, off, v);
         }
+    }
 }
 
 template <int C, int U>
@@ -150,12 +167,12 @@ template <int V> using iconst = std::integral_constant<int, V>;
 
 // Forward.  Rings: W1 chunks in 2 stages, W2 chunks in 2 stages.  Step j (after one barrier):
 // DMA W1(j+2), W2(j+1); GEMM1(j+1) on the MFMA pipe while GELU(j) runs on the VALU; GEMM2(j).
-// STORE_H: also write the pre-activation h = fc1(x) (bf16, M x 4C) for a GEMM-form backward
-template <int C, bool STORE_H>
+// DROP: hidden / output dropout and DropPath (MlpDrop)
+template <int C, bool DROP>
 __global__ __launch_bounds__(MT) void mlp_fwd_kernel(long M, const bf16* __restrict__ X, const bf16* __restrict__ W1,
                                                      const float* __restrict__ b1, const bf16* __restrict__ W2,
                                                      const float* __restrict__ b2, const float* __restrict__ res,
-                                                     float* __restrict__ out, bf16* __restrict__ hout) {
+                                                     float* __restrict__ out, MlpDrop dd) {
     constexpr int NCH = 4 * C / HC;     // hidden chunks
     constexpr int KS = C / 16;          // k-steps of GEMM1
     constexpr int TF = C / 32;          // 32-feature output tiles (all C, partial over the hidden half)
@@ -206,50 +223,30 @@ __global__ __launch_bounds__(MT) void mlp_fwd_kernel(long M, const bf16* __restr
     f32x16 acc[TF];
 #pragma unroll
     for (int i = 0; i < TF; ++i) acc[i] = f32x16{};
-    [[maybe_unused]] const unsigned long long t_entry = MLP_NOW();
-#ifdef MLP_TIMING
-    const unsigned long long t_clk0 = __builtin_amdgcn_s_memtime();
-#endif
-    [[maybe_unused]] unsigned long long t_wait = 0;
+    const long mg = m0 + tok;   // global token of this lane (dropout element index)
+    DropoutRng Rh;
+    if constexpr (DROP) Rh = load_rng(dd.rng, dd.site_h, dd.p);
     vmwait<0>();
     lds_sync();
-    MLP_STAMP(1, MLP_NOW() - t_entry);
     f32x16 ha = gemm1(w1r), hb;
 
     // par = j & 1 as a compile-time constant: every LDS address is a per-lane base + immediate
-    const auto rs_h = buf_rsrc(STORE_H ? hout + m0 * 4 * C : nullptr, STORE_H ? rows * 4 * C * 2 : 0);
     auto step = [&](auto more, auto par, int j, const f32x16& cur, f32x16& nxt) {
         constexpr int P = decltype(par)::value;
-#ifndef MLP_EXP_NOBAR
-        const unsigned long long tw = MLP_NOW();
-        // W1(j+1), W2(j): issued one step ago; after them only the previous step's 4 h stores
-        if constexpr (STORE_H) vmwait<4>(); else vmwait<0>();
+        vmwait<0>();                    // W1(j+1), W2(j): issued one step ago
         lds_sync();                     // every wave is past GEMM1(j) and GEMM2(j-1)
-        t_wait += MLP_NOW() - tw;
-#endif
-#ifndef MLP_EXP_NODMA
         if (j + 2 < NCH) dma<D1::NW>(rs_w1, d1.v, (unsigned)(j + 2) * HC * C * 2, w1r + P * IMG, wave);
         if (j + 1 < NCH) dma<D2::NW>(rs_w2, d2.v, (unsigned)(j + 1) * HC * 2, w2r + (1 - P) * IMG, wave);
-#endif
         float bv[16], gv[16];
         bias16(b1s, j * HC + hs, h, bv);
         if constexpr (decltype(more)::value) nxt = gemm1(w1r + (1 - P) * IMG);
 #pragma unroll
-        for (int e = 0; e < 16; ++e) {
-#ifdef MLP_EXP_NOGELU
-            gv[e] = cur[e] + bv[e];
-#else
-            gv[e] = gelu_fast(cur[e] + bv[e]);
-#endif
-        }
-        if constexpr (STORE_H) {   // h of chunk j: features hs + 8g + 4h .. + 3 of token tok
-            const unsigned base = ok ? (unsigned)(tok * 4 * C + j * HC + hs + 4 * h) * 2 : kOOB;
+        for (int e = 0; e < 16; ++e) gv[e] = gelu_fast(cur[e] + bv[e]);
+        if constexpr (DROP) {   // hidden dropout on g (features j*HC + hs + crow(e, h) of token mg)
+            if (dd.p > 0.f) {
+                const unsigned km = keep16_crow(Rh, ((uint64_t)mg * 4 * C + j * HC + hs) >> 3, h);
 #pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                float hv[4];
-#pragma unroll
-                for (int e = 0; e < 4; ++e) hv[e] = cur[4 * g + e] + bv[4 * g + e];
-                buf_st4bf(rs_h, base == kOOB ? kOOB : base + 16 * g, hv);
+                for (int e = 0; e < 16; ++e) gv[e] = ((km >> e) & 1u) ? gv[e] * Rh.scale : 0.f;
             }
         }
         const bf16* w2c = w2r + P * IMG;
@@ -278,8 +275,6 @@ __global__ __launch_bounds__(MT) void mlp_fwd_kernel(long M, const bf16* __restr
     }
     step(bconst<true>{}, iconst<0>{}, j, ha, hb);
     step(bconst<false>{}, iconst<1>{}, j + 1, hb, ha);
-    MLP_STAMP(2, MLP_NOW() - t_entry);
-    MLP_STAMP(3, t_wait);
 
     lds_sync();                         // ring free: partial-sum exchange
     float* xch = reinterpret_cast<float*>(ring);
@@ -287,151 +282,23 @@ __global__ __launch_bounds__(MT) void mlp_fwd_kernel(long M, const bf16* __restr
     const auto rs_out = buf_rsrc(out + m0 * C, rows * C * 4);
     if (u == 0) {
         exchange_half<C, 0>(acc, xch, wave, lane);
-        fwd_epilogue<C, 0>(acc, rs_res, rs_out, b2, tok, ok, h);
+        fwd_epilogue<C, 0, DROP>(acc, rs_res, rs_out, b2, tok, ok, h, mg, dd);
     } else {
         exchange_half<C, 1>(acc, xch, wave, lane);
-        fwd_epilogue<C, 1>(acc, rs_res, rs_out, b2, tok, ok, h);
+        fwd_epilogue<C, 1, DROP>(acc, rs_res, rs_out, b2, tok, ok, h, mg, dd);
     }
-    MLP_STAMP(0, t_entry);
-    MLP_STAMP(4, MLP_NOW() - t_entry);
-#ifdef MLP_TIMING
-    MLP_STAMP(5, __builtin_amdgcn_s_memtime() - t_clk0);   // shader-clock cycles over the same span
-#endif
-}
-
-// Forward, 8 waves (2 per SIMD) for C = 256, where the 4-wave kernel gets one wave per SIMD and
-// runs VALU (GELU) and MFMA back to back.  Wave w: token tile t = w & 1, hidden half u = (w >> 1) & 1
-// of each 64-feature chunk, input-channel half v = w >> 2 of GEMM1 (x fragments: C/2 channels,
-// half the registers).  Per chunk: GEMM1 partial (K = C/2) -> the two v waves swap halves of their
-// partial H through LDS and each finalises 8 of the 16 values (bias, GELU) -> g to a [64][64] LDS
-// image -> GEMM2 by wave (t, f = w >> 1): output features 64 f .. + 63, K = 64 hidden.  Every wave
-// ends with full sums of its 64 features (no final exchange).  Three barriers per chunk.
-template <int C, bool STORE_H>
-__global__ __launch_bounds__(2 * MT) void mlp_fwd8_kernel(long M, const bf16* __restrict__ X, const bf16* __restrict__ W1,
-                                                          const float* __restrict__ b1, const bf16* __restrict__ W2,
-                                                          const float* __restrict__ b2, const float* __restrict__ res,
-                                                          float* __restrict__ out, bf16* __restrict__ hout) {
-    constexpr int NCH = 4 * C / HC;
-    constexpr int KH = C / 2;           // GEMM1 input channels per wave
-    constexpr int KS = KH / 16;
-    constexpr int IMG = HC * C;
-    using D1 = Dma<HC, 2 * C, 8>;
-    using D2 = Dma<C, 2 * HC, 8>;
-    __shared__ __attribute__((aligned(1024))) bf16 ring[4 * IMG];   // W1 stages 0, 1 | W2 stages 0, 1
-    __shared__ __attribute__((aligned(1024))) bf16 gs[BM * HC];     // g of the chunk [token][hidden]
-    __shared__ __attribute__((aligned(16))) float xch[8][8][64];   // partial-H halves
-    __shared__ __attribute__((aligned(16))) float b1s[4 * C];
-    bf16* const w1r = ring;
-    bf16* const w2r = ring + 2 * IMG;
-
-    const long m0 = (long)blockIdx.x * BM;
-    const long rows = M - m0;
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int r = lane & 31, h = lane >> 5;
-    const int t = wave & 1, u = (wave >> 1) & 1, v = wave >> 2, f = wave >> 1;
-    const int tok = 32 * t + r;
-    const bool ok = tok < rows;
-    const int hs = 32 * u;
-    for (int i = threadIdx.x; i < 4 * C; i += 2 * MT) b1s[i] = b1[i];
-    bf16x8 xf[KS];
-    {
-        const auto rs = buf_rsrc(X + m0 * C, rows * C * 2);
-#pragma unroll
-        for (int s = 0; s < KS; ++s) {
-            const u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(rs, ok ? (unsigned)(tok * C + v * KH + 16 * s + 8 * h) * 2 : kOOB, 0, 0);
-            __builtin_memcpy(&xf[s], &q, 16);
-        }
-    }
-    D1 d1;
-    D2 d2;
-    d1.init(C, wave, lane);
-    d2.init(4 * C, wave, lane);
-    const i32x4 rs_w1 = rsrc4(W1, 4L * C * C * 2);
-    const i32x4 rs_w2 = rsrc4(W2, 4L * C * C * 2);
-    const auto rs_h = buf_rsrc(STORE_H ? hout + m0 * 4 * C : nullptr, STORE_H ? rows * 4 * C * 2 : 0);
-    asm volatile("" ::: "memory");
-    dma<D1::NW>(rs_w1, d1.v, 0, w1r, wave);
-    dma<D2::NW>(rs_w2, d2.v, 0, w2r, wave);
-
-    f32x16 acc[2] = {f32x16{}, f32x16{}};
-    for (int j = 0; j < NCH; ++j) {
-        const int P = j & 1;
-        vmwait<STORE_H ? 2 : 0>();      // chunk j landed (after it: only chunk j-1's 2 h stores)
-        lds_sync();                     // all waves past chunk j-1: its stages and gs are free
-        if (j + 1 < NCH) {
-            dma<D1::NW>(rs_w1, d1.v, (unsigned)(j + 1) * HC * C * 2, w1r + (1 - P) * IMG, wave);
-            dma<D2::NW>(rs_w2, d2.v, (unsigned)(j + 1) * HC * 2, w2r + (1 - P) * IMG, wave);
-        }
-        const bf16* w1c = w1r + P * IMG;
-        const bf16* w2c = w2r + P * IMG;
-        bf16x8 wf[KS];
-#pragma unroll
-        for (int s = 0; s < KS; ++s) wf[s] = frag(w1c, moff<2 * C>(hs + r, v * KH + 16 * s + 8 * h));
-        __builtin_amdgcn_sched_barrier(0);
-        f32x16 hp = f32x16{};
-#pragma unroll
-        for (int s = 0; s < KS; ++s) hp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[s], xf[s], hp, 0, 0, 0);
-        // swap halves: this wave finalises registers 8v .. 8v+7, the partner (w ^ 4) the others
-#pragma unroll
-        for (int e = 0; e < 8; ++e) xch[wave][e][lane] = hp[8 * (1 - v) + e];
-        lds_sync();
-        float hv[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) hv[e] = hp[8 * v + e] + xch[wave ^ 4][e][lane] + b1s[j * HC + hs + crow(8 * v + e, h)];
-        if constexpr (STORE_H) {
-            const unsigned base = ok ? (unsigned)(tok * 4 * C + j * HC + hs + 16 * v + 4 * h) * 2 : kOOB;
-            buf_st4bf(rs_h, base, hv);
-            buf_st4bf(rs_h, base == kOOB ? kOOB : base + 16, hv + 4);
-        }
-#pragma unroll
-        for (int g2 = 0; g2 < 2; ++g2) {   // register groups 2v + g2: hidden hs + 8 (2v + g2) + 4h .. + 3
-            float gv[4];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) gv[e] = gelu_fast(hv[4 * g2 + e]);
-            const bf16x4 b = {(bf16)gv[0], (bf16)gv[1], (bf16)gv[2], (bf16)gv[3]};
-            *reinterpret_cast<bf16x4*>(gs + moff<2 * HC>(tok, hs + 8 * (2 * v + g2) + 4 * h)) = b;
-        }
-        lds_sync();
-        bf16x8 gf[HC / 16], af[2][HC / 16];
-#pragma unroll
-        for (int s = 0; s < HC / 16; ++s) {
-            gf[s] = frag(gs, moff<2 * HC>(tok, 16 * s + 8 * h));
-#pragma unroll
-            for (int ft = 0; ft < 2; ++ft) af[ft][s] = frag(w2c, moff<2 * HC>(64 * f + 32 * ft + r, 16 * s + 8 * h));
-        }
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int s = 0; s < HC / 16; ++s)
-#pragma unroll
-            for (int ft = 0; ft < 2; ++ft) acc[ft] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[ft][s], gf[s], acc[ft], 0, 0, 0);
-    }
-    // y[token][feature] = acc + b2 + res; lane: token tok, features 64 f + 32 ft + 8 g + 4 h .. + 3
-    const auto rs_res = buf_rsrc(res + m0 * C, rows * C * 4);
-    const auto rs_out = buf_rsrc(out + m0 * C, rows * C * 4);
-#pragma unroll
-    for (int ft = 0; ft < 2; ++ft)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            const int fe = 64 * f + 32 * ft + 8 * g + 4 * h;
-            const unsigned off = ok ? (unsigned)(tok * C + fe) * 4 : kOOB;
-            float rv[4], bv[4], o[4];
-            buf_ld4(rs_res, off, rv);
-            load4(b2 + fe, bv);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) o[e] = acc[ft][4 * g + e] + bv[e] + rv[e];
-            buf_st4(rs_out, off, o);
-        }
 }
 
 // Backward.  Rings: W1 chunks in 3 stages (GEMM1 of chunk j+1 and GEMM4 of chunk j overlap, plus
 // the prefetch), W2 chunks in 2.  Step j (after one barrier): DMA W1(j+2), W2(j+2); GEMM1/GEMM3 of
 // chunk j+1 on the MFMA pipe while chunk j's GELU / GELU' / g, dH stores run on the VALU; GEMM4(j).
-template <int C>
+// DROP: dY is the gradient of the dropped fc2 output (the output mask / DropPath were applied by
+// the caller); the hidden mask is regenerated here: g stored = gelu(h) * mask, dH = (W2^T dY) * mask * gelu'(h).
+template <int C, bool DROP>
 __global__ __launch_bounds__(MT) void mlp_bwd_kernel(long M, const bf16* __restrict__ X, const bf16* __restrict__ dY,
                                                      const bf16* __restrict__ W1, const float* __restrict__ b1,
                                                      const bf16* __restrict__ W2, bf16* __restrict__ dH,
-                                                     bf16* __restrict__ G, bf16* __restrict__ dX) {
+                                                     bf16* __restrict__ G, bf16* __restrict__ dX, MlpDrop dd) {
     constexpr int NCH = 4 * C / HC;
     constexpr int KS = C / 16;
     constexpr int TF = C / 32;
@@ -510,12 +377,22 @@ __global__ __launch_bounds__(MT) void mlp_bwd_kernel(long M, const bf16* __restr
 #pragma unroll
     for (int i = 0; i < TF; ++i) acc[i] = f32x16{};
     // chunk j's epilogue (GELU, GELU', g / dH stores: 8 per wave) and GEMM4 (dx += W1_sub^T dH^T)
+    const long mg = m0 + tok;
+    DropoutRng Rh;
+    if constexpr (DROP) Rh = load_rng(dd.rng, dd.site_h, dd.p);
     auto finish = [&](int j, const f32x16& hc, const f32x16& gc, const float* bv, const bf16* w1c) {
         float gv[16], dv[16];
+        unsigned km = 0xffffu;
+        if constexpr (DROP) if (dd.p > 0.f) km = keep16_crow(Rh, ((uint64_t)mg * 4 * C + j * HC + hs) >> 3, h);
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
             float dg;
             gelu_pair_fast(hc[e] + bv[e], gv[e], dg);
+            if constexpr (DROP) {
+                const float ms = ((km >> e) & 1u) ? Rh.scale : 0.f;
+                gv[e] *= ms;                 // the dropped g feeds dW2
+                dg *= ms;
+            }
             dv[e] = gc[e] * dg;
         }
         const unsigned base = ok ? (unsigned)(tok * 4 * C + j * HC + hs + 4 * h) * 2 : kOOB;
@@ -596,47 +473,28 @@ __global__ __launch_bounds__(MT) void mlp_bwd_kernel(long M, const bf16* __restr
 }
 
 
-// CSU_MLP8=1 selects the 8-wave forward at C = 256.  Opt-in: parity-green but not faster
-// (43.3 vs 40-45 us per launch, 991 vs 997-1004 img/s on the graphed step, A/B r01ae)
-static bool use_fwd8() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("CSU_MLP8");
-        v = e ? atoi(e) : 0;
-    }
-    return v != 0;
-}
-
 template <int C>
 int fwd_launch(long M, const void* x, const void* w1, const float* b1, const void* w2, const float* b2, const float* res,
-               float* out, void* h, hipStream_t st) {
+               float* out, const MlpDrop* d, hipStream_t st) {
     const dim3 grid((unsigned)((M + BM - 1) / BM));
-    if constexpr (C == 256) {
-        if (use_fwd8()) {
-            if (h)
-                mlp_fwd8_kernel<C, true><<<grid, 2 * MT, 0, st>>>(M, (const bf16*)x, (const bf16*)w1, b1, (const bf16*)w2, b2,
-                                                                  res, out, (bf16*)h);
-            else
-                mlp_fwd8_kernel<C, false><<<grid, 2 * MT, 0, st>>>(M, (const bf16*)x, (const bf16*)w1, b1, (const bf16*)w2, b2,
-                                                                   res, out, nullptr);
-            return check_launch("mlp_fwd8");
-        }
-    }
-    if (h)
-        mlp_fwd_kernel<C, true><<<grid, MT, 0, st>>>(M, (const bf16*)x, (const bf16*)w1, b1, (const bf16*)w2, b2, res, out,
-                                                     (bf16*)h);
+    if (d)
+        mlp_fwd_kernel<C, true><<<grid, MT, 0, st>>>(M, (const bf16*)x, (const bf16*)w1, b1, (const bf16*)w2, b2, res, out, *d);
     else
         mlp_fwd_kernel<C, false><<<grid, MT, 0, st>>>(M, (const bf16*)x, (const bf16*)w1, b1, (const bf16*)w2, b2, res, out,
-                                                      nullptr);
+                                                      MlpDrop{});
     return check_launch("mlp_fwd");
 }
 
 template <int C>
 int bwd_launch(long M, const void* x, const void* dy, const void* w1, const float* b1, const void* w2, void* dh, void* g,
-               void* dx, hipStream_t st) {
-    mlp_bwd_kernel<C><<<dim3((unsigned)((M + BM - 1) / BM)), MT, 0, st>>>(M, (const bf16*)x, (const bf16*)dy,
-                                                                          (const bf16*)w1, b1, (const bf16*)w2, (bf16*)dh,
-                                                                          (bf16*)g, (bf16*)dx);
+               void* dx, const MlpDrop* d, hipStream_t st) {
+    const dim3 grid((unsigned)((M + BM - 1) / BM));
+    if (d)
+        mlp_bwd_kernel<C, true><<<grid, MT, 0, st>>>(M, (const bf16*)x, (const bf16*)dy, (const bf16*)w1, b1, (const bf16*)w2,
+                                                     (bf16*)dh, (bf16*)g, (bf16*)dx, *d);
+    else
+        mlp_bwd_kernel<C, false><<<grid, MT, 0, st>>>(M, (const bf16*)x, (const bf16*)dy, (const bf16*)w1, b1, (const bf16*)w2,
+                                                      (bf16*)dh, (bf16*)g, (bf16*)dx, MlpDrop{});
     return check_launch("mlp_bwd");
 }
 
@@ -647,42 +505,54 @@ using namespace csu;
 
 extern "C" int csu_mlp_supported(int C) { return C == 64 || C == 128 || C == 256; }
 
-extern "C" int csu_mlp_fwd_ex(long M, int C, const void* x, const void* w1, const float* b1, const void* w2,
-                              const float* b2, const float* res, float* out, void* h, void* stream);
+static int mlp_drop_of(const csu_mlp_dropout* d, MlpDrop& md) {
+    if (!d) return 0;
+    if (d->p < 0.f || d->p >= 1.f || (d->p > 0.f && !d->rng) || (d->row_scale && d->rows_per_sample < 1))
+        return fail(CSU_E_ARG, "mlp: bad dropout descriptor (0 <= p < 1, rng for p > 0, rows_per_sample >= 1)");
+    md = MlpDrop{d->rng, d->site_hidden, d->site_out, d->p, d->row_scale, (long)d->rows_per_sample};
+    return d->p > 0.f || d->row_scale ? 0 : 1;   // 1: nothing to apply -> the dropout-free kernel
+}
+
+extern "C" int csu_mlp_fwd_dp(long M, int C, const void* x, const void* w1, const float* b1, const void* w2, const float* b2,
+                              const float* res, float* out, const csu_mlp_dropout* d, void* stream) {
+    if (M < 1 || !x || !w1 || !b1 || !w2 || !b2 || !res || !out) return fail(CSU_E_ARG, "mlp_fwd: bad arguments");
+    if (M * 4L * C * 2 > 0x7fffffffL) return fail(CSU_E_ARG, "mlp_fwd: tensor exceeds 2 GB buffer range");
+    MlpDrop md{};
+    const int e = mlp_drop_of(d, md);
+    if (e < 0) return e;
+    const MlpDrop* dp = d && e == 0 ? &md : nullptr;
+    const hipStream_t st = as_stream(stream);
+    switch (C) {
+        case 64: return fwd_launch<64>(M, x, w1, b1, w2, b2, res, out, dp, st);
+        case 128: return fwd_launch<128>(M, x, w1, b1, w2, b2, res, out, dp, st);
+        case 256: return fwd_launch<256>(M, x, w1, b1, w2, b2, res, out, dp, st);
+        default: return fail(CSU_E_ARG, "mlp_fwd: C must be 64, 128 or 256");
+    }
+}
 
 extern "C" int csu_mlp_fwd(long M, int C, const void* x, const void* w1, const float* b1, const void* w2, const float* b2,
                            const float* res, float* out, void* stream) {
-    return csu_mlp_fwd_ex(M, C, x, w1, b1, w2, b2, res, out, nullptr, stream);
+    return csu_mlp_fwd_dp(M, C, x, w1, b1, w2, b2, res, out, nullptr, stream);
 }
 
-extern "C" int csu_mlp_fwd_ex(long M, int C, const void* x, const void* w1, const float* b1, const void* w2,
-                              const float* b2, const float* res, float* out, void* h, void* stream) {
-    if (M < 1 || !x || !w1 || !b1 || !w2 || !b2 || !res || !out) return fail(CSU_E_ARG, "mlp_fwd: bad arguments");
-    if (M * 4L * C * 2 > 0x7fffffffL) return fail(CSU_E_ARG, "mlp_fwd: tensor exceeds 2 GB buffer range");
+extern "C" int csu_mlp_bwd_dp(long M, int C, const void* x, const void* dy, const void* w1, const float* b1, const void* w2,
+                              void* dh, void* g, void* dx, const csu_mlp_dropout* d, void* stream) {
+    if (M < 1 || !x || !dy || !w1 || !b1 || !w2 || !dh || !g || !dx) return fail(CSU_E_ARG, "mlp_bwd: bad arguments");
+    if (M * 4L * C * 2 > 0x7fffffffL) return fail(CSU_E_ARG, "mlp_bwd: tensor exceeds 2 GB buffer range");
+    MlpDrop md{};
+    const int e = mlp_drop_of(d, md);
+    if (e < 0) return e;
+    const MlpDrop* dp = d && e == 0 ? &md : nullptr;
     const hipStream_t st = as_stream(stream);
     switch (C) {
-        case 64: return fwd_launch<64>(M, x, w1, b1, w2, b2, res, out, h, st);
-        case 128: return fwd_launch<128>(M, x, w1, b1, w2, b2, res, out, h, st);
-        case 256: return fwd_launch<256>(M, x, w1, b1, w2, b2, res, out, h, st);
-        default: return fail(CSU_E_ARG, "mlp_fwd: C must be 64, 128 or 256");
+        case 64: return bwd_launch<64>(M, x, dy, w1, b1, w2, dh, g, dx, dp, st);
+        case 128: return bwd_launch<128>(M, x, dy, w1, b1, w2, dh, g, dx, dp, st);
+        case 256: return bwd_launch<256>(M, x, dy, w1, b1, w2, dh, g, dx, dp, st);
+        default: return fail(CSU_E_ARG, "mlp_bwd: C must be 64, 128 or 256");
     }
 }
 
 extern "C" int csu_mlp_bwd(long M, int C, const void* x, const void* dy, const void* w1, const float* b1, const void* w2,
                            void* dh, void* g, void* dx, void* stream) {
-    if (M < 1 || !x || !dy || !w1 || !b1 || !w2 || !dh || !g || !dx) return fail(CSU_E_ARG, "mlp_bwd: bad arguments");
-    if (M * 4L * C * 2 > 0x7fffffffL) return fail(CSU_E_ARG, "mlp_bwd: tensor exceeds 2 GB buffer range");
-    const hipStream_t st = as_stream(stream);
-    switch (C) {
-        case 64: return bwd_launch<64>(M, x, dy, w1, b1, w2, dh, g, dx, st);
-        case 128: return bwd_launch<128>(M, x, dy, w1, b1, w2, dh, g, dx, st);
-        case 256: return bwd_launch<256>(M, x, dy, w1, b1, w2, dh, g, dx, st);
-        default: return fail(CSU_E_ARG, "mlp_bwd: C must be 64, 128 or 256");
-    }
+    return csu_mlp_bwd_dp(M, C, x, dy, w1, b1, w2, dh, g, dx, nullptr, stream);
 }
-
-#ifdef MLP_TIMING
-extern "C" int csu_debug_mlp_ts(unsigned long long* host, int n) {
-    return hipMemcpyFromSymbol(host, HIP_SYMBOL(csu::mlp_ts), (size_t)n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : 1;
-}
-#endif

@@ -20,6 +20,7 @@
 #include <cstdlib>
 
 #include "common.hpp"
+#include "rng.hpp"
 
 #include <type_traits>
 
@@ -216,10 +217,57 @@ __device__ __forceinline__ size_t stat_index(const csu_stripe_args& a, const Win
     return ((size_t)(w.br * a.B + w.b) * a.heads + w.h) * L + tok;
 }
 
+// ---- attention dropout (attn_drop on P, cswin:290) -------------------------------------------
+// Element (query q, key k) of the window-head has index wbase + q * Npad + k (csu.h), Npad = N
+// rounded up to 32, so every 32-key tile starts a group of 8 (rng.hpp: one Philox call = 8 keys).
+struct ADrop {
+    DropoutRng R;
+    uint64_t wbase;
+    int npad;
+};
+
+__device__ __forceinline__ ADrop attn_drop(const csu_stripe_args& a, const Win& w) {
+    ADrop d;
+    d.R = load_rng(a.drop_rng, a.drop_site + (unsigned)w.br, a.drop_p);
+    d.npad = (w.N + 31) & ~31;
+    const int nwx = a.reso / w.W_sp, nwin = (a.reso / w.H_sp) * nwx;
+    d.wbase = (((uint64_t)w.b * nwin + (uint64_t)w.wy * nwx + w.wx) * a.heads + w.h) * (uint64_t)w.N * d.npad;
+    return d;
+}
+
+// lane = query orientation: keep bits (bit i) of the 16 keys kt + crow(i, h) of query q (kt % 8 == 0)
+__device__ __forceinline__ unsigned keep_q16(const ADrop& d, int q, int kt, int h) {
+    return keep16_crow(d.R, (d.wbase + (uint64_t)q * d.npad + kt) >> 3, h);
+}
+
+// lane = key orientation: keep bits (bit i) of key kt + (lane & 31) for the 16 queries qb + crow(i, h)
+// (kt % 8 == 0).  The tile's 32 queries x 4 key groups = 128 Philox calls are spread over the 64
+// lanes and exchanged through `tbl`, 128 B of LDS private to this wave.
+__device__ __forceinline__ unsigned keep_k16(const ADrop& d, int qb, int kt, int lane, unsigned char* tbl) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int c = 2 * lane + j, qq = c >> 2, g = c & 3;
+        tbl[g * 32 + qq] = (unsigned char)keep8(d.R, ((d.wbase + (uint64_t)(qb + qq) * d.npad + kt) >> 3) + g);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    const int r = lane & 31, h = lane >> 5, b = r & 7;
+    const unsigned* t32 = reinterpret_cast<const unsigned*>(tbl + (r >> 3) * 32 + 4 * h);
+    unsigned m = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const unsigned wd = t32[2 * j];   // queries crow(4j + t, h) = 8j + 4h + t, t = 0..3
+#pragma unroll
+        for (int t = 0; t < 4; ++t) m |= ((wd >> (8 * t + b)) & 1u) << (4 * j + t);
+    }
+    asm volatile("" ::: "memory");   // the reads stay ahead of the next tile's writes
+    return m;
+}
+
 // =============================================================================================
 // Forward
 // =============================================================================================
-template <typename T>
+template <typename T, bool DROP>
 __global__ __launch_bounds__(NT) void stripe_fwd(csu_stripe_args a, const T* __restrict__ qkv,
                                                  T* __restrict__ out, float* __restrict__ lse) {
     __shared__ __attribute__((aligned(16))) T Ks[KC * Cfg<T>::KSTR];
@@ -243,6 +291,8 @@ __global__ __launch_bounds__(NT) void stripe_fwd(csu_stripe_args a, const T* __r
     const float c = a.scale * kLog2e;
     float m = -INFINITY, l = 0.f;
     f32x16 o = {};
+    ADrop dr;
+    if constexpr (DROP) dr = attn_drop(a, w);
 
     for (int k0 = 0; k0 < w.N; k0 += KC) {
         __syncthreads();
@@ -274,6 +324,11 @@ __global__ __launch_bounds__(NT) void stripe_fwd(csu_stripe_args a, const T* __r
             l = l * alpha + ls;
 #pragma unroll
             for (int i = 0; i < 16; ++i) o[i] *= alpha;
+            if constexpr (DROP) {   // the normaliser l keeps every key; O sees the dropped P
+                const unsigned km = keep_q16(dr, qn, k0 + kb, h);
+#pragma unroll
+                for (int i = 0; i < 16; ++i) s[i] = ((km >> i) & 1u) ? s[i] * dr.R.scale : 0.f;
+            }
             mma_acc_operand(o, Vt, kb, r, h, s);
         }
     }
@@ -297,7 +352,7 @@ __global__ __launch_bounds__(NT) void stripe_fwd(csu_stripe_args a, const T* __r
 // =============================================================================================
 // Backward, query owner: delta = rowsum(dO * O_attn), dQ
 // =============================================================================================
-template <typename T>
+template <typename T, bool DROP>
 __global__ __launch_bounds__(NT) void stripe_bwd_dq(csu_stripe_args a, const T* __restrict__ qkv,
                                                     const T* __restrict__ out, const T* __restrict__ dout,
                                                     const float* __restrict__ lse, float* __restrict__ delta,
@@ -347,6 +402,8 @@ __global__ __launch_bounds__(NT) void stripe_bwd_dq(csu_stripe_args a, const T* 
 
     const float c = a.scale * kLog2e;
     f32x16 dq = {};
+    ADrop dr;
+    if constexpr (DROP) dr = attn_drop(a, w);
     for (int k0 = 0; k0 < w.N; k0 += KC) {
         __syncthreads();
         stage_rows<T>(w, a.reso, img, C3, C + w.chq, k0, w.N, Ks, Kt);
@@ -358,11 +415,15 @@ __global__ __launch_bounds__(NT) void stripe_bwd_dq(csu_stripe_args a, const T* 
             f32x16 s = {}, dp = {};
             mma_rows(s, Ks + kb * Cfg<T>::KSTR, r, h, qf);
             mma_rows(dp, Vs + kb * Cfg<T>::KSTR, r, h, gf);
+            unsigned km = 0xffffu;
+            if constexpr (DROP) km = keep_q16(dr, qn, k0 + kb, h);
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
                 const bool kv = k0 + kb + crow(i, h) < w.N;
                 const float p = kv ? exp2f(s[i] * c - lq) : 0.f;
-                s[i] = p * (dp[i] - dl);   // dS^T
+                float g = dp[i];
+                if constexpr (DROP) g = ((km >> i) & 1u) ? g * dr.R.scale : 0.f;   // dP through the mask
+                s[i] = p * (g - dl);   // dS^T
             }
             mma_acc_operand(dq, Kt, kb, r, h, s);
         }
@@ -382,7 +443,7 @@ __global__ __launch_bounds__(NT) void stripe_bwd_dq(csu_stripe_args a, const T* 
 // =============================================================================================
 // Backward, key owner: dK, dV (+ LePE input gradient)
 // =============================================================================================
-template <typename T>
+template <typename T, bool DROP>
 __global__ __launch_bounds__(NT) void stripe_bwd_dkdv(csu_stripe_args a, const T* __restrict__ qkv,
                                                       const T* __restrict__ dout, const float* __restrict__ lse,
                                                       const float* __restrict__ delta, T* __restrict__ dqkv) {
@@ -392,6 +453,7 @@ __global__ __launch_bounds__(NT) void stripe_bwd_dkdv(csu_stripe_args a, const T
     __shared__ __attribute__((aligned(16))) T Gt[HD * Cfg<T>::VSTR];
     __shared__ float lse_s[KC], dl_s[KC];
     __shared__ float wts[HD * 10];
+    __shared__ __attribute__((aligned(16))) unsigned char dtbl[4][128];
 
     const Win w = decode_block(a);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -411,6 +473,8 @@ __global__ __launch_bounds__(NT) void stripe_bwd_dkdv(csu_stripe_args a, const T
 
     const float c = a.scale * kLog2e;
     f32x16 dk = {}, dv = {};
+    ADrop dr;
+    if constexpr (DROP) dr = attn_drop(a, w);
     for (int q0 = 0; q0 < w.N; q0 += KC) {
         __syncthreads();
         stage_rows<T>(w, a.reso, img, C3, w.chq, q0, w.N, Qs, Qt);
@@ -429,12 +493,20 @@ __global__ __launch_bounds__(NT) void stripe_bwd_dkdv(csu_stripe_args a, const T
             f32x16 s = {}, dp = {};
             mma_rows(s, Qs + qb * Cfg<T>::KSTR, r, h, kf);    // S[q][key]
             mma_rows(dp, Gs + qb * Cfg<T>::KSTR, r, h, vf);   // dP[q][key]
+            unsigned km = 0xffffu;
+            if constexpr (DROP) km = keep_k16(dr, q0 + qb, w.blk * QR + wave * 32, lane, dtbl[wave]);
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
                 const int qi = qb + crow(i, h);
                 const float p = exp2f(s[i] * c - lse_s[qi]);
-                s[i] = p;
-                dp[i] = p * (dp[i] - dl_s[qi]);   // dS
+                float ps = p, g = dp[i];
+                if constexpr (DROP) {
+                    const float ms = ((km >> i) & 1u) ? dr.R.scale : 0.f;
+                    ps = p * ms;
+                    g *= ms;
+                }
+                s[i] = ps;                         // dropped P: dV^T += dO^T P_drop
+                dp[i] = p * (g - dl_s[qi]);        // dS
             }
             mma_acc_operand(dv, Gt, qb, r, h, s);    // dV^T += dO^T P
             mma_acc_operand(dk, Qt, qb, r, h, dp);   // dK^T += Q^T dS
@@ -711,6 +783,7 @@ __device__ __forceinline__ Win decode_w(const csu_stripe_args& a, int split) {
     return w;
 }
 
+template <bool DROP>
 __global__ __launch_bounds__(NT) void stripe_fwd_w(csu_stripe_args a, int split, const bf16* __restrict__ qkv,
                                                    bf16* __restrict__ out, float* __restrict__ lse) {
     __shared__ __attribute__((aligned(16))) bf16 Ks[WMAX * HD];
@@ -735,6 +808,8 @@ __global__ __launch_bounds__(NT) void stripe_fwd_w(csu_stripe_args a, int split,
     stage_win2(w, a.reso, img, C3, C + w.chq, img, C3, 2 * C + w.chq, (npad + 63) & ~63, Ks, Vs);  // zero rows up to a 64-key step
     __syncthreads();
     const float c = a.scale * kLog2e;
+    ADrop dr;
+    if constexpr (DROP) dr = attn_drop(a, w);
     for (int q0 = qbeg + 32 * wave; q0 < qend; q0 += 128) {
         const int qn = q0 + r;
         const bool qvalid = qn < w.N;
@@ -786,6 +861,14 @@ __global__ __launch_bounds__(NT) void stripe_fwd_w(csu_stripe_args a, int split,
                 const f2 ov = f2{o[i], o[i + 1]} * al;
                 o[i] = ov.x; o[i + 1] = ov.y;
             }
+            if constexpr (DROP) {   // the normaliser l keeps every key; O sees the dropped P
+                const unsigned k0m = keep_q16(dr, qn, kb, h), k1m = keep_q16(dr, qn, kb + 32, h);
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    s0[i] = ((k0m >> i) & 1u) ? s0[i] * dr.R.scale : 0.f;
+                    s1[i] = ((k1m >> i) & 1u) ? s1[i] * dr.R.scale : 0.f;
+                }
+            }
             mma_acc_sw(o, Vs, kb, lane, s0);
             mma_acc_sw(o, Vs, kb + 32, lane, s1);
         };
@@ -809,6 +892,7 @@ __global__ __launch_bounds__(NT) void stripe_fwd_w(csu_stripe_args a, int split,
     }
 }
 
+template <bool DROP>
 __global__ __launch_bounds__(NT) void stripe_bwd_dq_w(csu_stripe_args a, int split, const bf16* __restrict__ qkv,
                                                       const bf16* __restrict__ out, const bf16* __restrict__ dout,
                                                       const float* __restrict__ lse, float* __restrict__ delta,
@@ -838,6 +922,8 @@ __global__ __launch_bounds__(NT) void stripe_bwd_dq_w(csu_stripe_args a, int spl
     stage_win2(w, a.reso, img, C3, C + w.chq, img, C3, 2 * C + w.chq, npad, Ks, Vs);
     __syncthreads();
     const float c = a.scale * kLog2e;
+    ADrop dr;
+    if constexpr (DROP) dr = attn_drop(a, w);
     for (int q0 = qbeg + 32 * wave; q0 < qend; q0 += 128) {
         const int qn = q0 + r;
         const bool qvalid = qn < w.N;
@@ -873,6 +959,11 @@ __global__ __launch_bounds__(NT) void stripe_bwd_dq_w(csu_stripe_args a, int spl
             f32x16 s = {}, dp = {};
             mma_rows_sw(s, Ks, kb, r, h, qf);
             mma_rows_sw(dp, Vs, kb, r, h, gf);
+            if constexpr (DROP) {   // dP through the mask
+                const unsigned km = keep_q16(dr, qn, kb, h);
+#pragma unroll
+                for (int i = 0; i < 16; ++i) dp[i] = ((km >> i) & 1u) ? dp[i] * dr.R.scale : 0.f;
+            }
 #pragma unroll
             for (int i = 0; i < 16; i += 2) {   // dS = P dP - P delta, packed pairs
                 f2 p = f2{s[i], s[i + 1]} * cc - lq2;
@@ -896,6 +987,7 @@ __global__ __launch_bounds__(NT) void stripe_bwd_dq_w(csu_stripe_args a, int spl
     }
 }
 
+template <bool DROP>
 __global__ __launch_bounds__(NT) void stripe_bwd_dkdv_w(csu_stripe_args a, int split, const bf16* __restrict__ qkv,
                                                         const bf16* __restrict__ dout, const float* __restrict__ lse,
                                                         const float* __restrict__ delta, bf16* __restrict__ dqkv) {
@@ -903,6 +995,7 @@ __global__ __launch_bounds__(NT) void stripe_bwd_dkdv_w(csu_stripe_args a, int s
     __shared__ __attribute__((aligned(16))) bf16 Gs[WMAX * HD];
     __shared__ __attribute__((aligned(16))) float lse_s[WMAX], dl_s[WMAX];
     __shared__ float wts[HD * 10];
+    __shared__ __attribute__((aligned(16))) unsigned char dtbl[4][128];
     const Win w = decode_w(a, split);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int r = lane & 31, h = lane >> 5;
@@ -930,6 +1023,8 @@ __global__ __launch_bounds__(NT) void stripe_bwd_dkdv_w(csu_stripe_args a, int s
     }
     __syncthreads();
     const float c = a.scale * kLog2e;
+    ADrop dr;
+    if constexpr (DROP) dr = attn_drop(a, w);
     for (int k0 = kbeg + 32 * wave; k0 < kend; k0 += 128) {
         const int kn = k0 + r;
         const bool kvalid = kn < w.N;
@@ -948,6 +1043,12 @@ __global__ __launch_bounds__(NT) void stripe_bwd_dkdv_w(csu_stripe_args a, int s
             f32x16 s = {}, dp = {};
             mma_rows_sw(s, Qs, qb, r, h, kf);
             mma_rows_sw(dp, Gs, qb, r, h, vf);
+            unsigned km = 0xffffu;
+            if constexpr (DROP) {
+                km = keep_k16(dr, qb, k0, lane, dtbl[wave]);
+#pragma unroll
+                for (int i = 0; i < 16; ++i) dp[i] = ((km >> i) & 1u) ? dp[i] * dr.R.scale : 0.f;
+            }
 #pragma unroll
             for (int g4 = 0; g4 < 4; ++g4) {   // rows qb + 8 g4 + 4 h + 0..3: one 16-B LDS read each
                 const f32x4 lq = *reinterpret_cast<const f32x4*>(lse_s + qb + 8 * g4 + 4 * h);
@@ -958,7 +1059,12 @@ __global__ __launch_bounds__(NT) void stripe_bwd_dkdv_w(csu_stripe_args a, int s
                     f2 p = f2{s[i], s[i + 1]} * cc - f2{lq[e], lq[e + 1]};
                     p = f2{__builtin_amdgcn_exp2f(p.x), __builtin_amdgcn_exp2f(p.y)};
                     const f2 t = p * (f2{dp[i], dp[i + 1]} - f2{dq4[e], dq4[e + 1]});
-                    s[i] = p.x; s[i + 1] = p.y;
+                    if constexpr (DROP) {   // dV sees the dropped P
+                        s[i] = ((km >> i) & 1u) ? p.x * dr.R.scale : 0.f;
+                        s[i + 1] = ((km >> (i + 1)) & 1u) ? p.y * dr.R.scale : 0.f;
+                    } else {
+                        s[i] = p.x; s[i + 1] = p.y;
+                    }
                     dp[i] = t.x; dp[i + 1] = t.y;
                 }
             }
@@ -1019,7 +1125,21 @@ int validate(const csu_stripe_args* a, int dtype) {
             return fail(CSU_E_ARG, "stripe_attn: branches must have equal window size");
         if (!g.lepe_w || !g.lepe_b) return fail(CSU_E_ARG, "stripe_attn: null LePE weights");
     }
+    if (a->drop_p < 0.f || a->drop_p >= 1.f || (a->drop_p > 0.f && !a->drop_rng))
+        return fail(CSU_E_ARG, "stripe_attn: attention dropout needs 0 <= p < 1 and an RNG snapshot");
     return 0;
+}
+
+template <typename T>
+void bwd_generic(const csu_stripe_args& a, dim3 grid, const T* qkv, const T* out, const T* dout, const float* lse,
+                 float* delta, T* dqkv, hipStream_t st) {
+    if (a.drop_p > 0.f) {
+        stripe_bwd_dq<T, true><<<grid, NT, 0, st>>>(a, qkv, out, dout, lse, delta, dqkv);
+        stripe_bwd_dkdv<T, true><<<grid, NT, 0, st>>>(a, qkv, dout, lse, delta, dqkv);
+    } else {
+        stripe_bwd_dq<T, false><<<grid, NT, 0, st>>>(a, qkv, out, dout, lse, delta, dqkv);
+        stripe_bwd_dkdv<T, false><<<grid, NT, 0, st>>>(a, qkv, dout, lse, delta, dqkv);
+    }
 }
 
 dim3 grid_of(const csu_stripe_args& a) {
@@ -1041,14 +1161,16 @@ extern "C" int csu_stripe_attn_fwd(const csu_stripe_args* a, int dtype, const vo
         const int sp = wsplit(*a);
         const int nwin = (a->reso / a->br[0].H_sp) * (a->reso / a->br[0].W_sp);
         const dim3 g(a->B * nwin * a->heads * sp, a->nbranch);
-        stripe_fwd_w<<<g, NT, 0, as_stream(stream)>>>(*a, sp, (const bf16*)qkv, (bf16*)out, lse);
+        if (a->drop_p > 0.f) stripe_fwd_w<true><<<g, NT, 0, as_stream(stream)>>>(*a, sp, (const bf16*)qkv, (bf16*)out, lse);
+        else stripe_fwd_w<false><<<g, NT, 0, as_stream(stream)>>>(*a, sp, (const bf16*)qkv, (bf16*)out, lse);
         return check_launch("stripe_attn_fwd");
     }
     const dim3 grid = grid_of(*a);
-    if (dtype == CSU_BF16)
-        stripe_fwd<bf16><<<grid, NT, 0, as_stream(stream)>>>(*a, (const bf16*)qkv, (bf16*)out, lse);
-    else
-        stripe_fwd<float><<<grid, NT, 0, as_stream(stream)>>>(*a, (const float*)qkv, (float*)out, lse);
+    const bool drop = a->drop_p > 0.f;
+    if (dtype == CSU_BF16 && drop) stripe_fwd<bf16, true><<<grid, NT, 0, as_stream(stream)>>>(*a, (const bf16*)qkv, (bf16*)out, lse);
+    else if (dtype == CSU_BF16) stripe_fwd<bf16, false><<<grid, NT, 0, as_stream(stream)>>>(*a, (const bf16*)qkv, (bf16*)out, lse);
+    else if (drop) stripe_fwd<float, true><<<grid, NT, 0, as_stream(stream)>>>(*a, (const float*)qkv, (float*)out, lse);
+    else stripe_fwd<float, false><<<grid, NT, 0, as_stream(stream)>>>(*a, (const float*)qkv, (float*)out, lse);
     return check_launch("stripe_attn_fwd");
 }
 
@@ -1084,14 +1206,17 @@ extern "C" int csu_stripe_attn_bwd(const csu_stripe_args* a, int dtype, const vo
         const int sp = wsplit(*a);
         const int nwin = (a->reso / a->br[0].H_sp) * (a->reso / a->br[0].W_sp);
         const dim3 g(a->B * nwin * a->heads * sp, a->nbranch);
-        stripe_bwd_dq_w<<<g, NT, 0, st>>>(*a, sp, (const bf16*)qkv, (const bf16*)out, (const bf16*)dout, lse, delta, (bf16*)dqkv);
-        stripe_bwd_dkdv_w<<<g, NT, 0, st>>>(*a, sp, (const bf16*)qkv, (const bf16*)dout, lse, delta, (bf16*)dqkv);
+        if (a->drop_p > 0.f) {
+            stripe_bwd_dq_w<true><<<g, NT, 0, st>>>(*a, sp, (const bf16*)qkv, (const bf16*)out, (const bf16*)dout, lse, delta, (bf16*)dqkv);
+            stripe_bwd_dkdv_w<true><<<g, NT, 0, st>>>(*a, sp, (const bf16*)qkv, (const bf16*)dout, lse, delta, (bf16*)dqkv);
+        } else {
+            stripe_bwd_dq_w<false><<<g, NT, 0, st>>>(*a, sp, (const bf16*)qkv, (const bf16*)out, (const bf16*)dout, lse, delta, (bf16*)dqkv);
+            stripe_bwd_dkdv_w<false><<<g, NT, 0, st>>>(*a, sp, (const bf16*)qkv, (const bf16*)dout, lse, delta, (bf16*)dqkv);
+        }
     } else if (dtype == CSU_BF16) {
-        stripe_bwd_dq<bf16><<<grid, NT, 0, st>>>(*a, (const bf16*)qkv, (const bf16*)out, (const bf16*)dout, lse, delta, (bf16*)dqkv);
-        stripe_bwd_dkdv<bf16><<<grid, NT, 0, st>>>(*a, (const bf16*)qkv, (const bf16*)dout, lse, delta, (bf16*)dqkv);
+        bwd_generic<bf16>(*a, grid, (const bf16*)qkv, (const bf16*)out, (const bf16*)dout, lse, delta, (bf16*)dqkv, st);
     } else {
-        stripe_bwd_dq<float><<<grid, NT, 0, st>>>(*a, (const float*)qkv, (const float*)out, (const float*)dout, lse, delta, (float*)dqkv);
-        stripe_bwd_dkdv<float><<<grid, NT, 0, st>>>(*a, (const float*)qkv, (const float*)dout, lse, delta, (float*)dqkv);
+        bwd_generic<float>(*a, grid, (const float*)qkv, (const float*)out, (const float*)dout, lse, delta, (float*)dqkv, st);
     }
     if (do_lepe) {
         if (dtype == CSU_BF16)

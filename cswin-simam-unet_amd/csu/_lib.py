@@ -27,7 +27,14 @@ class StripeBranch(ctypes.Structure):
 
 class StripeArgs(ctypes.Structure):
     _fields_ = [("B", c_int32), ("reso", c_int32), ("C", c_int32), ("heads", c_int32), ("head_dim", c_int32),
-                ("nbranch", c_int32), ("scale", c_float), ("_pad", c_int32), ("br", StripeBranch * 2)]
+                ("nbranch", c_int32), ("scale", c_float), ("_pad", c_int32), ("br", StripeBranch * 2),
+                ("drop_rng", c_void_p), ("drop_site", ctypes.c_uint32), ("drop_p", c_float)]
+
+
+class MlpDropout(ctypes.Structure):
+    """csu_mlp_dropout (include/csu.h)."""
+    _fields_ = [("rng", c_void_p), ("site_hidden", ctypes.c_uint32), ("site_out", ctypes.c_uint32), ("p", c_float),
+                ("row_scale", c_void_p), ("rows_per_sample", ctypes.c_int64)]
 
 
 class GemmDesc(ctypes.Structure):
@@ -92,13 +99,20 @@ _SIGS = {
                                       c_float, c_void_p, c_float, c_void_p]),
     "csu_gemm_ex": (ctypes.c_int, [ctypes.POINTER(GemmDesc), c_void_p]),
     "csu_mlp_supported": (ctypes.c_int, [ctypes.c_int]),
+    "csu_dropout_apply": (ctypes.c_int, [ctypes.c_long, ctypes.c_int, ctypes.c_int, c_void_p, c_void_p, ctypes.c_int,
+                                         c_void_p, c_void_p, ctypes.c_long, c_void_p, ctypes.c_uint, c_float, c_void_p]),
+    "csu_dropout_mask": (ctypes.c_int, [ctypes.c_long, c_void_p, ctypes.c_uint, c_float, c_void_p, c_void_p]),
+    "csu_rng_advance": (ctypes.c_int, [c_void_p, c_void_p, c_void_p]),
+    "csu_droppath_scale": (ctypes.c_int, [ctypes.c_long, c_void_p, ctypes.c_uint, c_float, c_void_p, c_void_p]),
     "csu_layernorm_param_reduce": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
     "csu_stripe_lepe_wgrad": (ctypes.c_int, [ctypes.POINTER(StripeArgs), ctypes.c_int, c_void_p, c_void_p, c_void_p, c_size_t,
                                              c_void_p]),
     "csu_mlp_fwd": (ctypes.c_int, [ctypes.c_long, ctypes.c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                    c_void_p, c_void_p]),
-    "csu_mlp_fwd_ex": (ctypes.c_int, [ctypes.c_long, ctypes.c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
-                                      c_void_p, c_void_p, c_void_p]),
+    "csu_mlp_fwd_dp": (ctypes.c_int, [ctypes.c_long, ctypes.c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                      c_void_p, ctypes.POINTER(MlpDropout), c_void_p]),
+    "csu_mlp_bwd_dp": (ctypes.c_int, [ctypes.c_long, ctypes.c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                      c_void_p, c_void_p, ctypes.POINTER(MlpDropout), c_void_p]),
     "csu_mlp_bwd": (ctypes.c_int, [ctypes.c_long, ctypes.c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                    c_void_p, c_void_p, c_void_p]),
     "csu_conv2d_fwd": (ctypes.c_int, [ctypes.POINTER(ConvGeom), ctypes.c_int, c_void_p, c_void_p, c_void_p, c_void_p,

@@ -21,7 +21,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from . import ops
+from . import ops, rng
 from .simam import SimAM
 
 
@@ -37,18 +37,21 @@ def trunc_normal_(t, std=1.0, a=-2.0, b=2.0):
 
 
 class DropPath(nn.Module):
-    """Stochastic depth (timm DropPath, cswin:344): per-sample Bernoulli(keep)/keep in training."""
+    """Stochastic depth (timm DropPath, cswin:344): per-sample Bernoulli(keep)/keep in training,
+    drawn from the counter-based RNG (csu.rng, site ``_site``) and applied by one kernel."""
 
     def __init__(self, drop_prob: float = 0.0):
         super().__init__()
         self.drop_prob = drop_prob
+        self._site = rng.SITE_BASE + rng.OFF_DROPPATH_ATTN
 
     def forward(self, x):
         if self.drop_prob == 0.0 or not self.training:
             return x
-        keep = 1.0 - self.drop_prob
-        mask = x.new_empty((x.shape[0],) + (1,) * (x.ndim - 1)).bernoulli_(keep)
-        return x * mask / keep
+        B = x.shape[0]
+        rows = x.numel() // x.shape[-1]
+        rs = ops.droppath_scale(B, self.drop_prob, self._site, x.device)
+        return ops.dropout(x, 0.0, self._site, row_scale=rs, rows_per_sample=rows // B)
 
 
 def _ln(x: torch.Tensor, norm: nn.LayerNorm, out_dtype=None) -> torch.Tensor:
@@ -78,10 +81,27 @@ class Mlp(nn.Module):
         self.act = act_layer()
         self.fc2 = nn.Linear(hidden_features, out_features)
         self.drop = nn.Dropout(drop)
+        self._site_h = rng.SITE_BASE + rng.OFF_MLP_HIDDEN
+        self._site_o = rng.SITE_BASE + rng.OFF_MLP_OUT
 
     def forward(self, x):
+        if self.training and self.drop.p > 0 and x.is_cuda:
+            with rng.ensure_scope(x.device) as snap:
+                return self.forward_residual(x, snap=snap)
+        return self.forward_residual(x)
+
+    def forward_residual(self, x, residual=None, row_scale=None, rows_per_sample=1, snap=None):
+        """[residual +] [row_scale *] Mlp(x): the dropout sites draw from `snap` (csu.rng) in
+        training, and the output dropout, DropPath scale and residual add are one kernel."""
+        p = self.drop.p if self.training and snap is not None else 0.0
         h = self.act(ops.linear(x, self.fc1.weight, self.fc1.bias))
-        return self.drop(ops.linear(self.drop(h), self.fc2.weight, self.fc2.bias))
+        if p > 0:
+            h = ops.dropout(h, p, self._site_h, snap)
+        y = ops.linear(h, self.fc2.weight, self.fc2.bias)
+        if p > 0 or row_scale is not None:
+            return ops.dropout(y, p, self._site_o, snap, row_scale=row_scale, rows_per_sample=rows_per_sample,
+                               residual=residual)
+        return y if residual is None else residual + y
 
 
 def img2windows(img: torch.Tensor, H_sp: int, W_sp: int) -> torch.Tensor:
@@ -125,14 +145,19 @@ class LePEAttention(nn.Module):
         self.get_v = nn.Conv2d(dim, dim, kernel_size=3, stride=1, padding=1, groups=dim)
         self.attn_drop_p = attn_drop
         self.attn_drop = nn.Dropout(attn_drop)
+        self._site = rng.SITE_BASE + rng.OFF_ATTN + max(idx, 0)
+
+    def drop_args(self, device) -> Optional[ops.AttnDrop]:
+        """Attention dropout (cswin:290) of a training forward: applied to P inside the kernels."""
+        if not (self.training and self.attn_drop.p > 0):
+            return None
+        return ops.AttnDrop(rng.snapshot(device), self._site, self.attn_drop.p)
 
     def forward(self, qkv):
-        if self.training and self.attn_drop_p > 0:
-            raise NotImplementedError("attention dropout inside the fused stripe kernel is not implemented yet")
         _, B, L, C = qkv.shape
         packed = torch.cat([qkv[0], qkv[1], qkv[2]], dim=-1)
         geom = ops.StripeGeometry(self.resolution, C, self.num_heads, [(self.H_sp, self.W_sp, 0)], self.scale)
-        return ops.stripe_attention(packed, geom, [self.get_v.weight], [self.get_v.bias])
+        return ops.stripe_attention(packed, geom, [self.get_v.weight], [self.get_v.bias], self.drop_args(qkv.device))
 
 
 class CSWinBlock(nn.Module):
@@ -171,30 +196,65 @@ class CSWinBlock(nn.Module):
         self._geom = ops.StripeGeometry(reso, dim, a0.num_heads,
                                         [(a.H_sp, a.W_sp, o) for a, o in zip(self.attns, offs)], a0.scale,
                                         head_dim=a0.dim // a0.num_heads)
+        self.set_drop_sites(rng.SITE_BASE)
+
+    def set_drop_sites(self, base: int):
+        """Dropout site ids of this block (csu.rng): attention branch i, Mlp hidden / output, and
+        the two DropPath draws (attention and Mlp residual, cswin:367-368)."""
+        self._site_base = base
+        for i, a in enumerate(self.attns):
+            a._site = base + rng.OFF_ATTN + i
+        self.mlp._site_h = base + rng.OFF_MLP_HIDDEN
+        self.mlp._site_o = base + rng.OFF_MLP_OUT
+        if isinstance(self.drop_path, DropPath):
+            self.drop_path._site = base + rng.OFF_DROPPATH_ATTN
 
     def forward(self, x):
+        tr = self.training
+        if tr and (self.attns[0].attn_drop.p > 0 or self.mlp.drop.p > 0
+                   or (isinstance(self.drop_path, DropPath) and self.drop_path.drop_prob > 0)) and x.is_cuda:
+            with rng.ensure_scope(x.device) as snap:   # every site of this block: one snapshot
+                return self._forward(x, snap)
+        return self._forward(x, None)
+
+    def _forward(self, x, snap):
         H = W = self.patches_resolution
         B, L, C = x.shape
         assert L == H * W, "flatten img_tokens has wrong size"
-        if self.training and self.attns[0].attn_drop_p > 0:
-            raise NotImplementedError("attention dropout inside the fused stripe kernel is not implemented yet")
         cd = _compute_dtype(x)
+        on = snap is not None
+        p_attn = self.attns[0].attn_drop.p if on else 0.0
+        p_mlp = self.mlp.drop.p if on else 0.0
+        p_path = self.drop_path.drop_prob if on and isinstance(self.drop_path, DropPath) else 0.0
+        base = self._site_base
         # residual junctions x -> (x, LN(x)): their backward adds the two branch gradients in the
         # LayerNorm-backward kernel and hands the upstream GEMMs a bf16 copy (ops.layer_norm_fork)
         n1, n2 = self.norm1, self.norm2
         xa, h1 = ops.layer_norm_fork(x, n1.weight, n1.bias, n1.eps, cd)
         qkv = ops.linear(h1, self.qkv.weight, self.qkv.bias)
+        ad = ops.AttnDrop(snap, base + rng.OFF_ATTN, p_attn) if p_attn > 0 else None
         att = ops.stripe_attention(qkv, self._geom, [a.get_v.weight for a in self.attns],
-                                   [a.get_v.bias for a in self.attns])
-        plain = isinstance(self.drop_path, nn.Identity) and not (self.training and self.mlp.drop.p > 0)
-        if plain and ops.fused_ok(x, C, self.mlp.fc1.out_features):
-            # bf16 fused path: proj + residual in one GEMM; fc1 -> GELU -> fc2 + residual in two
+                                   [a.get_v.bias for a in self.attns], ad)
+        # DropPath (cswin:367-368): per-sample scales of the two residual branches
+        rs1 = rs2 = None
+        if p_path > 0:
+            rs1 = ops.droppath_scale(B, p_path, base + rng.OFF_DROPPATH_ATTN, x.device, snap)
+            rs2 = ops.droppath_scale(B, p_path, base + rng.OFF_DROPPATH_MLP, x.device, snap)
+        fused = ops.fused_ok(x, C, self.mlp.fc1.out_features)
+        if fused and rs1 is None:
+            # bf16 fused path: proj + residual in one GEMM
             x = ops.linear_residual(xa, att, self.proj.weight, self.proj.bias)
-            xb, h2 = ops.layer_norm_fork(x, n2.weight, n2.bias, n2.eps, cd)
-            return ops.mlp_residual(xb, h2, self.mlp.fc1, self.mlp.fc2)
-        x = xa + self.drop_path(ops.linear(att, self.proj.weight, self.proj.bias))
+        else:
+            y = ops.linear(att, self.proj.weight, self.proj.bias)
+            x = ops.dropout(y, 0.0, 0, row_scale=rs1, rows_per_sample=L, residual=xa) if rs1 is not None else xa + y
         xb, h2 = ops.layer_norm_fork(x, n2.weight, n2.bias, n2.eps, cd)
-        return xb + self.drop_path(self.mlp(h2))
+        if fused:
+            # fc1 -> GELU -> [dropout] -> fc2 -> [dropout, DropPath] + residual (csrc/mlp.hip)
+            md = None
+            if on and (p_mlp > 0 or rs2 is not None):
+                md = ops.MlpDrop(snap, self.mlp._site_h, self.mlp._site_o, p_mlp, rs2, L)
+            return ops.mlp_residual(xb, h2, self.mlp.fc1, self.mlp.fc2, md)
+        return self.mlp.forward_residual(h2, xb, rs2, L, snap)
 
 
 class Merge_Block(nn.Module):
@@ -332,6 +392,7 @@ class CSWinTransformer(nn.Module):
         self.output = nn.Conv2d(in_channels=embed_dim, out_channels=self.num_classes, kernel_size=1, bias=False)
         self.simam = SimAM() if simam else None
         self.apply(self._init_weights)
+        rng.assign_sites(self)
 
     def _init_weights(self, m):
         if isinstance(m, nn.Linear):
@@ -380,7 +441,8 @@ class CSWinTransformer(nn.Module):
         y = ops.conv2d(x.permute(0, 2, 3, 1), conv.weight, conv.bias, conv.stride[0], conv.padding[0])
         y = y.reshape(B, -1, y.shape[-1])
         x = _ln(y, ln, torch.float32 if y.dtype == torch.bfloat16 else y.dtype)
-        x = self.pos_drop(x)
+        if self.training and self.pos_drop.p > 0:
+            x = ops.dropout(x, self.pos_drop.p, rng.SITE_POS_DROP)
         for blk in self.stage1:
             x = blk(x)
         self.x1 = x
@@ -459,7 +521,20 @@ class CSWinTransformer(nn.Module):
         finally:
             ops.set_cast_cache(None)
 
+    def _dropout_on(self) -> bool:
+        if not self.training:
+            return False
+        return any((isinstance(m, nn.Dropout) and m.p > 0) or (isinstance(m, DropPath) and m.drop_prob > 0)
+                   for m in self.modules())
+
     def _forward(self, x):
+        if x.is_cuda and self._dropout_on():
+            # one RNG snapshot for every dropout site of this forward (csu.rng)
+            with rng.scope(x.device):
+                return self._forward_impl(x)
+        return self._forward_impl(x)
+
+    def _forward_impl(self, x):
         x = self.forward_features(x)
         x = self.forward_up_features(x)
         if self.num_classes == 1:

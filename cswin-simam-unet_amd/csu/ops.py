@@ -43,8 +43,11 @@ class StripeGeometry:
                 raise ValueError(f"resolution {reso} not divisible by stripe window {hs}x{ws} (cswin:204)")
 
     def args(self, B: int, ws: Sequence[torch.Tensor], bs: Sequence[torch.Tensor],
-             dws: Optional[Sequence[torch.Tensor]] = None, dbs: Optional[Sequence[torch.Tensor]] = None):
+             dws: Optional[Sequence[torch.Tensor]] = None, dbs: Optional[Sequence[torch.Tensor]] = None,
+             drop: Optional["AttnDrop"] = None):
         a = _lib.StripeArgs()
+        if drop is not None and drop.p > 0:
+            a.drop_rng, a.drop_site, a.drop_p = drop.snap.data_ptr(), drop.site, drop.p
         a.B, a.reso, a.C, a.heads, a.head_dim = B, self.reso, self.C, self.heads, self.head_dim
         a.nbranch, a.scale = len(self.branches), self.scale
         for i, (hs, wsp, off) in enumerate(self.branches):
@@ -56,9 +59,17 @@ class StripeGeometry:
         return a
 
 
+class AttnDrop:
+    """Attention dropout of one stripe launch (attn_drop cswin:246/290): snapshot, first site
+    (branch i uses site + i), probability."""
+
+    def __init__(self, snap: torch.Tensor, site: int, p: float):
+        self.snap, self.site, self.p = snap, int(site), float(p)
+
+
 class _StripeAttnFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, qkv, geom: StripeGeometry, *lepe):
+    def forward(ctx, qkv, geom: StripeGeometry, drop, *lepe):
         nb = len(geom.branches)
         ws = [w.detach().float().contiguous() for w in lepe[:nb]]
         bs = [b.detach().float().contiguous() for b in lepe[nb:]]
@@ -69,12 +80,12 @@ class _StripeAttnFn(torch.autograd.Function):
             raise ValueError("flatten img_tokens has wrong size")  # cswin:281/356
         out = torch.empty(B, L, geom.C, dtype=qkv.dtype, device=qkv.device)
         lse = torch.empty(nb, B, geom.heads, L, dtype=torch.float32, device=qkv.device)
-        a = geom.args(B, ws, bs)
+        a = geom.args(B, ws, bs, drop=drop)
         nbytes, flops = _stripe_fwd_work(geom, B, qkv.element_size())
         _launch("stripe_attn_fwd", lambda: lib().csu_stripe_attn_fwd(ctypes.byref(a), dtype_code(qkv), ptr(qkv), ptr(out),
                                                                      ptr(lse), stream_ptr(qkv.device)),
                 flops, nbytes, prec=prec_of(qkv))
-        ctx.geom = geom
+        ctx.geom, ctx.drop = geom, drop
         ctx.lepe_dtypes = [t.dtype for t in lepe]
         ctx.save_for_backward(qkv, out, lse, *ws, *bs)
         return out
@@ -92,7 +103,7 @@ class _StripeAttnFn(torch.autograd.Function):
         L = lib()
         dws = [torch.empty_like(w) for w in ws]
         dbs = [torch.empty_like(b) for b in bs]
-        a = geom.args(B, ws, bs, dws, dbs)
+        a = geom.args(B, ws, bs, dws, dbs, drop=ctx.drop)
         nbytes = L.csu_stripe_attn_bwd_workspace(ctypes.byref(a))
         work = torch.empty(max(nbytes, 16), dtype=torch.uint8, device=qkv.device)
         e = qkv.element_size()
@@ -104,13 +115,78 @@ class _StripeAttnFn(torch.autograd.Function):
                                                                  nbytes, stream_ptr(qkv.device)),
                 2 * ff, bw, prec=prec_of(qkv))
         grads = [g.to(dt) for g, dt in zip(dws + dbs, ctx.lepe_dtypes)]
-        return (dqkv, None, *grads)
+        return (dqkv, None, None, *grads)
 
 
 def stripe_attention(qkv: torch.Tensor, geom: StripeGeometry, lepe_w: Sequence[torch.Tensor],
-                     lepe_b: Sequence[torch.Tensor]) -> torch.Tensor:
-    """(B, L, 3C) qkv -> (B, L, C) attention output of every branch (+LePE), channels concatenated."""
-    return _StripeAttnFn.apply(qkv, geom, *lepe_w, *lepe_b)
+                     lepe_b: Sequence[torch.Tensor], drop: Optional[AttnDrop] = None) -> torch.Tensor:
+    """(B, L, 3C) qkv -> (B, L, C) attention output of every branch (+LePE), channels concatenated.
+    ``drop``: attention dropout on the softmax probabilities inside the same kernels."""
+    return _StripeAttnFn.apply(qkv, geom, drop, *lepe_w, *lepe_b)
+
+
+# ---------------------------------------------------------------------------------------------
+# Dropout / DropPath (nn.Dropout cswin:188/512, timm DropPath cswin:344/367-368)
+# ---------------------------------------------------------------------------------------------
+def _dropout_launch(x2, res2, out, rs, rps, snap, site, p):
+    rows, cols = x2.shape
+    n = rows * cols
+    nb = n * (x2.element_size() + out.element_size() + (0 if res2 is None else 4))
+    _launch("dropout", lambda: lib().csu_dropout_apply(rows, cols, dtype_code(x2), ptr(x2),
+                                                      None if res2 is None else ptr(res2), dtype_code(out), ptr(out),
+                                                      None if rs is None else ptr(rs), rps,
+                                                      None if snap is None else ptr(snap), site, p,
+                                                      stream_ptr(x2.device)), 0, nb)
+
+
+class _DropoutFn(torch.autograd.Function):
+    """out = res + row_scale[row / rps] * keep(site) / (1 - p) * x in one pass (csu_dropout_apply);
+    backward regenerates the mask from the saved snapshot (dx = same op on dy, dres = dy)."""
+
+    @staticmethod
+    def forward(ctx, x, res, snap, site, p, rs, rps, odt):
+        cols = x.shape[-1]
+        x2 = x.reshape(-1, cols).contiguous()
+        res2 = None if res is None else res.float().reshape(-1, cols).contiguous()
+        out = torch.empty(x2.shape, dtype=torch.float32 if res is not None else (odt or x.dtype), device=x.device)
+        _dropout_launch(x2, res2, out, rs, rps, snap, site, p)
+        ctx.meta = (snap, site, p, rs, rps, x.dtype, x.shape, None if res is None else res.dtype)
+        return out.view(*x.shape[:-1], cols)
+
+    @staticmethod
+    def backward(ctx, dy):
+        snap, site, p, rs, rps, xdt, xshape, rdt = ctx.meta
+        cols = dy.shape[-1]
+        dy2 = dy.reshape(-1, cols).contiguous()
+        dx = torch.empty(dy2.shape, dtype=xdt, device=dy.device)
+        _dropout_launch(dy2, None, dx, rs, rps, snap, site, p)
+        dres = None if rdt is None else dy.to(rdt)
+        return dx.view(xshape), dres, None, None, None, None, None, None
+
+
+def dropout(x: torch.Tensor, p: float, site: int, snap: Optional[torch.Tensor] = None,
+            row_scale: Optional[torch.Tensor] = None, rows_per_sample: int = 1,
+            residual: Optional[torch.Tensor] = None, out_dtype=None) -> torch.Tensor:
+    """Train-mode nn.Dropout(p) of `x` drawn from site `site` of the RNG snapshot `snap` (the
+    enclosing forward's when None, csu.rng), optionally times a per-sample DropPath scale
+    (row_scale[row // rows_per_sample], rows = x.numel() // x.shape[-1]) and plus an fp32
+    residual, all in one kernel."""
+    from . import rng
+    require_device(x)
+    if x.shape[-1] % 8:
+        raise ValueError("dropout: last dim must be a multiple of 8")
+    if p > 0 and snap is None:
+        snap = rng.snapshot(x.device)
+    with torch.autocast("cuda", enabled=False):
+        return _DropoutFn.apply(x, residual, snap, int(site), float(p), row_scale, int(rows_per_sample), out_dtype)
+
+
+def droppath_scale(B: int, p: float, site: int, device, snap: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """(B,) fp32 DropPath per-sample scale (0 or 1 / (1 - p)) of `site`."""
+    from . import rng
+    if snap is None:
+        snap = rng.snapshot(device)
+    return rng.droppath_scale(snap, site, p, B)
 
 
 # ---------------------------------------------------------------------------------------------
@@ -711,32 +787,77 @@ class _LinearResidualFn(torch.autograd.Function):
         return dy.to(rdt), dx, dw.to(wdt), db.to(bdt), None
 
 
+class MlpDrop:
+    """Dropout of one Mlp + DropPath residual (Mlp.drop cswin:188/193/195, drop_path cswin:368):
+    snapshot, hidden / output sites, p, and the per-sample DropPath scale (or None)."""
+
+    def __init__(self, snap, site_h: int, site_o: int, p: float, row_scale=None, rows_per_sample: int = 1):
+        self.snap, self.site_h, self.site_o, self.p = snap, int(site_h), int(site_o), float(p)
+        self.row_scale, self.rps = row_scale, int(rows_per_sample)
+
+    def c_struct(self):
+        d = _lib.MlpDropout()
+        d.rng = None if self.snap is None else self.snap.data_ptr()
+        d.site_hidden, d.site_out, d.p = self.site_h, self.site_o, self.p
+        d.row_scale = None if self.row_scale is None else self.row_scale.data_ptr()
+        d.rows_per_sample = self.rps
+        return d
+
+    def out_grad(self, dy2, dt):
+        """dy of the dropped, DropPath-scaled fc2 output -> gradient of fc2's output (dtype dt)."""
+        dz = torch.empty(dy2.shape, dtype=dt, device=dy2.device)
+        _dropout_launch(dy2, None, dz, self.row_scale, self.rps, self.snap, self.site_o, self.p)
+        return dz
+
+
 class _MlpResidualFn(torch.autograd.Function):
     """res + fc2(gelu(fc1(x))) (Mlp cswin:180-196 + residual cswin:368) as two csu_gemm_ex calls:
     fc1's epilogue writes the pre-activation h and gelu(h) (bf16); fc2 adds bias and the residual
-    in its epilogue; backward fuses GELU' into the fc2 input-gradient epilogue."""
+    in its epilogue; backward fuses GELU' into the fc2 input-gradient epilogue.
+
+    With ``drop`` (MlpDrop): g is dropped (hidden site) before fc2, and fc2's bf16 output goes
+    through one dropout pass (output site, DropPath scale, residual); the backward applies the
+    output mask to dy, and the hidden mask after the GELU' epilogue (the two commute)."""
 
     @staticmethod
-    def forward(ctx, res, x, w1, b1, w2, b2, w1c, w2c):
-        res2 = res.float().contiguous().view(-1, res.shape[-1])
+    def forward(ctx, res, x, w1, b1, w2, b2, w1c, w2c, drop):
+        C = res.shape[-1]
+        res2 = res.float().contiguous().view(-1, C)
         x2 = x.reshape(-1, x.shape[-1]).contiguous()
         h, g = gemm(x2, w1c, False, torch.bfloat16, bias=b1.detach().float().contiguous(), gelu_out=True)
-        y = gemm(g, w2c, False, torch.float32, bias=b2.detach().float().contiguous(), resid=res2)
+        if drop is None:
+            y = gemm(g, w2c, False, torch.float32, bias=b2.detach().float().contiguous(), resid=res2)
+        else:
+            gd = torch.empty_like(g)
+            _dropout_launch(g, None, gd, None, 1, drop.snap, drop.site_h, drop.p)
+            g = gd
+            z = gemm(g, w2c, False, torch.bfloat16, bias=b2.detach().float().contiguous())
+            y = torch.empty_like(res2)
+            _dropout_launch(z, res2, y, drop.row_scale, drop.rps, drop.snap, drop.site_o, drop.p)
         ctx.save_for_backward(x2, h, g, _weight_t(w1, w1c), _weight_t(w2, w2c))
         ctx.meta = (res.dtype, x.shape, w1.dtype, b1.dtype, w2.dtype, b2.dtype)
         ctx.params = (w1, b1, w2, b2)
+        ctx.drop = drop
         return y.view(res.shape)
 
     @staticmethod
     def backward(ctx, dy):
         x2, h, g, w1t, w2t = ctx.saved_tensors
         rdt, xshape, w1dt, b1dt, w2dt, b2dt = ctx.meta
-        dyb = _bf16_of(dy).view(-1, dy.shape[-1])
+        drop = ctx.drop
+        if drop is None:
+            dyb = _bf16_of(dy).view(-1, dy.shape[-1])
+        else:
+            dyb = drop.out_grad(dy.reshape(-1, dy.shape[-1]).contiguous(), torch.bfloat16)
         dh = gemm(dyb, w2t, False, torch.bfloat16, gelu_aux=h)         # (dY W2) * gelu'(h)
+        if drop is not None:
+            dhm = torch.empty_like(dh)
+            _dropout_launch(dh, None, dhm, None, 1, drop.snap, drop.site_h, drop.p)
+            dh = dhm
         dw2, db2 = wgrad_maybe_side(dyb, g, w2dt, b2dt, params=ctx.params[2:])
         dx = gemm(dh, w1t, False, torch.bfloat16).view(xshape)
         dw1, db1 = wgrad_maybe_side(dh, x2, w1dt, b1dt, params=ctx.params[:2])
-        return dy.to(rdt), dx, dw1.to(w1dt), db1.to(b1dt), dw2.to(w2dt), db2.to(b2dt), None, None
+        return dy.to(rdt), dx, dw1.to(w1dt), db1.to(b1dt), dw2.to(w2dt), db2.to(b2dt), None, None, None
 
 
 def _weight_bf16(w):
@@ -758,10 +879,12 @@ def linear_residual(res, x, weight, bias):
 class _MlpFusedFn(torch.autograd.Function):
     """res + fc2(gelu(fc1(x))) (Mlp cswin:180-196 + residual cswin:368) in ONE csu_mlp_fwd launch
     (the 4C hidden layer never reaches HBM).  Backward: one csu_mlp_bwd launch recomputes h and
-    writes dh, g = gelu(h) and dx; then the two weight gradients."""
+    writes dh, g = gelu(h) and dx; then the two weight gradients.  ``drop`` (MlpDrop): hidden and
+    output dropout plus the DropPath scale inside the same two launches (csu_mlp_fwd_dp /
+    csu_mlp_bwd_dp), the output mask applied to dy by one dropout pass first."""
 
     @staticmethod
-    def forward(ctx, res, x, w1, b1, w2, b2, w1c, w2c):
+    def forward(ctx, res, x, w1, b1, w2, b2, w1c, w2c, drop):
         C = x.shape[-1]
         res2 = res.float().contiguous().view(-1, C)
         x2 = x.reshape(-1, C).contiguous()
@@ -769,9 +892,11 @@ class _MlpFusedFn(torch.autograd.Function):
         y = torch.empty_like(res2)
         M = x2.shape[0]
         b2f = b2.detach().float().contiguous()
-        _launch("mlp_fwd", lambda: lib().csu_mlp_fwd(M, C, ptr(x2), ptr(w1c), ptr(b1f), ptr(w2c), ptr(b2f), ptr(res2), ptr(y),
-                                                     stream_ptr(x2.device)),
+        dd = None if drop is None else ctypes.byref(drop.c_struct())
+        _launch("mlp_fwd", lambda: lib().csu_mlp_fwd_dp(M, C, ptr(x2), ptr(w1c), ptr(b1f), ptr(w2c), ptr(b2f), ptr(res2),
+                                                        ptr(y), dd, stream_ptr(x2.device)),
                 16 * M * C * C, M * C * (2 + 4 + 4) + 16 * C * C)
+        ctx.drop = drop
         ctx.save_for_backward(x2, w1c, b1f, w2c)
         ctx.meta = (res.dtype, x.shape, w1.dtype, b1.dtype, w2.dtype, b2.dtype)
         ctx.params = (w1, b1, w2, b2)
@@ -782,31 +907,38 @@ class _MlpFusedFn(torch.autograd.Function):
         rdt, xshape, w1dt, b1dt, w2dt, b2dt = ctx.meta
         x2, w1c, b1f, w2c = ctx.saved_tensors
         M, C = x2.shape
-        dyb = _bf16_of(dy).view(-1, C)
+        drop = ctx.drop
+        if drop is None:
+            dyb = _bf16_of(dy).view(-1, C)
+        else:
+            dyb = drop.out_grad(dy.reshape(-1, C).contiguous(), torch.bfloat16)
         dh = torch.empty(M, 4 * C, dtype=torch.bfloat16, device=x2.device)
         g = torch.empty_like(dh)
         dx = torch.empty(M, C, dtype=torch.bfloat16, device=x2.device)
-        _launch("mlp_bwd", lambda: lib().csu_mlp_bwd(M, C, ptr(x2), ptr(dyb), ptr(w1c), ptr(b1f), ptr(w2c), ptr(dh), ptr(g),
-                                                     ptr(dx), stream_ptr(x2.device)),
+        dd = None if drop is None else ctypes.byref(drop.c_struct())
+        _launch("mlp_bwd", lambda: lib().csu_mlp_bwd_dp(M, C, ptr(x2), ptr(dyb), ptr(w1c), ptr(b1f), ptr(w2c), ptr(dh),
+                                                        ptr(g), ptr(dx), dd, stream_ptr(x2.device)),
                 24 * M * C * C, M * C * (2 + 2 + 2) + M * 4 * C * (2 + 2) + 16 * C * C)
         dw2, db2 = wgrad_maybe_side(dyb, g, w2dt, b2dt, params=ctx.params[2:])
         dw1, db1 = wgrad_maybe_side(dh, x2, w1dt, b1dt, params=ctx.params[:2])
-        return dy.to(rdt), dx.view(xshape), dw1.to(w1dt), db1.to(b1dt), dw2.to(w2dt), db2.to(b2dt), None, None
+        return dy.to(rdt), dx.view(xshape), dw1.to(w1dt), db1.to(b1dt), dw2.to(w2dt), db2.to(b2dt), None, None, None
 
 
 # CSU_FUSED_MLP=0 selects the two-GEMM Mlp (A/B comparisons)
 FUSED_MLP = _os.environ.get("CSU_FUSED_MLP", "1") == "1"
 
 
-def mlp_residual(res, x, fc1: torch.nn.Linear, fc2: torch.nn.Linear):
+def mlp_residual(res, x, fc1: torch.nn.Linear, fc2: torch.nn.Linear, drop: Optional[MlpDrop] = None):
+    """res + DropPath(Dropout(fc2(Dropout(gelu(fc1(x)))))) on the bf16 path (``drop`` None: eval /
+    no dropout)."""
     C = x.shape[-1]
     if FUSED_MLP and fc1.out_features == 4 * C and lib().csu_mlp_supported(C):
         with torch.autocast("cuda", enabled=False):
             return _MlpFusedFn.apply(res, x, fc1.weight, fc1.bias, fc2.weight, fc2.bias, _weight_bf16(fc1.weight),
-                                     _weight_bf16(fc2.weight))
+                                     _weight_bf16(fc2.weight), drop)
     with torch.autocast("cuda", enabled=False):
         return _MlpResidualFn.apply(res, x, fc1.weight, fc1.bias, fc2.weight, fc2.bias, _weight_bf16(fc1.weight),
-                                    _weight_bf16(fc2.weight))
+                                    _weight_bf16(fc2.weight), drop)
 
 
 class CastCache:

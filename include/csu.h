@@ -61,6 +61,14 @@ typedef struct {
     float scale;             /* qk_scale or head_dim**-0.5 (cswin:231) */
     int32_t _pad;
     csu_stripe_branch br[2];
+    /* attention dropout on the softmax probabilities (attn_drop, cswin:290), p = 0: none.  rng =
+     * device [seed, counter] snapshot of the step (uint64 x 2), the same for forward and backward;
+     * branch i uses dropout site drop_site + i.  Mask element of (branch, image b, window win,
+     * head hh, query q, key k): ((((b * nwin + win) * heads + hh) * N + q) * Npad + k) with
+     * N = window tokens, Npad = N rounded up to 32 (csu_dropout_mask materialises it). */
+    const uint64_t* drop_rng;
+    uint32_t drop_site;
+    float drop_p;
 } csu_stripe_args;
 
 /* out (B, L, C) dtype; lse fp32 [nbranch][B][heads][L] (softmax log-sum-exp, saved for bwd). */
@@ -260,6 +268,26 @@ int csu_adamw_step(const csu_adamw_item* items, int count, long total_chunks, co
                    void* stream);
 
 /* ---------------------------------------------------------------------------------------
+ * Dropout / DropPath (nn.Dropout cswin:190/193/512, timm DropPath cswin:344/367-368) as one
+ * elementwise pass where no producing kernel fuses it:
+ *   out[i] = res[i] + row_scale[(i / cols) / rows_per_sample] * keep(site, i) / (1 - p) * x[i]
+ * over (rows, cols) row-major, cols % 8 == 0; res (fp32) and row_scale (fp32 per sample: 0 or
+ * 1/keep_prob of DropPath) may be NULL; p = 0: no mask.  keep(site, i): Philox4x32-7 counter-based
+ * bits (csrc/rng.hpp) of the [seed, counter] snapshot `rng` (device uint64 x 2).  The backward of
+ * a site is the same call with res = NULL on the incoming gradient.  csu_dropout_mask writes the
+ * 0/1 keep mask of elements [0, n) of a site (tests feed it to the CPU oracle).
+ * ------------------------------------------------------------------------------------- */
+int csu_dropout_apply(long rows, int cols, int xdtype, const void* x, const float* res, int odtype, void* out,
+                      const float* row_scale, long rows_per_sample, const uint64_t* rng, unsigned site, float p,
+                      void* stream);
+int csu_dropout_mask(long n, const uint64_t* rng, unsigned site, float p, uint8_t* out, void* stream);
+/* snap[0..1] = state[0..1]; state[1] += 1 (one kernel: the per-forward RNG snapshot, graph-safe) */
+int csu_rng_advance(uint64_t* state, uint64_t* snap, void* stream);
+/* DropPath per-sample scale (timm drop_path, cswin:344/367-368): out[b] = keep(site, b) / (1 - p)
+ * (element b of the site's mask, as csu_dropout_mask) -- the row_scale operand above. */
+int csu_droppath_scale(long n, const uint64_t* rng, unsigned site, float p, float* out, void* stream);
+
+/* ---------------------------------------------------------------------------------------
  * Fused Mlp + residual (Mlp cswin:180-196 with the residual add of CSWinBlock cswin:368):
  * fc1 -> GELU -> fc2 with the 4C hidden layer kept on chip.  x (M, C) bf16; w1 (4C, C) and
  * w2 (C, 4C) bf16 nn.Linear weights; b1 (4C), b2 (C) fp32; res / out (M, C) fp32 (may alias).
@@ -271,11 +299,24 @@ int csu_mlp_fwd(long M, int C, const void* x, const void* w1, const float* b1, c
                 const float* res, float* out, void* stream);
 int csu_mlp_bwd(long M, int C, const void* x, const void* dy, const void* w1, const float* b1, const void* w2,
                 void* dh, void* g, void* dx, void* stream);
-/* csu_mlp_fwd plus the pre-activation h = fc1(x) (bf16, M x 4C) written to `h` (NULL: not
- * written) -- the operand of the GEMM-form backward (dh = (dy w2) * gelu'(h) in a GEMM epilogue,
- * dW2 from gelu(h) on the fly in the weight-gradient GEMM). */
-int csu_mlp_fwd_ex(long M, int C, const void* x, const void* w1, const float* b1, const void* w2, const float* b2,
-                   const float* res, float* out, void* h, void* stream);
+/* Dropout inside the fused Mlp (Mlp.drop cswin:190/193, DropPath cswin:368), train mode:
+ *   g  = gelu(fc1(x)) * keep(site_hidden, m * 4C + f) / (1 - p)
+ *   out = res + row_scale[m / rows_per_sample] * keep(site_out, m * C + c) / (1 - p) * fc2(g)
+ * (keep(): rng.hpp's Philox mask of the snapshot rng = [seed, counter]; row_scale NULL = 1).
+ * The backward regenerates the hidden mask: dy must already carry the output mask and DropPath
+ * scale (csu_dropout_apply on the same site_out / row_scale), g is written dropped (dW2 operand)
+ * and dh = (dy w2) * mask * gelu'(h). */
+typedef struct {
+    const uint64_t* rng;
+    uint32_t site_hidden, site_out;
+    float p;                   /* 0 <= p < 1 (p = 0: no element masks, row_scale still applies) */
+    const float* row_scale;    /* per-sample DropPath scale (0 or 1/keep_prob), or NULL */
+    int64_t rows_per_sample;
+} csu_mlp_dropout;
+int csu_mlp_fwd_dp(long M, int C, const void* x, const void* w1, const float* b1, const void* w2, const float* b2,
+                   const float* res, float* out, const csu_mlp_dropout* d, void* stream);
+int csu_mlp_bwd_dp(long M, int C, const void* x, const void* dy, const void* w1, const float* b1, const void* w2,
+                   void* dh, void* g, void* dx, const csu_mlp_dropout* d, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * Implicit-GEMM NHWC convolution (patch embed cswin:505, Merge_Block.conv cswin:376, CARAFE

@@ -14,6 +14,13 @@ Citations: ``cswin:N`` = reference ``train_cswinunet_segmentation.py`` line N.
 
 Parameters are passed as a flat ``{state_dict_key: tensor}`` mapping using the reference's
 state_dict key names (cswin:489-688), so weights interchange with reference ``.pth`` files.
+
+Dropout (train mode, cswin:188-195/246/290/344/367-368/512): the functions take an optional mask
+provider ``drop(name, shape) -> scale tensor or None`` (0 or 1/keep per element; per sample for
+DropPath), so a parity test can replay exactly the masks the device drew.  Names: ``pos``
+(pos_drop), ``<block>.attn<i>`` (P of branch i, (B*nWin, heads, N, N)), ``<block>.mlp.h`` /
+``<block>.mlp.o`` (Mlp hidden / output), ``<block>.dp_attn`` / ``<block>.dp_mlp`` (the two
+DropPath draws, shape (B,)).  Without a provider the forward is the eval / p = 0 forward.
 """
 from __future__ import annotations
 
@@ -64,7 +71,7 @@ def stripe_geometry(reso: int, idx: int, split: int) -> Tuple[int, int]:
 # --------------------------------------------------------------------------------------------
 def lepe_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, reso: int, hs: int, ws: int,
                    heads: int, w: torch.Tensor, b: torch.Tensor, scale: float,
-                   attn_drop: float = 0.0, training: bool = False) -> torch.Tensor:
+                   attn_drop: float = 0.0, training: bool = False, attn_mask=None) -> torch.Tensor:
     """softmax(q*scale @ k^T) @ v + dwconv3x3(v) per stripe window, window-local zero padding.
 
     q, k, v: (B, L, Cb) with L == reso*reso (assert cswin:281).  w: (Cb,1,3,3), b: (Cb,).
@@ -88,7 +95,9 @@ def lepe_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, reso: int,
     # scores in the input dtype, softmax over keys (cswin:287-292)
     att = torch.matmul(qw * scale, kw.transpose(-2, -1))
     att = torch.softmax(att, dim=-1)
-    if attn_drop > 0 and training:
+    if attn_mask is not None:                                       # attn_drop with given masks (cswin:290)
+        att = att * attn_mask(att.shape)
+    elif attn_drop > 0 and training:
         att = F.dropout(att, attn_drop, training=True)
     o = torch.matmul(att, vw) + lepe
     o = o.transpose(1, 2).reshape(-1, N, Cb)                       # head merge (cswin:293)
@@ -106,13 +115,26 @@ def _lin(x, p, key):
     return F.linear(x, p[key + ".weight"], p.get(key + ".bias"))
 
 
-def mlp(x: torch.Tensor, p: Params, key: str) -> torch.Tensor:
-    """fc1 -> exact-erf GELU -> fc2 (cswin:180-196; dropout 0 in parity runs)."""
-    return _lin(F.gelu(_lin(x, p, key + ".fc1")), p, key + ".fc2")
+def _drop(drop, name, t):
+    """t times the provider's mask of `name` (identity without a provider / mask)."""
+    m = drop(name, tuple(t.shape)) if drop is not None else None
+    return t if m is None else t * m
+
+
+def _drop_path(drop, name, t):
+    """DropPath (timm drop_path, cswin:344): per-sample scale of `name`."""
+    m = drop(name, (t.shape[0],)) if drop is not None else None
+    return t if m is None else t * m.reshape(-1, *([1] * (t.dim() - 1)))
+
+
+def mlp(x: torch.Tensor, p: Params, key: str, drop=None) -> torch.Tensor:
+    """fc1 -> exact-erf GELU -> Dropout -> fc2 -> Dropout (cswin:180-196)."""
+    h = _drop(drop, key + ".h", F.gelu(_lin(x, p, key + ".fc1")))
+    return _drop(drop, key + ".o", _lin(h, p, key + ".fc2"))
 
 
 def cswin_block(x: torch.Tensor, p: Params, key: str, reso: int, heads: int, split: int,
-                last_stage: bool, qk_scale=None) -> torch.Tensor:
+                last_stage: bool, qk_scale=None, drop=None) -> torch.Tensor:
     """Pre-LN CSWin block (cswin:301-370)."""
     B, L, C = x.shape
     assert L == reso * reso, "flatten img_tokens has wrong size"
@@ -125,7 +147,8 @@ def cswin_block(x: torch.Tensor, p: Params, key: str, reso: int, heads: int, spl
         hs, ws = stripe_geometry(reso, -1, split)
         scale = qk_scale or (C // heads) ** -0.5
         a = lepe_attention(q, k, v, reso, hs, ws, heads,
-                           p[key + ".attns.0.get_v.weight"], p[key + ".attns.0.get_v.bias"], scale)
+                           p[key + ".attns.0.get_v.weight"], p[key + ".attns.0.get_v.bias"], scale,
+                           attn_mask=None if drop is None else (lambda shp: drop(key + ".attn0", shp)))
     else:
         h2, c2 = heads // 2, C // 2
         scale = qk_scale or (c2 // h2) ** -0.5
@@ -134,10 +157,12 @@ def cswin_block(x: torch.Tensor, p: Params, key: str, reso: int, heads: int, spl
             hs, ws = stripe_geometry(reso, i, split)
             outs.append(lepe_attention(q[..., sl], k[..., sl], v[..., sl], reso, hs, ws, h2,
                                        p[f"{key}.attns.{i}.get_v.weight"],
-                                       p[f"{key}.attns.{i}.get_v.bias"], scale))
+                                       p[f"{key}.attns.{i}.get_v.bias"], scale,
+                                       attn_mask=None if drop is None else
+                                       (lambda shp, i=i: drop(f"{key}.attn{i}", shp))))
         a = torch.cat(outs, dim=-1)
-    x = x + _lin(a, p, key + ".proj")                                # cswin:366-367
-    return x + mlp(_ln(x, p, key + ".norm2"), p, key + ".mlp")       # cswin:368
+    x = x + _drop_path(drop, key + ".dp_attn", _lin(a, p, key + ".proj"))          # cswin:366-367
+    return x + _drop_path(drop, key + ".dp_mlp", mlp(_ln(x, p, key + ".norm2"), p, key + ".mlp", drop))  # cswin:368
 
 
 def tokens_to_nchw(x: torch.Tensor) -> torch.Tensor:
@@ -278,18 +303,19 @@ def recipe_params(cfg: CSWinConfig, seed: int = 0, dtype=torch.float32) -> Param
     return recipe_from_contract(state_dict_contract(cfg), seed, dtype)
 
 
-def cswin_forward(p: Params, x: torch.Tensor, cfg: CSWinConfig, return_skips: bool = False):
-    """(B, 3, S, S) in [0,1] -> (B, num_classes, S, S) sigmoid probabilities (cswin:625-688)."""
+def cswin_forward(p: Params, x: torch.Tensor, cfg: CSWinConfig, return_skips: bool = False, drop=None):
+    """(B, 3, S, S) in [0,1] -> (B, num_classes, S, S) sigmoid probabilities (cswin:625-688).
+    ``drop``: train-mode dropout mask provider (module docstring)."""
     st = cfg.stages()
 
     def run(name, x):
         _, reso, heads, split, dim, depth, last = next(s for s in st if s[0] == name)
         for i in range(depth):
-            x = cswin_block(x, p, f"{name}.{i}", reso, heads, split, last, cfg.qk_scale)
+            x = cswin_block(x, p, f"{name}.{i}", reso, heads, split, last, cfg.qk_scale, drop)
         return x
 
     skip = simam if cfg.simam else (lambda t: t)
-    x = patch_embed(x, p)
+    x = _drop(drop, "pos", patch_embed(x, p))                        # pos_drop (cswin:628)
     x = run("stage1", x); x1 = x; x = merge_block(x, p, "merge1")
     x = run("stage2", x); x2 = x; x = merge_block(x, p, "merge2")
     x = run("stage3", x); x3 = x; x = merge_block(x, p, "merge3")

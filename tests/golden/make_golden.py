@@ -116,6 +116,53 @@ def f2_block(R):
     npz("f2_block.npz", **out)
 
 
+class _MaskRec(nn.Module):
+    """Stands in for one of the reference block's nn.Dropout / DropPath modules (same place in the
+    reference's own forward, cswin:193/195/290/367-368): draws a keep mask from a fixed generator,
+    applies it as nn.Dropout / timm DropPath do (mask / keep) and records it under the oracle's
+    name for that call (``names`` in call order)."""
+
+    def __init__(self, names, p, gen, per_sample=False):
+        super().__init__()
+        self.names, self.p, self.gen, self.per_sample, self.calls, self.masks = list(names), p, gen, per_sample, 0, {}
+
+    def forward(self, x):
+        name = self.names[self.calls]
+        self.calls += 1
+        shape = (x.shape[0],) if self.per_sample else tuple(x.shape)
+        keep = (torch.rand(shape, generator=self.gen) >= self.p)
+        self.masks[name] = keep
+        m = keep.double() / (1 - self.p)
+        if self.per_sample:
+            m = m.reshape(-1, *([1] * (x.dim() - 1)))
+        return x * m
+
+
+def f9_dropout(R):
+    """CSWinBlock in train mode with the reference main()'s rates (drop 0.3, attn_drop 0.3,
+    drop_path 0.3, cswin:930-932): its dropout modules replaced by mask recorders, so y / dx /
+    grads are the reference's forward under known masks (pins the oracle's dropout placement)."""
+    out = {}
+    for pre, (dim, reso, heads, sw, last) in {"two_": (64, 8, 2, 2, False), "last_": (64, 4, 2, 4, True)}.items():
+        torch.manual_seed(7)
+        m = R.CSWinBlock(dim=dim, reso=reso, num_heads=heads, split_size=sw, qkv_bias=True, last_stage=last,
+                         drop=0.3, attn_drop=0.3, drop_path=0.3).double().train()
+        gen = torch.Generator().manual_seed(21)
+        recs = [_MaskRec(["blk.mlp.h", "blk.mlp.o"], 0.3, gen), _MaskRec(["blk.dp_attn", "blk.dp_mlp"], 0.3, gen, True)]
+        m.mlp.drop, m.drop_path = recs
+        for i, a in enumerate(m.attns):
+            a.attn_drop = _MaskRec([f"blk.attn{i}"], 0.3, gen)
+            recs.append(a.attn_drop)
+        x = torch.randn(2, reso * reso, dim).double().requires_grad_(True)
+        out[pre + "meta"] = np.array([dim, reso, heads, sw, int(last)])
+        _module_case(m, x, out, pre)
+        for r in recs:
+            for k, v in r.masks.items():
+                out[pre + "mask:" + k] = v.numpy().astype(np.uint8)
+    out["p"] = np.array(0.3)
+    npz("f9_dropout.npz", **out)
+
+
 def f3_modules(R):
     out = {}
     torch.manual_seed(11)
@@ -245,7 +292,7 @@ if __name__ == "__main__":
     R, RU = load_reference()
     jobs = {"f1": lambda: f1_lepe(R), "f2": lambda: f2_block(R), "f3": lambda: f3_modules(R), "f4": lambda: f4_model(R),
             "f5": lambda: f5_metrics(R), "f6": lambda: f6_unet(RU), "f7": lambda: f7_contract(R, RU),
-            "f8": lambda: f8_trajectory(R)}
+            "f8": lambda: f8_trajectory(R), "f9": lambda: f9_dropout(R)}
     for k, fn in jobs.items():
         if a.only and k not in a.only.split(","):
             continue

@@ -29,12 +29,32 @@ def test_library_exports_every_header_symbol():
     assert b"gfx950" in L.csu_build_info()
 
 
-def test_struct_layout_matches_header():
+def test_struct_layout_matches_header(tmp_path):
+    """The ctypes mirrors of the C structs have the C compiler's sizes and field offsets
+    (include/csu.h compiled by gcc here)."""
+    import subprocess
     from csu import _lib
-    # csu_stripe_branch: 4 x int32 + 4 pointers; csu_stripe_args: 8 x int32/float + 2 branches
-    assert ctypes.sizeof(_lib.StripeBranch) == 16 + 4 * 8
-    assert ctypes.sizeof(_lib.StripeArgs) == 32 + 2 * ctypes.sizeof(_lib.StripeBranch)
-    assert _lib.StripeArgs.br.offset == 32
+    checks = {"csu_stripe_branch": (_lib.StripeBranch, ["H_sp", "ch_off", "lepe_w", "lepe_db"]),
+              "csu_stripe_args": (_lib.StripeArgs, ["scale", "br", "drop_rng", "drop_site", "drop_p"]),
+              "csu_gemm_desc": (_lib.GemmDesc, ["M", "a", "b_trans", "bias", "out", "ldc", "cfg"]),
+              "csu_mlp_dropout": (_lib.MlpDropout, ["rng", "site_out", "p", "row_scale", "rows_per_sample"]),
+              "csu_conv_geom": (_lib.ConvGeom, ["B", "KH", "pad"])}
+    lines = ["#include <stdio.h>", "#include <stddef.h>", '#include "csu.h"', "int main(void) {"]
+    for cname, (_, fields) in checks.items():
+        lines.append(f'printf("{cname} %zu\\n", sizeof({cname}));')
+        for f in fields:
+            lines.append(f'printf("{cname}.{f} %zu\\n", offsetof({cname}, {f}));')
+    lines.append("return 0; }")
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    inc = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include")
+    subprocess.run(["gcc", "-I", inc, str(src), "-o", str(exe)], check=True)
+    got = dict(line.split() for line in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.splitlines())
+    for cname, (cls, fields) in checks.items():
+        assert ctypes.sizeof(cls) == int(got[cname]), cname
+        for f in fields:
+            assert getattr(cls, f).offset == int(got[f"{cname}.{f}"]), (cname, f)
 
 
 def test_error_path_reports_text():

@@ -72,6 +72,40 @@ def test_f2_block(golden_dir):
         _check_grads(z, pre, p)
 
 
+def mask_provider(z, pre, p):
+    """Oracle drop provider over the masks the reference block recorded (f9_dropout.npz)."""
+    def drop(name, shape):
+        k = pre + "mask:" + name
+        if k not in z.files:
+            return None
+        m = t64(z[k]) / (1 - p)
+        assert tuple(m.shape) == tuple(shape), (name, m.shape, shape)
+        return m
+    return drop
+
+
+def test_f9_dropout_block(golden_dir):
+    """Train-mode CSWinBlock at the reference main() rates (drop / attn_drop / drop_path 0.3):
+    the oracle under the reference's recorded masks reproduces its y, dx and every gradient."""
+    z = load(golden_dir, "f9_dropout.npz")
+    p_drop = float(z["p"])
+    for pre in ("two_", "last_"):
+        dim, reso, heads, sw, last = (int(v) for v in z[pre + "meta"])
+        assert len([k for k in z.files if k.startswith(pre + "mask:")]) == (5 if last else 6)
+        p = _params(z, pre)
+        x = t64(z[pre + "x"]).requires_grad_(True)
+        y = O.cswin_block(x, {"blk." + k: v for k, v in p.items()}, "blk", reso, heads, sw, bool(last),
+                          drop=mask_provider(z, pre, p_drop))
+        close(y, z[pre + "y"])
+        y.backward(t64(z[pre + "gy"]))
+        close(x.grad, z[pre + "dx"])
+        _check_grads(z, pre, p)
+        # the masks matter: without them the forward differs
+        with torch.no_grad():
+            y0 = O.cswin_block(x, {"blk." + k: v for k, v in p.items()}, "blk", reso, heads, sw, bool(last))
+        assert float((y0 - t64(z[pre + "y"])).abs().max()) > 1e-2
+
+
 def test_f3_modules(golden_dir):
     z = load(golden_dir, "f3_modules.npz")
     cases = {
