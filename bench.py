@@ -49,6 +49,8 @@ def parse():
     ap.add_argument("--depth", default="1,2,9,1")
     ap.add_argument("--split", default="1,2,8,8")
     ap.add_argument("--simam", action="store_true")
+    ap.add_argument("--dropout", type=float, default=0.0,
+                    help="drop_rate = attn_drop_rate = drop_path_rate (the reference main() trains at 0.3, cswin:930-932)")
     ap.add_argument("--cpu-baseline", default="auto", choices=["auto", "on", "off"])
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--graph", default="auto", choices=["auto", "on", "off"],
@@ -90,6 +92,10 @@ def cpu_baseline(args, dtype):
     cfg = O.CSWinConfig(img_size=args.img, depth=[int(v) for v in args.depth.split(",")],
                         split_size=[int(v) for v in args.split.split(",")], simam=args.simam)
     m = O.OracleCSWin(cfg, O.recipe_params(cfg, seed=0))
+    pd = args.dropout
+    if pd > 0:   # Bernoulli masks at every site (the reference's train-mode dropout cost)
+        m.forward = lambda x: O.cswin_forward(m.params(), x, cfg, drop=lambda name, shape:
+                                              (torch.rand(shape) >= pd).float() / (1 - pd))
     opt = torch.optim.AdamW(m.parameters(), lr=1e-4, weight_decay=1e-4)
     from csu.data import ellipse_batch
     b = args.batch
@@ -141,7 +147,9 @@ def main():
     depth = [int(v) for v in args.depth.split(",")]
     split = [int(v) for v in args.split.split(",")]
     torch.manual_seed(0)
-    model = CSWinTransformer(img_size=args.img, depth=depth, split_size=split, simam=args.simam).to(device)
+    pd = args.dropout
+    model = CSWinTransformer(img_size=args.img, depth=depth, split_size=split, simam=args.simam,
+                             drop_rate=pd, attn_drop_rate=pd, drop_path_rate=pd).to(device)
     nparams = sum(p.numel() for p in model.parameters())
     use_graph = args.graph in ("on", "auto")
     reducer = None
@@ -228,9 +236,11 @@ def main():
                "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
                "vs_baseline": None, "dtype": args.dtype, "data": "synthetic (ellipse masks, SURVEY §8d), random-init weights",
                "config": {"workload": f"CSWin-UNet train step {args.img}x{args.img} depth {depth} split {split}"
-                                      f"{' +SimAM' if args.simam else ''}, AdamW",
+                                      f"{' +SimAM' if args.simam else ''}"
+                                      f"{f', dropout/attn_drop/drop_path {pd}' if pd > 0 else ''}, AdamW",
                           "model": "CSWinTransformer", "params": nparams, "global_batch": args.batch * world,
-                          "per_gpu_batch": args.batch, "img": args.img, "parallelism": f"dp{world}"},
+                          "per_gpu_batch": args.batch, "img": args.img, "parallelism": f"dp{world}",
+                          "dropout": pd},
                "roofline": roof, "cpu_baseline": cpu, "final_loss": round(float(loss.item()), 5),
                "hip_graph": use_graph,
                "grad_allreduce": None if not dp else ("graph-captured buckets" if reducer is not None else "DDP eager")}
@@ -242,13 +252,15 @@ def main():
 def _metric(args):
     """BASELINE.json's metric string for its headline workload (512x512 bf16, default depth); the
     same form naming the resolution / precision otherwise."""
-    if (args.img, args.dtype, args.depth, args.split) == (512, "bf16", "1,2,9,1", "1,2,8,8"):
+    if (args.img, args.dtype, args.depth, args.split, args.dropout, args.simam) == (512, "bf16", "1,2,9,1", "1,2,8,8", 0.0,
+                                                                                  False):
         try:
             with open(os.path.join(REPO, "BASELINE.json")) as f:
                 return json.load(f)["metric"]
         except Exception:
             pass
-    return f"images/sec at {args.img}x{args.img} {args.dtype} (CSWin-UNet train step)"
+    extra = "".join([", SimAM" if args.simam else "", f", dropout {args.dropout}" if args.dropout > 0 else ""])
+    return f"images/sec at {args.img}x{args.img} {args.dtype} (CSWin-UNet train step{extra})"
 
 
 def _roofline(kernels, ms_per_step, args):
@@ -277,7 +289,8 @@ def _pmc_traffic(kernel, args):
         return None
     try:
         with open(p) as f:
-            return json.load(f).get(f"{kernel}|{args.img}|{args.batch}|{args.dtype}")
+            key = f"{kernel}|{args.img}|{args.batch}|{args.dtype}" + (f"|d{args.dropout}" if args.dropout > 0 else "")
+            return json.load(f).get(key)
     except Exception:
         return None
 
