@@ -666,14 +666,14 @@ int wgrad_blocks(const csu_stripe_args& a) {
 }
 
 // =============================================================================================
-// v2 (bf16, window <= 256 tokens -- every stage of the 512x512 model): the whole window of the
-// head is resident in LDS.  Images are "natural" [token][32] rows of 64 B whose 16-B chunks are
+// v2 (bf16, window <= 1024 tokens -- every stage of the 512x512 and 1024x1024 models): the whole
+// window of the head is resident in LDS (images sized WM = 256 / 512 / 1024 tokens per launch).  Images are "natural" [token][32] rows of 64 B whose 16-B chunks are
 // XOR-swizzled by (row >> 2) & 3, which makes the 32-row ds_read_b128 fragment reads AND the
 // gfx950 transposing reads (ds_read_b64_tr_b16) used for the V^T / K^T / Q^T / dO^T operands
 // bank-conflict free; LePE neighbours are read from the same images.  One image serves both
 // orientations, so nothing is ever written transposed.
 // =============================================================================================
-constexpr int WMAX = 256;   // window tokens held in LDS
+constexpr int WMAX = 1024;  // largest window held in LDS (K + V images: 128 KiB of the 160 KiB)
 typedef float f2 __attribute__((ext_vector_type(2)));   // packed-f32 pairs (v_pk_fma/mul/add_f32)
 
 __device__ __forceinline__ int swz(int row, int col) {   // element offset in a swizzled image
@@ -723,24 +723,26 @@ __device__ __forceinline__ void mma_acc_sw(f32x16& acc, const bf16* img, int kba
 // staging costs one memory latency instead of one per row group.
 __device__ __forceinline__ void stage_win2(const Win& w, int reso, const bf16* imgA, int strideA, int chA,
                                            const bf16* imgB, int strideB, int chB, int npad, bf16* dstA, bf16* dstB) {
-    constexpr int MAXIT = WMAX * 4 / NT;
-    bf16x8 va[MAXIT], vb[MAXIT];
+    constexpr int IT = 4;   // 256 rows per pass: 8 x 16-B loads in flight per thread
+    for (int base = 0; base < npad * 4; base += IT * NT) {
+        bf16x8 va[IT], vb[IT];
 #pragma unroll
-    for (int i = 0; i < MAXIT; ++i) {
-        const int it = threadIdx.x + i * NT;
-        const int n = it >> 2, c = (it & 3) * 8;
-        const bool ok = it < npad * 4 && n < w.N;
-        const size_t tok = ok ? (size_t)tok_of(w, reso, n) : 0;
-        va[i] = ok ? *reinterpret_cast<const bf16x8*>(imgA + tok * strideA + chA + c) : bf16x8{};
-        vb[i] = ok ? *reinterpret_cast<const bf16x8*>(imgB + tok * strideB + chB + c) : bf16x8{};
-    }
-#pragma unroll
-    for (int i = 0; i < MAXIT; ++i) {
-        const int it = threadIdx.x + i * NT;
-        if (it < npad * 4) {
+        for (int i = 0; i < IT; ++i) {
+            const int it = base + threadIdx.x + i * NT;
             const int n = it >> 2, c = (it & 3) * 8;
-            *reinterpret_cast<bf16x8*>(dstA + swz(n, c)) = va[i];
-            *reinterpret_cast<bf16x8*>(dstB + swz(n, c)) = vb[i];
+            const bool ok = it < npad * 4 && n < w.N;
+            const size_t tok = ok ? (size_t)tok_of(w, reso, n) : 0;
+            va[i] = ok ? *reinterpret_cast<const bf16x8*>(imgA + tok * strideA + chA + c) : bf16x8{};
+            vb[i] = ok ? *reinterpret_cast<const bf16x8*>(imgB + tok * strideB + chB + c) : bf16x8{};
+        }
+#pragma unroll
+        for (int i = 0; i < IT; ++i) {
+            const int it = base + threadIdx.x + i * NT;
+            if (it < npad * 4) {
+                const int n = it >> 2, c = (it & 3) * 8;
+                *reinterpret_cast<bf16x8*>(dstA + swz(n, c)) = va[i];
+                *reinterpret_cast<bf16x8*>(dstB + swz(n, c)) = vb[i];
+            }
         }
     }
 }
@@ -783,11 +785,11 @@ __device__ __forceinline__ Win decode_w(const csu_stripe_args& a, int split) {
     return w;
 }
 
-template <bool DROP>
+template <int WM, bool DROP>
 __global__ __launch_bounds__(NT) void stripe_fwd_w(csu_stripe_args a, int split, const bf16* __restrict__ qkv,
                                                    bf16* __restrict__ out, float* __restrict__ lse) {
-    __shared__ __attribute__((aligned(16))) bf16 Ks[WMAX * HD];
-    __shared__ __attribute__((aligned(16))) bf16 Vs[WMAX * HD];
+    __shared__ __attribute__((aligned(16))) bf16 Ks[WM * HD];
+    __shared__ __attribute__((aligned(16))) bf16 Vs[WM * HD];
     __shared__ float wts[HD * 10];
     const Win w = decode_w(a, split);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -795,7 +797,7 @@ __global__ __launch_bounds__(NT) void stripe_fwd_w(csu_stripe_args a, int split,
     const int L = a.reso * a.reso, C = a.C, C3 = 3 * C;
     const bf16* img = qkv + (size_t)w.b * L * C3;
     const int npad = (w.N + 31) & ~31;
-    const int rows = (npad + split - 1) / split;            // query rows of this workgroup
+    const int rows = (((npad + split - 1) / split) + 31) & ~31;   // query rows of this workgroup (32-aligned)
     const int qbeg = w.blk * rows, qend = min(npad, qbeg + rows);
     // this wave's first query fragment is loaded together with the K/V staging loads
     Frag<bf16> qnext;
@@ -892,13 +894,13 @@ __global__ __launch_bounds__(NT) void stripe_fwd_w(csu_stripe_args a, int split,
     }
 }
 
-template <bool DROP>
+template <int WM, bool DROP>
 __global__ __launch_bounds__(NT) void stripe_bwd_dq_w(csu_stripe_args a, int split, const bf16* __restrict__ qkv,
                                                       const bf16* __restrict__ out, const bf16* __restrict__ dout,
                                                       const float* __restrict__ lse, float* __restrict__ delta,
                                                       bf16* __restrict__ dqkv) {
-    __shared__ __attribute__((aligned(16))) bf16 Ks[WMAX * HD];
-    __shared__ __attribute__((aligned(16))) bf16 Vs[WMAX * HD];
+    __shared__ __attribute__((aligned(16))) bf16 Ks[WM * HD];
+    __shared__ __attribute__((aligned(16))) bf16 Vs[WM * HD];
     __shared__ float wts[HD * 10];
     const Win w = decode_w(a, split);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -908,7 +910,7 @@ __global__ __launch_bounds__(NT) void stripe_bwd_dq_w(csu_stripe_args a, int spl
     const bf16* oimg = out + (size_t)w.b * L * C;
     const bf16* gimg = dout + (size_t)w.b * L * C;
     const int npad = (w.N + 31) & ~31;
-    const int rows = (npad + split - 1) / split;
+    const int rows = (((npad + split - 1) / split) + 31) & ~31;   // 32-aligned: mask groups start on 8
     const int qbeg = w.blk * rows, qend = min(npad, qbeg + rows);
     Frag<bf16> qn_f, gn_f;   // first query block's fragments, loaded with the staging loads
     {
@@ -987,13 +989,13 @@ __global__ __launch_bounds__(NT) void stripe_bwd_dq_w(csu_stripe_args a, int spl
     }
 }
 
-template <bool DROP>
+template <int WM, bool DROP>
 __global__ __launch_bounds__(NT) void stripe_bwd_dkdv_w(csu_stripe_args a, int split, const bf16* __restrict__ qkv,
                                                         const bf16* __restrict__ dout, const float* __restrict__ lse,
                                                         const float* __restrict__ delta, bf16* __restrict__ dqkv) {
-    __shared__ __attribute__((aligned(16))) bf16 Qs[WMAX * HD];
-    __shared__ __attribute__((aligned(16))) bf16 Gs[WMAX * HD];
-    __shared__ __attribute__((aligned(16))) float lse_s[WMAX], dl_s[WMAX];
+    __shared__ __attribute__((aligned(16))) bf16 Qs[WM * HD];
+    __shared__ __attribute__((aligned(16))) bf16 Gs[WM * HD];
+    __shared__ __attribute__((aligned(16))) float lse_s[WM], dl_s[WM];
     __shared__ float wts[HD * 10];
     __shared__ __attribute__((aligned(16))) unsigned char dtbl[4][128];
     const Win w = decode_w(a, split);
@@ -1003,7 +1005,7 @@ __global__ __launch_bounds__(NT) void stripe_bwd_dkdv_w(csu_stripe_args a, int s
     const bf16* img = qkv + (size_t)w.b * L * C3;
     const bf16* gimg = dout + (size_t)w.b * L * C;
     const int npad = (w.N + 31) & ~31;
-    const int rows = (npad + split - 1) / split;
+    const int rows = (((npad + split - 1) / split) + 31) & ~31;   // 32-aligned: mask groups start on 8
     const int kbeg = w.blk * rows, kend = min(npad, kbeg + rows);
     Frag<bf16> kn_f, vn_f;   // first key block's fragments, loaded with the staging loads
     {
@@ -1089,23 +1091,44 @@ __global__ __launch_bounds__(NT) void stripe_bwd_dkdv_w(csu_stripe_args a, int s
     }
 }
 
-// split factor of the whole-window kernels: 2 workgroups per window-head when one per window-head
-// would leave fewer than 1024 workgroups (stage 3/4 at 512x512), else 1
+// split factor of the whole-window kernels: workgroups per window-head, so that a launch has
+// about 1024 workgroups, each owning at least 128 query (key) rows -- one 32-row pass per wave
+// (512x512: 2 at stages 3/4; 1024x1024: 4 at stage 3 (N = 512), 8 at stage 4 (N = 1024))
 int wsplit(const csu_stripe_args& a) {
     const int N = a.br[0].H_sp * a.br[0].W_sp;
     const int nwin = (a.reso / a.br[0].H_sp) * (a.reso / a.br[0].W_sp);
     const long wgs = (long)a.B * nwin * a.heads * a.nbranch;
-    static int env = -1;   // CSU_ATTN_SPLIT=<n>: force the split of windows above 128 tokens (A/B)
-    if (env < 0) {
-        const char* e = getenv("CSU_ATTN_SPLIT");
-        env = e ? atoi(e) : 0;
-    }
-    if (env > 0 && N > 128) return env;
-    return (N > 128 && wgs < 1024) ? 2 : 1;
+    const int maxsp = (((N + 31) & ~31) + 127) / 128;
+    const long want = (1024 + wgs - 1) / wgs;
+    return (int)(want < maxsp ? want : maxsp);
 }
 
 bool use_window_path(const csu_stripe_args& a, int dtype) {
     return dtype == CSU_BF16 && a.br[0].H_sp * a.br[0].W_sp <= WMAX;
+}
+
+// LDS image rows of a launch: the window rounded up to 256 / 512 / 1024 tokens
+int wm_of(const csu_stripe_args& a) {
+    const int N = a.br[0].H_sp * a.br[0].W_sp;
+    return N <= 256 ? 256 : N <= 512 ? 512 : 1024;
+}
+
+template <int WM>
+void fwd_w(const csu_stripe_args& a, int sp, dim3 g, const bf16* qkv, bf16* out, float* lse, hipStream_t st) {
+    if (a.drop_p > 0.f) stripe_fwd_w<WM, true><<<g, NT, 0, st>>>(a, sp, qkv, out, lse);
+    else stripe_fwd_w<WM, false><<<g, NT, 0, st>>>(a, sp, qkv, out, lse);
+}
+
+template <int WM>
+void bwd_w(const csu_stripe_args& a, int sp, dim3 g, const bf16* qkv, const bf16* out, const bf16* dout,
+           const float* lse, float* delta, bf16* dqkv, hipStream_t st) {
+    if (a.drop_p > 0.f) {
+        stripe_bwd_dq_w<WM, true><<<g, NT, 0, st>>>(a, sp, qkv, out, dout, lse, delta, dqkv);
+        stripe_bwd_dkdv_w<WM, true><<<g, NT, 0, st>>>(a, sp, qkv, dout, lse, delta, dqkv);
+    } else {
+        stripe_bwd_dq_w<WM, false><<<g, NT, 0, st>>>(a, sp, qkv, out, dout, lse, delta, dqkv);
+        stripe_bwd_dkdv_w<WM, false><<<g, NT, 0, st>>>(a, sp, qkv, dout, lse, delta, dqkv);
+    }
 }
 
 int validate(const csu_stripe_args* a, int dtype) {
@@ -1161,8 +1184,12 @@ extern "C" int csu_stripe_attn_fwd(const csu_stripe_args* a, int dtype, const vo
         const int sp = wsplit(*a);
         const int nwin = (a->reso / a->br[0].H_sp) * (a->reso / a->br[0].W_sp);
         const dim3 g(a->B * nwin * a->heads * sp, a->nbranch);
-        if (a->drop_p > 0.f) stripe_fwd_w<true><<<g, NT, 0, as_stream(stream)>>>(*a, sp, (const bf16*)qkv, (bf16*)out, lse);
-        else stripe_fwd_w<false><<<g, NT, 0, as_stream(stream)>>>(*a, sp, (const bf16*)qkv, (bf16*)out, lse);
+        const hipStream_t st = as_stream(stream);
+        switch (wm_of(*a)) {
+            case 256: fwd_w<256>(*a, sp, g, (const bf16*)qkv, (bf16*)out, lse, st); break;
+            case 512: fwd_w<512>(*a, sp, g, (const bf16*)qkv, (bf16*)out, lse, st); break;
+            default: fwd_w<1024>(*a, sp, g, (const bf16*)qkv, (bf16*)out, lse, st); break;
+        }
         return check_launch("stripe_attn_fwd");
     }
     const dim3 grid = grid_of(*a);
@@ -1206,12 +1233,11 @@ extern "C" int csu_stripe_attn_bwd(const csu_stripe_args* a, int dtype, const vo
         const int sp = wsplit(*a);
         const int nwin = (a->reso / a->br[0].H_sp) * (a->reso / a->br[0].W_sp);
         const dim3 g(a->B * nwin * a->heads * sp, a->nbranch);
-        if (a->drop_p > 0.f) {
-            stripe_bwd_dq_w<true><<<g, NT, 0, st>>>(*a, sp, (const bf16*)qkv, (const bf16*)out, (const bf16*)dout, lse, delta, (bf16*)dqkv);
-            stripe_bwd_dkdv_w<true><<<g, NT, 0, st>>>(*a, sp, (const bf16*)qkv, (const bf16*)dout, lse, delta, (bf16*)dqkv);
-        } else {
-            stripe_bwd_dq_w<false><<<g, NT, 0, st>>>(*a, sp, (const bf16*)qkv, (const bf16*)out, (const bf16*)dout, lse, delta, (bf16*)dqkv);
-            stripe_bwd_dkdv_w<false><<<g, NT, 0, st>>>(*a, sp, (const bf16*)qkv, (const bf16*)dout, lse, delta, (bf16*)dqkv);
+        const bf16 *q = (const bf16*)qkv, *o = (const bf16*)out, *go = (const bf16*)dout;
+        switch (wm_of(*a)) {
+            case 256: bwd_w<256>(*a, sp, g, q, o, go, lse, delta, (bf16*)dqkv, st); break;
+            case 512: bwd_w<512>(*a, sp, g, q, o, go, lse, delta, (bf16*)dqkv, st); break;
+            default: bwd_w<1024>(*a, sp, g, q, o, go, lse, delta, (bf16*)dqkv, st); break;
         }
     } else if (dtype == CSU_BF16) {
         bwd_generic<bf16>(*a, grid, (const bf16*)qkv, (const bf16*)out, (const bf16*)dout, lse, delta, (bf16*)dqkv, st);

@@ -151,7 +151,8 @@ def _attn_provider(snap, site, p, nwin_heads_n):
 
 # (reso, C, heads, split, last): branch windows N = reso*split (two-branch) or reso^2 (last stage)
 ATTN_CASES = [(16, 64, 2, 2, False), (8, 64, 2, 8, True), (14, 128, 4, 7, False), (7, 128, 4, 7, True),
-              (32, 64, 2, 1, False), (16, 64, 2, 16, True), (64, 64, 2, 4, False)]
+              (32, 64, 2, 1, False), (16, 64, 2, 16, True), (64, 64, 2, 4, False),
+              (64, 64, 2, 8, False), (24, 64, 2, 24, True), (32, 128, 4, 32, True)]
 
 
 @pytest.mark.parametrize("case", ATTN_CASES)

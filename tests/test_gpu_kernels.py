@@ -39,6 +39,8 @@ ATTN_CASES = [
     (16, 0, 1, 32, 1, 2), (16, 1, 1, 32, 1, 2), (16, 0, 2, 64, 2, 2), (16, 1, 4, 64, 2, 1),
     (8, -1, 8, 128, 4, 2), (14, 0, 7, 64, 2, 1), (7, -1, 7, 64, 2, 2), (32, 0, 8, 128, 4, 1),
     (16, -1, 16, 64, 2, 1), (32, -1, 32, 32, 1, 1), (64, 1, 2, 64, 2, 1), (56, 0, 1, 32, 1, 1),
+    # 1024x1024-class windows held whole in LDS: 512 (stage 3, split 8), ragged 400 / 576, 1024 (stage 4)
+    (64, 0, 8, 64, 2, 1), (20, -1, 20, 32, 1, 2), (24, -1, 24, 64, 2, 1), (32, -1, 32, 128, 4, 1),
 ]
 
 
