@@ -178,8 +178,9 @@ def main():
 
     step = eager_step
     if use_graph:
-        # capture first (its eager warm-up runs on a side stream); eager steps on the default
-        # stream before the capture crash hipGraphInstantiate at this size (ROCm 7.2 / torch 2.10)
+        # capture first (its eager warm-up runs on a side stream).  Eager steps may precede the
+        # capture as long as nothing keeps their autograd graph alive (GraphedTrainStep raises
+        # otherwise; the cause of the former hipGraphInstantiate segfault)
         from csu.train import GraphedTrainStep
         gstep = GraphedTrainStep(model, opt, bce_loss, batches[0][0], batches[0][1], amp, warmup=args.warmup,
                                  reducer=reducer)

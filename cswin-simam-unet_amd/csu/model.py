@@ -535,6 +535,24 @@ class CSWinTransformer(nn.Module):
         return self._forward_impl(x)
 
     def _forward_impl(self, x):
+        try:
+            return self._forward_body(x)
+        finally:
+            self._release_skips()
+
+    def _release_skips(self):
+        """Keep the encoder skips (x1, x2, x3 as the reference exposes them, cswin:632-642) but not
+        the autograd graph behind them: a module attribute holding a graph of the last forward keeps
+        that step's AccumulateGrad nodes alive, and a later HIP-graph capture then runs them on the
+        stream they were created on (the legacy default stream) -> the capture breaks and
+        hipGraphInstantiate segfaults (tools/graph_after_eager.py)."""
+        for k in ("x1", "x2", "x3"):
+            t = getattr(self, k, None)
+            if t is not None and t.requires_grad:
+                setattr(self, k, t.detach())
+        self._x1s = self._x2s = self._x3s = None
+
+    def _forward_body(self, x):
         x = self.forward_features(x)
         x = self.forward_up_features(x)
         if self.num_classes == 1:

@@ -10,6 +10,8 @@ from __future__ import annotations
 
 from typing import Dict, List, Optional
 
+import warnings
+
 import torch
 import torch.distributed as dist
 import torch.nn.functional as F
@@ -193,10 +195,21 @@ class GraphedTrainStep:
         self.dtype = autocast_dtype
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(side):
-            for _ in range(warmup):
-                self._body()
+        with warnings.catch_warnings(record=True) as caught:
+            warnings.simplefilter("always")
+            with torch.cuda.stream(side):
+                for _ in range(warmup):
+                    self._body()
         torch.cuda.current_stream().wait_stream(side)
+        for w in caught:
+            if "AccumulateGrad node's stream does not match" in str(w.message):
+                # An autograd graph of an earlier step (e.g. a kept loss / output of an eager step)
+                # is alive: its AccumulateGrad nodes would run on the stream they were created on
+                # inside the capture, which breaks it (hipGraphInstantiate segfaults).
+                raise RuntimeError(
+                    "GraphedTrainStep: an autograd graph of an earlier step is still referenced (a kept "
+                    "output or loss of an eager step); delete those references before capturing")
+            warnings.warn_explicit(w.message, w.category, w.filename, w.lineno)
         # drain the warm-up (its RCCL work included) before capturing: nothing of it is pending
         # when the capture starts
         torch.cuda.synchronize()

@@ -179,3 +179,35 @@ def test_deep_config_vs_oracle():
     gr = np.array([pref[k].grad.norm().item() for k, _ in m.named_parameters()])
     big = gr >= 1e-6 * gr.max()
     np.testing.assert_allclose(gn[big], gr[big], rtol=2e-3)
+
+
+def test_capture_after_eager_steps():
+    """Eager default-stream steps, then a HIP-graph capture of the same model (the order that used
+    to segfault in hipGraphInstantiate): works once no earlier autograd graph is referenced (the
+    model releases its skip tensors' graph after each forward), and a still-referenced output of an
+    eager step is reported as an error before the capture instead of a crash."""
+    from csu.data import ellipse_batch
+    from csu.model import CSWinTransformer
+    from csu.train import GraphedTrainStep, bce_loss, make_optimizer
+    d = dev()
+    torch.manual_seed(0)
+    m = CSWinTransformer(img_size=128, split_size=[1, 2, 4, 4]).to(d)
+    opt = make_optimizer(m, capturable=True)
+    x, t = (v.to(d) for v in ellipse_batch(np.random.default_rng(0), 2, 128))
+
+    def eager():
+        opt.zero_grad(set_to_none=True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            y = m(x)
+        bce_loss(y, t).backward()
+        opt.step()
+        return y
+    kept = eager()
+    assert m.x1 is not None and not m.x1.requires_grad        # skips kept, their graph released
+    with pytest.raises(RuntimeError, match="still referenced"):
+        GraphedTrainStep(m, opt, bce_loss, x, t, torch.bfloat16, warmup=1)
+    del kept
+    eager()
+    gs = GraphedTrainStep(m, opt, bce_loss, x, t, torch.bfloat16, warmup=1)
+    losses = [float(gs(x, t)[0].item()) for _ in range(3)]
+    assert all(np.isfinite(losses)) and losses[2] < losses[0]
