@@ -517,11 +517,12 @@ def gemm(a2: torch.Tensor, b: torch.Tensor, b_trans: bool, out_dtype, bias=None,
 # (zero_grad(set_to_none=True)), no tensor hooks, and no post-accumulate hooks other than
 # csu.dist.GradAllReduce's (which order their reads after side_stream()).  Gradient accumulation
 # (an existing .grad: AccumulateGrad adds in place on the launching stream), DDP and user hooks run
-# the weight gradient inline.  Graph capture runs inline too (CSU_SIDE_IN_GRAPH=1 keeps the side
-# stream under capture; DESIGN.md §6 has the determinism record).  CSU_SIDE_WGRAD=0 disables.
+# the weight gradient inline.  A HIP-graph capture runs it inline too: inside a graph the side
+# stream measured slower (1075 vs 1090 img/s, 3 A/B pairs at 512x512) and its replays were not
+# bitwise reproducible at 512x512 (tools/det_graph.py DIAG=...).
+# CSU_SIDE_WGRAD=0 disables the side stream in eager steps as well.
 # ---------------------------------------------------------------------------------------------
 SIDE_WGRAD = _os.environ.get("CSU_SIDE_WGRAD", "1") == "1"
-SIDE_IN_GRAPH = _os.environ.get("CSU_SIDE_IN_GRAPH", "0") == "1"
 # CSU_PAD_CHANNELS=0: convolutions of inputs with C % 8 != 0 (the 3-channel image) without the zero
 # channel padding (per-element gathers; A/B)
 PAD_CHANNELS = _os.environ.get("CSU_PAD_CHANNELS", "1") == "1"
@@ -553,7 +554,7 @@ def _param_safe(p) -> bool:
 def _side_ok(t: torch.Tensor, *dtypes, params=()) -> bool:
     if not (SIDE_WGRAD and t.is_cuda) or any(d not in (None, torch.float32) for d in dtypes):
         return False
-    if not SIDE_IN_GRAPH and torch.cuda.is_current_stream_capturing():
+    if torch.cuda.is_current_stream_capturing():
         return False
     if not all(_param_safe(p) for p in params):
         return False

@@ -9,6 +9,22 @@ from csu.train import GraphedTrainStep, bce_loss, make_optimizer
 from csu.data import ellipse_batch
 
 d = torch.device("cuda:0")
+# DIAG=noconv / nolinear: keep that family of weight gradients off the side stream (bisecting a
+# side-stream-in-graph race)
+_diag = os.environ.get("DIAG", "")
+if _diag:
+    from csu import ops
+    _orig_ok, _in_conv = ops._side_ok, [False]
+    _cb = ops._Conv2dFn.backward
+
+    def _conv_bwd(ctx, dy):
+        _in_conv[0] = True
+        try:
+            return _cb(ctx, dy)
+        finally:
+            _in_conv[0] = False
+    ops._Conv2dFn.backward = staticmethod(_conv_bwd)
+    ops._side_ok = lambda *a, **k: (False if (_in_conv[0] == (_diag == "noconv")) else _orig_ok(*a, **k))
 img, K = int(os.environ.get("IMG", "256")), int(os.environ.get("K", "6"))
 torch.manual_seed(0)
 m0 = CSWinTransformer(img_size=img, depth=[1, 2, 9, 1], split_size=[1, 2, 8, 8])
