@@ -3,159 +3,323 @@
 // NOT in the reference: the public SimAM formula, per (b, c) over the
 // n = L positions:  mu = mean(x),  d = x - mu,  v = sum(d^2) / (n - 1),  s = 4 (v + lambda),
 // e = d^2 / s + 1/2,  y = x * sigmoid(e).
-// Statistics: per (image, 64-channel tile, token chunk) Welford partials combined in a fixed
-// order (Chan's formula) -> deterministic and cancellation-free.  Backward, with
-// a = g * x * sigma'(e), A1 = sum(a d), A2 = sum(a d^2):
+// Backward, with a = g * x * sigma'(e), A1 = sum(a d), A2 = sum(a d^2):
 //   dx = g sigma(e) + (2/s)(a d - A1/n) - 8 d A2 / ((n-1) s^2).
+//
+// Layout: one block = 64 channels x one token chunk of one image; lane quad q of a 16-lane row
+// group owns channels 4q..4q+3 (16-B fp32 / 8-B bf16 vector loads, a 64-channel row segment per
+// 16 lanes), the 16 row groups of the block stride over the chunk's tokens.  Statistics are
+// pivot-shifted sums (pivot = the (b, c) value at token 0: cancellation-free to O(1) std of pivot
+// offset) reduced in a fixed order -- per block through LDS, then over the chunks in chunk order
+// by every consumer -- so results are deterministic.  Two launches per direction: partial sums,
+// then the elementwise pass (which folds the chunk combine in and writes y in the consumer's
+// dtype, e.g. bf16 for the concat_linear GEMM that reads the gated skip).
 #include "common.hpp"
 
 namespace csu {
 namespace {
 
 constexpr int NT = 256;
-constexpr int CT = 64;         // channels per block (one per lane of a wave)
-constexpr int TL = NT / CT;    // token lanes per block
+constexpr int CW = 64;           // channels per block
+constexpr int QPR = CW / 4;      // channel quads per row group (16 lanes)
+constexpr int TPP = NT / QPR;    // tokens per pass (16 row groups)
 
-int simam_chunks(int L, int* chunk) {
-    int nch = (L + 1023) / 1024;
-    if (nch > 64) nch = 64;
+struct Geo {
+    int L, C, chunk, nch, ns;   // ns: partial stride per (b, c) = nch rounded up to even (16-B rows)
+};
+
+Geo geo(int B, int L, int C) {
+    Geo g{L, C, 0, 0, 0};
+    const long blocks = (long)B * ((C + CW - 1) / CW);
+    long nch = (1024 + blocks - 1) / blocks;               // ~1024 blocks per launch
+    const long maxc = (L + 4 * TPP - 1) / (4 * TPP);       // >= 4 passes per block
+    if (nch > maxc) nch = maxc;
     if (nch < 1) nch = 1;
-    *chunk = (L + nch - 1) / nch;
-    return nch;
-}
-
-// partial (count, mean, M2) per (b, c, chunk)
-template <typename T>
-__global__ __launch_bounds__(NT) void simam_stats_partial(int L, int C, int chunk, int nch, const T* __restrict__ x,
-                                                          float* __restrict__ part) {
-    __shared__ float sm[3][TL][CT];
-    const int b = blockIdx.z, ch = blockIdx.y;
-    const int cl = threadIdx.x % CT, tl = threadIdx.x / CT;
-    const int c = blockIdx.x * CT + cl;
-    const int t0 = ch * chunk, t1 = min(L, t0 + chunk);
-    float n = 0.f, mu = 0.f, m2 = 0.f;
-    if (c < C) {
-        for (int t = t0 + tl; t < t1; t += TL) {
-            const float v = to_f(x[((size_t)b * L + t) * C + c]);
-            n += 1.f;
-            const float dlt = v - mu;
-            mu += dlt / n;
-            m2 += dlt * (v - mu);
-        }
-    }
-    sm[0][tl][cl] = n; sm[1][tl][cl] = mu; sm[2][tl][cl] = m2;
-    __syncthreads();
-    if (tl == 0 && c < C) {
-        float N = 0.f, M = 0.f, Q = 0.f;
-        for (int j = 0; j < TL; ++j) {
-            const float nb = sm[0][j][cl];
-            if (nb == 0.f) continue;
-            const float dlt = sm[1][j][cl] - M, tot = N + nb;
-            M += dlt * nb / tot;
-            Q += sm[2][j][cl] + dlt * dlt * N * nb / tot;
-            N = tot;
-        }
-        float* p = part + (((size_t)b * C + c) * nch + ch) * 3;
-        p[0] = N; p[1] = M; p[2] = Q;
-    }
-}
-
-// combine chunk partials -> stats[b][c] = (mu, s)
-__global__ void simam_stats_final(int B, int L, int C, int nch, float lam, const float* __restrict__ part,
-                                  float* __restrict__ stats) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= B * C) return;
-    float N = 0.f, M = 0.f, Q = 0.f;
-    for (int j = 0; j < nch; ++j) {
-        const float* p = part + ((size_t)i * nch + j) * 3;
-        if (p[0] == 0.f) continue;
-        const float dlt = p[1] - M, tot = N + p[0];
-        M += dlt * p[0] / tot;
-        Q += p[2] + dlt * dlt * N * p[0] / tot;
-        N = tot;
-    }
-    stats[2 * i] = M;
-    stats[2 * i + 1] = 4.f * (Q / (float)(L - 1) + lam);
+    g.chunk = (int)((L + nch - 1) / nch);
+    g.nch = (int)((L + g.chunk - 1) / g.chunk);
+    g.ns = (g.nch + 1) & ~1;
+    return g;
 }
 
 __device__ __forceinline__ float sigm(float e) { return 1.f / (1.f + __expf(-e)); }
 
+// fixed-order sum over the 16 row groups of a block: sm[tl][k] -> row group 0's lanes
+template <int K>
+__device__ __forceinline__ void rowgroup_sum(float (*sm)[QPR * K], const float* v, float* out, int tl, int q) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) sm[tl][q * K + k] = v[k];
+    __syncthreads();
+    if (tl == 0) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) out[k] = 0.f;
+        for (int j = 0; j < TPP; ++j)
+#pragma unroll
+            for (int k = 0; k < K; ++k) out[k] += sm[j][q * K + k];
+    }
+}
+
+// (sum of [2j], sum of [2j+1]) over j < n, 8 chunks (4 x 16-B loads) in flight per step; fixed
+// order (lane-wise partial sums of the unrolled steps, then combined in a fixed pattern)
+__device__ __forceinline__ void chunk_sums(const float* p, int n, float& s1, float& s2) {
+    f32x4 acc[4] = {};
+    int j = 0;
+    for (; j + 8 <= n; j += 8) {
+        f32x4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const f32x4*>(p + 2 * j + 4 * u);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc[u] += v[u];
+    }
+    s1 = ((acc[0][0] + acc[0][2]) + (acc[1][0] + acc[1][2])) + ((acc[2][0] + acc[2][2]) + (acc[3][0] + acc[3][2]));
+    s2 = ((acc[0][1] + acc[0][3]) + (acc[1][1] + acc[1][3])) + ((acc[2][1] + acc[2][3]) + (acc[3][1] + acc[3][3]));
+    for (; j < n; ++j) {
+        s1 += p[2 * j];
+        s2 += p[2 * j + 1];
+    }
+}
+
+// (mu, s) of the 4 channels c0.. of image b from the chunk partials (chunk order)
+__device__ __forceinline__ void combine_stats(const Geo& g, const float* part, const float* piv, size_t bc0, float lam,
+                                              float* mu, float* s) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        float s1, s2;
+        chunk_sums(part + (bc0 + k) * g.ns * 2, g.nch, s1, s2);
+        const float n = (float)g.L, md = s1 / n;
+        mu[k] = piv[k] + md;
+        s[k] = 4.f * (fmaxf(s2 - s1 * md, 0.f) / (n - 1.f) + lam);
+    }
+}
+
+// partial pivot-shifted (sum d, sum d^2) per (b, c, chunk); part[b][c][chunk][2]
 template <typename T>
-__global__ __launch_bounds__(NT) void simam_apply(int L, int C, const T* __restrict__ x,
-                                                  const float* __restrict__ stats, T* __restrict__ y) {
-    const int b = blockIdx.z;
-    const int c = blockIdx.x * CT + threadIdx.x % CT;
-    if (c >= C) return;
-    const float mu = stats[2 * ((size_t)b * C + c)], rs = 1.f / stats[2 * ((size_t)b * C + c) + 1];
-    for (int t = blockIdx.y * TL + threadIdx.x / CT; t < L; t += gridDim.y * TL) {
-        const size_t i = ((size_t)b * L + t) * C + c;
-        const float v = to_f(x[i]), d = v - mu;
-        y[i] = from_f<T>(v * sigm(d * d * rs + 0.5f));
+__global__ __launch_bounds__(NT) void simam_stats(Geo g, const T* __restrict__ x, float* __restrict__ part) {
+    __shared__ float sm[TPP][QPR * 8];
+    const int b = blockIdx.z, ch = blockIdx.x;
+    const int q = threadIdx.x % QPR, tl = threadIdx.x / QPR;
+    const int c0 = blockIdx.y * CW + 4 * q;
+    const bool ok = c0 < g.C;
+    const int t0 = ch * g.chunk, t1 = min(g.L, t0 + g.chunk);
+    const T* xb = x + (size_t)b * g.L * g.C + c0;
+    float piv[4] = {}, acc[8] = {};
+    if (ok) {
+        load4(xb, piv);
+        auto body = [&](const float* v) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const float d = v[k] - piv[k];
+                acc[2 * k] += d;
+                acc[2 * k + 1] += d * d;
+            }
+        };
+        int t = t0 + tl;
+        for (; t + 3 * TPP < t1; t += 4 * TPP) {   // 4 tokens' loads in flight
+            float v[4][4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) load4(xb + (size_t)(t + u * TPP) * g.C, v[u]);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) body(v[u]);
+        }
+        for (; t < t1; t += TPP) {
+            float v[4];
+            load4(xb + (size_t)t * g.C, v);
+            body(v);
+        }
+    }
+    float tot[8];
+    rowgroup_sum<8>(sm, acc, tot, tl, q);
+    if (tl == 0 && ok) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            float* p = part + (((size_t)b * g.C + c0 + k) * g.ns + ch) * 2;
+            p[0] = tot[2 * k];
+            p[1] = tot[2 * k + 1];
+        }
+    }
+}
+
+// y = x * sigmoid(d^2 / s + 1/2); chunk-0 blocks also write stats[b][c] = (mu, s)
+template <typename T, typename TO>
+__global__ __launch_bounds__(NT) void simam_apply(Geo g, float lam, const T* __restrict__ x, const float* __restrict__ part,
+                                                  TO* __restrict__ y, float* __restrict__ stats) {
+    const int b = blockIdx.z, ch = blockIdx.x;
+    const int q = threadIdx.x % QPR, tl = threadIdx.x / QPR;
+    const int c0 = blockIdx.y * CW + 4 * q;
+    if (c0 >= g.C) return;
+    const size_t off = (size_t)b * g.L * g.C + c0;
+    float piv[4], mu[4], s[4], rs[4];
+    load4(x + off, piv);
+    combine_stats(g, part, piv, (size_t)b * g.C + c0, lam, mu, s);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) rs[k] = 1.f / s[k];
+    if (ch == 0 && tl == 0) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            stats[2 * ((size_t)b * g.C + c0 + k)] = mu[k];
+            stats[2 * ((size_t)b * g.C + c0 + k) + 1] = s[k];
+        }
+    }
+    const int t0 = ch * g.chunk, t1 = min(g.L, t0 + g.chunk);
+    auto body = [&](int t, const float* v) {
+        float o[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const float d = v[k] - mu[k];
+            o[k] = v[k] * sigm(d * d * rs[k] + 0.5f);
+        }
+        store4(y + off + (size_t)t * g.C, o);
+    };
+    int t = t0 + tl;
+    for (; t + 3 * TPP < t1; t += 4 * TPP) {
+        float v[4][4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) load4(x + off + (size_t)(t + u * TPP) * g.C, v[u]);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) body(t + u * TPP, v[u]);
+    }
+    for (; t < t1; t += TPP) {
+        float v[4];
+        load4(x + off + (size_t)t * g.C, v);
+        body(t, v);
     }
 }
 
 // partial (A1, A2) per (b, c, chunk)
-template <typename T>
-__global__ __launch_bounds__(NT) void simam_bwd_partial(int L, int C, int chunk, int nch, const T* __restrict__ x,
-                                                        const T* __restrict__ dy, const float* __restrict__ stats,
-                                                        float* __restrict__ part) {
-    __shared__ float sm[2][TL][CT];
-    const int b = blockIdx.z, ch = blockIdx.y;
-    const int cl = threadIdx.x % CT, tl = threadIdx.x / CT;
-    const int c = blockIdx.x * CT + cl;
-    const int t0 = ch * chunk, t1 = min(L, t0 + chunk);
-    float a1 = 0.f, a2 = 0.f;
-    if (c < C) {
-        const float mu = stats[2 * ((size_t)b * C + c)], rs = 1.f / stats[2 * ((size_t)b * C + c) + 1];
-        for (int t = t0 + tl; t < t1; t += TL) {
-            const size_t i = ((size_t)b * L + t) * C + c;
-            const float v = to_f(x[i]), g = to_f(dy[i]), d = v - mu;
-            const float sg = sigm(d * d * rs + 0.5f);
-            const float a = g * v * sg * (1.f - sg);
-            a1 += a * d;
-            a2 += a * d * d;
+template <typename T, typename TG>
+__global__ __launch_bounds__(NT) void simam_bwd_partial(Geo g, const T* __restrict__ x, const TG* __restrict__ dy,
+                                                        const float* __restrict__ stats, float* __restrict__ part) {
+    __shared__ float sm[TPP][QPR * 8];
+    const int b = blockIdx.z, ch = blockIdx.x;
+    const int q = threadIdx.x % QPR, tl = threadIdx.x / QPR;
+    const int c0 = blockIdx.y * CW + 4 * q;
+    const bool ok = c0 < g.C;
+    const int t0 = ch * g.chunk, t1 = min(g.L, t0 + g.chunk);
+    const size_t off = (size_t)b * g.L * g.C + c0;
+    float acc[8] = {};
+    if (ok) {
+        float mu[4], rs[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            mu[k] = stats[2 * ((size_t)b * g.C + c0 + k)];
+            rs[k] = 1.f / stats[2 * ((size_t)b * g.C + c0 + k) + 1];
+        }
+        auto body = [&](const float* v, const float* gv) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const float d = v[k] - mu[k];
+                const float sg = sigm(d * d * rs[k] + 0.5f);
+                const float a = gv[k] * v[k] * sg * (1.f - sg);
+                acc[2 * k] += a * d;
+                acc[2 * k + 1] += a * d * d;
+            }
+        };
+        int t = t0 + tl;
+        for (; t + 3 * TPP < t1; t += 4 * TPP) {
+            float v[4][4], gv[4][4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                load4(x + off + (size_t)(t + u * TPP) * g.C, v[u]);
+                load4(dy + off + (size_t)(t + u * TPP) * g.C, gv[u]);
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) body(v[u], gv[u]);
+        }
+        for (; t < t1; t += TPP) {
+            float v[4], gv[4];
+            load4(x + off + (size_t)t * g.C, v);
+            load4(dy + off + (size_t)t * g.C, gv);
+            body(v, gv);
         }
     }
-    sm[0][tl][cl] = a1; sm[1][tl][cl] = a2;
-    __syncthreads();
-    if (tl == 0 && c < C) {
-        float s1 = 0.f, s2 = 0.f;
-        for (int j = 0; j < TL; ++j) { s1 += sm[0][j][cl]; s2 += sm[1][j][cl]; }
-        float* p = part + (((size_t)b * C + c) * nch + ch) * 2;
-        p[0] = s1; p[1] = s2;
+    float tot[8];
+    rowgroup_sum<8>(sm, acc, tot, tl, q);
+    if (tl == 0 && ok) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            float* p = part + (((size_t)b * g.C + c0 + k) * g.ns + ch) * 2;
+            p[0] = tot[2 * k];
+            p[1] = tot[2 * k + 1];
+        }
     }
+}
+
+template <typename T, typename TG>
+__global__ __launch_bounds__(NT) void simam_bwd_apply(Geo g, const T* __restrict__ x, const TG* __restrict__ dy,
+                                                      const float* __restrict__ stats, const float* __restrict__ part,
+                                                      T* __restrict__ dx) {
+    const int b = blockIdx.z, ch = blockIdx.x;
+    const int q = threadIdx.x % QPR, tl = threadIdx.x / QPR;
+    const int c0 = blockIdx.y * CW + 4 * q;
+    if (c0 >= g.C) return;
+    const size_t off = (size_t)b * g.L * g.C + c0;
+    const float n = (float)g.L;
+    float mu[4], rs[4], k1[4], k1n[4], k2[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const size_t bc = (size_t)b * g.C + c0 + k;
+        float A1, A2;
+        chunk_sums(part + bc * g.ns * 2, g.nch, A1, A2);
+        mu[k] = stats[2 * bc];
+        rs[k] = 1.f / stats[2 * bc + 1];
+        k1[k] = 2.f * rs[k];
+        k1n[k] = 2.f * rs[k] * A1 / n;
+        k2[k] = 8.f * A2 * rs[k] * rs[k] / (n - 1.f);
+    }
+    const int t0 = ch * g.chunk, t1 = min(g.L, t0 + g.chunk);
+    auto body = [&](int t, const float* v, const float* gv) {
+        float o[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const float d = v[k] - mu[k];
+            const float sg = sigm(d * d * rs[k] + 0.5f);
+            const float a = gv[k] * v[k] * sg * (1.f - sg);
+            o[k] = gv[k] * sg + k1[k] * a * d - k1n[k] - k2[k] * d;
+        }
+        store4(dx + off + (size_t)t * g.C, o);
+    };
+    int t = t0 + tl;
+    for (; t + 3 * TPP < t1; t += 4 * TPP) {
+        float v[4][4], gv[4][4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            load4(x + off + (size_t)(t + u * TPP) * g.C, v[u]);
+            load4(dy + off + (size_t)(t + u * TPP) * g.C, gv[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) body(t + u * TPP, v[u], gv[u]);
+    }
+    for (; t < t1; t += TPP) {
+        float v[4], gv[4];
+        load4(x + off + (size_t)t * g.C, v);
+        load4(dy + off + (size_t)t * g.C, gv);
+        body(t, v, gv);
+    }
+}
+
+dim3 grid_of(int B, const Geo& g) { return dim3(g.nch, (g.C + CW - 1) / CW, B); }
+
+template <typename T>
+int fwd_typed(int B, const Geo& g, float lam, const T* x, int ydtype, void* y, float* stats, float* part, hipStream_t st) {
+    simam_stats<T><<<grid_of(B, g), NT, 0, st>>>(g, x, part);
+    if (ydtype == CSU_BF16) simam_apply<T, bf16><<<grid_of(B, g), NT, 0, st>>>(g, lam, x, part, (bf16*)y, stats);
+    else simam_apply<T, float><<<grid_of(B, g), NT, 0, st>>>(g, lam, x, part, (float*)y, stats);
+    return check_launch("simam_fwd");
 }
 
 template <typename T>
-__global__ __launch_bounds__(NT) void simam_bwd_apply(int L, int C, int nch, const T* __restrict__ x,
-                                                      const T* __restrict__ dy, const float* __restrict__ stats,
-                                                      const float* __restrict__ part, T* __restrict__ dx) {
-    const int b = blockIdx.z;
-    const int c = blockIdx.x * CT + threadIdx.x % CT;
-    if (c >= C) return;
-    const size_t bc = (size_t)b * C + c;
-    float A1 = 0.f, A2 = 0.f;
-    for (int j = 0; j < nch; ++j) {
-        A1 += part[(bc * nch + j) * 2];
-        A2 += part[(bc * nch + j) * 2 + 1];
+int bwd_typed(int B, const Geo& g, const T* x, const float* stats, int gdtype, const void* dy, T* dx, float* part,
+              hipStream_t st) {
+    if (gdtype == CSU_BF16) {
+        simam_bwd_partial<T, bf16><<<grid_of(B, g), NT, 0, st>>>(g, x, (const bf16*)dy, stats, part);
+        simam_bwd_apply<T, bf16><<<grid_of(B, g), NT, 0, st>>>(g, x, (const bf16*)dy, stats, part, dx);
+    } else {
+        simam_bwd_partial<T, float><<<grid_of(B, g), NT, 0, st>>>(g, x, (const float*)dy, stats, part);
+        simam_bwd_apply<T, float><<<grid_of(B, g), NT, 0, st>>>(g, x, (const float*)dy, stats, part, dx);
     }
-    const float mu = stats[2 * bc], s = stats[2 * bc + 1], rs = 1.f / s;
-    const float n = (float)L;
-    const float k1 = 2.f * rs, k1n = 2.f * rs * A1 / n, k2 = 8.f * A2 * rs * rs / (n - 1.f);
-    for (int t = blockIdx.y * TL + threadIdx.x / CT; t < L; t += gridDim.y * TL) {
-        const size_t i = ((size_t)b * L + t) * C + c;
-        const float v = to_f(x[i]), g = to_f(dy[i]), d = v - mu;
-        const float sg = sigm(d * d * rs + 0.5f);
-        const float a = g * v * sg * (1.f - sg);
-        dx[i] = from_f<T>(g * sg + k1 * a * d - k1n - k2 * d);
-    }
+    return check_launch("simam_bwd");
 }
 
-dim3 apply_grid(int B, int L, int C) {
-    int ty = (L + TL * 16 - 1) / (TL * 16);   // ~16 tokens per thread
-    if (ty < 1) ty = 1;
-    return dim3((C + CT - 1) / CT, ty, B);
-}
+bool dt_ok(int d) { return d == CSU_BF16 || d == CSU_F32; }
 
 }  // namespace
 }  // namespace csu
@@ -163,51 +327,30 @@ dim3 apply_grid(int B, int L, int C) {
 using namespace csu;
 
 extern "C" size_t csu_simam_workspace(int B, int L, int C) {
-    int chunk;
-    const int nch = simam_chunks(L, &chunk);
-    return (size_t)B * C * nch * 3 * sizeof(float);
+    if (B < 1 || L < 1 || C < 1) return 0;
+    const Geo g = geo(B, L, C);
+    return (size_t)B * C * g.ns * 2 * sizeof(float);
 }
 
-extern "C" int csu_simam_fwd(int B, int L, int C, float lam, int dtype, const void* x, void* y, float* stats,
-                             void* workspace, size_t ws_bytes, void* stream) {
-    if (B < 1 || L < 2 || C < 1 || !x || !y || !stats) return fail(CSU_E_ARG, "simam_fwd: bad args (need L >= 2)");
+extern "C" int csu_simam_fwd(int B, int L, int C, float lam, int xdtype, const void* x, int ydtype, void* y,
+                             float* stats, void* workspace, size_t ws_bytes, void* stream) {
+    if (B < 1 || L < 2 || C < 4 || C % 4 || !x || !y || !stats)
+        return fail(CSU_E_ARG, "simam_fwd: bad args (need L >= 2, C a multiple of 4)");
+    if (!dt_ok(xdtype) || !dt_ok(ydtype)) return fail(CSU_E_ARG, "simam_fwd: bad dtype");
     if (!workspace || ws_bytes < csu_simam_workspace(B, L, C)) return fail(CSU_E_WORKSPACE, "simam_fwd: workspace");
+    const Geo g = geo(B, L, C);
     hipStream_t st = as_stream(stream);
-    int chunk;
-    const int nch = simam_chunks(L, &chunk);
-    float* part = (float*)workspace;
-    const dim3 pg((C + CT - 1) / CT, nch, B);
-    if (dtype == CSU_BF16) {
-        simam_stats_partial<bf16><<<pg, NT, 0, st>>>(L, C, chunk, nch, (const bf16*)x, part);
-        simam_stats_final<<<(B * C + 255) / 256, 256, 0, st>>>(B, L, C, nch, lam, part, stats);
-        simam_apply<bf16><<<apply_grid(B, L, C), NT, 0, st>>>(L, C, (const bf16*)x, stats, (bf16*)y);
-    } else if (dtype == CSU_F32) {
-        simam_stats_partial<float><<<pg, NT, 0, st>>>(L, C, chunk, nch, (const float*)x, part);
-        simam_stats_final<<<(B * C + 255) / 256, 256, 0, st>>>(B, L, C, nch, lam, part, stats);
-        simam_apply<float><<<apply_grid(B, L, C), NT, 0, st>>>(L, C, (const float*)x, stats, (float*)y);
-    } else {
-        return fail(CSU_E_ARG, "simam_fwd: bad dtype");
-    }
-    return check_launch("simam_fwd");
+    if (xdtype == CSU_BF16) return fwd_typed<bf16>(B, g, lam, (const bf16*)x, ydtype, y, stats, (float*)workspace, st);
+    return fwd_typed<float>(B, g, lam, (const float*)x, ydtype, y, stats, (float*)workspace, st);
 }
 
-extern "C" int csu_simam_bwd(int B, int L, int C, int dtype, const void* x, const float* stats, const void* dy,
-                             void* dx, void* workspace, size_t ws_bytes, void* stream) {
-    if (B < 1 || L < 2 || C < 1 || !x || !stats || !dy || !dx) return fail(CSU_E_ARG, "simam_bwd: bad args");
+extern "C" int csu_simam_bwd(int B, int L, int C, int xdtype, const void* x, const float* stats, int gdtype,
+                             const void* dy, void* dx, void* workspace, size_t ws_bytes, void* stream) {
+    if (B < 1 || L < 2 || C < 4 || C % 4 || !x || !stats || !dy || !dx) return fail(CSU_E_ARG, "simam_bwd: bad args");
+    if (!dt_ok(xdtype) || !dt_ok(gdtype)) return fail(CSU_E_ARG, "simam_bwd: bad dtype");
     if (!workspace || ws_bytes < csu_simam_workspace(B, L, C)) return fail(CSU_E_WORKSPACE, "simam_bwd: workspace");
+    const Geo g = geo(B, L, C);
     hipStream_t st = as_stream(stream);
-    int chunk;
-    const int nch = simam_chunks(L, &chunk);
-    float* part = (float*)workspace;
-    const dim3 pg((C + CT - 1) / CT, nch, B);
-    if (dtype == CSU_BF16) {
-        simam_bwd_partial<bf16><<<pg, NT, 0, st>>>(L, C, chunk, nch, (const bf16*)x, (const bf16*)dy, stats, part);
-        simam_bwd_apply<bf16><<<apply_grid(B, L, C), NT, 0, st>>>(L, C, nch, (const bf16*)x, (const bf16*)dy, stats, part, (bf16*)dx);
-    } else if (dtype == CSU_F32) {
-        simam_bwd_partial<float><<<pg, NT, 0, st>>>(L, C, chunk, nch, (const float*)x, (const float*)dy, stats, part);
-        simam_bwd_apply<float><<<apply_grid(B, L, C), NT, 0, st>>>(L, C, nch, (const float*)x, (const float*)dy, stats, part, (float*)dx);
-    } else {
-        return fail(CSU_E_ARG, "simam_bwd: bad dtype");
-    }
-    return check_launch("simam_bwd");
+    if (xdtype == CSU_BF16) return bwd_typed<bf16>(B, g, (const bf16*)x, stats, gdtype, dy, (bf16*)dx, (float*)workspace, st);
+    return bwd_typed<float>(B, g, (const float*)x, stats, gdtype, dy, (float*)dx, (float*)workspace, st);
 }

@@ -67,10 +67,10 @@ _SIGS = {
                                             c_void_p, ctypes.c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                             c_void_p, c_void_p, c_size_t, c_void_p]),
     "csu_simam_workspace": (c_size_t, [ctypes.c_int, ctypes.c_int, ctypes.c_int]),
-    "csu_simam_fwd": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, c_float, ctypes.c_int, c_void_p, c_void_p,
-                                     c_void_p, c_void_p, c_size_t, c_void_p]),
-    "csu_simam_bwd": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_void_p, c_void_p, c_void_p,
-                                     c_void_p, c_void_p, c_size_t, c_void_p]),
+    "csu_simam_fwd": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, c_float, ctypes.c_int, c_void_p, ctypes.c_int,
+                                     c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "csu_simam_bwd": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_void_p, c_void_p, ctypes.c_int,
+                                     c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
     "csu_carafe_fwd": (ctypes.c_int, [ctypes.c_int] * 6 + [c_void_p] * 5),
     "csu_carafe_bwd": (ctypes.c_int, [ctypes.c_int] * 6 + [c_void_p] * 6),
     "csu_carafe_head_fwd": (ctypes.c_int, [ctypes.c_int] * 6 + [c_void_p] * 7),

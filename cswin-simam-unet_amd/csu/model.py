@@ -421,11 +421,15 @@ class CSWinTransformer(nn.Module):
         return self.simam(t) if self.simam is not None else t
 
     def _share_skip(self, x):
-        """(merge input, decoder skip) for an encoder stage output.  bf16 autocast on the device
-        without SimAM: one shared bf16 copy feeds both the Merge_Block conv and the split-weight
-        concat_linear (ops.shared_cast / ops.concat_linear); otherwise x twice (reference form)."""
-        if self.simam is None and x.is_cuda and torch.is_autocast_enabled("cuda") \
+        """(merge input, decoder skip in bf16 or None) for an encoder stage output.  bf16 autocast
+        on the device: without SimAM one shared bf16 copy feeds both the Merge_Block conv and the
+        split-weight concat_linear (ops.shared_cast / ops.concat_linear); with SimAM the gate writes
+        the bf16 skip for concat_linear in its own pass (no cat, no cast); otherwise x twice
+        (reference form)."""
+        if x.is_cuda and torch.is_autocast_enabled("cuda") \
                 and torch.get_autocast_dtype("cuda") == torch.bfloat16 and x.dtype == torch.float32:
+            if self.simam is not None:
+                return x, self.simam(x, out_dtype=torch.bfloat16)
             return ops.shared_cast(x, torch.bfloat16)
         return x, None
 

@@ -16,39 +16,44 @@ from .ledger import launch, prec_of
 
 class _SimAMFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, lam: float):
+    def forward(ctx, x, lam: float, out_dtype):
         require_device(x)
         x = x.contiguous()
         B, L, C = x.shape
-        y = torch.empty_like(x)
+        y = torch.empty(x.shape, dtype=out_dtype or x.dtype, device=x.device)
         stats = torch.empty(B, C, 2, dtype=torch.float32, device=x.device)
         Lb = lib()
         n = Lb.csu_simam_workspace(B, L, C)
         work = torch.empty(max(n, 16), dtype=torch.uint8, device=x.device)
-        launch("simam_fwd", lambda: Lb.csu_simam_fwd(B, L, C, float(lam), dtype_code(x), ptr(x), ptr(y), ptr(stats),
-                                                     ptr(work), n, stream_ptr(x.device)),
-               8 * x.numel(), 2 * x.numel() * x.element_size(), prec=prec_of(x))
+        # algorithmic bytes: x read twice (statistics pass, gate pass), y written once
+        launch("simam_fwd", lambda: Lb.csu_simam_fwd(B, L, C, float(lam), dtype_code(x), ptr(x), dtype_code(y), ptr(y),
+                                                     ptr(stats), ptr(work), n, stream_ptr(x.device)),
+               12 * x.numel(), x.numel() * (2 * x.element_size() + y.element_size()), prec=prec_of(x))
         ctx.save_for_backward(x, stats)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         x, stats = ctx.saved_tensors
-        dy = dy.to(x.dtype).contiguous()
+        if dy.dtype not in (torch.float32, torch.bfloat16):
+            dy = dy.float()
+        dy = dy.contiguous()
         B, L, C = x.shape
         dx = torch.empty_like(x)
         Lb = lib()
         n = Lb.csu_simam_workspace(B, L, C)
         work = torch.empty(max(n, 16), dtype=torch.uint8, device=x.device)
-        launch("simam_bwd", lambda: Lb.csu_simam_bwd(B, L, C, dtype_code(x), ptr(x), ptr(stats), ptr(dy), ptr(dx),
-                                                     ptr(work), n, stream_ptr(x.device)),
-               16 * x.numel(), 3 * x.numel() * x.element_size(), prec=prec_of(x))
-        return dx, None
+        # x and dy read twice (partial sums, gradient pass), dx written once
+        launch("simam_bwd", lambda: Lb.csu_simam_bwd(B, L, C, dtype_code(x), ptr(x), ptr(stats), dtype_code(dy), ptr(dy),
+                                                     ptr(dx), ptr(work), n, stream_ptr(x.device)),
+               30 * x.numel(), x.numel() * (3 * x.element_size() + 2 * dy.element_size()), prec=prec_of(x))
+        return dx, None, None
 
 
-def simam(x: torch.Tensor, lam: float = 1e-4) -> torch.Tensor:
-    """SimAM on (B, L, C) tokens."""
-    return _SimAMFn.apply(x, lam)
+def simam(x: torch.Tensor, lam: float = 1e-4, out_dtype=None) -> torch.Tensor:
+    """SimAM on (B, L, C) tokens (C a multiple of 4); ``out_dtype``: write the gated output in that
+    dtype (e.g. bf16 for the GEMM that consumes it) from the same pass."""
+    return _SimAMFn.apply(x, lam, out_dtype)
 
 
 class SimAM(nn.Module):
@@ -58,5 +63,5 @@ class SimAM(nn.Module):
         super().__init__()
         self.e_lambda = e_lambda
 
-    def forward(self, x):
-        return simam(x, self.e_lambda)
+    def forward(self, x, out_dtype=None):
+        return simam(x, self.e_lambda, out_dtype)

@@ -124,9 +124,11 @@ int csu_layernorm_bwd_ex(int rows, int C, int xdtype, const void* x, const float
 int csu_layernorm_param_reduce(int rows, int C, const void* workspace, float* dgamma, float* dbeta, void* stream);
 
 size_t csu_simam_workspace(int B, int L, int C);
-int csu_simam_fwd(int B, int L, int C, float lambda, int dtype, const void* x, void* y, float* stats,
+/* y (ydtype, e.g. bf16 for the GEMM that consumes the gated skip) = SimAM(x); C % 4 == 0 */
+int csu_simam_fwd(int B, int L, int C, float lambda, int xdtype, const void* x, int ydtype, void* y, float* stats,
                   void* workspace, size_t ws_bytes, void* stream);
-int csu_simam_bwd(int B, int L, int C, int dtype, const void* x, const float* stats, const void* dy,
+/* dx (xdtype) from dy (gdtype) */
+int csu_simam_bwd(int B, int L, int C, int xdtype, const void* x, const float* stats, int gdtype, const void* dy,
                   void* dx, void* workspace, size_t ws_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------------------

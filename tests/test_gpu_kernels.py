@@ -168,7 +168,8 @@ def test_layernorm_fork_residual_junction(C, gdt):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("shape", [(2, 64, 32), (2, 1024, 64), (1, 4096, 128), (3, 17, 200)])
+@pytest.mark.parametrize("shape", [(2, 64, 32), (2, 1024, 64), (1, 4096, 128), (3, 17, 200), (16, 16384, 64),
+                                   (2, 1000, 256)])
 def test_simam_vs_formula(shape, dtype):
     """SimAM vs the float64 formula (parity unpinned vs the reference, which has no SimAM)."""
     from csu.simam import simam
@@ -184,6 +185,14 @@ def test_simam_vs_formula(shape, dtype):
     y.backward(dy.to(d))
     assert_close(y, ref, dtype)
     assert_close(xd.grad, x64.grad, dtype)
+    # bf16 output for the GEMM consumer (model path), bf16 incoming gradient, x's dtype for dx
+    xb = x.to(d).requires_grad_(True)
+    yb = simam(xb, out_dtype=torch.bfloat16)
+    assert yb.dtype == torch.bfloat16
+    yb.backward(dy.to(d).bfloat16())
+    assert_close(yb, ref, torch.bfloat16)
+    assert xb.grad.dtype == dtype
+    assert_close(xb.grad, x64.grad, torch.bfloat16)
 
 
 def test_cpu_tensor_fails_loudly():
