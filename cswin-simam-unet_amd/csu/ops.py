@@ -467,12 +467,29 @@ def _splitk_wgrad(dy2: torch.Tensor, x2: torch.Tensor) -> torch.Tensor:
     return colsum(part.view(S, N * K)).view(N, K)
 
 
+def gemm_f32(layout: int, a: torch.Tensor, b: torch.Tensor, M: int, N: int, K: int, bias=None, resid=None):
+    """fp32 csu_gemm_f32: layout 0 C = A B^T (+bias, +resid), 1 C = A B, 2 C = A^T B; C (M, N)."""
+    require_device(a, b)
+    out = torch.empty(M, N, dtype=torch.float32, device=a.device)
+    L = lib()
+    n = L.csu_gemm_f32_workspace(layout, M, N, K)
+    work = torch.empty(max(n, 16), dtype=torch.uint8, device=a.device) if n else None
+    name = ("gemm", "gemm", "linear_wgrad")[layout]
+    _launch(name, lambda: L.csu_gemm_f32(layout, M, N, K, ptr(a), ptr(b), ptr(bias), ptr(resid), ptr(out),
+                                         ptr(work), n, stream_ptr(a.device)),
+            2 * M * N * K, (M * K + N * K + M * N) * 4 + (M * N * 4 if resid is not None else 0), prec="f32")
+    return out
+
+
 def linear_wgrad(dy2: torch.Tensor, x2: torch.Tensor, out=None, work=None):
     """(dW (N, K), db (N)) fp32 of a token Linear: one MFMA split-K kernel + one reduction.
     ``out`` / ``work``: caller-allocated result (N*K + N fp32) and workspace buffers."""
     require_device(dy2, x2)
     M, N = dy2.shape
     K = x2.shape[1]
+    if dy2.dtype == torch.float32 and out is None:
+        # fp32: MFMA GEMM dW = dy^T x (token splits + ordered slab sum) and the column sum for db
+        return gemm_f32(2, dy2.contiguous(), x2.contiguous(), N, K, M), colsum(dy2)
     L = lib()
     n = L.csu_linear_wgrad_workspace(M, N, K)
     if out is None:
@@ -625,12 +642,19 @@ class _LinearFn(torch.autograd.Function):
             wc = weight.to(cd)
         K, N = xc.shape[-1], wc.shape[0]
         ctx.fast = FUSED_GEMM and cd == torch.bfloat16 and xc.is_cuda and _gemm_ok(K, N)
+        ctx.f32 = False
         wt = None
         if ctx.fast:
             x2 = xc.reshape(-1, K).contiguous()
             y = gemm(x2, wc, False, odt or cd, bias=None if bias is None else bias.detach().float().contiguous())
             y = y.view(*xc.shape[:-1], N)
             wt = _weight_t(weight, wc)
+        elif cd == torch.float32 and xc.is_cuda and K % 4 == 0 and N % 4 == 0:
+            # fp32 path (no autocast, BASELINE config 2): csu fp32 MFMA GEMM, bias in its epilogue
+            x2 = xc.reshape(-1, K).contiguous()
+            y = gemm_f32(0, x2, wc.contiguous(), x2.shape[0], N, K,
+                         bias=None if bias is None else bias.detach().contiguous()).view(*xc.shape[:-1], N)
+            ctx.f32 = True
         else:
             bc = None
             if bias is not None:
@@ -660,6 +684,8 @@ class _LinearFn(torch.autograd.Function):
             if ctx.fast:
                 odt = xdt if xdt in (torch.float32, torch.bfloat16) else wc.dtype
                 dx = gemm(dy2, wc, False, odt).view(xc.shape)
+            elif ctx.f32:
+                dx = gemm_f32(1, dy2, wc.contiguous(), dy2.shape[0], K, N).view(xc.shape)
             else:
                 dx = (dy2 @ wc).view(xc.shape)
             if dx.dtype != xdt:

@@ -290,6 +290,19 @@ int csu_rng_advance(uint64_t* state, uint64_t* snap, void* stream);
 int csu_droppath_scale(long n, const uint64_t* rng, unsigned site, float p, float* out, void* stream);
 
 /* ---------------------------------------------------------------------------------------
+ * fp32 GEMMs of the fp32 training path (token Linear forward / input / weight gradient, BASELINE
+ * config 2), on the fp32 MFMA.  Row-major, C (M, N):
+ *   layout 0: C = A (M,K) B(N,K)^T [+ bias (N)] [+ resid (M,N)]   (nn.Linear forward)
+ *   layout 1: C = A (M,K) B(K,N)                                    (input gradient dy W)
+ *   layout 2: C = A(K,M)^T B(K,N)                                   (weight gradient dy^T x; token
+ *             splits reduced in a fixed order through `workspace`, csu_gemm_f32_workspace bytes)
+ * Row lengths (K for A in layouts 0/1, M in layout 2, N, K of B in layout 0) multiples of 4.
+ * ------------------------------------------------------------------------------------- */
+size_t csu_gemm_f32_workspace(int layout, long M, int N, long K);
+int csu_gemm_f32(int layout, long M, int N, long K, const float* A, const float* B, const float* bias,
+                 const float* resid, float* C, void* workspace, size_t ws_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------------------
  * Fused Mlp + residual (Mlp cswin:180-196 with the residual add of CSWinBlock cswin:368):
  * fc1 -> GELU -> fc2 with the 4C hidden layer kept on chip.  x (M, C) bf16; w1 (4C, C) and
  * w2 (C, 4C) bf16 nn.Linear weights; b1 (4C), b2 (C) fp32; res / out (M, C) fp32 (may alias).

@@ -645,3 +645,29 @@ def test_concat_linear_and_shared_cast_vs_fp64(B, L, C, N):
         ref = ref.detach()
         err = float((got.double() - ref).norm() / ref.norm().clamp_min(1e-30))
         assert err <= 2e-2, (name, err)
+
+
+@pytest.mark.parametrize("layout,M,N,K", [(0, 4096, 192, 64), (0, 37, 64, 128), (0, 1000, 256, 1024), (1, 4096, 64, 192),
+                                          (1, 300, 512, 128), (2, 192, 64, 32768), (2, 1024, 256, 4096), (2, 64, 16, 100)])
+def test_gemm_f32_layouts(layout, M, N, K):
+    """csu_gemm_f32 (fp32 MFMA: Linear forward / input gradient / weight gradient with ordered
+    token splits) vs fp64; bias + residual epilogue on layout 0; bitwise repeatable."""
+    from csu import ops
+    d = dev()
+    g = torch.Generator().manual_seed(M + N + K + layout)
+    if layout == 0:
+        a, b = torch.randn(M, K, generator=g), torch.randn(N, K, generator=g)
+        bias, res = torch.randn(N, generator=g), torch.randn(M, N, generator=g)
+        ref = a.double() @ b.double().T + bias.double() + res.double()
+        out = ops.gemm_f32(0, a.to(d), b.to(d), M, N, K, bias=bias.to(d), resid=res.to(d))
+    elif layout == 1:
+        a, b = torch.randn(M, K, generator=g), torch.randn(K, N, generator=g)
+        ref = a.double() @ b.double()
+        out = ops.gemm_f32(1, a.to(d), b.to(d), M, N, K)
+    else:
+        a, b = torch.randn(K, M, generator=g), torch.randn(K, N, generator=g)
+        ref = a.double().T @ b.double()
+        out = ops.gemm_f32(2, a.to(d), b.to(d), M, N, K)
+        again = ops.gemm_f32(2, a.to(d), b.to(d), M, N, K)
+        assert torch.equal(out, again)
+    assert_close(out, ref, torch.float32)
