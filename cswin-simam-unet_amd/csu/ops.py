@@ -467,18 +467,21 @@ def _splitk_wgrad(dy2: torch.Tensor, x2: torch.Tensor) -> torch.Tensor:
     return colsum(part.view(S, N * K)).view(N, K)
 
 
-def gemm_f32(layout: int, a: torch.Tensor, b: torch.Tensor, M: int, N: int, K: int, bias=None, resid=None):
-    """fp32 csu_gemm_f32: layout 0 C = A B^T (+bias, +resid), 1 C = A B, 2 C = A^T B; C (M, N)."""
+def gemm_f32(layout: int, a: torch.Tensor, b: torch.Tensor, M: int, N: int, K: int, bias=None, resid=None,
+             with_asum=False):
+    """fp32 csu_gemm_f32: layout 0 C = A B^T (+bias, +resid), 1 C = A B, 2 C = A^T B; C (M, N).
+    ``with_asum`` (layout 2): also return sum_k A[k][m] (the bias gradient) from the same launch."""
     require_device(a, b)
     out = torch.empty(M, N, dtype=torch.float32, device=a.device)
+    asum = torch.empty(M, dtype=torch.float32, device=a.device) if with_asum else None
     L = lib()
     n = L.csu_gemm_f32_workspace(layout, M, N, K)
     work = torch.empty(max(n, 16), dtype=torch.uint8, device=a.device) if n else None
     name = ("gemm", "gemm", "linear_wgrad")[layout]
-    _launch(name, lambda: L.csu_gemm_f32(layout, M, N, K, ptr(a), ptr(b), ptr(bias), ptr(resid), ptr(out),
+    _launch(name, lambda: L.csu_gemm_f32(layout, M, N, K, ptr(a), ptr(b), ptr(bias), ptr(resid), ptr(out), ptr(asum),
                                          ptr(work), n, stream_ptr(a.device)),
             2 * M * N * K, (M * K + N * K + M * N) * 4 + (M * N * 4 if resid is not None else 0), prec="f32")
-    return out
+    return (out, asum) if with_asum else out
 
 
 def linear_wgrad(dy2: torch.Tensor, x2: torch.Tensor, out=None, work=None):
@@ -489,7 +492,7 @@ def linear_wgrad(dy2: torch.Tensor, x2: torch.Tensor, out=None, work=None):
     K = x2.shape[1]
     if dy2.dtype == torch.float32 and out is None:
         # fp32: MFMA GEMM dW = dy^T x (token splits + ordered slab sum) and the column sum for db
-        return gemm_f32(2, dy2.contiguous(), x2.contiguous(), N, K, M), colsum(dy2)
+        return gemm_f32(2, dy2.contiguous(), x2.contiguous(), N, K, M, with_asum=True)
     L = lib()
     n = L.csu_linear_wgrad_workspace(M, N, K)
     if out is None:

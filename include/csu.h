@@ -297,10 +297,11 @@ int csu_droppath_scale(long n, const uint64_t* rng, unsigned site, float p, floa
  *   layout 2: C = A(K,M)^T B(K,N)                                   (weight gradient dy^T x; token
  *             splits reduced in a fixed order through `workspace`, csu_gemm_f32_workspace bytes)
  * Row lengths (K for A in layouts 0/1, M in layout 2, N, K of B in layout 0) multiples of 4.
+ * asum (layout 2 only, or NULL): asum[m] = sum_k A[k][m] -- the bias gradient of dW = dy^T x.
  * ------------------------------------------------------------------------------------- */
 size_t csu_gemm_f32_workspace(int layout, long M, int N, long K);
 int csu_gemm_f32(int layout, long M, int N, long K, const float* A, const float* B, const float* bias,
-                 const float* resid, float* C, void* workspace, size_t ws_bytes, void* stream);
+                 const float* resid, float* C, float* asum, void* workspace, size_t ws_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * Fused Mlp + residual (Mlp cswin:180-196 with the residual add of CSWinBlock cswin:368):

@@ -667,7 +667,8 @@ def test_gemm_f32_layouts(layout, M, N, K):
     else:
         a, b = torch.randn(K, M, generator=g), torch.randn(K, N, generator=g)
         ref = a.double().T @ b.double()
-        out = ops.gemm_f32(2, a.to(d), b.to(d), M, N, K)
-        again = ops.gemm_f32(2, a.to(d), b.to(d), M, N, K)
-        assert torch.equal(out, again)
+        out, asum = ops.gemm_f32(2, a.to(d), b.to(d), M, N, K, with_asum=True)
+        again, asum2 = ops.gemm_f32(2, a.to(d), b.to(d), M, N, K, with_asum=True)
+        assert torch.equal(out, again) and torch.equal(asum, asum2)
+        assert_close(asum, a.double().sum(0), torch.float32)
     assert_close(out, ref, torch.float32)
