@@ -45,7 +45,9 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=16, help="images per GPU")
     ap.add_argument("--img", type=int, default=512)
-    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32", "fp8"],
+                    help="fp8: e4m3 Linear weights (per-row power-of-two scales), bf16 activations, fp32 accumulate "
+                         "(BASELINE config 5)")
     ap.add_argument("--depth", default="1,2,9,1")
     ap.add_argument("--split", default="1,2,8,8")
     ap.add_argument("--simam", action="store_true")
@@ -138,7 +140,7 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     device = torch.device("cuda", local)
     torch.backends.cudnn.benchmark = True
-    dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+    dtype = torch.float32 if args.dtype == "fp32" else torch.bfloat16
 
     from csu import ops
     from csu.model import CSWinTransformer
@@ -150,6 +152,8 @@ def main():
     pd = args.dropout
     model = CSWinTransformer(img_size=args.img, depth=depth, split_size=split, simam=args.simam,
                              drop_rate=pd, attn_drop_rate=pd, drop_path_rate=pd).to(device)
+    if args.dtype == "fp8":
+        model.set_weight_format("fp8_e4m3")
     nparams = sum(p.numel() for p in model.parameters())
     use_graph = args.graph in ("on", "auto")
     reducer = None
@@ -235,7 +239,7 @@ def main():
         rec = {"metric": _metric(args), "value": round(images / el, 3),
                "unit": "images/sec", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
                "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
-               "vs_baseline": None, "dtype": args.dtype, "data": "synthetic (ellipse masks, SURVEY §8d), random-init weights",
+               "vs_baseline": None, "dtype": "bf16 (fp8-e4m3 weights)" if args.dtype == "fp8" else args.dtype, "data": "synthetic (ellipse masks, SURVEY §8d), random-init weights",
                "config": {"workload": f"CSWin-UNet train step {args.img}x{args.img} depth {depth} split {split}"
                                       f"{' +SimAM' if args.simam else ''}"
                                       f"{f', dropout/attn_drop/drop_path {pd}' if pd > 0 else ''}, AdamW",

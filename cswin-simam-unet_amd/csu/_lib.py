@@ -101,6 +101,7 @@ _SIGS = {
     "csu_gemm_f32_workspace": (c_size_t, [ctypes.c_int, ctypes.c_long, ctypes.c_int, ctypes.c_long]),
     "csu_gemm_f32": (ctypes.c_int, [ctypes.c_int, ctypes.c_long, ctypes.c_int, ctypes.c_long, c_void_p, c_void_p, c_void_p,
                                     c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "csu_quant_e4m3_batch": (ctypes.c_int, [c_void_p, ctypes.c_int, ctypes.c_long, c_void_p]),
     "csu_mlp_supported": (ctypes.c_int, [ctypes.c_int]),
     "csu_dropout_apply": (ctypes.c_int, [ctypes.c_long, ctypes.c_int, ctypes.c_int, c_void_p, c_void_p, ctypes.c_int,
                                          c_void_p, c_void_p, ctypes.c_long, c_void_p, ctypes.c_uint, c_float, c_void_p]),

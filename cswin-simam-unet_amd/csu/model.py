@@ -512,13 +512,28 @@ class CSWinTransformer(nn.Module):
             elif isinstance(m, CARAFE):
                 yield m.encoder.weight
 
+    def set_weight_format(self, fmt: str = "bf16"):
+        """'bf16' (default) or 'fp8_e4m3' (BASELINE config 5: fp8-e4m3 Linear weights with per-row
+        power-of-two scales, bf16 activations, fp32 accumulate; applies under bf16 autocast)."""
+        if fmt not in ("bf16", "fp8_e4m3"):
+            raise ValueError(f"weight format {fmt!r}")
+        self._weight_format = fmt
+        self._fp8 = None
+        return self
+
     def forward(self, x):
         cd = _compute_dtype(x)
         if cd != torch.float32 and x.is_cuda:
             if not hasattr(self, "_cast_cache"):
                 self._cast_cache = ops.CastCache()
+            weights = list(self._linear_weights())
+            sources = None
+            if getattr(self, "_weight_format", "bf16") == "fp8_e4m3" and cd == torch.bfloat16:
+                if self._fp8 is None or not self._fp8.valid_for(weights):
+                    self._fp8 = ops.Fp8Weights(weights)
+                sources = self._fp8.quantize()     # one launch: e4m3 per row, dequantised fp32 copies
             # one launch per step: bf16 shadows of every Linear weight (+ transposes) and conv layouts
-            self._cast_cache.refresh(self._linear_weights(), cd, self._conv_weights())
+            self._cast_cache.refresh(weights, cd, self._conv_weights(), sources=sources)
             ops.set_cast_cache(self._cast_cache)
         try:
             return self._forward(x)

@@ -995,8 +995,10 @@ class CastCache:
                                  ("tile0", "<i8"), ("taps", "<i4"), ("pad", "<i4")])
         return cls._REC
 
-    def _build(self, params, convs, dtype):
+    def _build(self, params, convs, dtype, sources=None):
         self.params, self.convs, self.dtype = params, convs, dtype
+        self.sources = sources
+        src = sources if sources is not None else params
         self.ptrs = [p.data_ptr() for p in params + convs]
         self.shadow = [torch.empty(p.shape, dtype=dtype, device=p.device) for p in params]
         self.shadow_t = [torch.empty(p.shape[1:].numel() if p.dim() > 1 else 0, p.shape[0], dtype=dtype, device=p.device)
@@ -1016,7 +1018,8 @@ class CastCache:
                 rows = p.shape[0] if p.dim() > 1 else 1
                 cols = p.numel() // rows
                 st = self.shadow_t[i]
-                rec[i] = (p.data_ptr(), self.shadow[i].data_ptr(), 0 if st is None else st.data_ptr(), rows, cols, t0, 0, 0)
+                rec[i] = (src[i].data_ptr(), self.shadow[i].data_ptr(), 0 if st is None else st.data_ptr(), rows, cols, t0,
+                          0, 0)
                 t0 += -(-rows // 64) * -(-cols // 64)
             for j, w in enumerate(convs):
                 N, C, KH, KW = w.shape
@@ -1026,13 +1029,17 @@ class CastCache:
             self.tiles = t0
             self.items = torch.frombuffer(bytearray(rec.tobytes()), dtype=torch.uint8).to(allp[0].device)
 
-    def refresh(self, params, dtype, convs=()):
+    def refresh(self, params, dtype, convs=(), sources=None):
+        """``sources``: per param, the fp32 tensor the shadow is made from (default: the param
+        itself; the fp8 weight format passes its dequantised e4m3 copies, Fp8Weights)."""
         params, convs = list(params), list(convs)
         allp = params + convs
         if (self.dtype != dtype or len(params) != len(self.params) or len(convs) != len(self.convs)
                 or any(a is not b for a, b in zip(allp, self.params + self.convs))
-                or any(p.data_ptr() != q for p, q in zip(allp, self.ptrs))):
-            self._build(params, convs, dtype)
+                or any(p.data_ptr() != q for p, q in zip(allp, self.ptrs))
+                or (sources is None) != (getattr(self, "sources", None) is None)
+                or (sources is not None and any(a is not b for a, b in zip(sources, self.sources)))):
+            self._build(params, convs, dtype, sources)
         if self.items is not None:
             n = sum(p.numel() for p in allp)
             nt = sum(p.numel() for p in self.params if p.dim() > 1) + sum(w.numel() for w in self.convs)
@@ -1040,10 +1047,11 @@ class CastCache:
                                                                          stream_ptr(allp[0].device)),
                     0, n * 6 + nt * 2)
             return
+        src = self.sources if getattr(self, "sources", None) is not None else self.params
         with torch.no_grad():
             if self.params:
-                torch._foreach_copy_(self.shadow, [p.detach() for p in self.params])
-            for st, p in zip(self.shadow_t, self.params):
+                torch._foreach_copy_(self.shadow, [p.detach() for p in src])
+            for st, p in zip(self.shadow_t, src):
                 if st is not None:
                     st.copy_(p.detach().reshape(p.shape[0], -1).t())
             for w, o, i in zip(self.convs, self.conv_o, self.conv_i):
@@ -1070,6 +1078,53 @@ class CastCache:
         if j is None or self.dtype != dtype or tuple(self.convs[j].shape) != tuple(w.shape):
             return None
         return self.conv_o[j], self.conv_i[j]
+
+
+class Fp8Weights:
+    """fp8-e4m3 weights (BASELINE config 5): the listed fp32 master weights quantised per output
+    row to e4m3 with power-of-two scales (csu_quant_e4m3_batch, one launch per step); ``deq`` are
+    the dequantised fp32 copies (exact in bf16) that the cast cache turns into the kernels' bf16
+    shadows, ``q`` / ``scales`` the e4m3 bytes and row scales.  Gradients flow to the fp32 masters
+    (straight-through).  1-D tensors (biases, LN) are not quantised."""
+
+    def __init__(self, params):
+        import numpy as np
+        self.params = list(params)
+        self.deq, self.q, self.scales = [], [], []
+        rec = np.zeros(0, dtype=[("src", "<u8"), ("dst", "<u8"), ("dq", "<u8"), ("sc", "<u8"), ("row0", "<i8"),
+                                 ("rows", "<i4"), ("cols", "<i4")])
+        recs, row0 = [], 0
+        for p in self.params:
+            if p.dim() < 2:
+                self.deq.append(p)
+                self.q.append(None)
+                self.scales.append(None)
+                continue
+            rows = p.shape[0]
+            cols = p.numel() // rows
+            d = torch.empty_like(p)
+            q = torch.empty(p.shape, dtype=torch.uint8, device=p.device)
+            sc = torch.empty(rows, dtype=torch.float32, device=p.device)
+            self.deq.append(d)
+            self.q.append(q)
+            self.scales.append(sc)
+            recs.append((p.data_ptr(), d.data_ptr(), q.data_ptr(), sc.data_ptr(), row0, rows, cols))
+            row0 += rows
+        rec = np.array(recs, dtype=rec.dtype)
+        self.count, self.rows = len(recs), row0
+        self.items = torch.frombuffer(bytearray(rec.tobytes()), dtype=torch.uint8).to(self.params[0].device)
+        self.ptrs = [p.data_ptr() for p in self.params]
+
+    def valid_for(self, params) -> bool:
+        params = list(params)
+        return len(params) == len(self.params) and all(a is b and a.data_ptr() == q
+                                                       for a, b, q in zip(params, self.params, self.ptrs))
+
+    def quantize(self):
+        dev = self.params[0].device
+        _launch("quant_e4m3", lambda: lib().csu_quant_e4m3_batch(ptr(self.items), self.count, self.rows, stream_ptr(dev)),
+                0, sum(p.numel() for p, q in zip(self.params, self.q) if q is not None) * 9)
+        return self.deq
 
 
 _ACTIVE_CACHE: Optional[CastCache] = None

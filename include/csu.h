@@ -248,6 +248,21 @@ typedef struct {
 } csu_cast_item;
 int csu_cast_bf16_batch(const csu_cast_item* items, int count, long total_tiles, void* stream);
 
+/* fp8-e4m3 weights (BASELINE config 5): per item (rows x cols fp32 row-major, row = output feature),
+ * per row the power-of-two scale s = 2^ceil(log2(amax/448)), q = e4m3fn(w / s) (RNE), and
+ * dst = q * s in fp32 (exact in bf16: the cast cache then makes the kernels' bf16 shadows from it);
+ * dst_q (optional) the e4m3 bytes, scales (optional) s per row.  items: DEVICE array sorted by
+ * row0 (prefix sum of rows); one block per row of every item. */
+typedef struct {
+    const float* src;
+    float* dst;
+    uint8_t* dst_q;
+    float* scales;
+    int64_t row0;
+    int32_t rows, cols;
+} csu_fp8_item;
+int csu_quant_e4m3_batch(const csu_fp8_item* items, int count, long total_rows, void* stream);
+
 /* ---------------------------------------------------------------------------------------
  * Fused multi-tensor AdamW step (torch.optim.AdamW semantics, cswin:937-941): for every item,
  * param *= 1 - lr*wd; m = lerp(m, g, 1-beta1); v = beta2 v + (1-beta2) g^2;
