@@ -639,6 +639,97 @@ __global__ __launch_bounds__(NT, 4) void lepe_wgrad_partial(csu_stripe_args a, c
     }
 }
 
+// LePE weight gradient, tiled (bf16 / fp32): block = (image b, TY image rows, one head's 32
+// channels of one branch).  The rows' dout and the V rows with a one-row halo are staged in LDS
+// with 16-B loads (each token's head slice is one contiguous 64 / 128-B piece), then thread
+// (quad q, token lane) accumulates dW[c][tap] += dout[q][c] * V[q + off(tap)][c] (window-local
+// zero padding) and db[c] += dout[q][c] for 4 channels over the tile's tokens from LDS; the 32
+// token lanes of a quad are reduced by a fixed xor tree + the 4 waves in order.  Partial layout
+// [branch][c * 10 + tap][block] as lepe_wgrad_partial's, block = b * nty + row tile.
+template <typename T>
+__global__ __launch_bounds__(NT) void lepe_wgrad_tiles(csu_stripe_args a, int ty_rows, const T* __restrict__ qkv,
+                                                      const T* __restrict__ dout, float* __restrict__ part) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lw_smem[];
+    __shared__ float red[4][8][40];
+    typedef typename Raw4<T>::type R4;
+    constexpr int CPT = HD * (int)sizeof(T) / 16;   // 16-B chunks per token slice
+    const int br = blockIdx.z, head = blockIdx.y;
+    const csu_stripe_branch& g = branch(a, br);
+    const int reso = a.reso, L = reso * reso, C = a.C, C3 = 3 * C;
+    const int nty = (reso + ty_rows - 1) / ty_rows;
+    const int b = blockIdx.x / nty, y0 = (blockIdx.x % nty) * ty_rows;
+    const int ch = g.ch_off + head * HD;
+    T* Vt = reinterpret_cast<T*>(lw_smem);                       // [(ty + 2)][reso][HD]
+    T* Gt = Vt + (size_t)(ty_rows + 2) * reso * HD;             // [ty][reso][HD]
+    const int vrows = ty_rows + 2;
+    const int nchunk = (vrows + ty_rows) * reso * CPT;
+    for (int i = threadIdx.x; i < nchunk; i += NT) {
+        const int part_ = i % CPT, tok = (i / CPT) % reso, row = i / (CPT * reso);
+        const bool isv = row < vrows;
+        const int y = isv ? y0 - 1 + row : y0 + row - vrows;
+        u32x4 v = {0, 0, 0, 0};
+        if (y >= 0 && y < reso) {
+            const T* src = isv ? qkv + ((size_t)b * L + (size_t)y * reso + tok) * C3 + 2 * C + ch
+                               : dout + ((size_t)b * L + (size_t)y * reso + tok) * C + ch;
+            v = *reinterpret_cast<const u32x4*>(reinterpret_cast<const unsigned char*>(src) + 16 * part_);
+        }
+        T* dst = (isv ? Vt + ((size_t)row * reso + tok) * HD : Gt + ((size_t)(row - vrows) * reso + tok) * HD);
+        *reinterpret_cast<u32x4*>(reinterpret_cast<unsigned char*>(dst) + 16 * part_) = v;
+    }
+    __syncthreads();
+    const int q = threadIdx.x & 7, tl = threadIdx.x >> 3;
+    float acc[40];
+#pragma unroll
+    for (int i = 0; i < 40; ++i) acc[i] = 0.f;
+    const int ntok = ty_rows * reso;
+    for (int t = tl; t < ntok; t += NT / 8) {
+        const int yy = t / reso, x = t - yy * reso, y = y0 + yy;
+        if (y >= reso) break;
+        const int iy = y % g.H_sp, ix = x % g.W_sp;
+        const R4 gq = *reinterpret_cast<const R4*>(Gt + ((size_t)yy * reso + x) * HD + 4 * q);
+#pragma unroll
+        for (int dy = 0; dy < 3; ++dy) {
+            const bool yok = iy + dy - 1 >= 0 && iy + dy - 1 < g.H_sp;
+#pragma unroll
+            for (int dx = 0; dx < 3; ++dx) {
+                const bool ok = yok && ix + dx - 1 >= 0 && ix + dx - 1 < g.W_sp;
+                if (!ok) continue;
+                const R4 vq = *reinterpret_cast<const R4*>(Vt + ((size_t)(yy + dy) * reso + x + dx - 1) * HD + 4 * q);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc[(dy * 3 + dx) * 4 + j] += Raw4<T>::at(gq, j) * Raw4<T>::at(vq, j);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[36 + j] += Raw4<T>::at(gq, j);
+    }
+    // token lanes of a quad: lane bits 3..5 inside the wave, then the 4 waves in order
+#pragma unroll
+    for (int m = 8; m < 64; m <<= 1)
+#pragma unroll
+        for (int i = 0; i < 40; ++i) acc[i] += __shfl_xor(acc[i], m, 64);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane < 8)
+#pragma unroll
+        for (int i = 0; i < 40; ++i) red[wave][lane][i] = acc[i];
+    __syncthreads();
+    const int Cb = a.heads * HD, nblk = a.B * nty;
+    for (int o = threadIdx.x; o < 8 * 40; o += NT) {
+        const int qq = o / 40, i = o % 40;
+        const float sum = ((red[0][qq][i] + red[1][qq][i]) + red[2][qq][i]) + red[3][qq][i];
+        const int k = i >> 2, c = head * HD + 4 * qq + (i & 3);
+        part[((size_t)br * Cb * 10 + c * 10 + k) * nblk + blockIdx.x] = sum;
+    }
+}
+
+// rows per LePE tile so that the staged V (+halo) and dout fit 64 KiB of dynamic LDS (two blocks
+// per CU); 0: use the untiled kernel
+int lepe_tile_rows(const csu_stripe_args& a, int dtype) {
+    const size_t es = dtype == CSU_BF16 ? 2 : 4;
+    for (int ty : {4, 2, 1})
+        if ((size_t)(2 * ty + 2) * a.reso * HD * es <= 64 * 1024) return ty;
+    return 0;
+}
+
 // one wave per (branch, value): lanes stride over the block partials (contiguous), then a fixed
 // xor-shuffle tree -- deterministic
 __global__ __launch_bounds__(256) void lepe_wgrad_reduce(csu_stripe_args a, int nblk, const float* __restrict__ part) {
@@ -1201,9 +1292,36 @@ extern "C" int csu_stripe_attn_fwd(const csu_stripe_args* a, int dtype, const vo
     return check_launch("stripe_attn_fwd");
 }
 
+// LePE weight-gradient partial blocks of a launch (tiled kernel if its tile fits, else untiled)
+int lepe_nblk(const csu_stripe_args& a, int dtype) {
+    const int ty = lepe_tile_rows(a, dtype);
+    return ty ? a.B * ((a.reso + ty - 1) / ty) : wgrad_blocks(a);
+}
+
+void lepe_wgrad_launch(const csu_stripe_args& a, int dtype, const void* qkv, const void* dout, float* part, hipStream_t st) {
+    const int ty = lepe_tile_rows(a, dtype);
+    const int nblk = lepe_nblk(a, dtype);
+    if (ty) {
+        const size_t es = dtype == CSU_BF16 ? 2 : 4;
+        const size_t lds = (size_t)(2 * ty + 2) * a.reso * HD * es;
+        const dim3 g((unsigned)nblk, (unsigned)a.heads, (unsigned)a.nbranch);
+        if (dtype == CSU_BF16) lepe_wgrad_tiles<bf16><<<g, NT, lds, st>>>(a, ty, (const bf16*)qkv, (const bf16*)dout, part);
+        else lepe_wgrad_tiles<float><<<g, NT, lds, st>>>(a, ty, (const float*)qkv, (const float*)dout, part);
+    } else if (dtype == CSU_BF16) {
+        lepe_wgrad_partial<bf16><<<dim3(nblk, a.nbranch), NT, 0, st>>>(a, (const bf16*)qkv, (const bf16*)dout, part);
+    } else {
+        lepe_wgrad_partial<float><<<dim3(nblk, a.nbranch), NT, 0, st>>>(a, (const float*)qkv, (const float*)dout, part);
+    }
+    const dim3 rgrid((a.nbranch * a.heads * HD * 10 + 3) / 4);
+    lepe_wgrad_reduce<<<rgrid, 256, 0, st>>>(a, nblk, part);
+}
+
 extern "C" size_t csu_stripe_attn_bwd_workspace(const csu_stripe_args* a) {
     if (!a) return 0;
-    return (size_t)a->nbranch * wgrad_blocks(*a) * a->heads * HD * 10 * sizeof(float);
+    // enough for either partial layout (dtype decided at launch)
+    int n = wgrad_blocks(*a);
+    for (int dt : {CSU_BF16, CSU_F32}) n = n > lepe_nblk(*a, dt) ? n : lepe_nblk(*a, dt);
+    return (size_t)a->nbranch * n * a->heads * HD * 10 * sizeof(float);
 }
 
 extern "C" int csu_stripe_attn_bwd(const csu_stripe_args* a, int dtype, const void* qkv, const void* out,
@@ -1225,10 +1343,7 @@ extern "C" int csu_stripe_attn_bwd(const csu_stripe_args* a, int dtype, const vo
     }
     hipStream_t st = as_stream(stream);
     const dim3 grid = grid_of(*a);
-    const int nblk = wgrad_blocks(*a);
     float* part = (float*)workspace;
-    const int Cb = a->heads * HD;
-    const dim3 rgrid((a->nbranch * Cb * 10 + 3) / 4);
     if (use_window_path(*a, dtype)) {
         const int sp = wsplit(*a);
         const int nwin = (a->reso / a->br[0].H_sp) * (a->reso / a->br[0].W_sp);
@@ -1244,13 +1359,7 @@ extern "C" int csu_stripe_attn_bwd(const csu_stripe_args* a, int dtype, const vo
     } else {
         bwd_generic<float>(*a, grid, (const float*)qkv, (const float*)out, (const float*)dout, lse, delta, (float*)dqkv, st);
     }
-    if (do_lepe) {
-        if (dtype == CSU_BF16)
-            lepe_wgrad_partial<bf16><<<dim3(nblk, a->nbranch), NT, 0, st>>>(*a, (const bf16*)qkv, (const bf16*)dout, part);
-        else
-            lepe_wgrad_partial<float><<<dim3(nblk, a->nbranch), NT, 0, st>>>(*a, (const float*)qkv, (const float*)dout, part);
-        lepe_wgrad_reduce<<<rgrid, 256, 0, st>>>(*a, nblk, part);
-    }
+    if (do_lepe) lepe_wgrad_launch(*a, dtype, qkv, dout, part, st);
     return check_launch("stripe_attn_bwd");
 }
 
@@ -1264,14 +1373,6 @@ extern "C" int csu_stripe_lepe_wgrad(const csu_stripe_args* a, int dtype, const 
         return fail(CSU_E_WORKSPACE, "stripe_lepe_wgrad: workspace too small");
     const int nq = a->heads * HD / 4;
     if (NT % nq || (nq & (nq - 1))) return fail(CSU_E_UNSUPPORTED, "stripe_lepe_wgrad: heads per branch must be a power of two <= 32");
-    hipStream_t st = as_stream(stream);
-    const int nblk = wgrad_blocks(*a);
-    float* part = (float*)workspace;
-    const dim3 rgrid((a->nbranch * a->heads * HD * 10 + 3) / 4);
-    if (dtype == CSU_BF16)
-        lepe_wgrad_partial<bf16><<<dim3(nblk, a->nbranch), NT, 0, st>>>(*a, (const bf16*)qkv, (const bf16*)dout, part);
-    else
-        lepe_wgrad_partial<float><<<dim3(nblk, a->nbranch), NT, 0, st>>>(*a, (const float*)qkv, (const float*)dout, part);
-    lepe_wgrad_reduce<<<rgrid, 256, 0, st>>>(*a, nblk, part);
+    lepe_wgrad_launch(*a, dtype, qkv, dout, (float*)workspace, as_stream(stream));
     return check_launch("stripe_lepe_wgrad");
 }
