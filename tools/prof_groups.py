@@ -8,7 +8,7 @@ import json
 import sys
 
 # kernel-name fragment -> ledger name (first match wins)
-GROUPS = [("wgrad_tile", "linear_wgrad"), ("wslab_reduce", "linear_wgrad"), ("wgrad_f32", "linear_wgrad"),
+GROUPS = [("lepe_wgrad", "stripe_attn_bwd"), ("wgrad_tile", "linear_wgrad"), ("wslab_reduce", "linear_wgrad"), ("wgrad_f32", "linear_wgrad"),
           ("stripe_fwd", "stripe_attn_fwd"), ("stripe_bwd", "stripe_attn_bwd"), ("lepe_wgrad", "stripe_attn_bwd"),
           ("stripe_delta", "stripe_attn_bwd"),
           ("gemm4_kernel", "gemm"), ("gemm3_kernel", "gemm"), ("gemm_kernel", "gemm"),
@@ -18,7 +18,9 @@ GROUPS = [("wgrad_tile", "linear_wgrad"), ("wslab_reduce", "linear_wgrad"), ("wg
           ("carafe_head_fwd", "carafe_head_fwd"), ("carafe_head_bwd", "carafe_head_bwd"),
           ("carafe_fwd", "carafe_fwd"), ("carafe_bwd", "carafe_bwd"),
           ("adamw_kernel", "adamw"), ("cast_batch", "cast_bf16_batch"), ("colsum", "colsum"),
-          ("simam", "simam"), ("head_fwd", "head_fwd"), ("head_bwd", "head_bwd")]
+          ("simam_stats", "simam_fwd"), ("simam_apply", "simam_fwd"), ("simam_bwd", "simam_bwd"),
+          ("head_fwd", "head_fwd"), ("head_bwd", "head_bwd"), ("gemm_f32", "gemm"), ("slab_sum", "gemm"),
+          ("dropout_apply", "dropout"), ("quant_e4m3", "quant_e4m3")]
 
 
 def group(name):
@@ -42,7 +44,7 @@ def main():
             n[g] += 1
     ledger = {}
     if len(sys.argv) > 3:
-        rec = json.loads(open(sys.argv[3]).read().strip().splitlines()[-1])
+        rec = json.loads([l for l in open(sys.argv[3]).read().splitlines() if l.startswith("{")][-1])
         for k in rec["roofline"]["kernels"]:
             ledger[k["kernel"]] = k
         ledger["conv_fwd+conv_dgrad"] = {"us_per_step": sum(ledger.get(x, {}).get("us_per_step", 0)
