@@ -663,18 +663,30 @@ __global__ __launch_bounds__(NT) void lepe_wgrad_tiles(csu_stripe_args a, int ty
     T* Gt = Vt + (size_t)(ty_rows + 2) * reso * HD;             // [ty][reso][HD]
     const int vrows = ty_rows + 2;
     const int nchunk = (vrows + ty_rows) * reso * CPT;
-    for (int i = threadIdx.x; i < nchunk; i += NT) {
-        const int part_ = i % CPT, tok = (i / CPT) % reso, row = i / (CPT * reso);
-        const bool isv = row < vrows;
-        const int y = isv ? y0 - 1 + row : y0 + row - vrows;
-        u32x4 v = {0, 0, 0, 0};
-        if (y >= 0 && y < reso) {
-            const T* src = isv ? qkv + ((size_t)b * L + (size_t)y * reso + tok) * C3 + 2 * C + ch
-                               : dout + ((size_t)b * L + (size_t)y * reso + tok) * C + ch;
-            v = *reinterpret_cast<const u32x4*>(reinterpret_cast<const unsigned char*>(src) + 16 * part_);
+    constexpr int IT = 8;   // 16-B loads in flight per thread before their LDS stores
+    for (int base = 0; base < nchunk; base += IT * NT) {
+        u32x4 v[IT];
+#pragma unroll
+        for (int u = 0; u < IT; ++u) {
+            const int i = base + u * NT + threadIdx.x;
+            const int part_ = i % CPT, tok = (i / CPT) % reso, row = i / (CPT * reso);
+            const bool isv = row < vrows;
+            const int y = isv ? y0 - 1 + row : y0 + row - vrows;
+            v[u] = u32x4{0, 0, 0, 0};
+            if (i < nchunk && y >= 0 && y < reso) {
+                const T* src = isv ? qkv + ((size_t)b * L + (size_t)y * reso + tok) * C3 + 2 * C + ch
+                                   : dout + ((size_t)b * L + (size_t)y * reso + tok) * C + ch;
+                v[u] = *reinterpret_cast<const u32x4*>(reinterpret_cast<const unsigned char*>(src) + 16 * part_);
+            }
         }
-        T* dst = (isv ? Vt + ((size_t)row * reso + tok) * HD : Gt + ((size_t)(row - vrows) * reso + tok) * HD);
-        *reinterpret_cast<u32x4*>(reinterpret_cast<unsigned char*>(dst) + 16 * part_) = v;
+#pragma unroll
+        for (int u = 0; u < IT; ++u) {
+            const int i = base + u * NT + threadIdx.x;
+            if (i >= nchunk) break;
+            const int part_ = i % CPT, tok = (i / CPT) % reso, row = i / (CPT * reso);
+            T* dst = row < vrows ? Vt + ((size_t)row * reso + tok) * HD : Gt + ((size_t)(row - vrows) * reso + tok) * HD;
+            *reinterpret_cast<u32x4*>(reinterpret_cast<unsigned char*>(dst) + 16 * part_) = v[u];
+        }
     }
     __syncthreads();
     const int q = threadIdx.x & 7, tl = threadIdx.x >> 3;
