@@ -647,8 +647,9 @@ __global__ __launch_bounds__(NT, 4) void lepe_wgrad_partial(csu_stripe_args a, c
 // token lanes of a quad are reduced by a fixed xor tree + the 4 waves in order.  Partial layout
 // [branch][c * 10 + tap][block] as lepe_wgrad_partial's, block = b * nty + row tile.
 template <typename T>
-__global__ __launch_bounds__(NT) void lepe_wgrad_tiles(csu_stripe_args a, int ty_rows, const T* __restrict__ qkv,
-                                                      const T* __restrict__ dout, float* __restrict__ part) {
+__global__ __launch_bounds__(NT) void lepe_wgrad_tiles(csu_stripe_args a, int ty_rows, int rows_blk,
+                                                      const T* __restrict__ qkv, const T* __restrict__ dout,
+                                                      float* __restrict__ part) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lw_smem[];
     __shared__ float red[4][8][40];
     typedef typename Raw4<T>::type R4;
@@ -656,13 +657,18 @@ __global__ __launch_bounds__(NT) void lepe_wgrad_tiles(csu_stripe_args a, int ty
     const int br = blockIdx.z, head = blockIdx.y;
     const csu_stripe_branch& g = branch(a, br);
     const int reso = a.reso, L = reso * reso, C = a.C, C3 = 3 * C;
-    const int nty = (reso + ty_rows - 1) / ty_rows;
-    const int b = blockIdx.x / nty, y0 = (blockIdx.x % nty) * ty_rows;
+    const int nrb = (reso + rows_blk - 1) / rows_blk;   // row blocks per image
+    const int b = blockIdx.x / nrb, yb = (blockIdx.x % nrb) * rows_blk, ye = min(reso, yb + rows_blk);
     const int ch = g.ch_off + head * HD;
     T* Vt = reinterpret_cast<T*>(lw_smem);                       // [(ty + 2)][reso][HD]
     T* Gt = Vt + (size_t)(ty_rows + 2) * reso * HD;             // [ty][reso][HD]
     const int vrows = ty_rows + 2;
     const int nchunk = (vrows + ty_rows) * reso * CPT;
+    const int q = threadIdx.x & 7, tl = threadIdx.x >> 3;
+    float acc[40];
+#pragma unroll
+    for (int i = 0; i < 40; ++i) acc[i] = 0.f;
+    for (int y0 = yb; y0 < ye; y0 += ty_rows) {   // row tiles of this block, one reduction at the end
     constexpr int IT = 8;   // 16-B loads in flight per thread before their LDS stores
     for (int base = 0; base < nchunk; base += IT * NT) {
         u32x4 v[IT];
@@ -689,30 +695,36 @@ __global__ __launch_bounds__(NT) void lepe_wgrad_tiles(csu_stripe_args a, int ty
         }
     }
     __syncthreads();
-    const int q = threadIdx.x & 7, tl = threadIdx.x >> 3;
-    float acc[40];
-#pragma unroll
-    for (int i = 0; i < 40; ++i) acc[i] = 0.f;
     const int ntok = ty_rows * reso;
     for (int t = tl; t < ntok; t += NT / 8) {
         const int yy = t / reso, x = t - yy * reso, y = y0 + yy;
-        if (y >= reso) break;
+        if (y >= ye) break;
         const int iy = y % g.H_sp, ix = x % g.W_sp;
         const R4 gq = *reinterpret_cast<const R4*>(Gt + ((size_t)yy * reso + x) * HD + 4 * q);
+        // all 9 neighbour reads issued unconditionally (clamped columns; the halo rows are staged,
+        // zero outside the image), window-local padding applied as a 0 / 1 factor
+        const int xs[3] = {max(x - 1, 0), x, min(x + 1, reso - 1)};
+        R4 vq[3][3];
+#pragma unroll
+        for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+            for (int dx = 0; dx < 3; ++dx)
+                vq[dy][dx] = *reinterpret_cast<const R4*>(Vt + ((size_t)(yy + dy) * reso + xs[dx]) * HD + 4 * q);
 #pragma unroll
         for (int dy = 0; dy < 3; ++dy) {
             const bool yok = iy + dy - 1 >= 0 && iy + dy - 1 < g.H_sp;
 #pragma unroll
             for (int dx = 0; dx < 3; ++dx) {
-                const bool ok = yok && ix + dx - 1 >= 0 && ix + dx - 1 < g.W_sp;
-                if (!ok) continue;
-                const R4 vq = *reinterpret_cast<const R4*>(Vt + ((size_t)(yy + dy) * reso + x + dx - 1) * HD + 4 * q);
+                const float m = (yok && ix + dx - 1 >= 0 && ix + dx - 1 < g.W_sp) ? 1.f : 0.f;
 #pragma unroll
-                for (int j = 0; j < 4; ++j) acc[(dy * 3 + dx) * 4 + j] += Raw4<T>::at(gq, j) * Raw4<T>::at(vq, j);
+                for (int j = 0; j < 4; ++j)
+                    acc[(dy * 3 + dx) * 4 + j] += Raw4<T>::at(gq, j) * (m * Raw4<T>::at(vq[dy][dx], j));
             }
         }
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[36 + j] += Raw4<T>::at(gq, j);
+    }
+    __syncthreads();   // the next row tile overwrites the images
     }
     // token lanes of a quad: lane bits 3..5 inside the wave, then the 4 waves in order
 #pragma unroll
@@ -724,7 +736,7 @@ __global__ __launch_bounds__(NT) void lepe_wgrad_tiles(csu_stripe_args a, int ty
 #pragma unroll
         for (int i = 0; i < 40; ++i) red[wave][lane][i] = acc[i];
     __syncthreads();
-    const int Cb = a.heads * HD, nblk = a.B * nty;
+    const int Cb = a.heads * HD, nblk = a.B * nrb;
     for (int o = threadIdx.x; o < 8 * 40; o += NT) {
         const int qq = o / 40, i = o % 40;
         const float sum = ((red[0][qq][i] + red[1][qq][i]) + red[2][qq][i]) + red[3][qq][i];
@@ -740,6 +752,18 @@ int lepe_tile_rows(const csu_stripe_args& a, int dtype) {
     for (int ty : {4, 2, 1})
         if ((size_t)(2 * ty + 2) * a.reso * HD * es <= 64 * 1024) return ty;
     return 0;
+}
+
+// rows per LePE block (a multiple of the tile rows): about 512 blocks per launch, so each block
+// amortises its reduction over several row tiles
+int lepe_rows_blk(const csu_stripe_args& a, int ty) {
+    const long per_img = (long)a.B * a.heads * a.nbranch;
+    long nrb = 512 / per_img;
+    const long nty = (a.reso + ty - 1) / ty;
+    if (nrb > nty) nrb = nty;
+    if (nrb < 1) nrb = 1;
+    const long rows = (a.reso + nrb - 1) / nrb;
+    return (int)((rows + ty - 1) / ty * ty);
 }
 
 // one wave per (branch, value): lanes stride over the block partials (contiguous), then a fixed
@@ -1307,7 +1331,9 @@ extern "C" int csu_stripe_attn_fwd(const csu_stripe_args* a, int dtype, const vo
 // LePE weight-gradient partial blocks of a launch (tiled kernel if its tile fits, else untiled)
 int lepe_nblk(const csu_stripe_args& a, int dtype) {
     const int ty = lepe_tile_rows(a, dtype);
-    return ty ? a.B * ((a.reso + ty - 1) / ty) : wgrad_blocks(a);
+    if (!ty) return wgrad_blocks(a);
+    const int rb = lepe_rows_blk(a, ty);
+    return a.B * ((a.reso + rb - 1) / rb);
 }
 
 void lepe_wgrad_launch(const csu_stripe_args& a, int dtype, const void* qkv, const void* dout, float* part, hipStream_t st) {
@@ -1317,8 +1343,9 @@ void lepe_wgrad_launch(const csu_stripe_args& a, int dtype, const void* qkv, con
         const size_t es = dtype == CSU_BF16 ? 2 : 4;
         const size_t lds = (size_t)(2 * ty + 2) * a.reso * HD * es;
         const dim3 g((unsigned)nblk, (unsigned)a.heads, (unsigned)a.nbranch);
-        if (dtype == CSU_BF16) lepe_wgrad_tiles<bf16><<<g, NT, lds, st>>>(a, ty, (const bf16*)qkv, (const bf16*)dout, part);
-        else lepe_wgrad_tiles<float><<<g, NT, lds, st>>>(a, ty, (const float*)qkv, (const float*)dout, part);
+        const int rb = lepe_rows_blk(a, ty);
+        if (dtype == CSU_BF16) lepe_wgrad_tiles<bf16><<<g, NT, lds, st>>>(a, ty, rb, (const bf16*)qkv, (const bf16*)dout, part);
+        else lepe_wgrad_tiles<float><<<g, NT, lds, st>>>(a, ty, rb, (const float*)qkv, (const float*)dout, part);
     } else if (dtype == CSU_BF16) {
         lepe_wgrad_partial<bf16><<<dim3(nblk, a.nbranch), NT, 0, st>>>(a, (const bf16*)qkv, (const bf16*)dout, part);
     } else {

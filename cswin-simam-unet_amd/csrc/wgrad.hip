@@ -386,26 +386,50 @@ struct Plan {
     long rpc;
 };
 
-// Plan (tools/wgrad_bench.py sweeps, 512x512 B16 step shapes): a step is bound by the per-CU load
-// rate, so per-workgroup fixed costs (first loads ~2 us, slab write ~1.5 us) must be amortised over
-// many 64-token steps: 128-wide tiles only when they still give >= 16 tiles, chunks for about one
-// workgroup per CU but >= 1024 tokens each (>= 2048 with <= 2 tiles).  tn / tk / chunks > 0 override
+// modelled launch time (us) of tile tn x tk with c chunks (tools/wgrad_bench.py): workgroup rounds x
+// (tile bytes / c at ~70 GB/s per CU + ~3 us fixed per workgroup) + the slab reduction (~2 us + slab
+// bytes at HBM rate).  One partial round doubles a launch (48 tiles: 6 chunks = 288 workgroups = 2
+// rounds, 5 chunks = 240 = 1 round).
+double model_us(long M, int N, int K, int tn, int tk, long c) {
+    const long cus = num_cus();
+    const long tiles = (long)((N + tn - 1) / tn) * ((K + tk - 1) / tk);
+    const long rounds = (tiles * c + cus - 1) / cus;
+    const double tile_us = (double)M * (tn + tk) * 2.0 / 70e3;   // 70 GB/s = 70e3 B/us
+    double t = (double)rounds * (tile_us / (double)c + 3.0);
+    if (c > 1) t += 2.0 + (double)c * ((double)N * K + N) * 8.0 / 8e6;
+    return t;
+}
+
+// Plan: tile size and token chunks minimising model_us (each chunk >= 1024 tokens, >= 2048 with
+// <= 2 tiles); 128-wide tiles need N, K multiples of 128.  tn / tk / chunks > 0 override
 // (csu_linear_wgrad_tuned).
 Plan make_plan(long M, int N, int K, int tn, int tk, int chunks) {
     Plan p;
-    const bool big = N % 128 == 0 && K % 128 == 0 && (N / 128) * (K / 128) >= 16;
-    p.tn = tn > 0 ? tn : (big ? 128 : 64);
-    p.tk = tk > 0 ? tk : (big ? 128 : 64);
+    double best = 1e30;
+    p.tn = p.tk = 64;
+    long want = 1;
+    const int sizes[2] = {64, 128};
+    for (int a = 0; a < 2; ++a)
+        for (int b = 0; b < 2; ++b) {
+            const int ctn = sizes[a], ctk = sizes[b];
+            if ((tn > 0 && ctn != tn) || (tk > 0 && ctk != tk)) continue;
+            if (tn <= 0 && tk <= 0 && ctn != ctk) continue;   // mixed tiles measured slower than the model says
+            if ((ctn == 128 && N % 128) || (ctk == 128 && K % 128)) continue;
+            const long tiles = (long)((N + ctn - 1) / ctn) * ((K + ctk - 1) / ctk);
+            const long mintok = tiles <= 2 ? 2048 : 1024;
+            const long maxc = chunks > 0 ? chunks : (M + mintok - 1) / mintok;
+            for (long c = chunks > 0 ? chunks : 1; c <= maxc && c <= 4 * num_cus(); ++c) {
+                const double t = model_us(M, N, K, ctn, ctk, c);
+                if (t < best - 1e-9) {
+                    best = t;
+                    p.tn = ctn;
+                    p.tk = ctk;
+                    want = c;
+                }
+            }
+        }
     p.nt = (N + p.tn - 1) / p.tn;
     p.kt = (K + p.tk - 1) / p.tk;
-    const long tiles = (long)p.nt * p.kt;
-    long want = chunks;
-    if (want <= 0) {
-        want = (num_cus() + tiles - 1) / tiles;
-        const long mintok = tiles <= 2 ? 2048 : 1024;
-        const long maxc = (M + mintok - 1) / mintok;
-        if (want > maxc) want = maxc;
-    }
     if (want < 1) want = 1;
     p.rpc = ((M + want - 1) / want + TM - 1) / TM * TM;
     p.chunks = (int)((M + p.rpc - 1) / p.rpc);
