@@ -280,6 +280,31 @@ extern "C" int csu_layernorm_bwd(int rows, int C, int xdtype, const void* x, con
                                 workspace, ws_bytes, stream);
 }
 
+// Batched parameter reduction: the item table travels as a kernel argument (no device table, so
+// a captured launch needs no host buffer); wave w of the launch handles value w - v0 of the item
+// whose value range [v0, v0 + 2C) contains it.
+constexpr int LNB_MAX = 48;
+struct LnBatch {
+    const float* part[LNB_MAX];
+    float* dg[LNB_MAX];
+    float* db[LNB_MAX];
+    int nb[LNB_MAX], C[LNB_MAX], v0[LNB_MAX + 1];
+    int count;
+};
+
+__global__ __launch_bounds__(NT) void ln_param_reduce_batch(LnBatch t) {
+    const int v = blockIdx.x * WAVES + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (v >= t.v0[t.count]) return;
+    int i = 0;
+    while (i + 1 < t.count && t.v0[i + 1] <= v) ++i;
+    const int u = v - t.v0[i], C = t.C[i], nb = t.nb[i];
+    const float* part = t.part[i];
+    float s = 0.f;
+    for (int b = lane; b < nb; b += 64) s += part[(size_t)u * nb + b];
+    s = wave_sum(s);
+    if (lane == 0) (u < C ? t.dg[i][u] : t.db[i][u - C]) = s;
+}
+
 // dgamma / dbeta from the per-block partials a csu_layernorm_bwd_ex call with NULL dgamma/dbeta
 // left in `workspace` (the same rows / C): lets the reduction run on another stream
 extern "C" int csu_layernorm_param_reduce(int rows, int C, const void* workspace, float* dgamma, float* dbeta,
@@ -291,4 +316,29 @@ extern "C" int csu_layernorm_param_reduce(int rows, int C, const void* workspace
     ln_param_reduce<<<(2 * C + WAVES - 1) / WAVES, NT, 0, as_stream(stream)>>>(C, nb, (const float*)workspace, dgamma,
                                                                                 dbeta);
     return check_launch("layernorm_param_reduce");
+}
+
+extern "C" int csu_layernorm_param_reduce_batch(const csu_ln_param_item* items, int count, void* stream) {
+    if (count < 0 || (count && !items)) return fail(CSU_E_ARG, "layernorm_param_reduce_batch: bad args");
+    for (int base = 0; base < count; base += LNB_MAX) {
+        LnBatch t;
+        t.count = count - base < LNB_MAX ? count - base : LNB_MAX;
+        t.v0[0] = 0;
+        for (int i = 0; i < t.count; ++i) {
+            const csu_ln_param_item& it = items[base + i];
+            if (int e = check_c(it.C)) return e;
+            if (it.rows < 1 || !it.workspace || !it.dgamma || !it.dbeta)
+                return fail(CSU_E_ARG, "layernorm_param_reduce_batch: bad item");
+            int rpb;
+            t.nb[i] = ln_blocks(it.rows, it.C >= 256 ? 1 : 256 / it.C, &rpb);
+            t.C[i] = it.C;
+            t.part[i] = (const float*)it.workspace;
+            t.dg[i] = it.dgamma;
+            t.db[i] = it.dbeta;
+            t.v0[i + 1] = t.v0[i] + 2 * it.C;
+        }
+        ln_param_reduce_batch<<<(t.v0[t.count] + WAVES - 1) / WAVES, NT, 0, as_stream(stream)>>>(t);
+        if (int e = check_launch("layernorm_param_reduce_batch")) return e;
+    }
+    return 0;
 }

@@ -31,6 +31,11 @@ class StripeArgs(ctypes.Structure):
                 ("drop_rng", c_void_p), ("drop_site", ctypes.c_uint32), ("drop_p", c_float)]
 
 
+class LnParamItem(ctypes.Structure):
+    """csu_ln_param_item (include/csu.h)."""
+    _fields_ = [("workspace", c_void_p), ("dgamma", c_void_p), ("dbeta", c_void_p), ("rows", c_int32), ("C", c_int32)]
+
+
 class MlpDropout(ctypes.Structure):
     """csu_mlp_dropout (include/csu.h)."""
     _fields_ = [("rng", c_void_p), ("site_hidden", ctypes.c_uint32), ("site_out", ctypes.c_uint32), ("p", c_float),
@@ -109,6 +114,7 @@ _SIGS = {
     "csu_rng_advance": (ctypes.c_int, [c_void_p, c_void_p, c_void_p]),
     "csu_droppath_scale": (ctypes.c_int, [ctypes.c_long, c_void_p, ctypes.c_uint, c_float, c_void_p, c_void_p]),
     "csu_layernorm_param_reduce": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "csu_layernorm_param_reduce_batch": (ctypes.c_int, [c_void_p, ctypes.c_int, c_void_p]),
     "csu_stripe_lepe_wgrad": (ctypes.c_int, [ctypes.POINTER(StripeArgs), ctypes.c_int, c_void_p, c_void_p, c_void_p, c_size_t,
                                              c_void_p]),
     "csu_mlp_fwd": (ctypes.c_int, [ctypes.c_long, ctypes.c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,

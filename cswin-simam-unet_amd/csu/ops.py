@@ -192,6 +192,52 @@ def droppath_scale(B: int, p: float, site: int, device, snap: Optional[torch.Ten
 # ---------------------------------------------------------------------------------------------
 # LayerNorm (nn.LayerNorm over the last dim; eps 1e-5)
 # ---------------------------------------------------------------------------------------------
+# LayerNorm dgamma / dbeta: the backward kernel leaves per-block partials in its workspace and ONE
+# batched launch (csu_layernorm_param_reduce_batch, queued as an end-of-backward callback) reduces
+# every LayerNorm's partials, instead of one small reduction launch per LayerNorm (58 per 512x512
+# step).  Only when nothing can read those .grad before the end of backward: no existing .grad
+# (AccumulateGrad steals the tensor) and no hooks; otherwise reduced inline.  CSU_DEFER_LN=0 disables.
+DEFER_LN = _os.environ.get("CSU_DEFER_LN", "1") == "1"
+_LN_PENDING: list = []
+_LN_QUEUED = [False]
+
+
+def _deferrable(*params) -> bool:
+    for p in params:
+        p = _leaf(p)
+        if p is None:
+            continue
+        if p.grad is not None or p._backward_hooks or getattr(p, "_post_accumulate_grad_hooks", None):
+            return False
+    return True
+
+
+def _ln_param_flush():
+    _LN_QUEUED[0] = False
+    pend, _LN_PENDING[:] = list(_LN_PENDING), []
+    if not pend:
+        return
+    dev = pend[0][1].device
+    items = (_lib.LnParamItem * len(pend))()
+    for i, (work, dgb, rows, C) in enumerate(pend):
+        items[i].workspace, items[i].dgamma, items[i].dbeta = work.data_ptr(), dgb.data_ptr(), dgb.data_ptr() + C * 4
+        items[i].rows, items[i].C = rows, C
+    nv = sum(2 * C for _, _, _, C in pend)
+    _launch("layernorm_bwd", lambda: lib().csu_layernorm_param_reduce_batch(items, len(pend), stream_ptr(dev)),
+            0, sum(w.numel() for w, _, _, _ in pend) + nv * 4)
+
+
+def _ln_params(ctx, rows, C, work, dgb):
+    """Reduce (later, batched) or report that the caller must pass dgamma / dbeta pointers."""
+    if not (DEFER_LN and _deferrable(*ctx.params)):
+        return False
+    _LN_PENDING.append((work, dgb, rows, C))
+    if not _LN_QUEUED[0]:
+        torch.autograd.Variable._execution_engine.queue_callback(_ln_param_flush)
+        _LN_QUEUED[0] = True
+    return True
+
+
 class _LayerNormFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, eps: float, out_dtype):
@@ -210,6 +256,7 @@ class _LayerNormFn(torch.autograd.Function):
                 8 * rows * C, rows * C * (esize(x) + esize(y)) + rows * 8, prec=prec_of(x))
         ctx.save_for_backward(x, w, mean, rstd)
         ctx.pdtypes = (weight.dtype, bias.dtype)
+        ctx.params = (weight, bias)
         return y
 
     @staticmethod
@@ -226,8 +273,10 @@ class _LayerNormFn(torch.autograd.Function):
         L = lib()
         nbytes = L.csu_layernorm_bwd_workspace(rows, C)
         work = torch.empty(max(nbytes, 16), dtype=torch.uint8, device=x.device)
+        late = _ln_params(ctx, rows, C, work, dgb)
+        pg, pb = (None, None) if late else (ptr(dg), ptr(db))
         _launch("layernorm_bwd", lambda: L.csu_layernorm_bwd(rows, C, dtype_code(x), ptr(x), ptr(w), ptr(mean), ptr(rstd),
-                                                             dtype_code(dy), ptr(dy), ptr(dx), ptr(dg), ptr(db), ptr(work),
+                                                             dtype_code(dy), ptr(dy), ptr(dx), pg, pb, ptr(work),
                                                              nbytes, stream_ptr(x.device)),
                 12 * rows * C, rows * C * (2 * esize(x) + esize(dy)) + rows * 8, prec=prec_of(x))
         return dx, dg.to(ctx.pdtypes[0]), db.to(ctx.pdtypes[1]), None, None
@@ -270,6 +319,7 @@ class _LayerNormForkFn(torch.autograd.Function):
                 8 * rows * C, rows * C * (esize(x) + esize(y)) + rows * 8, prec=prec_of(x))
         ctx.save_for_backward(x, w, mean, rstd)
         ctx.pdtypes = (weight.dtype, bias.dtype)
+        ctx.params = (weight, bias)
         return x.view_as(x), y
 
     @staticmethod
@@ -290,9 +340,11 @@ class _LayerNormForkFn(torch.autograd.Function):
         nbytes = L.csu_layernorm_bwd_workspace(rows, C)
         work = torch.empty(max(nbytes, 16), dtype=torch.uint8, device=x.device)
         dgb = torch.empty(2 * C, dtype=torch.float32, device=x.device)
+        late = _ln_params(ctx, rows, C, work, dgb)
+        pg, pb = (None, None) if late else (ptr(dgb[:C]), ptr(dgb[C:]))
         _launch("layernorm_bwd", lambda: L.csu_layernorm_bwd_ex(rows, C, dtype_code(x), ptr(x), ptr(w), ptr(mean),
                                                                 ptr(rstd), dtype_code(dy), ptr(dy), ptr(dres_k), ptr(dx),
-                                                                ptr(dxb), ptr(dgb[:C]), ptr(dgb[C:]), ptr(work), nbytes,
+                                                                ptr(dxb), pg, pb, ptr(work), nbytes,
                                                                 stream_ptr(x.device)),
                 12 * rows * C, rows * C * (2 * esize(x) + esize(dy) + esize(dres_k) + esize(dxb)) + rows * 8,
                 prec=prec_of(x))

@@ -122,6 +122,15 @@ int csu_layernorm_bwd_ex(int rows, int C, int xdtype, const void* x, const float
  * called with dgamma = dbeta = NULL (same rows / C): the parameter reduction can then run on a
  * second stream, off the input-gradient chain. */
 int csu_layernorm_param_reduce(int rows, int C, const void* workspace, float* dgamma, float* dbeta, void* stream);
+/* the same for many layers in one launch (the deferred end-of-backward reduction of every
+ * LayerNorm's dgamma / dbeta): items is a HOST array, copied into the kernel arguments */
+typedef struct {
+    const void* workspace;
+    float* dgamma;
+    float* dbeta;
+    int32_t rows, C;
+} csu_ln_param_item;
+int csu_layernorm_param_reduce_batch(const csu_ln_param_item* items, int count, void* stream);
 
 size_t csu_simam_workspace(int B, int L, int C);
 /* y (ydtype, e.g. bf16 for the GEMM that consumes the gated skip) = SimAM(x); C % 4 == 0 */
