@@ -26,13 +26,14 @@ __global__ __launch_bounds__(NT) void cast_batch(const csu_cast_item* __restrict
     if (it.taps > 0) {   // conv weight (rows = N, cols = C, taps = KH*KW): OHWI and IHWO bf16 layouts
         const int n_el = it.rows * it.cols * it.taps;       // < 2^31 (conv weights)
         const unsigned CT = it.cols * it.taps, TP = it.taps;
+        const unsigned CP = it.cols_pad > it.cols ? it.cols_pad : it.cols;
         bf16* o = (bf16*)it.dst;
         bf16* t = (bf16*)it.dst_t;
         const int e0 = (int)(b - it.tile0) * (T * T), e1 = min(n_el, e0 + T * T);
         for (int e = e0 + threadIdx.x; e < e1; e += NT) {
             const unsigned n = (unsigned)e / CT, rem = (unsigned)e - n * CT, c = rem / TP, k = rem - c * TP;
             const bf16 v = (bf16)it.src[e];                        // src [n][c][k]
-            o[(n * TP + k) * it.cols + c] = v;                     // OHWI [n][k][c]
+            o[(n * TP + k) * CP + c] = v;                          // OHWI [n][k][c] (channel stride CP)
             if (t) t[(c * TP + k) * it.rows + n] = v;              // IHWO [c][k][n]
         }
         return;

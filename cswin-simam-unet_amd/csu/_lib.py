@@ -115,6 +115,13 @@ _SIGS = {
     "csu_droppath_scale": (ctypes.c_int, [ctypes.c_long, c_void_p, ctypes.c_uint, c_float, c_void_p, c_void_p]),
     "csu_layernorm_param_reduce": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
     "csu_layernorm_param_reduce_batch": (ctypes.c_int, [c_void_p, ctypes.c_int, c_void_p]),
+    "csu_grad_join": (ctypes.c_int, [ctypes.c_long, ctypes.c_int, c_void_p, ctypes.c_int, c_void_p, c_void_p, c_void_p,
+                                     c_void_p]),
+    "csu_bce_loss_workspace": (c_size_t, [ctypes.c_long]),
+    "csu_bce_loss_fwd": (ctypes.c_int, [ctypes.c_long, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "csu_bce_loss_bwd": (ctypes.c_int, [ctypes.c_long, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "csu_pack_nhwc_bf16": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_void_p,
+                                          c_void_p, c_void_p]),
     "csu_stripe_lepe_wgrad": (ctypes.c_int, [ctypes.POINTER(StripeArgs), ctypes.c_int, c_void_p, c_void_p, c_void_p, c_size_t,
                                              c_void_p]),
     "csu_mlp_fwd": (ctypes.c_int, [ctypes.c_long, ctypes.c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,

@@ -304,8 +304,14 @@ class CARAFE(nn.Module):
         H = W = int(math.isqrt(L))
         if self.kernel_size != 3:
             raise NotImplementedError("the fused CARAFE kernel is specialised for kernel_size=3 (the reference's)")
-        xc = x.to(_compute_dtype(x))
-        d = ops.linear(xc, self.down.weight.reshape(C // 4, C), self.down.bias)
+        cd = _compute_dtype(x)
+        if x.is_cuda and x.dtype != cd:
+            # one bf16 copy for both consumers (down conv, reassembly): their two input gradients are
+            # joined in one pass (ops.grad_join) instead of autograd's add + cast
+            xd, xc = ops.shared_cast(x, cd)
+        else:
+            xd = xc = x.to(cd)
+        d = ops.linear(xd, self.down.weight.reshape(C // 4, C), self.down.bias)
         enc = ops.conv2d(d.reshape(B, H, W, C // 4), self.encoder.weight, self.encoder.bias, 1, self.kernel_size // 2)
         return xc, enc
 

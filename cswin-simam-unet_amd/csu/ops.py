@@ -777,11 +777,62 @@ class _SharedCastFn(torch.autograd.Function):
     def backward(ctx, g1, g2):
         if g1 is None and g2 is None:
             return None, None
-        if g1 is None or g2 is None:
-            return (g1 if g2 is None else g2).to(ctx.xdt), None
-        g = g1.to(ctx.xdt)
-        g.add_(g2)
-        return g, None
+        return grad_join(g1, g2, ctx.xdt), None
+
+
+def grad_join(g1: Optional[torch.Tensor], g2: Optional[torch.Tensor], dtype: torch.dtype) -> torch.Tensor:
+    """g1 + g2 in `dtype` (either may be None).  fp32 result on the device: one csu_grad_join pass
+    that also writes the bf16 copy the upstream GEMM backward consumes (attached as ``_csu_bf16``,
+    see _bf16_of) -- instead of autograd's cast, add and the consumer's cast."""
+    a, b = (g1, g2) if g1 is not None else (g2, None)
+    if dtype != torch.float32 or not a.is_cuda or a.numel() % 8:
+        g = a.to(dtype)
+        return g.add_(b) if b is not None else g
+    a = a.contiguous()
+    b = b.contiguous() if b is not None else None
+    out = torch.empty(a.shape, dtype=torch.float32, device=a.device)
+    outb = torch.empty(a.shape, dtype=torch.bfloat16, device=a.device)
+    n = a.numel()
+    _launch("grad_join", lambda: lib().csu_grad_join(n, dtype_code(a), ptr(a), dtype_code(b) if b is not None else 0,
+                                                     ptr(b), ptr(out), ptr(outb), stream_ptr(a.device)),
+            n, n * (esize(a) + (esize(b) if b is not None else 0) + 6), prec="f32")
+    out._csu_bf16 = outb
+    return out
+
+
+class _BCELossFn(torch.autograd.Function):
+    """nn.BCELoss() (mean) on fp32 probabilities (cswin:935): csu_bce_loss_fwd (fixed-order two-pass
+    sum) and csu_bce_loss_bwd (torch's clamps), 3 launches instead of torch's 5."""
+
+    @staticmethod
+    def forward(ctx, p, t):
+        p, t = p.contiguous(), t.contiguous()
+        n = p.numel()
+        loss = torch.empty((), dtype=torch.float32, device=p.device)
+        nws = lib().csu_bce_loss_workspace(n)
+        ws = torch.empty(nws // 4, dtype=torch.float32, device=p.device)
+        _launch("bce_loss", lambda: lib().csu_bce_loss_fwd(n, ptr(p), ptr(t), ptr(loss), ptr(ws), nws, stream_ptr(p.device)),
+                8 * n, 8 * n, prec="f32")
+        ctx.save_for_backward(p, t)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        p, t = ctx.saved_tensors
+        g = g.float().contiguous()
+        dp = torch.empty_like(p)
+        n = p.numel()
+        _launch("bce_loss_bwd", lambda: lib().csu_bce_loss_bwd(n, ptr(p), ptr(t), ptr(g), ptr(dp), stream_ptr(p.device)),
+                6 * n, 12 * n, prec="f32")
+        return dp, None
+
+
+def bce_loss(prob: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
+    """Mean binary cross-entropy of fp32 device probabilities (see _BCELossFn)."""
+    require_device(prob, target)
+    if prob.dtype != torch.float32 or target.dtype != torch.float32 or prob.shape != target.shape:
+        raise ValueError("bce_loss: fp32 probabilities and targets of one shape")
+    return _BCELossFn.apply(prob, target)
 
 
 def shared_cast(x: torch.Tensor, dtype: torch.dtype):
@@ -1055,8 +1106,14 @@ class CastCache:
         self.shadow = [torch.empty(p.shape, dtype=dtype, device=p.device) for p in params]
         self.shadow_t = [torch.empty(p.shape[1:].numel() if p.dim() > 1 else 0, p.shape[0], dtype=dtype, device=p.device)
                          if p.dim() > 1 else None for p in params]
-        self.conv_o = [torch.empty(w.shape[0], w.shape[2], w.shape[3], w.shape[1], dtype=dtype, device=w.device) for w in convs]
-        self.conv_i = [torch.empty(w.shape[1], w.shape[2], w.shape[3], w.shape[0], dtype=dtype, device=w.device) for w in convs]
+        # few-channel convs (the 3-channel patch embed): OHWI zero-padded to a multiple of 8 channels,
+        # the layout _Conv2dFn runs them in (pad channels zeroed here once, never written again); no
+        # IHWO (their input, the image, needs no gradient)
+        self.conv_cp = [_pad_channels(w.shape[1]) for w in convs]
+        self.conv_o = [torch.zeros(w.shape[0], w.shape[2], w.shape[3], cp, dtype=dtype, device=w.device)
+                       for w, cp in zip(convs, self.conv_cp)]
+        self.conv_i = [torch.empty(w.shape[1], w.shape[2], w.shape[3], w.shape[0], dtype=dtype, device=w.device)
+                       if cp == w.shape[1] else None for w, cp in zip(convs, self.conv_cp)]
         self.index = {p.data_ptr(): i for i, p in enumerate(params)}
         self.cindex = {w.data_ptr(): i for i, w in enumerate(convs)}
         self.items = None
@@ -1075,8 +1132,9 @@ class CastCache:
                 t0 += -(-rows // 64) * -(-cols // 64)
             for j, w in enumerate(convs):
                 N, C, KH, KW = w.shape
-                rec[len(params) + j] = (w.data_ptr(), self.conv_o[j].data_ptr(), self.conv_i[j].data_ptr(), N, C, t0,
-                                        KH * KW, 0)
+                ci = self.conv_i[j]
+                rec[len(params) + j] = (w.data_ptr(), self.conv_o[j].data_ptr(), 0 if ci is None else ci.data_ptr(), N, C,
+                                        t0, KH * KW, self.conv_cp[j])
                 t0 += -(-(N * C * KH * KW) // 4096)
             self.tiles = t0
             self.items = torch.frombuffer(bytearray(rec.tobytes()), dtype=torch.uint8).to(allp[0].device)
@@ -1107,8 +1165,9 @@ class CastCache:
                 if st is not None:
                     st.copy_(p.detach().reshape(p.shape[0], -1).t())
             for w, o, i in zip(self.convs, self.conv_o, self.conv_i):
-                o.copy_(w.detach().permute(0, 2, 3, 1))
-                i.copy_(w.detach().permute(1, 2, 3, 0))
+                o[..., :w.shape[1]].copy_(w.detach().permute(0, 2, 3, 1))
+                if i is not None:
+                    i.copy_(w.detach().permute(1, 2, 3, 0))
 
     def get(self, p, dtype):
         i = self.index.get(p.data_ptr())
@@ -1125,7 +1184,8 @@ class CastCache:
         return st if tuple(st.shape) == (p.shape[1], p.shape[0]) else None
 
     def get_conv(self, w, dtype):
-        """(OHWI, IHWO) bf16 layouts of a cached conv weight, or None."""
+        """(OHWI, IHWO) bf16 layouts of a cached conv weight, or None.  Few-channel weights: OHWI
+        channel-padded to _pad_channels(C), IHWO None."""
         j = self.cindex.get(w.data_ptr())
         if j is None or self.dtype != dtype or tuple(self.convs[j].shape) != tuple(w.shape):
             return None
@@ -1226,6 +1286,11 @@ def _conv_wgrad(g, x, dy, dt):
     return out[:k].view(g.N, g.KH, g.KW, g.C), out[k:]
 
 
+def _pad_channels(C: int) -> int:
+    """Channel count a conv input is run with: few-channel inputs zero-padded to a multiple of 8."""
+    return (C + 7) // 8 * 8 if (C % 8 and PAD_CHANNELS) else C
+
+
 class _Conv2dFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, stride: int, pad: int, cd):
@@ -1234,14 +1299,25 @@ class _Conv2dFn(torch.autograd.Function):
         N, Cw, KH, KW = weight.shape
         if Cw != C:
             raise ValueError(f"conv2d: input has {C} channels, weight expects {Cw}")
-        cp = (C + 7) // 8 * 8 if (C % 8 and PAD_CHANNELS) else C
+        cp = _pad_channels(C)
         if cp != C:
             # few-channel input (the 3-channel image of the patch embed): zero channels up to a
             # multiple of 8 in the image and the weight -- 16-B vector gathers in the conv kernels
             # instead of per-element ones; the padded taps add exact zeros
-            xc = torch.zeros(B, H, W, cp, dtype=cd, device=x.device)
-            xc[..., :C] = x
-            w_ohwi = torch.nn.functional.pad(weight.detach().permute(0, 2, 3, 1).to(cd), (0, cp - C)).contiguous()
+            xn = x.permute(0, 3, 1, 2)
+            if cd == torch.bfloat16 and x.dtype == torch.float32 and xn.is_contiguous():
+                # the NCHW fp32 image -> padded bf16 NHWC in one pass
+                xc = torch.empty(B, H, W, cp, dtype=cd, device=x.device)
+                _launch("pack_nhwc", lambda: lib().csu_pack_nhwc_bf16(B, C, H, W, cp, ptr(xn), ptr(xc), stream_ptr(x.device)),
+                        0, x.numel() * 4 + xc.numel() * 2, prec="f32")
+            else:
+                xc = torch.zeros(B, H, W, cp, dtype=cd, device=x.device)
+                xc[..., :C] = x
+            cached = _ACTIVE_CACHE.get_conv(weight, cd) if _ACTIVE_CACHE is not None else None
+            if cached is not None and cached[0].shape[-1] == cp:
+                w_ohwi = cached[0]
+            else:
+                w_ohwi = torch.nn.functional.pad(weight.detach().permute(0, 2, 3, 1).to(cd), (0, cp - C)).contiguous()
             cached = None
         else:
             xc = (x if x.dtype == cd else x.to(cd)).contiguous()

@@ -28,18 +28,28 @@ class FusedAdamW(torch.optim.Optimizer):
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, capturable=capturable))
         self._tables = {}
         self._gstate = {}
+        self._deferred = []
+        self._captured = []
         # one pinned table buffer per group, reserved for a HIP-graph capture of step()
         self._pinned = {gi: torch.empty(max(1, len(g["params"])) * _ITEM.itemsize, dtype=torch.uint8, pin_memory=True)
                         for gi, g in enumerate(self.param_groups)} if torch.cuda.is_available() else {}
+        # ... and its device image, allocated HERE, outside any capture: a buffer allocated inside the
+        # capture comes from the graph's private pool, where it may alias memory an earlier captured
+        # kernel writes on every replay -- fine for buffers the graph itself fills, fatal for one
+        # filled once after the capture (finish_capture)
+        self._capture_dev = {gi: torch.empty(max(1, len(g["params"])) * _ITEM.itemsize, dtype=torch.uint8,
+                                             device=g["params"][0].device)
+                             for gi, g in enumerate(self.param_groups) if g["params"] and g["params"][0].is_cuda}
 
     def _table(self, gi, items, device):
         """Device item table for the current (param, grad) buffers, rebuilt when they change
         (e.g. every step under zero_grad(set_to_none=True) when the allocator hands out other grad
         buffers).  Eager: an asynchronous copy from a fresh pinned buffer (no host sync; the
         caching host allocator keeps it alive until the copy has run).  Under HIP-graph capture:
-        an async copy from a pinned buffer reserved for that capture (pinned memory cannot be
-        allocated while capturing); the graph's copy node re-reads it on every replay, so it is
-        never rewritten."""
+        the host image goes to a pinned buffer reserved for that capture (pinned memory cannot be
+        allocated while capturing) and is copied ONCE after the capture (finish_capture) into a
+        device buffer allocated outside the graph's memory pool and kept for the optimizer's
+        lifetime -- no copy node in the replayed graph."""
         key = (gi,) + tuple(v for it in items for v in it[:4])
         t = self._tables.get(gi)
         if t is not None and t[0] == key:
@@ -53,12 +63,19 @@ class FusedAdamW(torch.optim.Optimizer):
         raw = np.frombuffer(rec.tobytes(), dtype=np.uint8)
         if torch.cuda.is_current_stream_capturing():
             host = self._pinned.get(gi)
-            if host is None or host.numel() < raw.size:
+            dev = self._capture_dev.get(gi)
+            if host is None or dev is None or host.numel() < raw.size:
                 raise RuntimeError("FusedAdamW: no pinned table buffer for this capture (one capture per optimizer)")
             del self._pinned[gi]                      # frozen: owned by the captured graph from now on
+            del self._capture_dev[gi]
             host[:raw.size].numpy()[:] = raw
-            dev = torch.empty(raw.size, dtype=torch.uint8, device=device)
-            dev.copy_(host[:raw.size], non_blocking=True)
+            dev = dev[:raw.size]
+            # the captured kernel reads this buffer on every replay: keep it (and its host image)
+            # alive for the optimizer's lifetime, whatever later eager steps put into _tables
+            self._captured.append((host, dev))
+            # the table is constant over replays: copied once after the capture (finish_capture)
+            # instead of by a copy node on every replay
+            self._deferred.append((dev, host[:raw.size]))
         else:
             host = torch.empty(raw.size, dtype=torch.uint8, pin_memory=True)
             host.numpy()[:] = raw
@@ -134,6 +151,14 @@ class FusedAdamW(torch.optim.Optimizer):
         super().load_state_dict(state_dict)
         self._gstate = {}
         self._tables = {}
+
+    def finish_capture(self):
+        """After a HIP-graph capture of step(): fill the device tables the captured kernel reads
+        (their host images were frozen during the capture).  Synchronous, once per capture."""
+        for dev, host in self._deferred:
+            dev.copy_(host)
+        self._deferred = []
+        torch.cuda.synchronize()
 
     def sync_lr(self):
         """Copy the host lr of every group into its device tensor (capturable groups read it at

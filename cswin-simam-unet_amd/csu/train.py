@@ -25,6 +25,9 @@ except ImportError:  # pragma: no cover
 def bce_loss(prob: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
     """nn.BCELoss() (mean; log clamped at -100) computed in fp32 (cswin:936)."""
     with torch.autocast(prob.device.type, enabled=False):   # BCE is autocast-unsafe; always fp32
+        if prob.is_cuda:
+            from . import ops
+            return ops.bce_loss(prob.float(), target.float())
         return F.binary_cross_entropy(prob.float(), target.float())
 
 
@@ -220,15 +223,25 @@ class GraphedTrainStep:
             # illegal in every thread (hipErrorStreamCaptureUnsupported -> the watchdog aborts the
             # process); a thread-local capture restricts only this thread, so the polling stays
             # legal whatever the watchdog's timing.  The barrier lines the ranks up so no rank's
-            # capture overlaps another rank's warm-up collectives.
+            # capture overlaps another rank's warm-up collectives.  Then the watchdog's own list is
+            # drained (ProcessGroup._wait_for_pending_works returns once every issued collective,
+            # the barrier's included, has been retired by the watchdog): with nothing left to poll
+            # it issues no event query while the capture runs (observed: a query landing inside the
+            # capture window still aborted the process now and then, thread-local mode or not).
             if dist.is_available() and dist.is_initialized():
                 dist.barrier()
                 torch.cuda.synchronize()
+                pg = dist.distributed_c10d._get_default_group()
+                if hasattr(pg, "_wait_for_pending_works"):
+                    pg._wait_for_pending_works()
             mode = "thread_local"
         self.graph = torch.cuda.CUDAGraph()
         self.opt.zero_grad(set_to_none=True)
         with torch.cuda.graph(self.graph, capture_error_mode=mode):
             self.loss, self.out = self._body(zero=False)
+        fin = getattr(self.opt, "finish_capture", None)
+        if fin is not None:
+            fin()
 
     def _body(self, zero=True):
         if zero:

@@ -253,7 +253,8 @@ typedef struct {
     int64_t tile0;
     int32_t taps;   /* 0: matrix item.  > 0: conv weight src (rows=N, cols=C, taps=KH*KW) -> dst = OHWI
                        [N][KH][KW][C], dst_t = IHWO [C][KH][KW][N] (or NULL); ceil(N*C*taps/4096) tiles */
-    int32_t pad_;
+    int32_t cols_pad;   /* conv items: channel stride of dst (0 = C; > C: channel-padded OHWI whose
+                           pad channels are left untouched, e.g. zeroed once by the caller) */
 } csu_cast_item;
 int csu_cast_bf16_batch(const csu_cast_item* items, int count, long total_tiles, void* stream);
 
@@ -380,6 +381,25 @@ size_t csu_conv2d_wgrad_workspace(const csu_conv_geom* g);
 /* dw_db fp32 [N*KH*KW*C + N] = dW in [N][KH][KW][C] order, then db (sum of dy) */
 int csu_conv2d_wgrad(const csu_conv_geom* g, int dtype, const void* x, const void* dy, float* dw_db,
                      void* workspace, size_t ws_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Step glue (csrc/glue.hip), the elementwise passes between the kernels above:
+ * grad_join: out (fp32, n) = a + b (b may be NULL), plus out_bf16 (bf16 copy, or NULL); a / b
+ *   bf16 or fp32, n % 8 == 0.  The gradient of an fp32 activation cast once to bf16 for two
+ *   consumers (encoder skip cswin:530-545/568-592, CARAFE input cswin:408-432).
+ * bce_loss: nn.BCELoss(reduction='mean') (cswin:935) on probabilities p and targets t (fp32, n):
+ *   loss[0] = mean(-(t max(log p, -100) + (1-t) max(log(1-p), -100))), deterministic; backward
+ *   dp = dloss[0] (p - t) / max((1-p) p, 1e-12) / n.
+ * pack_nhwc_bf16: fp32 NCHW image (B, C, H, W) -> bf16 NHWC (B, H, W, Cp), channels >= C zero
+ *   (the patch-embed conv input, cswin:505).
+ * ------------------------------------------------------------------------------------- */
+int csu_grad_join(long n, int adtype, const void* a, int bdtype, const void* b, float* out, void* out_bf16,
+                  void* stream);
+size_t csu_bce_loss_workspace(long n);
+int csu_bce_loss_fwd(long n, const float* p, const float* t, float* loss, void* workspace, size_t ws_bytes,
+                     void* stream);
+int csu_bce_loss_bwd(long n, const float* p, const float* t, const float* dloss, float* dp, void* stream);
+int csu_pack_nhwc_bf16(int B, int C, int H, int W, int Cp, const float* x, void* y, void* stream);
 
 #ifdef __cplusplus
 }

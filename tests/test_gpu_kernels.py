@@ -398,13 +398,19 @@ def test_cast_cache_batch_kernel():
             torch.testing.assert_close(c.get_t(v, torch.bfloat16), v.t().bfloat16(), rtol=0, atol=0)
     for w in convs:   # channels-last conv layouts written by the same launch
         o, i = c.get_conv(w, torch.bfloat16)
+        C = w.shape[1]
+        if C % 8:     # few-channel conv (patch embed): OHWI zero-padded to 8 channels, no IHWO
+            assert o.shape[-1] == 8 and i is None and not o[..., C:].any()
+            assert torch.equal(o[..., :C], w.permute(0, 2, 3, 1).bfloat16())
+            continue
         assert torch.equal(o, w.permute(0, 2, 3, 1).bfloat16()) and torch.equal(i, w.permute(1, 2, 3, 0).bfloat16())
     with torch.no_grad():
         ps[0].mul_(2)
         convs[1].mul_(3)
     c.refresh(ps, torch.bfloat16, convs)
     torch.testing.assert_close(c.get(ps[0], torch.bfloat16), ps[0].bfloat16(), rtol=0, atol=0)
-    assert torch.equal(c.get_conv(convs[1], torch.bfloat16)[0], convs[1].permute(0, 2, 3, 1).bfloat16())
+    o = c.get_conv(convs[1], torch.bfloat16)[0]
+    assert torch.equal(o[..., :3], convs[1].permute(0, 2, 3, 1).bfloat16()) and not o[..., 3:].any()
 
 
 def test_fused_mlp_residual_matches_unfused():
@@ -672,3 +678,50 @@ def test_gemm_f32_layouts(layout, M, N, K):
         assert torch.equal(out, again) and torch.equal(asum, asum2)
         assert_close(asum, a.double().sum(0), torch.float32)
     assert_close(out, ref, torch.float32)
+
+
+@pytest.mark.parametrize("n,adt,bdt", [(4096 * 64, torch.bfloat16, torch.bfloat16), (1000 * 8, torch.float32, torch.bfloat16),
+                                       (4096, torch.bfloat16, None)])
+def test_grad_join(n, adt, bdt):
+    """csu_grad_join: a + b in fp32 (exact: fp32 sum of the two inputs) plus its bf16 copy."""
+    from csu import ops
+    d = dev()
+    g = torch.Generator(device=d).manual_seed(n)
+    a = torch.randn(n // 64, 64, device=d, generator=g).to(adt)
+    b = torch.randn(n // 64, 64, device=d, generator=g).to(bdt) if bdt is not None else None
+    out = ops.grad_join(a, b, torch.float32)
+    ref = a.float() + (b.float() if b is not None else 0)
+    assert out.dtype == torch.float32 and torch.equal(out, ref)
+    assert torch.equal(out._csu_bf16, ref.bfloat16())
+
+
+@pytest.mark.parametrize("n", [16 * 512 * 512, 1000, 4 * 1024 + 3])
+def test_bce_loss_vs_torch(n):
+    """ops.bce_loss (nn.BCELoss mean, cswin:935) vs torch on probabilities incl. exact 0 / 1
+    (the -100 log clamp) and targets in {0, 1}; deterministic."""
+    from csu import ops
+    d = dev()
+    g = torch.Generator(device=d).manual_seed(n)
+    p = torch.rand(n, device=d, generator=g)
+    p[:7] = torch.tensor([0.0, 1.0, 1e-30, 1 - 1e-7, 0.5, 1.0, 0.0], device=d)
+    t = (torch.rand(n, device=d, generator=g) > 0.5).float()
+    t[:7] = torch.tensor([1.0, 0.0, 0.0, 1.0, 1.0, 1.0, 0.0], device=d)
+    pa = p.clone().requires_grad_(True)
+    pb = p.clone().requires_grad_(True)
+    la = ops.bce_loss(pa, t)
+    lb = torch.nn.functional.binary_cross_entropy(pb, t)
+    torch.testing.assert_close(la, lb, rtol=1e-5, atol=0)
+    la.backward()
+    lb.backward()
+    torch.testing.assert_close(pa.grad, pb.grad, rtol=1e-6, atol=0)
+    assert torch.equal(ops.bce_loss(p, t), ops.bce_loss(p, t))
+
+
+def test_pack_nhwc_image():
+    """csu_pack_nhwc_bf16: fp32 NCHW image -> bf16 NHWC, channels zero-padded to 8 (bit-exact)."""
+    from csu import _lib, ops
+    d = dev()
+    x = torch.randn(3, 3, 37, 41, device=d)
+    y = torch.empty(3, 37, 41, 8, dtype=torch.bfloat16, device=d)
+    _lib.check(_lib.lib().csu_pack_nhwc_bf16(3, 3, 37, 41, 8, ops.ptr(x), ops.ptr(y), ops.stream_ptr(d)), "pack")
+    assert torch.equal(y[..., :3], x.permute(0, 2, 3, 1).bfloat16()) and not y[..., 3:].any()

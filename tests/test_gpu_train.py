@@ -211,3 +211,9 @@ def test_capture_after_eager_steps():
     gs = GraphedTrainStep(m, opt, bce_loss, x, t, torch.bfloat16, warmup=1)
     losses = [float(gs(x, t)[0].item()) for _ in range(3)]
     assert all(np.isfinite(losses)) and losses[2] < losses[0]
+    # eager steps with the same optimizer AFTER the capture (bench.py's roofline leg) rebuild its
+    # eager pointer table; the captured step keeps reading its own (kept-alive) table
+    eager()
+    eager()
+    more = [float(gs(x, t)[0].item()) for _ in range(2)]
+    assert all(np.isfinite(more)) and more[1] < losses[0]

@@ -36,6 +36,20 @@ with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_sh
 ka = prof.key_averages(group_by_stack_n=6) if STACK else prof.key_averages(group_by_input_shape=True)
 rows = [e for e in ka if e.key.startswith("aten::") and e.self_device_time_total > 0]
 rows.sort(key=lambda e: -e.self_device_time_total)
-for e in rows[:40]:
-    where = " <- ".join(f.split("/")[-1] for f in e.stack[:6] if "csu" in f or "model" in f) if STACK else str(e.input_shapes)[:150]
+for e in rows[:60]:
+    where = " <- ".join(f.split("/")[-1] for f in e.stack[:6]) if STACK else str(e.input_shapes)[:150]
     print(f"{e.self_device_time_total:9.1f} us  n={e.count:4d}  {e.key:32s} {where}")
+
+if os.environ.get("TREE", "0") == "1":
+    # each aten op with device time, with its chain of CPU parents (autograd node names show where a
+    # backward-side copy/add comes from)
+    for e in prof.events():
+        if not e.key.startswith("aten::") or e.device_time_total <= 0 or e.cpu_parent is None:
+            continue
+        if e.cpu_parent.key.startswith("aten::") and e.cpu_parent.device_time_total > 0:
+            continue   # print the outermost aten op only
+        chain, p = [], e.cpu_parent
+        while p is not None and len(chain) < 5:
+            chain.append(p.key[:60])
+            p = p.cpu_parent
+        print(f"{e.device_time_total:8.1f} us {e.key:22s} {str(e.input_shapes)[:70]:70s} <- {' <- '.join(chain)}")
