@@ -334,10 +334,9 @@ __global__ __launch_bounds__(NT, D > 2 ? 1 : 2) void wgrad_tile(long M, int N, i
 }
 
 // dst[n][k] = sum_c slab[tile(n, k)][c][n % TN][k % TK] (c = 0 .. chunks-1 in order), then
-// dst[N*K + n] = sum_c bslab[n / TN][c][n % TN].  One thread per 4 outputs.
-__global__ __launch_bounds__(NT) void wslab_reduce(int N, int K, int TN, int TK, int chunks,
-                                                   const float* __restrict__ slab, float* __restrict__ dst) {
-    const long e = ((long)blockIdx.x * NT + threadIdx.x) * 4;
+// dst[N*K + n] = sum_c bslab[n / TN][c][n % TN].  One thread per 4 outputs (e = first output).
+__device__ __forceinline__ void wslab_sum4(long e, int N, int K, int TN, int TK, int chunks,
+                                           const float* __restrict__ slab, float* __restrict__ dst) {
     const long NK = (long)N * K;
     const int kt = (K + TK - 1) / TK, nt = (N + TN - 1) / TN;
     const long step = (long)TN * TK;
@@ -366,6 +365,29 @@ __global__ __launch_bounds__(NT) void wslab_reduce(int N, int K, int TN, int TK,
     }
     for (; c < chunks; ++c) s += *reinterpret_cast<const f32x4*>(p + c * stride);
     *reinterpret_cast<f32x4*>(dst + e) = s;
+}
+
+__global__ __launch_bounds__(NT) void wslab_reduce(int N, int K, int TN, int TK, int chunks,
+                                                   const float* __restrict__ slab, float* __restrict__ dst) {
+    wslab_sum4(((long)blockIdx.x * NT + threadIdx.x) * 4, N, K, TN, TK, chunks, slab, dst);
+}
+
+// many deferred slab reductions in one launch: item table in the kernel arguments (capturable),
+// workgroup -> item by a scan over the block prefix sums (workgroup-uniform: scalar loads)
+constexpr int WSB_MAX = 40;
+struct WsBatch {
+    const float* slab[WSB_MAX];
+    float* dst[WSB_MAX];
+    int N[WSB_MAX], K[WSB_MAX], tn[WSB_MAX], tk[WSB_MAX], chunks[WSB_MAX], b0[WSB_MAX + 1];
+    int count;
+};
+
+__global__ __launch_bounds__(NT) void wslab_reduce_batch(WsBatch t) {
+    const int b = blockIdx.x;
+    int i = 0;
+    while (i + 1 < t.count && t.b0[i + 1] <= b) ++i;
+    wslab_sum4(((long)(b - t.b0[i]) * NT + threadIdx.x) * 4, t.N[i], t.K[i], t.tn[i], t.tk[i], t.chunks[i], t.slab[i],
+               t.dst[i]);
 }
 
 int num_cus() {
@@ -449,7 +471,8 @@ void launch_tile(const Plan& p, unsigned grid, long M, int N, int K, const bf16*
     wgrad_tile<TN, TK, 2><<<grid, NT, 0, st>>>(M, N, K, p.rpc, p.chunks, dy, x, dst, slab);
 }
 
-int run_bf16(const Plan& p, long M, int N, int K, const bf16* dy, const bf16* x, float* dst, void* ws, hipStream_t st) {
+int run_bf16(const Plan& p, long M, int N, int K, const bf16* dy, const bf16* x, float* dst, void* ws, hipStream_t st,
+             bool defer = false) {
     const unsigned grid = (unsigned)((long)p.nt * p.kt * p.chunks);
     float* slab = p.chunks > 1 ? (float*)ws : nullptr;
     if (p.tn == 128 && p.tk == 128) launch_tile<128, 128>(p, grid, M, N, K, dy, x, dst, slab, st);
@@ -458,7 +481,7 @@ int run_bf16(const Plan& p, long M, int N, int K, const bf16* dy, const bf16* x,
     else if (p.tn == 64 && p.tk == 64) launch_tile<64, 64>(p, grid, M, N, K, dy, x, dst, slab, st);
     else return fail(CSU_E_ARG, "linear_wgrad: tile must be 64 or 128");
     if (int e = check_launch("linear_wgrad")) return e;
-    if (p.chunks > 1) {
+    if (p.chunks > 1 && !defer) {
         const long outs = ((long)N * K + N) / 4;
         wslab_reduce<<<(unsigned)((outs + NT - 1) / NT), NT, 0, st>>>(N, K, p.tn, p.tk, p.chunks, slab, dst);
         return check_launch("linear_wgrad reduce");
@@ -509,6 +532,44 @@ extern "C" int csu_linear_wgrad_tuned(long M, int N, int K, int dtype, const voi
 extern "C" int csu_linear_wgrad(long M, int N, int K, int dtype, const void* dy, const void* x, float* dw_db,
                                 void* workspace, size_t ws_bytes, void* stream) {
     return csu_linear_wgrad_tuned(M, N, K, dtype, dy, x, dw_db, workspace, ws_bytes, 0, 0, 0, stream);
+}
+
+extern "C" int csu_linear_wgrad_deferred(long M, int N, int K, const void* dy, const void* x, float* dw_db,
+                                         void* workspace, size_t ws_bytes, csu_wslab_item* item, void* stream) {
+    if (M < 1 || N < 1 || K < 1 || !dy || !x || !dw_db || !item) return fail(CSU_E_ARG, "linear_wgrad_deferred: bad args");
+    if (N % 8 || K % 8) return fail(CSU_E_ARG, "linear_wgrad_deferred: N and K must be multiples of 8");
+    const Plan p = make_plan(M, N, K, 0, 0, 0);
+    if (ws_bytes < plan_bytes(p) || (!workspace && plan_bytes(p))) return fail(CSU_E_WORKSPACE, "linear_wgrad_deferred: workspace");
+    *item = csu_wslab_item{(const float*)workspace, dw_db, N, K, p.tn, p.tk, p.chunks, 0};
+    return run_bf16(p, M, N, K, (const bf16*)dy, (const bf16*)x, dw_db, workspace, as_stream(stream), true);
+}
+
+extern "C" int csu_wslab_reduce_batch(const csu_wslab_item* items, int count, void* stream) {
+    if (count < 0 || (count && !items)) return fail(CSU_E_ARG, "wslab_reduce_batch: bad args");
+    WsBatch t;
+    t.count = 0;
+    t.b0[0] = 0;
+    auto flush = [&]() -> int {
+        if (!t.count) return 0;
+        wslab_reduce_batch<<<(unsigned)t.b0[t.count], NT, 0, as_stream(stream)>>>(t);
+        t.count = 0;
+        return check_launch("wslab_reduce_batch");
+    };
+    for (int i = 0; i < count; ++i) {
+        const csu_wslab_item& it = items[i];
+        if (it.chunks <= 1) continue;   // written by the tile kernel itself
+        if (!it.slab || !it.dst || it.N % 4 || it.K % 4) return fail(CSU_E_ARG, "wslab_reduce_batch: bad item");
+        const long blocks = (((long)it.N * it.K + it.N) / 4 + NT - 1) / NT;
+        if (t.count == WSB_MAX || (long)t.b0[t.count] + blocks > (1L << 30))
+            if (int e = flush()) return e;
+        const int c = t.count;
+        t.slab[c] = it.slab;
+        t.dst[c] = it.dst;
+        t.N[c] = it.N; t.K[c] = it.K; t.tn[c] = it.tn; t.tk[c] = it.tk; t.chunks[c] = it.chunks;
+        t.b0[c + 1] = t.b0[c] + (int)blocks;
+        t.count = c + 1;
+    }
+    return flush();
 }
 
 #ifdef WG_TIMING

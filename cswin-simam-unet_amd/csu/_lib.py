@@ -36,6 +36,12 @@ class LnParamItem(ctypes.Structure):
     _fields_ = [("workspace", c_void_p), ("dgamma", c_void_p), ("dbeta", c_void_p), ("rows", c_int32), ("C", c_int32)]
 
 
+class WslabItem(ctypes.Structure):
+    """csu_wslab_item (include/csu.h)."""
+    _fields_ = [("slab", c_void_p), ("dst", c_void_p), ("N", c_int32), ("K", c_int32), ("tn", c_int32), ("tk", c_int32),
+                ("chunks", c_int32), ("_pad", c_int32)]
+
+
 class MlpDropout(ctypes.Structure):
     """csu_mlp_dropout (include/csu.h)."""
     _fields_ = [("rng", c_void_p), ("site_hidden", ctypes.c_uint32), ("site_out", ctypes.c_uint32), ("p", c_float),
@@ -115,6 +121,9 @@ _SIGS = {
     "csu_droppath_scale": (ctypes.c_int, [ctypes.c_long, c_void_p, ctypes.c_uint, c_float, c_void_p, c_void_p]),
     "csu_layernorm_param_reduce": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
     "csu_layernorm_param_reduce_batch": (ctypes.c_int, [c_void_p, ctypes.c_int, c_void_p]),
+    "csu_linear_wgrad_deferred": (ctypes.c_int, [ctypes.c_long, ctypes.c_int, ctypes.c_int, c_void_p, c_void_p, c_void_p,
+                                                 c_void_p, c_size_t, ctypes.POINTER(WslabItem), c_void_p]),
+    "csu_wslab_reduce_batch": (ctypes.c_int, [c_void_p, ctypes.c_int, c_void_p]),
     "csu_grad_join": (ctypes.c_int, [ctypes.c_long, ctypes.c_int, c_void_p, ctypes.c_int, c_void_p, c_void_p, c_void_p,
                                      c_void_p]),
     "csu_bce_loss_workspace": (c_size_t, [ctypes.c_long]),

@@ -227,15 +227,54 @@ def _ln_param_flush():
             0, sum(w.numel() for w, _, _, _ in pend) + nv * 4)
 
 
+def _queue_flush():
+    """Queue the end-of-backward flush once per backward pass (outside a backward pass -- direct
+    calls, tests -- the caller flushes explicitly)."""
+    if not _LN_QUEUED[0] and torch._C._current_graph_task_id() != -1:
+        torch.autograd.Variable._execution_engine.queue_callback(_end_of_backward_flush)
+        _LN_QUEUED[0] = True
+
+
+def _end_of_backward_flush():
+    """The deferred parameter-gradient reductions of this backward pass: every LayerNorm's dgamma /
+    dbeta (one launch) and every deferred token-Linear weight-gradient slab sum (one launch per 40)."""
+    _ln_param_flush()
+    _wgrad_flush()
+
+
 def _ln_params(ctx, rows, C, work, dgb):
     """Reduce (later, batched) or report that the caller must pass dgamma / dbeta pointers."""
     if not (DEFER_LN and _deferrable(*ctx.params)):
         return False
     _LN_PENDING.append((work, dgb, rows, C))
-    if not _LN_QUEUED[0]:
-        torch.autograd.Variable._execution_engine.queue_callback(_ln_param_flush)
-        _LN_QUEUED[0] = True
+    _queue_flush()
     return True
+
+
+# Token-Linear weight gradients (bf16): the split-K chunk partials of every Linear whose dW / db
+# nothing reads before the end of backward (same conditions as the LayerNorm deferral) are summed
+# by ONE batched launch per 40 Linears at the end of backward (csu_wslab_reduce_batch) instead of
+# one small reduction launch each (~110 per 512x512 step).  CSU_DEFER_WGRAD=0 disables.
+DEFER_WGRAD = _os.environ.get("CSU_DEFER_WGRAD", "1") == "1"
+_WG_PENDING: list = []
+
+
+def _wgrad_flush():
+    pend, _WG_PENDING[:] = list(_WG_PENDING), []
+    if not pend:
+        return
+    dev = pend[0][1].device
+    items = (_lib.WslabItem * len(pend))()
+    nbytes = 0
+    for i, (it, out, work) in enumerate(pend):
+        items[i] = it
+        nbytes += it.chunks * (it.N * it.K + it.N) * 4 + (it.N * it.K + it.N) * 4
+    _launch("linear_wgrad", lambda: lib().csu_wslab_reduce_batch(items, len(pend), stream_ptr(dev)), 0, nbytes)
+
+
+def _wgrad_deferrable(dy2, wdt, bdt, params) -> bool:
+    return (DEFER_WGRAD and dy2.dtype == torch.bfloat16 and bool(params) and wdt in (None, torch.float32)
+            and bdt in (None, torch.float32) and _deferrable(*params))
 
 
 class _LayerNormFn(torch.autograd.Function):
@@ -536,9 +575,11 @@ def gemm_f32(layout: int, a: torch.Tensor, b: torch.Tensor, M: int, N: int, K: i
     return (out, asum) if with_asum else out
 
 
-def linear_wgrad(dy2: torch.Tensor, x2: torch.Tensor, out=None, work=None):
+def linear_wgrad(dy2: torch.Tensor, x2: torch.Tensor, out=None, work=None, defer: bool = False):
     """(dW (N, K), db (N)) fp32 of a token Linear: one MFMA split-K kernel + one reduction.
-    ``out`` / ``work``: caller-allocated result (N*K + N fp32) and workspace buffers."""
+    ``out`` / ``work``: caller-allocated result (N*K + N fp32) and workspace buffers.  ``defer``
+    (bf16): the reduction joins the end-of-backward batch (_wgrad_flush); the returned tensors are
+    filled then -- only for gradients nothing reads earlier (see _wgrad_deferrable)."""
     require_device(dy2, x2)
     M, N = dy2.shape
     K = x2.shape[1]
@@ -551,6 +592,15 @@ def linear_wgrad(dy2: torch.Tensor, x2: torch.Tensor, out=None, work=None):
         out = torch.empty(N * K + N, dtype=torch.float32, device=dy2.device)
     if work is None:
         work = torch.empty(max(n, 16), dtype=torch.uint8, device=dy2.device)
+    if defer and dy2.dtype == torch.bfloat16 and N % 8 == 0 and K % 8 == 0:
+        it = _lib.WslabItem()
+        _launch("linear_wgrad", lambda: L.csu_linear_wgrad_deferred(M, N, K, ptr(dy2), ptr(x2), ptr(out), ptr(work), n,
+                                                                    ctypes.byref(it), stream_ptr(dy2.device)),
+                2 * M * N * K, M * (N + K) * 2 + (N * K + N) * 4)
+        if it.chunks > 1:
+            _WG_PENDING.append((it, out, work))   # keeps the slab workspace and the result alive
+            _queue_flush()
+        return out[:N * K].view(N, K), out[N * K:]
     _launch("linear_wgrad", lambda: L.csu_linear_wgrad(M, N, K, dtype_code(dy2), ptr(dy2), ptr(x2), ptr(out), ptr(work), n,
                                                        stream_ptr(dy2.device)),
             2 * M * N * K, M * (N + K) * dy2.element_size() + (N * K + N) * 4, prec=prec_of(dy2))
@@ -671,7 +721,7 @@ def wgrad_maybe_side(dy2: torch.Tensor, x2: torch.Tensor, wdt, bdt, params=()):
     """linear_wgrad on the side stream when allowed (fp32 master weights, see above), else inline."""
     if _side_ok(dy2, wdt, bdt, params=params):
         return _side_run(lambda: linear_wgrad(dy2, x2), dy2, x2)
-    return linear_wgrad(dy2, x2)
+    return linear_wgrad(dy2, x2, defer=_wgrad_deferrable(dy2, wdt, bdt, params))
 
 
 # csu_gemm_ex (fused bias / GELU / GELU' / residual token GEMM) for the bf16 nn.Linear forward and

@@ -200,6 +200,19 @@ int csu_colsum(long rows, long cols, int dtype, const void* in, float* out, void
 size_t csu_linear_wgrad_workspace(long M, int N, int K);
 int csu_linear_wgrad(long M, int N, int K, int dtype, const void* dy, const void* x, float* dw_db,
                      void* workspace, size_t ws_bytes, void* stream);
+/* Deferred form (bf16): only the tile kernel runs now; when the plan splits the tokens
+ * (item->chunks > 1) the chunk partials stay in `workspace` and dw_db is written later by
+ * csu_wslab_reduce_batch over the returned items (one launch for many Linears, e.g. at the end of
+ * a backward pass; workspace and dw_db must stay allocated until then).  item->chunks == 1: dw_db
+ * is already written. */
+typedef struct {
+    const float* slab;
+    float* dst;
+    int32_t N, K, tn, tk, chunks, _pad;
+} csu_wslab_item;
+int csu_linear_wgrad_deferred(long M, int N, int K, const void* dy, const void* x, float* dw_db,
+                              void* workspace, size_t ws_bytes, csu_wslab_item* item, void* stream);
+int csu_wslab_reduce_batch(const csu_wslab_item* items, int count, void* stream);
 /* Same with the plan forced (tuning / tests): bf16 output tile tn x tk (64 or 128; 0 = auto) and
  * the number of token chunks (0 = auto).  The fp32 path ignores them. */
 size_t csu_linear_wgrad_tuned_workspace(long M, int N, int K, int tn, int tk, int chunks);

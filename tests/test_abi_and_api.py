@@ -38,7 +38,9 @@ def test_struct_layout_matches_header(tmp_path):
               "csu_stripe_args": (_lib.StripeArgs, ["scale", "br", "drop_rng", "drop_site", "drop_p"]),
               "csu_gemm_desc": (_lib.GemmDesc, ["M", "a", "b_trans", "bias", "out", "ldc", "cfg"]),
               "csu_mlp_dropout": (_lib.MlpDropout, ["rng", "site_out", "p", "row_scale", "rows_per_sample"]),
-              "csu_conv_geom": (_lib.ConvGeom, ["B", "KH", "pad"])}
+              "csu_conv_geom": (_lib.ConvGeom, ["B", "KH", "pad"]),
+              "csu_wslab_item": (_lib.WslabItem, ["slab", "dst", "N", "tk", "chunks"]),
+              "csu_ln_param_item": (_lib.LnParamItem, ["workspace", "dbeta", "rows", "C"])}
     lines = ["#include <stdio.h>", "#include <stddef.h>", '#include "csu.h"', "int main(void) {"]
     for cname, (_, fields) in checks.items():
         lines.append(f'printf("{cname} %zu\\n", sizeof({cname}));')

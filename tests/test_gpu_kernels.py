@@ -725,3 +725,25 @@ def test_pack_nhwc_image():
     y = torch.empty(3, 37, 41, 8, dtype=torch.bfloat16, device=d)
     _lib.check(_lib.lib().csu_pack_nhwc_bf16(3, 3, 37, 41, 8, ops.ptr(x), ops.ptr(y), ops.stream_ptr(d)), "pack")
     assert torch.equal(y[..., :3], x.permute(0, 2, 3, 1).bfloat16()) and not y[..., 3:].any()
+
+
+@pytest.mark.parametrize("M,N,K", [(16384, 1024, 256), (16384, 256, 1024), (65536, 384, 128), (4096, 512, 512),
+                                   (262144, 192, 64), (100, 64, 64)])
+def test_linear_wgrad_deferred_batch(M, N, K):
+    """Deferred weight gradients (tile kernels now, ONE batched slab reduction at the end of
+    backward) are bitwise equal to the inline reduction, across several Linears in one batch."""
+    from csu import ops
+    d = dev()
+    g = torch.Generator(device=d).manual_seed(M + N + K)
+    outs = []
+    for rep in range(3):   # three Linears of the same shape in one batch
+        dy = (torch.randn(M, N, device=d, generator=g) * 0.1).bfloat16()
+        x = torch.randn(M, K, device=d, generator=g).bfloat16()
+        dw, db = ops.linear_wgrad(dy, x)
+        dwd, dbd = ops.linear_wgrad(dy, x, defer=True)
+        outs.append((dw.clone(), db.clone(), dwd, dbd))
+    ops._wgrad_flush()
+    torch.cuda.synchronize()
+    assert not ops._WG_PENDING
+    for dw, db, dwd, dbd in outs:
+        assert torch.equal(dw, dwd) and torch.equal(db, dbd)
