@@ -801,6 +801,18 @@ int wgrad_blocks(const csu_stripe_args& a) {
 // orientations, so nothing is ever written transposed.
 // =============================================================================================
 constexpr int WMAX = 1024;  // largest window held in LDS (K + V images: 128 KiB of the 160 KiB)
+
+#ifdef WG_TIMING   // debug build only: per-workgroup phase stamps (100 MHz) of the last launch of each
+                   // whole-window kernel (0 fwd, 1 dq, 2 dkdv): start, staged, end + hardware id
+__device__ unsigned long long attn_ts[3][4][16384];
+#define ATT_STAMP(kern, k) do { \
+    const unsigned _b = blockIdx.x + blockIdx.y * gridDim.x; \
+    if (threadIdx.x == 0 && _b < 16384) { \
+        attn_ts[kern][k][_b + threadIdx.x] = __builtin_amdgcn_s_memrealtime(); \
+        if (k == 0) attn_ts[kern][3][_b + threadIdx.x] = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11)); } } while (0)
+#else
+#define ATT_STAMP(kern, k) do {} while (0)
+#endif
 typedef float f2 __attribute__((ext_vector_type(2)));   // packed-f32 pairs (v_pk_fma/mul/add_f32)
 
 __device__ __forceinline__ int swz(int row, int col) {   // element offset in a swizzled image
@@ -918,6 +930,7 @@ __global__ __launch_bounds__(NT) void stripe_fwd_w(csu_stripe_args a, int split,
     __shared__ __attribute__((aligned(16))) bf16 Ks[WM * HD];
     __shared__ __attribute__((aligned(16))) bf16 Vs[WM * HD];
     __shared__ float wts[HD * 10];
+    ATT_STAMP(0, 0);
     const Win w = decode_w(a, split);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int r = lane & 31, h = lane >> 5;
@@ -936,6 +949,7 @@ __global__ __launch_bounds__(NT) void stripe_fwd_w(csu_stripe_args a, int split,
     stage_lepe_weights(branch(a, w.br), w.h, wts);
     stage_win2(w, a.reso, img, C3, C + w.chq, img, C3, 2 * C + w.chq, (npad + 63) & ~63, Ks, Vs);  // zero rows up to a 64-key step
     __syncthreads();
+    ATT_STAMP(0, 1);
     const float c = a.scale * kLog2e;
     ADrop dr;
     if constexpr (DROP) dr = attn_drop(a, w);
@@ -1019,6 +1033,7 @@ __global__ __launch_bounds__(NT) void stripe_fwd_w(csu_stripe_args a, int split,
             store4(orow + d0, v);
         }
     }
+    ATT_STAMP(0, 2);
 }
 
 template <int WM, bool DROP>
@@ -1029,6 +1044,7 @@ __global__ __launch_bounds__(NT) void stripe_bwd_dq_w(csu_stripe_args a, int spl
     __shared__ __attribute__((aligned(16))) bf16 Ks[WM * HD];
     __shared__ __attribute__((aligned(16))) bf16 Vs[WM * HD];
     __shared__ float wts[HD * 10];
+    ATT_STAMP(1, 0);
     const Win w = decode_w(a, split);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int r = lane & 31, h = lane >> 5;
@@ -1039,17 +1055,25 @@ __global__ __launch_bounds__(NT) void stripe_bwd_dq_w(csu_stripe_args a, int spl
     const int npad = (w.N + 31) & ~31;
     const int rows = (((npad + split - 1) / split) + 31) & ~31;   // 32-aligned: mask groups start on 8
     const int qbeg = w.blk * rows, qend = min(npad, qbeg + rows);
-    Frag<bf16> qn_f, gn_f;   // first query block's fragments, loaded with the staging loads
-    {
-        const int qn = qbeg + 32 * wave + r;
-        const bool qv = qbeg + 32 * wave < qend && qn < w.N;
+    // the wave's query-block operands (Q, dO and O fragments, lse): the first block's are loaded
+    // with the staging loads, so their latency overlaps the K/V staging; later blocks (only when a
+    // workgroup owns > 128 query rows: the 1024x1024 stages) load at the top of their iteration
+    Frag<bf16> qf, gf, of;
+    float lq_raw;
+    auto load_q = [&](int q0) {
+        const int qn = q0 + r;
+        const bool qv = q0 < qend && qn < w.N;
         const size_t t = qv ? tok_of(w, a.reso, qn) : 0;
-        load_frag(qn_f, img + t * C3 + w.chq, h, qv);
-        load_frag(gn_f, gimg + t * C + w.chq, h, qv);
-    }
+        load_frag(qf, img + t * C3 + w.chq, h, qv);
+        load_frag(gf, gimg + t * C + w.chq, h, qv);
+        load_frag(of, oimg + t * C + w.chq, h, qv);
+        lq_raw = qv ? lse[stat_index(a, w, (int)t)] : 0.f;
+    };
+    load_q(qbeg + 32 * wave);
     stage_lepe_weights(branch(a, w.br), w.h, wts);
     stage_win2(w, a.reso, img, C3, C + w.chq, img, C3, 2 * C + w.chq, npad, Ks, Vs);
     __syncthreads();
+    ATT_STAMP(1, 1);
     const float c = a.scale * kLog2e;
     ADrop dr;
     if constexpr (DROP) dr = attn_drop(a, w);
@@ -1057,31 +1081,26 @@ __global__ __launch_bounds__(NT) void stripe_bwd_dq_w(csu_stripe_args a, int spl
         const int qn = q0 + r;
         const bool qvalid = qn < w.N;
         const int qtok = qvalid ? tok_of(w, a.reso, qn) : 0;
-        const Frag<bf16> qf = qn_f, gf = gn_f;
-        if (q0 + 128 < qend) {
-            const int qn2 = q0 + 128 + r;
-            const bool qv2 = qn2 < w.N;
-            const size_t t2 = qv2 ? tok_of(w, a.reso, qn2) : 0;
-            load_frag(qn_f, img + t2 * C3 + w.chq, h, qv2);
-            load_frag(gn_f, gimg + t2 * C + w.chq, h, qv2);
-        }
+        if (q0 != qbeg + 32 * wave) load_q(q0);
+        // delta = rowsum(dO * (O - LePE)) = rowsum(dO * attention output), over the fragment's 16
+        // channels (16 s + 8 h + 0..7) of this lane, then the other half's
         float dl = 0.f;
         if (qvalid) {
 #pragma unroll
-            for (int g4 = 0; g4 < 4; ++g4) {
-                const int d0 = 8 * g4 + 4 * h;
-                float lp[4], ov[4], gv[4];
-                lepe4_lds(w, Vs, qn, d0, wts, +1, lp);
-                load4(oimg + (size_t)qtok * C + w.chq + d0, ov);
-                load4(gimg + (size_t)qtok * C + w.chq + d0, gv);
+            for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
-                for (int j = 0; j < 4; ++j) dl += gv[j] * (ov[j] - lp[j]);
-            }
+                for (int p4 = 0; p4 < 2; ++p4) {
+                    float lp[4];
+                    lepe4_lds(w, Vs, qn, 16 * s2 + 8 * h + 4 * p4, wts, +1, lp);
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        dl += (float)gf.v[s2][4 * p4 + j] * ((float)of.v[s2][4 * p4 + j] - lp[j]);
+                }
         }
         dl += __shfl_xor(dl, 32, 64);
         const size_t si = stat_index(a, w, qtok);
         if (qvalid && h == 0) delta[si] = dl;
-        const float lq = qvalid ? lse[si] * kLog2e : 0.f;
+        const float lq = qvalid ? lq_raw * kLog2e : 0.f;
         f32x16 dq = {};
         const f2 cc = {c, c}, lq2 = {lq, lq}, dl2 = {dl, dl};
         for (int kb = 0; kb < npad; kb += 32) {
@@ -1114,6 +1133,7 @@ __global__ __launch_bounds__(NT) void stripe_bwd_dq_w(csu_stripe_args a, int spl
             store4(drow + d0, v);
         }
     }
+    ATT_STAMP(1, 2);
 }
 
 template <int WM, bool DROP>
@@ -1125,6 +1145,7 @@ __global__ __launch_bounds__(NT) void stripe_bwd_dkdv_w(csu_stripe_args a, int s
     __shared__ __attribute__((aligned(16))) float lse_s[WM], dl_s[WM];
     __shared__ float wts[HD * 10];
     __shared__ __attribute__((aligned(16))) unsigned char dtbl[4][128];
+    ATT_STAMP(2, 0);
     const Win w = decode_w(a, split);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int r = lane & 31, h = lane >> 5;
@@ -1134,13 +1155,16 @@ __global__ __launch_bounds__(NT) void stripe_bwd_dkdv_w(csu_stripe_args a, int s
     const int npad = (w.N + 31) & ~31;
     const int rows = (((npad + split - 1) / split) + 31) & ~31;   // 32-aligned: mask groups start on 8
     const int kbeg = w.blk * rows, kend = min(npad, kbeg + rows);
-    Frag<bf16> kn_f, vn_f;   // first key block's fragments, loaded with the staging loads
+    // the wave's key-block fragments: the first block's are loaded with the staging loads; later
+    // blocks (only when a workgroup owns > 128 key rows: the 1024x1024 stages) load at the top of
+    // their iteration -- no second register set, so the kernel stays at <= 128 VGPRs (4 waves/SIMD)
+    Frag<bf16> kf, vf;
     {
         const int kn = kbeg + 32 * wave + r;
         const bool kv = kbeg + 32 * wave < kend && kn < w.N;
         const size_t t = kv ? tok_of(w, a.reso, kn) : 0;
-        load_frag(kn_f, img + t * C3 + C + w.chq, h, kv);
-        load_frag(vn_f, img + t * C3 + 2 * C + w.chq, h, kv);
+        load_frag(kf, img + t * C3 + C + w.chq, h, kv);
+        load_frag(vf, img + t * C3 + 2 * C + w.chq, h, kv);
     }
     stage_lepe_weights(branch(a, w.br), w.h, wts);
     stage_win2(w, a.reso, img, C3, w.chq, gimg, C, w.chq, npad, Qs, Gs);
@@ -1151,6 +1175,7 @@ __global__ __launch_bounds__(NT) void stripe_bwd_dkdv_w(csu_stripe_args a, int s
         dl_s[i] = v ? delta[si] : 0.f;
     }
     __syncthreads();
+    ATT_STAMP(2, 1);
     const float c = a.scale * kLog2e;
     ADrop dr;
     if constexpr (DROP) dr = attn_drop(a, w);
@@ -1158,13 +1183,10 @@ __global__ __launch_bounds__(NT) void stripe_bwd_dkdv_w(csu_stripe_args a, int s
         const int kn = k0 + r;
         const bool kvalid = kn < w.N;
         const int ktok = kvalid ? tok_of(w, a.reso, kn) : 0;
-        const Frag<bf16> kf = kn_f, vf = vn_f;
-        if (k0 + 128 < kend) {
-            const int kn2 = k0 + 128 + r;
-            const bool kv2 = kn2 < w.N;
-            const size_t t2 = kv2 ? tok_of(w, a.reso, kn2) : 0;
-            load_frag(kn_f, img + t2 * C3 + C + w.chq, h, kv2);
-            load_frag(vn_f, img + t2 * C3 + 2 * C + w.chq, h, kv2);
+        if (k0 != kbeg + 32 * wave) {
+            const size_t t2 = kvalid ? tok_of(w, a.reso, kn) : 0;
+            load_frag(kf, img + t2 * C3 + C + w.chq, h, kvalid);
+            load_frag(vf, img + t2 * C3 + 2 * C + w.chq, h, kvalid);
         }
         f32x16 dk = {}, dv = {};
         const f2 cc = {c, c};
@@ -1216,6 +1238,7 @@ __global__ __launch_bounds__(NT) void stripe_bwd_dkdv_w(csu_stripe_args a, int s
             store4(drow + 2 * C + d0, vv);
         }
     }
+    ATT_STAMP(2, 2);
 }
 
 // split factor of the whole-window kernels: workgroups per window-head, so that a launch has
@@ -1415,3 +1438,9 @@ extern "C" int csu_stripe_lepe_wgrad(const csu_stripe_args* a, int dtype, const 
     lepe_wgrad_launch(*a, dtype, qkv, dout, (float*)workspace, as_stream(stream));
     return check_launch("stripe_lepe_wgrad");
 }
+
+#ifdef WG_TIMING
+extern "C" int csu_debug_attn_ts(unsigned long long* host) {
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(csu::attn_ts), sizeof(csu::attn_ts), 0, hipMemcpyDeviceToHost);
+}
+#endif

@@ -1,0 +1,62 @@
+"""Per-workgroup phase timeline of the whole-window attention kernels (debug build with WG_TIMING:
+start / K,V staged / end stamps at 100 MHz) for one stripe-attention forward + backward at a stage
+of the 512x512 B16 model.
+    CSU_LIB_PATH=.../libcsu_hip_dbg.so python tools/attn_wg_timeline.py [stage 1..4]"""
+import ctypes
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [REPO, os.path.join(REPO, "cswin-simam-unet_amd")]
+os.environ.setdefault("CSU_LIB_PATH", os.path.join(REPO, "cswin-simam-unet_amd", "csu", "_lib", "libcsu_hip_dbg.so"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from csu import ops  # noqa: E402
+from csu._lib import lib  # noqa: E402
+
+STAGES = {1: (128, 64, 2, 1), 2: (64, 128, 4, 2), 3: (32, 256, 8, 8), 4: (16, 512, 16, 16)}
+
+
+def main():
+    st = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+    reso, C, heads, sw = STAGES[st]
+    B = 16
+    d = torch.device("cuda")
+    nb = 1 if sw == reso else 2
+    brs = [(reso, sw, 0), (sw, reso, C // 2)] if nb == 2 else [(reso, reso, 0)]
+    geom = ops.StripeGeometry(reso, C, heads // nb, brs, 32 ** -0.5)
+    qkv = torch.randn(B, reso * reso, 3 * C, device=d, dtype=torch.bfloat16, requires_grad=True)
+    ws = [torch.randn(C // nb, 1, 3, 3, device=d, requires_grad=True) for _ in range(nb)]
+    bs = [torch.randn(C // nb, device=d, requires_grad=True) for _ in range(nb)]
+    g = torch.randn(B, reso * reso, C, device=d, dtype=torch.bfloat16)
+    for _ in range(3):
+        out = ops.stripe_attention(qkv, geom, ws, bs)
+        out.backward(g)
+    torch.cuda.synchronize()
+    L = lib()
+    fn = L.csu_debug_attn_ts
+    fn.restype, fn.argtypes = ctypes.c_int, [ctypes.c_void_p]
+    buf = np.zeros((3, 4, 16384), dtype=np.uint64)
+    assert fn(buf.ctypes.data) == 0
+    for k, name in enumerate(("fwd", "dq", "dkdv")):
+        t = buf[k, :3].astype(np.int64)
+        valid = t[0] > 0
+        t = t[:, valid]
+        n = t.shape[1]
+        t0 = t[0].min()
+        start, staged, end = (t[0] - t0) / 100.0, (t[1] - t0) / 100.0, (t[2] - t0) / 100.0   # us
+        stage_us, comp_us = staged - start, end - staged
+        span = end.max()
+        # resident workgroups over time (1 us bins)
+        bins = np.arange(0, span + 1.0, 1.0)
+        res = [int(((start <= b) & (end > b)).sum()) for b in bins]
+        print(f"stage {st} {name}: {n} workgroups, span {span:.1f} us; start spread p50 {np.median(start):.1f} "
+              f"p90 {np.percentile(start, 90):.1f} max {start.max():.1f}; staging p50 {np.median(stage_us):.1f} "
+              f"p90 {np.percentile(stage_us, 90):.1f}; compute p50 {np.median(comp_us):.1f} p90 {np.percentile(comp_us, 90):.1f}")
+        print("   resident WGs per us:", res[:40])
+
+
+if __name__ == "__main__":
+    main()
