@@ -357,7 +357,7 @@ __global__ __launch_bounds__(NT) void igemm_bf16(IG4 gs, const bf16* __restrict_
     constexpr int ACH = BM * 8 / NT, BCH = BN * 8 / NT, NP = 8 / VW;
     __shared__ __attribute__((aligned(16))) bf16 As[2][BM * BK];
     __shared__ __attribute__((aligned(16))) bf16 Bs[2][BN * BK];
-    __shared__ long ooff[BM];
+    __shared__ unsigned ooff[BM];   // byte offset of each tile row's output pixel (kOOB: none)
     // problem of this z-slice (selects, not a dynamic index into the kernel-argument struct)
     const int z = blockIdx.z;
     const IG g = z == 0 ? gs.g[0] : z == 1 ? gs.g[1] : z == 2 ? gs.g[2] : gs.g[3];
@@ -374,11 +374,12 @@ __global__ __launch_bounds__(NT) void igemm_bf16(IG4 gs, const bf16* __restrict_
 #pragma unroll
     for (int i = 0; i < ACH; ++i) {
         const long m = m0 + rbase + 32 * i;
-        if (m < g.M) {
-            const int rx = (int)(m % g.RW);
-            const long t = m / g.RW;
-            const int ry = (int)(t % g.RH);
-            rb[i] = (int)(t / g.RH) * g.Hs;
+        if (m < g.M) {   // 32-bit decomposition (check_geo: < 2^31 pixels)
+            const unsigned mu = (unsigned)m, t = mu / (unsigned)g.RW;
+            const int rx = (int)(mu - t * (unsigned)g.RW);
+            const unsigned b = t / (unsigned)g.RH;
+            const int ry = (int)(t - b * (unsigned)g.RH);
+            rb[i] = (int)b * g.Hs;
             ryb[i] = ry * g.ay + g.by;
             rxb[i] = rx * g.ax + g.bx;
         } else {
@@ -387,8 +388,16 @@ __global__ __launch_bounds__(NT) void igemm_bf16(IG4 gs, const bf16* __restrict_
             rxb[i] = 0;
         }
     }
-    bf16x8 ra[ACH], rbw[BCH];
-    auto load = [&](int k0) {
+    // two register sets: the loads of K slice k + 2 are issued while slice k is multiplied and slice
+    // k + 1 (loaded one step earlier) is stored to LDS -- two steps of MFMA work hide each load
+    bf16x8 ra2[2][ACH], rbw2[2][BCH];
+    // (pixel offsets fit 31 bits: check_geo bounds the pixel count, launch_ig the byte size)
+    // branch-free gathers: raw buffer loads whose out-of-image / out-of-range lanes get an offset
+    // past the resource (read as 0), so hipcc keeps every load of a slice in flight (a predicated
+    // load makes it wait vmcnt(0) at the join and the register prefetch is lost)
+    const __amdgpu_buffer_rsrc_t rs_src = buf_rsrc(src, (long)g.B * g.Hs * g.Ws * g.Cs * 2);
+    const __amdgpu_buffer_rsrc_t rs_w = buf_rsrc(Bw, (long)g.Ncols * g.ldw * 2);
+    auto load = [&](int k0, bf16x8* ra, bf16x8* rbw) {
 #pragma unroll
         for (int pc = 0; pc < NP; ++pc) {
             const int k = k0 + 8 * ch + VW * pc;
@@ -401,31 +410,37 @@ __global__ __launch_bounds__(NT) void igemm_bf16(IG4 gs, const bf16* __restrict_
             for (int i = 0; i < ACH; ++i) {
                 const int y = ryb[i] + oy, x = rxb[i] + ox;
                 const bool ok = kin && y >= 0 && y < g.Hs && x >= 0 && x < g.Ws;
-                const bf16* p = src + (((long)rb[i] + y) * g.Ws + x) * g.Cs + c;
+                const unsigned off = ok ? (unsigned)((((rb[i] + y) * g.Ws + x) * g.Cs + c) * 2) : kOOB;
                 if constexpr (VW == 8) {
-                    ra[i] = ok ? *reinterpret_cast<const bf16x8*>(p) : bf16x8{};
+                    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs_src, off, 0, 0);
+                    __builtin_memcpy(&ra[i], &v, 16);
                 } else {
-                    const bf16x4 v = ok ? *reinterpret_cast<const bf16x4*>(p) : bf16x4{};
+                    const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(rs_src, off, 0, 0);
+                    bf16x4 b;
+                    __builtin_memcpy(&b, &v, 8);
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) ra[i][4 * pc + j] = v[j];
+                    for (int j = 0; j < 4; ++j) ra[i][4 * pc + j] = b[j];
                 }
             }
 #pragma unroll
             for (int j = 0; j < BCH; ++j) {
                 const int n = n0 + rbase + 32 * j;
                 const bool ok = kin && n < g.Ncols;
-                const bf16* p = Bw + (long)n * g.ldw + wcol;
+                const unsigned off = ok ? (unsigned)((n * g.ldw + wcol) * 2) : kOOB;
                 if constexpr (VW == 8) {
-                    rbw[j] = ok ? *reinterpret_cast<const bf16x8*>(p) : bf16x8{};
+                    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs_w, off, 0, 0);
+                    __builtin_memcpy(&rbw[j], &v, 16);
                 } else {
-                    const bf16x4 v = ok ? *reinterpret_cast<const bf16x4*>(p) : bf16x4{};
+                    const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(rs_w, off, 0, 0);
+                    bf16x4 b;
+                    __builtin_memcpy(&b, &v, 8);
 #pragma unroll
-                    for (int e = 0; e < 4; ++e) rbw[j][4 * pc + e] = v[e];
+                    for (int e = 0; e < 4; ++e) rbw[j][4 * pc + e] = b[e];
                 }
             }
         }
     };
-    auto store = [&](int buf) {
+    auto store = [&](int buf, const bf16x8* ra, const bf16x8* rbw) {
 #pragma unroll
         for (int i = 0; i < ACH; ++i) *reinterpret_cast<bf16x8*>(&As[buf][swz128(rbase + 32 * i, ch)]) = ra[i];
 #pragma unroll
@@ -433,15 +448,7 @@ __global__ __launch_bounds__(NT) void igemm_bf16(IG4 gs, const bf16* __restrict_
     };
 
     f32x16 acc[2] = {f32x16{}, f32x16{}};
-    if (g.Kd > 0) {
-        load(0);
-        store(0);
-    }
-    __syncthreads();
-    int buf = 0;
-    for (int k0 = 0; k0 < g.Kd; k0 += BK) {
-        const bool more = k0 + BK < g.Kd;
-        if (more) load(k0 + BK);
+    auto mfmas = [&](int buf) {
 #pragma unroll
         for (int s = 0; s < BK / 16; ++s) {
             const bf16x8 b = *reinterpret_cast<const bf16x8*>(&Bs[buf][swz128(wn + r, 2 * s + h)]);
@@ -451,32 +458,53 @@ __global__ __launch_bounds__(NT) void igemm_bf16(IG4 gs, const bf16* __restrict_
                 acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc[i], 0, 0, 0);
             }
         }
-        if (more) store(buf ^ 1);
-        __syncthreads();
-        buf ^= 1;
+    };
+    if (g.Kd > 0) {
+        load(0, ra2[0], rbw2[0]);
+        load(BK, ra2[1], rbw2[1]);
+        store(0, ra2[0], rbw2[0]);
     }
-    // output pixel offsets of the BM rows
+    __syncthreads();
+    // step k: LDS buffer k & 1 holds slice k, register set (k + 1) & 1 slice k + 1 (in flight)
+    for (int k0 = 0; k0 < g.Kd; k0 += 2 * BK) {
+        load(k0 + 2 * BK, ra2[0], rbw2[0]);   // past the end: all offsets out of range, zeros
+        mfmas(0);
+        if (k0 + BK < g.Kd) store(1, ra2[1], rbw2[1]);
+        __syncthreads();
+        if (k0 + BK >= g.Kd) break;
+        load(k0 + 3 * BK, ra2[1], rbw2[1]);
+        mfmas(1);
+        if (k0 + 2 * BK < g.Kd) store(0, ra2[0], rbw2[0]);
+        __syncthreads();
+    }
+    // output pixel byte offsets of the BM rows (32-bit: launch_ig bounds the output to 2 GiB)
     for (int i = threadIdx.x; i < BM; i += NT) {
         const long m = m0 + i;
-        long o = -1;
+        unsigned o = kOOB;
         if (m < g.M) {
-            const int rx = (int)(m % g.RW);
-            const long t = m / g.RW;
-            const int ry = (int)(t % g.RH), b = (int)(t / g.RH);
-            o = (((long)b * g.OHo + ry * g.oya + g.oyb) * g.OWo + rx * g.oxa + g.oxb) * g.Ncols;
+            const unsigned mu = (unsigned)m, t = mu / (unsigned)g.RW;
+            const int rx = (int)(mu - t * (unsigned)g.RW);
+            const unsigned b = t / (unsigned)g.RH;
+            const int ry = (int)(t - b * (unsigned)g.RH);
+            o = (unsigned)((((int)b * g.OHo + ry * g.oya + g.oyb) * g.OWo + rx * g.oxa + g.oxb) * g.Ncols) * 2u;
         }
         ooff[i] = o;
     }
     __syncthreads();
+    // branch-free epilogue: raw buffer stores, rows outside the problem / columns past N dropped by
+    // the out-of-range offset
     const int n = n0 + wn + r;
-    if (n >= g.Ncols) return;
-    const float bv = bias ? bias[n] : 0.f;
+    const bool nv = n < g.Ncols;
+    const float bv = (bias && nv) ? bias[n] : 0.f;
+    const __amdgpu_buffer_rsrc_t rs_o = buf_rsrc(out, (long)g.B * g.OHo * g.OWo * g.Ncols * 2);
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int reg = 0; reg < 16; ++reg) {
-            const long o = ooff[wm + 32 * i + crow(reg, h)];
-            if (o >= 0) out[o + n] = (bf16)(acc[i][reg] + bv);
+            const unsigned o = ooff[wm + 32 * i + crow(reg, h)];
+            const unsigned off = (o != kOOB && nv) ? o + 2u * (unsigned)n : kOOB;
+            const bf16 v = (bf16)(acc[i][reg] + bv);
+            __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, v), rs_o, off, 0, 0);
         }
 }
 
@@ -489,6 +517,9 @@ int launch_ig(const IG* gv, int n, const void* src, const void* w, const float* 
         maxm = gv[i].M > maxm ? gv[i].M : maxm;
     }
     const IG& g = gv[0];
+    if ((long)g.B * g.Hs * g.Ws * g.Cs * 2 >= (1L << 31) || (long)g.Ncols * g.ldw * 2 >= (1L << 31) ||
+        (long)g.B * g.OHo * g.OWo * g.Ncols * 2 >= (1L << 31))
+        return fail(CSU_E_UNSUPPORTED, "conv2d: operand larger than 2 GiB (32-bit buffer offsets)");
     const int vw = g.Cs % 8 == 0 ? 8 : 4;
     const bool narrow = g.Ncols <= 32;
     const int BM = narrow ? 256 : 128, BN = narrow ? 32 : 64;
