@@ -20,7 +20,9 @@ GROUPS = [("lepe_wgrad", "stripe_attn_bwd"), ("wgrad_tile", "linear_wgrad"), ("w
           ("adamw_kernel", "adamw"), ("cast_batch", "cast_bf16_batch"), ("colsum", "colsum"),
           ("simam_stats", "simam_fwd"), ("simam_apply", "simam_fwd"), ("simam_bwd", "simam_bwd"),
           ("head_fwd", "head_fwd"), ("head_bwd", "head_bwd"), ("gemm_f32", "gemm"), ("slab_sum", "gemm"),
-          ("dropout_apply", "dropout"), ("quant_e4m3", "quant_e4m3")]
+          ("dropout_apply", "dropout"), ("quant_e4m3", "quant_e4m3"), ("grad_join", "grad_join"),
+          ("pack_nhwc", "pack_nhwc"), ("bce_partial", "bce_loss"), ("bce_final", "bce_loss"),
+          ("bce_backward", "bce_loss_bwd"), ("head_z", "carafe_head_fwd"), ("rng_advance", "dropout")]
 
 
 def group(name):
