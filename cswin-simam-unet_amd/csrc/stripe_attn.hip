@@ -199,13 +199,40 @@ __device__ __forceinline__ void lepe4(const Win& w, int reso, const T* img, int 
     }
 }
 
+constexpr int LW_IT = (HD * 10 + NT - 1) / NT;
+// the two halves of stage_lepe_weights for the whole-window kernels: issue the loads, and (after the
+// window staging loads have been issued) write LDS -- the LDS write waits for its loads, and vmcnt
+// counts in issue order, so writing right after the loads would drain everything issued before
+__device__ __forceinline__ void lepe_weights_load(const csu_stripe_branch& g, int h, float* v) {
+    const __amdgpu_buffer_rsrc_t rw = buf_rsrc(g.lepe_w + h * HD * 9, HD * 9 * 4), rb = buf_rsrc(g.lepe_b + h * HD, HD * 4);
+#pragma unroll
+    for (int k = 0; k < LW_IT; ++k) {
+        const int i = threadIdx.x + k * NT;
+        const float a = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rw, i < HD * 9 ? (unsigned)i * 4u : kOOB, 0, 0));
+        const float b = __uint_as_float(
+            __builtin_amdgcn_raw_buffer_load_b32(rb, (i >= HD * 9 && i < HD * 10) ? (unsigned)(i - HD * 9) * 4u : kOOB, 0, 0));
+        v[k] = i < HD * 9 ? a : b;
+    }
+}
+__device__ __forceinline__ void lepe_weights_store(const float* v, float* wts) {
+#pragma unroll
+    for (int k = 0; k < LW_IT; ++k)
+        if (threadIdx.x + k * NT < HD * 10) wts[threadIdx.x + k * NT] = v[k];
+}
+
 __device__ __forceinline__ void stage_lepe_weights(const csu_stripe_branch& g, int h, float* wts) {
     constexpr int IT = (HD * 10 + NT - 1) / NT;
     float v[IT];
+    // branch-free (raw buffer loads, masked lanes out of range): a predicated load here made hipcc
+    // wait vmcnt(0) before the window staging loads that follow
+    const __amdgpu_buffer_rsrc_t rw = buf_rsrc(g.lepe_w + h * HD * 9, HD * 9 * 4), rb = buf_rsrc(g.lepe_b + h * HD, HD * 4);
 #pragma unroll
     for (int k = 0; k < IT; ++k) {
         const int i = threadIdx.x + k * NT;
-        v[k] = i < HD * 9 ? g.lepe_w[h * HD * 9 + i] : (i < HD * 10 ? g.lepe_b[h * HD + i - HD * 9] : 0.f);
+        const float a = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rw, i < HD * 9 ? (unsigned)i * 4u : kOOB, 0, 0));
+        const float b = __uint_as_float(
+            __builtin_amdgcn_raw_buffer_load_b32(rb, (i >= HD * 9 && i < HD * 10) ? (unsigned)(i - HD * 9) * 4u : kOOB, 0, 0));
+        v[k] = i < HD * 9 ? a : b;
     }
 #pragma unroll
     for (int k = 0; k < IT; ++k)
@@ -824,6 +851,29 @@ __device__ __forceinline__ v4s tr_read(const bf16* p) {
     return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(p));
 }
 
+// ---- branch-free global loads for the whole-window kernels: raw buffer loads whose masked lanes
+// get an out-of-range offset (read as 0).  A predicated `cond ? *p : 0` load compiles to an
+// exec-masked branch and hipcc waits vmcnt(0) at every join, which serialised the staging loads
+// (10-12 full waits before the first barrier) instead of keeping them in flight together.
+__device__ __forceinline__ bf16x8 ld8_rs(__amdgpu_buffer_rsrc_t rs, unsigned off) {
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+    bf16x8 b;
+    __builtin_memcpy(&b, &v, 16);
+    return b;
+}
+__device__ __forceinline__ float ldf_rs(__amdgpu_buffer_rsrc_t rs, unsigned off) {
+    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0));
+}
+// fragment of row (element offset `row` of the resource), lane half h
+__device__ __forceinline__ void load_frag_rs(Frag<bf16>& f, __amdgpu_buffer_rsrc_t rs, size_t row, int h, bool valid) {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) f.v[s] = ld8_rs(rs, valid ? (unsigned)((row + 16 * s + 8 * h) * 2) : kOOB);
+}
+// per-(branch, image, head) statistics (lse / delta) tensor of the launch
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t stat_rsrc(const csu_stripe_args& a, const float* p) {
+    return buf_rsrc(p, (long)a.nbranch * a.B * a.heads * a.reso * a.reso * 4);
+}
+
 // A operand of X^T-orientation products: lane (r = channel d, h) gets image[k][d] for
 // k = kbase + 16s + 8(j>>2) + 4h + (j&3), the k order of an accumulator tile used as B operand.
 __device__ __forceinline__ bf16x8 tr_frag_acc(const bf16* img, int kbase, int s, int lane) {
@@ -863,6 +913,8 @@ __device__ __forceinline__ void mma_acc_sw(f32x16& acc, const bf16* img, int kba
 __device__ __forceinline__ void stage_win2(const Win& w, int reso, const bf16* imgA, int strideA, int chA,
                                            const bf16* imgB, int strideB, int chB, int npad, bf16* dstA, bf16* dstB) {
     constexpr int IT = 4;   // 256 rows per pass: 8 x 16-B loads in flight per thread
+    const long L = (long)reso * reso;
+    const __amdgpu_buffer_rsrc_t rsA = buf_rsrc(imgA, L * strideA * 2), rsB = buf_rsrc(imgB, L * strideB * 2);
     for (int base = 0; base < npad * 4; base += IT * NT) {
         bf16x8 va[IT], vb[IT];
 #pragma unroll
@@ -870,9 +922,9 @@ __device__ __forceinline__ void stage_win2(const Win& w, int reso, const bf16* i
             const int it = base + threadIdx.x + i * NT;
             const int n = it >> 2, c = (it & 3) * 8;
             const bool ok = it < npad * 4 && n < w.N;
-            const size_t tok = ok ? (size_t)tok_of(w, reso, n) : 0;
-            va[i] = ok ? *reinterpret_cast<const bf16x8*>(imgA + tok * strideA + chA + c) : bf16x8{};
-            vb[i] = ok ? *reinterpret_cast<const bf16x8*>(imgB + tok * strideB + chB + c) : bf16x8{};
+            const unsigned tok = ok ? (unsigned)tok_of(w, reso, n) : 0u;
+            va[i] = ld8_rs(rsA, ok ? (tok * (unsigned)strideA + chA + c) * 2u : kOOB);
+            vb[i] = ld8_rs(rsB, ok ? (tok * (unsigned)strideB + chB + c) * 2u : kOOB);
         }
 #pragma unroll
         for (int i = 0; i < IT; ++i) {
@@ -941,13 +993,16 @@ __global__ __launch_bounds__(NT) void stripe_fwd_w(csu_stripe_args a, int split,
     const int qbeg = w.blk * rows, qend = min(npad, qbeg + rows);
     // this wave's first query fragment is loaded together with the K/V staging loads
     Frag<bf16> qnext;
+    const __amdgpu_buffer_rsrc_t rs_img = buf_rsrc(img, (long)L * C3 * 2);
     {
         const int qn = qbeg + 32 * wave + r;
         const bool qv = qbeg + 32 * wave < qend && qn < w.N;
-        load_frag(qnext, img + (size_t)(qv ? tok_of(w, a.reso, qn) : 0) * C3 + w.chq, h, qv);
+        load_frag_rs(qnext, rs_img, (size_t)(qv ? tok_of(w, a.reso, qn) : 0) * C3 + w.chq, h, qv);
     }
-    stage_lepe_weights(branch(a, w.br), w.h, wts);
+    float lw[LW_IT];
+    lepe_weights_load(branch(a, w.br), w.h, lw);
     stage_win2(w, a.reso, img, C3, C + w.chq, img, C3, 2 * C + w.chq, (npad + 63) & ~63, Ks, Vs);  // zero rows up to a 64-key step
+    lepe_weights_store(lw, wts);
     __syncthreads();
     ATT_STAMP(0, 1);
     const float c = a.scale * kLog2e;
@@ -961,7 +1016,7 @@ __global__ __launch_bounds__(NT) void stripe_fwd_w(csu_stripe_args a, int split,
         if (q0 + 128 < qend) {
             const int qn2 = q0 + 128 + r;
             const bool qv2 = qn2 < w.N;
-            load_frag(qnext, img + (size_t)(qv2 ? tok_of(w, a.reso, qn2) : 0) * C3 + w.chq, h, qv2);
+            load_frag_rs(qnext, rs_img, (size_t)(qv2 ? tok_of(w, a.reso, qn2) : 0) * C3 + w.chq, h, qv2);
         }
         float m = -INFINITY, l = 0.f;
         f32x16 o = {};
@@ -1060,18 +1115,22 @@ __global__ __launch_bounds__(NT) void stripe_bwd_dq_w(csu_stripe_args a, int spl
     // workgroup owns > 128 query rows: the 1024x1024 stages) load at the top of their iteration
     Frag<bf16> qf, gf, of;
     float lq_raw;
+    const __amdgpu_buffer_rsrc_t rs_img = buf_rsrc(img, (long)L * C3 * 2), rs_g = buf_rsrc(gimg, (long)L * C * 2),
+                                 rs_o = buf_rsrc(oimg, (long)L * C * 2), rs_lse = stat_rsrc(a, lse);
     auto load_q = [&](int q0) {
         const int qn = q0 + r;
         const bool qv = q0 < qend && qn < w.N;
         const size_t t = qv ? tok_of(w, a.reso, qn) : 0;
-        load_frag(qf, img + t * C3 + w.chq, h, qv);
-        load_frag(gf, gimg + t * C + w.chq, h, qv);
-        load_frag(of, oimg + t * C + w.chq, h, qv);
-        lq_raw = qv ? lse[stat_index(a, w, (int)t)] : 0.f;
+        load_frag_rs(qf, rs_img, t * C3 + w.chq, h, qv);
+        load_frag_rs(gf, rs_g, t * C + w.chq, h, qv);
+        load_frag_rs(of, rs_o, t * C + w.chq, h, qv);
+        lq_raw = ldf_rs(rs_lse, qv ? (unsigned)(stat_index(a, w, (int)t) * 4) : kOOB);
     };
     load_q(qbeg + 32 * wave);
-    stage_lepe_weights(branch(a, w.br), w.h, wts);
+    float lw[LW_IT];
+    lepe_weights_load(branch(a, w.br), w.h, lw);
     stage_win2(w, a.reso, img, C3, C + w.chq, img, C3, 2 * C + w.chq, npad, Ks, Vs);
+    lepe_weights_store(lw, wts);
     __syncthreads();
     ATT_STAMP(1, 1);
     const float c = a.scale * kLog2e;
@@ -1159,20 +1218,38 @@ __global__ __launch_bounds__(NT) void stripe_bwd_dkdv_w(csu_stripe_args a, int s
     // blocks (only when a workgroup owns > 128 key rows: the 1024x1024 stages) load at the top of
     // their iteration -- no second register set, so the kernel stays at <= 128 VGPRs (4 waves/SIMD)
     Frag<bf16> kf, vf;
+    const __amdgpu_buffer_rsrc_t rs_img = buf_rsrc(img, (long)L * C3 * 2);
     {
         const int kn = kbeg + 32 * wave + r;
         const bool kv = kbeg + 32 * wave < kend && kn < w.N;
         const size_t t = kv ? tok_of(w, a.reso, kn) : 0;
-        load_frag(kf, img + t * C3 + C + w.chq, h, kv);
-        load_frag(vf, img + t * C3 + 2 * C + w.chq, h, kv);
+        load_frag_rs(kf, rs_img, t * C3 + C + w.chq, h, kv);
+        load_frag_rs(vf, rs_img, t * C3 + 2 * C + w.chq, h, kv);
     }
-    stage_lepe_weights(branch(a, w.br), w.h, wts);
-    stage_win2(w, a.reso, img, C3, w.chq, gimg, C, w.chq, npad, Qs, Gs);
-    for (int i = threadIdx.x; i < npad; i += NT) {
-        const bool v = i < w.N;
-        const size_t si = stat_index(a, w, v ? tok_of(w, a.reso, i) : 0);
-        lse_s[i] = v ? lse[si] * kLog2e : INFINITY;
-        dl_s[i] = v ? delta[si] : 0.f;
+    float lw[LW_IT];
+    lepe_weights_load(branch(a, w.br), w.h, lw);
+    {   // per-query statistics of the window: loads issued with the staging loads
+        const __amdgpu_buffer_rsrc_t rs_lse = stat_rsrc(a, lse), rs_dl = stat_rsrc(a, delta);
+        constexpr int SI = WM / NT;   // WM >= npad rows, one stat per thread per pass
+        float lv[SI], dv2[SI];
+#pragma unroll
+        for (int k = 0; k < SI; ++k) {
+            const int i = threadIdx.x + k * NT;
+            const bool v = i < w.N;
+            const unsigned off = v ? (unsigned)(stat_index(a, w, tok_of(w, a.reso, i)) * 4) : kOOB;
+            lv[k] = ldf_rs(rs_lse, off);
+            dv2[k] = ldf_rs(rs_dl, off);
+        }
+        stage_win2(w, a.reso, img, C3, w.chq, gimg, C, w.chq, npad, Qs, Gs);
+        lepe_weights_store(lw, wts);
+#pragma unroll
+        for (int k = 0; k < SI; ++k) {
+            const int i = threadIdx.x + k * NT;
+            if (i < npad) {
+                lse_s[i] = i < w.N ? lv[k] * kLog2e : INFINITY;
+                dl_s[i] = dv2[k];
+            }
+        }
     }
     __syncthreads();
     ATT_STAMP(2, 1);
@@ -1185,8 +1262,8 @@ __global__ __launch_bounds__(NT) void stripe_bwd_dkdv_w(csu_stripe_args a, int s
         const int ktok = kvalid ? tok_of(w, a.reso, kn) : 0;
         if (k0 != kbeg + 32 * wave) {
             const size_t t2 = kvalid ? tok_of(w, a.reso, kn) : 0;
-            load_frag(kf, img + t2 * C3 + C + w.chq, h, kvalid);
-            load_frag(vf, img + t2 * C3 + 2 * C + w.chq, h, kvalid);
+            load_frag_rs(kf, rs_img, t2 * C3 + C + w.chq, h, kvalid);
+            load_frag_rs(vf, rs_img, t2 * C3 + 2 * C + w.chq, h, kvalid);
         }
         f32x16 dk = {}, dv = {};
         const f2 cc = {c, c};
