@@ -186,18 +186,13 @@ struct TileCfg {
 // Pipeline per 64-token step i: stage step i+1 from registers into LDS buffer (i+1)&1, issue the
 // global loads of step i+3 into the register set just freed, MFMAs of step i, one barrier -- two
 // steps of MFMA work between a load's issue and its use, 64 KB LDS (T = 128) for 2 workgroups/CU.
+// Body: logical workgroup t of one Linear (t = chunk * tiles + tile).
 template <int TN, int TK, int D>
-__global__ __launch_bounds__(NT, D > 2 ? 1 : 2) void wgrad_tile(long M, int N, int K, long rpc, int chunks,
-                                                    const bf16* __restrict__ dy, const bf16* __restrict__ x,
-                                                    float* __restrict__ dst, float* __restrict__ slab) {
+__device__ __forceinline__ void wgrad_tile_body(bf16* lds, int t, long M, int N, int K, long rpc, int chunks,
+                                                const bf16* __restrict__ dy, const bf16* __restrict__ x,
+                                                float* __restrict__ dst, float* __restrict__ slab) {
     using C = TileCfg<TN, TK>;
-    __shared__ __attribute__((aligned(16))) bf16 lds[2 * C::BUF];
-    WG_STAMP(0);
     const int nt = (N + TN - 1) / TN, kt = (K + TK - 1) / TK, tiles = nt * kt;
-    // tiles of one token chunk are consecutive logical ids -> one XCD streams the chunk once
-    // (readfirstlane: keep the tile decode in SGPRs -- a buffer resource built from a VGPR base
-    // turns every buffer load into a waterfall loop)
-    const int t = __builtin_amdgcn_readfirstlane((int)xcd_tile(blockIdx.x, gridDim.x));
     const int chunk = __builtin_amdgcn_readfirstlane(t / tiles), tile = __builtin_amdgcn_readfirstlane(t % tiles);
     const int ntile = tile / kt;
     const int n0 = ntile * TN, k0 = (tile % kt) * TK;
@@ -330,7 +325,46 @@ __global__ __launch_bounds__(NT, D > 2 ? 1 : 2) void wgrad_tile(long M, int N, i
         }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template <int TN, int TK, int D>
+__global__ __launch_bounds__(NT, D > 2 ? 1 : 2) void wgrad_tile(long M, int N, int K, long rpc, int chunks,
+                                                    const bf16* __restrict__ dy, const bf16* __restrict__ x,
+                                                    float* __restrict__ dst, float* __restrict__ slab) {
+    __shared__ __attribute__((aligned(16))) bf16 lds[2 * TileCfg<TN, TK>::BUF];
+    WG_STAMP(0);
+    // tiles of one token chunk are consecutive logical ids -> one XCD streams the chunk once
+    // (readfirstlane: keep the tile decode in SGPRs -- a buffer resource built from a VGPR base
+    // turns every buffer load into a waterfall loop)
+    const int t = __builtin_amdgcn_readfirstlane((int)xcd_tile(blockIdx.x, gridDim.x));
+    wgrad_tile_body<TN, TK, D>(lds, t, M, N, K, rpc, chunks, dy, x, dst, slab);
     WG_STAMP(3);
+}
+
+// Grouped form: the weight gradients of many Linears in ONE launch (the end-of-backward batch of
+// every deferred token-Linear weight gradient).  Item table in the kernel arguments; logical
+// workgroup -> item by a scan over the prefix sums (scalar), then the same tile body.  One launch
+// has no per-Linear underfilled rounds or tails, so each Linear can use few token chunks (small
+// partial slabs) and still keep every CU busy.
+constexpr int WGG_MAX = 48;
+struct WgGroup {
+    const bf16* dy[WGG_MAX];
+    const bf16* x[WGG_MAX];
+    float* dst[WGG_MAX];
+    float* slab[WGG_MAX];
+    int M[WGG_MAX], N[WGG_MAX], K[WGG_MAX], chunks[WGG_MAX], rpc[WGG_MAX], b0[WGG_MAX + 1];
+    int count;
+};
+
+template <int TN, int TK>
+__global__ __launch_bounds__(NT, 2) void wgrad_group(WgGroup g) {
+    __shared__ __attribute__((aligned(16))) bf16 lds[2 * TileCfg<TN, TK>::BUF];
+    const int lt = __builtin_amdgcn_readfirstlane((int)xcd_tile(blockIdx.x, gridDim.x));
+    int i = 0;
+    while (i + 1 < g.count && g.b0[i + 1] <= lt) ++i;
+    i = __builtin_amdgcn_readfirstlane(i);
+    wgrad_tile_body<TN, TK, 2>(lds, lt - g.b0[i], g.M[i], g.N[i], g.K[i], g.rpc[i], g.chunks[i], g.dy[i], g.x[i],
+                               g.dst[i], g.slab[i]);
 }
 
 // dst[n][k] = sum_c slab[tile(n, k)][c][n % TN][k % TK] (c = 0 .. chunks-1 in order), then
@@ -542,6 +576,75 @@ extern "C" int csu_linear_wgrad_deferred(long M, int N, int K, const void* dy, c
     if (ws_bytes < plan_bytes(p) || (!workspace && plan_bytes(p))) return fail(CSU_E_WORKSPACE, "linear_wgrad_deferred: workspace");
     *item = csu_wslab_item{(const float*)workspace, dw_db, N, K, p.tn, p.tk, p.chunks, 0};
     return run_bf16(p, M, N, K, (const bf16*)dy, (const bf16*)x, dw_db, workspace, as_stream(stream), true);
+}
+
+// Plan of a Linear inside a grouped launch: 128 tiles when N and K allow, else 64; token chunks so
+// that the fp32 partial slabs stay <= ~1/4 of the operand bytes (chunks <= M (N + K) / (8 N K)),
+// >= 1024 tokens per chunk.  No occupancy target: the group fills the GPU.
+static void group_plan(long M, int N, int K, int* tn, int* tk, int* chunks, long* rpc) {
+    const int t = (N % 128 == 0 && K % 128 == 0) ? 128 : 64;
+    long c = (long)((double)M * (N + K) / (8.0 * N * K) + 0.5);
+    const long maxc = M / 1024 > 0 ? M / 1024 : 1;
+    if (c > maxc) c = maxc;
+    if (c < 1) c = 1;
+    long r = ((M + c - 1) / c + TM - 1) / TM * TM;
+    c = (M + r - 1) / r;
+    *tn = *tk = t;
+    *chunks = (int)c;
+    *rpc = r;
+}
+
+extern "C" size_t csu_linear_wgrad_group_plan(long M, int N, int K, int* tn, int* tk, int* chunks) {
+    int a, b, c;
+    long r;
+    group_plan(M, N, K, &a, &b, &c, &r);
+    if (tn) *tn = a;
+    if (tk) *tk = b;
+    if (chunks) *chunks = c;
+    if (c == 1) return 0;
+    const long nt = (N + a - 1) / a, kt = (K + b - 1) / b;
+    return ((size_t)nt * kt * a * b + (size_t)nt * a) * c * sizeof(float);
+}
+
+extern "C" int csu_linear_wgrad_group(const csu_wgrad_group_item* items, int count, void* stream) {
+    if (count < 0 || (count && !items)) return fail(CSU_E_ARG, "linear_wgrad_group: bad args");
+    hipStream_t st = as_stream(stream);
+    for (int pass = 0; pass < 2; ++pass) {   // 128-tile items, then 64-tile items
+        const int T = pass == 0 ? 128 : 64;
+        WgGroup g;
+        g.count = 0;
+        g.b0[0] = 0;
+        auto flush = [&]() -> int {
+            if (!g.count) return 0;
+            if (T == 128) wgrad_group<128, 128><<<(unsigned)g.b0[g.count], NT, 0, st>>>(g);
+            else wgrad_group<64, 64><<<(unsigned)g.b0[g.count], NT, 0, st>>>(g);
+            g.count = 0;
+            return check_launch("linear_wgrad_group");
+        };
+        for (int i = 0; i < count; ++i) {
+            const csu_wgrad_group_item& it = items[i];
+            if (it.M < 1 || it.N % 8 || it.K % 8 || !it.dy || !it.x || !it.dw_db)
+                return fail(CSU_E_ARG, "linear_wgrad_group: bad item");
+            int tn, tk, c;
+            long r;
+            group_plan(it.M, it.N, it.K, &tn, &tk, &c, &r);
+            if (tn != T) continue;
+            if (c > 1 && !it.slab) return fail(CSU_E_WORKSPACE, "linear_wgrad_group: item needs a slab workspace");
+            const long tiles = (long)((it.N + tn - 1) / tn) * ((it.K + tk - 1) / tk);
+            if (g.count == WGG_MAX || (long)g.b0[g.count] + tiles * c > (1L << 30))
+                if (int e = flush()) return e;
+            const int k = g.count;
+            g.dy[k] = (const bf16*)it.dy;
+            g.x[k] = (const bf16*)it.x;
+            g.dst[k] = it.dw_db;
+            g.slab[k] = it.slab;
+            g.M[k] = (int)it.M; g.N[k] = it.N; g.K[k] = it.K; g.chunks[k] = c; g.rpc[k] = (int)r;
+            g.b0[k + 1] = g.b0[k] + (int)(tiles * c);
+            g.count = k + 1;
+        }
+        if (int e = flush()) return e;
+    }
+    return 0;
 }
 
 extern "C" int csu_wslab_reduce_batch(const csu_wslab_item* items, int count, void* stream) {

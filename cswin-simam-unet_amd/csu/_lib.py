@@ -42,6 +42,12 @@ class WslabItem(ctypes.Structure):
                 ("chunks", c_int32), ("_pad", c_int32)]
 
 
+class WgradGroupItem(ctypes.Structure):
+    """csu_wgrad_group_item (include/csu.h)."""
+    _fields_ = [("dy", c_void_p), ("x", c_void_p), ("dw_db", c_void_p), ("slab", c_void_p), ("M", ctypes.c_int64),
+                ("N", c_int32), ("K", c_int32)]
+
+
 class MlpDropout(ctypes.Structure):
     """csu_mlp_dropout (include/csu.h)."""
     _fields_ = [("rng", c_void_p), ("site_hidden", ctypes.c_uint32), ("site_out", ctypes.c_uint32), ("p", c_float),
@@ -124,6 +130,9 @@ _SIGS = {
     "csu_linear_wgrad_deferred": (ctypes.c_int, [ctypes.c_long, ctypes.c_int, ctypes.c_int, c_void_p, c_void_p, c_void_p,
                                                  c_void_p, c_size_t, ctypes.POINTER(WslabItem), c_void_p]),
     "csu_wslab_reduce_batch": (ctypes.c_int, [c_void_p, ctypes.c_int, c_void_p]),
+    "csu_linear_wgrad_group_plan": (c_size_t, [ctypes.c_long, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int),
+                                               ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
+    "csu_linear_wgrad_group": (ctypes.c_int, [c_void_p, ctypes.c_int, c_void_p]),
     "csu_grad_join": (ctypes.c_int, [ctypes.c_long, ctypes.c_int, c_void_p, ctypes.c_int, c_void_p, c_void_p, c_void_p,
                                      c_void_p]),
     "csu_bce_loss_workspace": (c_size_t, [ctypes.c_long]),

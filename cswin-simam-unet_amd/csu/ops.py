@@ -251,15 +251,43 @@ def _ln_params(ctx, rows, C, work, dgb):
     return True
 
 
-# Token-Linear weight gradients (bf16): the split-K chunk partials of every Linear whose dW / db
-# nothing reads before the end of backward (same conditions as the LayerNorm deferral) are summed
-# by ONE batched launch per 40 Linears at the end of backward (csu_wslab_reduce_batch) instead of
-# one small reduction launch each (~110 per 512x512 step).  CSU_DEFER_WGRAD=0 disables.
+# Token-Linear weight gradients (bf16) of every Linear whose dW / db nothing reads before the end of
+# backward (same conditions as the LayerNorm deferral) are computed at the end of backward: ONE
+# grouped tile launch per tile size for all of them (csu_linear_wgrad_group: no per-Linear
+# underfilled workgroup rounds, so each Linear needs only a few token chunks) and ONE batched
+# fixed-order slab sum per 40 (csu_wslab_reduce_batch).  Their dY / X operands are kept alive until
+# then.  CSU_DEFER_WGRAD=0: one launch (+ reduction) per Linear, inline.
 DEFER_WGRAD = _os.environ.get("CSU_DEFER_WGRAD", "1") == "1"
-_WG_PENDING: list = []
+GROUP_WGRAD = _os.environ.get("CSU_GROUP_WGRAD", "1") == "1"   # 0: deferred slab sums only (A/B)
+_WG_PENDING: list = []   # (WslabItem, out, workspace): reductions of tile kernels already launched
+_WG_DEFER: list = []     # (dy2, x2, out): whole weight gradients deferred to the grouped launch
 
 
 def _wgrad_flush():
+    defer, _WG_DEFER[:] = list(_WG_DEFER), []
+    if defer:
+        L = lib()
+        dev = defer[0][0].device
+        gitems = (_lib.WgradGroupItem * len(defer))()
+        keep, flops, nbytes = [], 0, 0
+        for i, (dy2, x2, out) in enumerate(defer):
+            M, N = dy2.shape
+            K = x2.shape[1]
+            tn, tk, ch = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+            nws = L.csu_linear_wgrad_group_plan(M, N, K, ctypes.byref(tn), ctypes.byref(tk), ctypes.byref(ch))
+            slab = torch.empty(nws // 4, dtype=torch.float32, device=dev) if nws else None
+            keep.append(slab)
+            it = gitems[i]
+            it.dy, it.x, it.dw_db, it.slab, it.M, it.N, it.K = dy2.data_ptr(), x2.data_ptr(), out.data_ptr(), \
+                (slab.data_ptr() if slab is not None else None), M, N, K
+            if ch.value > 1:
+                w = _lib.WslabItem()
+                w.slab, w.dst, w.N, w.K, w.tn, w.tk, w.chunks = slab.data_ptr(), out.data_ptr(), N, K, tn.value, tk.value, \
+                    ch.value
+                _WG_PENDING.append((w, out, slab))
+            flops += 2 * M * N * K
+            nbytes += M * (N + K) * 2 + (N * K + N) * 4
+        _launch("linear_wgrad", lambda: L.csu_linear_wgrad_group(gitems, len(defer), stream_ptr(dev)), flops, nbytes)
     pend, _WG_PENDING[:] = list(_WG_PENDING), []
     if not pend:
         return
@@ -587,9 +615,14 @@ def linear_wgrad(dy2: torch.Tensor, x2: torch.Tensor, out=None, work=None, defer
         # fp32: MFMA GEMM dW = dy^T x (token splits + ordered slab sum) and the column sum for db
         return gemm_f32(2, dy2.contiguous(), x2.contiguous(), N, K, M, with_asum=True)
     L = lib()
-    n = L.csu_linear_wgrad_workspace(M, N, K)
     if out is None:
         out = torch.empty(N * K + N, dtype=torch.float32, device=dy2.device)
+    if defer and dy2.dtype == torch.bfloat16 and N % 8 == 0 and K % 8 == 0 and GROUP_WGRAD and M < 2 ** 31:
+        # the whole weight gradient joins the end-of-backward grouped launch
+        _WG_DEFER.append((dy2.contiguous(), x2.contiguous(), out))
+        _queue_flush()
+        return out[:N * K].view(N, K), out[N * K:]
+    n = L.csu_linear_wgrad_workspace(M, N, K)
     if work is None:
         work = torch.empty(max(n, 16), dtype=torch.uint8, device=dy2.device)
     if defer and dy2.dtype == torch.bfloat16 and N % 8 == 0 and K % 8 == 0:

@@ -213,6 +213,21 @@ typedef struct {
 int csu_linear_wgrad_deferred(long M, int N, int K, const void* dy, const void* x, float* dw_db,
                               void* workspace, size_t ws_bytes, csu_wslab_item* item, void* stream);
 int csu_wslab_reduce_batch(const csu_wslab_item* items, int count, void* stream);
+/* Grouped weight gradients (bf16): the tile kernels of many Linears in one launch per tile size
+ * (items: HOST array, copied into kernel arguments, <= 48 items per launch).  Each item's plan
+ * (tile, token chunks) comes from csu_linear_wgrad_group_plan, which returns the slab workspace
+ * bytes the item needs (0: dw_db is written directly); items with chunks > 1 are completed by
+ * csu_wslab_reduce_batch with {slab, dw_db, N, K, tn, tk, chunks}.  M < 2^31 tokens. */
+typedef struct {
+    const void* dy;      /* (M, N) bf16 */
+    const void* x;       /* (M, K) bf16 */
+    float* dw_db;        /* N*K + N fp32 */
+    float* slab;         /* workspace of csu_linear_wgrad_group_plan's size, or NULL if 0 */
+    int64_t M;
+    int32_t N, K;
+} csu_wgrad_group_item;
+size_t csu_linear_wgrad_group_plan(long M, int N, int K, int* tn, int* tk, int* chunks);
+int csu_linear_wgrad_group(const csu_wgrad_group_item* items, int count, void* stream);
 /* Same with the plan forced (tuning / tests): bf16 output tile tn x tk (64 or 128; 0 = auto) and
  * the number of token chunks (0 = auto).  The fp32 path ignores them. */
 size_t csu_linear_wgrad_tuned_workspace(long M, int N, int K, int tn, int tk, int chunks);

@@ -40,6 +40,7 @@ def test_struct_layout_matches_header(tmp_path):
               "csu_mlp_dropout": (_lib.MlpDropout, ["rng", "site_out", "p", "row_scale", "rows_per_sample"]),
               "csu_conv_geom": (_lib.ConvGeom, ["B", "KH", "pad"]),
               "csu_wslab_item": (_lib.WslabItem, ["slab", "dst", "N", "tk", "chunks"]),
+              "csu_wgrad_group_item": (_lib.WgradGroupItem, ["dy", "x", "dw_db", "slab", "M", "N", "K"]),
               "csu_ln_param_item": (_lib.LnParamItem, ["workspace", "dbeta", "rows", "C"])}
     lines = ["#include <stdio.h>", "#include <stddef.h>", '#include "csu.h"', "int main(void) {"]
     for cname, (_, fields) in checks.items():

@@ -501,11 +501,14 @@ def test_linear_wgrad_plans(M, N, K, tn, tk, chunks):
     assert float((db.double() - ref_b).abs().max()) <= 1e-2 * max(float(ref_b.abs().max()), M ** 0.5)
 
 
-def test_side_stream_wgrad_with_gradient_accumulation():
+def test_side_stream_wgrad_with_gradient_accumulation(monkeypatch):
     """Two backward passes without zeroing (gradient accumulation: AccumulateGrad adds in place on
     the launching stream) give bitwise the same .grad with the side stream on and off: a parameter
-    that already holds a .grad takes its weight gradient inline (ops._param_safe)."""
+    that already holds a .grad takes its weight gradient inline (ops._param_safe).  (The grouped
+    end-of-backward weight gradients use another token chunking -- equal to rounding, tested in
+    test_linear_wgrad_grouped -- so they are off here.)"""
     from csu import ops
+    monkeypatch.setattr(ops, "GROUP_WGRAD", False)
     d = dev()
     torch.manual_seed(0)
     res = {}
@@ -729,10 +732,11 @@ def test_pack_nhwc_image():
 
 @pytest.mark.parametrize("M,N,K", [(16384, 1024, 256), (16384, 256, 1024), (65536, 384, 128), (4096, 512, 512),
                                    (262144, 192, 64), (100, 64, 64)])
-def test_linear_wgrad_deferred_batch(M, N, K):
-    """Deferred weight gradients (tile kernels now, ONE batched slab reduction at the end of
-    backward) are bitwise equal to the inline reduction, across several Linears in one batch."""
+def test_linear_wgrad_deferred_batch(M, N, K, monkeypatch):
+    """Deferred slab sums (tile kernels now, ONE batched reduction at the end of backward) are
+    bitwise equal to the inline reduction, across several Linears in one batch."""
     from csu import ops
+    monkeypatch.setattr(ops, "GROUP_WGRAD", False)
     d = dev()
     g = torch.Generator(device=d).manual_seed(M + N + K)
     outs = []
@@ -747,3 +751,33 @@ def test_linear_wgrad_deferred_batch(M, N, K):
     assert not ops._WG_PENDING
     for dw, db, dwd, dbd in outs:
         assert torch.equal(dw, dwd) and torch.equal(db, dbd)
+
+
+def test_linear_wgrad_grouped():
+    """Grouped end-of-backward weight gradients (one tile launch per tile size for Linears of mixed
+    shapes, then the batched slab sums) vs the per-Linear kernel (fp32 sums in another chunk order:
+    rel 1e-5) and vs themselves (bitwise reproducible)."""
+    from csu import ops
+    d = dev()
+    g = torch.Generator(device=d).manual_seed(7)
+    shapes = [(16384, 768, 256), (16384, 256, 256), (16384, 1024, 256), (16384, 256, 1024), (262144, 192, 64),
+              (65536, 384, 128), (4096, 512, 512), (100, 64, 64), (262144, 64, 64), (4096, 1536, 512)]
+    ops_in = []
+    for M, N, K in shapes:
+        dy = (torch.randn(M, N, device=d, generator=g) * 0.1).bfloat16()
+        x = torch.randn(M, K, device=d, generator=g).bfloat16()
+        ops_in.append((dy, x))
+    ref = [tuple(t.clone() for t in ops.linear_wgrad(dy, x)) for dy, x in ops_in]
+    runs = []
+    for _ in range(2):
+        res = [ops.linear_wgrad(dy, x, defer=True) for dy, x in ops_in]
+        assert len(ops._WG_DEFER) == len(shapes)
+        ops._wgrad_flush()
+        torch.cuda.synchronize()
+        assert not ops._WG_DEFER and not ops._WG_PENDING
+        runs.append([(a.clone(), b.clone()) for a, b in res])
+    for (dw, db), (gw, gb), (hw, hb) in zip(ref, runs[0], runs[1]):
+        assert torch.equal(gw, hw) and torch.equal(gb, hb)
+        for got, want in ((gw, dw), (gb, db)):
+            err = float((got.double() - want.double()).norm() / want.double().norm().clamp_min(1e-30))
+            assert err < 1e-5, err
