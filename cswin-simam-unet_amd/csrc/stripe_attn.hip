@@ -1436,7 +1436,38 @@ int lepe_nblk(const csu_stripe_args& a, int dtype) {
     return a.B * ((a.reso + rb - 1) / rb);
 }
 
-void lepe_wgrad_launch(const csu_stripe_args& a, int dtype, const void* qkv, const void* dout, float* part, hipStream_t st) {
+// many LePE weight-gradient reductions in one launch (the end-of-backward batch): item table in the
+// kernel arguments, wave w -> (item, value) by a scan over the value prefix sums
+constexpr int LPB_MAX = 32;
+struct LpBatch {
+    const float* part[LPB_MAX];
+    float* dw[LPB_MAX][2];
+    float* db[LPB_MAX][2];
+    int nblk[LPB_MAX], cb[LPB_MAX], v0[LPB_MAX + 1];
+    int count;
+};
+
+__global__ __launch_bounds__(256) void lepe_reduce_batch(LpBatch t) {
+    const int v = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (v >= t.v0[t.count]) return;
+    int i = 0;
+    while (i + 1 < t.count && t.v0[i + 1] <= v) ++i;
+    const int u = v - t.v0[i], nblk = t.nblk[i], Cb = t.cb[i];
+    const float* src = t.part[i] + (size_t)u * nblk;
+    float s = 0.f;
+    for (int j = lane; j < nblk; j += 64) s += src[j];
+    s = wave_sum(s);
+    if (lane == 0) {
+        const int br = u / (Cb * 10), r = u % (Cb * 10), c = r / 10, k = r % 10;
+        float* dw = br ? t.dw[i][1] : t.dw[i][0];
+        float* db = br ? t.db[i][1] : t.db[i][0];
+        if (k < 9) dw[c * 9 + k] = s;
+        else db[c] = s;
+    }
+}
+
+void lepe_wgrad_launch(const csu_stripe_args& a, int dtype, const void* qkv, const void* dout, float* part, hipStream_t st,
+                       bool reduce = true) {
     const int ty = lepe_tile_rows(a, dtype);
     const int nblk = lepe_nblk(a, dtype);
     if (ty) {
@@ -1451,6 +1482,7 @@ void lepe_wgrad_launch(const csu_stripe_args& a, int dtype, const void* qkv, con
     } else {
         lepe_wgrad_partial<float><<<dim3(nblk, a.nbranch), NT, 0, st>>>(a, (const float*)qkv, (const float*)dout, part);
     }
+    if (!reduce) return;
     const dim3 rgrid((a.nbranch * a.heads * HD * 10 + 3) / 4);
     lepe_wgrad_reduce<<<rgrid, 256, 0, st>>>(a, nblk, part);
 }
@@ -1463,9 +1495,53 @@ extern "C" size_t csu_stripe_attn_bwd_workspace(const csu_stripe_args* a) {
     return (size_t)a->nbranch * n * a->heads * HD * 10 * sizeof(float);
 }
 
+extern "C" int csu_stripe_attn_bwd_ex(const csu_stripe_args* a, int dtype, const void* qkv, const void* out,
+                                      const void* dout, const float* lse, float* delta, void* dqkv,
+                                      void* workspace, size_t workspace_bytes, int lepe_deferred, void* stream);
+
 extern "C" int csu_stripe_attn_bwd(const csu_stripe_args* a, int dtype, const void* qkv, const void* out,
                                    const void* dout, const float* lse, float* delta, void* dqkv,
                                    void* workspace, size_t workspace_bytes, void* stream) {
+    return csu_stripe_attn_bwd_ex(a, dtype, qkv, out, dout, lse, delta, dqkv, workspace, workspace_bytes, 0, stream);
+}
+
+extern "C" int csu_stripe_lepe_nblk(const csu_stripe_args* a, int dtype) {
+    return a ? lepe_nblk(*a, dtype) : 0;
+}
+
+extern "C" int csu_stripe_lepe_reduce_batch(const csu_lepe_reduce_item* items, int count, void* stream) {
+    if (count < 0 || (count && !items)) return fail(CSU_E_ARG, "stripe_lepe_reduce_batch: bad args");
+    LpBatch t;
+    t.count = 0;
+    t.v0[0] = 0;
+    auto flush = [&]() -> int {
+        if (!t.count) return 0;
+        lepe_reduce_batch<<<(unsigned)((t.v0[t.count] + 3) / 4), 256, 0, as_stream(stream)>>>(t);
+        t.count = 0;
+        return check_launch("stripe_lepe_reduce_batch");
+    };
+    for (int i = 0; i < count; ++i) {
+        const csu_lepe_reduce_item& it = items[i];
+        if (!it.part || it.nblk < 1 || it.channels < 1 || it.nbranch < 1 || it.nbranch > 2) return fail(CSU_E_ARG, "stripe_lepe_reduce_batch: bad item");
+        for (int b = 0; b < it.nbranch; ++b)
+            if (!it.dw[b] || !it.db[b]) return fail(CSU_E_ARG, "stripe_lepe_reduce_batch: null gradient");
+        if (t.count == LPB_MAX)
+            if (int e = flush()) return e;
+        const int k = t.count;
+        t.part[k] = it.part;
+        t.dw[k][0] = it.dw[0]; t.dw[k][1] = it.nbranch > 1 ? it.dw[1] : it.dw[0];
+        t.db[k][0] = it.db[0]; t.db[k][1] = it.nbranch > 1 ? it.db[1] : it.db[0];
+        t.nblk[k] = it.nblk;
+        t.cb[k] = it.channels;
+        t.v0[k + 1] = t.v0[k] + it.nbranch * it.channels * 10;
+        t.count = k + 1;
+    }
+    return flush();
+}
+
+extern "C" int csu_stripe_attn_bwd_ex(const csu_stripe_args* a, int dtype, const void* qkv, const void* out,
+                                      const void* dout, const float* lse, float* delta, void* dqkv,
+                                      void* workspace, size_t workspace_bytes, int lepe_deferred, void* stream) {
     if (int e = validate(a, dtype)) return e;
     if (!qkv || !out || !dout || !lse || !delta || !dqkv) return fail(CSU_E_ARG, "stripe_attn_bwd: null buffer");
     // all LePE weight-gradient pointers NULL: skip that part (csu_stripe_lepe_wgrad, e.g. on another stream)
@@ -1498,7 +1574,7 @@ extern "C" int csu_stripe_attn_bwd(const csu_stripe_args* a, int dtype, const vo
     } else {
         bwd_generic<float>(*a, grid, (const float*)qkv, (const float*)out, (const float*)dout, lse, delta, (float*)dqkv, st);
     }
-    if (do_lepe) lepe_wgrad_launch(*a, dtype, qkv, dout, part, st);
+    if (do_lepe) lepe_wgrad_launch(*a, dtype, qkv, dout, part, st, !lepe_deferred);
     return check_launch("stripe_attn_bwd");
 }
 

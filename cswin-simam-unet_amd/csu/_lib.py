@@ -48,6 +48,12 @@ class WgradGroupItem(ctypes.Structure):
                 ("N", c_int32), ("K", c_int32)]
 
 
+class LepeReduceItem(ctypes.Structure):
+    """csu_lepe_reduce_item (include/csu.h)."""
+    _fields_ = [("part", c_void_p), ("dw", c_void_p * 2), ("db", c_void_p * 2), ("nblk", c_int32), ("channels", c_int32),
+                ("nbranch", c_int32), ("_pad", c_int32)]
+
+
 class MlpDropout(ctypes.Structure):
     """csu_mlp_dropout (include/csu.h)."""
     _fields_ = [("rng", c_void_p), ("site_hidden", ctypes.c_uint32), ("site_out", ctypes.c_uint32), ("p", c_float),
@@ -130,6 +136,10 @@ _SIGS = {
     "csu_linear_wgrad_deferred": (ctypes.c_int, [ctypes.c_long, ctypes.c_int, ctypes.c_int, c_void_p, c_void_p, c_void_p,
                                                  c_void_p, c_size_t, ctypes.POINTER(WslabItem), c_void_p]),
     "csu_wslab_reduce_batch": (ctypes.c_int, [c_void_p, ctypes.c_int, c_void_p]),
+    "csu_stripe_attn_bwd_ex": (ctypes.c_int, [ctypes.POINTER(StripeArgs), ctypes.c_int, c_void_p, c_void_p, c_void_p,
+                                              c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, ctypes.c_int, c_void_p]),
+    "csu_stripe_lepe_nblk": (ctypes.c_int, [ctypes.POINTER(StripeArgs), ctypes.c_int]),
+    "csu_stripe_lepe_reduce_batch": (ctypes.c_int, [c_void_p, ctypes.c_int, c_void_p]),
     "csu_linear_wgrad_group_plan": (c_size_t, [ctypes.c_long, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int),
                                                ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
     "csu_linear_wgrad_group": (ctypes.c_int, [c_void_p, ctypes.c_int, c_void_p]),

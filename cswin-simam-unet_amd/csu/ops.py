@@ -87,6 +87,8 @@ class _StripeAttnFn(torch.autograd.Function):
                 flops, nbytes, prec=prec_of(qkv))
         ctx.geom, ctx.drop = geom, drop
         ctx.lepe_dtypes = [t.dtype for t in lepe]
+        ctx.params = tuple(lepe)   # the caller's objects (saved tensors unpack into new wrappers)
+        _note_use(*ctx.params)
         ctx.save_for_backward(qkv, out, lse, *ws, *bs)
         return out
 
@@ -101,20 +103,40 @@ class _StripeAttnFn(torch.autograd.Function):
         dqkv = torch.empty_like(qkv)
         delta = torch.empty_like(lse)
         L = lib()
-        dws = [torch.empty_like(w) for w in ws]
-        dbs = [torch.empty_like(b) for b in bs]
+        # one flat buffer, views handed to autograd: a deferred reduction keeps the BASE alive, so the
+        # returned views stay singly referenced and AccumulateGrad steals them instead of copying
+        # them before the reduction has filled them
+        sizes = [w.numel() for w in ws] + [b.numel() for b in bs]
+        flat = torch.empty(sum(sizes), dtype=torch.float32, device=qkv.device)
+        views, o = [], 0
+        for t, n in zip(list(ws) + list(bs), sizes):
+            views.append(flat[o:o + n].view(t.shape))
+            o += n
+        dws, dbs = views[:nb], views[nb:]
         a = geom.args(B, ws, bs, dws, dbs, drop=ctx.drop)
         nbytes = L.csu_stripe_attn_bwd_workspace(ctypes.byref(a))
         work = torch.empty(max(nbytes, 16), dtype=torch.uint8, device=qkv.device)
         e = qkv.element_size()
         fb, ff = _stripe_fwd_work(geom, B, e)
+        # the LePE weight-gradient partials are reduced at the end of backward with every other
+        # block's (one csu_stripe_lepe_reduce_batch launch) when nothing reads those grads earlier
+        late = DEFER_WGRAD and all(t.dtype == torch.float32 for t in dws + dbs) and _deferrable(*ctx.params)
         # algorithmic: qkv + out + dout read, dqkv written, lse read; FLOPs 2x forward (dP, dV, dQ, dK)
         bw = B * geom.reso * geom.reso * (3 * geom.C * 2 + 2 * geom.C) * e + lse.numel() * 4
-        _launch("stripe_attn_bwd", lambda: L.csu_stripe_attn_bwd(ctypes.byref(a), dtype_code(qkv), ptr(qkv), ptr(out),
-                                                                 ptr(dout), ptr(lse), ptr(delta), ptr(dqkv), ptr(work),
-                                                                 nbytes, stream_ptr(qkv.device)),
+        _launch("stripe_attn_bwd", lambda: L.csu_stripe_attn_bwd_ex(ctypes.byref(a), dtype_code(qkv), ptr(qkv), ptr(out),
+                                                                    ptr(dout), ptr(lse), ptr(delta), ptr(dqkv), ptr(work),
+                                                                    nbytes, int(late), stream_ptr(qkv.device)),
                 2 * ff, bw, prec=prec_of(qkv))
-        grads = [g.to(dt) for g, dt in zip(dws + dbs, ctx.lepe_dtypes)]
+        if late:
+            it = _lib.LepeReduceItem()
+            it.part = work.data_ptr()
+            for i in range(nb):
+                it.dw[i], it.db[i] = dws[i].data_ptr(), dbs[i].data_ptr()
+            it.nblk = L.csu_stripe_lepe_nblk(ctypes.byref(a), dtype_code(qkv))
+            it.channels, it.nbranch = geom.heads * geom.head_dim, nb
+            _LEPE_PENDING.append((it, work, flat))
+            _queue_flush()
+        grads = [g.to(dt) for g, dt in zip(views, ctx.lepe_dtypes)]
         return (dqkv, None, None, *grads)
 
 
@@ -202,12 +224,30 @@ _LN_PENDING: list = []
 _LN_QUEUED = [False]
 
 
+# forward uses per parameter since the last end-of-backward flush: a parameter used more than once in
+# one graph (weight tying) gets its gradient contributions summed by the autograd engine as they
+# arrive, i.e. read before a deferred reduction has filled them -- such parameters are never deferred
+_USES: dict = {}
+
+
+def _note_use(*params):
+    if len(_USES) > 65536:
+        _USES.clear()
+    for p in params:
+        p = _leaf(p)
+        if p is not None:
+            _USES[id(p)] = _USES.get(id(p), 0) + 1
+
+
 def _deferrable(*params) -> bool:
+    _queue_flush()   # the end-of-backward flush also resets the use counts
     for p in params:
         p = _leaf(p)
         if p is None:
             continue
         if p.grad is not None or p._backward_hooks or getattr(p, "_post_accumulate_grad_hooks", None):
+            return False
+        if _USES.get(id(p), 0) > 1:
             return False
     return True
 
@@ -236,10 +276,29 @@ def _queue_flush():
 
 
 def _end_of_backward_flush():
-    """The deferred parameter-gradient reductions of this backward pass: every LayerNorm's dgamma /
-    dbeta (one launch) and every deferred token-Linear weight-gradient slab sum (one launch per 40)."""
+    """The deferred parameter gradients of this backward pass: every LayerNorm's dgamma / dbeta (one
+    launch), every deferrable token-Linear weight gradient (grouped tile launches + batched slab
+    sums) and every LePE weight-gradient reduction (one launch per 32 blocks)."""
     _ln_param_flush()
     _wgrad_flush()
+    _lepe_flush()
+    _USES.clear()
+
+
+_LEPE_PENDING: list = []   # (LepeReduceItem, partials workspace, flat gradient buffer)
+
+
+def _lepe_flush():
+    pend, _LEPE_PENDING[:] = list(_LEPE_PENDING), []
+    if not pend:
+        return
+    dev = pend[0][1].device
+    items = (_lib.LepeReduceItem * len(pend))()
+    nbytes = 0
+    for i, (it, work, _) in enumerate(pend):
+        items[i] = it
+        nbytes += it.nbranch * it.channels * 10 * (it.nblk + 1) * 4
+    _launch("stripe_attn_bwd", lambda: lib().csu_stripe_lepe_reduce_batch(items, len(pend), stream_ptr(dev)), 0, nbytes)
 
 
 def _ln_params(ctx, rows, C, work, dgb):
@@ -324,6 +383,7 @@ class _LayerNormFn(torch.autograd.Function):
         ctx.save_for_backward(x, w, mean, rstd)
         ctx.pdtypes = (weight.dtype, bias.dtype)
         ctx.params = (weight, bias)
+        _note_use(*ctx.params)
         return y
 
     @staticmethod
@@ -387,6 +447,7 @@ class _LayerNormForkFn(torch.autograd.Function):
         ctx.save_for_backward(x, w, mean, rstd)
         ctx.pdtypes = (weight.dtype, bias.dtype)
         ctx.params = (weight, bias)
+        _note_use(*ctx.params)
         return x.view_as(x), y
 
     @staticmethod
@@ -803,6 +864,7 @@ class _LinearFn(torch.autograd.Function):
         ctx.save_for_backward(xc, wt if ctx.fast else wc)
         ctx.meta = (x.dtype, weight.dtype, None if bias is None else bias.dtype)
         ctx.params = (weight, bias)
+        _note_use(*ctx.params)
         return y
 
     @staticmethod
@@ -948,6 +1010,7 @@ class _ConcatLinearFn(torch.autograd.Function):
         ctx.save_for_backward(a2, b2, _weight_t(weight, wc))
         ctx.meta = (a.shape, b.shape, a.dtype, b.dtype, weight.dtype, bias.dtype)
         ctx.params = (weight, bias)
+        _note_use(*ctx.params)
         return y.view(*a.shape[:-1], N)
 
     @staticmethod
@@ -991,6 +1054,7 @@ class _LinearResidualFn(torch.autograd.Function):
         ctx.save_for_backward(x2, _weight_t(weight, wc))
         ctx.meta = (res.dtype, x.shape, weight.dtype, bias.dtype)
         ctx.params = (weight, bias)
+        _note_use(*ctx.params)
         return y.view(res.shape)
 
     @staticmethod
@@ -1053,6 +1117,7 @@ class _MlpResidualFn(torch.autograd.Function):
         ctx.save_for_backward(x2, h, g, _weight_t(w1, w1c), _weight_t(w2, w2c))
         ctx.meta = (res.dtype, x.shape, w1.dtype, b1.dtype, w2.dtype, b2.dtype)
         ctx.params = (w1, b1, w2, b2)
+        _note_use(*ctx.params)
         ctx.drop = drop
         return y.view(res.shape)
 
@@ -1116,6 +1181,7 @@ class _MlpFusedFn(torch.autograd.Function):
         ctx.save_for_backward(x2, w1c, b1f, w2c)
         ctx.meta = (res.dtype, x.shape, w1.dtype, b1.dtype, w2.dtype, b2.dtype)
         ctx.params = (w1, b1, w2, b2)
+        _note_use(*ctx.params)
         return y.view(res.shape)
 
     @staticmethod

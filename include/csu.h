@@ -89,6 +89,21 @@ int csu_stripe_attn_bwd(const csu_stripe_args* a, int dtype, const void* qkv, co
  * Workspace: csu_stripe_attn_bwd_workspace bytes. */
 int csu_stripe_lepe_wgrad(const csu_stripe_args* a, int dtype, const void* qkv, const void* dout,
                           void* workspace, size_t workspace_bytes, void* stream);
+/* Deferred LePE weight gradient: csu_stripe_attn_bwd_ex with lepe_deferred = 1 leaves the per-block
+ * partials in `workspace` (csu_stripe_lepe_nblk(a, dtype) blocks) instead of reducing them; one
+ * csu_stripe_lepe_reduce_batch launch later reduces many such workspaces (e.g. every block's at the
+ * end of a backward pass).  channels = heads * 32 per branch; dw [channels][9], db [channels]. */
+int csu_stripe_attn_bwd_ex(const csu_stripe_args* a, int dtype, const void* qkv, const void* out, const void* dout,
+                           const float* lse, float* delta, void* dqkv, void* workspace, size_t workspace_bytes,
+                           int lepe_deferred, void* stream);
+int csu_stripe_lepe_nblk(const csu_stripe_args* a, int dtype);
+typedef struct {
+    const float* part;
+    float* dw[2];
+    float* db[2];
+    int32_t nblk, channels, nbranch, _pad;
+} csu_lepe_reduce_item;
+int csu_stripe_lepe_reduce_batch(const csu_lepe_reduce_item* items, int count, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * LayerNorm over the last dim C of (rows, C) (nn.LayerNorm: norm1/norm2 cswin:315/347,

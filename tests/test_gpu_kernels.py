@@ -781,3 +781,45 @@ def test_linear_wgrad_grouped():
         for got, want in ((gw, dw), (gb, db)):
             err = float((got.double() - want.double()).norm() / want.double().norm().clamp_min(1e-30))
             assert err < 1e-5, err
+
+
+@pytest.mark.parametrize("reso,C,heads,sw", [(32, 256, 8, 8), (64, 128, 4, 2), (16, 512, 16, 16)])
+def test_lepe_wgrad_deferred_reduce(reso, C, heads, sw, monkeypatch):
+    """LePE weight gradients reduced at the end of backward by one batched launch (several attention
+    calls in one backward) are bitwise equal to the per-call reduction."""
+    from csu import ops
+    d = dev()
+    nb = 1 if sw == reso else 2
+    brs = [(reso, sw, 0), (sw, reso, C // 2)] if nb == 2 else [(reso, reso, 0)]
+    geom = ops.StripeGeometry(reso, C, heads // nb, brs, 32 ** -0.5)
+    g = torch.Generator(device=d).manual_seed(reso + C)
+    qkvs = [torch.randn(2, reso * reso, 3 * C, device=d, generator=g).bfloat16() for _ in range(3)]
+    gys = [torch.randn(2, reso * reso, C, device=d, generator=g).bfloat16() for _ in range(3)]
+    w0 = [[torch.randn(C // nb, 1, 3, 3, device=d, generator=g) * 0.1 for _ in range(nb)] for _ in range(3)]
+    b0 = [[torch.randn(C // nb, device=d, generator=g) * 0.1 for _ in range(nb)] for _ in range(3)]
+    res = {}
+    for late in (False, True):
+        monkeypatch.setattr(ops, "DEFER_WGRAD", late)
+        ws = [[w.clone().requires_grad_(True) for w in ww] for ww in w0]
+        bs = [[b.clone().requires_grad_(True) for b in bb] for bb in b0]
+        loss = sum((ops.stripe_attention(q, geom, w, b).float() * gy.float()).sum()
+                   for q, gy, w, b in zip(qkvs, gys, ws, bs))
+        loss.backward()
+        torch.cuda.synchronize()
+        assert not ops._LEPE_PENDING
+        res[late] = [t.grad.clone() for ww, bb in zip(ws, bs) for t in ww + bb]
+    for a, b in zip(res[False], res[True]):
+        assert torch.equal(a, b)
+    # weights shared by the three calls (the engine sums their contributions as they arrive): never
+    # deferred (use counts), same result as the inline path
+    res2 = {}
+    for late in (False, True):
+        monkeypatch.setattr(ops, "DEFER_WGRAD", late)
+        ws = [w.clone().requires_grad_(True) for w in w0[0]]
+        bs = [b.clone().requires_grad_(True) for b in b0[0]]
+        loss = sum((ops.stripe_attention(q, geom, ws, bs).float() * gy.float()).sum() for q, gy in zip(qkvs, gys))
+        loss.backward()
+        torch.cuda.synchronize()
+        res2[late] = [t.grad.clone() for t in ws + bs]
+    for a, b in zip(res2[False], res2[True]):
+        assert torch.equal(a, b)
