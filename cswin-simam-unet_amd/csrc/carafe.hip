@@ -20,6 +20,25 @@ namespace {
 constexpr int NT = 256;
 constexpr int KT = 9;   // 3x3 taps
 
+// 8 consecutive elements at byte offset `off` of a raw buffer resource (kOOB: zeros).  The 9 tap
+// gathers are issued together: a predicated `if (inside) load` made hipcc wait vmcnt(0) per tap.
+__device__ __forceinline__ void ld8_rs(__amdgpu_buffer_rsrc_t rs, unsigned off, const bf16*, float* v) {
+    const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+    bf16x8 b;
+    __builtin_memcpy(&b, &x, 16);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = (float)b[k];
+}
+__device__ __forceinline__ void ld8_rs(__amdgpu_buffer_rsrc_t rs, unsigned off, const float*, float* v) {
+    const u32x4 a = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+    const u32x4 c = __builtin_amdgcn_raw_buffer_load_b128(rs, off == kOOB ? kOOB : off + 16, 0, 0);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        v[k] = __uint_as_float(a[k]);
+        v[4 + k] = __uint_as_float(c[k]);
+    }
+}
+
 template <typename T>
 __global__ __launch_bounds__(NT) void carafe_fwd(int B, int H, int W, int C, int s, const T* __restrict__ x,
                                                  const T* __restrict__ enc, T* __restrict__ out,
@@ -52,15 +71,19 @@ __global__ __launch_bounds__(NT) void carafe_fwd(int B, int H, int W, int C, int
     }
     const float inv = 1.f / den;
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    const __amdgpu_buffer_rsrc_t rx = buf_rsrc(x, (long)B * H * W * C * (long)sizeof(T));
+    float v[KT][8];
+#pragma unroll
+    for (int t = 0; t < KT; ++t) {
+        const int yy = y + t / 3 - 1, xq = xx + t % 3 - 1;
+        const bool in = yy >= 0 && yy < H && xq >= 0 && xq < W;
+        ld8_rs(rx, in ? (unsigned)(((((b * H + yy) * W + xq) * C) + 8 * g) * (int)sizeof(T)) : kOOB, x, v[t]);
+    }
 #pragma unroll
     for (int t = 0; t < KT; ++t) {
         lg[t] *= inv;
-        const int yy = y + t / 3 - 1, xq = xx + t % 3 - 1;
-        if (yy < 0 || yy >= H || xq < 0 || xq >= W) continue;
-        float v[8];
-        load8(x + (((size_t)b * H + yy) * W + xq) * C + 8 * g, v);
 #pragma unroll
-        for (int k = 0; k < 8; ++k) acc[k] += lg[t] * v[k];
+        for (int k = 0; k < 8; ++k) acc[k] += lg[t] * v[t][k];
     }
     store8(out + (((size_t)b * sH + Y) * sW + X) * C + 8 * g, acc);
     if (g == 0) {
@@ -93,16 +116,19 @@ __global__ __launch_bounds__(NT) void carafe_bwd_enc(int B, int H, int W, int C,
     float go[8];
     load8(dout + (((size_t)b * sH + Y) * sW + X) * C + 8 * g, go);
     float dw[KT];
+    const __amdgpu_buffer_rsrc_t rx = buf_rsrc(x, (long)B * H * W * C * (long)sizeof(T));
+    float v[KT][8];
 #pragma unroll
     for (int t = 0; t < KT; ++t) {
         const int yy = y + t / 3 - 1, xq = xx + t % 3 - 1;
-        float d = 0.f;
-        if (yy >= 0 && yy < H && xq >= 0 && xq < W) {
-            float v[8];
-            load8(x + (((size_t)b * H + yy) * W + xq) * C + 8 * g, v);
+        const bool in = yy >= 0 && yy < H && xq >= 0 && xq < W;
+        ld8_rs(rx, in ? (unsigned)(((((b * H + yy) * W + xq) * C) + 8 * g) * (int)sizeof(T)) : kOOB, x, v[t]);
+    }
 #pragma unroll
-            for (int k = 0; k < 8; ++k) d += go[k] * v[k];
-        }
+    for (int t = 0; t < KT; ++t) {
+        float d = 0.f;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) d += go[k] * v[t][k];
         dw[t] = d;
     }
     // reduce over the G lanes of this pixel (aligned groups of G consecutive lanes)
@@ -225,6 +251,8 @@ unsigned blocks(long threads) { return (unsigned)((threads + NT - 1) / NT); }
 int check_args(int B, int H, int W, int C, int s) {
     if (B < 1 || H < 1 || W < 1 || s < 1 || C < 8 || C % 8 || C / 8 > 64 || ((C / 8) & (C / 8 - 1)))
         return fail(CSU_E_ARG, "carafe: need C = 8 * 2^k <= 512");
+    if ((long)B * H * W * C * 4 >= (1L << 31))   // 32-bit buffer offsets into the input (fp32 worst case)
+        return fail(CSU_E_UNSUPPORTED, "carafe: input larger than 2 GiB");
     return 0;
 }
 
