@@ -274,22 +274,32 @@ __global__ __launch_bounds__(NT) void conv_wgrad_bf16(Geo g, long Mrows, int Nco
     const int kdy = ktap / g.KW - g.p, kdx = ktap % g.KW - g.p;
     const int n = n0 + sch * 8;
     const bool nval = n + 8 <= Ncols;      // Ncols % 8 == 0 on this path
-    for (long m0 = mb; m0 < me; m0 += TM) {
-        bf16x8 va[RG], vb[RG];
+    // branch-free gathers (raw buffer loads, out-of-range offsets read 0): the next step's loads
+    // stay in flight across this step's LDS stores and MFMAs
+    const __amdgpu_buffer_rsrc_t rs_dy = buf_rsrc(dy, Mrows * Ncols * 2);
+    const __amdgpu_buffer_rsrc_t rs_x = buf_rsrc(x, (long)g.B * g.H * g.W * g.C * 2);
+    bf16x8 va[RG], vb[RG];
+    auto load = [&](long m0) {
 #pragma unroll
         for (int q = 0; q < RG; ++q) {
             const long m = m0 + 32 * q + srow;
             const bool mv = m < me;
-            va[q] = (mv && nval) ? *reinterpret_cast<const bf16x8*>(dy + m * Ncols + n) : bf16x8{};
-            const int mi = (int)m;             // M < 2^31 (check_geo)
-            const int ox = mi % g.OW, t = mi / g.OW;
-            const int oy = t % g.OH, b = t / g.OH;
+            const unsigned mi = (unsigned)(mv ? m : 0);   // M < 2^31 (check_geo)
+            const unsigned t = mi / (unsigned)g.OW, b = t / (unsigned)g.OH;
+            const int ox = (int)(mi - t * (unsigned)g.OW), oy = (int)(t - b * (unsigned)g.OH);
             const int iy = oy * g.s + kdy, ix = ox * g.s + kdx;
-            vb[q] = (kval && mv && iy >= 0 && iy < g.H && ix >= 0 && ix < g.W)
-                        ? *reinterpret_cast<const bf16x8*>(x + (((long)b * g.H + iy) * g.W + ix) * g.C + kc)
-                        : bf16x8{};
+            const unsigned offa = (mv && nval) ? (unsigned)((m * Ncols + n) * 2) : kOOB;
+            const unsigned offb = (kval && mv && iy >= 0 && iy < g.H && ix >= 0 && ix < g.W)
+                                      ? (unsigned)(((((int)b * g.H + iy) * g.W + ix) * g.C + kc) * 2) : kOOB;
+            const u32x4 a4 = __builtin_amdgcn_raw_buffer_load_b128(rs_dy, offa, 0, 0);
+            const u32x4 b4 = __builtin_amdgcn_raw_buffer_load_b128(rs_x, offb, 0, 0);
+            __builtin_memcpy(&va[q], &a4, 16);
+            __builtin_memcpy(&vb[q], &b4, 16);
         }
-        __syncthreads();
+    };
+    load(mb);
+    for (long m0 = mb; m0 < me; m0 += TM) {
+        __syncthreads();   // the previous step's MFMAs are done with the LDS tiles
 #pragma unroll
         for (int q = 0; q < RG; ++q) {
             *reinterpret_cast<bf16x8*>(At + (32 * q + srow) * RS + sch * 8) = va[q];
@@ -299,6 +309,7 @@ __global__ __launch_bounds__(NT) void conv_wgrad_bf16(Geo g, long Mrows, int Nco
                 for (int j = 0; j < 8; ++j) bsum[j] += (float)va[q][j];
         }
         __syncthreads();
+        load(m0 + TM);   // past the chunk: out-of-range offsets, zeros (never stored)
 #pragma unroll
         for (int s = 0; s < TM / 16; ++s)
             acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ctr_frag<RS>(At, wn, s, lane), ctr_frag<RS>(Bt, wk, s, lane),
@@ -714,7 +725,8 @@ extern "C" int csu_conv2d_wgrad(const csu_conv_geom* gm, int dtype, const void* 
     const bool vec = g.C % 8 == 0;
     hipStream_t st = as_stream(stream);
     if (dtype == CSU_BF16) {
-        if (vec && g.N % 8 == 0 && conv_wgrad_v2())
+        const bool small = (long)g.B * g.H * g.W * g.C * 2 < (1L << 31) && M * g.N * 2 < (1L << 31);   // 32-bit offsets
+        if (vec && g.N % 8 == 0 && small && conv_wgrad_v2())
             conv_wgrad_bf16<<<grid, NT, 0, st>>>(g, M, g.N, K, p.rpc, (const bf16*)x, (const bf16*)dy, part);
         else if (vec) conv_wgrad_kernel<bf16, true><<<grid, NT, 0, st>>>(g, M, g.N, K, p.rpc, (const bf16*)x, (const bf16*)dy, part);
         else conv_wgrad_kernel<bf16, false><<<grid, NT, 0, st>>>(g, M, g.N, K, p.rpc, (const bf16*)x, (const bf16*)dy, part);

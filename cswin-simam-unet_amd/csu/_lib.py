@@ -143,6 +143,8 @@ _SIGS = {
     "csu_linear_wgrad_group_plan": (c_size_t, [ctypes.c_long, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int),
                                                ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
     "csu_linear_wgrad_group": (ctypes.c_int, [c_void_p, ctypes.c_int, c_void_p]),
+    "csu_augment_batch": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
+                                         c_void_p]),
     "csu_grad_join": (ctypes.c_int, [ctypes.c_long, ctypes.c_int, c_void_p, ctypes.c_int, c_void_p, c_void_p, c_void_p,
                                      c_void_p]),
     "csu_bce_loss_workspace": (c_size_t, [ctypes.c_long]),

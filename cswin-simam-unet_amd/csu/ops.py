@@ -980,6 +980,31 @@ def bce_loss(prob: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
     return _BCELossFn.apply(prob, target)
 
 
+def augment_batch(images: torch.Tensor, masks: torch.Tensor, params) -> Tuple[torch.Tensor, torch.Tensor]:
+    """csu_augment_batch: uint8 (B, S, S, 3) images / (B, S, S) masks on the device, params per image
+    (hflip, vflip, clockwise quarter turns, top, left, crop_h, crop_w) -> fp32 (B, 3, S, S) and
+    (B, 1, S, S) in [0, 1] (cswin:20-87 + 166-173)."""
+    require_device(images, masks)
+    if images.dtype != torch.uint8 or masks.dtype != torch.uint8:
+        raise ValueError("augment_batch: uint8 images and masks")
+    B, S = images.shape[0], images.shape[1]
+    p = torch.tensor([list(map(int, q)) for q in params], dtype=torch.int32)
+    if tuple(p.shape) != (B, 7):
+        raise ValueError("augment_batch: one 7-value parameter tuple per image")
+    if ((p[:, 3] < 0) | (p[:, 4] < 0) | (p[:, 5] < 1) | (p[:, 6] < 1) | (p[:, 3] + p[:, 5] > S)
+            | (p[:, 4] + p[:, 6] > S) | (p[:, 2] < 0) | (p[:, 2] > 3)).any():
+        raise ValueError("augment_batch: crop outside the image or bad rotation")
+    pd = p.to(images.device, non_blocking=True)
+    img = images.contiguous()
+    msk = masks.contiguous()
+    out = torch.empty(B, 3, S, S, dtype=torch.float32, device=images.device)
+    om = torch.empty(B, 1, S, S, dtype=torch.float32, device=images.device)
+    _launch("augment", lambda: lib().csu_augment_batch(B, S, ptr(img), ptr(msk), ptr(pd), ptr(out), ptr(om),
+                                                       stream_ptr(images.device)),
+            0, B * S * S * (4 + 16), prec="f32")
+    return out, om
+
+
 def shared_cast(x: torch.Tensor, dtype: torch.dtype):
     """(xc, xc) -- the same `dtype` copy of x for two consumers (see _SharedCastFn)."""
     return _SharedCastFn.apply(x, dtype)

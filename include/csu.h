@@ -444,6 +444,17 @@ int csu_bce_loss_fwd(long n, const float* p, const float* t, float* loss, void* 
 int csu_bce_loss_bwd(long n, const float* p, const float* t, const float* dloss, float* dp, void* stream);
 int csu_pack_nhwc_bf16(int B, int C, int H, int W, int Cp, const float* x, void* y, void* stream);
 
+/* ---------------------------------------------------------------------------------------
+ * Mask-aligned batch augmentation (AugmentationTransform cswin:20-87 + the dataset's /255 and
+ * HWC -> CHW, cswin:166-173), square S x S images: img uint8 (B, S, S, 3), mask uint8 (B, S, S),
+ * params int32 (B, 7) on the device = {hflip, vflip, clockwise quarter turns 0..3, crop top,
+ * crop left, crop height, crop width} (the crop taken from the flipped/rotated image and resized
+ * back to S x S bilinearly, half-pixel centres, results rounded to uint8 like the reference's
+ * uint8 resize); out_img fp32 (B, 3, S, S) = value / 255, out_mask fp32 (B, 1, S, S).
+ * ------------------------------------------------------------------------------------- */
+int csu_augment_batch(int B, int S, const void* img, const void* mask, const int* params, float* out_img,
+                      float* out_mask, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -177,6 +177,37 @@ def f3_modules(R):
     npz("f3_modules.npz", **out)
 
 
+def f10_augment(R):
+    """The reference's AugmentationTransform (cswin:20-87) on coordinate-valued arrays with
+    recording stand-ins for cv2.flip / cv2.rotate / cv2.resize: the array handed to cv2.resize is the
+    crop, so each case pins the np.random draw order and the flip / rotate / crop geometry."""
+    import cv2
+    rec = []
+    cv2.flip = lambda a, code: a[:, ::-1] if code == 1 else a[::-1]
+    cv2.ROTATE_90_CLOCKWISE, cv2.ROTATE_180, cv2.ROTATE_90_COUNTERCLOCKWISE = 0, 1, 2
+    cv2.rotate = lambda a, code: np.rot90(a, {0: -1, 1: 2, 2: 1}[code])
+    def resize(a, size):
+        rec.append((np.ascontiguousarray(a), size))
+        return a
+    cv2.resize = resize
+    out = {}
+    cases = [(16, 16, 0.5, 0.25, (0.75, 1.0))] * 24 + [(12, 20, 0.5, 0.25, (0.75, 1.0))] * 12 + \
+            [(16, 16, 0.5, 1.0, (0.5, 1.0))] * 12
+    for ci, (h, w, fp, rp, cs) in enumerate(cases):
+        t = R.AugmentationTransform(flip_prob=fp, rotate_prob=rp, crop_scale=cs)
+        coords = np.arange(h * w, dtype=np.int32).reshape(h, w)
+        img = np.stack([coords, coords + 100000, coords + 200000], axis=-1)
+        np.random.seed(1000 + ci)
+        rec.clear()
+        t(img, coords.copy())
+        (ci_, isz), (cm_, msz) = rec
+        pre = f"c{ci}_"
+        out.update({pre + "meta": np.array([h, w, 1000 + ci]), pre + "probs": np.array([fp, rp, cs[0], cs[1]]),
+                    pre + "crop_img": ci_, pre + "crop_mask": cm_, pre + "size": np.array(isz)})
+        assert tuple(msz) == tuple(isz)
+    npz("f10_augment.npz", **out)
+
+
 def ref_model(R, cfg):
     return R.CSWinTransformer(img_size=cfg.img_size, in_chans=cfg.in_chans, num_classes=cfg.num_classes,
                               embed_dim=cfg.embed_dim, depth=cfg.depth, split_size=cfg.split_size,
@@ -292,7 +323,8 @@ if __name__ == "__main__":
     R, RU = load_reference()
     jobs = {"f1": lambda: f1_lepe(R), "f2": lambda: f2_block(R), "f3": lambda: f3_modules(R), "f4": lambda: f4_model(R),
             "f5": lambda: f5_metrics(R), "f6": lambda: f6_unet(RU), "f7": lambda: f7_contract(R, RU),
-            "f8": lambda: f8_trajectory(R), "f9": lambda: f9_dropout(R)}
+            "f8": lambda: f8_trajectory(R), "f9": lambda: f9_dropout(R),
+            "f10": lambda: f10_augment(R)}
     for k, fn in jobs.items():
         if a.only and k not in a.only.split(","):
             continue

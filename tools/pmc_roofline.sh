@@ -11,5 +11,5 @@ for C in FETCH_SIZE WRITE_SIZE; do
 done
 cd $R
 python3 tools/pmc_traffic.py $(find $O/FETCH_SIZE -name '*counter_collection.csv') $(find $O/WRITE_SIZE -name '*counter_collection.csv') \
-  "$KEY" "$MARK" "$FR" profiles/pmc_traffic.json
+  "$KEY" "$MARK" "$FR" profiles/pmc_traffic.json $BENCH_JSON
 cp profiles/pmc_traffic.json gpurun_out/pmcroof/
