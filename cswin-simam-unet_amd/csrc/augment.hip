@@ -66,11 +66,11 @@ __global__ __launch_bounds__(NT) void augment_kernel(int B, int S, const uint8_t
                 for (int c = 0; c < 3; ++c) acc[c] += w * (float)img[pix * 3 + c];
                 acc[3] += w * (float)mask[pix];
             }
-        // uint8 results as the reference's resize yields them (round half up, as cv2's fixed-point resize), then / 255
+        // uint8 results as the reference's resize yields them (round half up, as cv2's fixed-point resize), then / 255 (an IEEE division, as the reference's float32 / 255.0; not a reciprocal multiply)
 #pragma unroll
         for (int c = 0; c < 3; ++c)
-            oimg[(((long)b * 3 + c) * S + oy) * S + ox] = fminf(fmaxf(floorf(acc[c] + 0.5f), 0.f), 255.f) * (1.f / 255.f);
-        omask[((long)b * S + oy) * S + ox] = fminf(fmaxf(floorf(acc[3] + 0.5f), 0.f), 255.f) * (1.f / 255.f);
+            oimg[(((long)b * 3 + c) * S + oy) * S + ox] = fminf(fmaxf(floorf(acc[c] + 0.5f), 0.f), 255.f) / 255.f;
+        omask[((long)b * S + oy) * S + ox] = fminf(fmaxf(floorf(acc[3] + 0.5f), 0.f), 255.f) / 255.f;
     }
 }
 
