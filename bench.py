@@ -48,6 +48,9 @@ def parse():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32", "fp8"],
                     help="fp8: e4m3 Linear weights (per-row power-of-two scales), bf16 activations, fp32 accumulate "
                          "(BASELINE config 5)")
+    ap.add_argument("--model", default="cswin", choices=["cswin", "unet"],
+                    help="unet: the plain UNet of train_unet_segmentation.py (BASELINE config 1's model; Adam, "
+                         "use --img 128 --batch 8)")
     ap.add_argument("--depth", default="1,2,9,1")
     ap.add_argument("--split", default="1,2,8,8")
     ap.add_argument("--simam", action="store_true")
@@ -82,6 +85,39 @@ def _cpu_model():
     except OSError:
         pass
     return "unknown"
+
+
+def cpu_baseline_unet(args, dtype):
+    """Plain-UNet oracle (oracle/unet_ref.py, parity-pinned to the reference by F6) fwd+BCE+bwd+Adam
+    on the same per-GPU batch: 1 warm-up + 2 timed steps."""
+    from oracle import unet_ref as U
+    from oracle.recipe import recipe_from_contract
+    threads = min(16, len(os.sched_getaffinity(0)))
+    torch.set_num_threads(threads)
+    p = recipe_from_contract(U.unet_contract(), seed=0)
+    params = {k: v.requires_grad_(True) for k, v in p.items() if "running" not in k and "num_batches" not in k}
+    opt = torch.optim.Adam(params.values(), lr=1e-3, weight_decay=1e-4)
+    from csu.data import ellipse_batch
+    b = args.batch
+    x, t = ellipse_batch(np.random.default_rng(7), b, args.img)
+
+    def step():
+        opt.zero_grad()
+        with torch.autocast("cpu", dtype=torch.bfloat16, enabled=dtype == torch.bfloat16):
+            y = U.unet_forward(p, x, training=True)
+        loss = torch.nn.functional.binary_cross_entropy(y.float(), t)
+        loss.backward()
+        opt.step()
+
+    step()
+    t0 = time.perf_counter()
+    for _ in range(2):
+        step()
+    el = time.perf_counter() - t0
+    return {"value": round(2 * b / el, 4), "unit": "images/sec", "cores": threads, "kind": "port", "cpu": _cpu_model(),
+            "sample": f"2 train steps x batch {b} at {args.img}x{args.img} "
+                      f"({'bf16 autocast' if dtype == torch.bfloat16 else 'fp32'}) after 1 warm-up step, "
+                      f"oracle/unet_ref.py, {el:.1f}s, {threads} threads"}
 
 
 def cpu_baseline(args, dtype):
@@ -150,8 +186,12 @@ def main():
     split = [int(v) for v in args.split.split(",")]
     torch.manual_seed(0)
     pd = args.dropout
-    model = CSWinTransformer(img_size=args.img, depth=depth, split_size=split, simam=args.simam,
-                             drop_rate=pd, attn_drop_rate=pd, drop_path_rate=pd).to(device)
+    if args.model == "unet":
+        from csu.unet import UNet
+        model = UNet(3, 1).to(device)
+    else:
+        model = CSWinTransformer(img_size=args.img, depth=depth, split_size=split, simam=args.simam,
+                                 drop_rate=pd, attn_drop_rate=pd, drop_path_rate=pd).to(device)
     if args.dtype == "fp8":
         model.set_weight_format("fp8_e4m3")
     nparams = sum(p.numel() for p in model.parameters())
@@ -164,7 +204,11 @@ def main():
     elif dp:
         model = torch.nn.parallel.DistributedDataParallel(model, device_ids=[local], gradient_as_bucket_view=True,
                                                           static_graph=True, bucket_cap_mb=64)
-    opt = make_optimizer(model, capturable=use_graph)
+    if args.model == "unet":   # optim.Adam(lr 1e-3, weight_decay 1e-4), unet:415-420 / 486-490
+        from csu.optim import FusedAdam
+        opt = FusedAdam(model.parameters(), lr=1e-3, weight_decay=1e-4, capturable=use_graph)
+    else:
+        opt = make_optimizer(model, capturable=use_graph)
     batches = synthetic_batches(2, args.batch, args.img, device, seed=1234 + rank)
     amp = torch.bfloat16 if dtype == torch.bfloat16 else None
 
@@ -232,7 +276,7 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and (args.cpu_baseline == "on" or (args.cpu_baseline == "auto")):
         try:
-            cpu = cpu_baseline(args, dtype)
+            cpu = (cpu_baseline_unet if args.model == "unet" else cpu_baseline)(args, dtype)
         except Exception as e:  # baseline is informational; never hide the GPU number
             cpu = {"value": None, "error": repr(e)[:200]}
     if rank == 0:
@@ -240,10 +284,11 @@ def main():
                "unit": "images/sec", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
                "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
                "vs_baseline": None, "dtype": "bf16 (fp8-e4m3 weights)" if args.dtype == "fp8" else args.dtype, "data": "synthetic (ellipse masks, SURVEY §8d), random-init weights",
-               "config": {"workload": f"CSWin-UNet train step {args.img}x{args.img} depth {depth} split {split}"
-                                      f"{' +SimAM' if args.simam else ''}"
-                                      f"{f', dropout/attn_drop/drop_path {pd}' if pd > 0 else ''}, AdamW",
-                          "model": "CSWinTransformer", "params": nparams, "global_batch": args.batch * world,
+               "config": {"workload": (f"plain UNet train step {args.img}x{args.img}, Adam" if args.model == "unet" else
+                                       f"CSWin-UNet train step {args.img}x{args.img} depth {depth} split {split}"
+                                       f"{' +SimAM' if args.simam else ''}"
+                                       f"{f', dropout/attn_drop/drop_path {pd}' if pd > 0 else ''}, AdamW"),
+                          "model": "UNet" if args.model == "unet" else "CSWinTransformer", "params": nparams, "global_batch": args.batch * world,
                           "per_gpu_batch": args.batch, "img": args.img, "parallelism": f"dp{world}",
                           "dropout": pd},
                "roofline": roof, "cpu_baseline": cpu, "final_loss": round(float(loss.item()), 5),
@@ -257,6 +302,8 @@ def main():
 def _metric(args):
     """BASELINE.json's metric string for its headline workload (512x512 bf16, default depth); the
     same form naming the resolution / precision otherwise."""
+    if args.model == "unet":
+        return f"images/sec at {args.img}x{args.img} {args.dtype} (plain UNet train step)"
     if (args.img, args.dtype, args.depth, args.split, args.dropout, args.simam) == (512, "bf16", "1,2,9,1", "1,2,8,8", 0.0,
                                                                                   False):
         try:

@@ -17,6 +17,9 @@ constexpr int NT = 256;
 constexpr int PER = 16;                  // elements per thread
 constexpr long CH = (long)NT * PER;      // elements per chunk (workgroup)
 
+// L2 = false: AdamW (decoupled decay, cswin:937-941); L2 = true: Adam with L2 weight decay, the
+// plain UNet's optim.Adam(weight_decay) (unet:486-490): g += wd * param before the moments
+template <bool L2>
 __global__ __launch_bounds__(NT) void adamw_kernel(const csu_adamw_item* __restrict__ items, int count, const float* lr_dev,
                                                    float lr_host, float beta1, float beta2, float eps, float wd,
                                                    const float* step_dev, float step_host) {
@@ -30,7 +33,7 @@ __global__ __launch_bounds__(NT) void adamw_kernel(const csu_adamw_item* __restr
     const float lr = lr_dev ? *lr_dev : lr_host;
     const float step = step_dev ? *step_dev : step_host;
     const float bc1 = 1.f - powf(beta1, step), bc2 = 1.f - powf(beta2, step);
-    const float step_size = lr / bc1, bc2s = sqrtf(bc2), decay = 1.f - lr * wd;
+    const float step_size = lr / bc1, bc2s = sqrtf(bc2), decay = L2 ? 1.f : 1.f - lr * wd;
     float* p = it.param;
     const float* g = it.grad;
     float* m = it.exp_avg;
@@ -55,7 +58,8 @@ __global__ __launch_bounds__(NT) void adamw_kernel(const csu_adamw_item* __restr
         }
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            pv[j] *= decay;
+            if constexpr (L2) gv[j] = fmaf(wd, pv[j], gv[j]);
+            else pv[j] *= decay;
             mv[j] = fmaf(1.f - beta1, gv[j] - mv[j], mv[j]);   // lerp(m, g, 1 - beta1)
             vv[j] = fmaf(1.f - beta2, gv[j] * gv[j], vv[j] * beta2);
             const float denom = sqrtf(vv[j]) / bc2s + eps;
@@ -82,7 +86,16 @@ extern "C" int csu_adamw_step(const csu_adamw_item* items, int count, long total
                               float beta1, float beta2, float eps, float weight_decay, const float* step_dev, float step,
                               void* stream) {
     if (!items || count < 1 || total_chunks < 1) return fail(CSU_E_ARG, "adamw: empty item table");
-    adamw_kernel<<<(unsigned)total_chunks, NT, 0, as_stream(stream)>>>(items, count, lr_dev, lr, beta1, beta2, eps,
-                                                                       weight_decay, step_dev, step);
+    adamw_kernel<false><<<(unsigned)total_chunks, NT, 0, as_stream(stream)>>>(items, count, lr_dev, lr, beta1, beta2, eps,
+                                                                              weight_decay, step_dev, step);
     return check_launch("adamw");
+}
+
+extern "C" int csu_adam_l2_step(const csu_adamw_item* items, int count, long total_chunks, const float* lr_dev, float lr,
+                                float beta1, float beta2, float eps, float weight_decay, const float* step_dev, float step,
+                                void* stream) {
+    if (!items || count < 1 || total_chunks < 1) return fail(CSU_E_ARG, "adam_l2: empty item table");
+    adamw_kernel<true><<<(unsigned)total_chunks, NT, 0, as_stream(stream)>>>(items, count, lr_dev, lr, beta1, beta2, eps,
+                                                                             weight_decay, step_dev, step);
+    return check_launch("adam_l2");
 }

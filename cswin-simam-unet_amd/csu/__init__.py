@@ -11,11 +11,11 @@ from .simam import SimAM, simam
 from .unet import DoubleConv, Down, UNet, Up
 from .train import (bce_loss, dice_coefficient, evaluate_model, iou_score, make_optimizer, make_scheduler,
                     train_model, train_step)
-from .optim import FusedAdamW
+from .optim import FusedAdam, FusedAdamW
 from . import rng
 from .rng import manual_seed
 
 __all__ = ["UNet", "DoubleConv", "Down", "Up", "CARAFE", "CARAFE4", "CSWinBlock", "CSWinTransformer", "DropPath", "LePEAttention", "Merge_Block", "Mlp",
            "img2windows", "windows2img", "SimAM", "simam", "bce_loss", "dice_coefficient", "evaluate_model",
-           "iou_score", "make_optimizer", "make_scheduler", "train_model", "train_step", "FusedAdamW",
+           "iou_score", "make_optimizer", "make_scheduler", "train_model", "train_step", "FusedAdamW", "FusedAdam",
            "rng", "manual_seed"]

@@ -120,6 +120,8 @@ _SIGS = {
     "csu_adamw_chunk_elems": (ctypes.c_long, []),
     "csu_adamw_step": (ctypes.c_int, [c_void_p, ctypes.c_int, ctypes.c_long, c_void_p, c_float, c_float, c_float, c_float,
                                       c_float, c_void_p, c_float, c_void_p]),
+    "csu_adam_l2_step": (ctypes.c_int, [c_void_p, ctypes.c_int, ctypes.c_long, c_void_p, c_float, c_float, c_float, c_float,
+                                      c_float, c_void_p, c_float, c_void_p]),
     "csu_gemm_ex": (ctypes.c_int, [ctypes.POINTER(GemmDesc), c_void_p]),
     "csu_gemm_f32_workspace": (c_size_t, [ctypes.c_int, ctypes.c_long, ctypes.c_int, ctypes.c_long]),
     "csu_gemm_f32": (ctypes.c_int, [ctypes.c_int, ctypes.c_long, ctypes.c_int, ctypes.c_long, c_void_p, c_void_p, c_void_p,
@@ -145,6 +147,15 @@ _SIGS = {
     "csu_linear_wgrad_group": (ctypes.c_int, [c_void_p, ctypes.c_int, c_void_p]),
     "csu_augment_batch": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                          c_void_p]),
+    "csu_bn_workspace": (c_size_t, [ctypes.c_long, ctypes.c_int]),
+    "csu_bn_relu_fwd": (ctypes.c_int, [ctypes.c_long, ctypes.c_int, ctypes.c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                                       c_void_p, c_float, c_float, ctypes.c_int, ctypes.c_int, c_void_p, c_void_p,
+                                       c_void_p, c_size_t, c_void_p]),
+    "csu_bn_relu_bwd": (ctypes.c_int, [ctypes.c_long, ctypes.c_int, ctypes.c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                                       ctypes.c_int, ctypes.c_int, ctypes.c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                                       c_void_p, c_size_t, c_void_p]),
+    "csu_maxpool2_fwd": (ctypes.c_int, [ctypes.c_int] * 5 + [c_void_p, c_void_p, c_void_p]),
+    "csu_maxpool2_bwd": (ctypes.c_int, [ctypes.c_int] * 5 + [c_void_p, ctypes.c_int, c_void_p, c_void_p, c_void_p]),
     "csu_grad_join": (ctypes.c_int, [ctypes.c_long, ctypes.c_int, c_void_p, ctypes.c_int, c_void_p, c_void_p, c_void_p,
                                      c_void_p]),
     "csu_bce_loss_workspace": (c_size_t, [ctypes.c_long]),

@@ -20,6 +20,8 @@ _ITEM = np.dtype([("param", "<u8"), ("grad", "<u8"), ("exp_avg", "<u8"), ("exp_a
 
 
 class FusedAdamW(torch.optim.Optimizer):
+    _L2 = False   # FusedAdam: coupled L2 weight decay (torch.optim.Adam)
+
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2, capturable=False):
         if not 0.0 <= lr or not 0.0 <= eps or not 0.0 <= weight_decay:
             raise ValueError("invalid AdamW hyper-parameter")
@@ -129,7 +131,8 @@ class FusedAdamW(torch.optim.Optimizer):
             lr_ptr = gs["lr"].data_ptr() if group["capturable"] else None
             b1, b2 = group["betas"]
             numel = sum(it[4] for it in items)
-            launch("adamw", lambda: lib().csu_adamw_step(table.data_ptr(), n, chunks, lr_ptr, float(group["lr"]), float(b1),
+            fn = lib().csu_adam_l2_step if self._L2 else lib().csu_adamw_step
+            launch("adamw", lambda: fn(table.data_ptr(), n, chunks, lr_ptr, float(group["lr"]), float(b1),
                                                          float(b2), float(group["eps"]), float(group["weight_decay"]),
                                                          gs["step"].data_ptr(), 0.0, stream_ptr(dev)),
                    12 * numel, 28 * numel, idem=False, prec="f32")
@@ -166,3 +169,12 @@ class FusedAdamW(torch.optim.Optimizer):
         for gi, g in enumerate(self.param_groups):
             if gi in self._gstate:
                 self._gstate[gi]["lr"].fill_(g["lr"])
+
+
+class FusedAdam(FusedAdamW):
+    """Drop-in for ``torch.optim.Adam`` (coupled L2 weight decay: g += weight_decay * param before the
+    moments) on the same one-launch kernel: the plain UNet's optimizer (unet:486-490)."""
+    _L2 = True
+
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, capturable=False):
+        super().__init__(params, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, capturable=capturable)

@@ -336,6 +336,11 @@ long csu_adamw_chunk_elems(void);
 int csu_adamw_step(const csu_adamw_item* items, int count, long total_chunks, const float* lr_dev, float lr,
                    float beta1, float beta2, float eps, float weight_decay, const float* step_dev, float step,
                    void* stream);
+/* The same step with torch.optim.Adam's coupled L2 decay (the plain UNet's optimizer,
+ * unet:486-490): g += wd * param, no decoupled decay. */
+int csu_adam_l2_step(const csu_adamw_item* items, int count, long total_chunks, const float* lr_dev, float lr,
+                     float beta1, float beta2, float eps, float weight_decay, const float* step_dev, float step,
+                     void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * Dropout / DropPath (nn.Dropout cswin:190/193/512, timm DropPath cswin:344/367-368) as one
@@ -454,6 +459,30 @@ int csu_pack_nhwc_bf16(int B, int C, int H, int W, int Cp, const float* x, void*
  * ------------------------------------------------------------------------------------- */
 int csu_augment_batch(int B, int S, const void* img, const void* mask, const int* params, float* out_img,
                       float* out_mask, void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Plain-UNet BatchNorm2d (+ ReLU) and MaxPool2d(2) on NHWC rows (DoubleConv / Down,
+ * train_unet_segmentation.py unet:177-204; replaces F.batch_norm + F.relu + F.max_pool2d there).
+ * x, y: M = B*H*W rows of C channels (C % 8 == 0), dtype bf16 or f32 (y and dx in x's dtype).
+ * training: batch statistics (biased variance) -> save = (mean[C], rstd[C]); running_mean /
+ * running_var (may both be NULL) updated with `momentum` and the unbiased variance; else the
+ * running statistics normalise.  relu != 0 fuses the following ReLU (backward masks by y > 0,
+ * recomputed).  Deterministic (fixed-order reductions); workspace csu_bn_workspace(M, C) bytes.
+ * ------------------------------------------------------------------------------------- */
+size_t csu_bn_workspace(long M, int C);
+int csu_bn_relu_fwd(long M, int C, int dtype, const void* x, const float* gamma, const float* beta,
+                    float* running_mean, float* running_var, float momentum, float eps, int training, int relu,
+                    float* save, void* y, void* workspace, size_t ws_bytes, void* stream);
+/* dx, dgamma, dbeta (either may be NULL) from dy (gdtype) and the forward's save */
+int csu_bn_relu_bwd(long M, int C, int dtype, const void* x, const float* gamma, const float* beta, const float* save,
+                    int training, int relu, int gdtype, const void* dy, void* dx, float* dgamma, float* dbeta,
+                    void* workspace, size_t ws_bytes, void* stream);
+/* MaxPool2d(2) of NHWC x (B, H, W, C) -> y (B, H/2, W/2, C); the backward writes every dx element
+ * of the pooled 2x2 windows (the first maximum in torch's scan order gets dy, NaN wins); rows /
+ * columns past 2*(H/2), 2*(W/2) are not written. */
+int csu_maxpool2_fwd(int B, int H, int W, int C, int dtype, const void* x, void* y, void* stream);
+int csu_maxpool2_bwd(int B, int H, int W, int C, int dtype, const void* x, int gdtype, const void* dy, void* dx,
+                     void* stream);
 
 #ifdef __cplusplus
 }

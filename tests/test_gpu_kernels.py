@@ -623,6 +623,30 @@ def test_fused_adamw_matches_torch(capturable):
         torch.testing.assert_close(o_mine.state[q]["exp_avg_sq"], o_ref.state[p]["exp_avg_sq"], rtol=5e-5, atol=1e-9)
 
 
+
+@pytest.mark.gpu
+def test_fused_adam_l2_matches_torch():
+    """csu_adam_l2_step == torch.optim.Adam(weight_decay) (coupled L2: the plain UNet's optimizer,
+    unet:486-490) over several steps, ragged numels."""
+    from csu.optim import FusedAdam
+    d = dev()
+    g = torch.Generator(device=d).manual_seed(1)
+    shapes = [(64, 3, 3, 3), (64,), (5, 13), (4099,)]
+    ps = [torch.randn(s, device=d, generator=g) for s in shapes]
+    ref = [p.clone().requires_grad_(True) for p in ps]
+    mine = [p.clone().requires_grad_(True) for p in ps]
+    o_ref = torch.optim.Adam(ref, lr=1e-3, weight_decay=1e-4, foreach=False)
+    o_mine = FusedAdam(mine, lr=1e-3, weight_decay=1e-4)
+    for _ in range(5):
+        grads = [torch.randn(s, device=d, generator=g) for s in shapes]
+        for p, q, gr in zip(ref, mine, grads):
+            p.grad, q.grad = gr.clone(), gr.clone()
+        o_ref.step()
+        o_mine.step()
+    for p, q in zip(ref, mine):
+        torch.testing.assert_close(q.detach(), p.detach(), rtol=1e-5, atol=1e-6)
+        torch.testing.assert_close(o_mine.state[q]["exp_avg"], o_ref.state[p]["exp_avg"], rtol=1e-5, atol=1e-7)
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("B,L,C,N", [(2, 4096, 64, 64), (2, 1024, 128, 128), (3, 256, 256, 256), (1, 100, 64, 64)])
 def test_concat_linear_and_shared_cast_vs_fp64(B, L, C, N):
