@@ -25,6 +25,7 @@ constexpr int CW = 64;         // channels per block
 constexpr int LPR = CW / 8;    // lanes per row (8 channels each)
 constexpr int RG = NT / LPR;   // row groups per block (32)
 constexpr int MAXCH = 256;     // row chunks per launch
+constexpr int RIF = 8;         // rows in flight per thread
 
 struct BnGeo {
     long M;
@@ -35,7 +36,7 @@ struct BnGeo {
 BnGeo bn_geo(long M, int C) {
     BnGeo g{M, C, (C + CW - 1) / CW, 0, 0};
     long nch = (512 + g.ncb - 1) / g.ncb;                 // ~512 partial blocks per launch
-    const long maxc = (M + 4 * RG - 1) / (4 * RG);        // >= 4 row passes per block
+    const long maxc = (M + RIF * RG - 1) / (RIF * RG);    // >= one full pass of rows in flight per block
     if (nch > maxc) nch = maxc;
     if (nch > MAXCH) nch = MAXCH;
     if (nch < 1) nch = 1;
@@ -58,28 +59,20 @@ __global__ __launch_bounds__(NT) void bn_stats_partial(BnGeo g, const T* __restr
     if (cv) load8(x + c0, p);
     const long r0 = ch * g.chunk, r1 = min(g.M, r0 + g.chunk);
     if (cv) {
-        long r = r0 + rg;
-        for (; r + 3 * RG < r1; r += 4 * RG) {   // 4 rows in flight
-            float v[4][8];
+        // 8 rows in flight per thread (branch-free: rows past the chunk read a clamped row and add 0)
+        for (long r = r0 + rg; r < r1; r += RIF * RG) {
+            float v[RIF][8];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) load8(x + (r + u * RG) * g.C + c0, v[u]);
+            for (int u = 0; u < RIF; ++u) load8(x + min(r + u * RG, r1 - 1) * g.C + c0, v[u]);
 #pragma unroll
-            for (int u = 0; u < 4; ++u)
+            for (int u = 0; u < RIF; ++u) {
+                const float on = r + u * RG < r1 ? 1.f : 0.f;
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
-                    const float d = v[u][j] - p[j];
+                    const float d = (v[u][j] - p[j]) * on;
                     s1[j] += d;
                     s2[j] = fmaf(d, d, s2[j]);
                 }
-        }
-        for (; r < r1; r += RG) {
-            float v[8];
-            load8(x + r * g.C + c0, v);
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const float d = v[j] - p[j];
-                s1[j] += d;
-                s2[j] = fmaf(d, d, s2[j]);
             }
         }
     }
@@ -120,22 +113,21 @@ __global__ __launch_bounds__(NT) void bn_grad_partial(BnGeo g, const T* __restri
         }
     const long r0 = ch * g.chunk, r1 = min(g.M, r0 + g.chunk);
     if (cv) {
-        for (long r = r0 + rg; r < r1; r += 2 * RG) {
-            const bool two = r + RG < r1;
-            float xv[2][8], gv[2][8];
-            load8(x + r * g.C + c0, xv[0]);
-            load8(dy + r * g.C + c0, gv[0]);
-            if (two) {
-                load8(x + (r + RG) * g.C + c0, xv[1]);
-                load8(dy + (r + RG) * g.C + c0, gv[1]);
+        for (long r = r0 + rg; r < r1; r += RIF * RG) {   // 8 rows of x and dy in flight
+            float xv[RIF][8], gv[RIF][8];
+#pragma unroll
+            for (int u = 0; u < RIF; ++u) {
+                const long rr = min(r + u * RG, r1 - 1);
+                load8(x + rr * g.C + c0, xv[u]);
+                load8(dy + rr * g.C + c0, gv[u]);
             }
 #pragma unroll
-            for (int u = 0; u < 2; ++u) {
-                if (u == 1 && !two) break;
+            for (int u = 0; u < RIF; ++u) {
+                const bool on = r + u * RG < r1;
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
                     const float d = xv[u][j] - mu[j];
-                    const float gg = (!relu || fmaf(d, a[j], b[j]) > 0.f) ? gv[u][j] : 0.f;
+                    const float gg = (on && (!relu || fmaf(d, a[j], b[j]) > 0.f)) ? gv[u][j] : 0.f;
                     sg[j] += gg;
                     sgx[j] = fmaf(gg, d, sgx[j]);
                 }

@@ -15,10 +15,6 @@
 #include "common.hpp"
 
 namespace csu {
-
-size_t colsum_workspace(long rows, long cols, int dtype);
-int colsum_launch(long rows, long cols, int dtype, const void* in, float* out, float* ws, hipStream_t st);
-
 namespace {
 
 constexpr int NT = 256;
@@ -267,6 +263,41 @@ int check_head(int B, int H, int W, int C, int s) {
     return 0;
 }
 
+// Output-head weight folding (cswin:674-688): the CARAFE `out` 1x1 conv (O x C weight w_out, bias
+// b_out) followed by the bias-free 1-class `output` conv (w_h, O) is linear, so the fused head
+// uses u = w_out^T w_h (C) and cb = w_h . b_out.  One block; fixed-order sums.
+__global__ __launch_bounds__(NT) void head_fold_fwd(int O, int C, const float* __restrict__ w_out,
+                                                    const float* __restrict__ b_out, const float* __restrict__ w_h,
+                                                    float* __restrict__ u, float* __restrict__ cb) {
+    for (int c = threadIdx.x; c < C; c += NT) {
+        float a = 0.f;
+        for (int o = 0; o < O; ++o) a = fmaf(w_out[(long)o * C + c], w_h[o], a);
+        u[c] = a;
+    }
+    if (threadIdx.x == 0) {
+        float a = 0.f;
+        for (int o = 0; o < O; ++o) a = fmaf(w_h[o], b_out[o], a);
+        cb[0] = a;
+    }
+}
+
+// gradients of the folding from du (C) and dcb: dw_out[o][c] = w_h[o] du[c], db_out[o] = w_h[o] dcb,
+// dw_h[o] = sum_c w_out[o][c] du[c] + b_out[o] dcb
+__global__ __launch_bounds__(NT) void head_fold_bwd(int O, int C, const float* __restrict__ w_out,
+                                                    const float* __restrict__ b_out, const float* __restrict__ w_h,
+                                                    const float* __restrict__ du, const float* __restrict__ dcb,
+                                                    float* __restrict__ dw_out, float* __restrict__ db_out,
+                                                    float* __restrict__ dw_h) {
+    const float g = dcb[0];
+    for (long i = threadIdx.x; i < (long)O * C; i += NT) dw_out[i] = w_h[i / C] * du[i % C];
+    for (int o = threadIdx.x; o < O; o += NT) {
+        float a = 0.f;
+        for (int c = 0; c < C; ++c) a = fmaf(w_out[(long)o * C + c], du[c], a);
+        dw_h[o] = fmaf(b_out[o], g, a);
+        db_out[o] = w_h[o] * g;
+    }
+}
+
 }  // namespace
 }  // namespace csu
 
@@ -298,12 +329,14 @@ extern "C" size_t csu_carafe_head_bwd_workspace(int B, int H, int W, int C, int 
     return hplan(B, H, W, C).total;
 }
 
-extern "C" int csu_carafe_head_bwd(int B, int H, int W, int C, int s, int dtype, const void* x, const void* enc,
-                                   const float* z, const float* u, const float* prob, const float* dprob, void* dx,
-                                   void* denc, float* du, float* dcb, void* workspace, size_t ws_bytes, void* stream) {
+static int head_bwd(int B, int H, int W, int C, int s, int dtype, const void* x, const void* enc, const float* z,
+                    const float* u, const float* prob, const float* dprob, void* dx, void* denc, float* du, float* dcb,
+                    const csu_head_fold* fold, void* workspace, size_t ws_bytes, void* stream) {
     if (int e = check_head(B, H, W, C, s)) return e;
-    if (!x || !enc || !z || !u || !prob || !dprob || !dx || !denc || !du || !dcb)
+    if (!x || !enc || !z || !u || !prob || !dprob || !dx || !denc || !du || (!dcb && !fold))
         return fail(CSU_E_ARG, "carafe_head_bwd: null buffer");
+    if (fold && (fold->O < 1 || !fold->w_out || !fold->b_out || !fold->w_h || !fold->dw_out || !fold->db_out || !fold->dw_h))
+        return fail(CSU_E_ARG, "carafe_head_bwd: bad fold");
     const HPlan p = hplan(B, H, W, C);
     if (!workspace || ws_bytes < p.total) return fail(CSU_E_WORKSPACE, "carafe_head_bwd: workspace");
     char* ws = (char*)workspace;
@@ -327,7 +360,36 @@ extern "C" int csu_carafe_head_bwd(int B, int H, int W, int C, int s, int dtype,
     if (int e = check_launch("carafe_head_bwd")) return e;
     if (int e = colsum_launch(p.nb2, C, CSU_F32, part2, du, (float*)(ws + p.off_cs2), st)) return e;
     if (int e = colsum_launch(p.nb1, 4, CSU_F32, part1, dc4, (float*)(ws + p.off_cs1), st)) return e;
-    if (hipMemcpyAsync(dcb, dc4, sizeof(float), hipMemcpyDeviceToDevice, st) != hipSuccess)
+    if (fold) {   // the head-weight gradients straight from du and the dcb partial sum
+        head_fold_bwd<<<1, NT, 0, st>>>(fold->O, C, fold->w_out, fold->b_out, fold->w_h, du, dc4, fold->dw_out,
+                                        fold->db_out, fold->dw_h);
+        if (int e = check_launch("carafe_head_bwd: fold")) return e;
+    }
+    if (dcb && hipMemcpyAsync(dcb, dc4, sizeof(float), hipMemcpyDeviceToDevice, st) != hipSuccess)
         return fail(CSU_E_ARG, "carafe_head_bwd: copy-out failed");
     return 0;
+}
+
+extern "C" int csu_carafe_head_bwd(int B, int H, int W, int C, int s, int dtype, const void* x, const void* enc,
+                                   const float* z, const float* u, const float* prob, const float* dprob, void* dx,
+                                   void* denc, float* du, float* dcb, void* workspace, size_t ws_bytes, void* stream) {
+    if (!dcb) return fail(CSU_E_ARG, "carafe_head_bwd: null dcb");
+    return head_bwd(B, H, W, C, s, dtype, x, enc, z, u, prob, dprob, dx, denc, du, dcb, nullptr, workspace, ws_bytes,
+                    stream);
+}
+
+extern "C" int csu_carafe_head_bwd_fold(int B, int H, int W, int C, int s, int dtype, const void* x, const void* enc,
+                                        const float* z, const float* u, const float* prob, const float* dprob, void* dx,
+                                        void* denc, float* du, const csu_head_fold* fold, void* workspace,
+                                        size_t ws_bytes, void* stream) {
+    if (!fold) return fail(CSU_E_ARG, "carafe_head_bwd_fold: null fold");
+    return head_bwd(B, H, W, C, s, dtype, x, enc, z, u, prob, dprob, dx, denc, du, nullptr, fold, workspace, ws_bytes,
+                    stream);
+}
+
+extern "C" int csu_head_fold_fwd(int O, int C, const float* w_out, const float* b_out, const float* w_h, float* u,
+                                 float* cb, void* stream) {
+    if (O < 1 || C < 1 || !w_out || !b_out || !w_h || !u || !cb) return fail(CSU_E_ARG, "head_fold_fwd: bad args");
+    head_fold_fwd<<<1, NT, 0, as_stream(stream)>>>(O, C, w_out, b_out, w_h, u, cb);
+    return check_launch("head_fold_fwd");
 }

@@ -78,9 +78,15 @@ __device__ __forceinline__ float wave_max(float v) {
 // row = (reg & 3) + 8 * (reg >> 2) + 4 * h, column = lane & 31.
 __device__ __forceinline__ constexpr int crow(int reg, int h) { return (reg & 3) + 8 * (reg >> 2) + 4 * h; }
 
-// deterministic column sum out[c] = sum_r in[r][c] (reduce.hip); ws of colsum_workspace() bytes
+// deterministic column sum out[c] = sum_r in[r][c] (reduce.hip); ws of colsum_workspace() bytes.
+// map (optional): write column c of a conv weight-gradient slab ([N][khw][C] weights + [N] bias) to
+// torch's OIHW position ([N][creal][khw] + [N]; channels >= creal and columns past the bias dropped)
+struct OutMap {
+    int on, N, khw, C, creal;
+};
 size_t colsum_workspace(long rows, long cols, int dtype);
-int colsum_launch(long rows, long cols, int dtype, const void* in, float* out, float* ws, hipStream_t st);
+int colsum_launch(long rows, long cols, int dtype, const void* in, float* out, float* ws, hipStream_t st,
+                  const OutMap* map = nullptr);
 
 // XCD-aware tile order.  Workgroups are dispatched round-robin over the 8 XCDs (workgroup id i
 // runs on XCD i % 8), each with its own L2.  Remap the hardware id so that XCD x walks a

@@ -709,11 +709,12 @@ extern "C" size_t csu_conv2d_wgrad_workspace(const csu_conv_geom* gm) {
     return (size_t)p.chunks * slab * sizeof(float) + stage + colsum_workspace(p.chunks, slab, CSU_F32);
 }
 
-extern "C" int csu_conv2d_wgrad(const csu_conv_geom* gm, int dtype, const void* x, const void* dy, float* dw_db,
-                                void* workspace, size_t ws_bytes, void* stream) {
+static int conv_wgrad_impl(const csu_conv_geom* gm, int dtype, const void* x, const void* dy, int creal, float* dw_db,
+                           void* workspace, size_t ws_bytes, void* stream) {
     if (int e = check_geo(gm)) return e;
     if (!x || !dy || !dw_db) return fail(CSU_E_ARG, "conv2d_wgrad: null buffer");
     if (!workspace || ws_bytes < csu_conv2d_wgrad_workspace(gm)) return fail(CSU_E_WORKSPACE, "conv2d_wgrad: workspace");
+    if (creal > gm->C) return fail(CSU_E_ARG, "conv2d_wgrad: c_real > C");
     const Geo g = to_geo(gm);
     const long M = (long)g.B * g.OH * g.OW;
     const int K = g.KH * g.KW * g.C;
@@ -737,10 +738,25 @@ extern "C" int csu_conv2d_wgrad(const csu_conv_geom* gm, int dtype, const void* 
         return fail(CSU_E_ARG, "conv2d_wgrad: bad dtype");
     }
     if (int e = check_launch("conv2d_wgrad")) return e;
+    if (creal > 0) {   // chunk sums written straight into torch's OIHW layout (+ db)
+        const OutMap om{1, g.N, g.KH * g.KW, g.C, creal};
+        return colsum_launch(p.chunks, slab, CSU_F32, part, dw_db, part + (size_t)p.chunks * slab, st, &om);
+    }
     if (slab == used) return colsum_launch(p.chunks, slab, CSU_F32, part, dw_db, part + (size_t)p.chunks * slab, st);
     float* stage = part + (size_t)p.chunks * slab;
     if (int e = colsum_launch(p.chunks, slab, CSU_F32, part, stage, stage + slab, st)) return e;
     if (hipMemcpyAsync(dw_db, stage, used * sizeof(float), hipMemcpyDeviceToDevice, st) != hipSuccess)
         return fail(CSU_E_ARG, "conv2d_wgrad: copy-out failed");
     return 0;
+}
+
+extern "C" int csu_conv2d_wgrad(const csu_conv_geom* gm, int dtype, const void* x, const void* dy, float* dw_db,
+                                void* workspace, size_t ws_bytes, void* stream) {
+    return conv_wgrad_impl(gm, dtype, x, dy, 0, dw_db, workspace, ws_bytes, stream);
+}
+
+extern "C" int csu_conv2d_wgrad_oihw(const csu_conv_geom* gm, int dtype, const void* x, const void* dy, int c_real,
+                                     float* dw_db, void* workspace, size_t ws_bytes, void* stream) {
+    if (c_real < 1) return fail(CSU_E_ARG, "conv2d_wgrad_oihw: c_real < 1");
+    return conv_wgrad_impl(gm, dtype, x, dy, c_real, dw_db, workspace, ws_bytes, stream);
 }

@@ -33,7 +33,7 @@ __global__ __launch_bounds__(NT) void grad_join_kernel(long n8, int adt, const v
 #pragma unroll
             for (int j = 0; j < 8; ++j) va[j] += vb[j];
         }
-        store8(out + e, va);
+        if (out) store8(out + e, va);
         if (outb) store8(outb + e, va);
     }
 }
@@ -120,7 +120,8 @@ using namespace csu;
 
 extern "C" int csu_grad_join(long n, int adtype, const void* a, int bdtype, const void* b, float* out, void* out_bf16,
                              void* stream) {
-    if (n < 0 || !a || !out || (n % 8)) return fail(CSU_E_ARG, "grad_join: bad args (n must be a multiple of 8)");
+    if (n < 0 || !a || (!out && !out_bf16) || (n % 8))
+        return fail(CSU_E_ARG, "grad_join: bad args (n must be a multiple of 8, one output at least)");
     if ((adtype != CSU_BF16 && adtype != CSU_F32) || (b && bdtype != CSU_BF16 && bdtype != CSU_F32))
         return fail(CSU_E_ARG, "grad_join: bad dtype");
     if (n == 0) return 0;

@@ -11,9 +11,20 @@ namespace {
 
 constexpr int NT = 256;
 
+// destination of column c of the final sums: identity, or (m.on) the conv weight-gradient slab
+// [N][KH*KW][C] + [N] bias re-laid out as torch's OIHW [N][Creal][KH*KW] + [N] (channels >= Creal,
+// the zero padding of few-channel inputs, and slab padding columns dropped: -1)
+__device__ __forceinline__ long out_index(const OutMap& m, long c) {
+    if (!m.on) return c;
+    const long k = (long)m.khw * m.C, w = (long)m.N * k;
+    if (c >= w) return c < w + m.N ? (long)m.N * m.khw * m.creal + (c - w) : -1;
+    const long n = c / k, rr = c - n * k, t = rr / m.C, ch = rr - t * m.C;
+    return ch < m.creal ? (n * m.creal + ch) * m.khw + t : -1;
+}
+
 template <typename T>
 __global__ __launch_bounds__(NT) void colsum_pass1(long rows, long cols, int tpr, long rows_per_chunk,
-                                                   const T* __restrict__ in, float* __restrict__ out) {
+                                                   const T* __restrict__ in, float* __restrict__ out, OutMap om) {
     constexpr int V = 16 / sizeof(T);
     __shared__ float red[NT][V + 1];
     const int cl = threadIdx.x % tpr, rl = threadIdx.x / tpr, rpi = NT / tpr;
@@ -57,16 +68,24 @@ __global__ __launch_bounds__(NT) void colsum_pass1(long rows, long cols, int tpr
         for (int q = 1; q < rpi; ++q)
 #pragma unroll
             for (int j = 0; j < V; ++j) acc[j] += red[q * tpr + cl][j];
-        float* o = out + (long)blockIdx.y * cols + c0;
+        if (om.on) {   // single chunk: the final sums, re-laid out
 #pragma unroll
-        for (int j = 0; j < V; ++j)
-            if (c0 + j < cols) o[j] = acc[j];
+            for (int j = 0; j < V; ++j) {
+                const long d = c0 + j < cols ? out_index(om, c0 + j) : -1;
+                if (d >= 0) out[d] = acc[j];
+            }
+        } else {
+            float* o = out + (long)blockIdx.y * cols + c0;
+#pragma unroll
+            for (int j = 0; j < V; ++j)
+                if (c0 + j < cols) o[j] = acc[j];
+        }
     }
 }
 
 // 32 columns x 8 chunk lanes per workgroup; lanes combined in lane order in LDS
 __global__ __launch_bounds__(NT) void colsum_pass2(long cols, int nchunks, const float* __restrict__ part,
-                                                   float* __restrict__ out) {
+                                                   float* __restrict__ out, OutMap om) {
     __shared__ float red[8][33];
     const int cl = threadIdx.x & 31, lane = threadIdx.x >> 5;
     const long c = (long)blockIdx.x * 32 + cl;
@@ -84,7 +103,8 @@ __global__ __launch_bounds__(NT) void colsum_pass2(long cols, int nchunks, const
     if (lane == 0 && c < cols) {
         float s = red[0][cl];
         for (int l = 1; l < 8; ++l) s += red[l][cl];
-        out[c] = s;
+        const long d = out_index(om, c);
+        if (d >= 0) out[d] = s;
     }
 }
 
@@ -120,17 +140,21 @@ size_t colsum_workspace(long rows, long cols, int dtype) {
     return p.chunks > 1 ? (size_t)p.chunks * cols * sizeof(float) : 0;
 }
 
-int colsum_launch(long rows, long cols, int dtype, const void* in, float* out, float* ws, hipStream_t st) {
+int colsum_launch(long rows, long cols, int dtype, const void* in, float* out, float* ws, hipStream_t st,
+                  const OutMap* map) {
+    const OutMap om = map ? *map : OutMap{0, 0, 0, 0, 0};
     const int V = dtype == CSU_BF16 ? 8 : 4;
     if (cols % V) return fail(CSU_E_ARG, "colsum: cols must be a multiple of 16 bytes");
     const Plan p = plan(rows, cols, V);
     float* dst = p.chunks > 1 ? ws : out;
     const dim3 grid(p.colblocks, p.chunks);
     if (dtype == CSU_BF16)
-        colsum_pass1<bf16><<<grid, NT, 0, st>>>(rows, cols, p.tpr, p.rpc, (const bf16*)in, dst);
+        colsum_pass1<bf16><<<grid, NT, 0, st>>>(rows, cols, p.tpr, p.rpc, (const bf16*)in, dst,
+                                                             p.chunks > 1 ? OutMap{0, 0, 0, 0, 0} : om);
     else
-        colsum_pass1<float><<<grid, NT, 0, st>>>(rows, cols, p.tpr, p.rpc, (const float*)in, dst);
-    if (p.chunks > 1) colsum_pass2<<<(unsigned)((cols + 31) / 32), NT, 0, st>>>(cols, p.chunks, ws, out);
+        colsum_pass1<float><<<grid, NT, 0, st>>>(rows, cols, p.tpr, p.rpc, (const float*)in, dst,
+                                                              p.chunks > 1 ? OutMap{0, 0, 0, 0, 0} : om);
+    if (p.chunks > 1) colsum_pass2<<<(unsigned)((cols + 31) / 32), NT, 0, st>>>(cols, p.chunks, ws, out, om);
     return check_launch("colsum");
 }
 

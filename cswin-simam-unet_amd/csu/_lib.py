@@ -68,6 +68,11 @@ class GemmDesc(ctypes.Structure):
                 ("ldc", c_int32), ("out_dtype", c_int32), ("cfg", c_int32), ("_pad", c_int32)]
 
 
+class HeadFold(ctypes.Structure):
+    _fields_ = [("O", c_int32), ("w_out", c_void_p), ("b_out", c_void_p), ("w_h", c_void_p), ("dw_out", c_void_p),
+                ("db_out", c_void_p), ("dw_h", c_void_p)]
+
+
 class ConvGeom(ctypes.Structure):
     _fields_ = [(n, c_int32) for n in ("B", "H", "W", "C", "OH", "OW", "N", "KH", "KW", "stride", "pad")]
 
@@ -99,6 +104,9 @@ _SIGS = {
     "csu_carafe_head_fwd": (ctypes.c_int, [ctypes.c_int] * 6 + [c_void_p] * 7),
     "csu_carafe_head_bwd_workspace": (c_size_t, [ctypes.c_int] * 5),
     "csu_carafe_head_bwd": (ctypes.c_int, [ctypes.c_int] * 6 + [c_void_p] * 11 + [c_size_t, c_void_p]),
+    "csu_carafe_head_bwd_fold": (ctypes.c_int, [ctypes.c_int] * 6 + [c_void_p] * 9 + [ctypes.POINTER(HeadFold), c_void_p,
+                                                                                     c_size_t, c_void_p]),
+    "csu_head_fold_fwd": (ctypes.c_int, [ctypes.c_int, ctypes.c_int] + [c_void_p] * 6),
     "csu_head_fwd": (ctypes.c_int, [ctypes.c_long, ctypes.c_int, ctypes.c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
     "csu_head_bwd_workspace": (c_size_t, [ctypes.c_long, ctypes.c_int]),
     "csu_head_bwd": (ctypes.c_int, [ctypes.c_long, ctypes.c_int, ctypes.c_int] + [c_void_p] * 7 + [c_size_t, c_void_p]),
@@ -180,6 +188,8 @@ _SIGS = {
     "csu_conv2d_wgrad_workspace": (c_size_t, [ctypes.POINTER(ConvGeom)]),
     "csu_conv2d_wgrad": (ctypes.c_int, [ctypes.POINTER(ConvGeom), ctypes.c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                                         c_size_t, c_void_p]),
+    "csu_conv2d_wgrad_oihw": (ctypes.c_int, [ctypes.POINTER(ConvGeom), ctypes.c_int, c_void_p, c_void_p, ctypes.c_int,
+                                             c_void_p, c_void_p, c_size_t, c_void_p]),
 }
 
 _lib = None

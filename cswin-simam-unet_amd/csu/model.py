@@ -305,9 +305,10 @@ class CARAFE(nn.Module):
         if self.kernel_size != 3:
             raise NotImplementedError("the fused CARAFE kernel is specialised for kernel_size=3 (the reference's)")
         cd = _compute_dtype(x)
-        if x.is_cuda and x.dtype != cd:
-            # one bf16 copy for both consumers (down conv, reassembly): their two input gradients are
-            # joined in one pass (ops.grad_join) instead of autograd's add + cast
+        if x.is_cuda:
+            # one bf16 copy (or x itself when already bf16) for both consumers (down conv,
+            # reassembly): their two input gradients are joined in one pass (ops.grad_join) instead
+            # of autograd's add (+ cast)
             xd, xc = ops.shared_cast(x, cd)
         else:
             xd = xc = x.to(cd)
@@ -320,11 +321,14 @@ def carafe_sigmoid_head(up: CARAFE, w_output: torch.Tensor, x: torch.Tensor) -> 
     """sigmoid(output(up(x))) for the 1-class bias-free `output` conv (cswin:674-688) in one pass.
 
     CARAFE reassembly -> `out` 1x1 conv -> `output` 1x1 conv is linear up to the sigmoid, so it
-    collapses to u = W_out^T w_output and c = w_output . b_out (tiny fp32 autograd ops here) and the
-    fused kernel ops.carafe_head.  Returns prob (B, 1, sH, sW) fp32."""
+    collapses to u = W_out^T w_output and c = w_output . b_out (folded by csu_head_fold_fwd, its
+    backward inside the head's backward) and the fused kernel ops.carafe_head.  Returns prob
+    (B, 1, sH, sW) fp32."""
     B, L, C = x.shape
     H = W = int(math.isqrt(L))
     xc, enc = up.kernels(x)
+    if xc.is_cuda:
+        return ops.carafe_head_folded(xc, enc, up.out.weight, up.out.bias, w_output, H, W, up.up_factor)
     w_out = up.out.weight.reshape(up.out.weight.shape[0], C).float()
     w_h = w_output.reshape(-1).float()
     u = w_out.t() @ w_h

@@ -9,7 +9,7 @@ from typing import List, Optional, Sequence, Tuple
 import torch
 
 from . import _lib
-from ._lib import check, dtype_code, lib, ptr, require_device, stream_ptr
+from ._lib import CSU_F32, check, dtype_code, lib, ptr, require_device, stream_ptr
 from .ledger import esize, launch as _launch, prec_of
 
 
@@ -395,6 +395,9 @@ class _LayerNormFn(torch.autograd.Function):
         C = x.shape[-1]
         rows = x.numel() // C
         dx = torch.empty_like(x)
+        # fp32 input (the residual stream under norm / norm_up, cswin:554/602): the bf16 copy of dx
+        # the upstream Mlp / GEMM backward consumes, written by the same pass (see _bf16_of)
+        dxb = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device) if x.dtype == torch.float32 else None
         dgb = torch.empty(2 * C, dtype=torch.float32, device=x.device)   # contiguous: one reduction pass
         dg, db = dgb[:C], dgb[C:]
         L = lib()
@@ -402,10 +405,12 @@ class _LayerNormFn(torch.autograd.Function):
         work = torch.empty(max(nbytes, 16), dtype=torch.uint8, device=x.device)
         late = _ln_params(ctx, rows, C, work, dgb)
         pg, pb = (None, None) if late else (ptr(dg), ptr(db))
-        _launch("layernorm_bwd", lambda: L.csu_layernorm_bwd(rows, C, dtype_code(x), ptr(x), ptr(w), ptr(mean), ptr(rstd),
-                                                             dtype_code(dy), ptr(dy), ptr(dx), pg, pb, ptr(work),
-                                                             nbytes, stream_ptr(x.device)),
-                12 * rows * C, rows * C * (2 * esize(x) + esize(dy)) + rows * 8, prec=prec_of(x))
+        _launch("layernorm_bwd", lambda: L.csu_layernorm_bwd_ex(rows, C, dtype_code(x), ptr(x), ptr(w), ptr(mean), ptr(rstd),
+                                                                dtype_code(dy), ptr(dy), None, ptr(dx), ptr(dxb), pg, pb,
+                                                                ptr(work), nbytes, stream_ptr(x.device)),
+                12 * rows * C, rows * C * (2 * esize(x) + esize(dy) + esize(dxb)) + rows * 8, prec=prec_of(x))
+        if dxb is not None:
+            dx._csu_bf16 = dxb
         return dx, dg.to(ctx.pdtypes[0]), db.to(ctx.pdtypes[1]), None, None
 
 
@@ -604,6 +609,73 @@ class _CarafeHeadFn(torch.autograd.Function):
                 B * H * W * (4 * C + 4 * T), B * H * W * (2 * C * e + 2 * T * e + 4 + s * s * 8), prec=prec_of(x))
         udt, cdt, cshape = ctx.dtypes
         return dx, denc, du.to(udt), dcb.to(cdt).reshape(cshape), None, None, None
+
+
+class _CarafeHeadFoldedFn(torch.autograd.Function):
+    """_CarafeHeadFn with the head-weight folding (u = w_out^T w_h, cb = w_h . b_out, cswin:674-688)
+    on csu kernels too: csu_head_fold_fwd before the head, the folding's backward inside
+    csu_carafe_head_bwd_fold -- no torch GEMV / reductions / casts between them; the weight
+    gradients come out in the parameters' own shapes (AccumulateGrad steals them)."""
+
+    @staticmethod
+    def forward(ctx, x, enc, w_out, b_out, w_h, H, W, s):
+        require_device(x, enc, w_out, b_out, w_h)
+        B, C = x.shape[0], x.shape[-1]
+        O = w_out.shape[0]
+        wo = w_out.detach().float().reshape(O, C).contiguous()
+        bo = b_out.detach().float().contiguous()
+        wh = w_h.detach().float().reshape(O).contiguous()
+        uf = torch.empty(C, dtype=torch.float32, device=x.device)
+        cf = torch.empty(1, dtype=torch.float32, device=x.device)
+        _launch("head_fold", lambda: lib().csu_head_fold_fwd(O, C, ptr(wo), ptr(bo), ptr(wh), ptr(uf), ptr(cf),
+                                                             stream_ptr(x.device)),
+                2 * O * C, (O * C + 2 * O + C + 1) * 4, prec="f32")
+        x, enc = x.contiguous(), enc.to(x.dtype).contiguous()
+        if x.numel() != B * H * W * C or enc.numel() != B * H * W * 9 * s * s:
+            raise ValueError("carafe_head: x must be (B, H*W, C) and enc (B, H, W, 9 s^2)")
+        z = torch.empty(B * H * W, dtype=torch.float32, device=x.device)
+        prob = torch.empty(B, 1, s * H, s * W, dtype=torch.float32, device=x.device)
+        e, T = x.element_size(), 9 * s * s
+        _launch("carafe_head_fwd", lambda: lib().csu_carafe_head_fwd(B, H, W, C, s, dtype_code(x), ptr(x), ptr(enc), ptr(uf),
+                                                                     ptr(cf), ptr(z), ptr(prob), stream_ptr(x.device)),
+                B * H * W * (2 * C + 2 * T), B * H * W * (C * e + T * e + 4 + s * s * 4), prec=prec_of(x))
+        ctx.save_for_backward(x, enc, z, uf, prob, wo, bo, wh)
+        ctx.geo = (B, H, W, C, s)
+        ctx.pshapes = ((w_out.shape, w_out.dtype), (b_out.shape, b_out.dtype), (w_h.shape, w_h.dtype))
+        return prob
+
+    @staticmethod
+    def backward(ctx, dprob):
+        x, enc, z, uf, prob, wo, bo, wh = ctx.saved_tensors
+        B, H, W, C, s = ctx.geo
+        dprob = dprob.float().contiguous()
+        dx, denc = torch.empty_like(x), torch.empty_like(enc)
+        du = torch.empty(C, dtype=torch.float32, device=x.device)
+        (sw, tw), (sb, tb), (sh, th) = ctx.pshapes
+        dwo = torch.empty(sw, dtype=torch.float32, device=x.device)
+        dbo = torch.empty(sb, dtype=torch.float32, device=x.device)
+        dwh = torch.empty(sh, dtype=torch.float32, device=x.device)
+        fold = _lib.HeadFold()
+        fold.O, fold.w_out, fold.b_out, fold.w_h = wo.shape[0], wo.data_ptr(), bo.data_ptr(), wh.data_ptr()
+        fold.dw_out, fold.db_out, fold.dw_h = dwo.data_ptr(), dbo.data_ptr(), dwh.data_ptr()
+        L = lib()
+        n = L.csu_carafe_head_bwd_workspace(B, H, W, C, s)
+        work = torch.empty(max(n, 16), dtype=torch.uint8, device=x.device)
+        e, T = x.element_size(), 9 * s * s
+        _launch("carafe_head_bwd", lambda: L.csu_carafe_head_bwd_fold(B, H, W, C, s, dtype_code(x), ptr(x), ptr(enc),
+                                                                      ptr(z), ptr(uf), ptr(prob), ptr(dprob), ptr(dx),
+                                                                      ptr(denc), ptr(du), ctypes.byref(fold), ptr(work), n,
+                                                                      stream_ptr(x.device)),
+                B * H * W * (4 * C + 4 * T), B * H * W * (2 * C * e + 2 * T * e + 4 + s * s * 8), prec=prec_of(x))
+        return dx, denc, dwo.to(tw), dbo.to(tb), dwh.to(th), None, None, None
+
+
+def carafe_head_folded(x: torch.Tensor, enc: torch.Tensor, w_out: torch.Tensor, b_out: torch.Tensor,
+                       w_h: torch.Tensor, H: int, W: int, s: int) -> torch.Tensor:
+    """sigmoid(output(CARAFE(x).out)) with the raw head weights: w_out (O, C[, 1, 1]) / b_out (O) of
+    the CARAFE `out` conv, w_h (1, O[, 1, 1]) of the 1-class bias-free `output` conv."""
+    with torch.autocast("cuda", enabled=False):
+        return _CarafeHeadFoldedFn.apply(x, enc, w_out, b_out, w_h, H, W, s)
 
 
 def carafe_head(x: torch.Tensor, enc: torch.Tensor, u: torch.Tensor, cb: torch.Tensor, H: int, W: int,
@@ -914,8 +986,19 @@ class _SharedCastFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, dtype):
-        y = x.to(dtype)
         ctx.xdt = x.dtype
+        if x.dtype == dtype:
+            # already in the compute dtype: a fork whose two gradients are summed by one csu pass
+            # (the bf16 norm_up output feeding CARAFE4's down conv and the head, cswin:674-682)
+            return x.view_as(x), x.view_as(x)
+        if x.is_cuda and dtype == torch.bfloat16 and x.dtype == torch.float32 and x.numel() % 8 == 0:
+            xc = x.contiguous()
+            y = torch.empty(x.shape, dtype=dtype, device=x.device)
+            n = x.numel()
+            _launch("cast_bf16", lambda: lib().csu_grad_join(n, CSU_F32, ptr(xc), 0, None, None, ptr(y),
+                                                             stream_ptr(x.device)), 0, n * 6, prec="f32")
+        else:
+            y = x.to(dtype)
         return y, y.view_as(y)
 
     @staticmethod
@@ -930,6 +1013,15 @@ def grad_join(g1: Optional[torch.Tensor], g2: Optional[torch.Tensor], dtype: tor
     that also writes the bf16 copy the upstream GEMM backward consumes (attached as ``_csu_bf16``,
     see _bf16_of) -- instead of autograd's cast, add and the consumer's cast."""
     a, b = (g1, g2) if g1 is not None else (g2, None)
+    if dtype == torch.bfloat16 and a.is_cuda and a.numel() % 8 == 0 and b is not None:
+        # bf16 sum (fp32 add, one rounding -- as autograd's bf16 add) in one pass
+        a, b = a.contiguous(), b.contiguous()
+        outb = torch.empty(a.shape, dtype=torch.bfloat16, device=a.device)
+        n = a.numel()
+        _launch("grad_join", lambda: lib().csu_grad_join(n, dtype_code(a), ptr(a), dtype_code(b), ptr(b), None, ptr(outb),
+                                                         stream_ptr(a.device)),
+                n, n * (esize(a) + esize(b) + 2), prec="bf16")
+        return outb
     if dtype != torch.float32 or not a.is_cuda or a.numel() % 8:
         g = a.to(dtype)
         return g.add_(b) if b is not None else g
@@ -1446,18 +1538,21 @@ def _conv_geom(B, H, W, C, N, KH, KW, stride, pad):
     return g
 
 
-def _conv_wgrad(g, x, dy, dt):
-    """fp32 (dW in [N][KH][KW][C] order, db) of the forward conv with geometry g."""
+def _conv_wgrad(g, x, dy, dt, c_real=None):
+    """fp32 (dW, db) of the forward conv with geometry g: dW in torch's (N, c_real, KH, KW) layout,
+    written so by the kernel's final reduction (input channels >= c_real, the zero padding of a
+    few-channel input, dropped); c_real defaults to g.C."""
     L = lib()
-    out = torch.empty(g.N * g.KH * g.KW * g.C + g.N, dtype=torch.float32, device=x.device)
+    cr = g.C if c_real is None else c_real
+    out = torch.empty(g.N * g.KH * g.KW * cr + g.N, dtype=torch.float32, device=x.device)
     n = L.csu_conv2d_wgrad_workspace(ctypes.byref(g))
     work = torch.empty(max(n, 16), dtype=torch.uint8, device=x.device)
-    _launch("conv_wgrad", lambda: L.csu_conv2d_wgrad(ctypes.byref(g), dt, ptr(x), ptr(dy), ptr(out), ptr(work), n,
-                                                     stream_ptr(x.device)),
+    _launch("conv_wgrad", lambda: L.csu_conv2d_wgrad_oihw(ctypes.byref(g), dt, ptr(x), ptr(dy), cr, ptr(out), ptr(work),
+                                                          n, stream_ptr(x.device)),
             2 * g.B * g.OH * g.OW * g.N * g.KH * g.KW * g.C,
             (g.B * g.H * g.W * g.C + g.B * g.OH * g.OW * g.N) * x.element_size() + out.numel() * 4, prec=prec_of(x))
-    k = g.N * g.KH * g.KW * g.C
-    return out[:k].view(g.N, g.KH, g.KW, g.C), out[k:]
+    k = g.N * g.KH * g.KW * cr
+    return out[:k].view(g.N, cr, g.KH, g.KW), out[k:]
 
 
 def _pad_channels(C: int) -> int:
@@ -1534,9 +1629,8 @@ class _Conv2dFn(torch.autograd.Function):
             if dx.dtype != xdt:
                 dx = dx.to(xdt)
 
-        def wg():   # (dW (N, C, KH, KW) contiguous, db): also the OIHW re-layout and the unpadding
-            w_, b_ = _conv_wgrad(g, xc, dy, dtype_code(dy))
-            return w_[..., :C].permute(0, 3, 1, 2).contiguous(), b_
+        def wg():   # (dW (N, C, KH, KW) contiguous, db), OIHW and unpadded by the kernel
+            return _conv_wgrad(g, xc, dy, dtype_code(dy), C)
         if _side_ok(dy, weight.dtype, bdt if has_b else None, params=(weight, ctx.bias)):
             # on the side stream, like the token-Linear weight gradients; the returned grad is
             # contiguous fp32, so autograd steals it without a kernel on this stream
@@ -1598,7 +1692,7 @@ class _ConvTranspose2dFn(torch.autograd.Function):
                 dx = dx.to(xdt)
         dw, _ = _conv_wgrad(g, dy, xc, dtype_code(dy))   # roles swapped: "input" = dy, "output grad" = x
         db = colsum(dy.view(-1, C)).to(bdt) if has_b else None
-        return dx, dw.permute(0, 3, 1, 2).to(weight.dtype), db, None, None
+        return dx, dw.to(weight.dtype), db, None, None
 
 
 def conv_transpose2d(x_nhwc: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor],

@@ -195,6 +195,25 @@ size_t csu_carafe_head_bwd_workspace(int B, int H, int W, int C, int s);
 int csu_carafe_head_bwd(int B, int H, int W, int C, int s, int dtype, const void* x, const void* enc,
                         const float* z, const float* u, const float* prob, const float* dprob, void* dx,
                         void* denc, float* du, float* dcb, void* workspace, size_t ws_bytes, void* stream);
+/* Head-weight folding (the `out` 1x1 conv w_out (O x C) + b_out (O) and the 1-class `output` conv
+ * w_h (O), cswin:674-688): u = w_out^T w_h, cb = w_h . b_out (fp32, one launch, fixed order). */
+int csu_head_fold_fwd(int O, int C, const float* w_out, const float* b_out, const float* w_h, float* u, float* cb,
+                      void* stream);
+typedef struct {
+    int32_t O;
+    const float* w_out;  /* (O, C) */
+    const float* b_out;  /* (O) */
+    const float* w_h;    /* (O) */
+    float* dw_out;       /* (O, C) = w_h du^T */
+    float* db_out;       /* (O) = w_h dcb */
+    float* dw_h;         /* (O) = w_out du + b_out dcb */
+} csu_head_fold;
+/* csu_carafe_head_bwd with the folding's backward appended (gradients of w_out, b_out, w_h from du
+ * and dcb inside the same call; dcb itself not returned) */
+int csu_carafe_head_bwd_fold(int B, int H, int W, int C, int s, int dtype, const void* x, const void* enc,
+                             const float* z, const float* u, const float* prob, const float* dprob, void* dx,
+                             void* denc, float* du, const csu_head_fold* fold, void* workspace, size_t ws_bytes,
+                             void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * Deterministic column sum out[c] = sum_r in[r][c], fp32 accumulation (rows x cols row-major,
@@ -429,11 +448,16 @@ size_t csu_conv2d_wgrad_workspace(const csu_conv_geom* g);
 /* dw_db fp32 [N*KH*KW*C + N] = dW in [N][KH][KW][C] order, then db (sum of dy) */
 int csu_conv2d_wgrad(const csu_conv_geom* g, int dtype, const void* x, const void* dy, float* dw_db,
                      void* workspace, size_t ws_bytes, void* stream);
+/* the same gradient written in torch's Conv2d weight layout: dw_db fp32 [N*c_real*KH*KW + N] = dW
+ * (N, c_real, KH, KW) then db; input channels >= c_real (zero padding of a few-channel input) are
+ * dropped.  Same workspace. */
+int csu_conv2d_wgrad_oihw(const csu_conv_geom* g, int dtype, const void* x, const void* dy, int c_real, float* dw_db,
+                          void* workspace, size_t ws_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * Step glue (csrc/glue.hip), the elementwise passes between the kernels above:
  * grad_join: out (fp32, n) = a + b (b may be NULL), plus out_bf16 (bf16 copy, or NULL); a / b
- *   bf16 or fp32, n % 8 == 0.  The gradient of an fp32 activation cast once to bf16 for two
+ *   bf16 or fp32, n % 8 == 0; out NULL with out_bf16 set: a bf16 cast of a (+ b).  The gradient of an fp32 activation cast once to bf16 for two
  *   consumers (encoder skip cswin:530-545/568-592, CARAFE input cswin:408-432).
  * bce_loss: nn.BCELoss(reduction='mean') (cswin:935) on probabilities p and targets t (fp32, n):
  *   loss[0] = mean(-(t max(log p, -100) + (1-t) max(log(1-p), -100))), deterministic; backward
