@@ -43,18 +43,24 @@ Geo geo(int B, int L, int C) {
 
 __device__ __forceinline__ float sigm(float e) { return 1.f / (1.f + __expf(-e)); }
 
-// fixed-order sum over the 16 row groups of a block: sm[tl][k] -> row group 0's lanes
+// fixed-order sum over the 16 row groups of a block -> row group 0's lanes: the 4 row groups of a
+// wave (lane bits 4, 5) by a wavefront xor-butterfly (every lane ends with the same bits), then
+// the 4 waves through LDS in wave order.  sm: [NT / 64][QPR * K]
 template <int K>
 __device__ __forceinline__ void rowgroup_sum(float (*sm)[QPR * K], const float* v, float* out, int tl, int q) {
+    float w[K];
 #pragma unroll
-    for (int k = 0; k < K; ++k) sm[tl][q * K + k] = v[k];
+    for (int k = 0; k < K; ++k) {
+        const float a = v[k] + __shfl_xor(v[k], 16, 64);
+        w[k] = a + __shfl_xor(a, 32, 64);
+    }
+    if ((tl & 3) == 0)
+#pragma unroll
+        for (int k = 0; k < K; ++k) sm[tl >> 2][q * K + k] = w[k];
     __syncthreads();
     if (tl == 0) {
 #pragma unroll
-        for (int k = 0; k < K; ++k) out[k] = 0.f;
-        for (int j = 0; j < TPP; ++j)
-#pragma unroll
-            for (int k = 0; k < K; ++k) out[k] += sm[j][q * K + k];
+        for (int k = 0; k < K; ++k) out[k] = ((sm[0][q * K + k] + sm[1][q * K + k]) + sm[2][q * K + k]) + sm[3][q * K + k];
     }
 }
 
@@ -94,7 +100,7 @@ __device__ __forceinline__ void combine_stats(const Geo& g, const float* part, c
 // partial pivot-shifted (sum d, sum d^2) per (b, c, chunk); part[b][c][chunk][2]
 template <typename T>
 __global__ __launch_bounds__(NT) void simam_stats(Geo g, const T* __restrict__ x, float* __restrict__ part) {
-    __shared__ float sm[TPP][QPR * 8];
+    __shared__ float sm[NT / 64][QPR * 8];
     const int b = blockIdx.z, ch = blockIdx.x;
     const int q = threadIdx.x % QPR, tl = threadIdx.x / QPR;
     const int c0 = blockIdx.y * CW + 4 * q;
@@ -188,7 +194,7 @@ __global__ __launch_bounds__(NT) void simam_apply(Geo g, float lam, const T* __r
 template <typename T, typename TG>
 __global__ __launch_bounds__(NT) void simam_bwd_partial(Geo g, const T* __restrict__ x, const TG* __restrict__ dy,
                                                         const float* __restrict__ stats, float* __restrict__ part) {
-    __shared__ float sm[TPP][QPR * 8];
+    __shared__ float sm[NT / 64][QPR * 8];
     const int b = blockIdx.z, ch = blockIdx.x;
     const int q = threadIdx.x % QPR, tl = threadIdx.x / QPR;
     const int c0 = blockIdx.y * CW + 4 * q;

@@ -811,6 +811,10 @@ def gemm(a2: torch.Tensor, b: torch.Tensor, b_trans: bool, out_dtype, bias=None,
 # CSU_SIDE_WGRAD=0 disables the side stream in eager steps as well.
 # ---------------------------------------------------------------------------------------------
 SIDE_WGRAD = _os.environ.get("CSU_SIDE_WGRAD", "1") == "1"
+# diagnostics of the side-stream-in-graph nondeterminism (tools/det_graph.py): allow the side
+# stream under capture / join every side launch at once
+_SIDE_IN_GRAPH = _os.environ.get("CSU_SIDE_IN_GRAPH", "0") == "1"
+_SIDE_JOIN_NOW = _os.environ.get("CSU_SIDE_JOIN_NOW", "0") == "1"
 # CSU_PAD_CHANNELS=0: convolutions of inputs with C % 8 != 0 (the 3-channel image) without the zero
 # channel padding (per-element gathers; A/B)
 PAD_CHANNELS = _os.environ.get("CSU_PAD_CHANNELS", "1") == "1"
@@ -842,7 +846,7 @@ def _param_safe(p) -> bool:
 def _side_ok(t: torch.Tensor, *dtypes, params=()) -> bool:
     if not (SIDE_WGRAD and t.is_cuda) or any(d not in (None, torch.float32) for d in dtypes):
         return False
-    if torch.cuda.is_current_stream_capturing():
+    if torch.cuda.is_current_stream_capturing() and not _SIDE_IN_GRAPH:
         return False
     if not all(_param_safe(p) for p in params):
         return False
@@ -876,6 +880,9 @@ def _side_run(fn, *inputs):
         t.record_stream(side)
     ev = torch.cuda.Event()
     ev.record(side)
+    if _SIDE_JOIN_NOW:
+        main.wait_event(ev)
+        return out
     _SIDE_PENDING.append((main, ev))
     if not _SIDE_JOIN_QUEUED[0]:
         torch.autograd.Variable._execution_engine.queue_callback(join_side_streams)

@@ -129,12 +129,17 @@ def test_fused_adamw_checkpoint_resume_and_torch_interop(tmp_path):
         torch.testing.assert_close(pt, pa, rtol=1e-5, atol=1e-6)
 
 
-def test_graph_replays_bitwise_reproducible():
+@pytest.mark.parametrize("side_in_graph", [False, True])
+def test_graph_replays_bitwise_reproducible(side_in_graph, monkeypatch):
     """Two independent captures of the whole bf16 train step (GraphedTrainStep) replayed on the
-    same batches give bitwise-equal losses and parameters (tools/det_graph.py as a test)."""
+    same batches give bitwise-equal losses and parameters (tools/det_graph.py as a test).
+    side_in_graph: the weight gradients on the second stream INSIDE the captured graph (round-1
+    drift of ~1e-6 in this mode no longer reproduces -- DESIGN.md §6)."""
+    from csu import ops
     from csu.data import ellipse_batch
     from csu.model import CSWinTransformer
     from csu.train import GraphedTrainStep, bce_loss, make_optimizer
+    monkeypatch.setattr(ops, "_SIDE_IN_GRAPH", side_in_graph)
     d = dev()
     torch.manual_seed(0)
     m0 = CSWinTransformer(img_size=128, split_size=[1, 2, 4, 4])
