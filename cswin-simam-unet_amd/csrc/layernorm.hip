@@ -32,6 +32,27 @@ template <typename T, int V> __device__ __forceinline__ void stv(T* p, const flo
     }
 }
 
+// branch-free V-element row segments through raw buffer ops (kOOB offsets: loads read 0, stores
+// dropped) -- a predicated load / store makes hipcc wait vmcnt(0) at every branch join
+template <typename T, int V> __device__ __forceinline__ void bld(__amdgpu_buffer_rsrc_t rs, unsigned off, float* v) {
+    if constexpr (sizeof(T) == 4) {
+        buf_ld4(rs, off, v);
+        if constexpr (V == 8) buf_ld4(rs, off == kOOB ? kOOB : off + 16, v + 4);
+    } else {
+        if constexpr (V == 8) buf_ld8bf(rs, off, v);
+        else buf_ld4bf(rs, off, v);
+    }
+}
+template <typename T, int V> __device__ __forceinline__ void bst(__amdgpu_buffer_rsrc_t rs, unsigned off, const float* v) {
+    if constexpr (sizeof(T) == 4) {
+        buf_st4(rs, off, v);
+        if constexpr (V == 8) buf_st4(rs, off == kOOB ? kOOB : off + 16, v + 4);
+    } else {
+        if constexpr (V == 8) buf_st8bf(rs, off, v);
+        else buf_st4bf(rs, off, v);
+    }
+}
+
 // LPR lanes per row (C = LPR * V, 16-B or 8-B vectors), 64 / LPR rows per wave: C = 64 rows take a
 // quarter wave each instead of a whole wave of 2-4-byte accesses.
 template <int LPR> __device__ __forceinline__ float group_sum(float v) {
@@ -98,31 +119,33 @@ __global__ __launch_bounds__(NT) void ln_bwd(int rows, int C, int rows_per_block
     for (int j = 0; j < V; ++j) dg[j] = db[j] = 0.f;
     const int r0 = blockIdx.x * rows_per_block, r1 = min(rows, r0 + rows_per_block);
     // LU row groups per wave iteration, all loads issued before any math: one memory round trip
-    // per LU rows instead of per row (the loop is latency-bound, not bandwidth-bound)
+    // per LU rows instead of per row (the loop is latency-bound, not bandwidth-bound).  Raw buffer
+    // loads / stores (rows past the end: out-of-range offsets) keep them in flight together.
+    const long n = (long)rows * C;
+    const auto rs_x = buf_rsrc(x, n * sizeof(TX)), rs_g = buf_rsrc(dy, n * sizeof(TG));
+    const auto rs_r = buf_rsrc(dres, dres ? n * 4 : 0), rs_dx = buf_rsrc(dx, n * sizeof(TX));
+    const auto rs_db = buf_rsrc(dxb, dxb ? n * 2 : 0);
+    const auto rs_m = buf_rsrc(mean, (long)rows * 4), rs_s = buf_rsrc(rstd, (long)rows * 4);
     for (int rb = r0 + wave * RPW * LU; rb < r1; rb += WAVES * RPW * LU) {
         float xv[LU][V], g[LU][V], rv[LU][V], mu[LU], rs[LU];
-        bool ok[LU];
+        unsigned e0[LU];
 #pragma unroll
         for (int u = 0; u < LU; ++u) {
             const int row = rb + u * RPW + lane / LPR;
-            ok[u] = row < r1;
-            mu[u] = rs[u] = 0.f;
-#pragma unroll
-            for (int j = 0; j < V; ++j) xv[u][j] = g[u][j] = rv[u][j] = 0.f;
-            if (ok[u]) {
-                ldv<TX, V>(x + (size_t)row * C + c0, xv[u]);
-                ldv<TG, V>(dy + (size_t)row * C + c0, g[u]);
-                if (dres) ldv<float, V>(dres + (size_t)row * C + c0, rv[u]);
-                mu[u] = mean[row];
-                rs[u] = rstd[row];
-            }
+            const bool ok = row < r1;
+            e0[u] = ok ? (unsigned)((long)row * C + c0) : kOOB;   // element offset of the lane's segment
+            bld<TX, V>(rs_x, ok ? e0[u] * (unsigned)sizeof(TX) : kOOB, xv[u]);
+            bld<TG, V>(rs_g, ok ? e0[u] * (unsigned)sizeof(TG) : kOOB, g[u]);
+            bld<float, V>(rs_r, ok ? e0[u] * 4u : kOOB, rv[u]);
+            mu[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_m, ok ? (unsigned)row * 4u : kOOB, 0, 0));
+            rs[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs_s, ok ? (unsigned)row * 4u : kOOB, 0, 0));
         }
 #pragma unroll
         for (int u = 0; u < LU; ++u) {
             float s1 = 0.f, s2 = 0.f;
 #pragma unroll
             for (int j = 0; j < V; ++j) {
-                xv[u][j] = (xv[u][j] - mu[u]) * rs[u];   // xhat
+                xv[u][j] = (xv[u][j] - mu[u]) * rs[u];   // xhat (0 on rows past the end: g = 0 there)
                 const float gg = g[u][j] * gw[j];
                 s1 += gg;
                 s2 += gg * xv[u][j];
@@ -131,13 +154,12 @@ __global__ __launch_bounds__(NT) void ln_bwd(int rows, int C, int rows_per_block
             }
             s1 = group_sum<LPR>(s1) / C;
             s2 = group_sum<LPR>(s2) / C;
-            if (!ok[u]) continue;
-            const int row = rb + u * RPW + lane / LPR;
             float o[V];
 #pragma unroll
             for (int j = 0; j < V; ++j) o[j] = rs[u] * (g[u][j] * gw[j] - s1 - xv[u][j] * s2) + rv[u][j];
-            stv<TX, V>(dx + (size_t)row * C + c0, o);
-            if (dxb) stv<bf16, V>(dxb + (size_t)row * C + c0, o);
+            const unsigned e = e0[u];
+            bst<TX, V>(rs_dx, e == kOOB ? kOOB : e * (unsigned)sizeof(TX), o);
+            if (dxb) bst<bf16, V>(rs_db, e == kOOB ? kOOB : e * 2u, o);
         }
     }
     // column partials: lanes of one column inside the wave (fixed xor tree), then the waves
@@ -185,6 +207,11 @@ int ln_blocks(int rows, int rpw, int* rpb) {   // <= 512 blocks, rows per block 
 
 int check_c(int C) {
     if (C % 64 || C < 64 || C > 512) return fail(CSU_E_UNSUPPORTED, "layernorm: C must be 64..512, multiple of 64");
+    return 0;
+}
+
+int check_rows(int rows, int C) {   // 32-bit byte offsets of the raw buffer ops (fp32 rows)
+    if ((long)rows * C * 4 >= 0x7fffffffL) return fail(CSU_E_UNSUPPORTED, "layernorm: rows * C * 4 must be < 2^31");
     return 0;
 }
 
@@ -256,6 +283,7 @@ extern "C" int csu_layernorm_bwd_ex(int rows, int C, int xdtype, const void* x, 
                                     void* dx_bf16, float* dgamma, float* dbeta, void* workspace, size_t ws_bytes,
                                     void* stream) {
     if (int e = check_c(C)) return e;
+    if (int e = check_rows(rows, C)) return e;
     if (rows < 1 || !x || !gamma || !mean || !rstd || !dy || !dx || (!dgamma) != (!dbeta))
         return fail(CSU_E_ARG, "layernorm_bwd: bad args");
     if (!workspace || ws_bytes < csu_layernorm_bwd_workspace(rows, C))
