@@ -51,7 +51,14 @@ struct Win {
     int br, b, h, wy, wx, blk;  // branch, image, head, window row/col, 128-row block
     int H_sp, W_sp, N;
     int chq;                    // channel of (branch, head) inside the C-wide Q/K/V slot
+    float rW;                   // 1 / W_sp (correctly rounded): window row of a position, see wrow
 };
+
+// window row n / W_sp of window position n without an integer division (~20 VALU ops each):
+// (n + 0.5) * (1 / W_sp) truncated -- exact for n < 4096, W_sp <= 1024 (checked exhaustively)
+__device__ __forceinline__ int wrow(const Win& w, int n) {
+    return (int)__fmul_rn(__fadd_rn((float)n, 0.5f), w.rW);
+}
 
 __device__ __forceinline__ Win decode_block(const csu_stripe_args& a) {
     Win w;
@@ -59,6 +66,7 @@ __device__ __forceinline__ Win decode_block(const csu_stripe_args& a) {
     const csu_stripe_branch& g = branch(a, w.br);
     w.H_sp = g.H_sp;
     w.W_sp = g.W_sp;
+    w.rW = __frcp_rn((float)g.W_sp);
     w.N = w.H_sp * w.W_sp;
     const int nwx = a.reso / w.W_sp, nwin = (a.reso / w.H_sp) * nwx;
     const int nblk = (w.N + QR - 1) / QR;
@@ -75,7 +83,7 @@ __device__ __forceinline__ Win decode_block(const csu_stripe_args& a) {
 
 // token index (inside its image) of window-local position n
 __device__ __forceinline__ int tok_of(const Win& w, int reso, int n) {
-    const int iy = n / w.W_sp, ix = n - iy * w.W_sp;
+    const int iy = wrow(w, n), ix = n - iy * w.W_sp;
     return (w.wy * w.H_sp + iy) * reso + w.wx * w.W_sp + ix;
 }
 
@@ -184,7 +192,7 @@ __device__ __forceinline__ void stage_rows(const Win& w, int reso, const T* img,
 template <typename T>
 __device__ __forceinline__ void lepe4(const Win& w, int reso, const T* img, int rstride, int ch, int n,
                                       int c0, const float* wts, int sign, float* acc) {
-    const int iy = n / w.W_sp, ix = n - iy * w.W_sp;
+    const int iy = wrow(w, n), ix = n - iy * w.W_sp;
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[j] = sign > 0 ? wts[HD * 9 + c0 + j] : 0.f;
 #pragma unroll
@@ -214,10 +222,16 @@ __device__ __forceinline__ void lepe_weights_load(const csu_stripe_branch& g, in
         v[k] = i < HD * 9 ? a : b;
     }
 }
+// whole-window kernels: LDS layout [tap][channel] (tap 9 = bias), so the 4 weights of a channel quad
+// for one tap are one 16-B read (lepe4_lds)
 __device__ __forceinline__ void lepe_weights_store(const float* v, float* wts) {
 #pragma unroll
-    for (int k = 0; k < LW_IT; ++k)
-        if (threadIdx.x + k * NT < HD * 10) wts[threadIdx.x + k * NT] = v[k];
+    for (int k = 0; k < LW_IT; ++k) {
+        const int i = threadIdx.x + k * NT;   // source element: weight c * 9 + t, or bias HD * 9 + c
+        const int c = i / 9, t = i - c * 9;
+        if (i < HD * 9) wts[t * HD + c] = v[k];
+        else if (i < HD * 10) wts[i] = v[k];
+    }
 }
 
 __device__ __forceinline__ void stage_lepe_weights(const csu_stripe_branch& g, int h, float* wts) {
@@ -479,7 +493,7 @@ __global__ __launch_bounds__(NT) void stripe_bwd_dkdv(csu_stripe_args a, const T
     __shared__ __attribute__((aligned(16))) T Qt[HD * Cfg<T>::VSTR];
     __shared__ __attribute__((aligned(16))) T Gt[HD * Cfg<T>::VSTR];
     __shared__ float lse_s[KC], dl_s[KC];
-    __shared__ float wts[HD * 10];
+    __shared__ __attribute__((aligned(16))) float wts[HD * 10];
     __shared__ __attribute__((aligned(16))) unsigned char dtbl[4][128];
 
     const Win w = decode_block(a);
@@ -938,20 +952,23 @@ __device__ __forceinline__ void stage_win2(const Win& w, int reso, const bf16* i
     }
 }
 
-// LePE of window position n, channels c0..c0+3, from a swizzled LDS image
+// LePE of window position n, channels c0..c0+3, from a swizzled LDS image; wts in the [tap][channel]
+// layout of lepe_weights_store
 __device__ __forceinline__ void lepe4_lds(const Win& w, const bf16* img, int n, int c0, const float* wts, int sign,
                                           float* acc) {
-    const int iy = n / w.W_sp, ix = n - iy * w.W_sp;
+    const int iy = wrow(w, n), ix = n - iy * w.W_sp;
+    const f32x4 bias = *reinterpret_cast<const f32x4*>(wts + HD * 9 + c0);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[j] = sign > 0 ? wts[HD * 9 + c0 + j] : 0.f;
+    for (int j = 0; j < 4; ++j) acc[j] = sign > 0 ? bias[j] : 0.f;
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
         const int dy = sign * (t / 3 - 1), dx = sign * (t % 3 - 1);
         const int y = iy + dy, x = ix + dx;
         if (y < 0 || y >= w.H_sp || x < 0 || x >= w.W_sp) continue;
         const bf16x4 v = *reinterpret_cast<const bf16x4*>(img + swz(y * w.W_sp + x, c0));
+        const f32x4 wt = *reinterpret_cast<const f32x4*>(wts + t * HD + c0);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[j] += wts[(c0 + j) * 9 + t] * (float)v[j];
+        for (int j = 0; j < 4; ++j) acc[j] += wt[j] * (float)v[j];
     }
 }
 
@@ -961,6 +978,7 @@ __device__ __forceinline__ Win decode_w(const csu_stripe_args& a, int split) {
     const csu_stripe_branch& g = branch(a, w.br);
     w.H_sp = g.H_sp;
     w.W_sp = g.W_sp;
+    w.rW = __frcp_rn((float)g.W_sp);
     w.N = w.H_sp * w.W_sp;
     const int nwx = a.reso / w.W_sp, nwin = (a.reso / w.H_sp) * nwx;
     // XCD-aware order: the split partners of a window-head (consecutive logical ids) run on one
@@ -981,7 +999,7 @@ __global__ __launch_bounds__(NT) void stripe_fwd_w(csu_stripe_args a, int split,
                                                    bf16* __restrict__ out, float* __restrict__ lse) {
     __shared__ __attribute__((aligned(16))) bf16 Ks[WM * HD];
     __shared__ __attribute__((aligned(16))) bf16 Vs[WM * HD];
-    __shared__ float wts[HD * 10];
+    __shared__ __attribute__((aligned(16))) float wts[HD * 10];
     ATT_STAMP(0, 0);
     const Win w = decode_w(a, split);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1098,7 +1116,7 @@ __global__ __launch_bounds__(NT) void stripe_bwd_dq_w(csu_stripe_args a, int spl
                                                       bf16* __restrict__ dqkv) {
     __shared__ __attribute__((aligned(16))) bf16 Ks[WM * HD];
     __shared__ __attribute__((aligned(16))) bf16 Vs[WM * HD];
-    __shared__ float wts[HD * 10];
+    __shared__ __attribute__((aligned(16))) float wts[HD * 10];
     ATT_STAMP(1, 0);
     const Win w = decode_w(a, split);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1202,7 +1220,7 @@ __global__ __launch_bounds__(NT) void stripe_bwd_dkdv_w(csu_stripe_args a, int s
     __shared__ __attribute__((aligned(16))) bf16 Qs[WM * HD];
     __shared__ __attribute__((aligned(16))) bf16 Gs[WM * HD];
     __shared__ __attribute__((aligned(16))) float lse_s[WM], dl_s[WM];
-    __shared__ float wts[HD * 10];
+    __shared__ __attribute__((aligned(16))) float wts[HD * 10];
     __shared__ __attribute__((aligned(16))) unsigned char dtbl[4][128];
     ATT_STAMP(2, 0);
     const Win w = decode_w(a, split);
@@ -1375,6 +1393,8 @@ int validate(const csu_stripe_args* a, int dtype) {
             return fail(CSU_E_ARG, "stripe_attn: branches must have equal window size");
         if (!g.lepe_w || !g.lepe_b) return fail(CSU_E_ARG, "stripe_attn: null LePE weights");
     }
+    if (a->br[0].H_sp * a->br[0].W_sp > 4096 || a->br[0].W_sp > 1024 || (a->nbranch > 1 && a->br[1].W_sp > 1024))
+        return fail(CSU_E_UNSUPPORTED, "stripe_attn: windows of <= 4096 tokens, <= 1024 wide");
     if (a->drop_p < 0.f || a->drop_p >= 1.f || (a->drop_p > 0.f && !a->drop_rng))
         return fail(CSU_E_ARG, "stripe_attn: attention dropout needs 0 <= p < 1 and an RNG snapshot");
     return 0;
