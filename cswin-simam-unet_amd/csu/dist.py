@@ -65,7 +65,8 @@ class GradAllReduce:
     (buckets in reverse registration order = backward order); a complete bucket is packed into its
     flat fp32 buffer (one ``cat``) and all-reduced on a side stream while backward continues.
     ``finish()`` (call after ``backward()``, before ``optimizer.step()``) launches any bucket still
-    pending, joins the side stream and re-points every ``p.grad`` at its averaged slice of the flat
+    pending (every bucket that completed while csu still held deferred parameter gradients: those
+    are written by the end-of-backward flush, so their all-reduce follows it), joins the side stream and re-points every ``p.grad`` at its averaged slice of the flat
     buffers, which the optimizer then reads in place.  Every call is a stream operation, so the same
     sequence is recorded into a graph on capture and replayed with one launch per step (RCCL
     collectives are capturable once the communicator exists: run one eager step first).
@@ -118,7 +119,9 @@ class GradAllReduce:
     def _hook(self, p):
         bi = self.where[id(p)]
         self.pending[bi] -= 1
-        if self.pending[bi] == 0:
+        # a bucket whose gradients may still be filled by csu's end-of-backward flush (deferred
+        # weight / LayerNorm / LePE gradients) is launched by finish(), after that flush
+        if self.pending[bi] == 0 and not self._ops.deferred_pending():
             self._launch(bi)
 
     def _launch(self, bi):

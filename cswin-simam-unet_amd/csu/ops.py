@@ -239,17 +239,34 @@ def _note_use(*params):
             _USES[id(p)] = _USES.get(id(p), 0) + 1
 
 
+def _reducer_hooks_only(hooks) -> bool:
+    """True when every post-accumulate-grad hook is a csu.dist.GradAllReduce bucket counter: that
+    reducer postpones a bucket holding deferred gradients until after the end-of-backward flush
+    (deferred_pending()), so deferral stays legal under data parallelism."""
+    from .dist import GradAllReduce
+    return all(getattr(h, "__func__", None) is GradAllReduce._hook for h in hooks.values())
+
+
 def _deferrable(*params) -> bool:
     _queue_flush()   # the end-of-backward flush also resets the use counts
     for p in params:
         p = _leaf(p)
         if p is None:
             continue
-        if p.grad is not None or p._backward_hooks or getattr(p, "_post_accumulate_grad_hooks", None):
+        if p.grad is not None or p._backward_hooks:
+            return False
+        hooks = getattr(p, "_post_accumulate_grad_hooks", None)
+        if hooks and not _reducer_hooks_only(hooks):
             return False
         if _USES.get(id(p), 0) > 1:
             return False
     return True
+
+
+def deferred_pending() -> bool:
+    """Parameter gradients of the running backward pass that are filled only by the end-of-backward
+    flush (LayerNorm dgamma / dbeta, token-Linear dW / db, LePE dW / db)."""
+    return bool(_LN_PENDING or _WG_DEFER or _WG_PENDING or _LEPE_PENDING)
 
 
 def _ln_param_flush():
