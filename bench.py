@@ -2,7 +2,8 @@
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
 N > 1 is launched by the driver with torch.distributed.run (one process per GPU, RCCL).
-One step = forward + BCE + backward (+ bucketed RCCL gradient all-reduce, captured in the same HIP
+One step = forward + BCE (with the reference loop's per-step thresholded Dice / IoU sums, cswin:789-795,
+fused into the loss kernel) + backward (+ bucketed RCCL gradient all-reduce, captured in the same HIP
 graph, csu.dist.GradAllReduce) + fused AdamW on a batch of
 synthetic 512x512 images already resident in HBM.  Prints ONE JSON line (rank 0).
 
@@ -180,7 +181,7 @@ def main():
 
     from csu import ops
     from csu.model import CSWinTransformer
-    from csu.train import bce_loss, make_optimizer
+    from csu.train import bce_loss, bce_loss_stats, make_optimizer
 
     depth = [int(v) for v in args.depth.split(",")]
     split = [int(v) for v in args.split.split(",")]
@@ -217,7 +218,7 @@ def main():
         opt.zero_grad(set_to_none=True)
         with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp is not None):
             y = model(x)
-        loss = bce_loss(y, t)
+        loss, _ = bce_loss_stats(y, t)   # + the reference loop's per-step Dice / IoU sums (cswin:789-795)
         loss.backward()
         if reducer is not None:
             reducer.finish()
@@ -231,7 +232,7 @@ def main():
         # otherwise; the cause of the former hipGraphInstantiate segfault)
         from csu.train import GraphedTrainStep
         gstep = GraphedTrainStep(model, opt, bce_loss, batches[0][0], batches[0][1], amp, warmup=args.warmup,
-                                 reducer=reducer)
+                                 reducer=reducer, metrics=True)
 
         def step(i):
             x, t = batches[i % len(batches)]

@@ -49,36 +49,61 @@ constexpr int BCE_BLOCKS = 1024;
 // partial[block] = sum over the block's fixed element range (fixed order: per-thread strided sum,
 // then a fixed shuffle + LDS tree)
 __global__ __launch_bounds__(NT) void bce_partial(long n, const float* __restrict__ p, const float* __restrict__ t,
-                                                  float* __restrict__ partial) {
-    __shared__ float red[NT / 64];
+                                                  float* __restrict__ partial, int stats) {
+    // stats: also the per-step segmentation sums of the reference loop (cswin:789-795, thresholded
+    // predictions pred = p > 0.5): sum(pred * t), sum(pred), sum(t) -> partial[k * gridDim.x + block]
+    __shared__ float red[4][NT / 64];
     const long per = (n + gridDim.x - 1) / gridDim.x;
     const long b0 = (long)blockIdx.x * per, b1 = min(n, b0 + per);
-    float s = 0.f;
+    float s = 0.f, si = 0.f, sp = 0.f, st = 0.f;
+    auto acc = [&](float pv, float tv) {
+        s += bce_term(pv, tv);
+        const float pr = pv > 0.5f ? 1.f : 0.f;
+        si += pr * tv;
+        sp += pr;
+        st += tv;
+    };
     if ((per & 3) == 0 && (n & 3) == 0) {
         for (long e = b0 + 4 * threadIdx.x; e < b1; e += 4 * NT) {
             float pv[4], tv[4];
             load4(p + e, pv);
             load4(t + e, tv);
 #pragma unroll
-            for (int j = 0; j < 4; ++j) s += bce_term(pv[j], tv[j]);
+            for (int j = 0; j < 4; ++j) acc(pv[j], tv[j]);
         }
     } else {
-        for (long e = b0 + threadIdx.x; e < b1; e += NT) s += bce_term(p[e], t[e]);
+        for (long e = b0 + threadIdx.x; e < b1; e += NT) acc(p[e], t[e]);
     }
-    s = wave_sum(s);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    const float v[4] = {s, si, sp, st};
+    const int nk = stats ? 4 : 1;
+    for (int k = 0; k < nk; ++k) {
+        const float w = wave_sum(v[k]);
+        if ((threadIdx.x & 63) == 0) red[k][threadIdx.x >> 6] = w;
+    }
     __syncthreads();
-    if (threadIdx.x == 0) partial[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+    if (threadIdx.x < nk) {
+        const int k = threadIdx.x;
+        partial[(long)k * gridDim.x + blockIdx.x] = (red[k][0] + red[k][1]) + (red[k][2] + red[k][3]);
+    }
 }
 
-__global__ __launch_bounds__(NT) void bce_final(int nb, long n, const float* __restrict__ partial, float* __restrict__ loss) {
+__global__ __launch_bounds__(NT) void bce_final(int nb, long n, const float* __restrict__ partial, float* __restrict__ loss,
+                                                float* __restrict__ stats) {
     __shared__ float red[NT / 64];
-    float s = 0.f;
-    for (int i = threadIdx.x; i < nb; i += NT) s += partial[i];
-    s = wave_sum(s);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
-    __syncthreads();
-    if (threadIdx.x == 0) loss[0] = ((red[0] + red[1]) + (red[2] + red[3])) / (float)n;
+    const int nk = stats ? 4 : 1;
+    for (int k = 0; k < nk; ++k) {
+        float s = 0.f;
+        for (int i = threadIdx.x; i < nb; i += NT) s += partial[(long)k * nb + i];
+        s = wave_sum(s);
+        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const float tot = (red[0] + red[1]) + (red[2] + red[3]);
+            if (k == 0) loss[0] = tot / (float)n;
+            else stats[k - 1] = tot;
+        }
+        __syncthreads();
+    }
 }
 
 // dp = dloss * (p - t) / max((1 - p) p, 1e-12) * (1 / n)   (torch: bce backward, then div by numel
@@ -129,19 +154,30 @@ extern "C" int csu_grad_join(long n, int adtype, const void* a, int bdtype, cons
     return check_launch("grad_join");
 }
 
-extern "C" size_t csu_bce_loss_workspace(long n) { return (size_t)BCE_BLOCKS * sizeof(float); }
+extern "C" size_t csu_bce_loss_workspace(long n) { return (size_t)4 * BCE_BLOCKS * sizeof(float); }
 
-extern "C" int csu_bce_loss_fwd(long n, const float* p, const float* t, float* loss, void* workspace, size_t ws_bytes,
-                                void* stream) {
+static int bce_fwd(long n, const float* p, const float* t, float* loss, float* stats, void* workspace, size_t ws_bytes,
+                   void* stream) {
     if (n < 1 || !p || !t || !loss) return fail(CSU_E_ARG, "bce_loss_fwd: bad args");
     if (!workspace || ws_bytes < csu_bce_loss_workspace(n)) return fail(CSU_E_WORKSPACE, "bce_loss_fwd: workspace");
     const long want = (n + 4 * NT - 1) / (4 * NT);
     const int nb = (int)(want < BCE_BLOCKS ? want : BCE_BLOCKS);
     hipStream_t st = as_stream(stream);
-    bce_partial<<<nb, NT, 0, st>>>(n, p, t, (float*)workspace);
+    bce_partial<<<nb, NT, 0, st>>>(n, p, t, (float*)workspace, stats != nullptr);
     if (int e = check_launch("bce_loss_fwd")) return e;
-    bce_final<<<1, NT, 0, st>>>(nb, n, (const float*)workspace, loss);
+    bce_final<<<1, NT, 0, st>>>(nb, n, (const float*)workspace, loss, stats);
     return check_launch("bce_loss_fwd");
+}
+
+extern "C" int csu_bce_loss_fwd(long n, const float* p, const float* t, float* loss, void* workspace, size_t ws_bytes,
+                                void* stream) {
+    return bce_fwd(n, p, t, loss, nullptr, workspace, ws_bytes, stream);
+}
+
+extern "C" int csu_bce_loss_fwd_stats(long n, const float* p, const float* t, float* loss, float* stats, void* workspace,
+                                      size_t ws_bytes, void* stream) {
+    if (!stats) return fail(CSU_E_ARG, "bce_loss_fwd_stats: null stats");
+    return bce_fwd(n, p, t, loss, stats, workspace, ws_bytes, stream);
 }
 
 extern "C" int csu_bce_loss_bwd(long n, const float* p, const float* t, const float* dloss, float* dp, void* stream) {

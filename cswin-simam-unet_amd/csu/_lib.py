@@ -168,6 +168,7 @@ _SIGS = {
                                      c_void_p]),
     "csu_bce_loss_workspace": (c_size_t, [ctypes.c_long]),
     "csu_bce_loss_fwd": (ctypes.c_int, [ctypes.c_long, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "csu_bce_loss_fwd_stats": (ctypes.c_int, [ctypes.c_long] + [c_void_p] * 5 + [c_size_t, c_void_p]),
     "csu_bce_loss_bwd": (ctypes.c_int, [ctypes.c_long, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "csu_pack_nhwc_bf16": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_void_p,
                                           c_void_p, c_void_p]),

@@ -1063,29 +1063,39 @@ def grad_join(g1: Optional[torch.Tensor], g2: Optional[torch.Tensor], dtype: tor
 
 class _BCELossFn(torch.autograd.Function):
     """nn.BCELoss() (mean) on fp32 probabilities (cswin:935): csu_bce_loss_fwd (fixed-order two-pass
-    sum) and csu_bce_loss_bwd (torch's clamps), 3 launches instead of torch's 5."""
+    sum) and csu_bce_loss_bwd (torch's clamps), 3 launches instead of torch's 5.  with_stats: the
+    same pass also returns the reference loop's per-step segmentation sums (cswin:789-795:
+    sum(pred * t), sum(pred), sum(t) of pred = p > 0.5) as a non-differentiable (3,) tensor."""
 
     @staticmethod
-    def forward(ctx, p, t):
+    def forward(ctx, p, t, with_stats: bool = False):
         p, t = p.contiguous(), t.contiguous()
         n = p.numel()
         loss = torch.empty((), dtype=torch.float32, device=p.device)
+        stats = torch.empty(3, dtype=torch.float32, device=p.device) if with_stats else None
         nws = lib().csu_bce_loss_workspace(n)
         ws = torch.empty(nws // 4, dtype=torch.float32, device=p.device)
-        _launch("bce_loss", lambda: lib().csu_bce_loss_fwd(n, ptr(p), ptr(t), ptr(loss), ptr(ws), nws, stream_ptr(p.device)),
-                8 * n, 8 * n, prec="f32")
+        if with_stats:
+            _launch("bce_loss", lambda: lib().csu_bce_loss_fwd_stats(n, ptr(p), ptr(t), ptr(loss), ptr(stats), ptr(ws), nws,
+                                                                     stream_ptr(p.device)), 12 * n, 8 * n, prec="f32")
+        else:
+            _launch("bce_loss", lambda: lib().csu_bce_loss_fwd(n, ptr(p), ptr(t), ptr(loss), ptr(ws), nws,
+                                                               stream_ptr(p.device)), 8 * n, 8 * n, prec="f32")
         ctx.save_for_backward(p, t)
+        if with_stats:
+            ctx.mark_non_differentiable(stats)
+            return loss, stats
         return loss
 
     @staticmethod
-    def backward(ctx, g):
+    def backward(ctx, g, *unused):
         p, t = ctx.saved_tensors
         g = g.float().contiguous()
         dp = torch.empty_like(p)
         n = p.numel()
         _launch("bce_loss_bwd", lambda: lib().csu_bce_loss_bwd(n, ptr(p), ptr(t), ptr(g), ptr(dp), stream_ptr(p.device)),
                 6 * n, 12 * n, prec="f32")
-        return dp, None
+        return dp, None, None
 
 
 def bce_loss(prob: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
@@ -1094,6 +1104,14 @@ def bce_loss(prob: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
     if prob.dtype != torch.float32 or target.dtype != torch.float32 or prob.shape != target.shape:
         raise ValueError("bce_loss: fp32 probabilities and targets of one shape")
     return _BCELossFn.apply(prob, target)
+
+
+def bce_loss_stats(prob: torch.Tensor, target: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """(bce_loss, (sum(pred * t), sum(pred), sum(t)) of pred = prob > 0.5) in one pass."""
+    require_device(prob, target)
+    if prob.dtype != torch.float32 or target.dtype != torch.float32 or prob.shape != target.shape:
+        raise ValueError("bce_loss: fp32 probabilities and targets of one shape")
+    return _BCELossFn.apply(prob, target, True)
 
 
 def augment_batch(images: torch.Tensor, masks: torch.Tensor, params) -> Tuple[torch.Tensor, torch.Tensor]:

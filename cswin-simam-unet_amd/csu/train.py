@@ -31,6 +31,18 @@ def bce_loss(prob: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
         return F.binary_cross_entropy(prob.float(), target.float())
 
 
+def bce_loss_stats(prob: torch.Tensor, target: torch.Tensor):
+    """bce_loss and the per-step segmentation sums (sum(pred*t), sum(pred), sum(t), pred = prob >
+    0.5; cswin:789-795) of the same pass (device: one fused csu kernel)."""
+    with torch.autocast(prob.device.type, enabled=False):
+        if prob.is_cuda:
+            from . import ops
+            return ops.bce_loss_stats(prob.float(), target.float())
+        p, t = prob.float(), target.float()
+        pred = (p > 0.5).float()
+        return F.binary_cross_entropy(p, t), torch.stack([(pred * t).sum(), pred.sum(), t.sum()]).detach()
+
+
 def _dice_t(pred, target, smooth=1e-6):
     pred, target = pred.reshape(-1), target.reshape(-1)
     inter = (pred * target).sum()
@@ -190,8 +202,12 @@ class GraphedTrainStep:
     not capturable)."""
 
     def __init__(self, model, optimizer, criterion, example_x, example_t, autocast_dtype=None, warmup=3,
-                 reducer=None):
+                 reducer=None, metrics=False):
         self.model, self.opt, self.crit = model, optimizer, criterion
+        # metrics (criterion bce_loss): the reference loop's per-step thresholded Dice / IoU sums
+        # (cswin:789-795) computed inside the graph by the loss kernel -> self.stats after a replay
+        self.metrics = metrics
+        self.stats = None
         self.reducer = reducer
         self.x = example_x.clone()
         self.t = example_t.clone()
@@ -239,6 +255,7 @@ class GraphedTrainStep:
         self.opt.zero_grad(set_to_none=True)
         with torch.cuda.graph(self.graph, capture_error_mode=mode):
             self.loss, self.out = self._body(zero=False)
+            self.stats = self._stats
         fin = getattr(self.opt, "finish_capture", None)
         if fin is not None:
             fin()
@@ -248,7 +265,12 @@ class GraphedTrainStep:
             self.opt.zero_grad(set_to_none=True)
         with torch.autocast("cuda", dtype=self.dtype or torch.float32, enabled=self.dtype is not None):
             out = self.model(self.x)
-        loss = self.crit(out, self.t)
+        if self.metrics:
+            if self.crit is not bce_loss:
+                raise ValueError("GraphedTrainStep(metrics=True) needs criterion=csu.train.bce_loss")
+            loss, self._stats = bce_loss_stats(out, self.t)
+        else:
+            loss, self._stats = self.crit(out, self.t), None
         loss.backward()
         if self.reducer is not None:
             self.reducer.finish()

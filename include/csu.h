@@ -470,6 +470,10 @@ int csu_grad_join(long n, int adtype, const void* a, int bdtype, const void* b, 
 size_t csu_bce_loss_workspace(long n);
 int csu_bce_loss_fwd(long n, const float* p, const float* t, float* loss, void* workspace, size_t ws_bytes,
                      void* stream);
+/* the same loss plus the reference loop's per-step segmentation sums (cswin:789-795, pred = p > 0.5):
+ * stats[0] = sum(pred * t), stats[1] = sum(pred), stats[2] = sum(t) (fp32, fixed order) */
+int csu_bce_loss_fwd_stats(long n, const float* p, const float* t, float* loss, float* stats, void* workspace,
+                           size_t ws_bytes, void* stream);
 int csu_bce_loss_bwd(long n, const float* p, const float* t, const float* dloss, float* dp, void* stream);
 int csu_pack_nhwc_bf16(int B, int C, int H, int W, int Cp, const float* x, void* y, void* stream);
 

@@ -158,6 +158,26 @@ def test_graph_replays_bitwise_reproducible(side_in_graph, monkeypatch):
     assert all(torch.equal(a, b) for a, b in zip(res[0][1], res[1][1]))
 
 
+def test_graphed_step_metrics_in_graph():
+    """GraphedTrainStep(metrics=True): the per-step segmentation sums (cswin:789-795) computed by the
+    fused loss kernel inside the graph equal torch's on the step's output (pred = p > 0.5)."""
+    from csu.data import ellipse_batch
+    from csu.model import CSWinTransformer
+    from csu.train import GraphedTrainStep, bce_loss, make_optimizer
+    d = dev()
+    torch.manual_seed(0)
+    m = CSWinTransformer(img_size=128, split_size=[1, 2, 4, 4]).to(d)
+    rng = np.random.default_rng(2)
+    x, t = (v.to(d) for v in ellipse_batch(rng, 4, 128))
+    gs = GraphedTrainStep(m, make_optimizer(m, capturable=True), bce_loss, x, t, torch.bfloat16, warmup=2, metrics=True)
+    loss, out = gs(x, t)
+    torch.cuda.synchronize()
+    pred = (out > 0.5).double()
+    ref = torch.stack([(pred * t).sum(), pred.sum(), t.double().sum()])
+    torch.testing.assert_close(gs.stats.double(), ref, rtol=1e-6, atol=1e-3)
+    torch.testing.assert_close(loss, bce_loss(out, t).detach(), rtol=1e-6, atol=1e-7)
+
+
 def test_deep_config_vs_oracle():
     """Deep CSWin (BASELINE config 4 depths [2,4,32,2]) at 128x128, split [1,2,4,4], fp32:
     probabilities, loss and every gradient norm vs the fp64 oracle on the same recipe weights."""
