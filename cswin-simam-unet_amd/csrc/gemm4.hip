@@ -23,7 +23,6 @@
 namespace csu {
 namespace {
 
-constexpr int G4_NT = 256;
 
 #ifdef G4_TIMING   // debug build only: per-workgroup phase timestamps (s_memtime), read by csu_debug_g4_ts
 __device__ unsigned long long g4_ts[8][4096];
@@ -43,11 +42,12 @@ __device__ __forceinline__ int g4_off(int row, int chunk) { return row * G4_BK +
 // slice origin) of a row-major matrix with leading dimension ld into a swizzled [ROWS][64] image:
 // wave instruction i of this wave fills image rows rb..rb+7 (rb = (wave * ROWS/32 + i) * 8), lane l
 // row rb + l/8, 16-B chunk (l & 7) ^ (row & 7).  Constant for the whole kernel.
-template <int ROWS>
+template <int ROWS, int NWV = 4>
 __device__ __forceinline__ void g4_voff(int ld, int wave, int lane, unsigned* voff) {
+    constexpr int NI = ROWS / (8 * NWV);
 #pragma unroll
-    for (int i = 0; i < ROWS / 32; ++i) {
-        const int row = (wave * (ROWS / 32) + i) * 8 + (lane >> 3);
+    for (int i = 0; i < NI; ++i) {
+        const int row = (wave * NI + i) * 8 + (lane >> 3);
         voff[i] = (unsigned)row * ld * 2 + (((lane & 7) ^ (row & 7)) << 4);
     }
 }
@@ -55,18 +55,19 @@ __device__ __forceinline__ void g4_voff(int ld, int wave, int lane, unsigned* vo
 // DMA the slice: raw buffer loads to LDS from a resource whose base is the slice's first row and
 // whose size ends at the matrix's last row, so rows past the end read as 0 (hardware range check);
 // soff = the k offset in bytes (scalar).  Only scalar work per call: the lane offsets are fixed.
-template <int ROWS>
+template <int ROWS, int NWV = 4>
 __device__ __forceinline__ void g4_dma(i32x4 rs, const unsigned* voff, unsigned soff, bf16* img, int wave) {
+    constexpr int NI = ROWS / (8 * NWV);
 #ifdef G4_BUILTIN_DMA
     const __amdgpu_buffer_rsrc_t r = __builtin_bit_cast(__amdgpu_buffer_rsrc_t, rs);
 #pragma unroll
-    for (int i = 0; i < ROWS / 32; ++i)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)(img + (wave * (ROWS / 32) + i) * 8 * G4_BK),
+    for (int i = 0; i < NI; ++i)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)(img + (wave * NI + i) * 8 * G4_BK),
                                                  16, voff[i], soff, 0, 0);
 #else
     // inline asm (lds_dma.hpp): the compiler would otherwise wait vmcnt(0) before LDS reads that may
     // alias an in-flight DMA stage, which makes every ring deeper than 2 stages useless
-    dma<ROWS / 32>(rs, voff, soff, img, wave);   // same lane-linear 1-KB blocks: (wave * ROWS/32 + i) * 512
+    dma<NI>(rs, voff, soff, img, wave);   // same lane-linear 1-KB blocks: (wave * NI + i) * 512
 #endif
 }
 
@@ -104,20 +105,22 @@ __device__ __forceinline__ void g4_vmwait_floor(int c) {
 // the last unit it re-fetches the last unit into the free stage), and a tile's last step issues
 // its L epilogue loads BEFORE its DMA (so waiting for them does not wait for the prefetch) and its
 // ST stores after the MFMAs.
-template <int BM, int BN, int S, int OCC, int EPI, typename TOUT>
-__global__ __launch_bounds__(G4_NT, OCC) void gemm4_kernel(long M, int N, int K, const bf16* __restrict__ A, int lda,
+template <int BM, int BN, int S, int OCC, int EPI, typename TOUT, int WM = 2, int WN = 2>
+__global__ __launch_bounds__(64 * WM * WN, OCC) void gemm4_kernel(long M, int N, int K, const bf16* __restrict__ A, int lda,
                                                            const bf16* __restrict__ W, int ldw, const float* __restrict__ bias,
                                                            const bf16* __restrict__ gaux, const float* __restrict__ resid,
                                                            TOUT* __restrict__ out, bf16* __restrict__ gout, int ldc) {
-    constexpr int TMW = BM / 64, TNW = BN / 64;      // 32x32 tiles per wave (tokens, features)
+    constexpr int NWV = WM * WN;                     // waves: WM along tokens x WN along features
+    constexpr int TMW = BM / (32 * WM), TNW = BN / (32 * WN);   // 32x32 tiles per wave (tokens, features)
+    static_assert(TMW >= 1 && TNW >= 1 && BM % (8 * NWV) == 0 && BN % (8 * NWV) == 0, "gemm4 wave layout");
     constexpr int STAGE = (BM + BN) * G4_BK;         // bf16 elements per stage
-    constexpr int D = (BM + BN) / 32;                // DMA instructions per wave per unit
+    constexpr int D = (BM + BN) / (8 * NWV);         // DMA instructions per wave per unit
     constexpr int P = S - 1;                         // units in flight ahead of the one multiplied
     constexpr bool PRE = EPI == G4_GAUX || EPI == G4_RESID;
     // epilogue: each wave transposes its (BM/2) x WC accumulator tile through its own fp32 LDS
     // region, 32 token rows per pass, and then reads/writes whole 8-feature row chunks (16/32-B
     // vectors, consecutive lanes along a row): row-contiguous loads and stores.
-    constexpr int WC = BN / 2;                       // features per wave
+    constexpr int WC = BN / WN;                      // features per wave
     constexpr int CPR = WC / 8;                      // 8-feature chunks per row
     constexpr int RPS = 64 / CPR;                    // rows per wave instruction
     constexpr int Q = 32 / RPS;                      // instructions per 32-row pass
@@ -126,7 +129,7 @@ __global__ __launch_bounds__(G4_NT, OCC) void gemm4_kernel(long M, int N, int K,
     constexpr int L = 2 + (EPI == G4_RESID ? 2 : EPI == G4_GAUX ? 1 : 0) * TMW * Q;   // epilogue loads per wave
     constexpr int ST = TMW * Q * ((OS == 4 ? 2 : 1) + (EPI == G4_GELU_OUT ? 1 : 0));   // epilogue stores per wave
     constexpr int EPB = 32 * ERS * 4;                // bytes per wave
-    __shared__ __attribute__((aligned(1024))) bf16 smem[S * STAGE + 4 * EPB / 2];
+    __shared__ __attribute__((aligned(1024))) bf16 smem[S * STAGE + NWV * EPB / 2];
     const unsigned nbn = (N + BN - 1) / BN;
     const unsigned T = (unsigned)((M + BM - 1) / BM) * nbn;
     // tiles of this workgroup: its XCD's contiguous tile range, strided by the XCD's workgroups
@@ -141,19 +144,19 @@ __global__ __launch_bounds__(G4_NT, OCC) void gemm4_kernel(long M, int N, int K,
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int r = lane & 31, h = lane >> 5;
-    const int wm = (wave >> 1) * (BM / 2), wn = (wave & 1) * (BN / 2);
+    const int wm = (wave / WN) * (BM / WM), wn = (wave % WN) * (BN / WN);
 
-    unsigned voffA[BM / 32], voffW[BN / 32];
-    g4_voff<BM>(lda, wave, lane, voffA);
-    g4_voff<BN>(ldw, wave, lane, voffW);
+    unsigned voffA[BM / (8 * NWV)], voffW[BN / (8 * NWV)];
+    g4_voff<BM, NWV>(lda, wave, lane, voffA);
+    g4_voff<BN, NWV>(ldw, wave, lane, voffW);
     auto issue = [&](int u) {   // DMA of unit min(u, U - 1) into stage u % S
         const int uu = u < U ? u : U - 1;
         const unsigned tile = lo + kk + (unsigned)(uu / nk) * nloc;
         const unsigned soff = (unsigned)(uu % nk) * G4_BK * 2;
         bf16* st = smem + (u % S) * STAGE;
         const long ra = (long)(tile / nbn) * BM, rw = (long)(tile % nbn) * BN;
-        g4_dma<BM>(rsrc4(A + ra * lda, (M - ra) * lda * 2), voffA, soff, st, wave);
-        g4_dma<BN>(rsrc4(W + rw * ldw, (N - rw) * ldw * 2), voffW, soff, st + BM * G4_BK, wave);
+        g4_dma<BM, NWV>(rsrc4(A + ra * lda, (M - ra) * lda * 2), voffA, soff, st, wave);
+        g4_dma<BN, NWV>(rsrc4(W + rw * ldw, (N - rw) * ldw * 2), voffW, soff, st + BM * G4_BK, wave);
     };
     auto wait_unit = [&](int u) {   // vector-memory ops issued after unit u's DMA (issued at step u - P)
         const int w = u - P;
@@ -305,10 +308,13 @@ __global__ __launch_bounds__(G4_NT, OCC) void gemm4_kernel(long M, int N, int K,
     G4_STAMP(5);
 }
 
-struct G4Cfg { int bm, bn, s, occ; };
-constexpr G4Cfg kG4Cfgs[] = {{64, 64, 3, 2}, {128, 64, 2, 2}, {128, 128, 2, 1}, {128, 128, 3, 1}, {64, 128, 2, 1},
-                             {128, 64, 3, 1}};
-constexpr int kG4NCfg = 6;
+// bm x bn tile, s-stage ring, occ workgroups per CU, wm x wn waves
+struct G4Cfg { int bm, bn, s, occ, wm, wn; };
+constexpr G4Cfg kG4Cfgs[] = {{64, 64, 3, 2, 2, 2}, {128, 64, 2, 2, 2, 2}, {128, 128, 2, 1, 2, 2}, {128, 128, 3, 1, 2, 2},
+                             {64, 128, 2, 1, 2, 2}, {128, 64, 3, 1, 2, 2},
+                             // 8-wave workgroups (as many DMA-issuing waves per CU as two 4-wave ones)
+                             {128, 128, 2, 1, 2, 4}, {128, 128, 3, 1, 2, 4}, {256, 128, 2, 1, 2, 4}, {128, 256, 2, 1, 1, 8}};
+constexpr int kG4NCfg = 10;
 
 int g4_grid(int occ) {
     static int cus = 0;
@@ -321,10 +327,10 @@ int g4_grid(int occ) {
     return cus * occ;
 }
 
-template <int BM, int BN, int S, int OCC, int EPI, typename TOUT>
+template <int BM, int BN, int S, int OCC, int EPI, typename TOUT, int WM, int WN>
 int g4_launch(long M, int N, int K, const bf16* A, int lda, const bf16* W, int ldw, const float* bias, const bf16* gaux,
               const float* resid, void* out, bf16* gout, int ldc, hipStream_t st) {
-    gemm4_kernel<BM, BN, S, OCC, EPI, TOUT><<<dim3(g4_grid(OCC)), G4_NT, 0, st>>>(M, N, K, A, lda, W, ldw, bias, gaux, resid,
+    gemm4_kernel<BM, BN, S, OCC, EPI, TOUT, WM, WN><<<dim3(g4_grid(OCC)), 64 * WM * WN, 0, st>>>(M, N, K, A, lda, W, ldw, bias, gaux, resid,
                                                                                  (TOUT*)out, gout, ldc);
     return check_launch("gemm4");
 }
@@ -332,29 +338,38 @@ int g4_launch(long M, int N, int K, const bf16* A, int lda, const bf16* W, int l
 template <int C>
 int g4_epi(int epi, int odt, long M, int N, int K, const bf16* A, int lda, const bf16* W, int ldw, const float* bias,
            const bf16* gaux, const float* resid, void* out, bf16* gout, int ldc, hipStream_t st) {
-    constexpr int BM = kG4Cfgs[C].bm, BN = kG4Cfgs[C].bn, S = kG4Cfgs[C].s, O = kG4Cfgs[C].occ;
+    constexpr int BM = kG4Cfgs[C].bm, BN = kG4Cfgs[C].bn, S = kG4Cfgs[C].s, O = kG4Cfgs[C].occ, WM = kG4Cfgs[C].wm,
+                  WN = kG4Cfgs[C].wn;
     switch (epi) {
-        case G4_GELU_OUT: return g4_launch<BM, BN, S, O, G4_GELU_OUT, bf16>(M, N, K, A, lda, W, ldw, bias, gaux, resid, out, gout, ldc, st);
+        case G4_GELU_OUT: return g4_launch<BM, BN, S, O, G4_GELU_OUT, bf16, WM, WN>(M, N, K, A, lda, W, ldw, bias, gaux, resid, out, gout, ldc, st);
         case G4_GAUX:
-            if (odt == CSU_F32) return g4_launch<BM, BN, S, O, G4_GAUX, float>(M, N, K, A, lda, W, ldw, bias, gaux, resid, out, gout, ldc, st);
-            return g4_launch<BM, BN, S, O, G4_GAUX, bf16>(M, N, K, A, lda, W, ldw, bias, gaux, resid, out, gout, ldc, st);
-        case G4_RESID: return g4_launch<BM, BN, S, O, G4_RESID, float>(M, N, K, A, lda, W, ldw, bias, gaux, resid, out, gout, ldc, st);
+            if (odt == CSU_F32) return g4_launch<BM, BN, S, O, G4_GAUX, float, WM, WN>(M, N, K, A, lda, W, ldw, bias, gaux, resid, out, gout, ldc, st);
+            return g4_launch<BM, BN, S, O, G4_GAUX, bf16, WM, WN>(M, N, K, A, lda, W, ldw, bias, gaux, resid, out, gout, ldc, st);
+        case G4_RESID: return g4_launch<BM, BN, S, O, G4_RESID, float, WM, WN>(M, N, K, A, lda, W, ldw, bias, gaux, resid, out, gout, ldc, st);
         default:
-            if (odt == CSU_F32) return g4_launch<BM, BN, S, O, G4_PLAIN, float>(M, N, K, A, lda, W, ldw, bias, gaux, resid, out, gout, ldc, st);
-            return g4_launch<BM, BN, S, O, G4_PLAIN, bf16>(M, N, K, A, lda, W, ldw, bias, gaux, resid, out, gout, ldc, st);
+            if (odt == CSU_F32) return g4_launch<BM, BN, S, O, G4_PLAIN, float, WM, WN>(M, N, K, A, lda, W, ldw, bias, gaux, resid, out, gout, ldc, st);
+            return g4_launch<BM, BN, S, O, G4_PLAIN, bf16, WM, WN>(M, N, K, A, lda, W, ldw, bias, gaux, resid, out, gout, ldc, st);
     }
 }
 
 }  // namespace
 
-// Tile choice (tools/linear_probe.py, every token-GEMM shape of the 512x512 step): 128 x 64 with a
-// 2-stage ring at 2 workgroups per CU was fastest or within 5 % everywhere.  cfg indexes kG4Cfgs.
-int gemm4_pick(long, int, int) { return 1; }
+// Tile choice (tools/linear_probe.py, tools/gemm_graph_probe.py: every token-GEMM shape of the 512x512
+// step, graph-timed, profiles/r02al_gemm_probe.txt): 128 x 64 with a 2-stage ring at 2 workgroups per
+// CU is fastest or within 5 % for N <= 256; the 8-wave 256 x 128 tile wins the wide-output shapes with
+// K >= 128 (qkv at C = 128: 21.2 -> 18.2 us, fc1 at C = 512: 17.7 -> 15.3, qkv at C = 256: 17.9 -> 17.3).
+// The time per tile hardly follows its L2 -> LDS bytes (the 8-wave 128 x 128 tile moves 2/3 of the
+// bytes of two 128 x 64 tiles in the same time).  cfg indexes kG4Cfgs.
+int gemm4_pick(long M, int N, int K) { return N >= 384 && K >= 128 && M >= 2048 ? 8 : 1; }
 
 int gemm4_run(int cfg, int epi, int odt, long M, int N, int K, const bf16* A, int lda, const bf16* W, int ldw,
               const float* bias, const bf16* gaux, const float* resid, void* out, bf16* gout, int ldc, hipStream_t st) {
     if (cfg < 0 || cfg >= kG4NCfg) cfg = gemm4_pick(M, N, K);
     switch (cfg) {
+        case 9: return g4_epi<9>(epi, odt, M, N, K, A, lda, W, ldw, bias, gaux, resid, out, gout, ldc, st);
+        case 8: return g4_epi<8>(epi, odt, M, N, K, A, lda, W, ldw, bias, gaux, resid, out, gout, ldc, st);
+        case 7: return g4_epi<7>(epi, odt, M, N, K, A, lda, W, ldw, bias, gaux, resid, out, gout, ldc, st);
+        case 6: return g4_epi<6>(epi, odt, M, N, K, A, lda, W, ldw, bias, gaux, resid, out, gout, ldc, st);
         case 5: return g4_epi<5>(epi, odt, M, N, K, A, lda, W, ldw, bias, gaux, resid, out, gout, ldc, st);
         case 4: return g4_epi<4>(epi, odt, M, N, K, A, lda, W, ldw, bias, gaux, resid, out, gout, ldc, st);
         case 3: return g4_epi<3>(epi, odt, M, N, K, A, lda, W, ldw, bias, gaux, resid, out, gout, ldc, st);

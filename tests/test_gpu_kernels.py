@@ -332,7 +332,7 @@ def _gelu(t):
 
 
 @pytest.mark.parametrize("M,N,K", [(1000, 64, 64), (4099, 192, 64), (2048, 768, 256), (300, 128, 1024), (513, 256, 32),
-                                   (65536, 128, 512)])
+                                   (65536, 128, 512), (1030, 520, 128)])
 @pytest.mark.parametrize("b_trans", [False, True])
 @pytest.mark.parametrize("mode", ["plain", "bias_gelu_a", "gelu_aux", "resid"])
 def test_gemm_vs_torch(M, N, K, b_trans, mode):
@@ -362,7 +362,7 @@ def test_gemm_vs_torch(M, N, K, b_trans, mode):
     assert_close(out, ref, torch.bfloat16)
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 10, 11, 12, 13, 14, 15])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19])
 @pytest.mark.parametrize("M,N,K", [(1000, 64, 64), (4099, 192, 128), (300, 520, 1024), (16384, 1024, 256)])
 def test_gemm_tile_configs_and_gelu_out(M, N, K, cfg):
     """Every tile configuration of the b[n][k] kernel, with the dual (h, gelu(h)) epilogue."""
