@@ -356,11 +356,13 @@ int g4_epi(int epi, int odt, long M, int N, int K, const bf16* A, int lda, const
 
 // Tile choice (tools/linear_probe.py, tools/gemm_graph_probe.py: every token-GEMM shape of the 512x512
 // step, graph-timed, profiles/r02al_gemm_probe.txt): 128 x 64 with a 2-stage ring at 2 workgroups per
-// CU is fastest or within 5 % for N <= 256; the 8-wave 256 x 128 tile wins the wide-output shapes with
-// K >= 128 (qkv at C = 128: 21.2 -> 18.2 us, fc1 at C = 512: 17.7 -> 15.3, qkv at C = 256: 17.9 -> 17.3).
+// CU is fastest or within 5 % for N <= 256.  The 8-wave 256 x 128 tile wins the wide-output shapes
+// with K >= 128 in isolation (qkv at C = 128: 21.2 -> 18.2 us, fc1 at C = 512: 17.7 -> 15.3), but the
+// whole step with it there ran 0.7 % SLOWER (3 interleaved A/B pairs, profiles/r02am_ab.txt), so
+// 128 x 64 stays everywhere; the 8-wave configurations stay selectable (cfg 16-19) and GPU-tested.
 // The time per tile hardly follows its L2 -> LDS bytes (the 8-wave 128 x 128 tile moves 2/3 of the
 // bytes of two 128 x 64 tiles in the same time).  cfg indexes kG4Cfgs.
-int gemm4_pick(long M, int N, int K) { return N >= 384 && K >= 128 && M >= 2048 ? 8 : 1; }
+int gemm4_pick(long, int, int) { return 1; }
 
 int gemm4_run(int cfg, int epi, int odt, long M, int N, int K, const bf16* A, int lda, const bf16* W, int ldw,
               const float* bias, const bf16* gaux, const float* resid, void* out, bf16* gout, int ldc, hipStream_t st) {
