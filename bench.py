@@ -240,10 +240,14 @@ def main():
     else:
         for i in range(args.warmup):
             eager_step(i)
-    # roofline leg: every kernel launch of 2 eager steps of the same workload, timed with HIP
-    # events on its launch stream (events cannot be recorded in graph replays)
+    # roofline leg.  Single process with the graph: AFTER the timed region, a second capture of the
+    # same step with an external HIP event-record node around every csu launch (csu_event_record_ext),
+    # replayed 3 times -> each kernel's time inside the replayed step.  Otherwise (eager bench, or
+    # N > 1 whose reducer buffers belong to the first capture): every launch of 2 eager steps, timed
+    # with HIP events on its launch stream.
     ledger = None
-    if not args.no_roofline:
+    graph_ledger = use_graph and not dp and not args.no_roofline
+    if not args.no_roofline and not graph_ledger:
         from csu.ledger import KernelLedger
         ledger = KernelLedger(repeat=4)
         side, ops.SIDE_WGRAD = ops.SIDE_WGRAD, False   # serialized, like the single-stream graph replay
@@ -271,9 +275,23 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     el = float(t.item())
     images = args.batch * world * args.steps
+    lsteps = 2
+    if graph_ledger:
+        # the timed graph is not replayed again: this capture re-fills the optimizer's pointer table
+        from csu.ledger import KernelLedger
+        from csu.train import GraphedTrainStep
+        ledger = KernelLedger(graph=True)
+        with ledger:
+            lstep = GraphedTrainStep(model, opt, bce_loss, batches[0][0], batches[0][1], amp, warmup=1,
+                                     metrics=True)
+        for i in range(3):
+            lstep(*batches[i % len(batches)])
+            ledger.collect()
+        lsteps = 1
     roof = None
     if ledger is not None:
-        roof = _roofline(ledger.summary(steps=2), el / args.steps * 1e3, args)
+        roof = _roofline(ledger.summary(steps=lsteps), el / args.steps * 1e3, args)
+        roof["ledger"] = "graph replays (external HIP event nodes)" if graph_ledger else "eager steps (HIP events)"
     cpu = None
     if rank == 0 and world == 1 and (args.cpu_baseline == "on" or (args.cpu_baseline == "auto")):
         try:
@@ -330,7 +348,7 @@ def _roofline(kernels, ms_per_step, args):
             "avg_us": top["avg_us"], "launches_per_step": top["launches_per_step"],
             "bytes_per_launch": top["bytes_per_launch"], "flops_per_launch": top["flops_per_launch"],
             "step_frac": round(t_roof_step / ms_per_step, 4), "step_t_roof_ms": round(t_roof_step, 3),
-            "eager_kernel_ms_per_step": round(sum(k["us_per_step"] for k in kernels) / 1e3, 3),
+            "kernel_ms_per_step": round(sum(k["us_per_step"] for k in kernels) / 1e3, 3),
             "kernels": kernels}
 
 

@@ -81,6 +81,10 @@ class ConvGeom(ctypes.Structure):
 _SIGS = {
     "csu_last_error_string": (ctypes.c_char_p, []),
     "csu_build_info": (ctypes.c_char_p, []),
+    "csu_event_create": (ctypes.c_int, [ctypes.POINTER(c_void_p)]),
+    "csu_event_destroy": (ctypes.c_int, [c_void_p]),
+    "csu_event_record_ext": (ctypes.c_int, [c_void_p, c_void_p]),
+    "csu_event_elapsed_ms": (ctypes.c_int, [c_void_p, c_void_p, ctypes.POINTER(c_float)]),
     "csu_stripe_attn_fwd": (ctypes.c_int, [ctypes.POINTER(StripeArgs), ctypes.c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
     "csu_stripe_attn_bwd_workspace": (c_size_t, [ctypes.POINTER(StripeArgs)]),
     "csu_stripe_attn_bwd": (ctypes.c_int, [ctypes.POINTER(StripeArgs), ctypes.c_int, c_void_p, c_void_p, c_void_p,

@@ -1,16 +1,21 @@
 """Per-kernel roofline ledger: every C-ABI launch of csu goes through ``launch()``, which names the
 call and states its ALGORITHMIC work (FLOPs; bytes = each input read once + each output written
-once).  While a ``KernelLedger`` is active (eager steps only -- HIP events cannot be recorded in a
-graph replay), each launch is timed with HIP events on its own stream: idempotent launches are
-re-run ``repeat`` times back-to-back between the two events (the per-event overhead then stays out
-of the per-launch time, which matches the rocprofv3 kernel trace); non-idempotent ones (the
-in-place AdamW) are timed once.  ``summary()`` gives, per call name, launches, measured time,
+once).  While a ``KernelLedger`` is active, each launch is timed with HIP events on its own stream.
+Eager mode: idempotent launches are re-run ``repeat`` times back-to-back between the two events
+(the per-event overhead then stays out of the per-launch time), non-idempotent ones (the in-place
+AdamW) are timed once; the repeats find their inputs in the caches, so memory-bound kernels read
+up to ~12 % faster than inside the step.  Graph mode (``graph=True``): the launches of a stream
+capture are bracketed by external HIP event-record nodes, so each replay of the captured step
+times every kernel where it really runs (bench.py's single-process roofline); a bracket adds the
+launch's dispatch and completion (~2-5 us per launch against the rocprofv3 kernel time: 5 % on the
+attention backward, 16 % on the 14-us token GEMMs), so graph-mode fractions err low.  ``summary()`` gives, per call name, launches, measured time,
 achieved GB/s / TFLOP/s, the roofline time t_roof = max(FLOPs / P_mfma, bytes / BW_hbm) and the
 fraction t_roof / t_measured (MI355X_MICROARCH.md peaks: HBM 8 TB/s, dense bf16 MFMA 2.5 PF/s,
 fp32 MFMA 157.3 TF/s)."""
 from __future__ import annotations
 
 import collections
+import ctypes
 from typing import Callable, Dict, List, Optional
 
 import torch
@@ -23,10 +28,56 @@ PEAK_TFLOPS = {"bf16": 2500.0, "f32": 157.3, "fp8": 5000.0}
 _ACTIVE: Optional["KernelLedger"] = None
 
 
+class _HipEvent:
+    """A HIP timing event recorded with hipEventRecordExternal (csu_event_record_ext): inside a stream
+    capture it is an event-record node of the graph, re-stamped by every replay."""
+
+    def __init__(self):
+        from ._lib import lib
+        self._lib = lib()
+        h = ctypes.c_void_p()
+        check(self._lib.csu_event_create(ctypes.byref(h)), "event_create")
+        self.h = h
+
+    def record(self):
+        check(self._lib.csu_event_record_ext(self.h, ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)),
+              "event_record_ext")
+
+    def elapsed_time(self, end: "_HipEvent") -> float:
+        ms = ctypes.c_float()
+        check(self._lib.csu_event_elapsed_ms(self.h, end.h, ctypes.byref(ms)), "event_elapsed_ms")
+        return float(ms.value)
+
+    def __del__(self):
+        try:
+            self._lib.csu_event_destroy(self.h)
+        except Exception:
+            pass
+
+
 class KernelLedger:
-    def __init__(self, repeat: int = 4):
+    """``graph=False``: time the launches of eager steps (idempotent ones repeated ``repeat`` times).
+    ``graph=True``: only launches made while a stream is being captured are recorded, each bracketed
+    by two external HIP event nodes inside the graph; call ``collect()`` after each replay of that
+    graph (synchronized) -- ``summary()`` then averages every launch over the collected replays, i.e.
+    the kernels' times as they run inside the replayed step (inputs left in the caches, or dirty, by
+    the kernel before: what rocprofv3 sees over the timed region)."""
+
+    def __init__(self, repeat: int = 4, graph: bool = False):
         self.repeat = max(1, int(repeat))
+        self.graph = bool(graph)
         self.rows: List[tuple] = []
+        self._acc: List[float] = []
+        self.replays = 0
+
+    def collect(self):
+        """Add the event-pair times of the replay that just finished (graph mode)."""
+        torch.cuda.synchronize()
+        if len(self._acc) < len(self.rows):
+            self._acc += [0.0] * (len(self.rows) - len(self._acc))
+        for i, r in enumerate(self.rows):
+            self._acc[i] += r[1].elapsed_time(r[2])
+        self.replays += 1
 
     def __enter__(self):
         global _ACTIVE
@@ -43,10 +94,12 @@ class KernelLedger:
         bytes / FLOPs per launch, achieved GB/s and TFLOP/s, bound, t_roof and frac."""
         torch.cuda.synchronize()
         agg = collections.OrderedDict()
-        for name, e0, e1, reps, flops, nbytes, prec in self.rows:
+        if self.graph and not self.replays:
+            raise RuntimeError("KernelLedger(graph=True): collect() after at least one replay")
+        for i, (name, e0, e1, reps, flops, nbytes, prec) in enumerate(self.rows):
             a = agg.setdefault(name, {"n": 0, "ms": 0.0, "flops": 0.0, "bytes": 0.0, "prec": prec})
             a["n"] += 1
-            a["ms"] += e0.elapsed_time(e1) / reps
+            a["ms"] += self._acc[i] / self.replays if self.graph else e0.elapsed_time(e1) / reps
             a["flops"] += flops
             a["bytes"] += nbytes
         out = []
@@ -74,8 +127,16 @@ def launch(name: str, fn: Callable[[], int], flops: float = 0.0, nbytes: float =
     active.  ``idem``: the call can be repeated without changing its result (outputs overwritten
     from unchanged inputs)."""
     led = _ACTIVE
-    if led is None or torch.cuda.is_current_stream_capturing():
+    capturing = torch.cuda.is_current_stream_capturing()
+    if led is None or capturing != led.graph:
         check(fn(), name)
+        return
+    if capturing:   # graph mode: event-record nodes around the launch, re-stamped by every replay
+        e0, e1 = _HipEvent(), _HipEvent()
+        e0.record()
+        check(fn(), name)
+        e1.record()
+        led.rows.append((name, e0, e1, 1, float(flops), float(nbytes), prec))
         return
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if idem:

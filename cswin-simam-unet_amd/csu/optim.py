@@ -43,6 +43,17 @@ class FusedAdamW(torch.optim.Optimizer):
                                              device=g["params"][0].device)
                              for gi, g in enumerate(self.param_groups) if g["params"] and g["params"][0].is_cuda}
 
+    def prepare_capture(self):
+        """Reserve the table buffers of one more capture (outside any graph pool; each captured graph
+        keeps its own).  GraphedTrainStep calls it before capturing; the first capture's buffers
+        come from the constructor.  A later capture re-fills the eager-side table cache only: the
+        graphs captured before keep their own tables."""
+        for gi, g in enumerate(self.param_groups):
+            if g["params"] and g["params"][0].is_cuda and (gi not in self._pinned or gi not in self._capture_dev):
+                n = max(1, len(g["params"])) * _ITEM.itemsize
+                self._pinned[gi] = torch.empty(n, dtype=torch.uint8, pin_memory=True)
+                self._capture_dev[gi] = torch.empty(n, dtype=torch.uint8, device=g["params"][0].device)
+
     def _table(self, gi, items, device):
         """Device item table for the current (param, grad) buffers, rebuilt when they change
         (e.g. every step under zero_grad(set_to_none=True) when the allocator hands out other grad
@@ -67,7 +78,7 @@ class FusedAdamW(torch.optim.Optimizer):
             host = self._pinned.get(gi)
             dev = self._capture_dev.get(gi)
             if host is None or dev is None or host.numel() < raw.size:
-                raise RuntimeError("FusedAdamW: no pinned table buffer for this capture (one capture per optimizer)")
+                raise RuntimeError("FusedAdamW: no pinned table buffer for this capture (call prepare_capture() before capturing)")
             del self._pinned[gi]                      # frozen: owned by the captured graph from now on
             del self._capture_dev[gi]
             host[:raw.size].numpy()[:] = raw

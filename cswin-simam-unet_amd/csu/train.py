@@ -251,6 +251,9 @@ class GraphedTrainStep:
                 if hasattr(pg, "_wait_for_pending_works"):
                     pg._wait_for_pending_works()
             mode = "thread_local"
+        prep = getattr(self.opt, "prepare_capture", None)
+        if prep is not None:
+            prep()
         self.graph = torch.cuda.CUDAGraph()
         self.opt.zero_grad(set_to_none=True)
         with torch.cuda.graph(self.graph, capture_error_mode=mode):

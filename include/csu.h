@@ -36,6 +36,17 @@ const char* csu_last_error_string(void);
 /* Library version and the offload arch it was built for ("gfx950"). */
 const char* csu_build_info(void);
 
+/* Timing events for bench.py's per-kernel roofline ledger (measurement plumbing, not part of the
+ * reference interface).  csu_event_record_ext: inside a stream capture it appends an event-record
+ * NODE to the graph being captured (hipGraphAddEventRecordNode after the stream's current
+ * dependencies, which it then replaces), so every replay re-stamps it and csu_event_elapsed_ms
+ * gives each captured kernel's time in that replay (torch refuses external events on ROCm).
+ * Outside a capture it is a plain hipEventRecord. */
+int csu_event_create(void** event);
+int csu_event_destroy(void* event);
+int csu_event_record_ext(void* event, void* stream);
+int csu_event_elapsed_ms(void* start, void* end, float* ms);
+
 /* ---------------------------------------------------------------------------------------
  * Cross-shaped stripe attention with LePE (LePEAttention.forward, cswin:271-298, geometry
  * cswin:232-240, get_v depthwise 3x3 cswin:244/256-269; branch split + concat of
