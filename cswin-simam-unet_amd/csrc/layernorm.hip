@@ -14,6 +14,7 @@ namespace {
 constexpr int NT = 256;
 constexpr int WAVES = NT / 64;
 constexpr int LU = 4;       // ln_bwd: row groups per wave iteration
+constexpr int FU = 4;       // ln_fwd: row groups per wave
 
 template <typename T, int V> __device__ __forceinline__ void ldv(const T* p, float* v) {
     if constexpr (V == 8) load8(p, v);
@@ -61,41 +62,53 @@ template <int LPR> __device__ __forceinline__ float group_sum(float v) {
     return v;
 }
 
+// FU row groups per wave, every load issued before any math (one memory round trip per FU rows:
+// the one-row-per-wave form was latency-bound at ~0.5 of the HBM roofline), branch-free raw
+// buffer loads / stores (rows past the end: out-of-range offsets).  Same arithmetic per row.
 template <typename TX, typename TY, int V, int LPR>
 __global__ __launch_bounds__(NT) void ln_fwd(int rows, int C, float eps, const TX* __restrict__ x,
                                              const float* __restrict__ gamma, const float* __restrict__ beta,
                                              TY* __restrict__ y, float* __restrict__ mean, float* __restrict__ rstd) {
     constexpr int RPW = 64 / LPR;
     const int lane = threadIdx.x & 63;
-    const int row = (blockIdx.x * WAVES + (threadIdx.x >> 6)) * RPW + lane / LPR;
+    const int rb = (blockIdx.x * WAVES + (threadIdx.x >> 6)) * RPW * FU + lane / LPR;
     const int c0 = (lane % LPR) * V;
-    const bool ok = row < rows;
-    float v[V];
-    if (ok) ldv<TX, V>(x + (size_t)row * C + c0, v);
-    else
+    const long n = (long)rows * C;
+    const auto rs_x = buf_rsrc(x, n * sizeof(TX)), rs_y = buf_rsrc(y, n * sizeof(TY));
+    const auto rs_m = buf_rsrc(mean, (long)rows * 4), rs_s = buf_rsrc(rstd, (long)rows * 4);
+    float v[FU][V];
+    unsigned e0[FU];
 #pragma unroll
-        for (int j = 0; j < V; ++j) v[j] = 0.f;
-    float s = 0.f;
-#pragma unroll
-    for (int j = 0; j < V; ++j) s += v[j];
-    const float mu = group_sum<LPR>(s) / C;
-    float q = 0.f;
-#pragma unroll
-    for (int j = 0; j < V; ++j) {
-        v[j] -= mu;
-        q += v[j] * v[j];
+    for (int u = 0; u < FU; ++u) {
+        const int row = rb + u * RPW;
+        e0[u] = row < rows ? (unsigned)((long)row * C + c0) : kOOB;   // element offset of the lane's segment
+        bld<TX, V>(rs_x, e0[u] == kOOB ? kOOB : e0[u] * (unsigned)sizeof(TX), v[u]);
     }
-    const float rs = rsqrtf(group_sum<LPR>(q) / C + eps);
-    if (!ok) return;
-    float gw[V], bw[V], o[V];
+    float gw[V], bw[V];
     ldv<float, V>(gamma + c0, gw);
     ldv<float, V>(beta + c0, bw);
 #pragma unroll
-    for (int j = 0; j < V; ++j) o[j] = v[j] * rs * gw[j] + bw[j];
-    stv<TY, V>(y + (size_t)row * C + c0, o);
-    if (lane % LPR == 0) {
-        mean[row] = mu;
-        rstd[row] = rs;
+    for (int u = 0; u < FU; ++u) {
+        float s = 0.f;
+#pragma unroll
+        for (int j = 0; j < V; ++j) s += v[u][j];
+        const float mu = group_sum<LPR>(s) / C;
+        float q = 0.f;
+#pragma unroll
+        for (int j = 0; j < V; ++j) {
+            v[u][j] -= mu;
+            q += v[u][j] * v[u][j];
+        }
+        const float rs = rsqrtf(group_sum<LPR>(q) / C + eps);
+        float o[V];
+#pragma unroll
+        for (int j = 0; j < V; ++j) o[j] = v[u][j] * rs * gw[j] + bw[j];
+        const unsigned e = e0[u];
+        bst<TY, V>(rs_y, e == kOOB ? kOOB : e * (unsigned)sizeof(TY), o);
+        const int row = rb + u * RPW;
+        const unsigned ro = (lane % LPR == 0 && row < rows) ? (unsigned)row * 4u : kOOB;
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(mu), rs_m, ro, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(rs), rs_s, ro, 0, 0);
     }
 }
 
@@ -219,7 +232,7 @@ template <typename TX, typename TY>
 int launch_fwd(int rows, int C, float eps, const void* x, const float* g, const float* b, void* y, float* m,
                float* r, hipStream_t st) {
 #define CSU_LNF(V, LPR)                                                                                           \
-    ln_fwd<TX, TY, V, LPR><<<(rows + WAVES * (64 / LPR) - 1) / (WAVES * (64 / LPR)), NT, 0, st>>>(rows, C, eps,      \
+    ln_fwd<TX, TY, V, LPR><<<(rows + WAVES * (64 / LPR) * FU - 1) / (WAVES * (64 / LPR) * FU), NT, 0, st>>>(rows, C, eps, \
                                                                                                   (const TX*)x, g, b, \
                                                                                                   (TY*)y, m, r)
     switch (C / 64) {
@@ -263,6 +276,7 @@ using namespace csu;
 extern "C" int csu_layernorm_fwd(int rows, int C, float eps, int xdtype, const void* x, const float* gamma,
                                  const float* beta, int ydtype, void* y, float* mean, float* rstd, void* stream) {
     if (int e = check_c(C)) return e;
+    if (int e = check_rows(rows, C)) return e;
     if (rows < 1 || !x || !gamma || !beta || !y || !mean || !rstd) return fail(CSU_E_ARG, "layernorm_fwd: bad args");
     hipStream_t st = as_stream(stream);
     if (xdtype == CSU_F32 && ydtype == CSU_F32) return launch_fwd<float, float>(rows, C, eps, x, gamma, beta, y, mean, rstd, st);
