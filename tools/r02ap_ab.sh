@@ -1,8 +1,8 @@
 #!/bin/bash
-# LayerNorm forward with 4 row groups per wave (ab/b.so) vs one row group (ab/a.so): LN / model GPU
+# LayerNorm forward row groups per wave: ab/a.so vs ab/b.so (r02ap: 4 vs 1; r02aq: 4 vs 8): LN / model GPU
 # tests on b, then 3 interleaved 512 B16 bench pairs
 set -e
-O=gpurun_out/r02ap; mkdir -p $O
+O=gpurun_out/${T:-r02ap}; mkdir -p $O
 CSU_LIB_PATH=ab/b.so timeout -k 10 400 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_model.py -k "layernorm or block or whole_model or graph" -x -q --timeout 200 --timeout-method thread > $O/pytest.log 2>&1 || { tail -40 $O/pytest.log; exit 1; }
 tail -1 $O/pytest.log
 for rep in 1 2 3; do
