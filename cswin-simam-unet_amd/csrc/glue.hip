@@ -38,10 +38,11 @@ __global__ __launch_bounds__(NT) void grad_join_kernel(long n8, int adt, const v
     }
 }
 
-// torch's BCE: -(t * max(log p, -100) + (1 - t) * max(log(1 - p), -100))
+// ATen's binary_cross_entropy: (t - 1) * max(log1p(-p), -100) - t * max(log p, -100) -- log1p, so
+// p near 0 contributes ~p, not the 0 that logf(1 - p) rounds to for p < 6e-8
 __device__ __forceinline__ float bce_term(float p, float t) {
-    const float lp = fmaxf(logf(p), -100.f), lq = fmaxf(logf(1.f - p), -100.f);
-    return -(t * lp + (1.f - t) * lq);
+    const float lp = fmaxf(logf(p), -100.f), lq = fmaxf(log1pf(-p), -100.f);
+    return (t - 1.f) * lq - t * lp;
 }
 
 constexpr int BCE_BLOCKS = 1024;

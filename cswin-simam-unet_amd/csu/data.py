@@ -131,7 +131,7 @@ class AugmentationTransform:
 class SegmentationDataset(torch.utils.data.Dataset):
     """The reference's dataset (cswin:91-175): ``*.jpg`` images of ``image_dir`` with same-named
     masks in ``mask_dir`` (missing / unreadable mask -> zeros, as the reference), resized to
-    ``image_size`` (height, width), optionally augmented, returned as (3, H, W) / (1, H, W) float32
+    ``image_size`` read as cv2.resize reads it, i.e. (width, height) (cswin:160-161), optionally augmented, returned as (3, H, W) / (1, H, W) float32
     in [0, 1].  Decoding uses PIL (cv2 is not in this image).  ``device_augment=True`` returns the
     resized uint8 (H, W, 3) image and (H, W) mask instead, for ``DeviceAugment`` to augment and
     normalise a whole batch on the GPU."""
@@ -160,7 +160,7 @@ class SegmentationDataset(torch.utils.data.Dataset):
             mask = np.asarray(Image.open(mpath).convert("L"))
         except (FileNotFoundError, OSError):
             mask = np.zeros(image.shape[:2], dtype=np.uint8)
-        h, w = self.image_size
+        w, h = self.image_size            # cv2.resize(image, dsize=(w, h)) (cswin:160-161)
         return resize_bilinear_u8(image, h, w), resize_bilinear_u8(mask, h, w)
 
     def __getitem__(self, idx):

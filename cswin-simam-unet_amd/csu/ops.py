@@ -249,6 +249,17 @@ def _reducer_hooks_only(hooks) -> bool:
 
 def _deferrable(*params) -> bool:
     _queue_flush()   # the end-of-backward flush also resets the use counts
+    # backward(create_graph=True): AccumulateGrad COPIES the incoming gradient (it does not take
+    # ownership), so the copy would be made before the end-of-backward flush filled the buffer
+    if torch.is_grad_enabled():
+        return False
+    # torch DDP's C++ reducer hooks the grad accumulators directly (invisible to the checks below) and
+    # reads p.grad as soon as it is accumulated: defer only without a process group, or under
+    # csu.dist.GradAllReduce (which postpones buckets holding deferred gradients, deferred_pending())
+    if not _DIST_SAFE[0]:
+        dist = torch.distributed
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            return False
     for p in params:
         p = _leaf(p)
         if p is None:

@@ -161,10 +161,34 @@ class FusedAdamW(torch.optim.Optimizer):
 
     def load_state_dict(self, state_dict):
         """Load an AdamW / FusedAdamW state; the device step / lr of every group and the pointer
-        tables are rebuilt from it on the next step()."""
+        tables are rebuilt from it on the next step().  Once a step has been captured into a HIP
+        graph, the graph keeps reading the current state tensors (step, lr, exp_avg, exp_avg_sq):
+        the loaded values are then copied INTO them, so the captured pointers stay valid."""
+        if not self._captured:
+            super().load_state_dict(state_dict)
+            self._gstate = {}
+            self._tables = {}
+            return
+        old = {p: dict(self.state[p]) for g in self.param_groups for p in g["params"] if self.state.get(p)}
         super().load_state_dict(state_dict)
-        self._gstate = {}
-        self._tables = {}
+        with torch.no_grad():
+            for gi, g in enumerate(self.param_groups):
+                gs = self._gstate.get(gi)
+                for p in g["params"]:
+                    st, o = self.state.get(p), old.get(p)
+                    if not st:
+                        continue
+                    if o is None:
+                        raise RuntimeError("FusedAdamW.load_state_dict after a capture: the loaded state has a "
+                                           "parameter the captured step has no state for")
+                    for k in ("exp_avg", "exp_avg_sq"):
+                        o[k].copy_(st[k])
+                        st[k] = o[k]
+                    if gs is not None:
+                        gs["step"].fill_(float(st["step"]))
+                        st["step"] = gs["step"]
+                if gs is not None:
+                    gs["lr"].fill_(g["lr"])
 
     def finish_capture(self):
         """After a HIP-graph capture of step(): fill the device tables the captured kernel reads

@@ -98,15 +98,81 @@ def _autocast(device, amp_dtype):
     return torch.autocast(dt, dtype=amp_dtype or torch.float32, enabled=amp_dtype is not None)
 
 
-def evaluate_model(model, data_loader, criterion, device, amp_dtype=None):
+_GRAPHS = None   # model -> {key: GraphedTrainStep | _GraphedEval}, kept across train_model calls
+
+
+def _graph_cache(model):
+    global _GRAPHS
+    if _GRAPHS is None:
+        import weakref
+        _GRAPHS = weakref.WeakKeyDictionary()
+    return _GRAPHS.setdefault(model, {})
+
+
+def _graphable(model, optimizer, device, criterion) -> bool:
+    """The whole step can be captured: csu model on a GPU (not wrapped in DDP, which cannot be
+    captured -- data parallel training passes a csu.dist.GradAllReduce instead) and csu's FusedAdamW."""
+    from .optim import FusedAdamW
+    dev = torch.device(device)
+    return (dev.type == "cuda" and isinstance(optimizer, FusedAdamW)
+            and not isinstance(model, torch.nn.parallel.DistributedDataParallel)
+            and all(p.is_cuda for p in model.parameters()))
+
+
+class _GraphedEval:
+    """evaluate_model's per-batch body (eval-mode forward, loss, thresholded sums) captured once
+    for a static batch shape and replayed."""
+
+    def __init__(self, model, criterion, x, t, amp_dtype):
+        self.model, self.crit, self.dtype = model, criterion, amp_dtype
+        self.x, self.t = x.clone(), t.clone()
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side), torch.no_grad():
+            self._body()                 # warm-up: lazily built caches / kernels outside the capture
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.no_grad(), torch.cuda.graph(self.graph):
+            self.stats = self._body()
+
+    def _body(self):
+        with torch.autocast("cuda", dtype=self.dtype or torch.float32, enabled=self.dtype is not None):
+            out = self.model(self.x)
+        if self.crit is bce_loss:
+            loss, st = bce_loss_stats(out, self.t)
+            return torch.cat([loss.detach().double().view(1), st.double()])
+        return _step_stats(self.crit(out, self.t), out, self.t)
+
+    def __call__(self, x, t):
+        self.x.copy_(x, non_blocking=True)
+        self.t.copy_(t, non_blocking=True)
+        self.graph.replay()
+        return self.stats.clone()
+
+
+def evaluate_model(model, data_loader, criterion, device, amp_dtype=None, graph=None):
     """eval mode, no grad; mean over batches of (loss, Dice, IoU) (cswin:712-747).  ``amp_dtype``
-    (not in the reference): run the forward under autocast (e.g. torch.bfloat16)."""
+    (not in the reference): run the forward under autocast (e.g. torch.bfloat16).  ``graph``
+    (None = automatic on a GPU): batches of the first batch's shape replay one captured HIP graph
+    of the forward + loss + metric sums; other shapes (a ragged last batch) run eagerly."""
     model.eval()
+    use_graph = (graph is not False and torch.device(device).type == "cuda" and torch.cuda.is_available()
+                 and not isinstance(model, torch.nn.parallel.DistributedDataParallel)
+                 and not torch.cuda.is_current_stream_capturing())
+    cache = _graph_cache(model) if use_graph else None
     stats = []
     with torch.no_grad():
         for images, masks in data_loader:
             images = images.to(device, non_blocking=True)
             masks = masks.to(device, non_blocking=True)
+            if use_graph:
+                key = ("eval", tuple(images.shape), tuple(masks.shape), amp_dtype, criterion)
+                g = cache.get(key)
+                if g is None:
+                    g = cache[key] = _GraphedEval(model, criterion, images, masks, amp_dtype)
+                stats.append(g(images, masks))
+                continue
             with _autocast(images.device, amp_dtype):
                 outputs = model(images)
             stats.append(_step_stats(criterion(outputs, masks), outputs, masks))
@@ -130,15 +196,53 @@ def train_step(model, images, masks, criterion, optimizer, reducer=None, amp_dty
         return _step_stats(loss, outputs, masks)
 
 
+class _GraphedTrain:
+    """train_model's step on a captured graph.  The first ``warmup`` batches of a shape are real
+    steps run eagerly on a side stream (the capture's warm-up: optimizer state, cast caches, RCCL
+    communicators), then the step is captured and every later batch of that shape replays it --
+    each batch is trained on exactly once, as in the reference loop."""
+
+    def __init__(self, model, optimizer, criterion, amp_dtype, reducer, warmup=2):
+        self.model, self.opt, self.crit, self.dtype, self.reducer = model, optimizer, criterion, amp_dtype, reducer
+        self.warmup, self.done, self.gs = warmup, 0, None
+
+    def __call__(self, images, masks):
+        if self.gs is None and self.done < self.warmup:
+            cur = torch.cuda.current_stream()
+            side = torch.cuda.Stream()
+            side.wait_stream(cur)
+            with torch.cuda.stream(side):
+                st = train_step(self.model, images, masks, self.crit, self.opt, self.reducer, self.dtype)
+            cur.wait_stream(side)
+            self.done += 1
+            return st
+        if self.gs is None:
+            for g in self.opt.param_groups:     # lr / step read from the device inside the graph
+                g["capturable"] = True
+            self.opt.sync_lr()
+            self.gs = GraphedTrainStep(self.model, self.opt, self.crit, images, masks, self.dtype, warmup=0,
+                                       reducer=self.reducer, metrics=self.crit is bce_loss)
+        loss, out = self.gs(images, masks)
+        if self.gs.stats is not None:
+            return torch.cat([loss.double().view(1), self.gs.stats.double()])
+        with torch.no_grad():
+            return _step_stats(loss, out, self.gs.t)
+
+
 def train_model(model, train_loader, test_loader, criterion, optimizer, scheduler, device, num_epochs=100,
                 verbose: bool = True, checkpoint_path: Optional[str] = None,
-                resume_from: Optional[str] = None, amp_dtype=None) -> Dict[str, List[float]]:
+                resume_from: Optional[str] = None, amp_dtype=None, graph=None, reducer=None) -> Dict[str, List[float]]:
     """Epoch loop with per-epoch history and ReduceLROnPlateau on the test loss (cswin:751-841).
 
     Beyond the reference: ``checkpoint_path`` writes a resumable checkpoint (model, optimizer,
     scheduler, epoch, history; csu.report.save_checkpoint) after every epoch, and ``resume_from``
     restores one and continues from the epoch after it (the history then covers all epochs);
-    ``amp_dtype`` runs the forward passes under autocast (the reference trains in fp32)."""
+    ``amp_dtype`` runs the forward passes under autocast (the reference trains in fp32).
+    ``graph`` (None = automatic): on a GPU with csu's FusedAdamW (csu.train.make_optimizer) each
+    batch shape's step is captured into one HIP graph after two eager steps and replayed (the
+    speed bench.py reports); a batch of another shape (ragged last batch) runs eagerly.  Graphs are
+    kept per model across calls.  ``reducer``: a csu.dist.GradAllReduce for data-parallel training
+    (captured with the step)."""
     history = {"train_loss": [], "train_dice": [], "train_iou": [], "test_loss": [], "test_dice": [], "test_iou": [],
                "learning_rates": []}
     rank0 = not (dist.is_available() and dist.is_initialized()) or dist.get_rank() == 0
@@ -148,6 +252,10 @@ def train_model(model, train_loader, test_loader, criterion, optimizer, schedule
         start, past = load_checkpoint(resume_from, model, optimizer, scheduler, map_location=device)
         for k in history:
             history[k] = list(past.get(k, []))
+    use_graph = graph is not False and _graphable(model, optimizer, device, criterion)
+    if graph and not use_graph:
+        raise ValueError("train_model(graph=True) needs a csu model on a GPU and csu.optim.FusedAdamW")
+    cache = _graph_cache(model) if use_graph else None
     for epoch in range(start, num_epochs):
         model.train()
         sampler = getattr(train_loader, "sampler", None)
@@ -160,9 +268,18 @@ def train_model(model, train_loader, test_loader, criterion, optimizer, schedule
         for images, masks in it:
             images = images.to(device, non_blocking=True)
             masks = masks.to(device, non_blocking=True)
-            stats.append(train_step(model, images, masks, criterion, optimizer, amp_dtype=amp_dtype))
+            if use_graph:
+                key = ("train", tuple(images.shape), tuple(masks.shape), amp_dtype, criterion, id(optimizer),
+                       id(reducer))
+                g = cache.get(key)
+                if g is None:
+                    g = cache[key] = _GraphedTrain(model, optimizer, criterion, amp_dtype, reducer)
+                stats.append(g(images, masks))
+            else:
+                stats.append(train_step(model, images, masks, criterion, optimizer, reducer, amp_dtype=amp_dtype))
         train_loss, train_dice, train_iou = _epoch_means(stats)
-        test_loss, test_dice, test_iou = evaluate_model(model, test_loader, criterion, device, amp_dtype=amp_dtype)
+        test_loss, test_dice, test_iou = evaluate_model(model, test_loader, criterion, device, amp_dtype=amp_dtype,
+                                                        graph=use_graph)
         if scheduler is not None:
             scheduler.step(test_loss)
             if hasattr(optimizer, "sync_lr"):   # FusedAdamW: the device lr a captured step reads

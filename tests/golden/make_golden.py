@@ -273,61 +273,81 @@ def f7_contract(R, RU):
     print("wrote f7_contract.json", {k: len(v) for k, v in res.items()})
 
 
-def f8_trajectory(R, steps=120, batch=8, size=128):
-    """fp32 AdamW(1e-4, wd 1e-4) trajectory on the synthetic generator (cswin:775-806, 937-941)."""
-    torch.set_num_threads(8)
-    cfg = O.CSWinConfig(img_size=size, split_size=(1, 2, 4, 4))
+TRAJ = {
+    # name: (file, img_size, split_size, batch, steps, eval_every, eval_n)
+    "f8": ("f8_trajectory", 128, (1, 2, 4, 4), 8, 400, 20, 16),
+    # F11: the headline geometry (BASELINE configs[2]: 512x512, split [1,2,8,8]) at B4
+    "f11": ("f11_trajectory_512", 512, (1, 2, 8, 8), 4, 300, 20, 8),
+}
+
+
+def trajectory(R, name, amp="fp32", threads=8):
+    """AdamW(1e-4, wd 1e-4) trajectory of the reference model on the synthetic generator
+    (cswin:775-806, 937-941; metrics cswin:692-708, eval cswin:712-747).  ``amp="bf16"`` runs the
+    reference's forward under CPU bf16 autocast (loss in fp32): the reference's own fp32-vs-bf16
+    spread, which sets from which step a "Dice within 1e-3" gate is meaningful."""
+    fname, size, split, batch, steps, every, n_eval = TRAJ[name]
+    torch.set_num_threads(threads)
+    cfg = O.CSWinConfig(img_size=size, split_size=split)
     m = ref_model(R, cfg)
     m.load_state_dict(O.recipe_params(cfg, seed=0))
     opt = torch.optim.AdamW(m.parameters(), lr=1e-4, weight_decay=1e-4)
     crit = nn.BCELoss()
     from csu.data import ellipse_batch
     rng = np.random.default_rng(1234)
-    xe, te = ellipse_batch(np.random.default_rng(99), 16, size)
+    xe, te = ellipse_batch(np.random.default_rng(99), n_eval, size)
     rec = {"loss": [], "dice": [], "iou": [], "eval_step": [], "eval_loss": [], "eval_dice": [], "eval_iou": []}
+    ac = torch.autocast("cpu", dtype=torch.bfloat16, enabled=amp == "bf16")
     t0 = time.time()
     for step in range(1, steps + 1):
         x, t = ellipse_batch(rng, batch, size)
         m.train()
         opt.zero_grad()
-        y = m(x)
-        loss = crit(y, t)
+        with ac:
+            y = m(x)
+        loss = crit(y.float(), t)
         loss.backward()
         opt.step()
         with torch.no_grad():
-            pred = (y > 0.5).float()
+            pred = (y.float() > 0.5).float()
             rec["loss"].append(loss.item())
             rec["dice"].append(R.dice_coefficient(pred, t))
             rec["iou"].append(R.iou_score(pred, t))
-        if step % 20 == 0:
+        if step % every == 0:
             m.eval()
-            with torch.no_grad():
-                ye = m(xe)
-                rec["eval_step"].append(step)
-                rec["eval_loss"].append(crit(ye, te).item())
-                pe = (ye > 0.5).float()
-                rec["eval_dice"].append(R.dice_coefficient(pe, te))
-                rec["eval_iou"].append(R.iou_score(pe, te))
-            print(f"step {step} loss {loss.item():.4f} eval dice {rec['eval_dice'][-1]:.5f} ({time.time() - t0:.0f}s)")
-    with open(os.path.join(HERE, "f8_trajectory.json"), "w") as f:
-        json.dump({"config": {"img_size": size, "split_size": [1, 2, 4, 4], "batch": batch, "steps": steps,
+            with torch.no_grad(), ac:
+                ye = m(xe).float()
+            rec["eval_step"].append(step)
+            rec["eval_loss"].append(crit(ye, te).item())
+            pe = (ye > 0.5).float()
+            rec["eval_dice"].append(R.dice_coefficient(pe, te))
+            rec["eval_iou"].append(R.iou_score(pe, te))
+            print(f"[{name} {amp}] step {step} loss {loss.item():.4f} eval dice {rec['eval_dice'][-1]:.5f} "
+                  f"({time.time() - t0:.0f}s)", flush=True)
+    out = os.path.join(HERE, fname + ("" if amp == "fp32" else "_" + amp) + ".json")
+    with open(out, "w") as f:
+        json.dump({"config": {"img_size": size, "split_size": list(split), "batch": batch, "steps": steps,
+                              "eval_every": every, "eval_n": n_eval, "amp": amp,
                               "lr": 1e-4, "weight_decay": 1e-4, "seed_weights": 0, "train_rng": 1234, "eval_rng": 99},
                    **rec}, f)
+    print("wrote", out)
 
 
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--skip-traj", action="store_true")
     ap.add_argument("--only", default="")
+    ap.add_argument("--amp", default="fp32", choices=["fp32", "bf16"], help="trajectories (f8, f11) only")
+    ap.add_argument("--threads", type=int, default=8)
     a = ap.parse_args()
     R, RU = load_reference()
     jobs = {"f1": lambda: f1_lepe(R), "f2": lambda: f2_block(R), "f3": lambda: f3_modules(R), "f4": lambda: f4_model(R),
             "f5": lambda: f5_metrics(R), "f6": lambda: f6_unet(RU), "f7": lambda: f7_contract(R, RU),
-            "f8": lambda: f8_trajectory(R), "f9": lambda: f9_dropout(R),
-            "f10": lambda: f10_augment(R)}
+            "f8": lambda: trajectory(R, "f8", a.amp, a.threads), "f9": lambda: f9_dropout(R),
+            "f10": lambda: f10_augment(R), "f11": lambda: trajectory(R, "f11", a.amp, a.threads)}
     for k, fn in jobs.items():
         if a.only and k not in a.only.split(","):
             continue
-        if k == "f8" and a.skip_traj:
-            continue
+        if k in ("f8", "f11") and (a.skip_traj or not a.only):
+            continue                      # trajectories are slow: run them explicitly (--only f8 / f11)
         fn()

@@ -96,7 +96,8 @@ def test_segmentation_dataset(tmp_path):
     ds = SegmentationDataset(str(tmp_path / "img"), str(tmp_path / "mask"), image_size=(32, 24))
     assert len(ds) == 3 and [os.path.basename(p) for p in ds.image_paths] == ["a.jpg", "b.jpg", "c.jpg"]
     x, m = ds[0]
-    assert x.shape == (3, 32, 24) and m.shape == (1, 32, 24) and x.dtype == torch.float32
+    # image_size is cv2's dsize = (width, height) (cswin:160-161): (32, 24) -> 24 rows x 32 columns
+    assert x.shape == (3, 24, 32) and m.shape == (1, 24, 32) and x.dtype == torch.float32
     assert 0 <= x.min() and x.max() <= 1 and m.max() > 0.5
     x, m = ds[1]                                        # missing mask -> zeros (cswin:155-157)
     assert float(m.abs().max()) == 0.0

@@ -41,6 +41,8 @@ ATTN_CASES = [
     (16, -1, 16, 64, 2, 1), (32, -1, 32, 32, 1, 1), (64, 1, 2, 64, 2, 1), (56, 0, 1, 32, 1, 1),
     # 1024x1024-class windows held whole in LDS: 512 (stage 3, split 8), ragged 400 / 576, 1024 (stage 4)
     (64, 0, 8, 64, 2, 1), (20, -1, 20, 32, 1, 2), (24, -1, 24, 64, 2, 1), (32, -1, 32, 128, 4, 1),
+    # the 512x512 headline's stage-1 (reso 128, width-1 stripes of 128 tokens, cswin:232-237) and stage-2 windows
+    (128, 0, 1, 32, 1, 1), (128, 1, 1, 32, 1, 1), (64, 0, 2, 64, 2, 1),
 ]
 
 
@@ -742,6 +744,21 @@ def test_bce_loss_vs_torch(n):
     lb.backward()
     torch.testing.assert_close(pa.grad, pb.grad, rtol=1e-6, atol=0)
     assert torch.equal(ops.bce_loss(p, t), ops.bce_loss(p, t))
+
+
+def test_bce_loss_tiny_probabilities():
+    """p in 1e-9..1e-6 with target 0: ATen's log1p(-p) term is ~p, which logf(1 - p) rounds to 0 --
+    a low-loss batch (a well-trained background) must not drift from torch's loss."""
+    from csu import ops
+    d = dev()
+    p = torch.logspace(-9, -6, 4096, device=d)
+    t = torch.zeros_like(p)
+    t[::7] = 1.0
+    p[::7] = 1.0 - p[::7]
+    la = ops.bce_loss(p, t)
+    lb = torch.nn.functional.binary_cross_entropy(p, t)
+    assert float(lb) > 0
+    torch.testing.assert_close(la, lb, rtol=1e-5, atol=0)
 
 
 def test_pack_nhwc_image():

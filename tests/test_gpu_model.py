@@ -91,6 +91,61 @@ def test_whole_model_bf16_vs_oracle(golden_dir):
     np.testing.assert_allclose(gn[big], gref[big], rtol=5e-2)
 
 
+def _oracle_step(p, cfg, x, t):
+    """fp64 oracle forward + BCE + backward on the CPU: (probabilities, loss, {name: grad})."""
+    pref = {k: v.double().requires_grad_(True) for k, v in p.items()}
+    yr = O.cswin_forward(pref, x.double(), cfg)
+    lr = O.bce_loss(yr, t.double())
+    lr.backward()
+    return yr.detach(), float(lr), {k: v.grad for k, v in pref.items()}
+
+
+@pytest.mark.parametrize("img,batch,amp", [(256, 2, None), (512, 1, torch.bfloat16)],
+                         ids=["cfg2_256_fp32_B2", "cfg3_512_bf16_B1"])
+def test_whole_model_baseline_geometry_vs_oracle(img, batch, amp):
+    """The csu model at the BASELINE geometries (split [1,2,8,8], cswin:489-688): config 2 (256x256
+    fp32, "fwd/bwd numerics parity") and config 3's 512x512 bf16 headline, vs the fp64 oracle on the
+    same recipe weights and ellipse batch.  Probabilities, loss and all 463 gradient norms; fp32:
+    1e-4 abs / 1e-5 rel loss / 2e-3 rel norms; bf16 (SURVEY §8c calibration): 1e-2 abs on
+    probabilities, 1e-2 rel loss, 5e-2 rel on norms >= 1e-3 of the largest; plus per-tensor rel-L2
+    <= 2e-2 (fp32: 2e-3) for gradients of the same size class."""
+    from csu.data import ellipse_batch
+    from csu.train import bce_loss
+    d = dev()
+    cfg = O.CSWinConfig(img_size=img, split_size=(1, 2, 8, 8))
+    p = O.recipe_params(cfg, seed=0)
+    m = _model(cfg, d, p)
+    x, t = ellipse_batch(np.random.default_rng(17), batch, img)
+    with torch.autocast("cuda", dtype=amp or torch.float32, enabled=amp is not None):
+        y = m(x.to(d))
+    loss = bce_loss(y, t.to(d))
+    loss.backward()
+    torch.cuda.synchronize()
+    yr, lr, gref = _oracle_step(p, cfg, x, t)
+    params = dict(m.named_parameters())
+    assert len(params) == 463
+    dy = float((y.detach().double().cpu() - yr).abs().max())
+    names = list(params)
+    gn = np.array([params[k].grad.double().norm().item() for k in names])
+    gr = np.array([gref[k].norm().item() for k in names])
+    rel = np.array([(params[k].grad.double().cpu() - gref[k]).norm().item() / max(gref[k].norm().item(), 1e-30)
+                    for k in names])
+    big = gr >= 1e-3 * gr.max()
+    worst = names[int(np.argmax(np.where(big, rel, 0)))]
+    print(f"img {img} B{batch} {'bf16' if amp else 'fp32'}: max|dprob| {dy:.2e}, loss {loss.item():.6f} vs {lr:.6f}, "
+          f"worst grad rel-L2 {rel[big].max():.2e} ({worst}), median {np.median(rel[big]):.2e}")
+    if amp is None:
+        assert dy < 1e-4
+        assert abs(loss.item() - lr) < 1e-5 * lr + 1e-6
+        np.testing.assert_allclose(gn[big], gr[big], rtol=2e-3)
+        assert rel[big].max() < 2e-3, worst
+    else:
+        assert dy < 1e-2
+        assert abs(loss.item() - lr) < 1e-2 * lr
+        np.testing.assert_allclose(gn[big], gr[big], rtol=5e-2)
+        assert np.median(rel[big]) < 2e-2, np.median(rel[big])
+
+
 def test_simam_model_runs_and_differs():
     """simam=True keeps the state_dict contract and changes the output (skips are gated)."""
     from csu.model import CSWinTransformer

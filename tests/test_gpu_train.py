@@ -1,15 +1,24 @@
 """Training-level parity on the MI355X (north_star: "Dice/IoU parity at fixed seed, Dice within
 1e-3 of the reference").
 
-* F8 trajectory: csu CSWinTransformer trained through csu.train.train_model for 120 AdamW steps
-  (128x128, B8, split [1,2,4,4], recipe weights, default_rng(1234) batches; eval every 20 steps on
-  the default_rng(99) batch) vs the reference's own run (tests/golden/f8_trajectory.json, made by
-  tests/golden/make_golden.py:198-237 = cswin:775-811 / 692-747).  Gate: |dDice|, |dIoU| <= 1e-3
-  on the eval batch at steps >= 100 in fp32; bf16 autocast (not what the reference trains in) is
-  gated at the fp32-vs-bf16 spread measured for the reference itself (up to 4.7e-3
-  mid-transient, 4e-4 converged) -> 5e-3.  Per-epoch mean train loss within 2 % (fp32) / 5 % (bf16).
+* F8 / F11 trajectories: the csu CSWinTransformer trained through csu.train.train_model (graph-
+  captured steps) on the reference's own batch stream (recipe weights, default_rng(1234) batches,
+  AdamW 1e-4 / wd 1e-4; eval every 20 steps on a default_rng(99) batch) vs the reference's own run
+  (tests/golden/f8_trajectory.json: 128x128 B8 split [1,2,4,4], 400 steps; f11_trajectory_512.json:
+  the headline geometry 512x512 B4 split [1,2,8,8], 300 steps; made by tests/golden/make_golden.py
+  = cswin:775-811 / 692-747).  The reference was also run under bf16 autocast (the *_bf16.json
+  files).  Its OWN fp32-vs-bf16 spread does not settle at 4e-4 (SURVEY §8c's 120-step estimate):
+  over 400 steps at 128x128 it keeps wandering between 4e-5 and 8.9e-4 in Dice (1.7e-3 in IoU)
+  from step 100 on -- the eval Dice moves by ~1e-3 between checkpoints at lr 1e-4, and any change
+  of rounding shifts that walk.  So the gate applies from the first eval step after which the
+  reference's own spread stays within the north_star tolerance (Dice 1e-3; IoU 2e-3, because for
+  batch-flattened metrics IoU = Dice / (2 - Dice), dIoU/dDice = 2 / (2 - Dice)^2 ~ 1.9) -- the
+  "converged" region -- and there csu (fp32 and bf16 alike) must be within the same tolerances of
+  the reference's fp32 run.  Per-epoch mean train loss within 2 %
+  (fp32) / 5 % (bf16).  Every eval point's deltas are written to $CSU_PARITY_LOG (default
+  gpurun_out/) as dice_parity_<fixture>_<precision>.json.
 * FusedAdamW checkpoints: save -> load -> continue equals the uninterrupted run; the state_dict
-  loads into torch.optim.AdamW.
+  loads into torch.optim.AdamW; a load after a capture keeps the captured step valid.
 * HIP-graph replays are bitwise reproducible across two independent captures.
 * Deep config (depth [2,4,32,2]) vs the oracle."""
 import copy
@@ -24,6 +33,9 @@ pytestmark = pytest.mark.gpu
 
 from oracle import cswin_ref as O
 
+DICE_TOL = 1e-3    # north_star: "Dice within 1e-3 of the reference"
+IOU_TOL = 2e-3     # the same tolerance carried to IoU = Dice / (2 - Dice) (dIoU/dDice ~ 1.9 at Dice ~ 0.98)
+
 
 def dev():
     if not torch.cuda.is_available():
@@ -32,56 +44,94 @@ def dev():
 
 
 class _Stream:
-    """The F8 batch stream: epoch e yields batches [20e, 20e + 20) of default_rng(1234)."""
+    """The fixture's batch stream, drawn lazily: epoch e yields batches [n*e, n*e + n) of
+    default_rng(train_rng) (the reference's order)."""
 
-    def __init__(self, batches, per_epoch=20):
-        self.batches, self.per_epoch, self.pos = batches, per_epoch, 0
+    def __init__(self, seed, batch, size, per_epoch):
+        self.rng, self.batch, self.size, self.per_epoch = np.random.default_rng(seed), batch, size, per_epoch
 
     def __iter__(self):
-        out = self.batches[self.pos:self.pos + self.per_epoch]
-        self.pos += self.per_epoch
-        return iter(out)
+        from csu.data import ellipse_batch
+        return iter([ellipse_batch(self.rng, self.batch, self.size) for _ in range(self.per_epoch)])
 
 
-def _f8_run(golden_dir, amp_dtype):
+def gate_step(ref, refb):
+    """First eval step from which the reference's own fp32-vs-bf16 |dDice| and |dIoU| stay within
+    DICE_TOL / IOU_TOL."""
+    ok = [abs(a - b) <= DICE_TOL and abs(c - e) <= IOU_TOL
+          for a, b, c, e in zip(ref["eval_dice"], refb["eval_dice"], ref["eval_iou"], refb["eval_iou"])]
+    i = len(ok)
+    while i > 0 and ok[i - 1]:
+        i -= 1
+    return ref["eval_step"][i] if i < len(ok) else None
+
+
+def _traj_run(golden_dir, fixture, amp_dtype):
     from csu.data import ellipse_batch
     from csu.model import CSWinTransformer
     from csu.train import bce_loss, make_optimizer, train_model
     d = dev()
-    ref = json.load(open(os.path.join(golden_dir, "f8_trajectory.json")))
+    ref = json.load(open(os.path.join(golden_dir, fixture + ".json")))
+    refb = json.load(open(os.path.join(golden_dir, fixture + "_bf16.json")))
     c = ref["config"]
+    every = c.get("eval_every", 20)
     cfg = O.CSWinConfig(img_size=c["img_size"], split_size=tuple(c["split_size"]))
     m = CSWinTransformer(img_size=c["img_size"], split_size=list(c["split_size"])).to(d)
     m.load_state_dict(O.recipe_params(cfg, seed=c["seed_weights"]))
-    rng = np.random.default_rng(c["train_rng"])
-    batches = [ellipse_batch(rng, c["batch"], c["img_size"]) for _ in range(c["steps"])]
-    test = [ellipse_batch(np.random.default_rng(c["eval_rng"]), 16, c["img_size"])]
+    test = [ellipse_batch(np.random.default_rng(c["eval_rng"]), c.get("eval_n", 16), c["img_size"])]
     opt = make_optimizer(m, lr=c["lr"], weight_decay=c["weight_decay"])
-    epochs = c["steps"] // 20
-    h = train_model(m, _Stream(batches), test, bce_loss, opt, None, d, num_epochs=epochs, verbose=False,
-                    amp_dtype=amp_dtype)
-    return ref, h
+    h = train_model(m, _Stream(c["train_rng"], c["batch"], c["img_size"], every), test, bce_loss, opt, None, d,
+                    num_epochs=c["steps"] // every, verbose=False, amp_dtype=amp_dtype)
+    return ref, refb, h
+
+
+def _check_trajectory(golden_dir, fixture, amp):
+    ref, refb, h = _traj_run(golden_dir, fixture, amp)
+    steps = ref["eval_step"]
+    every = ref["config"].get("eval_every", 20)
+    assert len(h["test_dice"]) == len(steps)
+    g = gate_step(ref, refb)
+    assert g is not None and sum(s >= g for s in steps) >= 3, \
+        f"{fixture}: the reference's own fp32/bf16 spread never settles within the tolerance for 3 eval points"
+    ltol = 0.02 if amp is None else 0.05
+    rows, bad = [], []
+    for i, s in enumerate(steps):
+        dd = abs(h["test_dice"][i] - ref["eval_dice"][i])
+        di = abs(h["test_iou"][i] - ref["eval_iou"][i])
+        mean_ref = float(np.mean(ref["loss"][every * i:every * i + every]))
+        rows.append({"step": s, "gated": s >= g, "csu_dice": h["test_dice"][i], "ref_dice": ref["eval_dice"][i],
+                     "ref_bf16_dice": refb["eval_dice"][i], "abs_d_dice": dd,
+                     "ref_own_spread_dice": abs(ref["eval_dice"][i] - refb["eval_dice"][i]),
+                     "ref_own_spread_iou": abs(ref["eval_iou"][i] - refb["eval_iou"][i]), "csu_iou": h["test_iou"][i],
+                     "ref_iou": ref["eval_iou"][i], "abs_d_iou": di, "csu_eval_loss": h["test_loss"][i],
+                     "ref_eval_loss": ref["eval_loss"][i], "csu_train_loss": h["train_loss"][i],
+                     "ref_train_loss": mean_ref})
+        if s >= g and (dd > DICE_TOL or di > IOU_TOL):
+            bad.append(f"step {s}: |dDice| {dd:.2e} |dIoU| {di:.2e}")
+        if abs(h["train_loss"][i] - mean_ref) > ltol * mean_ref:
+            bad.append(f"epoch {i}: train loss {h['train_loss'][i]:.5f} vs {mean_ref:.5f}")
+    prec = "fp32" if amp is None else "bf16"
+    gated = [r for r in rows if r["gated"]]
+    log = {"fixture": fixture, "precision": prec, "config": ref["config"], "gate_from_step": g, "dice_tolerance": DICE_TOL,
+           "iou_tolerance": IOU_TOL, "max_gated_abs_d_dice": max(r["abs_d_dice"] for r in gated),
+           "max_gated_abs_d_iou": max(r["abs_d_iou"] for r in gated), "rows": rows}
+    out = os.environ.get("CSU_PARITY_LOG", "gpurun_out")
+    os.makedirs(out, exist_ok=True)
+    with open(os.path.join(out, f"dice_parity_{fixture}_{prec}.json"), "w") as f:
+        json.dump(log, f, indent=1)
+    print(f"{fixture} {prec}: gate from step {g}, max |dDice| {log['max_gated_abs_d_dice']:.2e}, "
+          f"max |dIoU| {log['max_gated_abs_d_iou']:.2e}")
+    assert not bad, "\n".join(bad)
 
 
 @pytest.mark.parametrize("amp", [None, torch.bfloat16], ids=["fp32", "bf16"])
 def test_f8_dice_iou_trajectory(golden_dir, amp):
-    ref, h = _f8_run(golden_dir, amp)
-    steps = ref["eval_step"]
-    assert len(h["test_dice"]) == len(steps)
-    tol = 1e-3 if amp is None else 5e-3
-    ltol = 0.02 if amp is None else 0.05
-    report = []
-    for i, s in enumerate(steps):
-        dd = abs(h["test_dice"][i] - ref["eval_dice"][i])
-        di = abs(h["test_iou"][i] - ref["eval_iou"][i])
-        report.append(f"step {s}: dice {h['test_dice'][i]:.5f} vs {ref['eval_dice'][i]:.5f} (|d| {dd:.1e}), "
-                      f"iou {h['test_iou'][i]:.5f} vs {ref['eval_iou'][i]:.5f} (|d| {di:.1e}), "
-                      f"eval loss {h['test_loss'][i]:.5f} vs {ref['eval_loss'][i]:.5f}")
-        if s >= 100:
-            assert dd <= tol and di <= tol, "\n".join(report)
-        mean_ref = float(np.mean(ref["loss"][20 * i:20 * i + 20]))
-        assert abs(h["train_loss"][i] - mean_ref) <= ltol * mean_ref, "\n".join(report)
-    print("\n".join(report))
+    _check_trajectory(golden_dir, "f8_trajectory", amp)
+
+
+def test_f11_dice_iou_trajectory_512_bf16(golden_dir):
+    """The headline configuration's geometry and precision: 512x512 split [1,2,8,8], bf16."""
+    _check_trajectory(golden_dir, "f11_trajectory_512", torch.bfloat16)
 
 
 def test_fused_adamw_checkpoint_resume_and_torch_interop(tmp_path):
@@ -127,6 +177,58 @@ def test_fused_adamw_checkpoint_resume_and_torch_interop(tmp_path):
     assert {float(s["step"]) for s in ot.state_dict()["state"].values()} == {6.0}
     for pa, pt in zip(a.parameters(), t.parameters()):
         torch.testing.assert_close(pt, pa, rtol=1e-5, atol=1e-6)
+
+
+def test_optimizer_load_after_capture_keeps_graph_valid():
+    """FusedAdamW.load_state_dict after a HIP-graph capture copies the loaded moments / step / lr
+    into the tensors the captured step reads: rewinding model + optimizer to an earlier checkpoint
+    and replaying the same batches reproduces the original replays bitwise."""
+    from csu.data import ellipse_batch
+    from csu.model import CSWinTransformer
+    from csu.train import GraphedTrainStep, bce_loss, make_optimizer
+    d = dev()
+    torch.manual_seed(0)
+    m = CSWinTransformer(img_size=128, split_size=[1, 2, 4, 4]).to(d)
+    opt = make_optimizer(m, capturable=True)
+    rng = np.random.default_rng(4)
+    b = [tuple(v.to(d) for v in ellipse_batch(rng, 2, 128)) for _ in range(4)]
+    gs = GraphedTrainStep(m, opt, bce_loss, b[0][0], b[0][1], torch.bfloat16, warmup=1)
+    gs(*b[0])
+    gs(*b[1])
+    sd_m = copy.deepcopy(m.state_dict())
+    sd_o = copy.deepcopy(opt.state_dict())
+    la = [float(gs(*b[i])[0].item()) for i in (2, 3)]
+    pa = [p.detach().clone() for p in m.parameters()]
+    m.load_state_dict(sd_m)
+    opt.load_state_dict(sd_o)
+    lb = [float(gs(*b[i])[0].item()) for i in (2, 3)]
+    torch.cuda.synchronize()
+    assert la == lb
+    assert all(torch.equal(x, y) for x, y in zip(pa, m.parameters()))
+
+
+def test_train_model_graphed_equals_eager():
+    """train_model's captured path (graph=None on a GPU: two eager steps, then one replayed graph per
+    batch shape, incl. a ragged last batch run eagerly; eval replayed too) == graph=False."""
+    from csu.data import ellipse_batch
+    from csu.model import CSWinTransformer
+    from csu.train import bce_loss, make_optimizer, train_model
+    d = dev()
+    torch.manual_seed(0)
+    m0 = CSWinTransformer(img_size=128, split_size=[1, 2, 4, 4])
+    rng = np.random.default_rng(8)
+    train = [ellipse_batch(rng, 4, 128) for _ in range(5)] + [ellipse_batch(rng, 2, 128)]
+    test = [ellipse_batch(rng, 4, 128), ellipse_batch(rng, 3, 128)]
+    hs, ps = [], []
+    for graph in (None, False):
+        m = copy.deepcopy(m0).to(d)
+        opt = make_optimizer(m)
+        hs.append(train_model(m, train, test, bce_loss, opt, None, d, num_epochs=2, verbose=False, graph=graph))
+        ps.append([p.detach().clone() for p in m.parameters()])
+    for k in hs[0]:
+        np.testing.assert_allclose(hs[0][k], hs[1][k], rtol=1e-5, atol=1e-6, err_msg=k)
+    for a, b in zip(*ps):
+        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-5)
 
 
 @pytest.mark.parametrize("side_in_graph", [False, True])
