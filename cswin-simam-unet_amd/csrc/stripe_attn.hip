@@ -1336,6 +1336,293 @@ __global__ __launch_bounds__(NT) void stripe_bwd_dkdv_w(csu_stripe_args a, int s
     ATT_STAMP(2, 2);
 }
 
+// =============================================================================================
+// v3 one-pass backward (bf16, windows of <= 256 tokens: every stage of the 512x512 model, stages
+// 1-2 of the 1024x1024 one).  ONE workgroup per (branch, image, window, head) stages Q, K, V and
+// dO of the whole window once (swizzled images, 4 x 16 KiB) and produces dQ, dK, dV, the LePE
+// input gradient AND the LePE weight-gradient partials -- v2 needed two kernels that each staged
+// the window and recomputed P, plus a third kernel re-reading V and dO for the LePE weights.
+//   prologue: delta = rowsum(dO * (O - LePE(V))) and the per-window LePE weight-gradient partials
+//             sum_q dO[q] * V[q + tap] from the V / dO images (thread = channel quad x row group)
+//   main loop over 32-query tiles (all waves in step): the key is on the lane -- wave w owns key
+//             tiles w, w + 4 (dK^T, dV^T of its 64 keys stay in accumulators).  S and dP start from
+//             the row constants -lse/scale and -delta (no subtraction per score), P = exp2(c S),
+//             dS = P dP; dV^T += dO^T P, dK^T += Q^T dS take the accumulators as operands.  dS
+//             goes to LDS once ([key][query] image in the V image's space, which the prologue
+//             freed); after a barrier each wave computes a 16 x 16 quadrant of dQ^T = K^T dS over
+//             ALL keys (16x16x32 MFMAs, K^T fragments held in registers), so dQ needs no sum
+//             across waves or workgroups and is written once, deterministic.
+// Algorithmic bytes per launch are v2's minus the delta round trip and the LePE kernel's re-read.
+// =============================================================================================
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+
+// 16x16x32 operand from a [k][c] swizzled image read column-wise (T10): lane l gets
+// image[kb + 8 (l >> 4) + j][cb + (l & 15)], j = 0..7 -- A[m = c][k] or B[k][n = c]
+__device__ __forceinline__ bf16x8 tr_frag16(const bf16* img, int kb, int cb, int lane) {
+    const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+    const v4s lo = tr_read(img + swz(kb + 8 * g + q, cb + 4 * p));
+    const v4s hi = tr_read(img + swz(kb + 8 * g + 4 + q, cb + 4 * p));
+    const v4s v[2] = {lo, hi};
+    bf16x8 out;
+    __builtin_memcpy(&out, v, 16);
+    return out;
+}
+
+template <int WM, bool DROP>
+__global__ __launch_bounds__(NT, 2) void stripe_bwd_fused_w(csu_stripe_args a, const bf16* __restrict__ qkv,
+                                                            const bf16* __restrict__ out, const bf16* __restrict__ dout,
+                                                            const float* __restrict__ lse, bf16* __restrict__ dqkv,
+                                                            float* __restrict__ part) {
+    constexpr int KT = WM / 128;          // key tiles per wave
+    constexpr int RT = WM / 32;           // rows per thread in the prologue / 32-row tiles of the image
+    __shared__ __attribute__((aligned(16))) bf16 Qs[WM * HD];
+    __shared__ __attribute__((aligned(16))) bf16 Ks[WM * HD];
+    __shared__ __attribute__((aligned(16))) bf16 Vs[WM * HD];   // V image; from the main loop on: dS tile [key][q]
+    __shared__ __attribute__((aligned(16))) bf16 Gs[WM * HD];   // dO image
+    __shared__ __attribute__((aligned(16))) float lse_s[WM], dl_s[WM];
+    __shared__ __attribute__((aligned(16))) float wts[HD * 10];
+    __shared__ float red[4][8][41];
+    __shared__ __attribute__((aligned(16))) unsigned char dtbl[4][128];
+    ATT_STAMP(1, 0);
+    const Win w = decode_w(a, 1);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int r = lane & 31, h = lane >> 5;
+    const int L = a.reso * a.reso, C = a.C, C3 = 3 * C;
+    const bf16* img = qkv + (size_t)w.b * L * C3;
+    const bf16* gimg = dout + (size_t)w.b * L * C;
+    const int npad = (w.N + 31) & ~31, ntile = npad >> 5;
+    const float inv_scale = 1.f / a.scale;
+
+    // ---- staging: Q, K, V, dO images, the window's lse (as -lse / scale: the S accumulators' start)
+    {
+        const __amdgpu_buffer_rsrc_t rs_lse = stat_rsrc(a, lse);
+        float lv[RT / 8 > 0 ? RT / 8 : 1];
+#pragma unroll
+        for (int k = 0; k < WM / NT; ++k) {
+            const int i = threadIdx.x + k * NT;
+            lv[k] = ldf_rs(rs_lse, i < w.N ? (unsigned)(stat_index(a, w, tok_of(w, a.reso, i)) * 4) : kOOB);
+        }
+        float lw[LW_IT];
+        lepe_weights_load(branch(a, w.br), w.h, lw);
+        stage_win2(w, a.reso, img, C3, w.chq, img, C3, C + w.chq, npad, Qs, Ks);
+        stage_win2(w, a.reso, img, C3, 2 * C + w.chq, gimg, C, w.chq, npad, Vs, Gs);
+        lepe_weights_store(lw, wts);
+#pragma unroll
+        for (int k = 0; k < WM / NT; ++k) {
+            const int i = threadIdx.x + k * NT;
+            if (i < npad) lse_s[i] = i < w.N ? -lv[k] * inv_scale : -INFINITY;   // padded queries: P = 0
+        }
+    }
+    __syncthreads();
+    ATT_STAMP(1, 1);
+
+    // ---- prologue: delta and the LePE weight-gradient partials (thread: channel quad c4, rows rg + 32k)
+    {
+        const int c4 = threadIdx.x & 7, rg = threadIdx.x >> 3;
+        float wacc[40];
+#pragma unroll
+        for (int i = 0; i < 40; ++i) wacc[i] = 0.f;
+        const f32x4 bias = *reinterpret_cast<const f32x4*>(wts + HD * 9 + 4 * c4);
+        const __amdgpu_buffer_rsrc_t rs_o = buf_rsrc(out + (size_t)w.b * L * C, (long)L * C * 2);
+        auto load_o = [&](int n) {
+            return __builtin_amdgcn_raw_buffer_load_b64(
+                rs_o, n < w.N ? (unsigned)(((size_t)tok_of(w, a.reso, n) * C + w.chq + 4 * c4) * 2) : kOOB, 0, 0);
+        };
+        u32x2 o_next = load_o(rg), o_next2 = load_o(rg + 32);   // O rows two ahead
+        // rows one at a time (unrolled, the compiler turns the 40 accumulations into per-sum chains
+        // over all rows and keeps every row's V values live)
+#pragma unroll 1
+        for (int n = rg; n < npad; n += 32) {
+            const bool valid = n < w.N;                    // uniform over the 8 lanes of the row
+            const int nn = valid ? n : 0;
+            const u32x2 oraw = o_next;
+            o_next = o_next2;
+            o_next2 = load_o(n + 64);
+            const int iy = wrow(w, nn), ix = nn - iy * w.W_sp;
+            const bf16x4 g4 = *reinterpret_cast<const bf16x4*>(Gs + swz(nn, 4 * c4));
+            float gv[4], lp[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                gv[j] = valid ? (float)g4[j] : 0.f;
+                lp[j] = bias[j];
+            }
+#pragma unroll
+            for (int t = 0; t < 9; ++t) {
+                const int y = iy + t / 3 - 1, x = ix + t % 3 - 1;
+                const bool in = y >= 0 && y < w.H_sp && x >= 0 && x < w.W_sp;
+                const bf16x4 v4 = *reinterpret_cast<const bf16x4*>(Vs + swz(in ? y * w.W_sp + x : nn, 4 * c4));
+                const f32x4 wt = *reinterpret_cast<const f32x4*>(wts + t * HD + 4 * c4);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const float v = in ? (float)v4[j] : 0.f;
+                    lp[j] = fmaf(wt[j], v, lp[j]);
+                    wacc[4 * t + j] = fmaf(gv[j], v, wacc[4 * t + j]);
+                }
+            }
+            bf16x4 o4;
+            __builtin_memcpy(&o4, &oraw, 8);
+            float dl = 0.f;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                wacc[36 + j] += gv[j];
+                dl = fmaf(gv[j], (float)o4[j] - lp[j], dl);
+            }
+            dl += __shfl_xor(dl, 1, 64);
+            dl += __shfl_xor(dl, 2, 64);
+            dl += __shfl_xor(dl, 4, 64);
+            if (c4 == 0) dl_s[n] = dl;                     // padded rows: 0
+        }
+        if (part) {
+#pragma unroll
+            for (int m = 8; m < 64; m <<= 1)
+#pragma unroll
+                for (int i = 0; i < 40; ++i) wacc[i] += __shfl_xor(wacc[i], m, 64);
+            if (lane < 8)
+#pragma unroll
+                for (int i = 0; i < 40; ++i) red[wave][lane][i] = wacc[i];
+        }
+    }
+    // ---- registers for the main loop (loaded after the prologue, before the V image is overwritten):
+    // the own key tiles' K and V rows (B operands of S and dP)
+    const int dh = wave & 1, qh = wave >> 1;
+    Frag<bf16> kf[KT], vf[KT];
+#pragma unroll
+    for (int j = 0; j < KT; ++j) {
+        const int kt = wave + 4 * j;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            const int row = (kt < ntile ? kt : 0) * 32 + r;
+            kf[j].v[s] = *reinterpret_cast<const bf16x8*>(Ks + swz(row, 16 * s + 8 * h));
+            vf[j].v[s] = *reinterpret_cast<const bf16x8*>(Vs + swz(row, 16 * s + 8 * h));
+        }
+    }
+
+    __syncthreads();   // dl_s / red complete; every read of the V image is done (it becomes the dS tile)
+    if (part) {
+        const int nwx = a.reso / w.W_sp, nwin = (a.reso / w.H_sp) * nwx;
+        const int Cb = a.heads * HD, nblk = a.B * nwin, blk = w.b * nwin + w.wy * nwx + w.wx;
+        for (int o = threadIdx.x; o < 8 * 40; o += NT) {
+            const int qq = o / 40, i = o % 40;
+            const float sum = ((red[0][qq][i] + red[1][qq][i]) + red[2][qq][i]) + red[3][qq][i];
+            const int k = i >> 2, c = w.h * HD + 4 * qq + (i & 3);
+            part[((size_t)w.br * Cb * 10 + c * 10 + k) * nblk + blk] = sum;
+        }
+    }
+
+    // ---- main loop over query tiles
+    const float c = a.scale * kLog2e;
+    ADrop dr;
+    if constexpr (DROP) dr = attn_drop(a, w);
+    f32x16 dk[KT], dv[KT];
+#pragma unroll
+    for (int j = 0; j < KT; ++j) { dk[j] = f32x16{}; dv[j] = f32x16{}; }
+    bf16* const dS = Vs;
+    for (int qt = 0; qt < ntile; ++qt) {
+        const int qb = qt * 32;
+#pragma unroll
+        for (int j = 0; j < KT; ++j) {
+            const int kt = wave + 4 * j;
+            if (kt >= ntile) continue;                     // wave-uniform
+            f32x16 s, dp;
+#pragma unroll
+            for (int g4 = 0; g4 < 4; ++g4) {              // rows qb + 8 g4 + 4 h + 0..3
+                const f32x4 lq = *reinterpret_cast<const f32x4*>(lse_s + qb + 8 * g4 + 4 * h);
+                const f32x4 dq4 = *reinterpret_cast<const f32x4*>(dl_s + qb + 8 * g4 + 4 * h);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    s[4 * g4 + e] = lq[e];
+                    dp[4 * g4 + e] = DROP ? 0.f : -dq4[e];
+                }
+            }
+            mma_rows_sw(s, Qs, qb, r, h, kf[j]);           // S - lse/scale      [q][key]
+            mma_rows_sw(dp, Gs, qb, r, h, vf[j]);          // dP - delta         [q][key]
+            unsigned km = 0xffffu;
+            if constexpr (DROP) {
+                km = keep_k16(dr, qb, kt * 32, lane, dtbl[wave]);
+#pragma unroll
+                for (int g4 = 0; g4 < 4; ++g4) {
+                    const f32x4 dq4 = *reinterpret_cast<const f32x4*>(dl_s + qb + 8 * g4 + 4 * h);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const int i = 4 * g4 + e;
+                        dp[i] = (((km >> i) & 1u) ? dp[i] * dr.R.scale : 0.f) - dq4[e];
+                    }
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const float p = __builtin_amdgcn_exp2f(s[i] * c);
+                dp[i] = p * dp[i];                         // dS
+                if constexpr (DROP) s[i] = ((km >> i) & 1u) ? p * dr.R.scale : 0.f;   // dV sees the dropped P
+                else s[i] = p;
+            }
+            mma_acc_sw(dv[j], Gs, qb, lane, s);            // dV^T += dO^T P
+            mma_acc_sw(dk[j], Qs, qb, lane, dp);           // dK^T += Q^T dS
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {                  // dS -> [key][q] image: q = 8 g + 4 h + 0..3
+                const bf16x4 x = {(bf16)dp[4 * g], (bf16)dp[4 * g + 1], (bf16)dp[4 * g + 2], (bf16)dp[4 * g + 3]};
+                *reinterpret_cast<bf16x4*>(dS + swz(kt * 32 + r, 8 * g + 4 * h)) = x;
+            }
+        }
+        __syncthreads();
+        // dQ^T[d][q] quadrant (d = 16 dh + 4 (lane >> 4) + i, q = qb + 16 qh + (lane & 15)) over all keys
+        f32x4v acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kk = 0; kk < RT; ++kk)
+            if (kk < ntile)
+                acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr_frag16(Ks, kk * 32, 16 * dh, lane),
+                                                              tr_frag16(dS, kk * 32, 16 * qh, lane), acc, 0, 0, 0);
+        {
+            const int qn = qb + 16 * qh + (lane & 15);
+            if (qn < w.N) {
+                const int d0 = 16 * dh + 4 * (lane >> 4);
+                const float v[4] = {acc[0] * a.scale, acc[1] * a.scale, acc[2] * a.scale, acc[3] * a.scale};
+                store4(dqkv + ((size_t)w.b * L + tok_of(w, a.reso, qn)) * C3 + w.chq + d0, v);
+            }
+        }
+        __syncthreads();                                   // the dS tile is rewritten by the next query tile
+    }
+
+    // ---- dK, dV (+ LePE input gradient: the transposed conv of dO) of the own key tiles
+#pragma unroll
+    for (int j = 0; j < KT; ++j) {
+        const int kt = wave + 4 * j, kn = kt * 32 + r;
+        if (kt >= ntile || kn >= w.N) continue;
+        bf16* drow = dqkv + ((size_t)w.b * L + tok_of(w, a.reso, kn)) * C3 + w.chq;
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+            const int d0 = 8 * g4 + 4 * h;
+            float vk[4], vv[4], lp[4];
+            lepe4_lds(w, Gs, kn, d0, wts, -1, lp);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                vk[e] = dk[j][4 * g4 + e] * a.scale;
+                vv[e] = dv[j][4 * g4 + e] + lp[e];
+            }
+            store4(drow + C + d0, vk);
+            store4(drow + 2 * C + d0, vv);
+        }
+    }
+    ATT_STAMP(1, 2);
+}
+
+// the one-pass backward handles the launch (bf16, window <= 256 tokens)
+bool use_fused_bwd(const csu_stripe_args& a, int dtype) {
+    return dtype == CSU_BF16 && a.br[0].H_sp * a.br[0].W_sp <= 256;
+}
+int fused_nblk(const csu_stripe_args& a) {
+    return a.B * (a.reso / a.br[0].H_sp) * (a.reso / a.br[0].W_sp);
+}
+
+template <int WM>
+void bwd_fused(const csu_stripe_args& a, const bf16* qkv, const bf16* out, const bf16* dout, const float* lse, bf16* dqkv,
+               float* part, hipStream_t st) {
+    const int nwin = (a.reso / a.br[0].H_sp) * (a.reso / a.br[0].W_sp);
+    const dim3 g(a.B * nwin * a.heads, a.nbranch);
+    if (a.drop_p > 0.f) stripe_bwd_fused_w<WM, true><<<g, NT, 0, st>>>(a, qkv, out, dout, lse, dqkv, part);
+    else stripe_bwd_fused_w<WM, false><<<g, NT, 0, st>>>(a, qkv, out, dout, lse, dqkv, part);
+}
+
 // split factor of the whole-window kernels: workgroups per window-head, so that a launch has
 // about 1024 workgroups, each owning at least 128 query (key) rows -- one 32-row pass per wave
 // (512x512: 2 at stages 3/4; 1024x1024: 4 at stage 3 (N = 512), 8 at stage 4 (N = 1024))
@@ -1512,6 +1799,7 @@ extern "C" size_t csu_stripe_attn_bwd_workspace(const csu_stripe_args* a) {
     // enough for either partial layout (dtype decided at launch)
     int n = wgrad_blocks(*a);
     for (int dt : {CSU_BF16, CSU_F32}) n = n > lepe_nblk(*a, dt) ? n : lepe_nblk(*a, dt);
+    n = n > fused_nblk(*a) ? n : fused_nblk(*a);
     return (size_t)a->nbranch * n * a->heads * HD * 10 * sizeof(float);
 }
 
@@ -1525,8 +1813,10 @@ extern "C" int csu_stripe_attn_bwd(const csu_stripe_args* a, int dtype, const vo
     return csu_stripe_attn_bwd_ex(a, dtype, qkv, out, dout, lse, delta, dqkv, workspace, workspace_bytes, 0, stream);
 }
 
+// partial blocks csu_stripe_attn_bwd_ex(lepe_deferred = 1) leaves in its workspace
 extern "C" int csu_stripe_lepe_nblk(const csu_stripe_args* a, int dtype) {
-    return a ? lepe_nblk(*a, dtype) : 0;
+    if (!a) return 0;
+    return use_fused_bwd(*a, dtype) ? fused_nblk(*a) : lepe_nblk(*a, dtype);
 }
 
 extern "C" int csu_stripe_lepe_reduce_batch(const csu_lepe_reduce_item* items, int count, void* stream) {
@@ -1579,6 +1869,18 @@ extern "C" int csu_stripe_attn_bwd_ex(const csu_stripe_args* a, int dtype, const
     hipStream_t st = as_stream(stream);
     const dim3 grid = grid_of(*a);
     float* part = (float*)workspace;
+    if (use_fused_bwd(*a, dtype)) {
+        // one pass: dQ, dK, dV and (do_lepe) the LePE weight-gradient partials, reduced below or deferred
+        const bf16 *q = (const bf16*)qkv, *o = (const bf16*)out, *go = (const bf16*)dout;
+        float* pp = do_lepe ? part : nullptr;
+        if (a->br[0].H_sp * a->br[0].W_sp <= 128) bwd_fused<128>(*a, q, o, go, lse, (bf16*)dqkv, pp, st);
+        else bwd_fused<256>(*a, q, o, go, lse, (bf16*)dqkv, pp, st);
+        if (do_lepe && !lepe_deferred) {
+            const dim3 rgrid((a->nbranch * a->heads * HD * 10 + 3) / 4);
+            lepe_wgrad_reduce<<<rgrid, 256, 0, st>>>(*a, fused_nblk(*a), part);
+        }
+        return check_launch("stripe_attn_bwd");
+    }
     if (use_window_path(*a, dtype)) {
         const int sp = wsplit(*a);
         const int nwin = (a->reso / a->br[0].H_sp) * (a->reso / a->br[0].W_sp);

@@ -61,52 +61,72 @@ class GradAllReduce:
     ``DistributedDataParallel`` cannot sit inside ``GraphedTrainStep``'s capture, and an eager
     step costs ~3x a graph replay at 512x512 (51 vs 16 ms), so multi-GPU training would lose most
     of its per-GPU speed to host launches.  This reducer does DDP's job for a fixed parameter set:
-    post-accumulate-grad hooks count the gradients of each bucket as backward produces them
-    (buckets in reverse registration order = backward order); a complete bucket is packed into its
-    flat fp32 buffer (one ``cat``) and all-reduced on a side stream while backward continues.
-    ``finish()`` (call after ``backward()``, before ``optimizer.step()``) launches any bucket still
-    pending (every bucket that completed while csu still held deferred parameter gradients: those
-    are written by the end-of-backward flush, so their all-reduce follows it), joins the side stream and re-points every ``p.grad`` at its averaged slice of the flat
-    buffers, which the optimizer then reads in place.  Every call is a stream operation, so the same
-    sequence is recorded into a graph on capture and replayed with one launch per step (RCCL
-    collectives are capturable once the communicator exists: run one eager step first).
+    buckets are filled in reverse registration order (= backward order); inside a bucket the
+    parameters sit in registration order, so the weight and bias of a Linear / LayerNorm and a
+    block's LePE weights are adjacent, and csu's backward writes those gradients STRAIGHT into the
+    bucket (ops._GRAD_DEST: AccumulateGrad steals the bucket view -- nothing to pack).  Buckets are
+    cut only between modules (``named_parameters()`` input) so such groups never straddle two.
+    Post-accumulate-grad hooks count each bucket's gradients; a complete bucket is all-reduced on a
+    side stream while backward continues (any gradient that did not land in place -- e.g. a conv
+    weight -- is copied in by one multi-tensor copy first).  ``finish()`` (after ``backward()``,
+    before ``optimizer.step()``) launches every bucket still pending (buckets that completed while
+    csu still held deferred parameter gradients, which its end-of-backward flush writes), joins the
+    side stream and points every ``p.grad`` at its averaged slice, which the optimizer reads in
+    place.  Every call is a stream operation, so the sequence is recorded into a graph on capture and
+    replayed with one launch per step (RCCL collectives are capturable once the communicator exists:
+    run one eager step first).
 
-    Averaging: ``ReduceOp.AVG`` on nccl (= RCCL), SUM then a scale on gloo.  Bucket size 32 MB:
-    94 MB of CSWin-UNet gradients -> 3 all-reduces, the first two overlapped with backward, each
-    large enough to run the xGMI rings at bandwidth."""
+    Averaging: ``ReduceOp.AVG`` on nccl (= RCCL), SUM then a scale on gloo.  ``grad_dtype=
+    torch.bfloat16`` all-reduces a bf16 copy of each bucket (half the ring bytes; the averaged values
+    are cast back into the fp32 bucket).  Bucket size 32 MB: 94 MB of CSWin-UNet gradients -> 3
+    all-reduces, the first two overlapped with backward, each large enough to run the xGMI rings at
+    bandwidth."""
 
-    def __init__(self, params, bucket_mb: float = 32.0, group=None):
-        self.params = [p for p in params if p.requires_grad]
+    def __init__(self, params, bucket_mb: float = 32.0, group=None, grad_dtype=torch.float32):
+        items = list(params)
+        named = bool(items) and isinstance(items[0], tuple)
+        pairs = [(n, p) for n, p in items] if named else [(None, p) for p in items]
+        pairs = [(n, p) for n, p in pairs if p.requires_grad]
+        self.params = [p for _, p in pairs]
+        self.last_copied = 0
         if not self.params:
             raise ValueError("GradAllReduce: no trainable parameters")
+        if grad_dtype not in (torch.float32, torch.bfloat16):
+            raise ValueError("GradAllReduce: grad_dtype float32 or bfloat16")
         self.group = group
         self.world = dist.get_world_size(group)
         self.avg = dist.get_backend(group) == "nccl"
+        self.grad_dtype = grad_dtype
         dev = self.params[0].device
         cap = int(bucket_mb * (1 << 20)) // 4
+        owner = lambda n: None if n is None else n.rsplit(".", 1)[0]   # noqa: E731
         self.buckets, cur, size = [], [], 0
-        for p in reversed(self.params):
+        rev = list(reversed(pairs))
+        for i, (n, p) in enumerate(rev):
             if p.dtype != torch.float32 or not p.is_contiguous():
                 raise ValueError("GradAllReduce: contiguous fp32 parameters only")
             cur.append(p)
             size += p.numel()
-            if size >= cap:
-                self.buckets.append(cur)
+            nxt = rev[i + 1][0] if i + 1 < len(rev) else None
+            if size >= cap and (n is None or owner(nxt) != owner(n)):
+                self.buckets.append(cur[::-1])       # registration order inside the bucket
                 cur, size = [], 0
         if cur:
-            self.buckets.append(cur)
+            self.buckets.append(cur[::-1])
         self.flat = [torch.zeros(sum(p.numel() for p in b), dtype=torch.float32, device=dev) for b in self.buckets]
+        self.flat_lp = [f.to(grad_dtype) for f in self.flat] if grad_dtype != torch.float32 else None
+        from . import ops
+        self._ops = ops
         self.views = []
         for b, f in zip(self.buckets, self.flat):
             off, vs = 0, []
             for p in b:
                 vs.append(f[off:off + p.numel()].view_as(p))
+                ops._GRAD_DEST[id(p)] = (f, off)
                 off += p.numel()
             self.views.append(vs)
         self.where = {id(p): bi for bi, b in enumerate(self.buckets) for p in b}
         self.side = torch.cuda.Stream(dev) if dev.type == "cuda" else None
-        from . import ops
-        self._ops = ops
         ops._DIST_SAFE[0] = True   # side-stream weight gradients: ordered by _launch below
         self._reset()
         self.handles = [p.register_post_accumulate_grad_hook(self._hook) for p in self.params]
@@ -115,6 +135,7 @@ class GradAllReduce:
         self.pending = [len(b) for b in self.buckets]
         self.launched = [False] * len(self.buckets)
         self.held = []     # gradients read on the side stream: alive until finish() joined it
+        self._copied = 0   # gradients of this step that did not land in their bucket view
 
     def _hook(self, p):
         bi = self.where[id(p)]
@@ -129,12 +150,12 @@ class GradAllReduce:
         for p in self.buckets[bi]:
             if p.grad is None:      # parameter without a gradient this step: contributes zeros
                 p.grad = torch.zeros_like(p)
-            grads.append(p.grad.reshape(-1))
+            grads.append(p.grad)
         flat = self.flat[bi]
-        alias = [g.data_ptr() == v.data_ptr() for g, v in zip(grads, self.views[bi])]
-        if any(alias) and not all(alias):   # zero_grad(set_to_none=False) after a partial step
-            grads = [g.clone() if a else g for g, a in zip(grads, alias)]
+        # gradients not already in place (not written into the bucket by csu's backward)
+        todo = [(v, g) for v, g in zip(self.views[bi], grads) if g.data_ptr() != v.data_ptr()]
         self.held.append(grads)
+        self._copied += len(todo)
         if self.side is not None:
             self.side.wait_stream(torch.cuda.current_stream(flat.device))
             ws = self._ops.side_stream(flat.device)
@@ -146,13 +167,19 @@ class GradAllReduce:
         else:
             ctx = contextlib.nullcontext()
         with ctx:
-            if not all(alias):              # already in place: grads accumulated into the views
-                torch.cat(grads, out=flat)
+            if todo:
+                torch._foreach_copy_([v for v, _ in todo], [g for _, g in todo])
+            buf = flat
+            if self.flat_lp is not None:
+                buf = self.flat_lp[bi]
+                buf.copy_(flat)
             if self.avg:
-                dist.all_reduce(flat, op=dist.ReduceOp.AVG, group=self.group)
+                dist.all_reduce(buf, op=dist.ReduceOp.AVG, group=self.group)
             else:
-                dist.all_reduce(flat, group=self.group)
-                flat.mul_(1.0 / self.world)
+                dist.all_reduce(buf, group=self.group)
+                buf.mul_(1.0 / self.world)
+            if buf is not flat:
+                flat.copy_(buf)
         self.launched[bi] = True
 
     def finish(self):
@@ -164,9 +191,38 @@ class GradAllReduce:
         for b, vs in zip(self.buckets, self.views):
             for p, v in zip(b, vs):
                 p.grad = v
+        self.last_copied = self._copied   # how many gradients of the step needed the copy-in
         self._reset()
 
     def remove(self):
         for h in self.handles:
             h.remove()
+        self.handles = []
+        for b in self.buckets:
+            for p in b:
+                self._ops._GRAD_DEST.pop(id(p), None)
 
+
+def drain_collectives(group=None):
+    """Guarantee that no collective of the process group is in flight when a HIP-graph capture
+    starts (GraphedTrainStep with a reducer).  The RCCL watchdog thread polls the events of the
+    collectives it still tracks; one of those queries landing inside the capture window aborted the
+    process now and then.  Sequence: an async barrier whose Work is waited on and
+    checked complete through the public Work API, a device-wide synchronize (every stream, the
+    process group's included), then the watchdog's own list is drained.  torch exposes that last
+    step only as ProcessGroup._wait_for_pending_works: when a torch build lacks it the capture is
+    refused (RuntimeError) instead of risking the race."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return
+    work = dist.barrier(group=group, async_op=True)
+    work.wait()
+    torch.cuda.synchronize()
+    if not work.is_completed():
+        raise RuntimeError("drain_collectives: the barrier did not complete")
+    pg = group if group is not None else dist.distributed_c10d._get_default_group()
+    wait = getattr(pg, "_wait_for_pending_works", None)
+    if wait is None:
+        raise RuntimeError("drain_collectives: this torch build cannot drain the process group's watchdog list "
+                           "(no ProcessGroup._wait_for_pending_works); refusing to capture RCCL collectives")
+    wait()
+    torch.cuda.synchronize()

@@ -106,13 +106,18 @@ class _StripeAttnFn(torch.autograd.Function):
         # one flat buffer, views handed to autograd: a deferred reduction keeps the BASE alive, so the
         # returned views stay singly referenced and AccumulateGrad steals them instead of copying
         # them before the reduction has filled them
-        sizes = [w.numel() for w in ws] + [b.numel() for b in bs]
-        flat = torch.empty(sum(sizes), dtype=torch.float32, device=qkv.device)
-        views, o = [], 0
-        for t, n in zip(list(ws) + list(bs), sizes):
-            views.append(flat[o:o + n].view(t.shape))
-            o += n
-        dws, dbs = views[:nb], views[nb:]
+        # registration order (get_v.weight, get_v.bias of each branch): a GradAllReduce bucket's layout
+        order = [t for i in range(nb) for t in (ws[i], bs[i])]
+        porder = [p for i in range(nb) for p in (ctx.params[i], ctx.params[nb + i])]
+        flat = _grad_dest(porder) if all(dt == torch.float32 for dt in ctx.lepe_dtypes) else None
+        if flat is None:
+            flat = torch.empty(sum(t.numel() for t in order), dtype=torch.float32, device=qkv.device)
+        pv, o = [], 0
+        for t in order:
+            pv.append(flat[o:o + t.numel()].view(t.shape))
+            o += t.numel()
+        dws, dbs = pv[0::2], pv[1::2]
+        views = dws + dbs
         a = geom.args(B, ws, bs, dws, dbs, drop=ctx.drop)
         nbytes = L.csu_stripe_attn_bwd_workspace(ctypes.byref(a))
         work = torch.empty(max(nbytes, 16), dtype=torch.uint8, device=qkv.device)
@@ -426,7 +431,9 @@ class _LayerNormFn(torch.autograd.Function):
         # fp32 input (the residual stream under norm / norm_up, cswin:554/602): the bf16 copy of dx
         # the upstream Mlp / GEMM backward consumes, written by the same pass (see _bf16_of)
         dxb = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device) if x.dtype == torch.float32 else None
-        dgb = torch.empty(2 * C, dtype=torch.float32, device=x.device)   # contiguous: one reduction pass
+        dgb = _grad_dest(ctx.params)   # contiguous: one reduction pass
+        if dgb is None:
+            dgb = torch.empty(2 * C, dtype=torch.float32, device=x.device)
         dg, db = dgb[:C], dgb[C:]
         L = lib()
         nbytes = L.csu_layernorm_bwd_workspace(rows, C)
@@ -500,7 +507,9 @@ class _LayerNormForkFn(torch.autograd.Function):
         L = lib()
         nbytes = L.csu_layernorm_bwd_workspace(rows, C)
         work = torch.empty(max(nbytes, 16), dtype=torch.uint8, device=x.device)
-        dgb = torch.empty(2 * C, dtype=torch.float32, device=x.device)
+        dgb = _grad_dest(ctx.params)
+        if dgb is None:
+            dgb = torch.empty(2 * C, dtype=torch.float32, device=x.device)
         late = _ln_params(ctx, rows, C, work, dgb)
         pg, pb = (None, None) if late else (ptr(dgb[:C]), ptr(dgb[C:]))
         _launch("layernorm_bwd", lambda: L.csu_layernorm_bwd_ex(rows, C, dtype_code(x), ptr(x), ptr(w), ptr(mean),
@@ -860,6 +869,33 @@ def _leaf(p):
     return p
 
 
+# Gradient destinations registered by csu.dist.GradAllReduce: id(param) -> (flat fp32 bucket, element
+# offset).  An op whose weight gradients land in one buffer (a Linear's [dW | db], a LayerNorm's
+# [dgamma | dbeta], a block's LePE weights) writes them straight into the bucket when the params are
+# adjacent there: AccumulateGrad steals the (fresh) view, and the reducer has nothing to pack.
+_GRAD_DEST: dict = {}
+
+
+def _grad_dest(params) -> Optional[torch.Tensor]:
+    """One flat fp32 slice holding the gradients of ``params`` in this order (their bucket views), or
+    None.  Only for parameters without a .grad (nothing to accumulate into)."""
+    if not _GRAD_DEST:
+        return None
+    flat0, off0, n = None, 0, 0
+    for p in params:
+        p = _leaf(p)
+        e = _GRAD_DEST.get(id(p)) if p is not None else None
+        if e is None or p.grad is not None:
+            return None
+        flat, off = e
+        if flat0 is None:
+            flat0, off0 = flat, off
+        elif flat is not flat0 or off != off0 + n:
+            return None
+        n += p.numel()
+    return None if flat0 is None else flat0[off0:off0 + n]
+
+
 def _param_safe(p) -> bool:
     """True when no reader of p.grad can run before the end-of-backward join (see above)."""
     p = _leaf(p)
@@ -920,9 +956,12 @@ def _side_run(fn, *inputs):
 
 def wgrad_maybe_side(dy2: torch.Tensor, x2: torch.Tensor, wdt, bdt, params=()):
     """linear_wgrad on the side stream when allowed (fp32 master weights, see above), else inline."""
+    dest = None
+    if dy2.dtype == torch.bfloat16 and len(params) == 2 and params[1] is not None and wdt is not None and bdt is not None:
+        dest = _grad_dest(params)                 # [dW | db] straight into a GradAllReduce bucket
     if _side_ok(dy2, wdt, bdt, params=params):
-        return _side_run(lambda: linear_wgrad(dy2, x2), dy2, x2)
-    return linear_wgrad(dy2, x2, defer=_wgrad_deferrable(dy2, wdt, bdt, params))
+        return _side_run(lambda: linear_wgrad(dy2, x2, out=dest), dy2, x2)
+    return linear_wgrad(dy2, x2, out=dest, defer=_wgrad_deferrable(dy2, wdt, bdt, params))
 
 
 # csu_gemm_ex (fused bias / GELU / GELU' / residual token GEMM) for the bf16 nn.Linear forward and

@@ -361,12 +361,8 @@ class GraphedTrainStep:
             # the barrier's included, has been retired by the watchdog): with nothing left to poll
             # it issues no event query while the capture runs (observed: a query landing inside the
             # capture window still aborted the process now and then, thread-local mode or not).
-            if dist.is_available() and dist.is_initialized():
-                dist.barrier()
-                torch.cuda.synchronize()
-                pg = dist.distributed_c10d._get_default_group()
-                if hasattr(pg, "_wait_for_pending_works"):
-                    pg._wait_for_pending_works()
+            from .dist import drain_collectives
+            drain_collectives()
             mode = "thread_local"
         prep = getattr(self.opt, "prepare_capture", None)
         if prep is not None:
