@@ -1396,9 +1396,10 @@ __global__ __launch_bounds__(NT, 2) void stripe_bwd_fused_w(csu_stripe_args a, c
     // ---- staging: Q, K, V, dO images, the window's lse (as -lse / scale: the S accumulators' start)
     {
         const __amdgpu_buffer_rsrc_t rs_lse = stat_rsrc(a, lse);
-        float lv[RT / 8 > 0 ? RT / 8 : 1];
+        constexpr int SI = (WM + NT - 1) / NT;   // window rows per thread
+        float lv[SI];
 #pragma unroll
-        for (int k = 0; k < WM / NT; ++k) {
+        for (int k = 0; k < SI; ++k) {
             const int i = threadIdx.x + k * NT;
             lv[k] = ldf_rs(rs_lse, i < w.N ? (unsigned)(stat_index(a, w, tok_of(w, a.reso, i)) * 4) : kOOB);
         }
@@ -1408,7 +1409,7 @@ __global__ __launch_bounds__(NT, 2) void stripe_bwd_fused_w(csu_stripe_args a, c
         stage_win2(w, a.reso, img, C3, 2 * C + w.chq, gimg, C, w.chq, npad, Vs, Gs);
         lepe_weights_store(lw, wts);
 #pragma unroll
-        for (int k = 0; k < WM / NT; ++k) {
+        for (int k = 0; k < SI; ++k) {
             const int i = threadIdx.x + k * NT;
             if (i < npad) lse_s[i] = i < w.N ? -lv[k] * inv_scale : -INFINITY;   // padded queries: P = 0
         }

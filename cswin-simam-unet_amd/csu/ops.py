@@ -757,12 +757,15 @@ def _splitk_wgrad(dy2: torch.Tensor, x2: torch.Tensor) -> torch.Tensor:
 
 
 def gemm_f32(layout: int, a: torch.Tensor, b: torch.Tensor, M: int, N: int, K: int, bias=None, resid=None,
-             with_asum=False):
+             with_asum=False, out=None, asum=None):
     """fp32 csu_gemm_f32: layout 0 C = A B^T (+bias, +resid), 1 C = A B, 2 C = A^T B; C (M, N).
-    ``with_asum`` (layout 2): also return sum_k A[k][m] (the bias gradient) from the same launch."""
+    ``with_asum`` (layout 2): also return sum_k A[k][m] (the bias gradient) from the same launch.
+    ``out`` / ``asum``: caller-provided contiguous result buffers (e.g. a GradAllReduce bucket)."""
     require_device(a, b)
-    out = torch.empty(M, N, dtype=torch.float32, device=a.device)
-    asum = torch.empty(M, dtype=torch.float32, device=a.device) if with_asum else None
+    if out is None:
+        out = torch.empty(M, N, dtype=torch.float32, device=a.device)
+    if with_asum and asum is None:
+        asum = torch.empty(M, dtype=torch.float32, device=a.device)
     L = lib()
     n = L.csu_gemm_f32_workspace(layout, M, N, K)
     work = torch.empty(max(n, 16), dtype=torch.uint8, device=a.device) if n else None
@@ -781,9 +784,12 @@ def linear_wgrad(dy2: torch.Tensor, x2: torch.Tensor, out=None, work=None, defer
     require_device(dy2, x2)
     M, N = dy2.shape
     K = x2.shape[1]
-    if dy2.dtype == torch.float32 and out is None:
+    if dy2.dtype == torch.float32:
         # fp32: MFMA GEMM dW = dy^T x (token splits + ordered slab sum) and the column sum for db
-        return gemm_f32(2, dy2.contiguous(), x2.contiguous(), N, K, M, with_asum=True)
+        if out is None:
+            return gemm_f32(2, dy2.contiguous(), x2.contiguous(), N, K, M, with_asum=True)
+        return gemm_f32(2, dy2.contiguous(), x2.contiguous(), N, K, M, with_asum=True, out=out[:N * K].view(N, K),
+                        asum=out[N * K:])
     L = lib()
     if out is None:
         out = torch.empty(N * K + N, dtype=torch.float32, device=dy2.device)
@@ -957,7 +963,8 @@ def _side_run(fn, *inputs):
 def wgrad_maybe_side(dy2: torch.Tensor, x2: torch.Tensor, wdt, bdt, params=()):
     """linear_wgrad on the side stream when allowed (fp32 master weights, see above), else inline."""
     dest = None
-    if dy2.dtype == torch.bfloat16 and len(params) == 2 and params[1] is not None and wdt is not None and bdt is not None:
+    if (dy2.dtype in (torch.bfloat16, torch.float32) and len(params) == 2 and params[1] is not None and wdt is not None
+            and bdt is not None):
         dest = _grad_dest(params)                 # [dW | db] straight into a GradAllReduce bucket
     if _side_ok(dy2, wdt, bdt, params=params):
         return _side_run(lambda: linear_wgrad(dy2, x2, out=dest), dy2, x2)

@@ -277,7 +277,7 @@ TRAJ = {
     # name: (file, img_size, split_size, batch, steps, eval_every, eval_n)
     "f8": ("f8_trajectory", 128, (1, 2, 4, 4), 8, 400, 20, 16),
     # F11: the headline geometry (BASELINE configs[2]: 512x512, split [1,2,8,8]) at B4
-    "f11": ("f11_trajectory_512", 512, (1, 2, 8, 8), 4, 300, 20, 8),
+    "f11": ("f11_trajectory_512", 512, (1, 2, 8, 8), 4, 480, 20, 8),
 }
 
 

@@ -5,18 +5,22 @@
   captured steps) on the reference's own batch stream (recipe weights, default_rng(1234) batches,
   AdamW 1e-4 / wd 1e-4; eval every 20 steps on a default_rng(99) batch) vs the reference's own run
   (tests/golden/f8_trajectory.json: 128x128 B8 split [1,2,4,4], 400 steps; f11_trajectory_512.json:
-  the headline geometry 512x512 B4 split [1,2,8,8], 300 steps; made by tests/golden/make_golden.py
-  = cswin:775-811 / 692-747).  The reference was also run under bf16 autocast (the *_bf16.json
-  files).  Its OWN fp32-vs-bf16 spread does not settle at 4e-4 (SURVEY §8c's 120-step estimate):
-  over 400 steps at 128x128 it keeps wandering between 4e-5 and 8.9e-4 in Dice (1.7e-3 in IoU)
-  from step 100 on -- the eval Dice moves by ~1e-3 between checkpoints at lr 1e-4, and any change
-  of rounding shifts that walk.  So the gate applies from the first eval step after which the
-  reference's own spread stays within the north_star tolerance (Dice 1e-3; IoU 2e-3, because for
-  batch-flattened metrics IoU = Dice / (2 - Dice), dIoU/dDice = 2 / (2 - Dice)^2 ~ 1.9) -- the
-  "converged" region -- and there csu (fp32 and bf16 alike) must be within the same tolerances of
-  the reference's fp32 run.  Per-epoch mean train loss within 2 %
-  (fp32) / 5 % (bf16).  Every eval point's deltas are written to $CSU_PARITY_LOG (default
-  gpurun_out/) as dice_parity_<fixture>_<precision>.json.
+  the headline geometry 512x512 B4 split [1,2,8,8]; made by tests/golden/make_golden.py =
+  cswin:775-811 / 692-747).  The reference was also run under bf16 autocast (the *_bf16.json files).
+  Its OWN fp32-vs-bf16 spread does not settle at 4e-4 (SURVEY §8c's 120-step estimate): the eval
+  Dice moves by ~1e-3 between checkpoints at lr 1e-4, any change of rounding shifts that walk, and
+  the reference's bf16 run sits up to 8.9e-4 (128x128) / 4.5e-3 (512x512) away from its fp32 run at
+  single checkpoints.  Gates (north_star "Dice within 1e-3"; IoU = Dice / (2 - Dice) for these
+  batch-flattened metrics, so its tolerance is 2e-3):
+    - converged window = eval steps from the first one after which the reference's own fp32/bf16
+      spread stays within those tolerances;
+    - csu fp32: EVERY checkpoint of the window within 1e-3 / 2e-3 of the reference fp32 run (the
+      measured distance is ~3e-8: the same trajectory);
+    - csu bf16: the window's MEAN Dice / IoU within 1e-3 / 2e-3 of the reference fp32 run's, every
+      single checkpoint within 5e-3 (the reference's own worst bf16 checkpoint distance), and the
+      per-epoch mean train loss within 5 % in the window (fp32: 2 % everywhere).
+  Every eval point's values and deltas are written to $CSU_PARITY_LOG (default gpurun_out/) as
+  dice_parity_<fixture>_<precision>.json (committed copies: profiles/r03_dice_parity_*.json).
 * FusedAdamW checkpoints: save -> load -> continue equals the uninterrupted run; the state_dict
   loads into torch.optim.AdamW; a load after a capture keeps the captured step valid.
 * HIP-graph replays are bitwise reproducible across two independent captures.
@@ -94,6 +98,7 @@ def _check_trajectory(golden_dir, fixture, amp):
     assert g is not None and sum(s >= g for s in steps) >= 3, \
         f"{fixture}: the reference's own fp32/bf16 spread never settles within the tolerance for 3 eval points"
     ltol = 0.02 if amp is None else 0.05
+    point_tol = (DICE_TOL, IOU_TOL) if amp is None else (5e-3, 1e-2)
     rows, bad = [], []
     for i, s in enumerate(steps):
         dd = abs(h["test_dice"][i] - ref["eval_dice"][i])
@@ -102,25 +107,35 @@ def _check_trajectory(golden_dir, fixture, amp):
         rows.append({"step": s, "gated": s >= g, "csu_dice": h["test_dice"][i], "ref_dice": ref["eval_dice"][i],
                      "ref_bf16_dice": refb["eval_dice"][i], "abs_d_dice": dd,
                      "ref_own_spread_dice": abs(ref["eval_dice"][i] - refb["eval_dice"][i]),
-                     "ref_own_spread_iou": abs(ref["eval_iou"][i] - refb["eval_iou"][i]), "csu_iou": h["test_iou"][i],
+                     "ref_own_spread_iou": abs(ref["eval_iou"][i] - refb["eval_iou"][i]),
+                     "csu_iou": h["test_iou"][i],
                      "ref_iou": ref["eval_iou"][i], "abs_d_iou": di, "csu_eval_loss": h["test_loss"][i],
                      "ref_eval_loss": ref["eval_loss"][i], "csu_train_loss": h["train_loss"][i],
                      "ref_train_loss": mean_ref})
-        if s >= g and (dd > DICE_TOL or di > IOU_TOL):
+        if s >= g and (dd > point_tol[0] or di > point_tol[1]):
             bad.append(f"step {s}: |dDice| {dd:.2e} |dIoU| {di:.2e}")
-        if abs(h["train_loss"][i] - mean_ref) > ltol * mean_ref:
+        if (amp is None or s >= g) and abs(h["train_loss"][i] - mean_ref) > ltol * mean_ref:
             bad.append(f"epoch {i}: train loss {h['train_loss'][i]:.5f} vs {mean_ref:.5f}")
-    prec = "fp32" if amp is None else "bf16"
     gated = [r for r in rows if r["gated"]]
+    mean = lambda k: float(np.mean([r[k] for r in gated]))   # noqa: E731
+    win = {"csu_dice": mean("csu_dice"), "ref_dice": mean("ref_dice"), "ref_bf16_dice": mean("ref_bf16_dice"),
+           "csu_iou": mean("csu_iou"), "ref_iou": mean("ref_iou")}
+    win["abs_d_dice"] = abs(win["csu_dice"] - win["ref_dice"])
+    win["abs_d_iou"] = abs(win["csu_iou"] - win["ref_iou"])
+    win["ref_own_abs_d_dice"] = abs(win["ref_bf16_dice"] - win["ref_dice"])
+    if win["abs_d_dice"] > DICE_TOL or win["abs_d_iou"] > IOU_TOL:
+        bad.append(f"window mean: |dDice| {win['abs_d_dice']:.2e} |dIoU| {win['abs_d_iou']:.2e}")
+    prec = "fp32" if amp is None else "bf16"
     log = {"fixture": fixture, "precision": prec, "config": ref["config"], "gate_from_step": g, "dice_tolerance": DICE_TOL,
-           "iou_tolerance": IOU_TOL, "max_gated_abs_d_dice": max(r["abs_d_dice"] for r in gated),
+           "iou_tolerance": IOU_TOL, "checkpoint_tolerance": point_tol, "window_mean": win,
+           "max_gated_abs_d_dice": max(r["abs_d_dice"] for r in gated),
            "max_gated_abs_d_iou": max(r["abs_d_iou"] for r in gated), "rows": rows}
     out = os.environ.get("CSU_PARITY_LOG", "gpurun_out")
     os.makedirs(out, exist_ok=True)
     with open(os.path.join(out, f"dice_parity_{fixture}_{prec}.json"), "w") as f:
         json.dump(log, f, indent=1)
-    print(f"{fixture} {prec}: gate from step {g}, max |dDice| {log['max_gated_abs_d_dice']:.2e}, "
-          f"max |dIoU| {log['max_gated_abs_d_iou']:.2e}")
+    print(f"{fixture} {prec}: gate from step {g}, window mean |dDice| {win['abs_d_dice']:.2e} |dIoU| "
+          f"{win['abs_d_iou']:.2e}, max checkpoint |dDice| {log['max_gated_abs_d_dice']:.2e}")
     assert not bad, "\n".join(bad)
 
 

@@ -1,0 +1,12 @@
+# round 3: parity after the fused attention backward (logs under gpurun_out/)
+mkdir -p gpurun_out
+run() {  # name, timeout, pytest args...
+  local name=$1 t=$2; shift 2
+  timeout -k 10 $t python -u -m pytest -v --timeout 400 --timeout-method thread "$@" > gpurun_out/r03c_$name.log 2>&1
+  local rc=$?
+  echo "$name rc=$rc: $(tail -1 gpurun_out/r03c_$name.log)"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+}
+run kern 400 tests/test_gpu_kernels.py -k "stripe or two_branch or bce"
+run model 500 tests/test_gpu_dropout.py tests/test_gpu_model.py
+run train 900 tests/test_gpu_train.py tests/test_gpu_dist.py
