@@ -28,12 +28,6 @@
 //  * v_mfma_f32_32x32x16_bf16 with weights as the A operand: lane (r, h) of an accumulator holds
 //    token r and 4 consecutive features per register group; bias / GELU / GELU' / residual are
 //    elementwise on registers.
-//  * LN (csu_mlp_ln_*): the block's norm2 (cswin:347/368) inside the same launches -- a workgroup
-//    holds whole token rows, so the forward normalises its fp32 residual rows in registers (two-pass
-//    mean / variance, as csrc/layernorm.hip) into the x fragments and writes LN(x) once for the
-//    backward; the backward's epilogue turns dLN(x) into dx = dres + LN'(dLN(x)) (row sums over the
-//    two feature halves through LDS) and leaves per-workgroup dgamma / dbeta partials.  No
-//    standalone LayerNorm launch, LN(x) read once instead of written + read twice.
 #include "lds_dma.hpp"
 #include "rng.hpp"
 
@@ -54,20 +48,6 @@ struct MlpDrop {
     float p;
     const float* row_scale;
     long rps;
-};
-
-struct MlpLn {
-    const float* gamma;
-    const float* beta;
-    float eps;
-    bf16* xn;            // fwd: LN(x) (bf16, the backward's operand)
-    float* mean;         // fwd out / bwd in
-    float* rstd;
-    const float* x;      // bwd: the fp32 LN input
-    const float* dres;   // bwd: gradient of the block output reaching x through the residual
-    float* dx;           // bwd out
-    bf16* dxb;
-    float* part;         // bwd: dgamma | dbeta partials [2C][gridDim.x]
 };
 
 constexpr int BM = 64;    // tokens per workgroup
@@ -182,170 +162,17 @@ __device__ __forceinline__ void bias16(const float* b1s, int base, int h, float*
     }
 }
 
-// norm2 of 32 token rows into the B fragments (lane: row r, channels 16 s + 8 h .. + 7): the fp32 row
-// is read once (two 16-B loads per fragment), mean / variance two-pass over the lane's half row + the
-// other half (lane ^ 32), y = (x - mean) * rstd * gamma + beta rounded to bf16 (csrc/layernorm.hip's
-// arithmetic).  store: this wave writes LN(x) and mean / rstd (one of the two waves of a token block).
-template <int C>
-__device__ __forceinline__ void ln_bfrags(__amdgpu_buffer_rsrc_t rs, const MlpLn& ln, long m0, long rows, int tok, bool ok,
-                                          int h, bool store, bf16x8* f) {
-    constexpr int KS = C / 16;
-    float v[KS][8];
-#pragma unroll
-    for (int s = 0; s < KS; ++s) {
-        const unsigned off = ok ? (unsigned)(tok * C + 16 * s + 8 * h) * 4 : kOOB;
-        buf_ld4(rs, off, v[s]);
-        buf_ld4(rs, off == kOOB ? kOOB : off + 16, v[s] + 4);
-    }
-    float sum = 0.f;
-#pragma unroll
-    for (int s = 0; s < KS; ++s)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) sum += v[s][j];
-    sum += __shfl_xor(sum, 32, 64);
-    const float mu = sum / C;
-    float q = 0.f;
-#pragma unroll
-    for (int s = 0; s < KS; ++s)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            v[s][j] -= mu;
-            q += v[s][j] * v[s][j];
-        }
-    q += __shfl_xor(q, 32, 64);
-    const float rs_ = rsqrtf(q / C + ln.eps);
-    const auto rs_xn = buf_rsrc(ln.xn + m0 * C, rows * C * 2);
-#pragma unroll
-    for (int s = 0; s < KS; ++s) {
-        const f32x4 g0 = *reinterpret_cast<const f32x4*>(ln.gamma + 16 * s + 8 * h);
-        const f32x4 g1 = *reinterpret_cast<const f32x4*>(ln.gamma + 16 * s + 8 * h + 4);
-        const f32x4 b0 = *reinterpret_cast<const f32x4*>(ln.beta + 16 * s + 8 * h);
-        const f32x4 b1 = *reinterpret_cast<const f32x4*>(ln.beta + 16 * s + 8 * h + 4);
-        float o[8];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            o[j] = v[s][j] * rs_ * g0[j] + b0[j];
-            o[4 + j] = v[s][4 + j] * rs_ * g1[j] + b1[j];
-        }
-#pragma unroll
-        for (int j = 0; j < 8; ++j) f[s][j] = (bf16)o[j];
-        if (store) buf_st8bf(rs_xn, ok ? (unsigned)(tok * C + 16 * s + 8 * h) * 2 : kOOB, o);
-    }
-    if (store && h == 0) {
-        const unsigned ro = ok ? (unsigned)tok * 4u : kOOB;
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(mu), buf_rsrc(ln.mean + m0, rows * 4), ro, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(rs_), buf_rsrc(ln.rstd + m0, rows * 4), ro, 0, 0);
-    }
-}
-
-// Backward epilogue with norm2: acc holds dLN(x) of this wave's feature half U (after
-// exchange_half) for tokens 32 t + r.  dx = dres + rstd (gd - mean(gd) - xhat mean(gd xhat)), gd =
-// gamma dLN; the row means need the partner wave's half (LDS, `xs`).  dgamma / dbeta: per-feature
-// sums over the workgroup's 64 tokens (xor tree over the wave's 32 tokens, then the two token waves
-// in order through LDS `ps`) -> part[f][blockIdx.x], part[C + f][blockIdx.x].
-template <int C, int U>
-__device__ __forceinline__ void bwd_ln_epilogue(const f32x16* acc, const MlpLn& ln, long m0, long rows, int tok, bool ok,
-                                                int h, int t, int wave, int lane, float* xs, float* ps) {
-    constexpr int HT = C / 64;
-    const auto rs_x = buf_rsrc(ln.x + m0 * C, rows * C * 4);
-    const auto rs_r = buf_rsrc(ln.dres + m0 * C, rows * C * 4);
-    const auto rs_dx = buf_rsrc(ln.dx + m0 * C, rows * C * 4);
-    const auto rs_db = buf_rsrc(ln.dxb + m0 * C, rows * C * 2);
-    const unsigned so = ok ? (unsigned)tok * 4u : kOOB;
-    const float mu = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(buf_rsrc(ln.mean + m0, rows * 4), so, 0, 0));
-    const float rs = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(buf_rsrc(ln.rstd + m0, rows * 4), so, 0, 0));
-    float xh[HT][16], gd[HT][16];
-    float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-    for (int q = 0; q < HT; ++q)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            const int f = (U * HT + q) * 32 + 8 * g + 4 * h;
-            float xv[4];
-            buf_ld4(rs_x, ok ? (unsigned)(tok * C + f) * 4 : kOOB, xv);
-            const f32x4 gm = *reinterpret_cast<const f32x4*>(ln.gamma + f);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const float d = ok ? acc[U * HT + q][4 * g + e] : 0.f;
-                xh[q][4 * g + e] = (xv[e] - mu) * rs;
-                gd[q][4 * g + e] = d * gm[e];
-                s1 += gd[q][4 * g + e];
-                s2 += gd[q][4 * g + e] * xh[q][4 * g + e];
-            }
-        }
-    s1 += __shfl_xor(s1, 32, 64);
-    s2 += __shfl_xor(s2, 32, 64);
-    xs[(wave * 2) * 64 + lane] = s1;
-    xs[(wave * 2 + 1) * 64 + lane] = s2;
-    lds_sync();
-    s1 += xs[((wave ^ 1) * 2) * 64 + lane];
-    s2 += xs[((wave ^ 1) * 2 + 1) * 64 + lane];
-    const float c1 = s1 / C, c2 = s2 / C;
-#pragma unroll
-    for (int q = 0; q < HT; ++q)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-            const int f = (U * HT + q) * 32 + 8 * g + 4 * h;
-            const unsigned off = ok ? (unsigned)(tok * C + f) * 4 : kOOB;
-            float dr[4], v[4];
-            buf_ld4(rs_r, off, dr);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] = dr[e] + rs * (gd[q][4 * g + e] - c1 - xh[q][4 * g + e] * c2);
-            buf_st4(rs_dx, off, v);
-            buf_st4bf(rs_db, ok ? (unsigned)(tok * C + f) * 2 : kOOB, v);
-        }
-    // dgamma (dLN * xhat) and dbeta (dLN) over this wave's 32 tokens: xor tree over lane bits 0..4
-    float pv[2][HT][16];
-#pragma unroll
-    for (int q = 0; q < HT; ++q)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const float d = ok ? acc[U * HT + q][i] : 0.f;
-            pv[0][q][i] = d * xh[q][i];
-            pv[1][q][i] = d;
-        }
-#pragma unroll
-    for (int m = 1; m < 32; m <<= 1)
-#pragma unroll
-        for (int k = 0; k < 2; ++k)
-#pragma unroll
-            for (int q = 0; q < HT; ++q)
-#pragma unroll
-                for (int i = 0; i < 16; ++i) pv[k][q][i] += __shfl_xor(pv[k][q][i], m, 64);
-    // every lane of a half now holds the half's sums; lane r keeps values k*HT*16 + q*16 + i == r (mod 32)
-    const int r = lane & 31;
-#pragma unroll
-    for (int k = 0; k < 2; ++k)
-#pragma unroll
-        for (int q = 0; q < HT; ++q)
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                const int idx = (k * HT + q) * 16 + i;
-                if ((idx & 31) == r) ps[((t * 2 + U) * 2 + h) * (32 * HT) + idx] = pv[k][q][i];
-            }
-    lds_sync();
-    if (t == 0) {   // the two token waves of this feature half, in order
-        const int nb = gridDim.x;
-        for (int idx = r; idx < 2 * HT * 16; idx += 32) {
-            const float sum = ps[((0 * 2 + U) * 2 + h) * (32 * HT) + idx] + ps[((1 * 2 + U) * 2 + h) * (32 * HT) + idx];
-            const int k = idx / (HT * 16), qi = idx % (HT * 16), q = qi >> 4, i = qi & 15;
-            const int f = (U * HT + q) * 32 + 8 * (i >> 2) + 4 * h + (i & 3);
-            ln.part[(size_t)(k * C + f) * nb + blockIdx.x] = sum;
-        }
-    }
-}
-
 template <bool V> using bconst = std::integral_constant<bool, V>;
 template <int V> using iconst = std::integral_constant<int, V>;
 
 // Forward.  Rings: W1 chunks in 2 stages, W2 chunks in 2 stages.  Step j (after one barrier):
 // DMA W1(j+2), W2(j+1); GEMM1(j+1) on the MFMA pipe while GELU(j) runs on the VALU; GEMM2(j).
 // DROP: hidden / output dropout and DropPath (MlpDrop)
-template <int C, bool DROP, bool LN>
+template <int C, bool DROP>
 __global__ __launch_bounds__(MT) void mlp_fwd_kernel(long M, const bf16* __restrict__ X, const bf16* __restrict__ W1,
                                                      const float* __restrict__ b1, const bf16* __restrict__ W2,
                                                      const float* __restrict__ b2, const float* __restrict__ res,
-                                                     float* __restrict__ out, MlpDrop dd, MlpLn ln) {
+                                                     float* __restrict__ out, MlpDrop dd) {
     constexpr int NCH = 4 * C / HC;     // hidden chunks
     constexpr int KS = C / 16;          // k-steps of GEMM1
     constexpr int TF = C / 32;          // 32-feature output tiles (all C, partial over the hidden half)
@@ -368,8 +195,7 @@ __global__ __launch_bounds__(MT) void mlp_fwd_kernel(long M, const bf16* __restr
     const int hs = 32 * u;              // this wave's hidden features within a chunk
     for (int i = threadIdx.x; i < 4 * C; i += MT) b1s[i] = b1[i];
     bf16x8 xf[KS];
-    if constexpr (LN) ln_bfrags<C>(buf_rsrc(res + m0 * C, rows * C * 4), ln, m0, rows, tok, ok, h, u == 0, xf);
-    else load_bfrags<C>(buf_rsrc(X + m0 * C, rows * C * 2), tok, ok, h, xf);
+    load_bfrags<C>(buf_rsrc(X + m0 * C, rows * C * 2), tok, ok, h, xf);
 
     D1 d1;
     D2 d2;
@@ -468,11 +294,11 @@ __global__ __launch_bounds__(MT) void mlp_fwd_kernel(long M, const bf16* __restr
 // chunk j+1 on the MFMA pipe while chunk j's GELU / GELU' / g, dH stores run on the VALU; GEMM4(j).
 // DROP: dY is the gradient of the dropped fc2 output (the output mask / DropPath were applied by
 // the caller); the hidden mask is regenerated here: g stored = gelu(h) * mask, dH = (W2^T dY) * mask * gelu'(h).
-template <int C, bool DROP, bool LN>
+template <int C, bool DROP>
 __global__ __launch_bounds__(MT) void mlp_bwd_kernel(long M, const bf16* __restrict__ X, const bf16* __restrict__ dY,
                                                      const bf16* __restrict__ W1, const float* __restrict__ b1,
                                                      const bf16* __restrict__ W2, bf16* __restrict__ dH,
-                                                     bf16* __restrict__ G, bf16* __restrict__ dX, MlpDrop dd, MlpLn ln) {
+                                                     bf16* __restrict__ G, bf16* __restrict__ dX, MlpDrop dd) {
     constexpr int NCH = 4 * C / HC;
     constexpr int KS = C / 16;
     constexpr int TF = C / 32;
@@ -636,18 +462,6 @@ __global__ __launch_bounds__(MT) void mlp_bwd_kernel(long M, const bf16* __restr
 
     lds_sync();
     float* xch = reinterpret_cast<float*>(ring);
-    if constexpr (LN) {
-        float* xs = xch + 4 * (C / 64) * 16 * 64;        // past exchange_half's region
-        float* ps = xs + 4 * 2 * 64;
-        if (u == 0) {
-            exchange_half<C, 0>(acc, xch, wave, lane);
-            bwd_ln_epilogue<C, 0>(acc, ln, m0, rows, tok, ok, h, t, wave, lane, xs, ps);
-        } else {
-            exchange_half<C, 1>(acc, xch, wave, lane);
-            bwd_ln_epilogue<C, 1>(acc, ln, m0, rows, tok, ok, h, t, wave, lane, xs, ps);
-        }
-        return;
-    }
     const auto rs_dx = buf_rsrc(dX + m0 * C, rows * C * 2);
     if (u == 0) {
         exchange_half<C, 0>(acc, xch, wave, lane);
@@ -661,34 +475,26 @@ __global__ __launch_bounds__(MT) void mlp_bwd_kernel(long M, const bf16* __restr
 
 template <int C>
 int fwd_launch(long M, const void* x, const void* w1, const float* b1, const void* w2, const float* b2, const float* res,
-               float* out, const MlpDrop* d, const MlpLn* ln, hipStream_t st) {
+               float* out, const MlpDrop* d, hipStream_t st) {
     const dim3 grid((unsigned)((M + BM - 1) / BM));
-    const MlpDrop dz{};
-    const MlpLn lz{};
-#define CSU_MLPF(DR, L) mlp_fwd_kernel<C, DR, L><<<grid, MT, 0, st>>>(M, (const bf16*)x, (const bf16*)w1, b1, (const bf16*)w2, \
-                                                                       b2, res, out, d ? *d : dz, ln ? *ln : lz)
-    if (d && ln) CSU_MLPF(true, true);
-    else if (d) CSU_MLPF(true, false);
-    else if (ln) CSU_MLPF(false, true);
-    else CSU_MLPF(false, false);
-#undef CSU_MLPF
+    if (d)
+        mlp_fwd_kernel<C, true><<<grid, MT, 0, st>>>(M, (const bf16*)x, (const bf16*)w1, b1, (const bf16*)w2, b2, res, out, *d);
+    else
+        mlp_fwd_kernel<C, false><<<grid, MT, 0, st>>>(M, (const bf16*)x, (const bf16*)w1, b1, (const bf16*)w2, b2, res, out,
+                                                      MlpDrop{});
     return check_launch("mlp_fwd");
 }
 
 template <int C>
 int bwd_launch(long M, const void* x, const void* dy, const void* w1, const float* b1, const void* w2, void* dh, void* g,
-               void* dx, const MlpDrop* d, const MlpLn* ln, hipStream_t st) {
+               void* dx, const MlpDrop* d, hipStream_t st) {
     const dim3 grid((unsigned)((M + BM - 1) / BM));
-    const MlpDrop dz{};
-    const MlpLn lz{};
-#define CSU_MLPB(DR, L) mlp_bwd_kernel<C, DR, L><<<grid, MT, 0, st>>>(M, (const bf16*)x, (const bf16*)dy, (const bf16*)w1, b1, \
-                                                                       (const bf16*)w2, (bf16*)dh, (bf16*)g, (bf16*)dx,   \
-                                                                       d ? *d : dz, ln ? *ln : lz)
-    if (d && ln) CSU_MLPB(true, true);
-    else if (d) CSU_MLPB(true, false);
-    else if (ln) CSU_MLPB(false, true);
-    else CSU_MLPB(false, false);
-#undef CSU_MLPB
+    if (d)
+        mlp_bwd_kernel<C, true><<<grid, MT, 0, st>>>(M, (const bf16*)x, (const bf16*)dy, (const bf16*)w1, b1, (const bf16*)w2,
+                                                     (bf16*)dh, (bf16*)g, (bf16*)dx, *d);
+    else
+        mlp_bwd_kernel<C, false><<<grid, MT, 0, st>>>(M, (const bf16*)x, (const bf16*)dy, (const bf16*)w1, b1, (const bf16*)w2,
+                                                      (bf16*)dh, (bf16*)g, (bf16*)dx, MlpDrop{});
     return check_launch("mlp_bwd");
 }
 
@@ -717,9 +523,9 @@ extern "C" int csu_mlp_fwd_dp(long M, int C, const void* x, const void* w1, cons
     const MlpDrop* dp = d && e == 0 ? &md : nullptr;
     const hipStream_t st = as_stream(stream);
     switch (C) {
-        case 64: return fwd_launch<64>(M, x, w1, b1, w2, b2, res, out, dp, nullptr, st);
-        case 128: return fwd_launch<128>(M, x, w1, b1, w2, b2, res, out, dp, nullptr, st);
-        case 256: return fwd_launch<256>(M, x, w1, b1, w2, b2, res, out, dp, nullptr, st);
+        case 64: return fwd_launch<64>(M, x, w1, b1, w2, b2, res, out, dp, st);
+        case 128: return fwd_launch<128>(M, x, w1, b1, w2, b2, res, out, dp, st);
+        case 256: return fwd_launch<256>(M, x, w1, b1, w2, b2, res, out, dp, st);
         default: return fail(CSU_E_ARG, "mlp_fwd: C must be 64, 128 or 256");
     }
 }
@@ -739,9 +545,9 @@ extern "C" int csu_mlp_bwd_dp(long M, int C, const void* x, const void* dy, cons
     const MlpDrop* dp = d && e == 0 ? &md : nullptr;
     const hipStream_t st = as_stream(stream);
     switch (C) {
-        case 64: return bwd_launch<64>(M, x, dy, w1, b1, w2, dh, g, dx, dp, nullptr, st);
-        case 128: return bwd_launch<128>(M, x, dy, w1, b1, w2, dh, g, dx, dp, nullptr, st);
-        case 256: return bwd_launch<256>(M, x, dy, w1, b1, w2, dh, g, dx, dp, nullptr, st);
+        case 64: return bwd_launch<64>(M, x, dy, w1, b1, w2, dh, g, dx, dp, st);
+        case 128: return bwd_launch<128>(M, x, dy, w1, b1, w2, dh, g, dx, dp, st);
+        case 256: return bwd_launch<256>(M, x, dy, w1, b1, w2, dh, g, dx, dp, st);
         default: return fail(CSU_E_ARG, "mlp_bwd: C must be 64, 128 or 256");
     }
 }
@@ -749,47 +555,4 @@ extern "C" int csu_mlp_bwd_dp(long M, int C, const void* x, const void* dy, cons
 extern "C" int csu_mlp_bwd(long M, int C, const void* x, const void* dy, const void* w1, const float* b1, const void* w2,
                            void* dh, void* g, void* dx, void* stream) {
     return csu_mlp_bwd_dp(M, C, x, dy, w1, b1, w2, dh, g, dx, nullptr, stream);
-}
-
-// ---- norm2 fused (csu_mlp_ln): see the header note -------------------------------------------
-extern "C" int csu_mlp_ln_nblk(long M) { return (int)((M + BM - 1) / BM); }
-
-extern "C" int csu_mlp_ln_fwd(long M, int C, const float* x, const csu_mlp_ln* l, const void* w1, const float* b1,
-                              const void* w2, const float* b2, float* out, const csu_mlp_dropout* d, void* stream) {
-    if (M < 1 || !x || !l || !l->gamma || !l->beta || !l->xn || !l->mean || !l->rstd || !w1 || !b1 || !w2 || !b2 || !out)
-        return fail(CSU_E_ARG, "mlp_ln_fwd: bad arguments");
-    if (M * 4L * C * 2 > 0x7fffffffL) return fail(CSU_E_ARG, "mlp_ln_fwd: tensor exceeds 2 GB buffer range");
-    MlpDrop md{};
-    const int e = mlp_drop_of(d, md);
-    if (e < 0) return e;
-    const MlpDrop* dp = d && e == 0 ? &md : nullptr;
-    MlpLn ln{l->gamma, l->beta, l->eps, (bf16*)l->xn, l->mean, l->rstd, nullptr, nullptr, nullptr, nullptr, nullptr};
-    const hipStream_t st = as_stream(stream);
-    switch (C) {
-        case 64: return fwd_launch<64>(M, nullptr, w1, b1, w2, b2, x, out, dp, &ln, st);
-        case 128: return fwd_launch<128>(M, nullptr, w1, b1, w2, b2, x, out, dp, &ln, st);
-        case 256: return fwd_launch<256>(M, nullptr, w1, b1, w2, b2, x, out, dp, &ln, st);
-        default: return fail(CSU_E_ARG, "mlp_ln_fwd: C must be 64, 128 or 256");
-    }
-}
-
-extern "C" int csu_mlp_ln_bwd(long M, int C, const float* x, const csu_mlp_ln* l, const void* xn, const void* dy,
-                              const void* w1, const float* b1, const void* w2, void* dh, void* g,
-                              const csu_mlp_dropout* d, void* stream) {
-    if (M < 1 || !x || !l || !l->gamma || !l->mean || !l->rstd || !l->dres || !l->dx || !l->dx_bf16 || !l->part || !xn ||
-        !dy || !w1 || !b1 || !w2 || !dh || !g)
-        return fail(CSU_E_ARG, "mlp_ln_bwd: bad arguments");
-    if (M * 4L * C * 2 > 0x7fffffffL) return fail(CSU_E_ARG, "mlp_ln_bwd: tensor exceeds 2 GB buffer range");
-    MlpDrop md{};
-    const int e = mlp_drop_of(d, md);
-    if (e < 0) return e;
-    const MlpDrop* dp = d && e == 0 ? &md : nullptr;
-    MlpLn ln{l->gamma, l->beta, l->eps, nullptr, l->mean, l->rstd, x, l->dres, l->dx, (bf16*)l->dx_bf16, l->part};
-    const hipStream_t st = as_stream(stream);
-    switch (C) {
-        case 64: return bwd_launch<64>(M, xn, dy, w1, b1, w2, dh, g, nullptr, dp, &ln, st);
-        case 128: return bwd_launch<128>(M, xn, dy, w1, b1, w2, dh, g, nullptr, dp, &ln, st);
-        case 256: return bwd_launch<256>(M, xn, dy, w1, b1, w2, dh, g, nullptr, dp, &ln, st);
-        default: return fail(CSU_E_ARG, "mlp_ln_bwd: C must be 64, 128 or 256");
-    }
 }

@@ -33,14 +33,7 @@ class StripeArgs(ctypes.Structure):
 
 class LnParamItem(ctypes.Structure):
     """csu_ln_param_item (include/csu.h)."""
-    _fields_ = [("workspace", c_void_p), ("dgamma", c_void_p), ("dbeta", c_void_p), ("rows", c_int32), ("C", c_int32),
-                ("nblk", c_int32)]
-
-
-class MlpLn(ctypes.Structure):
-    """csu_mlp_ln (include/csu.h): the block's norm2 fused into the Mlp launches."""
-    _fields_ = [("gamma", c_void_p), ("beta", c_void_p), ("eps", c_float), ("xn", c_void_p), ("mean", c_void_p),
-                ("rstd", c_void_p), ("dres", c_void_p), ("dx", c_void_p), ("dx_bf16", c_void_p), ("part", c_void_p)]
+    _fields_ = [("workspace", c_void_p), ("dgamma", c_void_p), ("dbeta", c_void_p), ("rows", c_int32), ("C", c_int32)]
 
 
 class WslabItem(ctypes.Structure):
@@ -191,12 +184,6 @@ _SIGS = {
                                       c_void_p, ctypes.POINTER(MlpDropout), c_void_p]),
     "csu_mlp_bwd_dp": (ctypes.c_int, [ctypes.c_long, ctypes.c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                       c_void_p, c_void_p, ctypes.POINTER(MlpDropout), c_void_p]),
-    "csu_mlp_ln_nblk": (ctypes.c_int, [ctypes.c_long]),
-    "csu_mlp_ln_fwd": (ctypes.c_int, [ctypes.c_long, ctypes.c_int, c_void_p, ctypes.POINTER(MlpLn), c_void_p, c_void_p,
-                                      c_void_p, c_void_p, c_void_p, ctypes.POINTER(MlpDropout), c_void_p]),
-    "csu_mlp_ln_bwd": (ctypes.c_int, [ctypes.c_long, ctypes.c_int, c_void_p, ctypes.POINTER(MlpLn), c_void_p, c_void_p,
-                                      c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, ctypes.POINTER(MlpDropout),
-                                      c_void_p]),
     "csu_mlp_bwd": (ctypes.c_int, [ctypes.c_long, ctypes.c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p,
                                    c_void_p, c_void_p, c_void_p]),
     "csu_conv2d_fwd": (ctypes.c_int, [ctypes.POINTER(ConvGeom), ctypes.c_int, c_void_p, c_void_p, c_void_p, c_void_p,

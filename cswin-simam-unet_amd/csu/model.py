@@ -247,16 +247,12 @@ class CSWinBlock(nn.Module):
         else:
             y = ops.linear(att, self.proj.weight, self.proj.bias)
             x = ops.dropout(y, 0.0, 0, row_scale=rs1, rows_per_sample=L, residual=xa) if rs1 is not None else xa + y
-        md = None
-        if fused and on and (p_mlp > 0 or rs2 is not None):
-            md = ops.MlpDrop(snap, self.mlp._site_h, self.mlp._site_o, p_mlp, rs2, L)
-        if fused and ops.ln_mlp_ok(x, self.mlp.fc1):
-            # norm2 -> fc1 -> GELU -> [dropout] -> fc2 -> [dropout, DropPath] + residual: ONE launch
-            # (csrc/mlp.hip csu_mlp_ln_*), the LayerNorm inside the Mlp workgroups
-            return ops.ln_mlp_residual(x, n2, self.mlp.fc1, self.mlp.fc2, md)
         xb, h2 = ops.layer_norm_fork(x, n2.weight, n2.bias, n2.eps, cd)
         if fused:
             # fc1 -> GELU -> [dropout] -> fc2 -> [dropout, DropPath] + residual (csrc/mlp.hip)
+            md = None
+            if on and (p_mlp > 0 or rs2 is not None):
+                md = ops.MlpDrop(snap, self.mlp._site_h, self.mlp._site_o, p_mlp, rs2, L)
             return ops.mlp_residual(xb, h2, self.mlp.fc1, self.mlp.fc2, md)
         return self.mlp.forward_residual(h2, xb, rs2, L, snap)
 

@@ -292,12 +292,12 @@ def _ln_param_flush():
         return
     dev = pend[0][1].device
     items = (_lib.LnParamItem * len(pend))()
-    for i, (work, dgb, rows, C, nblk) in enumerate(pend):
+    for i, (work, dgb, rows, C) in enumerate(pend):
         items[i].workspace, items[i].dgamma, items[i].dbeta = work.data_ptr(), dgb.data_ptr(), dgb.data_ptr() + C * 4
-        items[i].rows, items[i].C, items[i].nblk = rows, C, nblk
-    nv = sum(2 * e[3] for e in pend)
+        items[i].rows, items[i].C = rows, C
+    nv = sum(2 * C for _, _, _, C in pend)
     _launch("layernorm_bwd", lambda: lib().csu_layernorm_param_reduce_batch(items, len(pend), stream_ptr(dev)),
-            0, sum(e[0].numel() * e[0].element_size() for e in pend) + nv * 4)
+            0, sum(w.numel() for w, _, _, _ in pend) + nv * 4)
 
 
 def _queue_flush():
@@ -338,7 +338,7 @@ def _ln_params(ctx, rows, C, work, dgb):
     """Reduce (later, batched) or report that the caller must pass dgamma / dbeta pointers."""
     if not (DEFER_LN and _deferrable(*ctx.params)):
         return False
-    _LN_PENDING.append((work, dgb, rows, C, 0))
+    _LN_PENDING.append((work, dgb, rows, C))
     _queue_flush()
     return True
 
@@ -1420,100 +1420,6 @@ class _MlpFusedFn(torch.autograd.Function):
         dw2, db2 = wgrad_maybe_side(dyb, g, w2dt, b2dt, params=ctx.params[2:])
         dw1, db1 = wgrad_maybe_side(dh, x2, w1dt, b1dt, params=ctx.params[:2])
         return dy.to(rdt), dx.view(xshape), dw1.to(w1dt), db1.to(b1dt), dw2.to(w2dt), db2.to(b2dt), None, None, None
-
-
-class _LnMlpFn(torch.autograd.Function):
-    """x + Mlp(LN(x)) of a CSWinBlock -- norm2 (cswin:347), Mlp (cswin:180-196) and the residual
-    (cswin:368) -- in ONE csu_mlp_ln_fwd launch: the workgroup normalises its fp32 token rows in
-    registers, so no LayerNorm launch reads the residual stream and writes LN(x) for the Mlp to read
-    back; LN(x) is written once, for the backward.  Backward: ONE csu_mlp_ln_bwd launch (Mlp backward
-    + the LayerNorm backward + the residual add, dx and its bf16 copy), dgamma / dbeta from its
-    per-workgroup partials (deferred to the end-of-backward batch like every LayerNorm's), then the
-    two Linear weight gradients."""
-
-    @staticmethod
-    def forward(ctx, x, lnw, lnb, eps: float, w1, b1, w2, b2, w1c, w2c, drop):
-        require_device(x, lnw, lnb)
-        C = x.shape[-1]
-        x2 = x.float().contiguous().view(-1, C)
-        M = x2.shape[0]
-        gam = lnw.detach().float().contiguous()
-        bet = lnb.detach().float().contiguous()
-        b1f = b1.detach().float().contiguous()
-        b2f = b2.detach().float().contiguous()
-        xn = torch.empty(M, C, dtype=torch.bfloat16, device=x.device)
-        mean = torch.empty(M, dtype=torch.float32, device=x.device)
-        rstd = torch.empty_like(mean)
-        y = torch.empty_like(x2)
-        ln = _lib.MlpLn()
-        ln.gamma, ln.beta, ln.eps, ln.xn, ln.mean, ln.rstd = ptr(gam), ptr(bet), float(eps), ptr(xn), ptr(mean), ptr(rstd)
-        dd = None if drop is None else ctypes.byref(drop.c_struct())
-        _launch("mlp_fwd", lambda: lib().csu_mlp_ln_fwd(M, C, ptr(x2), ctypes.byref(ln), ptr(w1c), ptr(b1f), ptr(w2c),
-                                                        ptr(b2f), ptr(y), dd, stream_ptr(x.device)),
-                16 * M * C * C, M * C * (4 + 2 + 4) + M * 8 + 16 * C * C)
-        ctx.drop = drop
-        ctx.save_for_backward(x2, xn, mean, rstd, gam, w1c, b1f, w2c)
-        ctx.meta = (x.dtype, x.shape, w1.dtype, b1.dtype, w2.dtype, b2.dtype)
-        ctx.params = (lnw, lnb, w1, b1, w2, b2)
-        _note_use(*ctx.params)
-        return y.view(x.shape)
-
-    @staticmethod
-    def backward(ctx, dy):
-        xdt, xshape, w1dt, b1dt, w2dt, b2dt = ctx.meta
-        x2, xn, mean, rstd, gam, w1c, b1f, w2c = ctx.saved_tensors
-        M, C = x2.shape
-        drop = ctx.drop
-        dres = dy.float().reshape(-1, C).contiguous()
-        dyb = _bf16_of(dy).view(-1, C) if drop is None else drop.out_grad(dres, torch.bfloat16)
-        dh = torch.empty(M, 4 * C, dtype=torch.bfloat16, device=x2.device)
-        g = torch.empty_like(dh)
-        dx = torch.empty(M, C, dtype=torch.float32, device=x2.device)
-        dxb = torch.empty(M, C, dtype=torch.bfloat16, device=x2.device)
-        L = lib()
-        nblk = L.csu_mlp_ln_nblk(M)
-        part = torch.empty(2 * C * nblk, dtype=torch.float32, device=x2.device)
-        dgb = _grad_dest(ctx.params[:2])
-        if dgb is None:
-            dgb = torch.empty(2 * C, dtype=torch.float32, device=x2.device)
-        ln = _lib.MlpLn()
-        ln.gamma, ln.mean, ln.rstd, ln.dres = ptr(gam), ptr(mean), ptr(rstd), ptr(dres)
-        ln.dx, ln.dx_bf16, ln.part = ptr(dx), ptr(dxb), ptr(part)
-        dd = None if drop is None else ctypes.byref(drop.c_struct())
-        _launch("mlp_bwd", lambda: L.csu_mlp_ln_bwd(M, C, ptr(x2), ctypes.byref(ln), ptr(xn), ptr(dyb), ptr(w1c), ptr(b1f),
-                                                    ptr(w2c), ptr(dh), ptr(g), dd, stream_ptr(x2.device)),
-                24 * M * C * C, M * C * (2 + 2 + 4 + 4 + 4 + 2) + M * 4 * C * (2 + 2) + 16 * C * C)
-        if DEFER_LN and _deferrable(*ctx.params[:2]):
-            _LN_PENDING.append((part, dgb, M, C, nblk))
-            _queue_flush()
-        else:
-            it = (_lib.LnParamItem * 1)()
-            it[0].workspace, it[0].dgamma, it[0].dbeta = part.data_ptr(), dgb.data_ptr(), dgb.data_ptr() + C * 4
-            it[0].rows, it[0].C, it[0].nblk = M, C, nblk
-            _launch("layernorm_bwd", lambda: L.csu_layernorm_param_reduce_batch(it, 1, stream_ptr(x2.device)),
-                    0, part.numel() * 4 + 2 * C * 4)
-        dw2, db2 = wgrad_maybe_side(dyb, g, w2dt, b2dt, params=ctx.params[4:])
-        dw1, db1 = wgrad_maybe_side(dh, xn, w1dt, b1dt, params=ctx.params[2:4])
-        dx._csu_bf16 = dxb
-        return (dx.view(xshape).to(xdt), dgb[:C], dgb[C:], None, dw1.to(w1dt), db1.to(b1dt), dw2.to(w2dt),
-                db2.to(b2dt), None, None, None)
-
-
-def ln_mlp_ok(x: torch.Tensor, fc1: torch.nn.Linear) -> bool:
-    """norm2 + Mlp + residual can run as one csu_mlp_ln launch: fp32 residual stream on the GPU,
-    C in {64, 128, 256} (the fused Mlp widths), hidden = 4 C."""
-    C = x.shape[-1]
-    return (FUSED_MLP and x.is_cuda and x.dtype == torch.float32 and fc1.out_features == 4 * C
-            and bool(lib().csu_mlp_supported(C)))
-
-
-def ln_mlp_residual(x, norm: torch.nn.LayerNorm, fc1: torch.nn.Linear, fc2: torch.nn.Linear,
-                    drop: Optional[MlpDrop] = None):
-    """x + DropPath(Dropout(fc2(Dropout(gelu(fc1(LN(x))))))) on the bf16 path, norm2 inside the Mlp
-    launches (csu_mlp_ln_fwd / _bwd)."""
-    with torch.autocast("cuda", enabled=False):
-        return _LnMlpFn.apply(x, norm.weight, norm.bias, float(norm.eps), fc1.weight, fc1.bias, fc2.weight, fc2.bias,
-                              _weight_bf16(fc1.weight), _weight_bf16(fc2.weight), drop)
 
 
 # CSU_FUSED_MLP=0 selects the two-GEMM Mlp (A/B comparisons)

@@ -155,7 +155,6 @@ typedef struct {
     float* dgamma;
     float* dbeta;
     int32_t rows, C;
-    int32_t nblk;          /* partial blocks; 0: those of csu_layernorm_bwd_ex(rows, C) (csu_mlp_ln_bwd: its own) */
 } csu_ln_param_item;
 int csu_layernorm_param_reduce_batch(const csu_ln_param_item* items, int count, void* stream);
 
@@ -437,33 +436,6 @@ int csu_mlp_fwd_dp(long M, int C, const void* x, const void* w1, const float* b1
                    const float* res, float* out, const csu_mlp_dropout* d, void* stream);
 int csu_mlp_bwd_dp(long M, int C, const void* x, const void* dy, const void* w1, const float* b1, const void* w2,
                    void* dh, void* g, void* dx, const csu_mlp_dropout* d, void* stream);
-
-/* The block's norm2 (CSWinBlock cswin:347/368) fused into the Mlp launches (replaces
- * layer_norm(x) -> csu_mlp_fwd -> layernorm backward):
- *   fwd: out = x + Mlp(LN(x)); x fp32 (M, C) is the LN input AND the residual; writes xn = LN(x)
- *        (bf16, the backward's operand) and the per-token mean / rstd.
- *   bwd: xn, dy = bf16 gradient of the Mlp output (dres rounded, times the output mask under
- *        dropout) as csu_mlp_bwd; dres = fp32 gradient of the block output; writes dh, g as
- *        csu_mlp_bwd and dx = dres + LN'(dLN) (fp32 + its bf16 copy), plus dgamma | dbeta
- *        per-workgroup partials part[2C][csu_mlp_ln_nblk(M)] (csu_layernorm_param_reduce_batch with
- *        nblk set). */
-typedef struct {
-    const float* gamma;
-    const float* beta;
-    float eps;
-    void* xn;              /* fwd out */
-    float* mean;           /* fwd out, bwd in */
-    float* rstd;
-    const float* dres;     /* bwd in */
-    float* dx;             /* bwd out */
-    void* dx_bf16;
-    float* part;
-} csu_mlp_ln;
-int csu_mlp_ln_nblk(long M);
-int csu_mlp_ln_fwd(long M, int C, const float* x, const csu_mlp_ln* ln, const void* w1, const float* b1, const void* w2,
-                   const float* b2, float* out, const csu_mlp_dropout* d, void* stream);
-int csu_mlp_ln_bwd(long M, int C, const float* x, const csu_mlp_ln* ln, const void* xn, const void* dy, const void* w1,
-                   const float* b1, const void* w2, void* dh, void* g, const csu_mlp_dropout* d, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * Implicit-GEMM NHWC convolution (patch embed cswin:505, Merge_Block.conv cswin:376, CARAFE
