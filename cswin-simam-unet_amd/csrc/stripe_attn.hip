@@ -845,12 +845,12 @@ constexpr int WMAX = 1024;  // largest window held in LDS (K + V images: 128 KiB
 
 #ifdef WG_TIMING   // debug build only: per-workgroup phase stamps (100 MHz) of the last launch of each
                    // whole-window kernel (0 fwd, 1 dq, 2 dkdv): start, staged, end + hardware id
-__device__ unsigned long long attn_ts[3][4][16384];
+__device__ unsigned long long attn_ts[3][6][16384];
 #define ATT_STAMP(kern, k) do { \
     const unsigned _b = blockIdx.x + blockIdx.y * gridDim.x; \
     if (threadIdx.x == 0 && _b < 16384) { \
         attn_ts[kern][k][_b + threadIdx.x] = __builtin_amdgcn_s_memrealtime(); \
-        if (k == 0) attn_ts[kern][3][_b + threadIdx.x] = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11)); } } while (0)
+        if (k == 0) attn_ts[kern][5][_b + threadIdx.x] = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11)); } } while (0)
 #else
 #define ATT_STAMP(kern, k) do {} while (0)
 #endif
@@ -1368,6 +1368,58 @@ __device__ __forceinline__ bf16x8 tr_frag16(const bf16* img, int kb, int cb, int
     return out;
 }
 
+// gather window rows [0, npad) of one head's channels of two tensors: A into a PLAIN [row][32] image
+// (the prologue's V: neighbour rows are base + constant, no swizzle arithmetic), B swizzled (swz);
+// rows >= N zero.  Loads first, then the LDS stores (one memory latency).
+__device__ __forceinline__ void stage_win2_pa(const Win& w, int reso, const bf16* imgA, int strideA, int chA,
+                                              const bf16* imgB, int strideB, int chB, int npad, bf16* dstA, bf16* dstB) {
+    constexpr int IT = 4;
+    const long L = (long)reso * reso;
+    const __amdgpu_buffer_rsrc_t rsA = buf_rsrc(imgA, L * strideA * 2), rsB = buf_rsrc(imgB, L * strideB * 2);
+    for (int base = 0; base < npad * 4; base += IT * NT) {
+        bf16x8 va[IT], vb[IT];
+#pragma unroll
+        for (int i = 0; i < IT; ++i) {
+            const int it = base + threadIdx.x + i * NT;
+            const int n = it >> 2, c = (it & 3) * 8;
+            const bool ok = it < npad * 4 && n < w.N;
+            const unsigned tok = ok ? (unsigned)tok_of(w, reso, n) : 0u;
+            va[i] = ld8_rs(rsA, ok ? (tok * (unsigned)strideA + chA + c) * 2u : kOOB);
+            vb[i] = ld8_rs(rsB, ok ? (tok * (unsigned)strideB + chB + c) * 2u : kOOB);
+        }
+#pragma unroll
+        for (int i = 0; i < IT; ++i) {
+            const int it = base + threadIdx.x + i * NT;
+            if (it < npad * 4) {
+                const int n = it >> 2, c = (it & 3) * 8;
+                *reinterpret_cast<bf16x8*>(dstA + n * HD + c) = va[i];
+                *reinterpret_cast<bf16x8*>(dstB + swz(n, c)) = vb[i];
+            }
+        }
+    }
+}
+
+// LePE (sign +1) / its transpose (sign -1) of window position n, channels c0..c0+3, from a swizzled
+// image whose row `zrow` is all zeros: out-of-window taps read that row instead of branching
+__device__ __forceinline__ void lepe4_lds_z(const Win& w, const bf16* img, int n, int c0, const float* wts, int sign,
+                                            int zrow, float* acc) {
+    const int iy = wrow(w, n), ix = n - iy * w.W_sp;
+    const bool ym = iy > 0, yp = iy + 1 < w.H_sp, xm = ix > 0, xp = ix + 1 < w.W_sp;
+    const f32x4 bias = *reinterpret_cast<const f32x4*>(wts + HD * 9 + c0);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[j] = sign > 0 ? bias[j] : 0.f;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+        const int dy = sign * (t / 3 - 1), dx = sign * (t % 3 - 1);
+        const bool in = (dy < 0 ? ym : dy > 0 ? yp : true) && (dx < 0 ? xm : dx > 0 ? xp : true);
+        const int row = in ? n + dy * w.W_sp + dx : zrow;
+        const bf16x4 v = *reinterpret_cast<const bf16x4*>(img + swz(row, c0));
+        const f32x4 wt = *reinterpret_cast<const f32x4*>(wts + t * HD + c0);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[j] += wt[j] * (float)v[j];
+    }
+}
+
 template <int WM, bool DROP>
 __global__ __launch_bounds__(NT, 2) void stripe_bwd_fused_w(csu_stripe_args a, const bf16* __restrict__ qkv,
                                                             const bf16* __restrict__ out, const bf16* __restrict__ dout,
@@ -1377,9 +1429,11 @@ __global__ __launch_bounds__(NT, 2) void stripe_bwd_fused_w(csu_stripe_args a, c
     constexpr int RT = WM / 32;           // rows per thread in the prologue / 32-row tiles of the image
     __shared__ __attribute__((aligned(16))) bf16 Qs[WM * HD];
     __shared__ __attribute__((aligned(16))) bf16 Ks[WM * HD];
-    __shared__ __attribute__((aligned(16))) bf16 Vs[WM * HD];   // V image; from the main loop on: dS tile [key][q]
-    __shared__ __attribute__((aligned(16))) bf16 Gs[WM * HD];   // dO image
-    __shared__ __attribute__((aligned(16))) float lse_s[WM], dl_s[WM];
+    // V: PLAIN [row][32] image + a zero row at WM (the prologue); from the main loop on the first WM
+    // rows hold the swizzled dS tile [key][q]
+    __shared__ __attribute__((aligned(16))) bf16 Vs[(WM + 1) * HD];
+    __shared__ __attribute__((aligned(16))) bf16 Gs[(WM + 1) * HD];   // dO (swizzled) + a zero row at WM
+    __shared__ __attribute__((aligned(16))) float nlse_s[WM], dl_s[WM];
     __shared__ __attribute__((aligned(16))) float wts[HD * 10];
     __shared__ float red[4][8][41];
     __shared__ __attribute__((aligned(16))) unsigned char dtbl[4][128];
@@ -1391,9 +1445,10 @@ __global__ __launch_bounds__(NT, 2) void stripe_bwd_fused_w(csu_stripe_args a, c
     const bf16* img = qkv + (size_t)w.b * L * C3;
     const bf16* gimg = dout + (size_t)w.b * L * C;
     const int npad = (w.N + 31) & ~31, ntile = npad >> 5;
-    const float inv_scale = 1.f / a.scale;
+    const int c4 = threadIdx.x & 7, rg = threadIdx.x >> 3;   // prologue: channel quad, row group
 
-    // ---- staging: Q, K, V, dO images, the window's lse (as -lse / scale: the S accumulators' start)
+    // ---- staging: Q, K, V, dO images, the window's -lse * log2(e) (the exponent offsets)
+    u32x2 orow[RT];   // O rows of the prologue, loaded with the staging loads (global latency once)
     {
         const __amdgpu_buffer_rsrc_t rs_lse = stat_rsrc(a, lse);
         constexpr int SI = (WM + NT - 1) / NT;   // window rows per thread
@@ -1405,13 +1460,26 @@ __global__ __launch_bounds__(NT, 2) void stripe_bwd_fused_w(csu_stripe_args a, c
         }
         float lw[LW_IT];
         lepe_weights_load(branch(a, w.br), w.h, lw);
+        {
+            const __amdgpu_buffer_rsrc_t rs_o = buf_rsrc(out + (size_t)w.b * L * C, (long)L * C * 2);
+#pragma unroll
+            for (int k = 0; k < RT; ++k) {
+                const int n = rg + 32 * k;
+                orow[k] = __builtin_amdgcn_raw_buffer_load_b64(
+                    rs_o, n < w.N ? (unsigned)(((size_t)tok_of(w, a.reso, n) * C + w.chq + 4 * c4) * 2) : kOOB, 0, 0);
+            }
+        }
         stage_win2(w, a.reso, img, C3, w.chq, img, C3, C + w.chq, npad, Qs, Ks);
-        stage_win2(w, a.reso, img, C3, 2 * C + w.chq, gimg, C, w.chq, npad, Vs, Gs);
+        stage_win2_pa(w, a.reso, img, C3, 2 * C + w.chq, gimg, C, w.chq, npad, Vs, Gs);
         lepe_weights_store(lw, wts);
+        if (threadIdx.x < 8) {   // the zero rows
+            const bf16x8 z = {};
+            *reinterpret_cast<bf16x8*>((threadIdx.x < 4 ? Vs : Gs) + WM * HD + 8 * (threadIdx.x & 3)) = z;
+        }
 #pragma unroll
         for (int k = 0; k < SI; ++k) {
             const int i = threadIdx.x + k * NT;
-            if (i < npad) lse_s[i] = i < w.N ? -lv[k] * inv_scale : -INFINITY;   // padded queries: P = 0
+            if (i < npad) nlse_s[i] = i < w.N ? -lv[k] * kLog2e : -INFINITY;   // padded queries: P = 0
         }
     }
     __syncthreads();
@@ -1419,27 +1487,23 @@ __global__ __launch_bounds__(NT, 2) void stripe_bwd_fused_w(csu_stripe_args a, c
 
     // ---- prologue: delta and the LePE weight-gradient partials (thread: channel quad c4, rows rg + 32k)
     {
-        const int c4 = threadIdx.x & 7, rg = threadIdx.x >> 3;
         float wacc[40];
 #pragma unroll
         for (int i = 0; i < 40; ++i) wacc[i] = 0.f;
         const f32x4 bias = *reinterpret_cast<const f32x4*>(wts + HD * 9 + 4 * c4);
-        const __amdgpu_buffer_rsrc_t rs_o = buf_rsrc(out + (size_t)w.b * L * C, (long)L * C * 2);
-        auto load_o = [&](int n) {
-            return __builtin_amdgcn_raw_buffer_load_b64(
-                rs_o, n < w.N ? (unsigned)(((size_t)tok_of(w, a.reso, n) * C + w.chq + 4 * c4) * 2) : kOOB, 0, 0);
-        };
-        u32x2 o_next = load_o(rg), o_next2 = load_o(rg + 32);   // O rows two ahead
+        const bf16* vq = Vs + 4 * c4;                  // plain image: row n of this quad at vq + 32 n
         // rows one at a time (unrolled, the compiler turns the 40 accumulations into per-sum chains
-        // over all rows and keeps every row's V values live)
+        // over all rows and keeps every row's V values live); the preloaded O rows rotate through
+        // orow[0] so every register index stays static.  Out-of-window taps read the zero row.
 #pragma unroll 1
         for (int n = rg; n < npad; n += 32) {
             const bool valid = n < w.N;                    // uniform over the 8 lanes of the row
             const int nn = valid ? n : 0;
-            const u32x2 oraw = o_next;
-            o_next = o_next2;
-            o_next2 = load_o(n + 64);
+            const u32x2 oraw = orow[0];
+#pragma unroll
+            for (int k = 0; k + 1 < RT; ++k) orow[k] = orow[k + 1];
             const int iy = wrow(w, nn), ix = nn - iy * w.W_sp;
+            const bool ym = iy > 0, yp = iy + 1 < w.H_sp, xm = ix > 0, xp = ix + 1 < w.W_sp;
             const bf16x4 g4 = *reinterpret_cast<const bf16x4*>(Gs + swz(nn, 4 * c4));
             float gv[4], lp[4];
 #pragma unroll
@@ -1449,13 +1513,14 @@ __global__ __launch_bounds__(NT, 2) void stripe_bwd_fused_w(csu_stripe_args a, c
             }
 #pragma unroll
             for (int t = 0; t < 9; ++t) {
-                const int y = iy + t / 3 - 1, x = ix + t % 3 - 1;
-                const bool in = y >= 0 && y < w.H_sp && x >= 0 && x < w.W_sp;
-                const bf16x4 v4 = *reinterpret_cast<const bf16x4*>(Vs + swz(in ? y * w.W_sp + x : nn, 4 * c4));
+                const int dy = t / 3 - 1, dx = t % 3 - 1;
+                const bool in = (dy < 0 ? ym : dy > 0 ? yp : true) && (dx < 0 ? xm : dx > 0 ? xp : true);
+                const int row = in ? nn + dy * w.W_sp + dx : WM;
+                const bf16x4 v4 = *reinterpret_cast<const bf16x4*>(vq + row * HD);
                 const f32x4 wt = *reinterpret_cast<const f32x4*>(wts + t * HD + 4 * c4);
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
-                    const float v = in ? (float)v4[j] : 0.f;
+                    const float v = (float)v4[j];
                     lp[j] = fmaf(wt[j], v, lp[j]);
                     wacc[4 * t + j] = fmaf(gv[j], v, wacc[4 * t + j]);
                 }
@@ -1485,19 +1550,17 @@ __global__ __launch_bounds__(NT, 2) void stripe_bwd_fused_w(csu_stripe_args a, c
     }
     // ---- registers for the main loop (loaded after the prologue, before the V image is overwritten):
     // the own key tiles' K and V rows (B operands of S and dP)
-    const int dh = wave & 1, qh = wave >> 1;
     Frag<bf16> kf[KT], vf[KT];
 #pragma unroll
     for (int j = 0; j < KT; ++j) {
         const int kt = wave + 4 * j;
+        const int row = (kt < ntile ? kt : 0) * 32 + r;
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
-            const int row = (kt < ntile ? kt : 0) * 32 + r;
             kf[j].v[s] = *reinterpret_cast<const bf16x8*>(Ks + swz(row, 16 * s + 8 * h));
-            vf[j].v[s] = *reinterpret_cast<const bf16x8*>(Vs + swz(row, 16 * s + 8 * h));
+            vf[j].v[s] = *reinterpret_cast<const bf16x8*>(Vs + row * HD + 16 * s + 8 * h);
         }
     }
-
     __syncthreads();   // dl_s / red complete; every read of the V image is done (it becomes the dS tile)
     if (part) {
         const int nwx = a.reso / w.W_sp, nwin = (a.reso / w.H_sp) * nwx;
@@ -1510,7 +1573,8 @@ __global__ __launch_bounds__(NT, 2) void stripe_bwd_fused_w(csu_stripe_args a, c
         }
     }
 
-    // ---- main loop over query tiles
+    // ---- main loop over query tiles.  Every LDS address of the loop is (tile base) + a per-lane offset
+    // computed here once: the swizzle depends only on the row's position inside its 32-row tile.
     const float c = a.scale * kLog2e;
     ADrop dr;
     if constexpr (DROP) dr = attn_drop(a, w);
@@ -1518,61 +1582,104 @@ __global__ __launch_bounds__(NT, 2) void stripe_bwd_fused_w(csu_stripe_args a, c
 #pragma unroll
     for (int j = 0; j < KT; ++j) { dk[j] = f32x16{}; dv[j] = f32x16{}; }
     bf16* const dS = Vs;
+    const int dh = wave & 1, qh = wave >> 1;
+    int o_row[2], o_tr[2][2], o_ds[4], o_k16[2], o_d16[2];
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+        o_row[s2] = swz(r, 16 * s2 + 8 * h);                        // A rows (mma_rows_sw)
+        const int grp = lane >> 4, l = lane & 15, q = l >> 2, p4 = l & 3;
+        const int col = 16 * (grp & 1) + 4 * p4, row = 16 * s2 + 4 * (grp >> 1) + q;
+        o_tr[s2][0] = swz(row, col);                                // transposed A (tr_frag_acc)
+        o_tr[s2][1] = swz(row + 8, col);
+        const int g16 = lane >> 4, i16 = lane & 15;
+        o_k16[s2] = swz(8 * g16 + 4 * s2 + (i16 >> 2), 16 * dh + 4 * (i16 & 3));   // 16x16x32 operands
+        o_d16[s2] = swz(8 * g16 + 4 * s2 + (i16 >> 2), 16 * qh + 4 * (i16 & 3));
+    }
+#pragma unroll
+    for (int g = 0; g < 4; ++g) o_ds[g] = swz(r, 8 * g + 4 * h);
+    auto trA = [&](const bf16* base, int s2) {
+        const v4s lo = tr_read(base + o_tr[s2][0]);
+        const v4s hi = tr_read(base + o_tr[s2][1]);
+        const v4s v[2] = {lo, hi};
+        bf16x8 o;
+        __builtin_memcpy(&o, v, 16);
+        return o;
+    };
+    auto tr16 = [&](const bf16* base, const int* off) {
+        const v4s lo = tr_read(base + off[0]);
+        const v4s hi = tr_read(base + off[1]);
+        const v4s v[2] = {lo, hi};
+        bf16x8 o;
+        __builtin_memcpy(&o, v, 16);
+        return o;
+    };
+    ATT_STAMP(1, 2);
     for (int qt = 0; qt < ntile; ++qt) {
         const int qb = qt * 32;
+        const bf16* qrow = Qs + qb * HD;
+        const bf16* grow = Gs + qb * HD;
+        f32x4 nl[4], dq4[4];                               // rows qb + 8 g4 + 4 h + 0..3
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+            nl[g4] = *reinterpret_cast<const f32x4*>(nlse_s + qb + 8 * g4 + 4 * h);
+            dq4[g4] = *reinterpret_cast<const f32x4*>(dl_s + qb + 8 * g4 + 4 * h);
+        }
+        // no early exit for key tiles past the window (ntile < RT): their results are discarded (dS rows
+        // >= npad are never read, dK / dV never stored) -- straight-line code lets the compiler
+        // interleave the two tiles' MFMA chains and VALU work
 #pragma unroll
         for (int j = 0; j < KT; ++j) {
             const int kt = wave + 4 * j;
-            if (kt >= ntile) continue;                     // wave-uniform
-            f32x16 s, dp;
+            f32x16 s = {}, dp = {};
 #pragma unroll
-            for (int g4 = 0; g4 < 4; ++g4) {              // rows qb + 8 g4 + 4 h + 0..3
-                const f32x4 lq = *reinterpret_cast<const f32x4*>(lse_s + qb + 8 * g4 + 4 * h);
-                const f32x4 dq4 = *reinterpret_cast<const f32x4*>(dl_s + qb + 8 * g4 + 4 * h);
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    s[4 * g4 + e] = lq[e];
-                    dp[4 * g4 + e] = DROP ? 0.f : -dq4[e];
-                }
+            for (int s2 = 0; s2 < 2; ++s2) {
+                s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<const bf16x8*>(qrow + o_row[s2]), kf[j].v[s2],
+                                                            s, 0, 0, 0);    // S   [q][key]
+                dp = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<const bf16x8*>(grow + o_row[s2]), vf[j].v[s2],
+                                                             dp, 0, 0, 0);  // dP  [q][key]
             }
-            mma_rows_sw(s, Qs, qb, r, h, kf[j]);           // S - lse/scale      [q][key]
-            mma_rows_sw(dp, Gs, qb, r, h, vf[j]);          // dP - delta         [q][key]
             unsigned km = 0xffffu;
-            if constexpr (DROP) {
-                km = keep_k16(dr, qb, kt * 32, lane, dtbl[wave]);
-#pragma unroll
-                for (int g4 = 0; g4 < 4; ++g4) {
-                    const f32x4 dq4 = *reinterpret_cast<const f32x4*>(dl_s + qb + 8 * g4 + 4 * h);
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        const int i = 4 * g4 + e;
-                        dp[i] = (((km >> i) & 1u) ? dp[i] * dr.R.scale : 0.f) - dq4[e];
-                    }
-                }
-            }
+            if constexpr (DROP) km = keep_k16(dr, qb, kt * 32, lane, dtbl[wave]);
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
-                const float p = __builtin_amdgcn_exp2f(s[i] * c);
-                dp[i] = p * dp[i];                         // dS
+                const int g4 = i >> 2, e = i & 3;
+                const float p = __builtin_amdgcn_exp2f(fmaf(s[i], c, nl[g4][e]));
+                float gdp = dp[i];
+                if constexpr (DROP) gdp = ((km >> i) & 1u) ? gdp * dr.R.scale : 0.f;   // dP through the mask
+                dp[i] = p * (gdp - dq4[g4][e]);             // dS
                 if constexpr (DROP) s[i] = ((km >> i) & 1u) ? p * dr.R.scale : 0.f;   // dV sees the dropped P
                 else s[i] = p;
             }
-            mma_acc_sw(dv[j], Gs, qb, lane, s);            // dV^T += dO^T P
-            mma_acc_sw(dk[j], Qs, qb, lane, dp);           // dK^T += Q^T dS
+            bf16x8 pb[2], db[2];
 #pragma unroll
-            for (int g = 0; g < 4; ++g) {                  // dS -> [key][q] image: q = 8 g + 4 h + 0..3
-                const bf16x4 x = {(bf16)dp[4 * g], (bf16)dp[4 * g + 1], (bf16)dp[4 * g + 2], (bf16)dp[4 * g + 3]};
-                *reinterpret_cast<bf16x4*>(dS + swz(kt * 32 + r, 8 * g + 4 * h)) = x;
+            for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    pb[s2][e] = (bf16)s[8 * s2 + e];
+                    db[s2][e] = (bf16)dp[8 * s2 + e];
+                }
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) {
+                dv[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trA(grow, s2), pb[s2], dv[j], 0, 0, 0);   // dV^T += dO^T P
+                dk[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trA(qrow, s2), db[s2], dk[j], 0, 0, 0);   // dK^T += Q^T dS
+            }
+            bf16* dst = dS + kt * 32 * HD;                 // dS -> [key][q] image: q = 8 g + 4 h + 0..3
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const bf16x4 x = {db[g >> 1][4 * (g & 1)], db[g >> 1][4 * (g & 1) + 1], db[g >> 1][4 * (g & 1) + 2],
+                                  db[g >> 1][4 * (g & 1) + 3]};
+                *reinterpret_cast<bf16x4*>(dst + o_ds[g]) = x;
             }
         }
         __syncthreads();
         // dQ^T[d][q] quadrant (d = 16 dh + 4 (lane >> 4) + i, q = qb + 16 qh + (lane & 15)) over all keys
-        f32x4v acc = {0.f, 0.f, 0.f, 0.f};
+        f32x4v acc2[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};   // two independent MFMA chains
 #pragma unroll
         for (int kk = 0; kk < RT; ++kk)
             if (kk < ntile)
-                acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr_frag16(Ks, kk * 32, 16 * dh, lane),
-                                                              tr_frag16(dS, kk * 32, 16 * qh, lane), acc, 0, 0, 0);
+                acc2[kk & 1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr16(Ks + kk * 32 * HD, o_k16),
+                                                                      tr16(dS + kk * 32 * HD, o_d16), acc2[kk & 1], 0, 0, 0);
+        const f32x4v acc = acc2[0] + acc2[1];
         {
             const int qn = qb + 16 * qh + (lane & 15);
             if (qn < w.N) {
@@ -1583,6 +1690,7 @@ __global__ __launch_bounds__(NT, 2) void stripe_bwd_fused_w(csu_stripe_args a, c
         }
         __syncthreads();                                   // the dS tile is rewritten by the next query tile
     }
+    ATT_STAMP(1, 3);
 
     // ---- dK, dV (+ LePE input gradient: the transposed conv of dO) of the own key tiles
 #pragma unroll
@@ -1594,7 +1702,7 @@ __global__ __launch_bounds__(NT, 2) void stripe_bwd_fused_w(csu_stripe_args a, c
         for (int g4 = 0; g4 < 4; ++g4) {
             const int d0 = 8 * g4 + 4 * h;
             float vk[4], vv[4], lp[4];
-            lepe4_lds(w, Gs, kn, d0, wts, -1, lp);
+            lepe4_lds_z(w, Gs, kn, d0, wts, -1, WM, lp);
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
                 vk[e] = dk[j][4 * g4 + e] * a.scale;
@@ -1604,7 +1712,7 @@ __global__ __launch_bounds__(NT, 2) void stripe_bwd_fused_w(csu_stripe_args a, c
             store4(drow + 2 * C + d0, vv);
         }
     }
-    ATT_STAMP(1, 2);
+    ATT_STAMP(1, 4);
 }
 
 // the one-pass backward handles the launch (bf16, window <= 256 tokens)

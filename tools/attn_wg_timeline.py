@@ -38,8 +38,18 @@ def main():
     L = lib()
     fn = L.csu_debug_attn_ts
     fn.restype, fn.argtypes = ctypes.c_int, [ctypes.c_void_p]
-    buf = np.zeros((3, 4, 16384), dtype=np.uint64)
+    buf = np.zeros((3, 6, 16384), dtype=np.uint64)
     assert fn(buf.ctypes.data) == 0
+    if st <= 4 and max(sw * reso, reso * reso if sw == reso else 0) <= 256 or True:
+        t = buf[1, :5].astype(np.int64)
+        valid = (t[0] > 0) & (t[4] > 0)
+        if valid.any():   # one-pass backward (stripe_bwd_fused_w): start, staged, prologue, main loop, end
+            t = t[:, valid]
+            ph = np.diff(t, axis=0) / 100.0
+            tot = (t[4] - t[0]) / 100.0
+            print(f"stage {st} fused bwd: {t.shape[1]} workgroups, span {(t[4].max() - t[0].min()) / 100:.1f} us, "
+                  f"per WG p50 {np.median(tot):.1f} us = staging {np.median(ph[0]):.1f} + prologue "
+                  f"{np.median(ph[1]):.1f} + main {np.median(ph[2]):.1f} + epilogue {np.median(ph[3]):.1f}")
     for k, name in enumerate(("fwd", "dq", "dkdv")):
         t = buf[k, :3].astype(np.int64)
         valid = t[0] > 0
