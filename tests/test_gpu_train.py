@@ -18,7 +18,9 @@
       measured distance is ~3e-8: the same trajectory);
     - csu bf16: the window's MEAN Dice / IoU within 1e-3 / 2e-3 of the reference fp32 run's, every
       single checkpoint within 5e-3 (the reference's own worst bf16 checkpoint distance), and the
-      per-epoch mean train loss within 5 % in the window (fp32: 2 % everywhere).
+      per-epoch mean train loss within max(5 %, 1.5 x the reference's own fp32/bf16 spread of that
+      epoch) in the window (the reference's bf16 run is up to 7.8 % off its fp32 run per epoch at
+      512x512 late in training, where the loss is ~5e-3; fp32: 2 % everywhere).
   Every eval point's values and deltas are written to $CSU_PARITY_LOG (default gpurun_out/) as
   dice_parity_<fixture>_<precision>.json (committed copies: profiles/r03_dice_parity_*.json).
 * FusedAdamW checkpoints: save -> load -> continue equals the uninterrupted run; the state_dict
@@ -104,6 +106,8 @@ def _check_trajectory(golden_dir, fixture, amp):
         dd = abs(h["test_dice"][i] - ref["eval_dice"][i])
         di = abs(h["test_iou"][i] - ref["eval_iou"][i])
         mean_ref = float(np.mean(ref["loss"][every * i:every * i + every]))
+        own = abs(float(np.mean(refb["loss"][every * i:every * i + every])) - mean_ref) / mean_ref
+        ltol_i = ltol if amp is None else max(ltol, 1.5 * own)
         rows.append({"step": s, "gated": s >= g, "csu_dice": h["test_dice"][i], "ref_dice": ref["eval_dice"][i],
                      "ref_bf16_dice": refb["eval_dice"][i], "abs_d_dice": dd,
                      "ref_own_spread_dice": abs(ref["eval_dice"][i] - refb["eval_dice"][i]),
@@ -111,10 +115,10 @@ def _check_trajectory(golden_dir, fixture, amp):
                      "csu_iou": h["test_iou"][i],
                      "ref_iou": ref["eval_iou"][i], "abs_d_iou": di, "csu_eval_loss": h["test_loss"][i],
                      "ref_eval_loss": ref["eval_loss"][i], "csu_train_loss": h["train_loss"][i],
-                     "ref_train_loss": mean_ref})
+                     "ref_train_loss": mean_ref, "ref_own_rel_spread_train_loss": own, "train_loss_rel_tol": ltol_i})
         if s >= g and (dd > point_tol[0] or di > point_tol[1]):
             bad.append(f"step {s}: |dDice| {dd:.2e} |dIoU| {di:.2e}")
-        if (amp is None or s >= g) and abs(h["train_loss"][i] - mean_ref) > ltol * mean_ref:
+        if (amp is None or s >= g) and abs(h["train_loss"][i] - mean_ref) > ltol_i * mean_ref:
             bad.append(f"epoch {i}: train loss {h['train_loss'][i]:.5f} vs {mean_ref:.5f}")
     gated = [r for r in rows if r["gated"]]
     mean = lambda k: float(np.mean([r[k] for r in gated]))   # noqa: E731
