@@ -16,6 +16,8 @@ constexpr int WAVES = NT / 64;
 constexpr int LU = 4;       // ln_bwd: row groups per wave iteration
 constexpr int FU = 4;       // ln_fwd: row groups per wave
 
+struct e4m3 { uint8_t v; };  // ln_fwd output type: OCP e4m3fn bytes + one power-of-two scale per row
+
 template <typename T, int V> __device__ __forceinline__ void ldv(const T* p, float* v) {
     if constexpr (V == 8) load8(p, v);
     else if constexpr (V == 4) load4(p, v);
@@ -68,7 +70,8 @@ template <int LPR> __device__ __forceinline__ float group_sum(float v) {
 template <typename TX, typename TY, int V, int LPR>
 __global__ __launch_bounds__(NT) void ln_fwd(int rows, int C, float eps, const TX* __restrict__ x,
                                              const float* __restrict__ gamma, const float* __restrict__ beta,
-                                             TY* __restrict__ y, float* __restrict__ mean, float* __restrict__ rstd) {
+                                             TY* __restrict__ y, float* __restrict__ mean, float* __restrict__ rstd,
+                                             float* __restrict__ ysc) {
     constexpr int RPW = 64 / LPR;
     const int lane = threadIdx.x & 63;
     const int rb = (blockIdx.x * WAVES + (threadIdx.x >> 6)) * RPW * FU + lane / LPR;
@@ -104,9 +107,31 @@ __global__ __launch_bounds__(NT) void ln_fwd(int rows, int C, float eps, const T
 #pragma unroll
         for (int j = 0; j < V; ++j) o[j] = v[u][j] * rs * gw[j] + bw[j];
         const unsigned e = e0[u];
-        bst<TY, V>(rs_y, e == kOOB ? kOOB : e * (unsigned)sizeof(TY), o);
         const int row = rb + u * RPW;
         const unsigned ro = (lane % LPR == 0 && row < rows) ? (unsigned)row * 4u : kOOB;
+        if constexpr (sizeof(TY) == 1) {
+            // fp8 output (the e4m3 GEMM's activation operand, csrc/fp8gemm.hip): the row's amax over
+            // its LPR lanes, power-of-two scale s = 2^ceil(log2(amax / 448)) as the weights'
+            // (csrc/fp8.hip), y / s rounded to e4m3 (RNE; |y / s| <= 448, nothing saturates)
+            float am = 0.f;
+#pragma unroll
+            for (int j = 0; j < V; ++j) am = fmaxf(am, fabsf(o[j]));
+#pragma unroll
+            for (int m = LPR / 2; m > 0; m >>= 1) am = fmaxf(am, __shfl_xor(am, m, 64));
+            const float s = am > 0.f ? exp2f(ceilf(log2f(am / 448.f))) : 1.f;
+            const float inv = 1.f / s;
+            unsigned w[V / 4];
+#pragma unroll
+            for (int k = 0; k < V / 4; ++k) {
+                int p = __builtin_amdgcn_cvt_pk_fp8_f32(o[4 * k] * inv, o[4 * k + 1] * inv, 0, false);
+                w[k] = (unsigned)__builtin_amdgcn_cvt_pk_fp8_f32(o[4 * k + 2] * inv, o[4 * k + 3] * inv, p, true);
+            }
+            if constexpr (V == 8) __builtin_amdgcn_raw_buffer_store_b64(u32x2{w[0], w[1]}, rs_y, e, 0, 0);
+            else __builtin_amdgcn_raw_buffer_store_b32(w[0], rs_y, e, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(s), buf_rsrc(ysc, (long)rows * 4), ro, 0, 0);
+        } else {
+            bst<TY, V>(rs_y, e == kOOB ? kOOB : e * (unsigned)sizeof(TY), o);
+        }
         __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(mu), rs_m, ro, 0, 0);
         __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(rs), rs_s, ro, 0, 0);
     }
@@ -230,11 +255,11 @@ int check_rows(int rows, int C) {   // 32-bit byte offsets of the raw buffer ops
 
 template <typename TX, typename TY>
 int launch_fwd(int rows, int C, float eps, const void* x, const float* g, const float* b, void* y, float* m,
-               float* r, hipStream_t st) {
+               float* r, hipStream_t st, float* ysc = nullptr) {
 #define CSU_LNF(V, LPR)                                                                                           \
     ln_fwd<TX, TY, V, LPR><<<(rows + WAVES * (64 / LPR) * FU - 1) / (WAVES * (64 / LPR) * FU), NT, 0, st>>>(rows, C, eps, \
                                                                                                   (const TX*)x, g, b, \
-                                                                                                  (TY*)y, m, r)
+                                                                                                  (TY*)y, m, r, ysc)
     switch (C / 64) {
         case 1: CSU_LNF(4, 16); break;
         case 2: CSU_LNF(4, 32); break;
@@ -284,6 +309,18 @@ extern "C" int csu_layernorm_fwd(int rows, int C, float eps, int xdtype, const v
     if (xdtype == CSU_BF16 && ydtype == CSU_F32) return launch_fwd<bf16, float>(rows, C, eps, x, gamma, beta, y, mean, rstd, st);
     if (xdtype == CSU_BF16 && ydtype == CSU_BF16) return launch_fwd<bf16, bf16>(rows, C, eps, x, gamma, beta, y, mean, rstd, st);
     return fail(CSU_E_ARG, "layernorm_fwd: bad dtype");
+}
+
+extern "C" int csu_layernorm_fwd_fp8(int rows, int C, float eps, int xdtype, const void* x, const float* gamma,
+                                     const float* beta, void* yq, float* yscale, float* mean, float* rstd, void* stream) {
+    if (int e = check_c(C)) return e;
+    if (int e = check_rows(rows, C)) return e;
+    if (rows < 1 || !x || !gamma || !beta || !yq || !yscale || !mean || !rstd)
+        return fail(CSU_E_ARG, "layernorm_fwd_fp8: bad args");
+    hipStream_t st = as_stream(stream);
+    if (xdtype == CSU_F32) return launch_fwd<float, e4m3>(rows, C, eps, x, gamma, beta, yq, mean, rstd, st, yscale);
+    if (xdtype == CSU_BF16) return launch_fwd<bf16, e4m3>(rows, C, eps, x, gamma, beta, yq, mean, rstd, st, yscale);
+    return fail(CSU_E_ARG, "layernorm_fwd_fp8: bad dtype");
 }
 
 extern "C" size_t csu_layernorm_bwd_workspace(int rows, int C) {

@@ -139,6 +139,9 @@ _SIGS = {
     "csu_gemm_f32": (ctypes.c_int, [ctypes.c_int, ctypes.c_long, ctypes.c_int, ctypes.c_long, c_void_p, c_void_p, c_void_p,
                                     c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
     "csu_quant_e4m3_batch": (ctypes.c_int, [c_void_p, ctypes.c_int, ctypes.c_long, c_void_p]),
+    "csu_fp8_gemm": (ctypes.c_int, [ctypes.c_long, ctypes.c_int, ctypes.c_int] + [c_void_p] * 7),
+    "csu_layernorm_fwd_fp8": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, c_float, ctypes.c_int] + [c_void_p] * 8),
+    "csu_dequant_e4m3_rows": (ctypes.c_int, [ctypes.c_long, ctypes.c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
     "csu_mlp_supported": (ctypes.c_int, [ctypes.c_int]),
     "csu_dropout_apply": (ctypes.c_int, [ctypes.c_long, ctypes.c_int, ctypes.c_int, c_void_p, c_void_p, ctypes.c_int,
                                          c_void_p, c_void_p, ctypes.c_long, c_void_p, ctypes.c_uint, c_float, c_void_p]),

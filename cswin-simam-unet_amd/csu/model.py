@@ -230,8 +230,12 @@ class CSWinBlock(nn.Module):
         # residual junctions x -> (x, LN(x)): their backward adds the two branch gradients in the
         # LayerNorm-backward kernel and hands the upstream GEMMs a bf16 copy (ops.layer_norm_fork)
         n1, n2 = self.norm1, self.norm2
-        xa, h1 = ops.layer_norm_fork(x, n1.weight, n1.bias, n1.eps, cd)
-        qkv = ops.linear(h1, self.qkv.weight, self.qkv.bias)
+        got = ops.ln_linear_fp8(x, n1, self.qkv) if cd == torch.bfloat16 else None
+        if got is not None:
+            xa, qkv = got        # fp8 weight format: e4m3 norm1 output x e4m3 qkv weight on fp8 MFMA
+        else:
+            xa, h1 = ops.layer_norm_fork(x, n1.weight, n1.bias, n1.eps, cd)
+            qkv = ops.linear(h1, self.qkv.weight, self.qkv.bias)
         ad = ops.AttnDrop(snap, base + rng.OFF_ATTN, p_attn) if p_attn > 0 else None
         att = ops.stripe_attention(qkv, self._geom, [a.get_v.weight for a in self.attns],
                                    [a.get_v.bias for a in self.attns], ad)
@@ -544,7 +548,7 @@ class CSWinTransformer(nn.Module):
                 sources = self._fp8.quantize()     # one launch: e4m3 per row, dequantised fp32 copies
             # one launch per step: bf16 shadows of every Linear weight (+ transposes) and conv layouts
             self._cast_cache.refresh(weights, cd, self._conv_weights(), sources=sources)
-            ops.set_cast_cache(self._cast_cache)
+            ops.set_cast_cache(self._cast_cache, self._fp8 if sources is not None else None)
         try:
             return self._forward(x)
         finally:

@@ -493,36 +493,44 @@ class _LayerNormForkFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dres, dy):
         x, w, mean, rstd = ctx.saved_tensors
-        C = x.shape[-1]
-        rows = x.numel() // C
-        if dy is None:
-            dy = torch.zeros(x.shape, dtype=torch.float32, device=x.device)
-        dy = dy.contiguous()
-        if dy.dtype not in (torch.float32, torch.bfloat16):
-            dy = dy.float()
-        fp32 = x.dtype == torch.float32
-        dres_k = dres.float().contiguous() if (dres is not None and fp32) else None
-        dx = torch.empty_like(x)
-        dxb = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device) if fp32 else None
-        L = lib()
-        nbytes = L.csu_layernorm_bwd_workspace(rows, C)
-        work = torch.empty(max(nbytes, 16), dtype=torch.uint8, device=x.device)
-        dgb = _grad_dest(ctx.params)
-        if dgb is None:
-            dgb = torch.empty(2 * C, dtype=torch.float32, device=x.device)
-        late = _ln_params(ctx, rows, C, work, dgb)
-        pg, pb = (None, None) if late else (ptr(dgb[:C]), ptr(dgb[C:]))
-        _launch("layernorm_bwd", lambda: L.csu_layernorm_bwd_ex(rows, C, dtype_code(x), ptr(x), ptr(w), ptr(mean),
-                                                                ptr(rstd), dtype_code(dy), ptr(dy), ptr(dres_k), ptr(dx),
-                                                                ptr(dxb), pg, pb, ptr(work), nbytes,
-                                                                stream_ptr(x.device)),
-                12 * rows * C, rows * C * (2 * esize(x) + esize(dy) + esize(dres_k) + esize(dxb)) + rows * 8,
-                prec=prec_of(x))
-        if dres is not None and not fp32:    # non-fp32 residual stream: plain add (not on the bf16 path)
-            dx = dx + dres.to(dx.dtype)
-        if dxb is not None:
-            dx._csu_bf16 = dxb
-        return dx, dgb[:C].to(ctx.pdtypes[0]), dgb[C:].to(ctx.pdtypes[1]), None, None
+        dx, dg, db = _ln_fork_backward(ctx, x, w, mean, rstd, dres, dy)
+        return dx, dg, db, None, None
+
+
+def _ln_fork_backward(ctx, x, w, mean, rstd, dres, dy):
+    """dx = dres + LN'(dy) in one csu_layernorm_bwd_ex pass (+ the bf16 copy of dx as
+    ``_csu_bf16``), dgamma / dbeta (deferred into the batched reduction when allowed).  ctx carries
+    the LN parameters (``params``, ``pdtypes``)."""
+    C = x.shape[-1]
+    rows = x.numel() // C
+    if dy is None:
+        dy = torch.zeros(x.shape, dtype=torch.float32, device=x.device)
+    dy = dy.contiguous()
+    if dy.dtype not in (torch.float32, torch.bfloat16):
+        dy = dy.float()
+    fp32 = x.dtype == torch.float32
+    dres_k = dres.float().contiguous() if (dres is not None and fp32) else None
+    dx = torch.empty_like(x)
+    dxb = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device) if fp32 else None
+    L = lib()
+    nbytes = L.csu_layernorm_bwd_workspace(rows, C)
+    work = torch.empty(max(nbytes, 16), dtype=torch.uint8, device=x.device)
+    dgb = _grad_dest(ctx.params)
+    if dgb is None:
+        dgb = torch.empty(2 * C, dtype=torch.float32, device=x.device)
+    late = _ln_params(ctx, rows, C, work, dgb)
+    pg, pb = (None, None) if late else (ptr(dgb[:C]), ptr(dgb[C:]))
+    _launch("layernorm_bwd", lambda: L.csu_layernorm_bwd_ex(rows, C, dtype_code(x), ptr(x), ptr(w), ptr(mean),
+                                                            ptr(rstd), dtype_code(dy), ptr(dy), ptr(dres_k), ptr(dx),
+                                                            ptr(dxb), pg, pb, ptr(work), nbytes,
+                                                            stream_ptr(x.device)),
+            12 * rows * C, rows * C * (2 * esize(x) + esize(dy) + esize(dres_k) + esize(dxb)) + rows * 8,
+            prec=prec_of(x))
+    if dres is not None and not fp32:    # non-fp32 residual stream: plain add (not on the bf16 path)
+        dx = dx + dres.to(dx.dtype)
+    if dxb is not None:
+        dx._csu_bf16 = dxb
+    return dx, dgb[:C].to(ctx.pdtypes[0]), dgb[C:].to(ctx.pdtypes[1])
 
 
 def layer_norm_fork(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, eps: float = 1e-5,
@@ -1439,13 +1447,50 @@ def mlp_residual(res, x, fc1: torch.nn.Linear, fc2: torch.nn.Linear, drop: Optio
                                     _weight_bf16(fc2.weight), drop)
 
 
+# fp32 master weight (by storage address) -> (weakref to it, its CastCache, index in the cache,
+# AdamW shadow spec): csu.optim.FusedAdamW writes the bf16 shadows of these weights in its update
+# pass (csu_adamw_step shadow modes), so the next forward needs no cast launch.
+_SHADOW_SPECS = {}
+
+
+def shadow_spec(p: torch.Tensor):
+    """(shadow ptr, shadow_t ptr, rows, cols, taps, cols_pad) of the bf16 layouts a CastCache keeps of
+    the fp32 weight p (csu_adamw_item shadow fields), or None."""
+    e = _SHADOW_SPECS.get(p.data_ptr())
+    if e is None or e[0]() is not p:
+        return None
+    return e[3]
+
+
+def shadows_written(params):
+    """FusedAdamW wrote the shadows of these weights (in its launch just enqueued): their caches
+    note the weights' current versions, so the next refresh skips the cast while nothing else has
+    modified them."""
+    for p in params:
+        e = _SHADOW_SPECS.get(p.data_ptr())
+        if e is not None and e[0]() is p:
+            e[1]._written[e[2]] = p._version
+
+
+def sync_shadows(model):
+    """Bring a model's cast cache up to date before replaying a captured graph whose forward
+    relies on the optimizer-written shadows (a weight modified in place since, e.g. by
+    load_state_dict, is re-cast here, outside the graph)."""
+    c = getattr(model, "_cast_cache", None)
+    if c is not None:
+        c.ensure_fresh()
+
+
 class CastCache:
-    """bf16 shadow copies of fp32 master weights, refreshed once per forward by ONE launch of
-    csu_cast_bf16_batch (instead of one cast kernel per Linear), plus a transposed (K, N) copy of
-    every 2-D weight for the input-gradient GEMM, and the two channels-last layouts (OHWI, IHWO)
-    of every KxK conv weight for the implicit-GEMM conv kernels.  Gradients still flow to the fp32
-    params.  Lookup is by storage address, so reshaped views of a cached weight (the CARAFE 1x1
-    convs used as token Linears) hit the cache too."""
+    """bf16 shadow copies of fp32 master weights, plus a transposed (K, N) copy of every 2-D weight
+    for the input-gradient GEMM, and the two channels-last layouts (OHWI, IHWO) of every KxK conv
+    weight for the implicit-GEMM conv kernels.  Gradients still flow to the fp32 params.  Lookup is
+    by storage address, so reshaped views of a cached weight (the CARAFE 1x1 convs used as token
+    Linears) hit the cache too.
+    Freshness: csu.optim.FusedAdamW writes every shadow in its update pass (shadow_spec), so a
+    forward after an optimizer step launches nothing; ONE csu_cast_bf16_batch launch re-makes all
+    of them whenever a weight's version counter moved since the last write (first forward,
+    load_state_dict, any in-place change), or always when they come from fp8 sources."""
 
     _REC = None
 
@@ -1483,6 +1528,9 @@ class CastCache:
         self.cindex = {w.data_ptr(): i for i, w in enumerate(convs)}
         self.items = None
         allp = params + convs
+        self._written = [None] * len(allp)
+        for k in [k for k, e in _SHADOW_SPECS.items() if e[1] is self]:
+            del _SHADOW_SPECS[k]
         if (dtype == torch.bfloat16 and allp and all(p.is_cuda and p.dtype == torch.float32 and p.is_contiguous()
                                                      for p in allp)):
             import numpy as np
@@ -1503,6 +1551,18 @@ class CastCache:
                 t0 += -(-(N * C * KH * KW) // 4096)
             self.tiles = t0
             self.items = torch.frombuffer(bytearray(rec.tobytes()), dtype=torch.uint8).to(allp[0].device)
+            if sources is None:
+                import weakref
+                for i, p in enumerate(params):
+                    rows = p.shape[0] if p.dim() > 1 else 1
+                    st = self.shadow_t[i]
+                    _SHADOW_SPECS[p.data_ptr()] = (weakref.ref(p), self, i, (
+                        self.shadow[i].data_ptr(), 0 if st is None else st.data_ptr(), rows, p.numel() // rows, 0, 0))
+                for j, w in enumerate(convs):
+                    ci = self.conv_i[j]
+                    _SHADOW_SPECS[w.data_ptr()] = (weakref.ref(w), self, len(params) + j, (
+                        self.conv_o[j].data_ptr(), 0 if ci is None else ci.data_ptr(), w.shape[0], w.shape[1],
+                        w.shape[2] * w.shape[3], self.conv_cp[j]))
 
     def refresh(self, params, dtype, convs=(), sources=None):
         """``sources``: per param, the fp32 tensor the shadow is made from (default: the param
@@ -1516,11 +1576,8 @@ class CastCache:
                 or (sources is not None and any(a is not b for a, b in zip(sources, self.sources)))):
             self._build(params, convs, dtype, sources)
         if self.items is not None:
-            n = sum(p.numel() for p in allp)
-            nt = sum(p.numel() for p in self.params if p.dim() > 1) + sum(w.numel() for w in self.convs)
-            _launch("cast_bf16_batch", lambda: lib().csu_cast_bf16_batch(ptr(self.items), len(allp), self.tiles,
-                                                                         stream_ptr(allp[0].device)),
-                    0, n * 6 + nt * 2)
+            if self.sources is not None or not self._fresh():
+                self._cast()
             return
         src = self.sources if getattr(self, "sources", None) is not None else self.params
         with torch.no_grad():
@@ -1533,6 +1590,24 @@ class CastCache:
                 o[..., :w.shape[1]].copy_(w.detach().permute(0, 2, 3, 1))
                 if i is not None:
                     i.copy_(w.detach().permute(1, 2, 3, 0))
+
+    def _fresh(self) -> bool:
+        return all(w is not None and w == p._version for w, p in zip(self._written, self.params + self.convs))
+
+    def _cast(self):
+        allp = self.params + self.convs
+        n = sum(p.numel() for p in allp)
+        nt = sum(p.numel() for p in self.params if p.dim() > 1) + sum(w.numel() for w in self.convs)
+        _launch("cast_bf16_batch", lambda: lib().csu_cast_bf16_batch(ptr(self.items), len(allp), self.tiles,
+                                                                     stream_ptr(allp[0].device)),
+                0, n * 6 + nt * 2)
+        if self.sources is None:
+            self._written = [p._version for p in allp]
+
+    def ensure_fresh(self):
+        """Re-cast now if a weight changed since its shadows were last written (see class doc)."""
+        if self.items is not None and self.sources is None and not self._fresh():
+            self._cast()
 
     def get(self, p, dtype):
         i = self.index.get(p.data_ptr())
@@ -1591,6 +1666,14 @@ class Fp8Weights:
         self.count, self.rows = len(recs), row0
         self.items = torch.frombuffer(bytearray(rec.tobytes()), dtype=torch.uint8).to(self.params[0].device)
         self.ptrs = [p.data_ptr() for p in self.params]
+        self.index = {p.data_ptr(): i for i, p in enumerate(self.params) if p.dim() >= 2}
+
+    def lookup(self, w):
+        """(e4m3 bytes, row scales) of a quantised weight, or None."""
+        i = self.index.get(w.data_ptr())
+        if i is None or self.params[i].shape != w.shape:
+            return None
+        return self.q[i], self.scales[i]
 
     def valid_for(self, params) -> bool:
         params = list(params)
@@ -1605,11 +1688,122 @@ class Fp8Weights:
 
 
 _ACTIVE_CACHE: Optional[CastCache] = None
+_ACTIVE_FP8: Optional[Fp8Weights] = None
 
 
-def set_cast_cache(cache: Optional[CastCache]):
-    global _ACTIVE_CACHE
+def set_cast_cache(cache: Optional[CastCache], fp8: Optional[Fp8Weights] = None):
+    global _ACTIVE_CACHE, _ACTIVE_FP8
     _ACTIVE_CACHE = cache
+    _ACTIVE_FP8 = fp8
+
+
+def fp8_gemm(aq: torch.Tensor, sa: torch.Tensor, wq: torch.Tensor, sw: torch.Tensor,
+             bias: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """bf16 (M, N) = (aq * sa[:, None]) @ (wq * sw[:, None])^T + bias on e4m3 MFMA (csu_fp8_gemm):
+    aq (M, K) / wq (N, K) uint8 e4m3fn bytes, sa / sw fp32 row scales."""
+    require_device(aq, wq)
+    M, K = aq.shape
+    N = wq.shape[0]
+    if wq.shape[1] != K or sa.numel() != M or sw.numel() != N or aq.dtype != torch.uint8 or wq.dtype != torch.uint8:
+        raise ValueError("fp8_gemm: shape / dtype mismatch")
+    aq, wq, sa, sw = aq.contiguous(), wq.contiguous(), sa.float().contiguous(), sw.float().contiguous()
+    b = None if bias is None else bias.detach().float().contiguous()
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=aq.device)
+    _launch("fp8_gemm", lambda: lib().csu_fp8_gemm(M, N, K, ptr(aq), ptr(sa), ptr(wq), ptr(sw), ptr(b), ptr(out),
+                                                   stream_ptr(aq.device)),
+            2 * M * N * K, M * K + N * K + M * N * 2 + (M + N) * 4, prec="fp8")
+    return out
+
+
+def dequant_e4m3_rows(q: torch.Tensor, scale: torch.Tensor) -> torch.Tensor:
+    """bf16 q * scale[:, None] of e4m3fn bytes (exact: power-of-two scales)."""
+    require_device(q)
+    rows, cols = q.shape
+    out = torch.empty(rows, cols, dtype=torch.bfloat16, device=q.device)
+    _launch("dequant_e4m3", lambda: lib().csu_dequant_e4m3_rows(rows, cols, ptr(q), ptr(scale), ptr(out),
+                                                                stream_ptr(q.device)),
+            0, rows * cols * 3 + rows * 4, prec="fp8")
+    return out
+
+
+def layer_norm_fp8(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, eps: float = 1e-5):
+    """(e4m3 bytes, row scales, mean, rstd) of LN(x) (csu_layernorm_fwd_fp8), no autograd."""
+    require_device(x, weight, bias)
+    x = x.contiguous()
+    C = x.shape[-1]
+    rows = x.numel() // C
+    w = weight.detach().float().contiguous()
+    b = bias.detach().float().contiguous()
+    q = torch.empty(rows, C, dtype=torch.uint8, device=x.device)
+    s = torch.empty(rows, dtype=torch.float32, device=x.device)
+    mean = torch.empty(rows, dtype=torch.float32, device=x.device)
+    rstd = torch.empty(rows, dtype=torch.float32, device=x.device)
+    _launch("layernorm_fwd_fp8", lambda: lib().csu_layernorm_fwd_fp8(rows, C, float(eps), dtype_code(x), ptr(x), ptr(w),
+                                                                     ptr(b), ptr(q), ptr(s), ptr(mean), ptr(rstd),
+                                                                     stream_ptr(x.device)),
+            10 * rows * C, rows * C * (esize(x) + 1) + rows * 12, prec=prec_of(x))
+    return q, s, mean, rstd
+
+
+class _LnLinearFp8Fn(torch.autograd.Function):
+    """Residual junction + LayerNorm + Linear with e4m3 operands (BASELINE config 5, "fp8 MFMA
+    weights"): x -> (x, LN(x) W^T + b) for CSWinBlock's norm1 -> qkv (cswin:357 -> cswin:337).
+    The LayerNorm writes its output as e4m3 with one power-of-two scale per token
+    (csu_layernorm_fwd_fp8: the kernel holds the whole token row, so the amax costs nothing) and
+    csu_fp8_gemm multiplies it with the e4m3 weight rows on v_mfma_scale_f32_32x32x64_f8f6f4.
+    Backward (straight-through for both quantisations): dh = dY W_q (bf16 GEMM on the dequantised
+    e4m3 weights, the cast cache's transpose), dW / db from dY and the dequantised e4m3 activation
+    the forward multiplied, and the norm1 backward fused with the residual gradient as in
+    _LayerNormForkFn."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, weight, bias, eps: float, wq, ws, wt):
+        x = x.contiguous()
+        C = x.shape[-1]
+        hq, hs, mean, rstd = layer_norm_fp8(x, gamma, beta, eps)
+        y = fp8_gemm(hq, hs, wq, ws, bias).view(*x.shape[:-1], wq.shape[0])
+        ctx.save_for_backward(x, gamma.detach().float().contiguous(), mean, rstd, hq, hs, wt)
+        ctx.params = (gamma, beta)
+        ctx.pdtypes = (gamma.dtype, beta.dtype)
+        ctx.lin = (weight, bias)
+        ctx.lmeta = (weight.dtype, None if bias is None else bias.dtype, C)
+        _note_use(gamma, beta, weight, bias)
+        return x.view_as(x), y
+
+    @staticmethod
+    def backward(ctx, dres, dy):
+        x, g, mean, rstd, hq, hs, wt = ctx.saved_tensors
+        wdt, bdt, C = ctx.lmeta
+        dh = dw = db = None
+        if dy is not None:
+            N = dy.shape[-1]
+            dy2 = _bf16_of(dy).reshape(-1, N).contiguous()
+            dh = gemm(dy2, wt, False, torch.bfloat16).view(x.shape)
+            need_w, need_b = ctx.needs_input_grad[3], bdt is not None and ctx.needs_input_grad[4]
+            if need_w or need_b:
+                h = dequant_e4m3_rows(hq, hs)
+                dwf, dbf = wgrad_maybe_side(dy2, h, wdt if need_w else None, bdt if need_b else None, params=ctx.lin)
+                dw = dwf.to(wdt) if need_w else None
+                db = dbf.to(bdt) if need_b else None
+        dx, dg, dbeta = _ln_fork_backward(ctx, x, g, mean, rstd, dres, dh)
+        return dx, dg, dbeta, dw, db, None, None, None, None
+
+
+def ln_linear_fp8(x: torch.Tensor, ln: torch.nn.LayerNorm, lin: torch.nn.Linear):
+    """(x, lin(ln(x))) through _LnLinearFp8Fn when the fp8 weight format holds lin's weight (bf16
+    autocast forward of a model in set_weight_format('fp8_e4m3')), else None."""
+    if _ACTIVE_FP8 is None or not x.is_cuda:
+        return None
+    got = _ACTIVE_FP8.lookup(lin.weight)
+    N, K = lin.weight.shape
+    if got is None or N % 64 or K % 64 or K > 512:
+        return None
+    wc = _ACTIVE_CACHE.get(lin.weight, torch.bfloat16) if _ACTIVE_CACHE is not None else None
+    if wc is None:
+        return None
+    wt = _weight_t(lin.weight, wc)      # (K, N) bf16 of the dequantised e4m3 weight: the dX GEMM's operand
+    with torch.autocast("cuda", enabled=False):
+        return _LnLinearFp8Fn.apply(x, ln.weight, ln.bias, lin.weight, lin.bias, ln.eps, got[0], got[1], wt)
 
 
 def linear(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None,

@@ -1,5 +1,9 @@
 """Fused AdamW on the csu_adamw_step kernel (the optimizer of cswin:937-941).
 
+The same pass writes the bf16 shadow copies of the updated weights that the model's cast cache
+keeps for the next forward (csu.ops.shadow_spec: W, W^T, conv OHWI / IHWO), so no separate cast
+launch re-reads the fp32 weights.
+
 Drop-in for ``torch.optim.AdamW`` (same constructor arguments, param_groups, state keys
 ``step`` / ``exp_avg`` / ``exp_avg_sq`` and state_dict format, ReduceLROnPlateau works on it): one
 kernel launch updates every parameter of a group from a device table of pointers.  The table is
@@ -16,7 +20,18 @@ from ._lib import lib, stream_ptr
 from .ledger import launch
 
 _ITEM = np.dtype([("param", "<u8"), ("grad", "<u8"), ("exp_avg", "<u8"), ("exp_avg_sq", "<u8"), ("numel", "<i8"),
-                  ("chunk0", "<i8")])
+                  ("chunk0", "<i8"), ("shadow", "<u8"), ("shadow_t", "<u8"), ("rows", "<i4"), ("cols", "<i4"),
+                  ("taps", "<i4"), ("cols_pad", "<i4")])
+_NO_SHADOW = (0, 0, 0, 0, 0, 0)
+
+
+def _chunks(n, spec, chunk):
+    """Chunk (workgroup) count of one item: 64 x 64 tiles for a matrix with a transposed shadow,
+    else ceil(numel / chunk) (csu.h, csu_adamw_item)."""
+    sh, sht, rows, cols, taps, _ = spec
+    if sh and sht and taps == 0:
+        return -(-rows // 64) * -(-cols // 64)
+    return -(-n // chunk)
 
 
 class FusedAdamW(torch.optim.Optimizer):
@@ -63,16 +78,16 @@ class FusedAdamW(torch.optim.Optimizer):
         allocated while capturing) and is copied ONCE after the capture (finish_capture) into a
         device buffer allocated outside the graph's memory pool and kept for the optimizer's
         lifetime -- no copy node in the replayed graph."""
-        key = (gi,) + tuple(v for it in items for v in it[:4])
+        key = (gi,) + tuple(v for it in items for v in it[:4] + it[5])
         t = self._tables.get(gi)
         if t is not None and t[0] == key:
             return t
         chunk = lib().csu_adamw_chunk_elems()
         rec = np.zeros(len(items), dtype=_ITEM)
         c0 = 0
-        for i, (p, g, m, v, n) in enumerate(items):
-            rec[i] = (p, g, m, v, n, c0)
-            c0 += -(-n // chunk)
+        for i, (p, g, m, v, n, spec) in enumerate(items):
+            rec[i] = (p, g, m, v, n, c0) + tuple(spec)
+            c0 += _chunks(n, spec, chunk)
         raw = np.frombuffer(rec.tobytes(), dtype=np.uint8)
         if torch.cuda.is_current_stream_capturing():
             host = self._pinned.get(gi)
@@ -104,8 +119,9 @@ class FusedAdamW(torch.optim.Optimizer):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
+        from .ops import shadow_spec, shadows_written
         for gi, group in enumerate(self.param_groups):
-            items, dev, keep = [], None, []
+            items, dev, keep, shadowed = [], None, [], []
             for p in group["params"]:
                 if p.grad is None:
                     continue
@@ -120,8 +136,13 @@ class FusedAdamW(torch.optim.Optimizer):
                 keep.append(g)          # a contiguous temporary must outlive the launch below
                 if not p.is_contiguous():
                     raise RuntimeError("FusedAdamW: contiguous parameters only")
+                # the bf16 copies the next forward reads (a CastCache's layouts of p), written by the
+                # same pass from the updated value
+                spec = shadow_spec(p)
+                if spec is not None:
+                    shadowed.append(p)
                 items.append((p.data_ptr(), g.data_ptr(), st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr(),
-                              p.numel()))
+                              p.numel(), spec or _NO_SHADOW))
                 dev = p.device
             if not items:
                 continue
@@ -143,10 +164,12 @@ class FusedAdamW(torch.optim.Optimizer):
             b1, b2 = group["betas"]
             numel = sum(it[4] for it in items)
             fn = lib().csu_adam_l2_step if self._L2 else lib().csu_adamw_step
+            nsh = sum(2 * it[4] * (1 + (it[5][1] != 0)) for it in items if it[5][0])
             launch("adamw", lambda: fn(table.data_ptr(), n, chunks, lr_ptr, float(group["lr"]), float(b1),
                                                          float(b2), float(group["eps"]), float(group["weight_decay"]),
                                                          gs["step"].data_ptr(), 0.0, stream_ptr(dev)),
-                   12 * numel, 28 * numel, idem=False, prec="f32")
+                   12 * numel, 28 * numel + nsh, idem=False, prec="f32")
+            shadows_written(shadowed)
         return loss
 
     def state_dict(self):

@@ -22,6 +22,11 @@ except ImportError:  # pragma: no cover
     tqdm = None
 
 
+def sync_shadows(model):
+    from .ops import sync_shadows as sync
+    sync(model)
+
+
 def bce_loss(prob: torch.Tensor, target: torch.Tensor) -> torch.Tensor:
     """nn.BCELoss() (mean; log clamped at -100) computed in fp32 (cswin:936)."""
     with torch.autocast(prob.device.type, enabled=False):   # BCE is autocast-unsafe; always fp32
@@ -147,6 +152,7 @@ class _GraphedEval:
     def __call__(self, x, t):
         self.x.copy_(x, non_blocking=True)
         self.t.copy_(t, non_blocking=True)
+        sync_shadows(self.model)     # the captured forward reads the optimizer-written weight shadows
         self.graph.replay()
         return self.stats.clone()
 
@@ -396,6 +402,7 @@ class GraphedTrainStep:
     def __call__(self, x, t):
         self.x.copy_(x, non_blocking=True)
         self.t.copy_(t, non_blocking=True)
+        sync_shadows(self.model)     # weights changed outside the graph since: re-cast before the replay
         self.graph.replay()
         return self.loss, self.out
 

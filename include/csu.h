@@ -346,13 +346,36 @@ typedef struct {
 } csu_fp8_item;
 int csu_quant_e4m3_batch(const csu_fp8_item* items, int count, long total_rows, void* stream);
 
+/* fp8-e4m3 token GEMM (BASELINE config 5 "fp8 MFMA weights"; replaces CSWinBlock.qkv, cswin:337,
+ * on the norm1 output, cswin:357):  out[m][n] = bf16(sa[m] sw[n] sum_k aq[m][k] wq[n][k] + bias[n]),
+ * aq (M x K) / wq (N x K) OCP e4m3fn bytes, sa / sw fp32 per-row scales, bias fp32 (or NULL),
+ * out bf16 (M x N).  v_mfma_scale_f32_32x32x64_f8f6f4, fp32 accumulation.  N % 64 == 0, K % 64 == 0. */
+int csu_fp8_gemm(long M, int N, int K, const void* aq, const float* sa, const void* wq, const float* sw,
+                 const float* bias, void* out, void* stream);
+/* LayerNorm forward with an e4m3 output: yq = e4m3fn(LN(x) / s) (RNE), yscale[row] = s =
+ * 2^ceil(log2(amax_row / 448)) (1 for an all-zero row); mean / rstd as csu_layernorm_fwd. */
+int csu_layernorm_fwd_fp8(int rows, int C, float eps, int xdtype, const void* x, const float* gamma,
+                          const float* beta, void* yq, float* yscale, float* mean, float* rstd, void* stream);
+/* out (bf16, rows x cols) = e4m3fn(q) * scale[row]; cols % 8 == 0 */
+int csu_dequant_e4m3_rows(long rows, int cols, const void* q, const float* scale, void* out, void* stream);
+
 /* ---------------------------------------------------------------------------------------
  * Fused multi-tensor AdamW step (torch.optim.AdamW semantics, cswin:937-941): for every item,
  * param *= 1 - lr*wd; m = lerp(m, g, 1-beta1); v = beta2 v + (1-beta2) g^2;
  * param -= lr/(1-beta1^t) * m / (sqrt(v)/sqrt(1-beta2^t) + eps).  items: DEVICE array sorted
- * by chunk0 = first chunk index of the item (chunk0[i+1] = chunk0[i] + ceil(numel /
- * csu_adamw_chunk_elems())); total_chunks = the sum.  lr_dev / step_dev: device scalars (HIP
- * graph capture) or NULL to use lr / step.  Replaces torch's fused AdamW launches.
+ * by chunk0 = first chunk index of the item (chunk0[i+1] = chunk0[i] + the item's chunk count,
+ * see below); total_chunks = the sum.  lr_dev / step_dev: device scalars (HIP graph capture) or
+ * NULL to use lr / step.  Replaces torch's fused AdamW launches.
+ * Optional bf16 shadows of the UPDATED parameter, written in the same pass (the weight copies the
+ * next forward's kernels read; they replace the csu_cast_bf16_batch refresh):
+ *   shadow == NULL                : no shadow; ceil(numel / csu_adamw_chunk_elems()) chunks.
+ *   taps == 0, shadow_t == NULL   : shadow = bf16 param (same layout); ceil(numel / chunk) chunks.
+ *   taps == 0, shadow_t != NULL   : the param is a rows x cols matrix processed in 64 x 64 tiles
+ *                                   (ceil(rows/64) * ceil(cols/64) chunks): shadow = bf16 W,
+ *                                   shadow_t = bf16 W^T (cols x rows).
+ *   taps > 0                      : conv weight [rows=N][cols=C][taps=KH*KW]: shadow = OHWI with
+ *                                   channel stride cols_pad (>= C), shadow_t = IHWO (or NULL);
+ *                                   ceil(numel / chunk) chunks.
  * ------------------------------------------------------------------------------------- */
 typedef struct {
     float* param;
@@ -361,6 +384,10 @@ typedef struct {
     float* exp_avg_sq;
     int64_t numel;
     int64_t chunk0;
+    void* shadow;
+    void* shadow_t;
+    int32_t rows, cols;
+    int32_t taps, cols_pad;
 } csu_adamw_item;
 long csu_adamw_chunk_elems(void);
 int csu_adamw_step(const csu_adamw_item* items, int count, long total_chunks, const float* lr_dev, float lr,

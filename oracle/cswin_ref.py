@@ -133,6 +133,11 @@ def mlp(x: torch.Tensor, p: Params, key: str, drop=None) -> torch.Tensor:
     return _drop(drop, key + ".o", _lin(h, p, key + ".fc2"))
 
 
+# Optional transform of the norm1 output before qkv (None: identity).  The fp8 parity test installs
+# the e4m3 per-token quantiser of BASELINE config 5 here (the format's activation rounding).
+QKV_INPUT_QUANT = None
+
+
 def cswin_block(x: torch.Tensor, p: Params, key: str, reso: int, heads: int, split: int,
                 last_stage: bool, qk_scale=None, drop=None) -> torch.Tensor:
     """Pre-LN CSWin block (cswin:301-370)."""
@@ -141,6 +146,8 @@ def cswin_block(x: torch.Tensor, p: Params, key: str, reso: int, heads: int, spl
     if reso == split:                                                # cswin:317-318
         last_stage = True
     y = _ln(x, p, key + ".norm1")
+    if QKV_INPUT_QUANT is not None:
+        y = QKV_INPUT_QUANT(y)
     qkv = _lin(y, p, key + ".qkv")                                   # (B, L, 3C): Q | K | V
     q, k, v = qkv[..., :C], qkv[..., C:2 * C], qkv[..., 2 * C:]
     if last_stage:

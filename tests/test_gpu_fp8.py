@@ -2,7 +2,15 @@
 
 * The quantiser (csu_quant_e4m3_batch) equals torch's float8_e4m3fn round-to-nearest-even under the
   same per-row power-of-two scales, bit for bit.
-* The model in the fp8 weight format equals the fp32 oracle run with the dequantised weights, at the
+* The LayerNorm's e4m3 output mode (csu_layernorm_fwd_fp8: per-token power-of-two scale) equals
+  torch's LayerNorm quantised by torch.float8_e4m3fn under the same rule.
+* The e4m3 GEMM (csu_fp8_gemm, v_mfma_scale_f32_32x32x64_f8f6f4) equals an fp64 GEMM of the
+  dequantised operands to bf16 output rounding plus the MFMA's summation error:
+  |out - ref| <= 2^-8 |ref| + 2^-14 sum_k |a_k w_k| (the e4m3 products are exact; measured on
+  gfx950 the f8f6f4 MFMA's internal sum is ~2^-17 of sum |a w| off an fp64 sum, above plain fp32
+  accumulation's ~K 2^-24).
+* The model in the fp8 weight format equals the fp64 oracle run with the dequantised weights and
+  the per-token e4m3 rounding of the qkv input (oracle.cswin_ref.QKV_INPUT_QUANT), at the
   bf16-autocast tolerances (probabilities 1e-2, loss 1e-2 rel, grad norms 5e-2 rel), at
   256x256 with split [1,2,8,8] (stage-3 windows of 128 tokens; the 512/1024-token windows of the
   1024 config are covered kernel-wise by ATTN_CASES)."""
@@ -30,6 +38,18 @@ def _ref_quant(w: torch.Tensor):
     return (q.float().double() * s[:, None]).float().reshape(w.shape), q.view(torch.uint8).reshape(w.shape), s.float()
 
 
+def _pow2_scale(amax):
+    return torch.where(amax > 0, torch.exp2(torch.ceil(torch.log2(amax / 448.0))), torch.ones_like(amax))
+
+
+def _tok_quant(y: torch.Tensor) -> torch.Tensor:
+    """Per-token e4m3 rounding of the qkv input, straight-through for autograd (the device's
+    backward uses dY W and the quantised activation as the forward did)."""
+    s = _pow2_scale(y.detach().abs().amax(-1, keepdim=True))
+    q = (y.detach() / s).float().to(torch.float8_e4m3fn).to(y.dtype) * s
+    return y + (q - y.detach())
+
+
 def test_quantizer_matches_torch_e4m3fn():
     from csu import ops
     d = dev()
@@ -49,7 +69,8 @@ def test_quantizer_matches_torch_e4m3fn():
         assert torch.equal(dq.cpu().bfloat16().float(), rd)     # exact in bf16
 
 
-def test_fp8_weight_model_vs_oracle_with_quantized_weights():
+def test_fp8_weight_model_vs_oracle_with_quantized_weights(monkeypatch):
+    from csu import ops
     from csu.data import ellipse_batch
     from csu.model import CSWinTransformer
     from csu.train import bce_loss
@@ -59,8 +80,12 @@ def test_fp8_weight_model_vs_oracle_with_quantized_weights():
     m = CSWinTransformer(img_size=256, split_size=[1, 2, 8, 8]).to(d).set_weight_format("fp8_e4m3")
     m.load_state_dict(p)
     x, t = ellipse_batch(np.random.default_rng(5), 1, 256)
+    calls = []
+    real = ops.fp8_gemm
+    monkeypatch.setattr(ops, "fp8_gemm", lambda *a, **k: calls.append(1) or real(*a, **k))
     with torch.autocast("cuda", dtype=torch.bfloat16):
         y = m(x.to(d))
+    assert len(calls) == sum(1 for mod in m.modules() if type(mod).__name__ == "CSWinBlock")   # every qkv on fp8 MFMA
     loss = bce_loss(y, t.to(d))
     loss.backward()
     # the oracle on the dequantised e4m3 weights of exactly the tensors the fp8 format quantises
@@ -73,6 +98,7 @@ def test_fp8_weight_model_vs_oracle_with_quantized_weights():
             pq[k] = _ref_quant(p[k])[0]
     assert sum(1 for w in m._linear_weights() if id(w) in quant) > 100
     pref = {k: v.double().requires_grad_(True) for k, v in pq.items()}
+    monkeypatch.setattr(O, "QKV_INPUT_QUANT", _tok_quant)
     yr = O.cswin_forward(pref, x.double(), cfg)
     lr = O.bce_loss(yr, t.double())
     lr.backward()
@@ -88,3 +114,65 @@ def test_fp8_weight_model_vs_oracle_with_quantized_weights():
     with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
         y2 = m2(x.to(d))
     assert float((y2 - y.detach()).abs().max()) > 1e-4
+
+
+@pytest.mark.parametrize("C", [64, 128, 256, 512])
+@pytest.mark.parametrize("xdt", [torch.float32, torch.bfloat16])
+def test_layernorm_fp8_output_matches_torch(C, xdt):
+    from csu import ops
+    d = dev()
+    g = torch.Generator().manual_seed(C)
+    rows = 1031                                   # ragged: not a multiple of any rows-per-block
+    x = (torch.randn(rows, C, generator=g) * 2 + 0.5).to(xdt)
+    x[5] = 0                                      # all-zero row: LN output = beta
+    w = torch.randn(C, generator=g) * 0.5 + 1
+    b = torch.randn(C, generator=g) * 0.1
+    q, s, mean, rstd = ops.layer_norm_fp8(x.to(d), w.to(d), b.to(d), 1e-5)
+    torch.cuda.synchronize()
+    y = torch.nn.functional.layer_norm(x.float(), (C,), w, b, 1e-5)
+    rs = _pow2_scale(y.abs().amax(1))
+    assert torch.equal(s.cpu(), rs)
+    rq = (y / rs[:, None]).to(torch.float8_e4m3fn)
+    mism = (q.cpu() != rq.view(torch.uint8))
+    assert mism.float().mean().item() < 1e-3       # fp32 LN rounding can move a rare value across a tie
+    deq = ops.dequant_e4m3_rows(q, s).float().cpu()
+    ref = rq.float() * rs[:, None]
+    assert (deq != ref).float().mean().item() < 1e-3
+    assert torch.allclose(deq, ref, rtol=0.13, atol=float(rs.max()) * 2.0 ** -9)   # at most one e4m3 step apart
+    torch.testing.assert_close(mean.cpu(), x.float().mean(1), rtol=1e-5, atol=1e-5)
+    assert torch.allclose(deq[5], (b / rs[5]).to(torch.float8_e4m3fn).float() * rs[5])
+
+
+@pytest.mark.parametrize("M,N,K", [(1000, 192, 64), (129, 384, 128), (4096, 768, 256), (257, 1536, 512),
+                                   (64, 64, 64)])
+def test_fp8_gemm_matches_fp64_on_quantized_operands(M, N, K):
+    from csu import ops
+    d = dev()
+    g = torch.Generator().manual_seed(M + N + K)
+    a = torch.randn(M, K, generator=g) * 3
+    w = torch.randn(N, K, generator=g) * 0.05
+    sa = _pow2_scale(a.abs().amax(1))
+    sw = _pow2_scale(w.abs().amax(1))
+    aq = (a / sa[:, None]).to(torch.float8_e4m3fn)
+    wq = (w / sw[:, None]).to(torch.float8_e4m3fn)
+    bias = torch.randn(N, generator=g)
+    out = ops.fp8_gemm(aq.view(torch.uint8).to(d), sa.to(d), wq.view(torch.uint8).to(d), sw.to(d), bias.to(d))
+    out0 = ops.fp8_gemm(aq.view(torch.uint8).to(d), sa.to(d), wq.view(torch.uint8).to(d), sw.to(d), None)
+    torch.cuda.synchronize()
+    ad = aq.double() * sa.double()[:, None]
+    wd = wq.double() * sw.double()[:, None]
+    ref = ad @ wd.t()
+    asum = ad.abs() @ wd.abs().t()      # sum_k |a_k w_k|: the scale of the summation error
+    for o, r in ((out, ref + bias.double()), (out0, ref)):
+        err = (o.double().cpu() - r).abs()
+        assert float((err - (2.0 ** -8) * r.abs() - (2.0 ** -14) * asum).max()) <= 0
+
+
+def test_fp8_gemm_rejects_bad_shapes():
+    from csu import ops
+    from csu._lib import CsuError
+    d = dev()
+    aq = torch.zeros(16, 96, dtype=torch.uint8, device=d)
+    wq = torch.zeros(64, 96, dtype=torch.uint8, device=d)
+    with pytest.raises(CsuError):
+        ops.fp8_gemm(aq, torch.ones(16, device=d), wq, torch.ones(64, device=d))

@@ -625,6 +625,57 @@ def test_fused_adamw_matches_torch(capturable):
         torch.testing.assert_close(o_mine.state[q]["exp_avg_sq"], o_ref.state[p]["exp_avg_sq"], rtol=5e-5, atol=1e-9)
 
 
+def test_fused_adamw_writes_cast_cache_shadows(monkeypatch):
+    """FusedAdamW writes the bf16 shadows a CastCache keeps (W, W^T in 64 x 64 tiles incl. ragged
+    edges, 1-D copies, conv OHWI (channel-padded) / IHWO) from the updated weights, bit-equal to a
+    fresh cast; the next refresh then launches nothing, and an in-place change of a weight (version
+    bump) makes it re-cast."""
+    from csu import ops
+    from csu.optim import FusedAdamW
+    d = dev()
+    torch.manual_seed(4)
+    ps = [torch.randn(192, 64, device=d), torch.randn(70, device=d), torch.randn(16, 64, 1, 1, device=d),
+          torch.randn(130, 333, device=d), torch.randn(5, device=d), torch.randn(512, 2048, device=d)]
+    convs = [torch.randn(36, 16, 3, 3, device=d), torch.randn(64, 3, 7, 7, device=d), torch.randn(256, 128, 3, 3, device=d)]
+    allp = [p.requires_grad_(True) for p in ps + convs]
+    plain = [p.detach().clone().requires_grad_(True) for p in allp]
+    c = ops.CastCache()
+    casts = []
+    real = ops.CastCache._cast
+    monkeypatch.setattr(ops.CastCache, "_cast", lambda self: casts.append(1) or real(self))
+    c.refresh(ps, torch.bfloat16, convs)
+    assert len(casts) == 1
+    o1 = FusedAdamW(allp, lr=1e-2, weight_decay=1e-2)
+    o2 = FusedAdamW(plain, lr=1e-2, weight_decay=1e-2)      # same update without shadows (other buffers)
+    for _ in range(3):
+        for p, q in zip(allp, plain):
+            gr = torch.randn_like(p)
+            p.grad, q.grad = gr, gr.clone()
+        o1.step()
+        o2.step()
+        c.refresh(ps, torch.bfloat16, convs)
+    assert len(casts) == 1                                   # the optimizer kept every shadow fresh
+    for p, q in zip(allp, plain):
+        assert torch.equal(p.detach(), q.detach())           # the shadow writes do not change the update
+    for p in ps:
+        assert torch.equal(c.get(p, torch.bfloat16), p.detach().bfloat16())
+        if p.dim() > 1:
+            v = p.detach().reshape(p.shape[0], -1)
+            assert torch.equal(c.get_t(v, torch.bfloat16), v.t().bfloat16())
+    for w in convs:
+        o, i = c.get_conv(w, torch.bfloat16)
+        C = w.shape[1]
+        assert torch.equal(o[..., :C], w.detach().permute(0, 2, 3, 1).bfloat16())
+        if C % 8:
+            assert i is None and not o[..., C:].any()
+        else:
+            assert torch.equal(i, w.detach().permute(1, 2, 3, 0).bfloat16())
+    with torch.no_grad():
+        ps[3].mul_(2)                                        # a change the optimizer did not make
+    c.refresh(ps, torch.bfloat16, convs)
+    assert len(casts) == 2
+    assert torch.equal(c.get(ps[3], torch.bfloat16), ps[3].detach().bfloat16())
+
 
 @pytest.mark.gpu
 def test_fused_adam_l2_matches_torch():
