@@ -17,6 +17,8 @@
 // first maximum (torch's scan order, NaN wins) and writes all four input gradients of the window.
 #include "common.hpp"
 
+#include <numeric>
+
 namespace csu {
 namespace {
 
@@ -214,45 +216,66 @@ __global__ __launch_bounds__(NT) void bn_grad_final(BnGeo g, const float* __rest
     }
 }
 
-// pass 3, forward: y = [relu]((x - mean) rstd gamma + beta); 8 channels per thread, grid-stride
+// pass 3, forward: y = [relu]((x - mean) rstd gamma + beta); 8 channels per thread, grid-stride.
+// The grid stride is a multiple of C/8 (grid_apply), so a thread's 8 channels never change: their
+// per-channel terms are loaded once, and the loop is a pure 16-B stream (per-element loads of the
+// small per-channel arrays made the backward VMEM-issue-bound at ~0.8 TB/s).
 template <typename T>
 __global__ __launch_bounds__(NT) void bn_apply(long n8, int C, const T* __restrict__ x, const float* __restrict__ save,
                                                const float* __restrict__ gamma, const float* __restrict__ beta,
                                                int relu, T* __restrict__ y) {
     const int c8 = C / 8;
-    for (long i = (long)blockIdx.x * NT + threadIdx.x; i < n8; i += (long)gridDim.x * NT) {
-        const int c0 = (int)(i % c8) * 8;
+    const long i0 = (long)blockIdx.x * NT + threadIdx.x;
+    const int c0 = (int)(i0 % c8) * 8;
+    float mu[8], a[8], b[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        mu[j] = save[c0 + j];
+        a[j] = save[C + c0 + j] * gamma[c0 + j];
+        b[j] = beta[c0 + j];
+    }
+    for (long i = i0; i < n8; i += (long)gridDim.x * NT) {
         float v[8];
         load8(x + i * 8, v);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-            const float a = save[C + c0 + j] * gamma[c0 + j];
-            float o = fmaf(v[j] - save[c0 + j], a, beta[c0 + j]);
+            const float o = fmaf(v[j] - mu[j], a[j], b[j]);
             v[j] = relu ? fmaxf(o, 0.f) : o;
         }
         store8(y + i * 8, v);
     }
 }
 
-// pass 3, backward: dx = gamma rstd (g - coef0 - (x - mean) rstd coef1)   (coef == nullptr: eval)
+// pass 3, backward: dx = gamma rstd (g - coef0 - (x - mean) rstd coef1)   (coef == nullptr: eval);
+// per-channel terms hoisted as in bn_apply
 template <typename T, typename G>
 __global__ __launch_bounds__(NT) void bn_grad_apply(long n8, int C, const T* __restrict__ x, const G* __restrict__ dy,
                                                     const float* __restrict__ save, const float* __restrict__ gamma,
                                                     const float* __restrict__ beta, const float* __restrict__ coef,
                                                     int relu, T* __restrict__ dx) {
     const int c8 = C / 8;
-    for (long i = (long)blockIdx.x * NT + threadIdx.x; i < n8; i += (long)gridDim.x * NT) {
-        const int c0 = (int)(i % c8) * 8;
+    const long i0 = (long)blockIdx.x * NT + threadIdx.x;
+    const int c0 = (int)(i0 % c8) * 8;
+    float mu[8], rs[8], a[8], b[8], k0[8], k1[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int c = c0 + j;
+        rs[j] = save[C + c];
+        mu[j] = save[c];
+        a[j] = rs[j] * gamma[c];
+        b[j] = beta[c];
+        k0[j] = coef ? coef[c] : 0.f;
+        k1[j] = coef ? coef[C + c] : 0.f;
+    }
+    for (long i = i0; i < n8; i += (long)gridDim.x * NT) {
         float xv[8], gv[8], o[8];
         load8(x + i * 8, xv);
         load8(dy + i * 8, gv);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-            const int c = c0 + j;
-            const float rs = save[C + c], a = rs * gamma[c];
-            const float d = xv[j] - save[c];
-            const float gg = (!relu || fmaf(d, a, beta[c]) > 0.f) ? gv[j] : 0.f;
-            o[j] = coef ? a * (gg - coef[c] - d * rs * coef[C + c]) : a * gg;
+            const float d = xv[j] - mu[j];
+            const float gg = (!relu || fmaf(d, a[j], b[j]) > 0.f) ? gv[j] : 0.f;
+            o[j] = coef ? a[j] * (gg - k0[j] - d * rs[j] * k1[j]) : a[j] * gg;
         }
         store8(dx + i * 8, o);
     }
@@ -331,6 +354,15 @@ unsigned grid_of(long n) {
     return (unsigned)(g < 8192 ? (g < 1 ? 1 : g) : 8192);
 }
 
+// apply grid: the stride grid * NT must be a multiple of C/8 (a thread keeps its channels)
+unsigned grid_apply(long n8, int C) {
+    const int c8 = C / 8;
+    unsigned g = grid_of(n8);
+    if (NT % c8 == 0) return g;
+    const long per = c8 / std::gcd(c8, NT);          // grid must be a multiple of per
+    return (unsigned)(((g + per - 1) / per) * per);
+}
+
 size_t bn_ws(long M, int C) {
     const BnGeo g = bn_geo(M, C);
     return ((size_t)g.nch * C * 2 + 2 * (size_t)C) * sizeof(float);
@@ -362,8 +394,8 @@ extern "C" int csu_bn_relu_fwd(long M, int C, int dtype, const void* x, const fl
         bn_eval_save<<<(C + 255) / 256, 256, 0, st>>>(C, running_mean, running_var, eps, save);
     }
     const long n8 = M * C / 8;
-    if (dtype == CSU_BF16) bn_apply<bf16><<<grid_of(n8), NT, 0, st>>>(n8, C, (const bf16*)x, save, gamma, beta, relu, (bf16*)y);
-    else bn_apply<float><<<grid_of(n8), NT, 0, st>>>(n8, C, (const float*)x, save, gamma, beta, relu, (float*)y);
+    if (dtype == CSU_BF16) bn_apply<bf16><<<grid_apply(n8, C), NT, 0, st>>>(n8, C, (const bf16*)x, save, gamma, beta, relu, (bf16*)y);
+    else bn_apply<float><<<grid_apply(n8, C), NT, 0, st>>>(n8, C, (const float*)x, save, gamma, beta, relu, (float*)y);
     return check_launch("bn_relu_fwd");
 }
 
@@ -386,7 +418,7 @@ extern "C" int csu_bn_relu_bwd(long M, int C, int dtype, const void* x, const fl
     bn_grad_final<<<g.ncb, NT, 0, st>>>(g, part, save, dgamma, dbeta, coef);
     const long n8 = M * C / 8;
     const float* cf = training ? coef : nullptr;
-#define BN_APPLY(T, G) bn_grad_apply<T, G><<<grid_of(n8), NT, 0, st>>>(n8, C, (const T*)x, (const G*)dy, save, gamma, beta, cf, relu, (T*)dx)
+#define BN_APPLY(T, G) bn_grad_apply<T, G><<<grid_apply(n8, C), NT, 0, st>>>(n8, C, (const T*)x, (const G*)dy, save, gamma, beta, cf, relu, (T*)dx)
     if (dtype == CSU_BF16) { if (gdtype == CSU_BF16) BN_APPLY(bf16, bf16); else BN_APPLY(bf16, float); }
     else { if (gdtype == CSU_BF16) BN_APPLY(float, bf16); else BN_APPLY(float, float); }
 #undef BN_APPLY
