@@ -313,6 +313,9 @@ def main():
     elif graph_ledger:
         ledger = None
     roof = None
+    if ledger is not None and os.environ.get("CSU_LEDGER_DUMP"):
+        with open(os.environ["CSU_LEDGER_DUMP"], "w") as f:
+            json.dump(ledger.launches(), f)
     if ledger is not None:
         roof = _roofline(ledger.summary(steps=lsteps), ledger_step_ms or el / args.steps * 1e3, args, graph=graph_ledger)
         if graph_ledger:

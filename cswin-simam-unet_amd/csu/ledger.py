@@ -89,6 +89,15 @@ class KernelLedger:
         _ACTIVE = self._prev
         return False
 
+    def launches(self) -> List[Dict]:
+        """Every recorded launch in order: name, shape tag, measured us, algorithmic bytes / FLOPs."""
+        torch.cuda.synchronize()
+        out = []
+        for i, (name, e0, e1, reps, flops, nbytes, prec, tag) in enumerate(self.rows):
+            ms = self._acc[i] / self.replays if self.graph else e0.elapsed_time(e1) / reps
+            out.append({"kernel": name, "tag": tag, "us": round(ms * 1e3, 2), "bytes": int(nbytes), "flops": int(flops)})
+        return out
+
     def summary(self, steps: int = 1) -> List[Dict]:
         """Per call name (sorted by measured time): launches per step, avg us per launch, algorithmic
         bytes / FLOPs per launch, achieved GB/s and TFLOP/s, bound, t_roof and frac."""
@@ -96,7 +105,7 @@ class KernelLedger:
         agg = collections.OrderedDict()
         if self.graph and not self.replays:
             raise RuntimeError("KernelLedger(graph=True): collect() after at least one replay")
-        for i, (name, e0, e1, reps, flops, nbytes, prec) in enumerate(self.rows):
+        for i, (name, e0, e1, reps, flops, nbytes, prec, _) in enumerate(self.rows):
             a = agg.setdefault(name, {"n": 0, "ms": 0.0, "flops": 0.0, "bytes": 0.0, "prec": prec})
             a["n"] += 1
             a["ms"] += self._acc[i] / self.replays if self.graph else e0.elapsed_time(e1) / reps
@@ -122,7 +131,7 @@ class KernelLedger:
 
 
 def launch(name: str, fn: Callable[[], int], flops: float = 0.0, nbytes: float = 0.0, idem: bool = True,
-           prec: str = "bf16"):
+           prec: str = "bf16", tag: str = ""):
     """Run ``fn`` (a C-ABI call returning its status code) and check it; time it when a ledger is
     active.  ``idem``: the call can be repeated without changing its result (outputs overwritten
     from unchanged inputs)."""
@@ -136,7 +145,7 @@ def launch(name: str, fn: Callable[[], int], flops: float = 0.0, nbytes: float =
         e0.record()
         check(fn(), name)
         e1.record()
-        led.rows.append((name, e0, e1, 1, float(flops), float(nbytes), prec))
+        led.rows.append((name, e0, e1, 1, float(flops), float(nbytes), prec, tag))
         return
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if idem:
@@ -151,7 +160,7 @@ def launch(name: str, fn: Callable[[], int], flops: float = 0.0, nbytes: float =
         check(fn(), name)
         e1.record()
         reps = 1
-    led.rows.append((name, e0, e1, reps, float(flops), float(nbytes), prec))
+    led.rows.append((name, e0, e1, reps, float(flops), float(nbytes), prec, tag))
 
 
 def esize(t) -> int:

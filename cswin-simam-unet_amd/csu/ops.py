@@ -839,7 +839,9 @@ def gemm(a2: torch.Tensor, b: torch.Tensor, b_trans: bool, out_dtype, bias=None,
     d.out, d.gelu_out, d.ldc, d.out_dtype, d.cfg = ptr(out), ptr(g), N, dtype_code(out), int(cfg)
     nb = (M * K * a2.element_size() + N * K * b.element_size() + M * N * out.element_size()
           + (M * N * 2 if gelu_aux is not None else 0) + (M * N * 4 if resid is not None else 0) + (M * N * 2 if gelu_out else 0))
-    _launch("gemm", lambda: lib().csu_gemm_ex(ctypes.byref(d), stream_ptr(a2.device)), 2 * M * N * K, nb, prec=prec_of(a2))
+    _launch("gemm", lambda: lib().csu_gemm_ex(ctypes.byref(d), stream_ptr(a2.device)), 2 * M * N * K, nb, prec=prec_of(a2),
+            tag=f"{M}x{N}x{K}{'T' if b_trans else ''}{'g' if a_gelu else ''}{'G' if gelu_out else ''}{'r' if resid is not None else ''}"
+                f"{'b' if bias is not None else ''}:{out_dtype}")
     return (out, g) if gelu_out else out
 
 
