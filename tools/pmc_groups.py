@@ -3,7 +3,11 @@ traffic from three rocprofv3 counter passes (tools/pmc_table.sh layout: p1 = SQ_
 SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE, p2 = FETCH_SIZE, p3 = WRITE_SIZE, eager bench steps),
 set against the ledger's ALGORITHMIC bytes of the same call from a bench JSON:
 
-    python tools/pmc_groups.py <pass dir> <bench.json> [top]
+    python tools/pmc_groups.py <pass dir> <bench.json> [top] [--traffic <pmc_traffic.json>]
+
+``--traffic``: also merge, per C-ABI call, the PMC HBM bytes per LEDGER launch (per-step bytes /
+the bench ledger's launches per step) into that JSON under "<call>|<img>|<batch>|<dtype>" -- the
+``roofline.traffic`` bench.py reports for its dominant kernel.
 
 * steps = AdamW dispatches after the first one (the warm-up step is dropped);
 * MFMA util = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 XCDs x 1024 SIMDs);
@@ -29,8 +33,14 @@ def per_step(passdir, counters):
 
 
 def main():
-    d, bj = sys.argv[1], sys.argv[2]
-    top = int(sys.argv[3]) if len(sys.argv) > 3 else 12
+    argv = list(sys.argv[1:])
+    tj = None
+    if "--traffic" in argv:
+        i = argv.index("--traffic")
+        tj = argv[i + 1]
+        del argv[i:i + 2]
+    d, bj = argv[0], argv[1]
+    top = int(argv[2]) if len(argv) > 2 else 12
     rec = json.loads([l for l in open(bj).read().splitlines() if l.startswith("{")][-1])
     ledger = {k["kernel"]: k for k in rec["roofline"]["kernels"]}
     for a, b in (("conv_fwd", "conv_dgrad"),):
@@ -81,6 +91,19 @@ def main():
         algs = f"{alg / 1e6:.1f}" if alg else "-"
         print(f"| {g} | {t:.1f} | {a['n_p1']:.0f} | {util * 100:.1f} % | {tf:.0f} | {hbm / 1e6:.1f} | {algs} | {ratio} | "
               f"{hbm / (t * 1e-6) / 1e9 if t else 0:.0f} |")
+    if tj:
+        c = rec["config"]
+        suffix = f"|{c.get('img')}|{c.get('per_gpu_batch')}|{rec['dtype']}"
+        db = json.load(open(tj)) if os.path.exists(tj) else {}
+        for g, a in G.items():
+            L = ledger.get(g)
+            if L and L.get("launches_per_step"):
+                db[g + suffix] = int(row(a)[1] / L["launches_per_step"])
+        db["_note"] = ("HBM bytes per ledger launch from rocprofv3 PMC passes (2 x FETCH_SIZE + WRITE_SIZE), "
+                       "tools/pmc_groups.py --traffic over profiles/r03k_pmc_*; key <call>|<img>|<batch>|<dtype>")
+        db.pop("_detail", None)
+        with open(tj, "w") as f:
+            json.dump(db, f, indent=1, sort_keys=True)
     print("\n## Per kernel (top by time; traffic ratio of the kernel's ABI call above)\n")
     print("| kernel | ABI call | us/step | launches | MFMA util | MFMA TFLOP/s | HBM MB (PMC) | HBM GB/s |")
     print("|---|---|---|---|---|---|---|---|")
