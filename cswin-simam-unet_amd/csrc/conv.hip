@@ -15,6 +15,7 @@
 #include <cstdlib>
 
 #include "common.hpp"
+#include "lds_dma.hpp"
 
 namespace csu {
 namespace {
@@ -335,6 +336,146 @@ __global__ __launch_bounds__(NT) void conv_wgrad_bf16(Geo g, long Mrows, int Nco
     }
 }
 
+// ---- bf16 weight gradient, v3 (C % 8 == 0, N % 8 == 0): LDS-DMA gathers, S-stage ring ------------
+// One TN x TK tile of dW over the rows of one chunk, 64 rows (output pixels m) per step.  Both
+// operand images are row-major [m][columns] and filled by buffer_load ... lds: the dy image straight
+// from the (rows, N) matrix (rows past the chunk end fall outside the step's resource and land as
+// zeros), the x image gathered per lane -- column k = (tap, c) of row m is the input pixel under tap
+// (ky, kx) of output pixel m, 8 channels per lane, out-of-image taps at an out-of-range offset.
+// The tap and channel of each lane's columns are fixed for the whole loop; only the pixel moves.
+// MFMA fragments are transposing reads (ds_read_b64_tr_b16) of the [m][...] images (trfrag); the
+// row swizzle is applied to the DMA source columns.  db (k tile 0) sums the dy fragments the MFMAs
+// read anyway.  Partial slabs per chunk as the v2 kernel: [chunk][N*K + N], reduced by colsum.
+template <int TN, int TK, int S, int WN, int WK>
+__global__ __launch_bounds__(64 * WN * WK, 1) void conv_wgrad_dma(Geo g, long Mrows, int Ncols, int Kdim, long rpc,
+                                                                  const bf16* __restrict__ x, const bf16* __restrict__ dy,
+                                                                  float* __restrict__ part) {
+    constexpr int NWV = WN * WK;
+    constexpr int RM = 64;                          // rows per step
+    constexpr int RBA = TN * 2, RBB = TK * 2;       // image row bytes
+    constexpr int STAGE = RM * (TN + TK);           // bf16 elements per ring stage
+    constexpr int NA = RM * RBA / (1024 * NWV), NB = RM * RBB / (1024 * NWV);
+    constexpr int D = NA + NB;                      // DMA instructions per wave per step
+    constexpr int P = S - 1;
+    constexpr int TNW = TN / (32 * WN), TKW = TK / (32 * WK);
+    static_assert(NA >= 1 && NB >= 1 && TNW >= 1 && TKW >= 1 && (P - 1) * D <= 63, "conv_wgrad_dma layout");
+    __shared__ __attribute__((aligned(1024))) bf16 smem[S * STAGE];
+    const int n0 = blockIdx.x * TN, k0 = blockIdx.y * TK;
+    const long mb = (long)blockIdx.z * rpc, me = min(Mrows, mb + rpc);
+    const int nsteps = (int)((me - mb + RM - 1) / RM);
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int h = lane >> 5;
+    const int wn = (wave / WK) * (TN / WN), wk = (wave % WK) * (TK / WK);
+    const bool do_bias = blockIdx.y == 0 && wave % WK == 0;
+
+    // dy image: lane's row and 16-B column chunk per instruction (fixed), byte offset within a step
+    unsigned voffA[NA];
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+        const int p = (wave * NA + i) * 1024 + lane * 16;
+        const int row = p / RBA, slot = (p % RBA) >> 4;
+        const int n = n0 + 8 * (slot ^ mkey<RBA>(row));
+        voffA[i] = n < Ncols ? (unsigned)(row * Ncols + n) * 2u : kOOB;
+    }
+    // x image: row, and the tap offsets / channel of the lane's 8 columns (fixed)
+    int brow[NB], bdy[NB], bdx[NB], bc[NB];
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+        const int p = (wave * NB + i) * 1024 + lane * 16;
+        const int row = p / RBB, slot = (p % RBB) >> 4;
+        const int k = k0 + 8 * (slot ^ mkey<RBB>(row));
+        const int tap = k / g.C, c = k - tap * g.C;
+        brow[i] = row;
+        bdy[i] = k < Kdim ? tap / g.KW - g.p : -(1 << 29);   // invalid column: never inside the image
+        bdx[i] = tap % g.KW - g.p;
+        bc[i] = c;
+    }
+    const i32x4 rsX = rsrc4(x, (long)g.B * g.H * g.W * g.C * 2);
+    auto issue = [&](int u) {   // step u (steps past the chunk: every offset out of range, zeros)
+        const long m0 = mb + (long)u * RM;
+        bf16* stg = smem + (u % S) * STAGE;
+        const long rows = me - m0;
+        dma<NA>(rsrc4(dy + (rows > 0 ? m0 : 0) * Ncols, rows > 0 ? rows * Ncols * 2 : 0), voffA, 0u, stg, wave);
+        unsigned vb[NB];
+#pragma unroll
+        for (int i = 0; i < NB; ++i) {
+            const long m = m0 + brow[i];
+            const bool mv = m < me;
+            const unsigned mu = (unsigned)(mv ? m : 0);   // < 2^31 (check_geo)
+            const unsigned t = mu / (unsigned)g.OW, b = t / (unsigned)g.OH;
+            const int ox = (int)(mu - t * (unsigned)g.OW), oy = (int)(t - b * (unsigned)g.OH);
+            const int iy = oy * g.s + bdy[i], ix = ox * g.s + bdx[i];
+            const bool ok = mv && iy >= 0 && iy < g.H && ix >= 0 && ix < g.W;
+            vb[i] = ok ? (unsigned)(((((int)b * g.H + iy) * g.W + ix) * g.C + bc[i]) * 2) : kOOB;
+        }
+        dma<NB>(rsX, vb, 0u, stg + RM * TN, wave);
+    };
+    f32x16 acc[TNW][TKW];
+#pragma unroll
+    for (int j = 0; j < TNW; ++j)
+#pragma unroll
+        for (int i = 0; i < TKW; ++i) acc[j][i] = f32x16{};
+    float bsum[TNW];
+#pragma unroll
+    for (int j = 0; j < TNW; ++j) bsum[j] = 0.f;
+    auto mma = [&](int u) {
+        const bf16* As = smem + (u % S) * STAGE;
+        const bf16* Bs = As + RM * TN;
+#pragma unroll
+        for (int s = 0; s < RM / 16; ++s) {
+            bf16x8 af[TNW], bfr[TKW];
+#pragma unroll
+            for (int j = 0; j < TNW; ++j) af[j] = trfrag<RBA>(As, wn + 32 * j, s, lane);
+#pragma unroll
+            for (int i = 0; i < TKW; ++i) bfr[i] = trfrag<RBB>(Bs, wk + 32 * i, s, lane);
+#pragma unroll
+            for (int j = 0; j < TNW; ++j)
+#pragma unroll
+                for (int i = 0; i < TKW; ++i) acc[j][i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[j], bfr[i], acc[j][i], 0, 0, 0);
+            if (do_bias)
+#pragma unroll
+                for (int j = 0; j < TNW; ++j)
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) bsum[j] += (float)af[j][e];
+        }
+    };
+#pragma unroll
+    for (int p = 0; p < P; ++p) issue(p);
+    for (int u = 0; u < nsteps; ++u) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        vmwait<(P - 1) * D>();             // step u landed (only the P - 1 later steps' DMAs in flight)
+        __builtin_amdgcn_s_barrier();      // ... for every wave; stage (u - 1) % S is free
+        __builtin_amdgcn_sched_barrier(0);
+        issue(u + P);
+        mma(u);
+    }
+    vmwait<0>();   // drain the prefetch past the chunk before the LDS is released
+    const long slab = ((long)Ncols * Kdim + Ncols + 3) & ~3L;
+    float* out = part + (long)blockIdx.z * slab;
+#pragma unroll
+    for (int j = 0; j < TNW; ++j)
+#pragma unroll
+        for (int i = 0; i < TKW; ++i)
+#pragma unroll
+            for (int reg = 0; reg < 16; ++reg) {
+                const int n = n0 + wn + 32 * j + crow(reg, h), k = k0 + wk + 32 * i + (lane & 31);
+                if (n < Ncols && k < Kdim) out[(long)n * Kdim + k] = acc[j][i][reg];
+            }
+    if (do_bias) {   // lanes r and r + 32 hold the two row halves of column wn + 32 j + r
+#pragma unroll
+        for (int j = 0; j < TNW; ++j) {
+            const float v = bsum[j] + __shfl_xor(bsum[j], 32, 64);
+            const int n = n0 + wn + 32 * j + (lane & 31);
+            if (h == 0 && n < Ncols) out[(long)Ncols * Kdim + n] = v;
+        }
+    }
+}
+
+struct WDCfg { int tn, tk, s, wn, wk; };
+constexpr WDCfg kWDCfgs[] = {{128, 128, 3, 2, 2}, {64, 256, 3, 1, 4}, {128, 128, 2, 2, 2}, {256, 128, 2, 4, 2}, {64, 128, 4, 1, 4}};
+constexpr int kWDNCfg = 5;
+
 // ---- bf16 implicit GEMM, v2: 128/256 x BN tiles, 64-deep K slices, double-buffered LDS ----------
 // One problem description covers the forward conv and each stride phase of the input gradient:
 //   row (b, ry, rx) gathers source pixel (ry*ay + by + ty*sty, rx*ax + bx + tx*stx) for tap (ty, tx),
@@ -519,8 +660,262 @@ __global__ __launch_bounds__(NT) void igemm_bf16(IG4 gs, const bf16* __restrict_
         }
 }
 
+// ---- bf16 implicit GEMM, v3 (Cs % 64 == 0, Ncols % BN == 0): persistent, LDS-DMA gathers ---------
+// Both operand images are filled by buffer_load ... lds (no VGPR round trip, lds_dma.hpp): the
+// A-image lanes gather their own 16 B (one pixel, one tap, 8 channels) through a per-lane offset --
+// taps outside the image get an out-of-range offset and land as zeros -- and the weight image is a
+// [BN][64] slice of the OHWI / IHWO matrix.  A 64-deep K slice lies inside one tap (Cs % 64 == 0), so
+// the tap, the weight column and the validity of each row are per-slice scalars / per-lane selects.
+// Workgroups are persistent and walk their tiles' K slices as one stream of units through an
+// S-stage ring (the scheme of gemm4.hip): the gathers of the next tile overlap the last slices and
+// the epilogue of the current one.  Tiles of one XCD are a contiguous range (xcd order), so the
+// halo rows a 3x3 tap re-reads and the A panel shared by the N tiles stay in that XCD's L2.
+// Accumulators hold [features][pixels] (the weight fragment is the MFMA A operand): lane (r, h) owns
+// pixel r and features 8g + 4h .. + 3, written as 8-B vectors straight from registers.
+constexpr int kIDMaxN = 1024;   // output columns of the LDS bias copy
+template <int BM, int BN, int S, int WM, int WN>
+__global__ __launch_bounds__(64 * WM * WN, 1) void igemm_dma(IG g, const bf16* __restrict__ src, const bf16* __restrict__ Bw,
+                                                             const float* __restrict__ bias, bf16* __restrict__ out) {
+    constexpr int NWV = WM * WN;
+    constexpr int TMW = BM / (32 * WM), TNW = BN / (32 * WN);   // 32x32 tiles per wave (pixels, features)
+    constexpr int BK = 64;
+    constexpr int STAGE = (BM + BN) * BK;                       // bf16 elements per ring stage
+    constexpr int NA = BM / (8 * NWV), NB = BN / (8 * NWV);     // DMA instructions per wave per unit
+    constexpr int D = NA + NB;
+    constexpr int P = S - 1;
+    constexpr int ST = TMW * TNW * 4;                           // epilogue stores per wave per tile
+    static_assert(NA >= 1 && NB >= 1 && TMW >= 1 && TNW >= 1, "igemm_dma wave layout");
+    __shared__ __attribute__((aligned(1024))) bf16 smem[S * STAGE];
+    __shared__ __attribute__((aligned(16))) float sbias[kIDMaxN];
+    const unsigned nbn = (unsigned)(g.Ncols / BN);
+    const unsigned T = (unsigned)((g.M + BM - 1) / BM) * nbn;
+    const unsigned x = blockIdx.x % kXcds, kk = blockIdx.x / kXcds, nloc = gridDim.x / kXcds;
+    const unsigned q = T / kXcds, rem = T % kXcds;
+    const unsigned lo = x < rem ? x * (q + 1) : rem * (q + 1) + (x - rem) * q;
+    const unsigned cnt = q + (x < rem ? 1 : 0);
+    const int mytiles = kk < cnt ? (int)((cnt - kk + nloc - 1) / nloc) : 0;
+    if (mytiles == 0) return;
+    const int nk = g.Kd / BK;
+    const int U = mytiles * nk;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int r = lane & 31, h = lane >> 5;
+    const int wm = (wave / WN) * (BM / WM), wn = (wave % WN) * (BN / WN);
+    // every output column's bias, once per workgroup (zeros without bias); vmcnt(0) here is before
+    // the first DMA, and the first wait_unit's barrier publishes the LDS copy
+    for (int n = threadIdx.x; n < g.Ncols; n += 64 * NWV) sbias[n] = bias ? bias[n] : 0.f;
+    vmwait<0>();
+
+    // DMA instruction i of this wave fills image rows (wave * N + i) * 8 .. + 7; lane l row + l / 8,
+    // 16-B chunk position l & 7 holding source chunk (l & 7) ^ (row & 7) (XOR swizzle, g4 layout)
+    unsigned achan[NA], voffW[NB];
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+        const int row = (wave * NA + i) * 8 + (lane >> 3);
+        achan[i] = (unsigned)(((lane & 7) ^ (row & 7)) << 4);
+    }
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+        const int row = (wave * NB + i) * 8 + (lane >> 3);
+        voffW[i] = (unsigned)row * g.ldw * 2 + (unsigned)(((lane & 7) ^ (row & 7)) << 4);
+    }
+    // gather bases of the lane's A rows for the tile being prefetched
+    int arb[NA], ary[NA], arx[NA];
+    unsigned ptile = 0xffffffffu;
+    auto bases = [&](unsigned tile) {
+        const long m0 = (long)(tile / nbn) * BM;
+#pragma unroll
+        for (int i = 0; i < NA; ++i) {
+            const long m = m0 + (wave * NA + i) * 8 + (lane >> 3);
+            const bool mv = m < g.M;   // branch-free: rows past the end get a never-valid y
+            const unsigned mu = (unsigned)(mv ? m : 0), t = mu / (unsigned)g.RW;   // 32-bit (check_geo)
+            const int rx = (int)(mu - t * (unsigned)g.RW);
+            const unsigned b = t / (unsigned)g.RH;
+            const int ry = (int)(t - b * (unsigned)g.RH);
+            arb[i] = (int)b * g.Hs;
+            ary[i] = mv ? ry * g.ay + g.by : -(1 << 29);
+            arx[i] = rx * g.ax + g.bx;
+        }
+    };
+    const i32x4 rsA = rsrc4(src, (long)g.B * g.Hs * g.Ws * g.Cs * 2);
+    auto issue = [&](int u) {   // DMA of unit min(u, U - 1) into stage u % S
+        const int uu = u < U ? u : U - 1;
+        const unsigned tile = lo + kk + (unsigned)(uu / nk) * nloc;
+        if (tile != ptile) {
+            bases(tile);
+            ptile = tile;
+        }
+        const int k0 = ((uu % nk + (kRot ? (int)(tile % (unsigned)nk) : 0)) % nk) * BK;   // rotated slice order
+        const int t = k0 / g.Cs, c0 = k0 - t * g.Cs;
+        const int ty = t / g.ntx, tx = t - ty * g.ntx;
+        const int oy = ty * g.sty, ox = tx * g.stx;
+        const int wcol = ((ty * g.wty + g.w0y) * g.KWf + tx * g.wtx + g.w0x) * g.Cs + c0;
+        unsigned va[NA];
+#pragma unroll
+        for (int i = 0; i < NA; ++i) {
+            const int y = ary[i] + oy, xx = arx[i] + ox;
+            const bool ok = y >= 0 && y < g.Hs && xx >= 0 && xx < g.Ws;
+            va[i] = ok ? (unsigned)((((arb[i] + y) * g.Ws + xx) * g.Cs + c0) * 2) + achan[i] : kOOB;
+        }
+        bf16* stg = smem + (u % S) * STAGE;
+        dma<NA>(rsA, va, 0u, stg, wave);
+        const long rw = (long)(tile % nbn) * BN;
+        dma<NB>(rsrc4(Bw + rw * g.ldw, (long)(g.Ncols - rw) * g.ldw * 2), voffW, (unsigned)wcol * 2u, stg + BM * BK, wave);
+    };
+    auto wait_unit = [&](int u) {   // vector-memory ops issued after unit u's DMA (issued at step u - P)
+        const int w = u - P;
+        int c = (w >= 0 && w % nk == nk - 1) ? ST : 0;
+        for (int v = w + 1; v < u; ++v) c += D + ((v >= 0 && v % nk == nk - 1) ? ST : 0);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        switch (c >= 63 ? 7 : c >> 3) {   // vmcnt(largest multiple of 8 <= c): waiting for more is safe
+            case 0: vmwait<0>(); break;
+            case 1: vmwait<8>(); break;
+            case 2: vmwait<16>(); break;
+            case 3: vmwait<24>(); break;
+            case 4: vmwait<32>(); break;
+            case 5: vmwait<40>(); break;
+            case 6: vmwait<48>(); break;
+            default: vmwait<56>(); break;
+        }
+        __builtin_amdgcn_s_barrier();   // unit u landed for every wave; stage (u - 1) % S is free
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    f32x16 acc[TMW][TNW];
+#pragma unroll
+    for (int i = 0; i < TMW; ++i)
+#pragma unroll
+        for (int j = 0; j < TNW; ++j) acc[i][j] = f32x16{};
+    auto mma = [&](int u) {
+        const bf16* As = smem + (u % S) * STAGE;
+        const bf16* Ws = As + BM * BK;
+        bf16x8 af[2][TMW], wf[2][TNW];   // fragments of k-step s + 1 read while step s multiplies
+        auto frags = [&](int s, int b) {
+#pragma unroll
+            for (int i = 0; i < TMW; ++i) af[b][i] = *reinterpret_cast<const bf16x8*>(As + swz128(wm + 32 * i + r, 2 * s + h));
+#pragma unroll
+            for (int j = 0; j < TNW; ++j) wf[b][j] = *reinterpret_cast<const bf16x8*>(Ws + swz128(wn + 32 * j + r, 2 * s + h));
+        };
+        frags(0, 0);
+#pragma unroll
+        for (int s = 0; s < BK / 16; ++s) {
+            if (s + 1 < BK / 16) frags(s + 1, (s + 1) & 1);
+#pragma unroll
+            for (int i = 0; i < TMW; ++i)
+#pragma unroll
+                for (int j = 0; j < TNW; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[s & 1][j], af[s & 1][i], acc[i][j], 0, 0, 0);
+        }
+    };
+    const __amdgpu_buffer_rsrc_t rs_o = buf_rsrc(out, (long)g.B * g.OHo * g.OWo * g.Ncols * 2);
+
+#pragma unroll
+    for (int p = 0; p < P; ++p) issue(p);
+    int u = 0;
+    for (int t = 0; t < mytiles; ++t) {
+        for (int ks = 0; ks + 1 < nk; ++ks, ++u) {   // all but the tile's last K slice
+            wait_unit(u);
+            issue(u + P);
+            mma(u);
+        }
+        wait_unit(u);
+        const unsigned tile = lo + kk + (unsigned)t * nloc;
+        const long m0 = (long)(tile / nbn) * BM;
+        const int n0 = (int)(tile % nbn) * BN;
+        unsigned orow[TMW];   // byte offset of the output pixel of rows wm + 32 i + r (kOOB: none)
+#pragma unroll
+        for (int i = 0; i < TMW; ++i) {
+            const long m = m0 + wm + 32 * i + r;
+            const bool mv = m < g.M;
+            const unsigned mu = (unsigned)(mv ? m : 0), tq = mu / (unsigned)g.RW;
+            const int rx = (int)(mu - tq * (unsigned)g.RW);
+            const unsigned b = tq / (unsigned)g.RH;
+            const int ry = (int)(tq - b * (unsigned)g.RH);
+            const unsigned o = (unsigned)((((int)b * g.OHo + ry * g.oya + g.oyb) * g.OWo + rx * g.oxa + g.oxb) * g.Ncols) * 2u;
+            orow[i] = mv ? o : kOOB;
+        }
+        issue(u + P);
+        mma(u);
+        // bias from the LDS copy (lgkmcnt: the vmcnt accounting of the ring is untouched)
+#pragma unroll
+        for (int j = 0; j < TNW; ++j)
+#pragma unroll
+            for (int gq = 0; gq < 4; ++gq) {
+                const int nf = n0 + wn + 32 * j + 8 * gq + 4 * h;
+                const f32x4 bv = *reinterpret_cast<const f32x4*>(sbias + nf);
+                const unsigned nb = (unsigned)nf * 2u;
+#pragma unroll
+                for (int i = 0; i < TMW; ++i) {
+                    const float v[4] = {acc[i][j][4 * gq] + bv[0], acc[i][j][4 * gq + 1] + bv[1], acc[i][j][4 * gq + 2] + bv[2],
+                                        acc[i][j][4 * gq + 3] + bv[3]};
+                    buf_st4bf(rs_o, orow[i] == kOOB ? kOOB : orow[i] + nb, v);
+                }
+            }
+#pragma unroll
+        for (int i = 0; i < TMW; ++i)
+#pragma unroll
+            for (int j = 0; j < TNW; ++j) acc[i][j] = f32x16{};
+        ++u;
+    }
+    vmwait<0>();   // drain the re-fetch DMAs before the workgroup's LDS is released
+}
+
+struct IDCfg { int bm, bn, s, wm, wn; };
+constexpr IDCfg kIDCfgs[] = {{128, 128, 3, 2, 2}, {256, 128, 2, 4, 2}, {256, 128, 3, 4, 2}, {128, 64, 4, 2, 2},
+                             {256, 64, 3, 4, 2},  {128, 64, 3, 2, 2},  {256, 256, 2, 2, 4}, {256, 256, 2, 4, 2},
+                             {512, 64, 2, 8, 1}};
+constexpr int kIDNCfg = 9;
+
+int id_cus() {
+    static int cus = 0;
+    if (!cus) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            cus = 256;
+        cus = (cus + kXcds - 1) / kXcds * kXcds;
+    }
+    return cus;
+}
+
+template <int C>
+int id_launch(const IG& g, const void* src, const void* w, const float* bias, void* out, hipStream_t st) {
+    constexpr IDCfg c = kIDCfgs[C];
+    if (g.Ncols % c.bn) return fail(CSU_E_ARG, "conv2d: Ncols not a multiple of the tile's BN");
+    igemm_dma<c.bm, c.bn, c.s, c.wm, c.wn><<<dim3(id_cus()), 64 * c.wm * c.wn, 0, st>>>(g, (const bf16*)src, (const bf16*)w, bias,
+                                                                                  (bf16*)out);
+    return check_launch("conv2d (igemm_dma)");
+}
+
+// v3 eligibility and tile choice (tools/conv_probe.py on the UNet 512x512 B16 and CSWin merge shapes,
+// profiles/r03q_conv_probe.txt): 256 x 256 tiles (MFMA busy 38-41 % at C >= 256) when they still give
+// every CU a tile, else 256 x 128 (25-30 %); Ncols = 64 stays on the v2 kernel, which the 64-wide v3
+// tiles do not beat (the A gathers dominate: 9 taps x 64 channels per 64 outputs).  -1: v2.
+int id_pick(const IG& g) {
+    if (g.Cs % 64 || g.Kd < 64 || g.Ncols > kIDMaxN) return -1;
+    const long mt = (g.M + 255) / 256;
+    if (g.Ncols % 256 == 0 && mt * (g.Ncols / 256) >= id_cus()) return 7;
+    if (g.Ncols % 128 == 0) return 2;
+    return -1;
+}
+
+int id_run(int cfg, const IG& g, const void* src, const void* w, const float* bias, void* out, hipStream_t st) {
+    switch (cfg) {
+        case 0: return id_launch<0>(g, src, w, bias, out, st);
+        case 1: return id_launch<1>(g, src, w, bias, out, st);
+        case 2: return id_launch<2>(g, src, w, bias, out, st);
+        case 3: return id_launch<3>(g, src, w, bias, out, st);
+        case 4: return id_launch<4>(g, src, w, bias, out, st);
+        case 5: return id_launch<5>(g, src, w, bias, out, st);
+        case 6: return id_launch<6>(g, src, w, bias, out, st);
+        case 7: return id_launch<7>(g, src, w, bias, out, st);
+        case 8: return id_launch<8>(g, src, w, bias, out, st);
+        default: return fail(CSU_E_ARG, "conv2d: bad igemm_dma configuration");
+    }
+}
+
 // n problems with equal Ncols and channel count (the phases of one input gradient, or one forward)
-int launch_ig(const IG* gv, int n, const void* src, const void* w, const float* bias, void* out, hipStream_t st) {
+// cfg: -1 per-shape choice (v3 where eligible), 0 the v2 kernel, 1 + k the v3 configuration k
+int launch_ig(const IG* gv, int n, const void* src, const void* w, const float* bias, void* out, hipStream_t st,
+              int cfg = -1) {
     IG4 gs{};
     long maxm = 0;
     for (int i = 0; i < n; ++i) {
@@ -531,6 +926,18 @@ int launch_ig(const IG* gv, int n, const void* src, const void* w, const float* 
     if ((long)g.B * g.Hs * g.Ws * g.Cs * 2 >= (1L << 31) || (long)g.Ncols * g.ldw * 2 >= (1L << 31) ||
         (long)g.B * g.OHo * g.OWo * g.Ncols * 2 >= (1L << 31))
         return fail(CSU_E_UNSUPPORTED, "conv2d: operand larger than 2 GiB (32-bit buffer offsets)");
+    if (cfg != 0) {   // v3: every phase must be eligible (64-channel slices, BN | Ncols)
+        int pick = cfg > 0 ? cfg - 1 : id_pick(g);
+        for (int i = 0; i < n && pick >= 0; ++i)
+            if (id_pick(gv[i]) < 0 || (cfg > 0 && gv[i].Ncols % kIDCfgs[pick].bn)) pick = -1;
+        if (cfg > 0 && (cfg - 1 >= kIDNCfg || pick < 0)) return fail(CSU_E_ARG, "conv2d: igemm_dma configuration not eligible");
+        if (pick >= 0) {
+            for (int i = 0; i < n; ++i)
+                if (gv[i].M > 0)
+                    if (int e = id_run(pick, gv[i], src, w, bias, out, st)) return e;
+            return 0;
+        }
+    }
     const int vw = g.Cs % 8 == 0 ? 8 : 4;
     const bool narrow = g.Ncols <= 32;
     const int BM = narrow ? 256 : 128, BN = narrow ? 32 : 64;
@@ -547,8 +954,8 @@ int launch_ig(const IG* gv, int n, const void* src, const void* w, const float* 
     }
     return check_launch("conv2d (igemm)");
 }
-int launch_ig(const IG& g, const void* src, const void* w, const float* bias, void* out, hipStream_t st) {
-    return launch_ig(&g, 1, src, w, bias, out, st);
+int launch_ig(const IG& g, const void* src, const void* w, const float* bias, void* out, hipStream_t st, int cfg = -1) {
+    return launch_ig(&g, 1, src, w, bias, out, st, cfg);
 }
 bool ig_phases_fused() {   // CSU_CONV_PHASE_LAUNCHES=1: one launch per stride phase (A/B)
     static int v = -1;
@@ -639,6 +1046,59 @@ WPl wplan(long M, int N, int K) {
     return p;
 }
 
+// v3 weight-gradient plan: TN x TK tiles, chunks of >= 16 steps so that tiles x chunks ~ 2 rounds of
+// the CUs (one 96-120 KB workgroup per CU)
+WPl wplan_dma(long M, int N, int K, const WDCfg& c) {
+    const long tiles = (long)((N + c.tn - 1) / c.tn) * ((K + c.tk - 1) / c.tk);
+    long want = (2L * id_cus() + tiles - 1) / tiles;
+    const long maxc = (M + 1023) / 1024;
+    if (want > maxc) want = maxc;
+    if (want > 512) want = 512;
+    if (want < 1) want = 1;
+    WPl p;
+    p.rpc = ((M + want - 1) / want + 63) / 64 * 64;
+    p.chunks = (int)((M + p.rpc - 1) / p.rpc);
+    return p;
+}
+
+// weight-gradient kernel of a geometry: -1 the v2 kernel, else a kWDCfgs index (cfg: -1 auto, 0 v2,
+// 1 + k forced; -2 when a forced v3 configuration is not eligible)
+int wd_pick(const csu_conv_geom* gm, int dtype, int cfg) {
+    const bool ok = dtype == CSU_BF16 && gm->C % 8 == 0 && gm->N % 8 == 0 &&
+                    (long)gm->B * gm->H * gm->W * gm->C * 2 < (1L << 31) && (long)gm->B * gm->OH * gm->OW * gm->N * 2 < (1L << 31);
+    if (cfg == 0) return -1;
+    if (cfg > 0) return ok && cfg - 1 < kWDNCfg ? cfg - 1 : -2;
+    if (!ok) return -1;
+    return gm->N >= 128 ? 0 : 1;
+}
+
+size_t wgrad_ws(const csu_conv_geom* gm, int pick) {
+    const long M = (long)gm->B * gm->OH * gm->OW;
+    const int K = gm->KH * gm->KW * gm->C;
+    const WPl p = pick >= 0 ? wplan_dma(M, gm->N, K, kWDCfgs[pick]) : wplan(M, gm->N, K);
+    const long slab = ((long)gm->N * K + gm->N + 3) & ~3L;
+    const size_t stage = slab != (long)gm->N * K + gm->N ? slab * sizeof(float) : 0;   // padded colsum output
+    return (size_t)p.chunks * slab * sizeof(float) + stage + colsum_workspace(p.chunks, slab, CSU_F32);
+}
+
+template <int C>
+void wd_launch(const Geo& g, long M, int N, int K, const WPl& p, const void* x, const void* dy, float* part, hipStream_t st) {
+    constexpr WDCfg c = kWDCfgs[C];
+    const dim3 grid((N + c.tn - 1) / c.tn, (K + c.tk - 1) / c.tk, p.chunks);
+    conv_wgrad_dma<c.tn, c.tk, c.s, c.wn, c.wk><<<grid, 64 * c.wn * c.wk, 0, st>>>(g, M, N, K, p.rpc, (const bf16*)x,
+                                                                                 (const bf16*)dy, part);
+}
+void wd_run(int pick, const Geo& g, long M, int N, int K, const WPl& p, const void* x, const void* dy, float* part,
+            hipStream_t st) {
+    switch (pick) {
+        case 0: wd_launch<0>(g, M, N, K, p, x, dy, part, st); break;
+        case 1: wd_launch<1>(g, M, N, K, p, x, dy, part, st); break;
+        case 2: wd_launch<2>(g, M, N, K, p, x, dy, part, st); break;
+        case 3: wd_launch<3>(g, M, N, K, p, x, dy, part, st); break;
+        default: wd_launch<4>(g, M, N, K, p, x, dy, part, st); break;
+    }
+}
+
 template <typename T, int MODE>
 int launch_gemm(const Geo& g, long M, int Ncols, int Kdim, const void* src, const void* w, const float* bias, void* out,
                 bool vec, hipStream_t st) {
@@ -655,8 +1115,8 @@ int launch_gemm(const Geo& g, long M, int Ncols, int Kdim, const void* src, cons
 
 using namespace csu;
 
-extern "C" int csu_conv2d_fwd(const csu_conv_geom* gm, int dtype, const void* x, const void* w_ohwi, const float* bias,
-                              void* out, void* stream) {
+static int conv_fwd_impl(const csu_conv_geom* gm, int dtype, const void* x, const void* w_ohwi, const float* bias, void* out,
+                         int cfg, void* stream) {
     if (int e = check_geo(gm)) return e;
     if (!x || !w_ohwi || !out) return fail(CSU_E_ARG, "conv2d_fwd: null buffer");
     const Geo g = to_geo(gm);
@@ -664,14 +1124,15 @@ extern "C" int csu_conv2d_fwd(const csu_conv_geom* gm, int dtype, const void* x,
     const int K = g.KH * g.KW * g.C;
     const bool vec = g.C % 8 == 0;
     hipStream_t st = as_stream(stream);
-    if (dtype == CSU_BF16 && g.C % 4 == 0) return launch_ig(ig_forward(*gm), x, w_ohwi, bias, out, st);
+    if (dtype == CSU_BF16 && g.C % 4 == 0) return launch_ig(ig_forward(*gm), x, w_ohwi, bias, out, st, cfg);
+    if (cfg > 0) return fail(CSU_E_ARG, "conv2d_fwd: igemm_dma needs bf16 with C % 64 == 0");
     if (dtype == CSU_BF16) return launch_gemm<bf16, 0>(g, M, g.N, K, x, w_ohwi, bias, out, vec, st);
     if (dtype == CSU_F32) return launch_gemm<float, 0>(g, M, g.N, K, x, w_ohwi, bias, out, vec, st);
     return fail(CSU_E_ARG, "conv2d_fwd: bad dtype");
 }
 
-extern "C" int csu_conv2d_dgrad(const csu_conv_geom* gm, int dtype, const void* dy, const void* w_ihwo,
-                                const float* bias, void* dx, void* stream) {
+static int conv_dgrad_impl(const csu_conv_geom* gm, int dtype, const void* dy, const void* w_ihwo, const float* bias, void* dx,
+                           int cfg, void* stream) {
     if (int e = check_geo(gm)) return e;
     if (!dy || !w_ihwo || !dx) return fail(CSU_E_ARG, "conv2d_dgrad: null buffer");
     const Geo g = to_geo(gm);
@@ -687,45 +1148,73 @@ extern "C" int csu_conv2d_dgrad(const csu_conv_geom* gm, int dtype, const void* 
                 const IG ig = ig_dgrad_phase(*gm, py, px);
                 if (ig.M == 0) continue;
                 if (np > 0 && (np == 4 || !ig_phases_fused())) {   // stride > 2 (or the A/B switch): flush
-                    if (int e = launch_ig(ph, np, dy, w_ihwo, bias, dx, st)) return e;
+                    if (int e = launch_ig(ph, np, dy, w_ihwo, bias, dx, st, cfg)) return e;
                     np = 0;
                 }
                 ph[np++] = ig;
             }
-        return np ? launch_ig(ph, np, dy, w_ihwo, bias, dx, st) : 0;
+        return np ? launch_ig(ph, np, dy, w_ihwo, bias, dx, st, cfg) : 0;
     }
+    if (cfg > 0) return fail(CSU_E_ARG, "conv2d_dgrad: igemm_dma needs bf16 with N % 64 == 0");
     if (dtype == CSU_BF16) return launch_gemm<bf16, 1>(g, M, g.C, K, dy, w_ihwo, bias, dx, vec, st);
     if (dtype == CSU_F32) return launch_gemm<float, 1>(g, M, g.C, K, dy, w_ihwo, bias, dx, vec, st);
     return fail(CSU_E_ARG, "conv2d_dgrad: bad dtype");
 }
 
+extern "C" int csu_conv2d_fwd(const csu_conv_geom* gm, int dtype, const void* x, const void* w_ohwi, const float* bias,
+                              void* out, void* stream) {
+    return conv_fwd_impl(gm, dtype, x, w_ohwi, bias, out, -1, stream);
+}
+
+extern "C" int csu_conv2d_dgrad(const csu_conv_geom* gm, int dtype, const void* dy, const void* w_ihwo,
+                                const float* bias, void* dx, void* stream) {
+    return conv_dgrad_impl(gm, dtype, dy, w_ihwo, bias, dx, -1, stream);
+}
+
+extern "C" int csu_conv2d_ex(int op, const csu_conv_geom* gm, int dtype, const void* src, const void* w, const float* bias,
+                             void* out, int cfg, void* stream) {
+    if (op == 0) return conv_fwd_impl(gm, dtype, src, w, bias, out, cfg, stream);
+    if (op == 1) return conv_dgrad_impl(gm, dtype, src, w, bias, out, cfg, stream);
+    return fail(CSU_E_ARG, "conv2d_ex: op must be 0 (forward) or 1 (input gradient)");
+}
+
 extern "C" size_t csu_conv2d_wgrad_workspace(const csu_conv_geom* gm) {
     if (check_geo(gm)) return 0;
-    const long M = (long)gm->B * gm->OH * gm->OW;
-    const int K = gm->KH * gm->KW * gm->C;
-    const WPl p = wplan(M, gm->N, K);
-    const long slab = ((long)gm->N * K + gm->N + 3) & ~3L;
-    const size_t stage = slab != (long)gm->N * K + gm->N ? slab * sizeof(float) : 0;   // padded colsum output
-    return (size_t)p.chunks * slab * sizeof(float) + stage + colsum_workspace(p.chunks, slab, CSU_F32);
+    // dtype-independent: enough for the v2 plan and for the v3 plan the bf16 call picks
+    const size_t a = wgrad_ws(gm, -1);
+    const int pk = wd_pick(gm, CSU_BF16, -1);
+    const size_t b = pk >= 0 ? wgrad_ws(gm, pk) : 0;
+    return a > b ? a : b;
+}
+
+extern "C" size_t csu_conv2d_wgrad_workspace_ex(const csu_conv_geom* gm, int cfg) {
+    if (check_geo(gm)) return 0;
+    if (cfg < 0) return csu_conv2d_wgrad_workspace(gm);
+    const int pk = wd_pick(gm, CSU_BF16, cfg);
+    return pk == -2 ? 0 : wgrad_ws(gm, pk);
 }
 
 static int conv_wgrad_impl(const csu_conv_geom* gm, int dtype, const void* x, const void* dy, int creal, float* dw_db,
-                           void* workspace, size_t ws_bytes, void* stream) {
+                           void* workspace, size_t ws_bytes, int cfg, void* stream) {
     if (int e = check_geo(gm)) return e;
     if (!x || !dy || !dw_db) return fail(CSU_E_ARG, "conv2d_wgrad: null buffer");
-    if (!workspace || ws_bytes < csu_conv2d_wgrad_workspace(gm)) return fail(CSU_E_WORKSPACE, "conv2d_wgrad: workspace");
+    const int pick = wd_pick(gm, dtype, cfg);
+    if (pick == -2) return fail(CSU_E_ARG, "conv2d_wgrad: configuration not eligible (bf16, C % 8 == 0, N % 8 == 0)");
+    if (!workspace || ws_bytes < wgrad_ws(gm, pick)) return fail(CSU_E_WORKSPACE, "conv2d_wgrad: workspace");
     if (creal > gm->C) return fail(CSU_E_ARG, "conv2d_wgrad: c_real > C");
     const Geo g = to_geo(gm);
     const long M = (long)g.B * g.OH * g.OW;
     const int K = g.KH * g.KW * g.C;
-    const WPl p = wplan(M, g.N, K);
+    const WPl p = pick >= 0 ? wplan_dma(M, g.N, K, kWDCfgs[pick]) : wplan(M, g.N, K);
     const long used = (long)g.N * K + g.N;
     const long slab = (used + 3) & ~3L;
     float* part = (float*)workspace;
     const dim3 grid((g.N + TBN - 1) / TBN, (K + TBN - 1) / TBN, p.chunks);
     const bool vec = g.C % 8 == 0;
     hipStream_t st = as_stream(stream);
-    if (dtype == CSU_BF16) {
+    if (pick >= 0) {
+        wd_run(pick, g, M, g.N, K, p, x, dy, part, st);
+    } else if (dtype == CSU_BF16) {
         const bool small = (long)g.B * g.H * g.W * g.C * 2 < (1L << 31) && M * g.N * 2 < (1L << 31);   // 32-bit offsets
         if (vec && g.N % 8 == 0 && small && conv_wgrad_v2())
             conv_wgrad_bf16<<<grid, NT, 0, st>>>(g, M, g.N, K, p.rpc, (const bf16*)x, (const bf16*)dy, part);
@@ -752,11 +1241,17 @@ static int conv_wgrad_impl(const csu_conv_geom* gm, int dtype, const void* x, co
 
 extern "C" int csu_conv2d_wgrad(const csu_conv_geom* gm, int dtype, const void* x, const void* dy, float* dw_db,
                                 void* workspace, size_t ws_bytes, void* stream) {
-    return conv_wgrad_impl(gm, dtype, x, dy, 0, dw_db, workspace, ws_bytes, stream);
+    return conv_wgrad_impl(gm, dtype, x, dy, 0, dw_db, workspace, ws_bytes, -1, stream);
 }
 
 extern "C" int csu_conv2d_wgrad_oihw(const csu_conv_geom* gm, int dtype, const void* x, const void* dy, int c_real,
                                      float* dw_db, void* workspace, size_t ws_bytes, void* stream) {
     if (c_real < 1) return fail(CSU_E_ARG, "conv2d_wgrad_oihw: c_real < 1");
-    return conv_wgrad_impl(gm, dtype, x, dy, c_real, dw_db, workspace, ws_bytes, stream);
+    return conv_wgrad_impl(gm, dtype, x, dy, c_real, dw_db, workspace, ws_bytes, -1, stream);
+}
+
+extern "C" int csu_conv2d_wgrad_ex(const csu_conv_geom* gm, int dtype, const void* x, const void* dy, int c_real, float* dw_db,
+                                   void* workspace, size_t ws_bytes, int cfg, void* stream) {
+    if (c_real < 0) return fail(CSU_E_ARG, "conv2d_wgrad_ex: c_real < 0");
+    return conv_wgrad_impl(gm, dtype, x, dy, c_real, dw_db, workspace, ws_bytes, cfg, stream);
 }

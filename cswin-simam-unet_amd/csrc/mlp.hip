@@ -193,6 +193,11 @@ __global__ __launch_bounds__(MT) void mlp_fwd_kernel(long M, const bf16* __restr
     const int tok = 32 * t + r;
     const bool ok = tok < rows;
     const int hs = 32 * u;              // this wave's hidden features within a chunk
+    // hidden chunk of loop step j: rotated by the panel, so the workgroups running together stream
+    // different weight chunks (every panel reads the same 2 x 4C x C weights: without the rotation
+    // all CUs of an XCD hit the same L2 lines at once)
+    const int j0 = kRot ? (int)(blockIdx.x & (NCH - 1)) : 0;
+    auto chk = [&](int j) { return (j + j0) & (NCH - 1); };
     for (int i = threadIdx.x; i < 4 * C; i += MT) b1s[i] = b1[i];
     bf16x8 xf[KS];
     load_bfrags<C>(buf_rsrc(X + m0 * C, rows * C * 2), tok, ok, h, xf);
@@ -204,9 +209,9 @@ __global__ __launch_bounds__(MT) void mlp_fwd_kernel(long M, const bf16* __restr
     const i32x4 rs_w1 = rsrc4(W1, 4L * C * C * 2);
     const i32x4 rs_w2 = rsrc4(W2, 4L * C * C * 2);
     asm volatile("" ::: "memory");
-    dma<D1::NW>(rs_w1, d1.v, 0, w1r, wave);
-    dma<D2::NW>(rs_w2, d2.v, 0, w2r, wave);
-    dma<D1::NW>(rs_w1, d1.v, HC * C * 2, w1r + IMG, wave);
+    dma<D1::NW>(rs_w1, d1.v, (unsigned)chk(0) * HC * C * 2, w1r, wave);
+    dma<D2::NW>(rs_w2, d2.v, (unsigned)chk(0) * HC * 2, w2r, wave);
+    dma<D1::NW>(rs_w1, d1.v, (unsigned)chk(1) * HC * C * 2, w1r + IMG, wave);
 
     auto gemm1 = [&](const bf16* img) {
         bf16x8 wf[KS];
@@ -235,16 +240,17 @@ __global__ __launch_bounds__(MT) void mlp_fwd_kernel(long M, const bf16* __restr
         constexpr int P = decltype(par)::value;
         vmwait<0>();                    // W1(j+1), W2(j): issued one step ago
         lds_sync();                     // every wave is past GEMM1(j) and GEMM2(j-1)
-        if (j + 2 < NCH) dma<D1::NW>(rs_w1, d1.v, (unsigned)(j + 2) * HC * C * 2, w1r + P * IMG, wave);
-        if (j + 1 < NCH) dma<D2::NW>(rs_w2, d2.v, (unsigned)(j + 1) * HC * 2, w2r + (1 - P) * IMG, wave);
+        if (j + 2 < NCH) dma<D1::NW>(rs_w1, d1.v, (unsigned)chk(j + 2) * HC * C * 2, w1r + P * IMG, wave);
+        if (j + 1 < NCH) dma<D2::NW>(rs_w2, d2.v, (unsigned)chk(j + 1) * HC * 2, w2r + (1 - P) * IMG, wave);
+        const int jc = chk(j);
         float bv[16], gv[16];
-        bias16(b1s, j * HC + hs, h, bv);
+        bias16(b1s, jc * HC + hs, h, bv);
         if constexpr (decltype(more)::value) nxt = gemm1(w1r + (1 - P) * IMG);
 #pragma unroll
         for (int e = 0; e < 16; ++e) gv[e] = gelu_fast(cur[e] + bv[e]);
         if constexpr (DROP) {   // hidden dropout on g (features j*HC + hs + crow(e, h) of token mg)
             if (dd.p > 0.f) {
-                const unsigned km = keep16_crow(Rh, ((uint64_t)mg * 4 * C + j * HC + hs) >> 3, h);
+                const unsigned km = keep16_crow(Rh, ((uint64_t)mg * 4 * C + jc * HC + hs) >> 3, h);
 #pragma unroll
                 for (int e = 0; e < 16; ++e) gv[e] = ((km >> e) & 1u) ? gv[e] * Rh.scale : 0.f;
             }
@@ -322,6 +328,8 @@ __global__ __launch_bounds__(MT) void mlp_bwd_kernel(long M, const bf16* __restr
     const int tok = 32 * t + r;
     const bool ok = tok < rows;
     const int hs = 32 * u;
+    const int j0 = kRot ? (int)(blockIdx.x & (NCH - 1)) : 0;   // rotated chunk order (see the forward)
+    auto chk = [&](int j) { return (j + j0) & (NCH - 1); };
     for (int i = threadIdx.x; i < 4 * C; i += MT) b1s[i] = b1[i];
     bf16x8 xf[KS], dyf[KS];
     load_bfrags<C>(buf_rsrc(X + m0 * C, rows * C * 2), tok, ok, h, xf);
@@ -336,11 +344,11 @@ __global__ __launch_bounds__(MT) void mlp_bwd_kernel(long M, const bf16* __restr
     const auto rs_dh = buf_rsrc(dH + m0 * 4 * C, rows * 4 * C * 2);
     const auto rs_g = buf_rsrc(G + m0 * 4 * C, rows * 4 * C * 2);
     asm volatile("" ::: "memory");
-    dma<D1::NW>(rs_w1, d1.v, 0, w1r, wave);
-    dma<D2::NW>(rs_w2, d2.v, 0, w2r, wave);
+    dma<D1::NW>(rs_w1, d1.v, (unsigned)chk(0) * HC * C * 2, w1r, wave);
+    dma<D2::NW>(rs_w2, d2.v, (unsigned)chk(0) * HC * 2, w2r, wave);
     if constexpr (PIPE) {
-        dma<D1::NW>(rs_w1, d1.v, HC * C * 2, w1r + IMG, wave);
-        dma<D2::NW>(rs_w2, d2.v, HC * 2, w2r + IMG, wave);
+        dma<D1::NW>(rs_w1, d1.v, (unsigned)chk(1) * HC * C * 2, w1r + IMG, wave);
+        dma<D2::NW>(rs_w2, d2.v, (unsigned)chk(1) * HC * 2, w2r + IMG, wave);
     }
 
     // GEMM1 (h = W1_sub x^T) and GEMM3 (dg = W2_sub^T dY^T) of one chunk
@@ -380,7 +388,8 @@ __global__ __launch_bounds__(MT) void mlp_bwd_kernel(long M, const bf16* __restr
     const long mg = m0 + tok;
     DropoutRng Rh;
     if constexpr (DROP) Rh = load_rng(dd.rng, dd.site_h, dd.p);
-    auto finish = [&](int j, const f32x16& hc, const f32x16& gc, const float* bv, const bf16* w1c) {
+    auto finish = [&](int jj, const f32x16& hc, const f32x16& gc, const float* bv, const bf16* w1c) {
+        const int j = chk(jj);   // the chunk's hidden features
         float gv[16], dv[16];
         unsigned km = 0xffffu;
         if constexpr (DROP) if (dd.p > 0.f) km = keep16_crow(Rh, ((uint64_t)mg * 4 * C + j * HC + hs) >> 3, h);
@@ -429,11 +438,11 @@ __global__ __launch_bounds__(MT) void mlp_bwd_kernel(long M, const bf16* __restr
             vmwait<8>();                // W1(j+1), W2(j+1) landed; only chunk j-1's 8 stores after them
             lds_sync();                 // every wave is past GEMM4(j-1) and GEMM3(j)
             if (j + 2 < NCH) {
-                dma<D1::NW>(rs_w1, d1.v, (unsigned)(j + 2) * HC * C * 2, w1r + ((j + 2) % 3) * IMG, wave);
-                dma<D2::NW>(rs_w2, d2.v, (unsigned)(j + 2) * HC * 2, w2r + (j & 1) * IMG, wave);
+                dma<D1::NW>(rs_w1, d1.v, (unsigned)chk(j + 2) * HC * C * 2, w1r + ((j + 2) % 3) * IMG, wave);
+                dma<D2::NW>(rs_w2, d2.v, (unsigned)chk(j + 2) * HC * 2, w2r + (j & 1) * IMG, wave);
             }
             float bv[16];
-            bias16(b1s, j * HC + hs, h, bv);
+            bias16(b1s, chk(j) * HC + hs, h, bv);
             if constexpr (decltype(more)::value) gemm13(w1r + ((j + 1) % 3) * IMG, w2r + ((j + 1) & 1) * IMG, hn, gn);
             finish(j, hc, gc, bv, w1r + (j % 3) * IMG);
         };
@@ -450,11 +459,11 @@ __global__ __launch_bounds__(MT) void mlp_bwd_kernel(long M, const bf16* __restr
             if (j == 0) vmwait<0>(); else vmwait<8>();
             lds_sync();                 // every wave is past chunk j-1: its stage is free
             if (j + 1 < NCH) {
-                dma<D1::NW>(rs_w1, d1.v, (unsigned)(j + 1) * HC * C * 2, w1r + ((j + 1) & 1) * IMG, wave);
-                dma<D2::NW>(rs_w2, d2.v, (unsigned)(j + 1) * HC * 2, w2r + ((j + 1) & 1) * IMG, wave);
+                dma<D1::NW>(rs_w1, d1.v, (unsigned)chk(j + 1) * HC * C * 2, w1r + ((j + 1) & 1) * IMG, wave);
+                dma<D2::NW>(rs_w2, d2.v, (unsigned)chk(j + 1) * HC * 2, w2r + ((j + 1) & 1) * IMG, wave);
             }
             float bv[16];
-            bias16(b1s, j * HC + hs, h, bv);
+            bias16(b1s, chk(j) * HC + hs, h, bv);
             gemm13(w1r + (j & 1) * IMG, w2r + (j & 1) * IMG, ha, ga);
             finish(j, ha, ga, bv, w1r + (j & 1) * IMG);
         }

@@ -193,7 +193,12 @@ _SIGS = {
                                       c_void_p]),
     "csu_conv2d_dgrad": (ctypes.c_int, [ctypes.POINTER(ConvGeom), ctypes.c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                                         c_void_p]),
+    "csu_conv2d_ex": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ConvGeom), ctypes.c_int, c_void_p, c_void_p, c_void_p,
+                                     c_void_p, ctypes.c_int, c_void_p]),
     "csu_conv2d_wgrad_workspace": (c_size_t, [ctypes.POINTER(ConvGeom)]),
+    "csu_conv2d_wgrad_workspace_ex": (c_size_t, [ctypes.POINTER(ConvGeom), ctypes.c_int]),
+    "csu_conv2d_wgrad_ex": (ctypes.c_int, [ctypes.POINTER(ConvGeom), ctypes.c_int, c_void_p, c_void_p, ctypes.c_int,
+                                           c_void_p, c_void_p, c_size_t, ctypes.c_int, c_void_p]),
     "csu_conv2d_wgrad": (ctypes.c_int, [ctypes.POINTER(ConvGeom), ctypes.c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                                         c_size_t, c_void_p]),
     "csu_conv2d_wgrad_oihw": (ctypes.c_int, [ctypes.POINTER(ConvGeom), ctypes.c_int, c_void_p, c_void_p, ctypes.c_int,

@@ -482,6 +482,13 @@ int csu_conv2d_fwd(const csu_conv_geom* g, int dtype, const void* x, const void*
 /* dx = conv^T(dy) (+ bias, used when this operator is a ConvTranspose2d forward) */
 int csu_conv2d_dgrad(const csu_conv_geom* g, int dtype, const void* dy, const void* w_ihwo, const float* bias,
                      void* dx, void* stream);
+/* Either operator with an explicit kernel choice (op 0: csu_conv2d_fwd, 1: csu_conv2d_dgrad; src /
+ * w as there).  cfg -1: the per-shape choice the plain entries make; 0: the register-staged v2
+ * implicit GEMM; 1 + k: the persistent LDS-DMA kernel (bf16, gathered channels % 64 == 0) in tile
+ * configuration k (0: 128x128 3-stage, 1: 256x128 2-stage 8 waves, 2: 256x128 3-stage 8 waves,
+ * 3: 128x64 4-stage, 4: 256x64 3-stage 8 waves, 5: 128x64 3-stage); CSU_E_ARG when not eligible. */
+int csu_conv2d_ex(int op, const csu_conv_geom* g, int dtype, const void* src, const void* w, const float* bias, void* out,
+                  int cfg, void* stream);
 size_t csu_conv2d_wgrad_workspace(const csu_conv_geom* g);
 /* dw_db fp32 [N*KH*KW*C + N] = dW in [N][KH][KW][C] order, then db (sum of dy) */
 int csu_conv2d_wgrad(const csu_conv_geom* g, int dtype, const void* x, const void* dy, float* dw_db,
@@ -491,6 +498,15 @@ int csu_conv2d_wgrad(const csu_conv_geom* g, int dtype, const void* x, const voi
  * dropped.  Same workspace. */
 int csu_conv2d_wgrad_oihw(const csu_conv_geom* g, int dtype, const void* x, const void* dy, int c_real, float* dw_db,
                           void* workspace, size_t ws_bytes, void* stream);
+/* Weight gradient with an explicit kernel choice: c_real 0 = csu_conv2d_wgrad's [N][KH][KW][C]
+ * layout, > 0 = csu_conv2d_wgrad_oihw's.  cfg -1: the per-shape choice of the plain entries; 0: the
+ * register-staged v2 kernel; 1 + k: the LDS-DMA kernel (bf16, C % 8 == 0, N % 8 == 0) in tile
+ * configuration k (0: 128x128 3-stage, 1: 64x256 3-stage, 2: 128x128 2-stage, 3: 256x128 2-stage 8
+ * waves, 4: 64x128 4-stage).  Its workspace: csu_conv2d_wgrad_workspace_ex(g, cfg) (0 when not
+ * eligible). */
+size_t csu_conv2d_wgrad_workspace_ex(const csu_conv_geom* g, int cfg);
+int csu_conv2d_wgrad_ex(const csu_conv_geom* g, int dtype, const void* x, const void* dy, int c_real, float* dw_db,
+                        void* workspace, size_t ws_bytes, int cfg, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * Step glue (csrc/glue.hip), the elementwise passes between the kernels above:

@@ -571,6 +571,86 @@ def test_conv2d_nhwc_vs_torch(case, dtype):
     assert_close(bd.grad, b64.grad, dtype)
 
 
+# persistent LDS-DMA implicit GEMM (csu_conv2d_ex cfg 1 + k): BN of each tile configuration
+IGEMM_DMA_BN = {1: 128, 2: 128, 3: 128, 4: 64, 5: 64, 6: 64, 7: 256, 8: 256, 9: 64}
+DMA_CONV_CASES = [  # (B, H, C, N, k, stride, pad): 64-channel gathers, partial M tiles
+    (1, 20, 64, 256, 3, 1, 1),     # UNet-like 3x3, M = 400 (partial 256-row tile), two N tiles of 128
+    (2, 9, 128, 512, 3, 2, 1),     # stride 2 on an odd size: 4 input-gradient phases of 1-4 taps
+    (1, 12, 256, 256, 2, 2, 0),    # ConvTranspose2d(k2, s2)-shaped
+    (2, 7, 64, 64, 1, 1, 0),       # 1x1
+]
+
+
+@pytest.mark.parametrize("case", DMA_CONV_CASES)
+def test_conv_igemm_dma_cfgs(case):
+    """Every tile configuration of the LDS-DMA implicit GEMM (forward and input gradient, bf16
+    operands, fp32 accumulation) vs float64 torch on the same bf16 operands; configurations whose
+    BN does not divide the output channels must refuse (CSU_E_ARG)."""
+    import ctypes
+    from csu import ops
+    from csu._lib import lib, CSU_BF16
+    d = dev()
+    B, H, C, N, k, s, p = case
+    gm = ops._conv_geom(B, H, H, C, N, k, k, s, p)
+    g = torch.Generator().manual_seed(sum(case) + 7)
+    x = torch.randn(B, H, H, C, generator=g).bfloat16()
+    w = (torch.randn(N, C, k, k, generator=g) / (C * k * k) ** 0.5).bfloat16()
+    b = torch.randn(N, generator=g)
+    dy = torch.randn(B, gm.OH, gm.OW, N, generator=g).bfloat16()
+    ref_f = torch.nn.functional.conv2d(x.double().permute(0, 3, 1, 2), w.double(), b.double(), s, p).permute(0, 2, 3, 1)
+    ref_d = torch.nn.functional.conv_transpose2d(dy.double().permute(0, 3, 1, 2), w.double(), None, s, p,
+                                                 output_padding=H - ((gm.OH - 1) * s - 2 * p + k)).permute(0, 2, 3, 1)
+    xd, dyd, bd = x.to(d), dy.to(d), b.to(d)
+    w_ohwi = w.permute(0, 2, 3, 1).contiguous().to(d)
+    w_ihwo = w.permute(1, 2, 3, 0).contiguous().to(d)
+    st = torch.cuda.current_stream().cuda_stream
+    for op, src, wt, bias, ncols, cs, ref in ((0, xd, w_ohwi, bd, N, C, ref_f), (1, dyd, w_ihwo, None, C, N, ref_d)):
+        for cfg, bn in IGEMM_DMA_BN.items():
+            out = torch.full(ref.shape, float("nan"), dtype=torch.bfloat16, device=d)
+            e = lib().csu_conv2d_ex(op, ctypes.byref(gm), CSU_BF16, src.data_ptr(), wt.data_ptr(),
+                                    bias.data_ptr() if bias is not None else None, out.data_ptr(), cfg, st)
+            if ncols % bn or cs % 64:
+                assert e != 0, (op, cfg)
+                continue
+            assert e == 0, (op, cfg, lib().csu_last_error_string())
+            torch.cuda.synchronize()
+            err = float((out.double().cpu() - ref).norm() / ref.norm())
+            assert err < 4e-3, (op, cfg, err)   # bf16 output rounding (2^-9 relative) dominates
+
+
+@pytest.mark.parametrize("case", DMA_CONV_CASES + [(2, 16, 64, 128, 3, 2, 1), (1, 70, 64, 72, 3, 1, 1), (2, 9, 32, 64, 3, 1, 1)])
+def test_conv_wgrad_cfgs(case):
+    """Weight + bias gradient by every csu_conv2d_wgrad_ex configuration (v2 and the LDS-DMA tile
+    configurations) vs float64 torch on the same bf16 operands, in both output layouts."""
+    import ctypes
+    from csu import ops
+    from csu._lib import lib, CSU_BF16
+    d = dev()
+    B, H, C, N, k, s, p = case
+    gm = ops._conv_geom(B, H, H, C, N, k, k, s, p)
+    g = torch.Generator().manual_seed(sum(case) + 11)
+    x = torch.randn(B, H, H, C, generator=g).bfloat16()
+    dy = torch.randn(B, gm.OH, gm.OW, N, generator=g).bfloat16()
+    dw = torch.nn.grad.conv2d_weight(x.double().permute(0, 3, 1, 2), (N, C, k, k), dy.double().permute(0, 3, 1, 2),
+                                     stride=s, padding=p)
+    db = dy.double().sum((0, 1, 2))
+    st = torch.cuda.current_stream().cuda_stream
+    for cfg in range(0, 6):
+        nws = lib().csu_conv2d_wgrad_workspace_ex(ctypes.byref(gm), cfg)
+        if nws == 0:
+            assert C % 8 or N % 8
+            continue
+        work = torch.empty(nws, dtype=torch.uint8, device=d)
+        for creal, ref in ((0, torch.cat([dw.permute(0, 2, 3, 1).reshape(-1), db])), (C, torch.cat([dw.reshape(-1), db]))):
+            out = torch.full((ref.numel(),), float("nan"), device=d)
+            e = lib().csu_conv2d_wgrad_ex(ctypes.byref(gm), CSU_BF16, x.to(d).data_ptr(), dy.to(d).data_ptr(), creal,
+                                          out.data_ptr(), work.data_ptr(), nws, cfg, st)
+            assert e == 0, (cfg, lib().csu_last_error_string())
+            torch.cuda.synchronize()
+            err = float((out.double().cpu() - ref).norm() / ref.norm())
+            assert err < 1e-5, (cfg, creal, err)   # fp32 accumulation of exact bf16 products
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("B,H,Cin,Cout", [(2, 8, 64, 32), (1, 5, 128, 64)])
 def test_conv_transpose2d_nhwc_vs_torch(B, H, Cin, Cout, dtype):
