@@ -472,6 +472,142 @@ __global__ __launch_bounds__(64 * WN * WK, 1) void conv_wgrad_dma(Geo g, long Mr
     }
 }
 
+// ---- bf16 weight gradient of a 3x3 / stride 1 / pad 1 conv, halo form (OW % 64 == 0, C % 64 == 0,
+// N % 64 == 0) ------------------------------------------------------------------------------------
+// dW[n][ky][kx][c] = sum_m dy[m][n] * x[m + (ky - 1, kx - 1)][c].  A step is one 64-pixel segment of
+// an output row: the dy image [64 px][NS] and, per tap row ky, ONE halo image of the 66 input pixels
+// under the segment [ox0 - 1, ox0 + 64] x 64 channels; tap kx is the halo image read from row kx on
+// (transposing fragment reads at a row offset).  The x bytes staged per step are 3 x 66 rows instead
+// of the 9 x 64 of a gathered im2col image, and the workgroup keeps the whole (NS x 64-channel x 9
+// taps) weight-gradient block in its accumulators, so dy is staged once per pixel.  Wave (nt, ct)
+// owns n rows nt*32.. and channels ct*32.. of all 9 taps (9 accumulator tiles).
+constexpr int kHaloRows = 72;   // 66 halo rows padded to whole 1-KB DMA blocks (9 per image)
+
+template <int RB>
+__device__ __forceinline__ bf16x8 trfrag_at(const bf16* img, int row0, int c0, int s, int lane) {
+    const int grp = lane >> 4, l = lane & 15, q = l >> 2, p = l & 3;
+    const int col = c0 + 16 * (grp & 1) + 4 * p;
+    const int row = row0 + 16 * s + 8 * (grp >> 1) + q;
+    return cat8(tr4(img + moff<RB>(row, col)), tr4(img + moff<RB>(row + 4, col)));
+}
+
+template <int NS, int S>
+__global__ __launch_bounds__(64 * NS / 16, 1) void conv3_wgrad_halo(Geo g, long nseg, long spc, const bf16* __restrict__ x,
+                                                                    const bf16* __restrict__ dy, float* __restrict__ part) {
+    constexpr int NTW = NS / 32;                    // n tiles
+    constexpr int NWV = NTW * 2;                    // waves: n tile x channel half
+    constexpr int RBD = NS * 2;                     // dy image row bytes
+    constexpr int XIMG = kHaloRows * 64;            // bf16 per halo image
+    constexpr int DIMG = 64 * NS;                   // bf16 per dy image
+    constexpr int XBLK = XIMG * 2 / 1024;           // 1-KB DMA blocks per halo image (9)
+    constexpr int NBLK = 3 * XBLK + DIMG * 2 / 1024;
+    constexpr int NI = (NBLK + NWV - 1) / NWV;      // DMA instructions per wave per step
+    constexpr int STAGE = NI * NWV * 512;           // bf16 per stage (spare blocks included)
+    constexpr int P = S - 1;
+    static_assert((P - 1) * NI <= 63, "conv3_wgrad_halo ring");
+    __shared__ __attribute__((aligned(1024))) bf16 smem[S * STAGE];
+    const int n0 = blockIdx.x * NS, c0 = blockIdx.y * 64;
+    const long sb = (long)blockIdx.z * spc, se = min(nseg, sb + spc);
+    const int nsteps = (int)(se - sb);
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int h = lane >> 5;
+    const int nt = wave % NTW, ct = wave / NTW;
+    const bool do_bias = blockIdx.y == 0 && ct == 0;
+    const int spr = g.OW / 64;                      // segments per output row
+    // per instruction: the lane's image row and channel / n column (block-aligned regions: the
+    // region -- halo image ky or the dy image -- is uniform per instruction)
+    int irow[NI], icol[NI];
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+        const int j = wave * NI + i;
+        if (j < 3 * XBLK) {
+            const int row = (j % XBLK) * 8 + (lane >> 3);
+            irow[i] = row;
+            icol[i] = 8 * ((lane & 7) ^ mkey<128>(row));
+        } else {
+            const int q = (j - 3 * XBLK) * 1024 + lane * 16;
+            const int row = q / RBD;
+            irow[i] = row;
+            icol[i] = 8 * (((q % RBD) >> 4) ^ mkey<RBD>(row));
+        }
+    }
+    const i32x4 rsX = rsrc4(x, (long)g.B * g.H * g.W * g.C * 2);
+    const i32x4 rsD = rsrc4(dy, (long)g.B * g.OH * g.OW * g.N * 2);
+    auto issue = [&](int u) {   // segment sb + u (past the chunk: every offset out of range, zeros)
+        const long seg = sb + u;
+        const bool sv = seg < se;
+        const unsigned su = (unsigned)(sv ? seg : 0);   // < 2^31 / 64 (check_geo)
+        const unsigned trow = su / (unsigned)spr, b = trow / (unsigned)g.OH;
+        const int ox0 = (int)(su - trow * (unsigned)spr) * 64, oy = (int)(trow - b * (unsigned)g.OH);
+        bf16* stg = smem + (u % S) * STAGE;
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+            const int j = wave * NI + i;
+            unsigned off = kOOB;
+            if (j < 3 * XBLK) {
+                const int iy = oy + j / XBLK - 1, ix = ox0 - 1 + irow[i];
+                const bool ok = sv && irow[i] < 66 && iy >= 0 && iy < g.H && ix >= 0 && ix < g.W;
+                if (ok) off = (unsigned)(((((int)b * g.H + iy) * g.W + ix) * g.C + c0 + icol[i]) * 2);
+                unsigned v[1] = {off};
+                dma<1>(rsX, v, 0u, stg + j * 512, 0);
+            } else {
+                if (sv && j < NBLK)
+                    off = (unsigned)((((((int)b * g.OH + oy) * g.OW + ox0 + irow[i]) * g.N) + n0 + icol[i]) * 2);
+                unsigned v[1] = {off};
+                dma<1>(rsD, v, 0u, stg + j * 512, 0);
+            }
+        }
+    };
+    f32x16 acc[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) acc[t] = f32x16{};
+    float bsum = 0.f;
+    auto mma = [&](int u) {
+        const bf16* st = smem + (u % S) * STAGE;
+        const bf16* dimg = st + 3 * XIMG;
+#pragma unroll
+        for (int s2 = 0; s2 < 4; ++s2) {
+            const bf16x8 a = trfrag<RBD>(dimg, nt * 32, s2, lane);
+#pragma unroll
+            for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+                for (int kx = 0; kx < 3; ++kx)
+                    acc[ky * 3 + kx] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                        a, trfrag_at<128>(st + ky * XIMG, kx, ct * 32, s2, lane), acc[ky * 3 + kx], 0, 0, 0);
+            if (do_bias)
+#pragma unroll
+                for (int e = 0; e < 8; ++e) bsum += (float)a[e];
+        }
+    };
+#pragma unroll
+    for (int p = 0; p < P; ++p) issue(p);
+    for (int u = 0; u < nsteps; ++u) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        vmwait<(P - 1) * NI>();
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        issue(u + P);
+        mma(u);
+    }
+    vmwait<0>();
+    const long K = 9L * g.C;
+    const long slab = ((long)g.N * K + g.N + 3) & ~3L;
+    float* out = part + (long)blockIdx.z * slab;
+    const int c = c0 + ct * 32 + (lane & 31);
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int reg = 0; reg < 16; ++reg) {
+            const int n = n0 + nt * 32 + crow(reg, h);
+            out[(long)n * K + t * g.C + c] = acc[t][reg];
+        }
+    if (do_bias) {
+        const float v = bsum + __shfl_xor(bsum, 32, 64);
+        if (h == 0) out[(long)g.N * K + n0 + nt * 32 + (lane & 31)] = v;
+    }
+}
+
 struct WDCfg { int tn, tk, s, wn, wk; };
 constexpr WDCfg kWDCfgs[] = {{128, 128, 3, 2, 2}, {64, 256, 3, 1, 4}, {128, 128, 2, 2, 2}, {256, 128, 2, 4, 2}, {64, 128, 4, 1, 4}};
 constexpr int kWDNCfg = 5;
@@ -889,8 +1025,9 @@ int id_launch(const IG& g, const void* src, const void* w, const float* bias, vo
 // profiles/r03q_conv_probe.txt): 256 x 256 tiles (MFMA busy 38-41 % at C >= 256) when they still give
 // every CU a tile, else 256 x 128 (25-30 %); Ncols = 64 stays on the v2 kernel, which the 64-wide v3
 // tiles do not beat (the A gathers dominate: 9 taps x 64 channels per 64 outputs).  -1: v2.
+bool id_eligible(const IG& g) { return g.Cs % 64 == 0 && g.Kd >= 64 && g.Ncols <= kIDMaxN; }
 int id_pick(const IG& g) {
-    if (g.Cs % 64 || g.Kd < 64 || g.Ncols > kIDMaxN) return -1;
+    if (!id_eligible(g)) return -1;
     const long mt = (g.M + 255) / 256;
     if (g.Ncols % 256 == 0 && mt * (g.Ncols / 256) >= id_cus()) return 7;
     if (g.Ncols % 128 == 0) return 2;
@@ -926,15 +1063,24 @@ int launch_ig(const IG* gv, int n, const void* src, const void* w, const float* 
     if ((long)g.B * g.Hs * g.Ws * g.Cs * 2 >= (1L << 31) || (long)g.Ncols * g.ldw * 2 >= (1L << 31) ||
         (long)g.B * g.OHo * g.OWo * g.Ncols * 2 >= (1L << 31))
         return fail(CSU_E_UNSUPPORTED, "conv2d: operand larger than 2 GiB (32-bit buffer offsets)");
-    if (cfg != 0) {   // v3: every phase must be eligible (64-channel slices, BN | Ncols)
-        int pick = cfg > 0 ? cfg - 1 : id_pick(g);
-        for (int i = 0; i < n && pick >= 0; ++i)
-            if (id_pick(gv[i]) < 0 || (cfg > 0 && gv[i].Ncols % kIDCfgs[pick].bn)) pick = -1;
-        if (cfg > 0 && (cfg - 1 >= kIDNCfg || pick < 0)) return fail(CSU_E_ARG, "conv2d: igemm_dma configuration not eligible");
-        if (pick >= 0) {
+    if (cfg > 0) {   // forced v3 configuration: every phase must be eligible for it
+        const int k = cfg - 1;
+        if (k >= kIDNCfg) return fail(CSU_E_ARG, "conv2d: bad igemm_dma configuration");
+        for (int i = 0; i < n; ++i)
+            if (!id_eligible(gv[i]) || gv[i].Ncols % kIDCfgs[k].bn) return fail(CSU_E_ARG, "conv2d: igemm_dma configuration not eligible");
+        for (int i = 0; i < n; ++i)
+            if (gv[i].M > 0)
+                if (int e = id_run(k, gv[i], src, w, bias, out, st)) return e;
+        return 0;
+    }
+    if (cfg < 0) {   // per-shape choice: v3 (each phase its own tile) when every phase has one
+        int pk[4];
+        bool all = true;
+        for (int i = 0; i < n; ++i) all = all && (pk[i] = id_pick(gv[i])) >= 0;
+        if (all) {
             for (int i = 0; i < n; ++i)
                 if (gv[i].M > 0)
-                    if (int e = id_run(pick, gv[i], src, w, bias, out, st)) return e;
+                    if (int e = id_run(pk[i], gv[i], src, w, bias, out, st)) return e;
             return 0;
         }
     }
@@ -1061,21 +1207,62 @@ WPl wplan_dma(long M, int N, int K, const WDCfg& c) {
     return p;
 }
 
-// weight-gradient kernel of a geometry: -1 the v2 kernel, else a kWDCfgs index (cfg: -1 auto, 0 v2,
-// 1 + k forced; -2 when a forced v3 configuration is not eligible)
+// halo plan (picks kHalo64 / kHalo128): 64-pixel segments per chunk, ~2 workgroup rounds
+constexpr int kHalo64 = kWDNCfg, kHalo128 = kWDNCfg + 1;
+bool halo_ok(const csu_conv_geom* gm, int ns) {
+    return gm->KH == 3 && gm->KW == 3 && gm->stride == 1 && gm->pad == 1 && gm->OW % 64 == 0 && gm->C % 64 == 0 &&
+           gm->N % ns == 0;
+}
+WPl wplan_halo(const csu_conv_geom* gm, int ns) {
+    const long nseg = (long)gm->B * gm->OH * (gm->OW / 64);
+    const long tiles = (long)(gm->N / ns) * (gm->C / 64);
+    long want = (2L * id_cus() + tiles - 1) / tiles;
+    const long maxc = (nseg + 15) / 16;
+    if (want > maxc) want = maxc;
+    if (want > 1024) want = 1024;
+    if (want < 1) want = 1;
+    WPl p;
+    p.rpc = (nseg + want - 1) / want;
+    p.chunks = (int)((nseg + p.rpc - 1) / p.rpc);
+    return p;
+}
+WPl wplan_any(const csu_conv_geom* gm, int pick) {
+    const long M = (long)gm->B * gm->OH * gm->OW;
+    const int K = gm->KH * gm->KW * gm->C;
+    if (pick == kHalo64) return wplan_halo(gm, 64);
+    if (pick == kHalo128) return wplan_halo(gm, 128);
+    return pick >= 0 ? wplan_dma(M, gm->N, K, kWDCfgs[pick]) : wplan(M, gm->N, K);
+}
+
+// weight-gradient kernel of a geometry: -1 the v2 kernel, else a kWDCfgs index or kHalo64 /
+// kHalo128 (cfg: -1 auto, 0 v2, 1 + k forced; -2 when a forced configuration is not eligible)
 int wd_pick(const csu_conv_geom* gm, int dtype, int cfg) {
     const bool ok = dtype == CSU_BF16 && gm->C % 8 == 0 && gm->N % 8 == 0 &&
                     (long)gm->B * gm->H * gm->W * gm->C * 2 < (1L << 31) && (long)gm->B * gm->OH * gm->OW * gm->N * 2 < (1L << 31);
     if (cfg == 0) return -1;
-    if (cfg > 0) return ok && cfg - 1 < kWDNCfg ? cfg - 1 : -2;
+    if (cfg > 0) {
+        const int k = cfg - 1;
+        if (!ok || k > kHalo128) return -2;
+        if (k == kHalo64 && !halo_ok(gm, 64)) return -2;
+        if (k == kHalo128 && !halo_ok(gm, 128)) return -2;
+        return k;
+    }
     if (!ok) return -1;
-    return gm->N >= 128 ? 0 : 1;
+    // tools/conv_wgrad_probe.py (profiles/r03r_wgrad_probe.txt, r03t_wgrad_probe.txt): the halo kernel
+    // for the 3x3 stride-1 convs it takes (MFMA busy 31-34 % with 128 output channels per workgroup,
+    // 20 % with 64, against 9-17 % for v2); otherwise the 8-wave 256 x 128 tile at N >= 256 (24-26 %),
+    // the 2-stage 128 x 128 tile at N = 128 with C <= 64 (the ConvTranspose2d gradients); v2 for the
+    // rest (64 output channels: both staged operands too narrow for the gathered DMA tiles)
+    if (halo_ok(gm, 128)) return kHalo128;
+    if (halo_ok(gm, 64)) return kHalo64;
+    if (gm->N >= 256 && gm->N % 128 == 0) return 3;
+    if (gm->N == 128 && gm->C <= 64) return 2;
+    return -1;
 }
 
 size_t wgrad_ws(const csu_conv_geom* gm, int pick) {
-    const long M = (long)gm->B * gm->OH * gm->OW;
     const int K = gm->KH * gm->KW * gm->C;
-    const WPl p = pick >= 0 ? wplan_dma(M, gm->N, K, kWDCfgs[pick]) : wplan(M, gm->N, K);
+    const WPl p = wplan_any(gm, pick);
     const long slab = ((long)gm->N * K + gm->N + 3) & ~3L;
     const size_t stage = slab != (long)gm->N * K + gm->N ? slab * sizeof(float) : 0;   // padded colsum output
     return (size_t)p.chunks * slab * sizeof(float) + stage + colsum_workspace(p.chunks, slab, CSU_F32);
@@ -1090,6 +1277,16 @@ void wd_launch(const Geo& g, long M, int N, int K, const WPl& p, const void* x, 
 }
 void wd_run(int pick, const Geo& g, long M, int N, int K, const WPl& p, const void* x, const void* dy, float* part,
             hipStream_t st) {
+    if (pick == kHalo64 || pick == kHalo128) {
+        const long nseg = (long)g.B * g.OH * (g.OW / 64);
+        const int ns = pick == kHalo64 ? 64 : 128;
+        const dim3 grid(N / ns, g.C / 64, p.chunks);
+        if (ns == 64)
+            conv3_wgrad_halo<64, 3><<<grid, 256, 0, st>>>(g, nseg, p.rpc, (const bf16*)x, (const bf16*)dy, part);
+        else
+            conv3_wgrad_halo<128, 2><<<grid, 512, 0, st>>>(g, nseg, p.rpc, (const bf16*)x, (const bf16*)dy, part);
+        return;
+    }
     switch (pick) {
         case 0: wd_launch<0>(g, M, N, K, p, x, dy, part, st); break;
         case 1: wd_launch<1>(g, M, N, K, p, x, dy, part, st); break;
@@ -1205,7 +1402,7 @@ static int conv_wgrad_impl(const csu_conv_geom* gm, int dtype, const void* x, co
     const Geo g = to_geo(gm);
     const long M = (long)g.B * g.OH * g.OW;
     const int K = g.KH * g.KW * g.C;
-    const WPl p = pick >= 0 ? wplan_dma(M, g.N, K, kWDCfgs[pick]) : wplan(M, g.N, K);
+    const WPl p = wplan_any(gm, pick);
     const long used = (long)g.N * K + g.N;
     const long slab = (used + 3) & ~3L;
     float* part = (float*)workspace;

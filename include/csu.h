@@ -502,7 +502,8 @@ int csu_conv2d_wgrad_oihw(const csu_conv_geom* g, int dtype, const void* x, cons
  * layout, > 0 = csu_conv2d_wgrad_oihw's.  cfg -1: the per-shape choice of the plain entries; 0: the
  * register-staged v2 kernel; 1 + k: the LDS-DMA kernel (bf16, C % 8 == 0, N % 8 == 0) in tile
  * configuration k (0: 128x128 3-stage, 1: 64x256 3-stage, 2: 128x128 2-stage, 3: 256x128 2-stage 8
- * waves, 4: 64x128 4-stage).  Its workspace: csu_conv2d_wgrad_workspace_ex(g, cfg) (0 when not
+ * waves, 4: 64x128 4-stage; 5 / 6: the halo kernel of 3x3 / stride 1 / pad 1 convs with OW % 64 == 0,
+ * C % 64 == 0 and N % 64 (5) / N % 128 (6) == 0).  Its workspace: csu_conv2d_wgrad_workspace_ex(g, cfg) (0 when not
  * eligible). */
 size_t csu_conv2d_wgrad_workspace_ex(const csu_conv_geom* g, int cfg);
 int csu_conv2d_wgrad_ex(const csu_conv_geom* g, int dtype, const void* x, const void* dy, int c_real, float* dw_db,

@@ -618,7 +618,8 @@ def test_conv_igemm_dma_cfgs(case):
             assert err < 4e-3, (op, cfg, err)   # bf16 output rounding (2^-9 relative) dominates
 
 
-@pytest.mark.parametrize("case", DMA_CONV_CASES + [(2, 16, 64, 128, 3, 2, 1), (1, 70, 64, 72, 3, 1, 1), (2, 9, 32, 64, 3, 1, 1)])
+@pytest.mark.parametrize("case", DMA_CONV_CASES + [(2, 16, 64, 128, 3, 2, 1), (1, 70, 64, 72, 3, 1, 1), (2, 9, 32, 64, 3, 1, 1),
+                                  (1, 64, 64, 128, 3, 1, 1), (2, 64, 128, 64, 3, 1, 1)])   # halo-eligible (OW % 64 == 0)
 def test_conv_wgrad_cfgs(case):
     """Weight + bias gradient by every csu_conv2d_wgrad_ex configuration (v2 and the LDS-DMA tile
     configurations) vs float64 torch on the same bf16 operands, in both output layouts."""
@@ -634,16 +635,18 @@ def test_conv_wgrad_cfgs(case):
     dw = torch.nn.grad.conv2d_weight(x.double().permute(0, 3, 1, 2), (N, C, k, k), dy.double().permute(0, 3, 1, 2),
                                      stride=s, padding=p)
     db = dy.double().sum((0, 1, 2))
+    xd, dyd = x.to(d), dy.to(d)   # kept alive across the asynchronous calls
     st = torch.cuda.current_stream().cuda_stream
-    for cfg in range(0, 6):
+    halo = k == 3 and s == 1 and p == 1 and H % 64 == 0 and C % 64 == 0
+    for cfg in range(0, 8):
         nws = lib().csu_conv2d_wgrad_workspace_ex(ctypes.byref(gm), cfg)
         if nws == 0:
-            assert C % 8 or N % 8
+            assert C % 8 or N % 8 or (cfg == 6 and not (halo and N % 64 == 0)) or (cfg == 7 and not (halo and N % 128 == 0))
             continue
         work = torch.empty(nws, dtype=torch.uint8, device=d)
         for creal, ref in ((0, torch.cat([dw.permute(0, 2, 3, 1).reshape(-1), db])), (C, torch.cat([dw.reshape(-1), db]))):
             out = torch.full((ref.numel(),), float("nan"), device=d)
-            e = lib().csu_conv2d_wgrad_ex(ctypes.byref(gm), CSU_BF16, x.to(d).data_ptr(), dy.to(d).data_ptr(), creal,
+            e = lib().csu_conv2d_wgrad_ex(ctypes.byref(gm), CSU_BF16, xd.data_ptr(), dyd.data_ptr(), creal,
                                           out.data_ptr(), work.data_ptr(), nws, cfg, st)
             assert e == 0, (cfg, lib().csu_last_error_string())
             torch.cuda.synchronize()
