@@ -493,6 +493,7 @@ __device__ __forceinline__ bf16x8 trfrag_at(const bf16* img, int row0, int c0, i
 
 template <int NS, int S>
 __global__ __launch_bounds__(64 * NS / 16, 1) void conv3_wgrad_halo(Geo g, long nseg, long spc, const bf16* __restrict__ x,
+                                                                    const bf16* __restrict__ x2, int csplit,
                                                                     const bf16* __restrict__ dy, float* __restrict__ part) {
     constexpr int NTW = NS / 32;                    // n tiles
     constexpr int NWV = NTW * 2;                    // waves: n tile x channel half
@@ -532,7 +533,10 @@ __global__ __launch_bounds__(64 * NS / 16, 1) void conv3_wgrad_halo(Geo g, long 
             icol[i] = 8 * (((q % RBD) >> 4) ^ mkey<RBD>(row));
         }
     }
-    const i32x4 rsX = rsrc4(x, (long)g.B * g.H * g.W * g.C * 2);
+    // two sources (csplit > 0, % 64): this workgroup's 64-channel slice lies in one of them
+    const bool sec = csplit > 0 && c0 >= csplit;
+    const int xst = csplit ? (sec ? g.C - csplit : csplit) : g.C, xc0 = sec ? c0 - csplit : c0;
+    const i32x4 rsX = sec ? rsrc4(x2, (long)g.B * g.H * g.W * xst * 2) : rsrc4(x, (long)g.B * g.H * g.W * xst * 2);
     const i32x4 rsD = rsrc4(dy, (long)g.B * g.OH * g.OW * g.N * 2);
     auto issue = [&](int u) {   // segment sb + u (past the chunk: every offset out of range, zeros)
         const long seg = sb + u;
@@ -548,7 +552,7 @@ __global__ __launch_bounds__(64 * NS / 16, 1) void conv3_wgrad_halo(Geo g, long 
             if (j < 3 * XBLK) {
                 const int iy = oy + j / XBLK - 1, ix = ox0 - 1 + irow[i];
                 const bool ok = sv && irow[i] < 66 && iy >= 0 && iy < g.H && ix >= 0 && ix < g.W;
-                if (ok) off = (unsigned)(((((int)b * g.H + iy) * g.W + ix) * g.C + c0 + icol[i]) * 2);
+                if (ok) off = (unsigned)(((((int)b * g.H + iy) * g.W + ix) * xst + xc0 + icol[i]) * 2);
                 unsigned v[1] = {off};
                 dma<1>(rsX, v, 0u, stg + j * 512, 0);
             } else {
@@ -627,7 +631,33 @@ struct IG {
     int OHo, OWo, oya, oyb, oxa, oxb;
     int B, Ncols, Kd;
     long M;
+    // two-source gathers / two-destination outputs (the channel concat of UNet Up, unet:213-216,
+    // without materialising it): channels [0, csplit) of the gathered operand come from src
+    // (csplit per pixel), [csplit, Cs) from src2 (Cs - csplit per pixel); output columns [0, nsplit)
+    // go to out (nsplit per pixel), [nsplit, Ncols) to out2.  0: one source / one output.
+    int csplit, nsplit;
+    const bf16* src2;
+    bf16* out2;
 };
+
+// gathered-channel slice c0 (64-aligned, one tap): the source holding it, its channel stride and the
+// channel inside it
+struct CSel {
+    bool second;
+    int stride, c;
+};
+__device__ __forceinline__ CSel csel(const IG& g, int c0) {
+    if (g.csplit == 0) return CSel{false, g.Cs, c0};
+    const bool sec = c0 >= g.csplit;
+    return CSel{sec, sec ? g.Cs - g.csplit : g.csplit, sec ? c0 - g.csplit : c0};
+}
+// output byte offset of column n of output pixel opix (out or out2), kOOB passes through
+__device__ __forceinline__ unsigned obyte(const IG& g, unsigned opix, int n) {
+    if (opix == kOOB) return kOOB;
+    if (g.nsplit == 0) return (opix * (unsigned)g.Ncols + (unsigned)n) * 2u;
+    return n < g.nsplit ? (opix * (unsigned)g.nsplit + (unsigned)n) * 2u
+                        : (opix * (unsigned)(g.Ncols - g.nsplit) + (unsigned)(n - g.nsplit)) * 2u;
+}
 
 __device__ __forceinline__ int swz128(int row, int chunk) { return row * 64 + ((chunk ^ (row & 7)) << 3); }
 
@@ -645,7 +675,7 @@ __global__ __launch_bounds__(NT) void igemm_bf16(IG4 gs, const bf16* __restrict_
     constexpr int ACH = BM * 8 / NT, BCH = BN * 8 / NT, NP = 8 / VW;
     __shared__ __attribute__((aligned(16))) bf16 As[2][BM * BK];
     __shared__ __attribute__((aligned(16))) bf16 Bs[2][BN * BK];
-    __shared__ unsigned ooff[BM];   // byte offset of each tile row's output pixel (kOOB: none)
+    __shared__ unsigned ooff[BM];   // output pixel of each tile row (kOOB: none)
     // problem of this z-slice (selects, not a dynamic index into the kernel-argument struct)
     const int z = blockIdx.z;
     const IG g = z == 0 ? gs.g[0] : z == 1 ? gs.g[1] : z == 2 ? gs.g[2] : gs.g[3];
@@ -683,9 +713,15 @@ __global__ __launch_bounds__(NT) void igemm_bf16(IG4 gs, const bf16* __restrict_
     // branch-free gathers: raw buffer loads whose out-of-image / out-of-range lanes get an offset
     // past the resource (read as 0), so hipcc keeps every load of a slice in flight (a predicated
     // load makes it wait vmcnt(0) at the join and the register prefetch is lost)
-    const __amdgpu_buffer_rsrc_t rs_src = buf_rsrc(src, (long)g.B * g.Hs * g.Ws * g.Cs * 2);
+    const int cs1 = g.csplit ? g.csplit : g.Cs;
+    const __amdgpu_buffer_rsrc_t rs_src = buf_rsrc(src, (long)g.B * g.Hs * g.Ws * cs1 * 2);
+    const __amdgpu_buffer_rsrc_t rs_src2 = buf_rsrc(g.src2, g.csplit ? (long)g.B * g.Hs * g.Ws * (g.Cs - g.csplit) * 2 : 0);
     const __amdgpu_buffer_rsrc_t rs_w = buf_rsrc(Bw, (long)g.Ncols * g.ldw * 2);
     auto load = [&](int k0, bf16x8* ra, bf16x8* rbw) {
+        // two sources (csplit % 64 == 0, Cs % 64 == 0): the slice's side is uniform
+        const CSel sl = csel(g, k0 % g.Cs);
+        const int cadj = g.csplit && sl.second ? g.csplit : 0;
+        const __amdgpu_buffer_rsrc_t rs_a = sl.second ? rs_src2 : rs_src;
 #pragma unroll
         for (int pc = 0; pc < NP; ++pc) {
             const int k = k0 + 8 * ch + VW * pc;
@@ -698,12 +734,12 @@ __global__ __launch_bounds__(NT) void igemm_bf16(IG4 gs, const bf16* __restrict_
             for (int i = 0; i < ACH; ++i) {
                 const int y = ryb[i] + oy, x = rxb[i] + ox;
                 const bool ok = kin && y >= 0 && y < g.Hs && x >= 0 && x < g.Ws;
-                const unsigned off = ok ? (unsigned)((((rb[i] + y) * g.Ws + x) * g.Cs + c) * 2) : kOOB;
+                const unsigned off = ok ? (unsigned)((((rb[i] + y) * g.Ws + x) * sl.stride + c - cadj) * 2) : kOOB;
                 if constexpr (VW == 8) {
-                    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs_src, off, 0, 0);
+                    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs_a, off, 0, 0);
                     __builtin_memcpy(&ra[i], &v, 16);
                 } else {
-                    const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(rs_src, off, 0, 0);
+                    const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(rs_a, off, 0, 0);
                     bf16x4 b;
                     __builtin_memcpy(&b, &v, 8);
 #pragma unroll
@@ -774,25 +810,30 @@ __global__ __launch_bounds__(NT) void igemm_bf16(IG4 gs, const bf16* __restrict_
             const int rx = (int)(mu - t * (unsigned)g.RW);
             const unsigned b = t / (unsigned)g.RH;
             const int ry = (int)(t - b * (unsigned)g.RH);
-            o = (unsigned)((((int)b * g.OHo + ry * g.oya + g.oyb) * g.OWo + rx * g.oxa + g.oxb) * g.Ncols) * 2u;
+            o = (unsigned)(((int)b * g.OHo + ry * g.oya + g.oyb) * g.OWo + rx * g.oxa + g.oxb);
         }
-        ooff[i] = o;
+        ooff[i] = o;   // output pixel index (obyte maps it to out / out2)
     }
     __syncthreads();
     // branch-free epilogue: raw buffer stores, rows outside the problem / columns past N dropped by
-    // the out-of-range offset
+    // the out-of-range offset.  acc[i][reg] = D[pixel wm + 32i + crow(reg, h)][feature wn + r]: per
+    // store instruction 32 consecutive features of 2 rows (64-B segments).  Measured faster here than
+    // 8-B feature-quad stores or an LDS-staged row-contiguous tile (profiles/r03v_conv_probe*.txt).
     const int n = n0 + wn + r;
     const bool nv = n < g.Ncols;
     const float bv = (bias && nv) ? bias[n] : 0.f;
-    const __amdgpu_buffer_rsrc_t rs_o = buf_rsrc(out, (long)g.B * g.OHo * g.OWo * g.Ncols * 2);
+    const long npix = (long)g.B * g.OHo * g.OWo;
+    const __amdgpu_buffer_rsrc_t rs_o = buf_rsrc(out, npix * (g.nsplit ? g.nsplit : g.Ncols) * 2);
+    const __amdgpu_buffer_rsrc_t rs_o2 = buf_rsrc(g.out2, g.nsplit ? npix * (g.Ncols - g.nsplit) * 2 : 0);
+    const bool sec = g.nsplit && n >= g.nsplit;   // lanes may straddle nsplit: one store per destination
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int reg = 0; reg < 16; ++reg) {
-            const unsigned o = ooff[wm + 32 * i + crow(reg, h)];
-            const unsigned off = (o != kOOB && nv) ? o + 2u * (unsigned)n : kOOB;
-            const bf16 v = (bf16)(acc[i][reg] + bv);
-            __builtin_amdgcn_raw_buffer_store_b16(__builtin_bit_cast(unsigned short, v), rs_o, off, 0, 0);
+            const unsigned off = nv ? obyte(g, ooff[wm + 32 * i + crow(reg, h)], n) : kOOB;
+            const unsigned short v = __builtin_bit_cast(unsigned short, (bf16)(acc[i][reg] + bv));
+            __builtin_amdgcn_raw_buffer_store_b16(v, rs_o, sec ? kOOB : off, 0, 0);
+            if (g.nsplit) __builtin_amdgcn_raw_buffer_store_b16(v, rs_o2, sec ? off : kOOB, 0, 0);
         }
 }
 
@@ -873,7 +914,8 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void igemm_dma(IG g, const bf16* _
             arx[i] = rx * g.ax + g.bx;
         }
     };
-    const i32x4 rsA = rsrc4(src, (long)g.B * g.Hs * g.Ws * g.Cs * 2);
+    const i32x4 rsA = rsrc4(src, (long)g.B * g.Hs * g.Ws * (g.csplit ? g.csplit : g.Cs) * 2);
+    const i32x4 rsA2 = rsrc4(g.src2, g.csplit ? (long)g.B * g.Hs * g.Ws * (g.Cs - g.csplit) * 2 : 0);
     auto issue = [&](int u) {   // DMA of unit min(u, U - 1) into stage u % S
         const int uu = u < U ? u : U - 1;
         const unsigned tile = lo + kk + (unsigned)(uu / nk) * nloc;
@@ -886,15 +928,16 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void igemm_dma(IG g, const bf16* _
         const int ty = t / g.ntx, tx = t - ty * g.ntx;
         const int oy = ty * g.sty, ox = tx * g.stx;
         const int wcol = ((ty * g.wty + g.w0y) * g.KWf + tx * g.wtx + g.w0x) * g.Cs + c0;
+        const CSel sl = csel(g, c0);
         unsigned va[NA];
 #pragma unroll
         for (int i = 0; i < NA; ++i) {
             const int y = ary[i] + oy, xx = arx[i] + ox;
             const bool ok = y >= 0 && y < g.Hs && xx >= 0 && xx < g.Ws;
-            va[i] = ok ? (unsigned)((((arb[i] + y) * g.Ws + xx) * g.Cs + c0) * 2) + achan[i] : kOOB;
+            va[i] = ok ? (unsigned)((((arb[i] + y) * g.Ws + xx) * sl.stride + sl.c) * 2) + achan[i] : kOOB;
         }
         bf16* stg = smem + (u % S) * STAGE;
-        dma<NA>(rsA, va, 0u, stg, wave);
+        dma<NA>(sl.second ? rsA2 : rsA, va, 0u, stg, wave);
         const long rw = (long)(tile % nbn) * BN;
         dma<NB>(rsrc4(Bw + rw * g.ldw, (long)(g.Ncols - rw) * g.ldw * 2), voffW, (unsigned)wcol * 2u, stg + BM * BK, wave);
     };
@@ -942,7 +985,9 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void igemm_dma(IG g, const bf16* _
                     acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[s & 1][j], af[s & 1][i], acc[i][j], 0, 0, 0);
         }
     };
-    const __amdgpu_buffer_rsrc_t rs_o = buf_rsrc(out, (long)g.B * g.OHo * g.OWo * g.Ncols * 2);
+    const long npix = (long)g.B * g.OHo * g.OWo;
+    const __amdgpu_buffer_rsrc_t rs_o = buf_rsrc(out, npix * (g.nsplit ? g.nsplit : g.Ncols) * 2);
+    const __amdgpu_buffer_rsrc_t rs_o2 = buf_rsrc(g.out2, g.nsplit ? npix * (g.Ncols - g.nsplit) * 2 : 0);
 
 #pragma unroll
     for (int p = 0; p < P; ++p) issue(p);
@@ -957,7 +1002,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void igemm_dma(IG g, const bf16* _
         const unsigned tile = lo + kk + (unsigned)t * nloc;
         const long m0 = (long)(tile / nbn) * BM;
         const int n0 = (int)(tile % nbn) * BN;
-        unsigned orow[TMW];   // byte offset of the output pixel of rows wm + 32 i + r (kOOB: none)
+        unsigned orow[TMW];   // output pixel of rows wm + 32 i + r (kOOB: none)
 #pragma unroll
         for (int i = 0; i < TMW; ++i) {
             const long m = m0 + wm + 32 * i + r;
@@ -966,7 +1011,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void igemm_dma(IG g, const bf16* _
             const int rx = (int)(mu - tq * (unsigned)g.RW);
             const unsigned b = tq / (unsigned)g.RH;
             const int ry = (int)(tq - b * (unsigned)g.RH);
-            const unsigned o = (unsigned)((((int)b * g.OHo + ry * g.oya + g.oyb) * g.OWo + rx * g.oxa + g.oxb) * g.Ncols) * 2u;
+            const unsigned o = (unsigned)(((int)b * g.OHo + ry * g.oya + g.oyb) * g.OWo + rx * g.oxa + g.oxb);
             orow[i] = mv ? o : kOOB;
         }
         issue(u + P);
@@ -978,12 +1023,12 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void igemm_dma(IG g, const bf16* _
             for (int gq = 0; gq < 4; ++gq) {
                 const int nf = n0 + wn + 32 * j + 8 * gq + 4 * h;
                 const f32x4 bv = *reinterpret_cast<const f32x4*>(sbias + nf);
-                const unsigned nb = (unsigned)nf * 2u;
+                const bool o2 = g.nsplit && n0 + wn + 32 * j + 8 * gq >= g.nsplit;   // nsplit % 8 == 0: uniform
 #pragma unroll
                 for (int i = 0; i < TMW; ++i) {
                     const float v[4] = {acc[i][j][4 * gq] + bv[0], acc[i][j][4 * gq + 1] + bv[1], acc[i][j][4 * gq + 2] + bv[2],
                                         acc[i][j][4 * gq + 3] + bv[3]};
-                    buf_st4bf(rs_o, orow[i] == kOOB ? kOOB : orow[i] + nb, v);
+                    buf_st4bf(o2 ? rs_o2 : rs_o, obyte(g, orow[i], nf), v);
                 }
             }
 #pragma unroll
@@ -1276,15 +1321,15 @@ void wd_launch(const Geo& g, long M, int N, int K, const WPl& p, const void* x, 
                                                                                  (const bf16*)dy, part);
 }
 void wd_run(int pick, const Geo& g, long M, int N, int K, const WPl& p, const void* x, const void* dy, float* part,
-            hipStream_t st) {
+            hipStream_t st, const void* x2 = nullptr, int csplit = 0) {
     if (pick == kHalo64 || pick == kHalo128) {
         const long nseg = (long)g.B * g.OH * (g.OW / 64);
         const int ns = pick == kHalo64 ? 64 : 128;
         const dim3 grid(N / ns, g.C / 64, p.chunks);
         if (ns == 64)
-            conv3_wgrad_halo<64, 3><<<grid, 256, 0, st>>>(g, nseg, p.rpc, (const bf16*)x, (const bf16*)dy, part);
+            conv3_wgrad_halo<64, 3><<<grid, 256, 0, st>>>(g, nseg, p.rpc, (const bf16*)x, (const bf16*)x2, csplit, (const bf16*)dy, part);
         else
-            conv3_wgrad_halo<128, 2><<<grid, 512, 0, st>>>(g, nseg, p.rpc, (const bf16*)x, (const bf16*)dy, part);
+            conv3_wgrad_halo<128, 2><<<grid, 512, 0, st>>>(g, nseg, p.rpc, (const bf16*)x, (const bf16*)x2, csplit, (const bf16*)dy, part);
         return;
     }
     switch (pick) {
@@ -1392,11 +1437,13 @@ extern "C" size_t csu_conv2d_wgrad_workspace_ex(const csu_conv_geom* gm, int cfg
 }
 
 static int conv_wgrad_impl(const csu_conv_geom* gm, int dtype, const void* x, const void* dy, int creal, float* dw_db,
-                           void* workspace, size_t ws_bytes, int cfg, void* stream) {
+                           void* workspace, size_t ws_bytes, int cfg, void* stream, const void* x2 = nullptr, int csplit = 0) {
     if (int e = check_geo(gm)) return e;
     if (!x || !dy || !dw_db) return fail(CSU_E_ARG, "conv2d_wgrad: null buffer");
     const int pick = wd_pick(gm, dtype, cfg);
     if (pick == -2) return fail(CSU_E_ARG, "conv2d_wgrad: configuration not eligible (bf16, C % 8 == 0, N % 8 == 0)");
+    if (csplit && pick != kHalo64 && pick != kHalo128)
+        return fail(CSU_E_UNSUPPORTED, "conv2d_wgrad: two-source input needs the halo kernel");
     if (!workspace || ws_bytes < wgrad_ws(gm, pick)) return fail(CSU_E_WORKSPACE, "conv2d_wgrad: workspace");
     if (creal > gm->C) return fail(CSU_E_ARG, "conv2d_wgrad: c_real > C");
     const Geo g = to_geo(gm);
@@ -1410,7 +1457,7 @@ static int conv_wgrad_impl(const csu_conv_geom* gm, int dtype, const void* x, co
     const bool vec = g.C % 8 == 0;
     hipStream_t st = as_stream(stream);
     if (pick >= 0) {
-        wd_run(pick, g, M, g.N, K, p, x, dy, part, st);
+        wd_run(pick, g, M, g.N, K, p, x, dy, part, st, x2, csplit);
     } else if (dtype == CSU_BF16) {
         const bool small = (long)g.B * g.H * g.W * g.C * 2 < (1L << 31) && M * g.N * 2 < (1L << 31);   // 32-bit offsets
         if (vec && g.N % 8 == 0 && small && conv_wgrad_v2())
@@ -1451,4 +1498,48 @@ extern "C" int csu_conv2d_wgrad_ex(const csu_conv_geom* gm, int dtype, const voi
                                    void* workspace, size_t ws_bytes, int cfg, void* stream) {
     if (c_real < 0) return fail(CSU_E_ARG, "conv2d_wgrad_ex: c_real < 0");
     return conv_wgrad_impl(gm, dtype, x, dy, c_real, dw_db, workspace, ws_bytes, cfg, stream);
+}
+
+// ---- two-source input (channel concat of UNet Up, unet:213-216, never materialised) -----------
+extern "C" int csu_conv2d_split_ok(const csu_conv_geom* gm, int c_split) {
+    if (check_geo(gm)) return 0;
+    return c_split > 0 && c_split < gm->C && c_split % 64 == 0 && gm->C % 64 == 0 && gm->N % 64 == 0 &&
+           (long)gm->B * gm->H * gm->W * gm->C * 2 < (1L << 31) && wd_pick(gm, CSU_BF16, -1) >= kHalo64;
+}
+
+extern "C" int csu_conv2d_fwd_split(const csu_conv_geom* gm, int dtype, const void* x, const void* x2, int c_split,
+                                    const void* w_ohwi, const float* bias, void* y, void* stream) {
+    if (int e = check_geo(gm)) return e;
+    if (dtype != CSU_BF16 || !csu_conv2d_split_ok(gm, c_split)) return fail(CSU_E_UNSUPPORTED, "conv2d_fwd_split: not eligible");
+    if (!x || !x2 || !w_ohwi || !y) return fail(CSU_E_ARG, "conv2d_fwd_split: null buffer");
+    IG g = ig_forward(*gm);
+    g.csplit = c_split;
+    g.src2 = (const bf16*)x2;
+    return launch_ig(g, x, w_ohwi, bias, y, as_stream(stream));
+}
+
+extern "C" int csu_conv2d_dgrad_split(const csu_conv_geom* gm, int dtype, const void* dy, const void* w_ihwo, void* dx, void* dx2,
+                                      int c_split, void* stream) {
+    if (int e = check_geo(gm)) return e;
+    if (dtype != CSU_BF16 || !csu_conv2d_split_ok(gm, c_split)) return fail(CSU_E_UNSUPPORTED, "conv2d_dgrad_split: not eligible");
+    if (!dy || !w_ihwo || !dx || !dx2) return fail(CSU_E_ARG, "conv2d_dgrad_split: null buffer");
+    IG ph[4];
+    int np = 0;
+    for (int py = 0; py < gm->stride; ++py)
+        for (int px = 0; px < gm->stride; ++px) {
+            IG ig = ig_dgrad_phase(*gm, py, px);
+            if (ig.M == 0) continue;
+            ig.nsplit = c_split;
+            ig.out2 = (bf16*)dx2;
+            ph[np++] = ig;
+        }
+    return np ? launch_ig(ph, np, dy, w_ihwo, nullptr, dx, as_stream(stream)) : 0;
+}
+
+extern "C" int csu_conv2d_wgrad_split_oihw(const csu_conv_geom* gm, int dtype, const void* x, const void* x2, int c_split,
+                                           const void* dy, float* dw_db, void* workspace, size_t ws_bytes, void* stream) {
+    if (int e = check_geo(gm)) return e;
+    if (dtype != CSU_BF16 || !csu_conv2d_split_ok(gm, c_split)) return fail(CSU_E_UNSUPPORTED, "conv2d_wgrad_split: not eligible");
+    if (!x2) return fail(CSU_E_ARG, "conv2d_wgrad_split: null buffer");
+    return conv_wgrad_impl(gm, dtype, x, dy, gm->C, dw_db, workspace, ws_bytes, -1, stream, x2, c_split);
 }

@@ -197,6 +197,13 @@ _SIGS = {
                                      c_void_p, ctypes.c_int, c_void_p]),
     "csu_conv2d_wgrad_workspace": (c_size_t, [ctypes.POINTER(ConvGeom)]),
     "csu_conv2d_wgrad_workspace_ex": (c_size_t, [ctypes.POINTER(ConvGeom), ctypes.c_int]),
+    "csu_conv2d_split_ok": (ctypes.c_int, [ctypes.POINTER(ConvGeom), ctypes.c_int]),
+    "csu_conv2d_fwd_split": (ctypes.c_int, [ctypes.POINTER(ConvGeom), ctypes.c_int, c_void_p, c_void_p, ctypes.c_int, c_void_p,
+                                            c_void_p, c_void_p, c_void_p]),
+    "csu_conv2d_dgrad_split": (ctypes.c_int, [ctypes.POINTER(ConvGeom), ctypes.c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                                              ctypes.c_int, c_void_p]),
+    "csu_conv2d_wgrad_split_oihw": (ctypes.c_int, [ctypes.POINTER(ConvGeom), ctypes.c_int, c_void_p, c_void_p, ctypes.c_int,
+                                                   c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
     "csu_conv2d_wgrad_ex": (ctypes.c_int, [ctypes.POINTER(ConvGeom), ctypes.c_int, c_void_p, c_void_p, ctypes.c_int,
                                            c_void_p, c_void_p, c_size_t, ctypes.c_int, c_void_p]),
     "csu_conv2d_wgrad": (ctypes.c_int, [ctypes.POINTER(ConvGeom), ctypes.c_int, c_void_p, c_void_p, c_void_p, c_void_p,

@@ -1946,6 +1946,85 @@ def conv2d(x_nhwc: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tens
         return _Conv2dFn.apply(x_nhwc, weight, bias, stride, pad, cd)
 
 
+class _CatConv2dFn(torch.autograd.Function):
+    """conv2d(cat([xa, xb], channels)) without the concatenated tensor (UNet Up, unet:213-216):
+    the gathers read input channels [0, Ca) from xa and [Ca, C) from xb, the input gradient is
+    written as (dxa, dxb), the weight gradient reads both (csu_conv2d_*_split)."""
+
+    @staticmethod
+    def forward(ctx, xa, xb, weight, bias, pad: int, cd):
+        require_device(xa, xb, weight)
+        xa, xb = xa.to(cd).contiguous(), xb.to(cd).contiguous()
+        B, H, W, Ca = xa.shape
+        N, C, KH, KW = weight.shape
+        g = _conv_geom(B, H, W, C, N, KH, KW, 1, pad)
+        cached = _ACTIVE_CACHE.get_conv(weight, cd) if _ACTIVE_CACHE is not None else None
+        w_ohwi = cached[0] if cached else weight.detach().permute(0, 2, 3, 1).to(cd).contiguous()
+        y = torch.empty(B, g.OH, g.OW, N, dtype=cd, device=xa.device)
+        bf = None if bias is None else bias.detach().float().contiguous()
+        _launch("conv_fwd", lambda: lib().csu_conv2d_fwd_split(ctypes.byref(g), dtype_code(xa), ptr(xa), ptr(xb), Ca, ptr(w_ohwi),
+                                                               ptr(bf), ptr(y), stream_ptr(xa.device)),
+                2 * y.numel() * KH * KW * C, (xa.numel() + xb.numel() + w_ohwi.numel() + y.numel()) * 2, prec=prec_of(xa))
+        ctx.save_for_backward(xa, xb, weight)
+        ctx.w_ihwo = cached[1] if cached else None
+        ctx.bias = bias
+        ctx.conf = (pad, cd, bias is not None, None if bias is None else bias.dtype)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        xa, xb, weight = ctx.saved_tensors
+        pad, cd, has_b, bdt = ctx.conf
+        B, H, W, Ca = xa.shape
+        N, C, KH, KW = weight.shape
+        g = _conv_geom(B, H, W, C, N, KH, KW, 1, pad)
+        dy = dy.to(cd).contiguous()
+        dxa = dxb = None
+        if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
+            w_ihwo = ctx.w_ihwo if ctx.w_ihwo is not None else weight.detach().permute(1, 2, 3, 0).to(cd).contiguous()
+            dxa = torch.empty_like(xa)
+            dxb = torch.empty_like(xb)
+            _launch("conv_dgrad", lambda: lib().csu_conv2d_dgrad_split(ctypes.byref(g), dtype_code(dy), ptr(dy), ptr(w_ihwo),
+                                                                       ptr(dxa), ptr(dxb), Ca, stream_ptr(dy.device)),
+                    2 * dy.numel() * KH * KW * C, (dy.numel() + w_ihwo.numel() + dxa.numel() + dxb.numel()) * 2, prec=prec_of(dy))
+
+        def wg():
+            L = lib()
+            out = torch.empty(N * KH * KW * C + N, dtype=torch.float32, device=dy.device)
+            n = L.csu_conv2d_wgrad_workspace(ctypes.byref(g))
+            work = torch.empty(max(n, 16), dtype=torch.uint8, device=dy.device)
+            _launch("conv_wgrad", lambda: L.csu_conv2d_wgrad_split_oihw(ctypes.byref(g), dtype_code(dy), ptr(xa), ptr(xb), Ca,
+                                                                        ptr(dy), ptr(out), ptr(work), n, stream_ptr(dy.device)),
+                    2 * dy.numel() * KH * KW * C, (xa.numel() + xb.numel() + dy.numel()) * 2 + out.numel() * 4, prec=prec_of(dy))
+            k = N * KH * KW * C
+            return out[:k].view(N, C, KH, KW), out[k:]
+        if _side_ok(dy, weight.dtype, bdt if has_b else None, params=(weight, ctx.bias)):
+            dw, db = _side_run(wg, xa, xb, dy)
+            return dxa, dxb, dw, (db if has_b else None), None, None
+        dw, db = wg()
+        return dxa, dxb, dw.to(weight.dtype), (db.to(bdt) if has_b else None), None, None
+
+
+def conv2d_cat(xa: torch.Tensor, xb: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor],
+               pad: int = 1) -> torch.Tensor:
+    """conv2d(torch.cat([xa, xb], -1), weight, bias, 1, pad) on channels-last tensors; the
+    concatenation is never materialised when csu_conv2d_split_ok accepts the geometry (bf16),
+    otherwise it is (and conv2d runs on it)."""
+    if xa.is_cuda and torch.is_autocast_enabled("cuda"):
+        cd = torch.get_autocast_dtype("cuda")
+    else:
+        cd = torch.promote_types(torch.promote_types(xa.dtype, xb.dtype), weight.dtype)
+    B, H, W, Ca = xa.shape
+    N, C, KH, KW = weight.shape
+    if Ca + xb.shape[-1] != C:
+        raise ValueError(f"conv2d_cat: {Ca} + {xb.shape[-1]} input channels, weight expects {C}")
+    g = _conv_geom(B, H, W, C, N, KH, KW, 1, pad)
+    if cd == torch.bfloat16 and xa.is_cuda and lib().csu_conv2d_split_ok(ctypes.byref(g), Ca):
+        with torch.autocast("cuda", enabled=False):
+            return _CatConv2dFn.apply(xa, xb, weight, bias, pad, cd)
+    return conv2d(torch.cat([xa.to(cd), xb.to(cd)], dim=-1), weight, bias, 1, pad)
+
+
 class _ConvTranspose2dFn(torch.autograd.Function):
     """ConvTranspose2d(k, stride=k, pad 0) = the input-gradient operator of the matching conv."""
 

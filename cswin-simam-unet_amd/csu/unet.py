@@ -133,9 +133,12 @@ class DoubleConv(nn.Module):
             nn.ReLU(inplace=True),
         )
 
-    def forward(self, x):
+    def forward(self, x, x_cat=None):
+        """x_cat: a second input concatenated after x on channels (Up; the concatenation is never
+        materialised when the two-source conv kernels take the geometry)."""
         c1, b1, _, c2, b2, _ = self.double_conv
-        x = bn_relu_nhwc(ops.conv2d(x, c1.weight, c1.bias, 1, 1), b1)
+        y = ops.conv2d(x, c1.weight, c1.bias, 1, 1) if x_cat is None else ops.conv2d_cat(x, x_cat, c1.weight, c1.bias, 1)
+        x = bn_relu_nhwc(y, b1)
         return bn_relu_nhwc(ops.conv2d(x, c2.weight, c2.bias, 1, 1), b2)
 
 
@@ -160,8 +163,7 @@ class Up(nn.Module):
 
     def forward(self, x1, x2):
         x1 = ops.conv_transpose2d(x1, self.up.weight, self.up.bias, 2)
-        x = torch.cat([x2.to(x1.dtype), x1], dim=-1)
-        return self.conv(x)
+        return self.conv(x2, x1)   # conv(cat([x2, x1], channels)), unet:213-216
 
 
 class UNet(nn.Module):

@@ -506,6 +506,20 @@ int csu_conv2d_wgrad_oihw(const csu_conv_geom* g, int dtype, const void* x, cons
  * C % 64 == 0 and N % 64 (5) / N % 128 (6) == 0).  Its workspace: csu_conv2d_wgrad_workspace_ex(g, cfg) (0 when not
  * eligible). */
 size_t csu_conv2d_wgrad_workspace_ex(const csu_conv_geom* g, int cfg);
+/* Two-source input: the conv of UNet Up over cat([x2, x1], channels) (unet:213-216) without the
+ * concatenated tensor.  x holds input channels [0, c_split) (c_split per pixel), x2 channels
+ * [c_split, C) (C - c_split per pixel); the input gradient is written the same way (dx / dx2), and
+ * the weight gradient reads both (torch OIHW layout + db, csu_conv2d_wgrad_oihw's workspace).
+ * csu_conv2d_split_ok: 1 when a geometry / split is supported (bf16 only; 3x3 stride-1 pad-1 with
+ * OW % 64 == 0, C, N and c_split multiples of 64); the three calls fail with CSU_E_UNSUPPORTED
+ * otherwise (the caller then materialises the concatenation). */
+int csu_conv2d_split_ok(const csu_conv_geom* g, int c_split);
+int csu_conv2d_fwd_split(const csu_conv_geom* g, int dtype, const void* x, const void* x2, int c_split, const void* w_ohwi,
+                         const float* bias, void* y, void* stream);
+int csu_conv2d_dgrad_split(const csu_conv_geom* g, int dtype, const void* dy, const void* w_ihwo, void* dx, void* dx2,
+                           int c_split, void* stream);
+int csu_conv2d_wgrad_split_oihw(const csu_conv_geom* g, int dtype, const void* x, const void* x2, int c_split, const void* dy,
+                                float* dw_db, void* workspace, size_t ws_bytes, void* stream);
 int csu_conv2d_wgrad_ex(const csu_conv_geom* g, int dtype, const void* x, const void* dy, int c_real, float* dw_db,
                         void* workspace, size_t ws_bytes, int cfg, void* stream);
 

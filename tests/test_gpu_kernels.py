@@ -654,6 +654,40 @@ def test_conv_wgrad_cfgs(case):
             assert err < 1e-5, (cfg, creal, err)   # fp32 accumulation of exact bf16 products
 
 
+@pytest.mark.parametrize("B,H,Ca,Cb,N", [(1, 64, 64, 64, 64), (2, 64, 128, 64, 128), (1, 32, 64, 64, 64)])
+def test_conv2d_cat_two_source(B, H, Ca, Cb, N):
+    """UNet Up's conv over cat([x2, x1], channels) (unet:213-216) on the two-source kernels (no
+    concatenated tensor; (1, 32, ...) is not eligible and runs on the materialised cat) vs float64
+    torch: output, both input gradients, weight and bias gradients (bf16 autocast tolerances)."""
+    import ctypes
+    from csu import ops
+    from csu._lib import lib
+    d = dev()
+    g = torch.Generator().manual_seed(B + H + Ca + Cb + N)
+    xa = torch.randn(B, H, H, Ca, generator=g).bfloat16()
+    xb = torch.randn(B, H, H, Cb, generator=g).bfloat16()
+    w = torch.randn(N, Ca + Cb, 3, 3, generator=g) * (1.0 / (9 * (Ca + Cb)) ** 0.5)
+    b = torch.randn(N, generator=g) * 0.1
+    xa64, xb64 = xa.double().requires_grad_(True), xb.double().requires_grad_(True)
+    w64, b64 = w.double().requires_grad_(True), b.double().requires_grad_(True)
+    ref = torch.nn.functional.conv2d(torch.cat([xa64, xb64], -1).permute(0, 3, 1, 2), w64, b64, 1, 1).permute(0, 2, 3, 1)
+    gy = torch.randn(ref.shape, generator=g).bfloat16()
+    ref.backward(gy.double())
+    gm = ops._conv_geom(B, H, H, Ca + Cb, N, 3, 3, 1, 1)
+    assert bool(lib().csu_conv2d_split_ok(ctypes.byref(gm), Ca)) == (H % 64 == 0)
+    xad, xbd = xa.to(d).requires_grad_(True), xb.to(d).requires_grad_(True)
+    wd, bd = w.to(d).requires_grad_(True), b.to(d).requires_grad_(True)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = ops.conv2d_cat(xad, xbd, wd, bd, 1)
+    y.backward(gy.to(d))
+    torch.cuda.synchronize()
+    assert_close(y.float(), ref, torch.bfloat16)
+    assert_close(xad.grad, xa64.grad, torch.bfloat16)
+    assert_close(xbd.grad, xb64.grad, torch.bfloat16)
+    assert_close(wd.grad, w64.grad, torch.bfloat16)
+    assert_close(bd.grad, b64.grad, torch.bfloat16)
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("B,H,Cin,Cout", [(2, 8, 64, 32), (1, 5, 128, 64)])
 def test_conv_transpose2d_nhwc_vs_torch(B, H, Cin, Cout, dtype):

@@ -19,7 +19,14 @@ shapes = [("u1 64->64", 0, 512, 512, 64, 64, 3, 1, 1), ("u1 128->64", 0, 512, 51
           ("u5 1024->1024", 0, 32, 32, 1024, 1024, 3, 1, 1),
           ("dg u1 64->64", 1, 512, 512, 64, 64, 3, 1, 1), ("dg u2 64->128", 1, 256, 256, 64, 128, 3, 1, 1),
           ("convT 128->64", 1, 512, 512, 64, 128, 2, 2, 0), ("convT 1024->512", 1, 64, 64, 512, 1024, 2, 2, 0),
-          ("merge 64->128 s2", 0, 128, 128, 64, 128, 3, 2, 1), ("dg merge 64->128 s2", 1, 128, 128, 64, 128, 3, 2, 1)]
+          ("merge 64->128 s2", 0, 128, 128, 64, 128, 3, 2, 1), ("dg merge 64->128 s2", 1, 128, 128, 64, 128, 3, 2, 1),
+          # CSWin 512x512: patch embed (3 -> 8 padded channels), CARAFE(4) encoders, merges
+          ("embed 8->64 7x7 s4", 0, 512, 512, 8, 64, 7, 4, 2), ("carafe4 enc 16->144", 0, 128, 128, 16, 144, 3, 1, 1),
+          ("dg carafe4 enc", 1, 128, 128, 16, 144, 3, 1, 1), ("carafe enc 32->36", 0, 64, 64, 32, 36, 3, 1, 1),
+          ("dg carafe enc 32->36", 1, 64, 64, 32, 36, 3, 1, 1), ("merge 128->256 s2", 0, 64, 64, 128, 256, 3, 2, 1),
+          ("dg merge 128->256 s2", 1, 64, 64, 128, 256, 3, 2, 1)]
+if os.environ.get("ONLY"):
+    shapes = [x for x in shapes if any(k in x[0] for k in os.environ["ONLY"].split(","))]
 
 
 def graph_time(fn, n=10, reps=5):

@@ -18,7 +18,11 @@ shapes = [("u1 64->64", 512, 512, 64, 64, 3, 1, 1), ("u1 128->64", 512, 512, 128
           ("u3 256->256", 128, 128, 256, 256, 3, 1, 1), ("u4 512->512", 64, 64, 512, 512, 3, 1, 1),
           ("u5 1024->1024", 32, 32, 1024, 1024, 3, 1, 1), ("convT 128->64", 512, 512, 64, 128, 2, 2, 0),
           ("convT 1024->512", 64, 64, 512, 1024, 2, 2, 0), ("merge 64->128 s2", 128, 128, 64, 128, 3, 2, 1),
-          ("merge 256->512 s2", 32, 32, 256, 512, 3, 2, 1)]
+          ("merge 256->512 s2", 32, 32, 256, 512, 3, 2, 1), ("embed 8->64 7x7 s4", 512, 512, 8, 64, 7, 4, 2),
+          ("carafe4 enc 16->144", 128, 128, 16, 144, 3, 1, 1), ("carafe enc 32->36", 64, 64, 32, 36, 3, 1, 1),
+          ("merge 128->256 s2", 64, 64, 128, 256, 3, 2, 1)]
+if os.environ.get("ONLY"):
+    shapes = [x for x in shapes if any(k in x[0] for k in os.environ["ONLY"].split(","))]
 
 
 def call(g, x, dy, out, work, cfg):
