@@ -553,13 +553,11 @@ __global__ __launch_bounds__(64 * NS / 16, 1) void conv3_wgrad_halo(Geo g, long 
                 const int iy = oy + j / XBLK - 1, ix = ox0 - 1 + irow[i];
                 const bool ok = sv && irow[i] < 66 && iy >= 0 && iy < g.H && ix >= 0 && ix < g.W;
                 if (ok) off = (unsigned)(((((int)b * g.H + iy) * g.W + ix) * xst + xc0 + icol[i]) * 2);
-                unsigned v[1] = {off};
-                dma<1>(rsX, v, 0u, stg + j * 512, 0);
+                dma1_u(rsX, off, 0u, stg + j * 512);
             } else {
                 if (sv && j < NBLK)
                     off = (unsigned)((((((int)b * g.OH + oy) * g.OW + ox0 + irow[i]) * g.N) + n0 + icol[i]) * 2);
-                unsigned v[1] = {off};
-                dma<1>(rsD, v, 0u, stg + j * 512, 0);
+                dma1_u(rsD, off, 0u, stg + j * 512);
             }
         }
     };
@@ -923,7 +921,7 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void igemm_dma(IG g, const bf16* _
             bases(tile);
             ptile = tile;
         }
-        const int k0 = ((uu % nk + (kRot ? (int)(tile % (unsigned)nk) : 0)) % nk) * BK;   // rotated slice order
+        const int k0 = (uu % nk) * BK;
         const int t = k0 / g.Cs, c0 = k0 - t * g.Cs;
         const int ty = t / g.ntx, tx = t - ty * g.ntx;
         const int oy = ty * g.sty, ox = tx * g.stx;
@@ -1075,7 +1073,9 @@ int id_pick(const IG& g) {
     if (!id_eligible(g)) return -1;
     const long mt = (g.M + 255) / 256;
     if (g.Ncols % 256 == 0 && mt * (g.Ncols / 256) >= id_cus()) return 7;
-    if (g.Ncols % 128 == 0) return 2;
+    // fewer 256 x 128 tiles than CUs (the CSWin merges at 64^2 / 32^2, the stride phases of their
+    // input gradients): the v2 kernel's 4x more 128 x 64 tiles win (profiles/r03v_conv_probe*.txt)
+    if (g.Ncols % 128 == 0 && mt * (g.Ncols / 128) >= id_cus()) return 2;
     return -1;
 }
 

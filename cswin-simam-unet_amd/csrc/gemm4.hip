@@ -152,7 +152,7 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm4_kernel(long M, int N,
     auto issue = [&](int u) {   // DMA of unit min(u, U - 1) into stage u % S
         const int uu = u < U ? u : U - 1;
         const unsigned tile = lo + kk + (unsigned)(uu / nk) * nloc;
-        const unsigned soff = (unsigned)((uu % nk + (kRot ? (int)(tile % (unsigned)nk) : 0)) % nk) * G4_BK * 2;
+        const unsigned soff = (unsigned)(uu % nk) * G4_BK * 2;   // natural K order: rotating it by the N tile measured +3 % (profiles/r03y_*)
         bf16* st = smem + (u % S) * STAGE;
         const long ra = (long)(tile / nbn) * BM, rw = (long)(tile % nbn) * BN;
         g4_dma<BM, NWV>(rsrc4(A + ra * lda, (M - ra) * lda * 2), voffA, soff, st, wave);

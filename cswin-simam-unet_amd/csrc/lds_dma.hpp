@@ -62,12 +62,21 @@ template <int NW>
 __device__ __forceinline__ void dma(i32x4 rs, const unsigned* voff, unsigned soff, bf16* img, int wave) {
 #pragma unroll
     for (int i = 0; i < NW; ++i) {
-        // uniform by construction; readfirstlane keeps it in an SGPR when the compiler cannot prove it
-        const unsigned lds = __builtin_amdgcn_readfirstlane((unsigned)reinterpret_cast<unsigned long>(
-            (__attribute__((address_space(3))) bf16*)(img + (wave * NW + i) * 512)));
+        const unsigned lds = (unsigned)reinterpret_cast<unsigned long>(
+            (__attribute__((address_space(3))) bf16*)(img + (wave * NW + i) * 512));
         asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
                      :: "s"(lds), "v"(voff[i]), "s"(rs), "s"(soff) : "memory", "m0");
     }
+}
+
+// One DMA instruction into the 1-KB block at img, the LDS address forced uniform (readfirstlane):
+// for kernels where hipcc cannot prove it (the address would land in a VGPR and the asm be
+// invalid).  Not used in dma(): there the extra readfirstlanes cost the fused Mlp its registers.
+__device__ __forceinline__ void dma1_u(i32x4 rs, unsigned voff, unsigned soff, bf16* img) {
+    const unsigned lds = __builtin_amdgcn_readfirstlane(
+        (unsigned)reinterpret_cast<unsigned long>((__attribute__((address_space(3))) bf16*)img));
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+                 :: "s"(lds), "v"(voff), "s"(rs), "s"(soff) : "memory", "m0");
 }
 
 template <int N> __device__ __forceinline__ void vmwait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }

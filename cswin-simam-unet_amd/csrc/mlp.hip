@@ -172,7 +172,7 @@ template <int C, bool DROP>
 __global__ __launch_bounds__(MT) void mlp_fwd_kernel(long M, const bf16* __restrict__ X, const bf16* __restrict__ W1,
                                                      const float* __restrict__ b1, const bf16* __restrict__ W2,
                                                      const float* __restrict__ b2, const float* __restrict__ res,
-                                                     float* __restrict__ out, MlpDrop dd) {
+                                                     float* __restrict__ out, MlpDrop dd, long rpi) {
     constexpr int NCH = 4 * C / HC;     // hidden chunks
     constexpr int KS = C / 16;          // k-steps of GEMM1
     constexpr int TF = C / 32;          // 32-feature output tiles (all C, partial over the hidden half)
@@ -193,10 +193,11 @@ __global__ __launch_bounds__(MT) void mlp_fwd_kernel(long M, const bf16* __restr
     const int tok = 32 * t + r;
     const bool ok = tok < rows;
     const int hs = 32 * u;              // this wave's hidden features within a chunk
-    // hidden chunk of loop step j: rotated by the panel, so the workgroups running together stream
-    // different weight chunks (every panel reads the same 2 x 4C x C weights: without the rotation
-    // all CUs of an XCD hit the same L2 lines at once)
-    const int j0 = kRot ? (int)(blockIdx.x & (NCH - 1)) : 0;
+    // hidden chunk of loop step j: rotated by the panel's position inside its image (rpi rows per
+    // image, a multiple of the panel), so the workgroups running together stream different weight
+    // chunks (every panel reads the same 2 x 4C x C weights: without the rotation all CUs of an XCD
+    // hit the same L2 lines at once) while a token's sum order does not depend on the batch split
+    const int j0 = kRot && rpi > 0 && rpi % BM == 0 ? (int)(((m0 % rpi) / BM) & (NCH - 1)) : 0;
     auto chk = [&](int j) { return (j + j0) & (NCH - 1); };
     for (int i = threadIdx.x; i < 4 * C; i += MT) b1s[i] = b1[i];
     bf16x8 xf[KS];
@@ -304,7 +305,7 @@ template <int C, bool DROP>
 __global__ __launch_bounds__(MT) void mlp_bwd_kernel(long M, const bf16* __restrict__ X, const bf16* __restrict__ dY,
                                                      const bf16* __restrict__ W1, const float* __restrict__ b1,
                                                      const bf16* __restrict__ W2, bf16* __restrict__ dH,
-                                                     bf16* __restrict__ G, bf16* __restrict__ dX, MlpDrop dd) {
+                                                     bf16* __restrict__ G, bf16* __restrict__ dX, MlpDrop dd, long rpi) {
     constexpr int NCH = 4 * C / HC;
     constexpr int KS = C / 16;
     constexpr int TF = C / 32;
@@ -328,7 +329,7 @@ __global__ __launch_bounds__(MT) void mlp_bwd_kernel(long M, const bf16* __restr
     const int tok = 32 * t + r;
     const bool ok = tok < rows;
     const int hs = 32 * u;
-    const int j0 = kRot ? (int)(blockIdx.x & (NCH - 1)) : 0;   // rotated chunk order (see the forward)
+    const int j0 = kRot && rpi > 0 && rpi % BM == 0 ? (int)(((m0 % rpi) / BM) & (NCH - 1)) : 0;   // see the forward
     auto chk = [&](int j) { return (j + j0) & (NCH - 1); };
     for (int i = threadIdx.x; i < 4 * C; i += MT) b1s[i] = b1[i];
     bf16x8 xf[KS], dyf[KS];
@@ -484,26 +485,26 @@ __global__ __launch_bounds__(MT) void mlp_bwd_kernel(long M, const bf16* __restr
 
 template <int C>
 int fwd_launch(long M, const void* x, const void* w1, const float* b1, const void* w2, const float* b2, const float* res,
-               float* out, const MlpDrop* d, hipStream_t st) {
+               float* out, const MlpDrop* d, long rpi, hipStream_t st) {
     const dim3 grid((unsigned)((M + BM - 1) / BM));
     if (d)
-        mlp_fwd_kernel<C, true><<<grid, MT, 0, st>>>(M, (const bf16*)x, (const bf16*)w1, b1, (const bf16*)w2, b2, res, out, *d);
+        mlp_fwd_kernel<C, true><<<grid, MT, 0, st>>>(M, (const bf16*)x, (const bf16*)w1, b1, (const bf16*)w2, b2, res, out, *d, rpi);
     else
         mlp_fwd_kernel<C, false><<<grid, MT, 0, st>>>(M, (const bf16*)x, (const bf16*)w1, b1, (const bf16*)w2, b2, res, out,
-                                                      MlpDrop{});
+                                                      MlpDrop{}, rpi);
     return check_launch("mlp_fwd");
 }
 
 template <int C>
 int bwd_launch(long M, const void* x, const void* dy, const void* w1, const float* b1, const void* w2, void* dh, void* g,
-               void* dx, const MlpDrop* d, hipStream_t st) {
+               void* dx, const MlpDrop* d, long rpi, hipStream_t st) {
     const dim3 grid((unsigned)((M + BM - 1) / BM));
     if (d)
         mlp_bwd_kernel<C, true><<<grid, MT, 0, st>>>(M, (const bf16*)x, (const bf16*)dy, (const bf16*)w1, b1, (const bf16*)w2,
-                                                     (bf16*)dh, (bf16*)g, (bf16*)dx, *d);
+                                                     (bf16*)dh, (bf16*)g, (bf16*)dx, *d, rpi);
     else
         mlp_bwd_kernel<C, false><<<grid, MT, 0, st>>>(M, (const bf16*)x, (const bf16*)dy, (const bf16*)w1, b1, (const bf16*)w2,
-                                                      (bf16*)dh, (bf16*)g, (bf16*)dx, MlpDrop{});
+                                                      (bf16*)dh, (bf16*)g, (bf16*)dx, MlpDrop{}, rpi);
     return check_launch("mlp_bwd");
 }
 
@@ -530,11 +531,12 @@ extern "C" int csu_mlp_fwd_dp(long M, int C, const void* x, const void* w1, cons
     const int e = mlp_drop_of(d, md);
     if (e < 0) return e;
     const MlpDrop* dp = d && e == 0 ? &md : nullptr;
+    const long rpi = d ? (long)d->rows_per_sample : 0;   // rows per image: the hidden-chunk rotation
     const hipStream_t st = as_stream(stream);
     switch (C) {
-        case 64: return fwd_launch<64>(M, x, w1, b1, w2, b2, res, out, dp, st);
-        case 128: return fwd_launch<128>(M, x, w1, b1, w2, b2, res, out, dp, st);
-        case 256: return fwd_launch<256>(M, x, w1, b1, w2, b2, res, out, dp, st);
+        case 64: return fwd_launch<64>(M, x, w1, b1, w2, b2, res, out, dp, rpi, st);
+        case 128: return fwd_launch<128>(M, x, w1, b1, w2, b2, res, out, dp, rpi, st);
+        case 256: return fwd_launch<256>(M, x, w1, b1, w2, b2, res, out, dp, rpi, st);
         default: return fail(CSU_E_ARG, "mlp_fwd: C must be 64, 128 or 256");
     }
 }
@@ -552,11 +554,12 @@ extern "C" int csu_mlp_bwd_dp(long M, int C, const void* x, const void* dy, cons
     const int e = mlp_drop_of(d, md);
     if (e < 0) return e;
     const MlpDrop* dp = d && e == 0 ? &md : nullptr;
+    const long rpi = d ? (long)d->rows_per_sample : 0;
     const hipStream_t st = as_stream(stream);
     switch (C) {
-        case 64: return bwd_launch<64>(M, x, dy, w1, b1, w2, dh, g, dx, dp, st);
-        case 128: return bwd_launch<128>(M, x, dy, w1, b1, w2, dh, g, dx, dp, st);
-        case 256: return bwd_launch<256>(M, x, dy, w1, b1, w2, dh, g, dx, dp, st);
+        case 64: return bwd_launch<64>(M, x, dy, w1, b1, w2, dh, g, dx, dp, rpi, st);
+        case 128: return bwd_launch<128>(M, x, dy, w1, b1, w2, dh, g, dx, dp, rpi, st);
+        case 256: return bwd_launch<256>(M, x, dy, w1, b1, w2, dh, g, dx, dp, rpi, st);
         default: return fail(CSU_E_ARG, "mlp_bwd: C must be 64, 128 or 256");
     }
 }

@@ -1383,6 +1383,19 @@ def linear_residual(res, x, weight, bias):
         return _LinearResidualFn.apply(res, x, weight, bias, _weight_bf16(weight))
 
 
+def _mlp_desc(drop: Optional[MlpDrop], rpi: int):
+    """csu_mlp_dropout of a fused-Mlp launch: the dropout / DropPath of ``drop``, or none (p = 0);
+    rows_per_sample = rows per image either way (DropPath's sample and the kernel's chunk rotation)."""
+    if drop is not None:
+        d = drop.c_struct()
+        if drop.row_scale is None:
+            d.rows_per_sample = rpi
+        return d
+    d = _lib.MlpDropout()
+    d.p, d.rows_per_sample = 0.0, rpi
+    return d
+
+
 class _MlpFusedFn(torch.autograd.Function):
     """res + fc2(gelu(fc1(x))) (Mlp cswin:180-196 + residual cswin:368) in ONE csu_mlp_fwd launch
     (the 4C hidden layer never reaches HBM).  Backward: one csu_mlp_bwd launch recomputes h and
@@ -1399,11 +1412,13 @@ class _MlpFusedFn(torch.autograd.Function):
         y = torch.empty_like(res2)
         M = x2.shape[0]
         b2f = b2.detach().float().contiguous()
-        dd = None if drop is None else ctypes.byref(drop.c_struct())
+        rpi = x.shape[1] if x.dim() == 3 else M   # rows per image: the kernel's hidden-chunk rotation
+        dd = ctypes.byref(_mlp_desc(drop, rpi))
         _launch("mlp_fwd", lambda: lib().csu_mlp_fwd_dp(M, C, ptr(x2), ptr(w1c), ptr(b1f), ptr(w2c), ptr(b2f), ptr(res2),
                                                         ptr(y), dd, stream_ptr(x2.device)),
                 16 * M * C * C, M * C * (2 + 4 + 4) + 16 * C * C)
         ctx.drop = drop
+        ctx.rpi = rpi
         ctx.save_for_backward(x2, w1c, b1f, w2c)
         ctx.meta = (res.dtype, x.shape, w1.dtype, b1.dtype, w2.dtype, b2.dtype)
         ctx.params = (w1, b1, w2, b2)
@@ -1423,7 +1438,7 @@ class _MlpFusedFn(torch.autograd.Function):
         dh = torch.empty(M, 4 * C, dtype=torch.bfloat16, device=x2.device)
         g = torch.empty_like(dh)
         dx = torch.empty(M, C, dtype=torch.bfloat16, device=x2.device)
-        dd = None if drop is None else ctypes.byref(drop.c_struct())
+        dd = ctypes.byref(_mlp_desc(drop, ctx.rpi))
         _launch("mlp_bwd", lambda: lib().csu_mlp_bwd_dp(M, C, ptr(x2), ptr(dyb), ptr(w1c), ptr(b1f), ptr(w2c), ptr(dh),
                                                         ptr(g), ptr(dx), dd, stream_ptr(x2.device)),
                 24 * M * C * C, M * C * (2 + 2 + 2) + M * 4 * C * (2 + 2) + 16 * C * C)

@@ -112,8 +112,10 @@ def test_two_ranks_on_csu_kernels_equal_global_batch(tmp_path, dtype, mode):
         assert copied < 0.25 * total, (copied, total)
     m, xs, ts, amp = _setup(dtype)
     ref = [g.cpu() for g in _grads(m, xs, ts, amp)]
-    # per-sample work is identical on both sides (every csu kernel is per token / window / image);
-    # only the batch sums (weight gradients, the loss mean) add in another order -> fp32 rounding
+    # per-sample work is identical on both sides (every csu kernel is per token / window / image, and
+    # the rotated reduction orders depend on a token's position inside its image or on the N tile,
+    # never on the batch); only the batch sums (weight gradients, the loss mean) add in another
+    # order -> fp32 rounding
     tol = 1e-4 if dtype == "fp32" else 1e-3
     if mode == "bf16_allreduce":
         tol = 1e-2   # the averaged gradients themselves are rounded to bf16 (2^-9 relative)
