@@ -1038,6 +1038,117 @@ __global__ __launch_bounds__(64 * WM * WN, 1) void igemm_dma(IG g, const bf16* _
     vmwait<0>();   // drain the re-fetch DMAs before the workgroup's LDS is released
 }
 
+// ---- bf16 3x3 / stride 1 / pad 1 conv with 64 gathered and 64 output channels, halo form ----------
+// (the UNet level-1 DoubleConv convs and their input gradients, unet:182-187: 64 -> 64 at full
+// resolution).  Persistent workgroups own the whole 9 x 64 x 64 weight slab in LDS (loaded once) and
+// walk items of two output rows x 64 pixels: per item the four input rows under them (66-pixel halo
+// images, 64 channels) are staged once through a 2-stage ring and read by all 9 taps at row offsets
+// (tap ky from halo row rr + ky, tap kx at pixel offset kx) -- 4 x 66 staged rows per 128 output
+// pixels instead of 9 x 128 gathered ones.  8 waves: wave (rr, pixel half, n tile).  flip: the
+// input gradient (IHWO weights, tap (ky, kx) = weight tap (2 - ky, 2 - kx)).
+template <bool FLIP>
+__global__ __launch_bounds__(512, 1) void conv3_halo64(int B, int H, int W, const bf16* __restrict__ src, const bf16* __restrict__ wt,
+                                                       const float* __restrict__ bias, bf16* __restrict__ out) {
+    constexpr int XIMG = kHaloRows * 64;    // bf16 per halo image (72 rows x 64 channels)
+    constexpr int NBLK = 4 * XIMG * 2 / 1024;   // 36 DMA blocks per item
+    constexpr int NI = (NBLK + 7) / 8;      // per wave (5)
+    constexpr int STAGE = NI * 8 * 512;     // bf16 per ring stage (40 blocks)
+    constexpr int WIMG = 64 * 64;           // bf16 per tap weight image [n][c]
+    __shared__ __attribute__((aligned(1024))) bf16 wsm[9 * WIMG];
+    __shared__ __attribute__((aligned(1024))) bf16 ring[2 * STAGE];
+    __shared__ float sbias[64];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int r = lane & 31, h = lane >> 5;
+    const int nt = wave & 1, ph = (wave >> 1) & 1, rr = wave >> 2;
+    const int spr = W / 64, prs = H / 2;    // segments per row, row pairs per image
+    const long items = (long)B * prs * spr;
+    // this workgroup's items: a contiguous range per XCD, strided by the XCD's workgroups
+    const long x = blockIdx.x % kXcds, kk = blockIdx.x / kXcds, nloc = gridDim.x / kXcds;
+    const long q = items / kXcds, rem = items % kXcds;
+    const long lo = x < rem ? x * (q + 1) : rem * (q + 1) + (x - rem) * q;
+    const long cnt = q + (x < rem ? 1 : 0);
+    const int my = kk < cnt ? (int)((cnt - kk + nloc - 1) / nloc) : 0;
+    if (my == 0) return;
+    if (threadIdx.x < 64) sbias[threadIdx.x] = bias ? bias[threadIdx.x] : 0.f;
+    // weight slab: tap image t rows n, columns c (OHWI [n][t][c], or IHWO [c'][t'][n'] with t' = 8 - t)
+    {
+        const i32x4 rw = rsrc4(wt, 64L * 9 * 64 * 2);
+#pragma unroll
+        for (int i = 0; i < 9; ++i) {   // 72 blocks: 9 per wave
+            const int j = wave * 9 + i, t = j / 8, row = (j % 8) * 8 + (lane >> 3);
+            const int tw = FLIP ? 8 - t : t;
+            const unsigned off = (unsigned)((row * 9 + tw) * 64 + 8 * ((lane & 7) ^ mkey<128>(row))) * 2u;
+            dma1_u(rw, off, 0u, wsm + j * 512);
+        }
+    }
+    const i32x4 rs = rsrc4(src, (long)B * H * W * 64 * 2);
+    auto issue = [&](int u) {   // halo images of item lo + kk + u * nloc (past the last: zeros)
+        const long it = lo + kk + (long)(u < my ? u : my - 1) * nloc;
+        const bool iv = u < my;
+        const long t1 = it / spr;
+        const int ox0 = (int)(it - t1 * spr) * 64;
+        const int b = (int)(t1 / prs), oy0 = (int)(t1 - (long)b * prs) * 2;
+        bf16* stg = ring + (u & 1) * STAGE;
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+            const int j = wave * NI + i;
+            const int img = j / 9, row = (j % 9) * 8 + (lane >> 3);
+            const int iy = oy0 + img - 1, ix = ox0 - 1 + row;
+            const bool ok = iv && j < NBLK && row < 66 && iy >= 0 && iy < H && ix >= 0 && ix < W;
+            const unsigned off = ok ? (unsigned)(((((long)b * H + iy) * W + ix) * 64 + 8 * ((lane & 7) ^ mkey<128>(row))) * 2) : kOOB;
+            dma1_u(rs, off, 0u, stg + j * 512);
+        }
+    };
+    const __amdgpu_buffer_rsrc_t rso = buf_rsrc(out, (long)B * H * W * 64 * 2);
+    issue(0);
+    for (int u = 0; u < my; ++u) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (u == 0) vmwait<0>(); else vmwait<4>();   // item u landed (after its DMA: item u-1's 4 stores)
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        issue(u + 1);
+        const bf16* st = ring + (u & 1) * STAGE;
+        f32x16 acc = f32x16{};
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky) {
+            const bf16* himg = st + (rr + ky) * XIMG;
+#pragma unroll
+            for (int kx = 0; kx < 3; ++kx) {
+                const bf16* wimg = wsm + (ky * 3 + kx) * WIMG;
+#pragma unroll
+                for (int s2 = 0; s2 < 4; ++s2) {
+                    const bf16x8 a = *reinterpret_cast<const bf16x8*>(wimg + moff<128>(nt * 32 + r, 16 * s2 + 8 * h));
+                    const bf16x8 bfr = *reinterpret_cast<const bf16x8*>(himg + moff<128>(ph * 32 + r + kx, 16 * s2 + 8 * h));
+                    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bfr, acc, 0, 0, 0);
+                }
+            }
+        }
+        // acc[4g + e] = out[pixel ph * 32 + r of row rr][n = nt * 32 + 8g + 4h + e]
+        const long it = lo + kk + (long)u * nloc;
+        const long t1 = it / spr;
+        const int ox0 = (int)(it - t1 * spr) * 64;
+        const int b = (int)(t1 / prs), oy = (int)(t1 - (long)b * prs) * 2 + rr;
+        const unsigned pix = (unsigned)(((long)b * H + oy) * W + ox0 + ph * 32 + r);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int n = nt * 32 + 8 * g + 4 * h;
+            const f32x4 bv = *reinterpret_cast<const f32x4*>(sbias + n);
+            const float v[4] = {acc[4 * g] + bv[0], acc[4 * g + 1] + bv[1], acc[4 * g + 2] + bv[2], acc[4 * g + 3] + bv[3]};
+            buf_st4bf(rso, (pix * 64u + (unsigned)n) * 2u, v);
+        }
+    }
+    vmwait<0>();
+}
+
+constexpr int kHalo64Cfg = 20;   // csu_conv2d_ex cfg selecting conv3_halo64
+bool halo64_ok(const IG& g, bool flip) {   // the forward conv (flip: its input gradient) this kernel takes
+    return g.Cs == 64 && g.Ncols == 64 && g.nty == 3 && g.ntx == 3 && g.csplit == 0 && g.nsplit == 0 && g.OHo == g.Hs &&
+           g.OWo == g.Ws && g.Hs % 2 == 0 && g.Ws % 64 == 0 && g.RH == g.Hs && g.RW == g.Ws &&
+           (flip ? (g.sty == -1 && g.stx == -1 && g.by == 1 && g.bx == 1 && g.wty == 1 && g.wtx == 1)
+                 : (g.sty == 1 && g.stx == 1 && g.ay == 1 && g.ax == 1 && g.by == -1 && g.bx == -1));
+}
+
 struct IDCfg { int bm, bn, s, wm, wn; };
 constexpr IDCfg kIDCfgs[] = {{128, 128, 3, 2, 2}, {256, 128, 2, 4, 2}, {256, 128, 3, 4, 2}, {128, 64, 4, 2, 2},
                              {256, 64, 3, 4, 2},  {128, 64, 3, 2, 2},  {256, 256, 2, 2, 4}, {256, 256, 2, 4, 2},
@@ -1108,6 +1219,15 @@ int launch_ig(const IG* gv, int n, const void* src, const void* w, const float* 
     if ((long)g.B * g.Hs * g.Ws * g.Cs * 2 >= (1L << 31) || (long)g.Ncols * g.ldw * 2 >= (1L << 31) ||
         (long)g.B * g.OHo * g.OWo * g.Ncols * 2 >= (1L << 31))
         return fail(CSU_E_UNSUPPORTED, "conv2d: operand larger than 2 GiB (32-bit buffer offsets)");
+    if ((cfg < 0 || cfg == kHalo64Cfg) && n == 1) {   // 64 -> 64 channel 3x3 stride-1 conv: the halo kernel
+        const bool flip = g.sty == -1;
+        if (halo64_ok(g, flip)) {
+            if (flip) conv3_halo64<true><<<dim3(id_cus()), 512, 0, st>>>(g.B, g.Hs, g.Ws, (const bf16*)src, (const bf16*)w, bias, (bf16*)out);
+            else conv3_halo64<false><<<dim3(id_cus()), 512, 0, st>>>(g.B, g.Hs, g.Ws, (const bf16*)src, (const bf16*)w, bias, (bf16*)out);
+            return check_launch("conv2d (halo64)");
+        }
+    }
+    if (cfg == kHalo64Cfg) return fail(CSU_E_ARG, "conv2d: halo64 configuration not eligible");
     if (cfg > 0) {   // forced v3 configuration: every phase must be eligible for it
         const int k = cfg - 1;
         if (k >= kIDNCfg) return fail(CSU_E_ARG, "conv2d: bad igemm_dma configuration");

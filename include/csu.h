@@ -486,7 +486,9 @@ int csu_conv2d_dgrad(const csu_conv_geom* g, int dtype, const void* dy, const vo
  * w as there).  cfg -1: the per-shape choice the plain entries make; 0: the register-staged v2
  * implicit GEMM; 1 + k: the persistent LDS-DMA kernel (bf16, gathered channels % 64 == 0) in tile
  * configuration k (0: 128x128 3-stage, 1: 256x128 2-stage 8 waves, 2: 256x128 3-stage 8 waves,
- * 3: 128x64 4-stage, 4: 256x64 3-stage 8 waves, 5: 128x64 3-stage); CSU_E_ARG when not eligible. */
+ * 3: 128x64 4-stage, 4: 256x64 3-stage 8 waves, 5: 128x64 3-stage, 6 / 7: 256x256 8 waves, 8:
+ * 512x64 8 waves); 20: the halo kernel of 3x3 stride-1 pad-1 convs with 64 gathered and 64 output
+ * channels (H % 2 == 0, W % 64 == 0); CSU_E_ARG when not eligible. */
 int csu_conv2d_ex(int op, const csu_conv_geom* g, int dtype, const void* src, const void* w, const float* bias, void* out,
                   int cfg, void* stream);
 size_t csu_conv2d_wgrad_workspace(const csu_conv_geom* g);

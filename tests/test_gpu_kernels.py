@@ -618,6 +618,39 @@ def test_conv_igemm_dma_cfgs(case):
             assert err < 4e-3, (op, cfg, err)   # bf16 output rounding (2^-9 relative) dominates
 
 
+@pytest.mark.parametrize("B,H,W", [(2, 64, 64), (1, 6, 128), (1, 5, 64)])
+def test_conv_halo64(B, H, W):
+    """The halo kernel of the 64 -> 64 channel 3x3 stride-1 conv (csu_conv2d_ex cfg 20), forward and
+    input gradient, vs float64 torch on the same bf16 operands; H odd is not eligible (CSU_E_ARG)."""
+    import ctypes
+    from csu import ops
+    from csu._lib import lib, CSU_BF16
+    d = dev()
+    gm = ops._conv_geom(B, H, W, 64, 64, 3, 3, 1, 1)
+    g = torch.Generator().manual_seed(B * 1000 + H + W)
+    x = torch.randn(B, H, W, 64, generator=g).bfloat16()
+    w = (torch.randn(64, 64, 3, 3, generator=g) / 24.0).bfloat16()
+    b = torch.randn(64, generator=g)
+    dy = torch.randn(B, H, W, 64, generator=g).bfloat16()
+    ref_f = torch.nn.functional.conv2d(x.double().permute(0, 3, 1, 2), w.double(), b.double(), 1, 1).permute(0, 2, 3, 1)
+    ref_d = torch.nn.functional.conv_transpose2d(dy.double().permute(0, 3, 1, 2), w.double(), None, 1, 1).permute(0, 2, 3, 1)
+    xd, dyd, bd = x.to(d), dy.to(d), b.to(d)
+    w_ohwi = w.permute(0, 2, 3, 1).contiguous().to(d)
+    w_ihwo = w.permute(1, 2, 3, 0).contiguous().to(d)
+    st = torch.cuda.current_stream().cuda_stream
+    for op, src, wt, bias, ref in ((0, xd, w_ohwi, bd, ref_f), (1, dyd, w_ihwo, None, ref_d)):
+        out = torch.full(ref.shape, float("nan"), dtype=torch.bfloat16, device=d)
+        e = lib().csu_conv2d_ex(op, ctypes.byref(gm), CSU_BF16, src.data_ptr(), wt.data_ptr(),
+                                bias.data_ptr() if bias is not None else None, out.data_ptr(), 20, st)
+        if H % 2:
+            assert e != 0
+            continue
+        assert e == 0, lib().csu_last_error_string()
+        torch.cuda.synchronize()
+        err = float((out.double().cpu() - ref).norm() / ref.norm())
+        assert err < 4e-3, (op, err)
+
+
 @pytest.mark.parametrize("case", DMA_CONV_CASES + [(2, 16, 64, 128, 3, 2, 1), (1, 70, 64, 72, 3, 1, 1), (2, 9, 32, 64, 3, 1, 1),
                                   (1, 64, 64, 128, 3, 1, 1), (2, 64, 128, 64, 3, 1, 1)])   # halo-eligible (OW % 64 == 0)
 def test_conv_wgrad_cfgs(case):
