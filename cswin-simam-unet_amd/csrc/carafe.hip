@@ -39,38 +39,24 @@ __device__ __forceinline__ void ld8_rs(__amdgpu_buffer_rsrc_t rs, unsigned off, 
     }
 }
 
-template <typename T>
-__global__ __launch_bounds__(NT) void carafe_fwd(int B, int H, int W, int C, int s, const T* __restrict__ x,
+// One thread = one INPUT pixel x 8 channels and all S^2 output sub-pixels of it: the 9 neighbour
+// vectors are gathered once per input pixel (not once per output pixel: S^2 x fewer L2 reads), and
+// the pixel's 9 S^2 logits are read as contiguous vectors.
+template <typename T, int S>
+__global__ __launch_bounds__(NT) void carafe_fwd(int B, int H, int W, int C, const T* __restrict__ x,
                                                  const T* __restrict__ enc, T* __restrict__ out,
                                                  float* __restrict__ wsave) {
+    constexpr int S2 = S * S;
     const int G = C / 8;
     const long gid = xcd_tile(blockIdx.x, gridDim.x) * NT + threadIdx.x;   // neighbour blocks share one L2
-    const int sW = s * W, sH = s * H;
-    const long total = (long)B * sH * sW * G;
+    const long total = (long)B * H * W * G;
     if (gid >= total) return;
     const int g = gid % G;
     long p = gid / G;
-    const int X = p % sW; p /= sW;
-    const int Y = p % sH;
-    const int b = p / sH;
-    const int y = Y / s, i = Y - y * s, xx = X / s, j = X - xx * s;
-    const int s2 = s * s, sub = i * s + j;
+    const int xx = p % W; p /= W;
+    const int y = p % H;
+    const int b = p / H;
     const size_t lpix = ((size_t)b * H + y) * W + xx;
-    const T* e = enc + lpix * KT * s2 + sub;
-    float lg[KT], mx = -INFINITY;
-#pragma unroll
-    for (int t = 0; t < KT; ++t) {
-        lg[t] = to_f(e[t * s2]);
-        mx = fmaxf(mx, lg[t]);
-    }
-    float den = 0.f;
-#pragma unroll
-    for (int t = 0; t < KT; ++t) {
-        lg[t] = __expf(lg[t] - mx);
-        den += lg[t];
-    }
-    const float inv = 1.f / den;
-    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     const __amdgpu_buffer_rsrc_t rx = buf_rsrc(x, (long)B * H * W * C * (long)sizeof(T));
     float v[KT][8];
 #pragma unroll
@@ -79,43 +65,60 @@ __global__ __launch_bounds__(NT) void carafe_fwd(int B, int H, int W, int C, int
         const bool in = yy >= 0 && yy < H && xq >= 0 && xq < W;
         ld8_rs(rx, in ? (unsigned)(((((b * H + yy) * W + xq) * C) + 8 * g) * (int)sizeof(T)) : kOOB, x, v[t]);
     }
+    float lg[KT * S2];   // logit of tap t, sub-pixel q at t * S2 + q
+    const T* e = enc + lpix * KT * S2;
 #pragma unroll
-    for (int t = 0; t < KT; ++t) {
-        lg[t] *= inv;
+    for (int k = 0; k < KT * S2; k += 4) load4(e + k, lg + k);   // 9 S^2 is a multiple of 4
+    const int sW = S * W, sH = S * H;
 #pragma unroll
-        for (int k = 0; k < 8; ++k) acc[k] += lg[t] * v[t][k];
-    }
-    store8(out + (((size_t)b * sH + Y) * sW + X) * C + 8 * g, acc);
-    if (g == 0) {
-        float* ws = wsave + lpix * KT * s2 + sub;
+    for (int q = 0; q < S2; ++q) {
+        float mx = -INFINITY;
 #pragma unroll
-        for (int t = 0; t < KT; ++t) ws[t * s2] = lg[t];
+        for (int t = 0; t < KT; ++t) mx = fmaxf(mx, lg[t * S2 + q]);
+        float w[KT], den = 0.f;
+#pragma unroll
+        for (int t = 0; t < KT; ++t) {
+            w[t] = __expf(lg[t * S2 + q] - mx);
+            den += w[t];
+        }
+        const float inv = 1.f / den;
+        float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int t = 0; t < KT; ++t) {
+            w[t] *= inv;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) acc[k] += w[t] * v[t][k];
+        }
+        const int Y = y * S + q / S, X = xx * S + q % S;
+        store8(out + (((size_t)b * sH + Y) * sW + X) * C + 8 * g, acc);
+        if (g == 0) {
+            float* ws = wsave + lpix * KT * S2 + q;
+#pragma unroll
+            for (int t = 0; t < KT; ++t) ws[t * S2] = w[t];
+        }
     }
 }
 
 // d enc: per output pixel, dw_t = sum_c dout[c] x[nbr_t][c]; dlogit_t = w_t (dw_t - sum_u w_u dw_u).
-// G = C/8 lanes cooperate on one output pixel (G in {8, 16, 32, 64} divides the wave).
-template <typename T>
-__global__ __launch_bounds__(NT) void carafe_bwd_enc(int B, int H, int W, int C, int s, const T* __restrict__ x,
+// One thread = one input pixel x 8 channels x its S^2 output sub-pixels (the neighbour gathers once
+// per input pixel); G = C/8 lanes cooperate on the channel sum (G in {8, 16, 32, 64} divides the wave).
+template <typename T, int S>
+__global__ __launch_bounds__(NT) void carafe_bwd_enc(int B, int H, int W, int C, const T* __restrict__ x,
                                                      const float* __restrict__ wsave, const T* __restrict__ dout,
                                                      T* __restrict__ denc) {
+    constexpr int S2 = S * S;
     const int G = C / 8;
     const long gid = xcd_tile(blockIdx.x, gridDim.x) * NT + threadIdx.x;   // neighbour blocks share one L2
-    const int sW = s * W, sH = s * H;
-    const long total = (long)B * sH * sW * G;
+    const long total = (long)B * H * W * G;
     const bool live = gid < total;
     const long gg = live ? gid : 0;
     const int g = gg % G;
     long p = gg / G;
-    const int X = p % sW; p /= sW;
-    const int Y = p % sH;
-    const int b = p / sH;
-    const int y = Y / s, i = Y - y * s, xx = X / s, j = X - xx * s;
-    const int s2 = s * s, sub = i * s + j;
+    const int xx = p % W; p /= W;
+    const int y = p % H;
+    const int b = p / H;
     const size_t lpix = ((size_t)b * H + y) * W + xx;
-    float go[8];
-    load8(dout + (((size_t)b * sH + Y) * sW + X) * C + 8 * g, go);
-    float dw[KT];
+    const int sW = S * W, sH = S * H;
     const __amdgpu_buffer_rsrc_t rx = buf_rsrc(x, (long)B * H * W * C * (long)sizeof(T));
     float v[KT][8];
 #pragma unroll
@@ -124,28 +127,40 @@ __global__ __launch_bounds__(NT) void carafe_bwd_enc(int B, int H, int W, int C,
         const bool in = yy >= 0 && yy < H && xq >= 0 && xq < W;
         ld8_rs(rx, in ? (unsigned)(((((b * H + yy) * W + xq) * C) + 8 * g) * (int)sizeof(T)) : kOOB, x, v[t]);
     }
+    float go[S2][8];
 #pragma unroll
-    for (int t = 0; t < KT; ++t) {
-        float d = 0.f;
+    for (int q = 0; q < S2; ++q)
+        load8(dout + (((size_t)b * sH + y * S + q / S) * sW + xx * S + q % S) * C + 8 * g, go[q]);
+    float dw[S2][KT];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) d += go[k] * v[t][k];
-        dw[t] = d;
-    }
+    for (int q = 0; q < S2; ++q)
+#pragma unroll
+        for (int t = 0; t < KT; ++t) {
+            float d = 0.f;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) d += go[q][k] * v[t][k];
+            dw[q][t] = d;
+        }
     // reduce over the G lanes of this pixel (aligned groups of G consecutive lanes)
+    for (int o = G >> 1; o > 0; o >>= 1)
 #pragma unroll
-    for (int t = 0; t < KT; ++t)
-        for (int o = G >> 1; o > 0; o >>= 1) dw[t] += __shfl_xor(dw[t], o, 64);
+        for (int q = 0; q < S2; ++q)
+#pragma unroll
+            for (int t = 0; t < KT; ++t) dw[q][t] += __shfl_xor(dw[q][t], o, 64);
     if (!live || g != 0) return;
-    const float* ws = wsave + lpix * KT * s2 + sub;
-    float wt[KT], sum = 0.f;
+    const float* ws = wsave + lpix * KT * S2;
+    T* de = denc + lpix * KT * S2;
 #pragma unroll
-    for (int t = 0; t < KT; ++t) {
-        wt[t] = ws[t * s2];
-        sum += wt[t] * dw[t];
+    for (int q = 0; q < S2; ++q) {
+        float wt[KT], sum = 0.f;
+#pragma unroll
+        for (int t = 0; t < KT; ++t) {
+            wt[t] = ws[t * S2 + q];
+            sum += wt[t] * dw[q][t];
+        }
+#pragma unroll
+        for (int t = 0; t < KT; ++t) de[t * S2 + q] = from_f<T>(wt[t] * (dw[q][t] - sum));
     }
-    T* de = denc + lpix * KT * s2 + sub;
-#pragma unroll
-    for (int t = 0; t < KT; ++t) de[t * s2] = from_f<T>(wt[t] * (dw[t] - sum));
 }
 
 // dx[y', x', c] = sum_t sum_{i,j} w[(y,x), t, (i,j)] dout[(y s + i, x s + j), c],  (y, x) = (y'-ky+1, x'-kx+1)
@@ -249,8 +264,8 @@ __global__ void head_wreduce(int C, int nb, const float* __restrict__ part, floa
 unsigned blocks(long threads) { return (unsigned)((threads + NT - 1) / NT); }
 
 int check_args(int B, int H, int W, int C, int s) {
-    if (B < 1 || H < 1 || W < 1 || s < 1 || C < 8 || C % 8 || C / 8 > 64 || ((C / 8) & (C / 8 - 1)))
-        return fail(CSU_E_ARG, "carafe: need C = 8 * 2^k <= 512");
+    if (B < 1 || H < 1 || W < 1 || (s != 2 && s != 4) || C < 8 || C % 8 || C / 8 > 64 || ((C / 8) & (C / 8 - 1)))
+        return fail(CSU_E_ARG, "carafe: need s in {2, 4} and C = 8 * 2^k <= 512");
     if ((long)B * H * W * C * 4 >= (1L << 31))   // 32-bit buffer offsets into the input (fp32 worst case)
         return fail(CSU_E_UNSUPPORTED, "carafe: input larger than 2 GiB");
     return 0;
@@ -265,14 +280,13 @@ extern "C" int csu_carafe_fwd(int B, int H, int W, int C, int s, int dtype, cons
                               void* out, float* wsave, void* stream) {
     if (int e = check_args(B, H, W, C, s)) return e;
     if (!x || !enc || !out || !wsave) return fail(CSU_E_ARG, "carafe_fwd: null buffer");
-    const long n = (long)B * H * s * W * s * (C / 8);
+    const long n = (long)B * H * W * (C / 8);   // one thread per input pixel x 8 channels
     hipStream_t st = as_stream(stream);
-    if (dtype == CSU_BF16)
-        carafe_fwd<bf16><<<blocks(n), NT, 0, st>>>(B, H, W, C, s, (const bf16*)x, (const bf16*)enc, (bf16*)out, wsave);
-    else if (dtype == CSU_F32)
-        carafe_fwd<float><<<blocks(n), NT, 0, st>>>(B, H, W, C, s, (const float*)x, (const float*)enc, (float*)out, wsave);
-    else
-        return fail(CSU_E_ARG, "carafe_fwd: bad dtype");
+#define CSU_CF(T, S_) carafe_fwd<T, S_><<<blocks(n), NT, 0, st>>>(B, H, W, C, (const T*)x, (const T*)enc, (T*)out, wsave)
+    if (dtype == CSU_BF16) { if (s == 4) CSU_CF(bf16, 4); else CSU_CF(bf16, 2); }
+    else if (dtype == CSU_F32) { if (s == 4) CSU_CF(float, 4); else CSU_CF(float, 2); }
+    else return fail(CSU_E_ARG, "carafe_fwd: bad dtype");
+#undef CSU_CF
     return check_launch("carafe_fwd");
 }
 
@@ -280,17 +294,19 @@ extern "C" int csu_carafe_bwd(int B, int H, int W, int C, int s, int dtype, cons
                               const void* dout, void* dx, void* denc, void* stream) {
     if (int e = check_args(B, H, W, C, s)) return e;
     if (!x || !wsave || !dout || !dx || !denc) return fail(CSU_E_ARG, "carafe_bwd: null buffer");
-    const long n_out = (long)B * H * s * W * s * (C / 8), n_in = (long)B * H * W * (C / 8);
+    const long n_in = (long)B * H * W * (C / 8);
     hipStream_t st = as_stream(stream);
+#define CSU_CE(T, S_) carafe_bwd_enc<T, S_><<<blocks(n_in), NT, 0, st>>>(B, H, W, C, (const T*)x, wsave, (const T*)dout, (T*)denc)
     if (dtype == CSU_BF16) {
-        carafe_bwd_enc<bf16><<<blocks(n_out), NT, 0, st>>>(B, H, W, C, s, (const bf16*)x, wsave, (const bf16*)dout, (bf16*)denc);
+        if (s == 4) CSU_CE(bf16, 4); else CSU_CE(bf16, 2);
         carafe_bwd_x<bf16><<<blocks(n_in), NT, 0, st>>>(B, H, W, C, s, wsave, (const bf16*)dout, (bf16*)dx);
     } else if (dtype == CSU_F32) {
-        carafe_bwd_enc<float><<<blocks(n_out), NT, 0, st>>>(B, H, W, C, s, (const float*)x, wsave, (const float*)dout, (float*)denc);
+        if (s == 4) CSU_CE(float, 4); else CSU_CE(float, 2);
         carafe_bwd_x<float><<<blocks(n_in), NT, 0, st>>>(B, H, W, C, s, wsave, (const float*)dout, (float*)dx);
     } else {
         return fail(CSU_E_ARG, "carafe_bwd: bad dtype");
     }
+#undef CSU_CE
     return check_launch("carafe_bwd");
 }
 

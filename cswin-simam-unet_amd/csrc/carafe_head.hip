@@ -265,24 +265,37 @@ int check_head(int B, int H, int W, int C, int s) {
 
 // Output-head weight folding (cswin:674-688): the CARAFE `out` 1x1 conv (O x C weight w_out, bias
 // b_out) followed by the bias-free 1-class `output` conv (w_h, O) is linear, so the fused head
-// uses u = w_out^T w_h (C) and cb = w_h . b_out.  One block; fixed-order sums.
+// uses u = w_out^T w_h (C) and cb = w_h . b_out.  One block: four o-quarters per column with 8
+// loads in flight each (a serial per-thread loop over O paid one L2 round trip per term: 28 us),
+// combined in a fixed order.  C <= 512 (check_head).
 __global__ __launch_bounds__(NT) void head_fold_fwd(int O, int C, const float* __restrict__ w_out,
                                                     const float* __restrict__ b_out, const float* __restrict__ w_h,
                                                     float* __restrict__ u, float* __restrict__ cb) {
-    for (int c = threadIdx.x; c < C; c += NT) {
+    __shared__ float red[4][512];
+    __shared__ float rb[NT];
+    const int q = threadIdx.x >> 6, l = threadIdx.x & 63;
+    const int per = (O + 3) / 4, o0 = q * per, o1 = min(O, o0 + per);
+    for (int c = l; c < C; c += 64) {
         float a = 0.f;
-        for (int o = 0; o < O; ++o) a = fmaf(w_out[(long)o * C + c], w_h[o], a);
-        u[c] = a;
+#pragma unroll 8
+        for (int o = o0; o < o1; ++o) a = fmaf(w_out[(long)o * C + c], w_h[o], a);
+        red[q][c] = a;
     }
-    if (threadIdx.x == 0) {
-        float a = 0.f;
-        for (int o = 0; o < O; ++o) a = fmaf(w_h[o], b_out[o], a);
-        cb[0] = a;
+    float bsum = 0.f;   // cb partial of thread t: o = t, t + NT, ...
+    for (int o = threadIdx.x; o < O; o += NT) bsum = fmaf(w_h[o], b_out[o], bsum);
+    rb[threadIdx.x] = bsum;
+    __syncthreads();
+    for (int c = threadIdx.x; c < C; c += NT) u[c] = (red[0][c] + red[1][c]) + (red[2][c] + red[3][c]);
+    if (threadIdx.x < 64) {   // fixed-order tree over the NT partials
+        float v = (rb[threadIdx.x] + rb[threadIdx.x + 64]) + (rb[threadIdx.x + 128] + rb[threadIdx.x + 192]);
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+        if (threadIdx.x == 0) cb[0] = v;
     }
 }
 
 // gradients of the folding from du (C) and dcb: dw_out[o][c] = w_h[o] du[c], db_out[o] = w_h[o] dcb,
-// dw_h[o] = sum_c w_out[o][c] du[c] + b_out[o] dcb
+// dw_h[o] = sum_c w_out[o][c] du[c] + b_out[o] dcb (four lanes per o, 8 loads in flight each,
+// combined by fixed xor-shuffles)
 __global__ __launch_bounds__(NT) void head_fold_bwd(int O, int C, const float* __restrict__ w_out,
                                                     const float* __restrict__ b_out, const float* __restrict__ w_h,
                                                     const float* __restrict__ du, const float* __restrict__ dcb,
@@ -290,11 +303,20 @@ __global__ __launch_bounds__(NT) void head_fold_bwd(int O, int C, const float* _
                                                     float* __restrict__ dw_h) {
     const float g = dcb[0];
     for (long i = threadIdx.x; i < (long)O * C; i += NT) dw_out[i] = w_h[i / C] * du[i % C];
-    for (int o = threadIdx.x; o < O; o += NT) {
+    const int part = threadIdx.x & 3, per = (C + 3) / 4, c0 = part * per, c1 = min(C, c0 + per);
+    for (int ob = 0; ob < O; ob += NT / 4) {   // every lane runs every round (shuffles need the whole wave)
+        const int o = ob + (threadIdx.x >> 2);
         float a = 0.f;
-        for (int c = 0; c < C; ++c) a = fmaf(w_out[(long)o * C + c], du[c], a);
-        dw_h[o] = fmaf(b_out[o], g, a);
-        db_out[o] = w_h[o] * g;
+        if (o < O) {
+#pragma unroll 8
+            for (int c = c0; c < c1; ++c) a = fmaf(w_out[(long)o * C + c], du[c], a);
+        }
+        a += __shfl_xor(a, 1, 64);
+        a += __shfl_xor(a, 2, 64);
+        if (o < O && part == 0) {
+            dw_h[o] = fmaf(b_out[o], g, a);
+            db_out[o] = w_h[o] * g;
+        }
     }
 }
 
