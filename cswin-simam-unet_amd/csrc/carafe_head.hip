@@ -43,11 +43,15 @@ __global__ __launch_bounds__(NT) void head_z(long P, int C, const T* __restrict_
     if (q < P && g == 0) z[q] = acc;
 }
 
-__device__ __forceinline__ void neighbours(const float* __restrict__ z, int b, int y, int x, int H, int W, float* zn) {
+// z of the 9 neighbours of (b, y, x) (0 in the zero padding): branch-free raw buffer loads, all 9
+// in flight (a predicated load per tap made hipcc wait for each one)
+__device__ __forceinline__ void neighbours(const float* __restrict__ z, int b, int y, int x, int B, int H, int W, float* zn) {
+    const __amdgpu_buffer_rsrc_t rz = buf_rsrc(z, (long)B * H * W * 4);
 #pragma unroll
     for (int t = 0; t < KT; ++t) {
         const int yy = y + t / 3 - 1, xx = x + t % 3 - 1;
-        zn[t] = (yy >= 0 && yy < H && xx >= 0 && xx < W) ? z[((long)b * H + yy) * W + xx] : 0.f;
+        const bool in = yy >= 0 && yy < H && xx >= 0 && xx < W;
+        zn[t] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rz, in ? (unsigned)((((long)b * H + yy) * W + xx) * 4) : kOOB, 0, 0));
     }
 }
 
@@ -61,7 +65,7 @@ __global__ __launch_bounds__(NT) void carafe_head_fwd(int B, int H, int W, const
     if (q >= (long)B * H * W) return;
     const int x = q % W, y = (q / W) % H, b = q / ((long)H * W);
     float zn[KT];
-    neighbours(z, b, y, x, H, W, zn);
+    neighbours(z, b, y, x, B, H, W, zn);
     const float c = *cb;
     const T* e = enc + q * KT * S2;
 #pragma unroll
@@ -114,7 +118,7 @@ __global__ __launch_bounds__(NT) void carafe_head_bwd_enc(int B, int H, int W, c
     if (q < (long)B * H * W) {
         const int x = q % W, y = (q / W) % H, b = q / ((long)H * W);
         float zn[KT], tk[KT];
-        neighbours(z, b, y, x, H, W, zn);
+        neighbours(z, b, y, x, B, H, W, zn);
 #pragma unroll
         for (int t = 0; t < KT; ++t) tk[t] = 0.f;
         const T* e = enc + q * KT * S2;
@@ -199,14 +203,20 @@ __global__ __launch_bounds__(NT) void carafe_head_bwd_x(int B, int H, int W, int
     float uw[8], acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     load4(u + 8 * g, uw);
     load4(u + 8 * g + 4, uw + 4);
+    const __amdgpu_buffer_rsrc_t rt = buf_rsrc(tsum, P * KT * 4);
     for (long q = q0 + rr; q < q1; q += RPL) {
         const int xq = q % W, y = (q / W) % H, b = q / ((long)H * W);
+        float tv[KT];
+#pragma unroll
+        for (int t = 0; t < KT; ++t) {   // branch-free gathers, all 9 in flight
+            const int yy = y - (t / 3 - 1), xx = xq - (t % 3 - 1);   // q = nbr_t(q')  <=>  q' = q - off_t
+            const bool in = yy >= 0 && yy < H && xx >= 0 && xx < W;
+            tv[t] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+                rt, in ? (unsigned)(((((long)b * H + yy) * W + xx) * KT + t) * 4) : kOOB, 0, 0));
+        }
         float dz = 0.f;
 #pragma unroll
-        for (int t = 0; t < KT; ++t) {
-            const int yy = y - (t / 3 - 1), xx = xq - (t % 3 - 1);   // q = nbr_t(q')  <=>  q' = q - off_t
-            if (yy >= 0 && yy < H && xx >= 0 && xx < W) dz += tsum[(((long)b * H + yy) * W + xx) * KT + t];
-        }
+        for (int t = 0; t < KT; ++t) dz += tv[t];
         float v[8], o[8];
         load8(x + q * C + 8 * g, v);
 #pragma unroll

@@ -483,6 +483,131 @@ __global__ __launch_bounds__(MT) void mlp_bwd_kernel(long M, const bf16* __restr
 }
 
 
+// Persistent backward for C = 64 (stage 1): W1 / W2 (2 x 256 x 64 bf16 = 64 KB) stay in LDS for the
+// workgroup's lifetime -- the per-panel kernel above re-stages them for every 64-token panel (4096
+// panels at 512x512 B16: 268 MB of L2 -> LDS traffic for 67 MB of token operands).  Two teams of 4
+// waves (2 waves per SIMD) run their own panel streams through the same weight images; wave (t, u)
+// of a team has the roles of the per-panel kernel; natural chunk order.  (The forward in this form
+// measured slower than the per-panel kernel: its per-chunk work is too short to hide the token
+// loads without the DMA ring's overlap.)
+template <bool DROP>
+__global__ __launch_bounds__(2 * MT) void mlp_bwd64_persist(long M, const bf16* __restrict__ X, const bf16* __restrict__ dY,
+                                                            const bf16* __restrict__ W1, const float* __restrict__ b1,
+                                                            const bf16* __restrict__ W2, bf16* __restrict__ dH,
+                                                            bf16* __restrict__ G, bf16* __restrict__ dX, MlpDrop dd) {
+    constexpr int C = 64, NCH = 4 * C / HC, KS = C / 16, TF = C / 32, IMG = HC * C;
+    using D1 = Dma<HC, 2 * C, 8>;
+    using D2 = Dma<C, 2 * HC, 8>;
+    __shared__ __attribute__((aligned(1024))) bf16 wimg[2 * NCH * IMG];
+    __shared__ __attribute__((aligned(16))) float b1s[4 * C];
+    __shared__ __attribute__((aligned(16))) float xch[2][4 * (C / 64) * 16 * 64];
+    const int lane = threadIdx.x & 63;
+    const int wave8 = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int team = wave8 >> 2, wave = wave8 & 3;
+    const int r = lane & 31, h = lane >> 5;
+    const int t = wave >> 1, u = wave & 1;
+    const int tok = 32 * t + r;
+    const int hs = 32 * u;
+    for (int i = threadIdx.x; i < 4 * C; i += 2 * MT) b1s[i] = b1[i];
+    {
+        D1 d1;
+        D2 d2;
+        d1.init(C, wave8, lane);
+        d2.init(4 * C, wave8, lane);
+        const i32x4 rs_w1 = rsrc4(W1, 4L * C * C * 2);
+        const i32x4 rs_w2 = rsrc4(W2, 4L * C * C * 2);
+#pragma unroll
+        for (int j = 0; j < NCH; ++j) {
+            dma<D1::NW>(rs_w1, d1.v, (unsigned)j * HC * C * 2, wimg + j * IMG, wave8);
+            dma<D2::NW>(rs_w2, d2.v, (unsigned)j * HC * 2, wimg + (NCH + j) * IMG, wave8);
+        }
+        vmwait<0>();
+        lds_sync();
+    }
+    const long npan = (M + BM - 1) / BM;
+    const long mine = blockIdx.x < npan ? (npan - 1 - blockIdx.x) / gridDim.x + 1 : 0;
+    const long iters = (mine + 1) / 2;
+    DropoutRng Rh;
+    if constexpr (DROP) Rh = load_rng(dd.rng, dd.site_h, dd.p);
+    float* xc = xch[team];
+    for (long it = 0; it < iters; ++it) {
+        const long k = 2 * it + team;
+        const long m0 = (blockIdx.x + k * (long)gridDim.x) * BM;
+        const long rows = k < mine ? M - m0 : 0;
+        const long mb = rows > 0 ? m0 : 0;
+        const bool ok = tok < rows;
+        bf16x8 xf[KS], dyf[KS];
+        load_bfrags<C>(buf_rsrc(X + mb * C, rows * C * 2), tok, ok, h, xf);
+        load_bfrags<C>(buf_rsrc(dY + mb * C, rows * C * 2), tok, ok, h, dyf);
+        const auto rs_dh = buf_rsrc(dH + mb * 4 * C, rows * 4 * C * 2);
+        const auto rs_g = buf_rsrc(G + mb * 4 * C, rows * 4 * C * 2);
+        const long mg = m0 + tok;
+        f32x16 acc[TF];
+#pragma unroll
+        for (int i = 0; i < TF; ++i) acc[i] = f32x16{};
+#pragma unroll
+        for (int j = 0; j < NCH; ++j) {
+            const bf16* w1c = wimg + j * IMG;
+            const bf16* w2c = wimg + (NCH + j) * IMG;
+            f32x16 ha = f32x16{}, ga = f32x16{};
+#pragma unroll
+            for (int s2 = 0; s2 < KS; ++s2) {
+                ha = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag(w1c, moff<2 * C>(hs + r, 16 * s2 + 8 * h)), xf[s2], ha, 0, 0, 0);
+                ga = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag<2 * HC>(w2c, hs, s2, lane), dyf[s2], ga, 0, 0, 0);
+            }
+            float bv[16], gv[16], dv[16];
+            bias16(b1s, j * HC + hs, h, bv);
+            unsigned km = 0xffffu;
+            if constexpr (DROP) if (dd.p > 0.f) km = keep16_crow(Rh, ((uint64_t)mg * 4 * C + j * HC + hs) >> 3, h);
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                float dg;
+                gelu_pair_fast(ha[e] + bv[e], gv[e], dg);
+                if constexpr (DROP) {
+                    const float ms = ((km >> e) & 1u) ? Rh.scale : 0.f;
+                    gv[e] *= ms;
+                    dg *= ms;
+                }
+                dv[e] = ga[e] * dg;
+            }
+            const unsigned base = ok ? (unsigned)(tok * 4 * C + j * HC + hs + 4 * h) * 2 : kOOB;
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const unsigned o = base == kOOB ? kOOB : base + 16 * g;
+                buf_st4bf(rs_g, o, gv + 4 * g);
+                buf_st4bf(rs_dh, o, dv + 4 * g);
+            }
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) {
+                const bf16x8 db = pack_b(dv, s2);
+#pragma unroll
+                for (int ft = 0; ft < TF; ++ft)
+                    acc[ft] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ptrfrag<2 * C>(w1c, 32 * ft, hs + 16 * s2, lane), db, acc[ft], 0, 0, 0);
+            }
+        }
+        const auto rs_dx = buf_rsrc(dX + mb * C, rows * C * 2);
+        if (u == 0) {
+            exchange_half<C, 0>(acc, xc, wave, lane);
+            bwd_epilogue<C, 0>(acc, rs_dx, tok, ok, h);
+        } else {
+            exchange_half<C, 1>(acc, xc, wave, lane);
+            bwd_epilogue<C, 1>(acc, rs_dx, tok, ok, h);
+        }
+        lds_sync();
+    }
+}
+
+int persist_grid(long M) {   // one workgroup (two panel streams) per CU, fewer for small M
+    static int cus = 0;
+    if (!cus) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            cus = 256;
+    }
+    const long pan = (M + BM - 1) / BM;
+    return (int)(pan < 2L * cus ? (pan + 1) / 2 : cus);
+}
+
 template <int C>
 int fwd_launch(long M, const void* x, const void* w1, const float* b1, const void* w2, const float* b2, const float* res,
                float* out, const MlpDrop* d, long rpi, hipStream_t st) {
@@ -499,6 +624,16 @@ template <int C>
 int bwd_launch(long M, const void* x, const void* dy, const void* w1, const float* b1, const void* w2, void* dh, void* g,
                void* dx, const MlpDrop* d, long rpi, hipStream_t st) {
     const dim3 grid((unsigned)((M + BM - 1) / BM));
+    if constexpr (C == 64) {   // persistent, weights resident (mlp_bwd64_persist)
+        const dim3 pg((unsigned)persist_grid(M));
+        if (d)
+            mlp_bwd64_persist<true><<<pg, 2 * MT, 0, st>>>(M, (const bf16*)x, (const bf16*)dy, (const bf16*)w1, b1, (const bf16*)w2,
+                                                           (bf16*)dh, (bf16*)g, (bf16*)dx, *d);
+        else
+            mlp_bwd64_persist<false><<<pg, 2 * MT, 0, st>>>(M, (const bf16*)x, (const bf16*)dy, (const bf16*)w1, b1, (const bf16*)w2,
+                                                            (bf16*)dh, (bf16*)g, (bf16*)dx, MlpDrop{});
+        return check_launch("mlp_bwd");
+    }
     if (d)
         mlp_bwd_kernel<C, true><<<grid, MT, 0, st>>>(M, (const bf16*)x, (const bf16*)dy, (const bf16*)w1, b1, (const bf16*)w2,
                                                      (bf16*)dh, (bf16*)g, (bf16*)dx, *d, rpi);
