@@ -68,6 +68,20 @@ __device__ __forceinline__ float wave_sum(float v) {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     return v;
 }
+// sum of p[j], j = sub, sub + G, ... < n, four independent loads in flight per round trip (a one-load
+// loop serialises on the load latency); fixed association -- deterministic
+template <int G> __device__ __forceinline__ float strided_sum(const float* __restrict__ p, int n, int sub) {
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+    int j = sub;
+    for (; j + 3 * G < n; j += 4 * G) {
+        s0 += p[j];
+        s1 += p[j + G];
+        s2 += p[j + 2 * G];
+        s3 += p[j + 3 * G];
+    }
+    for (; j < n; j += G) s0 += p[j];
+    return (s0 + s1) + (s2 + s3);
+}
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));

@@ -140,7 +140,8 @@ __global__ __launch_bounds__(NT) void ln_fwd(int rows, int C, float eps, const T
 // dx = dres + rstd * (g*gamma - mean(g*gamma) - xhat * mean(g*gamma*xhat)); optionally also a bf16
 // copy of dx (the next GEMM's operand).  dres = the gradient reaching x through the residual branch
 // (x + f(LN(x)) of CSWinBlock, cswin:367-368): the autograd add of the two branches is fused here.
-// dgamma/dbeta: per-block partials, written [2C][nblocks] for the wave-per-value reduction.
+// dgamma/dbeta: per-block partials, written [nblocks][2C] (one coalesced row per block: the
+// [2C][nblocks] column layout's scattered 4-B stores cost 3-4 us per launch) for ln_cols_sum.
 template <typename TX, typename TG, int V, int LPR>
 __global__ __launch_bounds__(NT) void ln_bwd(int rows, int C, int rows_per_block, const TX* __restrict__ x,
                                              const float* __restrict__ gamma, const float* __restrict__ mean,
@@ -220,24 +221,45 @@ __global__ __launch_bounds__(NT) void ln_bwd(int rows, int C, int rows_per_block
         float s = 0.f;
 #pragma unroll
         for (int wv = 0; wv < WAVES; ++wv) s += red[wv][k][c];
-        part[(size_t)i * gridDim.x + blockIdx.x] = s;
+        part[(size_t)blockIdx.x * 2 * C + i] = s;
     }
 }
 
-// out[v] = sum_b part[v][b] (v < 2C: dgamma | dbeta), one wave per value, fixed order
-__global__ __launch_bounds__(NT) void ln_param_reduce(int C, int nb, const float* __restrict__ part,
+// out[v] = sum_b part[b][v] (v < 2C: dgamma | dbeta) for the 64 values v0 + lane of one workgroup
+// of RT threads: wave w sums blocks w, w + RW, ... (8 loads in flight, coalesced 256-B rows), then
+// the RW wave sums in order -- fixed association, deterministic
+constexpr int RT = 1024, RW = RT / 64;
+__device__ __forceinline__ void ln_cols_sum(const float* __restrict__ part, int C, int nb, int v0,
+                                            float* __restrict__ dgamma, float* __restrict__ dbeta) {
+    __shared__ float red[RW][64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const long ld = 2L * C;
+    const float* p = part + v0 + lane;
+    float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    int b = wave;
+    for (; b + 7 * RW < nb; b += 8 * RW)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) a[k] += p[(b + k * RW) * ld];
+    for (; b < nb; b += RW) a[0] += p[b * ld];
+    red[wave][lane] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+    __syncthreads();
+    if (wave == 0) {
+        float s = 0.f;
+#pragma unroll
+        for (int w = 0; w < RW; ++w) s += red[w][lane];
+        const int v = v0 + lane;
+        (v < C ? dgamma[v] : dbeta[v - C]) = s;
+    }
+}
+
+__global__ __launch_bounds__(RT) void ln_param_reduce(int C, int nb, const float* __restrict__ part,
                                                       float* __restrict__ dgamma, float* __restrict__ dbeta) {
-    const int v = blockIdx.x * WAVES + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-    if (v >= 2 * C) return;
-    float s = 0.f;
-    for (int b = lane; b < nb; b += 64) s += part[(size_t)v * nb + b];
-    s = wave_sum(s);
-    if (lane == 0) (v < C ? dgamma[v] : dbeta[v - C]) = s;
+    ln_cols_sum(part, C, nb, blockIdx.x * 64, dgamma, dbeta);
 }
 
 int ln_blocks(int rows, int rpw, int* rpb) {   // <= 512 blocks, rows per block a multiple of a block's row step
     const int step = WAVES * rpw * LU;
-    int r = (rows + 511) / 512;   // (2048 blocks: ln_bwd -23 us/step but ln_param_reduce +160 us/step)
+    int r = (rows + 511) / 512;   // (1024 / 2048 blocks measured no faster: tools/ln_probe.py)
     r = ((r + step - 1) / step) * step;
     *rpb = r;
     return (rows + r - 1) / r;
@@ -289,7 +311,7 @@ int launch_bwd(int rows, int C, const void* x, const float* g, const float* m, c
 #undef CSU_LNB
     if (int e = check_launch("layernorm_bwd")) return e;
     if (!dgamma) return 0;   // partials stay in the workspace: csu_layernorm_param_reduce
-    ln_param_reduce<<<(2 * C + WAVES - 1) / WAVES, NT, 0, st>>>(C, nb, part, dgamma, dbeta);
+    ln_param_reduce<<<2 * C / 64, RT, 0, st>>>(C, nb, part, dgamma, dbeta);
     return check_launch("layernorm_bwd reduce");
 }
 
@@ -360,8 +382,8 @@ extern "C" int csu_layernorm_bwd(int rows, int C, int xdtype, const void* x, con
 }
 
 // Batched parameter reduction: the item table travels as a kernel argument (no device table, so
-// a captured launch needs no host buffer); wave w of the launch handles value w - v0 of the item
-// whose value range [v0, v0 + 2C) contains it.
+// a captured launch needs no host buffer); workgroup w of the launch handles the 64-value chunk
+// w - v0 of the item whose chunk range [v0, v0 + 2C / 64) contains it.
 constexpr int LNB_MAX = 48;
 struct LnBatch {
     const float* part[LNB_MAX];
@@ -371,17 +393,11 @@ struct LnBatch {
     int count;
 };
 
-__global__ __launch_bounds__(NT) void ln_param_reduce_batch(LnBatch t) {
-    const int v = blockIdx.x * WAVES + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-    if (v >= t.v0[t.count]) return;
+__global__ __launch_bounds__(RT) void ln_param_reduce_batch(LnBatch t) {
+    const int w = blockIdx.x;
     int i = 0;
-    while (i + 1 < t.count && t.v0[i + 1] <= v) ++i;
-    const int u = v - t.v0[i], C = t.C[i], nb = t.nb[i];
-    const float* part = t.part[i];
-    float s = 0.f;
-    for (int b = lane; b < nb; b += 64) s += part[(size_t)u * nb + b];
-    s = wave_sum(s);
-    if (lane == 0) (u < C ? t.dg[i][u] : t.db[i][u - C]) = s;
+    while (i + 1 < t.count && t.v0[i + 1] <= w) ++i;
+    ln_cols_sum(t.part[i], t.C[i], t.nb[i], (w - t.v0[i]) * 64, t.dg[i], t.db[i]);
 }
 
 // dgamma / dbeta from the per-block partials a csu_layernorm_bwd_ex call with NULL dgamma/dbeta
@@ -392,8 +408,7 @@ extern "C" int csu_layernorm_param_reduce(int rows, int C, const void* workspace
     if (rows < 1 || !workspace || !dgamma || !dbeta) return fail(CSU_E_ARG, "layernorm_param_reduce: bad args");
     int rpb;
     const int nb = ln_blocks(rows, C >= 256 ? 1 : 256 / C, &rpb);
-    ln_param_reduce<<<(2 * C + WAVES - 1) / WAVES, NT, 0, as_stream(stream)>>>(C, nb, (const float*)workspace, dgamma,
-                                                                                dbeta);
+    ln_param_reduce<<<2 * C / 64, RT, 0, as_stream(stream)>>>(C, nb, (const float*)workspace, dgamma, dbeta);
     return check_launch("layernorm_param_reduce");
 }
 
@@ -414,9 +429,9 @@ extern "C" int csu_layernorm_param_reduce_batch(const csu_ln_param_item* items, 
             t.part[i] = (const float*)it.workspace;
             t.dg[i] = it.dgamma;
             t.db[i] = it.dbeta;
-            t.v0[i + 1] = t.v0[i] + 2 * it.C;
+            t.v0[i + 1] = t.v0[i] + 2 * it.C / 64;
         }
-        ln_param_reduce_batch<<<(t.v0[t.count] + WAVES - 1) / WAVES, NT, 0, as_stream(stream)>>>(t);
+        ln_param_reduce_batch<<<t.v0[t.count], RT, 0, as_stream(stream)>>>(t);
         if (int e = check_launch("layernorm_param_reduce_batch")) return e;
     }
     return 0;

@@ -809,16 +809,39 @@ int lepe_rows_blk(const csu_stripe_args& a, int ty) {
 
 // one wave per (branch, value): lanes stride over the block partials (contiguous), then a fixed
 // xor-shuffle tree -- deterministic
+// 16 lanes per value (the block partials are 32..128 per value at the model's sizes: a wave per value
+// left lanes idle and launched 4x the waves); shared with lepe_reduce_batch, so the deferred batched
+// reduction is bitwise equal to this one
+// (nblk % 4 == 0: 16-B loads of 4 consecutive partials, four in flight per lane -- the fused
+// backward leaves B * windows = 256..2048 partials per value, ~60 MB per step at 512x512 B16)
+__device__ __forceinline__ float lepe_value_sum(const float* __restrict__ src, int nblk, int sub) {
+    float s;
+    if ((nblk & 3) == 0) {
+        f32x4 a0 = {}, a1 = {}, a2 = {}, a3 = {};
+        auto ld = [&](int j) { return *reinterpret_cast<const f32x4*>(src + j); };
+        int j = 4 * sub;
+        for (; j + 192 < nblk; j += 256) {
+            a0 += ld(j);
+            a1 += ld(j + 64);
+            a2 += ld(j + 128);
+            a3 += ld(j + 192);
+        }
+        for (; j < nblk; j += 64) a0 += ld(j);
+        const f32x4 t = (a0 + a1) + (a2 + a3);
+        s = (t[0] + t[1]) + (t[2] + t[3]);
+    } else {
+        s = strided_sum<16>(src, nblk, sub);
+    }
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    return s;
+}
+
 __global__ __launch_bounds__(256) void lepe_wgrad_reduce(csu_stripe_args a, int nblk, const float* __restrict__ part) {
-    const int Cb = a.heads * HD;
-    const int v = blockIdx.x * 4 + (threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    if (v >= a.nbranch * Cb * 10) return;
-    const float* src = part + (size_t)v * nblk;
-    float s = 0.f;
-    for (int j = lane; j < nblk; j += 64) s += src[j];
-    s = wave_sum(s);
-    if (lane == 0) {
+    const int Cb = a.heads * HD, vt = a.nbranch * Cb * 10;
+    const int v = blockIdx.x * 16 + (threadIdx.x >> 4), sub = threadIdx.x & 15;
+    const float s = lepe_value_sum(part + (size_t)(v < vt ? v : vt - 1) * nblk, nblk, sub);
+    if (sub == 0 && v < vt) {
         const int br = v / (Cb * 10), i = v % (Cb * 10);
         const csu_stripe_branch& g = branch(a, br);
         const int c = i / 10, k = i % 10;
@@ -1853,27 +1876,26 @@ int lepe_nblk(const csu_stripe_args& a, int dtype) {
 }
 
 // many LePE weight-gradient reductions in one launch (the end-of-backward batch): item table in the
-// kernel arguments, wave w -> (item, value) by a scan over the value prefix sums
+// kernel arguments, 16-value workgroup -> (item, values) by a scan over the value prefix sums
 constexpr int LPB_MAX = 32;
 struct LpBatch {
     const float* part[LPB_MAX];
     float* dw[LPB_MAX][2];
     float* db[LPB_MAX][2];
-    int nblk[LPB_MAX], cb[LPB_MAX], v0[LPB_MAX + 1];
+    int nblk[LPB_MAX], cb[LPB_MAX], nbranch[LPB_MAX], v0[LPB_MAX + 1];
     int count;
 };
 
+// lanes as lepe_wgrad_reduce; each item's value range starts on a multiple of 16 (v0), so the
+// workgroup's item is found by a uniform scan on blockIdx (scalar loads of the item table)
 __global__ __launch_bounds__(256) void lepe_reduce_batch(LpBatch t) {
-    const int v = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-    if (v >= t.v0[t.count]) return;
+    const int w0 = blockIdx.x * 16;
     int i = 0;
-    while (i + 1 < t.count && t.v0[i + 1] <= v) ++i;
-    const int u = v - t.v0[i], nblk = t.nblk[i], Cb = t.cb[i];
-    const float* src = t.part[i] + (size_t)u * nblk;
-    float s = 0.f;
-    for (int j = lane; j < nblk; j += 64) s += src[j];
-    s = wave_sum(s);
-    if (lane == 0) {
+    while (i + 1 < t.count && t.v0[i + 1] <= w0) ++i;
+    const int nblk = t.nblk[i], Cb = t.cb[i], nv = t.nbranch[i] * Cb * 10;
+    const int u = w0 - t.v0[i] + (threadIdx.x >> 4), sub = threadIdx.x & 15;
+    const float s = lepe_value_sum(t.part[i] + (size_t)(u < nv ? u : nv - 1) * nblk, nblk, sub);
+    if (sub == 0 && u < nv) {
         const int br = u / (Cb * 10), r = u % (Cb * 10), c = r / 10, k = r % 10;
         float* dw = br ? t.dw[i][1] : t.dw[i][0];
         float* db = br ? t.db[i][1] : t.db[i][0];
@@ -1899,7 +1921,7 @@ void lepe_wgrad_launch(const csu_stripe_args& a, int dtype, const void* qkv, con
         lepe_wgrad_partial<float><<<dim3(nblk, a.nbranch), NT, 0, st>>>(a, (const float*)qkv, (const float*)dout, part);
     }
     if (!reduce) return;
-    const dim3 rgrid((a.nbranch * a.heads * HD * 10 + 3) / 4);
+    const dim3 rgrid((a.nbranch * a.heads * HD * 10 + 15) / 16);
     lepe_wgrad_reduce<<<rgrid, 256, 0, st>>>(a, nblk, part);
 }
 
@@ -1935,7 +1957,7 @@ extern "C" int csu_stripe_lepe_reduce_batch(const csu_lepe_reduce_item* items, i
     t.v0[0] = 0;
     auto flush = [&]() -> int {
         if (!t.count) return 0;
-        lepe_reduce_batch<<<(unsigned)((t.v0[t.count] + 3) / 4), 256, 0, as_stream(stream)>>>(t);
+        lepe_reduce_batch<<<(unsigned)((t.v0[t.count] + 15) / 16), 256, 0, as_stream(stream)>>>(t);
         t.count = 0;
         return check_launch("stripe_lepe_reduce_batch");
     };
@@ -1952,7 +1974,8 @@ extern "C" int csu_stripe_lepe_reduce_batch(const csu_lepe_reduce_item* items, i
         t.db[k][0] = it.db[0]; t.db[k][1] = it.nbranch > 1 ? it.db[1] : it.db[0];
         t.nblk[k] = it.nblk;
         t.cb[k] = it.channels;
-        t.v0[k + 1] = t.v0[k] + it.nbranch * it.channels * 10;
+        t.nbranch[k] = it.nbranch;
+        t.v0[k + 1] = t.v0[k] + (it.nbranch * it.channels * 10 + 15) / 16 * 16;
         t.count = k + 1;
     }
     return flush();
@@ -1985,7 +2008,7 @@ extern "C" int csu_stripe_attn_bwd_ex(const csu_stripe_args* a, int dtype, const
         if (a->br[0].H_sp * a->br[0].W_sp <= 128) bwd_fused<128>(*a, q, o, go, lse, (bf16*)dqkv, pp, st);
         else bwd_fused<256>(*a, q, o, go, lse, (bf16*)dqkv, pp, st);
         if (do_lepe && !lepe_deferred) {
-            const dim3 rgrid((a->nbranch * a->heads * HD * 10 + 3) / 4);
+            const dim3 rgrid((a->nbranch * a->heads * HD * 10 + 15) / 16);
             lepe_wgrad_reduce<<<rgrid, 256, 0, st>>>(*a, fused_nblk(*a), part);
         }
         return check_launch("stripe_attn_bwd");
