@@ -282,7 +282,7 @@ def _deferrable(*params) -> bool:
 def deferred_pending() -> bool:
     """Parameter gradients of the running backward pass that are filled only by the end-of-backward
     flush (LayerNorm dgamma / dbeta, token-Linear dW / db, LePE dW / db)."""
-    return bool(_LN_PENDING or _WG_DEFER or _WG_PENDING or _LEPE_PENDING)
+    return bool(_LN_PENDING or _WG_DEFER or _WG_PENDING or _WG_POST or _LEPE_PENDING)
 
 
 def _ln_param_flush():
@@ -353,6 +353,7 @@ DEFER_WGRAD = _os.environ.get("CSU_DEFER_WGRAD", "1") == "1"
 GROUP_WGRAD = _os.environ.get("CSU_GROUP_WGRAD", "1") == "1"   # 0: deferred slab sums only (A/B)
 _WG_PENDING: list = []   # (WslabItem, out, workspace): reductions of tile kernels already launched
 _WG_DEFER: list = []     # (dy2, x2, out): whole weight gradients deferred to the grouped launch
+_WG_POST: list = []      # callables run after the deferred weight gradients are complete
 
 
 def _wgrad_flush():
@@ -382,6 +383,7 @@ def _wgrad_flush():
         _launch("linear_wgrad", lambda: L.csu_linear_wgrad_group(gitems, len(defer), stream_ptr(dev)), flops, nbytes)
     pend, _WG_PENDING[:] = list(_WG_PENDING), []
     if not pend:
+        _wgrad_post()
         return
     dev = pend[0][1].device
     items = (_lib.WslabItem * len(pend))()
@@ -390,6 +392,13 @@ def _wgrad_flush():
         items[i] = it
         nbytes += it.chunks * (it.N * it.K + it.N) * 4 + (it.N * it.K + it.N) * 4
     _launch("linear_wgrad", lambda: lib().csu_wslab_reduce_batch(items, len(pend), stream_ptr(dev)), 0, nbytes)
+    _wgrad_post()
+
+
+def _wgrad_post():
+    post, _WG_POST[:] = list(_WG_POST), []
+    for fn in post:
+        fn()
 
 
 def _wgrad_deferrable(dy2, wdt, bdt, params) -> bool:
@@ -1211,10 +1220,27 @@ def shared_cast(x: torch.Tensor, dtype: torch.dtype):
     return _SharedCastFn.apply(x, dtype)
 
 
-def _concat_wgrad(dy2, a2, b2):
-    dwa, db = linear_wgrad(dy2, a2)
-    dwb, _ = linear_wgrad(dy2, b2)
-    return torch.cat([dwa, dwb], 1), db
+def _concat_wgrad(dy2, a2, b2, defer: bool = False, dest=None):
+    """(dW (N, Ca + Cb), db) of the concat Linear.  ``defer``: both halves join the end-of-backward
+    grouped launch and are joined into dW (returned now) after it (_WG_POST); ``dest``: the params'
+    [dW | db] gradient-bucket slice (_grad_dest) the join writes."""
+    dwa, db = linear_wgrad(dy2, a2, defer=defer)
+    dwb, _ = linear_wgrad(dy2, b2, defer=defer)
+    if not defer:
+        return torch.cat([dwa, dwb], 1), db
+    # the join holds only the base buffers: the returned views must be sole references, so that
+    # AccumulateGrad steals them as .grad instead of copying them now (before the join)
+    N, K = dwa.shape[0], dwa.shape[1] + dwb.shape[1]
+    if dest is None:
+        buf = torch.empty(N * K, dtype=torch.float32, device=dy2.device)
+        _WG_POST.append(lambda: torch.cat([dwa, dwb], 1, out=buf.view(N, K)))
+        return buf.view(N, K), db
+
+    def join():
+        torch.cat([dwa, dwb], 1, out=dest[:N * K].view(N, K))
+        dest[N * K:].copy_(db)
+    _WG_POST.append(join)
+    return dest[:N * K].view(N, K), dest[N * K:]
 
 
 class _ConcatLinearFn(torch.autograd.Function):
@@ -1247,7 +1273,9 @@ class _ConcatLinearFn(torch.autograd.Function):
         dy2 = _bf16_of(dy).reshape(-1, dy.shape[-1]).contiguous()
         da = gemm(dy2, wt[:Ca], False, adt).view(ashape) if ctx.needs_input_grad[0] else None
         db_in = gemm(dy2, wt[Ca:], False, bdt_in).view(bshape) if ctx.needs_input_grad[1] else None
-        if _side_ok(dy2, wdt, bdt, params=ctx.params):
+        if _wgrad_deferrable(dy2, wdt, bdt, ctx.params):
+            dw, dbias = _concat_wgrad(dy2, a2, b2, defer=True, dest=_grad_dest(ctx.params))
+        elif _side_ok(dy2, wdt, bdt, params=ctx.params):
             dw, dbias = _side_run(lambda: _concat_wgrad(dy2, a2, b2), dy2, a2, b2)
         else:
             dw, dbias = _concat_wgrad(dy2, a2, b2)

@@ -18,14 +18,19 @@ def t(fn, n=20):
     return a.elapsed_time(b) / n * 1e3
 
 
-for B, reso, C, heads, sw in [(16, 32, 256, 8, 8), (16, 64, 128, 4, 2), (16, 128, 64, 2, 1), (16, 16, 512, 16, 16),
-                              (4, 64, 256, 8, 8), (4, 256, 64, 2, 1)]:
+# NOLEPE=1: LePE weights without gradients (no weight-gradient partials in the backward)
+LEPE_GRAD = os.environ.get("NOLEPE", "0") != "1"
+SHAPES = [(16, 32, 256, 8, 8), (16, 64, 128, 4, 2), (16, 128, 64, 2, 1), (16, 16, 512, 16, 16),
+          (4, 64, 256, 8, 8), (4, 256, 64, 2, 1)]
+if os.environ.get("ONLY"):
+    SHAPES = [SHAPES[int(i)] for i in os.environ["ONLY"].split(",")]
+for B, reso, C, heads, sw in SHAPES:
     nb = 1 if sw == reso else 2
     brs = [(reso, sw, 0), (sw, reso, C // 2)] if nb == 2 else [(reso, reso, 0)]
     geom = ops.StripeGeometry(reso, C, heads // nb, brs, 32 ** -0.5)
     qkv = torch.randn(B, reso * reso, 3 * C, device=d, dtype=torch.bfloat16, requires_grad=True)
-    ws = [torch.randn(C // nb, 1, 3, 3, device=d, requires_grad=True) for _ in range(nb)]
-    bs = [torch.randn(C // nb, device=d, requires_grad=True) for _ in range(nb)]
+    ws = [torch.randn(C // nb, 1, 3, 3, device=d, requires_grad=LEPE_GRAD) for _ in range(nb)]
+    bs = [torch.randn(C // nb, device=d, requires_grad=LEPE_GRAD) for _ in range(nb)]
     g = torch.randn(B, reso * reso, C, device=d, dtype=torch.bfloat16)
     f = t(lambda: ops.stripe_attention(qkv, geom, ws, bs))
     def fb():
