@@ -367,43 +367,71 @@ __global__ __launch_bounds__(NT, 2) void wgrad_group(WgGroup g) {
                                g.dst[i], g.slab[i]);
 }
 
-// dst[n][k] = sum_c slab[tile(n, k)][c][n % TN][k % TK] (c = 0 .. chunks-1 in order), then
-// dst[N*K + n] = sum_c bslab[n / TN][c][n % TN].  One thread per 4 outputs (e = first output).
-__device__ __forceinline__ void wslab_sum4(long e, int N, int K, int TN, int TK, int chunks,
-                                           const float* __restrict__ slab, float* __restrict__ dst) {
+// dst[n][k] = sum_c slab[tile(n, k)][c][n % TN][k % TK], then dst[N*K + n] = sum_c bslab[n / TN][c][n % TN].
+// A workgroup = NT / G output quads x G chunk groups: group g sums chunks g, g + G, ... (four 16-B
+// loads in flight), then group 0 adds the G partials in order -- fixed association, deterministic.
+// G grows with the chunk count: a Linear with ~170 chunks (stage 1, 262144 tokens) and few outputs
+// otherwise serialises ~40 load round trips on a few thousand threads.
+__host__ __device__ inline int wslab_groups(int chunks) {
+    int g = 1;
+    while (g < 16 && g * 8 < chunks) g <<= 1;
+    return g;
+}
+inline long wslab_blocks(int N, int K, int chunks) {
+    const long quads = ((long)N * K + N) / 4, qb = NT / wslab_groups(chunks);
+    return (quads + qb - 1) / qb;
+}
+
+__device__ __forceinline__ void wslab_sum(long blk, int N, int K, int TN, int TK, int chunks,
+                                          const float* __restrict__ slab, float* __restrict__ dst) {
+    __shared__ f32x4 red[NT];
+    const int G = wslab_groups(chunks), QB = NT / G;
+    const int g = threadIdx.x / QB, qi = threadIdx.x % QB;
+    const long e = (blk * QB + qi) * 4;   // first of the thread's 4 outputs
     const long NK = (long)N * K;
     const int kt = (K + TK - 1) / TK, nt = (N + TN - 1) / TN;
     const long step = (long)TN * TK;
-    const float* p;
-    long stride;
+    const float* p = slab;
+    long stride = 0;
+    const bool valid = e < NK + N;
     if (e < NK) {
         const int n = (int)(e / K), k = (int)(e % K);
         const long tile = (long)(n / TN) * kt + k / TK;
         p = slab + tile * chunks * step + (long)(n % TN) * TK + (k % TK);
         stride = step;
-    } else if (e < NK + N) {
+    } else if (valid) {
         const int n = (int)(e - NK);
         p = slab + (long)nt * kt * chunks * step + ((long)(n / TN) * chunks) * TN + (n % TN);
         stride = TN;
-    } else {
+    }
+    f32x4 a0 = {}, a1 = {}, a2 = {}, a3 = {};
+    if (valid) {
+        int c = g;
+        for (; c + 3 * G < chunks; c += 4 * G) {
+            a0 += *reinterpret_cast<const f32x4*>(p + c * stride);
+            a1 += *reinterpret_cast<const f32x4*>(p + (c + G) * stride);
+            a2 += *reinterpret_cast<const f32x4*>(p + (c + 2 * G) * stride);
+            a3 += *reinterpret_cast<const f32x4*>(p + (c + 3 * G) * stride);
+        }
+        for (; c < chunks; c += G) a0 += *reinterpret_cast<const f32x4*>(p + c * stride);
+    }
+    const f32x4 s = (a0 + a1) + (a2 + a3);
+    if (G == 1) {
+        if (valid) *reinterpret_cast<f32x4*>(dst + e) = s;
         return;
     }
-    f32x4 s = *reinterpret_cast<const f32x4*>(p);
-    int c = 1;
-    for (; c + 3 < chunks; c += 4) {   // 4 loads in flight, added in chunk order
-        const f32x4 v1 = *reinterpret_cast<const f32x4*>(p + c * stride);
-        const f32x4 v2 = *reinterpret_cast<const f32x4*>(p + (c + 1) * stride);
-        const f32x4 v3 = *reinterpret_cast<const f32x4*>(p + (c + 2) * stride);
-        const f32x4 v4 = *reinterpret_cast<const f32x4*>(p + (c + 3) * stride);
-        s += v1; s += v2; s += v3; s += v4;
+    red[threadIdx.x] = s;
+    __syncthreads();
+    if (g == 0 && valid) {
+        f32x4 t = red[qi];
+        for (int j = 1; j < G; ++j) t += red[j * QB + qi];
+        *reinterpret_cast<f32x4*>(dst + e) = t;
     }
-    for (; c < chunks; ++c) s += *reinterpret_cast<const f32x4*>(p + c * stride);
-    *reinterpret_cast<f32x4*>(dst + e) = s;
 }
 
 __global__ __launch_bounds__(NT) void wslab_reduce(int N, int K, int TN, int TK, int chunks,
                                                    const float* __restrict__ slab, float* __restrict__ dst) {
-    wslab_sum4(((long)blockIdx.x * NT + threadIdx.x) * 4, N, K, TN, TK, chunks, slab, dst);
+    wslab_sum(blockIdx.x, N, K, TN, TK, chunks, slab, dst);
 }
 
 // many deferred slab reductions in one launch: item table in the kernel arguments (capturable),
@@ -420,8 +448,7 @@ __global__ __launch_bounds__(NT) void wslab_reduce_batch(WsBatch t) {
     const int b = blockIdx.x;
     int i = 0;
     while (i + 1 < t.count && t.b0[i + 1] <= b) ++i;
-    wslab_sum4(((long)(b - t.b0[i]) * NT + threadIdx.x) * 4, t.N[i], t.K[i], t.tn[i], t.tk[i], t.chunks[i], t.slab[i],
-               t.dst[i]);
+    wslab_sum(b - t.b0[i], t.N[i], t.K[i], t.tn[i], t.tk[i], t.chunks[i], t.slab[i], t.dst[i]);
 }
 
 int num_cus() {
@@ -516,8 +543,7 @@ int run_bf16(const Plan& p, long M, int N, int K, const bf16* dy, const bf16* x,
     else return fail(CSU_E_ARG, "linear_wgrad: tile must be 64 or 128");
     if (int e = check_launch("linear_wgrad")) return e;
     if (p.chunks > 1 && !defer) {
-        const long outs = ((long)N * K + N) / 4;
-        wslab_reduce<<<(unsigned)((outs + NT - 1) / NT), NT, 0, st>>>(N, K, p.tn, p.tk, p.chunks, slab, dst);
+        wslab_reduce<<<(unsigned)wslab_blocks(N, K, p.chunks), NT, 0, st>>>(N, K, p.tn, p.tk, p.chunks, slab, dst);
         return check_launch("linear_wgrad reduce");
     }
     return 0;
@@ -671,7 +697,7 @@ extern "C" int csu_wslab_reduce_batch(const csu_wslab_item* items, int count, vo
         const csu_wslab_item& it = items[i];
         if (it.chunks <= 1) continue;   // written by the tile kernel itself
         if (!it.slab || !it.dst || it.N % 4 || it.K % 4) return fail(CSU_E_ARG, "wslab_reduce_batch: bad item");
-        const long blocks = (((long)it.N * it.K + it.N) / 4 + NT - 1) / NT;
+        const long blocks = wslab_blocks(it.N, it.K, it.chunks);
         if (t.count == WSB_MAX || (long)t.b0[t.count] + blocks > (1L << 30))
             if (int e = flush()) return e;
         const int c = t.count;
