@@ -1417,11 +1417,15 @@ int wd_pick(const csu_conv_geom* gm, int dtype, int cfg) {
     // for the 3x3 stride-1 convs it takes (MFMA busy 31-34 % with 128 output channels per workgroup,
     // 20 % with 64, against 9-17 % for v2); otherwise the 8-wave 256 x 128 tile at N >= 256 (24-26 %),
     // the 2-stage 128 x 128 tile at N = 128 with C <= 64 (the ConvTranspose2d gradients); v2 for the
-    // rest (64 output channels: both staged operands too narrow for the gathered DMA tiles)
+    // rest (64 output channels: both staged operands too narrow for the gathered DMA tiles), except
+    // the few-channel inputs with a wide K (the CSWin patch embed 8 x 7 x 7 -> 64: 79.6 -> 72.6 us,
+    // the CARAFE4 encoder 16 x 3 x 3 -> 144: 86.4 -> 73.2 us, profiles/r03v_wgrad_probe_cswin.txt),
+    // which take the 128 x 128 tile
     if (halo_ok(gm, 128)) return kHalo128;
     if (halo_ok(gm, 64)) return kHalo64;
     if (gm->N >= 256 && gm->N % 128 == 0) return 3;
     if (gm->N == 128 && gm->C <= 64) return 2;
+    if (gm->C <= 16 && gm->KH * gm->KW * gm->C >= 128) return 2;
     return -1;
 }
 
