@@ -107,11 +107,7 @@ int colsum_launch(long rows, long cols, int dtype, const void* in, float* out, f
 // contiguous range of logical tiles: tiles that share an operand panel (consecutive logical ids)
 // then run concurrently on one XCD and the panel is fetched from HBM once into that XCD's L2.
 constexpr int kXcds = 8;
-#ifdef CSU_NO_ROT   // A/B build: the fused Mlp's hidden chunks in natural order
-constexpr bool kRot = false;
-#else
 constexpr bool kRot = true;   // rotate the fused Mlp's hidden-chunk order (spreads concurrent L2 reads)
-#endif
 __device__ __forceinline__ long xcd_tile(long id, long total) {
     const long q = total / kXcds, rem = total % kXcds;
     const long x = id % kXcds, k = id / kXcds;

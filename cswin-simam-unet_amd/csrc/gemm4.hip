@@ -58,17 +58,9 @@ __device__ __forceinline__ void g4_voff(int ld, int wave, int lane, unsigned* vo
 template <int ROWS, int NWV = 4>
 __device__ __forceinline__ void g4_dma(i32x4 rs, const unsigned* voff, unsigned soff, bf16* img, int wave) {
     constexpr int NI = ROWS / (8 * NWV);
-#ifdef G4_BUILTIN_DMA
-    const __amdgpu_buffer_rsrc_t r = __builtin_bit_cast(__amdgpu_buffer_rsrc_t, rs);
-#pragma unroll
-    for (int i = 0; i < NI; ++i)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)(img + (wave * NI + i) * 8 * G4_BK),
-                                                 16, voff[i], soff, 0, 0);
-#else
     // inline asm (lds_dma.hpp): the compiler would otherwise wait vmcnt(0) before LDS reads that may
     // alias an in-flight DMA stage, which makes every ring deeper than 2 stages useless
     dma<NI>(rs, voff, soff, img, wave);   // same lane-linear 1-KB blocks: (wave * NI + i) * 512
-#endif
 }
 
 template <int N> __device__ __forceinline__ void g4_vmwait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }

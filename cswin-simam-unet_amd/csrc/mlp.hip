@@ -218,9 +218,7 @@ __global__ __launch_bounds__(MT) void mlp_fwd_kernel(long M, const bf16* __restr
         bf16x8 wf[KS];
 #pragma unroll
         for (int s = 0; s < KS; ++s) wf[s] = frag(img, moff<2 * C>(hs + r, 16 * s + 8 * h));
-#ifndef MLP_NO_PREF
         __builtin_amdgcn_sched_barrier(0);   // every fragment read in flight before the first MFMA
-#endif
         f32x16 a = f32x16{};
 #pragma unroll
         for (int s = 0; s < KS; ++s) a = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[s], xf[s], a, 0, 0, 0);
@@ -259,7 +257,6 @@ __global__ __launch_bounds__(MT) void mlp_fwd_kernel(long M, const bf16* __restr
         const bf16* w2c = w2r + P * IMG;
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) {
-#ifndef MLP_NO_PREF
             bf16x8 wf2[TF];
 #pragma unroll
             for (int ft = 0; ft < TF; ++ft) wf2[ft] = pfrag<2 * HC>(w2c, 32 * ft + r, hs + 16 * s2, h);
@@ -267,12 +264,6 @@ __global__ __launch_bounds__(MT) void mlp_fwd_kernel(long M, const bf16* __restr
             const bf16x8 gb = pack_b(gv, s2);
 #pragma unroll
             for (int ft = 0; ft < TF; ++ft) acc[ft] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf2[ft], gb, acc[ft], 0, 0, 0);
-#else
-            const bf16x8 gb = pack_b(gv, s2);
-#pragma unroll
-            for (int ft = 0; ft < TF; ++ft)
-                acc[ft] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pfrag<2 * HC>(w2c, 32 * ft + r, hs + 16 * s2, h), gb, acc[ft], 0, 0, 0);
-#endif
         }
     };
     int j = 0;
@@ -356,7 +347,6 @@ __global__ __launch_bounds__(MT) void mlp_bwd_kernel(long M, const bf16* __restr
     auto gemm13 = [&](const bf16* w1c, const bf16* w2c, f32x16& ha, f32x16& ga) {
         ha = f32x16{};
         ga = f32x16{};
-#ifndef MLP_NO_PREF
         // fragments of KS/2 k-steps in flight before their MFMAs (two halves: register budget)
         constexpr int KP = KS / 2;
 #pragma unroll
@@ -374,13 +364,6 @@ __global__ __launch_bounds__(MT) void mlp_bwd_kernel(long M, const bf16* __restr
                 ga = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[s], dyf[s0 + s], ga, 0, 0, 0);
             }
         }
-#else
-#pragma unroll
-        for (int s = 0; s < KS; ++s) {
-            ha = __builtin_amdgcn_mfma_f32_32x32x16_bf16(frag(w1c, moff<2 * C>(hs + r, 16 * s + 8 * h)), xf[s], ha, 0, 0, 0);
-            ga = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trfrag<2 * HC>(w2c, hs, s, lane), dyf[s], ga, 0, 0, 0);
-        }
-#endif
     };
     f32x16 acc[TF];
 #pragma unroll
@@ -415,18 +398,12 @@ __global__ __launch_bounds__(MT) void mlp_bwd_kernel(long M, const bf16* __restr
 #pragma unroll
         for (int s2 = 0; s2 < 2; ++s2) {
             const bf16x8 db = pack_b(dv, s2);
-#ifndef MLP_NO_PREF
             bf16x8 fw[TF];
 #pragma unroll
             for (int ft = 0; ft < TF; ++ft) fw[ft] = ptrfrag<2 * C>(w1c, 32 * ft, hs + 16 * s2, lane);
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int ft = 0; ft < TF; ++ft) acc[ft] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fw[ft], db, acc[ft], 0, 0, 0);
-#else
-#pragma unroll
-            for (int ft = 0; ft < TF; ++ft)
-                acc[ft] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ptrfrag<2 * C>(w1c, 32 * ft, hs + 16 * s2, lane), db, acc[ft], 0, 0, 0);
-#endif
         }
     };
     f32x16 ha, ga;

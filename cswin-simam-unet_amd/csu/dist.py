@@ -68,11 +68,12 @@ class GradAllReduce:
     cut only between modules (``named_parameters()`` input) so such groups never straddle two.
     Post-accumulate-grad hooks count each bucket's gradients; a complete bucket is all-reduced on a
     side stream while backward continues (any gradient that did not land in place -- e.g. a conv
-    weight -- is copied in by one multi-tensor copy first).  ``finish()`` (after ``backward()``,
-    before ``optimizer.step()``) launches every bucket still pending (buckets that completed while
-    csu still held deferred parameter gradients, which its end-of-backward flush writes), joins the
-    side stream and points every ``p.grad`` at its averaged slice, which the optimizer reads in
-    place.  Every call is a stream operation, so the sequence is recorded into a graph on capture and
+    weight -- is copied in by one multi-tensor copy first).  Gradients csu defers to grouped launches
+    (LayerNorm, token-Linear and LePE parameter gradients) are written by ``ops.flush_deferred()``
+    when the bucket completes, before its launch, so every bucket but the last starts during backward
+    (``last_early`` counts them).  ``finish()`` (after ``backward()``, before ``optimizer.step()``)
+    launches any bucket still pending, joins the side stream and points every ``p.grad`` at its
+    averaged slice, which the optimizer reads in place.  Every call is a stream operation, so the sequence is recorded into a graph on capture and
     replayed with one launch per step (RCCL collectives are capturable once the communicator exists:
     run one eager step first).
 
@@ -89,6 +90,7 @@ class GradAllReduce:
         pairs = [(n, p) for n, p in pairs if p.requires_grad]
         self.params = [p for _, p in pairs]
         self.last_copied = 0
+        self.last_early = 0
         if not self.params:
             raise ValueError("GradAllReduce: no trainable parameters")
         if grad_dtype not in (torch.float32, torch.bfloat16):
@@ -136,14 +138,20 @@ class GradAllReduce:
         self.launched = [False] * len(self.buckets)
         self.held = []     # gradients read on the side stream: alive until finish() joined it
         self._copied = 0   # gradients of this step that did not land in their bucket view
+        self._early = 0    # buckets launched from a hook (during backward) this step
 
     def _hook(self, p):
         bi = self.where[id(p)]
         self.pending[bi] -= 1
-        # a bucket whose gradients may still be filled by csu's end-of-backward flush (deferred
-        # weight / LayerNorm / LePE gradients) is launched by finish(), after that flush
-        if self.pending[bi] == 0 and not self._ops.deferred_pending():
+        if self.pending[bi] == 0:
+            # the bucket's last gradient has been accumulated, but csu may still hold some of its
+            # values deferred (LayerNorm dgamma / dbeta, token-Linear dW / db, LePE dW / db are
+            # written by grouped launches): write everything deferred so far, then start the bucket's
+            # all-reduce on the side stream while backward continues
+            if self._ops.deferred_pending():
+                self._ops.flush_deferred()
             self._launch(bi)
+            self._early += 1
 
     def _launch(self, bi):
         grads = []
@@ -192,6 +200,7 @@ class GradAllReduce:
             for p, v in zip(b, vs):
                 p.grad = v
         self.last_copied = self._copied   # how many gradients of the step needed the copy-in
+        self.last_early = self._early     # how many buckets started during backward (overlapped)
         self._reset()
 
     def remove(self):

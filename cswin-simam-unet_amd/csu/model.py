@@ -5,7 +5,8 @@ are those of the reference, so reference ``.pth`` files load unchanged (cswin:99
 ``model.apply(model._init_weights)`` reproduces the reference initialisation (cswin:605-614).
 Forward passes run the hand-written gfx950 kernels of libcsu_hip.so (``csu.ops``) on
 token-major (B, L, C) = NHWC activations; the dense projections (qkv/proj/fc1/fc2/concat_linear)
-and the remaining convolutions run on the platform GEMM/conv libraries (hipBLASLt/MIOpen).
+run on csu's token GEMMs and the convolutions on its implicit-GEMM NHWC kernels (no vendor GEMM /
+conv library on the path).
 
 Precision policy (bf16 under ``torch.autocast('cuda', torch.bfloat16)``, the BASELINE setting):
 residual stream fp32; LayerNorm emits the GEMM's input dtype directly; attention, MLP and
@@ -19,7 +20,6 @@ from typing import List, Optional
 import numpy as np
 import torch
 import torch.nn as nn
-import torch.nn.functional as F
 
 from . import ops, rng
 from .simam import SimAM
@@ -501,8 +501,12 @@ class CSWinTransformer(nn.Module):
         H = W = int(math.isqrt(new_HW))
         x = self.upsample1(x)                                             # (B, 16 L, 64) tokens
         w = self.output.weight.reshape(self.num_classes, -1)
-        logits = F.linear(x, w)
-        return logits.transpose(1, 2).reshape(B, self.num_classes, 4 * H, 4 * W)
+        nc = self.num_classes
+        n8 = (nc + 7) // 8 * 8        # csu token GEMM: output features padded to a multiple of 8
+        if n8 != nc:
+            w = torch.cat([w, w.new_zeros(n8 - nc, w.shape[1])], 0)
+        logits = ops.linear(x, w)[..., :nc]
+        return logits.transpose(1, 2).reshape(B, nc, 4 * H, 4 * W)
 
     def _linear_weights(self):
         """Weights the bf16 cast cache shadows: every nn.Linear and the CARAFE 1x1 convs that run

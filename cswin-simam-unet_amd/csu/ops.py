@@ -3,13 +3,12 @@ kernel; there is no CPU or eager-PyTorch fallback (CPU tensors raise ``CsuError`
 from __future__ import annotations
 
 import ctypes
-import os as _os
 from typing import List, Optional, Sequence, Tuple
 
 import torch
 
 from . import _lib
-from ._lib import CSU_F32, check, dtype_code, lib, ptr, require_device, stream_ptr
+from ._lib import CSU_F32, CsuError, check, dtype_code, lib, ptr, require_device, stream_ptr
 from .ledger import esize, launch as _launch, prec_of
 
 
@@ -223,8 +222,8 @@ def droppath_scale(B: int, p: float, site: int, device, snap: Optional[torch.Ten
 # batched launch (csu_layernorm_param_reduce_batch, queued as an end-of-backward callback) reduces
 # every LayerNorm's partials, instead of one small reduction launch per LayerNorm (58 per 512x512
 # step).  Only when nothing can read those .grad before the end of backward: no existing .grad
-# (AccumulateGrad steals the tensor) and no hooks; otherwise reduced inline.  CSU_DEFER_LN=0 disables.
-DEFER_LN = _os.environ.get("CSU_DEFER_LN", "1") == "1"
+# (AccumulateGrad steals the tensor) and no hooks; otherwise reduced inline.
+DEFER_LN = True
 _LN_PENDING: list = []
 _LN_QUEUED = [False]
 
@@ -286,7 +285,6 @@ def deferred_pending() -> bool:
 
 
 def _ln_param_flush():
-    _LN_QUEUED[0] = False
     pend, _LN_PENDING[:] = list(_LN_PENDING), []
     if not pend:
         return
@@ -312,10 +310,19 @@ def _end_of_backward_flush():
     """The deferred parameter gradients of this backward pass: every LayerNorm's dgamma / dbeta (one
     launch), every deferrable token-Linear weight gradient (grouped tile launches + batched slab
     sums) and every LePE weight-gradient reduction (one launch per 32 blocks)."""
+    _LN_QUEUED[0] = False
+    flush_deferred()
+    _USES.clear()
+
+
+def flush_deferred():
+    """Write every parameter gradient deferred so far in this backward pass (the grouped launches of
+    the end-of-backward flush, for what is pending now).  csu.dist.GradAllReduce calls it when a
+    bucket's last gradient has been accumulated, so that bucket's all-reduce can start while the rest
+    of backward runs; what later ops defer goes to the next bucket's flush or the end of backward."""
     _ln_param_flush()
     _wgrad_flush()
     _lepe_flush()
-    _USES.clear()
 
 
 _LEPE_PENDING: list = []   # (LepeReduceItem, partials workspace, flat gradient buffer)
@@ -348,9 +355,9 @@ def _ln_params(ctx, rows, C, work, dgb):
 # grouped tile launch per tile size for all of them (csu_linear_wgrad_group: no per-Linear
 # underfilled workgroup rounds, so each Linear needs only a few token chunks) and ONE batched
 # fixed-order slab sum per 40 (csu_wslab_reduce_batch).  Their dY / X operands are kept alive until
-# then.  CSU_DEFER_WGRAD=0: one launch (+ reduction) per Linear, inline.
-DEFER_WGRAD = _os.environ.get("CSU_DEFER_WGRAD", "1") == "1"
-GROUP_WGRAD = _os.environ.get("CSU_GROUP_WGRAD", "1") == "1"   # 0: deferred slab sums only (A/B)
+# then.  DEFER_WGRAD = False (tests): one launch (+ reduction) per Linear, inline.
+DEFER_WGRAD = True
+GROUP_WGRAD = True   # False (tests): deferred slab sums only
 _WG_PENDING: list = []   # (WslabItem, out, workspace): reductions of tile kernels already launched
 _WG_DEFER: list = []     # (dy2, x2, out): whole weight gradients deferred to the grouped launch
 _WG_POST: list = []      # callables run after the deferred weight gradients are complete
@@ -870,16 +877,15 @@ def gemm(a2: torch.Tensor, b: torch.Tensor, b_trans: bool, out_dtype, bias=None,
 # the weight gradient inline.  A HIP-graph capture runs it inline too: inside a graph the side
 # stream measured slower (1075 vs 1090 img/s, 3 A/B pairs at 512x512) and its replays were not
 # bitwise reproducible at 512x512 (tools/det_graph.py DIAG=...).
-# CSU_SIDE_WGRAD=0 disables the side stream in eager steps as well.
+# SIDE_WGRAD = False (tests, bench ledger) disables the side stream in eager steps as well.
 # ---------------------------------------------------------------------------------------------
-SIDE_WGRAD = _os.environ.get("CSU_SIDE_WGRAD", "1") == "1"
+SIDE_WGRAD = True
 # diagnostics of the side-stream-in-graph nondeterminism (tools/det_graph.py): allow the side
 # stream under capture / join every side launch at once
-_SIDE_IN_GRAPH = _os.environ.get("CSU_SIDE_IN_GRAPH", "0") == "1"
-_SIDE_JOIN_NOW = _os.environ.get("CSU_SIDE_JOIN_NOW", "0") == "1"
-# CSU_PAD_CHANNELS=0: convolutions of inputs with C % 8 != 0 (the 3-channel image) without the zero
-# channel padding (per-element gathers; A/B)
-PAD_CHANNELS = _os.environ.get("CSU_PAD_CHANNELS", "1") == "1"
+_SIDE_IN_GRAPH = False
+_SIDE_JOIN_NOW = False
+# convolutions of inputs with C % 8 != 0 (the 3-channel image) zero-pad the channels to 8
+PAD_CHANNELS = True
 _SIDE_STREAMS = {}
 _SIDE_PENDING = []
 _SIDE_JOIN_QUEUED = [False]
@@ -910,7 +916,10 @@ def _grad_dest(params) -> Optional[torch.Tensor]:
     for p in params:
         p = _leaf(p)
         e = _GRAD_DEST.get(id(p)) if p is not None else None
-        if e is None or p.grad is not None:
+        # a parameter used by several ops of this graph (shared weights): every call's backward would
+        # write the same bucket memory while the engine still holds an earlier call's gradient as an
+        # alias of it -- such gradients go to fresh buffers and are summed by the engine
+        if e is None or p.grad is not None or _USES.get(id(p), 0) > 1:
             return None
         flat, off = e
         if flat0 is None:
@@ -990,11 +999,8 @@ def wgrad_maybe_side(dy2: torch.Tensor, x2: torch.Tensor, wdt, bdt, params=()):
     return linear_wgrad(dy2, x2, out=dest, defer=_wgrad_deferrable(dy2, wdt, bdt, params))
 
 
-# csu_gemm_ex (fused bias / GELU / GELU' / residual token GEMM) for the bf16 nn.Linear forward and
-# input-gradient GEMMs; CSU_FUSED_GEMM=0 falls back to torch.matmul (hipBLASLt) for A/B checks.
-FUSED_GEMM = _os.environ.get("CSU_FUSED_GEMM", "1") == "1"
-
-
+# csu_gemm_ex (fused bias / GELU / GELU' / residual token GEMM) runs every bf16 nn.Linear forward
+# and input-gradient GEMM, csu_gemm_f32 every fp32 one; there is no vendor-GEMM path.
 def _gemm_ok(*dims):
     return all(d % 8 == 0 for d in dims)
 
@@ -1012,7 +1018,8 @@ class _LinearFn(torch.autograd.Function):
         if wc is None:
             wc = weight.to(cd)
         K, N = xc.shape[-1], wc.shape[0]
-        ctx.fast = FUSED_GEMM and cd == torch.bfloat16 and xc.is_cuda and _gemm_ok(K, N)
+        require_device(xc)
+        ctx.fast = cd == torch.bfloat16 and _gemm_ok(K, N)
         ctx.f32 = False
         wt = None
         if ctx.fast:
@@ -1020,19 +1027,15 @@ class _LinearFn(torch.autograd.Function):
             y = gemm(x2, wc, False, odt or cd, bias=None if bias is None else bias.detach().float().contiguous())
             y = y.view(*xc.shape[:-1], N)
             wt = _weight_t(weight, wc)
-        elif cd == torch.float32 and xc.is_cuda and K % 4 == 0 and N % 4 == 0:
+        elif cd == torch.float32 and K % 4 == 0 and N % 4 == 0:
             # fp32 path (no autocast, BASELINE config 2): csu fp32 MFMA GEMM, bias in its epilogue
             x2 = xc.reshape(-1, K).contiguous()
             y = gemm_f32(0, x2, wc.contiguous(), x2.shape[0], N, K,
                          bias=None if bias is None else bias.detach().contiguous()).view(*xc.shape[:-1], N)
             ctx.f32 = True
         else:
-            bc = None
-            if bias is not None:
-                bc = _ACTIVE_CACHE.get(bias, cd) if _ACTIVE_CACHE is not None else None
-                if bc is None:
-                    bc = bias.to(cd)
-            y = torch.nn.functional.linear(xc, wc, bc)
+            raise CsuError(f"linear: no csu GEMM for {cd} with in/out features {K}/{N} (bf16 needs multiples "
+                           f"of 8, fp32 multiples of 4)")
         ctx.save_for_backward(xc, wt if ctx.fast else wc)
         ctx.meta = (x.dtype, weight.dtype, None if bias is None else bias.dtype)
         ctx.params = (weight, bias)
@@ -1056,10 +1059,8 @@ class _LinearFn(torch.autograd.Function):
             if ctx.fast:
                 odt = xdt if xdt in (torch.float32, torch.bfloat16) else wc.dtype
                 dx = gemm(dy2, wc, False, odt).view(xc.shape)
-            elif ctx.f32:
-                dx = gemm_f32(1, dy2, wc.contiguous(), dy2.shape[0], K, N).view(xc.shape)
             else:
-                dx = (dy2 @ wc).view(xc.shape)
+                dx = gemm_f32(1, dy2, wc.contiguous(), dy2.shape[0], K, N).view(xc.shape)
             if dx.dtype != xdt:
                 dx = dx.to(xdt)
         vec = 16 // dy2.element_size()
@@ -1286,7 +1287,7 @@ def concat_linear(a: torch.Tensor, b: torch.Tensor, weight: torch.Tensor, bias: 
     """fp32 Linear(cat([a, b], -1)) for bf16 a, b under bf16 autocast (see _ConcatLinearFn); other
     inputs take the reference form (cat, then linear with an fp32 output)."""
     Ca, Cb, N = a.shape[-1], b.shape[-1], weight.shape[0]
-    if (a.is_cuda and FUSED_GEMM and torch.is_autocast_enabled("cuda")
+    if (a.is_cuda and torch.is_autocast_enabled("cuda")
             and torch.get_autocast_dtype("cuda") == torch.bfloat16 and a.dtype == b.dtype == torch.bfloat16
             and bias is not None and _gemm_ok(Ca, Cb, N)):
         wc = _ACTIVE_CACHE.get(weight, torch.bfloat16) if _ACTIVE_CACHE is not None else None
@@ -1475,8 +1476,8 @@ class _MlpFusedFn(torch.autograd.Function):
         return dy.to(rdt), dx.view(xshape), dw1.to(w1dt), db1.to(b1dt), dw2.to(w2dt), db2.to(b2dt), None, None, None
 
 
-# CSU_FUSED_MLP=0 selects the two-GEMM Mlp (A/B comparisons)
-FUSED_MLP = _os.environ.get("CSU_FUSED_MLP", "1") == "1"
+# the fused one-launch Mlp where the library has it (C in {64, 128, 256}); otherwise two gemm4 launches
+FUSED_MLP = True
 
 
 def mlp_residual(res, x, fc1: torch.nn.Linear, fc2: torch.nn.Linear, drop: Optional[MlpDrop] = None):

@@ -200,6 +200,11 @@ class FusedAdamW(torch.optim.Optimizer):
                 for p in g["params"]:
                     st, o = self.state.get(p), old.get(p)
                     if not st:
+                        if o is not None:
+                            # the captured step keeps updating this parameter with its old moments
+                            # and the group's step count: a "fresh" loaded state cannot be honoured
+                            raise RuntimeError("FusedAdamW.load_state_dict after a capture: the loaded state "
+                                               "has no state for a parameter the captured step updates")
                         continue
                     if o is None:
                         raise RuntimeError("FusedAdamW.load_state_dict after a capture: the loaded state has a "

@@ -103,15 +103,43 @@ def _autocast(device, amp_dtype):
     return torch.autocast(dt, dtype=amp_dtype or torch.float32, enabled=amp_dtype is not None)
 
 
-_GRAPHS = None   # model -> {key: GraphedTrainStep | _GraphedEval}, kept across train_model calls
+class _GraphCache(dict):
+    """Captured graphs of one model: {key: _GraphedTrain | _GraphedEval}, kept on the model itself
+    (``model._csu_graphs``) so that model and graphs form one collectable cycle -- a module-level
+    WeakKeyDictionary could never drop an entry, its values hold the model.  Copies and pickles of
+    the model start with an empty cache."""
+
+    def __deepcopy__(self, memo):
+        return _GraphCache()
+
+    def __reduce__(self):
+        return (_GraphCache, ())
 
 
 def _graph_cache(model):
-    global _GRAPHS
-    if _GRAPHS is None:
-        import weakref
-        _GRAPHS = weakref.WeakKeyDictionary()
-    return _GRAPHS.setdefault(model, {})
+    c = model.__dict__.get("_csu_graphs")
+    if c is None:
+        c = _GraphCache()
+        object.__setattr__(model, "_csu_graphs", c)
+    return c
+
+
+def _drop_stale_train_graphs(cache, optimizer, reducer):
+    """A new optimizer or reducer for the model: the train graphs captured for the old ones (and the
+    memory pools they hold) are released."""
+    for k in [k for k in cache if k[0] == "train" and (k[-2], k[-1]) != (id(optimizer), id(reducer))]:
+        del cache[k]
+
+
+def _capture_mode():
+    """HIP-graph capture mode: under a process group the RCCL watchdog polls its collectives' events
+    from another thread, so the capture is thread-local and starts with nothing in flight (see
+    GraphedTrainStep)."""
+    if dist.is_available() and dist.is_initialized():
+        from .dist import drain_collectives
+        drain_collectives()
+        return "thread_local"
+    return "global"
 
 
 def _graphable(model, optimizer, device, criterion) -> bool:
@@ -137,8 +165,9 @@ class _GraphedEval:
             self._body()                 # warm-up: lazily built caches / kernels outside the capture
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
+        mode = _capture_mode()
         self.graph = torch.cuda.CUDAGraph()
-        with torch.no_grad(), torch.cuda.graph(self.graph):
+        with torch.no_grad(), torch.cuda.graph(self.graph, capture_error_mode=mode):
             self.stats = self._body()
 
     def _body(self):
@@ -262,6 +291,8 @@ def train_model(model, train_loader, test_loader, criterion, optimizer, schedule
     if graph and not use_graph:
         raise ValueError("train_model(graph=True) needs a csu model on a GPU and csu.optim.FusedAdamW")
     cache = _graph_cache(model) if use_graph else None
+    if cache is not None:
+        _drop_stale_train_graphs(cache, optimizer, reducer)
     for epoch in range(start, num_epochs):
         model.train()
         sampler = getattr(train_loader, "sampler", None)

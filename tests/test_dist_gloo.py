@@ -68,6 +68,7 @@ def _worker(rank, world, port, out_path, mode="ddp"):
                                 grad_dtype=torch.bfloat16 if mode == "reducer_bf16" else torch.float32)
         assert len(red.buckets) > 2
         stats = _train(model, [(xs[shard], ts[shard])], reducer=red)
+        assert red.last_early >= len(red.buckets) - 1, (red.last_early, len(red.buckets))
     means = _epoch_means(stats)
     if r == 0:
         torch.save({"params": [p.detach().clone() for p in model.parameters()], "means": means}, out_path)
@@ -130,6 +131,11 @@ def test_grad_dest_registry_contiguity():
         assert ops._grad_dest((a, c)) is None            # not adjacent
         a.grad = torch.zeros(3, 4)
         assert ops._grad_dest((a, b)) is None            # gradient accumulation: no stealing
+        a.grad = None
+        ops._USES[id(b)] = 2
+        assert ops._grad_dest((a, b)) is None            # shared parameter: the engine sums its uses
+        assert ops._grad_dest((c,)) is not None
     finally:
+        ops._USES.clear()
         for p in (a, b, c):
             ops._GRAD_DEST.pop(id(p), None)

@@ -72,10 +72,12 @@ def worker(rank, world, port, out, dtype, mode="reducer"):
     if red is not None:
         assert len(red.buckets) > 2
     params = _grads(m, xs[rank * n:(rank + 1) * n], ts[rank * n:(rank + 1) * n], amp, red)
+    early = None
     if red is not None:
         copied = (red.last_copied, len(red.params))
+        early = (red.last_early, len(red.buckets))
     if rank == 0:
-        torch.save({"grads": [p.cpu() for p in params], "copied": copied}, out)
+        torch.save({"grads": [p.cpu() for p in params], "copied": copied, "early": early}, out)
     dist.destroy_process_group()
 
 
@@ -110,6 +112,11 @@ def test_two_ranks_on_csu_kernels_equal_global_batch(tmp_path, dtype, mode):
     if mode == "named":   # in place: everything but the few conv / CARAFE / head parameters
         copied, total = res["copied"]
         assert copied < 0.25 * total, (copied, total)
+    if res["early"] is not None:
+        # overlap: every bucket but the last starts its all-reduce from a hook, during backward
+        # (the deferred LayerNorm / Linear / LePE gradients are flushed per bucket)
+        early, nbuckets = res["early"]
+        assert early >= nbuckets - 1, (early, nbuckets)
     m, xs, ts, amp = _setup(dtype)
     ref = [g.cpu() for g in _grads(m, xs, ts, amp)]
     # per-sample work is identical on both sides (every csu kernel is per token / window / image, and
@@ -129,3 +136,122 @@ def test_two_ranks_on_csu_kernels_equal_global_batch(tmp_path, dtype, mode):
         assert rel <= tol, (name, rel)
         checked += 1
     assert checked > 0.9 * len(ref), (checked, len(ref))
+
+
+def shared_worker(port, out):
+    """One rank (gloo, world size 1): weights shared by several op calls (LayerNorm, Linear, LePE)
+    with a GradAllReduce registered: each call's gradient must be summed, not written twice into the
+    bucket slice (_grad_dest refuses parameters used more than once)."""
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1")
+    dist.init_process_group("gloo")
+    from csu import ops
+    from csu.dist import GradAllReduce
+    d = torch.device("cuda:0")
+    g = torch.Generator(device=d).manual_seed(5)
+    C, reso = 64, 16
+    geom = ops.StripeGeometry(reso, C, 1, [(reso, 2, 0), (2, reso, C // 2)], 32 ** -0.5)
+    xs = [torch.randn(2, reso * reso, C, device=d, generator=g) for _ in range(2)]
+    p0 = {"lnw": 1 + 0.1 * torch.randn(C, device=d, generator=g), "lnb": 0.1 * torch.randn(C, device=d, generator=g),
+          "w": 0.05 * torch.randn(3 * C, C, device=d, generator=g), "b": 0.05 * torch.randn(3 * C, device=d, generator=g),
+          "lw0": 0.1 * torch.randn(C // 2, 1, 3, 3, device=d, generator=g),
+          "lb0": 0.1 * torch.randn(C // 2, device=d, generator=g),
+          "lw1": 0.1 * torch.randn(C // 2, 1, 3, 3, device=d, generator=g),
+          "lb1": 0.1 * torch.randn(C // 2, device=d, generator=g)}
+    res = {}
+    for use_red in (False, True):
+        ps = {k: torch.nn.Parameter(v.clone()) for k, v in p0.items()}
+        red = GradAllReduce(list(ps.items()), bucket_mb=0.001) if use_red else None
+        for _ in range(2):
+            for p in ps.values():
+                p.grad = None
+            loss = 0
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                for x in xs:    # every parameter is used by both calls
+                    h = ops.layer_norm(x, ps["lnw"], ps["lnb"])
+                    qkv = ops.linear(h, ps["w"], ps["b"])
+                    o = ops.stripe_attention(qkv.bfloat16().contiguous(), geom, [ps["lw0"], ps["lw1"]],
+                                             [ps["lb0"], ps["lb1"]])
+                    loss = loss + (o.float() ** 2).sum()
+            loss.backward()
+            if red is not None:
+                red.finish()
+        torch.cuda.synchronize()
+        res[use_red] = {k: p.grad.detach().cpu().clone() for k, p in ps.items()}
+        if red is not None:
+            red.remove()
+    torch.save(res, out)
+    dist.destroy_process_group()
+
+
+def test_reducer_with_shared_weights_sums_every_use(tmp_path):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    out = str(tmp_path / "shared.pt")
+    env = dict(os.environ, PYTHONPATH=os.pathsep.join([REPO, os.path.join(REPO, "cswin-simam-unet_amd")]))
+    code = (f"import sys; sys.path[:0] = [{REPO!r}]; from tests.test_gpu_dist import shared_worker; "
+            f"shared_worker({port}, {out!r})")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = torch.load(out, weights_only=True)
+    for k, ref in res[False].items():
+        got = res[True][k]
+        rel = float((got.double() - ref.double()).norm() / ref.double().norm())
+        assert rel < 1e-5, (k, rel)
+
+
+def train_model_worker(port, out, use_pg):
+    """train_model with (use_pg) or without a process group: RCCL world size 1 + GradAllReduce
+    captured in the train graph, a ragged last train batch (eager reducer step), and the eval graph
+    captured right after the epoch's metric all-reduce (drained, thread-local capture)."""
+    import torch.distributed as dist
+    from oracle import cswin_ref as O
+    from csu.data import ellipse_batch
+    from csu.model import CSWinTransformer
+    from csu.train import bce_loss, make_optimizer, make_scheduler, train_model
+    d = torch.device("cuda:0")
+    red = None
+    m = CSWinTransformer(img_size=64, split_size=[1, 2, 2, 2]).to(d)
+    m.load_state_dict(O.recipe_params(O.CSWinConfig(img_size=64, split_size=(1, 2, 2, 2)), seed=0))
+    if use_pg:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1")
+        torch.cuda.set_device(0)
+        dist.init_process_group("nccl", device_id=d)
+        from csu.dist import GradAllReduce
+        red = GradAllReduce(m.named_parameters(), bucket_mb=0.5)
+    rng = np.random.default_rng(7)
+    train = [ellipse_batch(rng, 2, 64) for _ in range(4)] + [ellipse_batch(rng, 1, 64)]
+    test = [ellipse_batch(rng, 2, 64), ellipse_batch(rng, 1, 64)]
+    opt = make_optimizer(m, lr=1e-3)
+    h = train_model(m, train, test, bce_loss, opt, make_scheduler(opt), d, num_epochs=2, verbose=False,
+                    amp_dtype=torch.bfloat16, reducer=red)
+    torch.save({"hist": h, "early": None if red is None else (red.last_early, len(red.buckets))}, out)
+    if use_pg:
+        dist.destroy_process_group()
+
+
+def test_train_model_with_reducer_and_ragged_batches(tmp_path):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, PYTHONPATH=os.pathsep.join([REPO, os.path.join(REPO, "cswin-simam-unet_amd")]))
+    res = {}
+    for use_pg in (False, True):
+        out = str(tmp_path / f"tm{int(use_pg)}.pt")
+        code = (f"import sys; sys.path[:0] = [{REPO!r}]; from tests.test_gpu_dist import train_model_worker; "
+                f"train_model_worker({port}, {out!r}, {use_pg!r})")
+        r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, "\n".join(ln for ln in r.stderr.splitlines() if "frame #" not in ln)[-3000:]
+        res[use_pg] = torch.load(out, weights_only=True)
+    early, nb = res[True]["early"]
+    assert nb > 2 and early >= nb - 1, (early, nb)
+    for k, a in res[False]["hist"].items():
+        b = res[True]["hist"][k]
+        np.testing.assert_allclose(b, a, rtol=1e-4, atol=1e-6, err_msg=k)

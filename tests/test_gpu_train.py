@@ -224,6 +224,11 @@ def test_optimizer_load_after_capture_keeps_graph_valid():
     torch.cuda.synchronize()
     assert la == lb
     assert all(torch.equal(x, y) for x, y in zip(pa, m.parameters()))
+    # a loaded state missing a parameter the captured step updates cannot be honoured: refused
+    bad = copy.deepcopy(sd_o)
+    bad["state"].pop(next(iter(bad["state"])))
+    with pytest.raises(RuntimeError, match="no state for a parameter"):
+        opt.load_state_dict(bad)
 
 
 def test_train_model_graphed_equals_eager():
