@@ -1403,7 +1403,7 @@ def _weight_bf16(w):
 
 def fused_ok(x: torch.Tensor, *dims) -> bool:
     """True when the bf16 fused-GEMM path applies (CUDA, autocast bf16, 16-B aligned dims)."""
-    return (FUSED_GEMM and x.is_cuda and torch.is_autocast_enabled("cuda")
+    return (x.is_cuda and torch.is_autocast_enabled("cuda")
             and torch.get_autocast_dtype("cuda") == torch.bfloat16 and _gemm_ok(*dims))
 
 
