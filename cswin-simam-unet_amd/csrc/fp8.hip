@@ -46,6 +46,35 @@ __global__ __launch_bounds__(NT) void quant_e4m3_rows(const csu_fp8_item* __rest
     }
 }
 
+
+// e4m3 byte layouts (csu_e4m3_layout_batch): one thread per 4-byte dst word
+__global__ __launch_bounds__(NT) void e4m3_layout_kernel(const csu_e4m3_layout_item* __restrict__ items, int count,
+                                                         long total) {
+    const long w = (long)blockIdx.x * NT + threadIdx.x;
+    if (w >= total) return;
+    int lo = 0, hi = count - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (items[mid].word0 <= w) lo = mid; else hi = mid - 1;
+    }
+    const csu_e4m3_layout_item it = items[lo];
+    const bool tr = it.mode & 1, perm = it.mode & 2;
+    const int dcols = tr ? it.rows : it.cols;
+    const long p0 = (w - it.word0) * 4;                 // first dst byte of the word
+    const long drow = p0 / dcols;
+    int dcol = (int)(p0 % dcols);
+    if (perm) {   // dst 32h + 16t + 4g (+ i) <- 32t + 8g + 4h (+ i)
+        const int b = dcol & 63, h = b >> 5, t = (b >> 4) & 1, g = (b >> 2) & 3;
+        dcol = (dcol & ~63) + 32 * t + 8 * g + 4 * h;
+    }
+    unsigned v = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const long sidx = tr ? (long)(dcol + i) * it.cols + drow : drow * it.cols + dcol + i;
+        v |= (unsigned)it.src[sidx] << (8 * i);
+    }
+    *reinterpret_cast<unsigned*>(it.dst + p0) = v;
+}
 }  // namespace
 }  // namespace csu
 
@@ -55,4 +84,10 @@ extern "C" int csu_quant_e4m3_batch(const csu_fp8_item* items, int count, long t
     if (count < 1 || total_rows < 1 || !items) return fail(CSU_E_ARG, "quant_e4m3: bad args");
     quant_e4m3_rows<<<(unsigned)total_rows, NT, 0, as_stream(stream)>>>(items, count);
     return check_launch("quant_e4m3");
+}
+
+extern "C" int csu_e4m3_layout_batch(const csu_e4m3_layout_item* items, int count, long total_words, void* stream) {
+    if (count < 1 || total_words < 1 || !items) return fail(CSU_E_ARG, "e4m3_layout: bad args");
+    e4m3_layout_kernel<<<(unsigned)((total_words + NT - 1) / NT), NT, 0, as_stream(stream)>>>(items, count, total_words);
+    return check_launch("e4m3_layout");
 }

@@ -105,7 +105,8 @@ __device__ __forceinline__ void exchange_half(f32x16* acc, float* xch, int wave,
         for (int e = 0; e < 16; ++e) acc[U * HT + q][e] += xch[((partner * HT + q) * 16 + e) * 64 + lane];
 }
 
-template <int C, int U, bool DROP>
+// A0: index of the first of the HT accumulator tiles holding features [U C/2, (U+1) C/2)
+template <int C, int U, bool DROP, int A0 = U * (C / 64)>
 __device__ __forceinline__ void fwd_epilogue(const f32x16* acc, __amdgpu_buffer_rsrc_t rs_res, __amdgpu_buffer_rsrc_t rs_out,
                                              const float* b2, int tok, bool ok, int h, long mg, const MlpDrop& dd) {
     constexpr int HT = C / 64;
@@ -128,7 +129,7 @@ __device__ __forceinline__ void fwd_epilogue(const f32x16* acc, __amdgpu_buffer_
             load4(b2 + f, bv);
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-                float z = acc[U * HT + q][4 * g + e] + bv[e];
+                float z = acc[A0 + q][4 * g + e] + bv[e];
                 if constexpr (DROP) z *= ((km >> (4 * g + e)) & 1u) ? sdp * R.scale : 0.f;
                 v[e] = z + rv[e];
             }
@@ -620,6 +621,465 @@ int bwd_launch(long M, const void* x, const void* dy, const void* w1, const floa
     return check_launch("mlp_bwd");
 }
 
+
+// ================================================================================================
+// fp8-e4m3 fused Mlp (BASELINE config 5, "fp8 MFMA weights"): v_mfma_scale_f32_32x32x64_f8f6f4 with
+// MX block scales -- every operand lane carries an E8M0 exponent for its 32 k-values (probe:
+// tools/probes/mx_scale_probe.hip, 127 = 2^0, one scale per lane of A and of B).
+//   GEMM1  h = W1 x   : A = e4m3 rows of W1 (the row's power-of-two scale sw1[f] = 2^e as the lane's
+//                       E8M0), B = x quantised in registers per (token, 32 consecutive channels)
+//   GEMM2  y += W2 g  : B = g = gelu(h + b1) quantised in registers per (token, the 32 hidden features
+//                       the lane holds: inside each 64-feature group those whose index has bit 2 ==
+//                       lane half), A = e4m3 rows of W2 (per-row scale sw2[c] as the lane's E8M0) with
+//                       the columns permuted per 64-block so that a lane's 32 k-bytes are contiguous:
+//                       position 32h + 16t + 4g + i holds feature 32t + 8g + 4h + i (csu_e4m3_layout_batch)
+// Chunks of 128 hidden features (wave u: features 64u..64u+63 = two 32-row tiles, so one lane holds
+// the 32 values of one f8 k-step of GEMM2); 64-token panel per workgroup as in the bf16 kernel.  A
+// chunk's W1 + W2 bytes equal one 64-feature bf16 chunk's: half the weight stream per panel.  GEMM2
+// is split by OUTPUT features: wave (t, u) accumulates y features [u C/2, (u+1) C/2) over the whole
+// chunk, taking the partner wave's g_q through LDS (half the accumulators, no final exchange).
+constexpr int HC8 = 128;
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ int e8m0_of(float s) { return (__float_as_int(s) >> 23) & 0xff; }
+
+// MX quantisation of 32 values: scale 2^e, e the smallest integer with amax <= 448 * 2^e (clamped to
+// the E8M0 range; 0 for an all-zero block), e4m3fn bytes round-to-nearest-even (|v / 2^e| <= 448: no
+// saturation).  Byte j of the packed operand = v[j].  Returns the E8M0 byte e + 127.
+__device__ __forceinline__ int mx_quant32(const float* v, i32x8& q) {
+    float amax = 0.f;
+#pragma unroll
+    for (int i = 0; i < 32; ++i) amax = fmaxf(amax, fabsf(v[i]));
+    const int b = __float_as_int(amax);
+    int e = ((b >> 23) & 0xff) - 135 + ((b & 0x7fffff) > 0x600000 ? 1 : 0);
+    e = amax == 0.f ? 0 : (e < -127 ? -127 : (e > 127 ? 127 : e));
+#pragma unroll
+    for (int d = 0; d < 8; ++d) {
+        int w = __builtin_amdgcn_cvt_pk_fp8_f32(ldexpf(v[4 * d], -e), ldexpf(v[4 * d + 1], -e), 0, false);
+        w = __builtin_amdgcn_cvt_pk_fp8_f32(ldexpf(v[4 * d + 2], -e), ldexpf(v[4 * d + 3], -e), w, true);
+        q[d] = w;
+    }
+    return e + 127;
+}
+
+// 32 k-bytes [kb, kb + 32) of row `row` of a swizzled byte image with RB-byte rows (the bf16 images'
+// 16-B slot swizzle; two ds_read_b128)
+template <int RB>
+__device__ __forceinline__ i32x8 frag8(const bf16* img, int row, int kb) {
+    const u32x4 lo = *reinterpret_cast<const u32x4*>(img + moff<RB>(row, kb >> 1));
+    const u32x4 hi = *reinterpret_cast<const u32x4*>(img + moff<RB>(row, (kb + 16) >> 1));
+    return i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+}
+
+// token operand of GEMM1 (or of the backward's dY GEMM): row `tok`, k-step s = channels 64 s + 32 h
+// .. + 31, quantised per lane (optionally times a per-channel power-of-two factor colscale first)
+template <int C>
+__device__ __forceinline__ void load_q8(__amdgpu_buffer_rsrc_t rs, int tok, bool ok, int h, i32x8* q, int* sc,
+                                        const float* colscale = nullptr) {
+#pragma unroll
+    for (int s = 0; s < C / 64; ++s) {
+        float v[32];
+#pragma unroll
+        for (int p = 0; p < 4; ++p) buf_ld8bf(rs, ok ? (unsigned)(tok * C + 64 * s + 32 * h + 8 * p) * 2 : kOOB, v + 8 * p);
+        if (colscale) {
+#pragma unroll
+            for (int i = 0; i < 32; ++i) v[i] *= colscale[64 * s + 32 * h + i];
+        }
+        sc[s] = mx_quant32(v, q[s]);
+    }
+}
+
+__device__ __forceinline__ f32x16 mfma8(const i32x8& a, const i32x8& b, const f32x16& c, int sa, int sb) {
+    return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b, c, 0, 0, 0, sa, 0, sb);
+}
+
+// Forward.  Rings as the bf16 forward: W1 chunk images [128][C B] in 2 stages, W2 chunk images [C][128 B]
+// in 2 stages; step j: DMA W1(j+2), W2(j+1); GEMM1(j+1) on the MFMA pipe while GELU + quantisation of
+// chunk j run on the VALU; GEMM2(j).
+template <int C, bool DROP>
+__global__ __launch_bounds__(MT) void mlp_fp8_fwd_kernel(long M, const bf16* __restrict__ X, const uint8_t* __restrict__ W1,
+                                                         const float* __restrict__ sw1, const float* __restrict__ b1,
+                                                         const uint8_t* __restrict__ W2p, const float* __restrict__ sw2,
+                                                         const float* __restrict__ b2, const float* __restrict__ res,
+                                                         float* __restrict__ out, MlpDrop dd, long rpi) {
+    constexpr int NCH = 4 * C / HC8;    // hidden chunks (even)
+    constexpr int KS = C / 64;          // f8 k-steps of GEMM1
+    constexpr int TF = C / 32;
+    constexpr int IMG1 = HC8 * C / 2;   // bf16 units of a W1 chunk image
+    constexpr int IMG2 = C * HC8 / 2;   // and of a W2 chunk image
+    using D1 = Dma<HC8, C>;
+    using D2 = Dma<C, HC8>;
+    __shared__ __attribute__((aligned(1024))) bf16 ring[2 * IMG1 + 2 * IMG2];
+    __shared__ __attribute__((aligned(16))) float b1s[4 * C];
+    __shared__ int e1s[4 * C];
+    __shared__ __attribute__((aligned(32))) i32x8 xg[4][64];   // quantised g of every wave's lanes
+    __shared__ int xgs[4][64];
+    bf16* const w1r = ring;
+    bf16* const w2r = ring + 2 * IMG1;
+
+    const long m0 = (long)blockIdx.x * BM;
+    const long rows = M - m0;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int r = lane & 31, h = lane >> 5;
+    const int t = wave >> 1, u = wave & 1;
+    const int tok = 32 * t + r;
+    const bool ok = tok < rows;
+    const int hs = 64 * u;              // this wave's hidden features within a chunk
+    const int j0 = kRot && rpi > 0 && rpi % BM == 0 ? (int)(((m0 % rpi) / BM) & (NCH - 1)) : 0;   // see mlp_fwd_kernel
+    auto chk = [&](int j) { return (j + j0) & (NCH - 1); };
+    for (int i = threadIdx.x; i < 4 * C; i += MT) {
+        b1s[i] = b1[i];
+        e1s[i] = e8m0_of(sw1[i]);
+    }
+    constexpr int TH = TF / 2;          // output tiles of one wave: features [u C/2, (u+1) C/2)
+    int e2[TH];
+#pragma unroll
+    for (int q = 0; q < TH; ++q) e2[q] = e8m0_of(sw2[32 * (u * TH + q) + r]);
+    i32x8 xq[KS];
+    int xs[KS];
+    load_q8<C>(buf_rsrc(X + m0 * C, rows * C * 2), tok, ok, h, xq, xs);
+
+    D1 d1;
+    D2 d2;
+    d1.init(C / 2, wave, lane);         // ld in bf16 units: W1 rows are C bytes, W2p rows 4C bytes
+    d2.init(2 * C, wave, lane);
+    const i32x4 rs_w1 = rsrc4(W1, 4L * C * C);
+    const i32x4 rs_w2 = rsrc4(W2p, 4L * C * C);
+    asm volatile("" ::: "memory");
+    dma<D1::NW>(rs_w1, d1.v, (unsigned)chk(0) * HC8 * C, w1r, wave);
+    dma<D2::NW>(rs_w2, d2.v, (unsigned)chk(0) * HC8, w2r, wave);
+    dma<D1::NW>(rs_w1, d1.v, (unsigned)chk(1) * HC8 * C, w1r + IMG1, wave);
+
+    auto gemm1 = [&](const bf16* img, int jc, f32x16* ha) {
+        i32x8 wf[2][KS];
+#pragma unroll
+        for (int t2 = 0; t2 < 2; ++t2)
+#pragma unroll
+            for (int s = 0; s < KS; ++s) wf[t2][s] = frag8<C>(img, hs + 32 * t2 + r, 64 * s + 32 * h);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int t2 = 0; t2 < 2; ++t2) {
+            const int sa = e1s[jc * HC8 + hs + 32 * t2 + r];
+            f32x16 a = f32x16{};
+#pragma unroll
+            for (int s = 0; s < KS; ++s) a = mfma8(wf[t2][s], xq[s], a, sa, xs[s]);
+            ha[t2] = a;
+        }
+    };
+    f32x16 acc[TH];
+#pragma unroll
+    for (int i = 0; i < TH; ++i) acc[i] = f32x16{};
+    const long mg = m0 + tok;
+    DropoutRng Rh;
+    if constexpr (DROP) Rh = load_rng(dd.rng, dd.site_h, dd.p);
+    vmwait<0>();
+    lds_sync();
+    f32x16 ha[2], hb[2];
+    gemm1(w1r, chk(0), ha);
+
+    auto step = [&](auto more, auto par, int j, const f32x16* cur, f32x16* nxt) {
+        constexpr int P = decltype(par)::value;
+        vmwait<0>();                    // W1(j+1), W2(j): issued one step ago
+        lds_sync();                     // every wave is past GEMM1(j) and GEMM2(j-1)
+        if (j + 2 < NCH) dma<D1::NW>(rs_w1, d1.v, (unsigned)chk(j + 2) * HC8 * C, w1r + P * IMG1, wave);
+        if (j + 1 < NCH) dma<D2::NW>(rs_w2, d2.v, (unsigned)chk(j + 1) * HC8, w2r + (1 - P) * IMG2, wave);
+        const int jc = chk(j);
+        if constexpr (decltype(more)::value) gemm1(w1r + (1 - P) * IMG1, chk(j + 1), nxt);
+        float gv[32];
+#pragma unroll
+        for (int t2 = 0; t2 < 2; ++t2) {
+            float bv[16];
+            bias16(b1s, jc * HC8 + hs + 32 * t2, h, bv);
+#pragma unroll
+            for (int e = 0; e < 16; ++e) gv[16 * t2 + e] = gelu_fast(cur[t2][e] + bv[e]);
+            if constexpr (DROP) {
+                if (dd.p > 0.f) {
+                    const unsigned km = keep16_crow(Rh, ((uint64_t)mg * 4 * C + jc * HC8 + hs + 32 * t2) >> 3, h);
+#pragma unroll
+                    for (int e = 0; e < 16; ++e) gv[16 * t2 + e] = ((km >> e) & 1u) ? gv[16 * t2 + e] * Rh.scale : 0.f;
+                }
+            }
+        }
+        i32x8 gq;
+        const int gs = mx_quant32(gv, gq);
+        xg[wave][lane] = gq;
+        xgs[wave][lane] = gs;
+        lds_sync();                     // the partner wave's g_q (same tokens, the other 64 features)
+        const i32x8 gp = xg[wave ^ 1][lane];
+        const int gsp = xgs[wave ^ 1][lane];
+        const bf16* w2c = w2r + P * IMG2;
+        const int hp = 64 * (1 - u);
+        i32x8 wa[TH], wb[TH];
+#pragma unroll
+        for (int q = 0; q < TH; ++q) {
+            wa[q] = frag8<HC8>(w2c, 32 * (u * TH + q) + r, hs + 32 * h);
+            wb[q] = frag8<HC8>(w2c, 32 * (u * TH + q) + r, hp + 32 * h);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int q = 0; q < TH; ++q) {
+            acc[q] = mfma8(wa[q], gq, acc[q], e2[q], gs);
+            acc[q] = mfma8(wb[q], gp, acc[q], e2[q], gsp);
+        }
+    };
+    int j = 0;
+    for (; j + 2 < NCH; j += 2) {
+        step(bconst<true>{}, iconst<0>{}, j, ha, hb);
+        step(bconst<true>{}, iconst<1>{}, j + 1, hb, ha);
+    }
+    step(bconst<true>{}, iconst<0>{}, j, ha, hb);
+    step(bconst<false>{}, iconst<1>{}, j + 1, hb, ha);
+
+    const auto rs_res = buf_rsrc(res + m0 * C, rows * C * 4);
+    const auto rs_out = buf_rsrc(out + m0 * C, rows * C * 4);
+    if (u == 0)
+        fwd_epilogue<C, 0, DROP, 0>(acc, rs_res, rs_out, b2, tok, ok, h, mg, dd);
+    else
+        fwd_epilogue<C, 1, DROP, 0>(acc, rs_res, rs_out, b2, tok, ok, h, mg, dd);
+}
+
+template <int C>
+int fp8_fwd_launch(long M, const void* x, const void* w1, const float* sw1, const float* b1, const void* w2p, const float* sw2,
+                   const float* b2, const float* res, float* out, const MlpDrop* d, long rpi, hipStream_t st) {
+    const dim3 grid((unsigned)((M + BM - 1) / BM));
+    if (d)
+        mlp_fp8_fwd_kernel<C, true><<<grid, MT, 0, st>>>(M, (const bf16*)x, (const uint8_t*)w1, sw1, b1, (const uint8_t*)w2p,
+                                                         sw2, b2, res, out, *d, rpi);
+    else
+        mlp_fp8_fwd_kernel<C, false><<<grid, MT, 0, st>>>(M, (const bf16*)x, (const uint8_t*)w1, sw1, b1, (const uint8_t*)w2p,
+                                                          sw2, b2, res, out, MlpDrop{}, rpi);
+    return check_launch("mlp_fp8_fwd");
+}
+
+
+// 32 values of a packed e4m3 operand lane times 2^(e8 - 127)
+__device__ __forceinline__ void mx_dequant32(const i32x8& q, int e8, float* v) {
+#pragma unroll
+    for (int d = 0; d < 8; ++d) {
+        const auto lo = __builtin_amdgcn_cvt_pk_f32_fp8(q[d], false);
+        const auto hi = __builtin_amdgcn_cvt_pk_f32_fp8(q[d], true);
+        v[4 * d] = ldexpf(lo[0], e8 - 127);
+        v[4 * d + 1] = ldexpf(lo[1], e8 - 127);
+        v[4 * d + 2] = ldexpf(hi[0], e8 - 127);
+        v[4 * d + 3] = ldexpf(hi[1], e8 - 127);
+    }
+}
+
+// Backward (straight-through for every quantisation):
+//   h  = W1 x_q + b1 recomputed exactly as the forward (same operands, same instruction order),
+//   dg = W2^T dY: A = W2^T e4m3 (csu_e4m3_layout_batch mode 1), B = dY * sw2 quantised per (token,
+//        32 consecutive channels) -- the per-row scale of W2 lies along this contraction, so it is
+//        folded into the token operand;
+//   dh = dg * gelu'(h) (* hidden mask); dH (bf16) and G = the forward's g_q (bf16, exact) stored for
+//        dW1 = dH^T x and dW2 = dY^T G;
+//   dx = W1^T dh: A = W1^T e4m3 with permuted columns (mode 3), B = dh * sw1 quantised per lane as g.
+// GEMM4 is split by OUTPUT features: wave (t, u) accumulates dx features [u C/2, (u+1) C/2) over the
+// whole chunk, taking the partner wave's quantised dh (its 64 features) through LDS -- half the
+// accumulator registers of a hidden-half split and no final exchange.
+// LDS: W1 chunk images [128][C B] in 2 stages, one W2^T stage [128][C B], one W1^T stage [C][128 B]
+// (C = 256: 128 KB).  Step j: DMA W1(j+1); GEMM1 + GEMM3(j); barrier, DMA W2^T(j+1); GELU', stores,
+// quantisation, dh to LDS; wait for W1^T(j) by count; barrier; GEMM4(j); barrier, DMA W1^T(j+1).
+template <int C, bool DROP>
+__global__ __launch_bounds__(MT) void mlp_fp8_bwd_kernel(long M, const bf16* __restrict__ X, const bf16* __restrict__ dY,
+                                                         const uint8_t* __restrict__ W1, const float* __restrict__ sw1,
+                                                         const float* __restrict__ b1, const uint8_t* __restrict__ W2T,
+                                                         const float* __restrict__ sw2, const uint8_t* __restrict__ W1Tp,
+                                                         bf16* __restrict__ dH, bf16* __restrict__ G, bf16* __restrict__ dX,
+                                                         MlpDrop dd, long rpi) {
+    constexpr int NCH = 4 * C / HC8;
+    constexpr int KS = C / 64;
+    constexpr int TF = C / 32;
+    constexpr int TH = TF / 2;          // dx tiles of one wave
+    constexpr int IMG1 = HC8 * C / 2;   // W1 / W2^T chunk image (bf16 units)
+    constexpr int IMG3 = C * HC8 / 2;   // W1^T chunk image
+    using D1 = Dma<HC8, C>;
+    using D3 = Dma<C, HC8>;
+    constexpr int NST = 16;             // buffer stores per lane per chunk (8 G + 8 dH)
+    __shared__ __attribute__((aligned(1024))) bf16 ring[3 * IMG1 + IMG3];
+    __shared__ __attribute__((aligned(16))) float b1s[4 * C];
+    __shared__ __attribute__((aligned(16))) uint8_t e1s[4 * C];
+    __shared__ float s2s[C];
+    __shared__ __attribute__((aligned(32))) i32x8 xdh[4][64];   // quantised dh of every wave's lanes
+    __shared__ int xds[4][64];
+    bf16* const w1r = ring;
+    bf16* const w2r = ring + 2 * IMG1;
+    bf16* const w3r = ring + 3 * IMG1;
+
+    const long m0 = (long)blockIdx.x * BM;
+    const long rows = M - m0;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int r = lane & 31, h = lane >> 5;
+    const int t = wave >> 1, u = wave & 1;
+    const int tok = 32 * t + r;
+    const bool ok = tok < rows;
+    const int hs = 64 * u;
+    const int j0 = kRot && rpi > 0 && rpi % BM == 0 ? (int)(((m0 % rpi) / BM) & (NCH - 1)) : 0;   // see the forward
+    auto chk = [&](int j) { return (j + j0) & (NCH - 1); };
+    for (int i = threadIdx.x; i < 4 * C; i += MT) {
+        b1s[i] = b1[i];
+        e1s[i] = (uint8_t)e8m0_of(sw1[i]);
+    }
+    for (int i = threadIdx.x; i < C; i += MT) s2s[i] = sw2[i];
+    __syncthreads();
+    i32x8 xq[KS], dq[KS];
+    int xs[KS], ds[KS];
+    load_q8<C>(buf_rsrc(X + m0 * C, rows * C * 2), tok, ok, h, xq, xs);
+    load_q8<C>(buf_rsrc(dY + m0 * C, rows * C * 2), tok, ok, h, dq, ds, s2s);
+
+    D1 d1, d2;
+    D3 d3;
+    d1.init(C / 2, wave, lane);
+    d2.init(C / 2, wave, lane);
+    d3.init(2 * C, wave, lane);
+    const i32x4 rs_w1 = rsrc4(W1, 4L * C * C);
+    const i32x4 rs_w2 = rsrc4(W2T, 4L * C * C);
+    const i32x4 rs_w3 = rsrc4(W1Tp, 4L * C * C);
+    const auto rs_dh = buf_rsrc(dH + m0 * 4 * C, rows * 4 * C * 2);
+    const auto rs_g = buf_rsrc(G + m0 * 4 * C, rows * 4 * C * 2);
+    asm volatile("" ::: "memory");
+    dma<D1::NW>(rs_w1, d1.v, (unsigned)chk(0) * HC8 * C, w1r, wave);
+    dma<D1::NW>(rs_w2, d2.v, (unsigned)chk(0) * HC8 * C, w2r, wave);
+    dma<D3::NW>(rs_w3, d3.v, (unsigned)chk(0) * HC8, w3r, wave);
+
+    f32x16 acc[TH];
+#pragma unroll
+    for (int i = 0; i < TH; ++i) acc[i] = f32x16{};
+    const long mg = m0 + tok;
+    DropoutRng Rh;
+    if constexpr (DROP) Rh = load_rng(dd.rng, dd.site_h, dd.p);
+
+    auto step = [&](auto par, int j) {
+        constexpr int P = decltype(par)::value;
+        const bool more = j + 1 < NCH;
+        vmwait<D3::NW>();               // W1(j), W2^T(j) landed (W1^T(j), the youngest, may still fly)
+        lds_sync();
+        if (more) dma<D1::NW>(rs_w1, d1.v, (unsigned)chk(j + 1) * HC8 * C, w1r + (1 - P) * IMG1, wave);
+        const int jc = chk(j);
+        const bf16* w1c = w1r + P * IMG1;
+        float gv[32], dv[32];
+#pragma unroll
+        for (int t2 = 0; t2 < 2; ++t2) {
+            f32x16 ha, ga;
+            {
+                i32x8 fa[KS];
+#pragma unroll
+                for (int s = 0; s < KS; ++s) fa[s] = frag8<C>(w1c, hs + 32 * t2 + r, 64 * s + 32 * h);
+                __builtin_amdgcn_sched_barrier(0);
+                const int sa = e1s[jc * HC8 + hs + 32 * t2 + r];
+                ha = f32x16{};
+#pragma unroll
+                for (int s = 0; s < KS; ++s) ha = mfma8(fa[s], xq[s], ha, sa, xs[s]);   // as the forward
+            }
+            {
+                i32x8 fb[KS];
+#pragma unroll
+                for (int s = 0; s < KS; ++s) fb[s] = frag8<C>(w2r, hs + 32 * t2 + r, 64 * s + 32 * h);
+                __builtin_amdgcn_sched_barrier(0);
+                ga = f32x16{};
+#pragma unroll
+                for (int s = 0; s < KS; ++s) ga = mfma8(fb[s], dq[s], ga, 127, ds[s]);
+            }
+            float bv[16];
+            bias16(b1s, jc * HC8 + hs + 32 * t2, h, bv);
+            unsigned km = 0xffffu;
+            if constexpr (DROP) if (dd.p > 0.f) km = keep16_crow(Rh, ((uint64_t)mg * 4 * C + jc * HC8 + hs + 32 * t2) >> 3, h);
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                float gg, dg;
+                gelu_pair_fast(ha[e] + bv[e], gg, dg);
+                if constexpr (DROP) {
+                    const float ms = ((km >> e) & 1u) ? Rh.scale : 0.f;
+                    gg *= ms;
+                    dg *= ms;
+                }
+                gv[16 * t2 + e] = gg;
+                dv[16 * t2 + e] = ga[e] * dg;
+            }
+        }
+        lds_sync();                     // every wave is past GEMM3(j): the W2^T stage is free
+        if (more) dma<D1::NW>(rs_w2, d2.v, (unsigned)chk(j + 1) * HC8 * C, w2r, wave);
+        {   // G = the forward's g_q, exactly
+            i32x8 gq;
+            const int gs = mx_quant32(gv, gq);
+            mx_dequant32(gq, gs, gv);
+        }
+        const int fb0 = jc * HC8 + hs;
+#pragma unroll
+        for (int t2 = 0; t2 < 2; ++t2)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int f = fb0 + 32 * t2 + 8 * g + 4 * h;
+                const unsigned o = ok ? (unsigned)(tok * 4 * C + f) * 2 : kOOB;
+                buf_st4bf(rs_g, o, gv + 16 * t2 + 4 * g);
+                buf_st4bf(rs_dh, o, dv + 16 * t2 + 4 * g);
+            }
+        // dh * sw1 (the per-row scale of W1 lies along GEMM4's contraction), quantised per lane
+#pragma unroll
+        for (int t2 = 0; t2 < 2; ++t2)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const unsigned ew = *reinterpret_cast<const unsigned*>(e1s + fb0 + 32 * t2 + 8 * g + 4 * h);
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    dv[16 * t2 + 4 * g + i] = ldexpf(dv[16 * t2 + 4 * g + i], (int)((ew >> (8 * i)) & 0xff) - 127);
+            }
+        i32x8 dhq;
+        const int dhs = mx_quant32(dv, dhq);
+        xdh[wave][lane] = dhq;
+        xds[wave][lane] = dhs;
+        // W1^T(j) landed: younger than it are W1(j+1), W2^T(j+1) (when issued) and this chunk's stores
+        if (more) vmwait<2 * D1::NW + NST>(); else vmwait<NST>();
+        lds_sync();                     // W1^T(j) and every wave's dh visible
+        const i32x8 dhp = xdh[wave ^ 1][lane];
+        const int dsp = xds[wave ^ 1][lane];
+        const int hp = 64 * (1 - u);    // the partner's hidden features
+#pragma unroll
+        for (int q = 0; q < TH; ++q) {
+            const int ft = u * TH + q;
+            const i32x8 a0 = frag8<HC8>(w3r, 32 * ft + r, hs + 32 * h);
+            const i32x8 a1 = frag8<HC8>(w3r, 32 * ft + r, hp + 32 * h);
+            acc[q] = mfma8(a0, dhq, acc[q], 127, dhs);
+            acc[q] = mfma8(a1, dhp, acc[q], 127, dsp);
+        }
+        lds_sync();                     // every wave is past GEMM4(j): the W1^T stage and xdh are free
+        if (more) dma<D3::NW>(rs_w3, d3.v, (unsigned)chk(j + 1) * HC8, w3r, wave);
+    };
+    for (int j = 0; j < NCH; j += 2) {
+        step(iconst<0>{}, j);
+        step(iconst<1>{}, j + 1);
+    }
+
+    // dx features [u C/2, (u+1) C/2) of the wave's 32 tokens
+    const auto rs_dx = buf_rsrc(dX + m0 * C, rows * C * 2);
+#pragma unroll
+    for (int q = 0; q < TH; ++q)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int f = (u * TH + q) * 32 + 8 * g + 4 * h;
+            float v[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = acc[q][4 * g + e];
+            buf_st4bf(rs_dx, ok ? (unsigned)(tok * C + f) * 2 : kOOB, v);
+        }
+}
+
+template <int C>
+int fp8_bwd_launch(long M, const void* x, const void* dy, const void* w1, const float* sw1, const float* b1, const void* w2t,
+                   const float* sw2, const void* w1tp, void* dh, void* g, void* dx, const MlpDrop* d, long rpi, hipStream_t st) {
+    const dim3 grid((unsigned)((M + BM - 1) / BM));
+    if (d)
+        mlp_fp8_bwd_kernel<C, true><<<grid, MT, 0, st>>>(M, (const bf16*)x, (const bf16*)dy, (const uint8_t*)w1, sw1, b1,
+                                                         (const uint8_t*)w2t, sw2, (const uint8_t*)w1tp, (bf16*)dh, (bf16*)g,
+                                                         (bf16*)dx, *d, rpi);
+    else
+        mlp_fp8_bwd_kernel<C, false><<<grid, MT, 0, st>>>(M, (const bf16*)x, (const bf16*)dy, (const uint8_t*)w1, sw1, b1,
+                                                          (const uint8_t*)w2t, sw2, (const uint8_t*)w1tp, (bf16*)dh, (bf16*)g,
+                                                          (bf16*)dx, MlpDrop{}, rpi);
+    return check_launch("mlp_fp8_bwd");
+}
+
 }  // namespace
 }  // namespace csu
 
@@ -679,4 +1139,44 @@ extern "C" int csu_mlp_bwd_dp(long M, int C, const void* x, const void* dy, cons
 extern "C" int csu_mlp_bwd(long M, int C, const void* x, const void* dy, const void* w1, const float* b1, const void* w2,
                            void* dh, void* g, void* dx, void* stream) {
     return csu_mlp_bwd_dp(M, C, x, dy, w1, b1, w2, dh, g, dx, nullptr, stream);
+}
+
+extern "C" int csu_mlp_fp8_supported(int C) { return C == 128 || C == 256; }
+
+extern "C" int csu_mlp_fp8_fwd(long M, int C, const void* x, const void* w1q, const float* sw1, const float* b1,
+                               const void* w2p, const float* sw2, const float* b2, const float* res, float* out,
+                               const csu_mlp_dropout* d, void* stream) {
+    if (M < 1 || !x || !w1q || !sw1 || !b1 || !w2p || !sw2 || !b2 || !res || !out)
+        return fail(CSU_E_ARG, "mlp_fp8_fwd: bad arguments");
+    if (M * 4L * C * 2 > 0x7fffffffL) return fail(CSU_E_ARG, "mlp_fp8_fwd: tensor exceeds 2 GB buffer range");
+    MlpDrop md{};
+    const int e = mlp_drop_of(d, md);
+    if (e < 0) return e;
+    const MlpDrop* dp = d && e == 0 ? &md : nullptr;
+    const long rpi = d ? (long)d->rows_per_sample : 0;
+    const hipStream_t st = as_stream(stream);
+    switch (C) {
+        case 128: return fp8_fwd_launch<128>(M, x, w1q, sw1, b1, w2p, sw2, b2, res, out, dp, rpi, st);
+        case 256: return fp8_fwd_launch<256>(M, x, w1q, sw1, b1, w2p, sw2, b2, res, out, dp, rpi, st);
+        default: return fail(CSU_E_UNSUPPORTED, "mlp_fp8_fwd: C must be 128 or 256");
+    }
+}
+
+extern "C" int csu_mlp_fp8_bwd(long M, int C, const void* x, const void* dy, const void* w1q, const float* sw1,
+                               const float* b1, const void* w2t, const float* sw2, const void* w1tp, void* dh, void* g,
+                               void* dx, const csu_mlp_dropout* d, void* stream) {
+    if (M < 1 || !x || !dy || !w1q || !sw1 || !b1 || !w2t || !sw2 || !w1tp || !dh || !g || !dx)
+        return fail(CSU_E_ARG, "mlp_fp8_bwd: bad arguments");
+    if (M * 4L * C * 2 > 0x7fffffffL) return fail(CSU_E_ARG, "mlp_fp8_bwd: tensor exceeds 2 GB buffer range");
+    MlpDrop md{};
+    const int e = mlp_drop_of(d, md);
+    if (e < 0) return e;
+    const MlpDrop* dp = d && e == 0 ? &md : nullptr;
+    const long rpi = d ? (long)d->rows_per_sample : 0;
+    const hipStream_t st = as_stream(stream);
+    switch (C) {
+        case 128: return fp8_bwd_launch<128>(M, x, dy, w1q, sw1, b1, w2t, sw2, w1tp, dh, g, dx, dp, rpi, st);
+        case 256: return fp8_bwd_launch<256>(M, x, dy, w1q, sw1, b1, w2t, sw2, w1tp, dh, g, dx, dp, rpi, st);
+        default: return fail(CSU_E_UNSUPPORTED, "mlp_fp8_bwd: C must be 128 or 256");
+    }
 }

@@ -142,6 +142,11 @@ _SIGS = {
     "csu_fp8_gemm": (ctypes.c_int, [ctypes.c_long, ctypes.c_int, ctypes.c_int] + [c_void_p] * 7),
     "csu_layernorm_fwd_fp8": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, c_float, ctypes.c_int] + [c_void_p] * 8),
     "csu_dequant_e4m3_rows": (ctypes.c_int, [ctypes.c_long, ctypes.c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "csu_e4m3_layout_batch": (ctypes.c_int, [c_void_p, ctypes.c_int, ctypes.c_long, c_void_p]),
+    "csu_mlp_fp8_supported": (ctypes.c_int, [ctypes.c_int]),
+    "csu_mlp_fp8_fwd": (ctypes.c_int, [ctypes.c_long, ctypes.c_int] + [c_void_p] * 9 + [ctypes.POINTER(MlpDropout), c_void_p]),
+    "csu_mlp_fp8_bwd": (ctypes.c_int, [ctypes.c_long, ctypes.c_int] + [c_void_p] * 11 + [ctypes.POINTER(MlpDropout),
+                                                                                         c_void_p]),
     "csu_mlp_supported": (ctypes.c_int, [ctypes.c_int]),
     "csu_dropout_apply": (ctypes.c_int, [ctypes.c_long, ctypes.c_int, ctypes.c_int, c_void_p, c_void_p, ctypes.c_int,
                                          c_void_p, c_void_p, ctypes.c_long, c_void_p, ctypes.c_uint, c_float, c_void_p]),

@@ -548,7 +548,8 @@ class CSWinTransformer(nn.Module):
             sources = None
             if getattr(self, "_weight_format", "bf16") == "fp8_e4m3" and cd == torch.bfloat16:
                 if self._fp8 is None or not self._fp8.valid_for(weights):
-                    self._fp8 = ops.Fp8Weights(weights)
+                    pairs = [(m.fc1.weight, m.fc2.weight) for m in self.modules() if isinstance(m, Mlp)]
+                    self._fp8 = ops.Fp8Weights(weights, mlp_pairs=pairs)
                 sources = self._fp8.quantize()     # one launch: e4m3 per row, dequantised fp32 copies
             # one launch per step: bf16 shadows of every Linear weight (+ transposes) and conv layouts
             self._cast_cache.refresh(weights, cd, self._conv_weights(), sources=sources)

@@ -1476,6 +1476,77 @@ class _MlpFusedFn(torch.autograd.Function):
         return dy.to(rdt), dx.view(xshape), dw1.to(w1dt), db1.to(b1dt), dw2.to(w2dt), db2.to(b2dt), None, None, None
 
 
+class _MlpFp8Fn(torch.autograd.Function):
+    """res + fc2(gelu(fc1(x))) with e4m3 weights (BASELINE config 5, "fp8 MFMA weights") in ONE
+    csu_mlp_fp8_fwd launch on v_mfma_scale_f32_32x32x64_f8f6f4: x and the hidden activations are
+    quantised in registers with MX block scales (per token and 32-value block), the weights' per-row
+    power-of-two scales ride in the MFMA's E8M0 operands.  Backward (straight-through): one
+    csu_mlp_fp8_bwd launch recomputes h exactly, runs dY W2 and dh W1 on the same fp8 MFMA (dY / dh
+    quantised the same way, the weight scales folded into them) and writes dh, g_q (the forward's
+    fc2 input) and dx; then the two bf16 weight gradients dW1 = dh^T x, dW2 = dY^T g_q."""
+
+    @staticmethod
+    def forward(ctx, res, x, w1, b1, w2, b2, ops8, drop):
+        C = x.shape[-1]
+        res2 = res.float().contiguous().view(-1, C)
+        x2 = x.reshape(-1, C).contiguous()
+        if x2.dtype != torch.bfloat16:
+            x2 = x2.to(torch.bfloat16)
+        w1q, sw1, w2p, sw2, w2t, w1tp = ops8
+        b1f = b1.detach().float().contiguous()
+        b2f = b2.detach().float().contiguous()
+        y = torch.empty_like(res2)
+        M = x2.shape[0]
+        rpi = x.shape[1] if x.dim() == 3 else M
+        dd = ctypes.byref(_mlp_desc(drop, rpi))
+        _launch("mlp_fwd", lambda: lib().csu_mlp_fp8_fwd(M, C, ptr(x2), ptr(w1q), ptr(sw1), ptr(b1f), ptr(w2p), ptr(sw2),
+                                                         ptr(b2f), ptr(res2), ptr(y), dd, stream_ptr(x2.device)),
+                16 * M * C * C, M * C * (2 + 4 + 4) + 8 * C * C, prec="fp8")
+        ctx.drop, ctx.rpi = drop, rpi
+        ctx.save_for_backward(x2, b1f)
+        ctx.ops8 = ops8
+        ctx.meta = (res.dtype, x.shape, w1.dtype, b1.dtype, w2.dtype, b2.dtype)
+        ctx.params = (w1, b1, w2, b2)
+        _note_use(*ctx.params)
+        return y.view(res.shape)
+
+    @staticmethod
+    def backward(ctx, dy):
+        rdt, xshape, w1dt, b1dt, w2dt, b2dt = ctx.meta
+        x2, b1f = ctx.saved_tensors
+        w1q, sw1, w2p, sw2, w2t, w1tp = ctx.ops8
+        M, C = x2.shape
+        drop = ctx.drop
+        if drop is None:
+            dyb = _bf16_of(dy).view(-1, C)
+        else:
+            dyb = drop.out_grad(dy.reshape(-1, C).contiguous(), torch.bfloat16)
+        dyb = dyb.contiguous()
+        dh = torch.empty(M, 4 * C, dtype=torch.bfloat16, device=x2.device)
+        g = torch.empty_like(dh)
+        dx = torch.empty(M, C, dtype=torch.bfloat16, device=x2.device)
+        dd = ctypes.byref(_mlp_desc(drop, ctx.rpi))
+        _launch("mlp_bwd", lambda: lib().csu_mlp_fp8_bwd(M, C, ptr(x2), ptr(dyb), ptr(w1q), ptr(sw1), ptr(b1f), ptr(w2t),
+                                                         ptr(sw2), ptr(w1tp), ptr(dh), ptr(g), ptr(dx), dd,
+                                                         stream_ptr(x2.device)),
+                24 * M * C * C, M * C * (2 + 2 + 2) + M * 4 * C * (2 + 2) + 12 * C * C, prec="fp8")
+        dw2, db2 = wgrad_maybe_side(dyb, g, w2dt, b2dt, params=ctx.params[2:])
+        dw1, db1 = wgrad_maybe_side(dh, x2, w1dt, b1dt, params=ctx.params[:2])
+        return dy.to(rdt), dx.view(xshape), dw1.to(w1dt), db1.to(b1dt), dw2.to(w2dt), db2.to(b2dt), None, None
+
+
+def mlp_fp8(res, x, fc1: torch.nn.Linear, fc2: torch.nn.Linear, drop: Optional[MlpDrop] = None):
+    """The fp8 fused Mlp (_MlpFp8Fn) when the active fp8 weight format holds fc1 / fc2 as an Mlp pair
+    (model.set_weight_format('fp8_e4m3') under bf16 autocast), else None."""
+    if _ACTIVE_FP8 is None or not x.is_cuda:
+        return None
+    ops8 = _ACTIVE_FP8.mlp_operands(fc1.weight, fc2.weight)
+    if ops8 is None:
+        return None
+    with torch.autocast("cuda", enabled=False):
+        return _MlpFp8Fn.apply(res, x, fc1.weight, fc1.bias, fc2.weight, fc2.bias, ops8, drop)
+
+
 # the fused one-launch Mlp where the library has it (C in {64, 128, 256}); otherwise two gemm4 launches
 FUSED_MLP = True
 
@@ -1484,6 +1555,9 @@ def mlp_residual(res, x, fc1: torch.nn.Linear, fc2: torch.nn.Linear, drop: Optio
     """res + DropPath(Dropout(fc2(Dropout(gelu(fc1(x)))))) on the bf16 path (``drop`` None: eval /
     no dropout)."""
     C = x.shape[-1]
+    y = mlp_fp8(res, x, fc1, fc2, drop)
+    if y is not None:
+        return y
     if FUSED_MLP and fc1.out_features == 4 * C and lib().csu_mlp_supported(C):
         with torch.autocast("cuda", enabled=False):
             return _MlpFusedFn.apply(res, x, fc1.weight, fc1.bias, fc2.weight, fc2.bias, _weight_bf16(fc1.weight),
@@ -1685,7 +1759,7 @@ class Fp8Weights:
     shadows, ``q`` / ``scales`` the e4m3 bytes and row scales.  Gradients flow to the fp32 masters
     (straight-through).  1-D tensors (biases, LN) are not quantised."""
 
-    def __init__(self, params):
+    def __init__(self, params, mlp_pairs=()):
         import numpy as np
         self.params = list(params)
         self.deq, self.q, self.scales = [], [], []
@@ -1713,6 +1787,39 @@ class Fp8Weights:
         self.items = torch.frombuffer(bytearray(rec.tobytes()), dtype=torch.uint8).to(self.params[0].device)
         self.ptrs = [p.data_ptr() for p in self.params]
         self.index = {p.data_ptr(): i for i, p in enumerate(self.params) if p.dim() >= 2}
+        # operand layouts of the fp8 fused Mlp (csu_mlp_fp8_fwd / _bwd), rebuilt from the e4m3 bytes
+        # after every quantisation by one csu_e4m3_layout_batch launch: W2 with permuted columns,
+        # W2^T, W1^T with permuted columns
+        self.mlp = {}
+        lay, w0 = [], 0
+        for w1, w2 in mlp_pairs:
+            i1, i2 = self.index.get(w1.data_ptr()), self.index.get(w2.data_ptr())
+            if i1 is None or i2 is None:
+                continue
+            q1, q2 = self.q[i1], self.q[i2]
+            N4, C = q1.shape
+            if tuple(q2.shape) != (C, N4) or not lib().csu_mlp_fp8_supported(C):
+                continue
+            w2p = torch.empty_like(q2)
+            w2t = torch.empty(N4, C, dtype=torch.uint8, device=q2.device)
+            w1tp = torch.empty(C, N4, dtype=torch.uint8, device=q1.device)
+            for src, dst, rows, cols, mode in ((q2, w2p, C, N4, 2), (q2, w2t, C, N4, 1), (q1, w1tp, N4, C, 3)):
+                lay.append((src.data_ptr(), dst.data_ptr(), w0, rows, cols, mode, 0))
+                w0 += rows * cols // 4
+            self.mlp[w1.data_ptr()] = (w2.data_ptr(), q1, self.scales[i1], w2p, self.scales[i2], w2t, w1tp)
+        self.lay_count, self.lay_words = len(lay), w0
+        if lay:
+            lt = np.dtype([("src", "<u8"), ("dst", "<u8"), ("w0", "<i8"), ("rows", "<i4"), ("cols", "<i4"),
+                           ("mode", "<i4"), ("pad", "<i4")])
+            self.lay_items = torch.frombuffer(bytearray(np.array(lay, dtype=lt).tobytes()),
+                                              dtype=torch.uint8).to(self.params[0].device)
+
+    def mlp_operands(self, w1, w2):
+        """(w1q, sw1, w2p, sw2, w2t, w1tp) of the fused fp8 Mlp over fc1 / fc2 weights, or None."""
+        e = self.mlp.get(w1.data_ptr())
+        if e is None or e[0] != w2.data_ptr():
+            return None
+        return e[1:]
 
     def lookup(self, w):
         """(e4m3 bytes, row scales) of a quantised weight, or None."""
@@ -1730,6 +1837,9 @@ class Fp8Weights:
         dev = self.params[0].device
         _launch("quant_e4m3", lambda: lib().csu_quant_e4m3_batch(ptr(self.items), self.count, self.rows, stream_ptr(dev)),
                 0, sum(p.numel() for p, q in zip(self.params, self.q) if q is not None) * 9)
+        if self.lay_count:
+            _launch("quant_e4m3", lambda: lib().csu_e4m3_layout_batch(ptr(self.lay_items), self.lay_count, self.lay_words,
+                                                                     stream_ptr(dev)), 0, self.lay_words * 8)
         return self.deq
 
 

@@ -358,6 +358,22 @@ int csu_layernorm_fwd_fp8(int rows, int C, float eps, int xdtype, const void* x,
                           const float* beta, void* yq, float* yscale, float* mean, float* rstd, void* stream);
 /* out (bf16, rows x cols) = e4m3fn(q) * scale[row]; cols % 8 == 0 */
 int csu_dequant_e4m3_rows(long rows, int cols, const void* q, const float* scale, void* out, void* stream);
+/* e4m3 byte layouts of quantised weights (the fp8 fused Mlp's operand images): per item, src is a
+ * rows x cols byte matrix; mode bit 0 = transpose (dst is cols x rows), bit 1 = permute the dst
+ * columns inside every 64-column block: dst column 32h + 16t + 4g + i (h, t in {0,1}, g, i in 0..3)
+ * takes column 32t + 8g + 4h + i of the (transposed) source -- the k order in which a 32x32 MFMA
+ * accumulator tile pair reaches an f8 operand lane.  Permuting modes need a dst column count
+ * % 64 == 0; every mode needs dst columns % 4 == 0.  items: DEVICE array sorted by word0 (prefix sum
+ * of the items' dst sizes in 4-byte words); one thread per dst word. */
+typedef struct {
+    const uint8_t* src;
+    uint8_t* dst;
+    int64_t word0;
+    int32_t rows, cols;        /* of src */
+    int32_t mode;
+    int32_t pad;
+} csu_e4m3_layout_item;
+int csu_e4m3_layout_batch(const csu_e4m3_layout_item* items, int count, long total_words, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * Fused multi-tensor AdamW step (torch.optim.AdamW semantics, cswin:937-941): for every item,
@@ -463,6 +479,28 @@ int csu_mlp_fwd_dp(long M, int C, const void* x, const void* w1, const float* b1
                    const float* res, float* out, const csu_mlp_dropout* d, void* stream);
 int csu_mlp_bwd_dp(long M, int C, const void* x, const void* dy, const void* w1, const float* b1, const void* w2,
                    void* dh, void* g, void* dx, const csu_mlp_dropout* d, void* stream);
+/* fp8-e4m3 fused Mlp forward (BASELINE config 5, "fp8 MFMA weights"; same math and dropout as
+ * csu_mlp_fwd_dp) on v_mfma_scale_f32_32x32x64_f8f6f4 with MX block scales:
+ *   h   = x_q W1^T + b1, x_q = x quantised per (token, 32 consecutive channels): scale 2^e, e the
+ *         smallest integer with amax <= 448 * 2^e, e4m3fn round-to-nearest-even;
+ *   g   = gelu(h) (* hidden dropout), g_q = g quantised per (token, block), block = the 32
+ *         features of a 64-feature group whose index has equal bit 2 (f & 4);
+ *   out = res + (g_q W2^T + b2) (* output dropout, DropPath).
+ * w1q: (4C, C) e4m3 rows with power-of-two row scales sw1 (4C); w2p: (C, 4C) e4m3 rows (scales sw2,
+ * C) with the columns permuted as csu_e4m3_layout_batch mode 2.  C in {128, 256}. */
+int csu_mlp_fp8_supported(int C);
+int csu_mlp_fp8_fwd(long M, int C, const void* x, const void* w1q, const float* sw1, const float* b1,
+                    const void* w2p, const float* sw2, const float* b2, const float* res, float* out,
+                    const csu_mlp_dropout* d, void* stream);
+/* Its backward (straight-through for every quantisation): h recomputed exactly as the forward;
+ *   dg = (dy * sw2)_q W2q: w2t = W2q^T (4C, C) e4m3 (layout mode 1), dy quantised per (token, 32
+ *        consecutive channels) after the per-channel scale sw2 (W2's row scale lies along this sum);
+ *   dh = dg * gelu'(h) (* hidden mask) -> dh (bf16, M x 4C); g = g_q of the forward (bf16, exact);
+ *   dx = (dh * sw1)_q W1q: w1tp = W1q^T (C, 4C) with permuted columns (layout mode 3), dh * sw1
+ *        quantised per (token, block) as g.  dx bf16 (M, C).  dy carries the output mask. */
+int csu_mlp_fp8_bwd(long M, int C, const void* x, const void* dy, const void* w1q, const float* sw1,
+                    const float* b1, const void* w2t, const float* sw2, const void* w1tp, void* dh, void* g,
+                    void* dx, const csu_mlp_dropout* d, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * Implicit-GEMM NHWC convolution (patch embed cswin:505, Merge_Block.conv cswin:376, CARAFE

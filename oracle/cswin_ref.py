@@ -127,8 +127,20 @@ def _drop_path(drop, name, t):
     return t if m is None else t * m.reshape(-1, *([1] * (t.dim() - 1)))
 
 
+# Optional fp8 form of the Mlp (None: the reference form).  The fp8 parity tests install a function
+# (x, p, key, hidden_mask) -> fc2 output, or None to keep the reference form for that Mlp, that runs
+# the roundings of the fp8 weight format (oracle/fp8_ref.py).
+MLP_FP8 = None
+
+
 def mlp(x: torch.Tensor, p: Params, key: str, drop=None) -> torch.Tensor:
     """fc1 -> exact-erf GELU -> Dropout -> fc2 -> Dropout (cswin:180-196)."""
+    if MLP_FP8 is not None:
+        hshape = tuple(x.shape[:-1]) + (p[key + ".fc1.weight"].shape[0],)
+        m_h = drop(key + ".h", hshape) if drop is not None else None
+        y = MLP_FP8(x, p, key, m_h)
+        if y is not None:
+            return _drop(drop, key + ".o", y)
     h = _drop(drop, key + ".h", F.gelu(_lin(x, p, key + ".fc1")))
     return _drop(drop, key + ".o", _lin(h, p, key + ".fc2"))
 

@@ -1,0 +1,111 @@
+"""fp8-e4m3 pieces of BASELINE config 5 ("fp8 MFMA weights") -- TEST INFRASTRUCTURE ONLY.
+
+The reference trains in fp32 (cswin:865-941); it has no fp8 path.  These functions restate, in
+float64 on the CPU, the quantisation rules the csu fp8 kernels document (include/csu.h:
+csu_quant_e4m3_batch, csu_mlp_fp8_fwd / csu_mlp_fp8_bwd), so the parity tests can run the
+reference's Mlp (cswin:180-196) with exactly the roundings the device applies.  Parity of these
+rules against the reference is therefore "parity unpinned": the reference has no such format;
+what is pinned is that the device computes the reference Mlp on these rounded operands.
+
+* per-row weight quantisation: s = 2^ceil(log2(amax / 448)), q = e4m3fn(w / s) round-to-nearest-even
+* MX block quantisation (activations, gradients): per block of 32 values, s = 2^e with e the smallest
+  integer such that amax <= 448 * 2^e (0 for an all-zero block, clamped to [-127, 127]),
+  q = e4m3fn(v / s); blocks are 32 consecutive channels ("nat") or, along the Mlp's hidden features,
+  the 32 features of each 64-feature group whose index has the same bit 2 ("perm": the set a
+  32x32 MFMA accumulator-tile pair hands one operand lane).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as F
+
+E4M3_MAX = 448.0
+
+
+def _e4m3(v: torch.Tensor) -> torch.Tensor:
+    """Round to the nearest e4m3fn value (RNE; |v| <= 448 by construction of the scales)."""
+    return v.float().to(torch.float8_e4m3fn).to(torch.float64)
+
+
+def block_exponent(amax: torch.Tensor) -> torch.Tensor:
+    """e = the smallest integer with amax <= 448 * 2^e, 0 for amax == 0, clamped to [-127, 127]
+    (amax = m 2^E with m in [1, 2): e = E - 8 + (m > 1.75), since 448 = 1.75 * 2^8)."""
+    a = amax.double()
+    m, E = torch.frexp(a)                       # a = m 2^E, m in [0.5, 1)
+    e = (E - 1) - 8 + (2 * m > 1.75).to(E.dtype)
+    e = torch.where(a > 0, e, torch.zeros_like(e))
+    return e.clamp(-127, 127)
+
+
+def mx_quant_nat(v: torch.Tensor) -> torch.Tensor:
+    """MX e4m3 rounding (dequantised, float64) with blocks of 32 consecutive values of the last dim."""
+    shp = v.shape
+    b = v.double().reshape(*shp[:-1], shp[-1] // 32, 32)
+    s = torch.exp2(block_exponent(b.abs().amax(-1, keepdim=True)).double())
+    return (_e4m3(b / s) * s).reshape(shp)
+
+
+def mx_quant_perm(v: torch.Tensor) -> torch.Tensor:
+    """MX e4m3 rounding with the hidden-feature blocks of the fused Mlp: inside every 64-feature
+    group, the features with index bit 2 == 0 form one block, those with bit 2 == 1 the other."""
+    shp = v.shape
+    # feature 32 t + 8 g + 4 h + i of a group -> dims (t, g, h, i)
+    b = v.double().reshape(*shp[:-1], shp[-1] // 64, 2, 4, 2, 4)
+    s = torch.exp2(block_exponent(b.abs().amax(dim=(-4, -3, -1), keepdim=True)).double())
+    return (_e4m3(b / s) * s).reshape(shp)
+
+
+def quant_rows(w: torch.Tensor):
+    """(dequantised weight, e4m3 values q, row scales s) of csu_quant_e4m3_batch."""
+    w2 = w.reshape(w.shape[0], -1).double()
+    amax = w2.abs().amax(1)
+    s = torch.where(amax > 0, torch.exp2(torch.ceil(torch.log2(amax / E4M3_MAX))), torch.ones_like(amax))
+    q = _e4m3(w2 / s[:, None])
+    return (q * s[:, None]).reshape(w.shape), q.reshape(w.shape), s
+
+
+class Fp8MlpFn(torch.autograd.Function):
+    """fc2(Dropout(gelu(fc1(x)))) of cswin:180-196 with the fp8 fused Mlp's roundings (float64):
+
+    forward   h = mx_nat(x) W1^T + b1,  g = gelu(h) * m_h,  y = mx_perm(g) W2^T + b2
+    backward  (straight-through: gradients flow through every rounding unchanged, except that the
+              device multiplies rounded operands in the two input-gradient products as well)
+              dg = mx_nat(dy * s2) q2,  dh = dg * gelu'(h) * m_h,  dx = mx_perm(dh * s1) q1,
+              dW1 = dh^T x,  db1 = sum dh,  dW2 = dy^T mx_perm(g),  db2 = sum dy
+    w1 = q1 * s1[:, None], w2 = q2 * s2[:, None] are the dequantised e4m3 weights (quant_rows);
+    m_h the hidden dropout mask (scale 0 or 1/keep) or None."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2, s1, s2, m_h):
+        xd = x.double()
+        h = mx_quant_nat(xd) @ w1.double().t() + b1.double()
+        g = F.gelu(h)
+        if m_h is not None:
+            g = g * m_h
+        gq = mx_quant_perm(g)
+        ctx.save_for_backward(xd, h, gq, w1.double(), w2.double(), s1.double(), s2.double())
+        ctx.m_h = m_h
+        return gq @ w2.double().t() + b2.double()
+
+    @staticmethod
+    def backward(ctx, dy):
+        xd, h, gq, w1, w2, s1, s2 = ctx.saved_tensors
+        dy = dy.double()
+        q1, q2 = w1 / s1[:, None], w2 / s2[:, None]
+        dg = mx_quant_nat(dy * s2) @ q2
+        dgelu = 0.5 * (1 + torch.erf(h / math.sqrt(2))) + h * torch.exp(-0.5 * h * h) / math.sqrt(2 * math.pi)
+        dh = dg * dgelu
+        if ctx.m_h is not None:
+            dh = dh * ctx.m_h
+        dx = mx_quant_perm(dh * s1) @ q1
+        lead = dy.reshape(-1, dy.shape[-1])
+        dh2 = dh.reshape(-1, dh.shape[-1])
+        dw1 = dh2.t() @ xd.reshape(-1, xd.shape[-1])
+        dw2 = lead.t() @ gq.reshape(-1, gq.shape[-1])
+        return dx, dw1, dh2.sum(0), dw2, lead.sum(0), None, None, None
+
+
+def fp8_mlp(x, w1, b1, w2, b2, s1, s2, m_h=None):
+    return Fp8MlpFn.apply(x, w1, b1, w2, b2, s1, s2, m_h)

@@ -83,9 +83,15 @@ def test_fp8_weight_model_vs_oracle_with_quantized_weights(monkeypatch):
     calls = []
     real = ops.fp8_gemm
     monkeypatch.setattr(ops, "fp8_gemm", lambda *a, **k: calls.append(1) or real(*a, **k))
+    mcalls = []
+    real_mlp = ops.mlp_fp8
+    monkeypatch.setattr(ops, "mlp_fp8", lambda *a, **k: (lambda r: mcalls.append(r is not None) or r)(real_mlp(*a, **k)))
     with torch.autocast("cuda", dtype=torch.bfloat16):
         y = m(x.to(d))
     assert len(calls) == sum(1 for mod in m.modules() if type(mod).__name__ == "CSWinBlock")   # every qkv on fp8 MFMA
+    # every Mlp at C = 128 / 256 on the fp8 fused kernels
+    assert sum(mcalls) == sum(1 for mod in m.modules() if type(mod).__name__ == "Mlp" and mod.fc1.in_features in (128, 256))
+    assert sum(mcalls) > 10
     loss = bce_loss(y, t.to(d))
     loss.backward()
     # the oracle on the dequantised e4m3 weights of exactly the tensors the fp8 format quantises
@@ -99,6 +105,18 @@ def test_fp8_weight_model_vs_oracle_with_quantized_weights(monkeypatch):
     assert sum(1 for w in m._linear_weights() if id(w) in quant) > 100
     pref = {k: v.double().requires_grad_(True) for k, v in pq.items()}
     monkeypatch.setattr(O, "QKV_INPUT_QUANT", _tok_quant)
+    # the Mlps at C = 128 / 256 run the fp8 fused kernels: their MX roundings (oracle/fp8_ref.py)
+    from oracle import fp8_ref as Q
+
+    def mlp_fp8(xx, pp, key, m_h):
+        if xx.shape[-1] not in (128, 256):
+            return None
+        s1 = Q.quant_rows(p[key + ".fc1.weight"])[2]
+        s2 = Q.quant_rows(p[key + ".fc2.weight"])[2]
+        return Q.fp8_mlp(xx, pp[key + ".fc1.weight"], pp[key + ".fc1.bias"], pp[key + ".fc2.weight"],
+                         pp[key + ".fc2.bias"], s1, s2, m_h)
+    monkeypatch.setattr(O, "MLP_FP8", mlp_fp8)
+
     yr = O.cswin_forward(pref, x.double(), cfg)
     lr = O.bce_loss(yr, t.double())
     lr.backward()
@@ -176,3 +194,128 @@ def test_fp8_gemm_rejects_bad_shapes():
     wq = torch.zeros(64, 96, dtype=torch.uint8, device=d)
     with pytest.raises(CsuError):
         ops.fp8_gemm(aq, torch.ones(16, device=d), wq, torch.ones(64, device=d))
+
+
+def _perm64(q: torch.Tensor) -> torch.Tensor:
+    """columns permuted per 64-block: dst 32h + 16t + 4g + i <- src 32t + 8g + 4h + i"""
+    idx = torch.empty(64, dtype=torch.long)
+    for h in range(2):
+        for t in range(2):
+            for g in range(4):
+                for i in range(4):
+                    idx[32 * h + 16 * t + 4 * g + i] = 32 * t + 8 * g + 4 * h + i
+    n = q.shape[1]
+    full = (torch.arange(n // 64)[:, None] * 64 + idx[None, :]).reshape(-1)
+    return q[:, full]
+
+
+@pytest.mark.parametrize("C", [128, 256])
+def test_e4m3_mlp_layouts(C):
+    """csu_e4m3_layout_batch: W2 with permuted columns, W2^T, W1^T with permuted columns, bytewise."""
+    from csu import ops
+    d = dev()
+    g = torch.Generator().manual_seed(C)
+    w1 = (torch.randn(4 * C, C, generator=g) * 0.05).to(d)
+    w2 = (torch.randn(C, 4 * C, generator=g) * 0.05).to(d)
+    fp8 = ops.Fp8Weights([w1, w2], mlp_pairs=[(w1, w2)])
+    fp8.quantize()
+    w1q, sw1, w2p, sw2, w2t, w1tp = fp8.mlp_operands(w1, w2)
+    torch.cuda.synchronize()
+    q1, q2 = w1q.cpu(), fp8.q[1].cpu()
+    assert torch.equal(w2p.cpu(), _perm64(q2))
+    assert torch.equal(w2t.cpu(), q2.t().contiguous())
+    assert torch.equal(w1tp.cpu(), _perm64(q1.t().contiguous()))
+
+
+def _mx_torch_check():
+    """the oracle's MX rule on known values: block amax 448 -> e = 0, 449 -> 1, 1.75 * 2^-3 -> e = -11"""
+    from oracle import fp8_ref as Q
+    e = Q.block_exponent(torch.tensor([448.0, 449.0, 1.75 * 2 ** -3, 0.0, 1.0]))
+    assert e.tolist() == [0, 1, -11, 0, -8]
+
+
+@pytest.mark.parametrize("C,M,drop", [(128, 1000, False), (256, 4160, False), (256, 100, True), (128, 777, True)])
+def test_mlp_fp8_fused_vs_oracle(C, M, drop):
+    """csu_mlp_fp8_fwd / csu_mlp_fp8_bwd vs the fp64 restatement of the same roundings
+    (oracle/fp8_ref.py: MX-quantised x / g / dY / dh, e4m3 weights with per-row scales).  Only the
+    device's fast GELU (|err| < 1.3e-5) and fp32 accumulation differ from the oracle, which can flip
+    a rare e4m3 rounding of g or dh by one step: the gates are relative L2 errors, and the device is
+    required to sit far closer to the fp8 oracle than to the unrounded Mlp."""
+    import ctypes
+    from csu import ops, rng
+    from csu._lib import check, lib, ptr, stream_ptr
+    from oracle import fp8_ref as Q
+    _mx_torch_check()
+    d = dev()
+    torch.manual_seed(C + M)
+    x = torch.randn(M, C, device=d).bfloat16()
+    w1 = torch.randn(4 * C, C, device=d) * C ** -0.5
+    w2 = torch.randn(C, 4 * C, device=d) * (4 * C) ** -0.5
+    b1, b2 = torch.randn(4 * C, device=d) * 0.1, torch.randn(C, device=d) * 0.1
+    res = torch.randn(M, C, device=d)
+    dz = (torch.randn(M, C, device=d) * 1e-3).bfloat16()      # gradient of the (dropped) fc2 output
+    fp8 = ops.Fp8Weights([w1, w2], mlp_pairs=[(w1, w2)])
+    fp8.quantize()
+    w1q, sw1, w2p, sw2, w2t, w1tp = fp8.mlp_operands(w1, w2)
+    snap = _snap_t(d, 5, 2)
+    if drop:
+        rps = max(1, M // 3)
+        rs = rng.droppath_scale(snap, 30, 0.3, -(-M // rps))
+        md = ops.MlpDrop(snap, 21, 22, 0.3, rs, rps).c_struct()
+    else:
+        md = ops.MlpDrop(None, 0, 0, 0.0).c_struct()
+        md.rows_per_sample = M
+    st = stream_ptr(d)
+    y = torch.empty(M, C, device=d)
+    check(lib().csu_mlp_fp8_fwd(M, C, ptr(x), ptr(w1q), ptr(sw1), ptr(b1), ptr(w2p), ptr(sw2), ptr(b2), ptr(res), ptr(y),
+                                ctypes.byref(md), st), "mlp_fp8_fwd")
+    dh = torch.empty(M, 4 * C, device=d, dtype=torch.bfloat16)
+    gq = torch.empty_like(dh)
+    dx = torch.empty(M, C, device=d, dtype=torch.bfloat16)
+    check(lib().csu_mlp_fp8_bwd(M, C, ptr(x), ptr(dz), ptr(w1q), ptr(sw1), ptr(b1), ptr(w2t), ptr(sw2), ptr(w1tp),
+                                ptr(dh), ptr(gq), ptr(dx), ctypes.byref(md), st), "mlp_fp8_bwd")
+    torch.cuda.synchronize()
+    W1d, _, S1 = Q.quant_rows(w1.cpu())
+    W2d, _, S2 = Q.quant_rows(w2.cpu())
+    assert torch.equal(S1.float(), sw1.cpu()) and torch.equal(S2.float(), sw2.cpu())
+    X, B1, B2, R, DZ = (t.double().cpu() for t in (x, b1, b2, res, dz))
+    if drop:
+        mh = rng.dropout_mask(snap, 21, 0.3, M * 4 * C).view(M, 4 * C).double().cpu() / 0.7
+        mo = rng.dropout_mask(snap, 22, 0.3, M * C).view(M, C).double().cpu() / 0.7
+        rsr = rs.double().cpu()[torch.arange(M) // rps].view(M, 1)
+        outm = mo * rsr
+    else:
+        mh, outm = None, torch.ones(M, 1, dtype=torch.float64)
+    z = Q.fp8_mlp(X, W1d, B1, W2d, B2, S1, S2, mh)
+    yref = R + outm * z
+
+    def rel(a, b):
+        return float((a.double().cpu() - b).norm() / b.norm())
+
+    assert rel(y - res, yref - R) < 1e-2, rel(y - res, yref - R)
+    # the roundings are modelled: the unrounded Mlp (same dequantised weights) is much further away
+    h_plain = X @ W1d.T + B1
+    g_plain = torch.nn.functional.gelu(h_plain) * (mh if mh is not None else 1)
+    z_plain = g_plain @ W2d.T + B2
+    assert rel(y - res, outm * z_plain) > 5 * rel(y - res, yref - R)
+    # backward pieces
+    h = Q.mx_quant_nat(X) @ W1d.T + B1
+    g = torch.nn.functional.gelu(h) * (mh if mh is not None else 1)
+    gqr = Q.mx_quant_perm(g)
+    assert rel(gq, gqr) < 1e-2
+    assert float((gq.double().cpu() != gqr).double().mean()) < 2e-3      # rare one-step rounding flips only
+    q1, q2 = W1d / S1[:, None], W2d / S2[:, None]
+    dg = Q.mx_quant_nat(DZ * S2) @ q2
+    dgelu = 0.5 * (1 + torch.erf(h / 2 ** 0.5)) + h * torch.exp(-0.5 * h * h) / (2 * torch.pi) ** 0.5
+    dhr = dg * dgelu * (mh if mh is not None else 1)
+    assert rel(dh, dhr) < 5e-3, rel(dh, dhr)
+    dxr = Q.mx_quant_perm(dhr * S1) @ q1
+    assert rel(dx, dxr) < 1e-2, rel(dx, dxr)
+    # the autograd form of the oracle gives the same input gradient
+    Xg = X.clone().requires_grad_(True)
+    Q.fp8_mlp(Xg, W1d, B1, W2d, B2, S1, S2, mh).backward(DZ)
+    assert rel(dx, Xg.grad) < 1e-2
+
+
+def _snap_t(d, seed, ctr):
+    return torch.tensor([seed, ctr], dtype=torch.int64, device=d)
