@@ -1444,7 +1444,7 @@ __device__ __forceinline__ void lepe4_lds_z(const Win& w, const bf16* img, int n
 }
 
 template <int WM, bool DROP>
-__global__ __launch_bounds__(NT, 2) void stripe_bwd_fused_w(csu_stripe_args a, const bf16* __restrict__ qkv,
+__global__ __launch_bounds__(NT, WM <= 256 ? 2 : 1) void stripe_bwd_fused_w(csu_stripe_args a, const bf16* __restrict__ qkv,
                                                             const bf16* __restrict__ out, const bf16* __restrict__ dout,
                                                             const float* __restrict__ lse, bf16* __restrict__ dqkv,
                                                             float* __restrict__ part) {
@@ -1738,9 +1738,10 @@ __global__ __launch_bounds__(NT, 2) void stripe_bwd_fused_w(csu_stripe_args a, c
     ATT_STAMP(1, 4);
 }
 
-// the one-pass backward handles the launch (bf16, window <= 256 tokens)
+// the one-pass backward handles the launch (bf16, window <= 512 tokens: WM = 512 holds the four
+// window images in 128 KiB of LDS, one workgroup per CU)
 bool use_fused_bwd(const csu_stripe_args& a, int dtype) {
-    return dtype == CSU_BF16 && a.br[0].H_sp * a.br[0].W_sp <= 256;
+    return dtype == CSU_BF16 && a.br[0].H_sp * a.br[0].W_sp <= 512;
 }
 int fused_nblk(const csu_stripe_args& a) {
     return a.B * (a.reso / a.br[0].H_sp) * (a.reso / a.br[0].W_sp);
@@ -2005,8 +2006,10 @@ extern "C" int csu_stripe_attn_bwd_ex(const csu_stripe_args* a, int dtype, const
         // one pass: dQ, dK, dV and (do_lepe) the LePE weight-gradient partials, reduced below or deferred
         const bf16 *q = (const bf16*)qkv, *o = (const bf16*)out, *go = (const bf16*)dout;
         float* pp = do_lepe ? part : nullptr;
-        if (a->br[0].H_sp * a->br[0].W_sp <= 128) bwd_fused<128>(*a, q, o, go, lse, (bf16*)dqkv, pp, st);
-        else bwd_fused<256>(*a, q, o, go, lse, (bf16*)dqkv, pp, st);
+        const int N = a->br[0].H_sp * a->br[0].W_sp;
+        if (N <= 128) bwd_fused<128>(*a, q, o, go, lse, (bf16*)dqkv, pp, st);
+        else if (N <= 256) bwd_fused<256>(*a, q, o, go, lse, (bf16*)dqkv, pp, st);
+        else bwd_fused<512>(*a, q, o, go, lse, (bf16*)dqkv, pp, st);
         if (do_lepe && !lepe_deferred) {
             const dim3 rgrid((a->nbranch * a->heads * HD * 10 + 15) / 16);
             lepe_wgrad_reduce<<<rgrid, 256, 0, st>>>(*a, fused_nblk(*a), part);
