@@ -47,6 +47,93 @@ __global__ __launch_bounds__(NT) void quant_e4m3_rows(const csu_fp8_item* __rest
 }
 
 
+
+// Quantisation straight into the kernels' bf16 shadows (csu_quant_e4m3_shadow_batch): block = 64 rows of
+// one item.  Phase 1: a wave per row computes the row's amax (float4 loads, the lanes striding the row)
+// and its scale (the rule of quant_e4m3_rows, bit for bit).  Phase 2: 64-column tiles, thread = (row,
+// 16 columns): e4m3 bytes, the exact bf16 of q * s (the shadow), and the transposed shadow through an
+// LDS tile -- replaces the fp32 dequantised copy and the separate cast pass.
+__global__ __launch_bounds__(NT) void quant_e4m3_shadow(const csu_fp8_shadow_item* __restrict__ items, int count) {
+    __shared__ float srow[64];
+    __shared__ __attribute__((aligned(16))) bf16 T[64][64 + 8];
+    int lo = 0, hi = count - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (items[mid].blk0 <= (long)blockIdx.x) lo = mid; else hi = mid - 1;
+    }
+    const csu_fp8_shadow_item it = items[lo];
+    const int rows = it.rows, cols = it.cols;
+    const int rb = (int)((long)blockIdx.x - it.blk0) * 64;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (int i = 0; i < 16; ++i) {
+        const int lr = wave * 16 + i, row = rb + lr;
+        if (row >= rows) break;                                   // uniform per wave
+        const float* src = it.src + (long)row * cols;
+        float amax = 0.f;
+        for (int c = 4 * lane; c < cols; c += 256) {
+            const f32x4 v = *reinterpret_cast<const f32x4*>(src + c);
+            amax = fmaxf(amax, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
+        }
+        amax = wave_max(amax);
+        const float sc = amax > 0.f ? exp2f(ceilf(log2f(amax / 448.f))) : 1.f;
+        if (lane == 0) {
+            srow[lr] = sc;
+            if (it.scales) it.scales[row] = sc;
+        }
+    }
+    __syncthreads();
+    const int tr = threadIdx.x >> 2, tc = (threadIdx.x & 3) * 16;
+    const int row = rb + tr;
+    const float sc = row < rows ? srow[tr] : 1.f;
+    const float inv = 1.f / sc;   // exact: a power of two
+    bf16* const sh = (bf16*)it.shadow;
+    bf16* const st = (bf16*)it.shadow_t;
+    for (int c0 = 0; c0 < cols; c0 += 64) {
+        const int col = c0 + tc;
+        const bool ok = row < rows && col < cols;                 // cols % 16 == 0: whole 16-column runs
+        float v[16] = {};
+        if (ok) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const f32x4 x = *reinterpret_cast<const f32x4*>(it.src + (long)row * cols + col + 4 * k);
+                v[4 * k] = x[0]; v[4 * k + 1] = x[1]; v[4 * k + 2] = x[2]; v[4 * k + 3] = x[3];
+            }
+        }
+        unsigned w[4];
+        float dq[16];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            int p = __builtin_amdgcn_cvt_pk_fp8_f32(v[4 * k] * inv, v[4 * k + 1] * inv, 0, false);
+            p = __builtin_amdgcn_cvt_pk_fp8_f32(v[4 * k + 2] * inv, v[4 * k + 3] * inv, p, true);
+            w[k] = (unsigned)p;
+            const auto a = __builtin_amdgcn_cvt_pk_f32_fp8(p, false);
+            const auto b = __builtin_amdgcn_cvt_pk_f32_fp8(p, true);
+            dq[4 * k] = a[0] * sc; dq[4 * k + 1] = a[1] * sc; dq[4 * k + 2] = b[0] * sc; dq[4 * k + 3] = b[1] * sc;
+        }
+        if (ok) {
+            if (it.q) *reinterpret_cast<u32x4*>(it.q + (long)row * cols + col) = u32x4{w[0], w[1], w[2], w[3]};
+            store8(sh + (long)row * cols + col, dq);
+            store8(sh + (long)row * cols + col + 8, dq + 8);
+        }
+        if (st) {
+#pragma unroll
+            for (int j = 0; j < 16; ++j) T[tc + j][tr] = (bf16)dq[j];
+            __syncthreads();
+            const int tcol = threadIdx.x >> 2, r16 = (threadIdx.x & 3) * 16;   // shadow_t row = c0 + tcol
+            if (c0 + tcol < cols) {
+                bf16* dst = st + (long)(c0 + tcol) * rows + rb + r16;
+                if (rb + r16 + 16 <= rows && (rows & 7) == 0) {
+                    *reinterpret_cast<u32x4*>(dst) = *reinterpret_cast<const u32x4*>(&T[tcol][r16]);
+                    *reinterpret_cast<u32x4*>(dst + 8) = *reinterpret_cast<const u32x4*>(&T[tcol][r16 + 8]);
+                } else {
+                    for (int j = 0; j < 16 && rb + r16 + j < rows; ++j) dst[j] = T[tcol][r16 + j];
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
 // e4m3 byte layouts (csu_e4m3_layout_batch): one thread per 4-byte dst word
 __global__ __launch_bounds__(NT) void e4m3_layout_kernel(const csu_e4m3_layout_item* __restrict__ items, int count,
                                                          long total) {
@@ -90,4 +177,10 @@ extern "C" int csu_e4m3_layout_batch(const csu_e4m3_layout_item* items, int coun
     if (count < 1 || total_words < 1 || !items) return fail(CSU_E_ARG, "e4m3_layout: bad args");
     e4m3_layout_kernel<<<(unsigned)((total_words + NT - 1) / NT), NT, 0, as_stream(stream)>>>(items, count, total_words);
     return check_launch("e4m3_layout");
+}
+
+extern "C" int csu_quant_e4m3_shadow_batch(const csu_fp8_shadow_item* items, int count, long total_blocks, void* stream) {
+    if (count < 1 || total_blocks < 1 || !items) return fail(CSU_E_ARG, "quant_e4m3_shadow: bad args");
+    quant_e4m3_shadow<<<(unsigned)total_blocks, NT, 0, as_stream(stream)>>>(items, count);
+    return check_launch("quant_e4m3_shadow");
 }

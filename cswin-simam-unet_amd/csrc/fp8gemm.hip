@@ -15,9 +15,10 @@
 // features.  K in steps of 64 (one MFMA k-step): the next step's tiles are loaded into registers
 // while the current one is multiplied from LDS (two LDS buffers, one barrier per step).  LDS rows
 // are 64 B + 16 B pad: the 16-lane groups of a ds_read_b128 hit 16 distinct 4-bank ranges.
-// Operand lane map of the 32x32x64 f8 form (k per lane = 32 contiguous bytes, 32 (lane >> 5) + j,
-// as the 32x32x16 bf16 form's 8): A and B use the same map, so the contraction is exact whatever
-// the hardware's k order.
+// Operand lane map of the 32x32x64 f8 form: lane half h holds k = 16 h + 0..15 in bytes 0..15 and
+// k = 32 + 16 h + 0..15 in bytes 16..31 (tools/probes/mx_layout_probe.hip).  Here both operands take
+// the same 32 contiguous bytes per lane and the block scales are unit, so the contraction is exact
+// whatever the hardware's k order.
 #include "common.hpp"
 
 namespace csu {

@@ -71,7 +71,7 @@ template <typename TX, typename TY, int V, int LPR>
 __global__ __launch_bounds__(NT) void ln_fwd(int rows, int C, float eps, const TX* __restrict__ x,
                                              const float* __restrict__ gamma, const float* __restrict__ beta,
                                              TY* __restrict__ y, float* __restrict__ mean, float* __restrict__ rstd,
-                                             float* __restrict__ ysc) {
+                                             float* __restrict__ ysc, bf16* __restrict__ ydq) {
     constexpr int RPW = 64 / LPR;
     const int lane = threadIdx.x & 63;
     const int rb = (blockIdx.x * WAVES + (threadIdx.x >> 6)) * RPW * FU + lane / LPR;
@@ -129,6 +129,19 @@ __global__ __launch_bounds__(NT) void ln_fwd(int rows, int C, float eps, const T
             if constexpr (V == 8) __builtin_amdgcn_raw_buffer_store_b64(u32x2{w[0], w[1]}, rs_y, e, 0, 0);
             else __builtin_amdgcn_raw_buffer_store_b32(w[0], rs_y, e, 0, 0);
             __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(s), buf_rsrc(ysc, (long)rows * 4), ro, 0, 0);
+            if (ydq) {   // the dequantised value in bf16 (exact): the weight gradient's operand
+                float dq[V];
+#pragma unroll
+                for (int k = 0; k < V / 4; ++k) {
+                    const auto lo = __builtin_amdgcn_cvt_pk_f32_fp8((int)w[k], false);
+                    const auto hi = __builtin_amdgcn_cvt_pk_f32_fp8((int)w[k], true);
+                    dq[4 * k] = lo[0] * s;
+                    dq[4 * k + 1] = lo[1] * s;
+                    dq[4 * k + 2] = hi[0] * s;
+                    dq[4 * k + 3] = hi[1] * s;
+                }
+                bst<bf16, V>(buf_rsrc(ydq, n * 2), e == kOOB ? kOOB : e * 2u, dq);
+            }
         } else {
             bst<TY, V>(rs_y, e == kOOB ? kOOB : e * (unsigned)sizeof(TY), o);
         }
@@ -277,11 +290,11 @@ int check_rows(int rows, int C) {   // 32-bit byte offsets of the raw buffer ops
 
 template <typename TX, typename TY>
 int launch_fwd(int rows, int C, float eps, const void* x, const float* g, const float* b, void* y, float* m,
-               float* r, hipStream_t st, float* ysc = nullptr) {
+               float* r, hipStream_t st, float* ysc = nullptr, bf16* ydq = nullptr) {
 #define CSU_LNF(V, LPR)                                                                                           \
     ln_fwd<TX, TY, V, LPR><<<(rows + WAVES * (64 / LPR) * FU - 1) / (WAVES * (64 / LPR) * FU), NT, 0, st>>>(rows, C, eps, \
                                                                                                   (const TX*)x, g, b, \
-                                                                                                  (TY*)y, m, r, ysc)
+                                                                                                  (TY*)y, m, r, ysc, ydq)
     switch (C / 64) {
         case 1: CSU_LNF(4, 16); break;
         case 2: CSU_LNF(4, 32); break;
@@ -333,16 +346,23 @@ extern "C" int csu_layernorm_fwd(int rows, int C, float eps, int xdtype, const v
     return fail(CSU_E_ARG, "layernorm_fwd: bad dtype");
 }
 
-extern "C" int csu_layernorm_fwd_fp8(int rows, int C, float eps, int xdtype, const void* x, const float* gamma,
-                                     const float* beta, void* yq, float* yscale, float* mean, float* rstd, void* stream) {
+extern "C" int csu_layernorm_fwd_fp8_dq(int rows, int C, float eps, int xdtype, const void* x, const float* gamma,
+                                        const float* beta, void* yq, float* yscale, void* ydq, float* mean, float* rstd,
+                                        void* stream) {
     if (int e = check_c(C)) return e;
     if (int e = check_rows(rows, C)) return e;
     if (rows < 1 || !x || !gamma || !beta || !yq || !yscale || !mean || !rstd)
         return fail(CSU_E_ARG, "layernorm_fwd_fp8: bad args");
     hipStream_t st = as_stream(stream);
-    if (xdtype == CSU_F32) return launch_fwd<float, e4m3>(rows, C, eps, x, gamma, beta, yq, mean, rstd, st, yscale);
-    if (xdtype == CSU_BF16) return launch_fwd<bf16, e4m3>(rows, C, eps, x, gamma, beta, yq, mean, rstd, st, yscale);
+    bf16* dq = (bf16*)ydq;
+    if (xdtype == CSU_F32) return launch_fwd<float, e4m3>(rows, C, eps, x, gamma, beta, yq, mean, rstd, st, yscale, dq);
+    if (xdtype == CSU_BF16) return launch_fwd<bf16, e4m3>(rows, C, eps, x, gamma, beta, yq, mean, rstd, st, yscale, dq);
     return fail(CSU_E_ARG, "layernorm_fwd_fp8: bad dtype");
+}
+
+extern "C" int csu_layernorm_fwd_fp8(int rows, int C, float eps, int xdtype, const void* x, const float* gamma,
+                                     const float* beta, void* yq, float* yscale, float* mean, float* rstd, void* stream) {
+    return csu_layernorm_fwd_fp8_dq(rows, C, eps, xdtype, x, gamma, beta, yq, yscale, nullptr, mean, rstd, stream);
 }
 
 extern "C" size_t csu_layernorm_bwd_workspace(int rows, int C) {

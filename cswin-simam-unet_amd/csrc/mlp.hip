@@ -628,11 +628,13 @@ int bwd_launch(long M, const void* x, const void* dy, const void* w1, const floa
 // tools/probes/mx_scale_probe.hip, 127 = 2^0, one scale per lane of A and of B).
 //   GEMM1  h = W1 x   : A = e4m3 rows of W1 (the row's power-of-two scale sw1[f] = 2^e as the lane's
 //                       E8M0), B = x quantised in registers per (token, 32 consecutive channels)
-//   GEMM2  y += W2 g  : B = g = gelu(h + b1) quantised in registers per (token, the 32 hidden features
-//                       the lane holds: inside each 64-feature group those whose index has bit 2 ==
-//                       lane half), A = e4m3 rows of W2 (per-row scale sw2[c] as the lane's E8M0) with
-//                       the columns permuted per 64-block so that a lane's 32 k-bytes are contiguous:
-//                       position 32h + 16t + 4g + i holds feature 32t + 8g + 4h + i (csu_e4m3_layout_batch)
+//   GEMM2  y += W2 g  : B = g = gelu(h + b1) quantised in registers per (token, 32 consecutive hidden
+//                       features: the accumulator tile pair of a wave hands lane half h the features
+//                       32 t + 8 g + 4 h + i in byte 16 t + 4 g + i, and the hardware's block b is bytes
+//                       [16 b, 16 b + 16) of both halves = tile t = b), A = e4m3 rows of W2 (per-row scale
+//                       sw2[c] as the lane's E8M0) with the columns permuted per 64-block so that a lane's
+//                       32 k-bytes are contiguous: position 32h + 16t + 4g + i holds feature 32t + 8g +
+//                       4h + i (csu_e4m3_layout_batch)
 // Chunks of 128 hidden features (wave u: features 64u..64u+63 = two 32-row tiles, so one lane holds
 // the 32 values of one f8 k-step of GEMM2); 64-token panel per workgroup as in the bf16 kernel.  A
 // chunk's W1 + W2 bytes equal one 64-feature bf16 chunk's: half the weight stream per panel.  GEMM2
@@ -643,27 +645,54 @@ typedef int i32x8 __attribute__((ext_vector_type(8)));
 
 __device__ __forceinline__ int e8m0_of(float s) { return (__float_as_int(s) >> 23) & 0xff; }
 
-// MX quantisation of 32 values: scale 2^e, e the smallest integer with amax <= 448 * 2^e (clamped to
-// the E8M0 range; 0 for an all-zero block), e4m3fn bytes round-to-nearest-even (|v / 2^e| <= 448: no
-// saturation).  Byte j of the packed operand = v[j].  Returns the E8M0 byte e + 127.
-__device__ __forceinline__ int mx_quant32(const float* v, i32x8& q) {
-    float amax = 0.f;
-#pragma unroll
-    for (int i = 0; i < 32; ++i) amax = fmaxf(amax, fabsf(v[i]));
+// MX quantisation of one f8 operand lane.  The hardware's k layout (tools/probes/mx_layout_probe.hip):
+// bytes [0, 16) of lane half h are k = 16 h + 0..15 and bytes [16, 32) are k = 32 + 16 h + 0..15, and
+// the E8M0 scale of lane half b applies to block b = k [32 b, 32 b + 32) = bytes [16 b, 16 b + 16) of
+// BOTH lane halves.  So a block's amax combines this lane's half with the partner lane's (lane ^ 32):
+// scale 2^e, e the smallest integer with amax <= 448 * 2^e (0 for an all-zero block, clamped to the
+// E8M0 range), e4m3fn bytes round-to-nearest-even (no saturation).  v: the lane's 32 values in byte
+// order; returns the lane's scale operand (E8M0 of block h); e0 / e1: both blocks' exponents.
+__device__ __forceinline__ int mx_exp(float amax) {
     const int b = __float_as_int(amax);
-    int e = ((b >> 23) & 0xff) - 135 + ((b & 0x7fffff) > 0x600000 ? 1 : 0);
-    e = amax == 0.f ? 0 : (e < -127 ? -127 : (e > 127 ? 127 : e));
+    const int e = ((b >> 23) & 0xff) - 135 + ((b & 0x7fffff) > 0x600000 ? 1 : 0);
+    return amax == 0.f ? 0 : (e < -127 ? -127 : (e > 127 ? 127 : e));
+}
+__device__ __forceinline__ int mx_quant32(const float* v, i32x8& q, int& e0, int& e1) {
+    float a0 = 0.f, a1 = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        a0 = fmaxf(a0, fabsf(v[i]));
+        a1 = fmaxf(a1, fabsf(v[16 + i]));
+    }
+    a0 = fmaxf(a0, __shfl_xor(a0, 32, 64));
+    a1 = fmaxf(a1, __shfl_xor(a1, 32, 64));
+    e0 = mx_exp(a0);
+    e1 = mx_exp(a1);
 #pragma unroll
     for (int d = 0; d < 8; ++d) {
+        const int e = d < 4 ? e0 : e1;
         int w = __builtin_amdgcn_cvt_pk_fp8_f32(ldexpf(v[4 * d], -e), ldexpf(v[4 * d + 1], -e), 0, false);
         w = __builtin_amdgcn_cvt_pk_fp8_f32(ldexpf(v[4 * d + 2], -e), ldexpf(v[4 * d + 3], -e), w, true);
         q[d] = w;
     }
-    return e + 127;
+    return ((threadIdx.x & 63) >> 5 ? e1 : e0) + 127;
+}
+__device__ __forceinline__ int mx_quant32(const float* v, i32x8& q) {
+    int e0, e1;
+    return mx_quant32(v, q, e0, e1);
 }
 
-// 32 k-bytes [kb, kb + 32) of row `row` of a swizzled byte image with RB-byte rows (the bf16 images'
-// 16-B slot swizzle; two ds_read_b128)
+// 16 + 16 k-bytes of row `row` of a swizzled byte image with RB-byte rows: bytes [kb, kb + 16) and
+// [kb + 32, kb + 48) -- the k order of lane half h = (kb / 16) & 1 of an f8 k-step starting at kb - 16 h
+// (two ds_read_b128, the bf16 images' 16-B slot swizzle)
+template <int RB>
+__device__ __forceinline__ i32x8 frag8s(const bf16* img, int row, int kb) {
+    const u32x4 lo = *reinterpret_cast<const u32x4*>(img + moff<RB>(row, kb >> 1));
+    const u32x4 hi = *reinterpret_cast<const u32x4*>(img + moff<RB>(row, (kb + 32) >> 1));
+    return i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+}
+// 32 contiguous k-bytes [kb, kb + 32) of a row (operands whose k order is the accumulator tile
+// pair's: byte j = 16 t + 4 g + i, see csu_e4m3_layout_batch)
 template <int RB>
 __device__ __forceinline__ i32x8 frag8(const bf16* img, int row, int kb) {
     const u32x4 lo = *reinterpret_cast<const u32x4*>(img + moff<RB>(row, kb >> 1));
@@ -671,8 +700,9 @@ __device__ __forceinline__ i32x8 frag8(const bf16* img, int row, int kb) {
     return i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
 }
 
-// token operand of GEMM1 (or of the backward's dY GEMM): row `tok`, k-step s = channels 64 s + 32 h
-// .. + 31, quantised per lane (optionally times a per-channel power-of-two factor colscale first)
+// token operand of GEMM1 (or of the backward's dY GEMM): row `tok`, k-step s in the hardware's k
+// order (channels 64 s + 16 h + 0..15 and 64 s + 32 + 16 h + 0..15), so MX blocks are 32 consecutive
+// channels; optionally times a per-channel power-of-two factor colscale first
 template <int C>
 __device__ __forceinline__ void load_q8(__amdgpu_buffer_rsrc_t rs, int tok, bool ok, int h, i32x8* q, int* sc,
                                         const float* colscale = nullptr) {
@@ -680,10 +710,13 @@ __device__ __forceinline__ void load_q8(__amdgpu_buffer_rsrc_t rs, int tok, bool
     for (int s = 0; s < C / 64; ++s) {
         float v[32];
 #pragma unroll
-        for (int p = 0; p < 4; ++p) buf_ld8bf(rs, ok ? (unsigned)(tok * C + 64 * s + 32 * h + 8 * p) * 2 : kOOB, v + 8 * p);
-        if (colscale) {
+        for (int p = 0; p < 4; ++p) {
+            const int ch = 64 * s + 32 * (p >> 1) + 16 * h + 8 * (p & 1);
+            buf_ld8bf(rs, ok ? (unsigned)(tok * C + ch) * 2 : kOOB, v + 8 * p);
+            if (colscale) {
 #pragma unroll
-            for (int i = 0; i < 32; ++i) v[i] *= colscale[64 * s + 32 * h + i];
+                for (int i = 0; i < 8; ++i) v[8 * p + i] *= colscale[ch + i];
+            }
         }
         sc[s] = mx_quant32(v, q[s]);
     }
@@ -756,7 +789,7 @@ __global__ __launch_bounds__(MT) void mlp_fp8_fwd_kernel(long M, const bf16* __r
 #pragma unroll
         for (int t2 = 0; t2 < 2; ++t2)
 #pragma unroll
-            for (int s = 0; s < KS; ++s) wf[t2][s] = frag8<C>(img, hs + 32 * t2 + r, 64 * s + 32 * h);
+            for (int s = 0; s < KS; ++s) wf[t2][s] = frag8s<C>(img, hs + 32 * t2 + r, 64 * s + 16 * h);
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int t2 = 0; t2 < 2; ++t2) {
@@ -853,16 +886,17 @@ int fp8_fwd_launch(long M, const void* x, const void* w1, const float* sw1, cons
 }
 
 
-// 32 values of a packed e4m3 operand lane times 2^(e8 - 127)
-__device__ __forceinline__ void mx_dequant32(const i32x8& q, int e8, float* v) {
+// the 32 values of a packed e4m3 operand lane: bytes [0, 16) times 2^e0, [16, 32) times 2^e1
+__device__ __forceinline__ void mx_dequant32(const i32x8& q, int e0, int e1, float* v) {
 #pragma unroll
     for (int d = 0; d < 8; ++d) {
+        const int e = d < 4 ? e0 : e1;
         const auto lo = __builtin_amdgcn_cvt_pk_f32_fp8(q[d], false);
         const auto hi = __builtin_amdgcn_cvt_pk_f32_fp8(q[d], true);
-        v[4 * d] = ldexpf(lo[0], e8 - 127);
-        v[4 * d + 1] = ldexpf(lo[1], e8 - 127);
-        v[4 * d + 2] = ldexpf(hi[0], e8 - 127);
-        v[4 * d + 3] = ldexpf(hi[1], e8 - 127);
+        v[4 * d] = ldexpf(lo[0], e);
+        v[4 * d + 1] = ldexpf(lo[1], e);
+        v[4 * d + 2] = ldexpf(hi[0], e);
+        v[4 * d + 3] = ldexpf(hi[1], e);
     }
 }
 
@@ -965,7 +999,7 @@ __global__ __launch_bounds__(MT) void mlp_fp8_bwd_kernel(long M, const bf16* __r
             {
                 i32x8 fa[KS];
 #pragma unroll
-                for (int s = 0; s < KS; ++s) fa[s] = frag8<C>(w1c, hs + 32 * t2 + r, 64 * s + 32 * h);
+                for (int s = 0; s < KS; ++s) fa[s] = frag8s<C>(w1c, hs + 32 * t2 + r, 64 * s + 16 * h);
                 __builtin_amdgcn_sched_barrier(0);
                 const int sa = e1s[jc * HC8 + hs + 32 * t2 + r];
                 ha = f32x16{};
@@ -975,7 +1009,7 @@ __global__ __launch_bounds__(MT) void mlp_fp8_bwd_kernel(long M, const bf16* __r
             {
                 i32x8 fb[KS];
 #pragma unroll
-                for (int s = 0; s < KS; ++s) fb[s] = frag8<C>(w2r, hs + 32 * t2 + r, 64 * s + 32 * h);
+                for (int s = 0; s < KS; ++s) fb[s] = frag8s<C>(w2r, hs + 32 * t2 + r, 64 * s + 16 * h);
                 __builtin_amdgcn_sched_barrier(0);
                 ga = f32x16{};
 #pragma unroll
@@ -1002,8 +1036,9 @@ __global__ __launch_bounds__(MT) void mlp_fp8_bwd_kernel(long M, const bf16* __r
         if (more) dma<D1::NW>(rs_w2, d2.v, (unsigned)chk(j + 1) * HC8 * C, w2r, wave);
         {   // G = the forward's g_q, exactly
             i32x8 gq;
-            const int gs = mx_quant32(gv, gq);
-            mx_dequant32(gq, gs, gv);
+            int e0, e1;
+            mx_quant32(gv, gq, e0, e1);
+            mx_dequant32(gq, e0, e1, gv);
         }
         const int fb0 = jc * HC8 + hs;
 #pragma unroll

@@ -141,8 +141,10 @@ _SIGS = {
     "csu_quant_e4m3_batch": (ctypes.c_int, [c_void_p, ctypes.c_int, ctypes.c_long, c_void_p]),
     "csu_fp8_gemm": (ctypes.c_int, [ctypes.c_long, ctypes.c_int, ctypes.c_int] + [c_void_p] * 7),
     "csu_layernorm_fwd_fp8": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, c_float, ctypes.c_int] + [c_void_p] * 8),
+    "csu_layernorm_fwd_fp8_dq": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, c_float, ctypes.c_int] + [c_void_p] * 9),
     "csu_dequant_e4m3_rows": (ctypes.c_int, [ctypes.c_long, ctypes.c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
     "csu_e4m3_layout_batch": (ctypes.c_int, [c_void_p, ctypes.c_int, ctypes.c_long, c_void_p]),
+    "csu_quant_e4m3_shadow_batch": (ctypes.c_int, [c_void_p, ctypes.c_int, ctypes.c_long, c_void_p]),
     "csu_mlp_fp8_supported": (ctypes.c_int, [ctypes.c_int]),
     "csu_mlp_fp8_fwd": (ctypes.c_int, [ctypes.c_long, ctypes.c_int] + [c_void_p] * 9 + [ctypes.POINTER(MlpDropout), c_void_p]),
     "csu_mlp_fp8_bwd": (ctypes.c_int, [ctypes.c_long, ctypes.c_int] + [c_void_p] * 11 + [ctypes.POINTER(MlpDropout),

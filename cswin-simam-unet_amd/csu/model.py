@@ -550,9 +550,12 @@ class CSWinTransformer(nn.Module):
                 if self._fp8 is None or not self._fp8.valid_for(weights):
                     pairs = [(m.fc1.weight, m.fc2.weight) for m in self.modules() if isinstance(m, Mlp)]
                     self._fp8 = ops.Fp8Weights(weights, mlp_pairs=pairs)
-                sources = self._fp8.quantize()     # one launch: e4m3 per row, dequantised fp32 copies
-            # one launch per step: bf16 shadows of every Linear weight (+ transposes) and conv layouts
+                sources = self._fp8.sources()
+            # bf16 shadows of every Linear weight (+ transposes) and conv layouts: AdamW-written, or one
+            # cast launch; in the fp8 format the quantised weights' shadows come from the quantiser
             self._cast_cache.refresh(weights, cd, self._conv_weights(), sources=sources)
+            if sources is not None:
+                self._fp8.quantize(self._cast_cache)   # one launch: e4m3 + scales + exact bf16 shadows
             ops.set_cast_cache(self._cast_cache, self._fp8 if sources is not None else None)
         try:
             return self._forward(x)

@@ -1654,22 +1654,27 @@ class CastCache:
         if (dtype == torch.bfloat16 and allp and all(p.is_cuda and p.dtype == torch.float32 and p.is_contiguous()
                                                      for p in allp)):
             import numpy as np
-            rec = np.zeros(len(allp), dtype=self._rec())
+            # a None source: that shadow is written elsewhere (the fp8 quantiser), not by the cast batch
+            keep = [i for i in range(len(params)) if src[i] is not None]
+            rec = np.zeros(len(keep) + len(convs), dtype=self._rec())
             t0 = 0
-            for i, p in enumerate(params):
+            for k, i in enumerate(keep):
+                p = params[i]
                 rows = p.shape[0] if p.dim() > 1 else 1
                 cols = p.numel() // rows
                 st = self.shadow_t[i]
-                rec[i] = (src[i].data_ptr(), self.shadow[i].data_ptr(), 0 if st is None else st.data_ptr(), rows, cols, t0,
+                rec[k] = (src[i].data_ptr(), self.shadow[i].data_ptr(), 0 if st is None else st.data_ptr(), rows, cols, t0,
                           0, 0)
                 t0 += -(-rows // 64) * -(-cols // 64)
             for j, w in enumerate(convs):
                 N, C, KH, KW = w.shape
                 ci = self.conv_i[j]
-                rec[len(params) + j] = (w.data_ptr(), self.conv_o[j].data_ptr(), 0 if ci is None else ci.data_ptr(), N, C,
-                                        t0, KH * KW, self.conv_cp[j])
+                rec[len(keep) + j] = (w.data_ptr(), self.conv_o[j].data_ptr(), 0 if ci is None else ci.data_ptr(), N, C,
+                                      t0, KH * KW, self.conv_cp[j])
                 t0 += -(-(N * C * KH * KW) // 4096)
             self.tiles = t0
+            self.nitems = len(rec)
+            self.cast_numel = (sum(params[i].numel() for i in keep), sum(params[i].numel() for i in keep if params[i].dim() > 1))
             self.items = torch.frombuffer(bytearray(rec.tobytes()), dtype=torch.uint8).to(allp[0].device)
             if sources is None:
                 import weakref
@@ -1701,10 +1706,11 @@ class CastCache:
             return
         src = self.sources if getattr(self, "sources", None) is not None else self.params
         with torch.no_grad():
-            if self.params:
-                torch._foreach_copy_(self.shadow, [p.detach() for p in src])
+            pairs = [(sh, p) for sh, p in zip(self.shadow, src) if p is not None]
+            if pairs:
+                torch._foreach_copy_([a for a, _ in pairs], [p.detach() for _, p in pairs])
             for st, p in zip(self.shadow_t, src):
-                if st is not None:
+                if st is not None and p is not None:
                     st.copy_(p.detach().reshape(p.shape[0], -1).t())
             for w, o, i in zip(self.convs, self.conv_o, self.conv_i):
                 o[..., :w.shape[1]].copy_(w.detach().permute(0, 2, 3, 1))
@@ -1716,11 +1722,12 @@ class CastCache:
 
     def _cast(self):
         allp = self.params + self.convs
-        n = sum(p.numel() for p in allp)
-        nt = sum(p.numel() for p in self.params if p.dim() > 1) + sum(w.numel() for w in self.convs)
-        _launch("cast_bf16_batch", lambda: lib().csu_cast_bf16_batch(ptr(self.items), len(allp), self.tiles,
-                                                                     stream_ptr(allp[0].device)),
-                0, n * 6 + nt * 2)
+        n = self.cast_numel[0] + sum(w.numel() for w in self.convs)
+        nt = self.cast_numel[1] + sum(w.numel() for w in self.convs)
+        if self.nitems and self.tiles:
+            _launch("cast_bf16_batch", lambda: lib().csu_cast_bf16_batch(ptr(self.items), self.nitems, self.tiles,
+                                                                         stream_ptr(allp[0].device)),
+                    0, n * 6 + nt * 2)
         if self.sources is None:
             self._written = [p._version for p in allp]
 
@@ -1833,10 +1840,51 @@ class Fp8Weights:
         return len(params) == len(self.params) and all(a is b and a.data_ptr() == q
                                                        for a, b, q in zip(params, self.params, self.ptrs))
 
-    def quantize(self):
+    def sources(self):
+        """Per listed param, the fp32 tensor a CastCache should cast its bf16 shadow from: None for the
+        quantised weights (quantize(cache) writes their shadows itself), the param for 1-D tensors."""
+        return [None if q is not None else p for p, q in zip(self.params, self.q)]
+
+    def _shadow_items(self, cache):
+        """Item table of csu_quant_e4m3_shadow_batch into ``cache``'s shadows (rebuilt when they move)."""
+        import numpy as np
+        key = (id(cache), tuple(cache.shadow[cache.index[p.data_ptr()]].data_ptr() for p, q in zip(self.params, self.q)
+                                if q is not None))
+        if getattr(self, "_skey", None) == key:
+            return self._sitems, self._sblocks, self._scount
+        recs, b0 = [], 0
+        for p, q, sc in zip(self.params, self.q, self.scales):
+            if q is None:
+                continue
+            i = cache.index[p.data_ptr()]
+            st = cache.shadow_t[i]
+            rows = p.shape[0]
+            cols = p.numel() // rows
+            if cols % 16:
+                raise ValueError("Fp8Weights: weight columns must be a multiple of 16")
+            recs.append((p.data_ptr(), q.data_ptr(), sc.data_ptr(), cache.shadow[i].data_ptr(),
+                         0 if st is None else st.data_ptr(), b0, rows, cols))
+            b0 += -(-rows // 64)
+        dt = np.dtype([("src", "<u8"), ("q", "<u8"), ("sc", "<u8"), ("sh", "<u8"), ("st", "<u8"), ("b0", "<i8"),
+                       ("rows", "<i4"), ("cols", "<i4")])
+        self._sitems = torch.frombuffer(bytearray(np.array(recs, dtype=dt).tobytes()), dtype=torch.uint8).to(
+            self.params[0].device)
+        self._sblocks, self._scount, self._skey = b0, len(recs), key
+        return self._sitems, self._sblocks, self._scount
+
+    def quantize(self, cache: Optional["CastCache"] = None):
+        """One launch: e4m3 bytes + row scales of every listed weight, and either the dequantised fp32
+        copies (``deq``, returned) or -- with ``cache`` -- the bf16 shadows W and W^T straight in the
+        cache (csu_quant_e4m3_shadow_batch); then the fp8 Mlp operand layouts."""
         dev = self.params[0].device
-        _launch("quant_e4m3", lambda: lib().csu_quant_e4m3_batch(ptr(self.items), self.count, self.rows, stream_ptr(dev)),
-                0, sum(p.numel() for p, q in zip(self.params, self.q) if q is not None) * 9)
+        nq = sum(p.numel() for p, q in zip(self.params, self.q) if q is not None)
+        if cache is None:
+            _launch("quant_e4m3", lambda: lib().csu_quant_e4m3_batch(ptr(self.items), self.count, self.rows,
+                                                                     stream_ptr(dev)), 0, nq * 9)
+        else:
+            items, blocks, count = self._shadow_items(cache)
+            _launch("quant_e4m3", lambda: lib().csu_quant_e4m3_shadow_batch(ptr(items), count, blocks, stream_ptr(dev)),
+                    0, nq * (4 + 1 + 2 + 2))
         if self.lay_count:
             _launch("quant_e4m3", lambda: lib().csu_e4m3_layout_batch(ptr(self.lay_items), self.lay_count, self.lay_words,
                                                                      stream_ptr(dev)), 0, self.lay_words * 8)
@@ -1882,8 +1930,9 @@ def dequant_e4m3_rows(q: torch.Tensor, scale: torch.Tensor) -> torch.Tensor:
     return out
 
 
-def layer_norm_fp8(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, eps: float = 1e-5):
-    """(e4m3 bytes, row scales, mean, rstd) of LN(x) (csu_layernorm_fwd_fp8), no autograd."""
+def layer_norm_fp8(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, eps: float = 1e-5, dq: bool = False):
+    """(e4m3 bytes, row scales, mean, rstd[, bf16 dequantised copy]) of LN(x) (csu_layernorm_fwd_fp8_dq),
+    no autograd."""
     require_device(x, weight, bias)
     x = x.contiguous()
     C = x.shape[-1]
@@ -1894,11 +1943,12 @@ def layer_norm_fp8(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, ep
     s = torch.empty(rows, dtype=torch.float32, device=x.device)
     mean = torch.empty(rows, dtype=torch.float32, device=x.device)
     rstd = torch.empty(rows, dtype=torch.float32, device=x.device)
-    _launch("layernorm_fwd_fp8", lambda: lib().csu_layernorm_fwd_fp8(rows, C, float(eps), dtype_code(x), ptr(x), ptr(w),
-                                                                     ptr(b), ptr(q), ptr(s), ptr(mean), ptr(rstd),
-                                                                     stream_ptr(x.device)),
-            10 * rows * C, rows * C * (esize(x) + 1) + rows * 12, prec=prec_of(x))
-    return q, s, mean, rstd
+    ydq = torch.empty(rows, C, dtype=torch.bfloat16, device=x.device) if dq else None
+    _launch("layernorm_fwd_fp8", lambda: lib().csu_layernorm_fwd_fp8_dq(rows, C, float(eps), dtype_code(x), ptr(x),
+                                                                        ptr(w), ptr(b), ptr(q), ptr(s), ptr(ydq),
+                                                                        ptr(mean), ptr(rstd), stream_ptr(x.device)),
+            10 * rows * C, rows * C * (esize(x) + 1 + (2 if dq else 0)) + rows * 12, prec=prec_of(x))
+    return (q, s, mean, rstd, ydq) if dq else (q, s, mean, rstd)
 
 
 class _LnLinearFp8Fn(torch.autograd.Function):
@@ -1916,9 +1966,9 @@ class _LnLinearFp8Fn(torch.autograd.Function):
     def forward(ctx, x, gamma, beta, weight, bias, eps: float, wq, ws, wt):
         x = x.contiguous()
         C = x.shape[-1]
-        hq, hs, mean, rstd = layer_norm_fp8(x, gamma, beta, eps)
+        hq, hs, mean, rstd, hdq = layer_norm_fp8(x, gamma, beta, eps, dq=True)
         y = fp8_gemm(hq, hs, wq, ws, bias).view(*x.shape[:-1], wq.shape[0])
-        ctx.save_for_backward(x, gamma.detach().float().contiguous(), mean, rstd, hq, hs, wt)
+        ctx.save_for_backward(x, gamma.detach().float().contiguous(), mean, rstd, hdq, wt)
         ctx.params = (gamma, beta)
         ctx.pdtypes = (gamma.dtype, beta.dtype)
         ctx.lin = (weight, bias)
@@ -1928,7 +1978,7 @@ class _LnLinearFp8Fn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dres, dy):
-        x, g, mean, rstd, hq, hs, wt = ctx.saved_tensors
+        x, g, mean, rstd, h, wt = ctx.saved_tensors     # h: the dequantised e4m3 LN output (bf16, exact)
         wdt, bdt, C = ctx.lmeta
         dh = dw = db = None
         if dy is not None:
@@ -1937,7 +1987,6 @@ class _LnLinearFp8Fn(torch.autograd.Function):
             dh = gemm(dy2, wt, False, torch.bfloat16).view(x.shape)
             need_w, need_b = ctx.needs_input_grad[3], bdt is not None and ctx.needs_input_grad[4]
             if need_w or need_b:
-                h = dequant_e4m3_rows(hq, hs)
                 dwf, dbf = wgrad_maybe_side(dy2, h, wdt if need_w else None, bdt if need_b else None, params=ctx.lin)
                 dw = dwf.to(wdt) if need_w else None
                 db = dbf.to(bdt) if need_b else None

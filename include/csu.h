@@ -345,6 +345,20 @@ typedef struct {
     int32_t rows, cols;
 } csu_fp8_item;
 int csu_quant_e4m3_batch(const csu_fp8_item* items, int count, long total_rows, void* stream);
+/* The same quantisation written straight into bf16 shadows: per item (rows x cols fp32, cols % 16 ==
+ * 0), scales[row] = s (optional), q (optional) the e4m3 bytes, shadow (rows x cols bf16) = q * s exactly,
+ * shadow_t (cols x rows bf16, optional) its transpose.  items: DEVICE array sorted by blk0 (prefix sum of
+ * ceil(rows / 64)); one 256-thread block per 64 rows of every item. */
+typedef struct {
+    const float* src;
+    uint8_t* q;
+    float* scales;
+    void* shadow;
+    void* shadow_t;
+    int64_t blk0;
+    int32_t rows, cols;
+} csu_fp8_shadow_item;
+int csu_quant_e4m3_shadow_batch(const csu_fp8_shadow_item* items, int count, long total_blocks, void* stream);
 
 /* fp8-e4m3 token GEMM (BASELINE config 5 "fp8 MFMA weights"; replaces CSWinBlock.qkv, cswin:337,
  * on the norm1 output, cswin:357):  out[m][n] = bf16(sa[m] sw[n] sum_k aq[m][k] wq[n][k] + bias[n]),
@@ -356,6 +370,11 @@ int csu_fp8_gemm(long M, int N, int K, const void* aq, const float* sa, const vo
  * 2^ceil(log2(amax_row / 448)) (1 for an all-zero row); mean / rstd as csu_layernorm_fwd. */
 int csu_layernorm_fwd_fp8(int rows, int C, float eps, int xdtype, const void* x, const float* gamma,
                           const float* beta, void* yq, float* yscale, float* mean, float* rstd, void* stream);
+/* the same, also writing ydq (bf16, rows x C, or NULL) = e4m3fn(yq) * yscale[row] exactly: the
+ * operand the weight gradient of the consuming Linear reads */
+int csu_layernorm_fwd_fp8_dq(int rows, int C, float eps, int xdtype, const void* x, const float* gamma,
+                             const float* beta, void* yq, float* yscale, void* ydq, float* mean, float* rstd,
+                             void* stream);
 /* out (bf16, rows x cols) = e4m3fn(q) * scale[row]; cols % 8 == 0 */
 int csu_dequant_e4m3_rows(long rows, int cols, const void* q, const float* scale, void* out, void* stream);
 /* e4m3 byte layouts of quantised weights (the fp8 fused Mlp's operand images): per item, src is a
@@ -483,8 +502,7 @@ int csu_mlp_bwd_dp(long M, int C, const void* x, const void* dy, const void* w1,
  * csu_mlp_fwd_dp) on v_mfma_scale_f32_32x32x64_f8f6f4 with MX block scales:
  *   h   = x_q W1^T + b1, x_q = x quantised per (token, 32 consecutive channels): scale 2^e, e the
  *         smallest integer with amax <= 448 * 2^e, e4m3fn round-to-nearest-even;
- *   g   = gelu(h) (* hidden dropout), g_q = g quantised per (token, block), block = the 32
- *         features of a 64-feature group whose index has equal bit 2 (f & 4);
+ *   g   = gelu(h) (* hidden dropout), g_q = g quantised per (token, 32 consecutive features);
  *   out = res + (g_q W2^T + b2) (* output dropout, DropPath).
  * w1q: (4C, C) e4m3 rows with power-of-two row scales sw1 (4C); w2p: (C, 4C) e4m3 rows (scales sw2,
  * C) with the columns permuted as csu_e4m3_layout_batch mode 2.  C in {128, 256}. */
@@ -497,7 +515,7 @@ int csu_mlp_fp8_fwd(long M, int C, const void* x, const void* w1q, const float* 
  *        consecutive channels) after the per-channel scale sw2 (W2's row scale lies along this sum);
  *   dh = dg * gelu'(h) (* hidden mask) -> dh (bf16, M x 4C); g = g_q of the forward (bf16, exact);
  *   dx = (dh * sw1)_q W1q: w1tp = W1q^T (C, 4C) with permuted columns (layout mode 3), dh * sw1
- *        quantised per (token, block) as g.  dx bf16 (M, C).  dy carries the output mask. */
+ *        quantised per (token, 32 consecutive features).  dx bf16 (M, C).  dy carries the output mask. */
 int csu_mlp_fp8_bwd(long M, int C, const void* x, const void* dy, const void* w1q, const float* sw1,
                     const float* b1, const void* w2t, const float* sw2, const void* w1tp, void* dh, void* g,
                     void* dx, const csu_mlp_dropout* d, void* stream);

@@ -8,11 +8,10 @@ rules against the reference is therefore "parity unpinned": the reference has no
 what is pinned is that the device computes the reference Mlp on these rounded operands.
 
 * per-row weight quantisation: s = 2^ceil(log2(amax / 448)), q = e4m3fn(w / s) round-to-nearest-even
-* MX block quantisation (activations, gradients): per block of 32 values, s = 2^e with e the smallest
-  integer such that amax <= 448 * 2^e (0 for an all-zero block, clamped to [-127, 127]),
-  q = e4m3fn(v / s); blocks are 32 consecutive channels ("nat") or, along the Mlp's hidden features,
-  the 32 features of each 64-feature group whose index has the same bit 2 ("perm": the set a
-  32x32 MFMA accumulator-tile pair hands one operand lane).
+* MX block quantisation (activations, gradients): per block of 32 consecutive channels (or hidden
+  features), s = 2^e with e the smallest integer such that amax <= 448 * 2^e (0 for an all-zero
+  block, clamped to [-127, 127]), q = e4m3fn(v / s) -- the OCP MX rule with e4m3 elements, which the
+  kernels apply in registers in the hardware's k order (tools/probes/mx_layout_probe.hip).
 """
 from __future__ import annotations
 
@@ -39,21 +38,11 @@ def block_exponent(amax: torch.Tensor) -> torch.Tensor:
     return e.clamp(-127, 127)
 
 
-def mx_quant_nat(v: torch.Tensor) -> torch.Tensor:
+def mx_quant(v: torch.Tensor) -> torch.Tensor:
     """MX e4m3 rounding (dequantised, float64) with blocks of 32 consecutive values of the last dim."""
     shp = v.shape
     b = v.double().reshape(*shp[:-1], shp[-1] // 32, 32)
     s = torch.exp2(block_exponent(b.abs().amax(-1, keepdim=True)).double())
-    return (_e4m3(b / s) * s).reshape(shp)
-
-
-def mx_quant_perm(v: torch.Tensor) -> torch.Tensor:
-    """MX e4m3 rounding with the hidden-feature blocks of the fused Mlp: inside every 64-feature
-    group, the features with index bit 2 == 0 form one block, those with bit 2 == 1 the other."""
-    shp = v.shape
-    # feature 32 t + 8 g + 4 h + i of a group -> dims (t, g, h, i)
-    b = v.double().reshape(*shp[:-1], shp[-1] // 64, 2, 4, 2, 4)
-    s = torch.exp2(block_exponent(b.abs().amax(dim=(-4, -3, -1), keepdim=True)).double())
     return (_e4m3(b / s) * s).reshape(shp)
 
 
@@ -69,22 +58,22 @@ def quant_rows(w: torch.Tensor):
 class Fp8MlpFn(torch.autograd.Function):
     """fc2(Dropout(gelu(fc1(x)))) of cswin:180-196 with the fp8 fused Mlp's roundings (float64):
 
-    forward   h = mx_nat(x) W1^T + b1,  g = gelu(h) * m_h,  y = mx_perm(g) W2^T + b2
+    forward   h = mx(x) W1^T + b1,  g = gelu(h) * m_h,  y = mx(g) W2^T + b2
     backward  (straight-through: gradients flow through every rounding unchanged, except that the
               device multiplies rounded operands in the two input-gradient products as well)
-              dg = mx_nat(dy * s2) q2,  dh = dg * gelu'(h) * m_h,  dx = mx_perm(dh * s1) q1,
-              dW1 = dh^T x,  db1 = sum dh,  dW2 = dy^T mx_perm(g),  db2 = sum dy
+              dg = mx(dy * s2) q2,  dh = dg * gelu'(h) * m_h,  dx = mx(dh * s1) q1,
+              dW1 = dh^T x,  db1 = sum dh,  dW2 = dy^T mx(g),  db2 = sum dy
     w1 = q1 * s1[:, None], w2 = q2 * s2[:, None] are the dequantised e4m3 weights (quant_rows);
     m_h the hidden dropout mask (scale 0 or 1/keep) or None."""
 
     @staticmethod
     def forward(ctx, x, w1, b1, w2, b2, s1, s2, m_h):
         xd = x.double()
-        h = mx_quant_nat(xd) @ w1.double().t() + b1.double()
+        h = mx_quant(xd) @ w1.double().t() + b1.double()
         g = F.gelu(h)
         if m_h is not None:
             g = g * m_h
-        gq = mx_quant_perm(g)
+        gq = mx_quant(g)
         ctx.save_for_backward(xd, h, gq, w1.double(), w2.double(), s1.double(), s2.double())
         ctx.m_h = m_h
         return gq @ w2.double().t() + b2.double()
@@ -94,12 +83,12 @@ class Fp8MlpFn(torch.autograd.Function):
         xd, h, gq, w1, w2, s1, s2 = ctx.saved_tensors
         dy = dy.double()
         q1, q2 = w1 / s1[:, None], w2 / s2[:, None]
-        dg = mx_quant_nat(dy * s2) @ q2
+        dg = mx_quant(dy * s2) @ q2
         dgelu = 0.5 * (1 + torch.erf(h / math.sqrt(2))) + h * torch.exp(-0.5 * h * h) / math.sqrt(2 * math.pi)
         dh = dg * dgelu
         if ctx.m_h is not None:
             dh = dh * ctx.m_h
-        dx = mx_quant_perm(dh * s1) @ q1
+        dx = mx_quant(dh * s1) @ q1
         lead = dy.reshape(-1, dy.shape[-1])
         dh2 = dh.reshape(-1, dh.shape[-1])
         dw1 = dh2.t() @ xd.reshape(-1, xd.shape[-1])

@@ -69,6 +69,31 @@ def test_quantizer_matches_torch_e4m3fn():
         assert torch.equal(dq.cpu().bfloat16().float(), rd)     # exact in bf16
 
 
+def test_quantizer_into_cast_cache_shadows():
+    """csu_quant_e4m3_shadow_batch (the model's per-step path): the same bytes and scales as the
+    row quantiser, and the cast cache's bf16 shadows W and W^T equal the dequantised weights exactly
+    (ragged row counts: partial 64-row blocks and transposed tails)."""
+    from csu import ops
+    d = dev()
+    g = torch.Generator().manual_seed(1)
+    ws = [torch.randn(192, 64, generator=g) * 0.02, torch.randn(64, 256, generator=g) * 3.0,
+          torch.randn(100, 32, generator=g), torch.randn(1024, 256, generator=g) * 1e-3, torch.randn(16, 64, generator=g),
+          torch.randn(37, 48, generator=g)]
+    ps = [w.to(d) for w in ws] + [torch.randn(64, device=d)]          # + a 1-D tensor: cast, not quantised
+    fp8 = ops.Fp8Weights(ps)
+    cache = ops.CastCache()
+    cache.refresh(ps, torch.bfloat16, (), sources=fp8.sources())
+    fp8.quantize(cache)
+    torch.cuda.synchronize()
+    for i, w in enumerate(ws):
+        rd, rq, rs = _ref_quant(w)
+        assert torch.equal(fp8.scales[i].cpu(), rs)
+        assert torch.equal(fp8.q[i].cpu(), rq)
+        assert torch.equal(cache.shadow[i].float().cpu(), rd)
+        assert torch.equal(cache.shadow_t[i].float().cpu(), rd.t())
+    assert torch.equal(cache.shadow[-1], ps[-1].bfloat16())
+
+
 def test_fp8_weight_model_vs_oracle_with_quantized_weights(monkeypatch):
     from csu import ops
     from csu.data import ellipse_batch
@@ -125,7 +150,9 @@ def test_fp8_weight_model_vs_oracle_with_quantized_weights(monkeypatch):
     gn = np.array([q.grad.double().norm().item() for _, q in m.named_parameters()])
     gr = np.array([pref[k].grad.norm().item() for k, _ in m.named_parameters()])
     big = gr >= 1e-3 * gr.max()
-    np.testing.assert_allclose(gn[big], gr[big], rtol=5e-2)
+    names = [k for k, _ in m.named_parameters()]
+    off = [(names[i], float(gn[i] / gr[i] - 1)) for i in range(len(names)) if big[i] and abs(gn[i] / gr[i] - 1) > 5e-2]
+    assert not off, off
     # and the format matters: the bf16-weight model differs from the fp8 one
     m2 = CSWinTransformer(img_size=256, split_size=[1, 2, 8, 8]).to(d)
     m2.load_state_dict(p)
@@ -159,6 +186,11 @@ def test_layernorm_fp8_output_matches_torch(C, xdt):
     assert torch.allclose(deq, ref, rtol=0.13, atol=float(rs.max()) * 2.0 ** -9)   # at most one e4m3 step apart
     torch.testing.assert_close(mean.cpu(), x.float().mean(1), rtol=1e-5, atol=1e-5)
     assert torch.allclose(deq[5], (b / rs[5]).to(torch.float8_e4m3fn).float() * rs[5])
+    # the bf16 dequantised copy written by the same pass equals the dequantisation bitwise
+    q2, s2, _, _, dq = ops.layer_norm_fp8(x.to(d), w.to(d), b.to(d), 1e-5, dq=True)
+    torch.cuda.synchronize()
+    assert torch.equal(q2, q) and torch.equal(s2, s)
+    assert torch.equal(dq.cpu(), ops.dequant_e4m3_rows(q, s).cpu())
 
 
 @pytest.mark.parametrize("M,N,K", [(1000, 192, 64), (129, 384, 128), (4096, 768, 256), (257, 1536, 512),
@@ -237,7 +269,8 @@ def _mx_torch_check():
 @pytest.mark.parametrize("C,M,drop", [(128, 1000, False), (256, 4160, False), (256, 100, True), (128, 777, True)])
 def test_mlp_fp8_fused_vs_oracle(C, M, drop):
     """csu_mlp_fp8_fwd / csu_mlp_fp8_bwd vs the fp64 restatement of the same roundings
-    (oracle/fp8_ref.py: MX-quantised x / g / dY / dh, e4m3 weights with per-row scales).  Only the
+    (oracle/fp8_ref.py: x / g / dY / dh MX-quantised in blocks of 32 consecutive channels, e4m3
+    weights with per-row scales).  Only the
     device's fast GELU (|err| < 1.3e-5) and fp32 accumulation differ from the oracle, which can flip
     a rare e4m3 rounding of g or dh by one step: the gates are relative L2 errors, and the device is
     required to sit far closer to the fp8 oracle than to the unrounded Mlp."""
@@ -299,17 +332,17 @@ def test_mlp_fp8_fused_vs_oracle(C, M, drop):
     z_plain = g_plain @ W2d.T + B2
     assert rel(y - res, outm * z_plain) > 5 * rel(y - res, yref - R)
     # backward pieces
-    h = Q.mx_quant_nat(X) @ W1d.T + B1
+    h = Q.mx_quant(X) @ W1d.T + B1
     g = torch.nn.functional.gelu(h) * (mh if mh is not None else 1)
-    gqr = Q.mx_quant_perm(g)
+    gqr = Q.mx_quant(g)
     assert rel(gq, gqr) < 1e-2
     assert float((gq.double().cpu() != gqr).double().mean()) < 2e-3      # rare one-step rounding flips only
     q1, q2 = W1d / S1[:, None], W2d / S2[:, None]
-    dg = Q.mx_quant_nat(DZ * S2) @ q2
+    dg = Q.mx_quant(DZ * S2) @ q2
     dgelu = 0.5 * (1 + torch.erf(h / 2 ** 0.5)) + h * torch.exp(-0.5 * h * h) / (2 * torch.pi) ** 0.5
     dhr = dg * dgelu * (mh if mh is not None else 1)
     assert rel(dh, dhr) < 5e-3, rel(dh, dhr)
-    dxr = Q.mx_quant_perm(dhr * S1) @ q1
+    dxr = Q.mx_quant(dhr * S1) @ q1
     assert rel(dx, dxr) < 1e-2, rel(dx, dxr)
     # the autograd form of the oracle gives the same input gradient
     Xg = X.clone().requires_grad_(True)
