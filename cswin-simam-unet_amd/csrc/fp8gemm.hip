@@ -135,11 +135,20 @@ __global__ __launch_bounds__(NT) void dequant_rows_kernel(long rows, int cols, c
 
 using namespace csu;
 
+namespace csu {
+int gemm4_fp8_run(long M, int N, int K, const uint8_t* A, const float* sa, const uint8_t* W, const float* sw,
+                  const float* bias, bf16* out, hipStream_t st);
+}
+
 extern "C" int csu_fp8_gemm(long M, int N, int K, const void* aq, const float* sa, const void* wq, const float* sw,
                             const float* bias, void* out, void* stream) {
     if (M < 1 || N < 1 || K < 1 || !aq || !sa || !wq || !sw || !out) return fail(CSU_E_ARG, "fp8_gemm: bad arguments");
     if (N % BN || K % KS) return fail(CSU_E_UNSUPPORTED, "fp8_gemm: N % 64 == 0 and K % 64 == 0 required");
     if (M * (long)K > 0x7fffffffL || M * (long)N * 2 > 0x7fffffffL) return fail(CSU_E_ARG, "fp8_gemm: tensor exceeds 2 GB");
+    // K % 128 == 0: the persistent LDS-DMA design of the bf16 token GEMM (gemm4.hip, F8); K = 64 (the
+    // stage-1 qkv at C = 64): the register-prefetch tile below
+    if (K % 128 == 0) return gemm4_fp8_run(M, N, K, (const uint8_t*)aq, sa, (const uint8_t*)wq, sw, bias, (bf16*)out,
+                                           as_stream(stream));
     const long tiles = ((M + BM - 1) / BM) * (N / BN);
     fp8_gemm_kernel<<<(unsigned)tiles, NT, 0, as_stream(stream)>>>(M, N, K, (const uint8_t*)aq, sa, (const uint8_t*)wq, sw,
                                                                    bias, (bf16*)out);

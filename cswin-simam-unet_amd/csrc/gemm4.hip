@@ -97,11 +97,18 @@ __device__ __forceinline__ void g4_vmwait_floor(int c) {
 // the last unit it re-fetches the last unit into the free stage), and a tile's last step issues
 // its L epilogue loads BEFORE its DMA (so waiting for them does not wait for the prefetch) and its
 // ST stores after the MFMAs.
-template <int BM, int BN, int S, int OCC, int EPI, typename TOUT, int WM = 2, int WN = 2>
+// F8: e4m3 operands (BASELINE config 5): A (M, K) / W (N, K) are e4m3 BYTE matrices with one fp32
+// scale per row (sa per token, sw per output feature), K counted in bytes; a 128-byte K slice (the
+// bf16 slice's bytes) is two k-steps of v_mfma_scale_f32_32x32x64_f8f6f4 at unit block scales, and
+// the epilogue multiplies by sa[m] sw[n] before the bias.  lda / ldw are then given in bf16 units
+// (bytes / 2) so that the DMA code is shared.
+template <int BM, int BN, int S, int OCC, int EPI, typename TOUT, int WM = 2, int WN = 2, bool F8 = false>
 __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm4_kernel(long M, int N, int K, const bf16* __restrict__ A, int lda,
                                                            const bf16* __restrict__ W, int ldw, const float* __restrict__ bias,
                                                            const bf16* __restrict__ gaux, const float* __restrict__ resid,
-                                                           TOUT* __restrict__ out, bf16* __restrict__ gout, int ldc) {
+                                                           TOUT* __restrict__ out, bf16* __restrict__ gout, int ldc,
+                                                           const float* __restrict__ sa = nullptr,
+                                                           const float* __restrict__ sw = nullptr) {
     constexpr int NWV = WM * WN;                     // waves: WM along tokens x WN along features
     constexpr int TMW = BM / (32 * WM), TNW = BN / (32 * WN);   // 32x32 tiles per wave (tokens, features)
     static_assert(TMW >= 1 && TNW >= 1 && BM % (8 * NWV) == 0 && BN % (8 * NWV) == 0, "gemm4 wave layout");
@@ -118,7 +125,8 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm4_kernel(long M, int N,
     constexpr int Q = 32 / RPS;                      // instructions per 32-row pass
     constexpr int ERS = WC + 4;                      // fp32 row stride of the transposition region
     constexpr int OS = sizeof(TOUT);
-    constexpr int L = 2 + (EPI == G4_RESID ? 2 : EPI == G4_GAUX ? 1 : 0) * TMW * Q;   // epilogue loads per wave
+    constexpr int L = 2 + (EPI == G4_RESID ? 2 : EPI == G4_GAUX ? 1 : 0) * TMW * Q   // epilogue loads per wave
+                      + (F8 ? 2 + TMW * Q : 0);                                        // + sw (2), sa per row
     constexpr int ST = TMW * Q * ((OS == 4 ? 2 : 1) + (EPI == G4_GELU_OUT ? 1 : 0));   // epilogue stores per wave
     constexpr int EPB = 32 * ERS * 4;                // bytes per wave
     __shared__ __attribute__((aligned(1024))) bf16 smem[S * STAGE + NWV * EPB / 2];
@@ -131,7 +139,7 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm4_kernel(long M, int N,
     const unsigned cnt = q + (x < rem ? 1 : 0);
     const int mytiles = kk < cnt ? (int)((cnt - kk + nloc - 1) / nloc) : 0;
     if (mytiles == 0) return;
-    const int nk = K / G4_BK;
+    const int nk = F8 ? K / (2 * G4_BK) : K / G4_BK;   // K slices (F8: K in bytes, 128-byte slices)
     const int U = mytiles * nk;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -175,6 +183,33 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm4_kernel(long M, int N,
 #pragma unroll
             for (int j = 0; j < TNW; ++j) wf[b][j] = *reinterpret_cast<const bf16x8*>(Ws + g4_off(wn + 32 * j + r, 2 * s + h));
         };
+        if constexpr (F8) {
+            // 128-byte slice = k-steps s = 0, 1 of 64 bytes; lane (r, h) takes 32 contiguous bytes at 64 s + 32 h
+            // of its row in both operands (16-B chunks 4 s + 2 h, + 1): the pairing is exact whatever the
+            // hardware's k order, and the block scales are unit (the row scales come in the epilogue)
+            typedef int i32x8 __attribute__((ext_vector_type(8)));
+            auto f8 = [&](const bf16* img, int row, int s) {
+                const u32x4 lo = *reinterpret_cast<const u32x4*>(img + g4_off(row, 4 * s + 2 * h));
+                const u32x4 hi = *reinterpret_cast<const u32x4*>(img + g4_off(row, 4 * s + 2 * h + 1));
+                return i32x8{(int)lo[0], (int)lo[1], (int)lo[2], (int)lo[3], (int)hi[0], (int)hi[1], (int)hi[2], (int)hi[3]};
+            };
+            i32x8 a8[2][TMW], w8[2][TNW];
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+#pragma unroll
+                for (int i = 0; i < TMW; ++i) a8[s][i] = f8(As, wm + 32 * i + r, s);
+#pragma unroll
+                for (int j = 0; j < TNW; ++j) w8[s][j] = f8(Ws, wn + 32 * j + r, s);
+            }
+#pragma unroll
+            for (int s = 0; s < 2; ++s)
+#pragma unroll
+                for (int i = 0; i < TMW; ++i)
+#pragma unroll
+                    for (int j = 0; j < TNW; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(w8[s][j], a8[s][i], acc[i][j], 0, 0, 0, 0,
+                                                                                     0, 0);
+        } else {
         frags(0, 0);
 #pragma unroll
         for (int s = 0; s < G4_BK / 16; ++s) {
@@ -184,6 +219,7 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm4_kernel(long M, int N,
 #pragma unroll
                 for (int j = 0; j < TNW; ++j)
                     acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[s & 1][j], af[s & 1][i], acc[i][j], 0, 0, 0);
+        }
         }
     };
 
@@ -222,6 +258,19 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm4_kernel(long M, int N,
         const auto rs_b = buf_rsrc(bias, bias ? (long)N * 4 : 0);   // null bias: every load reads 0
         buf_ld4(rs_b, n < N ? (unsigned)n * 4 : kOOB, bv);
         buf_ld4(rs_b, n < N ? (unsigned)n * 4 + 16 : kOOB, bv + 4);
+        float swv[8], sav[TMW][Q];
+        if constexpr (F8) {
+            const auto rs_sw = buf_rsrc(sw, (long)N * 4);
+            buf_ld4(rs_sw, n < N ? (unsigned)n * 4 : kOOB, swv);
+            buf_ld4(rs_sw, n < N ? (unsigned)n * 4 + 16 : kOOB, swv + 4);
+            const auto rs_sa = buf_rsrc(sa + m0, rows * 4);
+#pragma unroll
+            for (int i = 0; i < TMW; ++i)
+#pragma unroll
+                for (int q = 0; q < Q; ++q)
+                    sav[i][q] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+                        rs_sa, (unsigned)(wm + 32 * i + RPS * q + rr) * 4, 0, 0));
+        }
         float pre[TMW][Q][8];
         if constexpr (PRE) {
             const auto rs_pre = EPI == G4_GAUX ? buf_rsrc(gaux + m0 * ldc, rows * ldc * 2) : buf_rsrc(resid + m0 * ldc, rows * ldc * 4);
@@ -262,10 +311,18 @@ __global__ __launch_bounds__(64 * WM * WN, OCC) void gemm4_kernel(long M, int N,
                 const f32x4 lo4 = *reinterpret_cast<const f32x4*>(src);
                 const f32x4 hi4 = *reinterpret_cast<const f32x4*>(src + 4);
                 float v[8];
+                if constexpr (F8) {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        v[e] = lo4[e] * (sav[i][q] * swv[e]) + bv[e];
+                        v[e + 4] = hi4[e] * (sav[i][q] * swv[e + 4]) + bv[e + 4];
+                    }
+                } else {
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     v[e] = lo4[e] + bv[e];
                     v[e + 4] = hi4[e] + bv[e + 4];
+                }
                 }
                 if constexpr (EPI == G4_GAUX) {
 #pragma unroll
@@ -345,6 +402,15 @@ int g4_epi(int epi, int odt, long M, int N, int K, const bf16* A, int lda, const
 }
 
 }  // namespace
+
+// fp8 token GEMM (csu_fp8_gemm for K % 128 == 0): the 128 x 64 tile, 2-stage ring, 2 workgroups per
+// CU of the bf16 path, bf16 output with bias
+int gemm4_fp8_run(long M, int N, int K, const uint8_t* A, const float* sa, const uint8_t* W, const float* sw,
+                  const float* bias, bf16* out, hipStream_t st) {
+    gemm4_kernel<128, 64, 2, 2, G4_PLAIN, bf16, 2, 2, true><<<dim3(g4_grid(2)), 256, 0, st>>>(
+        M, N, K, (const bf16*)A, K / 2, (const bf16*)W, K / 2, bias, nullptr, nullptr, out, nullptr, N, sa, sw);
+    return check_launch("fp8_gemm");
+}
 
 // Tile choice (tools/linear_probe.py, tools/gemm_graph_probe.py: every token-GEMM shape of the 512x512
 // step, graph-timed, profiles/r02al_gemm_probe.txt): 128 x 64 with a 2-stage ring at 2 workgroups per

@@ -41,10 +41,17 @@ def main():
     ends = [int(r["End_Timestamp"]) for r in rows if "adamw_kernel" in r["Kernel_Name"]]
     a, b = ends[-1 - nsteps], ends[-1]
     t, n = collections.defaultdict(float), collections.Counter()
+    prev = None
     for r in rows:
         s = int(r["Start_Timestamp"])
         if a < s <= b:
             g = group(r["Kernel_Name"])
+            # the fixed-order slab reduction inside a conv / Linear weight-gradient call (csu_colsum's
+            # kernels launched by csu_conv2d_wgrad_oihw) belongs to that call: a colsum kernel right
+            # after a weight-gradient kernel is charged to it (ops.colsum's own launches stay "colsum")
+            if g == "colsum" and prev in ("conv_wgrad", "linear_wgrad"):
+                g = prev
+            prev = g
             t[g] += (int(r["End_Timestamp"]) - s) / 1e3
             n[g] += 1
     ledger = {}
