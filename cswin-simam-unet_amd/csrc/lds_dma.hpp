@@ -10,11 +10,14 @@
 
 namespace csu {
 
-// swizzle key of an image row.  RB = bytes per row.  128-B rows: two rows share a 256-B bank row,
-// key = bitrev3((row >> 1) & 7); >= 256-B rows: key = bitrev4(row & 15).
+// swizzle key of an image row.  RB = bytes per row.  64-B rows: four rows share a 256-B bank row,
+// key = (row >> 2) & 3; 128-B rows: two rows share one, key = bitrev3((row >> 1) & 7); >= 256-B rows:
+// key = bitrev4(row & 15).
 template <int RB>
 __device__ __forceinline__ int mkey(int row) {
-    if constexpr (RB == 128) {
+    if constexpr (RB == 64) {
+        return (row >> 2) & 3;
+    } else if constexpr (RB == 128) {
         const int v = (row >> 1) & 7;
         return ((v & 1) << 2) | (v & 2) | ((v >> 2) & 1);
     } else {

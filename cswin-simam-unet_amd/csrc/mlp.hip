@@ -1176,7 +1176,7 @@ extern "C" int csu_mlp_bwd(long M, int C, const void* x, const void* dy, const v
     return csu_mlp_bwd_dp(M, C, x, dy, w1, b1, w2, dh, g, dx, nullptr, stream);
 }
 
-extern "C" int csu_mlp_fp8_supported(int C) { return C == 128 || C == 256; }
+extern "C" int csu_mlp_fp8_supported(int C) { return C == 64 || C == 128 || C == 256; }
 
 extern "C" int csu_mlp_fp8_fwd(long M, int C, const void* x, const void* w1q, const float* sw1, const float* b1,
                                const void* w2p, const float* sw2, const float* b2, const float* res, float* out,
@@ -1191,9 +1191,10 @@ extern "C" int csu_mlp_fp8_fwd(long M, int C, const void* x, const void* w1q, co
     const long rpi = d ? (long)d->rows_per_sample : 0;
     const hipStream_t st = as_stream(stream);
     switch (C) {
+        case 64: return fp8_fwd_launch<64>(M, x, w1q, sw1, b1, w2p, sw2, b2, res, out, dp, rpi, st);
         case 128: return fp8_fwd_launch<128>(M, x, w1q, sw1, b1, w2p, sw2, b2, res, out, dp, rpi, st);
         case 256: return fp8_fwd_launch<256>(M, x, w1q, sw1, b1, w2p, sw2, b2, res, out, dp, rpi, st);
-        default: return fail(CSU_E_UNSUPPORTED, "mlp_fp8_fwd: C must be 128 or 256");
+        default: return fail(CSU_E_UNSUPPORTED, "mlp_fp8_fwd: C must be 64, 128 or 256");
     }
 }
 
@@ -1210,8 +1211,9 @@ extern "C" int csu_mlp_fp8_bwd(long M, int C, const void* x, const void* dy, con
     const long rpi = d ? (long)d->rows_per_sample : 0;
     const hipStream_t st = as_stream(stream);
     switch (C) {
+        case 64: return fp8_bwd_launch<64>(M, x, dy, w1q, sw1, b1, w2t, sw2, w1tp, dh, g, dx, dp, rpi, st);
         case 128: return fp8_bwd_launch<128>(M, x, dy, w1q, sw1, b1, w2t, sw2, w1tp, dh, g, dx, dp, rpi, st);
         case 256: return fp8_bwd_launch<256>(M, x, dy, w1q, sw1, b1, w2t, sw2, w1tp, dh, g, dx, dp, rpi, st);
-        default: return fail(CSU_E_UNSUPPORTED, "mlp_fp8_bwd: C must be 128 or 256");
+        default: return fail(CSU_E_UNSUPPORTED, "mlp_fp8_bwd: C must be 64, 128 or 256");
     }
 }

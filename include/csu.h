@@ -505,7 +505,7 @@ int csu_mlp_bwd_dp(long M, int C, const void* x, const void* dy, const void* w1,
  *   g   = gelu(h) (* hidden dropout), g_q = g quantised per (token, 32 consecutive features);
  *   out = res + (g_q W2^T + b2) (* output dropout, DropPath).
  * w1q: (4C, C) e4m3 rows with power-of-two row scales sw1 (4C); w2p: (C, 4C) e4m3 rows (scales sw2,
- * C) with the columns permuted as csu_e4m3_layout_batch mode 2.  C in {128, 256}. */
+ * C) with the columns permuted as csu_e4m3_layout_batch mode 2.  C in {64, 128, 256}. */
 int csu_mlp_fp8_supported(int C);
 int csu_mlp_fp8_fwd(long M, int C, const void* x, const void* w1q, const float* sw1, const float* b1,
                     const void* w2p, const float* sw2, const float* b2, const float* res, float* out,

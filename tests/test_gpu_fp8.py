@@ -114,8 +114,8 @@ def test_fp8_weight_model_vs_oracle_with_quantized_weights(monkeypatch):
     with torch.autocast("cuda", dtype=torch.bfloat16):
         y = m(x.to(d))
     assert len(calls) == sum(1 for mod in m.modules() if type(mod).__name__ == "CSWinBlock")   # every qkv on fp8 MFMA
-    # every Mlp at C = 128 / 256 on the fp8 fused kernels
-    assert sum(mcalls) == sum(1 for mod in m.modules() if type(mod).__name__ == "Mlp" and mod.fc1.in_features in (128, 256))
+    # every Mlp at C = 64 / 128 / 256 on the fp8 fused kernels
+    assert sum(mcalls) == sum(1 for mod in m.modules() if type(mod).__name__ == "Mlp" and mod.fc1.in_features in (64, 128, 256))
     assert sum(mcalls) > 10
     loss = bce_loss(y, t.to(d))
     loss.backward()
@@ -130,11 +130,11 @@ def test_fp8_weight_model_vs_oracle_with_quantized_weights(monkeypatch):
     assert sum(1 for w in m._linear_weights() if id(w) in quant) > 100
     pref = {k: v.double().requires_grad_(True) for k, v in pq.items()}
     monkeypatch.setattr(O, "QKV_INPUT_QUANT", _tok_quant)
-    # the Mlps at C = 128 / 256 run the fp8 fused kernels: their MX roundings (oracle/fp8_ref.py)
+    # the Mlps at C = 64 / 128 / 256 run the fp8 fused kernels: their MX roundings (oracle/fp8_ref.py)
     from oracle import fp8_ref as Q
 
     def mlp_fp8(xx, pp, key, m_h):
-        if xx.shape[-1] not in (128, 256):
+        if xx.shape[-1] not in (64, 128, 256):
             return None
         s1 = Q.quant_rows(p[key + ".fc1.weight"])[2]
         s2 = Q.quant_rows(p[key + ".fc2.weight"])[2]
@@ -241,7 +241,7 @@ def _perm64(q: torch.Tensor) -> torch.Tensor:
     return q[:, full]
 
 
-@pytest.mark.parametrize("C", [128, 256])
+@pytest.mark.parametrize("C", [64, 128, 256])
 def test_e4m3_mlp_layouts(C):
     """csu_e4m3_layout_batch: W2 with permuted columns, W2^T, W1^T with permuted columns, bytewise."""
     from csu import ops
@@ -266,7 +266,8 @@ def _mx_torch_check():
     assert e.tolist() == [0, 1, -11, 0, -8]
 
 
-@pytest.mark.parametrize("C,M,drop", [(128, 1000, False), (256, 4160, False), (256, 100, True), (128, 777, True)])
+@pytest.mark.parametrize("C,M,drop", [(128, 1000, False), (256, 4160, False), (256, 100, True), (128, 777, True),
+                                      (64, 5000, False), (64, 333, True)])
 def test_mlp_fp8_fused_vs_oracle(C, M, drop):
     """csu_mlp_fp8_fwd / csu_mlp_fp8_bwd vs the fp64 restatement of the same roundings
     (oracle/fp8_ref.py: x / g / dY / dh MX-quantised in blocks of 32 consecutive channels, e4m3

@@ -3,7 +3,7 @@
 # Any other outcome -- success, a failure of the command, a refusal -- is returned as is.
 # usage: tools/gpuwait.sh <timeout-seconds> <command string>
 T=$1; shift
-for i in $(seq 1 12); do
+for i in $(seq 1 40); do
     /usr/local/graft/bin/gpurun --timeout "$T" -- "$@"
     rc=$?
     [ $rc -ne 3 ] && exit $rc

@@ -23,7 +23,7 @@ def t(fn, n=20):
 
 d = torch.device("cuda:0")
 st = stream_ptr(d)
-for C, M in [(128, 65536), (256, 16384)]:
+for C, M in [(64, 262144), (128, 65536), (256, 16384)]:
     x = torch.randn(M, C, device=d).bfloat16()
     w1f = torch.randn(4 * C, C, device=d) * C ** -0.5
     w2f = torch.randn(C, 4 * C, device=d) * (4 * C) ** -0.5
@@ -37,7 +37,7 @@ for C, M in [(128, 65536), (256, 16384)]:
     fp8.quantize()
     w1q, sw1, w2p, sw2, w2t, w1tp = fp8.mlp_operands(w1f, w2f)
     md = ops.MlpDrop(None, 0, 0, 0.0).c_struct()
-    md.rows_per_sample = 4096 if C == 256 else 16384
+    md.rows_per_sample = {64: 65536, 128: 16384, 256: 4096}[C]
     mdp = ctypes.byref(md)
     f = t(lambda: check(lib().csu_mlp_fwd_dp(M, C, ptr(x), ptr(w1), ptr(b1), ptr(w2), ptr(b2), ptr(res), ptr(y), mdp, st), "f"))
     bw = t(lambda: check(lib().csu_mlp_bwd_dp(M, C, ptr(x), ptr(dy), ptr(w1), ptr(b1), ptr(w2), ptr(dh), ptr(g), ptr(dx),
