@@ -93,12 +93,26 @@ def _cpu_model():
     return "unknown"
 
 
+def _cpu_threads():
+    """CPU threads of the baseline: this GPU's CPU share -- OMP_NUM_THREADS (16 per GPU on the MI355X
+    boxes), capped by the affinity mask.  The affinity mask lists the whole host (many times the
+    share); timing on all of it would measure other jobs' cores, not this GPU's host share."""
+    aff = len(os.sched_getaffinity(0))
+    share = int(os.environ.get("OMP_NUM_THREADS", "16") or 16)
+    return max(1, min(share, aff))
+
+
+def _cores_note(threads):
+    return (f"{threads} threads = the per-GPU CPU share (OMP_NUM_THREADS); affinity mask "
+            f"{len(os.sched_getaffinity(0))} cpus (the whole host)")
+
+
 def cpu_baseline_unet(args, dtype):
     """Plain-UNet oracle (oracle/unet_ref.py, parity-pinned to the reference by F6) fwd+BCE+bwd+Adam
     on the same per-GPU batch: 1 warm-up + 2 timed steps."""
     from oracle import unet_ref as U
     from oracle.recipe import recipe_from_contract
-    threads = min(16, len(os.sched_getaffinity(0)))
+    threads = _cpu_threads()
     torch.set_num_threads(threads)
     p = recipe_from_contract(U.unet_contract(), seed=0)
     params = {k: v.requires_grad_(True) for k, v in p.items() if "running" not in k and "num_batches" not in k}
@@ -121,6 +135,7 @@ def cpu_baseline_unet(args, dtype):
         step()
     el = time.perf_counter() - t0
     return {"value": round(2 * b / el, 4), "unit": "images/sec", "cores": threads, "kind": "port", "cpu": _cpu_model(),
+            "cores_note": _cores_note(threads),
             "sample": f"2 train steps x batch {b} at {args.img}x{args.img} "
                       f"({'bf16 autocast' if dtype == torch.bfloat16 else 'fp32'}) after 1 warm-up step, "
                       f"oracle/unet_ref.py, {el:.1f}s, {threads} threads"}
@@ -131,7 +146,7 @@ def cpu_baseline(args, dtype):
     1 warm-up + 2 timed steps (~10-30 s).  Threads: the process's CPU affinity, capped at 16 -- the
     GPU box's CPU share per GPU (more threads than the share only contend)."""
     from oracle import cswin_ref as O
-    threads = min(16, len(os.sched_getaffinity(0)))
+    threads = _cpu_threads()
     torch.set_num_threads(threads)
     cfg = O.CSWinConfig(img_size=args.img, depth=[int(v) for v in args.depth.split(",")],
                         split_size=[int(v) for v in args.split.split(",")], simam=args.simam)
@@ -160,7 +175,7 @@ def cpu_baseline(args, dtype):
         n += 1
     el = time.perf_counter() - t0
     return {"value": round(n * b / el, 4), "unit": "images/sec", "cores": threads, "kind": "port",
-            "cpu": _cpu_model(),
+            "cpu": _cpu_model(), "cores_note": _cores_note(threads),
             "sample": f"{n} train steps x batch {b} at {args.img}x{args.img} "
                       f"({'bf16 autocast' if dtype == torch.bfloat16 else 'fp32'}) after 1 warm-up step, "
                       f"oracle/cswin_ref.py, {el:.1f}s, {threads} threads"}

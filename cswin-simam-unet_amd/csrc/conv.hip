@@ -1141,7 +1141,131 @@ __global__ __launch_bounds__(512, 1) void conv3_halo64(int B, int H, int W, cons
     vmwait<0>();
 }
 
+
+// ---- few-channel 3x3 / stride 1 / pad 1 forward conv, 16 input channels, N outputs (N % 16 == 0):
+// the CARAFE4 encoder Conv2d(16, 144, 3, 1, 1) (cswin:446) at 128 x 128 / 256 x 256 ----------------
+// The generic implicit GEMM gathers the 16-channel input per tap into 64-deep K slices (a quarter of a
+// slice per tap) and tiles N = 144 as 3 x 64; its time was ~7x the 75 MB the 144-channel output is.
+// Here every wave holds the whole weight matrix as MFMA A fragments in registers (N x 160 k, k = tap *
+// 16 + c, tap 9 zero: 45 fragments of v_mfma_f32_16x16x32_bf16), the workgroup walks 64-pixel row
+// segments whose three 66-pixel input halo rows ([3][66][16] bf16, 7 DMA blocks) are fetched one item
+// ahead (2 stages), wave w computes pixels 16 w .. 16 w + 15 x all N outputs (k-step = two taps x 16
+// channels, 5 steps), and the 16 x N output tile goes through a wave-private LDS region so every
+// pixel's N outputs leave as contiguous 16-B stores.  2 workgroups per CU.
+template <int N>
+__global__ __launch_bounds__(256, 2) void conv3_c16(int B, int H, int W, const bf16* __restrict__ src, const bf16* __restrict__ w_ohwi,
+                                                    const float* __restrict__ bias, bf16* __restrict__ out) {
+    constexpr int NT16 = N / 16;                 // 16-output tiles
+    constexpr int HALO = 3 * 66 * 16;            // bf16 of a stage's halo image
+    constexpr int STAGE = 7 * 512;               // bf16 per stage (7 DMA blocks of 1 KB)
+    constexpr int EST = N + 8;                   // epilogue row stride (bf16)
+    constexpr int NST = (16 * N / 8 + 63) / 64;  // 16-B stores per lane per segment
+    static_assert(HALO <= STAGE, "halo image exceeds its stage");
+    __shared__ __attribute__((aligned(1024))) bf16 ring[2 * STAGE];
+    __shared__ __attribute__((aligned(16))) bf16 ep[4][16 * EST];
+    __shared__ __attribute__((aligned(16))) float sbias[N];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int spr = W / 64;
+    const long items = (long)B * H * spr;
+    const long x = blockIdx.x % kXcds, kk = blockIdx.x / kXcds, nloc = gridDim.x / kXcds;
+    const long q = items / kXcds, rem = items % kXcds;
+    const long lo = x < rem ? x * (q + 1) : rem * (q + 1) + (x - rem) * q;
+    const long cnt = q + (x < rem ? 1 : 0);
+    const int my = kk < cnt ? (int)((cnt - kk + nloc - 1) / nloc) : 0;
+    if (my == 0) return;
+    const int l16 = lane & 15, kg = lane >> 4;
+    // the weights as A fragments: lane (n = 16 t + l16, k-group kg) of k-step s = W[n][32 s + 8 kg .. + 7]
+    // (OHWI [n][tap][c] = [n][k]; k >= 144 zero)
+    bf16x8 aw[5][NT16];
+    {
+        const __amdgpu_buffer_rsrc_t rw = buf_rsrc(w_ohwi, (long)N * 144 * 2);
+#pragma unroll
+        for (int s2 = 0; s2 < 5; ++s2)
+#pragma unroll
+            for (int t = 0; t < NT16; ++t) {
+                const int k = 32 * s2 + 8 * kg;
+                const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rw, k < 144 ? (unsigned)(((16 * t + l16) * 144 + k) * 2) : kOOB, 0, 0);
+                __builtin_memcpy(&aw[s2][t], &v, 16);
+            }
+    }
+    for (int i = threadIdx.x; i < N; i += 256) sbias[i] = bias ? bias[i] : 0.f;
+    const i32x4 rs = rsrc4(src, (long)B * H * W * 16 * 2);
+    auto issue = [&](int u) {   // the 3 x 66-pixel halo of item lo + kk + u * nloc: blocks of 32 pixels
+        const long it = lo + kk + (long)(u < my ? u : my - 1) * nloc;
+        const bool iv = u < my;
+        const long t1 = it / spr;
+        const int ox0 = (int)(it - t1 * spr) * 64;
+        const int b = (int)(t1 / H), oy = (int)(t1 - (long)b * H);
+        bf16* stg = ring + (u & 1) * STAGE;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int j = wave * 2 + i;              // block j: halo pixels 32 j .. 32 j + 31 of [3][66]
+            if (j < 7) {
+                const int p = 32 * j + (lane >> 1), ky = p / 66, px = p - 66 * ky;
+                const int iy = oy + ky - 1, ix = ox0 - 1 + px;
+                const bool ok = iv && p < 3 * 66 && iy >= 0 && iy < H && ix >= 0 && ix < W;
+                const unsigned off = ok ? (unsigned)(((((long)b * H + iy) * W + ix) * 16 + 8 * (lane & 1)) * 2) : kOOB;
+                dma1_u(rs, off, 0u, stg + j * 512);
+            }
+        }
+    };
+    const __amdgpu_buffer_rsrc_t rso = buf_rsrc(out, (long)B * H * W * N * 2);
+    issue(0);
+    __syncthreads();   // bias in LDS
+    for (int u = 0; u < my; ++u) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (u == 0) vmwait<0>(); else vmwait<NST>();   // item u landed (younger: item u-1's stores)
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        issue(u + 1);
+        const bf16* st = ring + (u & 1) * STAGE;
+        f32x4 acc[NT16];
+#pragma unroll
+        for (int t = 0; t < NT16; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s2 = 0; s2 < 5; ++s2) {
+            const int tap = 2 * s2 + (kg >> 1), tp = tap < 9 ? tap : 8;   // tap 9: zero weights (finite operand)
+            const int ky = tp / 3, kx = tp % 3;
+            const bf16x8 bx = *reinterpret_cast<const bf16x8*>(st + (ky * 66 + 16 * wave + l16 + kx) * 16 + 8 * (kg & 1));
+#pragma unroll
+            for (int t = 0; t < NT16; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw[s2][t], bx, acc[t], 0, 0, 0);
+        }
+        // acc[t][i] = out[pixel 16 wave + l16][n = 16 t + 4 kg + i]
+        bf16* e = ep[wave];
+#pragma unroll
+        for (int t = 0; t < NT16; ++t) {
+            const int n = 16 * t + 4 * kg;
+            const f32x4 bv = *reinterpret_cast<const f32x4*>(sbias + n);
+            const bf16x4 v = {(bf16)(acc[t][0] + bv[0]), (bf16)(acc[t][1] + bv[1]), (bf16)(acc[t][2] + bv[2]), (bf16)(acc[t][3] + bv[3])};
+            *reinterpret_cast<bf16x4*>(e + l16 * EST + n) = v;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the wave's own LDS writes before its reads
+        const long it = lo + kk + (long)u * nloc;
+        const long t1 = it / spr;
+        const int ox0 = (int)(it - t1 * spr) * 64;
+        const long pix0 = t1 * W + ox0 + 16 * wave;             // (b * H + oy) * W + ox
+#pragma unroll
+        for (int k = 0; k < NST; ++k) {
+            const int c = lane + 64 * k;                         // 16-B chunk: pixel c / (N / 8), chunk c % (N / 8)
+            const int pp = c / (N / 8), ch = c % (N / 8);
+            const bool ok = c < 16 * N / 8;
+            u32x4 v = {};
+            if (ok) v = *reinterpret_cast<const u32x4*>(e + pp * EST + 8 * ch);
+            __builtin_amdgcn_raw_buffer_store_b128(v, rso, ok ? (unsigned)(((pix0 + pp) * N + 8 * ch) * 2) : kOOB, 0, 0);
+        }
+    }
+    vmwait<0>();
+}
+
+bool c16_ok(const IG& g) {   // the forward 3x3 / stride 1 / pad 1 conv of a 16-channel input, N <= 144
+    return g.Cs == 16 && g.Ncols == 144 && g.nty == 3 && g.ntx == 3 && g.csplit == 0 && g.nsplit == 0 && g.OHo == g.Hs &&
+           g.OWo == g.Ws && g.Ws % 64 == 0 && g.RH == g.Hs && g.RW == g.Ws && g.sty == 1 && g.stx == 1 && g.ay == 1 &&
+           g.ax == 1 && g.by == -1 && g.bx == -1;
+}
+
 constexpr int kHalo64Cfg = 20;   // csu_conv2d_ex cfg selecting conv3_halo64
+constexpr int kC16Cfg = 21;      // csu_conv2d_ex cfg selecting conv3_c16
 bool halo64_ok(const IG& g, bool flip) {   // the forward conv (flip: its input gradient) this kernel takes
     return g.Cs == 64 && g.Ncols == 64 && g.nty == 3 && g.ntx == 3 && g.csplit == 0 && g.nsplit == 0 && g.OHo == g.Hs &&
            g.OWo == g.Ws && g.Hs % 2 == 0 && g.Ws % 64 == 0 && g.RH == g.Hs && g.RW == g.Ws &&
@@ -1228,6 +1352,11 @@ int launch_ig(const IG* gv, int n, const void* src, const void* w, const float* 
         }
     }
     if (cfg == kHalo64Cfg) return fail(CSU_E_ARG, "conv2d: halo64 configuration not eligible");
+    if ((cfg < 0 || cfg == kC16Cfg) && n == 1 && c16_ok(g)) {   // 16 -> 144 channel 3x3 conv (CARAFE4 encoder)
+        conv3_c16<144><<<dim3(2 * id_cus()), 256, 0, st>>>(g.B, g.Hs, g.Ws, (const bf16*)src, (const bf16*)w, bias, (bf16*)out);
+        return check_launch("conv2d (c16)");
+    }
+    if (cfg == kC16Cfg) return fail(CSU_E_ARG, "conv2d: c16 configuration not eligible");
     if (cfg > 0) {   // forced v3 configuration: every phase must be eligible for it
         const int k = cfg - 1;
         if (k >= kIDNCfg) return fail(CSU_E_ARG, "conv2d: bad igemm_dma configuration");

@@ -537,6 +537,7 @@ CONV_CASES = [  # (B, H, C, N, k, stride, pad)
     (2, 32, 3, 64, 7, 4, 2),      # patch embed (cswin:505)
     (2, 16, 64, 128, 3, 2, 1),    # Merge_Block (cswin:376)
     (1, 8, 16, 144, 3, 1, 1),     # CARAFE4 encoder (cswin:446)
+    (2, 64, 16, 144, 3, 1, 1),    # CARAFE4 encoder at a width the few-channel kernel takes (conv3_c16)
     (2, 9, 32, 36, 3, 1, 1),      # CARAFE encoder, odd size / N % 8 != 0
     (1, 12, 8, 24, 3, 1, 1),      # UNet DoubleConv-like
     (2, 6, 40, 16, 1, 1, 0),      # 1x1
@@ -1065,3 +1066,39 @@ def test_lepe_wgrad_deferred_reduce(reso, C, heads, sw, monkeypatch):
         res2[late] = [t.grad.clone() for t in ws + bs]
     for a, b in zip(res2[False], res2[True]):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("B,H,W", [(2, 64, 64), (1, 5, 128), (3, 7, 192)])
+def test_conv_c16_carafe4_encoder(B, H, W):
+    """The few-channel kernel of the CARAFE4 encoder Conv2d(16, 144, 3, 1, 1) (cswin:446; csu_conv2d_ex
+    cfg 21, chosen by the default dispatch for W % 64 == 0): forward vs float64 torch on the same bf16
+    operands, bitwise equal to the default choice; W % 64 != 0 is not eligible (CSU_E_ARG)."""
+    import ctypes
+    from csu import ops
+    from csu._lib import lib, CSU_BF16
+    d = dev()
+    gm = ops._conv_geom(B, H, W, 16, 144, 3, 3, 1, 1)
+    g = torch.Generator().manual_seed(B * 1000 + H + W)
+    x = torch.randn(B, H, W, 16, generator=g).bfloat16()
+    w = (torch.randn(144, 16, 3, 3, generator=g) / 12.0).bfloat16()
+    b = torch.randn(144, generator=g)
+    ref = torch.nn.functional.conv2d(x.double().permute(0, 3, 1, 2), w.double(), b.double(), 1, 1).permute(0, 2, 3, 1)
+    xd, bd = x.to(d), b.to(d)
+    w_ohwi = w.permute(0, 2, 3, 1).contiguous().to(d)
+    st = torch.cuda.current_stream().cuda_stream
+    outs = []
+    for cfg in (21, -1):
+        out = torch.full(ref.shape, float("nan"), dtype=torch.bfloat16, device=d)
+        e = lib().csu_conv2d_ex(0, ctypes.byref(gm), CSU_BF16, xd.data_ptr(), w_ohwi.data_ptr(), bd.data_ptr(),
+                                out.data_ptr(), cfg, st)
+        assert e == 0, lib().csu_last_error_string()
+        outs.append(out)
+    torch.cuda.synchronize()
+    err = float((outs[0].double().cpu() - ref).norm() / ref.norm())
+    assert err < 4e-3, err
+    assert torch.equal(outs[0], outs[1])
+    gm2 = ops._conv_geom(1, 8, 40, 16, 144, 3, 3, 1, 1)
+    out = torch.empty(1, 8, 40, 144, dtype=torch.bfloat16, device=d)
+    xs = torch.zeros(1, 8, 40, 16, dtype=torch.bfloat16, device=d)
+    assert lib().csu_conv2d_ex(0, ctypes.byref(gm2), CSU_BF16, xs.data_ptr(), w_ohwi.data_ptr(), bd.data_ptr(),
+                               out.data_ptr(), 21, st) != 0
