@@ -1264,6 +1264,104 @@ bool c16_ok(const IG& g) {   // the forward 3x3 / stride 1 / pad 1 conv of a 16-
            g.ax == 1 && g.by == -1 && g.bx == -1;
 }
 
+
+// ---- its input gradient: 144 -> 16 channels, dx[p][c] = sum_{tap, n} dy[p + 1 - tap][n] W[n][tap][c] ----
+// Same scheme with the roles of the channel counts swapped: the weights (IHWO [c][tap][n]) are the
+// register-resident A fragments (16 rows c x 9 taps x 160 n, n >= 144 zero: 45 k-steps of 16x16x32),
+// the 3 x 66-pixel halo of dy (144 channels, pixel stride 304 B = 19 16-B chunks, the 19th zero) is
+// DMA'd one segment ahead, and wave w's 16 pixels x 16 channels leave as one contiguous 512-B store
+// per wave instruction (lane (pixel, 4-channel group)).  One workgroup per CU (2 x 60 KB halo stages).
+__global__ __launch_bounds__(256, 1) void conv3_c16d(int B, int H, int W, const bf16* __restrict__ dy, const bf16* __restrict__ w_ihwo,
+                                                    bf16* __restrict__ dx) {
+    constexpr int N = 144, PS = 152;             // dy channels, halo pixel stride (bf16)
+    constexpr int NBLK = (3 * 66 * PS * 2 + 1023) / 1024;   // DMA blocks per stage (59)
+    constexpr int STAGE = NBLK * 512;            // bf16 per stage
+    constexpr int NI = (NBLK + 3) / 4;           // per wave
+    __shared__ __attribute__((aligned(1024))) bf16 ring[2 * STAGE];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int spr = W / 64;
+    const long items = (long)B * H * spr;
+    const long x = blockIdx.x % kXcds, kk = blockIdx.x / kXcds, nloc = gridDim.x / kXcds;
+    const long q = items / kXcds, rem = items % kXcds;
+    const long lo = x < rem ? x * (q + 1) : rem * (q + 1) + (x - rem) * q;
+    const long cnt = q + (x < rem ? 1 : 0);
+    const int my = kk < cnt ? (int)((cnt - kk + nloc - 1) / nloc) : 0;
+    if (my == 0) return;
+    const int l16 = lane & 15, kg = lane >> 4;
+    // A fragments: lane (c = l16, kg) of k-step (tap, chunk j) = Wi[c][tap][32 j + 8 kg .. + 7]
+    bf16x8 aw[9][5];
+    {
+        const __amdgpu_buffer_rsrc_t rw = buf_rsrc(w_ihwo, 16L * 9 * N * 2);
+#pragma unroll
+        for (int t = 0; t < 9; ++t)
+#pragma unroll
+            for (int j = 0; j < 5; ++j) {
+                const int n = 32 * j + 8 * kg;
+                const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rw, n < N ? (unsigned)(((l16 * 9 + t) * N + n) * 2) : kOOB, 0, 0);
+                __builtin_memcpy(&aw[t][j], &v, 16);
+            }
+    }
+    const i32x4 rs = rsrc4(dy, (long)B * H * W * N * 2);
+    auto issue = [&](int u) {   // dy rows oy - 1 .. oy + 1, pixels ox0 - 1 .. ox0 + 64 of item u
+        const long it = lo + kk + (long)(u < my ? u : my - 1) * nloc;
+        const bool iv = u < my;
+        const long t1 = it / spr;
+        const int ox0 = (int)(it - t1 * spr) * 64;
+        const int b = (int)(t1 / H), oy = (int)(t1 - (long)b * H);
+        bf16* stg = ring + (u & 1) * STAGE;
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+            const int j = wave * NI + i;
+            if (j < NBLK) {
+                const int byte = 1024 * j + 16 * lane;
+                const int P = byte / (2 * PS), chunk = (byte - P * 2 * PS) >> 4;
+                const int ky = P / 66, px = P - 66 * ky;
+                const int iy = oy + ky - 1, ix = ox0 - 1 + px;
+                const bool ok = iv && P < 3 * 66 && chunk < N / 8 && iy >= 0 && iy < H && ix >= 0 && ix < W;
+                const unsigned off = ok ? (unsigned)(((((long)b * H + iy) * W + ix) * N + 8 * chunk) * 2) : kOOB;
+                dma1_u(rs, off, 0u, stg + j * 512);
+            }
+        }
+    };
+    const __amdgpu_buffer_rsrc_t rso = buf_rsrc(dx, (long)B * H * W * 16 * 2);
+    issue(0);
+    for (int u = 0; u < my; ++u) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (u == 0) vmwait<0>(); else vmwait<1>();   // item u landed (younger: item u-1's store)
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        issue(u + 1);
+        const bf16* st = ring + (u & 1) * STAGE;
+        f32x4 acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};   // two independent chains
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+            const int ky = t / 3, kx = t % 3;
+            const bf16* row = st + ((2 - ky) * 66 + 16 * wave + l16 + 2 - kx) * PS;
+#pragma unroll
+            for (int j = 0; j < 5; ++j) {
+                const int n = 32 * j + 8 * kg;
+                const bf16x8 bx = *reinterpret_cast<const bf16x8*>(row + (n < N ? n : n - 16));   // n >= 144: zero weights
+                acc[(t * 5 + j) & 1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw[t][j], bx, acc[(t * 5 + j) & 1], 0, 0, 0);
+            }
+        }
+        // acc[i] = dx[pixel 16 wave + l16][c = 4 kg + i]
+        const long it = lo + kk + (long)u * nloc;
+        const long t1 = it / spr;
+        const int ox0 = (int)(it - t1 * spr) * 64;
+        const long pix = t1 * W + ox0 + 16 * wave + l16;
+        const float v[4] = {acc[0][0] + acc[1][0], acc[0][1] + acc[1][1], acc[0][2] + acc[1][2], acc[0][3] + acc[1][3]};
+        buf_st4bf(rso, (unsigned)((pix * 16 + 4 * kg) * 2), v);
+    }
+    vmwait<0>();
+}
+
+bool c16d_ok(const IG& g) {   // the input gradient (flipped taps) of the 16 -> 144 3x3 stride-1 conv
+    return g.Cs == 144 && g.Ncols == 16 && g.nty == 3 && g.ntx == 3 && g.csplit == 0 && g.nsplit == 0 && g.OHo == g.Hs &&
+           g.OWo == g.Ws && g.Ws % 64 == 0 && g.RH == g.Hs && g.RW == g.Ws && g.sty == -1 && g.stx == -1 && g.by == 1 &&
+           g.bx == 1 && g.wty == 1 && g.wtx == 1;
+}
+
 constexpr int kHalo64Cfg = 20;   // csu_conv2d_ex cfg selecting conv3_halo64
 constexpr int kC16Cfg = 21;      // csu_conv2d_ex cfg selecting conv3_c16
 bool halo64_ok(const IG& g, bool flip) {   // the forward conv (flip: its input gradient) this kernel takes
@@ -1355,6 +1453,10 @@ int launch_ig(const IG* gv, int n, const void* src, const void* w, const float* 
     if ((cfg < 0 || cfg == kC16Cfg) && n == 1 && c16_ok(g)) {   // 16 -> 144 channel 3x3 conv (CARAFE4 encoder)
         conv3_c16<144><<<dim3(2 * id_cus()), 256, 0, st>>>(g.B, g.Hs, g.Ws, (const bf16*)src, (const bf16*)w, bias, (bf16*)out);
         return check_launch("conv2d (c16)");
+    }
+    if ((cfg < 0 || cfg == kC16Cfg) && n == 1 && c16d_ok(g)) {   // its input gradient (144 -> 16)
+        conv3_c16d<<<dim3(id_cus()), 256, 0, st>>>(g.B, g.Hs, g.Ws, (const bf16*)src, (const bf16*)w, (bf16*)out);
+        return check_launch("conv2d (c16d)");
     }
     if (cfg == kC16Cfg) return fail(CSU_E_ARG, "conv2d: c16 configuration not eligible");
     if (cfg > 0) {   // forced v3 configuration: every phase must be eligible for it

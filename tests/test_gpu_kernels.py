@@ -1070,9 +1070,10 @@ def test_lepe_wgrad_deferred_reduce(reso, C, heads, sw, monkeypatch):
 
 @pytest.mark.parametrize("B,H,W", [(2, 64, 64), (1, 5, 128), (3, 7, 192)])
 def test_conv_c16_carafe4_encoder(B, H, W):
-    """The few-channel kernel of the CARAFE4 encoder Conv2d(16, 144, 3, 1, 1) (cswin:446; csu_conv2d_ex
-    cfg 21, chosen by the default dispatch for W % 64 == 0): forward vs float64 torch on the same bf16
-    operands, bitwise equal to the default choice; W % 64 != 0 is not eligible (CSU_E_ARG)."""
+    """The few-channel kernels of the CARAFE4 encoder Conv2d(16, 144, 3, 1, 1) (cswin:446; csu_conv2d_ex
+    cfg 21, chosen by the default dispatch for W % 64 == 0): forward (conv3_c16) and input gradient
+    (conv3_c16d) vs float64 torch on the same bf16 operands, bitwise equal to the default choice;
+    W % 64 != 0 is not eligible (CSU_E_ARG)."""
     import ctypes
     from csu import ops
     from csu._lib import lib, CSU_BF16
@@ -1095,6 +1096,22 @@ def test_conv_c16_carafe4_encoder(B, H, W):
         outs.append(out)
     torch.cuda.synchronize()
     err = float((outs[0].double().cpu() - ref).norm() / ref.norm())
+    assert err < 4e-3, err
+    assert torch.equal(outs[0], outs[1])
+    # the input gradient (144 -> 16, conv3_c16d)
+    dy = torch.randn(B, H, W, 144, generator=g).bfloat16()
+    ref_d = torch.nn.functional.conv_transpose2d(dy.double().permute(0, 3, 1, 2), w.double(), None, 1, 1).permute(0, 2, 3, 1)
+    w_ihwo = w.permute(1, 2, 3, 0).contiguous().to(d)
+    dyd = dy.to(d)
+    outs = []
+    for cfg in (21, -1):
+        out = torch.full(ref_d.shape, float("nan"), dtype=torch.bfloat16, device=d)
+        e = lib().csu_conv2d_ex(1, ctypes.byref(gm), CSU_BF16, dyd.data_ptr(), w_ihwo.data_ptr(), None, out.data_ptr(),
+                                cfg, st)
+        assert e == 0, lib().csu_last_error_string()
+        outs.append(out)
+    torch.cuda.synchronize()
+    err = float((outs[0].double().cpu() - ref_d).norm() / ref_d.norm())
     assert err < 4e-3, err
     assert torch.equal(outs[0], outs[1])
     gm2 = ops._conv_geom(1, 8, 40, 16, 144, 3, 3, 1, 1)
