@@ -1115,6 +1115,172 @@ int fp8_bwd_launch(long M, const void* x, const void* dy, const void* w1, const 
     return check_launch("mlp_fp8_bwd");
 }
 
+
+// ================================================================================================
+// Deep-ring forward (bf16): the per-panel kernel above keeps ONE 64-KB weight chunk in flight, and
+// its step time is the DMA time of that chunk (~25 GB/s per CU: 2.5 us per chunk at C = 256, 16
+// chunks); the LDS-DMA path delivers several times that with more bytes in flight
+// (MI355X_MICROARCH.md, ring-gemm).  Here chunks are 32 hidden features (W1 [32][C] + W2 [C][32]
+// = 128 C bytes) in an RS-stage ring with RS - 1 chunks in flight, and the waves split the panel by
+// TOKENS: wave w owns tokens 16 w .. 16 w + 15 with every hidden feature of the chunk and every
+// output feature (v_mfma_f32_16x16x32_bf16), so nothing is exchanged between waves.
+//   GEMM1  h[32 hid][16 tok] = W1c x^T   (two 16-row tiles, k = C in steps of 32)
+//   GELU   lane (tok, kg) holds hidden 4 kg + i of both tiles -> the 8 k-values of GEMM2's B
+//          operand in the permuted order (4 kg + i, 16 + 4 kg + i); W2 is read in the same order
+//   GEMM2  y[C][16 tok] += W2c g        (C / 16 tiles, one k-step of 32)
+// Every step issues exactly one chunk's DMA (past the last chunk it re-fetches the last one into the
+// free stage), so the wait for chunk j is a fixed count.
+template <int C, int RS, bool DROP>
+__global__ __launch_bounds__(MT) void mlp_fwd_deep(long M, const bf16* __restrict__ X, const bf16* __restrict__ W1,
+                                                   const float* __restrict__ b1, const bf16* __restrict__ W2,
+                                                   const float* __restrict__ b2, const float* __restrict__ res,
+                                                   float* __restrict__ out, MlpDrop dd, long rpi) {
+    constexpr int HD = 32;                 // hidden features per chunk
+    constexpr int NCH = 4 * C / HD;
+    constexpr int KS = C / 32;             // GEMM1 k-steps
+    constexpr int OT = C / 16;             // output tiles
+    constexpr int IMG1 = HD * C;           // bf16 of a W1 chunk image [32][C]
+    constexpr int IMG2 = C * HD;           // and of a W2 chunk image [C][32]
+    constexpr int STAGE = IMG1 + IMG2;
+    using D1 = Dma<HD, 2 * C>;
+    using D2 = Dma<C, 2 * HD>;
+    constexpr int ND = D1::NW + D2::NW;    // DMA instructions per wave per chunk
+    __shared__ __attribute__((aligned(1024))) bf16 ring[RS * STAGE];
+    __shared__ __attribute__((aligned(16))) float b1s[4 * C];
+
+    const long m0 = (long)blockIdx.x * BM;
+    const long rows = M - m0;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int l16 = lane & 15, kg = lane >> 4;
+    const int tok = 16 * wave + l16;
+    const bool ok = tok < rows;
+    const int j0 = kRot && rpi > 0 && rpi % BM == 0 ? (int)(((m0 % rpi) / BM) & (NCH - 1)) : 0;   // see mlp_fwd_kernel
+    auto chk = [&](int j) { return (j + j0) & (NCH - 1); };
+    for (int i = threadIdx.x; i < 4 * C; i += MT) b1s[i] = b1[i];
+    // x as GEMM1 B fragments: lane (tok, kg) of k-step s = x[tok][32 s + 8 kg .. + 7]
+    bf16x8 xf[KS];
+    {
+        const auto rs = buf_rsrc(X + m0 * C, rows * C * 2);
+#pragma unroll
+        for (int s2 = 0; s2 < KS; ++s2) {
+            const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, ok ? (unsigned)(tok * C + 32 * s2 + 8 * kg) * 2 : kOOB, 0, 0);
+            __builtin_memcpy(&xf[s2], &v, 16);
+        }
+    }
+    D1 d1;
+    D2 d2;
+    d1.init(C, wave, lane);
+    d2.init(4 * C, wave, lane);
+    const i32x4 rs_w1 = rsrc4(W1, 4L * C * C * 2);
+    const i32x4 rs_w2 = rsrc4(W2, 4L * C * C * 2);
+    auto issue = [&](int j) {   // chunk min(j, NCH - 1) into stage j % RS
+        const int jc = chk(j < NCH ? j : NCH - 1);
+        bf16* st = ring + (j % RS) * STAGE;
+        dma<D1::NW>(rs_w1, d1.v, (unsigned)jc * HD * C * 2, st, wave);
+        dma<D2::NW>(rs_w2, d2.v, (unsigned)jc * HD * 2, st + IMG1, wave);
+    };
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int j = 0; j < RS - 1; ++j) issue(j);
+    f32x4 acc[OT];
+#pragma unroll
+    for (int i = 0; i < OT; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const long mg = m0 + tok;
+    DropoutRng Rh;
+    if constexpr (DROP) Rh = load_rng(dd.rng, dd.site_h, dd.p);
+    __syncthreads();   // b1s
+    for (int j = 0; j < NCH; ++j) {
+        vmwait<(RS - 2) * ND>();          // chunk j landed (younger: chunks j + 1 .. j + RS - 2)
+        lds_sync();                       // ... for every wave; stage (j - 1) % RS is free
+        issue(j + RS - 1);
+        const bf16* w1c = ring + (j % RS) * STAGE;
+        const bf16* w2c = w1c + IMG1;
+        const int jc = chk(j);
+        f32x4 h0 = {0.f, 0.f, 0.f, 0.f}, h1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s2 = 0; s2 < KS; ++s2) {
+            const bf16x8 a0 = frag(w1c, moff<2 * C>(l16, 32 * s2 + 8 * kg));
+            const bf16x8 a1 = frag(w1c, moff<2 * C>(16 + l16, 32 * s2 + 8 * kg));
+            h0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, xf[s2], h0, 0, 0, 0);
+            h1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, xf[s2], h1, 0, 0, 0);
+        }
+        // GELU: hidden jc * 32 + 4 kg + i (tile 0) and + 16 (tile 1)
+        const f32x4 bv0 = *reinterpret_cast<const f32x4*>(b1s + jc * HD + 4 * kg);
+        const f32x4 bv1 = *reinterpret_cast<const f32x4*>(b1s + jc * HD + 16 + 4 * kg);
+        float gv[8];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            gv[i] = gelu_fast(h0[i] + bv0[i]);
+            gv[4 + i] = gelu_fast(h1[i] + bv1[i]);
+        }
+        if constexpr (DROP) {
+            if (dd.p > 0.f) {
+                const uint64_t e0 = (uint64_t)mg * 4 * C + jc * HD + 4 * kg;   // 4-aligned; its 8-group
+                const unsigned m0b = keep8(Rh, e0 >> 3) >> (e0 & 7);
+                const unsigned m1b = keep8(Rh, (e0 + 16) >> 3) >> ((e0 + 16) & 7);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    gv[i] = ((m0b >> i) & 1u) ? gv[i] * Rh.scale : 0.f;
+                    gv[4 + i] = ((m1b >> i) & 1u) ? gv[4 + i] * Rh.scale : 0.f;
+                }
+            }
+        }
+        bf16x8 gb;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) gb[i] = (bf16)gv[i];
+#pragma unroll
+        for (int ot = 0; ot < OT; ++ot) {   // A: W2[out][hidden 4 kg + i, 16 + 4 kg + i] (the same k order)
+            const bf16x4 lo = *reinterpret_cast<const bf16x4*>(w2c + moff<2 * HD>(16 * ot + l16, 4 * kg));
+            const bf16x4 hi = *reinterpret_cast<const bf16x4*>(w2c + moff<2 * HD>(16 * ot + l16, 16 + 4 * kg));
+            const bf16x8 a = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+            acc[ot] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, gb, acc[ot], 0, 0, 0);
+        }
+    }
+    // epilogue: acc[ot][i] = y[tok][16 ot + 4 kg + i]
+    const auto rs_res = buf_rsrc(res + m0 * C, rows * C * 4);
+    const auto rs_out = buf_rsrc(out + m0 * C, rows * C * 4);
+    float sdp = 1.f;
+    DropoutRng R;
+    if constexpr (DROP) {
+        R = load_rng(dd.rng, dd.site_o, dd.p);
+        if (dd.row_scale) sdp = dd.row_scale[mg / dd.rps];
+    }
+#pragma unroll
+    for (int ot = 0; ot < OT; ++ot) {
+        const int f = 16 * ot + 4 * kg;
+        const unsigned off = ok ? (unsigned)(tok * C + f) * 4 : kOOB;
+        float rv[4], bv[4], v[4];
+        buf_ld4(rs_res, off, rv);
+        load4(b2 + f, bv);
+        unsigned km = 0xfu;
+        if constexpr (DROP) if (dd.p > 0.f) {
+            const uint64_t e = (uint64_t)mg * C + f;
+            km = keep8(R, e >> 3) >> (e & 7);
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            float z = acc[ot][e] + bv[e];
+            if constexpr (DROP) z *= ((km >> e) & 1u) ? sdp * R.scale : 0.f;
+            v[e] = z + rv[e];
+        }
+        buf_st4(rs_out, off, v);
+    }
+    vmwait<0>();   // the re-fetch DMAs drained before the workgroup's LDS is released
+}
+
+template <int C, int RS>
+int fwd_deep_launch(long M, const void* x, const void* w1, const float* b1, const void* w2, const float* b2, const float* res,
+                    float* out, const MlpDrop* d, long rpi, hipStream_t st) {
+    const dim3 grid((unsigned)((M + BM - 1) / BM));
+    if (d)
+        mlp_fwd_deep<C, RS, true><<<grid, MT, 0, st>>>(M, (const bf16*)x, (const bf16*)w1, b1, (const bf16*)w2, b2, res, out, *d, rpi);
+    else
+        mlp_fwd_deep<C, RS, false><<<grid, MT, 0, st>>>(M, (const bf16*)x, (const bf16*)w1, b1, (const bf16*)w2, b2, res, out,
+                                                        MlpDrop{}, rpi);
+    return check_launch("mlp_fwd (deep)");
+}
+
 }  // namespace
 }  // namespace csu
 
@@ -1215,5 +1381,34 @@ extern "C" int csu_mlp_fp8_bwd(long M, int C, const void* x, const void* dy, con
         case 128: return fp8_bwd_launch<128>(M, x, dy, w1q, sw1, b1, w2t, sw2, w1tp, dh, g, dx, dp, rpi, st);
         case 256: return fp8_bwd_launch<256>(M, x, dy, w1q, sw1, b1, w2t, sw2, w1tp, dh, g, dx, dp, rpi, st);
         default: return fail(CSU_E_UNSUPPORTED, "mlp_fp8_bwd: C must be 64, 128 or 256");
+    }
+}
+
+// explicit forward variant (tests, tools/mlp8_probe.py): cfg 0 = the per-panel kernel, 1 = the deep ring
+extern "C" int csu_mlp_fwd_ex(long M, int C, const void* x, const void* w1, const float* b1, const void* w2, const float* b2,
+                              const float* res, float* out, const csu_mlp_dropout* d, int cfg, void* stream) {
+    if (cfg == 0) return csu_mlp_fwd_dp(M, C, x, w1, b1, w2, b2, res, out, d, stream);
+    if (cfg != 1 && cfg != 2) return fail(CSU_E_ARG, "mlp_fwd_ex: cfg 0, 1 or 2");
+    if (M < 1 || !x || !w1 || !b1 || !w2 || !b2 || !res || !out) return fail(CSU_E_ARG, "mlp_fwd: bad arguments");
+    if (M * 4L * C * 2 > 0x7fffffffL) return fail(CSU_E_ARG, "mlp_fwd: tensor exceeds 2 GB buffer range");
+    MlpDrop md{};
+    const int e = mlp_drop_of(d, md);
+    if (e < 0) return e;
+    const MlpDrop* dp = d && e == 0 ? &md : nullptr;
+    const long rpi = d ? (long)d->rows_per_sample : 0;
+    const hipStream_t st = as_stream(stream);
+    if (cfg == 2) {   // deeper rings
+        switch (C) {
+            case 64: return fwd_deep_launch<64, 8>(M, x, w1, b1, w2, b2, res, out, dp, rpi, st);
+            case 128: return fwd_deep_launch<128, 6>(M, x, w1, b1, w2, b2, res, out, dp, rpi, st);
+            case 256: return fwd_deep_launch<256, 3>(M, x, w1, b1, w2, b2, res, out, dp, rpi, st);
+            default: return fail(CSU_E_ARG, "mlp_fwd: C must be 64, 128 or 256");
+        }
+    }
+    switch (C) {
+        case 64: return fwd_deep_launch<64, 6>(M, x, w1, b1, w2, b2, res, out, dp, rpi, st);
+        case 128: return fwd_deep_launch<128, 4>(M, x, w1, b1, w2, b2, res, out, dp, rpi, st);
+        case 256: return fwd_deep_launch<256, 4>(M, x, w1, b1, w2, b2, res, out, dp, rpi, st);
+        default: return fail(CSU_E_ARG, "mlp_fwd: C must be 64, 128 or 256");
     }
 }

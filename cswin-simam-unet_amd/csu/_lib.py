@@ -146,6 +146,8 @@ _SIGS = {
     "csu_e4m3_layout_batch": (ctypes.c_int, [c_void_p, ctypes.c_int, ctypes.c_long, c_void_p]),
     "csu_quant_e4m3_shadow_batch": (ctypes.c_int, [c_void_p, ctypes.c_int, ctypes.c_long, c_void_p]),
     "csu_mlp_fp8_supported": (ctypes.c_int, [ctypes.c_int]),
+    "csu_mlp_fwd_ex": (ctypes.c_int, [ctypes.c_long, ctypes.c_int] + [c_void_p] * 7 + [ctypes.POINTER(MlpDropout), ctypes.c_int,
+                                                                                       c_void_p]),
     "csu_mlp_fp8_fwd": (ctypes.c_int, [ctypes.c_long, ctypes.c_int] + [c_void_p] * 9 + [ctypes.POINTER(MlpDropout), c_void_p]),
     "csu_mlp_fp8_bwd": (ctypes.c_int, [ctypes.c_long, ctypes.c_int] + [c_void_p] * 11 + [ctypes.POINTER(MlpDropout),
                                                                                          c_void_p]),

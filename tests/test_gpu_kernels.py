@@ -1119,3 +1119,50 @@ def test_conv_c16_carafe4_encoder(B, H, W):
     xs = torch.zeros(1, 8, 40, 16, dtype=torch.bfloat16, device=d)
     assert lib().csu_conv2d_ex(0, ctypes.byref(gm2), CSU_BF16, xs.data_ptr(), w_ohwi.data_ptr(), bd.data_ptr(),
                                out.data_ptr(), 21, st) != 0
+
+
+@pytest.mark.parametrize("C,M", [(64, 4096), (128, 1000), (256, 4160), (256, 100)])
+@pytest.mark.parametrize("cfg", [1, 2])
+def test_mlp_fwd_deep_ring_vs_fp64(C, M, cfg):
+    """csu_mlp_fwd_ex cfg 1 / 2 (the deep-ring forward: 32-hidden weight chunks, waves split by tokens)
+    vs the fp64 Mlp + residual, without and with hidden / output dropout + DropPath (same masks as
+    the oracle composition); and it agrees with the per-panel kernel to bf16 rounding."""
+    import ctypes
+    from csu import rng
+    from csu._lib import check, lib, ptr, stream_ptr
+    from csu.ops import MlpDrop
+    d = dev()
+    torch.manual_seed(C + M + cfg)
+    x = torch.randn(M, C, device=d).bfloat16()
+    w1 = (torch.randn(4 * C, C, device=d) * C ** -0.5).bfloat16()
+    w2 = (torch.randn(C, 4 * C, device=d) * (4 * C) ** -0.5).bfloat16()
+    b1, b2 = torch.randn(4 * C, device=d) * 0.1, torch.randn(C, device=d) * 0.1
+    res = torch.randn(M, C, device=d)
+    st = stream_ptr(d)
+    X, W1, W2, B1, B2, R = (t.double().cpu() for t in (x, w1, w2, b1, b2, res))
+    F = torch.nn.functional
+    for drop in (False, True):
+        if drop:
+            snap = torch.tensor([5, 2], dtype=torch.int64, device=d)
+            rps = max(1, M // 3)
+            rs = rng.droppath_scale(snap, 30, 0.3, -(-M // rps))
+            md = MlpDrop(snap, 21, 22, 0.3, rs, rps).c_struct()
+            mh = rng.dropout_mask(snap, 21, 0.3, M * 4 * C).view(M, 4 * C).double().cpu() / 0.7
+            mo = rng.dropout_mask(snap, 22, 0.3, M * C).view(M, C).double().cpu() / 0.7
+            outm = mo * rs.double().cpu()[torch.arange(M) // rps].view(M, 1)
+        else:
+            md = MlpDrop(None, 0, 0, 0.0).c_struct()
+            md.rows_per_sample = M
+            mh, outm = 1.0, 1.0
+        ys = []
+        for c in (cfg, 0):
+            y = torch.empty(M, C, device=d)
+            check(lib().csu_mlp_fwd_ex(M, C, ptr(x), ptr(w1), ptr(b1), ptr(w2), ptr(b2), ptr(res), ptr(y),
+                                       ctypes.byref(md), c, st), "mlp_fwd_ex")
+            ys.append(y)
+        torch.cuda.synchronize()
+        ref = R + outm * ((F.gelu(X @ W1.T + B1) * mh) @ W2.T + B2)
+        err = float((ys[0].double().cpu() - ref).norm() / (ref - R).norm())
+        assert err < 1e-2, (drop, err)
+        d01 = float((ys[0] - ys[1]).double().norm() / (ys[1] - res).double().norm())
+        assert d01 < 1e-2, (drop, d01)
