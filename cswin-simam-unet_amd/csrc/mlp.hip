@@ -1281,6 +1281,179 @@ int fwd_deep_launch(long M, const void* x, const void* w1, const float* b1, cons
     return check_launch("mlp_fwd (deep)");
 }
 
+
+// 16x16x32 operand fragments transposed out of a moff<RB> image whose ROWS are k and COLUMNS are i
+// (ds_read_b64_tr_b16: lane 4q+p of a 16-lane group addresses row q, columns 4p..4p+3 and receives
+// column l of the 4 rows):  A[i = c0 + (lane & 15)][k], k = k0 + 8 kg + 0..7 (natural order) ...
+template <int RB>
+__device__ __forceinline__ bf16x8 tr16n(const bf16* img, int c0, int k0, int lane) {
+    const int kg = lane >> 4, l = lane & 15, q = l >> 2, p = l & 3;
+    return cat8(tr4(img + moff<RB>(k0 + 8 * kg + q, c0 + 4 * p)), tr4(img + moff<RB>(k0 + 8 * kg + 4 + q, c0 + 4 * p)));
+}
+// ... or k = k0 + 4 kg + 0..3, k0 + 16 + 4 kg + 0..3 (the deep-ring kernels' permuted hidden order)
+template <int RB>
+__device__ __forceinline__ bf16x8 tr16p(const bf16* img, int c0, int k0, int lane) {
+    const int kg = lane >> 4, l = lane & 15, q = l >> 2, p = l & 3;
+    return cat8(tr4(img + moff<RB>(k0 + 4 * kg + q, c0 + 4 * p)), tr4(img + moff<RB>(k0 + 16 + 4 * kg + q, c0 + 4 * p)));
+}
+
+template <int N> __device__ __forceinline__ void vmwait_le(int c) {   // s_waitcnt vmcnt(c), c in [0, N] (c multiple of 4)
+    if constexpr (N >= 4) {
+        if (c >= N) { vmwait<N>(); return; }
+        vmwait_le<N - 4>(c);
+    } else {
+        vmwait<0>();
+    }
+}
+
+// Deep-ring backward (bf16): the forward's chunking and token split.  Per chunk j (32 hidden):
+//   GEMM1  h  = W1c x^T                      (A: W1 image rows, as the forward)
+//   GEMM3  dg = W2c^T dY^T                   (A: transposed reads of the W2 image [C][32], k = C natural)
+//   dh = dg * gelu'(h) (* hidden mask), g = gelu(h) (* mask): stored (bf16) for the weight gradients
+//   GEMM4  dx += W1c^T dh                    (A: transposed reads of the W1 image, k = the chunk's hidden
+//                                             features in the permuted order the accumulators give)
+// The wait for chunk j counts its younger DMAs and this wave's 4 stores per step since.
+template <int C, int RS, bool DROP>
+__global__ __launch_bounds__(MT) void mlp_bwd_deep(long M, const bf16* __restrict__ X, const bf16* __restrict__ dY,
+                                                   const bf16* __restrict__ W1, const float* __restrict__ b1,
+                                                   const bf16* __restrict__ W2, bf16* __restrict__ dH, bf16* __restrict__ G,
+                                                   bf16* __restrict__ dX, MlpDrop dd, long rpi) {
+    constexpr int HD = 32;
+    constexpr int NCH = 4 * C / HD;
+    constexpr int KS = C / 32;
+    constexpr int OT = C / 16;
+    constexpr int IMG1 = HD * C;
+    constexpr int IMG2 = C * HD;
+    constexpr int STAGE = IMG1 + IMG2;
+    using D1 = Dma<HD, 2 * C>;
+    using D2 = Dma<C, 2 * HD>;
+    constexpr int ND = D1::NW + D2::NW;
+    constexpr int NS = 4;                  // buffer stores per lane per chunk (G, dH: 2 x 8 B each)
+    __shared__ __attribute__((aligned(1024))) bf16 ring[RS * STAGE];
+    __shared__ __attribute__((aligned(16))) float b1s[4 * C];
+
+    const long m0 = (long)blockIdx.x * BM;
+    const long rows = M - m0;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int l16 = lane & 15, kg = lane >> 4;
+    const int tok = 16 * wave + l16;
+    const bool ok = tok < rows;
+    const int j0 = kRot && rpi > 0 && rpi % BM == 0 ? (int)(((m0 % rpi) / BM) & (NCH - 1)) : 0;
+    auto chk = [&](int j) { return (j + j0) & (NCH - 1); };
+    for (int i = threadIdx.x; i < 4 * C; i += MT) b1s[i] = b1[i];
+    bf16x8 xf[KS], yf[KS];
+    {
+        const auto rx = buf_rsrc(X + m0 * C, rows * C * 2);
+        const auto ry = buf_rsrc(dY + m0 * C, rows * C * 2);
+#pragma unroll
+        for (int s2 = 0; s2 < KS; ++s2) {
+            const unsigned o = ok ? (unsigned)(tok * C + 32 * s2 + 8 * kg) * 2 : kOOB;
+            const u32x4 a = __builtin_amdgcn_raw_buffer_load_b128(rx, o, 0, 0);
+            const u32x4 b = __builtin_amdgcn_raw_buffer_load_b128(ry, o, 0, 0);
+            __builtin_memcpy(&xf[s2], &a, 16);
+            __builtin_memcpy(&yf[s2], &b, 16);
+        }
+    }
+    D1 d1;
+    D2 d2;
+    d1.init(C, wave, lane);
+    d2.init(4 * C, wave, lane);
+    const i32x4 rs_w1 = rsrc4(W1, 4L * C * C * 2);
+    const i32x4 rs_w2 = rsrc4(W2, 4L * C * C * 2);
+    const auto rs_dh = buf_rsrc(dH + m0 * 4 * C, rows * 4 * C * 2);
+    const auto rs_g = buf_rsrc(G + m0 * 4 * C, rows * 4 * C * 2);
+    auto issue = [&](int j) {
+        const int jc = chk(j < NCH ? j : NCH - 1);
+        bf16* st = ring + (j % RS) * STAGE;
+        dma<D1::NW>(rs_w1, d1.v, (unsigned)jc * HD * C * 2, st, wave);
+        dma<D2::NW>(rs_w2, d2.v, (unsigned)jc * HD * 2, st + IMG1, wave);
+    };
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int j = 0; j < RS - 1; ++j) issue(j);
+    f32x4 acc[OT];
+#pragma unroll
+    for (int i = 0; i < OT; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const long mg = m0 + tok;
+    DropoutRng Rh;
+    if constexpr (DROP) Rh = load_rng(dd.rng, dd.site_h, dd.p);
+    __syncthreads();
+    for (int j = 0; j < NCH; ++j) {
+        vmwait_le<(RS - 2) * ND + NS * (RS - 1)>((RS - 2) * ND + NS * (j < RS - 1 ? j : RS - 1));
+        lds_sync();
+        issue(j + RS - 1);
+        const bf16* w1c = ring + (j % RS) * STAGE;
+        const bf16* w2c = w1c + IMG1;
+        const int jc = chk(j);
+        f32x4 h[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}}, dg[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+        for (int s2 = 0; s2 < KS; ++s2)
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                h[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(frag(w1c, moff<2 * C>(16 * t + l16, 32 * s2 + 8 * kg)), xf[s2], h[t],
+                                                              0, 0, 0);
+                dg[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr16n<2 * HD>(w2c, 16 * t, 32 * s2, lane), yf[s2], dg[t], 0, 0, 0);
+            }
+        // lane (tok, kg): hidden jc * 32 + 16 t + 4 kg + i
+        float gv[8], dv[8];
+        unsigned km[2] = {0xfu, 0xfu};
+        if constexpr (DROP) if (dd.p > 0.f) {
+            const uint64_t e0 = (uint64_t)mg * 4 * C + jc * HD + 4 * kg;
+            km[0] = keep8(Rh, e0 >> 3) >> (e0 & 7);
+            km[1] = keep8(Rh, (e0 + 16) >> 3) >> ((e0 + 16) & 7);
+        }
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            const f32x4 bv = *reinterpret_cast<const f32x4*>(b1s + jc * HD + 16 * t + 4 * kg);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                float g, dgl;
+                gelu_pair_fast(h[t][i] + bv[i], g, dgl);
+                if constexpr (DROP) {
+                    const float ms = ((km[t] >> i) & 1u) ? Rh.scale : 0.f;
+                    g *= ms;
+                    dgl *= ms;
+                }
+                gv[4 * t + i] = g;
+                dv[4 * t + i] = dg[t][i] * dgl;
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            const unsigned o = ok ? (unsigned)(tok * 4 * C + jc * HD + 16 * t + 4 * kg) * 2 : kOOB;
+            buf_st4bf(rs_g, o, gv + 4 * t);
+            buf_st4bf(rs_dh, o, dv + 4 * t);
+        }
+        bf16x8 db;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) db[i] = (bf16)dv[i];
+#pragma unroll
+        for (int ot = 0; ot < OT; ++ot)
+            acc[ot] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr16p<2 * C>(w1c, 16 * ot, 0, lane), db, acc[ot], 0, 0, 0);
+    }
+    const auto rs_dx = buf_rsrc(dX + m0 * C, rows * C * 2);
+#pragma unroll
+    for (int ot = 0; ot < OT; ++ot) {
+        float v[4] = {acc[ot][0], acc[ot][1], acc[ot][2], acc[ot][3]};
+        buf_st4bf(rs_dx, ok ? (unsigned)(tok * C + 16 * ot + 4 * kg) * 2 : kOOB, v);
+    }
+    vmwait<0>();
+}
+
+template <int C, int RS>
+int bwd_deep_launch(long M, const void* x, const void* dy, const void* w1, const float* b1, const void* w2, void* dh, void* g,
+                    void* dx, const MlpDrop* d, long rpi, hipStream_t st) {
+    const dim3 grid((unsigned)((M + BM - 1) / BM));
+    if (d)
+        mlp_bwd_deep<C, RS, true><<<grid, MT, 0, st>>>(M, (const bf16*)x, (const bf16*)dy, (const bf16*)w1, b1, (const bf16*)w2,
+                                                       (bf16*)dh, (bf16*)g, (bf16*)dx, *d, rpi);
+    else
+        mlp_bwd_deep<C, RS, false><<<grid, MT, 0, st>>>(M, (const bf16*)x, (const bf16*)dy, (const bf16*)w1, b1, (const bf16*)w2,
+                                                        (bf16*)dh, (bf16*)g, (bf16*)dx, MlpDrop{}, rpi);
+    return check_launch("mlp_bwd (deep)");
+}
+
 }  // namespace
 }  // namespace csu
 
@@ -1410,5 +1583,34 @@ extern "C" int csu_mlp_fwd_ex(long M, int C, const void* x, const void* w1, cons
         case 128: return fwd_deep_launch<128, 4>(M, x, w1, b1, w2, b2, res, out, dp, rpi, st);
         case 256: return fwd_deep_launch<256, 4>(M, x, w1, b1, w2, b2, res, out, dp, rpi, st);
         default: return fail(CSU_E_ARG, "mlp_fwd: C must be 64, 128 or 256");
+    }
+}
+
+// explicit backward variant: cfg 0 = the per-panel / persistent kernels (csu_mlp_bwd_dp), 1 / 2 = the deep ring
+extern "C" int csu_mlp_bwd_ex(long M, int C, const void* x, const void* dy, const void* w1, const float* b1, const void* w2,
+                              void* dh, void* g, void* dx, const csu_mlp_dropout* d, int cfg, void* stream) {
+    if (cfg == 0) return csu_mlp_bwd_dp(M, C, x, dy, w1, b1, w2, dh, g, dx, d, stream);
+    if (cfg != 1 && cfg != 2) return fail(CSU_E_ARG, "mlp_bwd_ex: cfg 0, 1 or 2");
+    if (M < 1 || !x || !dy || !w1 || !b1 || !w2 || !dh || !g || !dx) return fail(CSU_E_ARG, "mlp_bwd: bad arguments");
+    if (M * 4L * C * 2 > 0x7fffffffL) return fail(CSU_E_ARG, "mlp_bwd: tensor exceeds 2 GB buffer range");
+    MlpDrop md{};
+    const int e = mlp_drop_of(d, md);
+    if (e < 0) return e;
+    const MlpDrop* dp = d && e == 0 ? &md : nullptr;
+    const long rpi = d ? (long)d->rows_per_sample : 0;
+    const hipStream_t st = as_stream(stream);
+    if (cfg == 2) {
+        switch (C) {
+            case 64: return bwd_deep_launch<64, 8>(M, x, dy, w1, b1, w2, dh, g, dx, dp, rpi, st);
+            case 128: return bwd_deep_launch<128, 6>(M, x, dy, w1, b1, w2, dh, g, dx, dp, rpi, st);
+            case 256: return bwd_deep_launch<256, 3>(M, x, dy, w1, b1, w2, dh, g, dx, dp, rpi, st);
+            default: return fail(CSU_E_ARG, "mlp_bwd: C must be 64, 128 or 256");
+        }
+    }
+    switch (C) {
+        case 64: return bwd_deep_launch<64, 6>(M, x, dy, w1, b1, w2, dh, g, dx, dp, rpi, st);
+        case 128: return bwd_deep_launch<128, 4>(M, x, dy, w1, b1, w2, dh, g, dx, dp, rpi, st);
+        case 256: return bwd_deep_launch<256, 4>(M, x, dy, w1, b1, w2, dh, g, dx, dp, rpi, st);
+        default: return fail(CSU_E_ARG, "mlp_bwd: C must be 64, 128 or 256");
     }
 }

@@ -1166,3 +1166,53 @@ def test_mlp_fwd_deep_ring_vs_fp64(C, M, cfg):
         assert err < 1e-2, (drop, err)
         d01 = float((ys[0] - ys[1]).double().norm() / (ys[1] - res).double().norm())
         assert d01 < 1e-2, (drop, d01)
+
+
+@pytest.mark.parametrize("C,M", [(64, 4096), (128, 1000), (256, 4160), (256, 100)])
+@pytest.mark.parametrize("cfg", [1, 2])
+def test_mlp_bwd_deep_ring_vs_fp64(C, M, cfg):
+    """csu_mlp_bwd_ex cfg 1 / 2 (the deep-ring backward) vs the fp64 composition: dh = (dy W2)
+    gelu'(h) m_h, g = gelu(h) m_h, dx = dh W1, without and with the hidden dropout mask; and it agrees
+    with the per-panel backward (cfg 0) to bf16 rounding."""
+    import ctypes
+    from csu import rng
+    from csu._lib import check, lib, ptr, stream_ptr
+    from csu.ops import MlpDrop
+    d = dev()
+    torch.manual_seed(C + M + cfg + 7)
+    x = torch.randn(M, C, device=d).bfloat16()
+    w1 = (torch.randn(4 * C, C, device=d) * C ** -0.5).bfloat16()
+    w2 = (torch.randn(C, 4 * C, device=d) * (4 * C) ** -0.5).bfloat16()
+    b1 = torch.randn(4 * C, device=d) * 0.1
+    dy = torch.randn(M, C, device=d).bfloat16()
+    st = stream_ptr(d)
+    X, W1, W2, B1, DY = (t.double().cpu() for t in (x, w1, w2, b1, dy))
+    F = torch.nn.functional
+    for drop in (False, True):
+        if drop:
+            snap = torch.tensor([9, 4], dtype=torch.int64, device=d)
+            md = MlpDrop(snap, 31, 32, 0.25).c_struct()
+            md.rows_per_sample = max(1, M // 2)
+            mh = rng.dropout_mask(snap, 31, 0.25, M * 4 * C).view(M, 4 * C).double().cpu() / 0.75
+        else:
+            md = MlpDrop(None, 0, 0, 0.0).c_struct()
+            md.rows_per_sample = M
+            mh = torch.ones(M, 4 * C, dtype=torch.float64)
+        outs = []
+        for c in (cfg, 0):
+            dh = torch.empty(M, 4 * C, device=d, dtype=torch.bfloat16)
+            g = torch.empty_like(dh)
+            dx = torch.empty(M, C, device=d, dtype=torch.bfloat16)
+            check(lib().csu_mlp_bwd_ex(M, C, ptr(x), ptr(dy), ptr(w1), ptr(b1), ptr(w2), ptr(dh), ptr(g), ptr(dx),
+                                       ctypes.byref(md), c, st), "mlp_bwd_ex")
+            outs.append((dh, g, dx))
+        torch.cuda.synchronize()
+        h = (X @ W1.T + B1).requires_grad_(True)
+        gr = F.gelu(h)
+        gr.backward((DY @ W2) * mh)
+        refs = (h.grad, gr.detach() * mh, h.grad @ W1)
+        for name, got, other, ref in zip(("dh", "g", "dx"), outs[0], outs[1], refs):
+            err = float((got.double().cpu() - ref).norm() / ref.norm())
+            assert err < 1e-2, (drop, name, err)
+            d01 = float((got - other).double().norm() / other.double().norm())
+            assert d01 < 1e-2, (drop, name, d01)

@@ -44,9 +44,13 @@ for C, M in [(64, 262144), (128, 65536), (256, 16384)]:
                                               mdp, st), "b"))
     fd1 = t(lambda: check(lib().csu_mlp_fwd_ex(M, C, ptr(x), ptr(w1), ptr(b1), ptr(w2), ptr(b2), ptr(res), ptr(y), mdp, 1, st), "d1"))
     fd2 = t(lambda: check(lib().csu_mlp_fwd_ex(M, C, ptr(x), ptr(w1), ptr(b1), ptr(w2), ptr(b2), ptr(res), ptr(y), mdp, 2, st), "d2"))
+    bd1 = t(lambda: check(lib().csu_mlp_bwd_ex(M, C, ptr(x), ptr(dy), ptr(w1), ptr(b1), ptr(w2), ptr(dh), ptr(g), ptr(dx),
+                                               mdp, 1, st), "bd1"))
+    bd2 = t(lambda: check(lib().csu_mlp_bwd_ex(M, C, ptr(x), ptr(dy), ptr(w1), ptr(b1), ptr(w2), ptr(dh), ptr(g), ptr(dx),
+                                               mdp, 2, st), "bd2"))
     f8 = t(lambda: check(lib().csu_mlp_fp8_fwd(M, C, ptr(x), ptr(w1q), ptr(sw1), ptr(b1), ptr(w2p), ptr(sw2), ptr(b2),
                                                ptr(res), ptr(y), mdp, st), "f8"))
     b8 = t(lambda: check(lib().csu_mlp_fp8_bwd(M, C, ptr(x), ptr(dy), ptr(w1q), ptr(sw1), ptr(b1), ptr(w2t), ptr(sw2),
                                                ptr(w1tp), ptr(dh), ptr(g), ptr(dx), mdp, st), "b8"))
-    print(f"C={C:4d} M={M:7d}  bf16 fwd {f:6.1f} us (deep ring {fd1:6.1f} / {fd2:6.1f})  bwd {bw:6.1f} us   "
+    print(f"C={C:4d} M={M:7d}  bf16 fwd {f:6.1f} us (deep ring {fd1:6.1f} / {fd2:6.1f})  bwd {bw:6.1f} us ({bd1:6.1f} / {bd2:6.1f})  "
           f"fp8 fwd {f8:6.1f} us  bwd {b8:6.1f} us", flush=True)
