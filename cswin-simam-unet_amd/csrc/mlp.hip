@@ -1504,7 +1504,9 @@ extern "C" int csu_mlp_bwd_dp(long M, int C, const void* x, const void* dy, cons
     const hipStream_t st = as_stream(stream);
     switch (C) {
         case 64: return bwd_launch<64>(M, x, dy, w1, b1, w2, dh, g, dx, dp, rpi, st);
-        case 128: return bwd_launch<128>(M, x, dy, w1, b1, w2, dh, g, dx, dp, rpi, st);
+        // C = 128: the deep ring (4 chunks of 32 hidden in flight) measured 61.0 vs 75.2 us at 65536
+        // tokens (profiles/r06b_mlp8_probe.txt); C = 64 / 256: the per-panel kernels (equal or faster)
+        case 128: return bwd_deep_launch<128, 4>(M, x, dy, w1, b1, w2, dh, g, dx, dp, rpi, st);
         case 256: return bwd_launch<256>(M, x, dy, w1, b1, w2, dh, g, dx, dp, rpi, st);
         default: return fail(CSU_E_ARG, "mlp_bwd: C must be 64, 128 or 256");
     }
@@ -1586,11 +1588,11 @@ extern "C" int csu_mlp_fwd_ex(long M, int C, const void* x, const void* w1, cons
     }
 }
 
-// explicit backward variant: cfg 0 = the per-panel / persistent kernels (csu_mlp_bwd_dp), 1 / 2 = the deep ring
+// explicit backward variant: cfg 0 = the per-panel / persistent kernels, 1 / 2 = the deep ring (csu_mlp_bwd_dp:
+// cfg 1 at C = 128, cfg 0 otherwise)
 extern "C" int csu_mlp_bwd_ex(long M, int C, const void* x, const void* dy, const void* w1, const float* b1, const void* w2,
                               void* dh, void* g, void* dx, const csu_mlp_dropout* d, int cfg, void* stream) {
-    if (cfg == 0) return csu_mlp_bwd_dp(M, C, x, dy, w1, b1, w2, dh, g, dx, d, stream);
-    if (cfg != 1 && cfg != 2) return fail(CSU_E_ARG, "mlp_bwd_ex: cfg 0, 1 or 2");
+    if (cfg != 0 && cfg != 1 && cfg != 2) return fail(CSU_E_ARG, "mlp_bwd_ex: cfg 0, 1 or 2");
     if (M < 1 || !x || !dy || !w1 || !b1 || !w2 || !dh || !g || !dx) return fail(CSU_E_ARG, "mlp_bwd: bad arguments");
     if (M * 4L * C * 2 > 0x7fffffffL) return fail(CSU_E_ARG, "mlp_bwd: tensor exceeds 2 GB buffer range");
     MlpDrop md{};
@@ -1599,6 +1601,14 @@ extern "C" int csu_mlp_bwd_ex(long M, int C, const void* x, const void* dy, cons
     const MlpDrop* dp = d && e == 0 ? &md : nullptr;
     const long rpi = d ? (long)d->rows_per_sample : 0;
     const hipStream_t st = as_stream(stream);
+    if (cfg == 0) {   // the per-panel / persistent kernels
+        switch (C) {
+            case 64: return bwd_launch<64>(M, x, dy, w1, b1, w2, dh, g, dx, dp, rpi, st);
+            case 128: return bwd_launch<128>(M, x, dy, w1, b1, w2, dh, g, dx, dp, rpi, st);
+            case 256: return bwd_launch<256>(M, x, dy, w1, b1, w2, dh, g, dx, dp, rpi, st);
+            default: return fail(CSU_E_ARG, "mlp_bwd: C must be 64, 128 or 256");
+        }
+    }
     if (cfg == 2) {
         switch (C) {
             case 64: return bwd_deep_launch<64, 8>(M, x, dy, w1, b1, w2, dh, g, dx, dp, rpi, st);

@@ -502,6 +502,8 @@ int csu_mlp_bwd_dp(long M, int C, const void* x, const void* dy, const void* w1,
  * weight ring (32-hidden chunks, several in flight, waves split by tokens; 2: another ring depth) */
 int csu_mlp_fwd_ex(long M, int C, const void* x, const void* w1, const float* b1, const void* w2, const float* b2,
                    const float* res, float* out, const csu_mlp_dropout* d, int cfg, void* stream);
+/* the backward with an explicit kernel: cfg 0 = the per-panel kernels, 1 / 2 = the deep ring (csu_mlp_bwd_dp
+ * runs cfg 1 at C = 128 and cfg 0 otherwise) */
 int csu_mlp_bwd_ex(long M, int C, const void* x, const void* dy, const void* w1, const float* b1, const void* w2,
                    void* dh, void* g, void* dx, const csu_mlp_dropout* d, int cfg, void* stream);
 /* fp8-e4m3 fused Mlp forward (BASELINE config 5, "fp8 MFMA weights"; same math and dropout as
