@@ -1499,15 +1499,6 @@ int launch_ig(const IG* gv, int n, const void* src, const void* w, const float* 
 int launch_ig(const IG& g, const void* src, const void* w, const float* bias, void* out, hipStream_t st, int cfg = -1) {
     return launch_ig(&g, 1, src, w, bias, out, st, cfg);
 }
-bool ig_phases_fused() {   // CSU_CONV_PHASE_LAUNCHES=1: one launch per stride phase (A/B)
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("CSU_CONV_PHASE_LAUNCHES");
-        v = !(e && e[0] == '1');
-    }
-    return v == 1;
-}
-
 IG ig_forward(const csu_conv_geom& c) {
     IG g{};
     g.Hs = c.H; g.Ws = c.W; g.Cs = c.C;
@@ -1559,25 +1550,10 @@ struct WPl {
     int chunks;
     long rpc;
 };
-bool conv_wgrad_v2() {   // CSU_CONV_WGRAD_V1=1: the transposed-staging v1 kernel (A/B)
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("CSU_CONV_WGRAD_V1");
-        v = !(e && e[0] == '1');
-    }
-    return v == 1;
-}
-int conv_wg_target() {   // CSU_CONV_WGS: target workgroups of the weight-gradient split (A/B)
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("CSU_CONV_WGS");
-        v = e ? atoi(e) : 2048;
-    }
-    return v;
-}
+constexpr int kConvWgs = 2048;   // target workgroups of the weight-gradient split
 WPl wplan(long M, int N, int K) {
     const long tiles = (long)((N + TBN - 1) / TBN) * ((K + TBN - 1) / TBN);
-    long want = (conv_wg_target() + tiles - 1) / tiles;
+    long want = (kConvWgs + tiles - 1) / tiles;
     const long maxc = (M + 255) / 256;
     if (want > maxc) want = maxc;
     if (want > 512) want = 512;
@@ -1744,7 +1720,7 @@ static int conv_dgrad_impl(const csu_conv_geom* gm, int dtype, const void* dy, c
             for (int px = 0; px < g.s; ++px) {
                 const IG ig = ig_dgrad_phase(*gm, py, px);
                 if (ig.M == 0) continue;
-                if (np > 0 && (np == 4 || !ig_phases_fused())) {   // stride > 2 (or the A/B switch): flush
+                if (np == 4) {   // stride > 2: flush
                     if (int e = launch_ig(ph, np, dy, w_ihwo, bias, dx, st, cfg)) return e;
                     np = 0;
                 }
@@ -1815,7 +1791,7 @@ static int conv_wgrad_impl(const csu_conv_geom* gm, int dtype, const void* x, co
         wd_run(pick, g, M, g.N, K, p, x, dy, part, st, x2, csplit);
     } else if (dtype == CSU_BF16) {
         const bool small = (long)g.B * g.H * g.W * g.C * 2 < (1L << 31) && M * g.N * 2 < (1L << 31);   // 32-bit offsets
-        if (vec && g.N % 8 == 0 && small && conv_wgrad_v2())
+        if (vec && g.N % 8 == 0 && small)
             conv_wgrad_bf16<<<grid, NT, 0, st>>>(g, M, g.N, K, p.rpc, (const bf16*)x, (const bf16*)dy, part);
         else if (vec) conv_wgrad_kernel<bf16, true><<<grid, NT, 0, st>>>(g, M, g.N, K, p.rpc, (const bf16*)x, (const bf16*)dy, part);
         else conv_wgrad_kernel<bf16, false><<<grid, NT, 0, st>>>(g, M, g.N, K, p.rpc, (const bf16*)x, (const bf16*)dy, part);

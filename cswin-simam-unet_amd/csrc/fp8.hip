@@ -49,13 +49,18 @@ __global__ __launch_bounds__(NT) void quant_e4m3_rows(const csu_fp8_item* __rest
 
 
 // Quantisation straight into the kernels' bf16 shadows (csu_quant_e4m3_shadow_batch): block = 64 rows of
-// one item.  Phase 1: a wave per row computes the row's amax (float4 loads, the lanes striding the row)
-// and its scale (the rule of quant_e4m3_rows, bit for bit).  Phase 2: 64-column tiles, thread = (row,
-// 16 columns): e4m3 bytes, the exact bf16 of q * s (the shadow), and the transposed shadow through an
-// LDS tile -- replaces the fp32 dequantised copy and the separate cast pass.
+// one item, thread = (row tr, 16 columns tc of each 64-column tile).  Phase 1: the row amax (two tiles
+// of loads in flight per thread, the 4 threads of a row combined by lane shuffles) and its scale (the
+// rule of quant_e4m3_rows, bit for bit).  Phase 2, per tile: e4m3 bytes, the exact bf16 of q * s (the
+// shadow), and through LDS tiles the transposed shadow and the fp8 fused Mlp's operand layouts
+// (q_perm: columns permuted within 64-groups; q_t: transposed; q_tp: transposed with permuted columns).
+constexpr int T8S = 68;   // byte row stride of the e4m3 transposition tile (4 column groups on distinct banks)
+
+__device__ __forceinline__ float row_scale_of(float amax) { return amax > 0.f ? exp2f(ceilf(log2f(amax / 448.f))) : 1.f; }
+
 __global__ __launch_bounds__(NT) void quant_e4m3_shadow(const csu_fp8_shadow_item* __restrict__ items, int count) {
-    __shared__ float srow[64];
     __shared__ __attribute__((aligned(16))) bf16 T[64][64 + 8];
+    __shared__ __attribute__((aligned(16))) uint8_t T8[64 * T8S];
     int lo = 0, hi = count - 1;
     while (lo < hi) {
         const int mid = (lo + hi + 1) >> 1;
@@ -64,41 +69,43 @@ __global__ __launch_bounds__(NT) void quant_e4m3_shadow(const csu_fp8_shadow_ite
     const csu_fp8_shadow_item it = items[lo];
     const int rows = it.rows, cols = it.cols;
     const int rb = (int)((long)blockIdx.x - it.blk0) * 64;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    for (int i = 0; i < 16; ++i) {
-        const int lr = wave * 16 + i, row = rb + lr;
-        if (row >= rows) break;                                   // uniform per wave
-        const float* src = it.src + (long)row * cols;
-        float amax = 0.f;
-        for (int c = 4 * lane; c < cols; c += 256) {
-            const f32x4 v = *reinterpret_cast<const f32x4*>(src + c);
-            amax = fmaxf(amax, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
-        }
-        amax = wave_max(amax);
-        const float sc = amax > 0.f ? exp2f(ceilf(log2f(amax / 448.f))) : 1.f;
-        if (lane == 0) {
-            srow[lr] = sc;
-            if (it.scales) it.scales[row] = sc;
-        }
-    }
-    __syncthreads();
     const int tr = threadIdx.x >> 2, tc = (threadIdx.x & 3) * 16;
     const int row = rb + tr;
-    const float sc = row < rows ? srow[tr] : 1.f;
+    const bool rok = row < rows;
+    const float* src = it.src + (long)(rok ? row : 0) * cols;
+    auto load16 = [&](int col, float* v) {   // cols % 16 == 0: whole 16-column runs
+        if (rok && col < cols) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const f32x4 x = *reinterpret_cast<const f32x4*>(src + col + 4 * k);
+                v[4 * k] = x[0]; v[4 * k + 1] = x[1]; v[4 * k + 2] = x[2]; v[4 * k + 3] = x[3];
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < 16; ++k) v[k] = 0.f;
+        }
+    };
+    float amax = 0.f;
+    for (int c0 = 0; c0 < cols; c0 += 128) {
+        float a[16], b[16];
+        load16(c0 + tc, a);
+        load16(c0 + 64 + tc, b);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) amax = fmaxf(amax, fmaxf(fabsf(a[k]), fabsf(b[k])));
+    }
+    amax = fmaxf(amax, __shfl_xor(amax, 1));
+    amax = fmaxf(amax, __shfl_xor(amax, 2));
+    const float sc = row_scale_of(amax);
+    if (rok && (threadIdx.x & 3) == 0 && it.scales) it.scales[row] = sc;
     const float inv = 1.f / sc;   // exact: a power of two
     bf16* const sh = (bf16*)it.shadow;
     bf16* const st = (bf16*)it.shadow_t;
+    const bool tiles = st || it.q_t || it.q_tp;
     for (int c0 = 0; c0 < cols; c0 += 64) {
         const int col = c0 + tc;
-        const bool ok = row < rows && col < cols;                 // cols % 16 == 0: whole 16-column runs
-        float v[16] = {};
-        if (ok) {
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const f32x4 x = *reinterpret_cast<const f32x4*>(it.src + (long)row * cols + col + 4 * k);
-                v[4 * k] = x[0]; v[4 * k + 1] = x[1]; v[4 * k + 2] = x[2]; v[4 * k + 3] = x[3];
-            }
-        }
+        const bool ok = rok && col < cols;
+        float v[16];
+        load16(col, v);
         unsigned w[4];
         float dq[16];
 #pragma unroll
@@ -111,22 +118,43 @@ __global__ __launch_bounds__(NT) void quant_e4m3_shadow(const csu_fp8_shadow_ite
             dq[4 * k] = a[0] * sc; dq[4 * k + 1] = a[1] * sc; dq[4 * k + 2] = b[0] * sc; dq[4 * k + 3] = b[1] * sc;
         }
         if (ok) {
-            if (it.q) *reinterpret_cast<u32x4*>(it.q + (long)row * cols + col) = u32x4{w[0], w[1], w[2], w[3]};
-            store8(sh + (long)row * cols + col, dq);
-            store8(sh + (long)row * cols + col + 8, dq + 8);
+            const long o = (long)row * cols + col;
+            if (it.q) *reinterpret_cast<u32x4*>(it.q + o) = u32x4{w[0], w[1], w[2], w[3]};
+            if (it.q_perm) {   // dst 32h + 16t + 4g + i <- src 32t + 8g + 4h + i within the 64-group
+                const int k = tc >> 4, t = k >> 1, d0 = 16 * t + 8 * (k & 1);
+                *reinterpret_cast<u32x2*>(it.q_perm + (long)row * cols + c0 + d0) = u32x2{w[0], w[2]};
+                *reinterpret_cast<u32x2*>(it.q_perm + (long)row * cols + c0 + 32 + d0) = u32x2{w[1], w[3]};
+            }
+            store8(sh + o, dq);
+            store8(sh + o + 8, dq + 8);
         }
-        if (st) {
+        if (tiles) {
 #pragma unroll
-            for (int j = 0; j < 16; ++j) T[tc + j][tr] = (bf16)dq[j];
+            for (int j = 0; j < 16; ++j) {
+                T[tc + j][tr] = (bf16)dq[j];
+                T8[(tc + j) * T8S + tr] = (uint8_t)(w[j >> 2] >> (8 * (j & 3)));
+            }
             __syncthreads();
-            const int tcol = threadIdx.x >> 2, r16 = (threadIdx.x & 3) * 16;   // shadow_t row = c0 + tcol
+            const int tcol = threadIdx.x >> 2, r16 = (threadIdx.x & 3) * 16;   // dst row = c0 + tcol
             if (c0 + tcol < cols) {
-                bf16* dst = st + (long)(c0 + tcol) * rows + rb + r16;
-                if (rb + r16 + 16 <= rows && (rows & 7) == 0) {
-                    *reinterpret_cast<u32x4*>(dst) = *reinterpret_cast<const u32x4*>(&T[tcol][r16]);
-                    *reinterpret_cast<u32x4*>(dst + 8) = *reinterpret_cast<const u32x4*>(&T[tcol][r16 + 8]);
-                } else {
-                    for (int j = 0; j < 16 && rb + r16 + j < rows; ++j) dst[j] = T[tcol][r16 + j];
+                const long drow = c0 + tcol;
+                if (st) {
+                    bf16* dst = st + drow * rows + rb + r16;
+                    if (rb + r16 + 16 <= rows && (rows & 7) == 0) {
+                        *reinterpret_cast<u32x4*>(dst) = *reinterpret_cast<const u32x4*>(&T[tcol][r16]);
+                        *reinterpret_cast<u32x4*>(dst + 8) = *reinterpret_cast<const u32x4*>(&T[tcol][r16 + 8]);
+                    } else {
+                        for (int j = 0; j < 16 && rb + r16 + j < rows; ++j) dst[j] = T[tcol][r16 + j];
+                    }
+                }
+                const unsigned* t8 = reinterpret_cast<const unsigned*>(T8 + tcol * T8S);
+                if (it.q_t)   // rows % 64 == 0 (host-checked)
+                    *reinterpret_cast<u32x4*>(it.q_t + drow * rows + rb + r16) =
+                        u32x4{t8[r16 / 4], t8[r16 / 4 + 1], t8[r16 / 4 + 2], t8[r16 / 4 + 3]};
+                if (it.q_tp) {   // dst col 32h + 16t + 4g + i <- src row 32t + 8g + 4h + i (k = r16 / 16 = 2h + t)
+                    const int k = r16 >> 4, b = 32 * (k & 1) + 4 * (k >> 1);
+                    *reinterpret_cast<u32x4*>(it.q_tp + drow * rows + rb + r16) =
+                        u32x4{t8[b / 4], t8[(b + 8) / 4], t8[(b + 16) / 4], t8[(b + 24) / 4]};
                 }
             }
             __syncthreads();

@@ -947,16 +947,17 @@ __device__ __forceinline__ void mma_acc_sw(f32x16& acc, const bf16* img, int kba
 // gather the window rows [0, npad) of one head's channels of two tensors into swizzled images
 // (rows >= N zero).  All global loads of the thread are issued before the first LDS store, so the
 // staging costs one memory latency instead of one per row group.
+template <int NTH = NT>
 __device__ __forceinline__ void stage_win2(const Win& w, int reso, const bf16* imgA, int strideA, int chA,
                                            const bf16* imgB, int strideB, int chB, int npad, bf16* dstA, bf16* dstB) {
-    constexpr int IT = 4;   // 256 rows per pass: 8 x 16-B loads in flight per thread
+    constexpr int IT = 4;   // NTH rows per pass: 8 x 16-B loads in flight per thread
     const long L = (long)reso * reso;
     const __amdgpu_buffer_rsrc_t rsA = buf_rsrc(imgA, L * strideA * 2), rsB = buf_rsrc(imgB, L * strideB * 2);
-    for (int base = 0; base < npad * 4; base += IT * NT) {
+    for (int base = 0; base < npad * 4; base += IT * NTH) {
         bf16x8 va[IT], vb[IT];
 #pragma unroll
         for (int i = 0; i < IT; ++i) {
-            const int it = base + threadIdx.x + i * NT;
+            const int it = base + threadIdx.x + i * NTH;
             const int n = it >> 2, c = (it & 3) * 8;
             const bool ok = it < npad * 4 && n < w.N;
             const unsigned tok = ok ? (unsigned)tok_of(w, reso, n) : 0u;
@@ -965,7 +966,7 @@ __device__ __forceinline__ void stage_win2(const Win& w, int reso, const bf16* i
         }
 #pragma unroll
         for (int i = 0; i < IT; ++i) {
-            const int it = base + threadIdx.x + i * NT;
+            const int it = base + threadIdx.x + i * NTH;
             if (it < npad * 4) {
                 const int n = it >> 2, c = (it & 3) * 8;
                 *reinterpret_cast<bf16x8*>(dstA + swz(n, c)) = va[i];
@@ -1394,16 +1395,17 @@ __device__ __forceinline__ bf16x8 tr_frag16(const bf16* img, int kb, int cb, int
 // gather window rows [0, npad) of one head's channels of two tensors: A into a PLAIN [row][32] image
 // (the prologue's V: neighbour rows are base + constant, no swizzle arithmetic), B swizzled (swz);
 // rows >= N zero.  Loads first, then the LDS stores (one memory latency).
+template <int NTH = NT>
 __device__ __forceinline__ void stage_win2_pa(const Win& w, int reso, const bf16* imgA, int strideA, int chA,
                                               const bf16* imgB, int strideB, int chB, int npad, bf16* dstA, bf16* dstB) {
     constexpr int IT = 4;
     const long L = (long)reso * reso;
     const __amdgpu_buffer_rsrc_t rsA = buf_rsrc(imgA, L * strideA * 2), rsB = buf_rsrc(imgB, L * strideB * 2);
-    for (int base = 0; base < npad * 4; base += IT * NT) {
+    for (int base = 0; base < npad * 4; base += IT * NTH) {
         bf16x8 va[IT], vb[IT];
 #pragma unroll
         for (int i = 0; i < IT; ++i) {
-            const int it = base + threadIdx.x + i * NT;
+            const int it = base + threadIdx.x + i * NTH;
             const int n = it >> 2, c = (it & 3) * 8;
             const bool ok = it < npad * 4 && n < w.N;
             const unsigned tok = ok ? (unsigned)tok_of(w, reso, n) : 0u;
@@ -1412,7 +1414,7 @@ __device__ __forceinline__ void stage_win2_pa(const Win& w, int reso, const bf16
         }
 #pragma unroll
         for (int i = 0; i < IT; ++i) {
-            const int it = base + threadIdx.x + i * NT;
+            const int it = base + threadIdx.x + i * NTH;
             if (it < npad * 4) {
                 const int n = it >> 2, c = (it & 3) * 8;
                 *reinterpret_cast<bf16x8*>(dstA + n * HD + c) = va[i];
@@ -1443,13 +1445,20 @@ __device__ __forceinline__ void lepe4_lds_z(const Win& w, const bf16* img, int n
     }
 }
 
-template <int WM, bool DROP>
-__global__ __launch_bounds__(NT, WM <= 256 ? 2 : 1) void stripe_bwd_fused_w(csu_stripe_args a, const bf16* __restrict__ qkv,
+// NW waves: 4, or 8 for the 512-token windows (one workgroup per CU: two waves per SIMD hide the MFMA /
+// LDS latencies of the per-tile chains); with 8 waves the dQ quadrants are split over two key halves
+// and the upper half's partials added through LDS.
+template <int WM, bool DROP, int NW = 4>
+__global__ __launch_bounds__(64 * NW, WM <= 256 ? 2 : 1) void stripe_bwd_fused_w(csu_stripe_args a, const bf16* __restrict__ qkv,
                                                             const bf16* __restrict__ out, const bf16* __restrict__ dout,
                                                             const float* __restrict__ lse, bf16* __restrict__ dqkv,
                                                             float* __restrict__ part) {
-    constexpr int KT = WM / 128;          // key tiles per wave
-    constexpr int RT = WM / 32;           // rows per thread in the prologue / 32-row tiles of the image
+    static_assert(NW == 4 || NW == 8, "stripe_bwd_fused_w: 4 or 8 waves");
+    constexpr int NTH = 64 * NW;
+    constexpr int KT = WM / (32 * NW);    // key tiles per wave
+    constexpr int RT = WM / 32;           // 32-row tiles of the image
+    constexpr int RS = NTH / 8;           // prologue: row stride (8 channel-quad lanes per row)
+    constexpr int PR = WM / RS;           // prologue rows per thread
     __shared__ __attribute__((aligned(16))) bf16 Qs[WM * HD];
     __shared__ __attribute__((aligned(16))) bf16 Ks[WM * HD];
     // V: PLAIN [row][32] image + a zero row at WM (the prologue); from the main loop on the first WM
@@ -1458,8 +1467,9 @@ __global__ __launch_bounds__(NT, WM <= 256 ? 2 : 1) void stripe_bwd_fused_w(csu_
     __shared__ __attribute__((aligned(16))) bf16 Gs[(WM + 1) * HD];   // dO (swizzled) + a zero row at WM
     __shared__ __attribute__((aligned(16))) float nlse_s[WM], dl_s[WM];
     __shared__ __attribute__((aligned(16))) float wts[HD * 10];
-    __shared__ float red[4][8][41];
-    __shared__ __attribute__((aligned(16))) unsigned char dtbl[4][128];
+    __shared__ float red[NW][8][41];
+    __shared__ __attribute__((aligned(16))) unsigned char dtbl[NW][128];
+    __shared__ __attribute__((aligned(16))) f32x4v xq[NW == 8 ? 4 : 1][64];   // upper key half's dQ partials
     ATT_STAMP(1, 0);
     const Win w = decode_w(a, 1);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1471,14 +1481,14 @@ __global__ __launch_bounds__(NT, WM <= 256 ? 2 : 1) void stripe_bwd_fused_w(csu_
     const int c4 = threadIdx.x & 7, rg = threadIdx.x >> 3;   // prologue: channel quad, row group
 
     // ---- staging: Q, K, V, dO images, the window's -lse * log2(e) (the exponent offsets)
-    u32x2 orow[RT];   // O rows of the prologue, loaded with the staging loads (global latency once)
+    u32x2 orow[PR];   // O rows of the prologue, loaded with the staging loads (global latency once)
     {
         const __amdgpu_buffer_rsrc_t rs_lse = stat_rsrc(a, lse);
-        constexpr int SI = (WM + NT - 1) / NT;   // window rows per thread
+        constexpr int SI = (WM + NTH - 1) / NTH;   // window rows per thread
         float lv[SI];
 #pragma unroll
         for (int k = 0; k < SI; ++k) {
-            const int i = threadIdx.x + k * NT;
+            const int i = threadIdx.x + k * NTH;
             lv[k] = ldf_rs(rs_lse, i < w.N ? (unsigned)(stat_index(a, w, tok_of(w, a.reso, i)) * 4) : kOOB);
         }
         float lw[LW_IT];
@@ -1486,14 +1496,14 @@ __global__ __launch_bounds__(NT, WM <= 256 ? 2 : 1) void stripe_bwd_fused_w(csu_
         {
             const __amdgpu_buffer_rsrc_t rs_o = buf_rsrc(out + (size_t)w.b * L * C, (long)L * C * 2);
 #pragma unroll
-            for (int k = 0; k < RT; ++k) {
-                const int n = rg + 32 * k;
+            for (int k = 0; k < PR; ++k) {
+                const int n = rg + RS * k;
                 orow[k] = __builtin_amdgcn_raw_buffer_load_b64(
                     rs_o, n < w.N ? (unsigned)(((size_t)tok_of(w, a.reso, n) * C + w.chq + 4 * c4) * 2) : kOOB, 0, 0);
             }
         }
-        stage_win2(w, a.reso, img, C3, w.chq, img, C3, C + w.chq, npad, Qs, Ks);
-        stage_win2_pa(w, a.reso, img, C3, 2 * C + w.chq, gimg, C, w.chq, npad, Vs, Gs);
+        stage_win2<NTH>(w, a.reso, img, C3, w.chq, img, C3, C + w.chq, npad, Qs, Ks);
+        stage_win2_pa<NTH>(w, a.reso, img, C3, 2 * C + w.chq, gimg, C, w.chq, npad, Vs, Gs);
         lepe_weights_store(lw, wts);
         if (threadIdx.x < 8) {   // the zero rows
             const bf16x8 z = {};
@@ -1501,14 +1511,14 @@ __global__ __launch_bounds__(NT, WM <= 256 ? 2 : 1) void stripe_bwd_fused_w(csu_
         }
 #pragma unroll
         for (int k = 0; k < SI; ++k) {
-            const int i = threadIdx.x + k * NT;
+            const int i = threadIdx.x + k * NTH;
             if (i < npad) nlse_s[i] = i < w.N ? -lv[k] * kLog2e : -INFINITY;   // padded queries: P = 0
         }
     }
     __syncthreads();
     ATT_STAMP(1, 1);
 
-    // ---- prologue: delta and the LePE weight-gradient partials (thread: channel quad c4, rows rg + 32k)
+    // ---- prologue: delta and the LePE weight-gradient partials (thread: channel quad c4, rows rg + RS k)
     {
         float wacc[40];
 #pragma unroll
@@ -1519,12 +1529,12 @@ __global__ __launch_bounds__(NT, WM <= 256 ? 2 : 1) void stripe_bwd_fused_w(csu_
         // over all rows and keeps every row's V values live); the preloaded O rows rotate through
         // orow[0] so every register index stays static.  Out-of-window taps read the zero row.
 #pragma unroll 1
-        for (int n = rg; n < npad; n += 32) {
+        for (int n = rg; n < npad; n += RS) {
             const bool valid = n < w.N;                    // uniform over the 8 lanes of the row
             const int nn = valid ? n : 0;
             const u32x2 oraw = orow[0];
 #pragma unroll
-            for (int k = 0; k + 1 < RT; ++k) orow[k] = orow[k + 1];
+            for (int k = 0; k + 1 < PR; ++k) orow[k] = orow[k + 1];
             const int iy = wrow(w, nn), ix = nn - iy * w.W_sp;
             const bool ym = iy > 0, yp = iy + 1 < w.H_sp, xm = ix > 0, xp = ix + 1 < w.W_sp;
             const bf16x4 g4 = *reinterpret_cast<const bf16x4*>(Gs + swz(nn, 4 * c4));
@@ -1576,7 +1586,7 @@ __global__ __launch_bounds__(NT, WM <= 256 ? 2 : 1) void stripe_bwd_fused_w(csu_
     Frag<bf16> kf[KT], vf[KT];
 #pragma unroll
     for (int j = 0; j < KT; ++j) {
-        const int kt = wave + 4 * j;
+        const int kt = wave + NW * j;
         const int row = (kt < ntile ? kt : 0) * 32 + r;
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
@@ -1588,9 +1598,11 @@ __global__ __launch_bounds__(NT, WM <= 256 ? 2 : 1) void stripe_bwd_fused_w(csu_
     if (part) {
         const int nwx = a.reso / w.W_sp, nwin = (a.reso / w.H_sp) * nwx;
         const int Cb = a.heads * HD, nblk = a.B * nwin, blk = w.b * nwin + w.wy * nwx + w.wx;
-        for (int o = threadIdx.x; o < 8 * 40; o += NT) {
+        for (int o = threadIdx.x; o < 8 * 40; o += NTH) {
             const int qq = o / 40, i = o % 40;
-            const float sum = ((red[0][qq][i] + red[1][qq][i]) + red[2][qq][i]) + red[3][qq][i];
+            float sum = red[0][qq][i];
+#pragma unroll
+            for (int v = 1; v < NW; ++v) sum += red[v][qq][i];
             const int k = i >> 2, c = w.h * HD + 4 * qq + (i & 3);
             part[((size_t)w.br * Cb * 10 + c * 10 + k) * nblk + blk] = sum;
         }
@@ -1605,7 +1617,8 @@ __global__ __launch_bounds__(NT, WM <= 256 ? 2 : 1) void stripe_bwd_fused_w(csu_
 #pragma unroll
     for (int j = 0; j < KT; ++j) { dk[j] = f32x16{}; dv[j] = f32x16{}; }
     bf16* const dS = Vs;
-    const int dh = wave & 1, qh = wave >> 1;
+    const int dh = wave & 1, qh = (wave >> 1) & 1, kh = wave >> 2;   // dQ quadrant; key half (NW = 8)
+    constexpr int KK = NW == 8 ? RT / 2 : RT;                      // key tiles per dQ quadrant pass
     int o_row[2], o_tr[2][2], o_ds[4], o_k16[2], o_d16[2];
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
@@ -1652,7 +1665,7 @@ __global__ __launch_bounds__(NT, WM <= 256 ? 2 : 1) void stripe_bwd_fused_w(csu_
         // interleave the two tiles' MFMA chains and VALU work
 #pragma unroll
         for (int j = 0; j < KT; ++j) {
-            const int kt = wave + 4 * j;
+            const int kt = wave + NW * j;
             f32x16 s = {}, dp = {};
 #pragma unroll
             for (int s2 = 0; s2 < 2; ++s2) {
@@ -1698,27 +1711,34 @@ __global__ __launch_bounds__(NT, WM <= 256 ? 2 : 1) void stripe_bwd_fused_w(csu_
         // dQ^T[d][q] quadrant (d = 16 dh + 4 (lane >> 4) + i, q = qb + 16 qh + (lane & 15)) over all keys
         f32x4v acc2[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};   // two independent MFMA chains
 #pragma unroll
-        for (int kk = 0; kk < RT; ++kk)
+        for (int k2 = 0; k2 < KK; ++k2) {
+            const int kk = kh * KK + k2;
             if (kk < ntile)
-                acc2[kk & 1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr16(Ks + kk * 32 * HD, o_k16),
-                                                                      tr16(dS + kk * 32 * HD, o_d16), acc2[kk & 1], 0, 0, 0);
-        const f32x4v acc = acc2[0] + acc2[1];
-        {
+                acc2[k2 & 1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr16(Ks + kk * 32 * HD, o_k16),
+                                                                      tr16(dS + kk * 32 * HD, o_d16), acc2[k2 & 1], 0, 0, 0);
+        }
+        f32x4v acc = acc2[0] + acc2[1];
+        if constexpr (NW == 8)
+            if (kh) xq[wave & 3][lane] = acc;              // the lower half adds it after the barrier
+        auto store_dq = [&](const f32x4v& v4) {
             const int qn = qb + 16 * qh + (lane & 15);
             if (qn < w.N) {
                 const int d0 = 16 * dh + 4 * (lane >> 4);
-                const float v[4] = {acc[0] * a.scale, acc[1] * a.scale, acc[2] * a.scale, acc[3] * a.scale};
+                const float v[4] = {v4[0] * a.scale, v4[1] * a.scale, v4[2] * a.scale, v4[3] * a.scale};
                 store4(dqkv + ((size_t)w.b * L + tok_of(w, a.reso, qn)) * C3 + w.chq + d0, v);
             }
-        }
+        };
+        if constexpr (NW == 4) store_dq(acc);
         __syncthreads();                                   // the dS tile is rewritten by the next query tile
+        if constexpr (NW == 8)
+            if (!kh) store_dq(acc + xq[wave][lane]);       // xq is rewritten only after the next tile's barrier
     }
     ATT_STAMP(1, 3);
 
     // ---- dK, dV (+ LePE input gradient: the transposed conv of dO) of the own key tiles
 #pragma unroll
     for (int j = 0; j < KT; ++j) {
-        const int kt = wave + 4 * j, kn = kt * 32 + r;
+        const int kt = wave + NW * j, kn = kt * 32 + r;
         if (kt >= ntile || kn >= w.N) continue;
         bf16* drow = dqkv + ((size_t)w.b * L + tok_of(w, a.reso, kn)) * C3 + w.chq;
 #pragma unroll
@@ -1747,13 +1767,13 @@ int fused_nblk(const csu_stripe_args& a) {
     return a.B * (a.reso / a.br[0].H_sp) * (a.reso / a.br[0].W_sp);
 }
 
-template <int WM>
+template <int WM, int NW = 4>
 void bwd_fused(const csu_stripe_args& a, const bf16* qkv, const bf16* out, const bf16* dout, const float* lse, bf16* dqkv,
                float* part, hipStream_t st) {
     const int nwin = (a.reso / a.br[0].H_sp) * (a.reso / a.br[0].W_sp);
     const dim3 g(a.B * nwin * a.heads, a.nbranch);
-    if (a.drop_p > 0.f) stripe_bwd_fused_w<WM, true><<<g, NT, 0, st>>>(a, qkv, out, dout, lse, dqkv, part);
-    else stripe_bwd_fused_w<WM, false><<<g, NT, 0, st>>>(a, qkv, out, dout, lse, dqkv, part);
+    if (a.drop_p > 0.f) stripe_bwd_fused_w<WM, true, NW><<<g, 64 * NW, 0, st>>>(a, qkv, out, dout, lse, dqkv, part);
+    else stripe_bwd_fused_w<WM, false, NW><<<g, 64 * NW, 0, st>>>(a, qkv, out, dout, lse, dqkv, part);
 }
 
 // split factor of the whole-window kernels: workgroups per window-head, so that a launch has
@@ -2009,7 +2029,7 @@ extern "C" int csu_stripe_attn_bwd_ex(const csu_stripe_args* a, int dtype, const
         const int N = a->br[0].H_sp * a->br[0].W_sp;
         if (N <= 128) bwd_fused<128>(*a, q, o, go, lse, (bf16*)dqkv, pp, st);
         else if (N <= 256) bwd_fused<256>(*a, q, o, go, lse, (bf16*)dqkv, pp, st);
-        else bwd_fused<512>(*a, q, o, go, lse, (bf16*)dqkv, pp, st);
+        else bwd_fused<512, 8>(*a, q, o, go, lse, (bf16*)dqkv, pp, st);
         if (do_lepe && !lepe_deferred) {
             const dim3 rgrid((a->nbranch * a->heads * HD * 10 + 15) / 16);
             lepe_wgrad_reduce<<<rgrid, 256, 0, st>>>(*a, fused_nblk(*a), part);

@@ -607,18 +607,11 @@ extern "C" int csu_linear_wgrad_deferred(long M, int N, int K, const void* dy, c
 // Plan of a Linear inside a grouped launch: 128 tiles when N and K allow, else 64; token chunks so
 // that the fp32 partial slabs stay <= ~1/16 of the operand bytes (chunks <= M (N + K) / (32 N K)),
 // >= 1024 tokens per chunk.  No occupancy target: the group fills the GPU.
-static int slab_div() {   // CSU_WGRAD_SLAB_DIV: slab bytes <= operand bytes * 2 / div (A/B)
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("CSU_WGRAD_SLAB_DIV");
-        v = e ? atoi(e) : 32;   // A/B at 512 B16: 8 -> 1231 img/s, 16 -> 1249, 32 -> 1255, 64 -> 1227
-        if (v < 1) v = 32;
-    }
-    return v;
-}
+// slab bytes <= operand bytes * 2 / kSlabDiv (A/B at 512 B16: 8 -> 1231 img/s, 16 -> 1249, 32 -> 1255, 64 -> 1227)
+constexpr int kSlabDiv = 32;
 static void group_plan(long M, int N, int K, int* tn, int* tk, int* chunks, long* rpc) {
     const int t = (N % 128 == 0 && K % 128 == 0) ? 128 : 64;
-    long c = (long)((double)M * (N + K) / ((double)slab_div() * N * K) + 0.5);
+    long c = (long)((double)M * (N + K) / ((double)kSlabDiv * N * K) + 0.5);
     const long maxc = M / 1024 > 0 ? M / 1024 : 1;
     if (c > maxc) c = maxc;
     if (c < 1) c = 1;

@@ -1798,6 +1798,7 @@ class Fp8Weights:
         # after every quantisation by one csu_e4m3_layout_batch launch: W2 with permuted columns,
         # W2^T, W1^T with permuted columns
         self.mlp = {}
+        self.lay_of = {}   # weight ptr -> (q_perm, q_t, q_tp) written by the shadow quantiser
         lay, w0 = [], 0
         for w1, w2 in mlp_pairs:
             i1, i2 = self.index.get(w1.data_ptr()), self.index.get(w2.data_ptr())
@@ -1814,6 +1815,8 @@ class Fp8Weights:
                 lay.append((src.data_ptr(), dst.data_ptr(), w0, rows, cols, mode, 0))
                 w0 += rows * cols // 4
             self.mlp[w1.data_ptr()] = (w2.data_ptr(), q1, self.scales[i1], w2p, self.scales[i2], w2t, w1tp)
+            self.lay_of[w1.data_ptr()] = (0, 0, w1tp.data_ptr())
+            self.lay_of[w2.data_ptr()] = (w2p.data_ptr(), w2t.data_ptr(), 0)
         self.lay_count, self.lay_words = len(lay), w0
         if lay:
             lt = np.dtype([("src", "<u8"), ("dst", "<u8"), ("w0", "<i8"), ("rows", "<i4"), ("cols", "<i4"),
@@ -1862,11 +1865,14 @@ class Fp8Weights:
             cols = p.numel() // rows
             if cols % 16:
                 raise ValueError("Fp8Weights: weight columns must be a multiple of 16")
+            lay = self.lay_of.get(p.data_ptr(), (0, 0, 0))
+            if any(lay) and (rows % 64 or cols % 64):
+                raise ValueError("Fp8Weights: fp8 Mlp layouts need rows % 64 == 0 and cols % 64 == 0")
             recs.append((p.data_ptr(), q.data_ptr(), sc.data_ptr(), cache.shadow[i].data_ptr(),
-                         0 if st is None else st.data_ptr(), b0, rows, cols))
+                         0 if st is None else st.data_ptr()) + lay + (b0, rows, cols))
             b0 += -(-rows // 64)
-        dt = np.dtype([("src", "<u8"), ("q", "<u8"), ("sc", "<u8"), ("sh", "<u8"), ("st", "<u8"), ("b0", "<i8"),
-                       ("rows", "<i4"), ("cols", "<i4")])
+        dt = np.dtype([("src", "<u8"), ("q", "<u8"), ("sc", "<u8"), ("sh", "<u8"), ("st", "<u8"), ("qp", "<u8"),
+                       ("qt", "<u8"), ("qtp", "<u8"), ("b0", "<i8"), ("rows", "<i4"), ("cols", "<i4")])
         self._sitems = torch.frombuffer(bytearray(np.array(recs, dtype=dt).tobytes()), dtype=torch.uint8).to(
             self.params[0].device)
         self._sblocks, self._scount, self._skey = b0, len(recs), key
@@ -1874,8 +1880,9 @@ class Fp8Weights:
 
     def quantize(self, cache: Optional["CastCache"] = None):
         """One launch: e4m3 bytes + row scales of every listed weight, and either the dequantised fp32
-        copies (``deq``, returned) or -- with ``cache`` -- the bf16 shadows W and W^T straight in the
-        cache (csu_quant_e4m3_shadow_batch); then the fp8 Mlp operand layouts."""
+        copies (``deq``, returned; then the fp8 Mlp operand layouts by csu_e4m3_layout_batch) or -- with
+        ``cache`` -- the bf16 shadows W and W^T straight in the cache and the fp8 Mlp operand layouts from
+        the same pass (csu_quant_e4m3_shadow_batch)."""
         dev = self.params[0].device
         nq = sum(p.numel() for p, q in zip(self.params, self.q) if q is not None)
         if cache is None:
@@ -1884,7 +1891,8 @@ class Fp8Weights:
         else:
             items, blocks, count = self._shadow_items(cache)
             _launch("quant_e4m3", lambda: lib().csu_quant_e4m3_shadow_batch(ptr(items), count, blocks, stream_ptr(dev)),
-                    0, nq * (4 + 1 + 2 + 2))
+                    0, nq * (4 + 1 + 2 + 2) + self.lay_words * 4)
+            return self.deq
         if self.lay_count:
             _launch("quant_e4m3", lambda: lib().csu_e4m3_layout_batch(ptr(self.lay_items), self.lay_count, self.lay_words,
                                                                      stream_ptr(dev)), 0, self.lay_words * 8)

@@ -347,7 +347,8 @@ typedef struct {
 int csu_quant_e4m3_batch(const csu_fp8_item* items, int count, long total_rows, void* stream);
 /* The same quantisation written straight into bf16 shadows: per item (rows x cols fp32, cols % 16 ==
  * 0), scales[row] = s (optional), q (optional) the e4m3 bytes, shadow (rows x cols bf16) = q * s exactly,
- * shadow_t (cols x rows bf16, optional) its transpose.  items: DEVICE array sorted by blk0 (prefix sum of
+ * shadow_t (cols x rows bf16, optional) its transpose; q_perm / q_t / q_tp (optional; rows % 64 == 0 and
+ * cols % 64 == 0) the fp8 fused Mlp's byte layouts of q.  items: DEVICE array sorted by blk0 (prefix sum of
  * ceil(rows / 64)); one 256-thread block per 64 rows of every item. */
 typedef struct {
     const float* src;
@@ -355,6 +356,9 @@ typedef struct {
     float* scales;
     void* shadow;
     void* shadow_t;
+    uint8_t* q_perm;   /* optional: e4m3 bytes with columns permuted in 64-groups (dst 32h+16t+4g+i <- src 32t+8g+4h+i) */
+    uint8_t* q_t;      /* optional: transposed e4m3 bytes (cols x rows) */
+    uint8_t* q_tp;     /* optional: transposed, columns permuted as q_perm (the fp8 fused Mlp's W1^T layout) */
     int64_t blk0;
     int32_t rows, cols;
 } csu_fp8_shadow_item;

@@ -243,7 +243,8 @@ def _perm64(q: torch.Tensor) -> torch.Tensor:
 
 @pytest.mark.parametrize("C", [64, 128, 256])
 def test_e4m3_mlp_layouts(C):
-    """csu_e4m3_layout_batch: W2 with permuted columns, W2^T, W1^T with permuted columns, bytewise."""
+    """csu_e4m3_layout_batch and csu_quant_e4m3_shadow_batch: W2 with permuted columns, W2^T, W1^T with
+    permuted columns, bytewise."""
     from csu import ops
     d = dev()
     g = torch.Generator().manual_seed(C)
@@ -254,6 +255,17 @@ def test_e4m3_mlp_layouts(C):
     w1q, sw1, w2p, sw2, w2t, w1tp = fp8.mlp_operands(w1, w2)
     torch.cuda.synchronize()
     q1, q2 = w1q.cpu(), fp8.q[1].cpu()
+    assert torch.equal(w2p.cpu(), _perm64(q2))
+    assert torch.equal(w2t.cpu(), q2.t().contiguous())
+    assert torch.equal(w1tp.cpu(), _perm64(q1.t().contiguous()))
+    # the model's per-step path: the shadow quantiser writes the same layouts in its own pass
+    for t in (w2p, w2t, w1tp):
+        t.zero_()
+    cache = ops.CastCache()
+    cache.refresh([w1, w2], torch.bfloat16, (), sources=fp8.sources())
+    fp8.quantize(cache)
+    torch.cuda.synchronize()
+    assert torch.equal(fp8.q[0].cpu(), q1) and torch.equal(fp8.q[1].cpu(), q2)
     assert torch.equal(w2p.cpu(), _perm64(q2))
     assert torch.equal(w2t.cpu(), q2.t().contiguous())
     assert torch.equal(w1tp.cpu(), _perm64(q1.t().contiguous()))
