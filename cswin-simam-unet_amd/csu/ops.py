@@ -1675,7 +1675,9 @@ class CastCache:
             self.tiles = t0
             self.nitems = len(rec)
             self.cast_numel = (sum(params[i].numel() for i in keep), sum(params[i].numel() for i in keep if params[i].dim() > 1))
-            self.items = torch.frombuffer(bytearray(rec.tobytes()), dtype=torch.uint8).to(allp[0].device)
+            # no item (every source written elsewhere): an empty table, no cast launch (_cast checks nitems)
+            self.items = (torch.frombuffer(bytearray(rec.tobytes()), dtype=torch.uint8).to(allp[0].device) if len(rec)
+                          else torch.zeros(1, dtype=torch.uint8, device=allp[0].device))
             if sources is None:
                 import weakref
                 for i, p in enumerate(params):
