@@ -1476,6 +1476,12 @@ class _MlpFusedFn(torch.autograd.Function):
         return dy.to(rdt), dx.view(xshape), dw1.to(w1dt), db1.to(b1dt), dw2.to(w2dt), db2.to(b2dt), None, None, None
 
 
+# widths whose fp8 Mlp backward runs the fp8 kernel; the others run the bf16 fused backward on the
+# dequantised (exact) bf16 shadows of the e4m3 weights -- faster there (C = 64: 106 vs 120 us, C = 128:
+# 64 vs 90 us per launch in the 1024x1024 B4 step, profiles/r06d_step_breakdown_1024_fp8.txt)
+FP8_MLP_BWD_C = (256,)
+
+
 class _MlpFp8Fn(torch.autograd.Function):
     """res + fc2(gelu(fc1(x))) with e4m3 weights (BASELINE config 5, "fp8 MFMA weights") in ONE
     csu_mlp_fp8_fwd launch on v_mfma_scale_f32_32x32x64_f8f6f4: x and the hidden activations are
@@ -1483,10 +1489,12 @@ class _MlpFp8Fn(torch.autograd.Function):
     power-of-two scales ride in the MFMA's E8M0 operands.  Backward (straight-through): one
     csu_mlp_fp8_bwd launch recomputes h exactly, runs dY W2 and dh W1 on the same fp8 MFMA (dY / dh
     quantised the same way, the weight scales folded into them) and writes dh, g_q (the forward's
-    fc2 input) and dx; then the two bf16 weight gradients dW1 = dh^T x, dW2 = dY^T g_q."""
+    fc2 input) and dx; then the two bf16 weight gradients dW1 = dh^T x, dW2 = dY^T g_q.  For C not in
+    FP8_MLP_BWD_C the backward is the bf16 fused one (_MlpFusedFn) on the dequantised weights w1c / w2c
+    (oracle: fp8_ref.Fp8MlpFn with bwd_fp8=False)."""
 
     @staticmethod
-    def forward(ctx, res, x, w1, b1, w2, b2, ops8, drop):
+    def forward(ctx, res, x, w1, b1, w2, b2, ops8, drop, w1c, w2c):
         C = x.shape[-1]
         res2 = res.float().contiguous().view(-1, C)
         x2 = x.reshape(-1, C).contiguous()
@@ -1505,6 +1513,7 @@ class _MlpFp8Fn(torch.autograd.Function):
         ctx.drop, ctx.rpi = drop, rpi
         ctx.save_for_backward(x2, b1f)
         ctx.ops8 = ops8
+        ctx.wc = (w1c, w2c)
         ctx.meta = (res.dtype, x.shape, w1.dtype, b1.dtype, w2.dtype, b2.dtype)
         ctx.params = (w1, b1, w2, b2)
         _note_use(*ctx.params)
@@ -1526,13 +1535,20 @@ class _MlpFp8Fn(torch.autograd.Function):
         g = torch.empty_like(dh)
         dx = torch.empty(M, C, dtype=torch.bfloat16, device=x2.device)
         dd = ctypes.byref(_mlp_desc(drop, ctx.rpi))
-        _launch("mlp_bwd", lambda: lib().csu_mlp_fp8_bwd(M, C, ptr(x2), ptr(dyb), ptr(w1q), ptr(sw1), ptr(b1f), ptr(w2t),
-                                                         ptr(sw2), ptr(w1tp), ptr(dh), ptr(g), ptr(dx), dd,
-                                                         stream_ptr(x2.device)),
-                24 * M * C * C, M * C * (2 + 2 + 2) + M * 4 * C * (2 + 2) + 12 * C * C, prec="fp8")
+        if C in FP8_MLP_BWD_C:
+            _launch("mlp_bwd", lambda: lib().csu_mlp_fp8_bwd(M, C, ptr(x2), ptr(dyb), ptr(w1q), ptr(sw1), ptr(b1f), ptr(w2t),
+                                                             ptr(sw2), ptr(w1tp), ptr(dh), ptr(g), ptr(dx), dd,
+                                                             stream_ptr(x2.device)),
+                    24 * M * C * C, M * C * (2 + 2 + 2) + M * 4 * C * (2 + 2) + 12 * C * C, prec="fp8")
+        else:
+            w1c, w2c = ctx.wc
+            _launch("mlp_bwd", lambda: lib().csu_mlp_bwd_dp(M, C, ptr(x2), ptr(dyb), ptr(w1c), ptr(b1f), ptr(w2c), ptr(dh),
+                                                            ptr(g), ptr(dx), dd, stream_ptr(x2.device)),
+                    24 * M * C * C, M * C * (2 + 2 + 2) + M * 4 * C * (2 + 2) + 16 * C * C)
         dw2, db2 = wgrad_maybe_side(dyb, g, w2dt, b2dt, params=ctx.params[2:])
         dw1, db1 = wgrad_maybe_side(dh, x2, w1dt, b1dt, params=ctx.params[:2])
-        return dy.to(rdt), dx.view(xshape), dw1.to(w1dt), db1.to(b1dt), dw2.to(w2dt), db2.to(b2dt), None, None
+        return (dy.to(rdt), dx.view(xshape), dw1.to(w1dt), db1.to(b1dt), dw2.to(w2dt), db2.to(b2dt), None, None, None,
+                None)
 
 
 def mlp_fp8(res, x, fc1: torch.nn.Linear, fc2: torch.nn.Linear, drop: Optional[MlpDrop] = None):
@@ -1543,8 +1559,11 @@ def mlp_fp8(res, x, fc1: torch.nn.Linear, fc2: torch.nn.Linear, drop: Optional[M
     ops8 = _ACTIVE_FP8.mlp_operands(fc1.weight, fc2.weight)
     if ops8 is None:
         return None
+    w1c = w2c = None
+    if x.shape[-1] not in FP8_MLP_BWD_C:   # the bf16 backward's operands: the exact dequantised shadows
+        w1c, w2c = _weight_bf16(fc1.weight), _weight_bf16(fc2.weight)
     with torch.autocast("cuda", enabled=False):
-        return _MlpFp8Fn.apply(res, x, fc1.weight, fc1.bias, fc2.weight, fc2.bias, ops8, drop)
+        return _MlpFp8Fn.apply(res, x, fc1.weight, fc1.bias, fc2.weight, fc2.bias, ops8, drop, w1c, w2c)
 
 
 # the fused one-launch Mlp where the library has it (C in {64, 128, 256}); otherwise two gemm4 launches

@@ -64,37 +64,47 @@ class Fp8MlpFn(torch.autograd.Function):
               dg = mx(dy * s2) q2,  dh = dg * gelu'(h) * m_h,  dx = mx(dh * s1) q1,
               dW1 = dh^T x,  db1 = sum dh,  dW2 = dy^T mx(g),  db2 = sum dy
     w1 = q1 * s1[:, None], w2 = q2 * s2[:, None] are the dequantised e4m3 weights (quant_rows);
-    m_h the hidden dropout mask (scale 0 or 1/keep) or None."""
+    m_h the hidden dropout mask (scale 0 or 1/keep) or None.
+    ``bwd_fp8`` False: the backward of csu's bf16 fused Mlp on the dequantised weights instead (what
+    the product runs where that kernel is the faster one, csu.ops.FP8_MLP_BWD_C): h recomputed from
+    the unrounded x, dg = dy w2, dh = dg gelu'(h) m_h, dx = dh w1, dW2 = dy^T (gelu(h) m_h)."""
 
     @staticmethod
-    def forward(ctx, x, w1, b1, w2, b2, s1, s2, m_h):
+    def forward(ctx, x, w1, b1, w2, b2, s1, s2, m_h, bwd_fp8=True):
         xd = x.double()
         h = mx_quant(xd) @ w1.double().t() + b1.double()
         g = F.gelu(h)
         if m_h is not None:
             g = g * m_h
         gq = mx_quant(g)
-        ctx.save_for_backward(xd, h, gq, w1.double(), w2.double(), s1.double(), s2.double())
+        ctx.save_for_backward(xd, h, gq, w1.double(), w2.double(), s1.double(), s2.double(), b1.double())
         ctx.m_h = m_h
+        ctx.bwd_fp8 = bwd_fp8
         return gq @ w2.double().t() + b2.double()
 
     @staticmethod
     def backward(ctx, dy):
-        xd, h, gq, w1, w2, s1, s2 = ctx.saved_tensors
+        xd, h, gq, w1, w2, s1, s2, b1 = ctx.saved_tensors
         dy = dy.double()
-        q1, q2 = w1 / s1[:, None], w2 / s2[:, None]
-        dg = mx_quant(dy * s2) @ q2
+        if not ctx.bwd_fp8:
+            h = xd @ w1.t() + b1
+            gq = F.gelu(h) if ctx.m_h is None else F.gelu(h) * ctx.m_h
         dgelu = 0.5 * (1 + torch.erf(h / math.sqrt(2))) + h * torch.exp(-0.5 * h * h) / math.sqrt(2 * math.pi)
+        if ctx.bwd_fp8:
+            q1, q2 = w1 / s1[:, None], w2 / s2[:, None]
+            dg = mx_quant(dy * s2) @ q2
+        else:
+            dg = dy @ w2
         dh = dg * dgelu
         if ctx.m_h is not None:
             dh = dh * ctx.m_h
-        dx = mx_quant(dh * s1) @ q1
+        dx = mx_quant(dh * s1) @ q1 if ctx.bwd_fp8 else dh @ w1
         lead = dy.reshape(-1, dy.shape[-1])
         dh2 = dh.reshape(-1, dh.shape[-1])
         dw1 = dh2.t() @ xd.reshape(-1, xd.shape[-1])
         dw2 = lead.t() @ gq.reshape(-1, gq.shape[-1])
-        return dx, dw1, dh2.sum(0), dw2, lead.sum(0), None, None, None
+        return dx, dw1, dh2.sum(0), dw2, lead.sum(0), None, None, None, None
 
 
-def fp8_mlp(x, w1, b1, w2, b2, s1, s2, m_h=None):
-    return Fp8MlpFn.apply(x, w1, b1, w2, b2, s1, s2, m_h)
+def fp8_mlp(x, w1, b1, w2, b2, s1, s2, m_h=None, bwd_fp8=True):
+    return Fp8MlpFn.apply(x, w1, b1, w2, b2, s1, s2, m_h, bwd_fp8)

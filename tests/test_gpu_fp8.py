@@ -139,7 +139,7 @@ def test_fp8_weight_model_vs_oracle_with_quantized_weights(monkeypatch):
         s1 = Q.quant_rows(p[key + ".fc1.weight"])[2]
         s2 = Q.quant_rows(p[key + ".fc2.weight"])[2]
         return Q.fp8_mlp(xx, pp[key + ".fc1.weight"], pp[key + ".fc1.bias"], pp[key + ".fc2.weight"],
-                         pp[key + ".fc2.bias"], s1, s2, m_h)
+                         pp[key + ".fc2.bias"], s1, s2, m_h, bwd_fp8=xx.shape[-1] in ops.FP8_MLP_BWD_C)
     monkeypatch.setattr(O, "MLP_FP8", mlp_fp8)
 
     yr = O.cswin_forward(pref, x.double(), cfg)
