@@ -664,6 +664,10 @@ __device__ __forceinline__ int swz128(int row, int chunk) { return row * 64 + ((
 // is 4 launches of 128 workgroups)
 struct IG4 {
     IG g[4];
+    // split-K (one problem, few tiles): blockIdx.z = K part of kper gathered columns (a multiple of
+    // 64); each part writes its fp32 partial tile to slab + z * M * Ncols, summed by conv_split_reduce
+    int ksplit, kper;
+    float* slab;
 };
 
 template <int BN, int VW>
@@ -676,9 +680,12 @@ __global__ __launch_bounds__(NT) void igemm_bf16(IG4 gs, const bf16* __restrict_
     __shared__ unsigned ooff[BM];   // output pixel of each tile row (kOOB: none)
     // problem of this z-slice (selects, not a dynamic index into the kernel-argument struct)
     const int z = blockIdx.z;
-    const IG g = z == 0 ? gs.g[0] : z == 1 ? gs.g[1] : z == 2 ? gs.g[2] : gs.g[3];
+    const bool split = gs.ksplit > 1;
+    const IG g = split || z == 0 ? gs.g[0] : z == 1 ? gs.g[1] : z == 2 ? gs.g[2] : gs.g[3];
     const long m0 = (long)blockIdx.x * BM;
     if (m0 >= g.M) return;   // phases differ in size: the grid covers the largest
+    const int kb = split ? z * gs.kper : 0;                       // this workgroup's K range
+    const int ke = split ? min(g.Kd, kb + gs.kper) : g.Kd;
     const int n0 = blockIdx.y * BN;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int r = lane & 31, h = lane >> 5;
@@ -723,7 +730,7 @@ __global__ __launch_bounds__(NT) void igemm_bf16(IG4 gs, const bf16* __restrict_
 #pragma unroll
         for (int pc = 0; pc < NP; ++pc) {
             const int k = k0 + 8 * ch + VW * pc;
-            const bool kin = k < g.Kd;
+            const bool kin = k < ke;
             const int t = kin ? k / g.Cs : 0, c = k - t * g.Cs;
             const int ty = t / g.ntx, tx = t - ty * g.ntx;
             const int oy = ty * g.sty, ox = tx * g.stx;
@@ -781,23 +788,36 @@ __global__ __launch_bounds__(NT) void igemm_bf16(IG4 gs, const bf16* __restrict_
             }
         }
     };
-    if (g.Kd > 0) {
-        load(0, ra2[0], rbw2[0]);
-        load(BK, ra2[1], rbw2[1]);
+    if (ke > kb) {
+        load(kb, ra2[0], rbw2[0]);
+        load(kb + BK, ra2[1], rbw2[1]);
         store(0, ra2[0], rbw2[0]);
     }
     __syncthreads();
     // step k: LDS buffer k & 1 holds slice k, register set (k + 1) & 1 slice k + 1 (in flight)
-    for (int k0 = 0; k0 < g.Kd; k0 += 2 * BK) {
+    for (int k0 = kb; k0 < ke; k0 += 2 * BK) {
         load(k0 + 2 * BK, ra2[0], rbw2[0]);   // past the end: all offsets out of range, zeros
         mfmas(0);
-        if (k0 + BK < g.Kd) store(1, ra2[1], rbw2[1]);
+        if (k0 + BK < ke) store(1, ra2[1], rbw2[1]);
         __syncthreads();
-        if (k0 + BK >= g.Kd) break;
+        if (k0 + BK >= ke) break;
         load(k0 + 3 * BK, ra2[1], rbw2[1]);
         mfmas(1);
-        if (k0 + 2 * BK < g.Kd) store(0, ra2[0], rbw2[0]);
+        if (k0 + 2 * BK < ke) store(0, ra2[0], rbw2[0]);
         __syncthreads();
+    }
+    if (split) {   // fp32 partial tile [row][Ncols] of K part z (rows / columns outside: dropped)
+        const int n = n0 + wn + r;
+        const __amdgpu_buffer_rsrc_t rs_s = buf_rsrc(gs.slab + (long)z * g.M * g.Ncols, g.M * g.Ncols * 4);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int reg = 0; reg < 16; ++reg) {
+                const long m = m0 + wm + 32 * i + crow(reg, h);
+                const unsigned off = (n < g.Ncols && m < g.M) ? (unsigned)((m * g.Ncols + n) * 4) : kOOB;
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[i][reg]), rs_s, off, 0, 0);
+            }
+        return;
     }
     // output pixel byte offsets of the BM rows (32-bit: launch_ig bounds the output to 2 GiB)
     for (int i = threadIdx.x; i < BM; i += NT) {
@@ -835,6 +855,56 @@ __global__ __launch_bounds__(NT) void igemm_bf16(IG4 gs, const bf16* __restrict_
         }
 }
 
+// out = bf16(sum of the K parts' fp32 partials (fixed order) + bias), 4 columns per thread, the output
+// pixel of each row as in igemm_bf16's epilogue (one problem, one destination; Ncols % 4 == 0)
+__global__ __launch_bounds__(NT) void conv_split_reduce(IG g, int ksplit, const float* __restrict__ slab,
+                                                        const float* __restrict__ bias, bf16* __restrict__ out) {
+    const int nq = g.Ncols / 4;
+    const long i = (long)blockIdx.x * NT + threadIdx.x;
+    if (i >= g.M * nq) return;
+    const long m = i / nq;
+    const int n = (int)(i - m * nq) * 4;
+    float v[4] = {0.f, 0.f, 0.f, 0.f};
+    if (bias) load4(bias + n, v);
+    const long ms = (long)g.M * g.Ncols;
+    f32x4 sum = *reinterpret_cast<const f32x4*>(slab + m * g.Ncols + n);
+    for (int k = 1; k < ksplit; ++k) sum += *reinterpret_cast<const f32x4*>(slab + k * ms + m * g.Ncols + n);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] += sum[e];
+    const unsigned mu = (unsigned)m, t = mu / (unsigned)g.RW;
+    const int rx = (int)(mu - t * (unsigned)g.RW);
+    const unsigned b = t / (unsigned)g.RH;
+    const int ry = (int)(t - b * (unsigned)g.RH);
+    const long opix = ((long)b * g.OHo + ry * g.oya + g.oyb) * g.OWo + rx * g.oxa + g.oxb;
+    store4(out + opix * g.Ncols + n, v);
+}
+
+// K split of a one-problem v2 launch: fewer than two workgroups per CU of tiles and >= 4 K slices ->
+// parts of >= 2 slices, up to 8, so that the launch has about three workgroups per CU (1: no split)
+struct KSplit {
+    int ksplit, kper;
+};
+KSplit ksplit_plan(const IG& g, int cus) {
+    const bool narrow = g.Ncols <= 32;
+    const int BM = narrow ? 256 : 128, BN = narrow ? 32 : 64, BK = 64;
+    const long tiles = ((g.M + BM - 1) / BM) * ((g.Ncols + BN - 1) / BN);
+    const int nk = (g.Kd + BK - 1) / BK;
+    if (g.csplit || g.nsplit || g.Ncols % 4 || tiles >= 2L * cus || nk < 4) return KSplit{1, g.Kd};
+    long want = (3L * cus + tiles - 1) / tiles;
+    want = want < nk / 2 ? want : nk / 2;
+    want = want < 8 ? want : 8;
+    if (want < 2) return KSplit{1, g.Kd};
+    const int kper = (int)((nk + want - 1) / want) * BK;
+    const int n = (g.Kd + kper - 1) / kper;
+    // the partials' round trip (2 x n x M x Ncols x 4 bytes) must stay small next to the work saved
+    if ((long)n * g.M * g.Ncols * 4 > (32L << 20)) return KSplit{1, g.Kd};
+    return KSplit{n, kper};
+}
+size_t ksplit_bytes(const IG& g, int cus) {
+    const KSplit k = ksplit_plan(g, cus);
+    return k.ksplit > 1 ? (size_t)k.ksplit * g.M * g.Ncols * 4 : 0;
+}
+
 // ---- bf16 implicit GEMM, v3 (Cs % 64 == 0, Ncols % BN == 0): persistent, LDS-DMA gathers ---------
 // Both operand images are filled by buffer_load ... lds (no VGPR round trip, lds_dma.hpp): the
 // A-image lanes gather their own 16 B (one pixel, one tap, 8 channels) through a per-lane offset --
@@ -848,8 +918,8 @@ __global__ __launch_bounds__(NT) void igemm_bf16(IG4 gs, const bf16* __restrict_
 // Accumulators hold [features][pixels] (the weight fragment is the MFMA A operand): lane (r, h) owns
 // pixel r and features 8g + 4h .. + 3, written as 8-B vectors straight from registers.
 constexpr int kIDMaxN = 1024;   // output columns of the LDS bias copy
-template <int BM, int BN, int S, int WM, int WN>
-__global__ __launch_bounds__(64 * WM * WN, 1) void igemm_dma(IG g, const bf16* __restrict__ src, const bf16* __restrict__ Bw,
+template <int BM, int BN, int S, int WM, int WN, int OCC = 1>
+__global__ __launch_bounds__(64 * WM * WN, OCC) void igemm_dma(IG g, const bf16* __restrict__ src, const bf16* __restrict__ Bw,
                                                              const float* __restrict__ bias, bf16* __restrict__ out) {
     constexpr int NWV = WM * WN;
     constexpr int TMW = BM / (32 * WM), TNW = BN / (32 * WN);   // 32x32 tiles per wave (pixels, features)
@@ -1371,11 +1441,13 @@ bool halo64_ok(const IG& g, bool flip) {   // the forward conv (flip: its input 
                  : (g.sty == 1 && g.stx == 1 && g.ay == 1 && g.ax == 1 && g.by == -1 && g.bx == -1));
 }
 
-struct IDCfg { int bm, bn, s, wm, wn; };
-constexpr IDCfg kIDCfgs[] = {{128, 128, 3, 2, 2}, {256, 128, 2, 4, 2}, {256, 128, 3, 4, 2}, {128, 64, 4, 2, 2},
-                             {256, 64, 3, 4, 2},  {128, 64, 3, 2, 2},  {256, 256, 2, 2, 4}, {256, 256, 2, 4, 2},
-                             {512, 64, 2, 8, 1}};
-constexpr int kIDNCfg = 9;
+// occ: workgroups per CU of the persistent grid (2: the small-tile configurations for few-tile shapes,
+// e.g. the CSWin merges, whose 128 x 64 tiles give one tile per CU)
+struct IDCfg { int bm, bn, s, wm, wn, occ; };
+constexpr IDCfg kIDCfgs[] = {{128, 128, 3, 2, 2, 1}, {256, 128, 2, 4, 2, 1}, {256, 128, 3, 4, 2, 1}, {128, 64, 4, 2, 2, 1},
+                             {256, 64, 3, 4, 2, 1},  {128, 64, 3, 2, 2, 1},  {256, 256, 2, 2, 4, 1}, {256, 256, 2, 4, 2, 1},
+                             {512, 64, 2, 8, 1, 1},  {64, 64, 4, 2, 2, 2},   {128, 64, 3, 2, 2, 2},  {64, 128, 3, 2, 2, 2}};
+constexpr int kIDNCfg = 12;
 
 int id_cus() {
     static int cus = 0;
@@ -1392,8 +1464,8 @@ template <int C>
 int id_launch(const IG& g, const void* src, const void* w, const float* bias, void* out, hipStream_t st) {
     constexpr IDCfg c = kIDCfgs[C];
     if (g.Ncols % c.bn) return fail(CSU_E_ARG, "conv2d: Ncols not a multiple of the tile's BN");
-    igemm_dma<c.bm, c.bn, c.s, c.wm, c.wn><<<dim3(id_cus()), 64 * c.wm * c.wn, 0, st>>>(g, (const bf16*)src, (const bf16*)w, bias,
-                                                                                  (bf16*)out);
+    igemm_dma<c.bm, c.bn, c.s, c.wm, c.wn, c.occ><<<dim3(c.occ * id_cus()), 64 * c.wm * c.wn, 0, st>>>(
+        g, (const bf16*)src, (const bf16*)w, bias, (bf16*)out);
     return check_launch("conv2d (igemm_dma)");
 }
 
@@ -1423,6 +1495,9 @@ int id_run(int cfg, const IG& g, const void* src, const void* w, const float* bi
         case 6: return id_launch<6>(g, src, w, bias, out, st);
         case 7: return id_launch<7>(g, src, w, bias, out, st);
         case 8: return id_launch<8>(g, src, w, bias, out, st);
+        case 9: return id_launch<9>(g, src, w, bias, out, st);
+        case 10: return id_launch<10>(g, src, w, bias, out, st);
+        case 11: return id_launch<11>(g, src, w, bias, out, st);
         default: return fail(CSU_E_ARG, "conv2d: bad igemm_dma configuration");
     }
 }
@@ -1430,7 +1505,7 @@ int id_run(int cfg, const IG& g, const void* src, const void* w, const float* bi
 // n problems with equal Ncols and channel count (the phases of one input gradient, or one forward)
 // cfg: -1 per-shape choice (v3 where eligible), 0 the v2 kernel, 1 + k the v3 configuration k
 int launch_ig(const IG* gv, int n, const void* src, const void* w, const float* bias, void* out, hipStream_t st,
-              int cfg = -1) {
+              int cfg = -1, float* ws = nullptr, size_t ws_bytes = 0) {
     IG4 gs{};
     long maxm = 0;
     for (int i = 0; i < n; ++i) {
@@ -1483,7 +1558,12 @@ int launch_ig(const IG* gv, int n, const void* src, const void* w, const float* 
     const int vw = g.Cs % 8 == 0 ? 8 : 4;
     const bool narrow = g.Ncols <= 32;
     const int BM = narrow ? 256 : 128, BN = narrow ? 32 : 64;
-    const dim3 grid((unsigned)((maxm + BM - 1) / BM), (g.Ncols + BN - 1) / BN, n);
+    const KSplit ks = n == 1 && cfg < 0 && ws ? ksplit_plan(g, id_cus()) : KSplit{1, g.Kd};
+    const bool split = ks.ksplit > 1 && ws_bytes >= (size_t)ks.ksplit * g.M * g.Ncols * 4;
+    gs.ksplit = split ? ks.ksplit : 1;
+    gs.kper = split ? ks.kper : g.Kd;
+    gs.slab = split ? ws : nullptr;
+    const dim3 grid((unsigned)((maxm + BM - 1) / BM), (g.Ncols + BN - 1) / BN, split ? ks.ksplit : n);
     const bf16* s = (const bf16*)src;
     const bf16* wb = (const bf16*)w;
     bf16* o = (bf16*)out;
@@ -1494,10 +1574,15 @@ int launch_ig(const IG* gv, int n, const void* src, const void* w, const float* 
         if (vw == 8) igemm_bf16<64, 8><<<grid, NT, 0, st>>>(gs, s, wb, bias, o);
         else igemm_bf16<64, 4><<<grid, NT, 0, st>>>(gs, s, wb, bias, o);
     }
+    if (split) {
+        const long nthr = g.M * (g.Ncols / 4);
+        conv_split_reduce<<<(unsigned)((nthr + NT - 1) / NT), NT, 0, st>>>(g, ks.ksplit, ws, bias, o);
+    }
     return check_launch("conv2d (igemm)");
 }
-int launch_ig(const IG& g, const void* src, const void* w, const float* bias, void* out, hipStream_t st, int cfg = -1) {
-    return launch_ig(&g, 1, src, w, bias, out, st, cfg);
+int launch_ig(const IG& g, const void* src, const void* w, const float* bias, void* out, hipStream_t st, int cfg = -1,
+              float* ws = nullptr, size_t ws_bytes = 0) {
+    return launch_ig(&g, 1, src, w, bias, out, st, cfg, ws, ws_bytes);
 }
 IG ig_forward(const csu_conv_geom& c) {
     IG g{};
@@ -1689,7 +1774,7 @@ int launch_gemm(const Geo& g, long M, int Ncols, int Kdim, const void* src, cons
 using namespace csu;
 
 static int conv_fwd_impl(const csu_conv_geom* gm, int dtype, const void* x, const void* w_ohwi, const float* bias, void* out,
-                         int cfg, void* stream) {
+                         int cfg, void* stream, void* ws = nullptr, size_t ws_bytes = 0) {
     if (int e = check_geo(gm)) return e;
     if (!x || !w_ohwi || !out) return fail(CSU_E_ARG, "conv2d_fwd: null buffer");
     const Geo g = to_geo(gm);
@@ -1697,7 +1782,7 @@ static int conv_fwd_impl(const csu_conv_geom* gm, int dtype, const void* x, cons
     const int K = g.KH * g.KW * g.C;
     const bool vec = g.C % 8 == 0;
     hipStream_t st = as_stream(stream);
-    if (dtype == CSU_BF16 && g.C % 4 == 0) return launch_ig(ig_forward(*gm), x, w_ohwi, bias, out, st, cfg);
+    if (dtype == CSU_BF16 && g.C % 4 == 0) return launch_ig(ig_forward(*gm), x, w_ohwi, bias, out, st, cfg, (float*)ws, ws_bytes);
     if (cfg > 0) return fail(CSU_E_ARG, "conv2d_fwd: igemm_dma needs bf16 with C % 64 == 0");
     if (dtype == CSU_BF16) return launch_gemm<bf16, 0>(g, M, g.N, K, x, w_ohwi, bias, out, vec, st);
     if (dtype == CSU_F32) return launch_gemm<float, 0>(g, M, g.N, K, x, w_ohwi, bias, out, vec, st);
@@ -1705,7 +1790,7 @@ static int conv_fwd_impl(const csu_conv_geom* gm, int dtype, const void* x, cons
 }
 
 static int conv_dgrad_impl(const csu_conv_geom* gm, int dtype, const void* dy, const void* w_ihwo, const float* bias, void* dx,
-                           int cfg, void* stream) {
+                           int cfg, void* stream, void* ws = nullptr, size_t ws_bytes = 0) {
     if (int e = check_geo(gm)) return e;
     if (!dy || !w_ihwo || !dx) return fail(CSU_E_ARG, "conv2d_dgrad: null buffer");
     const Geo g = to_geo(gm);
@@ -1726,6 +1811,7 @@ static int conv_dgrad_impl(const csu_conv_geom* gm, int dtype, const void* dy, c
                 }
                 ph[np++] = ig;
             }
+        if (np == 1) return launch_ig(ph, 1, dy, w_ihwo, bias, dx, st, cfg, (float*)ws, ws_bytes);
         return np ? launch_ig(ph, np, dy, w_ihwo, bias, dx, st, cfg) : 0;
     }
     if (cfg > 0) return fail(CSU_E_ARG, "conv2d_dgrad: igemm_dma needs bf16 with N % 64 == 0");
@@ -1742,6 +1828,29 @@ extern "C" int csu_conv2d_fwd(const csu_conv_geom* gm, int dtype, const void* x,
 extern "C" int csu_conv2d_dgrad(const csu_conv_geom* gm, int dtype, const void* dy, const void* w_ihwo,
                                 const float* bias, void* dx, void* stream) {
     return conv_dgrad_impl(gm, dtype, dy, w_ihwo, bias, dx, -1, stream);
+}
+
+// workspace of the K-split v2 launches (one-problem bf16 convs with few tiles; 0: never split)
+extern "C" size_t csu_conv2d_workspace(int op, const csu_conv_geom* gm, int dtype) {
+    if (check_geo(gm) || dtype != CSU_BF16 || (op != 0 && op != 1)) return 0;
+    if (op == 0) {
+        if (gm->C % 4) return 0;
+        const IG g = ig_forward(*gm);
+        return id_eligible(g) && id_pick(g) >= 0 ? 0 : ksplit_bytes(g, id_cus());
+    }
+    if (gm->N % 4 || gm->stride != 1) return 0;
+    const IG g = ig_dgrad_phase(*gm, 0, 0);
+    return id_eligible(g) && id_pick(g) >= 0 ? 0 : ksplit_bytes(g, id_cus());
+}
+
+extern "C" int csu_conv2d_fwd_ws(const csu_conv_geom* gm, int dtype, const void* x, const void* w_ohwi, const float* bias,
+                                 void* out, void* workspace, size_t ws_bytes, void* stream) {
+    return conv_fwd_impl(gm, dtype, x, w_ohwi, bias, out, -1, stream, workspace, ws_bytes);
+}
+
+extern "C" int csu_conv2d_dgrad_ws(const csu_conv_geom* gm, int dtype, const void* dy, const void* w_ihwo, const float* bias,
+                                   void* dx, void* workspace, size_t ws_bytes, void* stream) {
+    return conv_dgrad_impl(gm, dtype, dy, w_ihwo, bias, dx, -1, stream, workspace, ws_bytes);
 }
 
 extern "C" int csu_conv2d_ex(int op, const csu_conv_geom* gm, int dtype, const void* src, const void* w, const float* bias,

@@ -206,6 +206,9 @@ _SIGS = {
                                         c_void_p]),
     "csu_conv2d_ex": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ConvGeom), ctypes.c_int, c_void_p, c_void_p, c_void_p,
                                      c_void_p, ctypes.c_int, c_void_p]),
+    "csu_conv2d_workspace": (c_size_t, [ctypes.c_int, ctypes.POINTER(ConvGeom), ctypes.c_int]),
+    "csu_conv2d_fwd_ws": (ctypes.c_int, [ctypes.POINTER(ConvGeom), ctypes.c_int] + [c_void_p] * 5 + [c_size_t, c_void_p]),
+    "csu_conv2d_dgrad_ws": (ctypes.c_int, [ctypes.POINTER(ConvGeom), ctypes.c_int] + [c_void_p] * 5 + [c_size_t, c_void_p]),
     "csu_conv2d_wgrad_workspace": (c_size_t, [ctypes.POINTER(ConvGeom)]),
     "csu_conv2d_wgrad_workspace_ex": (c_size_t, [ctypes.POINTER(ConvGeom), ctypes.c_int]),
     "csu_conv2d_split_ok": (ctypes.c_int, [ctypes.POINTER(ConvGeom), ctypes.c_int]),

@@ -2087,6 +2087,15 @@ def _pad_channels(C: int) -> int:
     return (C + 7) // 8 * 8 if (C % 8 and PAD_CHANNELS) else C
 
 
+def _conv_ws(op: int, g, t: torch.Tensor):
+    """(workspace tensor or None, bytes) of csu_conv2d_fwd_ws / _dgrad_ws for geometry g: the K-split
+    partials of few-tile convolutions (csu_conv2d_workspace; 0 bytes: no split)."""
+    n = lib().csu_conv2d_workspace(op, ctypes.byref(g), dtype_code(t))
+    if not n:
+        return None, 0
+    return torch.empty(n, dtype=torch.uint8, device=t.device), n
+
+
 class _Conv2dFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, stride: int, pad: int, cd):
@@ -2122,8 +2131,9 @@ class _Conv2dFn(torch.autograd.Function):
         g = _conv_geom(B, H, W, cp, N, KH, KW, stride, pad)
         y = torch.empty(B, g.OH, g.OW, N, dtype=cd, device=x.device)
         bf = None if bias is None else bias.detach().float().contiguous()
-        _launch("conv_fwd", lambda: lib().csu_conv2d_fwd(ctypes.byref(g), dtype_code(xc), ptr(xc), ptr(w_ohwi), ptr(bf),
-                                                         ptr(y), stream_ptr(x.device)),
+        ws, nws = _conv_ws(0, g, xc)
+        _launch("conv_fwd", lambda: lib().csu_conv2d_fwd_ws(ctypes.byref(g), dtype_code(xc), ptr(xc), ptr(w_ohwi), ptr(bf),
+                                                            ptr(y), ptr(ws), nws, stream_ptr(x.device)),
                 2 * y.numel() * KH * KW * cp, (xc.numel() + w_ohwi.numel() + y.numel()) * xc.element_size(), prec=prec_of(xc))
         ctx.save_for_backward(xc, weight)
         ctx.w_ihwo = cached[1] if cached else None   # refreshed only by the next forward's cast
@@ -2147,8 +2157,9 @@ class _Conv2dFn(torch.autograd.Function):
             else:
                 w_ihwo = ctx.w_ihwo if ctx.w_ihwo is not None else weight.detach().permute(1, 2, 3, 0).to(cd).contiguous()
             dx = torch.empty(B, H, W, cp, dtype=cd, device=dy.device)
-            _launch("conv_dgrad", lambda: lib().csu_conv2d_dgrad(ctypes.byref(g), dtype_code(dy), ptr(dy), ptr(w_ihwo), None,
-                                                                 ptr(dx), stream_ptr(dy.device)),
+            ws, nws = _conv_ws(1, g, dy)
+            _launch("conv_dgrad", lambda: lib().csu_conv2d_dgrad_ws(ctypes.byref(g), dtype_code(dy), ptr(dy), ptr(w_ihwo),
+                                                                    None, ptr(dx), ptr(ws), nws, stream_ptr(dy.device)),
                     2 * dy.numel() * KH * KW * cp, (dy.numel() + w_ihwo.numel() + dx.numel()) * dy.element_size(),
                     prec=prec_of(dy))
             if cp != C:

@@ -559,6 +559,16 @@ int csu_conv2d_dgrad(const csu_conv_geom* g, int dtype, const void* dy, const vo
  * channels (H % 2 == 0, W % 64 == 0); CSU_E_ARG when not eligible. */
 int csu_conv2d_ex(int op, const csu_conv_geom* g, int dtype, const void* src, const void* w, const float* bias, void* out,
                   int cfg, void* stream);
+/* The plain operators with a workspace (op 0: csu_conv2d_fwd, 1: csu_conv2d_dgrad): one-problem bf16
+ * convolutions with fewer output tiles than two per CU (the CSWin CARAFE encoders at 16x16 / 32x32)
+ * split their K range over workgroups, write fp32 partials into the workspace and sum them in fixed
+ * order (+ bias) in a second kernel.  csu_conv2d_workspace: the bytes that split needs (0: no split
+ * for this geometry; a NULL or smaller workspace runs unsplit). */
+size_t csu_conv2d_workspace(int op, const csu_conv_geom* g, int dtype);
+int csu_conv2d_fwd_ws(const csu_conv_geom* g, int dtype, const void* x, const void* w_ohwi, const float* bias, void* y,
+                      void* workspace, size_t ws_bytes, void* stream);
+int csu_conv2d_dgrad_ws(const csu_conv_geom* g, int dtype, const void* dy, const void* w_ihwo, const float* bias,
+                        void* dx, void* workspace, size_t ws_bytes, void* stream);
 size_t csu_conv2d_wgrad_workspace(const csu_conv_geom* g);
 /* dw_db fp32 [N*KH*KW*C + N] = dW in [N][KH][KW][C] order, then db (sum of dy) */
 int csu_conv2d_wgrad(const csu_conv_geom* g, int dtype, const void* x, const void* dy, float* dw_db,

@@ -538,7 +538,9 @@ CONV_CASES = [  # (B, H, C, N, k, stride, pad)
     (2, 16, 64, 128, 3, 2, 1),    # Merge_Block (cswin:376)
     (1, 8, 16, 144, 3, 1, 1),     # CARAFE4 encoder (cswin:446)
     (2, 64, 16, 144, 3, 1, 1),    # CARAFE4 encoder at a width the few-channel kernel takes (conv3_c16)
-    (2, 9, 32, 36, 3, 1, 1),      # CARAFE encoder, odd size / N % 8 != 0
+    (2, 9, 32, 36, 3, 1, 1),      # CARAFE encoder, odd size / N % 8 != 0 (bf16: K split in 2, ragged last part)
+    (16, 16, 128, 36, 3, 1, 1),   # CARAFE encoder at 16x16 (512x512 decoder): 32 tiles -> K split (fwd and dgrad)
+    (16, 32, 64, 36, 3, 1, 1),    # CARAFE encoder at 32x32: 128 tiles -> K split
     (1, 12, 8, 24, 3, 1, 1),      # UNet DoubleConv-like
     (2, 6, 40, 16, 1, 1, 0),      # 1x1
     (2, 11, 64, 128, 3, 2, 1),    # stride 2 on an odd size (phase split of the input gradient)
@@ -573,7 +575,7 @@ def test_conv2d_nhwc_vs_torch(case, dtype):
 
 
 # persistent LDS-DMA implicit GEMM (csu_conv2d_ex cfg 1 + k): BN of each tile configuration
-IGEMM_DMA_BN = {1: 128, 2: 128, 3: 128, 4: 64, 5: 64, 6: 64, 7: 256, 8: 256, 9: 64}
+IGEMM_DMA_BN = {1: 128, 2: 128, 3: 128, 4: 64, 5: 64, 6: 64, 7: 256, 8: 256, 9: 64, 10: 64, 11: 64, 12: 128}
 DMA_CONV_CASES = [  # (B, H, C, N, k, stride, pad): 64-channel gathers, partial M tiles
     (1, 20, 64, 256, 3, 1, 1),     # UNet-like 3x3, M = 400 (partial 256-row tile), two N tiles of 128
     (2, 9, 128, 512, 3, 2, 1),     # stride 2 on an odd size: 4 input-gradient phases of 1-4 taps

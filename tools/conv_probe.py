@@ -24,7 +24,10 @@ shapes = [("u1 64->64", 0, 512, 512, 64, 64, 3, 1, 1), ("u1 128->64", 0, 512, 51
           ("embed 8->64 7x7 s4", 0, 512, 512, 8, 64, 7, 4, 2), ("carafe4 enc 16->144", 0, 128, 128, 16, 144, 3, 1, 1),
           ("dg carafe4 enc", 1, 128, 128, 16, 144, 3, 1, 1), ("carafe enc 32->36", 0, 64, 64, 32, 36, 3, 1, 1),
           ("dg carafe enc 32->36", 1, 64, 64, 32, 36, 3, 1, 1), ("merge 128->256 s2", 0, 64, 64, 128, 256, 3, 2, 1),
-          ("dg merge 128->256 s2", 1, 64, 64, 128, 256, 3, 2, 1)]
+          ("dg merge 128->256 s2", 1, 64, 64, 128, 256, 3, 2, 1), ("merge 256->512 s2", 0, 32, 32, 256, 512, 3, 2, 1),
+          ("dg merge 256->512 s2", 1, 32, 32, 256, 512, 3, 2, 1), ("carafe enc 128->36 16x16", 0, 16, 16, 128, 36, 3, 1, 1),
+          ("dg carafe enc 128->36 16x16", 1, 16, 16, 128, 36, 3, 1, 1), ("carafe enc 64->36 32x32", 0, 32, 32, 64, 36, 3, 1, 1),
+          ("dg carafe enc 64->36 32x32", 1, 32, 32, 64, 36, 3, 1, 1)]
 if os.environ.get("ONLY"):
     shapes = [x for x in shapes if any(k in x[0] for k in os.environ["ONLY"].split(","))]
 
@@ -56,6 +59,14 @@ def run(op, g, src, w, bias, out, cfg):
                             bias.data_ptr() if bias is not None else None, out.data_ptr(), cfg,
                             torch.cuda.current_stream().cuda_stream)
     return e
+
+
+def run_ws(op, g, src, w, bias, out, ws):
+    """the plain operator with its K-split workspace (csu_conv2d_fwd_ws / _dgrad_ws)"""
+    f = lib().csu_conv2d_fwd_ws if op == 0 else lib().csu_conv2d_dgrad_ws
+    return f(ctypes.byref(g), CSU_BF16, src.data_ptr(), w.data_ptr(), bias.data_ptr() if bias is not None else None,
+             out.data_ptr(), ws.data_ptr() if ws is not None else None, ws.numel() if ws is not None else 0,
+             torch.cuda.current_stream().cuda_stream)
 
 
 def case(name, op, H, W, C, N, k, s, p, b):
@@ -103,6 +114,11 @@ if __name__ == "__main__":
                 continue
             t = graph_time(lambda: run(op, g, src, w, bias, out, c))
             times.append(f"{c}:{t:7.1f}us {flops / t / 1e6 / 2500:4.0%}")
+        nws = lib().csu_conv2d_workspace(op, ctypes.byref(g), CSU_BF16)
+        if nws:
+            ws = torch.empty(nws, dtype=torch.uint8, device=d)
+            t = graph_time(lambda: run_ws(op, g, src, w, bias, out, ws))
+            times.append(f"ksplit:{t:7.1f}us {flops / t / 1e6 / 2500:4.0%}")
         # MIOpen (torch channels_last bf16) for reference
         try:
             xt = (src if op == 0 else src).permute(0, 3, 1, 2)
