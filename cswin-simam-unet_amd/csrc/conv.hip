@@ -889,7 +889,9 @@ KSplit ksplit_plan(const IG& g, int cus) {
     const int BM = narrow ? 256 : 128, BN = narrow ? 32 : 64, BK = 64;
     const long tiles = ((g.M + BM - 1) / BM) * ((g.Ncols + BN - 1) / BN);
     const int nk = (g.Kd + BK - 1) / BK;
-    if (g.csplit || g.nsplit || g.Ncols % 4 || tiles >= 2L * cus || nk < 4) return KSplit{1, g.Kd};
+    // profiles/r06f_conv_probe.txt: pays for the CARAFE encoders' 32 / 128-tile forwards (26.5 -> 12.5,
+    // 17.6 -> 14.9 us) and the 64-tile input gradient (15.4 -> 13.0), loses at 128 tiles of 6 slices
+    if (g.csplit || g.nsplit || g.Ncols % 4 || tiles >= cus || (2 * tiles >= cus && nk < 8) || nk < 4) return KSplit{1, g.Kd};
     long want = (3L * cus + tiles - 1) / tiles;
     want = want < nk / 2 ? want : nk / 2;
     want = want < 8 ? want : 8;
@@ -1474,13 +1476,17 @@ int id_launch(const IG& g, const void* src, const void* w, const float* bias, vo
 // every CU a tile, else 256 x 128 (25-30 %); Ncols = 64 stays on the v2 kernel, which the 64-wide v3
 // tiles do not beat (the A gathers dominate: 9 taps x 64 channels per 64 outputs).  -1: v2.
 bool id_eligible(const IG& g) { return g.Cs % 64 == 0 && g.Kd >= 64 && g.Ncols <= kIDMaxN; }
-int id_pick(const IG& g) {
+int id_pick(const IG& g, bool single = false) {
     if (!id_eligible(g)) return -1;
     const long mt = (g.M + 255) / 256;
     if (g.Ncols % 256 == 0 && mt * (g.Ncols / 256) >= id_cus()) return 7;
     // fewer 256 x 128 tiles than CUs (the CSWin merges at 64^2 / 32^2, the stride phases of their
-    // input gradients): the v2 kernel's 4x more 128 x 64 tiles win (profiles/r03v_conv_probe*.txt)
+    // input gradients): the v2 kernel's 4x more 128 x 64 tiles win (profiles/r03v_conv_probe*.txt) --
+    // except for a one-problem launch with a CU's worth of 64 x 128 tiles, which runs them two
+    // workgroups per CU (the merges' forwards: 33.9 -> 28.0 / 48.6 -> 34.9 us,
+    // profiles/r06f_conv_probe.txt; the 4-phase input gradients stay on v2)
     if (g.Ncols % 128 == 0 && mt * (g.Ncols / 128) >= id_cus()) return 2;
+    if (single && g.Ncols % 128 == 0 && ((g.M + 63) / 64) * (g.Ncols / 128) >= id_cus()) return 11;
     return -1;
 }
 
@@ -1547,7 +1553,7 @@ int launch_ig(const IG* gv, int n, const void* src, const void* w, const float* 
     if (cfg < 0) {   // per-shape choice: v3 (each phase its own tile) when every phase has one
         int pk[4];
         bool all = true;
-        for (int i = 0; i < n; ++i) all = all && (pk[i] = id_pick(gv[i])) >= 0;
+        for (int i = 0; i < n; ++i) all = all && (pk[i] = id_pick(gv[i], n == 1)) >= 0;
         if (all) {
             for (int i = 0; i < n; ++i)
                 if (gv[i].M > 0)
@@ -1836,11 +1842,11 @@ extern "C" size_t csu_conv2d_workspace(int op, const csu_conv_geom* gm, int dtyp
     if (op == 0) {
         if (gm->C % 4) return 0;
         const IG g = ig_forward(*gm);
-        return id_eligible(g) && id_pick(g) >= 0 ? 0 : ksplit_bytes(g, id_cus());
+        return id_pick(g, true) >= 0 ? 0 : ksplit_bytes(g, id_cus());
     }
     if (gm->N % 4 || gm->stride != 1) return 0;
     const IG g = ig_dgrad_phase(*gm, 0, 0);
-    return id_eligible(g) && id_pick(g) >= 0 ? 0 : ksplit_bytes(g, id_cus());
+    return id_pick(g, true) >= 0 ? 0 : ksplit_bytes(g, id_cus());
 }
 
 extern "C" int csu_conv2d_fwd_ws(const csu_conv_geom* gm, int dtype, const void* x, const void* w_ohwi, const float* bias,
