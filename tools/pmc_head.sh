@@ -1,7 +1,8 @@
-# PMC table at HEAD (MFMA busy, FETCH/WRITE vs algorithmic bytes): T=<tag>; configs "tag:bench args" (default the plain UNet and 512 B16)
+# PMC table at HEAD (MFMA busy, FETCH/WRITE vs algorithmic bytes): T=<tag>; CFGS = "tag:bench args|tag:bench args" (default the plain UNet and 512 B16)
 set -e
 R=$(pwd); O=$R/gpurun_out/${T:-r04d}; mkdir -p $O; export TMPDIR=/tmp
-for cfg in ${CFGS:-"unet:--model unet" "c512:--img 512 --batch 16"}; do
+IFS='|' read -ra LIST <<< "${CFGS:-unet:--model unet|c512:--img 512 --batch 16}"
+for cfg in "${LIST[@]}"; do
   tag=${cfg%%:*}; args=${cfg#*:}
   timeout -k 10 300 python -u bench.py $args --steps 6 --warmup 2 --cpu-baseline off > $O/bench_$tag.json 2> $O/bench_$tag.err || { tail -20 $O/bench_$tag.err; exit 1; }
   i=0
