@@ -20,7 +20,8 @@ shapes = [("u1 64->64", 512, 512, 64, 64, 3, 1, 1), ("u1 128->64", 512, 512, 128
           ("convT 1024->512", 64, 64, 512, 1024, 2, 2, 0), ("merge 64->128 s2", 128, 128, 64, 128, 3, 2, 1),
           ("merge 256->512 s2", 32, 32, 256, 512, 3, 2, 1), ("embed 8->64 7x7 s4", 512, 512, 8, 64, 7, 4, 2),
           ("carafe4 enc 16->144", 128, 128, 16, 144, 3, 1, 1), ("carafe enc 32->36", 64, 64, 32, 36, 3, 1, 1),
-          ("merge 128->256 s2", 64, 64, 128, 256, 3, 2, 1)]
+          ("merge 128->256 s2", 64, 64, 128, 256, 3, 2, 1), ("carafe enc 128->36 16x16", 16, 16, 128, 36, 3, 1, 1),
+          ("carafe enc 64->36 32x32", 32, 32, 64, 36, 3, 1, 1)]
 if os.environ.get("ONLY"):
     shapes = [x for x in shapes if any(k in x[0] for k in os.environ["ONLY"].split(","))]
 
