@@ -347,7 +347,7 @@ def main():
         rec = {"metric": _metric(args), "value": round(images / el, 3),
                "unit": "images/sec", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
                "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
-               "vs_baseline": None, "dtype": "bf16 (fp8-e4m3 weights)" if args.dtype == "fp8" else args.dtype, "data": "synthetic (ellipse masks, SURVEY §8d), random-init weights",
+               "vs_baseline": None, "dtype": "fp8-e4m3 x e4m3 MFMA (qkv, Mlp) + bf16 (fp8-e4m3 weights)" if args.dtype == "fp8" else args.dtype, "data": "synthetic (ellipse masks, SURVEY §8d), random-init weights",
                "config": {"workload": (f"plain UNet train step {args.img}x{args.img}, Adam" if args.model == "unet" else
                                        f"CSWin-UNet train step {args.img}x{args.img} depth {depth} split {split}"
                                        f"{' +SimAM' if args.simam else ''}"
