@@ -47,8 +47,9 @@ def parse():
     ap.add_argument("--batch", type=int, default=16, help="images per GPU")
     ap.add_argument("--img", type=int, default=512)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32", "fp8"],
-                    help="fp8: e4m3 Linear weights (per-row power-of-two scales), bf16 activations, fp32 accumulate "
-                         "(BASELINE config 5)")
+                    help="fp8: e4m3 Linear weights (per-row power-of-two scales), fp32 accumulate (BASELINE config 5); "
+                         "the qkv GEMM and the fused Mlp run e4m3 x e4m3 MFMA (activations quantised per token / "
+                         "per 32-value MX block), the other layers bf16 on the dequantised weights")
     ap.add_argument("--model", default="cswin", choices=["cswin", "unet"],
                     help="unet: the plain UNet of train_unet_segmentation.py (BASELINE config 1's model; Adam, "
                          "use --img 128 --batch 8)")
