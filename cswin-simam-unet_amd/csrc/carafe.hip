@@ -147,26 +147,62 @@ __global__ __launch_bounds__(NT) void carafe_bwd_enc(int B, int H, int W, int C,
         for (int q = 0; q < S2; ++q)
 #pragma unroll
             for (int t = 0; t < KT; ++t) dw[q][t] += __shfl_xor(dw[q][t], o, 64);
-    if (!live || g != 0) return;
+    if (!live) return;
+    if constexpr (S != 2) {   // S = 4 (144 values per pixel): one lane writes them
+        if (g != 0) return;
+        const float* ws = wsave + lpix * KT * S2;
+        T* de = denc + lpix * KT * S2;
+#pragma unroll
+        for (int q = 0; q < S2; ++q) {
+            float wt[KT], sum = 0.f;
+#pragma unroll
+            for (int t = 0; t < KT; ++t) {
+                wt[t] = ws[t * S2 + q];
+                sum += wt[t] * dw[q][t];
+            }
+#pragma unroll
+            for (int t = 0; t < KT; ++t) de[t * S2 + q] = from_f<T>(wt[t] * (dw[q][t] - sum));
+        }
+        return;
+    }
+    // S = 2: every lane of the pixel now holds all 9 S^2 sums: the lanes split the pixel's outputs
+    // (index i = t S^2 + q, consecutive lanes -> consecutive elements: coalesced stores instead of
+    // one lane writing all 9 S^2 values)
     const float* ws = wsave + lpix * KT * S2;
     T* de = denc + lpix * KT * S2;
+    float sum[S2];
 #pragma unroll
-    for (int q = 0; q < S2; ++q) {
-        float wt[KT], sum = 0.f;
+    for (int q = 0; q < S2; ++q) sum[q] = 0.f;
 #pragma unroll
-        for (int t = 0; t < KT; ++t) {
-            wt[t] = ws[t * S2 + q];
-            sum += wt[t] * dw[q][t];
+    for (int i = 0; i < KT * S2; i += 4) {   // the pixel's softmax weights (same 16-B vectors in every lane)
+        const f32x4 wv = *reinterpret_cast<const f32x4*>(ws + i);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) sum[(i + e) % S2] += wv[e] * dw[(i + e) % S2][(i + e) / S2];
+    }
+#pragma unroll
+    for (int r = 0; r < (KT * S2 + 7) / 8; ++r) {
+        const int i = g + G * r;
+        if (G * r < KT * S2 && i < KT * S2) {
+            // the lane's own (q, t) = (i % S2, i / S2): a runtime index into registers -> select chain
+            float d = 0.f, sq = 0.f;
+#pragma unroll
+            for (int k = 0; k < KT * S2; ++k)
+                if (k == i) { d = dw[k % S2][k / S2]; sq = sum[k % S2]; }
+            de[i] = from_f<T>(ws[i] * (d - sq));
         }
-#pragma unroll
-        for (int t = 0; t < KT; ++t) de[t * S2 + q] = from_f<T>(wt[t] * (dw[q][t] - sum));
     }
 }
 
-// dx[y', x', c] = sum_t sum_{i,j} w[(y,x), t, (i,j)] dout[(y s + i, x s + j), c],  (y, x) = (y'-ky+1, x'-kx+1)
-template <typename T>
-__global__ __launch_bounds__(NT) void carafe_bwd_x(int B, int H, int W, int C, int s, const float* __restrict__ wsave,
+// dx[y', x', c] = sum_t sum_{i,j} w[(y,x), t, (i,j)] dout[(y s + i, x s + j), c],  (y, x) = (y'-ky+1, x'-kx+1).
+// One thread = one input pixel x 8 channels; taps in groups whose loads (the S^2 weights as 16-B
+// vectors, the S^2 dout vectors) are all issued before their FMAs -- branch-free raw buffer loads,
+// out-of-image neighbours at an out-of-range offset (zeros): the per-tap `continue` loop with a runtime
+// s waited for every load in turn
+template <typename T, int S>
+__global__ __launch_bounds__(NT, 4) void carafe_bwd_x(int B, int H, int W, int C, const float* __restrict__ wsave,
                                                    const T* __restrict__ dout, T* __restrict__ dx) {
+    constexpr int S2 = S * S;
+    constexpr int TG = S == 2 && sizeof(T) == 2 ? 3 : 1;   // taps per load group
     const int G = C / 8;
     const long gid = xcd_tile(blockIdx.x, gridDim.x) * NT + threadIdx.x;   // neighbour blocks share one L2
     const long total = (long)B * H * W * G;
@@ -176,19 +212,53 @@ __global__ __launch_bounds__(NT) void carafe_bwd_x(int B, int H, int W, int C, i
     const int xp = p % W; p /= W;
     const int yp = p % H;
     const int b = p / H;
-    const int s2 = s * s, sW = s * W, sH = s * H;
+    const int sW = S * W, sH = S * H;
+    const __amdgpu_buffer_rsrc_t rd = buf_rsrc(dout, (long)B * sH * sW * C * (long)sizeof(T));
+    const __amdgpu_buffer_rsrc_t rw = buf_rsrc(wsave, (long)B * H * W * KT * S2 * 4);
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    for (int t = 0; t < KT; ++t) {
-        const int y = yp - (t / 3 - 1), xx = xp - (t % 3 - 1);
-        if (y < 0 || y >= H || xx < 0 || xx >= W) continue;
-        const float* ws = wsave + (((size_t)b * H + y) * W + xx) * KT * s2 + t * s2;
-        for (int i = 0; i < s; ++i)
-            for (int j = 0; j < s; ++j) {
-                const float w = ws[i * s + j];
-                float v[8];
-                load8(dout + (((size_t)b * sH + y * s + i) * sW + xx * s + j) * C + 8 * g, v);
+#pragma unroll 1
+    for (int t0 = 0; t0 < KT; t0 += TG) {
+        // dout vectors kept raw (bf16: 4 VGPRs per 8 channels) until their FMAs
+        u32x4 v[TG][S2][sizeof(T) / 2];
+        float w[TG][S2];
 #pragma unroll
-                for (int k = 0; k < 8; ++k) acc[k] += w * v[k];
+        for (int u = 0; u < TG; ++u) {
+            const int t = t0 + u;
+            const int y = yp - (t / 3 - 1), xx = xp - (t % 3 - 1);
+            const bool in = y >= 0 && y < H && xx >= 0 && xx < W;
+            const unsigned wo = in ? (unsigned)(((((long)b * H + y) * W + xx) * KT * S2 + t * S2) * 4) : kOOB;
+#pragma unroll
+            for (int q = 0; q < S2; q += 4) {
+                const u32x4 wv = __builtin_amdgcn_raw_buffer_load_b128(rw, wo == kOOB ? kOOB : wo + 4 * q, 0, 0);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) w[u][q + e] = __uint_as_float(wv[e]);
+            }
+#pragma unroll
+            for (int q = 0; q < S2; ++q) {
+                const unsigned o = in ? (unsigned)(((((long)b * sH + y * S + q / S) * sW + xx * S + q % S) * C + 8 * g) *
+                                                   (long)sizeof(T))
+                                      : kOOB;
+#pragma unroll
+                for (int h = 0; h < (int)(sizeof(T) / 2); ++h)
+                    v[u][q][h] = __builtin_amdgcn_raw_buffer_load_b128(rd, o == kOOB ? kOOB : o + 16 * h, 0, 0);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < TG; ++u)
+#pragma unroll
+            for (int q = 0; q < S2; ++q) {
+                float f[8];
+                if constexpr (sizeof(T) == 2) {
+                    bf16x8 bv;
+                    __builtin_memcpy(&bv, &v[u][q][0], 16);
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) f[k] = (float)bv[k];
+                } else {
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) f[k] = __uint_as_float(v[u][q][k / 4][k % 4]);
+                }
+#pragma unroll
+                for (int k = 0; k < 8; ++k) acc[k] += w[u][q] * f[k];
             }
     }
     store8(dx + (((size_t)b * H + yp) * W + xp) * C + 8 * g, acc);
@@ -297,16 +367,18 @@ extern "C" int csu_carafe_bwd(int B, int H, int W, int C, int s, int dtype, cons
     const long n_in = (long)B * H * W * (C / 8);
     hipStream_t st = as_stream(stream);
 #define CSU_CE(T, S_) carafe_bwd_enc<T, S_><<<blocks(n_in), NT, 0, st>>>(B, H, W, C, (const T*)x, wsave, (const T*)dout, (T*)denc)
+#define CSU_CX(T, S_) carafe_bwd_x<T, S_><<<blocks(n_in), NT, 0, st>>>(B, H, W, C, wsave, (const T*)dout, (T*)dx)
     if (dtype == CSU_BF16) {
         if (s == 4) CSU_CE(bf16, 4); else CSU_CE(bf16, 2);
-        carafe_bwd_x<bf16><<<blocks(n_in), NT, 0, st>>>(B, H, W, C, s, wsave, (const bf16*)dout, (bf16*)dx);
+        if (s == 4) CSU_CX(bf16, 4); else CSU_CX(bf16, 2);
     } else if (dtype == CSU_F32) {
         if (s == 4) CSU_CE(float, 4); else CSU_CE(float, 2);
-        carafe_bwd_x<float><<<blocks(n_in), NT, 0, st>>>(B, H, W, C, s, wsave, (const float*)dout, (float*)dx);
+        if (s == 4) CSU_CX(float, 4); else CSU_CX(float, 2);
     } else {
         return fail(CSU_E_ARG, "carafe_bwd: bad dtype");
     }
 #undef CSU_CE
+#undef CSU_CX
     return check_launch("carafe_bwd");
 }
 

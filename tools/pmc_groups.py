@@ -55,17 +55,24 @@ def main():
     for tag, cs in passes:
         per, dur, names, first, steps = per_step(os.path.join(d, tag), cs)
         nsteps[tag] = steps
-        for did, c in per.items():
+        prev = None
+        for did in sorted(per, key=int):
+            c = per[did]
             if int(did) <= first:
                 continue
             nm = names[did]
-            for tab, key in ((G, group(nm)), (K, short(nm))):
+            gk = group(nm)
+            # a colsum right after a weight-gradient kernel is that call's slab reduction (prof_groups.py)
+            if gk == "colsum" and prev in ("conv_wgrad", "linear_wgrad"):
+                gk = prev
+            prev = gk
+            for tab, key in ((G, gk), (K, short(nm))):
                 a = tab[key]
                 for k, v in c.items():
                     a[k] += v / steps
                 a["t_" + tag] += dur.get(did, 0.0) / steps * 1e6
                 a["n_" + tag] += 1.0 / steps
-            kgroup[short(nm)] = group(nm)
+            kgroup[short(nm)] = gk
 
     def row(a):
         util = a["SQ_VALU_MFMA_BUSY_CYCLES"] / (a["GRBM_GUI_ACTIVE"] / 8 * 1024) if a["GRBM_GUI_ACTIVE"] else 0.0
