@@ -143,7 +143,7 @@ __device__ __forceinline__ v4s tr_read(const bf16* p) {
 // key = 4 (row & 3); T = 64 (two rows per bank row): key = 4 ((row >> 1) & 1).
 template <int T>
 __device__ __forceinline__ int swz(int row, int chunk) {
-    const int key = T == 128 ? 4 * (row & 3) : 4 * ((row >> 1) & 1);
+    const int key = T >= 128 ? 4 * (row & 3) : 4 * ((row >> 1) & 1);   // T = 256: 512-B rows, same key
     return row * T + ((chunk ^ key) << 3);
 }
 
@@ -172,11 +172,16 @@ __device__ __forceinline__ void unroll_steps(F& f, int i) {
     }
 }
 
-template <int TN, int TK>
+// NTH threads = NTH / 64 waves in a (NW / 2) x 2 grid over the tile (N x K): 4 waves for the 64 / 128
+// tiles, 8 waves (64 x 64 per wave) for the 256 x 128 tile of the wide Linears (3/4 of the staged bytes
+// per output of the 128 x 128 tile: the step is bound by operand staging; a 256 x 256 tile's 128
+// accumulators per lane spilled)
+template <int TN, int TK, int NTH = NT>
 struct TileCfg {
-    static constexpr int CPRA = TN / 8, RPPA = NT / CPRA, NPA = TM / RPPA;   // 16-B chunks per row, rows per pass, passes
-    static constexpr int CPRB = TK / 8, RPPB = NT / CPRB, NPB = TM / RPPB;
-    static constexpr int AN = TN / 64, AK = TK / 64;            // 32x32 MFMA tiles per wave per dim
+    static constexpr int CPRA = TN / 8, RPPA = NTH / CPRA, NPA = TM / RPPA;   // 16-B chunks per row, rows per pass, passes
+    static constexpr int CPRB = TK / 8, RPPB = NTH / CPRB, NPB = TM / RPPB;
+    static constexpr int WNW = NTH / 128;                       // waves along N (2 along K)
+    static constexpr int AN = TN / (32 * WNW), AK = TK / 64;    // 32x32 MFMA tiles per wave per dim
     static constexpr int BUF = TM * (TN + TK);                  // bf16 per LDS buffer (A image then B image)
 };
 
@@ -187,11 +192,11 @@ struct TileCfg {
 // global loads of step i+3 into the register set just freed, MFMAs of step i, one barrier -- two
 // steps of MFMA work between a load's issue and its use, 64 KB LDS (T = 128) for 2 workgroups/CU.
 // Body: logical workgroup t of one Linear (t = chunk * tiles + tile).
-template <int TN, int TK, int D>
+template <int TN, int TK, int D, int NTH = NT>
 __device__ __forceinline__ void wgrad_tile_body(bf16* lds, int t, long M, int N, int K, long rpc, int chunks,
                                                 const bf16* __restrict__ dy, const bf16* __restrict__ x,
                                                 float* __restrict__ dst, float* __restrict__ slab) {
-    using C = TileCfg<TN, TK>;
+    using C = TileCfg<TN, TK, NTH>;
     const int nt = (N + TN - 1) / TN, kt = (K + TK - 1) / TK, tiles = nt * kt;
     const int chunk = __builtin_amdgcn_readfirstlane(t / tiles), tile = __builtin_amdgcn_readfirstlane(t % tiles);
     const int ntile = tile / kt;
@@ -201,7 +206,7 @@ __device__ __forceinline__ void wgrad_tile_body(bf16* lds, int t, long M, int N,
     const int nsteps = (int)((m_end - m_begin + TM - 1) / TM);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int r = lane & 31, h = lane >> 5;
-    const int wn = (wave >> 1) * (TN / 2), wk = (wave & 1) * (TK / 2);
+    const int wn = (wave >> 1) * (TN / C::WNW), wk = (wave & 1) * (TK / 2);
     const bool do_bias = k0 == 0;
     const int cga = threadIdx.x % C::CPRA, rra = threadIdx.x / C::CPRA;   // A: rows rra + RPPA i, chunk cga
     const int cgb = threadIdx.x % C::CPRB, rrb = threadIdx.x / C::CPRB;
@@ -308,14 +313,14 @@ __device__ __forceinline__ void wgrad_tile_body(bf16* lds, int t, long M, int N,
                     o[(wn + 32 * a + crow(reg, h)) * TK + wk + 32 * b + r] = acc[a][b][reg];
     }
     if (do_bias) {   // column sums of dY: threads with the same cga hold the same 8 columns
-        float* red = reinterpret_cast<float*>(lds);   // [NT][9]: both LDS buffers are free now
+        float* red = reinterpret_cast<float*>(lds);   // [NTH][9]: both LDS buffers are free now
 #pragma unroll
         for (int j = 0; j < 8; ++j) red[threadIdx.x * 9 + j] = bsum[j];
         __syncthreads();
         if (threadIdx.x < TN) {
             const int g = threadIdx.x >> 3, j = threadIdx.x & 7;   // column n0 + 8g + j
             float sum = 0.f;
-            for (int q = g; q < NT; q += C::CPRA) sum += red[q * 9 + j];
+            for (int q = g; q < NTH; q += C::CPRA) sum += red[q * 9 + j];
             if (chunks == 1) {
                 if (n0 + threadIdx.x < N) dst[(long)N * K + n0 + threadIdx.x] = sum;
             } else {
@@ -327,17 +332,17 @@ __device__ __forceinline__ void wgrad_tile_body(bf16* lds, int t, long M, int N,
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-template <int TN, int TK, int D>
-__global__ __launch_bounds__(NT, D > 2 ? 1 : 2) void wgrad_tile(long M, int N, int K, long rpc, int chunks,
+template <int TN, int TK, int D, int NTH = NT>
+__global__ __launch_bounds__(NTH, D > 2 || NTH > NT ? 1 : 2) void wgrad_tile(long M, int N, int K, long rpc, int chunks,
                                                     const bf16* __restrict__ dy, const bf16* __restrict__ x,
                                                     float* __restrict__ dst, float* __restrict__ slab) {
-    __shared__ __attribute__((aligned(16))) bf16 lds[2 * TileCfg<TN, TK>::BUF];
+    __shared__ __attribute__((aligned(16))) bf16 lds[2 * TileCfg<TN, TK, NTH>::BUF];
     WG_STAMP(0);
     // tiles of one token chunk are consecutive logical ids -> one XCD streams the chunk once
     // (readfirstlane: keep the tile decode in SGPRs -- a buffer resource built from a VGPR base
     // turns every buffer load into a waterfall loop)
     const int t = __builtin_amdgcn_readfirstlane((int)xcd_tile(blockIdx.x, gridDim.x));
-    wgrad_tile_body<TN, TK, D>(lds, t, M, N, K, rpc, chunks, dy, x, dst, slab);
+    wgrad_tile_body<TN, TK, D, NTH>(lds, t, M, N, K, rpc, chunks, dy, x, dst, slab);
     WG_STAMP(3);
 }
 
@@ -356,15 +361,15 @@ struct WgGroup {
     int count;
 };
 
-template <int TN, int TK>
-__global__ __launch_bounds__(NT, 2) void wgrad_group(WgGroup g) {
-    __shared__ __attribute__((aligned(16))) bf16 lds[2 * TileCfg<TN, TK>::BUF];
+template <int TN, int TK, int NTH = NT, int D = 2>
+__global__ __launch_bounds__(NTH, NTH > NT ? 1 : 2) void wgrad_group(WgGroup g) {
+    __shared__ __attribute__((aligned(16))) bf16 lds[2 * TileCfg<TN, TK, NTH>::BUF];
     const int lt = __builtin_amdgcn_readfirstlane((int)xcd_tile(blockIdx.x, gridDim.x));
     int i = 0;
     while (i + 1 < g.count && g.b0[i + 1] <= lt) ++i;
     i = __builtin_amdgcn_readfirstlane(i);
-    wgrad_tile_body<TN, TK, 2>(lds, lt - g.b0[i], g.M[i], g.N[i], g.K[i], g.rpc[i], g.chunks[i], g.dy[i], g.x[i],
-                               g.dst[i], g.slab[i]);
+    wgrad_tile_body<TN, TK, D, NTH>(lds, lt - g.b0[i], g.M[i], g.N[i], g.K[i], g.rpc[i], g.chunks[i], g.dy[i], g.x[i],
+                                    g.dst[i], g.slab[i]);
 }
 
 // dst[n][k] = sum_c slab[tile(n, k)][c][n % TN][k % TK], then dst[N*K + n] = sum_c bslab[n / TN][c][n % TN].
@@ -488,6 +493,17 @@ double model_us(long M, int N, int K, int tn, int tk, long c) {
 // (csu_linear_wgrad_tuned).
 Plan make_plan(long M, int N, int K, int tn, int tk, int chunks) {
     Plan p;
+    if (tn == 256) {   // explicit 256 x 128 tiles (the grouped path's choice for N % 256, K % 128 == 0)
+        p.tn = 256;
+        p.tk = 128;
+        p.nt = (N + 255) / 256;
+        p.kt = (K + 127) / 128;
+        const long c = chunks > 0 ? chunks : 1;
+        p.rpc = ((M + c - 1) / c + TM - 1) / TM * TM;
+        p.chunks = (int)((M + p.rpc - 1) / p.rpc);
+        p.depth = 2;
+        return p;
+    }
     double best = 1e30;
     p.tn = p.tk = 64;
     long want = 1;
@@ -529,18 +545,20 @@ size_t plan_bytes(const Plan& p) {
 template <int TN, int TK>
 void launch_tile(const Plan& p, unsigned grid, long M, int N, int K, const bf16* dy, const bf16* x, float* dst,
                  float* slab, hipStream_t st) {
-    wgrad_tile<TN, TK, 2><<<grid, NT, 0, st>>>(M, N, K, p.rpc, p.chunks, dy, x, dst, slab);
+    constexpr int NTH = TN == 256 ? 2 * NT : NT;
+    wgrad_tile<TN, TK, 2, NTH><<<grid, NTH, 0, st>>>(M, N, K, p.rpc, p.chunks, dy, x, dst, slab);
 }
 
 int run_bf16(const Plan& p, long M, int N, int K, const bf16* dy, const bf16* x, float* dst, void* ws, hipStream_t st,
              bool defer = false) {
     const unsigned grid = (unsigned)((long)p.nt * p.kt * p.chunks);
     float* slab = p.chunks > 1 ? (float*)ws : nullptr;
-    if (p.tn == 128 && p.tk == 128) launch_tile<128, 128>(p, grid, M, N, K, dy, x, dst, slab, st);
+    if (p.tn == 256 && p.tk == 128) launch_tile<256, 128>(p, grid, M, N, K, dy, x, dst, slab, st);
+    else if (p.tn == 128 && p.tk == 128) launch_tile<128, 128>(p, grid, M, N, K, dy, x, dst, slab, st);
     else if (p.tn == 128 && p.tk == 64) launch_tile<128, 64>(p, grid, M, N, K, dy, x, dst, slab, st);
     else if (p.tn == 64 && p.tk == 128) launch_tile<64, 128>(p, grid, M, N, K, dy, x, dst, slab, st);
     else if (p.tn == 64 && p.tk == 64) launch_tile<64, 64>(p, grid, M, N, K, dy, x, dst, slab, st);
-    else return fail(CSU_E_ARG, "linear_wgrad: tile must be 64 or 128");
+    else return fail(CSU_E_ARG, "linear_wgrad: tile must be 64 or 128 (or 256 x 128)");
     if (int e = check_launch("linear_wgrad")) return e;
     if (p.chunks > 1 && !defer) {
         wslab_reduce<<<(unsigned)wslab_blocks(N, K, p.chunks), NT, 0, st>>>(N, K, p.tn, p.tk, p.chunks, slab, dst);
@@ -576,7 +594,9 @@ extern "C" int csu_linear_wgrad_tuned(long M, int N, int K, int dtype, const voi
         return fail(CSU_E_WORKSPACE, "linear_wgrad: workspace");
     hipStream_t st = as_stream(stream);
     if (dtype == CSU_BF16) {
-        if ((tn && tn != 64 && tn != 128) || (tk && tk != 64 && tk != 128)) return fail(CSU_E_ARG, "linear_wgrad: tile");
+        if ((tn && tn != 64 && tn != 128 && tn != 256) || (tk && tk != 64 && tk != 128) ||
+            (tn == 256 && (tk != 128 || N % 256 || K % 128)))
+            return fail(CSU_E_ARG, "linear_wgrad: tile");
         const Plan p = make_plan(M, N, K, tn, tk, chunks);
         return run_bf16(p, M, N, K, (const bf16*)dy, (const bf16*)x, dw_db, workspace, st);
     }
@@ -604,20 +624,22 @@ extern "C" int csu_linear_wgrad_deferred(long M, int N, int K, const void* dy, c
     return run_bf16(p, M, N, K, (const bf16*)dy, (const bf16*)x, dw_db, workspace, as_stream(stream), true);
 }
 
-// Plan of a Linear inside a grouped launch: 128 tiles when N and K allow, else 64; token chunks so
+// Plan of a Linear inside a grouped launch: 256 x 128 tiles (8 waves) when N % 256 == 0 and K % 128 == 0,
+// 128 x 128 when both are multiples of 128, else 64 x 64; token chunks so
 // that the fp32 partial slabs stay <= ~1/16 of the operand bytes (chunks <= M (N + K) / (32 N K)),
 // >= 1024 tokens per chunk.  No occupancy target: the group fills the GPU.
 // slab bytes <= operand bytes * 2 / kSlabDiv (A/B at 512 B16: 8 -> 1231 img/s, 16 -> 1249, 32 -> 1255, 64 -> 1227)
 constexpr int kSlabDiv = 32;
 static void group_plan(long M, int N, int K, int* tn, int* tk, int* chunks, long* rpc) {
-    const int t = (N % 128 == 0 && K % 128 == 0) ? 128 : 64;
+    const int t = (N % 256 == 0 && K % 128 == 0) ? 256 : (N % 128 == 0 && K % 128 == 0) ? 128 : 64;
     long c = (long)((double)M * (N + K) / ((double)kSlabDiv * N * K) + 0.5);
     const long maxc = M / 1024 > 0 ? M / 1024 : 1;
     if (c > maxc) c = maxc;
     if (c < 1) c = 1;
     long r = ((M + c - 1) / c + TM - 1) / TM * TM;
     c = (M + r - 1) / r;
-    *tn = *tk = t;
+    *tn = t;
+    *tk = t == 256 ? 128 : t;
     *chunks = (int)c;
     *rpc = r;
 }
@@ -637,14 +659,15 @@ extern "C" size_t csu_linear_wgrad_group_plan(long M, int N, int K, int* tn, int
 extern "C" int csu_linear_wgrad_group(const csu_wgrad_group_item* items, int count, void* stream) {
     if (count < 0 || (count && !items)) return fail(CSU_E_ARG, "linear_wgrad_group: bad args");
     hipStream_t st = as_stream(stream);
-    for (int pass = 0; pass < 2; ++pass) {   // 128-tile items, then 64-tile items
-        const int T = pass == 0 ? 128 : 64;
+    for (int pass = 0; pass < 3; ++pass) {   // 256-tile items, then 128-tile, then 64-tile items
+        const int T = pass == 0 ? 256 : pass == 1 ? 128 : 64;
         WgGroup g;
         g.count = 0;
         g.b0[0] = 0;
         auto flush = [&]() -> int {
             if (!g.count) return 0;
-            if (T == 128) wgrad_group<128, 128><<<(unsigned)g.b0[g.count], NT, 0, st>>>(g);
+            if (T == 256) wgrad_group<256, 128, 2 * NT><<<(unsigned)g.b0[g.count], 2 * NT, 0, st>>>(g);
+            else if (T == 128) wgrad_group<128, 128><<<(unsigned)g.b0[g.count], NT, 0, st>>>(g);
             else wgrad_group<64, 64><<<(unsigned)g.b0[g.count], NT, 0, st>>>(g);
             g.count = 0;
             return check_launch("linear_wgrad_group");

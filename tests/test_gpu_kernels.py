@@ -503,6 +503,36 @@ def test_linear_wgrad_plans(M, N, K, tn, tk, chunks):
     assert float((db.double() - ref_b).abs().max()) <= 1e-2 * max(float(ref_b.abs().max()), M ** 0.5)
 
 
+@pytest.mark.parametrize("M,N,K,chunks", [(16384, 1024, 256, 1), (16384, 768, 256, 5), (4096, 2048, 512, 3),
+                                           (700, 256, 128, 2), (65536, 512, 128, 0)])
+def test_linear_wgrad_8wave_tile(M, N, K, chunks):
+    """The 8-wave 256 x 128 tile (the grouped path's choice for N % 256 == 0, K % 128 == 0) through
+    csu_linear_wgrad_tuned: == fp64 (dW and db), bitwise reproducible, ragged token chunks."""
+    from csu._lib import check, lib, ptr, stream_ptr
+    d = dev()
+    g = torch.Generator(device=d).manual_seed(M + N + K + chunks)
+    dy = torch.randn(M, N, device=d, generator=g).bfloat16()
+    x = torch.randn(M, K, device=d, generator=g).bfloat16()
+    L = lib()
+    outs = []
+    for _ in range(2):
+        n = L.csu_linear_wgrad_tuned_workspace(M, N, K, 256, 128, chunks)
+        ws = torch.full((max(n, 16) // 4,), float("nan"), device=d)
+        out = torch.full((N * K + N,), float("nan"), device=d)
+        check(L.csu_linear_wgrad_tuned(M, N, K, 1, ptr(dy), ptr(x), ptr(out), ptr(ws), n, 256, 128, chunks, stream_ptr(d)),
+              "linear_wgrad_tuned 256x128")
+        outs.append(out)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+    ref_w = dy.double().t() @ x.double()
+    ref_b = dy.double().sum(0)
+    dw, db = outs[0][:N * K].view(N, K), outs[0][N * K:]
+    assert float((dw.double() - ref_w).abs().max()) <= 1e-2 * max(float(ref_w.abs().max()), M ** 0.5)
+    assert float((db.double() - ref_b).abs().max()) <= 1e-2 * max(float(ref_b.abs().max()), M ** 0.5)
+    assert L.csu_linear_wgrad_tuned(M, 192, K, 1, ptr(dy), ptr(x), ptr(out), ptr(ws), n, 256, 128, chunks,
+                                    stream_ptr(d)) != 0   # N % 256 != 0: refused
+
+
 def test_side_stream_wgrad_with_gradient_accumulation(monkeypatch):
     """Two backward passes without zeroing (gradient accumulation: AccumulateGrad adds in place on
     the launching stream) give bitwise the same .grad with the side stream on and off: a parameter
