@@ -10,6 +10,8 @@ from __future__ import annotations
 
 from typing import Dict, List, Optional
 
+import contextlib
+import gc
 import warnings
 
 import torch
@@ -131,6 +133,22 @@ def _drop_stale_train_graphs(cache, optimizer, reducer):
         del cache[k]
 
 
+@contextlib.contextmanager
+def _gc_paused():
+    """Python's cyclic GC off for a graph capture (after one collection): a collection inside the
+    capture can run the finaliser of an unrelated object that calls the HIP runtime (a graph, stream
+    or event of an earlier step) -- an illegal call during a capture that aborts the process (seen as
+    'Fatal Python error: Aborted' while garbage-collecting inside a backward kernel launch)."""
+    was = gc.isenabled()
+    gc.collect()
+    gc.disable()
+    try:
+        yield
+    finally:
+        if was:
+            gc.enable()
+
+
 def _capture_mode():
     """HIP-graph capture mode: under a process group the RCCL watchdog polls its collectives' events
     from another thread, so the capture is thread-local and starts with nothing in flight (see
@@ -167,7 +185,7 @@ class _GraphedEval:
         torch.cuda.synchronize()
         mode = _capture_mode()
         self.graph = torch.cuda.CUDAGraph()
-        with torch.no_grad(), torch.cuda.graph(self.graph, capture_error_mode=mode):
+        with _gc_paused(), torch.no_grad(), torch.cuda.graph(self.graph, capture_error_mode=mode):
             self.stats = self._body()
 
     def _body(self):
@@ -406,7 +424,7 @@ class GraphedTrainStep:
             prep()
         self.graph = torch.cuda.CUDAGraph()
         self.opt.zero_grad(set_to_none=True)
-        with torch.cuda.graph(self.graph, capture_error_mode=mode):
+        with _gc_paused(), torch.cuda.graph(self.graph, capture_error_mode=mode):
             self.loss, self.out = self._body(zero=False)
             self.stats = self._stats
         fin = getattr(self.opt, "finish_capture", None)
