@@ -179,17 +179,14 @@ __global__ __launch_bounds__(NT) void carafe_bwd_enc(int B, int H, int W, int C,
 #pragma unroll
         for (int e = 0; e < 4; ++e) sum[(i + e) % S2] += wv[e] * dw[(i + e) % S2][(i + e) / S2];
     }
+    // outputs g, g + G, ... (G = C / 8 lanes: 1..64 -- every one of the 9 S^2 outputs is written)
+    for (int i = g; i < KT * S2; i += G) {
+        // the lane's own (q, t) = (i % S2, i / S2): a runtime index into registers -> select chain
+        float d = 0.f, sq = 0.f;
 #pragma unroll
-    for (int r = 0; r < (KT * S2 + 7) / 8; ++r) {
-        const int i = g + G * r;
-        if (G * r < KT * S2 && i < KT * S2) {
-            // the lane's own (q, t) = (i % S2, i / S2): a runtime index into registers -> select chain
-            float d = 0.f, sq = 0.f;
-#pragma unroll
-            for (int k = 0; k < KT * S2; ++k)
-                if (k == i) { d = dw[k % S2][k / S2]; sq = sum[k % S2]; }
-            de[i] = from_f<T>(ws[i] * (d - sq));
-        }
+        for (int k = 0; k < KT * S2; ++k)
+            if (k == i) { d = dw[k % S2][k / S2]; sq = sum[k % S2]; }
+        de[i] = from_f<T>(ws[i] * (d - sq));
     }
 }
 
