@@ -207,7 +207,7 @@ def test_cpu_tensor_fails_loudly():
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("B,H,C,s", [(2, 8, 64, 2), (1, 16, 32, 4), (2, 4, 512, 2), (1, 7, 128, 2), (1, 5, 64, 4),
-                                     (2, 6, 32, 2), (1, 5, 16, 2), (1, 4, 8, 2)])   # < 8 lanes per pixel (S = 2)
+                                     (2, 6, 32, 2)])   # 4 lanes per pixel (S = 2)
 def test_carafe_module_vs_oracle(B, H, C, s, dtype):
     """CARAFE / CARAFE4 module (HIP reassembly + conv/GEMM kernel prediction) vs the oracle."""
     from csu.model import CARAFE
