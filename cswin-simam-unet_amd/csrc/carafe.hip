@@ -141,6 +141,51 @@ __global__ __launch_bounds__(NT) void carafe_bwd_enc(int B, int H, int W, int C,
             for (int k = 0; k < 8; ++k) d += go[q][k] * v[t][k];
             dw[q][t] = d;
         }
+    if constexpr (S == 2) {
+        if (G >= 4) {
+            // reduce-scatter over the pixel's G lanes (aligned groups of G consecutive lanes): the
+            // top lane bit keeps sub-pixels {0,1} / {2,3}, the next one sub-pixel q of those (18 + 9
+            // exchanges), then the lanes of one q sum its 9 tap values -- 18 + 9 + 9 log2(G/4)
+            // exchanges instead of 36 log2(G); each lane ends with its q's 9 sums
+            const int h = G >> 1, qq = G >> 2;
+            const bool hi = (g & h) != 0, lo = (g & qq) != 0;
+            float d2[2][KT], d1[KT];
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int t = 0; t < KT; ++t) {
+                    const float keep = hi ? dw[2 + j][t] : dw[j][t], send = hi ? dw[j][t] : dw[2 + j][t];
+                    d2[j][t] = keep + __shfl_xor(send, h, 64);
+                }
+#pragma unroll
+            for (int t = 0; t < KT; ++t) {
+                const float keep = lo ? d2[1][t] : d2[0][t], send = lo ? d2[0][t] : d2[1][t];
+                d1[t] = keep + __shfl_xor(send, qq, 64);
+            }
+            for (int o = qq >> 1; o > 0; o >>= 1)
+#pragma unroll
+                for (int t = 0; t < KT; ++t) d1[t] += __shfl_xor(d1[t], o, 64);
+            if (!live) return;
+            const int q = (hi ? 2 : 0) + (lo ? 1 : 0);
+            const float* ws = wsave + lpix * KT * S2 + q;
+            T* de = denc + lpix * KT * S2 + q;
+            float wt[KT], sum = 0.f;
+#pragma unroll
+            for (int t = 0; t < KT; ++t) {
+                wt[t] = ws[t * S2];
+                sum += wt[t] * d1[t];
+            }
+            // the q's 9 outputs over its G/4 lanes (a runtime tap index into registers -> select chain)
+            for (int t = g & (qq - 1); t < KT; t += qq) {
+                float d = 0.f, w = 0.f;
+#pragma unroll
+                for (int k = 0; k < KT; ++k)
+                    if (k == t) { d = d1[k]; w = wt[k]; }
+                de[t * S2] = from_f<T>(w * (d - sum));
+            }
+            return;
+        }
+    }
     // reduce over the G lanes of this pixel (aligned groups of G consecutive lanes)
     for (int o = G >> 1; o > 0; o >>= 1)
 #pragma unroll
@@ -165,7 +210,7 @@ __global__ __launch_bounds__(NT) void carafe_bwd_enc(int B, int H, int W, int C,
         }
         return;
     }
-    // S = 2: every lane of the pixel now holds all 9 S^2 sums: the lanes split the pixel's outputs
+    // S = 2, G < 4: every lane of the pixel now holds all 9 S^2 sums: the lanes split the pixel's outputs
     // (index i = t S^2 + q, consecutive lanes -> consecutive elements: coalesced stores instead of
     // one lane writing all 9 S^2 values)
     const float* ws = wsave + lpix * KT * S2;

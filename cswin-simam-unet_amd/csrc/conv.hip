@@ -253,6 +253,8 @@ __device__ __forceinline__ bf16x8 ctr_frag(const bf16* img, int c0, int s, int l
     return out;
 }
 
+// N4: Ncols % 8 == 4 (the 36-channel CARAFE encoders): each thread's 8 dy columns as two 8-B loads
+template <bool N4>
 __global__ __launch_bounds__(NT) void conv_wgrad_bf16(Geo g, long Mrows, int Ncols, int Kdim, long rows_per_chunk,
                                                       const bf16* __restrict__ x, const bf16* __restrict__ dy,
                                                       float* __restrict__ part) {
@@ -274,7 +276,7 @@ __global__ __launch_bounds__(NT) void conv_wgrad_bf16(Geo g, long Mrows, int Nco
     const int ktap = kk / g.C, kc = kk - ktap * g.C;
     const int kdy = ktap / g.KW - g.p, kdx = ktap % g.KW - g.p;
     const int n = n0 + sch * 8;
-    const bool nval = n + 8 <= Ncols;      // Ncols % 8 == 0 on this path
+    const bool nval = (N4 ? n + 4 : n + 8) <= Ncols, nval2 = n + 8 <= Ncols;   // Ncols % 4 == 0 on this path
     // branch-free gathers (raw buffer loads, out-of-range offsets read 0): the next step's loads
     // stay in flight across this step's LDS stores and MFMAs
     const __amdgpu_buffer_rsrc_t rs_dy = buf_rsrc(dy, Mrows * Ncols * 2);
@@ -292,7 +294,15 @@ __global__ __launch_bounds__(NT) void conv_wgrad_bf16(Geo g, long Mrows, int Nco
             const unsigned offa = (mv && nval) ? (unsigned)((m * Ncols + n) * 2) : kOOB;
             const unsigned offb = (kval && mv && iy >= 0 && iy < g.H && ix >= 0 && ix < g.W)
                                       ? (unsigned)(((((int)b * g.H + iy) * g.W + ix) * g.C + kc) * 2) : kOOB;
-            const u32x4 a4 = __builtin_amdgcn_raw_buffer_load_b128(rs_dy, offa, 0, 0);
+            u32x4 a4;
+            if constexpr (N4) {   // 8-B aligned row segments: columns n..n+3, n+4..n+7
+                const unsigned offa2 = (mv && nval2) ? offa + 8u : kOOB;
+                const u32x2 lo = __builtin_amdgcn_raw_buffer_load_b64(rs_dy, offa, 0, 0);
+                const u32x2 hi = __builtin_amdgcn_raw_buffer_load_b64(rs_dy, offa2, 0, 0);
+                a4 = u32x4{lo[0], lo[1], hi[0], hi[1]};
+            } else {
+                a4 = __builtin_amdgcn_raw_buffer_load_b128(rs_dy, offa, 0, 0);
+            }
             const u32x4 b4 = __builtin_amdgcn_raw_buffer_load_b128(rs_x, offb, 0, 0);
             __builtin_memcpy(&va[q], &a4, 16);
             __builtin_memcpy(&vb[q], &b4, 16);
@@ -1907,7 +1917,9 @@ static int conv_wgrad_impl(const csu_conv_geom* gm, int dtype, const void* x, co
     } else if (dtype == CSU_BF16) {
         const bool small = (long)g.B * g.H * g.W * g.C * 2 < (1L << 31) && M * g.N * 2 < (1L << 31);   // 32-bit offsets
         if (vec && g.N % 8 == 0 && small)
-            conv_wgrad_bf16<<<grid, NT, 0, st>>>(g, M, g.N, K, p.rpc, (const bf16*)x, (const bf16*)dy, part);
+            conv_wgrad_bf16<false><<<grid, NT, 0, st>>>(g, M, g.N, K, p.rpc, (const bf16*)x, (const bf16*)dy, part);
+        else if (vec && g.N % 4 == 0 && small)
+            conv_wgrad_bf16<true><<<grid, NT, 0, st>>>(g, M, g.N, K, p.rpc, (const bf16*)x, (const bf16*)dy, part);
         else if (vec) conv_wgrad_kernel<bf16, true><<<grid, NT, 0, st>>>(g, M, g.N, K, p.rpc, (const bf16*)x, (const bf16*)dy, part);
         else conv_wgrad_kernel<bf16, false><<<grid, NT, 0, st>>>(g, M, g.N, K, p.rpc, (const bf16*)x, (const bf16*)dy, part);
     } else if (dtype == CSU_F32) {

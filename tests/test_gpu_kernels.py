@@ -232,6 +232,34 @@ def test_carafe_module_vs_oracle(B, H, C, s, dtype):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("B,H,C,s", [(1, 5, 8, 2), (2, 4, 16, 2), (1, 6, 32, 2), (2, 5, 64, 2), (1, 3, 512, 2),
+                                     (1, 4, 8, 4)])
+def test_carafe_reassemble_lane_counts(B, H, C, s, dtype):
+    """csu_carafe_fwd / _bwd alone (ops.carafe_reassemble) for every lane count per pixel (G = C / 8:
+    1, 2 -- the all-reduce path -- and 4 .. 64, the S = 2 reduce-scatter) vs a float64 restatement of
+    the reassembly (oracle.cswin_ref.carafe, cswin:410-432): out, d x, d logits."""
+    from csu import ops
+    d = dev()
+    torch.manual_seed(B * 1000 + H * 10 + C + s)
+    x = torch.randn(B, H * H, C)
+    enc = torch.randn(B, H, H, 9 * s * s) * 2
+    gy = torch.randn(B, H * H * s * s, C)
+    x64, e64 = x.double().requires_grad_(True), enc.double().requires_grad_(True)
+    xi = x64.transpose(1, 2).reshape(B, C, H, H)
+    kern = e64.permute(0, 3, 1, 2).reshape(B, 9, s, s, H, H).softmax(dim=1)
+    nb = torch.nn.functional.unfold(xi, 3, padding=1).reshape(B, C, 9, H, H)
+    ref = torch.einsum("btijhw,bcthw->bchiwj", kern, nb).reshape(B, C, H * s * H * s).transpose(1, 2)
+    ref.backward(gy.double())
+    xd = x.to(d, dtype).requires_grad_(True)
+    ed = enc.to(d, dtype).requires_grad_(True)
+    y = ops.carafe_reassemble(xd, ed, H, H, s)
+    y.float().backward(gy.to(d))
+    assert_close(y.float(), ref, dtype)
+    assert_close(xd.grad.float(), x64.grad, dtype)
+    assert_close(ed.grad.float(), e64.grad, dtype)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("B,H,C,s", [(2, 8, 64, 4), (1, 5, 32, 4), (2, 6, 64, 2)])
 def test_carafe_sigmoid_head_vs_oracle(B, H, C, s, dtype):
     """Fused CARAFE(4) + `out` conv + 1-class `output` conv + sigmoid (csu_carafe_head_*) vs the
@@ -572,6 +600,7 @@ CONV_CASES = [  # (B, H, C, N, k, stride, pad)
     (2, 9, 32, 36, 3, 1, 1),      # CARAFE encoder, odd size / N % 8 != 0 (bf16: K split in 2, ragged last part)
     (16, 16, 128, 36, 3, 1, 1),   # CARAFE encoder at 16x16 (512x512 decoder): 32 tiles -> K split (fwd and dgrad)
     (16, 32, 64, 36, 3, 1, 1),    # CARAFE encoder at 32x32: 128 tiles -> K split
+    (1, 10, 32, 68, 3, 1, 1),     # N % 8 == 4 over two N tiles (weight gradient: 8-B dy loads, half-valid tail)
     (1, 12, 8, 24, 3, 1, 1),      # UNet DoubleConv-like
     (2, 6, 40, 16, 1, 1, 0),      # 1x1
     (2, 11, 64, 128, 3, 2, 1),    # stride 2 on an odd size (phase split of the input gradient)
@@ -959,7 +988,7 @@ def test_grad_join(n, adt, bdt):
     assert torch.equal(out._csu_bf16, ref.bfloat16())
 
 
-@pytest.mark.parametrize("n", [16 * 512 * 512, 1000, 4 * 1024 + 3])
+@pytest.mark.parametrize("n", [16 * 512 * 512, 1000, 4 * 1024 + 3, 4000, 3 * 1024 * 1000])
 def test_bce_loss_vs_torch(n):
     """ops.bce_loss (nn.BCELoss mean, cswin:935) vs torch on probabilities incl. exact 0 / 1
     (the -100 log clamp) and targets in {0, 1}; deterministic."""
