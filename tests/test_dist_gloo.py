@@ -1,4 +1,4 @@
-"""Multi-process data-parallel logic on CPU (gloo, world size 2): DDP gradient averaging of the
+"""Multi-process data-parallel logic on CPU (gloo, world size 2 and 4): DDP gradient averaging of the
 sharded batch == the single-process global batch, and the all-reduced per-step metric sums give
 the reference's batch-flattened Dice/IoU of the global batch."""
 import os
@@ -50,7 +50,8 @@ def _worker(rank, world, port, out_path, mode="ddp"):
     from csu.train import _epoch_means
     r, w, device = init_distributed("gloo")
     model, xs, ts = _setup()
-    shard = slice(2 * r, 2 * r + 2)
+    per = 4 // w   # the global batch of 4, equal shards
+    shard = slice(per * r, per * (r + 1))
     if mode == "ddp":
         stats = _train(wrap_ddp(model, device), [(xs[shard], ts[shard])])
     else:   # the graph-capturable bucketed reducer bench.py uses at N > 1, here eager on gloo
@@ -75,10 +76,12 @@ def _worker(rank, world, port, out_path, mode="ddp"):
     torch.distributed.destroy_process_group()
 
 
-@pytest.mark.parametrize("mode", ["ddp", "reducer", "reducer_named", "reducer_bf16"])
-def test_ddp_two_ranks_equals_global_batch(tmp_path, mode):
+@pytest.mark.parametrize("mode,world", [("ddp", 2), ("reducer", 2), ("reducer_named", 2), ("reducer_bf16", 2),
+                                        ("reducer", 4)])
+def test_ddp_two_ranks_equals_global_batch(tmp_path, mode, world):
+    """world 4: one image per rank -- the bucketed reducer's average over more ranks than the 2-GPU case."""
     out = str(tmp_path / "ddp.pt")
-    mp.spawn(_worker, args=(2, _free_port(), out, mode), nprocs=2, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), out, mode), nprocs=world, join=True)
     got = torch.load(out, weights_only=True)
     from csu.train import _epoch_means
     torch.set_num_threads(4)
