@@ -359,6 +359,10 @@ def main():
                "roofline": roof, "cpu_baseline": cpu, "final_loss": round(float(loss.item()), 5),
                "hip_graph": use_graph,
                "grad_allreduce": None if not dp else ("graph-captured buckets" if reducer is not None else "DDP eager")}
+        if reducer is not None:   # of the captured step: buckets, how many started during backward, copy-ins
+            rec["grad_buckets"] = {"buckets": len(reducer.buckets), "started_in_backward": reducer.last_early,
+                                   "grads_copied_in": reducer.last_copied, "bucket_mb": args.bucket_mb,
+                                   "grad_dtype": args.grad_dtype}
         print(json.dumps(rec), flush=True)
     if dp:
         dist.destroy_process_group()

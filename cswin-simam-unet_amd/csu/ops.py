@@ -2065,13 +2065,15 @@ def _conv_geom(B, H, W, C, N, KH, KW, stride, pad):
     return g
 
 
-def _conv_wgrad(g, x, dy, dt, c_real=None):
+def _conv_wgrad(g, x, dy, dt, c_real=None, out=None):
     """fp32 (dW, db) of the forward conv with geometry g: dW in torch's (N, c_real, KH, KW) layout,
     written so by the kernel's final reduction (input channels >= c_real, the zero padding of a
-    few-channel input, dropped); c_real defaults to g.C."""
+    few-channel input, dropped); c_real defaults to g.C.  out: a flat fp32 [dW | db] destination
+    (a GradAllReduce bucket slice, _grad_dest) instead of a fresh buffer."""
     L = lib()
     cr = g.C if c_real is None else c_real
-    out = torch.empty(g.N * g.KH * g.KW * cr + g.N, dtype=torch.float32, device=x.device)
+    if out is None:
+        out = torch.empty(g.N * g.KH * g.KW * cr + g.N, dtype=torch.float32, device=x.device)
     n = L.csu_conv2d_wgrad_workspace(ctypes.byref(g))
     work = torch.empty(max(n, 16), dtype=torch.uint8, device=x.device)
     _launch("conv_wgrad", lambda: L.csu_conv2d_wgrad_oihw(ctypes.byref(g), dt, ptr(x), ptr(dy), cr, ptr(out), ptr(work),
@@ -2167,8 +2169,14 @@ class _Conv2dFn(torch.autograd.Function):
             if dx.dtype != xdt:
                 dx = dx.to(xdt)
 
+        dest = None
+        if has_b and weight.dtype == torch.float32 and bdt == torch.float32:
+            dest = _grad_dest((weight, ctx.bias))   # [dW | db] straight into a GradAllReduce bucket
+            if dest is not None and dest.numel() != N * KH * KW * C + N:
+                dest = None
+
         def wg():   # (dW (N, C, KH, KW) contiguous, db), OIHW and unpadded by the kernel
-            return _conv_wgrad(g, xc, dy, dtype_code(dy), C)
+            return _conv_wgrad(g, xc, dy, dtype_code(dy), C, out=dest)
         if _side_ok(dy, weight.dtype, bdt if has_b else None, params=(weight, ctx.bias)):
             # on the side stream, like the token-Linear weight gradients; the returned grad is
             # contiguous fp32, so autograd steals it without a kernel on this stream

@@ -301,4 +301,6 @@ def test_dp_path_graph_captured_allreduce_matches_single_process():
         assert r.returncode == 0, "\n".join(ln for ln in r.stderr.splitlines() if "frame #" not in ln)[-3000:]
         out[tag] = json.loads(r.stdout.strip().splitlines()[-1])
     assert out["dp"]["grad_allreduce"] == "graph-captured buckets" and out["dp"]["hip_graph"]
+    gb = out["dp"]["grad_buckets"]   # every bucket but the last starts during backward (overlap)
+    assert gb["started_in_backward"] >= gb["buckets"] - 1, gb
     assert out["dp"]["final_loss"] == out["single"]["final_loss"], out
