@@ -703,6 +703,7 @@ class _CarafeHeadFoldedFn(torch.autograd.Function):
         ctx.save_for_backward(x, enc, z, uf, prob, wo, bo, wh)
         ctx.geo = (B, H, W, C, s)
         ctx.pshapes = ((w_out.shape, w_out.dtype), (b_out.shape, b_out.dtype), (w_h.shape, w_h.dtype))
+        ctx.params = (w_out, b_out, w_h)   # for their GradAllReduce bucket slices (_grad_dest)
         return prob
 
     @staticmethod
@@ -713,9 +714,18 @@ class _CarafeHeadFoldedFn(torch.autograd.Function):
         dx, denc = torch.empty_like(x), torch.empty_like(enc)
         du = torch.empty(C, dtype=torch.float32, device=x.device)
         (sw, tw), (sb, tb), (sh, th) = ctx.pshapes
-        dwo = torch.empty(sw, dtype=torch.float32, device=x.device)
-        dbo = torch.empty(sb, dtype=torch.float32, device=x.device)
-        dwh = torch.empty(sh, dtype=torch.float32, device=x.device)
+        O = wo.shape[0]
+        # the folded head's weight gradients straight into their GradAllReduce bucket slices when the
+        # reducer holds them ([dW_out | db_out] adjacent, dw_h on its own), else fresh buffers
+        dest = _grad_dest(ctx.params[:2]) if tw == torch.float32 and tb == torch.float32 else None
+        if dest is not None and dest.numel() == O * C + O:
+            dwo, dbo = dest[:O * C].view(sw), dest[O * C:].view(sb)
+        else:
+            dwo = torch.empty(sw, dtype=torch.float32, device=x.device)
+            dbo = torch.empty(sb, dtype=torch.float32, device=x.device)
+        desth = _grad_dest(ctx.params[2:]) if th == torch.float32 else None
+        dwh = desth.view(sh) if desth is not None and desth.numel() == O else torch.empty(sh, dtype=torch.float32,
+                                                                                          device=x.device)
         fold = _lib.HeadFold()
         fold.O, fold.w_out, fold.b_out, fold.w_h = wo.shape[0], wo.data_ptr(), bo.data_ptr(), wh.data_ptr()
         fold.dw_out, fold.db_out, fold.dw_h = dwo.data_ptr(), dbo.data_ptr(), dwh.data_ptr()

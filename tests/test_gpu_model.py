@@ -303,4 +303,5 @@ def test_dp_path_graph_captured_allreduce_matches_single_process():
     assert out["dp"]["grad_allreduce"] == "graph-captured buckets" and out["dp"]["hip_graph"]
     gb = out["dp"]["grad_buckets"]   # every bucket but the last starts during backward (overlap)
     assert gb["started_in_backward"] >= gb["buckets"] - 1, gb
+    assert gb["grads_copied_in"] == 0, gb   # every gradient written straight into its bucket slice
     assert out["dp"]["final_loss"] == out["single"]["final_loss"], out
