@@ -68,6 +68,7 @@ def parse():
     ap.add_argument("--api", default="step", choices=["step", "train_model"],
                     help="train_model: time the drop-in csu.train.train_model (cswin:751-841) over --steps batches "
                          "(one epoch; its own graph capture after two eager steps) instead of GraphedTrainStep")
+    ap.add_argument("--traffic-key", action="store_true", help="print this workload's PMC traffic key and exit")
     ap.add_argument("--dp-force", action="store_true",
                     help="run the data-parallel path (RCCL process group + captured all-reduce) even at N = 1")
     return ap.parse_args()
@@ -185,7 +186,15 @@ def cpu_baseline(args, dtype):
 def main():
     faulthandler.enable()
     args = parse()
+    if args.traffic_key:
+        print(workload_key(args))
+        return 0
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return _spawn_workers(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus and not (args.gpus == 1 and "WORLD_SIZE" in os.environ):
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr, flush=True)
+        return 2
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dp = world > 1 or args.dp_force
@@ -355,7 +364,7 @@ def main():
                                        f"{f', dropout/attn_drop/drop_path {pd}' if pd > 0 else ''}, AdamW"),
                           "model": "UNet" if args.model == "unet" else "CSWinTransformer", "params": nparams, "global_batch": args.batch * world,
                           "per_gpu_batch": args.batch, "img": args.img, "parallelism": f"dp{world}",
-                          "dropout": pd},
+                          "dropout": pd, "workload_key": workload_key(args)},
                "roofline": roof, "cpu_baseline": cpu, "final_loss": round(float(loss.item()), 5),
                "hip_graph": use_graph,
                "grad_allreduce": None if not dp else ("graph-captured buckets" if reducer is not None else "DDP eager")}
@@ -476,19 +485,49 @@ def _roofline(kernels, ms_per_step, args, graph=False):
             "kernels": kernels}
 
 
+def workload_key(args) -> str:
+    """The workload a PMC traffic figure belongs to: model, depth / split / SimAM (CSWin), the --dtype
+    argument, image size, per-GPU batch and dropout.  Lines of another workload never share a key."""
+    if args.model == "unet":
+        k = f"unet|{args.dtype}|{args.img}|{args.batch}"
+    else:
+        k = (f"cswin|d{args.depth}|s{args.split}|{'simam' if args.simam else 'nosimam'}|{args.dtype}|{args.img}|"
+             f"{args.batch}")
+    return k + (f"|drop{args.dropout}" if args.dropout > 0 else "")
+
+
 def _pmc_traffic(kernel, args):
     """HBM bytes per launch of `kernel` for THIS workload from the committed rocprofv3 PMC summary
-    (profiles/pmc_traffic.json: {"<kernel>|<img>|<batch>|<dtype>": bytes}), else None."""
+    (profiles/pmc_traffic.json: {"<kernel>|<workload_key>": bytes}, tools/pmc_traffic.py), else None
+    (never another workload's counter)."""
     p = os.path.join(REPO, "profiles", "pmc_traffic.json")
     if not os.path.exists(p):
         return None
     try:
         with open(p) as f:
-            key = f"{kernel}|{args.img}|{args.batch}|{args.dtype}" + (f"|d{args.dropout}" if args.dropout > 0 else "")
-            return json.load(f).get(key)
+            return json.load(f).get(f"{kernel}|{workload_key(args)}")
     except Exception:
         return None
 
 
+def _spawn_workers(args) -> int:
+    """--gpus N > 1 without a torch.distributed launcher: start N ranks with torch.distributed.run as
+    a CHILD process (nothing here has touched the GPU yet) and return its exit code.  Refuses when
+    the node has fewer than N GPUs: a multi-GPU request never silently reports a 1-GPU number."""
+    import socket
+    import subprocess
+    n = torch.cuda.device_count()      # does not initialise the GPU on this image
+    if n < args.gpus:
+        print(f"bench.py: --gpus {args.gpus} requested but only {n} GPU(s) visible", file=sys.stderr, flush=True)
+        return 2
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

@@ -10,6 +10,7 @@ averaging, recorded into the train step's HIP graph (DDP is the eager fallback).
 from __future__ import annotations
 
 import contextlib
+import weakref
 import os
 
 import torch
@@ -124,7 +125,7 @@ class GradAllReduce:
             off, vs = 0, []
             for p in b:
                 vs.append(f[off:off + p.numel()].view_as(p))
-                ops._GRAD_DEST[id(p)] = (f, off)
+                ops._GRAD_DEST[id(p)] = (weakref.ref(p), f, off)
                 off += p.numel()
             self.views.append(vs)
         self.where = {id(p): bi for bi, b in enumerate(self.buckets) for p in b}

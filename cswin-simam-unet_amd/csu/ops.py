@@ -3,6 +3,7 @@ kernel; there is no CPU or eager-PyTorch fallback (CPU tensors raise ``CsuError`
 from __future__ import annotations
 
 import ctypes
+import weakref
 from typing import List, Optional, Sequence, Tuple
 
 import torch
@@ -140,6 +141,7 @@ class _StripeAttnFn(torch.autograd.Function):
             it.channels, it.nbranch = geom.heads * geom.head_dim, nb
             _LEPE_PENDING.append((it, work, flat))
             _queue_flush()
+            _late(ctx.params, views)
         grads = [g.to(dt) for g, dt in zip(views, ctx.lepe_dtypes)]
         return (dqkv, None, None, *grads)
 
@@ -230,17 +232,64 @@ _LN_QUEUED = [False]
 
 # forward uses per parameter since the last end-of-backward flush: a parameter used more than once in
 # one graph (weight tying) gets its gradient contributions summed by the autograd engine as they
-# arrive, i.e. read before a deferred reduction has filled them -- such parameters are never deferred
+# arrive, i.e. read before a deferred reduction has filled them -- such parameters are never deferred.
+# Keyed by id(p) with a weak reference that must still point at p: an entry left by a dead parameter
+# (a forward without backward) must not count for a new object that happens to get the same id.
+# Only forwards that can be differentiated count (no_grad / eval forwards leave nothing behind).
 _USES: dict = {}
 
 
 def _note_use(*params):
+    if not torch.is_grad_enabled():
+        return
     if len(_USES) > 65536:
         _USES.clear()
     for p in params:
         p = _leaf(p)
-        if p is not None:
-            _USES[id(p)] = _USES.get(id(p), 0) + 1
+        if p is not None and p.requires_grad:
+            e = _USES.get(id(p))
+            if e is not None and e[0]() is p:
+                e[1] += 1
+            else:
+                _USES[id(p)] = [weakref.ref(p), 1]
+
+
+def _uses(p) -> int:
+    e = _USES.get(id(p))
+    return e[1] if e is not None and e[0]() is p else 0
+
+
+# Gradients handed to autograd BEFORE their values are written (deferred to the end-of-backward
+# grouped launches, or computed on the side stream): AccumulateGrad must steal them (no existing
+# .grad, a singly referenced tensor).  Should it copy one instead, the copy would read the buffer
+# before the kernel that fills it -- a stale or uninitialised first-step gradient.  Every such
+# gradient is recorded here (parameter, data pointer, and the storage to rebuild it -- never the
+# tensor itself, which would add the reference that prevents the steal); after the values are
+# written the parameter's .grad is checked to BE that tensor, and repaired (copied, counted in
+# STATS["late_grad_fixups"]) if autograd copied it.
+_LATE_DEFER: list = []
+_LATE_SIDE: list = []
+STATS = {"late_grad_fixups": 0}
+
+
+def _late(params, grads, side: bool = False):
+    lst = _LATE_SIDE if side else _LATE_DEFER
+    for p, g in zip(params, grads):
+        p = _leaf(p)
+        if p is not None and g is not None:
+            lst.append((weakref.ref(p), g.data_ptr(), g.untyped_storage(), g.storage_offset(), tuple(g.shape),
+                        tuple(g.stride()), g.dtype))
+
+
+def _check_late(lst):
+    items, lst[:] = list(lst), []
+    for pref, dptr, st, off, shape, stride, dt in items:
+        p = pref()
+        if p is None or p.grad is None or p.grad.data_ptr() == dptr:
+            continue
+        src = torch.empty(0, dtype=dt, device=p.grad.device).set_(st, off, shape, stride)
+        p.grad.copy_(src)
+        STATS["late_grad_fixups"] += 1
 
 
 def _reducer_hooks_only(hooks) -> bool:
@@ -273,7 +322,7 @@ def _deferrable(*params) -> bool:
         hooks = getattr(p, "_post_accumulate_grad_hooks", None)
         if hooks and not _reducer_hooks_only(hooks):
             return False
-        if _USES.get(id(p), 0) > 1:
+        if _uses(p) > 1:
             return False
     return True
 
@@ -312,6 +361,7 @@ def _end_of_backward_flush():
     sums) and every LePE weight-gradient reduction (one launch per 32 blocks)."""
     _LN_QUEUED[0] = False
     flush_deferred()
+    _check_late(_LATE_DEFER)
     _USES.clear()
 
 
@@ -343,9 +393,10 @@ def _lepe_flush():
 
 def _ln_params(ctx, rows, C, work, dgb):
     """Reduce (later, batched) or report that the caller must pass dgamma / dbeta pointers."""
-    if not (DEFER_LN and _deferrable(*ctx.params)):
+    if not (DEFER_LN and all(dt == torch.float32 for dt in ctx.pdtypes) and _deferrable(*ctx.params)):
         return False
     _LN_PENDING.append((work, dgb, rows, C))
+    _late(ctx.params, (dgb[:C], dgb[C:]))
     _queue_flush()
     return True
 
@@ -704,6 +755,7 @@ class _CarafeHeadFoldedFn(torch.autograd.Function):
         ctx.geo = (B, H, W, C, s)
         ctx.pshapes = ((w_out.shape, w_out.dtype), (b_out.shape, b_out.dtype), (w_h.shape, w_h.dtype))
         ctx.params = (w_out, b_out, w_h)   # for their GradAllReduce bucket slices (_grad_dest)
+        _note_use(*ctx.params)
         return prob
 
     @staticmethod
@@ -776,18 +828,6 @@ def colsum(x2: torch.Tensor) -> torch.Tensor:
                                            stream_ptr(x2.device)),
             rows * cols, rows * cols * x2.element_size() + cols * 4, prec=prec_of(x2))
     return out
-
-
-def _splitk_wgrad(dy2: torch.Tensor, x2: torch.Tensor) -> torch.Tensor:
-    M = dy2.shape[0]
-    S = max(1, min(128, M // 2048))
-    while S > 1 and M % S:
-        S -= 1
-    if S == 1:
-        return (dy2.t() @ x2).float()
-    N, K = dy2.shape[1], x2.shape[1]
-    part = torch.bmm(dy2.view(S, M // S, N).transpose(1, 2), x2.view(S, M // S, K))
-    return colsum(part.view(S, N * K)).view(N, K)
 
 
 def gemm_f32(layout: int, a: torch.Tensor, b: torch.Tensor, M: int, N: int, K: int, bias=None, resid=None,
@@ -928,10 +968,11 @@ def _grad_dest(params) -> Optional[torch.Tensor]:
         e = _GRAD_DEST.get(id(p)) if p is not None else None
         # a parameter used by several ops of this graph (shared weights): every call's backward would
         # write the same bucket memory while the engine still holds an earlier call's gradient as an
-        # alias of it -- such gradients go to fresh buffers and are summed by the engine
-        if e is None or p.grad is not None or _USES.get(id(p), 0) > 1:
+        # alias of it -- such gradients go to fresh buffers and are summed by the engine.  The entry's
+        # weak reference must be p itself (an id reused by a new object is not registered).
+        if e is None or e[0]() is not p or p.grad is not None or _uses(p) > 1:
             return None
-        flat, off = e
+        _, flat, off = e
         if flat0 is None:
             flat0, off0 = flat, off
         elif flat is not flat0 or off != off0 + n:
@@ -945,8 +986,8 @@ def _param_safe(p) -> bool:
     p = _leaf(p)
     if p is None:
         return True
-    if p.grad is not None or p._backward_hooks:
-        return False
+    if p.grad is not None or p._backward_hooks or _uses(p) > 1:
+        return False   # (shared weights: the engine would sum the side-stream gradient before the join)
     hooks = getattr(p, "_post_accumulate_grad_hooks", None)
     return not hooks or _DIST_SAFE[0]
 
@@ -973,6 +1014,7 @@ def join_side_streams():
         main.wait_event(ev)
     _SIDE_PENDING.clear()
     _SIDE_JOIN_QUEUED[0] = False
+    _check_late(_LATE_SIDE)
 
 
 def _side_run(fn, *inputs):
@@ -1005,8 +1047,14 @@ def wgrad_maybe_side(dy2: torch.Tensor, x2: torch.Tensor, wdt, bdt, params=()):
             and bdt is not None):
         dest = _grad_dest(params)                 # [dW | db] straight into a GradAllReduce bucket
     if _side_ok(dy2, wdt, bdt, params=params):
-        return _side_run(lambda: linear_wgrad(dy2, x2, out=dest), dy2, x2)
-    return linear_wgrad(dy2, x2, out=dest, defer=_wgrad_deferrable(dy2, wdt, bdt, params))
+        r = _side_run(lambda: linear_wgrad(dy2, x2, out=dest), dy2, x2)
+        _late(params, r, side=True)
+        return r
+    defer = _wgrad_deferrable(dy2, wdt, bdt, params)
+    r = linear_wgrad(dy2, x2, out=dest, defer=defer)
+    if defer:
+        _late(params, r)
+    return r
 
 
 # csu_gemm_ex (fused bias / GELU / GELU' / residual token GEMM) runs every bf16 nn.Linear forward
@@ -1082,10 +1130,10 @@ class _LinearFn(torch.autograd.Function):
             if bdt is not None and ctx.needs_input_grad[2]:
                 db = dbf.to(bdt)
             return dx, dw, db, None, None, None
-        if ctx.needs_input_grad[1]:
-            dw = _splitk_wgrad(dy2, xc.reshape(-1, K)).to(wdt)
-        if bdt is not None and ctx.needs_input_grad[2]:
-            db = colsum(dy2).to(bdt)
+        if ctx.needs_input_grad[1] or (bdt is not None and ctx.needs_input_grad[2]):
+            # unreachable with the forward's width checks; no vendor-BLAS fallback
+            raise CsuError(f"linear backward: no csu weight-gradient kernel for {dy2.dtype} with in/out features "
+                           f"{K}/{N}")
         return dx, dw, db, None, None, None
 
 
@@ -1286,8 +1334,10 @@ class _ConcatLinearFn(torch.autograd.Function):
         db_in = gemm(dy2, wt[Ca:], False, bdt_in).view(bshape) if ctx.needs_input_grad[1] else None
         if _wgrad_deferrable(dy2, wdt, bdt, ctx.params):
             dw, dbias = _concat_wgrad(dy2, a2, b2, defer=True, dest=_grad_dest(ctx.params))
+            _late(ctx.params, (dw, dbias))
         elif _side_ok(dy2, wdt, bdt, params=ctx.params):
             dw, dbias = _side_run(lambda: _concat_wgrad(dy2, a2, b2), dy2, a2, b2)
+            _late(ctx.params, (dw, dbias), side=True)
         else:
             dw, dbias = _concat_wgrad(dy2, a2, b2)
         return da, db_in, dw.to(wdt), dbias.to(bdt), None
@@ -1564,7 +1614,7 @@ class _MlpFp8Fn(torch.autograd.Function):
 def mlp_fp8(res, x, fc1: torch.nn.Linear, fc2: torch.nn.Linear, drop: Optional[MlpDrop] = None):
     """The fp8 fused Mlp (_MlpFp8Fn) when the active fp8 weight format holds fc1 / fc2 as an Mlp pair
     (model.set_weight_format('fp8_e4m3') under bf16 autocast), else None."""
-    if _ACTIVE_FP8 is None or not x.is_cuda:
+    if _ACTIVE_FP8 is None or not x.is_cuda or fc1.out_features != 4 * x.shape[-1] or fc2.in_features != fc1.out_features:
         return None
     ops8 = _ACTIVE_FP8.mlp_operands(fc1.weight, fc2.weight)
     if ops8 is None:
@@ -1837,7 +1887,8 @@ class Fp8Weights:
                 continue
             q1, q2 = self.q[i1], self.q[i2]
             N4, C = q1.shape
-            if tuple(q2.shape) != (C, N4) or not lib().csu_mlp_fp8_supported(C):
+            # the fp8 kernels hard-code 4C hidden features (mlp_ratio 4, cswin:337)
+            if N4 != 4 * C or tuple(q2.shape) != (C, N4) or not lib().csu_mlp_fp8_supported(C):
                 continue
             w2p = torch.empty_like(q2)
             w2t = torch.empty(N4, C, dtype=torch.uint8, device=q2.device)
@@ -2054,7 +2105,11 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] =
            out_dtype: Optional[torch.dtype] = None) -> torch.Tensor:
     """nn.Linear on tokens in the autocast compute dtype (bf16 under autocast) with split-K dW.
     ``out_dtype`` (bf16 path only): write the output in that dtype from the fp32 accumulator, e.g.
-    fp32 for a Linear that starts a residual stream."""
+    fp32 for a Linear that starts a residual stream.
+
+    Contract (no vendor-BLAS fallback): device tensors; bf16 in / out features multiples of 8, fp32
+    multiples of 4 -- anything else raises ``CsuError`` (callers with narrower layers zero-pad them,
+    as the model's 1-class head does)."""
     if x.is_cuda and torch.is_autocast_enabled("cuda"):
         cd = torch.get_autocast_dtype("cuda")
     else:
@@ -2150,6 +2205,7 @@ class _Conv2dFn(torch.autograd.Function):
         ctx.save_for_backward(xc, weight)
         ctx.w_ihwo = cached[1] if cached else None   # refreshed only by the next forward's cast
         ctx.bias = bias
+        _note_use(weight, bias)
         ctx.conf = (stride, pad, cd, x.dtype, bias is not None, None if bias is None else bias.dtype)
         return y
 
@@ -2191,6 +2247,7 @@ class _Conv2dFn(torch.autograd.Function):
             # on the side stream, like the token-Linear weight gradients; the returned grad is
             # contiguous fp32, so autograd steals it without a kernel on this stream
             dw, db = _side_run(wg, xc, dy)
+            _late((weight, ctx.bias), (dw, db if has_b else None), side=True)
             return dx, dw, (db if has_b else None), None, None, None
         dw, db = wg()
         return dx, dw.to(weight.dtype), (db.to(bdt) if has_b else None), None, None, None
@@ -2229,6 +2286,7 @@ class _CatConv2dFn(torch.autograd.Function):
         ctx.save_for_backward(xa, xb, weight)
         ctx.w_ihwo = cached[1] if cached else None
         ctx.bias = bias
+        _note_use(weight, bias)
         ctx.conf = (pad, cd, bias is not None, None if bias is None else bias.dtype)
         return y
 
@@ -2261,6 +2319,7 @@ class _CatConv2dFn(torch.autograd.Function):
             return out[:k].view(N, C, KH, KW), out[k:]
         if _side_ok(dy, weight.dtype, bdt if has_b else None, params=(weight, ctx.bias)):
             dw, db = _side_run(wg, xa, xb, dy)
+            _late((weight, ctx.bias), (dw, db if has_b else None), side=True)
             return dxa, dxb, dw, (db if has_b else None), None, None
         dw, db = wg()
         return dxa, dxb, dw.to(weight.dtype), (db.to(bdt) if has_b else None), None, None

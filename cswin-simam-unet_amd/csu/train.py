@@ -374,7 +374,7 @@ class GraphedTrainStep:
     not capturable)."""
 
     def __init__(self, model, optimizer, criterion, example_x, example_t, autocast_dtype=None, warmup=3,
-                 reducer=None, metrics=False):
+                 reducer=None, metrics=False, capture=True):
         self.model, self.opt, self.crit = model, optimizer, criterion
         # metrics (criterion bce_loss): the reference loop's per-step thresholded Dice / IoU sums
         # (cswin:789-795) computed inside the graph by the loss kernel -> self.stats after a replay
@@ -384,6 +384,15 @@ class GraphedTrainStep:
         self.x = example_x.clone()
         self.t = example_t.clone()
         self.dtype = autocast_dtype
+        # capture=False: the same sequence (warm-up steps, static input buffers, the reducer's
+        # bucket hooks + finish, the optimizer) run eagerly at every call -- no streams, no graph, so
+        # it runs on a CPU process group too (the world > 1 reducer order is tested that way on gloo)
+        self.capture = bool(capture)
+        self.graph = None
+        if not self.capture:
+            for _ in range(warmup):
+                self._body()
+            return
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         with warnings.catch_warnings(record=True) as caught:
@@ -451,6 +460,10 @@ class GraphedTrainStep:
     def __call__(self, x, t):
         self.x.copy_(x, non_blocking=True)
         self.t.copy_(t, non_blocking=True)
+        if not self.capture:
+            self.loss, self.out = self._body()
+            self.stats = self._stats
+            return self.loss, self.out
         sync_shadows(self.model)     # weights changed outside the graph since: re-cast before the replay
         self.graph.replay()
         return self.loss, self.out

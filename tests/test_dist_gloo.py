@@ -68,7 +68,22 @@ def _worker(rank, world, port, out_path, mode="ddp"):
             red = GradAllReduce(model.parameters(), bucket_mb=0.05,   # tiny buckets: several per step
                                 grad_dtype=torch.bfloat16 if mode == "reducer_bf16" else torch.float32)
         assert len(red.buckets) > 2
-        stats = _train(model, [(xs[shard], ts[shard])], reducer=red)
+        if mode == "graphed":
+            # GraphedTrainStep(reducer=...)'s own sequence (static input buffers, backward with the
+            # bucket hooks, finish(), optimizer) at world > 1 -- the capture itself needs a GPU
+            from csu.train import GraphedTrainStep, _step_stats, bce_loss
+            opt = torch.optim.AdamW(model.parameters(), lr=1e-3, weight_decay=1e-4)
+            x, t = xs[shard], ts[shard]
+            gs = GraphedTrainStep(model, opt, bce_loss, x, t, None, warmup=0, reducer=red, capture=False)
+            stats = []
+            for _ in range(2):
+                loss, out = gs(x, t)
+                stats.append(_step_stats(loss, out, t))
+                assert red.last_early >= len(red.buckets) - 1, (red.last_early, len(red.buckets))
+                assert all(p.grad.data_ptr() == v.data_ptr() for b, vs in zip(red.buckets, red.views)
+                           for p, v in zip(b, vs))   # every .grad is its averaged bucket slice
+        else:
+            stats = _train(model, [(xs[shard], ts[shard])], reducer=red)
         assert red.last_early >= len(red.buckets) - 1, (red.last_early, len(red.buckets))
     means = _epoch_means(stats)
     if r == 0:
@@ -77,7 +92,7 @@ def _worker(rank, world, port, out_path, mode="ddp"):
 
 
 @pytest.mark.parametrize("mode,world", [("ddp", 2), ("reducer", 2), ("reducer_named", 2), ("reducer_bf16", 2),
-                                        ("reducer", 4)])
+                                        ("reducer", 4), ("graphed", 2)])
 def test_ddp_two_ranks_equals_global_batch(tmp_path, mode, world):
     """world 4: one image per rank -- the bucketed reducer's average over more ranks than the 2-GPU case."""
     out = str(tmp_path / "ddp.pt")
@@ -121,11 +136,13 @@ def test_epoch_means_match_reference_formula():
 def test_grad_dest_registry_contiguity():
     """ops._grad_dest hands out a bucket slice only for parameters adjacent in registration order
     with no existing .grad (csu.dist.GradAllReduce registers them; the ops then write in place)."""
+    import weakref
     sys.path[:0] = [REPO, os.path.join(REPO, "cswin-simam-unet_amd")]
     from csu import ops
     a, b, c = (torch.nn.Parameter(torch.zeros(*s)) for s in ((3, 4), (3,), (5,)))
     flat = torch.zeros(20)
-    ops._GRAD_DEST.update({id(a): (flat, 0), id(b): (flat, 12), id(c): (flat, 15)})
+    ops._GRAD_DEST.update({id(a): (weakref.ref(a), flat, 0), id(b): (weakref.ref(b), flat, 12),
+                           id(c): (weakref.ref(c), flat, 15)})
     try:
         d = ops._grad_dest((a, b))
         assert d is not None and d.data_ptr() == flat.data_ptr() and d.numel() == 15
@@ -135,10 +152,87 @@ def test_grad_dest_registry_contiguity():
         a.grad = torch.zeros(3, 4)
         assert ops._grad_dest((a, b)) is None            # gradient accumulation: no stealing
         a.grad = None
-        ops._USES[id(b)] = 2
+        ops._note_use(b)
+        ops._note_use(b)
+        assert ops._uses(b) == 2
         assert ops._grad_dest((a, b)) is None            # shared parameter: the engine sums its uses
         assert ops._grad_dest((c,)) is not None
     finally:
         ops._USES.clear()
         for p in (a, b, c):
             ops._GRAD_DEST.pop(id(p), None)
+
+
+def test_stale_ids_do_not_leak_into_new_parameters():
+    """_USES / _GRAD_DEST are keyed by id(p): an entry left behind by a dead parameter (a forward
+    without backward, a reducer never removed) must not apply to a new object that reuses the id --
+    otherwise a parameter's deferral / bucket destination would depend on the allocation history
+    (the cause of the intermittent concat-Linear bias differences)."""
+    import weakref
+    sys.path[:0] = [REPO, os.path.join(REPO, "cswin-simam-unet_amd")]
+    from csu import ops
+    old = torch.nn.Parameter(torch.zeros(4))
+    ops._note_use(old)
+    ops._note_use(old)
+    flat = torch.zeros(4)
+    ops._GRAD_DEST[id(old)] = (weakref.ref(old), flat, 0)
+    ops._USES[id(old)][0] = weakref.ref(torch.nn.Parameter(torch.zeros(1)))   # now points elsewhere
+    ops._GRAD_DEST[id(old)] = (weakref.ref(torch.nn.Parameter(torch.zeros(1))), flat, 0)
+    try:
+        assert ops._uses(old) == 0                      # the entry is someone else's
+        assert ops._grad_dest((old,)) is None
+        # no_grad forwards count nothing
+        new = torch.nn.Parameter(torch.zeros(4))
+        with torch.no_grad():
+            ops._note_use(new)
+        assert ops._uses(new) == 0
+        ops._note_use(new)
+        assert ops._uses(new) == 1
+    finally:
+        ops._USES.clear()
+        ops._GRAD_DEST.pop(id(old), None)
+
+
+def test_late_gradient_copied_by_autograd_is_repaired():
+    """A gradient handed to autograd before its values exist (deferred / side stream) must be stolen
+    by AccumulateGrad; if autograd copies it instead (an extra reference), the end-of-backward check
+    copies the final values into .grad (ops._check_late) and counts it."""
+    sys.path[:0] = [REPO, os.path.join(REPO, "cswin-simam-unet_amd")]
+    from csu import ops
+    p = torch.nn.Parameter(torch.zeros(6))
+    buf = torch.zeros(8)
+    keep = []
+
+    class Late(torch.autograd.Function):
+        @staticmethod
+        def forward(ctx, x, w):
+            return x * 1.0
+
+        @staticmethod
+        def backward(ctx, g):
+            gw = buf[2:]
+            keep.append(gw)            # a second reference: AccumulateGrad must copy it now
+            ops._late((p,), (gw,))
+            return g, gw
+
+    n0 = ops.STATS["late_grad_fixups"]
+    Late.apply(torch.ones(3, requires_grad=True), p).sum().backward()
+    assert p.grad is not None and p.grad.data_ptr() != buf[2:].data_ptr()
+    buf[2:] = torch.arange(6.0)      # the "deferred kernel" writes the values after the copy
+    ops._check_late(ops._LATE_DEFER)
+    assert ops.STATS["late_grad_fixups"] == n0 + 1
+    assert torch.equal(p.grad, torch.arange(6.0))
+    # a stolen gradient is left alone
+    p.grad = None
+    keep.clear()
+
+    class Steal(Late):
+        @staticmethod
+        def backward(ctx, g):
+            gw = buf[2:]
+            ops._late((p,), (gw,))
+            return g, gw
+    Steal.apply(torch.ones(3, requires_grad=True), p).sum().backward()
+    assert p.grad.data_ptr() == buf[2:].data_ptr()
+    ops._check_late(ops._LATE_DEFER)
+    assert ops.STATS["late_grad_fixups"] == n0 + 1

@@ -365,3 +365,24 @@ def test_mlp_fp8_fused_vs_oracle(C, M, drop):
 
 def _snap_t(d, seed, ctr):
     return torch.tensor([seed, ctr], dtype=torch.int64, device=d)
+
+
+def test_fp8_mlp_ratio_not_4_falls_back_to_bf16_mlp(monkeypatch):
+    """The fp8 fused Mlp kernels hard-code 4C hidden features: a model built with mlp_ratio 2 in the
+    fp8 weight format registers no fp8 Mlp pair and runs its Mlps on the bf16 path."""
+    from csu import ops
+    from csu.model import CSWinTransformer
+    d = dev()
+    torch.manual_seed(0)
+    m = CSWinTransformer(img_size=128, split_size=[1, 2, 4, 4], mlp_ratio=2.0).to(d).set_weight_format("fp8_e4m3")
+    got = []
+    real = ops.mlp_fp8
+    monkeypatch.setattr(ops, "mlp_fp8", lambda *a, **k: (lambda r: got.append(r is not None) or r)(real(*a, **k)))
+    x = torch.randn(2, 3, 128, 128, device=d)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = m(x)
+    y.sum().backward()
+    assert got and not any(got)
+    assert not m._fp8.mlp
+    assert torch.isfinite(y).all()
+    assert all(torch.isfinite(p.grad).all() for p in m.parameters() if p.grad is not None)

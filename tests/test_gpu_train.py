@@ -281,9 +281,6 @@ def test_train_model_graphed_equals_eager():
 
 
 @pytest.mark.parametrize("side_in_graph", [False, True])
-@pytest.mark.xfail(strict=False, reason="known issue (DESIGN.md §6): about one full-suite run in three, two independent "
-                   "captures differ by ~1 ulp in the concat-Linear bias gradients only (concat_linear3/4.bias, "
-                   "r06r_gpu_tests.log); losses and every other parameter stay bitwise equal -- root cause open")
 def test_graph_replays_bitwise_reproducible(side_in_graph, monkeypatch):
     """Two independent captures of the whole bf16 train step (GraphedTrainStep) replayed on the
     same batches give bitwise-equal losses and parameters (tools/det_graph.py as a test).
@@ -312,6 +309,74 @@ def test_graph_replays_bitwise_reproducible(side_in_graph, monkeypatch):
     names = [n for n, _ in m0.named_parameters()]
     diff = [(n, float((a - b).abs().max())) for n, a, b in zip(names, res[0][1], res[1][1]) if not torch.equal(a, b)]
     assert not diff, diff
+
+
+def test_late_gradients_are_stolen_not_copied():
+    """Every gradient csu hands to autograd before writing it (deferred LayerNorm / Linear / concat
+    Linear / LePE parameter gradients) is taken over by AccumulateGrad as the parameter's .grad in the
+    eager steps and in the capture -- no copy made before the values exist (ops._check_late would
+    repair one and count it; DESIGN.md §6: the round-4 concat-Linear bias nondeterminism)."""
+    from csu import ops
+    from csu.data import ellipse_batch
+    from csu.model import CSWinTransformer
+    from csu.train import GraphedTrainStep, bce_loss, make_optimizer
+    d = dev()
+    torch.manual_seed(0)
+    m = CSWinTransformer(img_size=128, split_size=[1, 2, 4, 4]).to(d)
+    x, t = (v.to(d) for v in ellipse_batch(np.random.default_rng(1), 4, 128))
+    n0 = ops.STATS["late_grad_fixups"]
+    ops._LATE_DEFER.clear()
+    seen = []
+    real = ops._late
+    ops_late = lambda params, grads, side=False: (seen.append(len(params)), real(params, grads, side))  # noqa: E731
+    import unittest.mock as um
+    with um.patch.object(ops, "_late", ops_late):
+        gs = GraphedTrainStep(m, make_optimizer(m, capturable=True), bce_loss, x, t, torch.bfloat16, warmup=2)
+        gs(x, t)
+    torch.cuda.synchronize()
+    assert sum(seen) > 100                       # the deferred gradients were registered
+    assert ops.STATS["late_grad_fixups"] == n0, ops.STATS
+    assert not ops._LATE_DEFER
+
+
+FULL_CONFIGS = [
+    # (img, batch, depth, split, simam, fmt) -- BASELINE configs[2..4] at their full per-GPU sizes
+    (512, 16, [1, 2, 9, 1], [1, 2, 8, 8], False, None),
+    (512, 16, [1, 2, 9, 1], [1, 2, 8, 8], True, None),
+    (512, 16, [2, 4, 32, 2], [1, 2, 8, 8], False, None),
+    (1024, 4, [1, 2, 9, 1], [1, 2, 8, 8], False, None),
+    (1024, 4, [1, 2, 9, 1], [1, 2, 8, 8], False, "fp8_e4m3"),
+]
+
+
+@pytest.mark.parametrize("img,batch,depth,split,simam,fmt", FULL_CONFIGS)
+def test_full_size_config_graphed_steps(img, batch, depth, split, simam, fmt):
+    """One captured train step of every BASELINE GPU config at its full size (the bench shapes):
+    finite loss, finite and non-zero gradient norm of every parameter, and the loss falls over 3
+    replays on one batch."""
+    from csu.data import ellipse_batch
+    from csu.model import CSWinTransformer
+    from csu.train import GraphedTrainStep, bce_loss, make_optimizer
+    d = dev()
+    torch.manual_seed(0)
+    m = CSWinTransformer(img_size=img, depth=depth, split_size=split, simam=simam).to(d)
+    if fmt:
+        m.set_weight_format(fmt)
+    x, t = (v.to(d) for v in ellipse_batch(np.random.default_rng(3), batch, img))
+    opt = make_optimizer(m, lr=1e-4, capturable=True)
+    gs = GraphedTrainStep(m, opt, bce_loss, x, t, torch.bfloat16, warmup=1)
+    losses = []
+    for _ in range(3):
+        loss, _ = gs(x, t)
+        losses.append(float(loss.item()))
+    torch.cuda.synchronize()
+    assert all(np.isfinite(losses)), losses
+    assert losses[2] < losses[0], losses
+    norms = {n: float(p.grad.float().norm()) for n, p in m.named_parameters()}
+    bad = {n: v for n, v in norms.items() if not (np.isfinite(v) and v > 0)}
+    assert not bad, bad
+    del gs, opt, m
+    torch.cuda.empty_cache()
 
 
 def test_graphed_step_metrics_in_graph():

@@ -100,14 +100,16 @@ def main():
               f"{hbm / (t * 1e-6) / 1e9 if t else 0:.0f} |")
     if tj:
         c = rec["config"]
-        suffix = f"|{c.get('img')}|{c.get('per_gpu_batch')}|{rec['dtype']}"
+        if "workload_key" not in c:
+            raise SystemExit("bench JSON without config.workload_key (bench.py before round 5): traffic not merged")
+        suffix = "|" + c["workload_key"]
         db = json.load(open(tj)) if os.path.exists(tj) else {}
         for g, a in G.items():
             L = ledger.get(g)
             if L and L.get("launches_per_step"):
                 db[g + suffix] = int(row(a)[1] / L["launches_per_step"])
         db["_note"] = ("HBM bytes per ledger launch from rocprofv3 PMC passes (2 x FETCH_SIZE + WRITE_SIZE), "
-                       "tools/pmc_groups.py --traffic over profiles/r03k_pmc_*; key <call>|<img>|<batch>|<dtype>")
+                       "tools/pmc_groups.py --traffic over profiles/r03k_pmc_*; key <call>|<bench.py workload_key>")
         db.pop("_detail", None)
         with open(tj, "w") as f:
             json.dump(db, f, indent=1, sort_keys=True)
