@@ -88,7 +88,7 @@ class _StripeAttnFn(torch.autograd.Function):
         ctx.geom, ctx.drop = geom, drop
         ctx.lepe_dtypes = [t.dtype for t in lepe]
         ctx.params = tuple(lepe)   # the caller's objects (saved tensors unpack into new wrappers)
-        _note_use(*ctx.params)
+        _note_use(ctx, *ctx.params)
         ctx.save_for_backward(qkv, out, lse, *ws, *bs)
         return out
 
@@ -239,8 +239,12 @@ _LN_QUEUED = [False]
 _USES: dict = {}
 
 
-def _note_use(*params):
-    if not torch.is_grad_enabled():
+def _note_use(ctx, *params):
+    """Count one use of each parameter by the op whose autograd context is ``ctx`` -- only when that
+    call is recorded for backward (inside Function.forward grad mode is always off and
+    needs_input_grad ignores it; a recorded call's node has its next edges already: no_grad / eval
+    forwards have none).  ctx None: count unconditionally."""
+    if ctx is not None and not ctx.next_functions:
         return
     if len(_USES) > 65536:
         _USES.clear()
@@ -483,7 +487,7 @@ class _LayerNormFn(torch.autograd.Function):
         ctx.save_for_backward(x, w, mean, rstd)
         ctx.pdtypes = (weight.dtype, bias.dtype)
         ctx.params = (weight, bias)
-        _note_use(*ctx.params)
+        _note_use(ctx, *ctx.params)
         return y
 
     @staticmethod
@@ -554,7 +558,7 @@ class _LayerNormForkFn(torch.autograd.Function):
         ctx.save_for_backward(x, w, mean, rstd)
         ctx.pdtypes = (weight.dtype, bias.dtype)
         ctx.params = (weight, bias)
-        _note_use(*ctx.params)
+        _note_use(ctx, *ctx.params)
         return x.view_as(x), y
 
     @staticmethod
@@ -755,7 +759,7 @@ class _CarafeHeadFoldedFn(torch.autograd.Function):
         ctx.geo = (B, H, W, C, s)
         ctx.pshapes = ((w_out.shape, w_out.dtype), (b_out.shape, b_out.dtype), (w_h.shape, w_h.dtype))
         ctx.params = (w_out, b_out, w_h)   # for their GradAllReduce bucket slices (_grad_dest)
-        _note_use(*ctx.params)
+        _note_use(ctx, *ctx.params)
         return prob
 
     @staticmethod
@@ -1097,7 +1101,7 @@ class _LinearFn(torch.autograd.Function):
         ctx.save_for_backward(xc, wt if ctx.fast else wc)
         ctx.meta = (x.dtype, weight.dtype, None if bias is None else bias.dtype)
         ctx.params = (weight, bias)
-        _note_use(*ctx.params)
+        _note_use(ctx, *ctx.params)
         return y
 
     @staticmethod
@@ -1321,7 +1325,7 @@ class _ConcatLinearFn(torch.autograd.Function):
         ctx.save_for_backward(a2, b2, _weight_t(weight, wc))
         ctx.meta = (a.shape, b.shape, a.dtype, b.dtype, weight.dtype, bias.dtype)
         ctx.params = (weight, bias)
-        _note_use(*ctx.params)
+        _note_use(ctx, *ctx.params)
         return y.view(*a.shape[:-1], N)
 
     @staticmethod
@@ -1369,7 +1373,7 @@ class _LinearResidualFn(torch.autograd.Function):
         ctx.save_for_backward(x2, _weight_t(weight, wc))
         ctx.meta = (res.dtype, x.shape, weight.dtype, bias.dtype)
         ctx.params = (weight, bias)
-        _note_use(*ctx.params)
+        _note_use(ctx, *ctx.params)
         return y.view(res.shape)
 
     @staticmethod
@@ -1432,7 +1436,7 @@ class _MlpResidualFn(torch.autograd.Function):
         ctx.save_for_backward(x2, h, g, _weight_t(w1, w1c), _weight_t(w2, w2c))
         ctx.meta = (res.dtype, x.shape, w1.dtype, b1.dtype, w2.dtype, b2.dtype)
         ctx.params = (w1, b1, w2, b2)
-        _note_use(*ctx.params)
+        _note_use(ctx, *ctx.params)
         ctx.drop = drop
         return y.view(res.shape)
 
@@ -1511,7 +1515,7 @@ class _MlpFusedFn(torch.autograd.Function):
         ctx.save_for_backward(x2, w1c, b1f, w2c)
         ctx.meta = (res.dtype, x.shape, w1.dtype, b1.dtype, w2.dtype, b2.dtype)
         ctx.params = (w1, b1, w2, b2)
-        _note_use(*ctx.params)
+        _note_use(ctx, *ctx.params)
         return y.view(res.shape)
 
     @staticmethod
@@ -1576,7 +1580,7 @@ class _MlpFp8Fn(torch.autograd.Function):
         ctx.wc = (w1c, w2c)
         ctx.meta = (res.dtype, x.shape, w1.dtype, b1.dtype, w2.dtype, b2.dtype)
         ctx.params = (w1, b1, w2, b2)
-        _note_use(*ctx.params)
+        _note_use(ctx, *ctx.params)
         return y.view(res.shape)
 
     @staticmethod
@@ -2063,7 +2067,7 @@ class _LnLinearFp8Fn(torch.autograd.Function):
         ctx.pdtypes = (gamma.dtype, beta.dtype)
         ctx.lin = (weight, bias)
         ctx.lmeta = (weight.dtype, None if bias is None else bias.dtype, C)
-        _note_use(gamma, beta, weight, bias)
+        _note_use(ctx, gamma, beta, weight, bias)
         return x.view_as(x), y
 
     @staticmethod
@@ -2205,7 +2209,7 @@ class _Conv2dFn(torch.autograd.Function):
         ctx.save_for_backward(xc, weight)
         ctx.w_ihwo = cached[1] if cached else None   # refreshed only by the next forward's cast
         ctx.bias = bias
-        _note_use(weight, bias)
+        _note_use(ctx, weight, bias)
         ctx.conf = (stride, pad, cd, x.dtype, bias is not None, None if bias is None else bias.dtype)
         return y
 
@@ -2286,7 +2290,7 @@ class _CatConv2dFn(torch.autograd.Function):
         ctx.save_for_backward(xa, xb, weight)
         ctx.w_ihwo = cached[1] if cached else None
         ctx.bias = bias
-        _note_use(weight, bias)
+        _note_use(ctx, weight, bias)
         ctx.conf = (pad, cd, bias is not None, None if bias is None else bias.dtype)
         return y
 

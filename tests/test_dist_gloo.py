@@ -152,8 +152,8 @@ def test_grad_dest_registry_contiguity():
         a.grad = torch.zeros(3, 4)
         assert ops._grad_dest((a, b)) is None            # gradient accumulation: no stealing
         a.grad = None
-        ops._note_use(b)
-        ops._note_use(b)
+        ops._note_use(None, b)
+        ops._note_use(None, b)
         assert ops._uses(b) == 2
         assert ops._grad_dest((a, b)) is None            # shared parameter: the engine sums its uses
         assert ops._grad_dest((c,)) is not None
@@ -172,8 +172,8 @@ def test_stale_ids_do_not_leak_into_new_parameters():
     sys.path[:0] = [REPO, os.path.join(REPO, "cswin-simam-unet_amd")]
     from csu import ops
     old = torch.nn.Parameter(torch.zeros(4))
-    ops._note_use(old)
-    ops._note_use(old)
+    ops._note_use(None, old)
+    ops._note_use(None, old)
     flat = torch.zeros(4)
     ops._GRAD_DEST[id(old)] = (weakref.ref(old), flat, 0)
     ops._USES[id(old)][0] = weakref.ref(torch.nn.Parameter(torch.zeros(1)))   # now points elsewhere
@@ -181,13 +181,27 @@ def test_stale_ids_do_not_leak_into_new_parameters():
     try:
         assert ops._uses(old) == 0                      # the entry is someone else's
         assert ops._grad_dest((old,)) is None
-        # no_grad forwards count nothing
+        # calls that cannot be differentiated (no_grad / eval forwards) count nothing: the op's ctx says so
         new = torch.nn.Parameter(torch.zeros(4))
+        seen = []
+
+        class Op(torch.autograd.Function):
+            @staticmethod
+            def forward(ctx, x, w):
+                ops._note_use(ctx, w)
+                seen.append(ops._uses(w))
+                return x * 1.0
+
+            @staticmethod
+            def backward(ctx, g):
+                return g, None
         with torch.no_grad():
-            ops._note_use(new)
-        assert ops._uses(new) == 0
-        ops._note_use(new)
-        assert ops._uses(new) == 1
+            Op.apply(torch.ones(2), new)
+        assert seen[-1] == 0
+        Op.apply(torch.ones(2), new)
+        assert seen[-1] == 1
+        Op.apply(torch.ones(2), new)
+        assert seen[-1] == 2
     finally:
         ops._USES.clear()
         ops._GRAD_DEST.pop(id(old), None)
