@@ -556,6 +556,7 @@ class CSWinTransformer(nn.Module):
             self._cast_cache.refresh(weights, cd, self._conv_weights(), sources=sources)
             if sources is not None:
                 self._fp8.quantize(self._cast_cache)   # one launch: e4m3 + scales + exact bf16 shadows
+            self._cast_cache.refresh_frag()   # fragment-ordered W / W^T of the qkv / proj Linears (csu_gemm_ws)
             ops.set_cast_cache(self._cast_cache, self._fp8 if sources is not None else None)
         try:
             return self._forward(x)

@@ -9,7 +9,7 @@ from typing import List, Optional, Sequence, Tuple
 import torch
 
 from . import _lib
-from ._lib import CSU_F32, CsuError, check, dtype_code, lib, ptr, require_device, stream_ptr
+from ._lib import CSU_BF16, CSU_F32, CsuError, check, dtype_code, lib, ptr, require_device, stream_ptr
 from .ledger import esize, launch as _launch, prec_of
 
 
@@ -915,6 +915,31 @@ def gemm(a2: torch.Tensor, b: torch.Tensor, b_trans: bool, out_dtype, bias=None,
     return (out, g) if gelu_out else out
 
 
+# csu_gemm_ws (weight-streaming token GEMM, csrc/gemm_ws.hip) for the shapes it is instantiated for,
+# when the cast cache holds the fragment-ordered weight; gemm4 otherwise
+USE_GEMM_WS = True
+
+
+def gemm_ws(x2: torch.Tensor, w_frag: torch.Tensor, N: int, out_dtype, bias=None, resid=None) -> torch.Tensor:
+    """out (M, N) = x2 (M, K) @ W^T (+ bias) (+ resid) with W given fragment-ordered (CastCache.get_frag)."""
+    M, K = x2.shape
+    out = torch.empty(M, N, dtype=out_dtype, device=x2.device)
+    nb = M * K * 2 + N * K * 2 + M * N * out.element_size() + (M * N * 4 if resid is not None else 0)
+    _launch("gemm", lambda: lib().csu_gemm_ws(M, N, K, ptr(x2), x2.stride(0), ptr(w_frag), ptr(bias), ptr(resid),
+                                              dtype_code(out), ptr(out), stream_ptr(x2.device)),
+            2 * M * N * K, nb, prec="bf16",
+            tag=f"{M}x{N}x{K}{'r' if resid is not None else ''}{'b' if bias is not None else ''}:{out_dtype}:ws")
+    return out
+
+
+def _ws_ok(M, N, K, out_dtype, resid=False) -> bool:
+    return USE_GEMM_WS and bool(lib().csu_gemm_ws_supported(M, N, K, int(resid), dtype_code_of(out_dtype)))
+
+
+def dtype_code_of(dt) -> int:
+    return CSU_F32 if dt == torch.float32 else 1
+
+
 # ---------------------------------------------------------------------------------------------
 # Weight gradients on a side stream.  dW = dY^T X of a Linear is off the backward critical path
 # (nothing in the rest of backward reads it), so in eager steps it runs on a second HIP stream
@@ -1084,11 +1109,18 @@ class _LinearFn(torch.autograd.Function):
         ctx.fast = cd == torch.bfloat16 and _gemm_ok(K, N)
         ctx.f32 = False
         wt = None
+        ctx.wtf = None
         if ctx.fast:
             x2 = xc.reshape(-1, K).contiguous()
-            y = gemm(x2, wc, False, odt or cd, bias=None if bias is None else bias.detach().float().contiguous())
+            bf = None if bias is None else bias.detach().float().contiguous()
+            wf = _ACTIVE_CACHE.get_frag(weight) if _ACTIVE_CACHE is not None else None
+            if wf is not None and _ws_ok(x2.shape[0], N, K, odt or cd):
+                y = gemm_ws(x2, wf, N, odt or cd, bias=bf)
+            else:
+                y = gemm(x2, wc, False, odt or cd, bias=bf)
             y = y.view(*xc.shape[:-1], N)
             wt = _weight_t(weight, wc)
+            ctx.wtf = _ACTIVE_CACHE.get_frag_t(weight) if _ACTIVE_CACHE is not None else None
         elif cd == torch.float32 and K % 4 == 0 and N % 4 == 0:
             # fp32 path (no autocast, BASELINE config 2): csu fp32 MFMA GEMM, bias in its epilogue
             x2 = xc.reshape(-1, K).contiguous()
@@ -1120,7 +1152,10 @@ class _LinearFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             if ctx.fast:
                 odt = xdt if xdt in (torch.float32, torch.bfloat16) else wc.dtype
-                dx = gemm(dy2, wc, False, odt).view(xc.shape)
+                if ctx.wtf is not None and _ws_ok(dy2.shape[0], K, N, odt):
+                    dx = gemm_ws(dy2, ctx.wtf, K, odt).view(xc.shape)
+                else:
+                    dx = gemm(dy2, wc, False, odt).view(xc.shape)
             else:
                 dx = gemm_f32(1, dy2, wc.contiguous(), dy2.shape[0], K, N).view(xc.shape)
             if dx.dtype != xdt:
@@ -1369,8 +1404,15 @@ class _LinearResidualFn(torch.autograd.Function):
     def forward(ctx, res, x, weight, bias, wc):
         res2 = res.float().contiguous().view(-1, res.shape[-1])
         x2 = x.reshape(-1, x.shape[-1]).contiguous()
-        y = gemm(x2, wc, False, torch.float32, bias=bias.detach().float().contiguous(), resid=res2)
+        M, K, N = x2.shape[0], x2.shape[1], wc.shape[0]
+        bf = bias.detach().float().contiguous()
+        wf = _ACTIVE_CACHE.get_frag(weight) if _ACTIVE_CACHE is not None else None
+        if wf is not None and _ws_ok(M, N, K, torch.float32, resid=True):
+            y = gemm_ws(x2, wf, N, torch.float32, bias=bf, resid=res2)
+        else:
+            y = gemm(x2, wc, False, torch.float32, bias=bf, resid=res2)
         ctx.save_for_backward(x2, _weight_t(weight, wc))
+        ctx.wtf = _ACTIVE_CACHE.get_frag_t(weight) if _ACTIVE_CACHE is not None else None
         ctx.meta = (res.dtype, x.shape, weight.dtype, bias.dtype)
         ctx.params = (weight, bias)
         _note_use(ctx, *ctx.params)
@@ -1381,7 +1423,11 @@ class _LinearResidualFn(torch.autograd.Function):
         x2, wt = ctx.saved_tensors
         rdt, xshape, wdt, bdt = ctx.meta
         dyb = _bf16_of(dy).view(-1, dy.shape[-1])
-        dx = gemm(dyb, wt, False, torch.bfloat16).view(xshape)
+        M, N, K = dyb.shape[0], dyb.shape[1], x2.shape[1]
+        if ctx.wtf is not None and _ws_ok(M, K, N, torch.bfloat16):
+            dx = gemm_ws(dyb.contiguous(), ctx.wtf, K, torch.bfloat16).view(xshape)
+        else:
+            dx = gemm(dyb, wt, False, torch.bfloat16).view(xshape)
         dw, db = wgrad_maybe_side(dyb, x2, wdt, bdt, params=ctx.params)
         return dy.to(rdt), dx, dw.to(wdt), db.to(bdt), None
 
@@ -1730,6 +1776,7 @@ class CastCache:
         self.index = {p.data_ptr(): i for i, p in enumerate(params)}
         self.cindex = {w.data_ptr(): i for i, w in enumerate(convs)}
         self.items = None
+        self._build_frag(params, dtype)
         allp = params + convs
         self._written = [None] * len(allp)
         for k in [k for k, e in _SHADOW_SPECS.items() if e[1] is self]:
@@ -1804,6 +1851,60 @@ class CastCache:
 
     def _fresh(self) -> bool:
         return all(w is not None and w == p._version for w, p in zip(self._written, self.params + self.convs))
+
+    # Fragment-ordered copies of the bf16 shadows W / W^T that the weight-streaming GEMM reads
+    # (csu_gemm_ws: the qkv / proj Linears and their input gradients at C = 128 / 256), made from the
+    # finished natural-layout shadows by ONE csu_frag_layout_batch launch per forward (refresh_frag,
+    # after AdamW / the cast batch / the fp8 quantiser wrote them).
+    def _build_frag(self, params, dtype):
+        import numpy as np
+        self.frag_w, self.frag_t = [None] * len(params), [None] * len(params)
+        self.frag_items, self.frag_n, self.frag_chunks = None, 0, 0
+        if not USE_GEMM_WS or dtype != torch.bfloat16 or not params or not all(p.is_cuda for p in params):
+            return
+        L = lib()
+        recs = []
+        for i, p in enumerate(params):
+            if p.dim() != 2:
+                continue
+            N, K = p.shape
+            if L.csu_gemm_ws_supported(64, N, K, 0, CSU_BF16):
+                self.frag_w[i] = torch.empty(N * K, dtype=dtype, device=p.device)
+                recs.append((self.shadow[i], self.frag_w[i], N, K))
+            if L.csu_gemm_ws_supported(64, K, N, 0, CSU_BF16) and self.shadow_t[i] is not None:
+                self.frag_t[i] = torch.empty(N * K, dtype=dtype, device=p.device)
+                recs.append((self.shadow_t[i], self.frag_t[i], K, N))
+        if not recs:
+            return
+        rec = np.zeros(len(recs), dtype=[("src", "<u8"), ("dst", "<u8"), ("rows", "<i4"), ("cols", "<i4"), ("chunk0", "<i8")])
+        c0 = 0
+        for k, (src, dst, rows, cols) in enumerate(recs):
+            rec[k] = (src.data_ptr(), dst.data_ptr(), rows, cols, c0)
+            c0 += rows * cols // 8
+        self.frag_n, self.frag_chunks = len(recs), c0
+        self.frag_items = torch.frombuffer(bytearray(rec.tobytes()), dtype=torch.uint8).to(params[0].device)
+
+    def refresh_frag(self):
+        """Re-make the fragment-ordered shadows from the current natural ones (one launch)."""
+        if self.frag_items is None:
+            return
+        n = self.frag_chunks * 16
+        _launch("frag_layout", lambda: lib().csu_frag_layout_batch(ptr(self.frag_items), self.frag_n, self.frag_chunks,
+                                                                    stream_ptr(self.frag_items.device)), 0, 2 * n)
+
+    def get_frag(self, p):
+        """Fragment-ordered bf16 W of a cached 2-D (N, K) weight (csu_gemm_ws operand), or None."""
+        i = self.index.get(p.data_ptr())
+        if i is None or p.dim() != 2 or self.frag_w[i] is None or self.params[i].shape != p.shape:
+            return None
+        return self.frag_w[i]
+
+    def get_frag_t(self, p):
+        """Fragment-ordered bf16 W^T (K, N) of a cached 2-D (N, K) weight, or None."""
+        i = self.index.get(p.data_ptr())
+        if i is None or p.dim() != 2 or self.frag_t[i] is None or self.params[i].shape != p.shape:
+            return None
+        return self.frag_t[i]
 
     def _cast(self):
         allp = self.params + self.convs

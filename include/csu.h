@@ -313,6 +313,31 @@ typedef struct {
 int csu_gemm_ex(const csu_gemm_desc* d, void* stream);
 
 /* ---------------------------------------------------------------------------------------
+ * Weight-streaming token GEMM (csrc/gemm_ws.hip): out (M, N) = x (M, K) @ W^T (+ bias) (+ resid),
+ * for the CSWinBlock qkv / proj Linears (cswin:337, 366) and their input gradients at C = 128 / 256.
+ * x bf16 with row stride ldx; w_frag = W (N, K) bf16 in FRAGMENT order (csu_frag_layout_batch);
+ * bias fp32 (N) or NULL; resid fp32 (M, N) or NULL (then out_dtype must be CSU_F32); out_dtype
+ * CSU_BF16 or CSU_F32, out (M, N) contiguous.  csu_gemm_ws_supported says whether (M, N, K, resid,
+ * out_dtype) is instantiated (M % 64 == 0; (K, N) in {(128,384), (256,768), (384,128), (768,256),
+ * (128,128), (256,256)}); other shapes return CSU_E_ARG.
+ * ------------------------------------------------------------------------------------- */
+int csu_gemm_ws_supported(long M, int N, int K, int resid, int out_dtype);
+int csu_gemm_ws(long M, int N, int K, const void* x, int ldx, const void* w_frag, const float* bias, const float* resid,
+                int out_dtype, void* out, void* stream);
+/* Fragment-ordered copy of a bf16 (rows x cols) matrix, rows % 32 == 0, cols % 16 == 0: 16-B chunk
+ * q of row n (k = 8q .. 8q+7) goes to chunk ((n / 32) * (cols / 16) + q / 2) * 64 + n % 32 + 32 (q % 2),
+ * i.e. [rows/32][cols/16][64 lanes][8] -- the MFMA 32x32x16 A-operand fragment of lane (n % 32, half).
+ * items: DEVICE array sorted by chunk0 (first 16-B chunk of the item; chunk0[i+1] = chunk0[i] +
+ * rows * cols / 8); total_chunks = the sum. */
+typedef struct {
+    const void* src;
+    void* dst;
+    int32_t rows, cols;
+    int64_t chunk0;
+} csu_frag_item;
+int csu_frag_layout_batch(const csu_frag_item* items, int count, long total_chunks, void* stream);
+
+/* ---------------------------------------------------------------------------------------
  * Batched weight cast: for each item, dst (rows, cols) bf16 = src fp32, and when dst_t is not
  * NULL also dst_t (cols, rows) bf16 = src^T.  items is a DEVICE array sorted by tile0, the first
  * 64x64-tile index of the item (tile0[i+1] = tile0[i] + ceil(rows/64) * ceil(cols/64));

@@ -1278,3 +1278,68 @@ def test_mlp_bwd_deep_ring_vs_fp64(C, M, cfg):
             assert err < 1e-2, (drop, name, err)
             d01 = float((got - other).double().norm() / other.double().norm())
             assert d01 < 1e-2, (drop, name, d01)
+
+
+def _frag_ref(w: torch.Tensor) -> torch.Tensor:
+    """Fragment order of csu_frag_layout_batch (include/csu.h): [rows/32][cols/16][64 lanes][8],
+    lane = row % 32 + 32 * ((k % 16) // 8)."""
+    R, Cc = w.shape
+    t = w.reshape(R // 32, 32, Cc // 16, 2, 8)          # [nt][r][s][half][8]
+    return t.permute(0, 2, 3, 1, 4).reshape(-1)         # [nt][s][half][r][8] = [nt][s][lane][8]
+
+
+@pytest.mark.parametrize("rows,cols", [(32, 16), (768, 256), (128, 384), (256, 768)])
+def test_frag_layout_batch(rows, cols):
+    import ctypes
+    import numpy as np
+    from csu._lib import lib
+    d = dev()
+    g = torch.Generator(device=d).manual_seed(rows + cols)
+    ws = [torch.randn(rows, cols, device=d, generator=g).bfloat16(), torch.randn(64, 128, device=d, generator=g).bfloat16()]
+    outs = [torch.empty_like(w).view(-1) for w in ws]
+    rec = np.zeros(len(ws), dtype=[("src", "<u8"), ("dst", "<u8"), ("rows", "<i4"), ("cols", "<i4"), ("chunk0", "<i8")])
+    c0 = 0
+    for k, (w, o) in enumerate(zip(ws, outs)):
+        rec[k] = (w.data_ptr(), o.data_ptr(), w.shape[0], w.shape[1], c0)
+        c0 += w.numel() // 8
+    items = torch.frombuffer(bytearray(rec.tobytes()), dtype=torch.uint8).to(d)
+    assert lib().csu_frag_layout_batch(ctypes.c_void_p(items.data_ptr()), len(ws), c0, None) == 0
+    torch.cuda.synchronize()
+    for w, o in zip(ws, outs):
+        assert torch.equal(o, _frag_ref(w))
+
+
+GEMM_WS_SHAPES = [(16384, 768, 256), (16384, 256, 768), (16384, 256, 256), (1024, 384, 128), (65536, 128, 384),
+                  (192, 128, 128)]
+
+
+@pytest.mark.parametrize("M,N,K", GEMM_WS_SHAPES)
+@pytest.mark.parametrize("mode", ["bf16_bias", "f32", "resid"])
+def test_gemm_ws_vs_fp64(M, N, K, mode):
+    """csu_gemm_ws (weight-streaming token GEMM) against an fp64 GEMM of the same bf16 operands:
+    fp32 out within 1e-5 of max |ref| (fp32 accumulation), bf16 out within bf16 rounding."""
+    from csu import ops
+    d = dev()
+    g = torch.Generator(device=d).manual_seed(M + N + K)
+    ldx = K + 64 if M <= 1024 else K          # a strided token operand on the small shapes
+    xfull = torch.randn(M, ldx, device=d, generator=g).bfloat16()
+    x = xfull[:, :K]
+    w = (torch.randn(N, K, device=d, generator=g) / K ** 0.5).bfloat16()
+    bias = torch.randn(N, device=d, generator=g) if mode != "f32" else None
+    resid = torch.randn(M, N, device=d, generator=g) if mode == "resid" else None
+    odt = torch.bfloat16 if mode == "bf16_bias" else torch.float32
+    out = ops.gemm_ws(x, _frag_ref(w).contiguous(), N, odt, bias=bias, resid=resid)
+    torch.cuda.synchronize()
+    ref = x.double() @ w.double().t()
+    if bias is not None:
+        ref = ref + bias.double()
+    if resid is not None:
+        ref = ref + resid.double()
+    err = float((out.double() - ref).abs().max())
+    scale = float(ref.abs().max())
+    if odt == torch.float32:
+        assert err <= 1e-5 * scale, (err, scale)
+    else:
+        assert err <= 2 ** -8 * scale + 1e-6, (err, scale)
+    with pytest.raises(Exception):
+        ops.gemm_ws(x[:M - 8], _frag_ref(w).contiguous(), N, odt)   # M % 64 != 0: refused
