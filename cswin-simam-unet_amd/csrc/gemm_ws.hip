@@ -29,14 +29,21 @@ enum { WS_PLAIN = 0, WS_RESID = 1 };
 
 constexpr int WS_BM = 64;   // tokens per workgroup
 
+constexpr int ws_unit(int ks) {
+    for (int u = 16; u > 1; --u)
+        if (ks % u == 0) return u;
+    return 1;
+}
+
 template <int K, int NT, int EPI, typename TOUT>
 __global__ __launch_bounds__(256) void gemm_ws_kernel(long M, const bf16* __restrict__ X, int ldx,
                                                       const bf16* __restrict__ Wf, const float* __restrict__ bias,
                                                       const float* __restrict__ resid, TOUT* __restrict__ out) {
     constexpr int N = 128 * NT;
     constexpr int KS = K / 16;                     // k-steps
-    constexpr int UK = KS < 16 ? KS : 16;          // k-steps per unit
+    constexpr int UK = ws_unit(KS);                // k-steps per unit (a divisor of KS, <= 16)
     constexpr int CH = KS / UK;                    // units per tile
+    static_assert(CH * UK == KS, "unit size");
     constexpr int U = NT * CH;                     // units per wave
     constexpr bool XREG = K <= 256;                // B fragments held in registers
     constexpr int XS = K + 8;                      // LDS row stride of the token panel (bf16)
