@@ -548,7 +548,15 @@ __global__ __launch_bounds__(256) void ws_gemm8(int M, int, const bf16* __restri
     }
 }
 
-int main() {
+__global__ void fill_rand(bf16* p, long n, unsigned seed) {
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    unsigned x = (unsigned)i * 2654435761u ^ seed;
+    x ^= x >> 13; x *= 0x5bd1e995u; x ^= x >> 15;
+    p[i] = (bf16)(((float)(x & 0xffff) / 65536.f - 0.5f) * 0.1f);
+}
+
+int main(int argc, char** argv) {
     const int M = 16384;
     int Ns[] = {256, 768, 1024};
     bf16 *X, *W, *O;
@@ -557,6 +565,12 @@ int main() {
     hipMalloc(&O, (size_t)M * 2048 * 2);
     hipMemset(X, 0, (size_t)M * K * 2);
     hipMemset(W, 0, (size_t)2048 * K * 2);
+    if (argc > 1) {   // random operands instead of zeros
+        fill_rand<<<(M * K + 255) / 256, 256>>>(X, (long)M * K, 1u);
+        fill_rand<<<(2048 * K + 255) / 256, 256>>>(W, 2048L * K, 2u);
+        hipDeviceSynchronize();
+        printf("random operands\n");
+    }
     hipEvent_t e0, e1;
     hipEventCreate(&e0);
     hipEventCreate(&e1);
