@@ -107,8 +107,9 @@ __device__ __forceinline__ void exchange_half(f32x16* acc, float* xch, int wave,
 
 // A0: index of the first of the HT accumulator tiles holding features [U C/2, (U+1) C/2)
 template <int C, int U, bool DROP, int A0 = U * (C / 64)>
-__device__ __forceinline__ void fwd_epilogue(const f32x16* acc, __amdgpu_buffer_rsrc_t rs_res, __amdgpu_buffer_rsrc_t rs_out,
-                                             const float* b2, int tok, bool ok, int h, long mg, const MlpDrop& dd) {
+__device__ __forceinline__ void fwd_epilogue(f32x16* acc, __amdgpu_buffer_rsrc_t rs_res, __amdgpu_buffer_rsrc_t rs_out,
+                                             const float* b2, int tok, bool ok, int h, long mg, const MlpDrop& dd,
+                                             bool keep = false) {
     constexpr int HT = C / 64;
     float sdp = 1.f;
     DropoutRng R;
@@ -132,11 +133,73 @@ __device__ __forceinline__ void fwd_epilogue(const f32x16* acc, __amdgpu_buffer_
                 float z = acc[A0 + q][4 * g + e] + bv[e];
                 if constexpr (DROP) z *= ((km >> (4 * g + e)) & 1u) ? sdp * R.scale : 0.f;
                 v[e] = z + rv[e];
+                if (keep) acc[A0 + q][4 * g + e] = v[e];   // the block output, for ln_epilogue
             }
             buf_st4(rs_out, off, v);
         }
     }
 }
+
+// LayerNorm of the Mlp block's output (the NEXT CSWinBlock's norm1, cswin:357 -- the residual stream
+// y = res + Mlp(x) is fully formed here): per token mean and rstd over its C values, two passes as
+// ln_fwd (mean, then the centred sum of squares).  Lane (r, h) of wave (t, U) holds token 32 t + r,
+// features (U HT + q) 32 + 8 g + 4 h + e in yv[q][4 g + e]; the two feature halves of a token meet by
+// a shuffle (h) and the LDS exchange lnx with the partner wave (U ^ 1); both waves take part in the
+// two barriers.  Writes the bf16 LN output and (wave U = 0) mean / rstd.
+template <int C, int U, int A0 = U * (C / 64)>
+__device__ __forceinline__ void ln_epilogue(const f32x16* yv, float* lnx, int wave, int r, int h, int tok, bool ok,
+                                            const float* __restrict__ gam, const float* __restrict__ bet, float eps,
+                                            __amdgpu_buffer_rsrc_t rs_ln, __amdgpu_buffer_rsrc_t rs_mean,
+                                            __amdgpu_buffer_rsrc_t rs_rstd) {
+    constexpr int HT = C / 64;
+    float s = 0.f;
+#pragma unroll
+    for (int q = 0; q < HT; ++q)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) s += yv[A0 + q][i];
+    s += __shfl_xor(s, 32, 64);
+    if (h == 0) lnx[wave * 32 + r] = s;
+    lds_sync();
+    const float mu = (s + lnx[(wave ^ 1) * 32 + r]) / C;
+    float q2 = 0.f;
+#pragma unroll
+    for (int q = 0; q < HT; ++q)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const float d = yv[A0 + q][i] - mu;
+            q2 += d * d;
+        }
+    q2 += __shfl_xor(q2, 32, 64);
+    if (h == 0) lnx[128 + wave * 32 + r] = q2;
+    lds_sync();
+    const float rs = rsqrtf((q2 + lnx[128 + (wave ^ 1) * 32 + r]) / C + eps);
+#pragma unroll
+    for (int q = 0; q < HT; ++q)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int f = (U * HT + q) * 32 + 8 * g + 4 * h;
+            float gw[4], bw[4], o[4];
+            load4(gam + f, gw);
+            load4(bet + f, bw);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) o[e] = (yv[A0 + q][4 * g + e] - mu) * rs * gw[e] + bw[e];
+            buf_st4bf(rs_ln, ok ? (unsigned)(tok * C + f) * 2 : kOOB, o);
+        }
+    if (U == 0 && h == 0) {
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(mu), rs_mean, ok ? (unsigned)tok * 4 : kOOB, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(rs), rs_rstd, ok ? (unsigned)tok * 4 : kOOB, 0, 0);
+    }
+}
+
+// the next block's norm1 (ln_epilogue) for the fused forward, or all-null
+struct MlpLn {
+    const float* gamma;
+    const float* beta;
+    float eps;
+    bf16* out;
+    float* mean;
+    float* rstd;
+};
 
 template <int C, int U>
 __device__ __forceinline__ void bwd_epilogue(const f32x16* acc, __amdgpu_buffer_rsrc_t rs_dx, int tok, bool ok, int h) {
@@ -169,11 +232,11 @@ template <int V> using iconst = std::integral_constant<int, V>;
 // Forward.  Rings: W1 chunks in 2 stages, W2 chunks in 2 stages.  Step j (after one barrier):
 // DMA W1(j+2), W2(j+1); GEMM1(j+1) on the MFMA pipe while GELU(j) runs on the VALU; GEMM2(j).
 // DROP: hidden / output dropout and DropPath (MlpDrop)
-template <int C, bool DROP>
+template <int C, bool DROP, bool LN = false>
 __global__ __launch_bounds__(MT) void mlp_fwd_kernel(long M, const bf16* __restrict__ X, const bf16* __restrict__ W1,
                                                      const float* __restrict__ b1, const bf16* __restrict__ W2,
                                                      const float* __restrict__ b2, const float* __restrict__ res,
-                                                     float* __restrict__ out, MlpDrop dd, long rpi) {
+                                                     float* __restrict__ out, MlpDrop dd, long rpi, MlpLn ln = MlpLn{}) {
     constexpr int NCH = 4 * C / HC;     // hidden chunks
     constexpr int KS = C / 16;          // k-steps of GEMM1
     constexpr int TF = C / 32;          // 32-feature output tiles (all C, partial over the hidden half)
@@ -279,6 +342,21 @@ __global__ __launch_bounds__(MT) void mlp_fwd_kernel(long M, const bf16* __restr
     float* xch = reinterpret_cast<float*>(ring);
     const auto rs_res = buf_rsrc(res + m0 * C, rows * C * 4);
     const auto rs_out = buf_rsrc(out + m0 * C, rows * C * 4);
+    if constexpr (LN) {
+        __shared__ float lnx[256];
+        const auto rs_ln = buf_rsrc(ln.out + m0 * C, rows * C * 2);
+        const auto rs_mean = buf_rsrc(ln.mean + m0, rows * 4), rs_rstd = buf_rsrc(ln.rstd + m0, rows * 4);
+        if (u == 0) {
+            exchange_half<C, 0>(acc, xch, wave, lane);
+            fwd_epilogue<C, 0, DROP>(acc, rs_res, rs_out, b2, tok, ok, h, mg, dd, true);
+            ln_epilogue<C, 0>(acc, lnx, wave, r, h, tok, ok, ln.gamma, ln.beta, ln.eps, rs_ln, rs_mean, rs_rstd);
+        } else {
+            exchange_half<C, 1>(acc, xch, wave, lane);
+            fwd_epilogue<C, 1, DROP>(acc, rs_res, rs_out, b2, tok, ok, h, mg, dd, true);
+            ln_epilogue<C, 1>(acc, lnx, wave, r, h, tok, ok, ln.gamma, ln.beta, ln.eps, rs_ln, rs_mean, rs_rstd);
+        }
+        return;
+    }
     if (u == 0) {
         exchange_half<C, 0>(acc, xch, wave, lane);
         fwd_epilogue<C, 0, DROP>(acc, rs_res, rs_out, b2, tok, ok, h, mg, dd);
@@ -588,8 +666,17 @@ int persist_grid(long M) {   // one workgroup (two panel streams) per CU, fewer 
 
 template <int C>
 int fwd_launch(long M, const void* x, const void* w1, const float* b1, const void* w2, const float* b2, const float* res,
-               float* out, const MlpDrop* d, long rpi, hipStream_t st) {
+               float* out, const MlpDrop* d, long rpi, hipStream_t st, const MlpLn* ln = nullptr) {
     const dim3 grid((unsigned)((M + BM - 1) / BM));
+    if (ln) {
+        if (d)
+            mlp_fwd_kernel<C, true, true><<<grid, MT, 0, st>>>(M, (const bf16*)x, (const bf16*)w1, b1, (const bf16*)w2, b2, res,
+                                                                out, *d, rpi, *ln);
+        else
+            mlp_fwd_kernel<C, false, true><<<grid, MT, 0, st>>>(M, (const bf16*)x, (const bf16*)w1, b1, (const bf16*)w2, b2,
+                                                                 res, out, MlpDrop{}, rpi, *ln);
+        return check_launch("mlp_fwd_ln");
+    }
     if (d)
         mlp_fwd_kernel<C, true><<<grid, MT, 0, st>>>(M, (const bf16*)x, (const bf16*)w1, b1, (const bf16*)w2, b2, res, out, *d, rpi);
     else
@@ -1484,6 +1571,29 @@ extern "C" int csu_mlp_fwd_dp(long M, int C, const void* x, const void* w1, cons
         case 128: return fwd_launch<128>(M, x, w1, b1, w2, b2, res, out, dp, rpi, st);
         case 256: return fwd_launch<256>(M, x, w1, b1, w2, b2, res, out, dp, rpi, st);
         default: return fail(CSU_E_ARG, "mlp_fwd: C must be 64, 128 or 256");
+    }
+}
+
+extern "C" int csu_mlp_fwd_ln(long M, int C, const void* x, const void* w1, const float* b1, const void* w2, const float* b2,
+                              const float* res, float* out, const csu_mlp_dropout* d, const float* ln_gamma,
+                              const float* ln_beta, float ln_eps, void* ln_out, float* ln_mean, float* ln_rstd,
+                              void* stream) {
+    if (M < 1 || !x || !w1 || !b1 || !w2 || !b2 || !res || !out || !ln_gamma || !ln_beta || !ln_out || !ln_mean || !ln_rstd)
+        return fail(CSU_E_ARG, "mlp_fwd_ln: bad arguments");
+    if (M * 4L * C * 2 > 0x7fffffffL) return fail(CSU_E_ARG, "mlp_fwd_ln: tensor exceeds 2 GB buffer range");
+    if (res == out) return fail(CSU_E_ARG, "mlp_fwd_ln: out must not alias res");
+    MlpDrop md{};
+    const int e = mlp_drop_of(d, md);
+    if (e < 0) return e;
+    const MlpDrop* dp = d && e == 0 ? &md : nullptr;
+    const long rpi = d ? (long)d->rows_per_sample : 0;
+    const MlpLn ln{ln_gamma, ln_beta, ln_eps, (bf16*)ln_out, ln_mean, ln_rstd};
+    const hipStream_t st = as_stream(stream);
+    switch (C) {
+        case 64: return fwd_launch<64>(M, x, w1, b1, w2, b2, res, out, dp, rpi, st, &ln);
+        case 128: return fwd_launch<128>(M, x, w1, b1, w2, b2, res, out, dp, rpi, st, &ln);
+        case 256: return fwd_launch<256>(M, x, w1, b1, w2, b2, res, out, dp, rpi, st, &ln);
+        default: return fail(CSU_E_ARG, "mlp_fwd_ln: C must be 64, 128 or 256");
     }
 }
 

@@ -135,6 +135,8 @@ _SIGS = {
     "csu_adam_l2_step": (ctypes.c_int, [c_void_p, ctypes.c_int, ctypes.c_long, c_void_p, c_float, c_float, c_float, c_float,
                                       c_float, c_void_p, c_float, c_void_p]),
     "csu_gemm_ex": (ctypes.c_int, [ctypes.POINTER(GemmDesc), c_void_p]),
+    "csu_mlp_fwd_ln": (ctypes.c_int, [ctypes.c_long, ctypes.c_int] + [c_void_p] * 8 + [c_void_p, c_void_p, c_float, c_void_p,
+                                                                               c_void_p, c_void_p, c_void_p]),
     "csu_gemm_ws_supported": (ctypes.c_int, [ctypes.c_long, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     "csu_gemm_ws": (ctypes.c_int, [ctypes.c_long, ctypes.c_int, ctypes.c_int, c_void_p, ctypes.c_int, c_void_p, c_void_p,
                                    c_void_p, ctypes.c_int, c_void_p, c_void_p]),

@@ -257,7 +257,9 @@ class CSWinBlock(nn.Module):
             md = None
             if on and (p_mlp > 0 or rs2 is not None):
                 md = ops.MlpDrop(snap, self.mlp._site_h, self.mlp._site_o, p_mlp, rs2, L)
-            return ops.mlp_residual(xb, h2, self.mlp.fc1, self.mlp.fc2, md)
+            nn1 = getattr(self, "_next_norm", None)   # the next block's norm1: computed in the Mlp's epilogue
+            ln_next = (nn1.weight, nn1.bias, nn1.eps) if nn1 is not None and cd == torch.bfloat16 else None
+            return ops.mlp_residual(xb, h2, self.mlp.fc1, self.mlp.fc2, md, ln_next=ln_next)
         return self.mlp.forward_residual(h2, xb, rs2, L, snap)
 
 
@@ -407,6 +409,14 @@ class CSWinTransformer(nn.Module):
         self.simam = SimAM() if simam else None
         self.apply(self._init_weights)
         rng.assign_sites(self)
+        # the LayerNorm that consumes each block's output, when it is the next block's norm1 (or norm_up
+        # after the last decoder block): the block's fused Mlp computes it in its epilogue
+        # (ops.mlp_residual(ln_next=...)); a plain attribute, not a registered submodule
+        for st in (self.stage1, self.stage2, self.stage3, self.stage4, self.stage_up4, self.stage_up3, self.stage_up2,
+                   self.stage_up1):
+            for a, b in zip(list(st)[:-1], list(st)[1:]):
+                object.__setattr__(a, "_next_norm", b.norm1)
+        object.__setattr__(self.stage_up1[-1], "_next_norm", self.norm_up)
 
     def _init_weights(self, m):
         if isinstance(m, nn.Linear):

@@ -470,20 +470,23 @@ def _wgrad_deferrable(dy2, wdt, bdt, params) -> bool:
 
 class _LayerNormFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, eps: float, out_dtype):
+    def forward(ctx, x, weight, bias, eps: float, out_dtype, pre=None):
         require_device(x, weight, bias)
         x = x.contiguous()
         C = x.shape[-1]
         rows = x.numel() // C
         w = weight.detach().float().contiguous()
-        b = bias.detach().float().contiguous()
-        y = torch.empty(x.shape, dtype=out_dtype, device=x.device)
-        mean = torch.empty(rows, dtype=torch.float32, device=x.device)
-        rstd = torch.empty(rows, dtype=torch.float32, device=x.device)
-        _launch("layernorm_fwd", lambda: lib().csu_layernorm_fwd(rows, C, float(eps), dtype_code(x), ptr(x), ptr(w), ptr(b),
-                                                                 dtype_code(y), ptr(y), ptr(mean), ptr(rstd),
-                                                                 stream_ptr(x.device)),
-                8 * rows * C, rows * C * (esize(x) + esize(y)) + rows * 8, prec=prec_of(x))
+        if pre is not None:   # computed by the producing fused Mlp (csu_mlp_fwd_ln)
+            y, mean, rstd = pre[3].view(x.shape), pre[4], pre[5]
+        else:
+            b = bias.detach().float().contiguous()
+            y = torch.empty(x.shape, dtype=out_dtype, device=x.device)
+            mean = torch.empty(rows, dtype=torch.float32, device=x.device)
+            rstd = torch.empty(rows, dtype=torch.float32, device=x.device)
+            _launch("layernorm_fwd", lambda: lib().csu_layernorm_fwd(rows, C, float(eps), dtype_code(x), ptr(x), ptr(w),
+                                                                     ptr(b), dtype_code(y), ptr(y), ptr(mean), ptr(rstd),
+                                                                     stream_ptr(x.device)),
+                    8 * rows * C, rows * C * (esize(x) + esize(y)) + rows * 8, prec=prec_of(x))
         ctx.save_for_backward(x, w, mean, rstd)
         ctx.pdtypes = (weight.dtype, bias.dtype)
         ctx.params = (weight, bias)
@@ -517,12 +520,25 @@ class _LayerNormFn(torch.autograd.Function):
                 12 * rows * C, rows * C * (2 * esize(x) + esize(dy) + esize(dxb)) + rows * 8, prec=prec_of(x))
         if dxb is not None:
             dx._csu_bf16 = dxb
-        return dx, dg.to(ctx.pdtypes[0]), db.to(ctx.pdtypes[1]), None, None
+        return dx, dg.to(ctx.pdtypes[0]), db.to(ctx.pdtypes[1]), None, None, None
+
+
+def _ln_pre(x, weight, bias, eps, od):
+    """The LayerNorm of x already computed by the fused Mlp that produced it (``_csu_ln``), or None."""
+    pre = getattr(x, "_csu_ln", None)
+    if (pre is not None and pre[0] is weight and pre[1] is bias and pre[2] == float(eps) and pre[3].dtype == od
+            and pre[3].numel() == x.numel() and x.is_contiguous()):
+        return pre
+    return None
 
 
 def layer_norm(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, eps: float = 1e-5,
                out_dtype: Optional[torch.dtype] = None) -> torch.Tensor:
-    return _LayerNormFn.apply(x, weight, bias, eps, out_dtype or x.dtype)
+    od = out_dtype or x.dtype
+    pre = _ln_pre(x, weight, bias, eps, od)
+    if pre is not None:
+        return _LayerNormFn.apply(x, weight, bias, eps, od, pre)
+    return _LayerNormFn.apply(x, weight, bias, eps, od)
 
 
 def _bf16_of(g: torch.Tensor) -> torch.Tensor:
@@ -541,20 +557,24 @@ class _LayerNormForkFn(torch.autograd.Function):
     GEMM backward consumes (attached to dx as ``_csu_bf16``)."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, eps: float, out_dtype):
+    def forward(ctx, x, weight, bias, eps: float, out_dtype, pre=None):
         require_device(x, weight, bias)
         x = x.contiguous()
         C = x.shape[-1]
         rows = x.numel() // C
         w = weight.detach().float().contiguous()
-        b = bias.detach().float().contiguous()
-        y = torch.empty(x.shape, dtype=out_dtype, device=x.device)
-        mean = torch.empty(rows, dtype=torch.float32, device=x.device)
-        rstd = torch.empty(rows, dtype=torch.float32, device=x.device)
-        _launch("layernorm_fwd", lambda: lib().csu_layernorm_fwd(rows, C, float(eps), dtype_code(x), ptr(x), ptr(w), ptr(b),
-                                                                 dtype_code(y), ptr(y), ptr(mean), ptr(rstd),
-                                                                 stream_ptr(x.device)),
-                8 * rows * C, rows * C * (esize(x) + esize(y)) + rows * 8, prec=prec_of(x))
+        if pre is not None:
+            # computed by the producing fused Mlp's epilogue (csu_mlp_fwd_ln): no launch here
+            y, mean, rstd = pre[3].view(x.shape), pre[4], pre[5]
+        else:
+            b = bias.detach().float().contiguous()
+            y = torch.empty(x.shape, dtype=out_dtype, device=x.device)
+            mean = torch.empty(rows, dtype=torch.float32, device=x.device)
+            rstd = torch.empty(rows, dtype=torch.float32, device=x.device)
+            _launch("layernorm_fwd", lambda: lib().csu_layernorm_fwd(rows, C, float(eps), dtype_code(x), ptr(x), ptr(w),
+                                                                     ptr(b), dtype_code(y), ptr(y), ptr(mean), ptr(rstd),
+                                                                     stream_ptr(x.device)),
+                    8 * rows * C, rows * C * (esize(x) + esize(y)) + rows * 8, prec=prec_of(x))
         ctx.save_for_backward(x, w, mean, rstd)
         ctx.pdtypes = (weight.dtype, bias.dtype)
         ctx.params = (weight, bias)
@@ -565,7 +585,7 @@ class _LayerNormForkFn(torch.autograd.Function):
     def backward(ctx, dres, dy):
         x, w, mean, rstd = ctx.saved_tensors
         dx, dg, db = _ln_fork_backward(ctx, x, w, mean, rstd, dres, dy)
-        return dx, dg, db, None, None
+        return dx, dg, db, None, None, None
 
 
 def _ln_fork_backward(ctx, x, w, mean, rstd, dres, dy):
@@ -606,8 +626,14 @@ def _ln_fork_backward(ctx, x, w, mean, rstd, dres, dy):
 
 def layer_norm_fork(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, eps: float = 1e-5,
                     out_dtype: Optional[torch.dtype] = None):
-    """(x, LN(x)) for a residual junction; use the first output as the residual input."""
-    return _LayerNormForkFn.apply(x, weight, bias, eps, out_dtype or x.dtype)
+    """(x, LN(x)) for a residual junction; use the first output as the residual input.  When x is a
+    fused Mlp output that already carries this LayerNorm (mlp_residual(ln_next=...)), its values are
+    used instead of a LayerNorm launch."""
+    od = out_dtype or x.dtype
+    pre = _ln_pre(x, weight, bias, eps, od)
+    if pre is not None:
+        return _LayerNormForkFn.apply(x, weight, bias, eps, od, pre)
+    return _LayerNormForkFn.apply(x, weight, bias, eps, od)
 
 
 # ---------------------------------------------------------------------------------------------
@@ -1543,7 +1569,7 @@ class _MlpFusedFn(torch.autograd.Function):
     csu_mlp_bwd_dp), the output mask applied to dy by one dropout pass first."""
 
     @staticmethod
-    def forward(ctx, res, x, w1, b1, w2, b2, w1c, w2c, drop):
+    def forward(ctx, res, x, w1, b1, w2, b2, w1c, w2c, drop, ln=None):
         C = x.shape[-1]
         res2 = res.float().contiguous().view(-1, C)
         x2 = x.reshape(-1, C).contiguous()
@@ -1553,9 +1579,22 @@ class _MlpFusedFn(torch.autograd.Function):
         b2f = b2.detach().float().contiguous()
         rpi = x.shape[1] if x.dim() == 3 else M   # rows per image: the kernel's hidden-chunk rotation
         dd = ctypes.byref(_mlp_desc(drop, rpi))
-        _launch("mlp_fwd", lambda: lib().csu_mlp_fwd_dp(M, C, ptr(x2), ptr(w1c), ptr(b1f), ptr(w2c), ptr(b2f), ptr(res2),
-                                                        ptr(y), dd, stream_ptr(x2.device)),
-                16 * M * C * C, M * C * (2 + 4 + 4) + 16 * C * C)
+        if ln is not None:
+            # + the next block's norm1 on the output (csu_mlp_fwd_ln); handed to its layer_norm_fork
+            gam, bet, eps = ln
+            gf, bf_ = gam.detach().float().contiguous(), bet.detach().float().contiguous()
+            h1 = torch.empty(M, C, dtype=torch.bfloat16, device=x2.device)
+            mean = torch.empty(M, dtype=torch.float32, device=x2.device)
+            rstd = torch.empty(M, dtype=torch.float32, device=x2.device)
+            _launch("mlp_fwd", lambda: lib().csu_mlp_fwd_ln(M, C, ptr(x2), ptr(w1c), ptr(b1f), ptr(w2c), ptr(b2f), ptr(res2),
+                                                            ptr(y), dd, ptr(gf), ptr(bf_), float(eps), ptr(h1), ptr(mean),
+                                                            ptr(rstd), stream_ptr(x2.device)),
+                    16 * M * C * C + 8 * M * C, M * C * (2 + 4 + 4 + 2) + 16 * C * C + 8 * M)
+            _LN_STASH[0] = (gam, bet, float(eps), h1, mean, rstd)
+        else:
+            _launch("mlp_fwd", lambda: lib().csu_mlp_fwd_dp(M, C, ptr(x2), ptr(w1c), ptr(b1f), ptr(w2c), ptr(b2f), ptr(res2),
+                                                            ptr(y), dd, stream_ptr(x2.device)),
+                    16 * M * C * C, M * C * (2 + 4 + 4) + 16 * C * C)
         ctx.drop = drop
         ctx.rpi = rpi
         ctx.save_for_backward(x2, w1c, b1f, w2c)
@@ -1583,7 +1622,12 @@ class _MlpFusedFn(torch.autograd.Function):
                 24 * M * C * C, M * C * (2 + 2 + 2) + M * 4 * C * (2 + 2) + 16 * C * C)
         dw2, db2 = wgrad_maybe_side(dyb, g, w2dt, b2dt, params=ctx.params[2:])
         dw1, db1 = wgrad_maybe_side(dh, x2, w1dt, b1dt, params=ctx.params[:2])
-        return dy.to(rdt), dx.view(xshape), dw1.to(w1dt), db1.to(b1dt), dw2.to(w2dt), db2.to(b2dt), None, None, None
+        return dy.to(rdt), dx.view(xshape), dw1.to(w1dt), db1.to(b1dt), dw2.to(w2dt), db2.to(b2dt), None, None, None, None
+
+
+# the fused Mlp's LayerNorm of its output for the next block (csu_mlp_fwd_ln): (gamma, beta, eps, ln_out,
+# mean, rstd), set by _MlpFusedFn.forward and attached to its output by mlp_residual as ``_csu_ln``
+_LN_STASH: list = [None]
 
 
 # widths whose fp8 Mlp backward runs the fp8 kernel; the others run the bf16 fused backward on the
@@ -1680,17 +1724,30 @@ def mlp_fp8(res, x, fc1: torch.nn.Linear, fc2: torch.nn.Linear, drop: Optional[M
 FUSED_MLP = True
 
 
-def mlp_residual(res, x, fc1: torch.nn.Linear, fc2: torch.nn.Linear, drop: Optional[MlpDrop] = None):
+# the fused Mlp forward also computes the next CSWinBlock's norm1 (csu_mlp_fwd_ln), which that block's
+# layer_norm_fork then uses instead of its own LayerNorm launch
+FUSE_NEXT_LN = True
+
+
+def mlp_residual(res, x, fc1: torch.nn.Linear, fc2: torch.nn.Linear, drop: Optional[MlpDrop] = None, ln_next=None):
     """res + DropPath(Dropout(fc2(Dropout(gelu(fc1(x)))))) on the bf16 path (``drop`` None: eval /
-    no dropout)."""
+    no dropout).  ``ln_next`` (the next block's norm1 as (weight, bias, eps)): its LayerNorm of the
+    output is computed in the same launch and attached to the output for layer_norm_fork."""
     C = x.shape[-1]
     y = mlp_fp8(res, x, fc1, fc2, drop)
     if y is not None:
         return y
     if FUSED_MLP and fc1.out_features == 4 * C and lib().csu_mlp_supported(C):
+        ln = ln_next if (FUSE_NEXT_LN and ln_next is not None and ln_next[0].dtype == torch.float32
+                         and ln_next[0].numel() == C) else None
+        _LN_STASH[0] = None
         with torch.autocast("cuda", enabled=False):
-            return _MlpFusedFn.apply(res, x, fc1.weight, fc1.bias, fc2.weight, fc2.bias, _weight_bf16(fc1.weight),
-                                     _weight_bf16(fc2.weight), drop)
+            out = _MlpFusedFn.apply(res, x, fc1.weight, fc1.bias, fc2.weight, fc2.bias, _weight_bf16(fc1.weight),
+                                    _weight_bf16(fc2.weight), drop, ln)
+        if ln is not None and _LN_STASH[0] is not None:
+            out._csu_ln = _LN_STASH[0]
+            _LN_STASH[0] = None
+        return out
     with torch.autocast("cuda", enabled=False):
         return _MlpResidualFn.apply(res, x, fc1.weight, fc1.bias, fc2.weight, fc2.bias, _weight_bf16(fc1.weight),
                                     _weight_bf16(fc2.weight), drop)

@@ -527,6 +527,12 @@ int csu_mlp_fwd_dp(long M, int C, const void* x, const void* w1, const float* b1
                    const float* res, float* out, const csu_mlp_dropout* d, void* stream);
 int csu_mlp_bwd_dp(long M, int C, const void* x, const void* dy, const void* w1, const float* b1, const void* w2,
                    void* dh, void* g, void* dx, const csu_mlp_dropout* d, void* stream);
+/* csu_mlp_fwd_dp that also applies the NEXT CSWinBlock's norm1 LayerNorm (cswin:357) to its output
+ * out (M, C) fp32 in the same launch: ln_out (M, C) bf16 = LN(out) * ln_gamma + ln_beta (eps
+ * ln_eps), ln_mean / ln_rstd (M) fp32 as csu_layernorm_fwd writes them.  out must not alias res. */
+int csu_mlp_fwd_ln(long M, int C, const void* x, const void* w1, const float* b1, const void* w2, const float* b2,
+                   const float* res, float* out, const csu_mlp_dropout* d, const float* ln_gamma, const float* ln_beta,
+                   float ln_eps, void* ln_out, float* ln_mean, float* ln_rstd, void* stream);
 /* the forward with an explicit kernel: cfg 0 = the per-panel kernel (csu_mlp_fwd_dp), 1 / 2 = the deep
  * weight ring (32-hidden chunks, several in flight, waves split by tokens; 2: another ring depth) */
 int csu_mlp_fwd_ex(long M, int C, const void* x, const void* w1, const float* b1, const void* w2, const float* b2,

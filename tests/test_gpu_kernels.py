@@ -1343,3 +1343,47 @@ def test_gemm_ws_vs_fp64(M, N, K, mode):
         assert err <= 2 ** -8 * scale + 1e-6, (err, scale)
     with pytest.raises(Exception):
         ops.gemm_ws(x[:M - 8], _frag_ref(w).contiguous(), N, odt)   # M % 64 != 0: refused
+
+
+@pytest.mark.parametrize("C", [64, 128, 256])
+@pytest.mark.parametrize("drop", [False, True])
+def test_mlp_fwd_ln_next(C, drop):
+    """csu_mlp_fwd_ln: the fused Mlp forward that also applies the next block's norm1 to its output
+    (cswin:357): the output equals csu_mlp_fwd_dp's bit for bit, the LayerNorm output / mean / rstd
+    equal an fp64 LayerNorm of that output to bf16 / fp32 rounding; layer_norm_fork then uses them
+    without a LayerNorm launch."""
+    from csu import ops, rng
+    d = dev()
+    g = torch.Generator(device=d).manual_seed(C + int(drop))
+    B, L = 2, 1024
+    x = torch.randn(B, L, C, device=d, generator=g).bfloat16()
+    res = torch.randn(B, L, C, device=d, generator=g)
+    fc1, fc2 = torch.nn.Linear(C, 4 * C).to(d), torch.nn.Linear(4 * C, C).to(d)
+    ln = torch.nn.LayerNorm(C).to(d)
+    with torch.no_grad():
+        ln.weight.uniform_(0.5, 1.5)
+        ln.bias.uniform_(-0.2, 0.2)
+    md = None
+    if drop:
+        snap = rng.snapshot(d)
+        md = ops.MlpDrop(snap, 7, 8, 0.2, torch.tensor([1.25, 0.0], device=d), L)
+    y0 = ops.mlp_residual(res, x, fc1, fc2, md)
+    y1 = ops.mlp_residual(res, x, fc1, fc2, md, ln_next=(ln.weight, ln.bias, ln.eps))
+    torch.cuda.synchronize()
+    assert torch.equal(y0, y1)
+    pre = y1._csu_ln
+    yd = y1.double().view(-1, C)
+    mu = yd.mean(-1)
+    var = ((yd - mu[:, None]) ** 2).mean(-1)
+    ref = (yd - mu[:, None]) / torch.sqrt(var[:, None] + ln.eps) * ln.weight.double() + ln.bias.double()
+    torch.testing.assert_close(pre[4].double(), mu, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(pre[5].double(), 1 / torch.sqrt(var + ln.eps), rtol=1e-4, atol=0)
+    assert float((pre[3].double().view(-1, C) - ref).abs().max()) <= 2 ** -7 * float(ref.abs().max())
+    calls = []
+    real = ops._launch
+    ops._launch = lambda name, *a, **k: (calls.append(name), real(name, *a, **k))[1]
+    try:
+        xa, h = ops.layer_norm_fork(y1, ln.weight, ln.bias, ln.eps, torch.bfloat16)
+    finally:
+        ops._launch = real
+    assert "layernorm_fwd" not in calls and torch.equal(h.view(-1), pre[3].view(-1))
