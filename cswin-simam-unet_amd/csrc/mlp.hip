@@ -152,27 +152,38 @@ __device__ __forceinline__ void ln_epilogue(const f32x16* yv, float* lnx, int wa
                                             __amdgpu_buffer_rsrc_t rs_ln, __amdgpu_buffer_rsrc_t rs_mean,
                                             __amdgpu_buffer_rsrc_t rs_rstd) {
     constexpr int HT = C / 64;
-    float s = 0.f;
-#pragma unroll
-    for (int q = 0; q < HT; ++q)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) s += yv[A0 + q][i];
-    s += __shfl_xor(s, 32, 64);
-    if (h == 0) lnx[wave * 32 + r] = s;
-    lds_sync();
-    const float mu = (s + lnx[(wave ^ 1) * 32 + r]) / C;
-    float q2 = 0.f;
+    // shifted one-pass moments (shift = the lane's first value, shared with the partner half and wave
+    // through the exchange): one barrier instead of two, no cancellation for a large mean
+    float sh = yv[A0][0];
+    sh = __shfl(sh, r, 64);                         // token r's shift from lane (r, 0) of this wave
+    if (h == 0) lnx[256 + wave * 32 + r] = sh;
+    float s = 0.f, q2 = 0.f;
 #pragma unroll
     for (int q = 0; q < HT; ++q)
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-            const float d = yv[A0 + q][i] - mu;
+            const float d = yv[A0 + q][i] - sh;
+            s += d;
             q2 += d * d;
         }
+    s += __shfl_xor(s, 32, 64);
     q2 += __shfl_xor(q2, 32, 64);
-    if (h == 0) lnx[128 + wave * 32 + r] = q2;
+    if (h == 0) {
+        lnx[wave * 32 + r] = s;
+        lnx[128 + wave * 32 + r] = q2;
+    }
     lds_sync();
-    const float rs = rsqrtf((q2 + lnx[128 + (wave ^ 1) * 32 + r]) / C + eps);
+    const int pw = (wave ^ 1) * 32 + r;
+    const float shp = lnx[256 + pw];                 // the partner wave's shift for this token
+    const float dsh = shp - sh;
+    // partner moments re-centred on this wave's shift: sum(d + dsh), sum((d + dsh)^2)
+    const float sp = lnx[pw], qp = lnx[128 + pw];
+    constexpr float HN = C / 2;
+    const float S = s + sp + HN * dsh;
+    const float Q = q2 + qp + 2.f * dsh * sp + HN * dsh * dsh;
+    const float mu_s = S / C;                        // mean - sh
+    const float mu = sh + mu_s;
+    const float rs = rsqrtf(fmaxf(Q / C - mu_s * mu_s, 0.f) + eps);
 #pragma unroll
     for (int q = 0; q < HT; ++q)
 #pragma unroll
@@ -264,6 +275,11 @@ __global__ __launch_bounds__(MT) void mlp_fwd_kernel(long M, const bf16* __restr
     const int j0 = kRot && rpi > 0 && rpi % BM == 0 ? (int)(((m0 % rpi) / BM) & (NCH - 1)) : 0;
     auto chk = [&](int j) { return (j + j0) & (NCH - 1); };
     for (int i = threadIdx.x; i < 4 * C; i += MT) b1s[i] = b1[i];
+    // LN epilogue: gamma / beta staged in LDS here -- read in the epilogue from LDS, a global load there
+    // would wait (vmcnt, issue order) for the completion of every output store before it
+    __shared__ __attribute__((aligned(16))) float lngb[LN ? 2 * C : 4];
+    if constexpr (LN)
+        for (int i = threadIdx.x; i < 2 * C; i += MT) lngb[i] = i < C ? ln.gamma[i] : ln.beta[i - C];
     bf16x8 xf[KS];
     load_bfrags<C>(buf_rsrc(X + m0 * C, rows * C * 2), tok, ok, h, xf);
 
@@ -343,17 +359,17 @@ __global__ __launch_bounds__(MT) void mlp_fwd_kernel(long M, const bf16* __restr
     const auto rs_res = buf_rsrc(res + m0 * C, rows * C * 4);
     const auto rs_out = buf_rsrc(out + m0 * C, rows * C * 4);
     if constexpr (LN) {
-        __shared__ float lnx[256];
+        __shared__ float lnx[384];
         const auto rs_ln = buf_rsrc(ln.out + m0 * C, rows * C * 2);
         const auto rs_mean = buf_rsrc(ln.mean + m0, rows * 4), rs_rstd = buf_rsrc(ln.rstd + m0, rows * 4);
         if (u == 0) {
             exchange_half<C, 0>(acc, xch, wave, lane);
             fwd_epilogue<C, 0, DROP>(acc, rs_res, rs_out, b2, tok, ok, h, mg, dd, true);
-            ln_epilogue<C, 0>(acc, lnx, wave, r, h, tok, ok, ln.gamma, ln.beta, ln.eps, rs_ln, rs_mean, rs_rstd);
+            ln_epilogue<C, 0>(acc, lnx, wave, r, h, tok, ok, lngb, lngb + C, ln.eps, rs_ln, rs_mean, rs_rstd);
         } else {
             exchange_half<C, 1>(acc, xch, wave, lane);
             fwd_epilogue<C, 1, DROP>(acc, rs_res, rs_out, b2, tok, ok, h, mg, dd, true);
-            ln_epilogue<C, 1>(acc, lnx, wave, r, h, tok, ok, ln.gamma, ln.beta, ln.eps, rs_ln, rs_mean, rs_rstd);
+            ln_epilogue<C, 1>(acc, lnx, wave, r, h, tok, ok, lngb, lngb + C, ln.eps, rs_ln, rs_mean, rs_rstd);
         }
         return;
     }
