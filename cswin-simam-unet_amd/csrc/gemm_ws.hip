@@ -28,6 +28,7 @@ namespace {
 enum { WS_PLAIN = 0, WS_RESID = 1 };
 
 constexpr int WS_BM = 64;   // tokens per workgroup
+constexpr bool WS_ROT = true;
 
 constexpr int ws_unit(int ks) {
     for (int u = 16; u > 1; --u)
@@ -57,9 +58,13 @@ __global__ __launch_bounds__(256) void gemm_ws_kernel(long M, const bf16* __rest
     const long m0 = (long)blockIdx.x * WS_BM;
     float* ep = ep_all + wave * WS_BM * ES;
 
+    // tile order rotated per workgroup (its index within the XCD: ids x, x + 8, ... run on XCD x), so
+    // the CUs of an XCD do not all read the same weight lines at the same moment
+    const int rot = WS_ROT ? (int)((blockIdx.x >> 3) % NT) : 0;
+    auto tile_of = [&](int i) { return i + rot < NT ? i + rot : i + rot - NT; };
     bf16x8 wf[2][UK];
     auto wload1 = [&](int u, int s) {   // k-step s of unit u of this wave into buffer u & 1
-        const int nt = wave + 4 * (u / CH), ks = (u % CH) * UK + s;
+        const int nt = wave + 4 * tile_of(u / CH), ks = (u % CH) * UK + s;
         wf[u & 1][s] = *reinterpret_cast<const bf16x8*>(Wf + ((long)(nt * KS + ks) * 64 + lane) * 8);
     };
 #pragma unroll
@@ -92,7 +97,7 @@ __global__ __launch_bounds__(256) void gemm_ws_kernel(long M, const bf16* __rest
     for (int u = 0; u < U; ++u) {
         const int c = u % CH;
         if (c == CH - 1) {
-            const int n0 = 32 * (wave + 4 * (u / CH));
+            const int n0 = 32 * (wave + 4 * tile_of(u / CH));
             if constexpr (BF) {
                 const int cc = 8 * (lane & 3);
                 buf_ld4(rs_b, (unsigned)(n0 + cc) * 4, bv);
@@ -129,7 +134,7 @@ __global__ __launch_bounds__(256) void gemm_ws_kernel(long M, const bf16* __rest
         __builtin_amdgcn_sched_barrier(0);
         if (c != CH - 1) continue;
         // ---- epilogue of tile nt: acc element (token 32 t + r, feature 32 nt + 8 g + 4 h + e)
-        const int nt = wave + 4 * (u / CH);
+        const int nt = wave + 4 * tile_of(u / CH);
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
             const f32x16& a = t ? a1 : a0;
