@@ -25,7 +25,23 @@
 namespace csu {
 namespace {
 
-enum { WS_PLAIN = 0, WS_RESID = 1 };
+enum { WS_PLAIN = 0, WS_RESID = 1, WS_LNBWD = 2 };
+
+// WS_LNBWD epilogue: the GEMM is the input gradient dh of a LayerNorm's output (the qkv Linear's
+// input, CSWinBlock norm1, cswin:357 / 337): instead of writing dh, the workgroup (64 tokens x all
+// C = N features) runs the LayerNorm backward on it -- dx = dres + rstd (g - mean(g) - xhat
+// mean(g xhat)), g = dh * gamma -- and writes dx (fp32) + its bf16 copy and the block's dgamma / dbeta
+// column partials (row blockIdx.x of part [M / 64][2C], csu_layernorm_param_reduce_batch's layout).
+struct WsLn {
+    const float* x;      // LayerNorm input (M, C) fp32
+    const float* gamma;  // (C)
+    const float* mean;   // (M)
+    const float* rstd;   // (M)
+    const float* dres;   // (M, C) fp32 gradient of the residual branch, or NULL
+    float* dx;           // (M, C)
+    bf16* dxb;           // (M, C) bf16 copy of dx
+    float* part;         // [M / 64][2C]
+};
 
 constexpr int WS_BM = 64;   // tokens per workgroup
 constexpr bool WS_ROT = true;
@@ -39,7 +55,8 @@ constexpr int ws_unit(int ks) {
 template <int K, int NT, int EPI, typename TOUT>
 __global__ __launch_bounds__(256) void gemm_ws_kernel(long M, const bf16* __restrict__ X, int ldx,
                                                       const bf16* __restrict__ Wf, const float* __restrict__ bias,
-                                                      const float* __restrict__ resid, TOUT* __restrict__ out) {
+                                                      const float* __restrict__ resid, TOUT* __restrict__ out,
+                                                      WsLn ln = WsLn{}) {
     constexpr int N = 128 * NT;
     constexpr int KS = K / 16;                     // k-steps
     constexpr int UK = ws_unit(KS);                // k-steps per unit (a divisor of KS, <= 16)
@@ -93,10 +110,11 @@ __global__ __launch_bounds__(256) void gemm_ws_kernel(long M, const bf16* __rest
     // epilogue loads of a tile are issued at the start of its last unit, BEFORE the next unit's
     // weight loads: vmcnt counts in issue order, so waiting for them then does not wait for the prefetch
     float bv[8], rv[8][4];
+    f32x16 keep[EPI == WS_LNBWD ? NT : 1][2];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         const int c = u % CH;
-        if (c == CH - 1) {
+        if (EPI != WS_LNBWD && c == CH - 1) {
             const int n0 = 32 * (wave + 4 * tile_of(u / CH));
             if constexpr (BF) {
                 const int cc = 8 * (lane & 3);
@@ -133,6 +151,13 @@ __global__ __launch_bounds__(256) void gemm_ws_kernel(long M, const bf16* __rest
         }
         __builtin_amdgcn_sched_barrier(0);
         if (c != CH - 1) continue;
+        if constexpr (EPI == WS_LNBWD) {
+            keep[u / CH][0] = a0;
+            keep[u / CH][1] = a1;
+            a0 = f32x16{};
+            a1 = f32x16{};
+            continue;
+        }
         // ---- epilogue of tile nt: acc element (token 32 t + r, feature 32 nt + 8 g + 4 h + e)
         const int nt = wave + 4 * tile_of(u / CH);
 #pragma unroll
@@ -179,12 +204,128 @@ __global__ __launch_bounds__(256) void gemm_ws_kernel(long M, const bf16* __rest
         a1 = f32x16{};
         __builtin_amdgcn_sched_barrier(0);
     }
+    if constexpr (EPI == WS_LNBWD) {
+        // lane (r, h) holds dh of tokens r (t = 0) and 32 + r (t = 1), features
+        // 32 nt(i) + 8 g + 4 h + e of its tiles i.  Pass 1: xhat, g = dh gamma, the token sums of g and
+        // g xhat (lane -> half pair by a shuffle -> the 4 waves through LDS in wave order) and the
+        // column partials of dh xhat / dh over the 64 tokens.  Pass 2: dx.
+        constexpr int C = N;
+        const auto rs_x = buf_rsrc(ln.x + m0 * C, (M - m0) * C * 4);
+        const auto rs_r = buf_rsrc(ln.dres ? ln.dres + m0 * C : nullptr, ln.dres ? (M - m0) * C * 4 : 0);
+        float mu[2], rs[2];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            mu[t] = ln.mean[m0 + 32 * t + r];
+            rs[t] = ln.rstd[m0 + 32 * t + r];
+        }
+        float xh[NT][2][16], gam[NT][16];
+        float rv2[NT][2][16];
+#pragma unroll
+        for (int i = 0; i < NT; ++i) {
+            const int n0 = 32 * (wave + 4 * tile_of(i));
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                load4(ln.gamma + n0 + 8 * g + 4 * h, gam[i] + 4 * g);
+#pragma unroll
+                for (int t = 0; t < 2; ++t) {
+                    const unsigned off = (unsigned)((32 * t + r) * C + n0 + 8 * g + 4 * h) * 4;
+                    buf_ld4(rs_x, off, xh[i][t] + 4 * g);
+                    buf_ld4(rs_r, off, rv2[i][t] + 4 * g);
+                }
+            }
+        }
+        float s1[2] = {0.f, 0.f}, s2[2] = {0.f, 0.f};
+        float dgc[NT][16], dbc[NT][16];
+#pragma unroll
+        for (int i = 0; i < NT; ++i)
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                dgc[i][j] = 0.f;
+                dbc[i][j] = 0.f;
+#pragma unroll
+                for (int t = 0; t < 2; ++t) {
+                    const float dh = keep[i][t][j];
+                    const float x_h = (xh[i][t][j] - mu[t]) * rs[t];
+                    xh[i][t][j] = x_h;
+                    const float gg = dh * gam[i][j];
+                    s1[t] += gg;
+                    s2[t] += gg * x_h;
+                    dgc[i][j] += dh * x_h;
+                    dbc[i][j] += dh;
+                }
+            }
+        float* lnx = ep_all;   // [4 waves][2 sums][64 tokens]
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            s1[t] += __shfl_xor(s1[t], 32, 64);
+            s2[t] += __shfl_xor(s2[t], 32, 64);
+            if (h == 0) {
+                lnx[(wave * 2 + 0) * 64 + 32 * t + r] = s1[t];
+                lnx[(wave * 2 + 1) * 64 + 32 * t + r] = s2[t];
+            }
+        }
+        __syncthreads();
+        float S1[2], S2[2];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            S1[t] = S2[t] = 0.f;
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                S1[t] += lnx[(w * 2 + 0) * 64 + 32 * t + r];
+                S2[t] += lnx[(w * 2 + 1) * 64 + 32 * t + r];
+            }
+            S1[t] *= 1.f / C;
+            S2[t] *= 1.f / C;
+        }
+        const auto rs_dx = buf_rsrc(ln.dx + m0 * C, (M - m0) * C * 4);
+        const auto rs_dxb = buf_rsrc(ln.dxb + m0 * C, (M - m0) * C * 2);
+#pragma unroll
+        for (int i = 0; i < NT; ++i) {
+            const int n0 = 32 * (wave + 4 * tile_of(i));
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    float o[4];
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const int j = 4 * g + e;
+                        o[e] = rs[t] * (keep[i][t][j] * gam[i][j] - S1[t] - xh[i][t][j] * S2[t]) + rv2[i][t][j];
+                    }
+                    const unsigned off = (unsigned)((32 * t + r) * C + n0 + 8 * g + 4 * h);
+                    buf_st4(rs_dx, off * 4, o);
+                    buf_st4bf(rs_dxb, off * 2, o);
+                }
+        }
+        // column partials: the 32 token lanes of each half (xor tree), then lanes r = 0 write the row
+#pragma unroll
+        for (int o = 1; o < 32; o <<= 1)
+#pragma unroll
+            for (int i = 0; i < NT; ++i)
+#pragma unroll
+                for (int j = 0; j < 16; ++j) {
+                    dgc[i][j] += __shfl_xor(dgc[i][j], o, 64);
+                    dbc[i][j] += __shfl_xor(dbc[i][j], o, 64);
+                }
+        if (r == 0) {
+            float* prow = ln.part + (size_t)blockIdx.x * 2 * C;
+#pragma unroll
+            for (int i = 0; i < NT; ++i) {
+                const int n0 = 32 * (wave + 4 * tile_of(i));
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    store4(prow + n0 + 8 * g + 4 * h, dgc[i] + 4 * g);
+                    store4(prow + C + n0 + 8 * g + 4 * h, dbc[i] + 4 * g);
+                }
+            }
+        }
+    }
 }
 
 template <int K, int NT, int EPI, typename TOUT>
 int ws_launch(long M, const bf16* X, int ldx, const bf16* Wf, const float* bias, const float* resid, void* out,
-              hipStream_t st) {
-    gemm_ws_kernel<K, NT, EPI, TOUT><<<dim3((unsigned)(M / WS_BM)), 256, 0, st>>>(M, X, ldx, Wf, bias, resid, (TOUT*)out);
+              hipStream_t st, const WsLn& ln = WsLn{}) {
+    gemm_ws_kernel<K, NT, EPI, TOUT><<<dim3((unsigned)(M / WS_BM)), 256, 0, st>>>(M, X, ldx, Wf, bias, resid, (TOUT*)out, ln);
     return check_launch("gemm_ws");
 }
 
@@ -215,6 +356,18 @@ int gemm_ws_run(long M, int N, int K, const bf16* X, int ldx, const bf16* Wf, co
     WS_SHAPES(WS_GO)
 #undef WS_GO
     return fail(CSU_E_ARG, "gemm_ws: shape not instantiated");
+}
+
+// the LayerNorm-backward epilogue: the qkv input gradients at C = 128 / 256
+int gemm_ws_lnbwd_supported(long M, int N, int K) {
+    if (M < WS_BM || M % WS_BM || M > (1L << 30)) return 0;
+    return (K == 384 && N == 128) || (K == 768 && N == 256);
+}
+
+int gemm_ws_lnbwd_run(long M, int N, int K, const bf16* dy, const bf16* Wtf, const WsLn& ln, hipStream_t st) {
+    if (K == 384 && N == 128) return ws_launch<384, 1, WS_LNBWD, float>(M, dy, K, Wtf, nullptr, nullptr, nullptr, st, ln);
+    if (K == 768 && N == 256) return ws_launch<768, 2, WS_LNBWD, float>(M, dy, K, Wtf, nullptr, nullptr, nullptr, st, ln);
+    return fail(CSU_E_ARG, "gemm_ws_lnbwd: shape not instantiated");
 }
 
 // ---- fragment-ordered weight layout: 16-B chunk q (k 8q..8q+7) of row n of a bf16 (rows x cols)
@@ -249,6 +402,18 @@ extern "C" int csu_gemm_ws(long M, int N, int K, const void* x, int ldx, const v
     if (!gemm_ws_supported(M, N, K, resid != nullptr, out_dtype)) return fail(CSU_E_ARG, "gemm_ws: unsupported shape");
     if (ldx < K || ldx % 8) return fail(CSU_E_ARG, "gemm_ws: ldx must be >= K and a multiple of 8");
     return gemm_ws_run(M, N, K, (const bf16*)x, ldx, (const bf16*)w_frag, bias, resid, out_dtype, out, as_stream(stream));
+}
+
+extern "C" int csu_gemm_ws_lnbwd_supported(long M, int C, int K) { return gemm_ws_lnbwd_supported(M, C, K); }
+
+extern "C" int csu_gemm_ws_lnbwd(long M, int C, int K, const void* dy, const void* wt_frag, const float* x,
+                                 const float* gamma, const float* mean, const float* rstd, const float* dres, float* dx,
+                                 void* dx_bf16, float* part, void* stream) {
+    if (!dy || !wt_frag || !x || !gamma || !mean || !rstd || !dx || !dx_bf16 || !part)
+        return fail(CSU_E_ARG, "gemm_ws_lnbwd: null pointer");
+    if (!gemm_ws_lnbwd_supported(M, C, K)) return fail(CSU_E_ARG, "gemm_ws_lnbwd: unsupported shape");
+    const WsLn ln{x, gamma, mean, rstd, dres, dx, (bf16*)dx_bf16, part};
+    return gemm_ws_lnbwd_run(M, C, K, (const bf16*)dy, (const bf16*)wt_frag, ln, as_stream(stream));
 }
 
 extern "C" int csu_frag_layout_batch(const csu_frag_item* items, int count, long total_chunks, void* stream) {

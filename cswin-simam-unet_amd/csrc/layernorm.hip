@@ -444,7 +444,7 @@ extern "C" int csu_layernorm_param_reduce_batch(const csu_ln_param_item* items, 
             if (it.rows < 1 || !it.workspace || !it.dgamma || !it.dbeta)
                 return fail(CSU_E_ARG, "layernorm_param_reduce_batch: bad item");
             int rpb;
-            t.nb[i] = ln_blocks(it.rows, it.C >= 256 ? 1 : 256 / it.C, &rpb);
+            t.nb[i] = it.nblocks > 0 ? it.nblocks : ln_blocks(it.rows, it.C >= 256 ? 1 : 256 / it.C, &rpb);
             t.C[i] = it.C;
             t.part[i] = (const float*)it.workspace;
             t.dg[i] = it.dgamma;

@@ -33,7 +33,8 @@ class StripeArgs(ctypes.Structure):
 
 class LnParamItem(ctypes.Structure):
     """csu_ln_param_item (include/csu.h)."""
-    _fields_ = [("workspace", c_void_p), ("dgamma", c_void_p), ("dbeta", c_void_p), ("rows", c_int32), ("C", c_int32)]
+    _fields_ = [("workspace", c_void_p), ("dgamma", c_void_p), ("dbeta", c_void_p), ("rows", c_int32), ("C", c_int32),
+                ("nblocks", c_int32), ("_pad", c_int32)]
 
 
 class WslabItem(ctypes.Structure):
@@ -140,6 +141,8 @@ _SIGS = {
     "csu_gemm_ws_supported": (ctypes.c_int, [ctypes.c_long, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     "csu_gemm_ws": (ctypes.c_int, [ctypes.c_long, ctypes.c_int, ctypes.c_int, c_void_p, ctypes.c_int, c_void_p, c_void_p,
                                    c_void_p, ctypes.c_int, c_void_p, c_void_p]),
+    "csu_gemm_ws_lnbwd_supported": (ctypes.c_int, [ctypes.c_long, ctypes.c_int, ctypes.c_int]),
+    "csu_gemm_ws_lnbwd": (ctypes.c_int, [ctypes.c_long, ctypes.c_int, ctypes.c_int] + [c_void_p] * 11),
     "csu_frag_layout_batch": (ctypes.c_int, [c_void_p, ctypes.c_int, ctypes.c_long, c_void_p]),
     "csu_gemm_f32_workspace": (c_size_t, [ctypes.c_int, ctypes.c_long, ctypes.c_int, ctypes.c_long]),
     "csu_gemm_f32": (ctypes.c_int, [ctypes.c_int, ctypes.c_long, ctypes.c_int, ctypes.c_long, c_void_p, c_void_p, c_void_p,

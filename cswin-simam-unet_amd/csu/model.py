@@ -231,6 +231,8 @@ class CSWinBlock(nn.Module):
         # LayerNorm-backward kernel and hands the upstream GEMMs a bf16 copy (ops.layer_norm_fork)
         n1, n2 = self.norm1, self.norm2
         got = ops.ln_linear_fp8(x, n1, self.qkv) if cd == torch.bfloat16 else None
+        if got is None and cd == torch.bfloat16:
+            got = ops.ln_linear_ws(x, n1, self.qkv)   # norm1 backward inside the qkv input-gradient GEMM
         if got is not None:
             xa, qkv = got        # fp8 weight format: e4m3 norm1 output x e4m3 qkv weight on fp8 MFMA
         else:

@@ -343,12 +343,12 @@ def _ln_param_flush():
         return
     dev = pend[0][1].device
     items = (_lib.LnParamItem * len(pend))()
-    for i, (work, dgb, rows, C) in enumerate(pend):
+    for i, (work, dgb, rows, C, nblk) in enumerate(pend):
         items[i].workspace, items[i].dgamma, items[i].dbeta = work.data_ptr(), dgb.data_ptr(), dgb.data_ptr() + C * 4
-        items[i].rows, items[i].C = rows, C
-    nv = sum(2 * C for _, _, _, C in pend)
+        items[i].rows, items[i].C, items[i].nblocks = rows, C, nblk
+    nv = sum(2 * e[3] for e in pend)
     _launch("layernorm_bwd", lambda: lib().csu_layernorm_param_reduce_batch(items, len(pend), stream_ptr(dev)),
-            0, sum(w.numel() for w, _, _, _ in pend) + nv * 4)
+            0, sum(e[0].numel() for e in pend) + nv * 4)
 
 
 def _queue_flush():
@@ -395,11 +395,12 @@ def _lepe_flush():
     _launch("stripe_attn_bwd", lambda: lib().csu_stripe_lepe_reduce_batch(items, len(pend), stream_ptr(dev)), 0, nbytes)
 
 
-def _ln_params(ctx, rows, C, work, dgb):
-    """Reduce (later, batched) or report that the caller must pass dgamma / dbeta pointers."""
+def _ln_params(ctx, rows, C, work, dgb, nblocks=0):
+    """Reduce (later, batched) or report that the caller must pass dgamma / dbeta pointers.
+    ``nblocks``: partial rows in ``work`` (0: csu_layernorm_bwd_ex's for ``rows``)."""
     if not (DEFER_LN and all(dt == torch.float32 for dt in ctx.pdtypes) and _deferrable(*ctx.params)):
         return False
-    _LN_PENDING.append((work, dgb, rows, C))
+    _LN_PENDING.append((work, dgb, rows, C, nblocks))
     _late(ctx.params, (dgb[:C], dgb[C:]))
     _queue_flush()
     return True
@@ -2244,6 +2245,103 @@ class _LnLinearFp8Fn(torch.autograd.Function):
                 db = dbf.to(bdt) if need_b else None
         dx, dg, dbeta = _ln_fork_backward(ctx, x, g, mean, rstd, dres, dh)
         return dx, dg, dbeta, dw, db, None, None, None, None
+
+
+class _LnLinearWsFn(torch.autograd.Function):
+    """Residual junction + LayerNorm + Linear on the weight-streaming GEMM (bf16): x -> (x, LN(x) W^T
+    + b) for CSWinBlock's norm1 -> qkv (cswin:357 -> cswin:337) at C = 128 / 256.  Forward: the
+    LayerNorm (or the values the producing fused Mlp already computed, _ln_pre) and csu_gemm_ws.
+    Backward: ONE csu_gemm_ws_lnbwd launch computes dh = dY W and runs the norm1 backward on it in
+    its epilogue (dx = dres + LN'(dh), its bf16 copy and the dgamma / dbeta block partials) -- dh
+    never reaches HBM and the LayerNorm-backward launch is gone; dW / db of the Linear as _LinearFn."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, weight, bias, eps: float, wf, wtf, pre):
+        x = x.contiguous()
+        C = x.shape[-1]
+        rows = x.numel() // C
+        g = gamma.detach().float().contiguous()
+        if pre is not None:
+            h1, mean, rstd = pre[3].view(x.shape), pre[4], pre[5]
+        else:
+            b = beta.detach().float().contiguous()
+            h1 = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device)
+            mean = torch.empty(rows, dtype=torch.float32, device=x.device)
+            rstd = torch.empty(rows, dtype=torch.float32, device=x.device)
+            _launch("layernorm_fwd", lambda: lib().csu_layernorm_fwd(rows, C, float(eps), dtype_code(x), ptr(x), ptr(g),
+                                                                     ptr(b), CSU_BF16, ptr(h1), ptr(mean), ptr(rstd),
+                                                                     stream_ptr(x.device)),
+                    8 * rows * C, rows * C * (4 + 2) + rows * 8, prec="f32")
+        N = weight.shape[0]
+        h2 = h1.view(rows, C)
+        y = gemm_ws(h2, wf, N, torch.bfloat16, bias=None if bias is None else bias.detach().float().contiguous())
+        ctx.save_for_backward(x, g, mean, rstd, h2, wtf)
+        ctx.params = (gamma, beta)
+        ctx.pdtypes = (gamma.dtype, beta.dtype)
+        ctx.lin = (weight, bias)
+        ctx.lmeta = (weight.dtype, None if bias is None else bias.dtype)
+        _note_use(ctx, gamma, beta, weight, bias)
+        return x.view_as(x), y.view(*x.shape[:-1], N)
+
+    @staticmethod
+    def backward(ctx, dres, dy):
+        x, g, mean, rstd, h, wtf = ctx.saved_tensors
+        wdt, bdt = ctx.lmeta
+        C = x.shape[-1]
+        rows = x.numel() // C
+        if dy is None:    # no gradient through the Linear: the plain fork backward
+            dx, dg, dbeta = _ln_fork_backward(ctx, x, g, mean, rstd, dres, None)
+            return dx, dg, dbeta, None, None, None, None, None, None
+        N = dy.shape[-1]
+        dy2 = _bf16_of(dy).reshape(-1, N).contiguous()
+        dres_k = dres.float().contiguous() if dres is not None else None
+        dx = torch.empty_like(x)
+        dxb = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device)
+        nblk = rows // 64
+        work = torch.empty(nblk * 2 * C, dtype=torch.float32, device=x.device)
+        _launch("gemm", lambda: lib().csu_gemm_ws_lnbwd(rows, C, N, ptr(dy2), ptr(wtf), ptr(x), ptr(g), ptr(mean), ptr(rstd),
+                                                       ptr(dres_k), ptr(dx), ptr(dxb), ptr(work), stream_ptr(x.device)),
+                2 * rows * N * C + 12 * rows * C,
+                rows * N * 2 + N * C * 2 + rows * C * (4 + (4 if dres_k is not None else 0) + 4 + 2) + rows * 8,
+                prec="bf16", tag=f"{rows}x{C}x{N}:lnbwd:ws")
+        dgb = _grad_dest(ctx.params)
+        if dgb is None:
+            dgb = torch.empty(2 * C, dtype=torch.float32, device=x.device)
+        if not _ln_params(ctx, rows, C, work, dgb, nblocks=nblk):
+            it = (_lib.LnParamItem * 1)()
+            it[0].workspace, it[0].dgamma, it[0].dbeta = work.data_ptr(), dgb.data_ptr(), dgb.data_ptr() + C * 4
+            it[0].rows, it[0].C, it[0].nblocks = rows, C, nblk
+            _launch("layernorm_bwd", lambda: lib().csu_layernorm_param_reduce_batch(it, 1, stream_ptr(x.device)),
+                    0, work.numel() * 4 + 2 * C * 4)
+        dw = db = None
+        need_w, need_b = ctx.needs_input_grad[3], bdt is not None and ctx.needs_input_grad[4]
+        if need_w or need_b:
+            dwf, dbf = wgrad_maybe_side(dy2, h, wdt if need_w else None, bdt if need_b else None, params=ctx.lin)
+            dw = dwf.to(wdt) if need_w else None
+            db = dbf.to(bdt) if need_b else None
+        dx._csu_bf16 = dxb
+        return dx, dgb[:C].to(ctx.pdtypes[0]), dgb[C:].to(ctx.pdtypes[1]), dw, db, None, None, None, None
+
+
+# the norm1 -> qkv pair on csu_gemm_ws with the LayerNorm backward in the input-gradient GEMM
+FUSE_LN_QKV = True
+
+
+def ln_linear_ws(x: torch.Tensor, ln: torch.nn.LayerNorm, lin: torch.nn.Linear):
+    """(x, lin(ln(x))) through _LnLinearWsFn (bf16 autocast, fp32 residual stream x, shapes with the
+    weight-streaming GEMM and its LayerNorm-backward epilogue instantiated), else None."""
+    if not (FUSE_LN_QKV and USE_GEMM_WS and x.is_cuda and x.dtype == torch.float32 and _ACTIVE_CACHE is not None):
+        return None
+    N, K = lin.weight.shape
+    if x.shape[-1] != K or ln.weight.numel() != K or ln.weight.dtype != torch.float32:
+        return None
+    wf, wtf = _ACTIVE_CACHE.get_frag(lin.weight), _ACTIVE_CACHE.get_frag_t(lin.weight)
+    M = x.numel() // K
+    if wf is None or wtf is None or not _ws_ok(M, N, K, torch.bfloat16) or not lib().csu_gemm_ws_lnbwd_supported(M, K, N):
+        return None
+    pre = _ln_pre(x, ln.weight, ln.bias, ln.eps, torch.bfloat16)
+    with torch.autocast("cuda", enabled=False):
+        return _LnLinearWsFn.apply(x, ln.weight, ln.bias, lin.weight, lin.bias, ln.eps, wf, wtf, pre)
 
 
 def ln_linear_fp8(x: torch.Tensor, ln: torch.nn.LayerNorm, lin: torch.nn.Linear):

@@ -155,6 +155,8 @@ typedef struct {
     float* dgamma;
     float* dbeta;
     int32_t rows, C;
+    int32_t nblocks;   /* partial rows in the workspace; 0: those of csu_layernorm_bwd_ex for `rows` */
+    int32_t _pad;
 } csu_ln_param_item;
 int csu_layernorm_param_reduce_batch(const csu_ln_param_item* items, int count, void* stream);
 
@@ -324,6 +326,17 @@ int csu_gemm_ex(const csu_gemm_desc* d, void* stream);
 int csu_gemm_ws_supported(long M, int N, int K, int resid, int out_dtype);
 int csu_gemm_ws(long M, int N, int K, const void* x, int ldx, const void* w_frag, const float* bias, const float* resid,
                 int out_dtype, void* out, void* stream);
+/* The input gradient of a LayerNorm -> Linear pair (CSWinBlock norm1 -> qkv, cswin:357 / 337) with the
+ * LayerNorm backward in the GEMM's epilogue: dh = dy (M, K) @ W^T-fragments (wt_frag: the (C, K) weight
+ * transpose, fragment-ordered) is never written; instead dx (M, C) fp32 = dres + rstd (g - mean(g) -
+ * xhat mean(g xhat)), g = dh * gamma, xhat = (x - mean) rstd, its bf16 copy dx_bf16, and the dgamma /
+ * dbeta column partials of every 64-token block into part [M / 64][2C] (reduce them with
+ * csu_layernorm_param_reduce_batch, nblocks = M / 64).  x fp32 (M, C); dres fp32 (M, C) or NULL.
+ * Instantiated for (C, K) = (128, 384), (256, 768); M % 64 == 0 (csu_gemm_ws_lnbwd_supported). */
+int csu_gemm_ws_lnbwd_supported(long M, int C, int K);
+int csu_gemm_ws_lnbwd(long M, int C, int K, const void* dy, const void* wt_frag, const float* x, const float* gamma,
+                      const float* mean, const float* rstd, const float* dres, float* dx, void* dx_bf16, float* part,
+                      void* stream);
 /* Fragment-ordered copy of a bf16 (rows x cols) matrix, rows % 32 == 0, cols % 16 == 0: 16-B chunk
  * q of row n (k = 8q .. 8q+7) goes to chunk ((n / 32) * (cols / 16) + q / 2) * 64 + n % 32 + 32 (q % 2),
  * i.e. [rows/32][cols/16][64 lanes][8] -- the MFMA 32x32x16 A-operand fragment of lane (n % 32, half).

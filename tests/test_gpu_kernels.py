@@ -1387,3 +1387,45 @@ def test_mlp_fwd_ln_next(C, drop):
     finally:
         ops._launch = real
     assert "layernorm_fwd" not in calls and torch.equal(h.view(-1), pre[3].view(-1))
+
+
+@pytest.mark.parametrize("C", [128, 256])
+def test_ln_linear_ws_vs_unfused(C):
+    """_LnLinearWsFn (norm1 -> qkv with the LayerNorm backward in csu_gemm_ws_lnbwd's epilogue) against
+    the unfused layer_norm_fork + linear: outputs and every gradient (dx, dgamma, dbeta, dW, db) agree
+    to bf16 rounding (the fused path feeds the LayerNorm backward dh in fp32, the unfused one rounds it
+    to bf16 first)."""
+    from csu import ops
+    d = dev()
+    torch.manual_seed(C)
+    B, L = 2, 1024
+    x0 = torch.randn(B, L, C, device=d)
+    ln = torch.nn.LayerNorm(C).to(d)
+    lin = torch.nn.Linear(C, 3 * C).to(d)
+    with torch.no_grad():
+        ln.weight.uniform_(0.5, 1.5)
+        ln.bias.uniform_(-0.2, 0.2)
+        lin.bias.uniform_(-0.1, 0.1)
+    G = torch.randn(B, L, 3 * C, device=d)
+    R = torch.randn(B, L, C, device=d)
+
+    def run(fused):
+        for p in (*ln.parameters(), *lin.parameters()):
+            p.grad = None
+        x = x0.clone().requires_grad_(True)
+        if fused:
+            wc = lin.weight.detach().bfloat16()
+            wf, wtf = _frag_ref(wc).contiguous(), _frag_ref(wc.t().contiguous()).contiguous()
+            xa, y = ops._LnLinearWsFn.apply(x, ln.weight, ln.bias, lin.weight, lin.bias, ln.eps, wf, wtf, None)
+        else:
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                xa, h = ops.layer_norm_fork(x, ln.weight, ln.bias, ln.eps, torch.bfloat16)
+                y = ops.linear(h, lin.weight, lin.bias)
+        ((y.float() * G).sum() + (xa * R).sum()).backward()
+        torch.cuda.synchronize()
+        return [y.detach().float(), x.grad, ln.weight.grad, ln.bias.grad, lin.weight.grad, lin.bias.grad]
+
+    a, b = run(True), run(False)
+    for name, u, v in zip(["y", "dx", "dgamma", "dbeta", "dW", "db"], a, b):
+        rel = float((u - v).norm() / v.norm())
+        assert rel < 1e-2, (name, rel)
