@@ -41,7 +41,7 @@ Geo geo(int B, int L, int C) {
     return g;
 }
 
-__device__ __forceinline__ float sigm(float e) { return 1.f / (1.f + __expf(-e)); }
+__device__ __forceinline__ float sigm(float e) { return __builtin_amdgcn_rcpf(1.f + __expf(-e)); }
 
 // fixed-order sum over the 16 row groups of a block -> row group 0's lanes: the 4 row groups of a
 // wave (lane bits 4, 5) by a wavefront xor-butterfly (every lane ends with the same bits), then
@@ -82,6 +82,40 @@ __device__ __forceinline__ void chunk_sums(const float* p, int n, float& s1, flo
         s1 += p[2 * j];
         s2 += p[2 * j + 1];
     }
+}
+
+// Sums (over the g.nch chunk partials) of the 8 values (pairs of 4 channels) of channel quad q, computed
+// by the whole block ONCE: row group tl sums chunks tl, tl + 16, ... (fixed order), row group 0 adds
+// the 16 row groups in order and publishes the totals in LDS (sm2[q][8]); every thread then reads its
+// quad's 8 totals.  (Each of the 16 row groups re-reading all partials of its quad cost 16x the
+// partial bytes per block -- most of the apply passes' time at ~1024 blocks per launch.)
+__device__ __forceinline__ void coop_chunk_sums(const Geo& g, const float* part, size_t bc0, int tl, int q, bool ok,
+                                                float (*sm)[QPR * 8], float (*sm2)[8], float* tot) {
+    float a[8] = {};
+    if (ok)
+        for (int j = tl; j < g.nch; j += 16) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const float2 v = *reinterpret_cast<const float2*>(part + ((bc0 + k) * g.ns + j) * 2);
+                a[2 * k] += v.x;
+                a[2 * k + 1] += v.y;
+            }
+        }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) sm[tl][q * 8 + i] = a[i];
+    __syncthreads();
+    if (tl == 0) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            float t = 0.f;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) t += sm[r][q * 8 + i];
+            sm2[q][i] = t;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 8; ++i) tot[i] = sm2[q][i];
 }
 
 // (mu, s) of the 4 channels c0.. of image b from the chunk partials (chunk order)
@@ -148,16 +182,24 @@ __global__ __launch_bounds__(NT) void simam_stats(Geo g, const T* __restrict__ x
 template <typename T, typename TO>
 __global__ __launch_bounds__(NT) void simam_apply(Geo g, float lam, const T* __restrict__ x, const float* __restrict__ part,
                                                   TO* __restrict__ y, float* __restrict__ stats) {
+    __shared__ float sm[16][QPR * 8];
+    __shared__ float sm2[QPR][8];
     const int b = blockIdx.z, ch = blockIdx.x;
     const int q = threadIdx.x % QPR, tl = threadIdx.x / QPR;
     const int c0 = blockIdx.y * CW + 4 * q;
-    if (c0 >= g.C) return;
-    const size_t off = (size_t)b * g.L * g.C + c0;
-    float piv[4], mu[4], s[4], rs[4];
+    const bool ok = c0 < g.C;
+    const size_t off = (size_t)b * g.L * g.C + (ok ? c0 : 0);
+    float piv[4], mu[4], s[4], rs[4], tot[8];
+    coop_chunk_sums(g, part, (size_t)b * g.C + c0, tl, q, ok, sm, sm2, tot);
+    if (!ok) return;
     load4(x + off, piv);
-    combine_stats(g, part, piv, (size_t)b * g.C + c0, lam, mu, s);
 #pragma unroll
-    for (int k = 0; k < 4; ++k) rs[k] = 1.f / s[k];
+    for (int k = 0; k < 4; ++k) {
+        const float n = (float)g.L, md = tot[2 * k] / n;
+        mu[k] = piv[k] + md;
+        s[k] = 4.f * (fmaxf(tot[2 * k + 1] - tot[2 * k] * md, 0.f) / (n - 1.f) + lam);
+        rs[k] = 1.f / s[k];
+    }
     if (ch == 0 && tl == 0) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -253,18 +295,22 @@ template <typename T, typename TG>
 __global__ __launch_bounds__(NT) void simam_bwd_apply(Geo g, const T* __restrict__ x, const TG* __restrict__ dy,
                                                       const float* __restrict__ stats, const float* __restrict__ part,
                                                       T* __restrict__ dx) {
+    __shared__ float sm[16][QPR * 8];
+    __shared__ float sm2[QPR][8];
     const int b = blockIdx.z, ch = blockIdx.x;
     const int q = threadIdx.x % QPR, tl = threadIdx.x / QPR;
     const int c0 = blockIdx.y * CW + 4 * q;
-    if (c0 >= g.C) return;
+    const bool ok = c0 < g.C;
+    float tot[8];
+    coop_chunk_sums(g, part, (size_t)b * g.C + c0, tl, q, ok, sm, sm2, tot);
+    if (!ok) return;
     const size_t off = (size_t)b * g.L * g.C + c0;
     const float n = (float)g.L;
     float mu[4], rs[4], k1[4], k1n[4], k2[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const size_t bc = (size_t)b * g.C + c0 + k;
-        float A1, A2;
-        chunk_sums(part + bc * g.ns * 2, g.nch, A1, A2);
+        const float A1 = tot[2 * k], A2 = tot[2 * k + 1];
         mu[k] = stats[2 * bc];
         rs[k] = 1.f / stats[2 * bc + 1];
         k1[k] = 2.f * rs[k];

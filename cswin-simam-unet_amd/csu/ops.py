@@ -2324,7 +2324,7 @@ class _LnLinearWsFn(torch.autograd.Function):
 
 
 # the norm1 -> qkv pair on csu_gemm_ws with the LayerNorm backward in the input-gradient GEMM
-FUSE_LN_QKV = True
+FUSE_LN_QKV = False   # measured: the epilogue phase costs what the LayerNorm launch saved
 
 
 def ln_linear_ws(x: torch.Tensor, ln: torch.nn.LayerNorm, lin: torch.nn.Linear):
