@@ -64,26 +64,6 @@ __device__ __forceinline__ void rowgroup_sum(float (*sm)[QPR * K], const float* 
     }
 }
 
-// (sum of [2j], sum of [2j+1]) over j < n, 8 chunks (4 x 16-B loads) in flight per step; fixed
-// order (lane-wise partial sums of the unrolled steps, then combined in a fixed pattern)
-__device__ __forceinline__ void chunk_sums(const float* p, int n, float& s1, float& s2) {
-    f32x4 acc[4] = {};
-    int j = 0;
-    for (; j + 8 <= n; j += 8) {
-        f32x4 v[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const f32x4*>(p + 2 * j + 4 * u);
-#pragma unroll
-        for (int u = 0; u < 4; ++u) acc[u] += v[u];
-    }
-    s1 = ((acc[0][0] + acc[0][2]) + (acc[1][0] + acc[1][2])) + ((acc[2][0] + acc[2][2]) + (acc[3][0] + acc[3][2]));
-    s2 = ((acc[0][1] + acc[0][3]) + (acc[1][1] + acc[1][3])) + ((acc[2][1] + acc[2][3]) + (acc[3][1] + acc[3][3]));
-    for (; j < n; ++j) {
-        s1 += p[2 * j];
-        s2 += p[2 * j + 1];
-    }
-}
-
 // Sums (over the g.nch chunk partials) of the 8 values (pairs of 4 channels) of channel quad q, computed
 // by the whole block ONCE: row group tl sums chunks tl, tl + 16, ... (fixed order), row group 0 adds
 // the 16 row groups in order and publishes the totals in LDS (sm2[q][8]); every thread then reads its
@@ -116,19 +96,6 @@ __device__ __forceinline__ void coop_chunk_sums(const Geo& g, const float* part,
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < 8; ++i) tot[i] = sm2[q][i];
-}
-
-// (mu, s) of the 4 channels c0.. of image b from the chunk partials (chunk order)
-__device__ __forceinline__ void combine_stats(const Geo& g, const float* part, const float* piv, size_t bc0, float lam,
-                                              float* mu, float* s) {
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        float s1, s2;
-        chunk_sums(part + (bc0 + k) * g.ns * 2, g.nch, s1, s2);
-        const float n = (float)g.L, md = s1 / n;
-        mu[k] = piv[k] + md;
-        s[k] = 4.f * (fmaxf(s2 - s1 * md, 0.f) / (n - 1.f) + lam);
-    }
 }
 
 // partial pivot-shifted (sum d, sum d^2) per (b, c, chunk); part[b][c][chunk][2]
