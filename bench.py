@@ -55,7 +55,12 @@ def parse():
                          "use --img 128 --batch 8)")
     ap.add_argument("--depth", default="1,2,9,1")
     ap.add_argument("--split", default="1,2,8,8")
-    ap.add_argument("--simam", action="store_true")
+    ap.add_argument("--simam", action=argparse.BooleanOptionalAction, default=True,
+                    help="SimAM gate on the skip features: the CSWin-SimAM-UNet of BASELINE configs[2] (default); "
+                         "--no-simam: the reference's own architecture (train_cswinunet_segmentation.py has no SimAM)")
+    ap.add_argument("--no-ref-arch", action="store_true",
+                    help="skip the second timed run of the reference architecture (no SimAM) that a SimAM bench "
+                         "line carries as 'reference_architecture' (N = 1 only)")
     ap.add_argument("--dropout", type=float, default=0.0,
                     help="drop_rate = attn_drop_rate = drop_path_rate (the reference main() trains at 0.3, cswin:930-932)")
     ap.add_argument("--cpu-baseline", default="auto", choices=["auto", "on", "off"])
@@ -347,6 +352,9 @@ def main():
             roof["step_frac"] = round(roof["step_t_roof_ms"] / (el / args.steps * 1e3), 4)   # vs the TIMED step
             roof["ledger_step_ms"] = round(ledger_step_ms, 3)
         roof["ledger"] = "graph replays (external HIP event nodes)" if graph_ledger else "eager steps (HIP events)"
+    ref_arch = None
+    if (args.model == "cswin" and args.simam and world == 1 and not dp and use_graph and not args.no_ref_arch):
+        ref_arch = _time_ref_arch(args, device, amp, batches, depth, split, pd)
     cpu = None
     if rank == 0 and world == 1 and (args.cpu_baseline == "on" or (args.cpu_baseline == "auto")):
         try:
@@ -368,6 +376,8 @@ def main():
                "roofline": roof, "cpu_baseline": cpu, "final_loss": round(float(loss.item()), 5),
                "hip_graph": use_graph,
                "grad_allreduce": None if not dp else ("graph-captured buckets" if reducer is not None else "DDP eager")}
+        if ref_arch is not None:
+            rec["reference_architecture"] = ref_arch
         if reducer is not None:   # of the captured step: buckets, how many started during backward, copy-ins
             rec["grad_buckets"] = {"buckets": len(reducer.buckets), "started_in_backward": reducer.last_early,
                                    "grads_copied_in": reducer.last_copied, "bucket_mb": args.bucket_mb,
@@ -375,6 +385,36 @@ def main():
         print(json.dumps(rec), flush=True)
     if dp:
         dist.destroy_process_group()
+
+
+def _time_ref_arch(args, device, amp, batches, depth, split, pd):
+    """The same step (graph-captured, same batches, warm-up and step count) on the reference's own
+    architecture -- CSWinTransformer without SimAM, the model train_cswinunet_segmentation.py trains
+    and the Dice parity is pinned on -- timed right after the headline SimAM line."""
+    from csu.model import CSWinTransformer
+    from csu.train import GraphedTrainStep, bce_loss, make_optimizer
+    torch.manual_seed(0)
+    m = CSWinTransformer(img_size=args.img, depth=depth, split_size=split, simam=False, drop_rate=pd,
+                         attn_drop_rate=pd, drop_path_rate=pd).to(device)
+    if args.dtype == "fp8":
+        m.set_weight_format("fp8_e4m3")
+    opt = make_optimizer(m, capturable=True)
+    gs = GraphedTrainStep(m, opt, bce_loss, batches[0][0], batches[0][1], amp, warmup=args.warmup, metrics=True)
+    for i in range(2):
+        gs(*batches[i % len(batches)])
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        gs(*batches[i % len(batches)])
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    out = {"value": round(args.batch * args.steps / el, 3), "unit": "images/sec", "ms_per_step": round(el / args.steps * 1e3, 3),
+           "steps": args.steps, "warmup": args.warmup,
+           "workload": f"CSWin-UNet train step {args.img}x{args.img} depth {depth} split {split} without SimAM "
+                       f"(the reference architecture, cswin:489-688), AdamW, same batches"}
+    del gs, opt, m
+    torch.cuda.empty_cache()
+    return out
 
 
 def _bench_train_model(args, model, batches, reducer, amp, nparams, world, rank, dp, device):
@@ -424,13 +464,14 @@ def _metric(args):
     if args.model == "unet":
         return f"images/sec at {args.img}x{args.img} {args.dtype} (plain UNet train step)"
     if (args.img, args.dtype, args.depth, args.split, args.dropout, args.simam) == (512, "bf16", "1,2,9,1", "1,2,8,8", 0.0,
-                                                                                  False):
+                                                                                  True):
         try:
             with open(os.path.join(REPO, "BASELINE.json")) as f:
                 return json.load(f)["metric"]
         except Exception:
             pass
-    extra = "".join([", SimAM" if args.simam else "", f", dropout {args.dropout}" if args.dropout > 0 else ""])
+    extra = "".join([", SimAM" if args.simam else ", reference architecture (no SimAM)",
+                     f", dropout {args.dropout}" if args.dropout > 0 else ""])
     return f"images/sec at {args.img}x{args.img} {args.dtype} (CSWin-UNet train step{extra})"
 
 
