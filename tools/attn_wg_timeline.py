@@ -55,6 +55,8 @@ def main():
         valid = t[0] > 0
         t = t[:, valid]
         n = t.shape[1]
+        if n == 0:
+            continue
         t0 = t[0].min()
         start, staged, end = (t[0] - t0) / 100.0, (t[1] - t0) / 100.0, (t[2] - t0) / 100.0   # us
         stage_us, comp_us = staged - start, end - staged
