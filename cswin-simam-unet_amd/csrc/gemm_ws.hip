@@ -43,36 +43,49 @@ struct WsLn {
     float* part;         // [M / 64][2C]
 };
 
-constexpr int WS_BM = 64;   // tokens per workgroup
+constexpr int WS_BM = 64;   // tokens per wave group (the 64-token panel a wave's B fragments hold)
 constexpr bool WS_ROT = true;
 
-constexpr int ws_unit(int ks) {
+// k-steps per unit: the largest divisor of ks <= 16 that still gives the wave >= 2 units (so the
+// next unit's weight loads overlap this unit's MFMAs), else the largest divisor <= 16
+constexpr int ws_unit(int ks, int nt) {
+    for (int u = 16; u > 1; --u)
+        if (ks % u == 0 && nt * (ks / u) >= 2) return u;
     for (int u = 16; u > 1; --u)
         if (ks % u == 0) return u;
     return 1;
 }
+// waves along N: 4 when the 32-feature tiles split evenly over 4 waves, else 2 (N = 64, 192: two token
+// groups of 64 per workgroup, each split over 2 waves) or 1
+constexpr int ws_wn(int n) { return (n / 32) % 4 == 0 ? 4 : (n / 32) % 2 == 0 ? 2 : 1; }
+constexpr int ws_tokens(int n) { return WS_BM * (4 / ws_wn(n)); }   // tokens per workgroup
 
-template <int K, int NT, int EPI, typename TOUT>
-__global__ __launch_bounds__(256) void gemm_ws_kernel(long M, const bf16* __restrict__ X, int ldx,
+template <int K, int N, int EPI, typename TOUT>
+__global__ __launch_bounds__(256, ws_wn(N) < 4 ? 2 : 1) void gemm_ws_kernel(long M, const bf16* __restrict__ X, int ldx,
                                                       const bf16* __restrict__ Wf, const float* __restrict__ bias,
                                                       const float* __restrict__ resid, TOUT* __restrict__ out,
                                                       WsLn ln = WsLn{}) {
-    constexpr int N = 128 * NT;
+    constexpr int WN = ws_wn(N);                   // waves along N
+    constexpr int NT = N / (32 * WN);              // 32-feature tiles per wave
+    static_assert(NT * 32 * WN == N, "gemm_ws: N = 32 WN NT");
+    static_assert(EPI != WS_LNBWD || WN == 4, "gemm_ws: the LayerNorm epilogue needs all C features in one token group");
     constexpr int KS = K / 16;                     // k-steps
-    constexpr int UK = ws_unit(KS);                // k-steps per unit (a divisor of KS, <= 16)
+    constexpr int UK = ws_unit(KS, NT);            // k-steps per unit (a divisor of KS, <= 16)
     constexpr int CH = KS / UK;                    // units per tile
     static_assert(CH * UK == KS, "unit size");
     constexpr int U = NT * CH;                     // units per wave
     constexpr bool XREG = K <= 256;                // B fragments held in registers
+    constexpr bool XLDS = !XREG || WN == 4;        // token panel staged through LDS (else direct fragment loads)
     constexpr int XS = K + 8;                      // LDS row stride of the token panel (bf16)
     constexpr int ES = 36;                         // fp32 row stride of the epilogue region
-    __shared__ __attribute__((aligned(16))) bf16 xs[WS_BM * XS];
+    __shared__ __attribute__((aligned(16))) bf16 xs[XLDS ? WS_BM * XS : 8];
     __shared__ __attribute__((aligned(16))) float ep_all[4 * WS_BM * ES];
 
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wn = wave % WN;                      // this wave's N slot
     const int r = lane & 31, h = lane >> 5;
-    const long m0 = (long)blockIdx.x * WS_BM;
+    const long m0 = (long)blockIdx.x * ws_tokens(N) + WS_BM * (wave / WN);   // the wave's 64-token panel
     float* ep = ep_all + wave * WS_BM * ES;
 
     // tile order rotated per workgroup (its index within the XCD: ids x, x + 8, ... run on XCD x), so
@@ -81,26 +94,36 @@ __global__ __launch_bounds__(256) void gemm_ws_kernel(long M, const bf16* __rest
     auto tile_of = [&](int i) { return i + rot < NT ? i + rot : i + rot - NT; };
     bf16x8 wf[2][UK];
     auto wload1 = [&](int u, int s) {   // k-step s of unit u of this wave into buffer u & 1
-        const int nt = wave + 4 * tile_of(u / CH), ks = (u % CH) * UK + s;
+        const int nt = wn + WN * tile_of(u / CH), ks = (u % CH) * UK + s;
         wf[u & 1][s] = *reinterpret_cast<const bf16x8*>(Wf + ((long)(nt * KS + ks) * 64 + lane) * 8);
     };
 #pragma unroll
     for (int s = 0; s < UK; ++s) wload1(0, s);
     __builtin_amdgcn_sched_barrier(0);
-    // token panel -> LDS (16-B pieces, row-contiguous)
-    constexpr int PR = K / 8;   // pieces per row
-#pragma unroll
-    for (int i = 0; i < WS_BM * PR / 256; ++i) {
-        const int p = threadIdx.x + 256 * i, row = p / PR, c = 8 * (p % PR);
-        *reinterpret_cast<bf16x8*>(xs + row * XS + c) = *reinterpret_cast<const bf16x8*>(X + (m0 + row) * ldx + c);
-    }
-    __syncthreads();
     bf16x8 xf[XREG ? 2 : 1][XREG ? KS : 1];
-    if constexpr (XREG) {
+    if constexpr (XLDS) {
+        // token panel -> LDS (16-B pieces, row-contiguous; one token group: WN = 4)
+        constexpr int PR = K / 8;   // pieces per row
+#pragma unroll
+        for (int i = 0; i < WS_BM * PR / 256; ++i) {
+            const int p = threadIdx.x + 256 * i, row = p / PR, c = 8 * (p % PR);
+            *reinterpret_cast<bf16x8*>(xs + row * XS + c) = *reinterpret_cast<const bf16x8*>(X + (m0 + row) * ldx + c);
+        }
+        __syncthreads();
+        if constexpr (XREG) {
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+#pragma unroll
+                for (int s = 0; s < KS; ++s) xf[t][s] = *reinterpret_cast<const bf16x8*>(xs + (32 * t + r) * XS + 16 * s + 8 * h);
+        }
+    } else {
+        // B fragments straight from the token rows (lane (r, h): row r, k 16 s + 8 h .. + 7; a row's
+        // 16-B pieces over the KS loads cover its lines once)
 #pragma unroll
         for (int t = 0; t < 2; ++t)
 #pragma unroll
-            for (int s = 0; s < KS; ++s) xf[t][s] = *reinterpret_cast<const bf16x8*>(xs + (32 * t + r) * XS + 16 * s + 8 * h);
+            for (int s = 0; s < KS; ++s)
+                xf[t][s] = *reinterpret_cast<const bf16x8*>(X + (m0 + 32 * t + r) * ldx + 16 * s + 8 * h);
     }
     __builtin_amdgcn_sched_barrier(0);
 
@@ -115,7 +138,7 @@ __global__ __launch_bounds__(256) void gemm_ws_kernel(long M, const bf16* __rest
     for (int u = 0; u < U; ++u) {
         const int c = u % CH;
         if (EPI != WS_LNBWD && c == CH - 1) {
-            const int n0 = 32 * (wave + 4 * tile_of(u / CH));
+            const int n0 = 32 * (wn + WN * tile_of(u / CH));
             if constexpr (BF) {
                 const int cc = 8 * (lane & 3);
                 buf_ld4(rs_b, (unsigned)(n0 + cc) * 4, bv);
@@ -159,7 +182,7 @@ __global__ __launch_bounds__(256) void gemm_ws_kernel(long M, const bf16* __rest
             continue;
         }
         // ---- epilogue of tile nt: acc element (token 32 t + r, feature 32 nt + 8 g + 4 h + e)
-        const int nt = wave + 4 * tile_of(u / CH);
+        const int nt = wn + WN * tile_of(u / CH);
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
             const f32x16& a = t ? a1 : a0;
@@ -222,7 +245,7 @@ __global__ __launch_bounds__(256) void gemm_ws_kernel(long M, const bf16* __rest
         float rv2[NT][2][16];
 #pragma unroll
         for (int i = 0; i < NT; ++i) {
-            const int n0 = 32 * (wave + 4 * tile_of(i));
+            const int n0 = 32 * (wn + WN * tile_of(i));
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
                 load4(ln.gamma + n0 + 8 * g + 4 * h, gam[i] + 4 * g);
@@ -281,7 +304,7 @@ __global__ __launch_bounds__(256) void gemm_ws_kernel(long M, const bf16* __rest
         const auto rs_dxb = buf_rsrc(ln.dxb + m0 * C, (M - m0) * C * 2);
 #pragma unroll
         for (int i = 0; i < NT; ++i) {
-            const int n0 = 32 * (wave + 4 * tile_of(i));
+            const int n0 = 32 * (wn + WN * tile_of(i));
 #pragma unroll
             for (int t = 0; t < 2; ++t)
 #pragma unroll
@@ -311,7 +334,7 @@ __global__ __launch_bounds__(256) void gemm_ws_kernel(long M, const bf16* __rest
             float* prow = ln.part + (size_t)blockIdx.x * 2 * C;
 #pragma unroll
             for (int i = 0; i < NT; ++i) {
-                const int n0 = 32 * (wave + 4 * tile_of(i));
+                const int n0 = 32 * (wn + WN * tile_of(i));
 #pragma unroll
                 for (int g = 0; g < 4; ++g) {
                     store4(prow + n0 + 8 * g + 4 * h, dgc[i] + 4 * g);
@@ -322,21 +345,23 @@ __global__ __launch_bounds__(256) void gemm_ws_kernel(long M, const bf16* __rest
     }
 }
 
-template <int K, int NT, int EPI, typename TOUT>
+template <int K, int N, int EPI, typename TOUT>
 int ws_launch(long M, const bf16* X, int ldx, const bf16* Wf, const float* bias, const float* resid, void* out,
               hipStream_t st, const WsLn& ln = WsLn{}) {
-    gemm_ws_kernel<K, NT, EPI, TOUT><<<dim3((unsigned)(M / WS_BM)), 256, 0, st>>>(M, X, ldx, Wf, bias, resid, (TOUT*)out, ln);
+    gemm_ws_kernel<K, N, EPI, TOUT><<<dim3((unsigned)(M / ws_tokens(N))), 256, 0, st>>>(M, X, ldx, Wf, bias, resid, (TOUT*)out, ln);
     return check_launch("gemm_ws");
 }
 
-// the shapes instantiated: (K, N) of the CSWinBlock qkv / proj Linears at C = 128 / 256 and their
-// input gradients (qkv^T: K = 3C, N = C)
-#define WS_SHAPES(X_) X_(128, 384) X_(256, 768) X_(384, 128) X_(768, 256) X_(128, 128) X_(256, 256)
+// the shapes instantiated: (K, N) of the CSWinBlock qkv / proj Linears at C = 64 / 128 / 256 and their
+// input gradients (qkv^T: K = 3C, N = C).  Not (192, 64), the C = 64 qkv input gradient: 82.4 vs 67.7
+// us/step on gemm4 in the step (profiles/r07q_ws_s1.txt); the C = 64 forward 60.7 vs 73.0.
+#define WS_SHAPES(X_) X_(128, 384) X_(256, 768) X_(384, 128) X_(768, 256) X_(128, 128) X_(256, 256) \
+    X_(64, 192) X_(64, 64)
 
 }  // namespace
 
 int gemm_ws_supported(long M, int N, int K, int resid, int out_dtype) {
-    if (M < WS_BM || M % WS_BM || M > (1L << 30)) return 0;
+    if (M < ws_tokens(N) || M % ws_tokens(N) || M > (1L << 30)) return 0;
     if (resid && out_dtype != CSU_F32) return 0;
     if (out_dtype != CSU_F32 && out_dtype != CSU_BF16) return 0;
 #define WS_HAS(KK, NN) if (K == KK && N == NN) return 1;
@@ -349,9 +374,9 @@ int gemm_ws_run(long M, int N, int K, const bf16* X, int ldx, const bf16* Wf, co
                 int out_dtype, void* out, hipStream_t st) {
 #define WS_GO(KK, NN)                                                                                             \
     if (K == KK && N == NN) {                                                                                     \
-        if (resid) return ws_launch<KK, NN / 128, WS_RESID, float>(M, X, ldx, Wf, bias, resid, out, st);          \
-        if (out_dtype == CSU_F32) return ws_launch<KK, NN / 128, WS_PLAIN, float>(M, X, ldx, Wf, bias, nullptr, out, st); \
-        return ws_launch<KK, NN / 128, WS_PLAIN, bf16>(M, X, ldx, Wf, bias, nullptr, out, st);                    \
+        if (resid) return ws_launch<KK, NN, WS_RESID, float>(M, X, ldx, Wf, bias, resid, out, st);          \
+        if (out_dtype == CSU_F32) return ws_launch<KK, NN, WS_PLAIN, float>(M, X, ldx, Wf, bias, nullptr, out, st); \
+        return ws_launch<KK, NN, WS_PLAIN, bf16>(M, X, ldx, Wf, bias, nullptr, out, st);                    \
     }
     WS_SHAPES(WS_GO)
 #undef WS_GO
@@ -365,8 +390,8 @@ int gemm_ws_lnbwd_supported(long M, int N, int K) {
 }
 
 int gemm_ws_lnbwd_run(long M, int N, int K, const bf16* dy, const bf16* Wtf, const WsLn& ln, hipStream_t st) {
-    if (K == 384 && N == 128) return ws_launch<384, 1, WS_LNBWD, float>(M, dy, K, Wtf, nullptr, nullptr, nullptr, st, ln);
-    if (K == 768 && N == 256) return ws_launch<768, 2, WS_LNBWD, float>(M, dy, K, Wtf, nullptr, nullptr, nullptr, st, ln);
+    if (K == 384 && N == 128) return ws_launch<384, 128, WS_LNBWD, float>(M, dy, K, Wtf, nullptr, nullptr, nullptr, st, ln);
+    if (K == 768 && N == 256) return ws_launch<768, 256, WS_LNBWD, float>(M, dy, K, Wtf, nullptr, nullptr, nullptr, st, ln);
     return fail(CSU_E_ARG, "gemm_ws_lnbwd: shape not instantiated");
 }
 

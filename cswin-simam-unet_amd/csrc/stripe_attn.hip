@@ -1392,34 +1392,60 @@ __device__ __forceinline__ bf16x8 tr_frag16(const bf16* img, int kb, int cb, int
     return out;
 }
 
-// gather window rows [0, npad) of one head's channels of two tensors: A into a PLAIN [row][32] image
-// (the prologue's V: neighbour rows are base + constant, no swizzle arithmetic), B swizzled (swz);
-// rows >= N zero.  Loads first, then the LDS stores (one memory latency).
-template <int NTH = NT>
-__device__ __forceinline__ void stage_win2_pa(const Win& w, int reso, const bf16* imgA, int strideA, int chA,
-                                              const bf16* imgB, int strideB, int chB, int npad, bf16* dstA, bf16* dstB) {
-    constexpr int IT = 4;
+// cross-lane sums on the VALU: DPP moves (quad_perm / row_half_mirror / row_ror) and the CDNA4 permlane
+// swaps (xsum16: rows 2i <-> 2i+1, xsum32: half-waves) -- no LDS round trip
+template <int CTRL>
+__device__ __forceinline__ float dppf(float x) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), CTRL, 0xF, 0xF, true));
+}
+__device__ __forceinline__ float sum8_dpp(float x) {   // sum over each aligned group of 8 lanes
+    x += dppf<0xB1>(x);    // quad_perm [1,0,3,2]
+    x += dppf<0x4E>(x);    // quad_perm [2,3,0,1]
+    return x + dppf<0x141>(x);   // row_half_mirror: lane i <- 7 - i of its 8-lane group
+}
+__device__ __forceinline__ float xsum16(float x) {   // x + x of lane ^ 16
+    const unsigned u = __builtin_bit_cast(unsigned, x);
+    const auto r = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+    return __builtin_bit_cast(float, (unsigned)r[0]) + __builtin_bit_cast(float, (unsigned)r[1]);
+}
+__device__ __forceinline__ float xsum32(float x) {   // x + x of lane ^ 32
+    const unsigned u = __builtin_bit_cast(unsigned, x);
+    const auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+    return __builtin_bit_cast(float, (unsigned)r[0]) + __builtin_bit_cast(float, (unsigned)r[1]);
+}
+
+// the fused backward's four window images in ONE pass (one memory latency instead of two): Q, K and
+// dO swizzled (swz), V into a PLAIN [row][32] image; rows [N, npad) zero.  All loads of the pass are
+// issued before the first LDS store (16 IT VGPRs of staged data).
+template <int NTH, int WM>
+__device__ __forceinline__ void stage_win4(const Win& w, int reso, const bf16* img, int C, const bf16* gimg, int npad,
+                                           bf16* Qs, bf16* Ks, bf16* Vs, bf16* Gs) {
+    constexpr int IT = (WM * 4 + NTH - 1) / NTH;   // 16-B items per thread (npad <= WM)
     const long L = (long)reso * reso;
-    const __amdgpu_buffer_rsrc_t rsA = buf_rsrc(imgA, L * strideA * 2), rsB = buf_rsrc(imgB, L * strideB * 2);
-    for (int base = 0; base < npad * 4; base += IT * NTH) {
-        bf16x8 va[IT], vb[IT];
+    const unsigned C3 = 3u * (unsigned)C;
+    const __amdgpu_buffer_rsrc_t rs = buf_rsrc(img, L * C3 * 2), rg = buf_rsrc(gimg, L * C * 2);
+    bf16x8 vq[IT], vk[IT], vv[IT], vg[IT];
 #pragma unroll
-        for (int i = 0; i < IT; ++i) {
-            const int it = base + threadIdx.x + i * NTH;
+    for (int i = 0; i < IT; ++i) {
+        const int it = threadIdx.x + i * NTH;
+        const int n = it >> 2, c = (it & 3) * 8;
+        const bool ok = it < npad * 4 && n < w.N;
+        const unsigned tok = ok ? (unsigned)tok_of(w, reso, n) : 0u;
+        const unsigned oq = (tok * C3 + w.chq + c) * 2u;
+        vq[i] = ld8_rs(rs, ok ? oq : kOOB);
+        vk[i] = ld8_rs(rs, ok ? oq + 2u * C : kOOB);
+        vv[i] = ld8_rs(rs, ok ? oq + 4u * C : kOOB);
+        vg[i] = ld8_rs(rg, ok ? (tok * (unsigned)C + w.chq + c) * 2u : kOOB);
+    }
+#pragma unroll
+    for (int i = 0; i < IT; ++i) {
+        const int it = threadIdx.x + i * NTH;
+        if (it < npad * 4) {
             const int n = it >> 2, c = (it & 3) * 8;
-            const bool ok = it < npad * 4 && n < w.N;
-            const unsigned tok = ok ? (unsigned)tok_of(w, reso, n) : 0u;
-            va[i] = ld8_rs(rsA, ok ? (tok * (unsigned)strideA + chA + c) * 2u : kOOB);
-            vb[i] = ld8_rs(rsB, ok ? (tok * (unsigned)strideB + chB + c) * 2u : kOOB);
-        }
-#pragma unroll
-        for (int i = 0; i < IT; ++i) {
-            const int it = base + threadIdx.x + i * NTH;
-            if (it < npad * 4) {
-                const int n = it >> 2, c = (it & 3) * 8;
-                *reinterpret_cast<bf16x8*>(dstA + n * HD + c) = va[i];
-                *reinterpret_cast<bf16x8*>(dstB + swz(n, c)) = vb[i];
-            }
+            *reinterpret_cast<bf16x8*>(Qs + swz(n, c)) = vq[i];
+            *reinterpret_cast<bf16x8*>(Ks + swz(n, c)) = vk[i];
+            *reinterpret_cast<bf16x8*>(Vs + n * HD + c) = vv[i];
+            *reinterpret_cast<bf16x8*>(Gs + swz(n, c)) = vg[i];
         }
     }
 }
@@ -1502,8 +1528,7 @@ __global__ __launch_bounds__(64 * NW, WM <= 256 ? 2 : 1) void stripe_bwd_fused_w
                     rs_o, n < w.N ? (unsigned)(((size_t)tok_of(w, a.reso, n) * C + w.chq + 4 * c4) * 2) : kOOB, 0, 0);
             }
         }
-        stage_win2<NTH>(w, a.reso, img, C3, w.chq, img, C3, C + w.chq, npad, Qs, Ks);
-        stage_win2_pa<NTH>(w, a.reso, img, C3, 2 * C + w.chq, gimg, C, w.chq, npad, Vs, Gs);
+        stage_win4<NTH, WM>(w, a.reso, img, C, gimg, npad, Qs, Ks, Vs, Gs);
         lepe_weights_store(lw, wts);
         if (threadIdx.x < 8) {   // the zero rows
             const bf16x8 z = {};
@@ -1519,63 +1544,85 @@ __global__ __launch_bounds__(64 * NW, WM <= 256 ? 2 : 1) void stripe_bwd_fused_w
     ATT_STAMP(1, 1);
 
     // ---- prologue: delta and the LePE weight-gradient partials (thread: channel quad c4, rows rg + RS k)
+    // RP rows per iteration with all their LDS reads issued before any use (one LDS latency per
+    // iteration; r07n: one row per iteration waited on four read batches and three ds_bpermute round
+    // trips); the cross-lane sums are DPP / permlane-swap VALU ops, not LDS permutes.  RP = 1 at
+    // WM = 128: a second row's V values would push the kernel past 168 VGPRs (3 waves per SIMD).
     {
+        constexpr int RP = WM <= 128 ? 1 : 2;
+        static_assert(PR % RP == 0, "prologue: whole row groups per thread");
         float wacc[40];
 #pragma unroll
         for (int i = 0; i < 40; ++i) wacc[i] = 0.f;
         const f32x4 bias = *reinterpret_cast<const f32x4*>(wts + HD * 9 + 4 * c4);
         const bf16* vq = Vs + 4 * c4;                  // plain image: row n of this quad at vq + 32 n
-        // rows one at a time (unrolled, the compiler turns the 40 accumulations into per-sum chains
-        // over all rows and keeps every row's V values live); the preloaded O rows rotate through
-        // orow[0] so every register index stays static.  Out-of-window taps read the zero row.
+        // the preloaded O rows rotate through orow[0..RP) so every register index stays static.
+        // Out-of-window taps read the zero row.
 #pragma unroll 1
-        for (int n = rg; n < npad; n += RS) {
-            const bool valid = n < w.N;                    // uniform over the 8 lanes of the row
-            const int nn = valid ? n : 0;
-            const u32x2 oraw = orow[0];
+        for (int n0 = rg; n0 < npad; n0 += RP * RS) {
+            bf16x4 g4[RP], v4[RP][9];
+            bool valid[RP];
+            u32x2 oraw[RP];
 #pragma unroll
-            for (int k = 0; k + 1 < PR; ++k) orow[k] = orow[k + 1];
-            const int iy = wrow(w, nn), ix = nn - iy * w.W_sp;
-            const bool ym = iy > 0, yp = iy + 1 < w.H_sp, xm = ix > 0, xp = ix + 1 < w.W_sp;
-            const bf16x4 g4 = *reinterpret_cast<const bf16x4*>(Gs + swz(nn, 4 * c4));
-            float gv[4], lp[4];
+            for (int p = 0; p < RP; ++p) {
+                const int n = n0 + p * RS;
+                valid[p] = n < w.N;                        // uniform over the 8 lanes of the row
+                const int nn = valid[p] ? n : 0;
+                oraw[p] = orow[p];
+                const int iy = wrow(w, nn), ix = nn - iy * w.W_sp;
+                const bool ym = iy > 0, yp = iy + 1 < w.H_sp, xm = ix > 0, xp = ix + 1 < w.W_sp;
+                g4[p] = *reinterpret_cast<const bf16x4*>(Gs + swz(nn, 4 * c4));
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                gv[j] = valid ? (float)g4[j] : 0.f;
-                lp[j] = bias[j];
-            }
-#pragma unroll
-            for (int t = 0; t < 9; ++t) {
-                const int dy = t / 3 - 1, dx = t % 3 - 1;
-                const bool in = (dy < 0 ? ym : dy > 0 ? yp : true) && (dx < 0 ? xm : dx > 0 ? xp : true);
-                const int row = in ? nn + dy * w.W_sp + dx : WM;
-                const bf16x4 v4 = *reinterpret_cast<const bf16x4*>(vq + row * HD);
-                const f32x4 wt = *reinterpret_cast<const f32x4*>(wts + t * HD + 4 * c4);
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const float v = (float)v4[j];
-                    lp[j] = fmaf(wt[j], v, lp[j]);
-                    wacc[4 * t + j] = fmaf(gv[j], v, wacc[4 * t + j]);
+                for (int t = 0; t < 9; ++t) {
+                    const int dy = t / 3 - 1, dx = t % 3 - 1;
+                    const bool in = (dy < 0 ? ym : dy > 0 ? yp : true) && (dx < 0 ? xm : dx > 0 ? xp : true);
+                    const int row = in ? nn + dy * w.W_sp + dx : WM;
+                    v4[p][t] = *reinterpret_cast<const bf16x4*>(vq + row * HD);
                 }
             }
-            bf16x4 o4;
-            __builtin_memcpy(&o4, &oraw, 8);
-            float dl = 0.f;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                wacc[36 + j] += gv[j];
-                dl = fmaf(gv[j], (float)o4[j] - lp[j], dl);
+            for (int k = 0; k + RP < PR; ++k) orow[k] = orow[k + RP];
+            __builtin_amdgcn_sched_barrier(0);             // every read above issues before the math
+            float dl[RP];
+#pragma unroll
+            for (int p = 0; p < RP; ++p) {
+                float gv[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) gv[j] = valid[p] ? (float)g4[p][j] : 0.f;
+                // LePE in packed pairs (v_pk_fma_f32: half the VALU issue of per-channel FMAs)
+                f2 lp[2] = {f2{bias[0], bias[1]}, f2{bias[2], bias[3]}};
+#pragma unroll
+                for (int t = 0; t < 9; ++t) {
+                    const f32x4 wt = *reinterpret_cast<const f32x4*>(wts + t * HD + 4 * c4);
+#pragma unroll
+                    for (int j2 = 0; j2 < 2; ++j2) {
+                        const f2 v = {(float)v4[p][t][2 * j2], (float)v4[p][t][2 * j2 + 1]};
+                        lp[j2] = __builtin_elementwise_fma(f2{wt[2 * j2], wt[2 * j2 + 1]}, v, lp[j2]);
+                        wacc[4 * t + 2 * j2] = fmaf(gv[2 * j2], v.x, wacc[4 * t + 2 * j2]);
+                        wacc[4 * t + 2 * j2 + 1] = fmaf(gv[2 * j2 + 1], v.y, wacc[4 * t + 2 * j2 + 1]);
+                    }
+                }
+                bf16x4 o4;
+                __builtin_memcpy(&o4, &oraw[p], 8);
+                float d = 0.f;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    wacc[36 + j] += gv[j];
+                    d = fmaf(gv[j], (float)o4[j] - lp[j >> 1][j & 1], d);
+                }
+                dl[p] = sum8_dpp(d);
             }
-            dl += __shfl_xor(dl, 1, 64);
-            dl += __shfl_xor(dl, 2, 64);
-            dl += __shfl_xor(dl, 4, 64);
-            if (c4 == 0) dl_s[n] = dl;                     // padded rows: 0
+            if (c4 == 0) {                                 // padded rows: 0
+#pragma unroll
+                for (int p = 0; p < RP; ++p)
+                    if (n0 + p * RS < npad) dl_s[n0 + p * RS] = dl[p];
+            }
         }
         if (part) {
+            // sum over the wave's 8 row groups (lanes of equal c4 = lane & 7): row_ror:8 pairs the two
+            // halves of each 16-lane row, the permlane swaps the rows
 #pragma unroll
-            for (int m = 8; m < 64; m <<= 1)
-#pragma unroll
-                for (int i = 0; i < 40; ++i) wacc[i] += __shfl_xor(wacc[i], m, 64);
+            for (int i = 0; i < 40; ++i) wacc[i] = xsum32(xsum16(wacc[i] + dppf<0x128>(wacc[i])));
             if (lane < 8)
 #pragma unroll
                 for (int i = 0; i < 40; ++i) red[wave][lane][i] = wacc[i];

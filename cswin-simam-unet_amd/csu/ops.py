@@ -1926,10 +1926,10 @@ class CastCache:
             if p.dim() != 2:
                 continue
             N, K = p.shape
-            if L.csu_gemm_ws_supported(64, N, K, 0, CSU_BF16):
+            if L.csu_gemm_ws_supported(1024, N, K, 0, CSU_BF16):
                 self.frag_w[i] = torch.empty(N * K, dtype=dtype, device=p.device)
                 recs.append((self.shadow[i], self.frag_w[i], N, K))
-            if L.csu_gemm_ws_supported(64, K, N, 0, CSU_BF16) and self.shadow_t[i] is not None:
+            if L.csu_gemm_ws_supported(1024, K, N, 0, CSU_BF16) and self.shadow_t[i] is not None:
                 self.frag_t[i] = torch.empty(N * K, dtype=dtype, device=p.device)
                 recs.append((self.shadow_t[i], self.frag_t[i], K, N))
         if not recs:

@@ -1310,7 +1310,9 @@ def test_frag_layout_batch(rows, cols):
 
 
 GEMM_WS_SHAPES = [(16384, 768, 256), (16384, 256, 768), (16384, 256, 256), (1024, 384, 128), (65536, 128, 384),
-                  (192, 128, 128)]
+                  (192, 128, 128),
+                  # stage-1 shapes (C = 64): two 64-token groups per workgroup, direct fragment loads
+                  (262144, 192, 64), (1024, 64, 64), (384, 192, 64)]
 
 
 @pytest.mark.parametrize("M,N,K", GEMM_WS_SHAPES)
@@ -1343,6 +1345,9 @@ def test_gemm_ws_vs_fp64(M, N, K, mode):
         assert err <= 2 ** -8 * scale + 1e-6, (err, scale)
     with pytest.raises(Exception):
         ops.gemm_ws(x[:M - 8], _frag_ref(w).contiguous(), N, odt)   # M % 64 != 0: refused
+    if N in (64, 192):
+        with pytest.raises(Exception):
+            ops.gemm_ws(x[:M - 64], _frag_ref(w).contiguous(), N, odt)   # two token groups: M % 128 != 0
 
 
 @pytest.mark.parametrize("C", [64, 128, 256])

@@ -34,14 +34,17 @@ def t_us(fn, cold, it=20):
 
 
 d = torch.device("cuda")
-for M, N, K, mode in [(16384, 768, 256, "b"), (16384, 256, 768, ""), (16384, 256, 256, "rb"), (16384, 256, 256, ""),
-                      (65536, 384, 128, "b"), (65536, 128, 384, ""), (65536, 128, 128, "rb")]:
+SHAPES = [(16384, 768, 256, "b"), (16384, 256, 768, ""), (16384, 256, 256, "rb"), (16384, 256, 256, ""),
+          (65536, 384, 128, "b"), (65536, 128, 384, ""), (65536, 128, 128, "rb")]
+# SHAPES=s1: the stage-1 (262144-token, C = 64) qkv / proj Linears and their input gradients
+S1 = [(262144, 192, 64, "b"), (262144, 64, 192, ""), (262144, 64, 64, "rb"), (262144, 64, 64, ""), (262144, 64, 64, "bf")]
+for M, N, K, mode in (S1 if os.environ.get("SHAPES") == "s1" else SHAPES):
     x = torch.randn(M, K, device=d).bfloat16()
     w = (torch.randn(N, K, device=d) / K ** 0.5).bfloat16()
     wf = frag(w)
     bias = torch.randn(N, device=d) if "b" in mode else None
     res = torch.randn(M, N, device=d) if "r" in mode else None
-    odt = torch.float32 if res is not None else torch.bfloat16
+    odt = torch.float32 if res is not None or "f" in mode else torch.bfloat16
     f_ws = lambda: ops.gemm_ws(x, wf, N, odt, bias=bias, resid=res)  # noqa: E731
     f_g4 = lambda: ops.gemm(x, w, False, odt, bias=bias, resid=res)  # noqa: E731
     print(f"{M:6d}x{N:4d}x{K:4d}{mode:3s} ws hot {t_us(f_ws, False):6.2f} cold {t_us(f_ws, True):6.2f} | "
