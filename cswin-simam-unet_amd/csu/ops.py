@@ -1646,7 +1646,10 @@ class _MlpFp8Fn(torch.autograd.Function):
     quantised the same way, the weight scales folded into them) and writes dh, g_q (the forward's
     fc2 input) and dx; then the two bf16 weight gradients dW1 = dh^T x, dW2 = dY^T g_q.  For C not in
     FP8_MLP_BWD_C the backward is the bf16 fused one (_MlpFusedFn) on the dequantised weights w1c / w2c
-    (oracle: fp8_ref.Fp8MlpFn with bwd_fp8=False)."""
+    (oracle: fp8_ref.Fp8MlpFn with bwd_fp8=False).  That backward recomputes h and g from the
+    UNQUANTISED bf16 x, so at C = 64 / 128 dW2 = dY^T g (not the forward's g_q) and dW1 uses the
+    unquantised x: a different straight-through estimator from C = 256's, chosen deliberately because
+    the fp8 backward kernel is slower than the bf16 one at those widths."""
 
     @staticmethod
     def forward(ctx, res, x, w1, b1, w2, b2, ops8, drop, w1c, w2c):

@@ -50,6 +50,12 @@ def main():
             print(f"stage {st} fused bwd: {t.shape[1]} workgroups, span {(t[4].max() - t[0].min()) / 100:.1f} us, "
                   f"per WG p50 {np.median(tot):.1f} us = staging {np.median(ph[0]):.1f} + prologue "
                   f"{np.median(ph[1]):.1f} + main {np.median(ph[2]):.1f} + epilogue {np.median(ph[3]):.1f}")
+            s2 = buf[2, :3].astype(np.int64)[:, valid]
+            if (s2 > 0).all():   # the prologue's sub-phases (stamped into the unused dkdv slots)
+                sub = np.diff(np.vstack([t[1], s2, t[2]]), axis=0) / 100.0
+                print(f"   prologue p50: rows {np.median(sub[0]):.1f} + weight-gradient sums {np.median(sub[1]):.1f} + "
+                      f"fragments and barrier {np.median(sub[2]):.1f} + partial stores {np.median(sub[3]):.1f} us")
+                buf[2] = 0
     for k, name in enumerate(("fwd", "dq", "dkdv")):
         t = buf[k, :3].astype(np.int64)
         valid = t[0] > 0
