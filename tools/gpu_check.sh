@@ -20,7 +20,7 @@ cat $OUT/bench.json
 R=$(pwd)
 cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$OUT/prof -o $TAG -- \
-  python3 $R/bench.py --steps 5 --warmup 2 --cpu-baseline off > $R/$OUT/prof_bench.json 2> $R/$OUT/prof.err \
+  python3 $R/bench.py --steps 5 --warmup 2 --cpu-baseline off --no-ref-arch > $R/$OUT/prof_bench.json 2> $R/$OUT/prof.err \
   || { tail -30 $R/$OUT/prof.err; exit 1; }
 cd $R
 KT=$(find $OUT/prof -name '*kernel_trace.csv' -print -quit)
