@@ -264,6 +264,8 @@ __device__ __forceinline__ void wgrad_tile_body(bf16* lds, int t, long M, int N,
 #pragma unroll
                 for (int b = 0; b < C::AK; ++b)
                     acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[a], fb[b], acc[a][b], 0, 0, 0);
+            // 256 x 256: one k-step's fragments live at a time (the 256 accumulators fill the AGPRs)
+            if constexpr (TN * TK > 256 * 128) __builtin_amdgcn_sched_barrier(0);
         }
     };
     // Register set s % D holds step s, LDS buffer s & 1.  The loop runs a multiple of lcm(D, 2) steps
@@ -362,7 +364,7 @@ struct WgGroup {
 };
 
 template <int TN, int TK, int NTH = NT, int D = 2>
-__global__ __launch_bounds__(NTH, NTH > NT ? 1 : 2) void wgrad_group(WgGroup g) {
+__global__ __launch_bounds__(NTH, NTH > NT || TN * TK > 256 * 128 ? 1 : 2) void wgrad_group(WgGroup g) {
     __shared__ __attribute__((aligned(16))) bf16 lds[2 * TileCfg<TN, TK, NTH>::BUF];
     const int lt = __builtin_amdgcn_readfirstlane((int)xcd_tile(blockIdx.x, gridDim.x));
     int i = 0;
@@ -630,7 +632,15 @@ extern "C" int csu_linear_wgrad_deferred(long M, int N, int K, const void* dy, c
 // >= 1024 tokens per chunk.  No occupancy target: the group fills the GPU.
 // slab bytes <= operand bytes * 2 / kSlabDiv (A/B at 512 B16: 8 -> 1231 img/s, 16 -> 1249, 32 -> 1255, 64 -> 1227)
 constexpr int kSlabDiv = 32;
+// WG_SQ256: 256 x 256 tiles (4 waves, one per SIMD, 256 accumulators per lane, one register prefetch
+// set: two spill) when N and K are both multiples of 256 -- 2/3 of the 256 x 128 tile's staged operand
+// bytes per output, but measured slower in the step (linear_wgrad 1533 vs 1419 us/step, 512 B16,
+// profiles/r07v_wgrad_sq256_ab.txt): one wave per SIMD does not keep enough loads in flight.  Off.
+#ifndef WG_SQ256
+#define WG_SQ256 0
+#endif
 static void group_plan(long M, int N, int K, int* tn, int* tk, int* chunks, long* rpc) {
+    const bool sq = WG_SQ256 && N % 256 == 0 && K % 256 == 0;
     const int t = (N % 256 == 0 && K % 128 == 0) ? 256 : (N % 128 == 0 && K % 128 == 0) ? 128 : 64;
     long c = (long)((double)M * (N + K) / ((double)kSlabDiv * N * K) + 0.5);
     const long maxc = M / 1024 > 0 ? M / 1024 : 1;
@@ -639,7 +649,7 @@ static void group_plan(long M, int N, int K, int* tn, int* tk, int* chunks, long
     long r = ((M + c - 1) / c + TM - 1) / TM * TM;
     c = (M + r - 1) / r;
     *tn = t;
-    *tk = t == 256 ? 128 : t;
+    *tk = sq ? 256 : t == 256 ? 128 : t;
     *chunks = (int)c;
     *rpc = r;
 }
@@ -659,14 +669,15 @@ extern "C" size_t csu_linear_wgrad_group_plan(long M, int N, int K, int* tn, int
 extern "C" int csu_linear_wgrad_group(const csu_wgrad_group_item* items, int count, void* stream) {
     if (count < 0 || (count && !items)) return fail(CSU_E_ARG, "linear_wgrad_group: bad args");
     hipStream_t st = as_stream(stream);
-    for (int pass = 0; pass < 3; ++pass) {   // 256-tile items, then 128-tile, then 64-tile items
-        const int T = pass == 0 ? 256 : pass == 1 ? 128 : 64;
+    for (int pass = 0; pass < 4; ++pass) {   // 256 x 256, 256 x 128, 128 x 128, then 64 x 64 items
+        const int T = pass <= 1 ? 256 : pass == 2 ? 128 : 64, TK = pass == 0 ? 256 : T == 256 ? 128 : T;
         WgGroup g;
         g.count = 0;
         g.b0[0] = 0;
         auto flush = [&]() -> int {
             if (!g.count) return 0;
-            if (T == 256) wgrad_group<256, 128, 2 * NT><<<(unsigned)g.b0[g.count], 2 * NT, 0, st>>>(g);
+            if (TK == 256) wgrad_group<256, 256, NT, 1><<<(unsigned)g.b0[g.count], NT, 0, st>>>(g);
+            else if (T == 256) wgrad_group<256, 128, 2 * NT><<<(unsigned)g.b0[g.count], 2 * NT, 0, st>>>(g);
             else if (T == 128) wgrad_group<128, 128><<<(unsigned)g.b0[g.count], NT, 0, st>>>(g);
             else wgrad_group<64, 64><<<(unsigned)g.b0[g.count], NT, 0, st>>>(g);
             g.count = 0;
@@ -679,7 +690,7 @@ extern "C" int csu_linear_wgrad_group(const csu_wgrad_group_item* items, int cou
             int tn, tk, c;
             long r;
             group_plan(it.M, it.N, it.K, &tn, &tk, &c, &r);
-            if (tn != T) continue;
+            if (tn != T || tk != TK) continue;
             if (c > 1 && !it.slab) return fail(CSU_E_WORKSPACE, "linear_wgrad_group: item needs a slab workspace");
             const long tiles = (long)((it.N + tn - 1) / tn) * ((it.K + tk - 1) / tk);
             if (g.count == WGG_MAX || (long)g.b0[g.count] + tiles * c > (1L << 30))
