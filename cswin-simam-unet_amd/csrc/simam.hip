@@ -146,9 +146,10 @@ __global__ __launch_bounds__(NT) void simam_stats(Geo g, const T* __restrict__ x
 }
 
 // y = x * sigmoid(d^2 / s + 1/2); chunk-0 blocks also write stats[b][c] = (mu, s)
-template <typename T, typename TO>
+// CAST: also write xc = bf16(x) (the fork's second consumer, the Merge_Block conv) from the same pass
+template <typename T, typename TO, bool CAST = false>
 __global__ __launch_bounds__(NT) void simam_apply(Geo g, float lam, const T* __restrict__ x, const float* __restrict__ part,
-                                                  TO* __restrict__ y, float* __restrict__ stats) {
+                                                  TO* __restrict__ y, float* __restrict__ stats, bf16* __restrict__ xc = nullptr) {
     __shared__ float sm[16][QPR * 8];
     __shared__ float sm2[QPR][8];
     const int b = blockIdx.z, ch = blockIdx.x;
@@ -183,6 +184,7 @@ __global__ __launch_bounds__(NT) void simam_apply(Geo g, float lam, const T* __r
             o[k] = v[k] * sigm(d * d * rs[k] + 0.5f);
         }
         store4(y + off + (size_t)t * g.C, o);
+        if constexpr (CAST) store4(xc + off + (size_t)t * g.C, v);
     };
     int t = t0 + tl;
     for (; t + 3 * TPP < t1; t += 4 * TPP) {
@@ -258,10 +260,13 @@ __global__ __launch_bounds__(NT) void simam_bwd_partial(Geo g, const T* __restri
     }
 }
 
-template <typename T, typename TG>
+// JOIN: dx = g2 + (the SimAM input gradient) with g2 (bf16) the fork's other gradient, and dxb =
+// bf16(dx) for the upstream GEMM backward -- grad_join's outputs, in the same pass
+template <typename T, typename TG, bool JOIN = false>
 __global__ __launch_bounds__(NT) void simam_bwd_apply(Geo g, const T* __restrict__ x, const TG* __restrict__ dy,
                                                       const float* __restrict__ stats, const float* __restrict__ part,
-                                                      T* __restrict__ dx) {
+                                                      T* __restrict__ dx, const bf16* __restrict__ g2 = nullptr,
+                                                      bf16* __restrict__ dxb = nullptr) {
     __shared__ float sm[16][QPR * 8];
     __shared__ float sm2[QPR][8];
     const int b = blockIdx.z, ch = blockIdx.x;
@@ -293,6 +298,13 @@ __global__ __launch_bounds__(NT) void simam_bwd_apply(Geo g, const T* __restrict
             const float sg = sigm(d * d * rs[k] + 0.5f);
             const float a = gv[k] * v[k] * sg * (1.f - sg);
             o[k] = gv[k] * sg + k1[k] * a * d - k1n[k] - k2[k] * d;
+        }
+        if constexpr (JOIN) {
+            float v2[4];
+            load4(g2 + off + (size_t)t * g.C, v2);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) o[k] += v2[k];
+            store4(dxb + off + (size_t)t * g.C, o);
         }
         store4(dx + off + (size_t)t * g.C, o);
     };
@@ -361,6 +373,42 @@ extern "C" int csu_simam_fwd(int B, int L, int C, float lam, int xdtype, const v
     hipStream_t st = as_stream(stream);
     if (xdtype == CSU_BF16) return fwd_typed<bf16>(B, g, lam, (const bf16*)x, ydtype, y, stats, (float*)workspace, st);
     return fwd_typed<float>(B, g, lam, (const float*)x, ydtype, y, stats, (float*)workspace, st);
+}
+
+extern "C" int csu_simam_fwd_fork(int B, int L, int C, float lam, const float* x, void* y_, void* xc_, float* stats,
+                                  void* workspace, size_t ws_bytes, void* stream) {
+    bf16* y = (bf16*)y_;
+    bf16* xc = (bf16*)xc_;
+    if (B < 1 || L < 2 || C < 4 || C % 4 || !x || !y || !xc || !stats)
+        return fail(CSU_E_ARG, "simam_fwd_fork: bad args (need L >= 2, C a multiple of 4)");
+    if (!workspace || ws_bytes < csu_simam_workspace(B, L, C)) return fail(CSU_E_WORKSPACE, "simam_fwd_fork: workspace");
+    const Geo g = geo(B, L, C);
+    hipStream_t st = as_stream(stream);
+    float* part = (float*)workspace;
+    simam_stats<float><<<grid_of(B, g), NT, 0, st>>>(g, x, part);
+    simam_apply<float, bf16, true><<<grid_of(B, g), NT, 0, st>>>(g, lam, x, part, y, stats, xc);
+    return check_launch("simam_fwd_fork");
+}
+
+extern "C" int csu_simam_bwd_join(int B, int L, int C, const float* x, const float* stats, int gdtype, const void* dy,
+                                  const void* g2_, float* dx, void* dxb_, void* workspace, size_t ws_bytes, void* stream) {
+    const bf16* g2 = (const bf16*)g2_;
+    bf16* dxb = (bf16*)dxb_;
+    if (B < 1 || L < 2 || C < 4 || C % 4 || !x || !stats || !dy || !g2 || !dx || !dxb)
+        return fail(CSU_E_ARG, "simam_bwd_join: bad args");
+    if (!dt_ok(gdtype)) return fail(CSU_E_ARG, "simam_bwd_join: bad dtype");
+    if (!workspace || ws_bytes < csu_simam_workspace(B, L, C)) return fail(CSU_E_WORKSPACE, "simam_bwd_join: workspace");
+    const Geo g = geo(B, L, C);
+    hipStream_t st = as_stream(stream);
+    float* part = (float*)workspace;
+    if (gdtype == CSU_BF16) {
+        simam_bwd_partial<float, bf16><<<grid_of(B, g), NT, 0, st>>>(g, x, (const bf16*)dy, stats, part);
+        simam_bwd_apply<float, bf16, true><<<grid_of(B, g), NT, 0, st>>>(g, x, (const bf16*)dy, stats, part, dx, g2, dxb);
+    } else {
+        simam_bwd_partial<float, float><<<grid_of(B, g), NT, 0, st>>>(g, x, (const float*)dy, stats, part);
+        simam_bwd_apply<float, float, true><<<grid_of(B, g), NT, 0, st>>>(g, x, (const float*)dy, stats, part, dx, g2, dxb);
+    }
+    return check_launch("simam_bwd_join");
 }
 
 extern "C" int csu_simam_bwd(int B, int L, int C, int xdtype, const void* x, const float* stats, int gdtype,

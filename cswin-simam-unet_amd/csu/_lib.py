@@ -104,6 +104,10 @@ _SIGS = {
                                      c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
     "csu_simam_bwd": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, c_void_p, c_void_p, ctypes.c_int,
                                      c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "csu_simam_fwd_fork": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, c_float, c_void_p, c_void_p, c_void_p,
+                                          c_void_p, c_void_p, c_size_t, c_void_p]),
+    "csu_simam_bwd_join": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, c_void_p, c_void_p, ctypes.c_int,
+                                          c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
     "csu_carafe_fwd": (ctypes.c_int, [ctypes.c_int] * 6 + [c_void_p] * 5),
     "csu_carafe_bwd": (ctypes.c_int, [ctypes.c_int] * 6 + [c_void_p] * 6),
     "csu_carafe_head_fwd": (ctypes.c_int, [ctypes.c_int] * 6 + [c_void_p] * 7),

@@ -449,13 +449,13 @@ class CSWinTransformer(nn.Module):
     def _share_skip(self, x):
         """(merge input, decoder skip in bf16 or None) for an encoder stage output.  bf16 autocast
         on the device: without SimAM one shared bf16 copy feeds both the Merge_Block conv and the
-        split-weight concat_linear (ops.shared_cast / ops.concat_linear); with SimAM the gate writes
-        the bf16 skip for concat_linear in its own pass (no cat, no cast); otherwise x twice
-        (reference form)."""
+        split-weight concat_linear (ops.shared_cast / ops.concat_linear); with SimAM the gate's passes
+        write both the bf16 copy for the conv and the gated bf16 skip (simam_fork: no cat, no cast,
+        one joined backward pass); otherwise x twice (reference form)."""
         if x.is_cuda and torch.is_autocast_enabled("cuda") \
                 and torch.get_autocast_dtype("cuda") == torch.bfloat16 and x.dtype == torch.float32:
             if self.simam is not None:
-                return x, self.simam(x, out_dtype=torch.bfloat16)
+                return self.simam.fork(x)
             return ops.shared_cast(x, torch.bfloat16)
         return x, None
 

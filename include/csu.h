@@ -167,6 +167,15 @@ int csu_simam_fwd(int B, int L, int C, float lambda, int xdtype, const void* x, 
 /* dx (xdtype) from dy (gdtype) */
 int csu_simam_bwd(int B, int L, int C, int xdtype, const void* x, const float* stats, int gdtype, const void* dy,
                   void* dx, void* workspace, size_t ws_bytes, void* stream);
+/* The skip fork of the CSWin-SimAM-UNet encoder (an fp32 stage output feeding the Merge_Block conv
+ * and, through SimAM, the decoder's concat_linear -- cswin:530-545 / 568-592 + the SimAM gate):
+ * y = bf16(SimAM(x)) and xc = bf16(x) from the same passes (no separate cast of x). */
+int csu_simam_fwd_fork(int B, int L, int C, float lambda, const float* x, void* y, void* xc, float* stats,
+                       void* workspace, size_t ws_bytes, void* stream);
+/* its backward: dx = g2 + (SimAM input gradient of dy), dxb = bf16(dx); g2 bf16 (the conv's input
+ * gradient), dy gdtype -- the autograd sum and both casts in the gate-gradient pass */
+int csu_simam_bwd_join(int B, int L, int C, const float* x, const float* stats, int gdtype, const void* dy,
+                       const void* g2, float* dx, void* dxb, void* workspace, size_t ws_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------------------
  * CARAFE content-aware reassembly (CARAFE/CARAFE4.forward cswin:401-437 / 450-486, from the

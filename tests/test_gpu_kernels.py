@@ -197,6 +197,36 @@ def test_simam_vs_formula(shape, dtype):
     assert_close(xb.grad, x64.grad, torch.bfloat16)
 
 
+@pytest.mark.parametrize("shape", [(2, 4096, 64), (3, 1024, 128), (2, 256, 256)])
+def test_simam_fork_vs_unfused(shape):
+    """simam_fork (the encoder skip fork with SimAM: bf16 x for the Merge_Block conv + the gated bf16
+    skip, one joined backward pass) equals the unfused form -- bf16 cast, simam(out_dtype=bf16),
+    autograd's sum of the two input gradients: outputs bit for bit, the fp32 gradient within a few
+    ulps, and its bf16 gradient copy is the cast of its fp32 gradient."""
+    from csu.simam import simam, simam_fork
+    d = dev()
+    g = torch.Generator(device=d).manual_seed(sum(shape))
+    x0 = torch.randn(*shape, device=d, generator=g) * 1.5 + 0.3
+    g1 = torch.randn(*shape, device=d, generator=g).bfloat16()
+    dy = torch.randn(*shape, device=d, generator=g).bfloat16()
+    x = x0.clone().requires_grad_(True)
+    xc, y = simam_fork(x)
+    assert xc.dtype == y.dtype == torch.bfloat16
+    captured = {}
+    def hook(gr):
+        captured["bf16"] = getattr(gr, "_csu_bf16", None)   # returns None: the gradient is unchanged
+    x.register_hook(hook)
+    torch.autograd.backward([xc, y], [g1, dy])
+    xr = x0.clone().requires_grad_(True)
+    xcr, yr = xr.to(torch.bfloat16), simam(xr, out_dtype=torch.bfloat16)
+    torch.autograd.backward([xcr, yr], [g1, dy])
+    assert torch.equal(xc, xcr) and torch.equal(y, yr)
+    # fp32 gradient: the same terms, one more add in the joined pass (FMA contraction may differ): ulps
+    err = float((x.grad - xr.grad).abs().max())
+    assert err <= 2 ** -20 * float(xr.grad.abs().max()), err
+    assert captured["bf16"] is not None and torch.equal(captured["bf16"], x.grad.bfloat16())
+
+
 def test_cpu_tensor_fails_loudly():
     from csu import ops
     from csu._lib import CsuError
