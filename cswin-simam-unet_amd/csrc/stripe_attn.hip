@@ -1831,12 +1831,15 @@ void bwd_fused(const csu_stripe_args& a, const bf16* qkv, const bf16* out, const
 // split factor of the whole-window kernels: workgroups per window-head, so that a launch has
 // about 1024 workgroups, each owning at least 128 query (key) rows -- one 32-row pass per wave
 // (512x512: 2 at stages 3/4; 1024x1024: 4 at stage 3 (N = 512), 8 at stage 4 (N = 1024))
+#ifndef ATTN_SPLIT_WGS
+#define ATTN_SPLIT_WGS 1024
+#endif
 int wsplit(const csu_stripe_args& a) {
     const int N = a.br[0].H_sp * a.br[0].W_sp;
     const int nwin = (a.reso / a.br[0].H_sp) * (a.reso / a.br[0].W_sp);
     const long wgs = (long)a.B * nwin * a.heads * a.nbranch;
     const int maxsp = (((N + 31) & ~31) + 127) / 128;
-    const long want = (1024 + wgs - 1) / wgs;
+    const long want = (ATTN_SPLIT_WGS + wgs - 1) / wgs;
     return (int)(want < maxsp ? want : maxsp);
 }
 

@@ -639,6 +639,10 @@ constexpr int kSlabDiv = 32;
 #ifndef WG_SQ256
 #define WG_SQ256 0
 #endif
+// WG_RECT: 128 x 64 / 64 x 128 tiles for the C = 64 Linears whose other side is a multiple of 128
+#ifndef WG_RECT
+#define WG_RECT 1
+#endif
 static void group_plan(long M, int N, int K, int* tn, int* tk, int* chunks, long* rpc) {
     const bool sq = WG_SQ256 && N % 256 == 0 && K % 256 == 0;
     const int t = (N % 256 == 0 && K % 128 == 0) ? 256 : (N % 128 == 0 && K % 128 == 0) ? 128 : 64;
@@ -650,6 +654,10 @@ static void group_plan(long M, int N, int K, int* tn, int* tk, int* chunks, long
     c = (M + r - 1) / r;
     *tn = t;
     *tk = sq ? 256 : t == 256 ? 128 : t;
+    if (WG_RECT && t == 64) {   // one 128-wide side where it divides: 3/4 of the 64 x 64 tile's staged bytes per output
+        if (N % 128 == 0) *tn = 128;
+        else if (K % 128 == 0) *tk = 128;
+    }
     *chunks = (int)c;
     *rpc = r;
 }
@@ -669,8 +677,9 @@ extern "C" size_t csu_linear_wgrad_group_plan(long M, int N, int K, int* tn, int
 extern "C" int csu_linear_wgrad_group(const csu_wgrad_group_item* items, int count, void* stream) {
     if (count < 0 || (count && !items)) return fail(CSU_E_ARG, "linear_wgrad_group: bad args");
     hipStream_t st = as_stream(stream);
-    for (int pass = 0; pass < 4; ++pass) {   // 256 x 256, 256 x 128, 128 x 128, then 64 x 64 items
-        const int T = pass <= 1 ? 256 : pass == 2 ? 128 : 64, TK = pass == 0 ? 256 : T == 256 ? 128 : T;
+    constexpr int kPass[6][2] = {{256, 256}, {256, 128}, {128, 128}, {128, 64}, {64, 128}, {64, 64}};
+    for (int pass = 0; pass < 6; ++pass) {   // one launch per tile shape present
+        const int T = kPass[pass][0], TK = kPass[pass][1];
         WgGroup g;
         g.count = 0;
         g.b0[0] = 0;
@@ -678,7 +687,9 @@ extern "C" int csu_linear_wgrad_group(const csu_wgrad_group_item* items, int cou
             if (!g.count) return 0;
             if (TK == 256) wgrad_group<256, 256, NT, 1><<<(unsigned)g.b0[g.count], NT, 0, st>>>(g);
             else if (T == 256) wgrad_group<256, 128, 2 * NT><<<(unsigned)g.b0[g.count], 2 * NT, 0, st>>>(g);
-            else if (T == 128) wgrad_group<128, 128><<<(unsigned)g.b0[g.count], NT, 0, st>>>(g);
+            else if (T == 128 && TK == 128) wgrad_group<128, 128><<<(unsigned)g.b0[g.count], NT, 0, st>>>(g);
+            else if (T == 128) wgrad_group<128, 64><<<(unsigned)g.b0[g.count], NT, 0, st>>>(g);
+            else if (TK == 128) wgrad_group<64, 128><<<(unsigned)g.b0[g.count], NT, 0, st>>>(g);
             else wgrad_group<64, 64><<<(unsigned)g.b0[g.count], NT, 0, st>>>(g);
             g.count = 0;
             return check_launch("linear_wgrad_group");
