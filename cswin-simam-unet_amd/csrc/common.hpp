@@ -201,6 +201,28 @@ __device__ __forceinline__ float half_erfc_as(float x, float& ex) {   // 0.5 erf
     ex = __builtin_amdgcn_exp2f(-0.72134752f * (x * x));
     return t * (0.1740121f + t * (-0.0479399f + t * 0.3739278f)) * ex;
 }
+// cross-lane sums on the VALU: DPP moves (quad_perm / row_half_mirror / row_ror) and the CDNA4 permlane
+// swaps (xsum16: rows 2i <-> 2i+1, xsum32: half-waves) -- no LDS round trip
+template <int CTRL>
+__device__ __forceinline__ float dppf(float x) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), CTRL, 0xF, 0xF, true));
+}
+__device__ __forceinline__ float sum8_dpp(float x) {   // sum over each aligned group of 8 lanes
+    x += dppf<0xB1>(x);    // quad_perm [1,0,3,2]
+    x += dppf<0x4E>(x);    // quad_perm [2,3,0,1]
+    return x + dppf<0x141>(x);   // row_half_mirror: lane i <- 7 - i of its 8-lane group
+}
+__device__ __forceinline__ float xsum16(float x) {   // x + x of lane ^ 16
+    const unsigned u = __builtin_bit_cast(unsigned, x);
+    const auto r = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+    return __builtin_bit_cast(float, (unsigned)r[0]) + __builtin_bit_cast(float, (unsigned)r[1]);
+}
+__device__ __forceinline__ float xsum32(float x) {   // x + x of lane ^ 32
+    const unsigned u = __builtin_bit_cast(unsigned, x);
+    const auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+    return __builtin_bit_cast(float, (unsigned)r[0]) + __builtin_bit_cast(float, (unsigned)r[1]);
+}
+
 __device__ __forceinline__ float gelu_fast(float x) {
     float ex;
     const float q = half_erfc_as(x, ex);

@@ -25,7 +25,19 @@
 namespace csu {
 namespace {
 
-enum { WS_PLAIN = 0, WS_RESID = 1, WS_LNBWD = 2 };
+enum { WS_PLAIN = 0, WS_RESID = 1, WS_LNBWD = 2, WS_RESID_LN = 3 };
+
+// WS_RESID_LN epilogue: y = res + x W^T + b (fp32, written as WS_RESID) is the residual stream that
+// CSWinBlock's norm2 normalises next (cswin:366-368): the workgroup holds all N = C features of its
+// tokens, so it also writes LayerNorm(y) (bf16) and the per-token mean / rstd for norm2's backward.
+struct WsLnF {
+    const float* gamma;   // (C)
+    const float* beta;    // (C)
+    float eps;
+    bf16* out;            // (M, C)
+    float* mean;          // (M)
+    float* rstd;          // (M)
+};
 
 // WS_LNBWD epilogue: the GEMM is the input gradient dh of a LayerNorm's output (the qkv Linear's
 // input, CSWinBlock norm1, cswin:357 / 337): instead of writing dh, the workgroup (64 tokens x all
@@ -64,7 +76,7 @@ template <int K, int N, int EPI, typename TOUT>
 __global__ __launch_bounds__(256, ws_wn(N) < 4 ? 2 : 1) void gemm_ws_kernel(long M, const bf16* __restrict__ X, int ldx,
                                                       const bf16* __restrict__ Wf, const float* __restrict__ bias,
                                                       const float* __restrict__ resid, TOUT* __restrict__ out,
-                                                      WsLn ln = WsLn{}) {
+                                                      WsLn ln = WsLn{}, WsLnF lnf = WsLnF{}) {
     constexpr int WN = ws_wn(N);                   // waves along N
     constexpr int NT = N / (32 * WN);              // 32-feature tiles per wave
     static_assert(NT * 32 * WN == N, "gemm_ws: N = 32 WN NT");
@@ -132,8 +144,20 @@ __global__ __launch_bounds__(256, ws_wn(N) < 4 ? 2 : 1) void gemm_ws_kernel(long
     constexpr bool BF = sizeof(TOUT) == 2;
     // epilogue loads of a tile are issued at the start of its last unit, BEFORE the next unit's
     // weight loads: vmcnt counts in issue order, so waiting for them then does not wait for the prefetch
+    constexpr bool RES = EPI == WS_RESID || EPI == WS_RESID_LN;
+    static_assert(EPI != WS_RESID_LN || !BF, "gemm_ws: the LayerNorm epilogue writes the fp32 residual stream");
     float bv[8], rv[8][4];
     f32x16 keep[EPI == WS_LNBWD ? NT : 1][2];
+    float yk[EPI == WS_RESID_LN ? NT : 1][8][4];   // y of the wave's tiles in the store layout (LayerNorm)
+    float lg[EPI == WS_RESID_LN ? NT : 1][4], lb[EPI == WS_RESID_LN ? NT : 1][4];
+    if constexpr (EPI == WS_RESID_LN) {   // gamma / beta of the lane's 4 features of each tile
+        const int cc = 4 * (lane & 7);
+#pragma unroll
+        for (int i = 0; i < NT; ++i) {
+            load4(lnf.gamma + 32 * (wn + WN * tile_of(i)) + cc, lg[i]);
+            load4(lnf.beta + 32 * (wn + WN * tile_of(i)) + cc, lb[i]);
+        }
+    }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
         const int c = u % CH;
@@ -146,7 +170,7 @@ __global__ __launch_bounds__(256, ws_wn(N) < 4 ? 2 : 1) void gemm_ws_kernel(long
             } else {
                 const int cc = 4 * (lane & 7);
                 buf_ld4(rs_b, (unsigned)(n0 + cc) * 4, bv);
-                if constexpr (EPI == WS_RESID) {
+                if constexpr (RES) {
                     const auto rs_res = buf_rsrc(resid + m0 * N, (M - m0) * N * 4);
 #pragma unroll
                     for (int q = 0; q < 8; ++q) buf_ld4(rs_res, (unsigned)((8 * q + (lane >> 3)) * N + n0 + cc) * 4, rv[q]);
@@ -218,7 +242,8 @@ __global__ __launch_bounds__(256, ws_wn(N) < 4 ? 2 : 1) void gemm_ws_kernel(long
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     v[e] += bv[e];
-                    if constexpr (EPI == WS_RESID) v[e] += rv[q][e];
+                    if constexpr (RES) v[e] += rv[q][e];
+                    if constexpr (EPI == WS_RESID_LN) yk[u / CH][q][e] = v[e];
                 }
                 buf_st4(rs_out, (unsigned)(row * N + n0 + cc) * 4, v);
             }
@@ -226,6 +251,59 @@ __global__ __launch_bounds__(256, ws_wn(N) < 4 ? 2 : 1) void gemm_ws_kernel(long
         a0 = f32x16{};
         a1 = f32x16{};
         __builtin_amdgcn_sched_barrier(0);
+    }
+    if constexpr (EPI == WS_RESID_LN) {
+        // lane: rows 8 q + (lane >> 3) of its 64-token panel, features cc..cc+3 of each of its tiles.
+        // Two passes over the registers (mean, then the centred sum of squares), each: the lane's
+        // sum, the 8 lanes of the row (DPP), the WN waves of the token group through LDS.
+        __shared__ float lnx[2][4][WS_BM];
+        const int rq = lane >> 3, g0 = (wave / WN) * WN;
+        float mu[8], rsd[8];
+#pragma unroll
+        for (int pass = 0; pass < 2; ++pass) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                float a = 0.f;
+#pragma unroll
+                for (int i = 0; i < NT; ++i)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const float d = pass ? yk[i][q][e] - mu[q] : yk[i][q][e];
+                        a = pass ? fmaf(d, d, a) : a + d;
+                    }
+                a = sum8_dpp(a);
+                if ((lane & 7) == 0) lnx[pass][wave][8 * q + rq] = a;
+            }
+            __syncthreads();
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                float t = 0.f;
+#pragma unroll
+                for (int j = 0; j < WN; ++j) t += lnx[pass][g0 + j][8 * q + rq];
+                if (pass) rsd[q] = rsqrtf(t * (1.f / N) + lnf.eps);
+                else mu[q] = t * (1.f / N);
+            }
+        }
+        const auto rs_ln = buf_rsrc(lnf.out + m0 * N, (M - m0) * N * 2);
+        const int cc = 4 * (lane & 7);
+#pragma unroll
+        for (int i = 0; i < NT; ++i) {
+            const int n0 = 32 * (wn + WN * tile_of(i));
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                float o[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) o[e] = (yk[i][q][e] - mu[q]) * rsd[q] * lg[i][e] + lb[i][e];
+                buf_st4bf(rs_ln, (unsigned)((8 * q + rq) * N + n0 + cc) * 2, o);
+            }
+        }
+        if (wn == 0 && (lane & 7) == 0) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                lnf.mean[m0 + 8 * q + rq] = mu[q];
+                lnf.rstd[m0 + 8 * q + rq] = rsd[q];
+            }
+        }
     }
     if constexpr (EPI == WS_LNBWD) {
         // lane (r, h) holds dh of tokens r (t = 0) and 32 + r (t = 1), features
@@ -347,8 +425,9 @@ __global__ __launch_bounds__(256, ws_wn(N) < 4 ? 2 : 1) void gemm_ws_kernel(long
 
 template <int K, int N, int EPI, typename TOUT>
 int ws_launch(long M, const bf16* X, int ldx, const bf16* Wf, const float* bias, const float* resid, void* out,
-              hipStream_t st, const WsLn& ln = WsLn{}) {
-    gemm_ws_kernel<K, N, EPI, TOUT><<<dim3((unsigned)(M / ws_tokens(N))), 256, 0, st>>>(M, X, ldx, Wf, bias, resid, (TOUT*)out, ln);
+              hipStream_t st, const WsLn& ln = WsLn{}, const WsLnF& lnf = WsLnF{}) {
+    gemm_ws_kernel<K, N, EPI, TOUT><<<dim3((unsigned)(M / ws_tokens(N))), 256, 0, st>>>(M, X, ldx, Wf, bias, resid, (TOUT*)out, ln,
+                                                                                       lnf);
     return check_launch("gemm_ws");
 }
 
@@ -381,6 +460,20 @@ int gemm_ws_run(long M, int N, int K, const bf16* X, int ldx, const bf16* Wf, co
     WS_SHAPES(WS_GO)
 #undef WS_GO
     return fail(CSU_E_ARG, "gemm_ws: shape not instantiated");
+}
+
+// the LayerNorm (norm2) epilogue: proj + residual, K = N = C
+int gemm_ws_ln_supported(long M, int N, int K) {
+    if (M < ws_tokens(N) || M % ws_tokens(N) || M > (1L << 30)) return 0;
+    return K == N && (N == 64 || N == 128 || N == 256);
+}
+
+int gemm_ws_ln_run(long M, int N, const bf16* X, int ldx, const bf16* Wf, const float* bias, const float* resid, float* out,
+                   const WsLnF& lnf, hipStream_t st) {
+    if (N == 64) return ws_launch<64, 64, WS_RESID_LN, float>(M, X, ldx, Wf, bias, resid, out, st, WsLn{}, lnf);
+    if (N == 128) return ws_launch<128, 128, WS_RESID_LN, float>(M, X, ldx, Wf, bias, resid, out, st, WsLn{}, lnf);
+    if (N == 256) return ws_launch<256, 256, WS_RESID_LN, float>(M, X, ldx, Wf, bias, resid, out, st, WsLn{}, lnf);
+    return fail(CSU_E_ARG, "gemm_ws_ln: shape not instantiated");
 }
 
 // the LayerNorm-backward epilogue: the qkv input gradients at C = 128 / 256
@@ -439,6 +532,19 @@ extern "C" int csu_gemm_ws_lnbwd(long M, int C, int K, const void* dy, const voi
     if (!gemm_ws_lnbwd_supported(M, C, K)) return fail(CSU_E_ARG, "gemm_ws_lnbwd: unsupported shape");
     const WsLn ln{x, gamma, mean, rstd, dres, dx, (bf16*)dx_bf16, part};
     return gemm_ws_lnbwd_run(M, C, K, (const bf16*)dy, (const bf16*)wt_frag, ln, as_stream(stream));
+}
+
+extern "C" int csu_gemm_ws_ln_supported(long M, int C, int K) { return gemm_ws_ln_supported(M, C, K); }
+
+extern "C" int csu_gemm_ws_ln(long M, int C, const void* x, int ldx, const void* w_frag, const float* bias,
+                              const float* resid, float* out, const float* gamma, const float* beta, float eps,
+                              void* ln_out, float* mean, float* rstd, void* stream) {
+    if (!x || !w_frag || !resid || !out || !gamma || !beta || !ln_out || !mean || !rstd)
+        return fail(CSU_E_ARG, "gemm_ws_ln: null pointer");
+    if (!gemm_ws_ln_supported(M, C, C)) return fail(CSU_E_ARG, "gemm_ws_ln: unsupported shape");
+    if (ldx < C || ldx % 8) return fail(CSU_E_ARG, "gemm_ws_ln: ldx must be >= C and a multiple of 8");
+    const WsLnF lnf{gamma, beta, eps, (bf16*)ln_out, mean, rstd};
+    return gemm_ws_ln_run(M, C, (const bf16*)x, ldx, (const bf16*)w_frag, bias, resid, out, lnf, as_stream(stream));
 }
 
 extern "C" int csu_frag_layout_batch(const csu_frag_item* items, int count, long total_chunks, void* stream) {

@@ -1392,28 +1392,6 @@ __device__ __forceinline__ bf16x8 tr_frag16(const bf16* img, int kb, int cb, int
     return out;
 }
 
-// cross-lane sums on the VALU: DPP moves (quad_perm / row_half_mirror / row_ror) and the CDNA4 permlane
-// swaps (xsum16: rows 2i <-> 2i+1, xsum32: half-waves) -- no LDS round trip
-template <int CTRL>
-__device__ __forceinline__ float dppf(float x) {
-    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), CTRL, 0xF, 0xF, true));
-}
-__device__ __forceinline__ float sum8_dpp(float x) {   // sum over each aligned group of 8 lanes
-    x += dppf<0xB1>(x);    // quad_perm [1,0,3,2]
-    x += dppf<0x4E>(x);    // quad_perm [2,3,0,1]
-    return x + dppf<0x141>(x);   // row_half_mirror: lane i <- 7 - i of its 8-lane group
-}
-__device__ __forceinline__ float xsum16(float x) {   // x + x of lane ^ 16
-    const unsigned u = __builtin_bit_cast(unsigned, x);
-    const auto r = __builtin_amdgcn_permlane16_swap(u, u, false, false);
-    return __builtin_bit_cast(float, (unsigned)r[0]) + __builtin_bit_cast(float, (unsigned)r[1]);
-}
-__device__ __forceinline__ float xsum32(float x) {   // x + x of lane ^ 32
-    const unsigned u = __builtin_bit_cast(unsigned, x);
-    const auto r = __builtin_amdgcn_permlane32_swap(u, u, false, false);
-    return __builtin_bit_cast(float, (unsigned)r[0]) + __builtin_bit_cast(float, (unsigned)r[1]);
-}
-
 // the fused backward's four window images in ONE pass (one memory latency instead of two): Q, K and
 // dO swizzled (swz), V into a PLAIN [row][32] image; rows [N, npad) zero.  All loads of the pass are
 // issued before the first LDS store (16 IT VGPRs of staged data).

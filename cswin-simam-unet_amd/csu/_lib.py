@@ -145,6 +145,9 @@ _SIGS = {
     "csu_gemm_ws_supported": (ctypes.c_int, [ctypes.c_long, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     "csu_gemm_ws": (ctypes.c_int, [ctypes.c_long, ctypes.c_int, ctypes.c_int, c_void_p, ctypes.c_int, c_void_p, c_void_p,
                                    c_void_p, ctypes.c_int, c_void_p, c_void_p]),
+    "csu_gemm_ws_ln_supported": (ctypes.c_int, [ctypes.c_long, ctypes.c_int, ctypes.c_int]),
+    "csu_gemm_ws_ln": (ctypes.c_int, [ctypes.c_long, ctypes.c_int, c_void_p, ctypes.c_int, c_void_p, c_void_p, c_void_p,
+                                      c_void_p, c_void_p, c_void_p, c_float, c_void_p, c_void_p, c_void_p, c_void_p]),
     "csu_gemm_ws_lnbwd_supported": (ctypes.c_int, [ctypes.c_long, ctypes.c_int, ctypes.c_int]),
     "csu_gemm_ws_lnbwd": (ctypes.c_int, [ctypes.c_long, ctypes.c_int, ctypes.c_int] + [c_void_p] * 11),
     "csu_frag_layout_batch": (ctypes.c_int, [c_void_p, ctypes.c_int, ctypes.c_long, c_void_p]),

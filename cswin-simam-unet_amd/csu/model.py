@@ -249,7 +249,9 @@ class CSWinBlock(nn.Module):
         fused = ops.fused_ok(x, C, self.mlp.fc1.out_features)
         if fused and rs1 is None:
             # bf16 fused path: proj + residual in one GEMM
-            x = ops.linear_residual(xa, att, self.proj.weight, self.proj.bias)
+            # ... and norm2 in its epilogue where the weight-streaming GEMM has the shape
+            x = ops.linear_residual(xa, att, self.proj.weight, self.proj.bias,
+                                    ln_next=(n2.weight, n2.bias, n2.eps) if cd == torch.bfloat16 else None)
         else:
             y = ops.linear(att, self.proj.weight, self.proj.bias)
             x = ops.dropout(y, 0.0, 0, row_scale=rs1, rows_per_sample=L, residual=xa) if rs1 is not None else xa + y

@@ -3,6 +3,7 @@ kernel; there is no CPU or eager-PyTorch fallback (CPU tensors raise ``CsuError`
 from __future__ import annotations
 
 import ctypes
+import os
 import weakref
 from typing import List, Optional, Sequence, Tuple
 
@@ -1428,13 +1429,27 @@ class _LinearResidualFn(torch.autograd.Function):
     """res + x @ W^T + b in one csu_gemm (fp32 out): proj + residual of CSWinBlock (cswin:366-367)."""
 
     @staticmethod
-    def forward(ctx, res, x, weight, bias, wc):
+    def forward(ctx, res, x, weight, bias, wc, ln=None):
         res2 = res.float().contiguous().view(-1, res.shape[-1])
         x2 = x.reshape(-1, x.shape[-1]).contiguous()
         M, K, N = x2.shape[0], x2.shape[1], wc.shape[0]
         bf = bias.detach().float().contiguous()
         wf = _ACTIVE_CACHE.get_frag(weight) if _ACTIVE_CACHE is not None else None
-        if wf is not None and _ws_ok(M, N, K, torch.float32, resid=True):
+        if (ln is not None and wf is not None and USE_GEMM_WS and K == N
+                and lib().csu_gemm_ws_ln_supported(M, N, K)):
+            # + norm2 in the epilogue (csu_gemm_ws_ln), handed to the block's layer_norm_fork
+            gam, bet, eps = ln
+            gf, bf_ = gam.detach().float().contiguous(), bet.detach().float().contiguous()
+            y = torch.empty(M, N, dtype=torch.float32, device=x2.device)
+            h = torch.empty(M, N, dtype=torch.bfloat16, device=x2.device)
+            mean = torch.empty(M, dtype=torch.float32, device=x2.device)
+            rstd = torch.empty(M, dtype=torch.float32, device=x2.device)
+            _launch("gemm", lambda: lib().csu_gemm_ws_ln(M, N, ptr(x2), K, ptr(wf), ptr(bf), ptr(res2), ptr(y), ptr(gf),
+                                                         ptr(bf_), float(eps), ptr(h), ptr(mean), ptr(rstd),
+                                                         stream_ptr(x2.device)),
+                    2 * M * N * K + 8 * M * N, M * K * 2 + N * K * 2 + M * N * (4 + 4 + 2) + 8 * M, tag=f"{M}x{N}x{K}rbln:ws")
+            _LN_STASH[0] = (gam, bet, float(eps), h, mean, rstd)
+        elif wf is not None and _ws_ok(M, N, K, torch.float32, resid=True):
             y = gemm_ws(x2, wf, N, torch.float32, bias=bf, resid=res2)
         else:
             y = gemm(x2, wc, False, torch.float32, bias=bf, resid=res2)
@@ -1456,7 +1471,7 @@ class _LinearResidualFn(torch.autograd.Function):
         else:
             dx = gemm(dyb, wt, False, torch.bfloat16).view(xshape)
         dw, db = wgrad_maybe_side(dyb, x2, wdt, bdt, params=ctx.params)
-        return dy.to(rdt), dx, dw.to(wdt), db.to(bdt), None
+        return dy.to(rdt), dx, dw.to(wdt), db.to(bdt), None, None
 
 
 class MlpDrop:
@@ -1544,9 +1559,22 @@ def fused_ok(x: torch.Tensor, *dims) -> bool:
             and torch.get_autocast_dtype("cuda") == torch.bfloat16 and _gemm_ok(*dims))
 
 
-def linear_residual(res, x, weight, bias):
+FUSE_PROJ_LN = os.environ.get("CSU_FUSE_PROJ_LN", "1") != "0"   # norm2 in the proj + residual epilogue (csu_gemm_ws_ln)
+
+
+def linear_residual(res, x, weight, bias, ln_next=None):
+    """res + x @ W^T + b (fp32).  ``ln_next`` ((weight, bias, eps) of the LayerNorm that reads the
+    result, CSWinBlock's norm2): computed in the same launch where gemm_ws has the shape and attached
+    to the output for layer_norm_fork (``_csu_ln``)."""
+    ln = ln_next if (FUSE_PROJ_LN and ln_next is not None and ln_next[0].dtype == torch.float32
+                     and ln_next[0].numel() == weight.shape[0]) else None
+    _LN_STASH[0] = None
     with torch.autocast("cuda", enabled=False):
-        return _LinearResidualFn.apply(res, x, weight, bias, _weight_bf16(weight))
+        out = _LinearResidualFn.apply(res, x, weight, bias, _weight_bf16(weight), ln)
+    if ln is not None and _LN_STASH[0] is not None:
+        out._csu_ln = _LN_STASH[0]
+        _LN_STASH[0] = None
+    return out
 
 
 def _mlp_desc(drop: Optional[MlpDrop], rpi: int):

@@ -323,6 +323,15 @@ typedef struct {
 } csu_gemm_desc;
 int csu_gemm_ex(const csu_gemm_desc* d, void* stream);
 
+/* The proj Linear + residual of CSWinBlock (cswin:366-367, K = N = C in {64, 128, 256}) with the
+ * block's norm2 LayerNorm (cswin:368 -> Mlp input) in the epilogue: out = resid + x W^T + bias (fp32,
+ * as csu_gemm_ws with resid) and ln_out = bf16(LayerNorm(out; gamma, beta, eps)) + the per-token mean /
+ * rstd (fp32) for its backward.  M % (64 or 128) == 0 (csu_gemm_ws_ln_supported). */
+int csu_gemm_ws_ln_supported(long M, int C, int K);
+int csu_gemm_ws_ln(long M, int C, const void* x, int ldx, const void* w_frag, const float* bias, const float* resid,
+                   float* out, const float* gamma, const float* beta, float eps, void* ln_out, float* mean, float* rstd,
+                   void* stream);
+
 /* ---------------------------------------------------------------------------------------
  * Weight-streaming token GEMM (csrc/gemm_ws.hip): out (M, N) = x (M, K) @ W^T (+ bias) (+ resid),
  * for the CSWinBlock qkv / proj Linears (cswin:337, 366) and their input gradients at C = 128 / 256.

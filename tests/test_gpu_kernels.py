@@ -1380,6 +1380,87 @@ def test_gemm_ws_vs_fp64(M, N, K, mode):
             ops.gemm_ws(x[:M - 64], _frag_ref(w).contiguous(), N, odt)   # two token groups: M % 128 != 0
 
 
+@pytest.mark.parametrize("M,C", [(16384, 256), (65536, 128), (262144, 64), (384, 64), (1024, 128)])
+def test_gemm_ws_ln_vs_fp64(M, C):
+    """csu_gemm_ws_ln (proj + residual with norm2 in the epilogue, cswin:366-368): the fp32 output
+    equals csu_gemm_ws's residual epilogue bit for bit; the LayerNorm output / mean / rstd match an
+    fp64 LayerNorm of that output to bf16 / fp32 rounding."""
+    from csu import ops
+    from csu._lib import lib, ptr, stream_ptr
+    d = dev()
+    g = torch.Generator(device=d).manual_seed(M + C)
+    x = torch.randn(M, C, device=d, generator=g).bfloat16()
+    w = (torch.randn(C, C, device=d, generator=g) / C ** 0.5).bfloat16()
+    bias = torch.randn(C, device=d, generator=g)
+    res = torch.randn(M, C, device=d, generator=g) * 2 + 0.5
+    gam = torch.randn(C, device=d, generator=g) * 0.5 + 1
+    bet = torch.randn(C, device=d, generator=g) * 0.1
+    wf = _frag_ref(w).contiguous()
+    ref_y = ops.gemm_ws(x, wf, C, torch.float32, bias=bias, resid=res)
+    assert lib().csu_gemm_ws_ln_supported(M, C, C)
+    y = torch.empty(M, C, device=d)
+    h = torch.empty(M, C, device=d, dtype=torch.bfloat16)
+    mean = torch.empty(M, device=d)
+    rstd = torch.empty(M, device=d)
+    rc = lib().csu_gemm_ws_ln(M, C, ptr(x), C, ptr(wf), ptr(bias), ptr(res), ptr(y), ptr(gam), ptr(bet), 1e-5, ptr(h),
+                              ptr(mean), ptr(rstd), stream_ptr(x.device))
+    torch.cuda.synchronize()
+    assert rc == 0
+    assert torch.equal(y, ref_y)
+    y64 = y.double()
+    mu = y64.mean(-1)
+    var = y64.var(-1, unbiased=False)
+    h64 = (y64 - mu[:, None]) / torch.sqrt(var[:, None] + 1e-5) * gam.double() + bet.double()
+    assert float((mean.double() - mu).abs().max()) <= 1e-6 * float(y64.abs().max())
+    assert float((rstd.double() / torch.rsqrt(var + 1e-5) - 1).abs().max()) <= 1e-5
+    assert float((h.double() - h64).abs().max()) <= 2 ** -8 * float(h64.abs().max())
+    assert not lib().csu_gemm_ws_ln_supported(M - 32, C, C)
+
+
+def test_linear_residual_ln_next_matches_unfused(monkeypatch):
+    """proj + residual with norm2 fused (ops.linear_residual(ln_next=...)) feeding layer_norm_fork:
+    the same forward values (bf16 rounding) and gradients (fp32 sums) as the unfused launch pair."""
+    from csu import ops
+    d = dev()
+    g = torch.Generator(device=d).manual_seed(5)
+    B, L, C = 2, 1024, 128
+    res0 = torch.randn(B, L, C, device=d, generator=g)
+    x0 = torch.randn(B, L, C, device=d, generator=g).bfloat16()
+    lin = torch.nn.Linear(C, C).to(d)
+    ln = torch.nn.LayerNorm(C).to(d)
+    with torch.no_grad():
+        ln.weight.uniform_(0.5, 1.5)
+        ln.bias.uniform_(-0.2, 0.2)
+    cache = ops.CastCache()
+    cache.refresh([lin.weight], torch.bfloat16)
+    cache.refresh_frag()
+    assert cache.get_frag(lin.weight) is not None
+    outs = {}
+    try:
+        ops.set_cast_cache(cache)
+        for fused in (False, True):
+            monkeypatch.setattr(ops, "FUSE_PROJ_LN", fused)
+            for p in (*lin.parameters(), *ln.parameters()):
+                p.grad = None
+            res, x = res0.clone().requires_grad_(True), x0.clone().requires_grad_(True)
+            y = ops.linear_residual(res, x, lin.weight, lin.bias, ln_next=(ln.weight, ln.bias, ln.eps))
+            assert hasattr(y, "_csu_ln") == fused
+            yb, h = ops.layer_norm_fork(y, ln.weight, ln.bias, ln.eps, torch.bfloat16)
+            loss = (h.float() * torch.linspace(-1, 1, C, device=d)).sum() + (yb.float() ** 2).sum() * 1e-3
+            loss.backward()
+            torch.cuda.synchronize()
+            grads = [res.grad, x.grad, lin.weight.grad, lin.bias.grad, ln.weight.grad, ln.bias.grad]
+            outs[fused] = (yb.detach(), h.detach(), [gr.detach().clone() for gr in grads])
+    finally:
+        ops.set_cast_cache(None)
+    (y0, h0, g0), (y1, h1, g1) = outs[False], outs[True]
+    assert torch.equal(y0, y1)
+    assert float((h0.float() - h1.float()).abs().max()) <= 2 ** -7 * float(h0.float().abs().max())
+    for a, b in zip(g0, g1):
+        err = float((a.double() - b.double()).norm() / b.double().norm().clamp_min(1e-30))
+        assert err < 2e-2, err
+
+
 @pytest.mark.parametrize("C", [64, 128, 256])
 @pytest.mark.parametrize("drop", [False, True])
 def test_mlp_fwd_ln_next(C, drop):
