@@ -146,7 +146,7 @@ __device__ __forceinline__ void fwd_epilogue(f32x16* acc, __amdgpu_buffer_rsrc_t
 // features (U HT + q) 32 + 8 g + 4 h + e in yv[q][4 g + e]; the two feature halves of a token meet by
 // a shuffle (h) and the LDS exchange lnx with the partner wave (U ^ 1); both waves take part in the
 // two barriers.  Writes the bf16 LN output and (wave U = 0) mean / rstd.
-template <int C, int U, int A0 = U * (C / 64)>
+template <int C, int U, int NWV = 4, int A0 = U * (C / 64)>
 __device__ __forceinline__ void ln_epilogue(const f32x16* yv, float* lnx, int wave, int r, int h, int tok, bool ok,
                                             const float* __restrict__ gam, const float* __restrict__ bet, float eps,
                                             __amdgpu_buffer_rsrc_t rs_ln, __amdgpu_buffer_rsrc_t rs_mean,
@@ -156,7 +156,8 @@ __device__ __forceinline__ void ln_epilogue(const f32x16* yv, float* lnx, int wa
     // through the exchange): one barrier instead of two, no cancellation for a large mean
     float sh = yv[A0][0];
     sh = __shfl(sh, r, 64);                         // token r's shift from lane (r, 0) of this wave
-    if (h == 0) lnx[256 + wave * 32 + r] = sh;
+    constexpr int SEC = 32 * NWV;                   // lnx: [sums | squares | shifts] x NWV waves x 32 tokens
+    if (h == 0) lnx[2 * SEC + wave * 32 + r] = sh;
     float s = 0.f, q2 = 0.f;
 #pragma unroll
     for (int q = 0; q < HT; ++q)
@@ -170,14 +171,14 @@ __device__ __forceinline__ void ln_epilogue(const f32x16* yv, float* lnx, int wa
     q2 += __shfl_xor(q2, 32, 64);
     if (h == 0) {
         lnx[wave * 32 + r] = s;
-        lnx[128 + wave * 32 + r] = q2;
+        lnx[SEC + wave * 32 + r] = q2;
     }
     lds_sync();
     const int pw = (wave ^ 1) * 32 + r;
-    const float shp = lnx[256 + pw];                 // the partner wave's shift for this token
+    const float shp = lnx[2 * SEC + pw];             // the partner wave's shift for this token
     const float dsh = shp - sh;
     // partner moments re-centred on this wave's shift: sum(d + dsh), sum((d + dsh)^2)
-    const float sp = lnx[pw], qp = lnx[128 + pw];
+    const float sp = lnx[pw], qp = lnx[SEC + pw];
     constexpr float HN = C / 2;
     const float S = s + sp + HN * dsh;
     const float Q = q2 + qp + 2.f * dsh * sp + HN * dsh * dsh;
@@ -243,8 +244,11 @@ template <int V> using iconst = std::integral_constant<int, V>;
 // Forward.  Rings: W1 chunks in 2 stages, W2 chunks in 2 stages.  Step j (after one barrier):
 // DMA W1(j+2), W2(j+1); GEMM1(j+1) on the MFMA pipe while GELU(j) runs on the VALU; GEMM2(j).
 // DROP: hidden / output dropout and DropPath (MlpDrop)
-template <int C, bool DROP, bool LN = false>
-__global__ __launch_bounds__(MT) void mlp_fwd_kernel(long M, const bf16* __restrict__ X, const bf16* __restrict__ W1,
+// TEAMS = 2 (C <= 128): two 4-wave teams, one 64-token panel each, share ONE weight ring -- every
+// streamed weight chunk feeds 128 tokens (half the L2 -> LDS weight bytes per token: the per-CU fill
+// rate bounds these kernels)
+template <int C, bool DROP, bool LN = false, int TEAMS = 1>
+__global__ __launch_bounds__(MT * TEAMS) void mlp_fwd_kernel(long M, const bf16* __restrict__ X, const bf16* __restrict__ W1,
                                                      const float* __restrict__ b1, const bf16* __restrict__ W2,
                                                      const float* __restrict__ b2, const float* __restrict__ res,
                                                      float* __restrict__ out, MlpDrop dd, long rpi, MlpLn ln = MlpLn{}) {
@@ -252,19 +256,22 @@ __global__ __launch_bounds__(MT) void mlp_fwd_kernel(long M, const bf16* __restr
     constexpr int KS = C / 16;          // k-steps of GEMM1
     constexpr int TF = C / 32;          // 32-feature output tiles (all C, partial over the hidden half)
     constexpr int IMG = HC * C;         // bf16 per weight-chunk image (W1 [HC][C] or W2 [C][HC])
-    using D1 = Dma<HC, 2 * C>;
-    using D2 = Dma<C, 2 * HC>;
+    constexpr int NWV = 4 * TEAMS, NTH = MT * TEAMS;
+    static_assert(TEAMS == 1 || NWV * (C / 64) * 16 * 64 * 4 <= 4 * IMG * 2, "partial-sum exchange must fit the ring");
+    using D1 = Dma<HC, 2 * C, NWV>;
+    using D2 = Dma<C, 2 * HC, NWV>;
     __shared__ __attribute__((aligned(1024))) bf16 ring[4 * IMG];
     __shared__ __attribute__((aligned(16))) float b1s[4 * C];
     bf16* const w1r = ring;
     bf16* const w2r = ring + 2 * IMG;
 
-    const long m0 = (long)blockIdx.x * BM;
-    const long rows = M - m0;
+    const long mw = (long)blockIdx.x * BM * TEAMS;   // the workgroup's first token
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const long m0 = mw + BM * (wave >> 2);           // this wave's team's panel
+    const long rows = M - m0 > 0 ? M - m0 : 0;
     const int r = lane & 31, h = lane >> 5;
-    const int t = wave >> 1, u = wave & 1;
+    const int t = (wave & 3) >> 1, u = wave & 1;
     const int tok = 32 * t + r;
     const bool ok = tok < rows;
     const int hs = 32 * u;              // this wave's hidden features within a chunk
@@ -272,14 +279,14 @@ __global__ __launch_bounds__(MT) void mlp_fwd_kernel(long M, const bf16* __restr
     // image, a multiple of the panel), so the workgroups running together stream different weight
     // chunks (every panel reads the same 2 x 4C x C weights: without the rotation all CUs of an XCD
     // hit the same L2 lines at once) while a token's sum order does not depend on the batch split
-    const int j0 = kRot && rpi > 0 && rpi % BM == 0 ? (int)(((m0 % rpi) / BM) & (NCH - 1)) : 0;
+    const int j0 = kRot && rpi > 0 && rpi % BM == 0 ? (int)(((mw % rpi) / BM) & (NCH - 1)) : 0;
     auto chk = [&](int j) { return (j + j0) & (NCH - 1); };
-    for (int i = threadIdx.x; i < 4 * C; i += MT) b1s[i] = b1[i];
+    for (int i = threadIdx.x; i < 4 * C; i += NTH) b1s[i] = b1[i];
     // LN epilogue: gamma / beta staged in LDS here -- read in the epilogue from LDS, a global load there
     // would wait (vmcnt, issue order) for the completion of every output store before it
     __shared__ __attribute__((aligned(16))) float lngb[LN ? 2 * C : 4];
     if constexpr (LN)
-        for (int i = threadIdx.x; i < 2 * C; i += MT) lngb[i] = i < C ? ln.gamma[i] : ln.beta[i - C];
+        for (int i = threadIdx.x; i < 2 * C; i += NTH) lngb[i] = i < C ? ln.gamma[i] : ln.beta[i - C];
     bf16x8 xf[KS];
     load_bfrags<C>(buf_rsrc(X + m0 * C, rows * C * 2), tok, ok, h, xf);
 
@@ -359,17 +366,17 @@ __global__ __launch_bounds__(MT) void mlp_fwd_kernel(long M, const bf16* __restr
     const auto rs_res = buf_rsrc(res + m0 * C, rows * C * 4);
     const auto rs_out = buf_rsrc(out + m0 * C, rows * C * 4);
     if constexpr (LN) {
-        __shared__ float lnx[384];
+        __shared__ float lnx[3 * 32 * NWV];
         const auto rs_ln = buf_rsrc(ln.out + m0 * C, rows * C * 2);
         const auto rs_mean = buf_rsrc(ln.mean + m0, rows * 4), rs_rstd = buf_rsrc(ln.rstd + m0, rows * 4);
         if (u == 0) {
             exchange_half<C, 0>(acc, xch, wave, lane);
             fwd_epilogue<C, 0, DROP>(acc, rs_res, rs_out, b2, tok, ok, h, mg, dd, true);
-            ln_epilogue<C, 0>(acc, lnx, wave, r, h, tok, ok, lngb, lngb + C, ln.eps, rs_ln, rs_mean, rs_rstd);
+            ln_epilogue<C, 0, NWV>(acc, lnx, wave, r, h, tok, ok, lngb, lngb + C, ln.eps, rs_ln, rs_mean, rs_rstd);
         } else {
             exchange_half<C, 1>(acc, xch, wave, lane);
             fwd_epilogue<C, 1, DROP>(acc, rs_res, rs_out, b2, tok, ok, h, mg, dd, true);
-            ln_epilogue<C, 1>(acc, lnx, wave, r, h, tok, ok, lngb, lngb + C, ln.eps, rs_ln, rs_mean, rs_rstd);
+            ln_epilogue<C, 1, NWV>(acc, lnx, wave, r, h, tok, ok, lngb, lngb + C, ln.eps, rs_ln, rs_mean, rs_rstd);
         }
         return;
     }
@@ -680,24 +687,36 @@ int persist_grid(long M) {   // one workgroup (two panel streams) per CU, fewer 
     return (int)(pan < 2L * cus ? (pan + 1) / 2 : cus);
 }
 
+// teams per workgroup of the fused forward: 2 = two 64-token panels on one weight ring (half the
+// streamed weight bytes per token; C = 128: 228 VGPRs, two waves per SIMD).  Measured no faster in the
+// step (mlp_fwd 1176-1180 vs 1180-1182 us/step, profiles/r07zb_mlp_teams_ab.txt): the C = 128 forward
+// is bound by its per-chunk barrier -> GEMM1 -> GELU -> GEMM2 chain, not by weight bytes.  Off.
+#ifndef MLP_FWD_TEAMS
+#define MLP_FWD_TEAMS 1
+#endif
+#ifndef MLP_FWD_TEAMS64
+#define MLP_FWD_TEAMS64 1
+#endif
 template <int C>
 int fwd_launch(long M, const void* x, const void* w1, const float* b1, const void* w2, const float* b2, const float* res,
                float* out, const MlpDrop* d, long rpi, hipStream_t st, const MlpLn* ln = nullptr) {
-    const dim3 grid((unsigned)((M + BM - 1) / BM));
+    constexpr int T = C == 128 ? MLP_FWD_TEAMS : C == 64 ? MLP_FWD_TEAMS64 : 1;
+    const dim3 grid((unsigned)((M + BM * T - 1) / (BM * T)));
     if (ln) {
         if (d)
-            mlp_fwd_kernel<C, true, true><<<grid, MT, 0, st>>>(M, (const bf16*)x, (const bf16*)w1, b1, (const bf16*)w2, b2, res,
-                                                                out, *d, rpi, *ln);
+            mlp_fwd_kernel<C, true, true, T><<<grid, MT * T, 0, st>>>(M, (const bf16*)x, (const bf16*)w1, b1, (const bf16*)w2, b2,
+                                                                      res, out, *d, rpi, *ln);
         else
-            mlp_fwd_kernel<C, false, true><<<grid, MT, 0, st>>>(M, (const bf16*)x, (const bf16*)w1, b1, (const bf16*)w2, b2,
-                                                                 res, out, MlpDrop{}, rpi, *ln);
+            mlp_fwd_kernel<C, false, true, T><<<grid, MT * T, 0, st>>>(M, (const bf16*)x, (const bf16*)w1, b1, (const bf16*)w2,
+                                                                       b2, res, out, MlpDrop{}, rpi, *ln);
         return check_launch("mlp_fwd_ln");
     }
     if (d)
-        mlp_fwd_kernel<C, true><<<grid, MT, 0, st>>>(M, (const bf16*)x, (const bf16*)w1, b1, (const bf16*)w2, b2, res, out, *d, rpi);
+        mlp_fwd_kernel<C, true, false, T><<<grid, MT * T, 0, st>>>(M, (const bf16*)x, (const bf16*)w1, b1, (const bf16*)w2, b2, res,
+                                                                   out, *d, rpi);
     else
-        mlp_fwd_kernel<C, false><<<grid, MT, 0, st>>>(M, (const bf16*)x, (const bf16*)w1, b1, (const bf16*)w2, b2, res, out,
-                                                      MlpDrop{}, rpi);
+        mlp_fwd_kernel<C, false, false, T><<<grid, MT * T, 0, st>>>(M, (const bf16*)x, (const bf16*)w1, b1, (const bf16*)w2, b2,
+                                                                    res, out, MlpDrop{}, rpi);
     return check_launch("mlp_fwd");
 }
 
