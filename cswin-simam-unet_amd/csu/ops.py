@@ -2375,10 +2375,18 @@ def ln_linear_ws(x: torch.Tensor, ln: torch.nn.LayerNorm, lin: torch.nn.Linear):
         return _LnLinearWsFn.apply(x, ln.weight, ln.bias, lin.weight, lin.bias, ln.eps, wf, wtf, pre)
 
 
+# qkv in the fp8 weight format.  False: the bf16 weight-streaming GEMM on the EXACT dequantised e4m3
+# weight (the cast cache's shadow), norm1 in bf16 (fused into the previous block's Mlp epilogue where
+# it can be); True: e4m3 norm1 output x e4m3 weight on the fp8 MFMA (_LnLinearFp8Fn).  Measured at
+# 1024x1024 B4: fp8 qkv 422 us/step + its e4m3 LayerNorms 303 against ~320 (gemm_ws) + a share of 138
+# for bf16 (profiles/r07zd_*): the fp8 qkv made the fp8 format slower than bf16 (340.1 vs 345.8 img/s).
+FP8_QKV = os.environ.get("CSU_FP8_QKV", "0") != "0"
+
+
 def ln_linear_fp8(x: torch.Tensor, ln: torch.nn.LayerNorm, lin: torch.nn.Linear):
     """(x, lin(ln(x))) through _LnLinearFp8Fn when the fp8 weight format holds lin's weight (bf16
-    autocast forward of a model in set_weight_format('fp8_e4m3')), else None."""
-    if _ACTIVE_FP8 is None or not x.is_cuda:
+    autocast forward of a model in set_weight_format('fp8_e4m3')) and FP8_QKV, else None."""
+    if _ACTIVE_FP8 is None or not x.is_cuda or not FP8_QKV:
         return None
     got = _ACTIVE_FP8.lookup(lin.weight)
     N, K = lin.weight.shape

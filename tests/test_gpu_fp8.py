@@ -94,12 +94,17 @@ def test_quantizer_into_cast_cache_shadows():
     assert torch.equal(cache.shadow[-1], ps[-1].bfloat16())
 
 
-def test_fp8_weight_model_vs_oracle_with_quantized_weights(monkeypatch):
+@pytest.mark.parametrize("fp8_qkv", [False, True])
+def test_fp8_weight_model_vs_oracle_with_quantized_weights(monkeypatch, fp8_qkv):
+    """fp8_qkv (ops.FP8_QKV): True -- every qkv on the fp8 MFMA (e4m3 norm1 output, the oracle's
+    QKV_INPUT_QUANT); False (the default) -- qkv on the bf16 kernels with the exact dequantised weight
+    (no activation quantisation).  Every Mlp at C = 64 / 128 / 256 on the fp8 kernels either way."""
     from csu import ops
     from csu.data import ellipse_batch
     from csu.model import CSWinTransformer
     from csu.train import bce_loss
     d = dev()
+    monkeypatch.setattr(ops, "FP8_QKV", fp8_qkv)
     cfg = O.CSWinConfig(img_size=256, split_size=(1, 2, 8, 8))
     p = O.recipe_params(cfg, seed=0)
     m = CSWinTransformer(img_size=256, split_size=[1, 2, 8, 8]).to(d).set_weight_format("fp8_e4m3")
@@ -113,7 +118,8 @@ def test_fp8_weight_model_vs_oracle_with_quantized_weights(monkeypatch):
     monkeypatch.setattr(ops, "mlp_fp8", lambda *a, **k: (lambda r: mcalls.append(r is not None) or r)(real_mlp(*a, **k)))
     with torch.autocast("cuda", dtype=torch.bfloat16):
         y = m(x.to(d))
-    assert len(calls) == sum(1 for mod in m.modules() if type(mod).__name__ == "CSWinBlock")   # every qkv on fp8 MFMA
+    nblk = sum(1 for mod in m.modules() if type(mod).__name__ == "CSWinBlock")
+    assert len(calls) == (nblk if fp8_qkv else 0)   # every qkv on fp8 MFMA, or none
     # every Mlp at C = 64 / 128 / 256 on the fp8 fused kernels
     assert sum(mcalls) == sum(1 for mod in m.modules() if type(mod).__name__ == "Mlp" and mod.fc1.in_features in (64, 128, 256))
     assert sum(mcalls) > 10
@@ -129,7 +135,8 @@ def test_fp8_weight_model_vs_oracle_with_quantized_weights(monkeypatch):
             pq[k] = _ref_quant(p[k])[0]
     assert sum(1 for w in m._linear_weights() if id(w) in quant) > 100
     pref = {k: v.double().requires_grad_(True) for k, v in pq.items()}
-    monkeypatch.setattr(O, "QKV_INPUT_QUANT", _tok_quant)
+    if fp8_qkv:
+        monkeypatch.setattr(O, "QKV_INPUT_QUANT", _tok_quant)
     # the Mlps at C = 64 / 128 / 256 run the fp8 fused kernels: their MX roundings (oracle/fp8_ref.py)
     from oracle import fp8_ref as Q
 
