@@ -851,12 +851,13 @@ __device__ __forceinline__ f32x16 mfma8(const i32x8& a, const i32x8& b, const f3
 // Forward.  Rings as the bf16 forward: W1 chunk images [128][C B] in 2 stages, W2 chunk images [C][128 B]
 // in 2 stages; step j: DMA W1(j+2), W2(j+1); GEMM1(j+1) on the MFMA pipe while GELU + quantisation of
 // chunk j run on the VALU; GEMM2(j).
-template <int C, bool DROP>
+// LN: also the next block's norm1 on the output (ln_epilogue, as mlp_fwd_kernel's)
+template <int C, bool DROP, bool LN = false>
 __global__ __launch_bounds__(MT) void mlp_fp8_fwd_kernel(long M, const bf16* __restrict__ X, const uint8_t* __restrict__ W1,
                                                          const float* __restrict__ sw1, const float* __restrict__ b1,
                                                          const uint8_t* __restrict__ W2p, const float* __restrict__ sw2,
                                                          const float* __restrict__ b2, const float* __restrict__ res,
-                                                         float* __restrict__ out, MlpDrop dd, long rpi) {
+                                                         float* __restrict__ out, MlpDrop dd, long rpi, MlpLn ln = MlpLn{}) {
     constexpr int NCH = 4 * C / HC8;    // hidden chunks (even)
     constexpr int KS = C / 64;          // f8 k-steps of GEMM1
     constexpr int TF = C / 32;
@@ -887,6 +888,9 @@ __global__ __launch_bounds__(MT) void mlp_fp8_fwd_kernel(long M, const bf16* __r
         b1s[i] = b1[i];
         e1s[i] = e8m0_of(sw1[i]);
     }
+    __shared__ __attribute__((aligned(16))) float lngb[LN ? 2 * C : 4];   // gamma / beta (see mlp_fwd_kernel)
+    if constexpr (LN)
+        for (int i = threadIdx.x; i < 2 * C; i += MT) lngb[i] = i < C ? ln.gamma[i] : ln.beta[i - C];
     constexpr int TH = TF / 2;          // output tiles of one wave: features [u C/2, (u+1) C/2)
     int e2[TH];
 #pragma unroll
@@ -988,6 +992,19 @@ __global__ __launch_bounds__(MT) void mlp_fp8_fwd_kernel(long M, const bf16* __r
 
     const auto rs_res = buf_rsrc(res + m0 * C, rows * C * 4);
     const auto rs_out = buf_rsrc(out + m0 * C, rows * C * 4);
+    if constexpr (LN) {
+        __shared__ float lnx[384];
+        const auto rs_ln = buf_rsrc(ln.out + m0 * C, rows * C * 2);
+        const auto rs_mean = buf_rsrc(ln.mean + m0, rows * 4), rs_rstd = buf_rsrc(ln.rstd + m0, rows * 4);
+        if (u == 0) {
+            fwd_epilogue<C, 0, DROP, 0>(acc, rs_res, rs_out, b2, tok, ok, h, mg, dd, true);
+            ln_epilogue<C, 0, 4, 0>(acc, lnx, wave, r, h, tok, ok, lngb, lngb + C, ln.eps, rs_ln, rs_mean, rs_rstd);
+        } else {
+            fwd_epilogue<C, 1, DROP, 0>(acc, rs_res, rs_out, b2, tok, ok, h, mg, dd, true);
+            ln_epilogue<C, 1, 4, 0>(acc, lnx, wave, r, h, tok, ok, lngb, lngb + C, ln.eps, rs_ln, rs_mean, rs_rstd);
+        }
+        return;
+    }
     if (u == 0)
         fwd_epilogue<C, 0, DROP, 0>(acc, rs_res, rs_out, b2, tok, ok, h, mg, dd);
     else
@@ -996,8 +1013,18 @@ __global__ __launch_bounds__(MT) void mlp_fp8_fwd_kernel(long M, const bf16* __r
 
 template <int C>
 int fp8_fwd_launch(long M, const void* x, const void* w1, const float* sw1, const float* b1, const void* w2p, const float* sw2,
-                   const float* b2, const float* res, float* out, const MlpDrop* d, long rpi, hipStream_t st) {
+                   const float* b2, const float* res, float* out, const MlpDrop* d, long rpi, hipStream_t st,
+                   const MlpLn* ln = nullptr) {
     const dim3 grid((unsigned)((M + BM - 1) / BM));
+    if (ln) {
+        if (d)
+            mlp_fp8_fwd_kernel<C, true, true><<<grid, MT, 0, st>>>(M, (const bf16*)x, (const uint8_t*)w1, sw1, b1,
+                                                                   (const uint8_t*)w2p, sw2, b2, res, out, *d, rpi, *ln);
+        else
+            mlp_fp8_fwd_kernel<C, false, true><<<grid, MT, 0, st>>>(M, (const bf16*)x, (const uint8_t*)w1, sw1, b1,
+                                                                    (const uint8_t*)w2p, sw2, b2, res, out, MlpDrop{}, rpi, *ln);
+        return check_launch("mlp_fp8_fwd_ln");
+    }
     if (d)
         mlp_fp8_fwd_kernel<C, true><<<grid, MT, 0, st>>>(M, (const bf16*)x, (const uint8_t*)w1, sw1, b1, (const uint8_t*)w2p,
                                                          sw2, b2, res, out, *d, rpi);
@@ -1663,6 +1690,30 @@ extern "C" int csu_mlp_bwd(long M, int C, const void* x, const void* dy, const v
 }
 
 extern "C" int csu_mlp_fp8_supported(int C) { return C == 64 || C == 128 || C == 256; }
+
+extern "C" int csu_mlp_fp8_fwd_ln(long M, int C, const void* x, const void* w1q, const float* sw1, const float* b1,
+                                  const void* w2p, const float* sw2, const float* b2, const float* res, float* out,
+                                  const csu_mlp_dropout* d, const float* ln_gamma, const float* ln_beta, float ln_eps,
+                                  void* ln_out, float* ln_mean, float* ln_rstd, void* stream) {
+    if (M < 1 || !x || !w1q || !sw1 || !b1 || !w2p || !sw2 || !b2 || !res || !out || !ln_gamma || !ln_beta || !ln_out ||
+        !ln_mean || !ln_rstd)
+        return fail(CSU_E_ARG, "mlp_fp8_fwd_ln: bad arguments");
+    if (M * 4L * C * 2 > 0x7fffffffL) return fail(CSU_E_ARG, "mlp_fp8_fwd_ln: tensor exceeds 2 GB buffer range");
+    if (res == out) return fail(CSU_E_ARG, "mlp_fp8_fwd_ln: out must not alias res");
+    MlpDrop md{};
+    const int e = mlp_drop_of(d, md);
+    if (e < 0) return e;
+    const MlpDrop* dp = d && e == 0 ? &md : nullptr;
+    const long rpi = d ? (long)d->rows_per_sample : 0;
+    const MlpLn ln{ln_gamma, ln_beta, ln_eps, (bf16*)ln_out, ln_mean, ln_rstd};
+    const hipStream_t st = as_stream(stream);
+    switch (C) {
+        case 64: return fp8_fwd_launch<64>(M, x, w1q, sw1, b1, w2p, sw2, b2, res, out, dp, rpi, st, &ln);
+        case 128: return fp8_fwd_launch<128>(M, x, w1q, sw1, b1, w2p, sw2, b2, res, out, dp, rpi, st, &ln);
+        case 256: return fp8_fwd_launch<256>(M, x, w1q, sw1, b1, w2p, sw2, b2, res, out, dp, rpi, st, &ln);
+        default: return fail(CSU_E_UNSUPPORTED, "mlp_fp8_fwd_ln: C must be 64, 128 or 256");
+    }
+}
 
 extern "C" int csu_mlp_fp8_fwd(long M, int C, const void* x, const void* w1q, const float* sw1, const float* b1,
                                const void* w2p, const float* sw2, const float* b2, const float* res, float* out,

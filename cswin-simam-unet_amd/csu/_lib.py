@@ -167,6 +167,8 @@ _SIGS = {
     "csu_mlp_bwd_ex": (ctypes.c_int, [ctypes.c_long, ctypes.c_int] + [c_void_p] * 8 + [ctypes.POINTER(MlpDropout), ctypes.c_int,
                                                                                        c_void_p]),
     "csu_mlp_fp8_fwd": (ctypes.c_int, [ctypes.c_long, ctypes.c_int] + [c_void_p] * 9 + [ctypes.POINTER(MlpDropout), c_void_p]),
+    "csu_mlp_fp8_fwd_ln": (ctypes.c_int, [ctypes.c_long, ctypes.c_int] + [c_void_p] * 9 + [ctypes.POINTER(MlpDropout), c_void_p,
+                                          c_void_p, c_float, c_void_p, c_void_p, c_void_p, c_void_p]),
     "csu_mlp_fp8_bwd": (ctypes.c_int, [ctypes.c_long, ctypes.c_int] + [c_void_p] * 11 + [ctypes.POINTER(MlpDropout),
                                                                                          c_void_p]),
     "csu_mlp_supported": (ctypes.c_int, [ctypes.c_int]),

@@ -1680,7 +1680,7 @@ class _MlpFp8Fn(torch.autograd.Function):
     the fp8 backward kernel is slower than the bf16 one at those widths."""
 
     @staticmethod
-    def forward(ctx, res, x, w1, b1, w2, b2, ops8, drop, w1c, w2c):
+    def forward(ctx, res, x, w1, b1, w2, b2, ops8, drop, w1c, w2c, ln=None):
         C = x.shape[-1]
         res2 = res.float().contiguous().view(-1, C)
         x2 = x.reshape(-1, C).contiguous()
@@ -1693,9 +1693,22 @@ class _MlpFp8Fn(torch.autograd.Function):
         M = x2.shape[0]
         rpi = x.shape[1] if x.dim() == 3 else M
         dd = ctypes.byref(_mlp_desc(drop, rpi))
-        _launch("mlp_fwd", lambda: lib().csu_mlp_fp8_fwd(M, C, ptr(x2), ptr(w1q), ptr(sw1), ptr(b1f), ptr(w2p), ptr(sw2),
-                                                         ptr(b2f), ptr(res2), ptr(y), dd, stream_ptr(x2.device)),
-                16 * M * C * C, M * C * (2 + 4 + 4) + 8 * C * C, prec="fp8")
+        if ln is not None:
+            # + the next block's norm1 on the output (csu_mlp_fp8_fwd_ln), as _MlpFusedFn
+            gam, bet, eps = ln
+            gf, bf_ = gam.detach().float().contiguous(), bet.detach().float().contiguous()
+            h1 = torch.empty(M, C, dtype=torch.bfloat16, device=x2.device)
+            mean = torch.empty(M, dtype=torch.float32, device=x2.device)
+            rstd = torch.empty(M, dtype=torch.float32, device=x2.device)
+            _launch("mlp_fwd", lambda: lib().csu_mlp_fp8_fwd_ln(M, C, ptr(x2), ptr(w1q), ptr(sw1), ptr(b1f), ptr(w2p), ptr(sw2),
+                                                                ptr(b2f), ptr(res2), ptr(y), dd, ptr(gf), ptr(bf_), float(eps),
+                                                                ptr(h1), ptr(mean), ptr(rstd), stream_ptr(x2.device)),
+                    16 * M * C * C + 8 * M * C, M * C * (2 + 4 + 4 + 2) + 8 * C * C + 8 * M, prec="fp8")
+            _LN_STASH[0] = (gam, bet, float(eps), h1, mean, rstd)
+        else:
+            _launch("mlp_fwd", lambda: lib().csu_mlp_fp8_fwd(M, C, ptr(x2), ptr(w1q), ptr(sw1), ptr(b1f), ptr(w2p), ptr(sw2),
+                                                             ptr(b2f), ptr(res2), ptr(y), dd, stream_ptr(x2.device)),
+                    16 * M * C * C, M * C * (2 + 4 + 4) + 8 * C * C, prec="fp8")
         ctx.drop, ctx.rpi = drop, rpi
         ctx.save_for_backward(x2, b1f)
         ctx.ops8 = ops8
@@ -1734,12 +1747,13 @@ class _MlpFp8Fn(torch.autograd.Function):
         dw2, db2 = wgrad_maybe_side(dyb, g, w2dt, b2dt, params=ctx.params[2:])
         dw1, db1 = wgrad_maybe_side(dh, x2, w1dt, b1dt, params=ctx.params[:2])
         return (dy.to(rdt), dx.view(xshape), dw1.to(w1dt), db1.to(b1dt), dw2.to(w2dt), db2.to(b2dt), None, None, None,
-                None)
+                None, None)
 
 
-def mlp_fp8(res, x, fc1: torch.nn.Linear, fc2: torch.nn.Linear, drop: Optional[MlpDrop] = None):
+def mlp_fp8(res, x, fc1: torch.nn.Linear, fc2: torch.nn.Linear, drop: Optional[MlpDrop] = None, ln=None):
     """The fp8 fused Mlp (_MlpFp8Fn) when the active fp8 weight format holds fc1 / fc2 as an Mlp pair
-    (model.set_weight_format('fp8_e4m3') under bf16 autocast), else None."""
+    (model.set_weight_format('fp8_e4m3') under bf16 autocast), else None.  ``ln``: (weight, bias, eps)
+    of the next block's norm1, computed in the same launch (left in _LN_STASH for the caller)."""
     if _ACTIVE_FP8 is None or not x.is_cuda or fc1.out_features != 4 * x.shape[-1] or fc2.in_features != fc1.out_features:
         return None
     ops8 = _ACTIVE_FP8.mlp_operands(fc1.weight, fc2.weight)
@@ -1749,7 +1763,7 @@ def mlp_fp8(res, x, fc1: torch.nn.Linear, fc2: torch.nn.Linear, drop: Optional[M
     if x.shape[-1] not in FP8_MLP_BWD_C:   # the bf16 backward's operands: the exact dequantised shadows
         w1c, w2c = _weight_bf16(fc1.weight), _weight_bf16(fc2.weight)
     with torch.autocast("cuda", enabled=False):
-        return _MlpFp8Fn.apply(res, x, fc1.weight, fc1.bias, fc2.weight, fc2.bias, ops8, drop, w1c, w2c)
+        return _MlpFp8Fn.apply(res, x, fc1.weight, fc1.bias, fc2.weight, fc2.bias, ops8, drop, w1c, w2c, ln)
 
 
 # the fused one-launch Mlp where the library has it (C in {64, 128, 256}); otherwise two gemm4 launches
@@ -1766,13 +1780,16 @@ def mlp_residual(res, x, fc1: torch.nn.Linear, fc2: torch.nn.Linear, drop: Optio
     no dropout).  ``ln_next`` (the next block's norm1 as (weight, bias, eps)): its LayerNorm of the
     output is computed in the same launch and attached to the output for layer_norm_fork."""
     C = x.shape[-1]
-    y = mlp_fp8(res, x, fc1, fc2, drop)
+    ln = ln_next if (FUSE_NEXT_LN and ln_next is not None and ln_next[0].dtype == torch.float32
+                     and ln_next[0].numel() == C) else None
+    _LN_STASH[0] = None
+    y = mlp_fp8(res, x, fc1, fc2, drop, ln=None if FP8_QKV else ln)   # FP8_QKV: norm1 is the e4m3 LN
     if y is not None:
+        if ln is not None and _LN_STASH[0] is not None:
+            y._csu_ln = _LN_STASH[0]
+            _LN_STASH[0] = None
         return y
     if FUSED_MLP and fc1.out_features == 4 * C and lib().csu_mlp_supported(C):
-        ln = ln_next if (FUSE_NEXT_LN and ln_next is not None and ln_next[0].dtype == torch.float32
-                         and ln_next[0].numel() == C) else None
-        _LN_STASH[0] = None
         with torch.autocast("cuda", enabled=False):
             out = _MlpFusedFn.apply(res, x, fc1.weight, fc1.bias, fc2.weight, fc2.bias, _weight_bf16(fc1.weight),
                                     _weight_bf16(fc2.weight), drop, ln)

@@ -584,6 +584,12 @@ int csu_mlp_fp8_supported(int C);
 int csu_mlp_fp8_fwd(long M, int C, const void* x, const void* w1q, const float* sw1, const float* b1,
                     const void* w2p, const float* sw2, const float* b2, const float* res, float* out,
                     const csu_mlp_dropout* d, void* stream);
+/* the same with the NEXT CSWinBlock's norm1 (cswin:357) on its output, as csu_mlp_fwd_ln (bf16 ln_out,
+ * fp32 mean / rstd; out must not alias res) */
+int csu_mlp_fp8_fwd_ln(long M, int C, const void* x, const void* w1q, const float* sw1, const float* b1,
+                       const void* w2p, const float* sw2, const float* b2, const float* res, float* out,
+                       const csu_mlp_dropout* d, const float* ln_gamma, const float* ln_beta, float ln_eps, void* ln_out,
+                       float* ln_mean, float* ln_rstd, void* stream);
 /* Its backward (straight-through for every quantisation): h recomputed exactly as the forward;
  *   dg = (dy * sw2)_q W2q: w2t = W2q^T (4C, C) e4m3 (layout mode 1), dy quantised per (token, 32
  *        consecutive channels) after the per-channel scale sw2 (W2's row scale lies along this sum);
