@@ -1845,7 +1845,8 @@ class CastCache:
     Freshness: csu.optim.FusedAdamW writes every shadow in its update pass (shadow_spec), so a
     forward after an optimizer step launches nothing; ONE csu_cast_bf16_batch launch re-makes all
     of them whenever a weight's version counter moved since the last write (first forward,
-    load_state_dict, any in-place change), or always when they come from fp8 sources."""
+    load_state_dict, any in-place change).  In the fp8 format the quantised weights' shadows come from
+    the quantiser (every step); the cast batch covers the rest under the same freshness rule."""
 
     _REC = None
 
@@ -1885,6 +1886,7 @@ class CastCache:
         self._build_frag(params, dtype)
         allp = params + convs
         self._written = [None] * len(allp)
+        self._cast_idx = list(range(len(allp)))
         for k in [k for k, e in _SHADOW_SPECS.items() if e[1] is self]:
             del _SHADOW_SPECS[k]
         if (dtype == torch.bfloat16 and allp and all(p.is_cuda and p.dtype == torch.float32 and p.is_contiguous()
@@ -1892,6 +1894,7 @@ class CastCache:
             import numpy as np
             # a None source: that shadow is written elsewhere (the fp8 quantiser), not by the cast batch
             keep = [i for i in range(len(params)) if src[i] is not None]
+            self._cast_idx = keep + [len(params) + j for j in range(len(convs))]   # what the cast batch writes
             rec = np.zeros(len(keep) + len(convs), dtype=self._rec())
             t0 = 0
             for k, i in enumerate(keep):
@@ -1914,9 +1917,13 @@ class CastCache:
             # no item (every source written elsewhere): an empty table, no cast launch (_cast checks nitems)
             self.items = (torch.frombuffer(bytearray(rec.tobytes()), dtype=torch.uint8).to(allp[0].device) if len(rec)
                           else torch.zeros(1, dtype=torch.uint8, device=allp[0].device))
-            if sources is None:
+            # FusedAdamW writes the shadows of every weight cast from itself (all of them in bf16; in
+            # the fp8 format the unquantised 1-D tensors and the convs -- the quantiser writes the rest)
+            if True:
                 import weakref
                 for i, p in enumerate(params):
+                    if src[i] is not p:
+                        continue
                     rows = p.shape[0] if p.dim() > 1 else 1
                     st = self.shadow_t[i]
                     _SHADOW_SPECS[p.data_ptr()] = (weakref.ref(p), self, i, (
@@ -1939,7 +1946,7 @@ class CastCache:
                 or (sources is not None and any(a is not b for a, b in zip(sources, self.sources)))):
             self._build(params, convs, dtype, sources)
         if self.items is not None:
-            if self.sources is not None or not self._fresh():
+            if not self._fresh():
                 self._cast()
             return
         src = self.sources if getattr(self, "sources", None) is not None else self.params
@@ -1956,7 +1963,10 @@ class CastCache:
                     i.copy_(w.detach().permute(1, 2, 3, 0))
 
     def _fresh(self) -> bool:
-        return all(w is not None and w == p._version for w, p in zip(self._written, self.params + self.convs))
+        """Every shadow the cast batch writes is current (the fp8 quantiser's own are not its concern)."""
+        allp = self.params + self.convs
+        idx = getattr(self, "_cast_idx", None) or range(len(allp))
+        return all(self._written[i] is not None and self._written[i] == allp[i]._version for i in idx)
 
     # Fragment-ordered copies of the bf16 shadows W / W^T that the weight-streaming GEMM reads
     # (csu_gemm_ws: the qkv / proj Linears and their input gradients at C = 128 / 256), made from the
@@ -2020,12 +2030,12 @@ class CastCache:
             _launch("cast_bf16_batch", lambda: lib().csu_cast_bf16_batch(ptr(self.items), self.nitems, self.tiles,
                                                                          stream_ptr(allp[0].device)),
                     0, n * 6 + nt * 2)
-        if self.sources is None:
-            self._written = [p._version for p in allp]
+        for i in getattr(self, "_cast_idx", None) or range(len(allp)):
+            self._written[i] = allp[i]._version
 
     def ensure_fresh(self):
         """Re-cast now if a weight changed since its shadows were last written (see class doc)."""
-        if self.items is not None and self.sources is None and not self._fresh():
+        if self.items is not None and not self._fresh():
             self._cast()
 
     def get(self, p, dtype):

@@ -1,0 +1,12 @@
+# fp8 format: AdamW keeps the unquantised shadows fresh (no per-step cast batch): fp8 + shadow tests, bench
+O=gpurun_out/r07zg; mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -k "fp8 or full_size or shadow or cast or adamw or resume or graph" > $O/t1.log 2>&1
+rc=$?; echo "tests rc=$rc"; tail -2 $O/t1.log; [ $rc -eq 0 ] || exit $rc
+for i in 1 2; do
+  timeout -k 10 300 python -u bench.py --img 1024 --batch 4 --dtype fp8 --steps 10 --warmup 3 --cpu-baseline off --no-ref-arch > $O/fp8_$i.json 2> $O/bench.err || exit 1
+  python tools/bench_summary.py $O/fp8_$i.json | grep images
+  python -c "
+import json;r=json.loads(open('$O/fp8_$i.json').read().splitlines()[-1]); print('   ', [(k['kernel'],round(k['us_per_step'])) for k in r['roofline']['kernels'] if k['kernel'] in ('cast_bf16_batch','quant_e4m3','adamw')])"
+  timeout -k 10 300 python -u bench.py --img 1024 --batch 4 --steps 10 --warmup 3 --cpu-baseline off --no-ref-arch > $O/bf16_$i.json 2> $O/bench.err || exit 1
+  python tools/bench_summary.py $O/bf16_$i.json | grep images
+done
