@@ -1600,13 +1600,31 @@ __global__ __launch_bounds__(64 * NW, WM <= 256 ? 2 : 1) void stripe_bwd_fused_w
         }
         ATT_STAMP(2, 0);   // (debug build: the prologue's sub-phases in the dkdv slots, unused here)
         if (part) {
-            // sum over the wave's 8 row groups (lanes of equal c4 = lane & 7): row_ror:8 pairs the two
-            // halves of each 16-lane row, the permlane swaps the rows
+            // sum over the wave's 8 row groups (lanes of equal c4 = lane & 7) as a reduce-scatter:
+            // row_ror:8 pairs the two halves of each 16-lane row (40 values), then one permlane16_swap
+            // of the pair (i, i + 20) leaves value i summed over a row pair in the even rows and value
+            // i + 20 in the odd rows (20 values), one permlane32_swap of (j, j + 10) the same over the
+            // half-waves (10 values): lane (row parity p, half q) ends with values i + 10 q + 20 p.
+            // The same additions in the same pairing as a full all-reduce, half the VALU.
 #pragma unroll
-            for (int i = 0; i < 40; ++i) wacc[i] = xsum32(xsum16(wacc[i] + dppf<0x128>(wacc[i])));
-            if (lane < 8)
+            for (int i = 0; i < 40; ++i) wacc[i] += dppf<0x128>(wacc[i]);
 #pragma unroll
-                for (int i = 0; i < 40; ++i) red[wave][lane][i] = wacc[i];
+            for (int i = 0; i < 20; ++i) {
+                const auto r2 = __builtin_amdgcn_permlane16_swap(__builtin_bit_cast(unsigned, wacc[i]),
+                                                                 __builtin_bit_cast(unsigned, wacc[i + 20]), false, false);
+                wacc[i] = __builtin_bit_cast(float, (unsigned)r2[0]) + __builtin_bit_cast(float, (unsigned)r2[1]);
+            }
+#pragma unroll
+            for (int i = 0; i < 10; ++i) {
+                const auto r2 = __builtin_amdgcn_permlane32_swap(__builtin_bit_cast(unsigned, wacc[i]),
+                                                                 __builtin_bit_cast(unsigned, wacc[i + 10]), false, false);
+                wacc[i] = __builtin_bit_cast(float, (unsigned)r2[0]) + __builtin_bit_cast(float, (unsigned)r2[1]);
+            }
+            if ((lane & 8) == 0) {
+                const int i0 = 10 * (lane >> 5) + 20 * ((lane >> 4) & 1);
+#pragma unroll
+                for (int i = 0; i < 10; ++i) red[wave][lane & 7][i0 + i] = wacc[i];
+            }
         }
     }
     ATT_STAMP(2, 1);
