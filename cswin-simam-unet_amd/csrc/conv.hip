@@ -621,7 +621,11 @@ __global__ __launch_bounds__(64 * NS / 16, 1) void conv3_wgrad_halo(Geo g, long 
 }
 
 struct WDCfg { int tn, tk, s, wn, wk; };
+#ifdef WD_PROBE256   // probe build only (tools/probes/wgrad_tile_probe.py): slot 4 = the 256 x 256 tile, 8 waves
+constexpr WDCfg kWDCfgs[] = {{128, 128, 3, 2, 2}, {64, 256, 3, 1, 4}, {128, 128, 2, 2, 2}, {256, 128, 2, 4, 2}, {256, 256, 2, 2, 4}};
+#else
 constexpr WDCfg kWDCfgs[] = {{128, 128, 3, 2, 2}, {64, 256, 3, 1, 4}, {128, 128, 2, 2, 2}, {256, 128, 2, 4, 2}, {64, 128, 4, 1, 4}};
+#endif
 constexpr int kWDNCfg = 5;
 
 // ---- bf16 implicit GEMM, v2: 128/256 x BN tiles, 64-deep K slices, double-buffered LDS ----------
