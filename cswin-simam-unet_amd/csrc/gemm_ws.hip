@@ -60,10 +60,10 @@ constexpr bool WS_ROT = true;
 
 // k-steps per unit: the largest divisor of ks <= 16 that still gives the wave >= 2 units (so the
 // next unit's weight loads overlap this unit's MFMAs), else the largest divisor <= 16
-constexpr int ws_unit(int ks, int nt) {
-    for (int u = 16; u > 1; --u)
+constexpr int ws_unit(int ks, int nt, int umax = 16) {
+    for (int u = umax; u > 1; --u)
         if (ks % u == 0 && nt * (ks / u) >= 2) return u;
-    for (int u = 16; u > 1; --u)
+    for (int u = umax; u > 1; --u)
         if (ks % u == 0) return u;
     return 1;
 }
@@ -71,18 +71,28 @@ constexpr int ws_unit(int ks, int nt) {
 // groups of 64 per workgroup, each split over 2 waves) or 1
 constexpr int ws_wn(int n) { return (n / 32) % 4 == 0 ? 4 : (n / 32) % 2 == 0 ? 2 : 1; }
 constexpr int ws_tokens(int n) { return WS_BM * (4 / ws_wn(n)); }   // tokens per workgroup
+// N split over NS workgroups per token panel (grid.y): each streams 1/NS of the weight and writes 1/NS
+// of the features, two workgroups per CU.  Only for the plain epilogue (bias; RESID spills), K <= 256 (the token
+// panel in registers, two workgroups' LDS fit) and an even tile count per wave.  WS_NSPLIT = 1: off.
+#ifndef WS_NSPLIT
+#define WS_NSPLIT 1
+#endif
+constexpr int ws_ns(int k, int n, int epi) {
+    return WS_NSPLIT > 1 && epi == 0 && k <= 256 && ws_wn(n) == 4 && (n / 128) % WS_NSPLIT == 0 ? WS_NSPLIT : 1;
+}
 
-template <int K, int N, int EPI, typename TOUT>
-__global__ __launch_bounds__(256, ws_wn(N) < 4 ? 2 : 1) void gemm_ws_kernel(long M, const bf16* __restrict__ X, int ldx,
+template <int K, int N, int EPI, typename TOUT, int NS = 1>
+__global__ __launch_bounds__(256, ws_wn(N) < 4 || NS > 1 ? 2 : 1) void gemm_ws_kernel(long M, const bf16* __restrict__ X, int ldx,
                                                       const bf16* __restrict__ Wf, const float* __restrict__ bias,
                                                       const float* __restrict__ resid, TOUT* __restrict__ out,
                                                       WsLn ln = WsLn{}, WsLnF lnf = WsLnF{}) {
     constexpr int WN = ws_wn(N);                   // waves along N
-    constexpr int NT = N / (32 * WN);              // 32-feature tiles per wave
-    static_assert(NT * 32 * WN == N, "gemm_ws: N = 32 WN NT");
+    constexpr int NT = N / (32 * WN * NS);         // 32-feature tiles per wave (of this workgroup's N / NS)
+    static_assert(NT * 32 * WN * NS == N, "gemm_ws: N = 32 WN NT NS");
+    static_assert(NS == 1 || EPI == WS_PLAIN || EPI == WS_RESID, "gemm_ws: the LayerNorm epilogues need all N features");
     static_assert(EPI != WS_LNBWD || WN == 4, "gemm_ws: the LayerNorm epilogue needs all C features in one token group");
     constexpr int KS = K / 16;                     // k-steps
-    constexpr int UK = ws_unit(KS, NT);            // k-steps per unit (a divisor of KS, <= 16)
+    constexpr int UK = ws_unit(KS, NT, NS > 1 ? 8 : 16);   // k-steps per unit (a divisor of KS; <= 8 at two WGs/CU)
     constexpr int CH = KS / UK;                    // units per tile
     static_assert(CH * UK == KS, "unit size");
     constexpr int U = NT * CH;                     // units per wave
@@ -103,7 +113,8 @@ __global__ __launch_bounds__(256, ws_wn(N) < 4 ? 2 : 1) void gemm_ws_kernel(long
     // tile order rotated per workgroup (its index within the XCD: ids x, x + 8, ... run on XCD x), so
     // the CUs of an XCD do not all read the same weight lines at the same moment
     const int rot = WS_ROT ? (int)((blockIdx.x >> 3) % NT) : 0;
-    auto tile_of = [&](int i) { return i + rot < NT ? i + rot : i + rot - NT; };
+    const int tb = NS > 1 ? (int)blockIdx.y * NT : 0;   // this workgroup's first tile of each wave
+    auto tile_of = [&](int i) { return tb + (i + rot < NT ? i + rot : i + rot - NT); };
     bf16x8 wf[2][UK];
     auto wload1 = [&](int u, int s) {   // k-step s of unit u of this wave into buffer u & 1
         const int nt = wn + WN * tile_of(u / CH), ks = (u % CH) * UK + s;
@@ -426,8 +437,9 @@ __global__ __launch_bounds__(256, ws_wn(N) < 4 ? 2 : 1) void gemm_ws_kernel(long
 template <int K, int N, int EPI, typename TOUT>
 int ws_launch(long M, const bf16* X, int ldx, const bf16* Wf, const float* bias, const float* resid, void* out,
               hipStream_t st, const WsLn& ln = WsLn{}, const WsLnF& lnf = WsLnF{}) {
-    gemm_ws_kernel<K, N, EPI, TOUT><<<dim3((unsigned)(M / ws_tokens(N))), 256, 0, st>>>(M, X, ldx, Wf, bias, resid, (TOUT*)out, ln,
-                                                                                       lnf);
+    constexpr int NS = ws_ns(K, N, EPI);
+    gemm_ws_kernel<K, N, EPI, TOUT, NS><<<dim3((unsigned)(M / ws_tokens(N)), NS), 256, 0, st>>>(M, X, ldx, Wf, bias, resid,
+                                                                                                (TOUT*)out, ln, lnf);
     return check_launch("gemm_ws");
 }
 
