@@ -1018,9 +1018,9 @@ __device__ __forceinline__ Win decode_w(const csu_stripe_args& a, int split) {
     return w;
 }
 
-template <int WM, bool DROP>
-__global__ __launch_bounds__(NT) void stripe_fwd_w(csu_stripe_args a, int split, const bf16* __restrict__ qkv,
-                                                   bf16* __restrict__ out, float* __restrict__ lse) {
+template <int WM, bool DROP, int NW = 4>
+__global__ __launch_bounds__(64 * NW) void stripe_fwd_w(csu_stripe_args a, int split, const bf16* __restrict__ qkv,
+                                                        bf16* __restrict__ out, float* __restrict__ lse) {
     __shared__ __attribute__((aligned(16))) bf16 Ks[WM * HD];
     __shared__ __attribute__((aligned(16))) bf16 Vs[WM * HD];
     __shared__ __attribute__((aligned(16))) float wts[HD * 10];
@@ -1043,20 +1043,20 @@ __global__ __launch_bounds__(NT) void stripe_fwd_w(csu_stripe_args a, int split,
     }
     float lw[LW_IT];
     lepe_weights_load(branch(a, w.br), w.h, lw);
-    stage_win2(w, a.reso, img, C3, C + w.chq, img, C3, 2 * C + w.chq, (npad + 63) & ~63, Ks, Vs);  // zero rows up to a 64-key step
+    stage_win2<64 * NW>(w, a.reso, img, C3, C + w.chq, img, C3, 2 * C + w.chq, (npad + 63) & ~63, Ks, Vs);  // zero rows up to a 64-key step
     lepe_weights_store(lw, wts);
     __syncthreads();
     ATT_STAMP(0, 1);
     const float c = a.scale * kLog2e;
     ADrop dr;
     if constexpr (DROP) dr = attn_drop(a, w);
-    for (int q0 = qbeg + 32 * wave; q0 < qend; q0 += 128) {
+    for (int q0 = qbeg + 32 * wave; q0 < qend; q0 += 32 * NW) {
         const int qn = q0 + r;
         const bool qvalid = qn < w.N;
         const int qtok = qvalid ? tok_of(w, a.reso, qn) : 0;
         const Frag<bf16> qf = qnext;
-        if (q0 + 128 < qend) {
-            const int qn2 = q0 + 128 + r;
+        if (q0 + 32 * NW < qend) {
+            const int qn2 = q0 + 32 * NW + r;
             const bool qv2 = qn2 < w.N;
             load_frag_rs(qnext, rs_img, (size_t)(qv2 ? tok_of(w, a.reso, qn2) : 0) * C3 + w.chq, h, qv2);
         }
@@ -1849,8 +1849,19 @@ int wm_of(const csu_stripe_args& a) {
     return N <= 256 ? 256 : N <= 512 ? 512 : 1024;
 }
 
+// ATTN_FWD_WAVES = 8: the forward's split partners merged into one 8-wave workgroup (the window's
+// K / V staged once per window-head instead of once per partner)
+#ifndef ATTN_FWD_WAVES
+#define ATTN_FWD_WAVES 8
+#endif
 template <int WM>
 void fwd_w(const csu_stripe_args& a, int sp, dim3 g, const bf16* qkv, bf16* out, float* lse, hipStream_t st) {
+    if (ATTN_FWD_WAVES == 8 && sp % 2 == 0) {
+        g.x /= 2;
+        if (a.drop_p > 0.f) stripe_fwd_w<WM, true, 8><<<g, 512, 0, st>>>(a, sp / 2, qkv, out, lse);
+        else stripe_fwd_w<WM, false, 8><<<g, 512, 0, st>>>(a, sp / 2, qkv, out, lse);
+        return;
+    }
     if (a.drop_p > 0.f) stripe_fwd_w<WM, true><<<g, NT, 0, st>>>(a, sp, qkv, out, lse);
     else stripe_fwd_w<WM, false><<<g, NT, 0, st>>>(a, sp, qkv, out, lse);
 }
