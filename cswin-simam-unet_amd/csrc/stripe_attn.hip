@@ -1133,8 +1133,8 @@ __global__ __launch_bounds__(64 * NW) void stripe_fwd_w(csu_stripe_args a, int s
     ATT_STAMP(0, 2);
 }
 
-template <int WM, bool DROP>
-__global__ __launch_bounds__(NT) void stripe_bwd_dq_w(csu_stripe_args a, int split, const bf16* __restrict__ qkv,
+template <int WM, bool DROP, int NW = 4>
+__global__ __launch_bounds__(64 * NW) void stripe_bwd_dq_w(csu_stripe_args a, int split, const bf16* __restrict__ qkv,
                                                       const bf16* __restrict__ out, const bf16* __restrict__ dout,
                                                       const float* __restrict__ lse, float* __restrict__ delta,
                                                       bf16* __restrict__ dqkv) {
@@ -1171,14 +1171,14 @@ __global__ __launch_bounds__(NT) void stripe_bwd_dq_w(csu_stripe_args a, int spl
     load_q(qbeg + 32 * wave);
     float lw[LW_IT];
     lepe_weights_load(branch(a, w.br), w.h, lw);
-    stage_win2(w, a.reso, img, C3, C + w.chq, img, C3, 2 * C + w.chq, npad, Ks, Vs);
+    stage_win2<64 * NW>(w, a.reso, img, C3, C + w.chq, img, C3, 2 * C + w.chq, npad, Ks, Vs);
     lepe_weights_store(lw, wts);
     __syncthreads();
     ATT_STAMP(1, 1);
     const float c = a.scale * kLog2e;
     ADrop dr;
     if constexpr (DROP) dr = attn_drop(a, w);
-    for (int q0 = qbeg + 32 * wave; q0 < qend; q0 += 128) {
+    for (int q0 = qbeg + 32 * wave; q0 < qend; q0 += 32 * NW) {
         const int qn = q0 + r;
         const bool qvalid = qn < w.N;
         const int qtok = qvalid ? tok_of(w, a.reso, qn) : 0;
@@ -1237,15 +1237,15 @@ __global__ __launch_bounds__(NT) void stripe_bwd_dq_w(csu_stripe_args a, int spl
     ATT_STAMP(1, 2);
 }
 
-template <int WM, bool DROP>
-__global__ __launch_bounds__(NT) void stripe_bwd_dkdv_w(csu_stripe_args a, int split, const bf16* __restrict__ qkv,
+template <int WM, bool DROP, int NW = 4>
+__global__ __launch_bounds__(64 * NW) void stripe_bwd_dkdv_w(csu_stripe_args a, int split, const bf16* __restrict__ qkv,
                                                         const bf16* __restrict__ dout, const float* __restrict__ lse,
                                                         const float* __restrict__ delta, bf16* __restrict__ dqkv) {
     __shared__ __attribute__((aligned(16))) bf16 Qs[WM * HD];
     __shared__ __attribute__((aligned(16))) bf16 Gs[WM * HD];
     __shared__ __attribute__((aligned(16))) float lse_s[WM], dl_s[WM];
     __shared__ __attribute__((aligned(16))) float wts[HD * 10];
-    __shared__ __attribute__((aligned(16))) unsigned char dtbl[4][128];
+    __shared__ __attribute__((aligned(16))) unsigned char dtbl[NW][128];
     ATT_STAMP(2, 0);
     const Win w = decode_w(a, split);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1272,21 +1272,22 @@ __global__ __launch_bounds__(NT) void stripe_bwd_dkdv_w(csu_stripe_args a, int s
     lepe_weights_load(branch(a, w.br), w.h, lw);
     {   // per-query statistics of the window: loads issued with the staging loads
         const __amdgpu_buffer_rsrc_t rs_lse = stat_rsrc(a, lse), rs_dl = stat_rsrc(a, delta);
-        constexpr int SI = WM / NT;   // WM >= npad rows, one stat per thread per pass
+        constexpr int NTH = 64 * NW, SI = WM / NTH;   // WM >= npad rows, one stat per thread per pass
+        static_assert(SI * NTH == WM, "stripe_bwd_dkdv_w: WM a multiple of the workgroup");
         float lv[SI], dv2[SI];
 #pragma unroll
         for (int k = 0; k < SI; ++k) {
-            const int i = threadIdx.x + k * NT;
+            const int i = threadIdx.x + k * NTH;
             const bool v = i < w.N;
             const unsigned off = v ? (unsigned)(stat_index(a, w, tok_of(w, a.reso, i)) * 4) : kOOB;
             lv[k] = ldf_rs(rs_lse, off);
             dv2[k] = ldf_rs(rs_dl, off);
         }
-        stage_win2(w, a.reso, img, C3, w.chq, gimg, C, w.chq, npad, Qs, Gs);
+        stage_win2<NTH>(w, a.reso, img, C3, w.chq, gimg, C, w.chq, npad, Qs, Gs);
         lepe_weights_store(lw, wts);
 #pragma unroll
         for (int k = 0; k < SI; ++k) {
-            const int i = threadIdx.x + k * NT;
+            const int i = threadIdx.x + k * NTH;
             if (i < npad) {
                 lse_s[i] = i < w.N ? lv[k] * kLog2e : INFINITY;
                 dl_s[i] = dv2[k];
@@ -1298,7 +1299,7 @@ __global__ __launch_bounds__(NT) void stripe_bwd_dkdv_w(csu_stripe_args a, int s
     const float c = a.scale * kLog2e;
     ADrop dr;
     if constexpr (DROP) dr = attn_drop(a, w);
-    for (int k0 = kbeg + 32 * wave; k0 < kend; k0 += 128) {
+    for (int k0 = kbeg + 32 * wave; k0 < kend; k0 += 32 * NW) {
         const int kn = k0 + r;
         const bool kvalid = kn < w.N;
         const int ktok = kvalid ? tok_of(w, a.reso, kn) : 0;
@@ -1854,6 +1855,9 @@ int wm_of(const csu_stripe_args& a) {
 #ifndef ATTN_FWD_WAVES
 #define ATTN_FWD_WAVES 8
 #endif
+#ifndef ATTN_BWD_WAVES
+#define ATTN_BWD_WAVES 8
+#endif
 template <int WM>
 void fwd_w(const csu_stripe_args& a, int sp, dim3 g, const bf16* qkv, bf16* out, float* lse, hipStream_t st) {
     if (ATTN_FWD_WAVES == 8 && sp % 2 == 0) {
@@ -1869,6 +1873,21 @@ void fwd_w(const csu_stripe_args& a, int sp, dim3 g, const bf16* qkv, bf16* out,
 template <int WM>
 void bwd_w(const csu_stripe_args& a, int sp, dim3 g, const bf16* qkv, const bf16* out, const bf16* dout,
            const float* lse, float* delta, bf16* dqkv, hipStream_t st) {
+    // windows of >= 512 tokens (their K / V or Q / dO images bound residency): split partners merged
+    // into 8-wave workgroups, as the forward (ATTN_FWD_WAVES)
+    if constexpr (WM >= 512) {
+        if (ATTN_BWD_WAVES == 8 && sp % 2 == 0) {
+            g.x /= 2;
+            if (a.drop_p > 0.f) {
+                stripe_bwd_dq_w<WM, true, 8><<<g, 512, 0, st>>>(a, sp / 2, qkv, out, dout, lse, delta, dqkv);
+                stripe_bwd_dkdv_w<WM, true, 8><<<g, 512, 0, st>>>(a, sp / 2, qkv, dout, lse, delta, dqkv);
+            } else {
+                stripe_bwd_dq_w<WM, false, 8><<<g, 512, 0, st>>>(a, sp / 2, qkv, out, dout, lse, delta, dqkv);
+                stripe_bwd_dkdv_w<WM, false, 8><<<g, 512, 0, st>>>(a, sp / 2, qkv, dout, lse, delta, dqkv);
+            }
+            return;
+        }
+    }
     if (a.drop_p > 0.f) {
         stripe_bwd_dq_w<WM, true><<<g, NT, 0, st>>>(a, sp, qkv, out, dout, lse, delta, dqkv);
         stripe_bwd_dkdv_w<WM, true><<<g, NT, 0, st>>>(a, sp, qkv, dout, lse, delta, dqkv);
