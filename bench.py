@@ -48,8 +48,10 @@ def parse():
     ap.add_argument("--img", type=int, default=512)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32", "fp8"],
                     help="fp8: e4m3 Linear weights (per-row power-of-two scales), fp32 accumulate (BASELINE config 5); "
-                         "the qkv GEMM and the fused Mlp run e4m3 x e4m3 MFMA (activations quantised per token / "
-                         "per 32-value MX block), the other layers bf16 on the dequantised weights")
+                         "by default only the fused Mlp (C = 64 / 128 / 256 forward, C = 256 backward) runs e4m3 x e4m3 "
+                         "MFMA (activations MX-quantised per 32-value block in registers); qkv, proj, concat_linear "
+                         "and the C = 512 Mlp run bf16 on the exact dequantised e4m3 weights (CSU_FP8_QKV=1: qkv on "
+                         "the fp8 MFMA too)")
     ap.add_argument("--model", default="cswin", choices=["cswin", "unet"],
                     help="unet: the plain UNet of train_unet_segmentation.py (BASELINE config 1's model; Adam, "
                          "use --img 128 --batch 8)")
@@ -74,6 +76,11 @@ def parse():
                     help="train_model: time the drop-in csu.train.train_model (cswin:751-841) over --steps batches "
                          "(one epoch; its own graph capture after two eager steps) instead of GraphedTrainStep")
     ap.add_argument("--traffic-key", action="store_true", help="print this workload's PMC traffic key and exit")
+    ap.add_argument("--side-wgrad", action="store_true",
+                    help="eager steps (--graph off) compute weight gradients on the side stream (the eager "
+                         "product default); without it eager steps launch exactly the kernels the captured step "
+                         "replays (grouped end-of-backward weight gradients on the launch stream) -- the PMC passes "
+                         "of tools/pmc_head.sh then describe the timed graph's kernels")
     ap.add_argument("--dp-force", action="store_true",
                     help="run the data-parallel path (RCCL process group + captured all-reduce) even at N = 1")
     return ap.parse_args()
@@ -261,6 +268,8 @@ def main():
         opt.step()
         return loss
 
+    if not use_graph and not args.side_wgrad:
+        ops.SIDE_WGRAD = False   # the captured step never uses the side stream (ops._side_ok)
     if args.api == "train_model":
         return _bench_train_model(args, model, batches, reducer, amp, nparams, world, rank, dp, device)
     step = eager_step
@@ -365,7 +374,7 @@ def main():
         rec = {"metric": _metric(args), "value": round(images / el, 3),
                "unit": "images/sec", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
                "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
-               "vs_baseline": None, "dtype": "fp8-e4m3 x e4m3 MFMA (qkv, Mlp) + bf16 (fp8-e4m3 weights)" if args.dtype == "fp8" else args.dtype, "data": "synthetic (ellipse masks, SURVEY §8d), random-init weights",
+               "vs_baseline": None, "dtype": _dtype_label(args), "data": "synthetic (ellipse masks, SURVEY §8d), random-init weights",
                "config": {"workload": (f"plain UNet train step {args.img}x{args.img}, Adam" if args.model == "unet" else
                                        f"CSWin-UNet train step {args.img}x{args.img} depth {depth} split {split}"
                                        f"{' +SimAM' if args.simam else ''}"
@@ -456,6 +465,15 @@ def _bench_train_model(args, model, batches, reducer, amp, nparams, world, rank,
         print(json.dumps(rec), flush=True)
     if dp:
         dist.destroy_process_group()
+
+
+def _dtype_label(args):
+    """The arithmetic the step runs in.  fp8: which GEMMs run e4m3 x e4m3 MFMA at this HEAD's defaults."""
+    if args.dtype != "fp8":
+        return args.dtype
+    from csu import ops
+    scope = "fused Mlp fwd (C 64/128/256) + bwd (C 256)" + (" + qkv" if ops.FP8_QKV else "")
+    return f"fp8-e4m3 x e4m3 MFMA ({scope}); bf16 MFMA on the dequantised e4m3 weights elsewhere"
 
 
 def _metric(args):

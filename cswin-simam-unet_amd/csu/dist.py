@@ -2,8 +2,8 @@
 
 The reference is single-device (cswin:865); SURVEY §8e: CSWin-UNet has no BatchNorm, so averaging
 per-rank gradients of equal per-rank batches equals the global-batch gradient.  Buckets are sized
-for xGMI point-to-point rings: 94 MB of fp32 gradients go in 64 MB buckets (2 all-reduces per step,
-the first overlapped with the rest of backward).
+for xGMI point-to-point rings: 94 MB of fp32 gradients go in 32 MB buckets (3 all-reduces per step,
+the first two overlapped with the rest of backward, ``GradAllReduce``).
 
 ``GradAllReduce`` is the graph-capturable replacement bench.py uses at N > 1: the same bucketed
 averaging, recorded into the train step's HIP graph (DDP is the eager fallback)."""
@@ -161,6 +161,12 @@ class GradAllReduce:
                 p.grad = torch.zeros_like(p)
             grads.append(p.grad)
         flat = self.flat[bi]
+        # late gradients of this bucket (written by a deferred launch or on the csu side stream after
+        # autograd received them): if AccumulateGrad copied one instead of stealing it, its .grad holds
+        # the values from before the write -- repaired below, ordered after the writers, before the
+        # bucket reads it (ops.take_late; the end-of-backward check would come after the all-reduce)
+        late = [(p, src) for p, src in self._ops.take_late(self.buckets[bi])
+                if p.grad is not None and p.grad.data_ptr() != src.data_ptr()]
         # gradients not already in place (not written into the bucket by csu's backward)
         todo = [(v, g) for v, g in zip(self.views[bi], grads) if g.data_ptr() != v.data_ptr()]
         self.held.append(grads)
@@ -176,6 +182,9 @@ class GradAllReduce:
         else:
             ctx = contextlib.nullcontext()
         with ctx:
+            for p, src in late:
+                p.grad.copy_(src)
+                self._ops.STATS["late_grad_fixups"] += 1
             if todo:
                 torch._foreach_copy_([v for v, _ in todo], [g for _, g in todo])
             buf = flat

@@ -4,6 +4,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import threading
 import weakref
 from typing import List, Optional, Sequence, Tuple
 
@@ -297,6 +298,25 @@ def _check_late(lst):
         STATS["late_grad_fixups"] += 1
 
 
+def take_late(params):
+    """Remove and return the late-gradient entries of ``params`` as (param, registered gradient)
+    pairs.  csu.dist.GradAllReduce calls it when a bucket is launched: a copied late gradient must be
+    repaired BEFORE the bucket reads p.grad (the end-of-backward check comes after the all-reduce)."""
+    want = {id(_leaf(p)) for p in params}
+    out = []
+    for lst in (_LATE_DEFER, _LATE_SIDE):
+        keep = []
+        for e in lst:
+            p = e[0]()
+            if p is not None and id(p) in want:
+                pref, dptr, st, off, shape, stride, dt = e
+                out.append((p, torch.empty(0, dtype=dt, device=st.device).set_(st, off, shape, stride)))
+            else:
+                keep.append(e)
+        lst[:] = keep
+    return out
+
+
 def _reducer_hooks_only(hooks) -> bool:
     """True when every post-accumulate-grad hook is a csu.dist.GradAllReduce bucket counter: that
     reducer postpones a bucket holding deferred gradients until after the end-of-backward flush
@@ -529,7 +549,7 @@ def _ln_pre(x, weight, bias, eps, od):
     """The LayerNorm of x already computed by the fused Mlp that produced it (``_csu_ln``), or None."""
     pre = getattr(x, "_csu_ln", None)
     if (pre is not None and pre[0] is weight and pre[1] is bias and pre[2] == float(eps) and pre[3].dtype == od
-            and pre[3].numel() == x.numel() and x.is_contiguous()):
+            and pre[3].numel() == x.numel() and x.is_contiguous() and pre[6] == x._version):
         return pre
     return None
 
@@ -965,7 +985,9 @@ def _ws_ok(M, N, K, out_dtype, resid=False) -> bool:
 
 
 def dtype_code_of(dt) -> int:
-    return CSU_F32 if dt == torch.float32 else 1
+    """csu dtype code of a torch dtype; -1 for dtypes the kernels cannot write (csu_gemm_ws_supported
+    then rejects the shape and the caller takes gemm4, whose own checks raise CsuError)."""
+    return CSU_F32 if dt == torch.float32 else CSU_BF16 if dt == torch.bfloat16 else -1
 
 
 # ---------------------------------------------------------------------------------------------
@@ -1040,6 +1062,11 @@ def _grad_dest(params) -> Optional[torch.Tensor]:
 
 def _param_safe(p) -> bool:
     """True when no reader of p.grad can run before the end-of-backward join (see above)."""
+    # the end-of-backward flush resets the forward use counts (_USES): queue it from every backward
+    # that consults them, not only from deferring ones (a model with no deferrable LayerNorm / Linear /
+    # LePE work -- the plain UNet -- would otherwise keep counting across steps, and from its second
+    # step every conv weight would look shared and lose the side stream)
+    _queue_flush()
     p = _leaf(p)
     if p is None:
         return True
@@ -1221,7 +1248,8 @@ class _SharedCastFn(torch.autograd.Function):
             xc = x.contiguous()
             y = torch.empty(x.shape, dtype=dtype, device=x.device)
             n = x.numel()
-            _launch("cast_bf16", lambda: lib().csu_grad_join(n, CSU_F32, ptr(xc), 0, None, None, ptr(y),
+            # the bare bf16 cast runs csu_grad_join's kernel: one ledger name per kernel (rocprof groups)
+            _launch("grad_join", lambda: lib().csu_grad_join(n, CSU_F32, ptr(xc), 0, None, None, ptr(y),
                                                              stream_ptr(x.device)), 0, n * 6, prec="f32")
         else:
             y = x.to(dtype)
@@ -1571,9 +1599,8 @@ def linear_residual(res, x, weight, bias, ln_next=None):
     _LN_STASH[0] = None
     with torch.autocast("cuda", enabled=False):
         out = _LinearResidualFn.apply(res, x, weight, bias, _weight_bf16(weight), ln)
-    if ln is not None and _LN_STASH[0] is not None:
-        out._csu_ln = _LN_STASH[0]
-        _LN_STASH[0] = None
+    if ln is not None:
+        _attach_ln(out)
     return out
 
 
@@ -1655,8 +1682,28 @@ class _MlpFusedFn(torch.autograd.Function):
 
 
 # the fused Mlp's LayerNorm of its output for the next block (csu_mlp_fwd_ln): (gamma, beta, eps, ln_out,
-# mean, rstd), set by _MlpFusedFn.forward and attached to its output by mlp_residual as ``_csu_ln``
-_LN_STASH: list = [None]
+# mean, rstd), set by _MlpFusedFn.forward (or the proj GEMM's) and attached to its output by
+# mlp_residual / linear_residual as ``_csu_ln`` together with the output's version counter (an in-place
+# change of the output after the launch invalidates it: _ln_pre).  One slot per thread (one thread per
+# device runs its own forward).
+class _ThreadSlot(threading.local):
+    def __init__(self):
+        self.v = None
+
+    def __getitem__(self, i):
+        return self.v
+
+    def __setitem__(self, i, v):
+        self.v = v
+
+
+_LN_STASH = _ThreadSlot()
+
+
+def _attach_ln(out):
+    st, _LN_STASH[0] = _LN_STASH[0], None
+    if st is not None:
+        out._csu_ln = tuple(st) + (out._version,)
 
 
 # widths whose fp8 Mlp backward runs the fp8 kernel; the others run the bf16 fused backward on the
@@ -1785,17 +1832,15 @@ def mlp_residual(res, x, fc1: torch.nn.Linear, fc2: torch.nn.Linear, drop: Optio
     _LN_STASH[0] = None
     y = mlp_fp8(res, x, fc1, fc2, drop, ln=None if FP8_QKV else ln)   # FP8_QKV: norm1 is the e4m3 LN
     if y is not None:
-        if ln is not None and _LN_STASH[0] is not None:
-            y._csu_ln = _LN_STASH[0]
-            _LN_STASH[0] = None
+        if ln is not None:
+            _attach_ln(y)
         return y
     if FUSED_MLP and fc1.out_features == 4 * C and lib().csu_mlp_supported(C):
         with torch.autocast("cuda", enabled=False):
             out = _MlpFusedFn.apply(res, x, fc1.weight, fc1.bias, fc2.weight, fc2.bias, _weight_bf16(fc1.weight),
                                     _weight_bf16(fc2.weight), drop, ln)
-        if ln is not None and _LN_STASH[0] is not None:
-            out._csu_ln = _LN_STASH[0]
-            _LN_STASH[0] = None
+        if ln is not None:
+            _attach_ln(out)
         return out
     with torch.autocast("cuda", enabled=False):
         return _MlpResidualFn.apply(res, x, fc1.weight, fc1.bias, fc2.weight, fc2.bias, _weight_bf16(fc1.weight),

@@ -29,6 +29,15 @@ def test_library_exports_every_header_symbol():
     assert b"gfx950" in L.csu_build_info()
 
 
+def test_gemm_ws_rejects_unwritable_out_dtype():
+    """the weight-streaming GEMM's support query sees the real output dtype (fp16 or any
+    non-fp32 / bf16 dtype is rejected, so the caller falls back instead of failing in gemm_ws)."""
+    from csu import ops
+    assert ops.dtype_code_of(torch.float16) == -1 and ops.dtype_code_of(torch.bfloat16) == 1
+    assert ops._ws_ok(1024, 768, 256, torch.bfloat16) and ops._ws_ok(1024, 768, 256, torch.float32)
+    assert not ops._ws_ok(1024, 768, 256, torch.float16)
+
+
 def test_struct_layout_matches_header(tmp_path):
     """The ctypes mirrors of the C structs have the C compiler's sizes and field offsets
     (include/csu.h compiled by gcc here)."""

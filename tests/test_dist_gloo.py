@@ -250,3 +250,78 @@ def test_late_gradient_copied_by_autograd_is_repaired():
     assert p.grad.data_ptr() == buf[2:].data_ptr()
     ops._check_late(ops._LATE_DEFER)
     assert ops.STATS["late_grad_fixups"] == n0 + 1
+
+
+def _late_reducer_worker(rank, world, port, out_path):
+    sys.path[:0] = [REPO, os.path.join(REPO, "cswin-simam-unet_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    torch.distributed.init_process_group("gloo")
+    from csu import ops
+    from csu.dist import GradAllReduce
+    p = torch.nn.Parameter(torch.zeros(6))
+    red = GradAllReduce([p], bucket_mb=1.0)
+    buf = torch.zeros(8)
+    keep = []
+
+    class Late(torch.autograd.Function):
+        @staticmethod
+        def forward(ctx, x, w):
+            return x * 1.0
+
+        @staticmethod
+        def backward(ctx, g):
+            gw = buf[2:]
+            keep.append(gw)            # a second reference: AccumulateGrad copies it (stale zeros)
+            ops._late((p,), (gw,))
+            # the "deferred kernel": runs in the flush the bucket hook triggers, AFTER the copy
+            ops._WG_POST.append(lambda: buf[2:].copy_(torch.arange(6.0) * (rank + 1)))
+            return g, gw
+
+    n0 = ops.STATS["late_grad_fixups"]
+    Late.apply(torch.ones(3, requires_grad=True), p).sum().backward()
+    red.finish()
+    torch.save({"grad": p.grad.clone(), "fixups": ops.STATS["late_grad_fixups"] - n0,
+                "left": len(ops._LATE_DEFER)}, f"{out_path}.{rank}")
+    torch.distributed.destroy_process_group()
+
+
+def test_late_gradient_repaired_before_bucket_allreduce(tmp_path):
+    """with csu.dist.GradAllReduce attached, a late gradient that AccumulateGrad copied must
+    be repaired before the bucket all-reduce reads it (not after, by the end-of-backward check): the
+    averaged gradient is the mean of the values the deferred launches wrote."""
+    out = str(tmp_path / "late")
+    mp.spawn(_late_reducer_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    for r in range(2):
+        got = torch.load(f"{out}.{r}", weights_only=True)
+        assert got["fixups"] == 1 and got["left"] == 0
+        torch.testing.assert_close(got["grad"], torch.arange(6.0) * 1.5)
+
+
+def test_use_counts_reset_without_deferred_work():
+    """a backward with no deferrable LayerNorm / Linear / LePE work (the plain UNet's convs)
+    must still reset the forward use counts at its end, or the second step sees every weight as
+    shared (_uses > 1) and loses the side-stream / in-bucket gradient paths."""
+    sys.path[:0] = [REPO, os.path.join(REPO, "cswin-simam-unet_amd")]
+    from csu import ops
+    w = torch.nn.Parameter(torch.ones(4))
+    safe = []
+
+    class ConvLike(torch.autograd.Function):
+        @staticmethod
+        def forward(ctx, x, weight):
+            ops._note_use(ctx, weight)
+            return x * 1.0
+
+        @staticmethod
+        def backward(ctx, g):
+            safe.append(ops._param_safe(w))   # what a conv backward asks (ops._side_ok)
+            return g, None
+
+    try:
+        for _ in range(3):
+            w.grad = None
+            ConvLike.apply(torch.ones(4, requires_grad=True), w).sum().backward()
+            assert ops._uses(w) == 0
+        assert safe == [True, True, True]
+    finally:
+        ops._USES.clear()

@@ -139,7 +139,7 @@ def test_two_ranks_on_csu_kernels_equal_global_batch(tmp_path, dtype, mode):
 
 
 def shared_worker(port, out):
-    """One rank (gloo, world size 1): weights shared by several op calls (LayerNorm, Linear, LePE)
+    """One rank (gloo, world size 1): weights shared by several op calls (LayerNorm, Linear, LePE, conv)
     with a GradAllReduce registered: each call's gradient must be summed, not written twice into the
     bucket slice (_grad_dest refuses parameters used more than once)."""
     import torch.distributed as dist
@@ -157,7 +157,8 @@ def shared_worker(port, out):
           "lw0": 0.1 * torch.randn(C // 2, 1, 3, 3, device=d, generator=g),
           "lb0": 0.1 * torch.randn(C // 2, device=d, generator=g),
           "lw1": 0.1 * torch.randn(C // 2, 1, 3, 3, device=d, generator=g),
-          "lb1": 0.1 * torch.randn(C // 2, device=d, generator=g)}
+          "lb1": 0.1 * torch.randn(C // 2, device=d, generator=g),
+          "cw": 0.05 * torch.randn(C, C, 3, 3, device=d, generator=g), "cb": 0.05 * torch.randn(C, device=d, generator=g)}
     res = {}
     for use_red in (False, True):
         ps = {k: torch.nn.Parameter(v.clone()) for k, v in p0.items()}
@@ -172,7 +173,9 @@ def shared_worker(port, out):
                     qkv = ops.linear(h, ps["w"], ps["b"])
                     o = ops.stripe_attention(qkv.bfloat16().contiguous(), geom, [ps["lw0"], ps["lw1"]],
                                              [ps["lb0"], ps["lb1"]])
-                    loss = loss + (o.float() ** 2).sum()
+                    # a conv weight / bias used by both calls too (conv params count uses)
+                    c = ops.conv2d(o.view(2, reso, reso, C), ps["cw"], ps["cb"], 1, 1)
+                    loss = loss + (o.float() ** 2).sum() + (c.float() ** 2).sum()
             loss.backward()
             if red is not None:
                 red.finish()

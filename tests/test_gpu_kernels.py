@@ -1096,7 +1096,10 @@ def test_linear_wgrad_grouped():
     d = dev()
     g = torch.Generator(device=d).manual_seed(7)
     shapes = [(16384, 768, 256), (16384, 256, 256), (16384, 1024, 256), (16384, 256, 1024), (262144, 192, 64),
-              (65536, 384, 128), (4096, 512, 512), (100, 64, 64), (262144, 64, 64), (4096, 1536, 512)]
+              (65536, 384, 128), (4096, 512, 512), (100, 64, 64), (262144, 64, 64), (4096, 1536, 512),
+              # the C = 64 fc1 / fc2 weight gradients on the rectangular 128x64 / 64x128 group tiles
+              # (WG_RECT), full and with a ragged token count
+              (262144, 256, 64), (262144, 64, 256), (99999, 256, 64), (65537, 64, 128)]
     ops_in = []
     for M, N, K in shapes:
         dy = (torch.randn(M, N, device=d, generator=g) * 0.1).bfloat16()
@@ -1503,6 +1506,16 @@ def test_mlp_fwd_ln_next(C, drop):
     finally:
         ops._launch = real
     assert "layernorm_fwd" not in calls and torch.equal(h.view(-1), pre[3].view(-1))
+    # an in-place change of the output after the launch invalidates the attached LayerNorm
+    with torch.no_grad():
+        y1.mul_(1.0)
+    calls.clear()
+    ops._launch = lambda name, *a, **k: (calls.append(name), real(name, *a, **k))[1]
+    try:
+        ops.layer_norm_fork(y1, ln.weight, ln.bias, ln.eps, torch.bfloat16)
+    finally:
+        ops._launch = real
+    assert "layernorm_fwd" in calls
 
 
 @pytest.mark.parametrize("C", [128, 256])

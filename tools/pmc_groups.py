@@ -82,7 +82,8 @@ def main():
 
     cfg = rec["config"].get("workload", "")
     print(f"# PMC table: {cfg} (batch {rec['config'].get('per_gpu_batch')}, {rec['dtype']})\n")
-    print(f"Counter passes: eager steps of `bench.py --graph off`, {nsteps.get('p1')} steps after the warm-up step; "
+    print(f"Counter passes: eager steps of `bench.py --graph off` (no side stream: the kernels the captured step "
+          f"replays, checked by tools/kernel_match.py), {nsteps.get('p1')} steps after the warm-up step; "
           f"algorithmic bytes: the bench ledger (`{os.path.basename(bj)}`).\n")
     print("## Per C-ABI call (per step)\n")
     print("| ABI call | us/step (p1) | launches | MFMA util | MFMA TFLOP/s | HBM MB (PMC) | algorithmic MB | traffic ratio | HBM GB/s |")

@@ -8,7 +8,7 @@ import json
 import sys
 
 # kernel-name fragment -> ledger name (first match wins)
-GROUPS = [("gemm_ws_kernel", "gemm"), ("frag_layout", "frag_layout"), ("lepe_wgrad", "stripe_attn_bwd"), ("wgrad_tile", "linear_wgrad"), ("wgrad_group", "linear_wgrad"), ("lepe_reduce", "stripe_attn_bwd"), ("wslab_reduce", "linear_wgrad"), ("wgrad_f32", "linear_wgrad"),
+GROUPS = [("head_fold_bwd", "carafe_head_bwd"), ("head_fold_fwd", "head_fold"), ("gemm_ws_kernel", "gemm"), ("frag_layout", "frag_layout"), ("lepe_wgrad", "stripe_attn_bwd"), ("wgrad_tile", "linear_wgrad"), ("wgrad_group", "linear_wgrad"), ("lepe_reduce", "stripe_attn_bwd"), ("wslab_reduce", "linear_wgrad"), ("wgrad_f32", "linear_wgrad"),
           ("stripe_fwd", "stripe_attn_fwd"), ("stripe_bwd", "stripe_attn_bwd"), ("lepe_wgrad", "stripe_attn_bwd"),
           ("stripe_delta", "stripe_attn_bwd"),
           ("gemm4_kernel", "gemm"), ("gemm3_kernel", "gemm"), ("gemm_kernel", "gemm"),
