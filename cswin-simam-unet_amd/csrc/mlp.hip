@@ -244,11 +244,8 @@ template <int V> using iconst = std::integral_constant<int, V>;
 // Forward.  Rings: W1 chunks in 2 stages, W2 chunks in 2 stages.  Step j (after one barrier):
 // DMA W1(j+2), W2(j+1); GEMM1(j+1) on the MFMA pipe while GELU(j) runs on the VALU; GEMM2(j).
 // DROP: hidden / output dropout and DropPath (MlpDrop)
-// TEAMS = 2 (C <= 128): two 4-wave teams, one 64-token panel each, share ONE weight ring -- every
-// streamed weight chunk feeds 128 tokens (half the L2 -> LDS weight bytes per token: the per-CU fill
-// rate bounds these kernels)
-template <int C, bool DROP, bool LN = false, int TEAMS = 1>
-__global__ __launch_bounds__(MT * TEAMS) void mlp_fwd_kernel(long M, const bf16* __restrict__ X, const bf16* __restrict__ W1,
+template <int C, bool DROP, bool LN = false>
+__global__ __launch_bounds__(MT) void mlp_fwd_kernel(long M, const bf16* __restrict__ X, const bf16* __restrict__ W1,
                                                      const float* __restrict__ b1, const bf16* __restrict__ W2,
                                                      const float* __restrict__ b2, const float* __restrict__ res,
                                                      float* __restrict__ out, MlpDrop dd, long rpi, MlpLn ln = MlpLn{}) {
@@ -256,8 +253,7 @@ __global__ __launch_bounds__(MT * TEAMS) void mlp_fwd_kernel(long M, const bf16*
     constexpr int KS = C / 16;          // k-steps of GEMM1
     constexpr int TF = C / 32;          // 32-feature output tiles (all C, partial over the hidden half)
     constexpr int IMG = HC * C;         // bf16 per weight-chunk image (W1 [HC][C] or W2 [C][HC])
-    constexpr int NWV = 4 * TEAMS, NTH = MT * TEAMS;
-    static_assert(TEAMS == 1 || NWV * (C / 64) * 16 * 64 * 4 <= 4 * IMG * 2, "partial-sum exchange must fit the ring");
+    constexpr int NWV = 4, NTH = MT;
     using D1 = Dma<HC, 2 * C, NWV>;
     using D2 = Dma<C, 2 * HC, NWV>;
     __shared__ __attribute__((aligned(1024))) bf16 ring[4 * IMG];
@@ -265,10 +261,10 @@ __global__ __launch_bounds__(MT * TEAMS) void mlp_fwd_kernel(long M, const bf16*
     bf16* const w1r = ring;
     bf16* const w2r = ring + 2 * IMG;
 
-    const long mw = (long)blockIdx.x * BM * TEAMS;   // the workgroup's first token
+    const long mw = (long)blockIdx.x * BM;           // the workgroup's first token
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const long m0 = mw + BM * (wave >> 2);           // this wave's team's panel
+    const long m0 = mw;
     const long rows = M - m0 > 0 ? M - m0 : 0;
     const int r = lane & 31, h = lane >> 5;
     const int t = (wave & 3) >> 1, u = wave & 1;
@@ -687,35 +683,24 @@ int persist_grid(long M) {   // one workgroup (two panel streams) per CU, fewer 
     return (int)(pan < 2L * cus ? (pan + 1) / 2 : cus);
 }
 
-// teams per workgroup of the fused forward: 2 = two 64-token panels on one weight ring (half the
-// streamed weight bytes per token; C = 128: 228 VGPRs, two waves per SIMD).  Measured no faster in the
-// step (mlp_fwd 1176-1180 vs 1180-1182 us/step, profiles/r07zb_mlp_teams_ab.txt): the C = 128 forward
-// is bound by its per-chunk barrier -> GEMM1 -> GELU -> GEMM2 chain, not by weight bytes.  Off.
-#ifndef MLP_FWD_TEAMS
-#define MLP_FWD_TEAMS 1
-#endif
-#ifndef MLP_FWD_TEAMS64
-#define MLP_FWD_TEAMS64 1
-#endif
 template <int C>
 int fwd_launch(long M, const void* x, const void* w1, const float* b1, const void* w2, const float* b2, const float* res,
                float* out, const MlpDrop* d, long rpi, hipStream_t st, const MlpLn* ln = nullptr) {
-    constexpr int T = C == 128 ? MLP_FWD_TEAMS : C == 64 ? MLP_FWD_TEAMS64 : 1;
-    const dim3 grid((unsigned)((M + BM * T - 1) / (BM * T)));
+    const dim3 grid((unsigned)((M + BM - 1) / BM));
     if (ln) {
         if (d)
-            mlp_fwd_kernel<C, true, true, T><<<grid, MT * T, 0, st>>>(M, (const bf16*)x, (const bf16*)w1, b1, (const bf16*)w2, b2,
+            mlp_fwd_kernel<C, true, true><<<grid, MT, 0, st>>>(M, (const bf16*)x, (const bf16*)w1, b1, (const bf16*)w2, b2,
                                                                       res, out, *d, rpi, *ln);
         else
-            mlp_fwd_kernel<C, false, true, T><<<grid, MT * T, 0, st>>>(M, (const bf16*)x, (const bf16*)w1, b1, (const bf16*)w2,
+            mlp_fwd_kernel<C, false, true><<<grid, MT, 0, st>>>(M, (const bf16*)x, (const bf16*)w1, b1, (const bf16*)w2,
                                                                        b2, res, out, MlpDrop{}, rpi, *ln);
         return check_launch("mlp_fwd_ln");
     }
     if (d)
-        mlp_fwd_kernel<C, true, false, T><<<grid, MT * T, 0, st>>>(M, (const bf16*)x, (const bf16*)w1, b1, (const bf16*)w2, b2, res,
+        mlp_fwd_kernel<C, true, false><<<grid, MT, 0, st>>>(M, (const bf16*)x, (const bf16*)w1, b1, (const bf16*)w2, b2, res,
                                                                    out, *d, rpi);
     else
-        mlp_fwd_kernel<C, false, false, T><<<grid, MT * T, 0, st>>>(M, (const bf16*)x, (const bf16*)w1, b1, (const bf16*)w2, b2,
+        mlp_fwd_kernel<C, false, false><<<grid, MT, 0, st>>>(M, (const bf16*)x, (const bf16*)w1, b1, (const bf16*)w2, b2,
                                                                     res, out, MlpDrop{}, rpi);
     return check_launch("mlp_fwd");
 }

@@ -632,19 +632,11 @@ extern "C" int csu_linear_wgrad_deferred(long M, int N, int K, const void* dy, c
 // >= 1024 tokens per chunk.  No occupancy target: the group fills the GPU.
 // slab bytes <= operand bytes * 2 / kSlabDiv (A/B at 512 B16: 8 -> 1231 img/s, 16 -> 1249, 32 -> 1255, 64 -> 1227)
 constexpr int kSlabDiv = 32;
-// WG_SQ256: 256 x 256 tiles (4 waves, one per SIMD, 256 accumulators per lane, one register prefetch
-// set: two spill) when N and K are both multiples of 256 -- 2/3 of the 256 x 128 tile's staged operand
-// bytes per output, but measured slower in the step (linear_wgrad 1533 vs 1419 us/step, 512 B16,
-// profiles/r07v_wgrad_sq256_ab.txt): one wave per SIMD does not keep enough loads in flight.  Off.
-#ifndef WG_SQ256
-#define WG_SQ256 0
-#endif
 // WG_RECT: 128 x 64 / 64 x 128 tiles for the C = 64 Linears whose other side is a multiple of 128
 #ifndef WG_RECT
 #define WG_RECT 1
 #endif
 static void group_plan(long M, int N, int K, int* tn, int* tk, int* chunks, long* rpc) {
-    const bool sq = WG_SQ256 && N % 256 == 0 && K % 256 == 0;
     const int t = (N % 256 == 0 && K % 128 == 0) ? 256 : (N % 128 == 0 && K % 128 == 0) ? 128 : 64;
     long c = (long)((double)M * (N + K) / ((double)kSlabDiv * N * K) + 0.5);
     const long maxc = M / 1024 > 0 ? M / 1024 : 1;
@@ -653,7 +645,7 @@ static void group_plan(long M, int N, int K, int* tn, int* tk, int* chunks, long
     long r = ((M + c - 1) / c + TM - 1) / TM * TM;
     c = (M + r - 1) / r;
     *tn = t;
-    *tk = sq ? 256 : t == 256 ? 128 : t;
+    *tk = t == 256 ? 128 : t;
     if (WG_RECT && t == 64) {   // one 128-wide side where it divides: 3/4 of the 64 x 64 tile's staged bytes per output
         if (N % 128 == 0) *tn = 128;
         else if (K % 128 == 0) *tk = 128;
@@ -677,16 +669,15 @@ extern "C" size_t csu_linear_wgrad_group_plan(long M, int N, int K, int* tn, int
 extern "C" int csu_linear_wgrad_group(const csu_wgrad_group_item* items, int count, void* stream) {
     if (count < 0 || (count && !items)) return fail(CSU_E_ARG, "linear_wgrad_group: bad args");
     hipStream_t st = as_stream(stream);
-    constexpr int kPass[6][2] = {{256, 256}, {256, 128}, {128, 128}, {128, 64}, {64, 128}, {64, 64}};
-    for (int pass = 0; pass < 6; ++pass) {   // one launch per tile shape present
+    constexpr int kPass[5][2] = {{256, 128}, {128, 128}, {128, 64}, {64, 128}, {64, 64}};
+    for (int pass = 0; pass < 5; ++pass) {   // one launch per tile shape present
         const int T = kPass[pass][0], TK = kPass[pass][1];
         WgGroup g;
         g.count = 0;
         g.b0[0] = 0;
         auto flush = [&]() -> int {
             if (!g.count) return 0;
-            if (TK == 256) wgrad_group<256, 256, NT, 1><<<(unsigned)g.b0[g.count], NT, 0, st>>>(g);
-            else if (T == 256) wgrad_group<256, 128, 2 * NT><<<(unsigned)g.b0[g.count], 2 * NT, 0, st>>>(g);
+            if (T == 256) wgrad_group<256, 128, 2 * NT><<<(unsigned)g.b0[g.count], 2 * NT, 0, st>>>(g);
             else if (T == 128 && TK == 128) wgrad_group<128, 128><<<(unsigned)g.b0[g.count], NT, 0, st>>>(g);
             else if (T == 128) wgrad_group<128, 64><<<(unsigned)g.b0[g.count], NT, 0, st>>>(g);
             else if (TK == 128) wgrad_group<64, 128><<<(unsigned)g.b0[g.count], NT, 0, st>>>(g);
