@@ -1508,7 +1508,7 @@ def test_mlp_fwd_ln_next(C, drop):
     assert "layernorm_fwd" not in calls and torch.equal(h.view(-1), pre[3].view(-1))
     # an in-place change of the output after the launch invalidates the attached LayerNorm
     with torch.no_grad():
-        y1.mul_(1.0)
+        y1.detach().mul_(1.0)     # shares y1's version counter
     calls.clear()
     ops._launch = lambda name, *a, **k: (calls.append(name), real(name, *a, **k))[1]
     try:
