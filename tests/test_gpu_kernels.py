@@ -1507,12 +1507,14 @@ def test_mlp_fwd_ln_next(C, drop):
         ops._launch = real
     assert "layernorm_fwd" not in calls and torch.equal(h.view(-1), pre[3].view(-1))
     # an in-place change of the output after the launch invalidates the attached LayerNorm
-    with torch.no_grad():
-        y1.detach().mul_(1.0)     # shares y1's version counter
+    # (autograd itself forbids using an in-place-modified view output of a custom Function with grad
+    # enabled; the stale-stash case is a no_grad one)
     calls.clear()
     ops._launch = lambda name, *a, **k: (calls.append(name), real(name, *a, **k))[1]
     try:
-        ops.layer_norm_fork(y1, ln.weight, ln.bias, ln.eps, torch.bfloat16)
+        with torch.no_grad():
+            y1.detach().mul_(1.0)     # shares y1's version counter
+            ops.layer_norm_fork(y1, ln.weight, ln.bias, ln.eps, torch.bfloat16)
     finally:
         ops._launch = real
     assert "layernorm_fwd" in calls
