@@ -683,10 +683,237 @@ int persist_grid(long M) {   // one workgroup (two panel streams) per CU, fewer 
     return (int)(pan < 2L * cus ? (pan + 1) / 2 : cus);
 }
 
+// ================================================================================================
+// Forward at C = 256 with two waves per SIMD (mlp_fwd8_kernel; no dropout: DROP launches keep the
+// 4-wave kernel).  The 4-wave kernel keeps a C x 32 partial output per wave (128 accumulator
+// registers) so that every wave needs every hidden feature of its token half, and one wave per SIMD
+// runs the whole barrier -> GEMM1 -> GELU -> GEMM2 chain serially (profiles/r08b_mlp_ablate.txt:
+// removing the DMA, the GELU or the MFMAs each saves 6-10 of 41 us, none dominates).  Here the
+// hidden activations go through LDS, which splits the two GEMMs differently:
+//  * GEMM1 + GELU: wave (tg, hq) = (wave >> 2, wave & 3) computes h = W1 x^T for the 16 hidden
+//    features 16 hq .. of every 64-feature chunk and the 32 tokens 32 tg .. on 16x16x32 MFMAs (x as
+//    B fragments in registers, W1 rows as A fragments from the ring), applies bias + GELU and writes
+//    g (bf16) into a [64 tokens][64 hidden] LDS image (double-buffered by chunk parity);
+//  * GEMM2: wave w owns the output features 32 w .. 32 w + 31 for all 64 tokens (two 32x32x16 tiles,
+//    K = the chunk's 64 hidden): A = W2 rows from the ring, B = g from the LDS image -- no partial
+//    outputs to exchange at the end, 32 accumulator registers per token tile.
+// ~220 VGPRs: two waves per SIMD.  Step j (one barrier): DMA W1(j+1), W2(j); GEMM1 + GELU of chunk j;
+// GEMM2 of chunk j-1.  LDS per step and CU: 160 KB of fragment reads + 64 KB of DMA (256 B/clk: ~900
+// cycles) against 1024 MFMA cycles per SIMD.
+template <int C, bool LN>
+__global__ __launch_bounds__(2 * MT) void mlp_fwd8_kernel(long M, const bf16* __restrict__ X, const bf16* __restrict__ W1,
+                                                          const float* __restrict__ b1, const bf16* __restrict__ W2,
+                                                          const float* __restrict__ b2, const float* __restrict__ res,
+                                                          float* __restrict__ out, long rpi, MlpLn ln) {
+    static_assert(C == 256, "mlp_fwd8: C = 256 (32 output features per wave)");
+    constexpr int NCH = 4 * C / HC;     // hidden chunks
+    constexpr int IMG = HC * C;         // bf16 per weight-chunk image
+    constexpr int NWV = 8, NTH = 2 * MT;
+    constexpr int KS = C / 32;          // GEMM1 k-steps (16x16x32)
+    using D1 = Dma<HC, 2 * C, NWV>;
+    using D2 = Dma<C, 2 * HC, NWV>;
+    __shared__ __attribute__((aligned(1024))) bf16 ring[4 * IMG];     // W1 x 2 | W2 x 2 stages
+    __shared__ __attribute__((aligned(1024))) bf16 gimg[2][BM * HC];  // g of a chunk: [token][hidden]
+    __shared__ __attribute__((aligned(16))) float b1s[4 * C];
+    __shared__ __attribute__((aligned(16))) float lngb[LN ? 2 * C : 4];
+    bf16* const w1r = ring;
+    bf16* const w2r = ring + 2 * IMG;
+
+    const long m0 = (long)blockIdx.x * BM;
+    const long rows = M - m0 > 0 ? M - m0 : 0;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int tg = wave >> 2, hq = wave & 3;        // GEMM1 role
+    const int l16 = lane & 15, q4 = lane >> 4;      // 16x16x32 lane split
+    const int r = lane & 31, h = lane >> 5;         // 32x32x16 lane split
+    const int fo = 32 * wave;                       // GEMM2 role: output features fo .. fo + 31
+    const int j0 = kRot && rpi > 0 && rpi % BM == 0 ? (int)(((m0 % rpi) / BM) & (NCH - 1)) : 0;
+    auto chk = [&](int j) { return (j + j0) & (NCH - 1); };
+    for (int i = threadIdx.x; i < 4 * C; i += NTH) b1s[i] = b1[i];
+    if constexpr (LN)
+        for (int i = threadIdx.x; i < 2 * C; i += NTH) lngb[i] = i < C ? ln.gamma[i] : ln.beta[i - C];
+
+    // x as 16x16x32 B fragments: token 32 tg + 16 tt + l16, k = 32 s + 8 q4 .. + 7
+    bf16x8 xf[2][KS];
+    {
+        const auto rs_x = buf_rsrc(X + m0 * C, rows * C * 2);
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt) {
+            const int tok = 32 * tg + 16 * tt + l16;
+#pragma unroll
+            for (int s = 0; s < KS; ++s) {
+                const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(
+                    rs_x, tok < rows ? (unsigned)(tok * C + 32 * s + 8 * q4) * 2 : kOOB, 0, 0);
+                __builtin_memcpy(&xf[tt][s], &v, 16);
+            }
+        }
+    }
+    D1 d1;
+    D2 d2;
+    d1.init(C, wave, lane);
+    d2.init(4 * C, wave, lane);
+    const i32x4 rs_w1 = rsrc4(W1, 4L * C * C * 2);
+    const i32x4 rs_w2 = rsrc4(W2, 4L * C * C * 2);
+    asm volatile("" ::: "memory");
+    dma<D1::NW>(rs_w1, d1.v, (unsigned)chk(0) * HC * C * 2, w1r, wave);
+
+    f32x16 acc[2];
+    acc[0] = f32x16{};
+    acc[1] = f32x16{};
+
+    // chunk j: h for (16 hidden of hq) x (32 tokens of tg), bias + GELU, g -> gimg[j & 1]
+    auto gemm1 = [&](int j) {
+        const bf16* w1c = w1r + (j & 1) * IMG;
+        bf16x8 wf[KS];
+#pragma unroll
+        for (int s = 0; s < KS; ++s) wf[s] = frag(w1c, moff<2 * C>(16 * hq + l16, 32 * s + 8 * q4));
+        f32x4 ha = f32x4{}, hb = f32x4{};
+#pragma unroll
+        for (int s = 0; s < KS; ++s) {
+            ha = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[s], xf[0][s], ha, 0, 0, 0);
+            hb = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[s], xf[1][s], hb, 0, 0, 0);
+        }
+        const f32x4 bv = *reinterpret_cast<const f32x4*>(b1s + chk(j) * HC + 16 * hq + 4 * q4);
+        bf16* gi = gimg[j & 1];
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt) {
+            const f32x4& hv = tt ? hb : ha;
+            bf16x4 gq;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) gq[e] = (bf16)gelu_fast(hv[e] + bv[e]);
+            // token 32 tg + 16 tt + l16, hidden 16 hq + 4 q4 .. + 3
+            *reinterpret_cast<bf16x4*>(gi + moff<2 * HC>(32 * tg + 16 * tt + l16, 16 * hq + 4 * q4)) = gq;
+        }
+    };
+    // chunk j: acc[tt] += W2[fo .. fo + 31][chunk] g[chunk][32 tt ..]
+    auto gemm2 = [&](int j) {
+        const bf16* w2c = w2r + (j & 1) * IMG;
+        const bf16* gi = gimg[j & 1];
+        bf16x8 af[4], bf[2][4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            af[s] = frag(w2c, moff<2 * HC>(fo + r, 16 * s + 8 * h));
+            bf[0][s] = frag(gi, moff<2 * HC>(r, 16 * s + 8 * h));
+            bf[1][s] = frag(gi, moff<2 * HC>(32 + r, 16 * s + 8 * h));
+        }
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[s], bf[0][s], acc[0], 0, 0, 0);
+            acc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[s], bf[1][s], acc[1], 0, 0, 0);
+        }
+    };
+
+    vmwait<0>();
+    lds_sync();
+    // step 0: W1(1), W2(0) in flight; chunk 0's GEMM1
+    dma<D1::NW>(rs_w1, d1.v, (unsigned)chk(1) * HC * C * 2, w1r + IMG, wave);
+    dma<D2::NW>(rs_w2, d2.v, (unsigned)chk(0) * HC * 2, w2r, wave);
+    gemm1(0);
+    for (int j = 1; j < NCH; ++j) {
+        vmwait<0>();                    // W1(j), W2(j-1): issued one step ago
+        lds_sync();                     // every wave is past step j-1 (its stages and g image are free)
+        if (j + 1 < NCH) dma<D1::NW>(rs_w1, d1.v, (unsigned)chk(j + 1) * HC * C * 2, w1r + ((j + 1) & 1) * IMG, wave);
+        dma<D2::NW>(rs_w2, d2.v, (unsigned)chk(j) * HC * 2, w2r + (j & 1) * IMG, wave);
+        gemm1(j);
+        gemm2(j - 1);
+    }
+    vmwait<0>();
+    lds_sync();
+    gemm2(NCH - 1);
+
+    // epilogue: lane holds token 32 tt + r, features fo + 8 g + 4 h + 0..3 in acc[tt][4 g + e]
+    const auto rs_res = buf_rsrc(res + m0 * C, rows * C * 4);
+    const auto rs_out = buf_rsrc(out + m0 * C, rows * C * 4);
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt) {
+        const int tok = 32 * tt + r;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int f = fo + 8 * g + 4 * h;
+            const unsigned off = tok < rows ? (unsigned)(tok * C + f) * 4 : kOOB;
+            float rv[4], v[4];
+            buf_ld4(rs_res, off, rv);
+            const f32x4 bv = *reinterpret_cast<const f32x4*>(b2 + f);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                v[e] = acc[tt][4 * g + e] + bv[e] + rv[e];
+                acc[tt][4 * g + e] = v[e];
+            }
+            buf_st4(rs_out, off, v);
+        }
+    }
+    if constexpr (LN) {
+        // the next block's norm1 over the token's C values, spread over the 8 waves: two passes
+        // (mean, centred squares) through an LDS [wave][token] table in the (now free) ring
+        float* red = reinterpret_cast<float*>(ring);
+        float mu[2], rs[2];
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt) {
+            float s = 0.f;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) s += acc[tt][i];
+            s = xsum32(s);
+            if (h == 0) red[wave * 64 + 32 * tt + r] = s;
+        }
+        lds_sync();
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt) {
+            float s = 0.f;
+#pragma unroll
+            for (int w = 0; w < NWV; ++w) s += red[w * 64 + 32 * tt + r];
+            mu[tt] = s * (1.f / C);
+            float q = 0.f;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const float d = acc[tt][i] - mu[tt];
+                q += d * d;
+            }
+            q = xsum32(q);
+            if (h == 0) red[NWV * 64 + wave * 64 + 32 * tt + r] = q;
+        }
+        lds_sync();
+        const auto rs_ln = buf_rsrc(ln.out + m0 * C, rows * C * 2);
+        const auto rs_mean = buf_rsrc(ln.mean + m0, rows * 4), rs_rstd = buf_rsrc(ln.rstd + m0, rows * 4);
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt) {
+            float q = 0.f;
+#pragma unroll
+            for (int w = 0; w < NWV; ++w) q += red[NWV * 64 + w * 64 + 32 * tt + r];
+            rs[tt] = rsqrtf(q * (1.f / C) + ln.eps);
+            const int tok = 32 * tt + r;
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int f = fo + 8 * g + 4 * h;
+                const f32x4 gw = *reinterpret_cast<const f32x4*>(lngb + f);
+                const f32x4 bw = *reinterpret_cast<const f32x4*>(lngb + C + f);
+                float o[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) o[e] = (acc[tt][4 * g + e] - mu[tt]) * rs[tt] * gw[e] + bw[e];
+                buf_st4bf(rs_ln, tok < rows ? (unsigned)(tok * C + f) * 2 : kOOB, o);
+            }
+            if (wave == 0 && h == 0) {
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(mu[tt]), rs_mean, tok < rows ? (unsigned)tok * 4 : kOOB, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(rs[tt]), rs_rstd, tok < rows ? (unsigned)tok * 4 : kOOB, 0, 0);
+            }
+        }
+    }
+}
+
 template <int C>
 int fwd_launch(long M, const void* x, const void* w1, const float* b1, const void* w2, const float* b2, const float* res,
                float* out, const MlpDrop* d, long rpi, hipStream_t st, const MlpLn* ln = nullptr) {
     const dim3 grid((unsigned)((M + BM - 1) / BM));
+    if constexpr (C == 256) {
+        if (!d) {   // two waves per SIMD (dropout launches keep the 4-wave kernel)
+            if (ln)
+                mlp_fwd8_kernel<C, true><<<grid, 2 * MT, 0, st>>>(M, (const bf16*)x, (const bf16*)w1, b1, (const bf16*)w2, b2,
+                                                                   res, out, rpi, *ln);
+            else
+                mlp_fwd8_kernel<C, false><<<grid, 2 * MT, 0, st>>>(M, (const bf16*)x, (const bf16*)w1, b1, (const bf16*)w2, b2,
+                                                                    res, out, rpi, MlpLn{});
+            return check_launch(ln ? "mlp_fwd_ln" : "mlp_fwd");
+        }
+    }
     if (ln) {
         if (d)
             mlp_fwd_kernel<C, true, true><<<grid, MT, 0, st>>>(M, (const bf16*)x, (const bf16*)w1, b1, (const bf16*)w2, b2,
