@@ -899,6 +899,208 @@ __global__ __launch_bounds__(2 * MT) void mlp_fwd8_kernel(long M, const bf16* __
     }
 }
 
+// Backward at C = 256 with two waves per SIMD (mlp_bwd8_kernel; no dropout: DROP launches keep the
+// 4-wave kernel).  The 4-wave kernel holds x, dY (64 + 64 registers) and a C x 32 partial dX (128) per
+// wave, so at C = 256 it runs one wave per SIMD with no overlap between chunks (PIPE off); removing
+// its DMA, MFMAs or g / dH stores each saved 11-17 of 60 us (profiles/r08b_mlp_ablate.txt).  Here
+// per 64-hidden chunk, three phases separated by barriers, both waves of a SIMD busy in each:
+//  A  waves 0-3: h = W1 x^T + b1 for (32 hidden of hh) x (32 tokens of tg) on 16x16x32 MFMAs (x in
+//     registers); waves 4-7: dg = W2^T dY^T for the same tiles (dY in registers, W2 read transposed);
+//     both written as bf16 (the reference's autocast rounds fc1's output and fc2's input gradient to
+//     bf16 as well) into [token][hidden] LDS images;
+//  B  all 512 threads: 8 consecutive hidden features of one token each -- g = gelu(h), dH = dg gelu'(h),
+//     16-B stores of g and dH (the weight-gradient operands) and dH into an LDS image;
+//  C  dX += W1^T dH: wave w owns the dX features 32 w .. for all 64 tokens (32x32x16, W1 read
+//     transposed from the ring) -- no partial outputs to exchange.
+// The next chunk's W1 / W2 land during the three phases (2-stage ring).
+#ifndef MLP_BWD8
+#define MLP_BWD8 1
+#endif
+constexpr bool kMlpBwd8 = MLP_BWD8;
+template <int C>
+__global__ __launch_bounds__(2 * MT) void mlp_bwd8_kernel(long M, const bf16* __restrict__ X, const bf16* __restrict__ dY,
+                                                          const bf16* __restrict__ W1, const float* __restrict__ b1,
+                                                          const bf16* __restrict__ W2, bf16* __restrict__ dH,
+                                                          bf16* __restrict__ G, bf16* __restrict__ dX, long rpi) {
+    static_assert(C == 256, "mlp_bwd8: C = 256 (32 dX features per wave)");
+    constexpr int NCH = 4 * C / HC;
+    constexpr int IMG = HC * C;
+    constexpr int NWV = 8, NTH = 2 * MT;
+    constexpr int KS = C / 32;          // k-steps of GEMM1 / GEMM3 (16x16x32)
+    using D1 = Dma<HC, 2 * C, NWV>;
+    using D2 = Dma<C, 2 * HC, NWV>;
+    __shared__ __attribute__((aligned(1024))) bf16 ring[4 * IMG];      // W1 x 2 | W2 x 2 stages
+    __shared__ __attribute__((aligned(1024))) bf16 himg[BM * HC];      // h + b1 (bf16), [token][hidden]
+    __shared__ __attribute__((aligned(1024))) bf16 dgimg[BM * HC];     // dg
+    __shared__ __attribute__((aligned(1024))) bf16 dhimg[BM * HC];     // dH
+    __shared__ __attribute__((aligned(16))) float b1s[4 * C];
+    bf16* const w1r = ring;
+    bf16* const w2r = ring + 2 * IMG;
+
+    const long m0 = (long)blockIdx.x * BM;
+    const long rows = M - m0 > 0 ? M - m0 : 0;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const bool g1 = wave < 4;                       // GEMM1 (h) or GEMM3 (dg) role in phase A
+    const int tg = (wave >> 1) & 1, hh = wave & 1;  // phase A tile: tokens 32 tg .., hidden 32 hh ..
+    const int l16 = lane & 15, q4 = lane >> 4;
+    const int r = lane & 31, h = lane >> 5;
+    const int fo = 32 * wave;                       // phase C: dX features fo .. fo + 31
+    const int j0 = kRot && rpi > 0 && rpi % BM == 0 ? (int)(((m0 % rpi) / BM) & (NCH - 1)) : 0;
+    auto chk = [&](int j) { return (j + j0) & (NCH - 1); };
+    for (int i = threadIdx.x; i < 4 * C; i += NTH) b1s[i] = b1[i];
+
+    // phase-A token operand as 16x16x32 B fragments: x (GEMM1 waves) or dY (GEMM3 waves)
+    bf16x8 tf[2][KS];
+    {
+        const auto rs_t = buf_rsrc((g1 ? X : dY) + m0 * C, rows * C * 2);
+#pragma unroll
+        for (int tt = 0; tt < 2; ++tt) {
+            const int tok = 32 * tg + 16 * tt + l16;
+#pragma unroll
+            for (int s = 0; s < KS; ++s) {
+                const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(
+                    rs_t, tok < rows ? (unsigned)(tok * C + 32 * s + 8 * q4) * 2 : kOOB, 0, 0);
+                __builtin_memcpy(&tf[tt][s], &v, 16);
+            }
+        }
+    }
+    D1 d1;
+    D2 d2;
+    d1.init(C, wave, lane);
+    d2.init(4 * C, wave, lane);
+    const i32x4 rs_w1 = rsrc4(W1, 4L * C * C * 2);
+    const i32x4 rs_w2 = rsrc4(W2, 4L * C * C * 2);
+    const auto rs_dh = buf_rsrc(dH + m0 * 4 * C, rows * 4 * C * 2);
+    const auto rs_g = buf_rsrc(G + m0 * 4 * C, rows * 4 * C * 2);
+    asm volatile("" ::: "memory");
+    dma<D1::NW>(rs_w1, d1.v, (unsigned)chk(0) * HC * C * 2, w1r, wave);
+    dma<D2::NW>(rs_w2, d2.v, (unsigned)chk(0) * HC * 2, w2r, wave);
+
+    f32x16 acc[2];
+    acc[0] = f32x16{};
+    acc[1] = f32x16{};
+    // phase B element of this thread: token tb, hidden 8 hb .. 8 hb + 7 of the chunk
+    const int tb = threadIdx.x >> 3, hb = threadIdx.x & 7;
+
+    for (int j = 0; j < NCH; ++j) {
+        const int jc = chk(j);
+        // chunk j landed; after its DMA this thread issued only chunk j-1's two phase-B stores
+        if (j == 0) vmwait<0>(); else vmwait<2>();
+        lds_sync();                     // every wave is past chunk j-1 (stages, images free)
+        if (j + 1 < NCH) {
+            dma<D1::NW>(rs_w1, d1.v, (unsigned)chk(j + 1) * HC * C * 2, w1r + ((j + 1) & 1) * IMG, wave);
+            dma<D2::NW>(rs_w2, d2.v, (unsigned)chk(j + 1) * HC * 2, w2r + ((j + 1) & 1) * IMG, wave);
+        }
+        // ---- phase A
+        {
+            f32x4 a[2][2];
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+                for (int tt = 0; tt < 2; ++tt) a[mt][tt] = f32x4{};
+            if (g1) {
+                const bf16* w1c = w1r + (j & 1) * IMG;
+#pragma unroll
+                for (int mt = 0; mt < 2; ++mt) {
+                    bf16x8 wf[KS];
+#pragma unroll
+                    for (int s = 0; s < KS; ++s) wf[s] = frag(w1c, moff<2 * C>(32 * hh + 16 * mt + l16, 32 * s + 8 * q4));
+#pragma unroll
+                    for (int s = 0; s < KS; ++s) {
+                        a[mt][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[s], tf[0][s], a[mt][0], 0, 0, 0);
+                        a[mt][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[s], tf[1][s], a[mt][1], 0, 0, 0);
+                    }
+                }
+            } else {
+                const bf16* w2c = w2r + (j & 1) * IMG;
+                const int grp = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+#pragma unroll
+                for (int mt = 0; mt < 2; ++mt) {
+                    // A[m = hidden 32 hh + 16 mt + l16][k = 32 s + 8 q4 ..]: W2 image rows k, columns m
+                    bf16x8 wf[KS];
+                    const int col = 32 * hh + 16 * mt + 4 * p;
+#pragma unroll
+                    for (int s = 0; s < KS; ++s) {
+                        const int row = 32 * s + 8 * grp + q;
+                        wf[s] = cat8(tr4(w2c + moff<2 * HC>(row, col)), tr4(w2c + moff<2 * HC>(row + 4, col)));
+                    }
+#pragma unroll
+                    for (int s = 0; s < KS; ++s) {
+                        a[mt][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[s], tf[0][s], a[mt][0], 0, 0, 0);
+                        a[mt][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[s], tf[1][s], a[mt][1], 0, 0, 0);
+                    }
+                }
+            }
+            // D[m = 4 q4 + i][n = l16]: hidden 32 hh + 16 mt + 4 q4 + i, token 32 tg + 16 tt + l16
+            bf16* img = g1 ? himg : dgimg;
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt) {
+                const int hf = 32 * hh + 16 * mt + 4 * q4;
+                f32x4 bv = f32x4{};
+                if (g1) bv = *reinterpret_cast<const f32x4*>(b1s + jc * HC + hf);
+#pragma unroll
+                for (int tt = 0; tt < 2; ++tt) {
+                    bf16x4 o;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) o[e] = (bf16)(a[mt][tt][e] + bv[e]);
+                    *reinterpret_cast<bf16x4*>(img + moff<2 * HC>(32 * tg + 16 * tt + l16, hf)) = o;
+                }
+            }
+        }
+        lds_sync();
+        // ---- phase B
+        {
+            const bf16x8 hv = frag(himg, moff<2 * HC>(tb, 8 * hb));
+            const bf16x8 dv = frag(dgimg, moff<2 * HC>(tb, 8 * hb));
+            float gv[8], dd[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                float dg;
+                gelu_pair_fast((float)hv[e], gv[e], dg);
+                dd[e] = (float)dv[e] * dg;
+            }
+            const unsigned o = tb < rows ? (unsigned)(tb * 4 * C + jc * HC + 8 * hb) * 2 : kOOB;
+            buf_st8bf(rs_g, o, gv);
+            buf_st8bf(rs_dh, o, dd);
+            bf16x8 db;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) db[e] = (bf16)dd[e];
+            *reinterpret_cast<bf16x8*>(dhimg + moff<2 * HC>(tb, 8 * hb)) = db;
+        }
+        lds_sync();
+        // ---- phase C: acc[tt] += W1[chunk]^T[fo ..][hidden] dH[hidden][32 tt ..]
+        {
+            const bf16* w1c = w1r + (j & 1) * IMG;
+            bf16x8 af[4], bf[2][4];
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                af[s] = trfrag<2 * C>(w1c, fo, s, lane);
+                bf[0][s] = frag(dhimg, moff<2 * HC>(r, 16 * s + 8 * h));
+                bf[1][s] = frag(dhimg, moff<2 * HC>(32 + r, 16 * s + 8 * h));
+            }
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[s], bf[0][s], acc[0], 0, 0, 0);
+                acc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[s], bf[1][s], acc[1], 0, 0, 0);
+            }
+        }
+    }
+    // dX: lane holds token 32 tt + r, features fo + 8 g + 4 h + 0..3
+    const auto rs_dx = buf_rsrc(dX + m0 * C, rows * C * 2);
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt) {
+        const int tok = 32 * tt + r;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            float v[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = acc[tt][4 * g + e];
+            buf_st4bf(rs_dx, tok < rows ? (unsigned)(tok * C + fo + 8 * g + 4 * h) * 2 : kOOB, v);
+        }
+    }
+}
+
 template <int C>
 int fwd_launch(long M, const void* x, const void* w1, const float* b1, const void* w2, const float* b2, const float* res,
                float* out, const MlpDrop* d, long rpi, hipStream_t st, const MlpLn* ln = nullptr) {
@@ -936,6 +1138,13 @@ template <int C>
 int bwd_launch(long M, const void* x, const void* dy, const void* w1, const float* b1, const void* w2, void* dh, void* g,
                void* dx, const MlpDrop* d, long rpi, hipStream_t st) {
     const dim3 grid((unsigned)((M + BM - 1) / BM));
+    if constexpr (C == 256) {
+        if (!d && kMlpBwd8) {   // two waves per SIMD (dropout launches keep the 4-wave kernel)
+            mlp_bwd8_kernel<C><<<grid, 2 * MT, 0, st>>>(M, (const bf16*)x, (const bf16*)dy, (const bf16*)w1, b1, (const bf16*)w2,
+                                                        (bf16*)dh, (bf16*)g, (bf16*)dx, rpi);
+            return check_launch("mlp_bwd");
+        }
+    }
     if constexpr (C == 64) {   // persistent, weights resident (mlp_bwd64_persist)
         const dim3 pg((unsigned)persist_grid(M));
         if (d)

@@ -21,10 +21,36 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(os.path.dirname(HERE))
 CSRC = os.path.join(REPO, "cswin-simam-unet_amd", "csrc")
 OUT = os.path.join(HERE, "mlp_abl")
-VARIANTS = ["base", "nodma", "nosync", "nogelu", "nomfma", "nostore"]
+# round 6 set: "old" = the 4-wave kernels (the ablations of those, base / nodma / nosync / nogelu / nomfma /
+# nostore, are in profiles/r08b_mlp_ablate.txt), "w8" = the 8-wave kernels as built, and their ablations
+VARIANTS = ["old", "w8", "w8_nodma", "w8_nomfma", "w8_dmaonly"]
+OLD_ONLY = ("base", "nodma", "nosync", "nogelu", "nomfma", "nostore", "old")
 
 
 def edit(src: str, v: str) -> str:
+    if v == "w8":
+        return src
+    if v in OLD_ONLY:   # C = 256 dispatches to the 4-wave kernels
+        src = src.replace("if (!d) {   // two waves per SIMD", "if (false) {   // two waves per SIMD")
+        src = src.replace("#define MLP_BWD8 1", "#define MLP_BWD8 0")
+    if v.startswith("w8_"):   # the 8-wave C = 256 kernels (mlp_fwd8_kernel / mlp_bwd8_kernel)
+        a = src.index("// Forward at C = 256 with two waves per SIMD")
+        b = src.index("template <int C>\nint fwd_launch(")
+        body = src[a:b]
+        if v == "w8_nodma":
+            body = body.replace("if (j + 1 < NCH) dma<D1::NW>", "if (false) dma<D1::NW>")
+            body = body.replace("dma<D2::NW>(rs_w2, d2.v, (unsigned)chk(j) * HC * 2", "if (false) dma<D2::NW>(rs_w2, d2.v, (unsigned)chk(j) * HC * 2")
+            body = body.replace("if (j + 1 < NCH) {\n            dma", "if (false) {\n            dma")
+        if v in ("w8_nomfma", "w8_dmaonly"):
+            body = re.sub(r"(\w+(?:\[\w+\])*) = __builtin_amdgcn_mfma_f32_(?:32x32x16|16x16x32)_bf16\(([^;]*?), ([\w\[\]]+), \1, 0, 0, 0\);",
+                          r'asm volatile("" :: "v"(\2), "v"(\3));', body)
+        if v == "w8_dmaonly":     # DMA + barriers only: no fragment reads, no GELU, no phase work
+            body = body.replace("        gemm1(j);\n        gemm2(j - 1);\n", "")
+            body = body.replace("    gemm1(0);\n", "").replace("    gemm2(NCH - 1);\n", "")
+            for ph in ("// ---- phase A\n        {", "// ---- phase B\n        {", "// ---- phase C: acc[tt] += W1[chunk]^T[fo ..][hidden] dH[hidden][32 tt ..]\n        {"):
+                assert ph in body, ph
+                body = body.replace(ph, ph.replace("{", "if (M < 0) {"))
+        return src[:a] + body + src[b:]
     a = src.index("__global__ __launch_bounds__(MT) void mlp_fwd_kernel")
     b = src.index("// Persistent backward for C = 64")
     body = src[a:b]
@@ -59,7 +85,7 @@ def build():
     subprocess.run(["hipcc", *flags, "-x", "hip", "-c", os.path.join(CSRC, "common.cpp"), "-o", common], check=True)
     for v in VARIANTS:
         s = edit(src, v)
-        if v != "base":
+        if v != "w8":
             assert s != src, v
         p = os.path.join(OUT, f"mlp_{v}.hip")
         open(p, "w").write(s)

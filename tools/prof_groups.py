@@ -13,7 +13,7 @@ GROUPS = [("head_fold_bwd", "carafe_head_bwd"), ("head_fold_fwd", "head_fold"), 
           ("stripe_delta", "stripe_attn_bwd"),
           ("gemm4_kernel", "gemm"), ("gemm3_kernel", "gemm"), ("gemm_kernel", "gemm"),
           ("ln_fwd", "layernorm_fwd"), ("ln_bwd", "layernorm_bwd"), ("ln_param_reduce", "layernorm_bwd"),
-          ("mlp_fwd_kernel", "mlp_fwd"), ("mlp_bwd_kernel", "mlp_bwd"), ("mlp_bwd64_persist", "mlp_bwd"), ("mlp_bwd_deep", "mlp_bwd"), ("mlp_fwd_deep", "mlp_fwd"), ("mlp_fp8_fwd", "mlp_fwd"), ("mlp_fp8_bwd", "mlp_bwd"),
+          ("mlp_fwd_kernel", "mlp_fwd"), ("mlp_bwd_kernel", "mlp_bwd"), ("mlp_fwd8_kernel", "mlp_fwd"), ("mlp_bwd8_kernel", "mlp_bwd"), ("mlp_bwd64_persist", "mlp_bwd"), ("mlp_bwd_deep", "mlp_bwd"), ("mlp_fwd_deep", "mlp_fwd"), ("mlp_fp8_fwd", "mlp_fwd"), ("mlp_fp8_bwd", "mlp_bwd"),
           ("conv_wgrad", "conv_wgrad"), ("conv3_wgrad_halo", "conv_wgrad"), ("igemm_bf16", "conv_fwd+conv_dgrad"),
           ("igemm_dma", "conv_fwd+conv_dgrad"), ("conv3_halo64", "conv_fwd+conv_dgrad"), ("conv3_c16", "conv_fwd+conv_dgrad"), ("conv3_c16d", "conv_fwd+conv_dgrad"), ("conv_split_reduce", "conv_fwd+conv_dgrad"), ("conv_gemm", "conv_fwd+conv_dgrad"),
           ("bn_stats", "bn_relu_fwd"), ("bn_apply", "bn_relu_fwd"), ("bn_grad", "bn_relu_bwd"), ("maxpool2_fwd", "maxpool2_fwd"),
