@@ -700,30 +700,40 @@ int persist_grid(long M) {   // one workgroup (two panel streams) per CU, fewer 
 // ~220 VGPRs: two waves per SIMD.  Step j (one barrier): DMA W1(j+1), W2(j); GEMM1 + GELU of chunk j;
 // GEMM2 of chunk j-1.  LDS per step and CU: 160 KB of fragment reads + 64 KB of DMA (256 B/clk: ~900
 // cycles) against 1024 MFMA cycles per SIMD.
-template <int C, bool LN>
+// HCK = 32 (default, MLP_FWD8_HC): 32-hidden chunks through a 4-stage ring (the same 128 KB), so the
+// weight DMA runs up to three chunks ahead instead of one: the DMA stream alone takes 22 of the 38 us
+// at HCK = 64 with one chunk of prefetch (w8_dmaonly in profiles/r08e_mlp_ablate.txt).  Then GEMM1's
+// wave tile is 16 hidden x 16 tokens (one token tile) and GEMM2's K is 32.
+template <int C, bool LN, int HCK>
 __global__ __launch_bounds__(2 * MT) void mlp_fwd8_kernel(long M, const bf16* __restrict__ X, const bf16* __restrict__ W1,
                                                           const float* __restrict__ b1, const bf16* __restrict__ W2,
                                                           const float* __restrict__ b2, const float* __restrict__ res,
                                                           float* __restrict__ out, long rpi, MlpLn ln) {
     static_assert(C == 256, "mlp_fwd8: C = 256 (32 output features per wave)");
-    constexpr int NCH = 4 * C / HC;     // hidden chunks
-    constexpr int IMG = HC * C;         // bf16 per weight-chunk image
+    static_assert(HCK == 64 || HCK == 32, "mlp_fwd8: 64- or 32-hidden chunks");
+    constexpr int NCH = 4 * C / HCK;    // hidden chunks
+    constexpr int IMG = HCK * C;        // bf16 per weight-chunk image
+    constexpr int NST = 128 * 1024 / (4 * IMG);   // ring stages per matrix (2 at HCK 64, 4 at 32)
     constexpr int NWV = 8, NTH = 2 * MT;
     constexpr int KS = C / 32;          // GEMM1 k-steps (16x16x32)
-    using D1 = Dma<HC, 2 * C, NWV>;
-    using D2 = Dma<C, 2 * HC, NWV>;
-    __shared__ __attribute__((aligned(1024))) bf16 ring[4 * IMG];     // W1 x 2 | W2 x 2 stages
-    __shared__ __attribute__((aligned(1024))) bf16 gimg[2][BM * HC];  // g of a chunk: [token][hidden]
+    constexpr int HG = HCK / 16;        // GEMM1 hidden groups of 16 per chunk
+    constexpr int TT = 4 / (NWV / HG);  // GEMM1 16-token tiles per wave (2 at HCK 64, 1 at 32)
+    constexpr int K2 = HCK / 16;        // GEMM2 k-steps per chunk
+    using D1 = Dma<HCK, 2 * C, NWV>;
+    using D2 = Dma<C, 2 * HCK, NWV>;
+    constexpr int DPS = D1::NW + D2::NW;   // DMA instructions per wave per step
+    __shared__ __attribute__((aligned(1024))) bf16 ring[2 * NST * IMG];   // W1 x NST | W2 x NST stages
+    __shared__ __attribute__((aligned(1024))) bf16 gimg[2][BM * HCK];    // g of a chunk: [token][hidden]
     __shared__ __attribute__((aligned(16))) float b1s[4 * C];
     __shared__ __attribute__((aligned(16))) float lngb[LN ? 2 * C : 4];
     bf16* const w1r = ring;
-    bf16* const w2r = ring + 2 * IMG;
+    bf16* const w2r = ring + NST * IMG;
 
     const long m0 = (long)blockIdx.x * BM;
     const long rows = M - m0 > 0 ? M - m0 : 0;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int tg = wave >> 2, hq = wave & 3;        // GEMM1 role
+    const int tg = wave / HG, hq = wave % HG;       // GEMM1 role: tokens 16 TT tg .., hidden 16 hq ..
     const int l16 = lane & 15, q4 = lane >> 4;      // 16x16x32 lane split
     const int r = lane & 31, h = lane >> 5;         // 32x32x16 lane split
     const int fo = 32 * wave;                       // GEMM2 role: output features fo .. fo + 31
@@ -733,13 +743,13 @@ __global__ __launch_bounds__(2 * MT) void mlp_fwd8_kernel(long M, const bf16* __
     if constexpr (LN)
         for (int i = threadIdx.x; i < 2 * C; i += NTH) lngb[i] = i < C ? ln.gamma[i] : ln.beta[i - C];
 
-    // x as 16x16x32 B fragments: token 32 tg + 16 tt + l16, k = 32 s + 8 q4 .. + 7
-    bf16x8 xf[2][KS];
+    // x as 16x16x32 B fragments: token 16 TT tg + 16 tt + l16, k = 32 s + 8 q4 .. + 7
+    bf16x8 xf[TT][KS];
     {
         const auto rs_x = buf_rsrc(X + m0 * C, rows * C * 2);
 #pragma unroll
-        for (int tt = 0; tt < 2; ++tt) {
-            const int tok = 32 * tg + 16 * tt + l16;
+        for (int tt = 0; tt < TT; ++tt) {
+            const int tok = 16 * TT * tg + 16 * tt + l16;
 #pragma unroll
             for (int s = 0; s < KS; ++s) {
                 const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(
@@ -754,72 +764,75 @@ __global__ __launch_bounds__(2 * MT) void mlp_fwd8_kernel(long M, const bf16* __
     d2.init(4 * C, wave, lane);
     const i32x4 rs_w1 = rsrc4(W1, 4L * C * C * 2);
     const i32x4 rs_w2 = rsrc4(W2, 4L * C * C * 2);
+    auto dma1 = [&](int c) { dma<D1::NW>(rs_w1, d1.v, (unsigned)chk(c) * HCK * C * 2, w1r + (c % NST) * IMG, wave); };
+    auto dma2 = [&](int c) { dma<D2::NW>(rs_w2, d2.v, (unsigned)chk(c) * HCK * 2, w2r + (c % NST) * IMG, wave); };
     asm volatile("" ::: "memory");
-    dma<D1::NW>(rs_w1, d1.v, (unsigned)chk(0) * HC * C * 2, w1r, wave);
+    // prefetch: W1 runs NST - 1 chunks ahead of GEMM1, W2 NST - 2 ahead of GEMM2 (= GEMM1 - 1)
+    dma1(0);
+#pragma unroll
+    for (int p = 1; p <= NST - 2; ++p) {
+        dma1(p);
+        dma2(p - 1);
+    }
 
     f32x16 acc[2];
     acc[0] = f32x16{};
     acc[1] = f32x16{};
 
-    // chunk j: h for (16 hidden of hq) x (32 tokens of tg), bias + GELU, g -> gimg[j & 1]
+    // chunk j: h for (16 hidden of hq) x (16 TT tokens of tg), bias + GELU, g -> gimg[j & 1]
     auto gemm1 = [&](int j) {
-        const bf16* w1c = w1r + (j & 1) * IMG;
+        const bf16* w1c = w1r + (j % NST) * IMG;
         bf16x8 wf[KS];
 #pragma unroll
         for (int s = 0; s < KS; ++s) wf[s] = frag(w1c, moff<2 * C>(16 * hq + l16, 32 * s + 8 * q4));
-        f32x4 ha = f32x4{}, hb = f32x4{};
+        f32x4 hv[TT];
 #pragma unroll
-        for (int s = 0; s < KS; ++s) {
-            ha = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[s], xf[0][s], ha, 0, 0, 0);
-            hb = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[s], xf[1][s], hb, 0, 0, 0);
-        }
-        const f32x4 bv = *reinterpret_cast<const f32x4*>(b1s + chk(j) * HC + 16 * hq + 4 * q4);
+        for (int tt = 0; tt < TT; ++tt) hv[tt] = f32x4{};
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+#pragma unroll
+            for (int tt = 0; tt < TT; ++tt) hv[tt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[s], xf[tt][s], hv[tt], 0, 0, 0);
+        const f32x4 bv = *reinterpret_cast<const f32x4*>(b1s + chk(j) * HCK + 16 * hq + 4 * q4);
         bf16* gi = gimg[j & 1];
 #pragma unroll
-        for (int tt = 0; tt < 2; ++tt) {
-            const f32x4& hv = tt ? hb : ha;
+        for (int tt = 0; tt < TT; ++tt) {
             bf16x4 gq;
 #pragma unroll
-            for (int e = 0; e < 4; ++e) gq[e] = (bf16)gelu_fast(hv[e] + bv[e]);
-            // token 32 tg + 16 tt + l16, hidden 16 hq + 4 q4 .. + 3
-            *reinterpret_cast<bf16x4*>(gi + moff<2 * HC>(32 * tg + 16 * tt + l16, 16 * hq + 4 * q4)) = gq;
+            for (int e = 0; e < 4; ++e) gq[e] = (bf16)gelu_fast(hv[tt][e] + bv[e]);
+            // token 16 TT tg + 16 tt + l16, hidden 16 hq + 4 q4 .. + 3
+            *reinterpret_cast<bf16x4*>(gi + moff<2 * HCK>(16 * TT * tg + 16 * tt + l16, 16 * hq + 4 * q4)) = gq;
         }
     };
     // chunk j: acc[tt] += W2[fo .. fo + 31][chunk] g[chunk][32 tt ..]
     auto gemm2 = [&](int j) {
-        const bf16* w2c = w2r + (j & 1) * IMG;
+        const bf16* w2c = w2r + (j % NST) * IMG;
         const bf16* gi = gimg[j & 1];
-        bf16x8 af[4], bf[2][4];
+        bf16x8 af[K2], bf[2][K2];
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
-            af[s] = frag(w2c, moff<2 * HC>(fo + r, 16 * s + 8 * h));
-            bf[0][s] = frag(gi, moff<2 * HC>(r, 16 * s + 8 * h));
-            bf[1][s] = frag(gi, moff<2 * HC>(32 + r, 16 * s + 8 * h));
+        for (int s = 0; s < K2; ++s) {
+            af[s] = frag(w2c, moff<2 * HCK>(fo + r, 16 * s + 8 * h));
+            bf[0][s] = frag(gi, moff<2 * HCK>(r, 16 * s + 8 * h));
+            bf[1][s] = frag(gi, moff<2 * HCK>(32 + r, 16 * s + 8 * h));
         }
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
+        for (int s = 0; s < K2; ++s) {
             acc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[s], bf[0][s], acc[0], 0, 0, 0);
             acc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[s], bf[1][s], acc[1], 0, 0, 0);
         }
     };
 
-    vmwait<0>();
-    lds_sync();
-    // step 0: W1(1), W2(0) in flight; chunk 0's GEMM1
-    dma<D1::NW>(rs_w1, d1.v, (unsigned)chk(1) * HC * C * 2, w1r + IMG, wave);
-    dma<D2::NW>(rs_w2, d2.v, (unsigned)chk(0) * HC * 2, w2r, wave);
-    gemm1(0);
-    for (int j = 1; j < NCH; ++j) {
-        vmwait<0>();                    // W1(j), W2(j-1): issued one step ago
+    // step j (one barrier): DMA W1(j + NST - 1), W2(j + NST - 2); GEMM1 + GELU of chunk j; GEMM2 of
+    // chunk j - 1.  The wait leaves the last NST - 2 steps' DMAs in flight (all of them full groups
+    // except near the end, where it waits for everything)
+    for (int j = 0; j <= NCH; ++j) {
+        if (NST > 2 && j + NST - 2 < NCH) vmwait<(NST > 2 ? (NST - 2) * DPS : 0)>();
+        else vmwait<0>();
         lds_sync();                     // every wave is past step j-1 (its stages and g image are free)
-        if (j + 1 < NCH) dma<D1::NW>(rs_w1, d1.v, (unsigned)chk(j + 1) * HC * C * 2, w1r + ((j + 1) & 1) * IMG, wave);
-        dma<D2::NW>(rs_w2, d2.v, (unsigned)chk(j) * HC * 2, w2r + (j & 1) * IMG, wave);
-        gemm1(j);
-        gemm2(j - 1);
+        if (j + NST - 1 < NCH) dma1(j + NST - 1);
+        if (j + NST - 2 < NCH) dma2(j + NST - 2);
+        if (j < NCH) gemm1(j);
+        if (j > 0) gemm2(j - 1);
     }
-    vmwait<0>();
-    lds_sync();
-    gemm2(NCH - 1);
 
     // epilogue: lane holds token 32 tt + r, features fo + 8 g + 4 h + 0..3 in acc[tt][4 g + e]
     const auto rs_res = buf_rsrc(res + m0 * C, rows * C * 4);
@@ -915,6 +928,9 @@ __global__ __launch_bounds__(2 * MT) void mlp_fwd8_kernel(long M, const bf16* __
 // The next chunk's W1 / W2 land during the three phases (2-stage ring).
 #ifndef MLP_BWD8
 #define MLP_BWD8 1
+#endif
+#ifndef MLP_FWD8_HC
+#define MLP_FWD8_HC 32
 #endif
 constexpr bool kMlpBwd8 = MLP_BWD8;
 template <int C>
@@ -1108,10 +1124,10 @@ int fwd_launch(long M, const void* x, const void* w1, const float* b1, const voi
     if constexpr (C == 256) {
         if (!d) {   // two waves per SIMD (dropout launches keep the 4-wave kernel)
             if (ln)
-                mlp_fwd8_kernel<C, true><<<grid, 2 * MT, 0, st>>>(M, (const bf16*)x, (const bf16*)w1, b1, (const bf16*)w2, b2,
+                mlp_fwd8_kernel<C, true, MLP_FWD8_HC><<<grid, 2 * MT, 0, st>>>(M, (const bf16*)x, (const bf16*)w1, b1, (const bf16*)w2, b2,
                                                                    res, out, rpi, *ln);
             else
-                mlp_fwd8_kernel<C, false><<<grid, 2 * MT, 0, st>>>(M, (const bf16*)x, (const bf16*)w1, b1, (const bf16*)w2, b2,
+                mlp_fwd8_kernel<C, false, MLP_FWD8_HC><<<grid, 2 * MT, 0, st>>>(M, (const bf16*)x, (const bf16*)w1, b1, (const bf16*)w2, b2,
                                                                     res, out, rpi, MlpLn{});
             return check_launch(ln ? "mlp_fwd_ln" : "mlp_fwd");
         }

@@ -23,7 +23,7 @@ CSRC = os.path.join(REPO, "cswin-simam-unet_amd", "csrc")
 OUT = os.path.join(HERE, "mlp_abl")
 # round 6 set: "old" = the 4-wave kernels (the ablations of those, base / nodma / nosync / nogelu / nomfma /
 # nostore, are in profiles/r08b_mlp_ablate.txt), "w8" = the 8-wave kernels as built, and their ablations
-VARIANTS = ["old", "w8", "w8_nodma", "w8_nomfma", "w8_dmaonly"]
+VARIANTS = ["old", "w8", "w8_hc64", "w8_nodma", "w8_nomfma", "w8_dmaonly"]
 OLD_ONLY = ("base", "nodma", "nosync", "nogelu", "nomfma", "nostore", "old")
 
 
@@ -37,16 +37,16 @@ def edit(src: str, v: str) -> str:
         a = src.index("// Forward at C = 256 with two waves per SIMD")
         b = src.index("template <int C>\nint fwd_launch(")
         body = src[a:b]
+        if v == "w8_hc64":        # one chunk of weight prefetch (64-hidden chunks, 2-stage ring)
+            return src.replace("#define MLP_FWD8_HC 32", "#define MLP_FWD8_HC 64")
         if v == "w8_nodma":
-            body = body.replace("if (j + 1 < NCH) dma<D1::NW>", "if (false) dma<D1::NW>")
-            body = body.replace("dma<D2::NW>(rs_w2, d2.v, (unsigned)chk(j) * HC * 2", "if (false) dma<D2::NW>(rs_w2, d2.v, (unsigned)chk(j) * HC * 2")
+            body = body.replace("if (j + NST - 1 < NCH) dma1(", "if (false) dma1(").replace("if (j + NST - 2 < NCH) dma2(", "if (false) dma2(")
             body = body.replace("if (j + 1 < NCH) {\n            dma", "if (false) {\n            dma")
         if v in ("w8_nomfma", "w8_dmaonly"):
             body = re.sub(r"(\w+(?:\[\w+\])*) = __builtin_amdgcn_mfma_f32_(?:32x32x16|16x16x32)_bf16\(([^;]*?), ([\w\[\]]+), \1, 0, 0, 0\);",
                           r'asm volatile("" :: "v"(\2), "v"(\3));', body)
         if v == "w8_dmaonly":     # DMA + barriers only: no fragment reads, no GELU, no phase work
-            body = body.replace("        gemm1(j);\n        gemm2(j - 1);\n", "")
-            body = body.replace("    gemm1(0);\n", "").replace("    gemm2(NCH - 1);\n", "")
+            body = body.replace("if (j < NCH) gemm1(j);", "").replace("if (j > 0) gemm2(j - 1);", "")
             for ph in ("// ---- phase A\n        {", "// ---- phase B\n        {", "// ---- phase C: acc[tt] += W1[chunk]^T[fo ..][hidden] dH[hidden][32 tt ..]\n        {"):
                 assert ph in body, ph
                 body = body.replace(ph, ph.replace("{", "if (M < 0) {"))
