@@ -700,10 +700,10 @@ int persist_grid(long M) {   // one workgroup (two panel streams) per CU, fewer 
 // ~220 VGPRs: two waves per SIMD.  Step j (one barrier): DMA W1(j+1), W2(j); GEMM1 + GELU of chunk j;
 // GEMM2 of chunk j-1.  LDS per step and CU: 160 KB of fragment reads + 64 KB of DMA (256 B/clk: ~900
 // cycles) against 1024 MFMA cycles per SIMD.
-// HCK = 32 (default, MLP_FWD8_HC): 32-hidden chunks through a 4-stage ring (the same 128 KB), so the
-// weight DMA runs up to three chunks ahead instead of one: the DMA stream alone takes 22 of the 38 us
-// at HCK = 64 with one chunk of prefetch (w8_dmaonly in profiles/r08e_mlp_ablate.txt).  Then GEMM1's
-// wave tile is 16 hidden x 16 tokens (one token tile) and GEMM2's K is 32.
+// HCK = 32: 32-hidden chunks through a 4-stage ring (the same 128 KB), the weight DMA up to three
+// chunks ahead instead of one (GEMM1's wave tile 16 hidden x 16 tokens, GEMM2's K 32) -- measured, not
+// used (kFwd8Hc): the DMA stream alone is 21-22 us of the 37-38 either way (w8_dmaonly,
+// profiles/r08e_mlp_ablate.txt, r08f_mlp_ablate.txt), the rest is the compute chain.
 template <int C, bool LN, int HCK>
 __global__ __launch_bounds__(2 * MT) void mlp_fwd8_kernel(long M, const bf16* __restrict__ X, const bf16* __restrict__ W1,
                                                           const float* __restrict__ b1, const bf16* __restrict__ W2,
@@ -926,13 +926,10 @@ __global__ __launch_bounds__(2 * MT) void mlp_fwd8_kernel(long M, const bf16* __
 //  C  dX += W1^T dH: wave w owns the dX features 32 w .. for all 64 tokens (32x32x16, W1 read
 //     transposed from the ring) -- no partial outputs to exchange.
 // The next chunk's W1 / W2 land during the three phases (2-stage ring).
-#ifndef MLP_BWD8
-#define MLP_BWD8 1
-#endif
-#ifndef MLP_FWD8_HC
-#define MLP_FWD8_HC 32
-#endif
-constexpr bool kMlpBwd8 = MLP_BWD8;
+// 64-hidden chunks for mlp_fwd8_kernel: 32-hidden chunks with the weight DMA three chunks ahead (a
+// 4-stage ring) measured no faster (38.6 vs 37.4 us isolated, mlp_fwd 1072-1079 vs 1038-1049 us/step
+// in the step: profiles/r08f_mlp_ablate.txt, r08f bench pairs)
+constexpr int kFwd8Hc = 64;
 template <int C>
 __global__ __launch_bounds__(2 * MT) void mlp_bwd8_kernel(long M, const bf16* __restrict__ X, const bf16* __restrict__ dY,
                                                           const bf16* __restrict__ W1, const float* __restrict__ b1,
@@ -1124,10 +1121,10 @@ int fwd_launch(long M, const void* x, const void* w1, const float* b1, const voi
     if constexpr (C == 256) {
         if (!d) {   // two waves per SIMD (dropout launches keep the 4-wave kernel)
             if (ln)
-                mlp_fwd8_kernel<C, true, MLP_FWD8_HC><<<grid, 2 * MT, 0, st>>>(M, (const bf16*)x, (const bf16*)w1, b1, (const bf16*)w2, b2,
+                mlp_fwd8_kernel<C, true, kFwd8Hc><<<grid, 2 * MT, 0, st>>>(M, (const bf16*)x, (const bf16*)w1, b1, (const bf16*)w2, b2,
                                                                    res, out, rpi, *ln);
             else
-                mlp_fwd8_kernel<C, false, MLP_FWD8_HC><<<grid, 2 * MT, 0, st>>>(M, (const bf16*)x, (const bf16*)w1, b1, (const bf16*)w2, b2,
+                mlp_fwd8_kernel<C, false, kFwd8Hc><<<grid, 2 * MT, 0, st>>>(M, (const bf16*)x, (const bf16*)w1, b1, (const bf16*)w2, b2,
                                                                     res, out, rpi, MlpLn{});
             return check_launch(ln ? "mlp_fwd_ln" : "mlp_fwd");
         }
@@ -1155,7 +1152,7 @@ int bwd_launch(long M, const void* x, const void* dy, const void* w1, const floa
                void* dx, const MlpDrop* d, long rpi, hipStream_t st) {
     const dim3 grid((unsigned)((M + BM - 1) / BM));
     if constexpr (C == 256) {
-        if (!d && kMlpBwd8) {   // two waves per SIMD (dropout launches keep the 4-wave kernel)
+        if (!d) {   // two waves per SIMD (dropout launches keep the 4-wave kernel)
             mlp_bwd8_kernel<C><<<grid, 2 * MT, 0, st>>>(M, (const bf16*)x, (const bf16*)dy, (const bf16*)w1, b1, (const bf16*)w2,
                                                         (bf16*)dh, (bf16*)g, (bf16*)dx, rpi);
             return check_launch("mlp_bwd");

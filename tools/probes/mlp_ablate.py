@@ -31,14 +31,14 @@ def edit(src: str, v: str) -> str:
     if v == "w8":
         return src
     if v in OLD_ONLY:   # C = 256 dispatches to the 4-wave kernels
+        assert src.count("if (!d) {   // two waves per SIMD") == 2
         src = src.replace("if (!d) {   // two waves per SIMD", "if (false) {   // two waves per SIMD")
-        src = src.replace("#define MLP_BWD8 1", "#define MLP_BWD8 0")
     if v.startswith("w8_"):   # the 8-wave C = 256 kernels (mlp_fwd8_kernel / mlp_bwd8_kernel)
         a = src.index("// Forward at C = 256 with two waves per SIMD")
         b = src.index("template <int C>\nint fwd_launch(")
         body = src[a:b]
-        if v == "w8_hc64":        # one chunk of weight prefetch (64-hidden chunks, 2-stage ring)
-            return src.replace("#define MLP_FWD8_HC 32", "#define MLP_FWD8_HC 64")
+        if v == "w8_hc64":        # (name kept from r08f) the other chunk size: 32-hidden chunks, 4-stage ring
+            return src.replace("constexpr int kFwd8Hc = 64;", "constexpr int kFwd8Hc = 32;")
         if v == "w8_nodma":
             body = body.replace("if (j + NST - 1 < NCH) dma1(", "if (false) dma1(").replace("if (j + NST - 2 < NCH) dma2(", "if (false) dma2(")
             body = body.replace("if (j + 1 < NCH) {\n            dma", "if (false) {\n            dma")
