@@ -20,7 +20,18 @@
 //  * epilogue per tile through a per-wave LDS region (fp32 [64][36]): bias, residual, output
 //    dtype, row-contiguous 16-B stores.
 // Measured (probe, 16384 x 768 x 256): 8.6 us vs 18.0 (gemm4) / 19.6 (hipBLASLt).
+//
+// e4m3 weights (BASELINE config 5, F8 != 0): the same kernel streams the fp8 format's e4m3 bytes in
+// the same fragment order ([N/32][K/16][64 lanes][8 bytes]: half the bytes of the weight stream that
+// bounds these GEMMs at the 16384-token stage) and widens each fragment to bf16 in registers
+// (v_cvt_scalef32_pk_bf16_fp8, scale 1) right before its MFMA; activations stay bf16.  The per-row
+// power-of-two scales s[n] of W = q s are applied exactly: F8 = 1 (x W^T) multiplies the accumulator
+// of output column n by s[n] in the epilogue, F8 = 2 (dy W: the weight operand is W^T, whose k index
+// is n) multiplies the token panel's column n by s[n] once when it is loaded.  Both are exact for
+// power-of-two scales, so the outputs are bitwise those of the bf16 kernel on the dequantised weight.
 #include "common.hpp"
+
+#include <type_traits>
 
 namespace csu {
 namespace {
@@ -81,11 +92,23 @@ constexpr int ws_ns(int k, int n, int epi) {
     return WS_NSPLIT > 1 && epi == 0 && k <= 256 && ws_wn(n) == 4 && (n / 128) % WS_NSPLIT == 0 ? WS_NSPLIT : 1;
 }
 
-template <int K, int N, int EPI, typename TOUT, int NS = 1>
+// 8 e4m3 bytes (one 32x32x16 A-fragment half-lane) -> 8 bf16, exactly
+__device__ __forceinline__ bf16x8 e4m3x8_bf16(u32x2 w) {
+    typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+    const bf16x2v p0 = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w[0], 1.f, false);
+    const bf16x2v p1 = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w[0], 1.f, true);
+    const bf16x2v p2 = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w[1], 1.f, false);
+    const bf16x2v p3 = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w[1], 1.f, true);
+    return bf16x8{p0[0], p0[1], p1[0], p1[1], p2[0], p2[1], p3[0], p3[1]};
+}
+
+template <int K, int N, int EPI, typename TOUT, int NS = 1, int F8 = 0>
 __global__ __launch_bounds__(256, ws_wn(N) < 4 || NS > 1 ? 2 : 1) void gemm_ws_kernel(long M, const bf16* __restrict__ X, int ldx,
                                                       const bf16* __restrict__ Wf, const float* __restrict__ bias,
                                                       const float* __restrict__ resid, TOUT* __restrict__ out,
-                                                      WsLn ln = WsLn{}, WsLnF lnf = WsLnF{}) {
+                                                      WsLn ln = WsLn{}, WsLnF lnf = WsLnF{},
+                                                      const float* __restrict__ wsc = nullptr) {
+    static_assert(F8 == 0 || EPI != WS_LNBWD, "gemm_ws: e4m3 weights not with the LayerNorm-backward epilogue");
     constexpr int WN = ws_wn(N);                   // waves along N
     constexpr int NT = N / (32 * WN * NS);         // 32-feature tiles per wave (of this workgroup's N / NS)
     static_assert(NT * 32 * WN * NS == N, "gemm_ws: N = 32 WN NT NS");
@@ -115,10 +138,19 @@ __global__ __launch_bounds__(256, ws_wn(N) < 4 || NS > 1 ? 2 : 1) void gemm_ws_k
     const int rot = WS_ROT ? (int)((blockIdx.x >> 3) % NT) : 0;
     const int tb = NS > 1 ? (int)blockIdx.y * NT : 0;   // this workgroup's first tile of each wave
     auto tile_of = [&](int i) { return tb + (i + rot < NT ? i + rot : i + rot - NT); };
-    bf16x8 wf[2][UK];
+    using WFR = std::conditional_t<F8 != 0, u32x2, bf16x8>;   // a lane's weight fragment as loaded
+    WFR wf[2][UK];
     auto wload1 = [&](int u, int s) {   // k-step s of unit u of this wave into buffer u & 1
         const int nt = wn + WN * tile_of(u / CH), ks = (u % CH) * UK + s;
-        wf[u & 1][s] = *reinterpret_cast<const bf16x8*>(Wf + ((long)(nt * KS + ks) * 64 + lane) * 8);
+        if constexpr (F8 != 0)
+            wf[u & 1][s] = *reinterpret_cast<const u32x2*>(reinterpret_cast<const uint8_t*>(Wf) +
+                                                           ((long)(nt * KS + ks) * 64 + lane) * 8);
+        else
+            wf[u & 1][s] = *reinterpret_cast<const bf16x8*>(Wf + ((long)(nt * KS + ks) * 64 + lane) * 8);
+    };
+    auto wfrag = [&](const WFR& w) {
+        if constexpr (F8 != 0) return e4m3x8_bf16(w);
+        else return w;
     };
 #pragma unroll
     for (int s = 0; s < UK; ++s) wload1(0, s);
@@ -130,7 +162,16 @@ __global__ __launch_bounds__(256, ws_wn(N) < 4 || NS > 1 ? 2 : 1) void gemm_ws_k
 #pragma unroll
         for (int i = 0; i < WS_BM * PR / 256; ++i) {
             const int p = threadIdx.x + 256 * i, row = p / PR, c = 8 * (p % PR);
-            *reinterpret_cast<bf16x8*>(xs + row * XS + c) = *reinterpret_cast<const bf16x8*>(X + (m0 + row) * ldx + c);
+            bf16x8 v = *reinterpret_cast<const bf16x8*>(X + (m0 + row) * ldx + c);
+            if constexpr (F8 == 2) {   // column c + e of the panel is k = n of W: times s[n] (exact)
+                const f32x4 s0 = *reinterpret_cast<const f32x4*>(wsc + c), s1 = *reinterpret_cast<const f32x4*>(wsc + c + 4);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    v[e] = (bf16)((float)v[e] * s0[e]);
+                    v[4 + e] = (bf16)((float)v[4 + e] * s1[e]);
+                }
+            }
+            *reinterpret_cast<bf16x8*>(xs + row * XS + c) = v;
         }
         __syncthreads();
         if constexpr (XREG) {
@@ -145,8 +186,13 @@ __global__ __launch_bounds__(256, ws_wn(N) < 4 || NS > 1 ? 2 : 1) void gemm_ws_k
 #pragma unroll
         for (int t = 0; t < 2; ++t)
 #pragma unroll
-            for (int s = 0; s < KS; ++s)
+            for (int s = 0; s < KS; ++s) {
                 xf[t][s] = *reinterpret_cast<const bf16x8*>(X + (m0 + 32 * t + r) * ldx + 16 * s + 8 * h);
+                if constexpr (F8 == 2) {
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) xf[t][s][e] = (bf16)((float)xf[t][s][e] * wsc[16 * s + 8 * h + e]);
+                }
+            }
     }
     __builtin_amdgcn_sched_barrier(0);
 
@@ -157,7 +203,8 @@ __global__ __launch_bounds__(256, ws_wn(N) < 4 || NS > 1 ? 2 : 1) void gemm_ws_k
     // weight loads: vmcnt counts in issue order, so waiting for them then does not wait for the prefetch
     constexpr bool RES = EPI == WS_RESID || EPI == WS_RESID_LN;
     static_assert(EPI != WS_RESID_LN || !BF, "gemm_ws: the LayerNorm epilogue writes the fp32 residual stream");
-    float bv[8], rv[8][4];
+    float bv[8], rv[8][4], sv[8];
+    const auto rs_s = buf_rsrc(wsc, F8 == 1 ? (long)N * 4 : 0);
     f32x16 keep[EPI == WS_LNBWD ? NT : 1][2];
     float yk[EPI == WS_RESID_LN ? NT : 1][8][4];   // y of the wave's tiles in the store layout (LayerNorm)
     float lg[EPI == WS_RESID_LN ? NT : 1][4], lb[EPI == WS_RESID_LN ? NT : 1][4];
@@ -178,9 +225,14 @@ __global__ __launch_bounds__(256, ws_wn(N) < 4 || NS > 1 ? 2 : 1) void gemm_ws_k
                 const int cc = 8 * (lane & 3);
                 buf_ld4(rs_b, (unsigned)(n0 + cc) * 4, bv);
                 buf_ld4(rs_b, (unsigned)(n0 + cc + 4) * 4, bv + 4);
+                if constexpr (F8 == 1) {
+                    buf_ld4(rs_s, (unsigned)(n0 + cc) * 4, sv);
+                    buf_ld4(rs_s, (unsigned)(n0 + cc + 4) * 4, sv + 4);
+                }
             } else {
                 const int cc = 4 * (lane & 7);
                 buf_ld4(rs_b, (unsigned)(n0 + cc) * 4, bv);
+                if constexpr (F8 == 1) buf_ld4(rs_s, (unsigned)(n0 + cc) * 4, sv);
                 if constexpr (RES) {
                     const auto rs_res = buf_rsrc(resid + m0 * N, (M - m0) * N * 4);
 #pragma unroll
@@ -201,8 +253,9 @@ __global__ __launch_bounds__(256, ws_wn(N) < 4 || NS > 1 ? 2 : 1) void gemm_ws_k
                 b0 = *reinterpret_cast<const bf16x8*>(xs + r * XS + 16 * ks + 8 * h);
                 b1 = *reinterpret_cast<const bf16x8*>(xs + (32 + r) * XS + 16 * ks + 8 * h);
             }
-            a0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[u & 1][s], b0, a0, 0, 0, 0);
-            a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[u & 1][s], b1, a1, 0, 0, 0);
+            const bf16x8 wa = wfrag(wf[u & 1][s]);
+            a0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa, b0, a0, 0, 0, 0);
+            a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa, b1, a1, 0, 0, 0);
             if (u + 1 < U) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);   // one weight load
             if constexpr (!XREG) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);   // two fragment reads
             __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);                 // two MFMAs
@@ -239,7 +292,10 @@ __global__ __launch_bounds__(256, ws_wn(N) < 4 || NS > 1 ? 2 : 1) void gemm_ws_k
                 load4(ep + row * ES + cc, v);
                 load4(ep + row * ES + cc + 4, v + 4);
 #pragma unroll
-                for (int e = 0; e < 8; ++e) v[e] += bv[e];
+                for (int e = 0; e < 8; ++e) {
+                    if constexpr (F8 == 1) v[e] *= sv[e];   // s[n] x (x q^T): exact (power of two)
+                    v[e] += bv[e];
+                }
                 buf_st8bf(rs_out, (unsigned)(row * N + n0 + cc) * 2, v);
             }
         } else {
@@ -252,6 +308,7 @@ __global__ __launch_bounds__(256, ws_wn(N) < 4 || NS > 1 ? 2 : 1) void gemm_ws_k
                 load4(ep + row * ES + cc, v);
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
+                    if constexpr (F8 == 1) v[e] *= sv[e];
                     v[e] += bv[e];
                     if constexpr (RES) v[e] += rv[q][e];
                     if constexpr (EPI == WS_RESID_LN) yk[u / CH][q][e] = v[e];
@@ -434,12 +491,12 @@ __global__ __launch_bounds__(256, ws_wn(N) < 4 || NS > 1 ? 2 : 1) void gemm_ws_k
     }
 }
 
-template <int K, int N, int EPI, typename TOUT>
+template <int K, int N, int EPI, typename TOUT, int F8 = 0>
 int ws_launch(long M, const bf16* X, int ldx, const bf16* Wf, const float* bias, const float* resid, void* out,
-              hipStream_t st, const WsLn& ln = WsLn{}, const WsLnF& lnf = WsLnF{}) {
-    constexpr int NS = ws_ns(K, N, EPI);
-    gemm_ws_kernel<K, N, EPI, TOUT, NS><<<dim3((unsigned)(M / ws_tokens(N)), NS), 256, 0, st>>>(M, X, ldx, Wf, bias, resid,
-                                                                                                (TOUT*)out, ln, lnf);
+              hipStream_t st, const WsLn& ln = WsLn{}, const WsLnF& lnf = WsLnF{}, const float* wsc = nullptr) {
+    constexpr int NS = F8 ? 1 : ws_ns(K, N, EPI);
+    gemm_ws_kernel<K, N, EPI, TOUT, NS, F8><<<dim3((unsigned)(M / ws_tokens(N)), NS), 256, 0, st>>>(
+        M, X, ldx, Wf, bias, resid, (TOUT*)out, ln, lnf, wsc);
     return check_launch("gemm_ws");
 }
 
@@ -474,6 +531,25 @@ int gemm_ws_run(long M, int N, int K, const bf16* X, int ldx, const bf16* Wf, co
     return fail(CSU_E_ARG, "gemm_ws: shape not instantiated");
 }
 
+// e4m3 weights: mode 1 (x W^T, per-column scales in the epilogue) or 2 (dy W through the W^T fragments,
+// per-k scales on the token panel); any epilogue of gemm_ws_run
+int gemm_ws_e4m3_run(long M, int N, int K, const bf16* X, int ldx, const uint8_t* Wq, const float* wsc, int mode,
+                     const float* bias, const float* resid, int out_dtype, void* out, hipStream_t st) {
+    const bf16* W = reinterpret_cast<const bf16*>(Wq);
+#define WS_GO8(KK, NN, MODE)                                                                                      \
+    if (K == KK && N == NN && mode == MODE) {                                                                     \
+        if (resid) return ws_launch<KK, NN, WS_RESID, float, MODE>(M, X, ldx, W, bias, resid, out, st, {}, {}, wsc); \
+        if (out_dtype == CSU_F32)                                                                                 \
+            return ws_launch<KK, NN, WS_PLAIN, float, MODE>(M, X, ldx, W, bias, nullptr, out, st, {}, {}, wsc);   \
+        return ws_launch<KK, NN, WS_PLAIN, bf16, MODE>(M, X, ldx, W, bias, nullptr, out, st, {}, {}, wsc);        \
+    }
+#define WS_GO8B(KK, NN) WS_GO8(KK, NN, 1) WS_GO8(KK, NN, 2)
+    WS_SHAPES(WS_GO8B)
+#undef WS_GO8B
+#undef WS_GO8
+    return fail(CSU_E_ARG, "gemm_ws_e4m3: shape not instantiated");
+}
+
 // the LayerNorm (norm2) epilogue: proj + residual, K = N = C
 int gemm_ws_ln_supported(long M, int N, int K) {
     if (M < ws_tokens(N) || M % ws_tokens(N) || M > (1L << 30)) return 0;
@@ -481,7 +557,13 @@ int gemm_ws_ln_supported(long M, int N, int K) {
 }
 
 int gemm_ws_ln_run(long M, int N, const bf16* X, int ldx, const bf16* Wf, const float* bias, const float* resid, float* out,
-                   const WsLnF& lnf, hipStream_t st) {
+                   const WsLnF& lnf, hipStream_t st, const float* wsc = nullptr) {
+    if (wsc) {   // e4m3 weight fragments, per-column scales
+        if (N == 64) return ws_launch<64, 64, WS_RESID_LN, float, 1>(M, X, ldx, Wf, bias, resid, out, st, WsLn{}, lnf, wsc);
+        if (N == 128) return ws_launch<128, 128, WS_RESID_LN, float, 1>(M, X, ldx, Wf, bias, resid, out, st, WsLn{}, lnf, wsc);
+        if (N == 256) return ws_launch<256, 256, WS_RESID_LN, float, 1>(M, X, ldx, Wf, bias, resid, out, st, WsLn{}, lnf, wsc);
+        return fail(CSU_E_ARG, "gemm_ws_ln_e4m3: shape not instantiated");
+    }
     if (N == 64) return ws_launch<64, 64, WS_RESID_LN, float>(M, X, ldx, Wf, bias, resid, out, st, WsLn{}, lnf);
     if (N == 128) return ws_launch<128, 128, WS_RESID_LN, float>(M, X, ldx, Wf, bias, resid, out, st, WsLn{}, lnf);
     if (N == 256) return ws_launch<256, 256, WS_RESID_LN, float>(M, X, ldx, Wf, bias, resid, out, st, WsLn{}, lnf);
@@ -518,6 +600,47 @@ __global__ __launch_bounds__(256) void frag_layout_kernel(const csu_frag_item* _
     *reinterpret_cast<u32x4*>((bf16*)it.dst + dst) = *reinterpret_cast<const u32x4*>((const bf16*)it.src + q * 8);
 }
 
+// ---- e4m3 fragment order (csu_frag8_layout_batch): output matrix O (rows x cols) = src (transpose 0)
+// or src^T (transpose 1) of an e4m3 (N x K) matrix; 8-byte chunk (row, c8 = col / 8) of O goes to chunk
+// ((row / 32) * (cols / 16) + c8 / 2) * 64 + row % 32 + 32 (c8 % 2).  One thread per 8 x 8 byte block of
+// the source: 8 rows x 8 bytes loaded, written as 8 chunks (transposed in registers for mode 1).
+__device__ __forceinline__ long frag8_chunk(int row, int c8, int cols) {
+    return ((long)(row >> 5) * (cols >> 4) + (c8 >> 1)) * 64 + (row & 31) + 32 * (c8 & 1);
+}
+__global__ __launch_bounds__(256) void frag8_layout_kernel(const csu_frag8_item* __restrict__ items, int count) {
+    const long g = (long)blockIdx.x * 256 + threadIdx.x;   // global 8x8 block index
+    int lo = 0, hi = count - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (items[mid].block0 <= g) lo = mid; else hi = mid - 1;
+    }
+    const csu_frag8_item it = items[lo];
+    const long b = g - it.block0;
+    const int kb = it.K / 8;   // source column blocks
+    if (b < 0 || b >= (long)(it.N / 8) * kb) return;
+    const int n0 = 8 * (int)(b / kb), k0 = 8 * (int)(b % kb);
+    const uint8_t* src = reinterpret_cast<const uint8_t*>(it.src);
+    u32x2 v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = *reinterpret_cast<const u32x2*>(src + (long)(n0 + i) * it.K + k0);
+    u32x2* dst = reinterpret_cast<u32x2*>(it.dst);
+    if (!it.transpose) {   // O = src (N x K): chunk (n0 + i, k0 / 8)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) dst[frag8_chunk(n0 + i, k0 >> 3, it.K)] = v[i];
+    } else {               // O = src^T (K x N): chunk (k0 + j, n0 / 8) = bytes src[n0 + i][k0 + j], i = 0..7
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            unsigned lo4 = 0, hi4 = 0;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                lo4 |= ((v[i][j >> 2] >> (8 * (j & 3))) & 0xffu) << (8 * i);
+                hi4 |= ((v[4 + i][j >> 2] >> (8 * (j & 3))) & 0xffu) << (8 * i);
+            }
+            dst[frag8_chunk(k0 + j, n0 >> 3, it.N)] = u32x2{lo4, hi4};
+        }
+    }
+}
+
 }  // namespace csu
 
 using namespace csu;
@@ -532,6 +655,34 @@ extern "C" int csu_gemm_ws(long M, int N, int K, const void* x, int ldx, const v
     if (!gemm_ws_supported(M, N, K, resid != nullptr, out_dtype)) return fail(CSU_E_ARG, "gemm_ws: unsupported shape");
     if (ldx < K || ldx % 8) return fail(CSU_E_ARG, "gemm_ws: ldx must be >= K and a multiple of 8");
     return gemm_ws_run(M, N, K, (const bf16*)x, ldx, (const bf16*)w_frag, bias, resid, out_dtype, out, as_stream(stream));
+}
+
+extern "C" int csu_gemm_ws_e4m3(long M, int N, int K, const void* x, int ldx, const void* w_frag8, const float* w_scale,
+                                int scale_mode, const float* bias, const float* resid, int out_dtype, void* out,
+                                void* stream) {
+    if (!x || !w_frag8 || !w_scale || !out) return fail(CSU_E_ARG, "gemm_ws_e4m3: null pointer");
+    if (scale_mode != 1 && scale_mode != 2) return fail(CSU_E_ARG, "gemm_ws_e4m3: scale_mode 1 (x W^T) or 2 (dy W)");
+    if (!gemm_ws_supported(M, N, K, resid != nullptr, out_dtype)) return fail(CSU_E_ARG, "gemm_ws_e4m3: unsupported shape");
+    if (ldx < K || ldx % 8) return fail(CSU_E_ARG, "gemm_ws_e4m3: ldx must be >= K and a multiple of 8");
+    return gemm_ws_e4m3_run(M, N, K, (const bf16*)x, ldx, (const uint8_t*)w_frag8, w_scale, scale_mode, bias, resid,
+                            out_dtype, out, as_stream(stream));
+}
+
+extern "C" int csu_gemm_ws_ln_e4m3(long M, int C, const void* x, int ldx, const void* w_frag8, const float* w_scale,
+                                   const float* bias, const float* resid, float* out, const float* gamma, const float* beta,
+                                   float eps, void* ln_out, float* mean, float* rstd, void* stream) {
+    if (!x || !w_frag8 || !w_scale || !resid || !out || !gamma || !beta || !ln_out || !mean || !rstd)
+        return fail(CSU_E_ARG, "gemm_ws_ln_e4m3: null pointer");
+    if (!gemm_ws_ln_supported(M, C, C)) return fail(CSU_E_ARG, "gemm_ws_ln_e4m3: unsupported shape");
+    if (ldx < C || ldx % 8) return fail(CSU_E_ARG, "gemm_ws_ln_e4m3: ldx must be >= C and a multiple of 8");
+    const WsLnF lnf{gamma, beta, eps, (bf16*)ln_out, mean, rstd};
+    return gemm_ws_ln_run(M, C, (const bf16*)x, ldx, (const bf16*)w_frag8, bias, resid, out, lnf, as_stream(stream), w_scale);
+}
+
+extern "C" int csu_frag8_layout_batch(const csu_frag8_item* items, int count, long total_blocks, void* stream) {
+    if (!items || count < 1 || total_blocks < 1) return fail(CSU_E_ARG, "frag8_layout: empty item table");
+    frag8_layout_kernel<<<(unsigned)((total_blocks + 255) / 256), 256, 0, as_stream(stream)>>>(items, count);
+    return check_launch("frag8_layout");
 }
 
 extern "C" int csu_gemm_ws_lnbwd_supported(long M, int C, int K) { return gemm_ws_lnbwd_supported(M, C, K); }

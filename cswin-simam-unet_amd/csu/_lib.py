@@ -151,6 +151,12 @@ _SIGS = {
     "csu_gemm_ws_lnbwd_supported": (ctypes.c_int, [ctypes.c_long, ctypes.c_int, ctypes.c_int]),
     "csu_gemm_ws_lnbwd": (ctypes.c_int, [ctypes.c_long, ctypes.c_int, ctypes.c_int] + [c_void_p] * 11),
     "csu_frag_layout_batch": (ctypes.c_int, [c_void_p, ctypes.c_int, ctypes.c_long, c_void_p]),
+    "csu_frag8_layout_batch": (ctypes.c_int, [c_void_p, ctypes.c_int, ctypes.c_long, c_void_p]),
+    "csu_gemm_ws_e4m3": (ctypes.c_int, [ctypes.c_long, ctypes.c_int, ctypes.c_int, c_void_p, ctypes.c_int, c_void_p,
+                                        c_void_p, ctypes.c_int, c_void_p, c_void_p, ctypes.c_int, c_void_p, c_void_p]),
+    "csu_gemm_ws_ln_e4m3": (ctypes.c_int, [ctypes.c_long, ctypes.c_int, c_void_p, ctypes.c_int, c_void_p, c_void_p,
+                                           c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, ctypes.c_float, c_void_p,
+                                           c_void_p, c_void_p, c_void_p]),
     "csu_gemm_f32_workspace": (c_size_t, [ctypes.c_int, ctypes.c_long, ctypes.c_int, ctypes.c_long]),
     "csu_gemm_f32": (ctypes.c_int, [ctypes.c_int, ctypes.c_long, ctypes.c_int, ctypes.c_long, c_void_p, c_void_p, c_void_p,
                                     c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),

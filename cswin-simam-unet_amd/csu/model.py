@@ -570,7 +570,10 @@ class CSWinTransformer(nn.Module):
             self._cast_cache.refresh(weights, cd, self._conv_weights(), sources=sources)
             if sources is not None:
                 self._fp8.quantize(self._cast_cache)   # one launch: e4m3 + scales + exact bf16 shadows
-            self._cast_cache.refresh_frag()   # fragment-ordered W / W^T of the qkv / proj Linears (csu_gemm_ws)
+            if sources is None or not ops.FP8_WS:
+                # fragment-ordered W / W^T of the qkv / proj Linears (csu_gemm_ws); the fp8 format streams
+                # the e4m3 fragments its quantiser lays out instead (ops.FP8_WS, csu_gemm_ws_e4m3)
+                self._cast_cache.refresh_frag()
             ops.set_cast_cache(self._cast_cache, self._fp8 if sources is not None else None)
         try:
             return self._forward(x)

@@ -968,16 +968,41 @@ def gemm(a2: torch.Tensor, b: torch.Tensor, b_trans: bool, out_dtype, bias=None,
 USE_GEMM_WS = True
 
 
-def gemm_ws(x2: torch.Tensor, w_frag: torch.Tensor, N: int, out_dtype, bias=None, resid=None) -> torch.Tensor:
-    """out (M, N) = x2 (M, K) @ W^T (+ bias) (+ resid) with W given fragment-ordered (CastCache.get_frag)."""
+def gemm_ws(x2: torch.Tensor, w_frag, N: int, out_dtype, bias=None, resid=None) -> torch.Tensor:
+    """out (M, N) = x2 (M, K) @ W^T (+ bias) (+ resid) with W given fragment-ordered: a bf16 tensor
+    (CastCache.get_frag) or an e4m3 operand (frag8, scales, scale_mode) of the fp8 weight format
+    (Fp8Weights.get_frag8, csu_gemm_ws_e4m3: half the streamed weight bytes, bitwise the same result)."""
     M, K = x2.shape
     out = torch.empty(M, N, dtype=out_dtype, device=x2.device)
-    nb = M * K * 2 + N * K * 2 + M * N * out.element_size() + (M * N * 4 if resid is not None else 0)
+    e4 = isinstance(w_frag, tuple)
+    nb = M * K * 2 + N * K * (1 if e4 else 2) + M * N * out.element_size() + (M * N * 4 if resid is not None else 0)
+    tag = f"{M}x{N}x{K}{'r' if resid is not None else ''}{'b' if bias is not None else ''}:{out_dtype}:ws"
+    if e4:
+        wq, sc, mode = w_frag
+        _launch("gemm", lambda: lib().csu_gemm_ws_e4m3(M, N, K, ptr(x2), x2.stride(0), ptr(wq), ptr(sc), mode, ptr(bias),
+                                                       ptr(resid), dtype_code(out), ptr(out), stream_ptr(x2.device)),
+                2 * M * N * K, nb, prec="bf16", tag=tag + "8")
+        return out
     _launch("gemm", lambda: lib().csu_gemm_ws(M, N, K, ptr(x2), x2.stride(0), ptr(w_frag), ptr(bias), ptr(resid),
                                               dtype_code(out), ptr(out), stream_ptr(x2.device)),
-            2 * M * N * K, nb, prec="bf16",
-            tag=f"{M}x{N}x{K}{'r' if resid is not None else ''}{'b' if bias is not None else ''}:{out_dtype}:ws")
+            2 * M * N * K, nb, prec="bf16", tag=tag)
     return out
+
+
+# the fp8 weight format's qkv / proj Linears (and their input gradients) stream e4m3 weight fragments
+# in csu_gemm_ws_e4m3 (False: the bf16 fragments of the exact dequantised weights, same results)
+FP8_WS = os.environ.get("CSU_FP8_WS", "1") != "0"
+
+
+def _ws_operand(weight, transposed: bool = False):
+    """The weight-streaming GEMM operand of a cached 2-D weight: the e4m3 fragments (frag8, scales,
+    scale_mode) in the fp8 weight format, else the bf16 fragments of the cast cache, or None."""
+    if FP8_WS and _ACTIVE_FP8 is not None:
+        # the fp8 format makes no bf16 fragments (CSWinTransformer.forward skips refresh_frag)
+        return _ACTIVE_FP8.get_frag8(weight, transposed)
+    if _ACTIVE_CACHE is None:
+        return None
+    return _ACTIVE_CACHE.get_frag_t(weight) if transposed else _ACTIVE_CACHE.get_frag(weight)
 
 
 def _ws_ok(M, N, K, out_dtype, resid=False) -> bool:
@@ -1168,14 +1193,14 @@ class _LinearFn(torch.autograd.Function):
         if ctx.fast:
             x2 = xc.reshape(-1, K).contiguous()
             bf = None if bias is None else bias.detach().float().contiguous()
-            wf = _ACTIVE_CACHE.get_frag(weight) if _ACTIVE_CACHE is not None else None
+            wf = _ws_operand(weight)
             if wf is not None and _ws_ok(x2.shape[0], N, K, odt or cd):
                 y = gemm_ws(x2, wf, N, odt or cd, bias=bf)
             else:
                 y = gemm(x2, wc, False, odt or cd, bias=bf)
             y = y.view(*xc.shape[:-1], N)
             wt = _weight_t(weight, wc)
-            ctx.wtf = _ACTIVE_CACHE.get_frag_t(weight) if _ACTIVE_CACHE is not None else None
+            ctx.wtf = _ws_operand(weight, True)
         elif cd == torch.float32 and K % 4 == 0 and N % 4 == 0:
             # fp32 path (no autocast, BASELINE config 2): csu fp32 MFMA GEMM, bias in its epilogue
             x2 = xc.reshape(-1, K).contiguous()
@@ -1462,7 +1487,7 @@ class _LinearResidualFn(torch.autograd.Function):
         x2 = x.reshape(-1, x.shape[-1]).contiguous()
         M, K, N = x2.shape[0], x2.shape[1], wc.shape[0]
         bf = bias.detach().float().contiguous()
-        wf = _ACTIVE_CACHE.get_frag(weight) if _ACTIVE_CACHE is not None else None
+        wf = _ws_operand(weight)
         if (ln is not None and wf is not None and USE_GEMM_WS and K == N
                 and lib().csu_gemm_ws_ln_supported(M, N, K)):
             # + norm2 in the epilogue (csu_gemm_ws_ln), handed to the block's layer_norm_fork
@@ -1472,17 +1497,26 @@ class _LinearResidualFn(torch.autograd.Function):
             h = torch.empty(M, N, dtype=torch.bfloat16, device=x2.device)
             mean = torch.empty(M, dtype=torch.float32, device=x2.device)
             rstd = torch.empty(M, dtype=torch.float32, device=x2.device)
-            _launch("gemm", lambda: lib().csu_gemm_ws_ln(M, N, ptr(x2), K, ptr(wf), ptr(bf), ptr(res2), ptr(y), ptr(gf),
-                                                         ptr(bf_), float(eps), ptr(h), ptr(mean), ptr(rstd),
-                                                         stream_ptr(x2.device)),
-                    2 * M * N * K + 8 * M * N, M * K * 2 + N * K * 2 + M * N * (4 + 4 + 2) + 8 * M, tag=f"{M}x{N}x{K}rbln:ws")
+            if isinstance(wf, tuple):   # e4m3 weight fragments (fp8 format)
+                wq, sc, _ = wf
+                _launch("gemm", lambda: lib().csu_gemm_ws_ln_e4m3(M, N, ptr(x2), K, ptr(wq), ptr(sc), ptr(bf), ptr(res2),
+                                                                  ptr(y), ptr(gf), ptr(bf_), float(eps), ptr(h), ptr(mean),
+                                                                  ptr(rstd), stream_ptr(x2.device)),
+                        2 * M * N * K + 8 * M * N, M * K * 2 + N * K + M * N * (4 + 4 + 2) + 8 * M,
+                        tag=f"{M}x{N}x{K}rbln:ws8")
+            else:
+                _launch("gemm", lambda: lib().csu_gemm_ws_ln(M, N, ptr(x2), K, ptr(wf), ptr(bf), ptr(res2), ptr(y), ptr(gf),
+                                                             ptr(bf_), float(eps), ptr(h), ptr(mean), ptr(rstd),
+                                                             stream_ptr(x2.device)),
+                        2 * M * N * K + 8 * M * N, M * K * 2 + N * K * 2 + M * N * (4 + 4 + 2) + 8 * M,
+                        tag=f"{M}x{N}x{K}rbln:ws")
             _LN_STASH[0] = (gam, bet, float(eps), h, mean, rstd)
         elif wf is not None and _ws_ok(M, N, K, torch.float32, resid=True):
             y = gemm_ws(x2, wf, N, torch.float32, bias=bf, resid=res2)
         else:
             y = gemm(x2, wc, False, torch.float32, bias=bf, resid=res2)
         ctx.save_for_backward(x2, _weight_t(weight, wc))
-        ctx.wtf = _ACTIVE_CACHE.get_frag_t(weight) if _ACTIVE_CACHE is not None else None
+        ctx.wtf = _ws_operand(weight, True)
         ctx.meta = (res.dtype, x.shape, weight.dtype, bias.dtype)
         ctx.params = (weight, bias)
         _note_use(ctx, *ctx.params)
@@ -2166,11 +2200,48 @@ class Fp8Weights:
             self.lay_of[w1.data_ptr()] = (0, 0, w1tp.data_ptr())
             self.lay_of[w2.data_ptr()] = (w2p.data_ptr(), w2t.data_ptr(), 0)
         self.lay_count, self.lay_words = len(lay), w0
+        # e4m3 fragment-ordered W and W^T of the weights the weight-streaming GEMM runs (the qkv / proj
+        # Linears, csu_gemm_ws_e4m3), rebuilt from the e4m3 bytes after every quantisation (one launch)
+        self.frag8 = {}
+        f8, b0 = [], 0
+        L = lib()
+        for i, (p, q) in enumerate(zip(self.params, self.q)):
+            if q is None or p.dim() != 2:
+                continue
+            N, K = q.shape
+            if N % 32 or K % 32:
+                continue
+            fw = ft = None
+            if L.csu_gemm_ws_supported(1024, N, K, 0, CSU_BF16):
+                fw = torch.empty(N * K, dtype=torch.uint8, device=q.device)
+                f8.append((q.data_ptr(), fw.data_ptr(), N, K, 0, 0, b0))
+                b0 += N * K // 64
+            if L.csu_gemm_ws_supported(1024, K, N, 0, CSU_BF16):
+                ft = torch.empty(N * K, dtype=torch.uint8, device=q.device)
+                f8.append((q.data_ptr(), ft.data_ptr(), N, K, 1, 0, b0))
+                b0 += N * K // 64
+            if fw is not None or ft is not None:
+                self.frag8[p.data_ptr()] = (fw, ft, self.scales[i], tuple(p.shape))
+        self.frag8_count, self.frag8_blocks = len(f8), b0
+        if f8:
+            dt8 = np.dtype([("src", "<u8"), ("dst", "<u8"), ("N", "<i4"), ("K", "<i4"), ("transpose", "<i4"),
+                            ("pad", "<i4"), ("block0", "<i8")])
+            self.frag8_items = torch.frombuffer(bytearray(np.array(f8, dtype=dt8).tobytes()),
+                                                dtype=torch.uint8).to(self.params[0].device)
         if lay:
             lt = np.dtype([("src", "<u8"), ("dst", "<u8"), ("w0", "<i8"), ("rows", "<i4"), ("cols", "<i4"),
                            ("mode", "<i4"), ("pad", "<i4")])
             self.lay_items = torch.frombuffer(bytearray(np.array(lay, dtype=lt).tobytes()),
                                               dtype=torch.uint8).to(self.params[0].device)
+
+    def get_frag8(self, w, transposed: bool = False):
+        """(e4m3 fragments, row scales, csu_gemm_ws_e4m3 scale_mode) of W (mode 1) or W^T (mode 2) of
+        a quantised weight, or None."""
+        e = self.frag8.get(w.data_ptr())
+        if e is None or e[3] != tuple(w.shape):
+            return None
+        f = e[1] if transposed else e[0]
+        return None if f is None else (f, e[2], 2 if transposed else 1)
 
     def mlp_operands(self, w1, w2):
         """(w1q, sw1, w2p, sw2, w2t, w1tp) of the fused fp8 Mlp over fc1 / fc2 weights, or None."""
@@ -2240,11 +2311,19 @@ class Fp8Weights:
             items, blocks, count = self._shadow_items(cache)
             _launch("quant_e4m3", lambda: lib().csu_quant_e4m3_shadow_batch(ptr(items), count, blocks, stream_ptr(dev)),
                     0, nq * (4 + 1 + 2 + 2) + self.lay_words * 4)
+            self._layout_frag8(dev)
             return self.deq
         if self.lay_count:
             _launch("quant_e4m3", lambda: lib().csu_e4m3_layout_batch(ptr(self.lay_items), self.lay_count, self.lay_words,
                                                                      stream_ptr(dev)), 0, self.lay_words * 8)
+        self._layout_frag8(dev)
         return self.deq
+
+    def _layout_frag8(self, dev):
+        if self.frag8_count and FP8_WS:
+            n = self.frag8_blocks * 64
+            _launch("quant_e4m3", lambda: lib().csu_frag8_layout_batch(ptr(self.frag8_items), self.frag8_count,
+                                                                      self.frag8_blocks, stream_ptr(dev)), 0, 2 * n)
 
 
 _ACTIVE_CACHE: Optional[CastCache] = None
@@ -2433,7 +2512,8 @@ FUSE_LN_QKV = False   # measured: the epilogue phase costs what the LayerNorm la
 def ln_linear_ws(x: torch.Tensor, ln: torch.nn.LayerNorm, lin: torch.nn.Linear):
     """(x, lin(ln(x))) through _LnLinearWsFn (bf16 autocast, fp32 residual stream x, shapes with the
     weight-streaming GEMM and its LayerNorm-backward epilogue instantiated), else None."""
-    if not (FUSE_LN_QKV and USE_GEMM_WS and x.is_cuda and x.dtype == torch.float32 and _ACTIVE_CACHE is not None):
+    if not (FUSE_LN_QKV and USE_GEMM_WS and x.is_cuda and x.dtype == torch.float32 and _ACTIVE_CACHE is not None
+            and (_ACTIVE_FP8 is None or not FP8_WS)):
         return None
     N, K = lin.weight.shape
     if x.shape[-1] != K or ln.weight.numel() != K or ln.weight.dtype != torch.float32:

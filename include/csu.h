@@ -368,6 +368,30 @@ typedef struct {
 } csu_frag_item;
 int csu_frag_layout_batch(const csu_frag_item* items, int count, long total_chunks, void* stream);
 
+/* e4m3 weights (BASELINE config 5, the fp8 format's qkv / proj Linears): csu_gemm_ws with W = q * s[n]
+ * given as e4m3 bytes q in fragment order (csu_frag8_layout_batch: [N/32][K/16][64 lanes][8 bytes]) and
+ * per-row power-of-two scales s (fp32, length N of the Linear).  scale_mode 1: out = x W^T (w_frag8 =
+ * the fragments of q, s indexed by the output column); 2: out = dy W, the input gradient (w_frag8 = the
+ * fragments of q^T, s indexed by the reduction index).  Bitwise equal to csu_gemm_ws on the dequantised
+ * bf16 weight (power-of-two scales are applied exactly); same shapes / epilogues as csu_gemm_ws.
+ * csu_gemm_ws_ln_e4m3: csu_gemm_ws_ln with e4m3 weights (scale_mode 1). */
+int csu_gemm_ws_e4m3(long M, int N, int K, const void* x, int ldx, const void* w_frag8, const float* w_scale,
+                     int scale_mode, const float* bias, const float* resid, int out_dtype, void* out, void* stream);
+int csu_gemm_ws_ln_e4m3(long M, int C, const void* x, int ldx, const void* w_frag8, const float* w_scale,
+                        const float* bias, const float* resid, float* out, const float* gamma, const float* beta,
+                        float eps, void* ln_out, float* mean, float* rstd, void* stream);
+/* e4m3 fragment order of an e4m3 (N x K) matrix src (transpose 0: of src itself, rows N; 1: of src^T,
+ * rows K); N % 32 == 0, K % 32 == 0.  items: DEVICE array sorted by block0, the first 8x8-byte source
+ * block of the item (block0[i+1] = block0[i] + N * K / 64); total_blocks = the sum. */
+typedef struct {
+    const void* src;
+    void* dst;
+    int32_t N, K;
+    int32_t transpose, _pad;
+    int64_t block0;
+} csu_frag8_item;
+int csu_frag8_layout_batch(const csu_frag8_item* items, int count, long total_blocks, void* stream);
+
 /* ---------------------------------------------------------------------------------------
  * Batched weight cast: for each item, dst (rows, cols) bf16 = src fp32, and when dst_t is not
  * NULL also dst_t (cols, rows) bf16 = src^T.  items is a DEVICE array sorted by tile0, the first

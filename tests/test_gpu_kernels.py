@@ -1560,3 +1560,93 @@ def test_ln_linear_ws_vs_unfused(C):
     for name, u, v in zip(["y", "dx", "dgamma", "dbeta", "dW", "db"], a, b):
         rel = float((u - v).norm() / v.norm())
         assert rel < 1e-2, (name, rel)
+
+
+def _e4m3_rows(w):
+    """Per-row power-of-two e4m3 quantisation (the fp8 format's, oracle/fp8_ref.py): bytes q, scales s,
+    and the exact bf16 dequantisation q * s."""
+    amax = w.float().abs().amax(1).clamp_min(1e-30)
+    s = torch.exp2(torch.ceil(torch.log2(amax / 448.0)))
+    q = (w.float() / s[:, None]).to(torch.float8_e4m3fn)
+    return q.view(torch.uint8), s.contiguous(), (q.float() * s[:, None]).bfloat16()
+
+
+def _frag8(q, transpose):
+    """csu_frag8_layout_batch of one e4m3 (N, K) matrix."""
+    import numpy as np
+    from csu._lib import check, lib, ptr, stream_ptr
+    N, K = q.shape
+    out = torch.empty(N * K, dtype=torch.uint8, device=q.device)
+    dt = np.dtype([("src", "<u8"), ("dst", "<u8"), ("N", "<i4"), ("K", "<i4"), ("transpose", "<i4"), ("pad", "<i4"),
+                   ("block0", "<i8")])
+    it = torch.frombuffer(bytearray(np.array([(q.data_ptr(), out.data_ptr(), N, K, int(transpose), 0, 0)], dtype=dt)
+                                    .tobytes()), dtype=torch.uint8).to(q.device)
+    check(lib().csu_frag8_layout_batch(ptr(it), 1, N * K // 64, stream_ptr(q.device)), "frag8")
+    torch.cuda.synchronize()
+    return out
+
+
+@pytest.mark.parametrize("M,N,K,mode", [(16384, 768, 256, "bf16_bias"), (4096, 256, 256, "resid"), (4096, 384, 128, "f32"),
+                                        (8192, 192, 64, "bf16_bias"), (1024, 64, 64, "resid"),
+                                        (4096, 256, 768, "dgrad"), (4096, 128, 384, "dgrad"), (2048, 128, 128, "dgrad"),
+                                        (2048, 64, 64, "dgrad")])
+def test_gemm_ws_e4m3_bitwise_vs_dequantised(M, N, K, mode):
+    """fp8 weight format (BASELINE config 5): csu_gemm_ws_e4m3 streams e4m3 weight fragments and widens
+    them to bf16 in registers -- bitwise equal to csu_gemm_ws on the exact bf16 dequantisation, for x W^T
+    (scale_mode 1: per-column scales in the epilogue) and the input gradient dy W (scale_mode 2: the
+    weight is W^T, per-k scales on the token panel)."""
+    from csu import ops
+    d = dev()
+    g = torch.Generator(device=d).manual_seed(M + N + K)
+    x = torch.randn(M, K, device=d, generator=g).bfloat16()
+    qa, _, _ = _e4m3_rows(torch.randn(N, K, device=d, generator=g))
+    assert torch.equal(_frag8(qa, False), _frag_ref(qa)) and torch.equal(_frag8(qa, True), _frag_ref(qa.t().contiguous()))
+    if mode == "dgrad":
+        # the Linear's weight is Wl (K_l = N, N_l = K): out (M, N) = dy (M, K) @ Wl, Wl = q s (K x N rows)
+        wl = torch.randn(K, N, device=d, generator=g) / N ** 0.5
+        q, s, wd = _e4m3_rows(wl)
+        ref = ops.gemm_ws(x, _frag_ref(wd.t().contiguous()).contiguous(), N, torch.bfloat16)
+        got = ops.gemm_ws(x, (_frag8(q, True), s, 2), N, torch.bfloat16)
+    else:
+        w = torch.randn(N, K, device=d, generator=g) / K ** 0.5
+        q, s, wd = _e4m3_rows(w)
+        bias = torch.randn(N, device=d, generator=g) if mode != "f32" else None
+        resid = torch.randn(M, N, device=d, generator=g) if mode == "resid" else None
+        odt = torch.bfloat16 if mode == "bf16_bias" else torch.float32
+        ref = ops.gemm_ws(x, _frag_ref(wd).contiguous(), N, odt, bias=bias, resid=resid)
+        got = ops.gemm_ws(x, (_frag8(q, False), s, 1), N, odt, bias=bias, resid=resid)
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref), float((got.double() - ref.double()).abs().max())
+
+
+@pytest.mark.parametrize("M,C", [(16384, 256), (4096, 128), (8192, 64)])
+def test_gemm_ws_ln_e4m3_bitwise_vs_dequantised(M, C):
+    """csu_gemm_ws_ln_e4m3 (proj + residual + norm2 on e4m3 weights) == csu_gemm_ws_ln on the
+    dequantised bf16 weight, every output bit for bit."""
+    from csu._lib import lib, ptr, stream_ptr
+    d = dev()
+    g = torch.Generator(device=d).manual_seed(M + C + 1)
+    x = torch.randn(M, C, device=d, generator=g).bfloat16()
+    q, s, wd = _e4m3_rows(torch.randn(C, C, device=d, generator=g) / C ** 0.5)
+    bias = torch.randn(C, device=d, generator=g)
+    res = torch.randn(M, C, device=d, generator=g) * 2 + 0.5
+    gam = torch.randn(C, device=d, generator=g) * 0.5 + 1
+    bet = torch.randn(C, device=d, generator=g) * 0.1
+    outs = []
+    for e4 in (False, True):
+        y = torch.empty(M, C, device=d)
+        h = torch.empty(M, C, device=d, dtype=torch.bfloat16)
+        mean, rstd = torch.empty(M, device=d), torch.empty(M, device=d)
+        if e4:
+            f8 = _frag8(q, False)
+            rc = lib().csu_gemm_ws_ln_e4m3(M, C, ptr(x), C, ptr(f8), ptr(s), ptr(bias), ptr(res), ptr(y), ptr(gam), ptr(bet),
+                                           1e-5, ptr(h), ptr(mean), ptr(rstd), stream_ptr(d))
+        else:
+            wf = _frag_ref(wd).contiguous()
+            rc = lib().csu_gemm_ws_ln(M, C, ptr(x), C, ptr(wf), ptr(bias), ptr(res), ptr(y), ptr(gam), ptr(bet), 1e-5,
+                                      ptr(h), ptr(mean), ptr(rstd), stream_ptr(d))
+        torch.cuda.synchronize()
+        assert rc == 0
+        outs.append((y, h, mean, rstd))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
