@@ -472,8 +472,10 @@ def _dtype_label(args):
     if args.dtype != "fp8":
         return args.dtype
     from csu import ops
-    scope = "fused Mlp fwd (C 64/128/256) + bwd (C 256)" + (" + qkv" if ops.FP8_QKV else "")
-    return f"fp8-e4m3 x e4m3 MFMA ({scope}); bf16 MFMA on the dequantised e4m3 weights elsewhere"
+    bwd = "/".join(str(c) for c in ops.FP8_MLP_BWD_C)
+    scope = "fused Mlp fwd (C 64/128/256)" + (f" + bwd (C {bwd})" if bwd else "") + (" + qkv" if ops.FP8_QKV else "")
+    ws = "; qkv / proj weights streamed as e4m3 (widened to bf16 in registers)" if ops.FP8_WS else ""
+    return f"fp8-e4m3 x e4m3 MFMA ({scope}){ws}; bf16 MFMA on the dequantised e4m3 weights elsewhere"
 
 
 def _metric(args):

@@ -1740,10 +1740,12 @@ def _attach_ln(out):
         out._csu_ln = tuple(st) + (out._version,)
 
 
-# widths whose fp8 Mlp backward runs the fp8 kernel; the others run the bf16 fused backward on the
-# dequantised (exact) bf16 shadows of the e4m3 weights -- faster there (C = 64: 106 vs 120 us, C = 128:
-# 64 vs 90 us per launch in the 1024x1024 B4 step, profiles/r06d_step_breakdown_1024_fp8.txt)
-FP8_MLP_BWD_C = (256,)
+# widths whose fp8 Mlp backward runs the fp8 kernel (csu_mlp_fp8_bwd); the others run the bf16 fused
+# backward on the dequantised (exact) bf16 shadows of the e4m3 weights -- faster at every width since
+# round 6: C = 64: 106 vs 120 us, C = 128: 64 vs 90 us per launch (profiles/r06d_step_breakdown_1024_fp8.txt),
+# C = 256: the 8-wave bf16 backward (mlp_bwd8_kernel), mlp_bwd 1360 vs 1447 us/step at 1024x1024 B4
+# (profiles/r08g_fp8_ab.txt).  The fp8 kernel stays a tested entry point (tests/test_gpu_fp8.py).
+FP8_MLP_BWD_C = ()
 
 
 class _MlpFp8Fn(torch.autograd.Function):
