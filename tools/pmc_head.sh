@@ -24,6 +24,7 @@ for cfg in "${LIST[@]}"; do
   python tools/kernel_match.py "$KT" 5 $O/$tag/p1 > $O/match_$tag.txt || true
   cat $O/match_$tag.txt
   python tools/prof_groups.py "$KT" 5 $O/bench_$tag.json > $O/groups_$tag.md
-  python tools/pmc_groups.py $O/$tag $O/bench_$tag.json 12 > $O/pmc_$tag.md
+  [ -f $O/pmc_traffic.json ] || cp profiles/pmc_traffic.json $O/pmc_traffic.json
+  python tools/pmc_groups.py $O/$tag $O/bench_$tag.json 12 --traffic $O/pmc_traffic.json > $O/pmc_$tag.md
   head -30 $O/pmc_$tag.md
 done
