@@ -81,7 +81,7 @@ constexpr int ws_unit(int ks, int nt, int umax = 16) {
 // waves along N: 4 when the 32-feature tiles split evenly over 4 waves, else 2 (N = 64, 192: two token
 // groups of 64 per workgroup, each split over 2 waves) or 1
 constexpr int ws_wn(int n) { return (n / 32) % 4 == 0 ? 4 : (n / 32) % 2 == 0 ? 2 : 1; }
-constexpr int ws_tokens(int n, int bm = WS_BM) { return bm * (4 / ws_wn(n)); }   // tokens per workgroup
+constexpr int ws_tokens(int n) { return WS_BM * (4 / ws_wn(n)); }   // tokens per workgroup
 // N split over NS workgroups per token panel (grid.y): each streams 1/NS of the weight and writes 1/NS
 // of the features, two workgroups per CU.  Only for the plain epilogue (bias; RESID spills), K <= 256 (the token
 // panel in registers, two workgroups' LDS fit) and an even tile count per wave.  WS_NSPLIT = 1: off.
@@ -102,24 +102,20 @@ __device__ __forceinline__ bf16x8 e4m3x8_bf16(u32x2 w) {
     return bf16x8{p0[0], p0[1], p1[0], p1[1], p2[0], p2[1], p3[0], p3[1]};
 }
 
-// BM = 32 (round 6): 32-token panels, i.e. twice the workgroups, for the 16384-token stage where 64-token
-// panels give one workgroup -- one wave per SIMD -- per CU; at <= 256 registers two workgroups share a CU
-template <int K, int N, int EPI, typename TOUT, int NS = 1, int F8 = 0, int BM = WS_BM>
-__global__ __launch_bounds__(256, ws_wn(N) < 4 || NS > 1 || BM < WS_BM ? 2 : 1) void gemm_ws_kernel(long M, const bf16* __restrict__ X, int ldx,
+template <int K, int N, int EPI, typename TOUT, int NS = 1, int F8 = 0>
+__global__ __launch_bounds__(256, ws_wn(N) < 4 || NS > 1 ? 2 : 1) void gemm_ws_kernel(long M, const bf16* __restrict__ X, int ldx,
                                                       const bf16* __restrict__ Wf, const float* __restrict__ bias,
                                                       const float* __restrict__ resid, TOUT* __restrict__ out,
                                                       WsLn ln = WsLn{}, WsLnF lnf = WsLnF{},
                                                       const float* __restrict__ wsc = nullptr) {
     static_assert(F8 == 0 || EPI != WS_LNBWD, "gemm_ws: e4m3 weights not with the LayerNorm-backward epilogue");
-    static_assert(BM == WS_BM || (BM == 32 && EPI != WS_LNBWD && NS == 1), "gemm_ws: 32-token panels: no LayerNorm backward");
-    constexpr int TT = BM / 32;                    // 32-token tiles per wave
     constexpr int WN = ws_wn(N);                   // waves along N
     constexpr int NT = N / (32 * WN * NS);         // 32-feature tiles per wave (of this workgroup's N / NS)
     static_assert(NT * 32 * WN * NS == N, "gemm_ws: N = 32 WN NT NS");
     static_assert(NS == 1 || EPI == WS_PLAIN || EPI == WS_RESID, "gemm_ws: the LayerNorm epilogues need all N features");
     static_assert(EPI != WS_LNBWD || WN == 4, "gemm_ws: the LayerNorm epilogue needs all C features in one token group");
     constexpr int KS = K / 16;                     // k-steps
-    constexpr int UK = ws_unit(KS, NT, NS > 1 || BM < WS_BM ? 8 : 16);   // k-steps per unit (a divisor of KS; <= 8 at two WGs/CU)
+    constexpr int UK = ws_unit(KS, NT, NS > 1 ? 8 : 16);   // k-steps per unit (a divisor of KS; <= 8 at two WGs/CU)
     constexpr int CH = KS / UK;                    // units per tile
     static_assert(CH * UK == KS, "unit size");
     constexpr int U = NT * CH;                     // units per wave
@@ -127,15 +123,15 @@ __global__ __launch_bounds__(256, ws_wn(N) < 4 || NS > 1 || BM < WS_BM ? 2 : 1) 
     constexpr bool XLDS = !XREG || WN == 4;        // token panel staged through LDS (else direct fragment loads)
     constexpr int XS = K + 8;                      // LDS row stride of the token panel (bf16)
     constexpr int ES = 36;                         // fp32 row stride of the epilogue region
-    __shared__ __attribute__((aligned(16))) bf16 xs[XLDS ? BM * XS : 8];
-    __shared__ __attribute__((aligned(16))) float ep_all[4 * BM * ES];
+    __shared__ __attribute__((aligned(16))) bf16 xs[XLDS ? WS_BM * XS : 8];
+    __shared__ __attribute__((aligned(16))) float ep_all[4 * WS_BM * ES];
 
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int wn = wave % WN;                      // this wave's N slot
     const int r = lane & 31, h = lane >> 5;
-    const long m0 = (long)blockIdx.x * ws_tokens(N, BM) + BM * (wave / WN);   // the wave's BM-token panel
-    float* ep = ep_all + wave * BM * ES;
+    const long m0 = (long)blockIdx.x * ws_tokens(N) + WS_BM * (wave / WN);   // the wave's 64-token panel
+    float* ep = ep_all + wave * WS_BM * ES;
 
     // tile order rotated per workgroup (its index within the XCD: ids x, x + 8, ... run on XCD x), so
     // the CUs of an XCD do not all read the same weight lines at the same moment
@@ -159,13 +155,12 @@ __global__ __launch_bounds__(256, ws_wn(N) < 4 || NS > 1 || BM < WS_BM ? 2 : 1) 
 #pragma unroll
     for (int s = 0; s < UK; ++s) wload1(0, s);
     __builtin_amdgcn_sched_barrier(0);
-    bf16x8 xf[XREG ? TT : 1][XREG ? KS : 1];
+    bf16x8 xf[XREG ? 2 : 1][XREG ? KS : 1];
     if constexpr (XLDS) {
         // token panel -> LDS (16-B pieces, row-contiguous; one token group: WN = 4)
         constexpr int PR = K / 8;   // pieces per row
-        static_assert(BM * PR % 256 == 0, "gemm_ws: panel pieces per thread");
 #pragma unroll
-        for (int i = 0; i < BM * PR / 256; ++i) {
+        for (int i = 0; i < WS_BM * PR / 256; ++i) {
             const int p = threadIdx.x + 256 * i, row = p / PR, c = 8 * (p % PR);
             bf16x8 v = *reinterpret_cast<const bf16x8*>(X + (m0 + row) * ldx + c);
             if constexpr (F8 == 2) {   // column c + e of the panel is k = n of W: times s[n] (exact)
@@ -181,7 +176,7 @@ __global__ __launch_bounds__(256, ws_wn(N) < 4 || NS > 1 || BM < WS_BM ? 2 : 1) 
         __syncthreads();
         if constexpr (XREG) {
 #pragma unroll
-            for (int t = 0; t < TT; ++t)
+            for (int t = 0; t < 2; ++t)
 #pragma unroll
                 for (int s = 0; s < KS; ++s) xf[t][s] = *reinterpret_cast<const bf16x8*>(xs + (32 * t + r) * XS + 16 * s + 8 * h);
         }
@@ -189,7 +184,7 @@ __global__ __launch_bounds__(256, ws_wn(N) < 4 || NS > 1 || BM < WS_BM ? 2 : 1) 
         // B fragments straight from the token rows (lane (r, h): row r, k 16 s + 8 h .. + 7; a row's
         // 16-B pieces over the KS loads cover its lines once)
 #pragma unroll
-        for (int t = 0; t < TT; ++t)
+        for (int t = 0; t < 2; ++t)
 #pragma unroll
             for (int s = 0; s < KS; ++s) {
                 xf[t][s] = *reinterpret_cast<const bf16x8*>(X + (m0 + 32 * t + r) * ldx + 16 * s + 8 * h);
@@ -241,7 +236,7 @@ __global__ __launch_bounds__(256, ws_wn(N) < 4 || NS > 1 || BM < WS_BM ? 2 : 1) 
                 if constexpr (RES) {
                     const auto rs_res = buf_rsrc(resid + m0 * N, (M - m0) * N * 4);
 #pragma unroll
-                    for (int q = 0; q < BM / 8; ++q) buf_ld4(rs_res, (unsigned)((8 * q + (lane >> 3)) * N + n0 + cc) * 4, rv[q]);
+                    for (int q = 0; q < 8; ++q) buf_ld4(rs_res, (unsigned)((8 * q + (lane >> 3)) * N + n0 + cc) * 4, rv[q]);
                 }
             }
         }
@@ -253,17 +248,17 @@ __global__ __launch_bounds__(256, ws_wn(N) < 4 || NS > 1 || BM < WS_BM ? 2 : 1) 
             bf16x8 b0, b1;
             if constexpr (XREG) {
                 b0 = xf[0][ks];
-                b1 = xf[TT - 1][ks];
+                b1 = xf[XREG ? 1 : 0][ks];
             } else {
                 b0 = *reinterpret_cast<const bf16x8*>(xs + r * XS + 16 * ks + 8 * h);
-                b1 = *reinterpret_cast<const bf16x8*>(xs + (32 * (TT - 1) + r) * XS + 16 * ks + 8 * h);
+                b1 = *reinterpret_cast<const bf16x8*>(xs + (32 + r) * XS + 16 * ks + 8 * h);
             }
             const bf16x8 wa = wfrag(wf[u & 1][s]);
             a0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa, b0, a0, 0, 0, 0);
-            if constexpr (TT > 1) a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa, b1, a1, 0, 0, 0);
+            a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wa, b1, a1, 0, 0, 0);
             if (u + 1 < U) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);   // one weight load
-            if constexpr (!XREG) __builtin_amdgcn_sched_group_barrier(0x100, TT, 0);   // the fragment reads
-            __builtin_amdgcn_sched_group_barrier(0x008, TT, 0);                 // the MFMAs
+            if constexpr (!XREG) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);   // two fragment reads
+            __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);                 // two MFMAs
         }
         __builtin_amdgcn_sched_barrier(0);
         if (c != CH - 1) continue;
@@ -277,7 +272,7 @@ __global__ __launch_bounds__(256, ws_wn(N) < 4 || NS > 1 || BM < WS_BM ? 2 : 1) 
         // ---- epilogue of tile nt: acc element (token 32 t + r, feature 32 nt + 8 g + 4 h + e)
         const int nt = wn + WN * tile_of(u / CH);
 #pragma unroll
-        for (int t = 0; t < TT; ++t) {
+        for (int t = 0; t < 2; ++t) {
             const f32x16& a = t ? a1 : a0;
 #pragma unroll
             for (int g = 0; g < 4; ++g)
@@ -291,7 +286,7 @@ __global__ __launch_bounds__(256, ws_wn(N) < 4 || NS > 1 || BM < WS_BM ? 2 : 1) 
             // 4 lanes x 8 features per token row, 16 rows per instruction
             const int cc = 8 * (lane & 3);
 #pragma unroll
-            for (int q = 0; q < BM / 16; ++q) {
+            for (int q = 0; q < 4; ++q) {
                 const int row = 16 * q + (lane >> 2);
                 float v[8];
                 load4(ep + row * ES + cc, v);
@@ -307,7 +302,7 @@ __global__ __launch_bounds__(256, ws_wn(N) < 4 || NS > 1 || BM < WS_BM ? 2 : 1) 
             // fp32: 8 lanes x 4 features per token row, 8 rows per instruction
             const int cc = 4 * (lane & 7);
 #pragma unroll
-            for (int q = 0; q < BM / 8; ++q) {
+            for (int q = 0; q < 8; ++q) {
                 const int row = 8 * q + (lane >> 3);
                 float v[4];
                 load4(ep + row * ES + cc, v);
@@ -329,13 +324,13 @@ __global__ __launch_bounds__(256, ws_wn(N) < 4 || NS > 1 || BM < WS_BM ? 2 : 1) 
         // lane: rows 8 q + (lane >> 3) of its 64-token panel, features cc..cc+3 of each of its tiles.
         // Two passes over the registers (mean, then the centred sum of squares), each: the lane's
         // sum, the 8 lanes of the row (DPP), the WN waves of the token group through LDS.
-        __shared__ float lnx[2][4][BM];
+        __shared__ float lnx[2][4][WS_BM];
         const int rq = lane >> 3, g0 = (wave / WN) * WN;
         float mu[8], rsd[8];
 #pragma unroll
         for (int pass = 0; pass < 2; ++pass) {
 #pragma unroll
-            for (int q = 0; q < BM / 8; ++q) {
+            for (int q = 0; q < 8; ++q) {
                 float a = 0.f;
 #pragma unroll
                 for (int i = 0; i < NT; ++i)
@@ -349,7 +344,7 @@ __global__ __launch_bounds__(256, ws_wn(N) < 4 || NS > 1 || BM < WS_BM ? 2 : 1) 
             }
             __syncthreads();
 #pragma unroll
-            for (int q = 0; q < BM / 8; ++q) {
+            for (int q = 0; q < 8; ++q) {
                 float t = 0.f;
 #pragma unroll
                 for (int j = 0; j < WN; ++j) t += lnx[pass][g0 + j][8 * q + rq];
@@ -363,7 +358,7 @@ __global__ __launch_bounds__(256, ws_wn(N) < 4 || NS > 1 || BM < WS_BM ? 2 : 1) 
         for (int i = 0; i < NT; ++i) {
             const int n0 = 32 * (wn + WN * tile_of(i));
 #pragma unroll
-            for (int q = 0; q < BM / 8; ++q) {
+            for (int q = 0; q < 8; ++q) {
                 float o[4];
 #pragma unroll
                 for (int e = 0; e < 4; ++e) o[e] = (yk[i][q][e] - mu[q]) * rsd[q] * lg[i][e] + lb[i][e];
@@ -372,7 +367,7 @@ __global__ __launch_bounds__(256, ws_wn(N) < 4 || NS > 1 || BM < WS_BM ? 2 : 1) 
         }
         if (wn == 0 && (lane & 7) == 0) {
 #pragma unroll
-            for (int q = 0; q < BM / 8; ++q) {
+            for (int q = 0; q < 8; ++q) {
                 lnf.mean[m0 + 8 * q + rq] = mu[q];
                 lnf.rstd[m0 + 8 * q + rq] = rsd[q];
             }
@@ -496,21 +491,10 @@ __global__ __launch_bounds__(256, ws_wn(N) < 4 || NS > 1 || BM < WS_BM ? 2 : 1) 
     }
 }
 
-#ifndef WS_HALF
-#define WS_HALF 1
-#endif
 template <int K, int N, int EPI, typename TOUT, int F8 = 0>
 int ws_launch(long M, const bf16* X, int ldx, const bf16* Wf, const float* bias, const float* resid, void* out,
               hipStream_t st, const WsLn& ln = WsLn{}, const WsLnF& lnf = WsLnF{}, const float* wsc = nullptr) {
     constexpr int NS = F8 ? 1 : ws_ns(K, N, EPI);
-    if constexpr (ws_wn(N) == 4 && EPI != WS_LNBWD && NS == 1) {
-        // fewer than two 64-token workgroups per CU (the 16384-token stage): 32-token panels
-        if (WS_HALF && M / WS_BM < 512 && M % 32 == 0) {
-            gemm_ws_kernel<K, N, EPI, TOUT, 1, F8, 32><<<dim3((unsigned)(M / 32), 1), 256, 0, st>>>(
-                M, X, ldx, Wf, bias, resid, (TOUT*)out, ln, lnf, wsc);
-            return check_launch("gemm_ws");
-        }
-    }
     gemm_ws_kernel<K, N, EPI, TOUT, NS, F8><<<dim3((unsigned)(M / ws_tokens(N)), NS), 256, 0, st>>>(
         M, X, ldx, Wf, bias, resid, (TOUT*)out, ln, lnf, wsc);
     return check_launch("gemm_ws");
