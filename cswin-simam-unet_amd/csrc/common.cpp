@@ -33,7 +33,10 @@ extern "C" const char* csu_build_info(void) { return "libcsu_hip 0.1 (gfx950, CD
 extern "C" int csu_event_create(void** event) {
     if (!event) return csu::fail(CSU_E_ARG, "event_create: null");
     hipEvent_t e = nullptr;
-    if (hipEventCreate(&e) != hipSuccess) return csu::fail(CSU_E_ARG, "event_create: hipEventCreate failed");
+    // timing only (the ledger reads them after a full synchronize): no system-scope fence, so recording
+    // one between two kernels of a replayed graph does not add an L2 write-back to the kernel before it
+    if (hipEventCreateWithFlags(&e, hipEventDisableSystemFence) != hipSuccess)
+        return csu::fail(CSU_E_ARG, "event_create: hipEventCreateWithFlags failed");
     *event = e;
     return CSU_OK;
 }

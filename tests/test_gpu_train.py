@@ -346,6 +346,7 @@ FULL_CONFIGS = [
     (512, 16, [2, 4, 32, 2], [1, 2, 8, 8], False, None),
     (1024, 4, [1, 2, 9, 1], [1, 2, 8, 8], False, None),
     (1024, 4, [1, 2, 9, 1], [1, 2, 8, 8], False, "fp8_e4m3"),
+    (1024, 4, [1, 2, 9, 1], [1, 2, 8, 8], True, "fp8_e4m3"),     # configs[4] as named: +SimAM, fp8
 ]
 
 

@@ -49,7 +49,8 @@ def main():
             # the fixed-order slab reduction inside a conv / Linear weight-gradient call (csu_colsum's
             # kernels launched by csu_conv2d_wgrad_oihw) belongs to that call: a colsum kernel right
             # after a weight-gradient kernel is charged to it (ops.colsum's own launches stay "colsum")
-            if g == "colsum" and prev in ("conv_wgrad", "linear_wgrad"):
+            # (and the head's bias / encoder-bias sums launched by csu_carafe_head_bwd)
+            if g == "colsum" and prev in ("conv_wgrad", "linear_wgrad", "carafe_head_bwd"):
                 g = prev
             prev = g
             t[g] += (int(r["End_Timestamp"]) - s) / 1e3
