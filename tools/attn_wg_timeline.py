@@ -16,13 +16,15 @@ import torch  # noqa: E402
 from csu import ops  # noqa: E402
 from csu._lib import lib  # noqa: E402
 
-STAGES = {1: (128, 64, 2, 1), 2: (64, 128, 4, 2), 3: (32, 256, 8, 8), 4: (16, 512, 16, 16)}
+STAGES = {1: (128, 64, 2, 1), 2: (64, 128, 4, 2), 3: (32, 256, 8, 8), 4: (16, 512, 16, 16),
+          # 1024x1024 B4: stage 3 (512-token windows, stripe_bwd_fused_w<512, 8 waves>)
+          13: (64, 256, 8, 8)}
 
 
 def main():
     st = int(sys.argv[1]) if len(sys.argv) > 1 else 3
     reso, C, heads, sw = STAGES[st]
-    B = 16
+    B = 4 if st >= 10 else 16
     d = torch.device("cuda")
     nb = 1 if sw == reso else 2
     brs = [(reso, sw, 0), (sw, reso, C // 2)] if nb == 2 else [(reso, reso, 0)]

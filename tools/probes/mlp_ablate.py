@@ -24,6 +24,9 @@ OUT = os.path.join(HERE, "mlp_abl")
 # round 6 set: "old" = the 4-wave kernels (the ablations of those, base / nodma / nosync / nogelu / nomfma /
 # nostore, are in profiles/r08b_mlp_ablate.txt), "w8" = the 8-wave kernels as built, and their ablations
 VARIANTS = ["old", "w8", "w8_hc64", "w8_nodma", "w8_nomfma", "w8_dmaonly"]
+# per-phase ablations of the 8-wave backward (phase A / B / C of mlp_bwd8_kernel skipped, one at a time)
+if os.environ.get("MLP_ABL_SET") == "bwd8":
+    VARIANTS = ["w8", "w8_nodma", "w8_noA", "w8_noB", "w8_noC", "w8_noAC", "w8_dmaonly"]
 OLD_ONLY = ("base", "nodma", "nosync", "nogelu", "nomfma", "nostore", "old")
 
 
@@ -45,6 +48,13 @@ def edit(src: str, v: str) -> str:
         if v in ("w8_nomfma", "w8_dmaonly"):
             body = re.sub(r"(\w+(?:\[\w+\])*) = __builtin_amdgcn_mfma_f32_(?:32x32x16|16x16x32)_bf16\(([^;]*?), ([\w\[\]]+), \1, 0, 0, 0\);",
                           r'asm volatile("" :: "v"(\2), "v"(\3));', body)
+        phases = {"A": "// ---- phase A\n        {", "B": "// ---- phase B\n        {",
+                  "C": "// ---- phase C: acc[tt] += W1[chunk]^T[fo ..][hidden] dH[hidden][32 tt ..]\n        {"}
+        if v in ("w8_noA", "w8_noB", "w8_noC", "w8_noAC"):
+            for k in v[len("w8_no"):]:
+                assert phases[k] in body, k
+                body = body.replace(phases[k], phases[k].replace("{", "if (M < 0) {"))
+            return src[:a] + body + src[b:]
         if v == "w8_dmaonly":     # DMA + barriers only: no fragment reads, no GELU, no phase work
             body = body.replace("if (j < NCH) gemm1(j);", "").replace("if (j > 0) gemm2(j - 1);", "")
             for ph in ("// ---- phase A\n        {", "// ---- phase B\n        {", "// ---- phase C: acc[tt] += W1[chunk]^T[fo ..][hidden] dH[hidden][32 tt ..]\n        {"):
