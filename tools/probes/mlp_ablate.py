@@ -27,7 +27,7 @@ VARIANTS = ["old", "w8", "w8_hc64", "w8_nodma", "w8_nomfma", "w8_dmaonly"]
 # per-phase ablations of the 8-wave backward (phase A / B / C of mlp_bwd8_kernel skipped, one at a time)
 if os.environ.get("MLP_ABL_SET") == "bwd8":
     VARIANTS = ["w8", "w8_nodma", "w8_noA", "w8_noB", "w8_noC", "w8_noAC", "w8_dmaonly"]
-
+OLD_ONLY = ("base", "nodma", "nosync", "nogelu", "nomfma", "nostore", "old")
 
 
 def edit(src: str, v: str) -> str:
