@@ -13,7 +13,9 @@ namespace {
 
 constexpr int NT = 256;
 constexpr int WAVES = NT / 64;
-constexpr int LU = 4;       // ln_bwd: row groups per wave iteration
+// ln_bwd: row groups per wave iteration -- 8 (4 at V = 8, C = 512: the registers of 8 would not fit).
+// 8 vs 4: layernorm_bwd 1086-1093 vs 1103-1105 us/step at 512x512 B16 (profiles/r08z_ln_lu_ab.txt)
+template <int V> constexpr int lu_of() { return V == 8 ? 4 : 8; }
 constexpr int FU = 4;       // ln_fwd: row groups per wave
 
 struct e4m3 { uint8_t v; };  // ln_fwd output type: OCP e4m3fn bytes + one power-of-two scale per row
@@ -162,6 +164,7 @@ __global__ __launch_bounds__(NT) void ln_bwd(int rows, int C, int rows_per_block
                                              const float* __restrict__ dres, TX* __restrict__ dx,
                                              bf16* __restrict__ dxb, float* __restrict__ part) {
     constexpr int RPW = 64 / LPR;
+    constexpr int LU = lu_of<V>();
     __shared__ float red[WAVES][2][512];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int c0 = (lane % LPR) * V;
@@ -270,13 +273,16 @@ __global__ __launch_bounds__(RT) void ln_param_reduce(int C, int nb, const float
     ln_cols_sum(part, C, nb, blockIdx.x * 64, dgamma, dbeta);
 }
 
-int ln_blocks(int rows, int rpw, int* rpb) {   // <= 512 blocks, rows per block a multiple of a block's row step
-    const int step = WAVES * rpw * LU;
+int ln_blocks(int rows, int rpw, int lu, int* rpb) {   // <= 512 blocks, rows per block a multiple of a block's row step
+    const int step = WAVES * rpw * lu;
     int r = (rows + 511) / 512;   // (1024 / 2048 blocks measured no faster: tools/ln_probe.py)
     r = ((r + step - 1) / step) * step;
     *rpb = r;
     return (rows + r - 1) / r;
 }
+
+// the backward's block count for rows x C (rows per wave 64 / LPR = C >= 256 ? 1 : 256 / C; V = 8 at C = 512)
+int ln_bwd_blocks(int rows, int C, int* rpb) { return ln_blocks(rows, C >= 256 ? 1 : 256 / C, C == 512 ? 4 : 8, rpb); }
 
 int check_c(int C) {
     if (C % 64 || C < 64 || C > 512) return fail(CSU_E_UNSUPPORTED, "layernorm: C must be 64..512, multiple of 64");
@@ -311,7 +317,7 @@ int launch_bwd(int rows, int C, const void* x, const float* g, const float* m, c
                const float* dres, void* dx, bf16* dxb, float* dgamma, float* dbeta, float* part, hipStream_t st) {
     int rpb, nb;
 #define CSU_LNB(V, LPR)                                                                                              \
-    nb = ln_blocks(rows, 64 / LPR, &rpb);                                                                            \
+    nb = ln_bwd_blocks(rows, C, &rpb);                                                                               \
     ln_bwd<TX, TG, V, LPR><<<nb, NT, 0, st>>>(rows, C, rpb, (const TX*)x, g, m, r, (const TG*)dy, dres, (TX*)dx, dxb, \
                                              part)
     switch (C / 64) {
@@ -367,7 +373,7 @@ extern "C" int csu_layernorm_fwd_fp8(int rows, int C, float eps, int xdtype, con
 
 extern "C" size_t csu_layernorm_bwd_workspace(int rows, int C) {
     int rpb;
-    const int nb = ln_blocks(rows, C >= 256 ? 1 : 256 / C, &rpb);   // rows per wave = 64 / LPR, LPR = min(64, C/4)
+    const int nb = ln_bwd_blocks(rows, C, &rpb);
     return (size_t)nb * 2 * C * sizeof(float);
 }
 
@@ -427,7 +433,7 @@ extern "C" int csu_layernorm_param_reduce(int rows, int C, const void* workspace
     if (int e = check_c(C)) return e;
     if (rows < 1 || !workspace || !dgamma || !dbeta) return fail(CSU_E_ARG, "layernorm_param_reduce: bad args");
     int rpb;
-    const int nb = ln_blocks(rows, C >= 256 ? 1 : 256 / C, &rpb);
+    const int nb = ln_bwd_blocks(rows, C, &rpb);
     ln_param_reduce<<<2 * C / 64, RT, 0, as_stream(stream)>>>(C, nb, (const float*)workspace, dgamma, dbeta);
     return check_launch("layernorm_param_reduce");
 }
@@ -444,7 +450,7 @@ extern "C" int csu_layernorm_param_reduce_batch(const csu_ln_param_item* items, 
             if (it.rows < 1 || !it.workspace || !it.dgamma || !it.dbeta)
                 return fail(CSU_E_ARG, "layernorm_param_reduce_batch: bad item");
             int rpb;
-            t.nb[i] = it.nblocks > 0 ? it.nblocks : ln_blocks(it.rows, it.C >= 256 ? 1 : 256 / it.C, &rpb);
+            t.nb[i] = it.nblocks > 0 ? it.nblocks : ln_bwd_blocks(it.rows, it.C, &rpb);
             t.C[i] = it.C;
             t.part[i] = (const float*)it.workspace;
             t.dg[i] = it.dgamma;
