@@ -697,7 +697,7 @@ int persist_grid(long M) {   // one workgroup (two panel streams) per CU, fewer 
 //  * GEMM2: wave w owns the output features 32 w .. 32 w + 31 for all 64 tokens (two 32x32x16 tiles,
 //    K = the chunk's 64 hidden): A = W2 rows from the ring, B = g from the LDS image -- no partial
 //    outputs to exchange at the end, 32 accumulator registers per token tile.
-// ~220 VGPRs: two waves per SIMD.  Step j (one barrier): DMA W1(j+1), W2(j); GEMM1 + GELU of chunk j;
+// 154-158 VGPRs: two waves per SIMD.  Step j (one barrier): DMA W1(j+1), W2(j); GEMM1 + GELU of chunk j;
 // GEMM2 of chunk j-1.  LDS per step and CU: 160 KB of fragment reads + 64 KB of DMA (256 B/clk: ~900
 // cycles) against 1024 MFMA cycles per SIMD.
 // HCK = 32: 32-hidden chunks through a 4-stage ring (the same 128 KB), the weight DMA up to three
