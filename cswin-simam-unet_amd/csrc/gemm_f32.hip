@@ -140,19 +140,22 @@ __global__ __launch_bounds__(NT) void gemm_f32_kernel(long M, long N, long K, lo
     }
 }
 
-// sum over the splits of the A column sums (layout-2 bias gradient), split order
-__global__ __launch_bounds__(NT) void asum_sum(long M, int splits, const float* __restrict__ part, float* __restrict__ out) {
-    const long m = (long)blockIdx.x * NT + threadIdx.x;
-    if (m >= M) return;
-    float s = part[m];
-    for (int z = 1; z < splits; ++z) s += part[(long)z * M + m];
-    out[m] = s;
-}
-
-// out[e] = sum_z slab[z][e] in z order (+ bias[e % N], + resid[e])
+// out[e] = sum_z slab[z][e] in z order (+ bias[e % N], + resid[e]); the blocks past the slab's also
+// sum the splits' A column sums (layout-2 bias gradient, asum[m] = sum_z apart[z][m], split order) --
+// one launch instead of two (the fp32 path's per-Linear weight gradients: 105 launches of ~4 us each)
 __global__ __launch_bounds__(NT) void slab_sum(long n4, int N, int splits, long slab, const float* __restrict__ part,
                                                const float* __restrict__ bias, const float* __restrict__ resid,
-                                               float* __restrict__ out) {
+                                               float* __restrict__ out, long M, const float* __restrict__ apart,
+                                               float* __restrict__ aout) {
+    const long nb1 = (n4 + NT - 1) / NT;
+    if ((long)blockIdx.x >= nb1) {
+        const long m = ((long)blockIdx.x - nb1) * NT + threadIdx.x;
+        if (m >= M) return;
+        float s = apart[m];
+        for (int z = 1; z < splits; ++z) s += apart[(long)z * M + m];
+        aout[m] = s;
+        return;
+    }
     const long e = ((long)blockIdx.x * NT + threadIdx.x) * 4;
     if (e >= n4 * 4) return;
     f32x4 s = *reinterpret_cast<const f32x4*>(part + e);
@@ -241,9 +244,9 @@ extern "C" int csu_gemm_f32(int layout, long M, int N, long K, const float* A, c
     if (int e = check_launch("gemm_f32")) return e;
     if (split) {
         const long n4 = M * N / 4;
-        slab_sum<<<(unsigned)((n4 + NT - 1) / NT), NT, 0, st>>>(n4, N, (int)p.splits, M * N, (const float*)workspace, bias,
-                                                               resid, C);
-        if (asum) asum_sum<<<(unsigned)((M + NT - 1) / NT), NT, 0, st>>>(M, (int)p.splits, sdst, asum);
+        const long nb = (n4 + NT - 1) / NT + (asum ? (M + NT - 1) / NT : 0);
+        slab_sum<<<(unsigned)nb, NT, 0, st>>>(n4, N, (int)p.splits, M * N, (const float*)workspace, bias, resid, C,
+                                              asum ? M : 0, sdst, asum);
         return check_launch("gemm_f32 slab sum");
     }
     return 0;
