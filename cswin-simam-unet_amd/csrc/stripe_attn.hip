@@ -1534,6 +1534,12 @@ __global__ __launch_bounds__(64 * NW, WM <= 256 ? 2 : 1) void stripe_bwd_fused_w
 #pragma unroll
         for (int i = 0; i < 40; ++i) wacc[i] = 0.f;
         const f32x4 bias = *reinterpret_cast<const f32x4*>(wts + HD * 9 + 4 * c4);
+        // the thread's 9 x 4 LePE weights are the same for all its rows: read once, kept in registers
+        // (inside the row loop they were re-read per row in dependent batches of LDS round trips;
+        // stripe_attn_bwd -6 / -17 us per step at 512 / 1024, profiles/r09k_att_wreg_ab.txt)
+        f32x4 wreg[9];
+#pragma unroll
+        for (int t = 0; t < 9; ++t) wreg[t] = *reinterpret_cast<const f32x4*>(wts + t * HD + 4 * c4);
         const bf16* vq = Vs + 4 * c4;                  // plain image: row n of this quad at vq + 32 n
         // the preloaded O rows rotate through orow[0..RP) so every register index stays static.
         // Out-of-window taps read the zero row.
@@ -1575,7 +1581,7 @@ __global__ __launch_bounds__(64 * NW, WM <= 256 ? 2 : 1) void stripe_bwd_fused_w
                 for (int j = 0; j < 4; ++j) lp[j] = bias[j];
 #pragma unroll
                 for (int t = 0; t < 9; ++t) {
-                    const f32x4 wt = *reinterpret_cast<const f32x4*>(wts + t * HD + 4 * c4);
+                    const f32x4 wt = wreg[t];
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
                         const float v = (float)v4[p][t][j];
