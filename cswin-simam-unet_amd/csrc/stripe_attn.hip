@@ -1765,12 +1765,25 @@ __global__ __launch_bounds__(64 * NW, WM <= 256 ? 2 : 1) void stripe_bwd_fused_w
         __syncthreads();
         // dQ^T[d][q] quadrant (d = 16 dh + 4 (lane >> 4) + i, q = qb + 16 qh + (lane & 15)) over all keys
         f32x4v acc2[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};   // two independent MFMA chains
+        if (NW == 4 && ntile == RT) {   // (8 waves: the extra live fragments spilled)
+            // the whole window (the common case): no per-tile condition, so the fragment reads of the
+            // next key tiles issue while this one's MFMA runs (with the condition every tile was a
+            // branch: its reads, a full LDS wait, then its MFMA -- ~120 cycles per key tile).
+            // stripe_attn_bwd -32 us/step at 512x512 B16 (profiles/r09n_att_dq_full_ab.txt)
 #pragma unroll
-        for (int k2 = 0; k2 < KK; ++k2) {
-            const int kk = kh * KK + k2;
-            if (kk < ntile)
+            for (int k2 = 0; k2 < KK; ++k2) {
+                const int kk = kh * KK + k2;
                 acc2[k2 & 1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr16(Ks + kk * 32 * HD, o_k16),
                                                                       tr16(dS + kk * 32 * HD, o_d16), acc2[k2 & 1], 0, 0, 0);
+            }
+        } else {
+#pragma unroll
+            for (int k2 = 0; k2 < KK; ++k2) {
+                const int kk = kh * KK + k2;
+                if (kk < ntile)
+                    acc2[k2 & 1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(tr16(Ks + kk * 32 * HD, o_k16),
+                                                                          tr16(dS + kk * 32 * HD, o_d16), acc2[k2 & 1], 0, 0, 0);
+            }
         }
         f32x4v acc = acc2[0] + acc2[1];
         if constexpr (NW == 8)
