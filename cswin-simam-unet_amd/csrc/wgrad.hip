@@ -137,6 +137,10 @@ __device__ __forceinline__ v4s tr_read(const bf16* p) {
     return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(p));
 }
 
+#ifndef WG_SB128
+#define WG_SB128 1
+#endif
+
 // LDS operand images are [TM tokens][T columns] bf16 with no padding; the 16-B chunks of a row are
 // XOR-swizzled so that a ds_read_b64_tr_b16 (each 32-lane half reads 4 consecutive rows x 64 B)
 // and the ds_write_b128 staging are bank-conflict free: T = 128 (256-B rows, one bank row each):
@@ -265,7 +269,10 @@ __device__ __forceinline__ void wgrad_tile_body(bf16* lds, int t, long M, int N,
                 for (int b = 0; b < C::AK; ++b)
                     acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[a], fb[b], acc[a][b], 0, 0, 0);
             // 256 x 256: one k-step's fragments live at a time (the 256 accumulators fill the AGPRs)
-            if constexpr (TN * TK > 256 * 128) __builtin_amdgcn_sched_barrier(0);
+            // 128 x 128 (4 waves, 2 workgroups per CU): the same -- with every k-step's fragments hoisted
+            // the kernel spilled an LDS address whose reload (vmcnt) waited for the whole load prefetch
+            if constexpr (TN * TK > 256 * 128 || (WG_SB128 && TN * TK == 128 * 128 && NTH == NT))
+                __builtin_amdgcn_sched_barrier(0);
         }
     };
     // Register set s % D holds step s, LDS buffer s & 1.  The loop runs a multiple of lcm(D, 2) steps
