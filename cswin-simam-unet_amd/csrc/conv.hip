@@ -143,6 +143,20 @@ __global__ __launch_bounds__(NT) void conv_gemm(Geo g, long Mrows, int Ncols, in
     }
 }
 
+// weight-gradient grids are (n tile, k tile, token chunk): the tiles of one chunk read the same dy rows
+// and input pixels, so they run on one XCD (consecutive logical ids, xcd_block) and share its L2 --
+// in hardware order consecutive workgroups go to different XCDs and each re-fetched the chunk
+#ifndef CW_XCD
+#define CW_XCD 1
+#endif
+struct Blk3 { int x, y, z; };
+__device__ __forceinline__ Blk3 wg_block() {
+    if (!CW_XCD) return {(int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z};
+    const int t = __builtin_amdgcn_readfirstlane((int)xcd_block());
+    const int gx = gridDim.x, gy = gridDim.y;
+    return {t % gx, (t / gx) % gy, t / (gx * gy)};
+}
+
 // dW partial slabs: workgroup (n tile, k tile, m chunk) accumulates dY^T X_gather over its rows.
 // Operands staged transposed ([n][m], [k][m]) in LDS; db from the k-tile-0 workgroups.
 template <typename T, bool VEC>
@@ -154,12 +168,13 @@ __global__ __launch_bounds__(NT) void conv_wgrad_kernel(Geo g, long Mrows, int N
     constexpr int S = TM + (sizeof(T) == 2 ? 8 : 4);
     __shared__ __attribute__((aligned(16))) T At[TBN * S];   // dy^T [n][m]
     __shared__ __attribute__((aligned(16))) T Bt[TBN * S];   // X^T  [k][m]
-    const int n0 = blockIdx.x * TBN, k0 = blockIdx.y * TBN;
-    const long mb = (long)blockIdx.z * rows_per_chunk, me = min(Mrows, mb + rows_per_chunk);
+    const Blk3 wb = wg_block();
+    const int n0 = wb.x * TBN, k0 = wb.y * TBN;
+    const long mb = (long)wb.z * rows_per_chunk, me = min(Mrows, mb + rows_per_chunk);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int r = lane & 31, h = lane >> 5;
     const int wn = (wave >> 1) * 32, wk = (wave & 1) * 32;
-    const bool do_bias = blockIdx.y == 0;
+    const bool do_bias = wb.y == 0;
     f32x16 acc = {};
     float bsum = 0.f;
     // staging: RG x (32 rows x 8 chunks) = RG chunks per operand per thread, all loads issued
@@ -224,7 +239,7 @@ __global__ __launch_bounds__(NT) void conv_wgrad_kernel(Geo g, long Mrows, int N
         }
     }
     const long slab = ((long)Ncols * Kdim + Ncols + 3) & ~3L;   // 16-B aligned slab rows for colsum
-    float* out = part + (long)blockIdx.z * slab;
+    float* out = part + (long)wb.z * slab;
 #pragma unroll
     for (int reg = 0; reg < 16; ++reg) {
         const int n = n0 + wn + crow(reg, h), k = k0 + wk + r;
@@ -262,12 +277,13 @@ __global__ __launch_bounds__(NT) void conv_wgrad_bf16(Geo g, long Mrows, int Nco
     constexpr int RS = TBN + 32;          // 64 data + 64 B pad: conflict-free transposing reads
     __shared__ __attribute__((aligned(16))) bf16 At[TM * RS];   // dy tile [m][n]
     __shared__ __attribute__((aligned(16))) bf16 Bt[TM * RS];   // x  tile [m][k] (gathered)
-    const int n0 = blockIdx.x * TBN, k0 = blockIdx.y * TBN;
-    const long mb = (long)blockIdx.z * rows_per_chunk, me = min(Mrows, mb + rows_per_chunk);
+    const Blk3 wb = wg_block();
+    const int n0 = wb.x * TBN, k0 = wb.y * TBN;
+    const long mb = (long)wb.z * rows_per_chunk, me = min(Mrows, mb + rows_per_chunk);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int h = lane >> 5;
     const int wn = (wave >> 1) * 32, wk = (wave & 1) * 32;
-    const bool do_bias = blockIdx.y == 0;
+    const bool do_bias = wb.y == 0;
     f32x16 acc = {};
     float bsum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
     const int srow = threadIdx.x >> 3, sch = threadIdx.x & 7;
@@ -327,7 +343,7 @@ __global__ __launch_bounds__(NT) void conv_wgrad_bf16(Geo g, long Mrows, int Nco
                                                           acc, 0, 0, 0);
     }
     const long slab = ((long)Ncols * Kdim + Ncols + 3) & ~3L;   // 16-B aligned slab rows for colsum
-    float* out = part + (long)blockIdx.z * slab;
+    float* out = part + (long)wb.z * slab;
 #pragma unroll
     for (int reg = 0; reg < 16; ++reg) {
         const int nn = n0 + wn + crow(reg, h), k = k0 + wk + (lane & 31);
@@ -370,14 +386,15 @@ __global__ __launch_bounds__(64 * WN * WK, 1) void conv_wgrad_dma(Geo g, long Mr
     constexpr int TNW = TN / (32 * WN), TKW = TK / (32 * WK);
     static_assert(NA >= 1 && NB >= 1 && TNW >= 1 && TKW >= 1 && (P - 1) * D <= 63, "conv_wgrad_dma layout");
     __shared__ __attribute__((aligned(1024))) bf16 smem[S * STAGE];
-    const int n0 = blockIdx.x * TN, k0 = blockIdx.y * TK;
-    const long mb = (long)blockIdx.z * rpc, me = min(Mrows, mb + rpc);
+    const Blk3 wb = wg_block();
+    const int n0 = wb.x * TN, k0 = wb.y * TK;
+    const long mb = (long)wb.z * rpc, me = min(Mrows, mb + rpc);
     const int nsteps = (int)((me - mb + RM - 1) / RM);
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int h = lane >> 5;
     const int wn = (wave / WK) * (TN / WN), wk = (wave % WK) * (TK / WK);
-    const bool do_bias = blockIdx.y == 0 && wave % WK == 0;
+    const bool do_bias = wb.y == 0 && wave % WK == 0;
 
     // dy image: lane's row and 16-B column chunk per instruction (fixed), byte offset within a step
     unsigned voffA[NA];
@@ -462,7 +479,7 @@ __global__ __launch_bounds__(64 * WN * WK, 1) void conv_wgrad_dma(Geo g, long Mr
     }
     vmwait<0>();   // drain the prefetch past the chunk before the LDS is released
     const long slab = ((long)Ncols * Kdim + Ncols + 3) & ~3L;
-    float* out = part + (long)blockIdx.z * slab;
+    float* out = part + (long)wb.z * slab;
 #pragma unroll
     for (int j = 0; j < TNW; ++j)
 #pragma unroll
@@ -517,14 +534,15 @@ __global__ __launch_bounds__(64 * NS / 16, 1) void conv3_wgrad_halo(Geo g, long 
     constexpr int P = S - 1;
     static_assert((P - 1) * NI <= 63, "conv3_wgrad_halo ring");
     __shared__ __attribute__((aligned(1024))) bf16 smem[S * STAGE];
-    const int n0 = blockIdx.x * NS, c0 = blockIdx.y * 64;
-    const long sb = (long)blockIdx.z * spc, se = min(nseg, sb + spc);
+    const Blk3 wb = wg_block();
+    const int n0 = wb.x * NS, c0 = wb.y * 64;
+    const long sb = (long)wb.z * spc, se = min(nseg, sb + spc);
     const int nsteps = (int)(se - sb);
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int h = lane >> 5;
     const int nt = wave % NTW, ct = wave / NTW;
-    const bool do_bias = blockIdx.y == 0 && ct == 0;
+    const bool do_bias = wb.y == 0 && ct == 0;
     const int spr = g.OW / 64;                      // segments per output row
     // per instruction: the lane's image row and channel / n column (block-aligned regions: the
     // region -- halo image ky or the dy image -- is uniform per instruction)
@@ -605,7 +623,7 @@ __global__ __launch_bounds__(64 * NS / 16, 1) void conv3_wgrad_halo(Geo g, long 
     vmwait<0>();
     const long K = 9L * g.C;
     const long slab = ((long)g.N * K + g.N + 3) & ~3L;
-    float* out = part + (long)blockIdx.z * slab;
+    float* out = part + (long)wb.z * slab;
     const int c = c0 + ct * 32 + (lane & 31);
 #pragma unroll
     for (int t = 0; t < 9; ++t)
