@@ -420,7 +420,16 @@ int gemm4_fp8_run(long M, int N, int K, const uint8_t* A, const float* sa, const
 // 128 x 64 stays everywhere; the 8-wave configurations stay selectable (cfg 16-19) and GPU-tested.
 // The time per tile hardly follows its L2 -> LDS bytes (the 8-wave 128 x 128 tile moves 2/3 of the
 // bytes of two 128 x 64 tiles in the same time).  cfg indexes kG4Cfgs.
-int gemm4_pick(long, int, int) { return 1; }
+// Exception (G4_SMALLM): when the 128 x 64 tiles cannot give every one of the 2 x CUs workgroups a
+// tile (the 4096-token stage: 4096 x 512 outputs = 256 tiles), the 64 x 64 tile with a 3-stage ring
+// doubles the tiles in flight -- those launches are latency-bound, one K loop per CU.
+#ifndef G4_SMALLM
+#define G4_SMALLM 1
+#endif
+int gemm4_pick(long M, int N, int) {
+    if (G4_SMALLM && ((M + 127) / 128) * (long)((N + 63) / 64) < (long)g4_grid(2)) return 0;
+    return 1;
+}
 
 int gemm4_run(int cfg, int epi, int odt, long M, int N, int K, const bf16* A, int lda, const bf16* W, int ldw,
               const float* bias, const bf16* gaux, const float* resid, void* out, bf16* gout, int ldc, hipStream_t st) {
