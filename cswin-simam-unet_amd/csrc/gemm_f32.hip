@@ -24,20 +24,24 @@ namespace csu {
 namespace {
 
 constexpr int NT = 256;
-constexpr int BK = 16, PAD = 4;
+#ifndef F32_BK
+#define F32_BK 32
+#endif
+constexpr int BK = F32_BK, PAD = 4;
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-// TM x 16 tile of operand X into regs (TM / 64 float4 per thread): element (i, k) of X at
+// TM x BK tile of operand X into regs (TM BK / 1024 float4 per thread): element (i, k) of X at
 // X[i * ld + k] (KC) or X[k * ld + i]
 template <int TM, bool KC>
 __device__ __forceinline__ void load_tile(const float* X, long ld, long i0, long ni, long k0, long k1, int tid, f32x4* v) {
     constexpr int QR = TM / 4;   // float4 per k row (!KC)
+    constexpr int QK = BK / 4;   // float4 per i row (KC)
 #pragma unroll
-    for (int u = 0; u < TM / 64; ++u) {
+    for (int u = 0; u < TM * BK / 1024; ++u) {
         const int f = tid + u * NT;
         long i, k;
-        if constexpr (KC) { i = i0 + (f >> 2); k = k0 + 4 * (f & 3); }
+        if constexpr (KC) { i = i0 + f / QK; k = k0 + 4 * (f % QK); }
         else { k = k0 + f / QR; i = i0 + 4 * (f % QR); }
         const bool ok = i < ni && k < k1;   // the contiguous dimension is a multiple of 4
         v[u] = ok ? *reinterpret_cast<const f32x4*>(X + (KC ? i * ld + k : k * ld + i)) : f32x4{};
@@ -46,12 +50,12 @@ __device__ __forceinline__ void load_tile(const float* X, long ld, long i0, long
 
 template <int TM, bool KC, int W>
 __device__ __forceinline__ void store_tile(float (*S)[W], int tid, const f32x4* v) {
-    constexpr int QR = TM / 4;
+    constexpr int QR = TM / 4, QK = BK / 4;
 #pragma unroll
-    for (int u = 0; u < TM / 64; ++u) {
+    for (int u = 0; u < TM * BK / 1024; ++u) {
         const int f = tid + u * NT;
         if constexpr (KC) {
-            const int i = f >> 2, k = 4 * (f & 3);
+            const int i = f / QK, k = 4 * (f % QK);
 #pragma unroll
             for (int e = 0; e < 4; ++e) S[k + e][i] = v[u][e];
         } else {
@@ -68,7 +72,7 @@ __global__ __launch_bounds__(NT) void gemm_f32_kernel(long M, long N, long K, lo
                                                       long lda, const float* __restrict__ B, long ldb,
                                                       const float* __restrict__ bias, const float* __restrict__ resid,
                                                       float* __restrict__ C, long slab, float* __restrict__ asum) {
-    constexpr int F = TM / 64, WT = TM / 2, NV = TM / 64;
+    constexpr int F = TM / 64, WT = TM / 2, NV = TM * BK / 1024;
     // asum (layout 2: the bias gradient): sum over this split's k of A(m, k), by the n-tile-0 blocks
     const bool do_sum = asum != nullptr && blockIdx.x == 0;
     float colacc = 0.f;
