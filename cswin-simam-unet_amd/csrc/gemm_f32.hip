@@ -24,6 +24,9 @@ namespace csu {
 namespace {
 
 constexpr int NT = 256;
+#ifndef F32_T128
+#define F32_T128 4   // 128-tiles when they give >= F32_T128 workgroups per CU
+#endif
 #ifndef F32_BK
 #define F32_BK 32
 #endif
@@ -190,7 +193,7 @@ PlanF32 plan_f32(int layout, long M, long N, long K) {
     PlanF32 p;
     const long cus = num_cus_f32();
     const long t128 = ((M + 127) / 128) * ((N + 127) / 128);
-    p.tm = t128 >= 2 * cus ? 128 : 64;
+    p.tm = t128 >= F32_T128 * cus ? 128 : 64;
     const long tiles = ((M + p.tm - 1) / p.tm) * ((N + p.tm - 1) / p.tm);
     long s = (2 * cus + tiles - 1) / tiles;
     const long mink = layout == 2 ? 512 : 256;
