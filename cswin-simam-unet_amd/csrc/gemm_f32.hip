@@ -27,6 +27,9 @@ constexpr int NT = 256;
 #ifndef F32_T128
 #define F32_T128 4   // 128-tiles when they give >= F32_T128 workgroups per CU
 #endif
+#ifndef F32_MINK2
+#define F32_MINK2 256   // minimum split depth of the weight gradient (layout 2, tokens)
+#endif
 #ifndef F32_BK
 #define F32_BK 32
 #endif
@@ -196,7 +199,7 @@ PlanF32 plan_f32(int layout, long M, long N, long K) {
     p.tm = t128 >= F32_T128 * cus ? 128 : 64;
     const long tiles = ((M + p.tm - 1) / p.tm) * ((N + p.tm - 1) / p.tm);
     long s = (2 * cus + tiles - 1) / tiles;
-    const long mink = layout == 2 ? 512 : 256;
+    const long mink = layout == 2 ? F32_MINK2 : 256;
     const long maxs = (K + mink - 1) / mink;
     if (s > maxs) s = maxs;
     if (s < 1) s = 1;
